@@ -1,0 +1,291 @@
+"""ctypes front-end for the CPU oracle (oracle/kaolin_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package (kaolin-windows_amd/).
+All functions take / return numpy arrays and mirror the argument meaning of the
+reference's ``kaolin._C`` entry points, plus the thin PyTorch
+glue of the reference front-ends where a test needs the whole chain.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, '_build', 'libkaolin_oracle.so')
+_lib = None
+
+_P = ctypes.c_void_p
+
+
+def build():
+    subprocess.check_call(['make', '-s', '-C', _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+        _lib.or_mesh_to_spc_leaves.restype = ctypes.c_int64
+        _lib.or_morton_to_octree.restype = ctypes.c_int64
+        _lib.or_raytrace.restype = ctypes.c_int64
+        _lib.or_scan_octrees.restype = ctypes.c_int
+        _lib.or_to_morton.restype = ctypes.c_uint64
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(_P) if a is not None else None
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def _suffix(dtype):
+    if dtype == np.float32:
+        return 'f32'
+    if dtype == np.float64:
+        return 'f64'
+    raise TypeError(f'oracle supports float32/float64, got {dtype}')
+
+
+# ----------------------------------------------------------------- rasterize
+def packed_rasterize_forward(height, width, fvz, fvi, bboxes, feat, first_idx, multiplier, eps):
+    """rasterization.cpp:49-104 (packed inputs, coordinates already x multiplier)."""
+    dt = np.asarray(fvz).dtype
+    sfx = _suffix(dt)
+    fvz, fvi, bboxes, feat = (_c(a, dt) for a in (fvz, fvi, bboxes, feat))
+    first_idx = _c(first_idx, np.int64)
+    B = first_idx.shape[0] - 1
+    D = feat.shape[-1]
+    out_feat = np.zeros((B, height, width, D), dt)
+    out_idx = np.full((B, height, width), -1, np.int64)
+    out_w = np.zeros((B, height, width, 3), dt)
+    getattr(lib(), f'or_rasterize_fwd_{sfx}')(
+        height, width, B, D, _p(fvz), _p(fvi), _p(bboxes), _p(feat), _p(first_idx),
+        ctypes.c_float(multiplier), ctypes.c_float(eps), _p(out_feat), _p(out_idx), _p(out_w))
+    return out_feat, out_idx, out_w
+
+
+def rasterize_backward(grad_feat, face_idx, weights, fvi, feat, eps):
+    """rasterization.cpp:106-168 (face_idx = original per-mesh face index)."""
+    dt = np.asarray(grad_feat).dtype
+    sfx = _suffix(dt)
+    grad_feat, weights, fvi, feat = (_c(a, dt) for a in (grad_feat, weights, fvi, feat))
+    face_idx = _c(face_idx, np.int64)
+    B, H, W, D = grad_feat.shape
+    F = fvi.shape[1]
+    g_img = np.zeros_like(fvi)
+    g_feat = np.zeros_like(feat)
+    getattr(lib(), f'or_rasterize_bwd_{sfx}')(
+        B, H, W, F, D, _p(grad_feat), _p(face_idx), _p(weights), _p(fvi), _p(feat),
+        ctypes.c_float(eps), _p(g_img), _p(g_feat))
+    return g_img, g_feat
+
+
+def rasterize(height, width, fvz, fvi, feat, valid_faces=None, multiplier=1000, eps=1e-8):
+    """Whole rasterize() chain of rasterization.py:290-369 in numpy + the oracle kernel.
+    Returns (features, face_idx, weights)."""
+    dt = np.asarray(fvz).dtype
+    B, F = fvz.shape[:2]
+    D = feat.shape[-1]
+    if valid_faces is None:
+        valid_faces = np.ones((B, F), bool)
+    bi, fi = np.nonzero(valid_faces)
+    vfvi = fvi[bi, fi] * dt.type(multiplier)
+    vfvz = fvz[bi, fi]
+    vfeat = feat[bi, fi]
+    first = np.zeros(B + 1, np.int64)
+    first[1:] = np.cumsum(valid_faces.reshape(B, -1).sum(1))
+    bbox = np.concatenate([vfvi.min(1), vfvi.max(1)], 1)
+    out_feat, sel, w = packed_rasterize_forward(height, width, vfvz, vfvi, bbox, vfeat.reshape(-1, 3, D),
+                                                first, multiplier, eps)
+    face_idx = np.where(sel >= 0, fi[np.clip(sel + first[:-1, None, None], 0, max(len(fi) - 1, 0))] if len(fi) else -1, -1)
+    return out_feat, face_idx.astype(np.int64), w
+
+
+# ----------------------------------------------------------------- soft mask
+def dibr_soft_mask_forward(fvi_m, bboxes, sel, sigmainv, knum, multiplier):
+    """dibr_soft_mask.cpp:48-108 (fvi_m / bboxes already x multiplier)."""
+    dt = np.asarray(fvi_m).dtype
+    sfx = _suffix(dt)
+    fvi_m, bboxes = _c(fvi_m, dt), _c(bboxes, dt)
+    sel = _c(sel, np.int64)
+    B, F = fvi_m.shape[:2]
+    H, W = sel.shape[1:]
+    mask = np.zeros((B, H, W), dt)
+    prob = np.zeros((B, H, W, knum), dt)
+    cidx = np.full((B, H, W, knum), -1, np.int64)
+    ctype = np.zeros((B, H, W, knum), np.uint8)
+    getattr(lib(), f'or_soft_mask_fwd_{sfx}')(
+        B, H, W, F, knum, _p(fvi_m), _p(bboxes), _p(sel), ctypes.c_float(sigmainv),
+        ctypes.c_float(multiplier), _p(mask), _p(prob), _p(cidx), _p(ctype))
+    return mask, prob, cidx, ctype
+
+
+def dibr_soft_mask_backward(grad, mask, sel, prob, cidx, ctype, fvi_m, sigmainv, multiplier):
+    dt = np.asarray(grad).dtype
+    sfx = _suffix(dt)
+    grad, mask, prob, fvi_m = (_c(a, dt) for a in (grad, mask, prob, fvi_m))
+    sel, cidx = _c(sel, np.int64), _c(cidx, np.int64)
+    ctype = _c(ctype, np.uint8)
+    B, F = fvi_m.shape[:2]
+    H, W = sel.shape[1:]
+    K = cidx.shape[-1]
+    g = np.zeros_like(fvi_m)
+    getattr(lib(), f'or_soft_mask_bwd_{sfx}')(
+        B, H, W, F, K, _p(grad), _p(mask), _p(sel), _p(prob), _p(cidx), _p(ctype), _p(fvi_m),
+        ctypes.c_float(sigmainv), ctypes.c_float(multiplier), _p(g))
+    return g
+
+
+def soft_mask_bboxes(fvi, boxlen, multiplier):
+    """dibr.py:31-39 glue: scale by multiplier and enlarge the bounding boxes."""
+    dt = np.asarray(fvi).dtype
+    fm = fvi * dt.type(multiplier)
+    pmin = fm.min(-2)
+    pmax = fm.max(-2)
+    bl = dt.type(boxlen * multiplier)
+    return fm, np.concatenate([pmin - bl, pmax + bl], -1)
+
+
+# ----------------------------------------------------------------- distances
+def unbatched_triangle_distance_forward(points, face_vertices):
+    dt = np.asarray(points).dtype
+    sfx = _suffix(dt)
+    points, fv = _c(points, dt), _c(face_vertices, dt)
+    P, F = points.shape[0], fv.shape[0]
+    dist = np.zeros(P, dt)
+    idx = np.zeros(P, np.int64)
+    typ = np.zeros(P, np.int32)
+    getattr(lib(), f'or_p2m_fwd_{sfx}')(P, F, _p(points), _p(fv), _p(dist), _p(idx), _p(typ))
+    return dist, idx, typ
+
+
+def unbatched_triangle_distance_backward(grad, points, face_vertices, idx, typ):
+    dt = np.asarray(points).dtype
+    sfx = _suffix(dt)
+    grad, points, fv = _c(grad, dt), _c(points, dt), _c(face_vertices, dt)
+    idx, typ = _c(idx, np.int64), _c(typ, np.int32)
+    gp = np.zeros_like(points)
+    gf = np.zeros_like(fv)
+    getattr(lib(), f'or_p2m_bwd_{sfx}')(points.shape[0], fv.shape[0], _p(grad), _p(points), _p(fv),
+                                        _p(idx), _p(typ), _p(gp), _p(gf))
+    return gp, gf
+
+
+def sided_distance_forward(p1, p2):
+    dt = np.asarray(p1).dtype
+    sfx = _suffix(dt)
+    p1, p2 = _c(p1, dt), _c(p2, dt)
+    B, N, M = p1.shape[0], p1.shape[1], p2.shape[1]
+    dist = np.zeros((B, N), dt)
+    idx = np.zeros((B, N), np.int64)
+    getattr(lib(), f'or_sided_fwd_{sfx}')(B, N, M, _p(p1), _p(p2), _p(dist), _p(idx))
+    return dist, idx
+
+
+def sided_distance_backward(grad, p1, p2, idx):
+    dt = np.asarray(p1).dtype
+    sfx = _suffix(dt)
+    grad, p1, p2 = _c(grad, dt), _c(p1, dt), _c(p2, dt)
+    idx = _c(idx, np.int64)
+    B, N, M = p1.shape[0], p1.shape[1], p2.shape[1]
+    g1 = np.zeros_like(p1)
+    g2 = np.zeros_like(p2)
+    getattr(lib(), f'or_sided_bwd_{sfx}')(B, N, M, _p(grad), _p(p1), _p(p2), _p(idx), _p(g1), _p(g2))
+    return g1, g2
+
+
+# ----------------------------------------------------------------------- SPC
+def to_morton(points):
+    pts = np.asarray(points)
+    return np.array([lib().or_to_morton(int(x), int(y), int(z)) for x, y, z in pts], np.uint64)
+
+
+def morton_to_octree(mortons, level):
+    m = _c(mortons, np.uint64)
+    out = ctypes.POINTER(ctypes.c_uint8)()
+    n = lib().or_morton_to_octree(_p(m), m.shape[0], level, ctypes.byref(out))
+    res = np.ctypeslib.as_array(out, shape=(max(n, 1),))[:n].copy()
+    lib().or_free(out)
+    return res
+
+
+def mesh_to_spc(face_vertices, level):
+    """mesh_to_spc.cpp:28-44 -> (octree u8, face_idx i64, bary f32 (N,2)); empty -> (0,),(0,),(0,3)."""
+    fv = _c(face_vertices, np.float32)
+    pm = ctypes.POINTER(ctypes.c_uint64)()
+    pf = ctypes.POINTER(ctypes.c_int64)()
+    n = lib().or_mesh_to_spc_leaves(_p(fv), fv.shape[0], level, ctypes.byref(pm), ctypes.byref(pf))
+    if n == 0:
+        return np.zeros(0, np.uint8), np.zeros(0, np.int64), np.zeros((0, 3), np.float32)
+    mort = np.ctypeslib.as_array(pm, shape=(n,)).copy()
+    face = np.ctypeslib.as_array(pf, shape=(n,)).copy()
+    lib().or_free(pm)
+    lib().or_free(pf)
+    bary = np.zeros((n, 2), np.float32)
+    flat = fv.reshape(-1, 9)
+    for i in range(n):
+        lib().or_bary(_p(np.ascontiguousarray(flat[face[i]])), ctypes.c_uint64(int(mort[i])), level,
+                      bary[i].ctypes.data_as(_P))
+    return morton_to_octree(mort, level), face, bary
+
+
+def scan_octrees(octrees, lengths):
+    o = _c(octrees, np.uint8)
+    ln = _c(lengths, np.int32)
+    B = ln.shape[0]
+    pyr = np.zeros((B, 2, 17), np.int32)
+    ex = np.zeros(int(ln.sum()) + B, np.int32)
+    level = lib().or_scan_octrees(_p(o), _p(ln), B, _p(pyr), _p(ex))
+    return level, np.ascontiguousarray(pyr[:, :, :level + 2]), ex
+
+
+def generate_points(octrees, pyramids, exsum):
+    o = _c(octrees, np.uint8)
+    pyr = _c(pyramids, np.int32)
+    ex = _c(exsum, np.int32)
+    B, L = pyr.shape[0], pyr.shape[2] - 2
+    total = int(pyr[:, 1, L + 1].sum())
+    pts = np.zeros((total, 3), np.int16)
+    lib().or_generate_points(_p(o), _p(pyr), B, L, _p(ex), _p(pts))
+    return pts
+
+
+def raytrace(octree, points, pyramid, exsum, origin, direction, level, return_depth=True, with_exit=False):
+    """raytrace.cpp:170-214 -> nuggets (N,2) int32 [, depth (N,1|2) f32]."""
+    o = _c(octree, np.uint8)
+    pts = _c(points, np.int16)
+    ex = _c(exsum, np.int32)
+    ro = _c(origin, np.float32)
+    rd = _c(direction, np.float32)
+    pn = ctypes.POINTER(ctypes.c_int32)()
+    pd = ctypes.POINTER(ctypes.c_float)()
+    n = lib().or_raytrace(_p(o), _p(pts), _p(ex), _p(ro), _p(rd), ro.shape[0], level,
+                          int(return_depth), int(with_exit), ctypes.byref(pn), ctypes.byref(pd))
+    dd = 2 if with_exit else 1
+    nug = np.ctypeslib.as_array(pn, shape=(max(n, 1) * 2,))[:2 * n].reshape(n, 2).copy()
+    lib().or_free(pn)
+    if return_depth:
+        dep = np.ctypeslib.as_array(pd, shape=(max(n, 1) * dd,))[:n * dd].reshape(n, dd).copy()
+        lib().or_free(pd)
+        return nug, dep
+    return (nug,)
+
+
+def voxelgrid(vertices, faces, resolution, origin=None, scale=None):
+    """trianglemeshes_to_voxelgrids (float32): dense (B,R,R,R) uint8 occupancy."""
+    v = _c(vertices, np.float32)
+    f = _c(faces, np.int64)
+    B, V = v.shape[:2]
+    R = int(resolution)
+    grid = np.zeros((B, R, R, R), np.uint8)
+    o = _c(origin, np.float32) if origin is not None else None
+    s = _c(scale, np.float32) if scale is not None else None
+    lib().or_voxelgrid_f32(_p(v), B, V, _p(f), f.shape[0], R, _p(o), _p(s), _p(grid))
+    return grid

@@ -1,0 +1,240 @@
+"""Pin the CPU oracle (oracle/) against the reference's own golden vectors.
+
+CPU-only.  Every expected value here comes from tests/golden/*.npz, written by
+tests/golden/make_golden.py from the reference (Kaolin 0.14.0) golden files,
+its pure-PyTorch test oracles, or KATs transcribed from its test sources.
+Tolerances are the reference tests' own (cited per test).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+
+def _mask_iou_grad(soft_mask, target):
+    """d mask_iou / d soft_mask (kaolin/metrics/render.py:18-40) via torch autograd."""
+    s = torch.from_numpy(np.ascontiguousarray(soft_mask)).requires_grad_(True)
+    r = torch.from_numpy(np.ascontiguousarray(target)).to(s.dtype)
+    B = s.shape[0]
+    mul = s * r
+    add = s + r
+    up = torch.sum(mul.reshape(B, -1), dim=1)
+    down = torch.sum((add - mul).reshape(B, -1), dim=1)
+    loss = 1.0 - torch.mean(up / (down + 1e-10))
+    loss.backward()
+    return s.grad.numpy()
+
+
+def _shifted_mask(sel):
+    mask = sel != -1
+    out = np.zeros_like(mask)
+    out[..., :-5] = mask[..., 5:]
+    return out
+
+
+# ------------------------------------------------------------ DIB-R simple
+@pytest.mark.parametrize('dtype', [np.float32, np.float64])
+@pytest.mark.parametrize('sig,box', [(7000, 0.02), (7000, 0.2), (70, 0.02), (70, 0.2)])
+@pytest.mark.parametrize('knum', [30, 20])
+@pytest.mark.parametrize('multiplier', [1000, 100, 1])
+def test_soft_mask_simple(golden, dtype, sig, box, knum, multiplier):
+    """test_dibr.py:108-191: 1e-5 on mask/prob/grad, exact idx/type."""
+    g = golden('dibr_simple.npz')
+    fvi = g['face_vertices_image'].astype(dtype)
+    fvz = g['face_vertices_z'].astype(dtype)
+    feat = np.zeros(fvz.shape + (1,), dtype)
+    _, sel, _ = orc.rasterize(35, 31, fvz, fvi, feat)
+    assert np.array_equal(sel, g['selected_face_idx'])
+    fm, bb = orc.soft_mask_bboxes(fvi, box, multiplier)
+    mask, prob, cidx, ctype = orc.dibr_soft_mask_forward(fm, bb, sel, sig, knum, multiplier)
+    np.testing.assert_allclose(mask, g[f'soft_mask_{sig}_{box}'], atol=1e-5, rtol=1e-5)
+    assert np.array_equal(cidx, g[f'close_face_idx_{sig}_{box}'][..., :knum])
+    np.testing.assert_allclose(prob, g[f'close_face_prob_{sig}_{box}'][..., :knum], atol=1e-5, rtol=1e-5)
+    assert np.array_equal(ctype, g[f'close_face_dist_type_{sig}_{box}'][..., :knum])
+    gmask = _mask_iou_grad(mask, _shifted_mask(sel))
+    gimg = orc.dibr_soft_mask_backward(gmask, mask, sel, prob, cidx, ctype, fm, sig, multiplier)
+    np.testing.assert_allclose(gimg, g[f'grad_{sig}_{box}'], atol=1e-5, rtol=1e-5)
+
+
+# ------------------------------------------------------------ DIB-R sphere
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('flip', [0, 1])
+@pytest.mark.parametrize('valid', [0, 1])
+def test_rasterize_sphere(golden, dname, flip, valid):
+    """test_rasterization.py:133-232: face_idx exact, features 1e-5,
+    grads rtol 1e-3 / atol 1e-2 (vertices), 1e-3 (features)."""
+    g = golden('dibr_sphere.npz')
+    p = f'{dname}_flip{flip}_'
+    q = p + f'valid{valid}_'
+    vf = g[p + 'valid_faces'] if valid else None
+    feat, fidx, w = orc.rasterize(35, 31, g[p + 'face_vertices_z'], g[p + 'face_vertices_image'],
+                                  g[p + 'face_uvs'], valid_faces=vf)
+    assert np.array_equal(fidx, g[q + 'face_idx'])
+    np.testing.assert_allclose(feat, g[q + 'features'], rtol=1e-5, atol=1e-5)
+    gimg, gfeat = orc.rasterize_backward(g[q + 'grad_out'], fidx, w, g[p + 'face_vertices_image'],
+                                         g[p + 'face_uvs'], 1e-8)
+    np.testing.assert_allclose(gimg, g[q + 'grad_face_vertices_image'], rtol=1e-3, atol=1e-2)
+    np.testing.assert_allclose(gfeat, g[q + 'grad_face_uvs'], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('flip', [0, 1])
+@pytest.mark.parametrize('sig,box', [(7000, 0.02), (7000, 0.01), (70, 0.02), (70, 0.01)])
+@pytest.mark.parametrize('knum', [30, 40])
+def test_soft_mask_sphere(golden, dname, flip, sig, box, knum):
+    """test_dibr.py:297-394: mask/prob 1e-5, idx exact, type <=1% mismatch, grad 1e-1."""
+    g = golden('dibr_sphere.npz')
+    p = f'{dname}_flip{flip}_'
+    fvi = g[p + 'face_vertices_image']
+    fvz = g[p + 'face_vertices_z']
+    _, sel, _ = orc.rasterize(35, 31, fvz, fvi, np.zeros(fvz.shape + (1,), fvz.dtype))
+    for multiplier in (1000, 100):
+        fm, bb = orc.soft_mask_bboxes(fvi, box, multiplier)
+        mask, prob, cidx, ctype = orc.dibr_soft_mask_forward(fm, bb, sel, sig, knum, multiplier)
+        np.testing.assert_allclose(mask, g[f'soft_mask_{sig}_{box}'], atol=1e-5, rtol=1e-5)
+        assert np.array_equal(cidx, g[f'close_face_idx_{sig}_{box}'][..., :knum])
+        np.testing.assert_allclose(prob, g[f'close_face_prob_{sig}_{box}'][..., :knum], atol=1e-5, rtol=1e-5)
+        assert np.mean(ctype != g[f'close_face_dist_type_{sig}_{box}'][..., :knum]) <= 0.01
+        gmask = _mask_iou_grad(mask, _shifted_mask(sel))
+        gimg = orc.dibr_soft_mask_backward(gmask, mask, sel, prob, cidx, ctype, fm, sig, multiplier)
+        np.testing.assert_allclose(gimg, g[f'grad_{sig}_{box}'], atol=1e-1, rtol=1e-1)
+
+
+# ------------------------------------------------------- point_to_mesh
+def test_p2m_kat(golden):
+    """metrics/test_trianglemesh.py:24-79."""
+    g = golden('p2m.npz')
+    for dt in (np.float32, np.float64):
+        d, i, t = orc.unbatched_triangle_distance_forward(g['kat_points'].astype(dt),
+                                                          g['kat_face_vertices'].astype(dt))
+        np.testing.assert_allclose(d, g['kat_dist'], rtol=1e-5, atol=1e-8)
+        assert np.array_equal(i, g['kat_face_idx'])
+        assert np.array_equal(t, g['kat_dist_type'])
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_p2m_random(golden, dname):
+    """metrics/test_trianglemesh.py:81-152: allclose dist, exact idx/type, grads 1e-5."""
+    g = golden('p2m.npz')
+    p = f'rand_{dname}_'
+    d, i, t = orc.unbatched_triangle_distance_forward(g[p + 'points'], g[p + 'face_vertices'])
+    np.testing.assert_allclose(d, g[p + 'dist'], rtol=1e-5, atol=1e-8)
+    assert np.array_equal(i, g[p + 'face_idx'])
+    assert np.array_equal(t, g[p + 'dist_type'])
+    gp, gf = orc.unbatched_triangle_distance_backward(g[p + 'grad_out'], g[p + 'points'],
+                                                      g[p + 'face_vertices'], i, t)
+    np.testing.assert_allclose(gp, g[p + 'grad_points'], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(gf, g[p + 'grad_face_vertices'], rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------- sided_distance
+def test_sided_kat(golden):
+    """metrics/test_pointcloud.py:97-104 (float tol 1e-5 / 1e-4)."""
+    g = golden('sided.npz')
+    for dt in (np.float32, np.float64):
+        d, i = orc.sided_distance_forward(g['kat_p1'].astype(dt), g['kat_p2'].astype(dt))
+        np.testing.assert_allclose(d, g['kat_dist'], atol=1e-5 if dt == np.float32 else 1e-4, rtol=1e-4)
+        assert np.array_equal(i, g['kat_idx'])
+
+
+def test_sided_large_and_random(golden):
+    """metrics/test_pointcloud.py:106-113 (integer points: exact ties, lowest index)."""
+    g = golden('sided.npz')
+    d, i = orc.sided_distance_forward(g['large_p1'], g['large_p2'])
+    np.testing.assert_allclose(d, g['large_dist'], atol=1e-6, rtol=1e-5)
+    full = ((g['large_p1'][:, :, None] - g['large_p2'][:, None]) ** 2).sum(-1)
+    assert np.array_equal(i, np.argmin(full, -1))  # numpy argmin = first minimum
+    d, i = orc.sided_distance_forward(g['rand_p1'], g['rand_p2'])
+    np.testing.assert_allclose(d, g['rand_dist'], atol=1e-5, rtol=1e-4)
+
+
+def test_sided_backward_matches_autograd(golden):
+    g = golden('sided.npz')
+    p1 = torch.from_numpy(g['rand_p1']).double().requires_grad_(True)
+    p2 = torch.from_numpy(g['rand_p2']).double().requires_grad_(True)
+    d, i = orc.sided_distance_forward(p1.detach().numpy(), p2.detach().numpy())
+    gr = np.random.default_rng(0).random(d.shape)
+    sel = torch.gather(p2, 1, torch.from_numpy(i)[..., None].expand(-1, -1, 3))
+    dd = ((p1 - sel) ** 2).sum(-1)
+    dd.backward(torch.from_numpy(gr))
+    g1, g2 = orc.sided_distance_backward(gr, p1.detach().numpy(), p2.detach().numpy(), i)
+    np.testing.assert_allclose(g1, p1.grad.numpy(), rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(g2, p2.grad.numpy(), rtol=1e-10, atol=1e-10)
+
+
+# ------------------------------------------------------------ voxelgrid
+@pytest.mark.parametrize('name', ['batched', 'origins', 'scale', 'res7', 'default_os', 'sphere32', 'random24'])
+def test_voxelgrid(golden, name):
+    """ops/conversions/test_trianglemesh.py:45-242 + reference-run sphere / random meshes: exact."""
+    g = golden('voxelgrid.npz')
+    o = g[f'{name}_origin'] if f'{name}_origin' in g else None
+    s = g[f'{name}_scale'] if f'{name}_scale' in g else None
+    grid = orc.voxelgrid(g[f'{name}_vertices'], g[f'{name}_faces'], int(g[f'{name}_resolution']), o, s)
+    occ = np.argwhere(grid).astype(np.int32)
+    assert np.array_equal(occ, g[f'{name}_occupied'])
+
+
+# ------------------------------------------------------------------ SPC
+def test_mesh_to_spc_kat(golden):
+    """ops/conversions/test_trianglemesh.py:244-369 (bary atol/rtol 1e-3)."""
+    g = golden('spc.npz')
+    octree, fidx, bary = orc.mesh_to_spc(g['m2s_face_vertices'], int(g['m2s_level']))
+    assert np.array_equal(octree, g['m2s_octree'])
+    assert np.array_equal(fidx, g['m2s_face_idx'])
+    np.testing.assert_allclose(bary, g['m2s_bary'], atol=1e-3, rtol=1e-3)
+
+
+def test_mesh_to_spc_empty():
+    fv = np.array([[[5., 5., 5.], [6., 5., 5.], [5., 6., 5.]]], np.float32)
+    octree, fidx, bary = orc.mesh_to_spc(fv, 3)
+    assert octree.shape == (0,) and fidx.shape == (0,) and bary.shape == (0, 3)
+
+
+def test_scan_generate_kat(golden):
+    """ops/spc/test_spc.py:51-80."""
+    g = golden('spc.npz')
+    level, pyr, ex = orc.scan_octrees(g['scan_octrees'], g['scan_lengths'])
+    assert level == int(g['scan_max_level'])
+    assert np.array_equal(pyr, g['scan_pyramids'])
+    assert np.array_equal(ex, g['scan_exsum'])
+    pts = orc.generate_points(g['scan_octrees'], pyr, ex)
+    assert np.array_equal(pts, g['scan_points'])
+
+
+@pytest.mark.parametrize('name', ['positive', 'negative', 'none', 'coarser', 'depth', 'depth_exit',
+                                  'inside_nodepth', 'inside_depth', 'inside_exit'])
+def test_raytrace_kat(golden, name):
+    """render/spc/test_raytrace.py:64-268."""
+    g = golden('spc.npz')
+    octree = g['rt_octree']
+    level, pyr, ex = orc.scan_octrees(octree, np.array([len(octree)], np.int32))
+    pts = orc.generate_points(octree, pyr, ex)
+    lv, rd, we = (int(x) for x in g[f'rt_{name}_cfg'])
+    out = orc.raytrace(octree, pts, pyr[0], ex, g[f'rt_{name}_origin'], g[f'rt_{name}_direction'], lv, rd, we)
+    assert np.array_equal(out[0], g[f'rt_{name}_nuggets'])
+    if rd:
+        if name.startswith('inside'):
+            np.testing.assert_allclose(out[1], g[f'rt_{name}_depth'], rtol=1e-5, atol=1e-6)
+        else:
+            assert np.array_equal(out[1], g[f'rt_{name}_depth'])
+
+
+def test_raytrace_ambiguous(golden):
+    """render/spc/test_raytrace.py:270-300 (rays exactly between voxels hit all neighbours)."""
+    g = golden('spc.npz')
+    octree = g['rt_ambiguous_octree']
+    level, pyr, ex = orc.scan_octrees(octree, np.array([1], np.int32))
+    pts = orc.generate_points(octree, pyr, ex)
+    nug, dep = orc.raytrace(octree, pts, pyr[0], ex, g['rt_ambiguous_origin'], g['rt_ambiguous_direction'], 1, True)
+    assert np.array_equal(nug, g['rt_ambiguous_nuggets'])
+
+
+def test_voxel_order_matches_front_to_back_rule():
+    import ctypes
+    order = (ctypes.c_uint8 * 64)()
+    orc.lib().or_voxel_order(order)
+    o = np.array(order).reshape(8, 8)
+    assert list(o[0]) == [0, 1, 2, 4, 3, 5, 6, 7]
+    assert list(o[5]) == [5, 1, 4, 7, 0, 3, 6, 2]
+    assert list(o[7]) == [7, 3, 5, 6, 1, 2, 4, 0]
