@@ -1,0 +1,192 @@
+/* kaolin_hip.h -- C ABI of the MI355X (gfx950) hot-path library libkaolin_hip.so.
+ *
+ * Plain pointers + sizes, no torch types.  Every pointer argument is DEVICE memory
+ * unless the name ends in `_host`.  `stream` is a hipStream_t (NULL = legacy default
+ * stream).  All functions return 0 on success or a negative KL_E* code; the message
+ * of the last failure on the calling thread is returned by kl_last_error().
+ * Nothing in the library exits the process (the reference's CubDebugExit did,
+ * mesh_to_spc_cuda.cu:22,50,347).
+ *
+ * Each entry point replaces one reference `kaolin._C` binding (bindings.cpp:37-99);
+ * the reference dispatcher it stands in for is cited above the declaration.  Output
+ * buffers are caller-allocated (the reference allocated them in C++ with at::zeros /
+ * at::full; here the kernels write every element, so callers may pass
+ * uninitialised memory).  Data-dependent outputs (mesh_to_spc, raytrace, voxel
+ * subdivision) are allocated through a caller-supplied allocator callback so that
+ * device memory comes from the caller's caching allocator.
+ */
+#ifndef KAOLIN_HIP_H_
+#define KAOLIN_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  KL_F32 = 0,
+  KL_F64 = 1,
+  KL_F16 = 2,
+  KL_U8 = 3,
+  KL_I8 = 4,
+  KL_I16 = 5,
+  KL_I32 = 6,
+  KL_I64 = 7
+} kl_dtype;
+
+enum {
+  KL_OK = 0,
+  KL_E_INVALID = -1,   /* bad argument / unsupported dtype */
+  KL_E_HIP = -2,       /* HIP runtime error */
+  KL_E_ALLOC = -3      /* allocator callback returned NULL */
+};
+
+typedef void *kl_stream;
+/* Device allocator: returns `bytes` of device memory that stays valid until the
+ * caller releases `ctx`'s allocations (after the call returns). */
+typedef void *(*kl_alloc_fn)(void *ctx, size_t bytes);
+
+const char *kl_last_error(void);
+int kl_abi_version(void);
+
+/* ---------------------------------------------------------------- DIB-R */
+
+/* Workspace for the screen-space face bins of packed_rasterize_forward.
+ * max_faces_per_mesh: upper bound on (first_idx[b+1] - first_idx[b]). */
+size_t kl_rasterize_workspace_bytes(int batch, int height, int width, int64_t max_faces_per_mesh);
+
+/* rasterization.cpp:49-104  packed_rasterize_forward_cuda.
+ * face_vertices_z (Nv,3), face_vertices_image (Nv,3,2) (x multiplier), face_bboxes (Nv,4),
+ * face_features (Nv,3,D), first_idx (B+1) int64 on device.
+ * Outputs: interpolated_features (B,H,W,D), selected_face_idx (B,H,W) int64 (per-mesh
+ * packed index, -1 = none), output_weights (B,H,W,3).  dtype: KL_F32 | KL_F64. */
+int kl_packed_rasterize_forward(kl_dtype dtype, int height, int width, int batch, int64_t num_faces,
+                                int feat_dim, int64_t max_faces_per_mesh,
+                                const void *face_vertices_z, const void *face_vertices_image,
+                                const void *face_bboxes, const void *face_features,
+                                const int64_t *first_idx, float multiplier, float eps,
+                                void *interpolated_features, int64_t *selected_face_idx,
+                                void *output_weights, void *workspace, size_t workspace_bytes,
+                                kl_stream stream);
+
+/* rasterization.cpp:106-168  rasterize_backward_cuda.
+ * face_idx: (B,H,W) ORIGINAL face index per mesh; face_vertices_image (B,F,3,2) unscaled.
+ * Outputs (fully written): grad_face_vertices_image (B,F,3,2), grad_face_features (B,F,3,D). */
+int kl_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
+                          const void *grad_interpolated_features, const int64_t *face_idx,
+                          const void *output_weights, const void *face_vertices_image,
+                          const void *face_features, float eps,
+                          void *grad_face_vertices_image, void *grad_face_features,
+                          kl_stream stream);
+
+size_t kl_soft_mask_workspace_bytes(int batch, int height, int width, int num_faces);
+
+/* dibr_soft_mask.cpp:48-108  dibr_soft_mask_forward_cuda.
+ * face_vertices_image (B,F,3,2) and face_large_bboxes (B,F,4) already x multiplier.
+ * Outputs (fully written): soft_mask (B,H,W), close_face_prob (B,H,W,K),
+ * close_face_idx (B,H,W,K) int64 (-1 pad), close_face_dist_type (B,H,W,K) uint8 (0 pad). */
+int kl_dibr_soft_mask_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
+                              const void *face_vertices_image, const void *face_large_bboxes,
+                              const int64_t *selected_face_idx, float sigmainv, float multiplier,
+                              void *soft_mask, void *close_face_prob, int64_t *close_face_idx,
+                              uint8_t *close_face_dist_type, void *workspace, size_t workspace_bytes,
+                              kl_stream stream);
+
+/* dibr_soft_mask.cpp:110-183  dibr_soft_mask_backward_cuda.
+ * Output grad_face_vertices_image (B,F,3,2) (fully written). */
+int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
+                               const void *grad_soft_mask, const void *soft_mask,
+                               const int64_t *selected_face_idx, const void *close_face_prob,
+                               const int64_t *close_face_idx, const uint8_t *close_face_dist_type,
+                               const void *face_vertices_image, float sigmainv, float multiplier,
+                               void *grad_face_vertices_image, kl_stream stream);
+
+/* ------------------------------------------------------------ distances */
+
+/* unbatched_triangle_distance.cpp:43-72.  points (P,3), face_vertices (F,3,3).
+ * Outputs dist (P), face_idx (P) int64, dist_type (P) int32. dtype KL_F32 | KL_F64. */
+int kl_unbatched_triangle_distance_forward(kl_dtype dtype, int64_t num_points, int64_t num_faces,
+                                           const void *points, const void *face_vertices,
+                                           void *dist, int64_t *face_idx, int32_t *dist_type,
+                                           kl_stream stream);
+
+/* unbatched_triangle_distance.cpp:74-114.  grad_points (P,3) fully written;
+ * grad_face_vertices (F,3,3) fully written (zero where no point selected the face). */
+int kl_unbatched_triangle_distance_backward(kl_dtype dtype, int64_t num_points, int64_t num_faces,
+                                            const void *grad_dist, const void *points,
+                                            const void *face_vertices, const int64_t *face_idx,
+                                            const int32_t *dist_type, void *grad_points,
+                                            void *grad_face_vertices, kl_stream stream);
+
+/* sided_distance.cpp:65-89.  p1 (B,N,3), p2 (B,M,3) -> dist (B,N), idx (B,N) int64.
+ * dtype: any kl_dtype (half/float/double and the integer types of DISPATCH_NUM_TYPES). */
+int kl_sided_distance_forward(kl_dtype dtype, int batch, int64_t n, int64_t m,
+                              const void *p1, const void *p2, void *dist, int64_t *idx,
+                              kl_stream stream);
+
+/* sided_distance.cpp:91-122.  grad_p1 (B,N,3), grad_p2 (B,M,3) fully written. */
+int kl_sided_distance_backward(kl_dtype dtype, int batch, int64_t n, int64_t m,
+                               const void *grad_dist, const void *p1, const void *p2,
+                               const int64_t *idx, void *grad_p1, void *grad_p2, kl_stream stream);
+
+/* ------------------------------------------------------------------ SPC */
+
+/* mesh_to_spc.cpp:28-44 (mesh_to_spc_cuda_impl, mesh_to_spc_cuda.cu:309-463).
+ * face_vertices (F,3,3) float32.  Outputs allocated through `alloc`:
+ * *octree (num_nodes) u8, *face_idx (num_leaves) int64, *bary (num_leaves,2) f32.
+ * Sizes returned in *num_nodes / *num_leaves (0 / 0 for an empty result). */
+int kl_mesh_to_spc(int64_t num_faces, const float *face_vertices, uint32_t level,
+                   kl_alloc_fn alloc, void *alloc_ctx,
+                   uint8_t **octree, int64_t *num_nodes, int64_t **face_idx, float **bary,
+                   int64_t *num_leaves, kl_stream stream);
+
+/* spc.cpp:55-65 morton_to_octree: sorted unique leaf morton codes -> octree bytes. */
+int kl_morton_to_octree(int64_t num_points, const uint64_t *morton, uint32_t level,
+                        kl_alloc_fn alloc, void *alloc_ctx, uint8_t **octree, int64_t *num_nodes,
+                        kl_stream stream);
+
+/* spc.cpp:79-107 scan_octrees_cuda.  lengths_host (B) int32 on the host.
+ * exsum (sum(lengths) + B) int32 device output; pyramid_host (B,2,17) int32 host output
+ * (zero-filled by the callee); returns the level through *level. */
+int kl_scan_octrees(int batch, const uint8_t *octrees, const int32_t *lengths_host,
+                    int32_t *exsum, int32_t *pyramid_host, int *level, kl_stream stream);
+
+/* spc.cpp:109-134 generate_points_cuda.  pyramids_host (B,2,L+2) int32 host.
+ * points: (sum_b pyramids[b,1,L+1], 3) int16 device output. */
+int kl_generate_points(int batch, int max_level, const uint8_t *octrees, const int32_t *pyramids_host,
+                       const int32_t *exsum, int16_t *points, kl_stream stream);
+
+/* raytrace.cpp:170-214 raytrace_cuda (raytrace_cuda.cu:485-607).
+ * Outputs allocated through `alloc`: *nuggets (N,2) int32, *depth (N, with_exit?2:1) f32. */
+int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int16_t *points, int64_t num_points,
+                const int32_t *exsum, int max_level, const float *ray_o, const float *ray_d,
+                int64_t num_rays, uint32_t target_level, int return_depth, int with_exit,
+                kl_alloc_fn alloc, void *alloc_ctx, int32_t **nuggets, float **depth,
+                int64_t *num_hits, kl_stream stream);
+
+/* raytrace.cpp:216-240 mark_pack_boundaries_cuda: boundaries (N) int32 (1 at pack starts). */
+int kl_mark_pack_boundaries(kl_dtype dtype, int64_t num, const void *pack_ids, int32_t *boundaries,
+                            kl_stream stream);
+
+/* ------------------------------------------------------------ voxelgrid */
+
+/* trianglemeshes_to_voxelgrids (ops/conversions/trianglemesh.py:29-110) for ONE batch
+ * element, float32.  points (V,3) are the already normalised vertices
+ * ((v - origin) / scale); faces (F,3) int64.  Writes occupancy into grid (R,R,R) of
+ * `grid_dtype` (KL_F32 | KL_F64 | KL_F16 | KL_U8); the grid must be zeroed by the caller. */
+int kl_voxelgrid_mark(int64_t num_vertices, const float *points, int64_t num_faces, const int64_t *faces,
+                      int resolution, kl_dtype grid_dtype, void *grid, kl_alloc_fn alloc, void *alloc_ctx,
+                      kl_stream stream);
+
+/* Same for float64 vertices (the reference subdivides in the vertex dtype). */
+int kl_voxelgrid_mark_f64(int64_t num_vertices, const double *points, int64_t num_faces, const int64_t *faces,
+                          int resolution, kl_dtype grid_dtype, void *grid, kl_alloc_fn alloc, void *alloc_ctx,
+                          kl_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KAOLIN_HIP_H_ */

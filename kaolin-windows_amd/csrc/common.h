@@ -1,0 +1,104 @@
+// common.h -- shared helpers for the gfx950 kernels of libkaolin_hip.so.
+// Compiled with -ffp-contract=off: every multiply-add is rounded twice, exactly as
+// written, so results match the CPU oracle bit for bit (explicit fmaf() only where
+// the reference wrote fmaf()).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <string>
+
+#include "../../include/kaolin_hip.h"
+
+namespace kl {
+
+void set_error(const std::string &msg);
+
+#define KL_CHECK_HIP(expr)                                                              \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      ::kl::set_error(std::string(#expr) + ": " + hipGetErrorString(_e));               \
+      return KL_E_HIP;                                                                  \
+    }                                                                                   \
+  } while (0)
+
+#define KL_CHECK_LAUNCH() KL_CHECK_HIP(hipGetLastError())
+
+#define KL_REQUIRE(cond, msg)                                                           \
+  do {                                                                                  \
+    if (!(cond)) {                                                                      \
+      ::kl::set_error(msg);                                                             \
+      return KL_E_INVALID;                                                              \
+    }                                                                                   \
+  } while (0)
+
+inline hipStream_t S(kl_stream s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+constexpr int WAVE = 64;
+
+// Pixel centres (rasterization_cuda.cu:85-86, dibr_soft_mask_cuda.cu:74-75):
+// `multiplier / width * (2 * wididx + 1 - width)` is evaluated in float.
+template <typename T>
+__device__ __forceinline__ T pix_x(float m, int W, int i) {
+  return (T)((m / (float)W) * (float)(2 * i + 1 - W));
+}
+template <typename T>
+__device__ __forceinline__ T pix_y(float m, int H, int j) {
+  return (T)((m / (float)H) * (float)(H - 2 * j - 1));
+}
+
+// wave64 helpers
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T u = __shfl_xor(v, o);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    T u = __shfl_xor(v, o);
+    v = u > v ? u : v;
+  }
+  return v;
+}
+
+// Broadcast lane `src` (wave-uniform) of v to all lanes through the scalar unit.
+__device__ __forceinline__ float bcast(float v, int src) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
+}
+__device__ __forceinline__ int bcast(int v, int src) { return __builtin_amdgcn_readlane(v, src); }
+__device__ __forceinline__ double bcast(double v, int src) {
+  int64_t b = __double_as_longlong(v);
+  int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), src);
+  int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+  return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
+}
+
+template <typename T>
+__device__ __forceinline__ T kl_exp(T x);
+template <>
+__device__ __forceinline__ float kl_exp<float>(float x) { return expf(x); }
+template <>
+__device__ __forceinline__ double kl_exp<double>(double x) { return exp(x); }
+
+template <typename T>
+__device__ __forceinline__ T kl_sqrt(T x);
+template <>
+__device__ __forceinline__ float kl_sqrt<float>(float x) { return sqrtf(x); }
+template <>
+__device__ __forceinline__ double kl_sqrt<double>(double x) { return sqrt(x); }
+
+}  // namespace kl

@@ -1,0 +1,424 @@
+// distance.hip -- point->triangle distance and point-cloud sided distance for gfx950.
+//
+// point_to_mesh (unbatched_triangle_distance_cuda.cu:237-317): brute force over faces,
+// one point per lane.  Faces are staged through LDS in tiles; per face the quantities
+// that do not depend on the point (edges, normal, squared edge lengths, unit normal,
+// edge normals) are computed ONCE while staging -- with exactly the reference's
+// expressions, so every per-pair value is bit-identical to the oracle -- and the
+// per-pair classification (types 1..6, 0) is evaluated branch-free with selects
+// (no wave divergence across the seven cases).  The reference's 512-face tile
+// argmin semantics (first face of a tile taken unconditionally, strict '>' inside a
+// tile, strict '>' across tiles) are kept independently of the LDS tile size.
+//
+// sided_distance (sided_distance_cuda.cu:52-201): one p1 point per lane, p2 staged in
+// LDS, 512-point argmin tiles as in the reference; the grid covers (batch, points)
+// instead of the reference's fixed 32x16 grid.
+#include "common.h"
+
+#include <hip/hip_fp16.h>
+
+#include <type_traits>
+
+namespace kl {
+
+template <typename T>
+struct V3 {
+  T x, y, z;
+};
+template <typename T>
+__device__ __forceinline__ V3<T> mk(T x, T y, T z) { return V3<T>{x, y, z}; }
+template <typename T>
+__device__ __forceinline__ V3<T> operator-(V3<T> a, V3<T> b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+template <typename T>
+__device__ __forceinline__ V3<T> operator+(V3<T> a, V3<T> b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+template <typename T>
+__device__ __forceinline__ V3<T> operator*(V3<T> a, T s) { return mk(a.x * s, a.y * s, a.z * s); }
+template <typename T>
+__device__ __forceinline__ V3<T> operator/(V3<T> a, T s) { return mk(a.x / s, a.y / s, a.z / s); }
+template <typename T>
+__device__ __forceinline__ T dot(V3<T> a, V3<T> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+template <typename T>
+__device__ __forceinline__ V3<T> cross(V3<T> a, V3<T> b) {
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+template <typename T>
+__device__ __forceinline__ V3<T> sel3(bool c, V3<T> a, V3<T> b) {
+  return mk(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z);
+}
+
+// Per-face precomputed record (all point-independent subexpressions of the reference).
+template <typename T>
+struct FaceRec {
+  V3<T> v1, v2, v3, e12, e23, e31, un, en12, en23, en31;
+  T l12, l23, l31;
+};
+
+template <typename T>
+__device__ __forceinline__ void make_face(const T *v, FaceRec<T> &r) {
+  r.v1 = mk(v[0], v[1], v[2]);
+  r.v2 = mk(v[3], v[4], v[5]);
+  r.v3 = mk(v[6], v[7], v[8]);
+  r.e12 = r.v2 - r.v1;
+  r.e23 = r.v3 - r.v2;
+  r.e31 = r.v1 - r.v3;
+  const V3<T> normal = cross(r.v1 - r.v2, r.e31);
+  r.l12 = dot(r.e12, r.e12);
+  r.l23 = dot(r.e23, r.e23);
+  r.l31 = dot(r.e31, r.e31);
+  const T inv_len = (T)1 / kl_sqrt<T>(dot(normal, normal));
+  r.un = normal * inv_len;
+  r.en12 = cross(normal, r.e12);
+  r.en23 = cross(normal, r.e23);
+  r.en31 = cross(normal, r.e31);
+}
+
+// squared distance (as float, :302) + type of one point to one face
+template <typename T>
+__device__ __forceinline__ float point_face(const V3<T> &p, const FaceRec<T> &f, int &type) {
+  const V3<T> pv1 = p - f.v1, pv2 = p - f.v2, pv3 = p - f.v3;
+  const T uab = dot(pv1, f.e12) / f.l12;
+  const T uca = dot(pv3, f.e31) / f.l31;
+  const T ubc = dot(pv2, f.e23) / f.l23;
+  const bool t1 = uca > (T)1 && uab < (T)0;
+  const bool t2 = !t1 && uab > (T)1 && ubc < (T)0;
+  const bool t3 = !t1 && !t2 && ubc > (T)1 && uca < (T)0;
+  const bool rest = !t1 && !t2 && !t3;
+  const bool t4 = rest && (uab <= (T)1 && uab >= (T)0) && dot(f.en12, pv1) <= (T)0;
+  const bool t5 = rest && !t4 && (ubc <= (T)1 && ubc >= (T)0) && dot(f.en23, pv2) <= (T)0;
+  const bool t6 = rest && !t4 && !t5 && (uca <= (T)1 && uca >= (T)0) && dot(f.en31, pv3) <= (T)0;
+  // point_at(vertex, edge, float t) -- the reference passes the parameter as float
+  const T tp = t4 ? (T)(float)uab : (t5 ? (T)(float)ubc : (T)(float)uca);
+  const V3<T> ev = t4 ? f.e12 : (t5 ? f.e23 : f.e31);
+  const V3<T> vv = t4 ? f.v1 : (t5 ? f.v2 : f.v3);
+  const V3<T> cp_edge = vv + ev * tp;
+  const T dist = (p.x - f.v1.x) * f.un.x + (p.y - f.v1.y) * f.un.y + (p.z - f.v1.z) * f.un.z;
+  const V3<T> cp_plane = p - f.un * dist;
+  V3<T> cp = sel3(t4 || t5 || t6, cp_edge, cp_plane);
+  cp = sel3(t3, f.v3, cp);
+  cp = sel3(t2, f.v2, cp);
+  cp = sel3(t1, f.v1, cp);
+  type = t1 ? 1 : t2 ? 2 : t3 ? 3 : t4 ? 4 : t5 ? 5 : t6 ? 6 : 0;
+  const V3<T> dv = p - cp;
+  return (float)dot(dv, dv);
+}
+
+constexpr int P2M_TILE = 256;  // faces per LDS tile (a divisor of the reference's 512)
+
+template <typename T>
+__global__ void __launch_bounds__(256) p2m_fwd_kernel(const T *__restrict__ pts, const T *__restrict__ fv,
+                                                       int64_t P, int64_t F, T *__restrict__ out_dist,
+                                                       int64_t *__restrict__ out_idx, int32_t *__restrict__ out_type) {
+  __shared__ FaceRec<T> sf[P2M_TILE];
+  const int64_t pi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool valid = pi < P;
+  V3<T> p = mk((T)0, (T)0, (T)0);
+  if (valid) p = mk(pts[pi * 3], pts[pi * 3 + 1], pts[pi * 3 + 2]);
+  T best = (T)INFINITY, tbest = (T)INFINITY;
+  int64_t best_f = 0, tbest_f = 0;
+  int best_t = 0, tbest_t = 0;
+  for (int64_t start = 0; start < F; start += P2M_TILE) {
+    const int n = (int)min((int64_t)P2M_TILE, F - start);
+    __syncthreads();
+    for (int s = threadIdx.x; s < n; s += blockDim.x) make_face<T>(fv + (start + s) * 9, sf[s]);
+    __syncthreads();
+    for (int s = 0; s < n; s++) {
+      const int64_t f = start + s;
+      int t;
+      const float d = point_face<T>(p, sf[s], t);
+      if ((f & 511) == 0) {  // a reference tile begins: merge the previous tile, restart
+        if (f > 0 && (f == 512 || best > tbest)) {
+          best = tbest; best_f = tbest_f; best_t = tbest_t;
+        }
+        tbest = (T)d; tbest_f = f; tbest_t = t;
+      } else if (tbest > (T)d) {
+        tbest = (T)d; tbest_f = f; tbest_t = t;
+      }
+    }
+  }
+  if (!valid) return;
+  if (F > 0 && (F <= 512 || best > tbest)) {
+    best = tbest; best_f = tbest_f; best_t = tbest_t;
+  }
+  out_dist[pi] = best;
+  out_idx[pi] = best_f;
+  out_type[pi] = best_t;
+}
+
+template <typename T>
+__device__ __forceinline__ void edge_bwd(V3<T> vab, V3<T> pb, T *ga, T *gb, T *gp, T grad) {
+  const T l = dot(vab, pb);
+  const T m = dot(vab, vab);
+  const T k = l / m;
+  const T j = (T)fmax(0.0, fmin(1.0, (double)k));
+  const V3<T> i = vab * j - pb;
+  const V3<T> i_bar = i * grad;
+  const T j_bar = dot(i_bar, vab);
+  const T dj_dk = (k > 0 && k < 1) ? (T)1 : (T)0;
+  const T k_bar = j_bar * dj_dk;
+  const T m_bar = k_bar * (-l / (m * m));
+  const T l_bar = k_bar * ((T)1 / m);
+  const V3<T> di_dpb = mk(-i_bar.x, -i_bar.y, -i_bar.z);
+  const V3<T> pb_bar = vab * l_bar + di_dpb;
+  const V3<T> dm_dvab = vab * (T)2.;
+  const V3<T> di_dvab = i_bar * j;
+  const V3<T> vab_bar = (dm_dvab * m_bar + pb * l_bar) + di_dvab;
+  const V3<T> vb_bar = mk(-vab_bar.x - pb_bar.x, -vab_bar.y - pb_bar.y, -vab_bar.z - pb_bar.z);
+  gp[0] = pb_bar.x; gp[1] = pb_bar.y; gp[2] = pb_bar.z;
+  atomicAdd(ga + 0, vab_bar.x); atomicAdd(ga + 1, vab_bar.y); atomicAdd(ga + 2, vab_bar.z);
+  atomicAdd(gb + 0, vb_bar.x); atomicAdd(gb + 1, vb_bar.y); atomicAdd(gb + 2, vb_bar.z);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) p2m_bwd_kernel(const T *__restrict__ grad_dist, const T *__restrict__ pts,
+                                                       const T *__restrict__ fv, const int64_t *__restrict__ fidx,
+                                                       const int32_t *__restrict__ ftype, int64_t P,
+                                                       T *__restrict__ gpts, T *__restrict__ gfv) {
+  const int64_t pi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (pi >= P) return;
+  const int type = ftype[pi];
+  const int64_t f = fidx[pi];
+  const V3<T> p = mk(pts[pi * 3], pts[pi * 3 + 1], pts[pi * 3 + 2]);
+  const T *v = fv + f * 9;
+  const V3<T> v1 = mk(v[0], v[1], v[2]), v2 = mk(v[3], v[4], v[5]), v3 = mk(v[6], v[7], v[8]);
+  const V3<T> e12 = v2 - v1, e23 = v3 - v2, e31 = v1 - v3;
+  const T go = (T)(2. * (double)grad_dist[pi]);
+  T *g = gfv + f * 9;
+  T *gp = gpts + pi * 3;
+  if (type == 0) {
+    const V3<T> pv = p - v1;
+    const V3<T> e21 = v1 - v2;
+    const V3<T> normal = cross(e21, e31);
+    const T len = kl_sqrt<T>(dot(normal, normal));
+    const V3<T> un = normal / len;
+    const T dist = dot(pv, un);
+    const V3<T> gdv = un * (dist * go);
+    const T gd = dot(un, gdv);
+    const V3<T> gpv = un * gd;
+    const V3<T> gun = gdv * dist + pv * gd;
+    const T glen = -dot(normal, gun) / (len * len);
+    const T gd2 = glen / ((T)2 * kl_sqrt<T>(dot(normal, normal)));
+    const V3<T> gn = gun / len + normal * (gd2 * (T)2.);
+    const V3<T> ge31 = cross(gn, e21);
+    const V3<T> ge21 = cross(e31, gn);
+    gp[0] = gpv.x; gp[1] = gpv.y; gp[2] = gpv.z;
+    const V3<T> tmp = (ge31 + ge21) - gpv;
+    atomicAdd(g + 0, tmp.x); atomicAdd(g + 1, tmp.y); atomicAdd(g + 2, tmp.z);
+    atomicAdd(g + 3, -ge21.x); atomicAdd(g + 4, -ge21.y); atomicAdd(g + 5, -ge21.z);
+    atomicAdd(g + 6, -ge31.x); atomicAdd(g + 7, -ge31.y); atomicAdd(g + 8, -ge31.z);
+  } else if (type >= 1 && type <= 3) {
+    const V3<T> vv = type == 1 ? v1 : (type == 2 ? v2 : v3);
+    const V3<T> gdv = (p - vv) * go;
+    T *gg = g + (type - 1) * 3;
+    atomicAdd(gg + 0, -gdv.x); atomicAdd(gg + 1, -gdv.y); atomicAdd(gg + 2, -gdv.z);
+    gp[0] = gdv.x; gp[1] = gdv.y; gp[2] = gdv.z;
+  } else if (type == 4) {
+    edge_bwd<T>(e12, p - v1, g + 3, g + 0, gp, go);
+  } else if (type == 5) {
+    edge_bwd<T>(e23, p - v2, g + 6, g + 3, gp, go);
+  } else {
+    edge_bwd<T>(e31, p - v3, g + 0, g + 6, gp, go);
+  }
+}
+
+// ---------------------------------------------------------------- sided distance
+// Arithmetic happens in the storage type itself (half in half, integers in their own
+// type), as the reference's scalar_t arithmetic does.
+constexpr int SD_TILE = 512;
+
+template <typename S>
+__global__ void __launch_bounds__(256) sided_fwd_kernel(const S *__restrict__ p1, const S *__restrict__ p2,
+                                                         int64_t N, int64_t M, S *__restrict__ dist,
+                                                         int64_t *__restrict__ idx) {
+  __shared__ S buf[SD_TILE * 3];
+  const int b = blockIdx.y;
+  const int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool valid = n < N;
+  const S *a = p1 + ((int64_t)b * N + (valid ? n : 0)) * 3;
+  const S x1 = a[0], y1 = a[1], z1 = a[2];
+  S best_all = S(0);
+  int64_t best_all_i = 0;
+  for (int64_t k2 = 0; k2 < M; k2 += SD_TILE) {
+    const int end_k = (int)min((int64_t)SD_TILE, M - k2);
+    __syncthreads();
+    for (int t = threadIdx.x; t < end_k * 3; t += blockDim.x) buf[t] = p2[((int64_t)b * M + k2) * 3 + t];
+    __syncthreads();
+    S best = S(0);
+    int64_t best_i = 0;
+    for (int k = 0; k < end_k; k++) {
+      const S dx = buf[k * 3 + 0] - x1;
+      const S dy = buf[k * 3 + 1] - y1;
+      const S dz = buf[k * 3 + 2] - z1;
+      const S d = dx * dx + dy * dy + dz * dz;
+      if (k == 0 || d < best) {
+        best = d;
+        best_i = k + k2;
+      }
+    }
+    if (k2 == 0 || best_all > best) {
+      best_all = best;
+      best_all_i = best_i;
+    }
+  }
+  if (!valid) return;
+  dist[(int64_t)b * N + n] = best_all;
+  idx[(int64_t)b * N + n] = best_all_i;
+}
+
+template <typename S>
+__device__ __forceinline__ void atomic_add_any(S *p, S v) { atomicAdd(p, v); }
+template <>
+__device__ __forceinline__ void atomic_add_any<__half>(__half *p, __half v) {
+  // emulate with a 32-bit CAS on the containing word
+  uintptr_t addr = reinterpret_cast<uintptr_t>(p);
+  unsigned int *w = reinterpret_cast<unsigned int *>(addr & ~(uintptr_t)3);
+  const bool hi = (addr & 2) != 0;
+  unsigned int old = *w, assumed;
+  do {
+    assumed = old;
+    unsigned short h = hi ? (unsigned short)(assumed >> 16) : (unsigned short)(assumed & 0xffff);
+    __half cur = __ushort_as_half(h);
+    unsigned short nh = __half_as_ushort(__hadd(cur, v));
+    unsigned int nw = hi ? ((assumed & 0xffffu) | ((unsigned int)nh << 16)) : ((assumed & 0xffff0000u) | nh);
+    old = atomicCAS(w, assumed, nw);
+  } while (old != assumed);
+}
+template <typename S>
+__device__ __forceinline__ void atomic_add_small_int(S *p, S v) {
+  uintptr_t addr = reinterpret_cast<uintptr_t>(p);
+  unsigned int *w = reinterpret_cast<unsigned int *>(addr & ~(uintptr_t)3);
+  const int sh = (int)(addr & 3) * 8;
+  const unsigned int msk = (sizeof(S) == 1 ? 0xffu : 0xffffu) << sh;
+  unsigned int old = *w, assumed;
+  do {
+    assumed = old;
+    S cur = (S)((assumed & msk) >> sh);
+    S nv = (S)(cur + v);
+    unsigned int nw = (assumed & ~msk) | (((unsigned int)(std::make_unsigned_t<S>)nv << sh) & msk);
+    old = atomicCAS(w, assumed, nw);
+  } while (old != assumed);
+}
+template <>
+__device__ __forceinline__ void atomic_add_any<uint8_t>(uint8_t *p, uint8_t v) { atomic_add_small_int(p, v); }
+template <>
+__device__ __forceinline__ void atomic_add_any<int8_t>(int8_t *p, int8_t v) { atomic_add_small_int(p, v); }
+template <>
+__device__ __forceinline__ void atomic_add_any<int16_t>(int16_t *p, int16_t v) { atomic_add_small_int(p, v); }
+template <>
+__device__ __forceinline__ void atomic_add_any<int64_t>(int64_t *p, int64_t v) {
+  atomicAdd(reinterpret_cast<unsigned long long *>(p), (unsigned long long)v);
+}
+
+template <typename S>
+__global__ void __launch_bounds__(256) sided_bwd_kernel(const S *__restrict__ grad, const S *__restrict__ p1,
+                                                         const S *__restrict__ p2, const int64_t *__restrict__ idx,
+                                                         int64_t N, int64_t M, S *__restrict__ g1, S *__restrict__ g2) {
+  const int b = blockIdx.y;
+  const int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int64_t mi = (int64_t)b * N + n;
+  const S x1 = p1[mi * 3], y1 = p1[mi * 3 + 1], z1 = p1[mi * 3 + 2];
+  const int64_t j = (idx[mi] + (int64_t)b * M) * 3;
+  const S x2 = p2[j], y2 = p2[j + 1], z2 = p2[j + 2];
+  const S g = grad[mi];
+  const S two = S(2);
+  g1[mi * 3 + 0] = two * (x1 - x2) * g;
+  g1[mi * 3 + 1] = two * (y1 - y2) * g;
+  g1[mi * 3 + 2] = two * (z1 - z2) * g;
+  atomic_add_any<S>(g2 + j + 0, two * (x2 - x1) * g);
+  atomic_add_any<S>(g2 + j + 1, two * (y2 - y1) * g);
+  atomic_add_any<S>(g2 + j + 2, two * (z2 - z1) * g);
+}
+
+template <typename T>
+static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *dist, int64_t *idx, int32_t *type,
+                   hipStream_t st) {
+  if (P == 0) return KL_OK;
+  KL_REQUIRE(F > 0, "unbatched_triangle_distance_forward: face_vertices must not be empty");
+  hipLaunchKernelGGL(p2m_fwd_kernel<T>, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, (const T *)pts,
+                     (const T *)fv, P, F, (T *)dist, idx, type);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+template <typename T>
+static int p2m_bwd(int64_t P, int64_t F, const void *grad, const void *pts, const void *fv, const int64_t *idx,
+                   const int32_t *type, void *gp, void *gf, hipStream_t st) {
+  KL_CHECK_HIP(hipMemsetAsync(gf, 0, sizeof(T) * (size_t)F * 9, st));
+  if (P == 0) return KL_OK;
+  hipLaunchKernelGGL(p2m_bwd_kernel<T>, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, (const T *)grad,
+                     (const T *)pts, (const T *)fv, idx, type, P, (T *)gp, (T *)gf);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+template <typename S>
+static int sided_fwd(int B, int64_t N, int64_t M, const void *p1, const void *p2, void *dist, int64_t *idx,
+                     hipStream_t st) {
+  if (B == 0 || N == 0) return KL_OK;
+  KL_REQUIRE(M > 0, "sided_distance_forward: p2 must not be empty");
+  hipLaunchKernelGGL(sided_fwd_kernel<S>, dim3((unsigned)cdiv(N, 256), B), dim3(256), 0, st, (const S *)p1,
+                     (const S *)p2, N, M, (S *)dist, idx);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+template <typename S>
+static int sided_bwd(int B, int64_t N, int64_t M, const void *grad, const void *p1, const void *p2,
+                     const int64_t *idx, void *g1, void *g2, hipStream_t st) {
+  KL_CHECK_HIP(hipMemsetAsync(g2, 0, sizeof(S) * (size_t)B * M * 3, st));
+  if (B == 0 || N == 0) return KL_OK;
+  hipLaunchKernelGGL(sided_bwd_kernel<S>, dim3((unsigned)cdiv(N, 256), B), dim3(256), 0, st, (const S *)grad,
+                     (const S *)p1, (const S *)p2, idx, N, M, (S *)g1, (S *)g2);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+#define KL_DISPATCH_NUM(dt, FN, ...)                                   \
+  switch (dt) {                                                        \
+    case KL_F32: return FN<float>(__VA_ARGS__);                        \
+    case KL_F64: return FN<double>(__VA_ARGS__);                       \
+    case KL_F16: return FN<__half>(__VA_ARGS__);                       \
+    case KL_U8: return FN<uint8_t>(__VA_ARGS__);                       \
+    case KL_I8: return FN<int8_t>(__VA_ARGS__);                        \
+    case KL_I16: return FN<int16_t>(__VA_ARGS__);                      \
+    case KL_I32: return FN<int32_t>(__VA_ARGS__);                      \
+    case KL_I64: return FN<int64_t>(__VA_ARGS__);                      \
+    default: break;                                                    \
+  }
+
+}  // namespace kl
+
+using namespace kl;
+
+extern "C" int kl_unbatched_triangle_distance_forward(kl_dtype dtype, int64_t P, int64_t F, const void *pts,
+                                                      const void *fv, void *dist, int64_t *idx, int32_t *type,
+                                                      kl_stream stream) {
+  if (dtype == KL_F32) return p2m_fwd<float>(P, F, pts, fv, dist, idx, type, S(stream));
+  if (dtype == KL_F64) return p2m_fwd<double>(P, F, pts, fv, dist, idx, type, S(stream));
+  set_error("unbatched_triangle_distance_forward_cuda not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_unbatched_triangle_distance_backward(kl_dtype dtype, int64_t P, int64_t F, const void *grad,
+                                                       const void *pts, const void *fv, const int64_t *idx,
+                                                       const int32_t *type, void *gp, void *gf, kl_stream stream) {
+  if (dtype == KL_F32) return p2m_bwd<float>(P, F, grad, pts, fv, idx, type, gp, gf, S(stream));
+  if (dtype == KL_F64) return p2m_bwd<double>(P, F, grad, pts, fv, idx, type, gp, gf, S(stream));
+  set_error("unbatched_triangle_distance_backward_cuda not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_sided_distance_forward(kl_dtype dtype, int batch, int64_t n, int64_t m, const void *p1,
+                                         const void *p2, void *dist, int64_t *idx, kl_stream stream) {
+  KL_DISPATCH_NUM(dtype, sided_fwd, batch, n, m, p1, p2, dist, idx, S(stream));
+  set_error("sided_distance_forward_cuda not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_sided_distance_backward(kl_dtype dtype, int batch, int64_t n, int64_t m, const void *grad,
+                                          const void *p1, const void *p2, const int64_t *idx, void *g1, void *g2,
+                                          kl_stream stream) {
+  KL_DISPATCH_NUM(dtype, sided_bwd, batch, n, m, grad, p1, p2, idx, g1, g2, S(stream));
+  set_error("sided_distance_backward_cuda not implemented for this dtype");
+  return KL_E_INVALID;
+}

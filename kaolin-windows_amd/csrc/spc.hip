@@ -1,0 +1,774 @@
+// spc.hip -- structured point cloud paths for gfx950: mesh -> SPC conversion,
+// morton -> octree, octree scan / point generation and the level-synchronous ray march.
+//
+// References:
+//   mesh_to_spc       kaolin/csrc/ops/conversions/mesh_to_spc/mesh_to_spc_cuda.cu:59-463
+//   morton_to_octree  kaolin/csrc/ops/spc/spc_cuda.cu:45-163
+//   scan_octrees      kaolin/csrc/ops/spc/scan_octrees.cu:43-114
+//   generate_points   kaolin/csrc/ops/spc/generate_points.cu:28-81 (+ spc_utils.cuh:140-160)
+//   raytrace          kaolin/csrc/render/spc/raytrace_cuda.cu:63-304,485-607
+//                     kaolin/csrc/render/spc/spc_render_utils.cuh:21-143
+//
+// Differences in structure (not in results):
+//   * every kernel runs on the caller's stream (the reference used the legacy default
+//     stream with synchronous cudaMemcpy);
+//   * per level the only host round-trip is ONE 4-byte count read (needed to size the
+//     next level's buffers through the caller's allocator); octree level sizes in
+//     morton_to_octree and the whole pyramid of scan_octrees are computed on device
+//     and read back once;
+//   * the child order of the ray march (VOXEL_ORDER) is derived, not tabulated:
+//     children sorted by (popcount(code ^ j), j).
+#include "common.h"
+
+#include <hipcub/hipcub.hpp>
+
+#include <vector>
+
+namespace kl {
+
+constexpr int SPC_MAX_LEVELS = 15;
+
+__host__ __device__ __forceinline__ uint64_t to_morton(int x, int y, int z) {
+  uint64_t m = 0;
+  const uint64_t X = (uint16_t)x, Y = (uint16_t)y, Z = (uint16_t)z;
+#pragma unroll
+  for (unsigned i = 0; i < SPC_MAX_LEVELS; i++) {
+    const unsigned i2 = i + i;
+    m |= (Z & (1ull << i)) << i2;
+    m |= (Y & (1ull << i)) << (i2 + 1);
+    m |= (X & (1ull << i)) << (i2 + 2);
+  }
+  return m;
+}
+
+__host__ __device__ __forceinline__ void to_point(uint64_t m, int16_t &px, int16_t &py, int16_t &pz) {
+  uint16_t x = 0, y = 0, z = 0;
+#pragma unroll
+  for (int i = 0; i < SPC_MAX_LEVELS; i++) {
+    x |= (uint16_t)((m & (1ull << (3 * i + 2))) >> (2 * i + 2));
+    y |= (uint16_t)((m & (1ull << (3 * i + 1))) >> (2 * i + 1));
+    z |= (uint16_t)((m & (1ull << (3 * i + 0))) >> (2 * i + 0));
+  }
+  px = (int16_t)x;
+  py = (int16_t)y;
+  pz = (int16_t)z;
+}
+
+// ------------------------------------------------------------------ scan helper
+// Exclusive scan of n uint32 into out (n+1 entries, out[n] = total); returns total on host.
+struct Scratch {
+  kl_alloc_fn alloc;
+  void *ctx;
+  void *get(size_t bytes) { return alloc(ctx, bytes > 0 ? bytes : 16); }
+};
+
+static int exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, Scratch &sc, hipStream_t st,
+                          uint32_t *total_host) {
+  size_t tb = 0;
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, (int)n + 1, st));
+  void *tmp = sc.get(tb);
+  if (!tmp) return KL_E_ALLOC;
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, (int)n + 1, st));
+  if (total_host) {
+    KL_CHECK_HIP(hipMemcpyAsync(total_host, out + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    KL_CHECK_HIP(hipStreamSynchronize(st));
+  }
+  return KL_OK;
+}
+
+// ------------------------------------------------------------------ mesh_to_spc
+struct D3 {
+  double x, y, z;
+};
+__device__ __forceinline__ D3 d3(double x, double y, double z) { return D3{x, y, z}; }
+__device__ __forceinline__ D3 dsub(D3 a, D3 b) { return d3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ double ddot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ D3 dcross(D3 a, D3 b) {
+  return d3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ D3 dnorm(D3 v) {
+  const double inv = 1.0 / sqrt(ddot(v, v));
+  return d3(inv * v.x, inv * v.y, inv * v.z);
+}
+
+// TriangleVoxelSAT (mesh_to_spc_cuda.cu:96-111): fp64 projections, float-cast compare
+__device__ __forceinline__ bool sat_axis(D3 v0, D3 v1, D3 v2, float h, D3 axis) {
+  const double d0 = ddot(v0, axis), d1 = ddot(v1, axis), d2 = ddot(v2, axis);
+  const double maxd = fmax(d0, fmax(d1, d2));
+  const double mind = fmin(d0, fmin(d1, d2));
+  const double r = (double)h * (fabs(axis.x) + fabs(axis.y) + fabs(axis.z));
+  const float fd = (float)fmax(-maxd, mind);
+  const float fr = (float)r;
+  return fd <= fr;
+}
+
+__device__ bool tri_voxel_test(const float *fa, const float *fb, const float *fc, float cx, float cy, float cz,
+                               float h) {
+  const D3 va = d3((double)(fa[0] - cx), (double)(fa[1] - cy), (double)(fa[2] - cz));
+  const D3 vb = d3((double)(fb[0] - cx), (double)(fb[1] - cy), (double)(fb[2] - cz));
+  const D3 vc = d3((double)(fc[0] - cx), (double)(fc[1] - cy), (double)(fc[2] - cz));
+  const D3 ab = dnorm(dsub(vb, va)), bc = dnorm(dsub(vc, vb)), ca = dnorm(dsub(va, vc));
+  if (!sat_axis(va, vb, vc, h, d3(0.0, -ab.z, ab.y))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(0.0, -bc.z, bc.y))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(0.0, -ca.z, ca.y))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(ab.z, 0.0, -ab.x))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(bc.z, 0.0, -bc.x))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(ca.z, 0.0, -ca.x))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(-ab.y, ab.x, 0.0))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(-bc.y, bc.x, 0.0))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(-ca.y, ca.x, 0.0))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(1, 0, 0))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(0, 1, 0))) return false;
+  if (!sat_axis(va, vb, vc, h, d3(0, 0, 1))) return false;
+  if (!sat_axis(va, vb, vc, h, dcross(ab, bc))) return false;
+  return true;
+}
+
+__device__ __forceinline__ void voxel_center(uint64_t m, uint32_t level, float &cx, float &cy, float &cz,
+                                             float &h) {
+  const float two_level = (float)(1u << level);
+  const float vs = 2.0f / two_level;
+  h = (float)(0.5 * vs);
+  int16_t px, py, pz;
+  to_point(m, px, py, pz);
+  cx = fmaf((float)px, vs, h - 1.0f);
+  cy = fmaf((float)py, vs, h - 1.0f);
+  cz = fmaf((float)pz, vs, h - 1.0f);
+}
+
+__global__ void m2s_decide_kernel(int64_t num, const float *__restrict__ fv, const uint64_t *__restrict__ morton,
+                                  const int64_t *__restrict__ tri, uint32_t *__restrict__ occ, uint32_t level,
+                                  uint32_t not_done) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t > num) return;
+  if (t == num) {
+    occ[t] = 0;
+    return;
+  }
+  float cx, cy, cz, h;
+  voxel_center(morton[t], level, cx, cy, cz, h);
+  const float *v = fv + tri[t] * 9;
+  occ[t] = tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h) ? (not_done ? 8u : 1u) : 0u;
+}
+
+__global__ void m2s_subdivide_kernel(int64_t num, const uint64_t *__restrict__ min_, const int64_t *__restrict__ tin,
+                                     uint64_t *__restrict__ mout, int64_t *__restrict__ tout,
+                                     const uint32_t *__restrict__ occ, const uint32_t *__restrict__ psum,
+                                     int subdivide) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= num || !occ[t]) return;
+  const int64_t tr = tin[t];
+  uint32_t o = psum[t];
+  if (!subdivide) {
+    mout[o] = min_[t];
+    tout[o] = tr;
+    return;
+  }
+  int16_t px, py, pz;
+  to_point(min_[t], px, py, pz);
+  for (uint32_t i = 0; i < 8; i++) {
+    mout[o] = to_morton(2 * px + (i >> 2), 2 * py + ((i >> 1) & 1), 2 * pz + (i & 1));
+    tout[o] = tr;
+    o++;
+  }
+}
+
+__global__ void mark_unique_kernel(int64_t num, const uint64_t *__restrict__ m, uint32_t *__restrict__ flag) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t > num) return;
+  flag[t] = (t == num) ? 0u : ((t == 0 || m[t - 1] != m[t]) ? 1u : 0u);
+}
+
+// float closest point (spc_math.h:229-258), used for the leaf barycentrics
+struct F3 {
+  float x, y, z;
+};
+__device__ __forceinline__ F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+__device__ __forceinline__ F3 fsub(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ F3 fadd(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ F3 fmul(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ float fdot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ F3 fcross(F3 a, F3 b) {
+  return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ float fpe(F3 v, F3 e, F3 p) {
+  const F3 pv = fsub(p, v);
+  const float len = fdot(e, e);
+  return fdot(pv, e) / len;
+}
+__device__ __forceinline__ bool fna(F3 v, F3 e, F3 n, F3 p) { return fdot(fcross(n, e), fsub(p, v)) <= 0; }
+
+__device__ F3 tri_closest(F3 v1, F3 v2, F3 v3, F3 p) {
+  const F3 e12 = fsub(v2, v1), e23 = fsub(v3, v2), e31 = fsub(v1, v3);
+  const F3 n = fcross(fsub(v1, v2), e31);
+  const float uab = fpe(v1, e12, p), uca = fpe(v3, e31, p);
+  if (uca > 1 && uab < 0) return v1;
+  const float ubc = fpe(v2, e23, p);
+  if (uab > 1 && ubc < 0) return v2;
+  if (ubc > 1 && uca < 0) return v3;
+  if (uab <= 1.f && uab >= 0.f && fna(v1, e12, n, p)) return fadd(v1, fmul(e12, uab));
+  if (ubc <= 1.f && ubc >= 0.f && fna(v2, e23, n, p)) return fadd(v2, fmul(e23, ubc));
+  if (uca <= 1.f && uca >= 0.f && fna(v3, e31, n, p)) return fadd(v3, fmul(e31, uca));
+  const float inv = 1.0f / sqrtf(fdot(n, n));
+  const F3 un = fmul(n, inv);
+  const float dist = (p.x - v1.x) * un.x + (p.y - v1.y) * un.y + (p.z - v1.z) * un.z;
+  return fsub(p, fmul(un, dist));
+}
+
+// compaction of the sorted (morton, face) pairs to unique leaves + barycentrics
+__global__ void m2s_leaves_kernel(int64_t num, const uint64_t *__restrict__ ms, const int64_t *__restrict__ ts,
+                                  const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
+                                  const float *__restrict__ fv, uint32_t level, uint64_t *__restrict__ mout,
+                                  int64_t *__restrict__ fout, float *__restrict__ bary) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= num || !flag[t]) return;
+  const uint32_t o = psum[t];
+  const uint64_t m = ms[t];
+  const int64_t f = ts[t];
+  mout[o] = m;
+  fout[o] = f;
+  float cx, cy, cz, h;
+  voxel_center(m, level, cx, cy, cz, h);
+  const float *v = fv + f * 9;
+  const F3 v1 = f3(v[0], v[1], v[2]), v2 = f3(v[3], v[4], v[5]), v3 = f3(v[6], v[7], v[8]);
+  const F3 cp = tri_closest(v1, v2, v3, f3(cx, cy, cz));
+  const F3 cr = fcross(fsub(v1, v2), fsub(v1, v3));
+  const float delta = fdot(cr, cr);
+  const F3 d1 = fsub(cp, v1), d2 = fsub(cp, v2), d3v = fsub(cp, v3);
+  F3 q = fcross(d2, d3v);
+  const float da = sqrtf(fdot(q, q));
+  q = fcross(d1, d3v);
+  const float db = sqrtf(fdot(q, q));
+  q = fcross(d1, d2);
+  const float dc = sqrtf(fdot(q, q));
+  const float rs = 1.0f / sqrtf(delta);
+  float bx = da * rs, by = db * rs, bz = dc * rs;
+  if (bx < 0.0f) bx = 0.f;
+  if (by < 0.0f) by = 0.f;
+  if (bz < 0.0f) bz = 0.f;
+  const float s = (float)(1. / (double)(bx + by + bz));
+  bary[o * 2 + 0] = bx * s;
+  bary[o * 2 + 1] = by * s;
+}
+
+// ------------------------------------------------------------------ morton -> octree
+__global__ void parent_flag_kernel(int64_t num, const uint64_t *__restrict__ m, uint32_t *__restrict__ flag) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t > num) return;
+  flag[t] = (t == num) ? 0u : ((t == 0 || (m[t - 1] >> 3) != (m[t] >> 3)) ? 1u : 0u);
+}
+
+__global__ void compact_nodes_kernel(int64_t num, const uint64_t *__restrict__ m, const uint32_t *__restrict__ flag,
+                                     const uint32_t *__restrict__ psum, uint64_t *__restrict__ parent,
+                                     uint8_t *__restrict__ bytes) {
+  int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= num || !flag[t]) return;
+  const uint32_t o = psum[t];
+  parent[o] = m[t] >> 3;
+  uint32_t code = 0;
+  do {
+    code |= 1u << (uint32_t)(m[t] & 7);
+    t++;
+  } while (t < num && !flag[t]);
+  bytes[o] = (uint8_t)code;
+}
+
+static int morton_to_octree_impl(int64_t n, const uint64_t *morton, uint32_t level, Scratch &sc, uint8_t **octree,
+                                 int64_t *num_nodes, hipStream_t st) {
+  std::vector<uint8_t *> lv(level, nullptr);
+  std::vector<int64_t> ln(level, 0);
+  const uint64_t *cur = morton;
+  int64_t prev = n;
+  for (uint32_t i = level; i > 0; i--) {
+    uint32_t *flag = (uint32_t *)sc.get((prev + 1) * sizeof(uint32_t));
+    uint32_t *psum = (uint32_t *)sc.get((prev + 2) * sizeof(uint32_t));
+    if (!flag || !psum) return KL_E_ALLOC;
+    const unsigned g = (unsigned)cdiv(prev + 1, 256);
+    hipLaunchKernelGGL(parent_flag_kernel, dim3(g), dim3(256), 0, st, prev, cur, flag);
+    KL_CHECK_LAUNCH();
+    uint32_t cnt = 0;
+    int rc = exclusive_scan(flag, psum, prev, sc, st, &cnt);
+    if (rc) return rc;
+    uint64_t *par = (uint64_t *)sc.get((size_t)cnt * sizeof(uint64_t));
+    uint8_t *bytes = (uint8_t *)sc.get(cnt);
+    if (!par || !bytes) return KL_E_ALLOC;
+    if (prev > 0) {
+      hipLaunchKernelGGL(compact_nodes_kernel, dim3((unsigned)cdiv(prev, 256)), dim3(256), 0, st, prev, cur, flag,
+                         psum, par, bytes);
+      KL_CHECK_LAUNCH();
+    }
+    lv[i - 1] = bytes;
+    ln[i - 1] = cnt;
+    cur = par;
+    prev = cnt;
+  }
+  int64_t total = 0;
+  for (uint32_t l = 0; l < level; l++) total += ln[l];
+  uint8_t *out = (uint8_t *)sc.get((size_t)total);
+  if (!out) return KL_E_ALLOC;
+  int64_t o = 0;
+  for (uint32_t l = 0; l < level; l++) {
+    if (ln[l]) KL_CHECK_HIP(hipMemcpyAsync(out + o, lv[l], ln[l], hipMemcpyDeviceToDevice, st));
+    o += ln[l];
+  }
+  *octree = out;
+  *num_nodes = total;
+  return KL_OK;
+}
+
+__global__ void iota_kernel(int64_t n, int64_t *__restrict__ t, uint64_t *__restrict__ m) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) {
+    t[i] = i;
+    m[i] = 0;
+  }
+}
+
+static int mesh_to_spc_impl(int64_t F, const float *fv, uint32_t L, Scratch &sc, uint8_t **octree,
+                            int64_t *num_nodes, int64_t **face_idx, float **bary, int64_t *num_leaves,
+                            hipStream_t st) {
+  *num_nodes = 0;
+  *num_leaves = 0;
+  *octree = nullptr;
+  *face_idx = nullptr;
+  *bary = nullptr;
+  int64_t cnt = F;
+  uint64_t *m0 = (uint64_t *)sc.get(cnt * sizeof(uint64_t));
+  int64_t *t0 = (int64_t *)sc.get(cnt * sizeof(int64_t));
+  if (!m0 || !t0) return KL_E_ALLOC;
+  if (cnt > 0) {
+    hipLaunchKernelGGL(iota_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, t0, m0);
+    KL_CHECK_LAUNCH();
+  }
+  for (uint32_t l = 0; l <= L; l++) {
+    uint32_t *occ = (uint32_t *)sc.get((cnt + 1) * sizeof(uint32_t));
+    uint32_t *psum = (uint32_t *)sc.get((cnt + 2) * sizeof(uint32_t));
+    if (!occ || !psum) return KL_E_ALLOC;
+    hipLaunchKernelGGL(m2s_decide_kernel, dim3((unsigned)cdiv(cnt + 1, 256)), dim3(256), 0, st, cnt, fv, m0, t0,
+                       occ, l, L - l);
+    KL_CHECK_LAUNCH();
+    uint32_t next = 0;
+    int rc = exclusive_scan(occ, psum, cnt, sc, st, &next);
+    if (rc) return rc;
+    if (next == 0) return KL_OK;  // empty: (0,) u8, (0,) i64, (0,3) f32 built by the caller
+    uint64_t *m1 = (uint64_t *)sc.get((size_t)next * sizeof(uint64_t));
+    int64_t *t1 = (int64_t *)sc.get((size_t)next * sizeof(int64_t));
+    if (!m1 || !t1) return KL_E_ALLOC;
+    hipLaunchKernelGGL(m2s_subdivide_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, m0, t0, m1, t1,
+                       occ, psum, l < L ? 1 : 0);
+    KL_CHECK_LAUNCH();
+    m0 = m1;
+    t0 = t1;
+    cnt = next;
+  }
+  // stable radix sort of (morton, face) on the 3L significant bits: keeps generation
+  // order (= ascending face id) among equal mortons, as CUB's SortPairs did.
+  uint64_t *ms = (uint64_t *)sc.get(cnt * sizeof(uint64_t));
+  int64_t *ts = (int64_t *)sc.get(cnt * sizeof(int64_t));
+  if (!ms || !ts) return KL_E_ALLOC;
+  size_t tb = 0;
+  const int end_bit = (int)(3 * L) > 0 ? (int)(3 * L) : 1;
+  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, m0, ms, t0, ts, (int)cnt, 0, end_bit, st));
+  void *tmp = sc.get(tb);
+  if (!tmp) return KL_E_ALLOC;
+  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, m0, ms, t0, ts, (int)cnt, 0, end_bit, st));
+  uint32_t *flag = (uint32_t *)sc.get((cnt + 1) * sizeof(uint32_t));
+  uint32_t *psum = (uint32_t *)sc.get((cnt + 2) * sizeof(uint32_t));
+  if (!flag || !psum) return KL_E_ALLOC;
+  hipLaunchKernelGGL(mark_unique_kernel, dim3((unsigned)cdiv(cnt + 1, 256)), dim3(256), 0, st, cnt, ms, flag);
+  KL_CHECK_LAUNCH();
+  uint32_t uniq = 0;
+  int rc = exclusive_scan(flag, psum, cnt, sc, st, &uniq);
+  if (rc) return rc;
+  uint64_t *mu = (uint64_t *)sc.get((size_t)uniq * sizeof(uint64_t));
+  int64_t *fu = (int64_t *)sc.get((size_t)uniq * sizeof(int64_t));
+  float *bu = (float *)sc.get((size_t)uniq * 2 * sizeof(float));
+  if (!mu || !fu || !bu) return KL_E_ALLOC;
+  hipLaunchKernelGGL(m2s_leaves_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, ms, ts, flag, psum, fv,
+                     L, mu, fu, bu);
+  KL_CHECK_LAUNCH();
+  rc = morton_to_octree_impl(uniq, mu, L, sc, octree, num_nodes, st);
+  if (rc) return rc;
+  *face_idx = fu;
+  *bary = bu;
+  *num_leaves = uniq;
+  return KL_OK;
+}
+
+// ------------------------------------------------------------------ scan_octrees
+__global__ void popc_kernel(int64_t n, const uint8_t *__restrict__ o, uint32_t *__restrict__ c) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t < n) c[t] = (uint32_t)__popc(o[t]);
+  if (t == n) c[t] = 0;
+}
+
+// pyramid walk of scan_octrees.cu:66-103 on device (one thread)
+__global__ void pyramid_kernel(const int32_t *__restrict__ ex, uint32_t osize, int32_t *__restrict__ pyr,
+                               int32_t *__restrict__ level_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int STR = SPC_MAX_LEVELS + 2;
+  for (int i = 0; i < 2 * STR; i++) pyr[i] = 0;
+  int32_t *Pmid = pyr, *PmidSum = pyr + STR;
+  uint32_t prevSum = 0, sum = 1;
+  Pmid[0] = 1;
+  PmidSum[0] = 0;
+  PmidSum[1] = 1;
+  int level = 0;
+  while (sum <= osize && level < SPC_MAX_LEVELS) {
+    const uint32_t currSum = (uint32_t)ex[prevSum + 1];
+    const uint32_t Lsize = currSum - prevSum;
+    prevSum = currSum;
+    Pmid[++level] = (int32_t)Lsize;
+    sum += Lsize;
+    PmidSum[level + 1] = (int32_t)sum;
+  }
+  *level_out = level;
+}
+
+// nodes_to_morton (spc_utils.cuh:140-160)
+__global__ void nodes_to_morton_kernel(const uint8_t *__restrict__ octree, const int32_t *__restrict__ incl,
+                                       const uint64_t *__restrict__ min_, uint64_t *__restrict__ mall, int n) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const uint8_t bits = octree[t];
+  const uint64_t code = min_[t];
+  int addr = incl[t];
+  for (int i = 7; i >= 0; i--)
+    if (bits & (1u << i)) mall[addr--] = 8 * code + (uint64_t)i;
+}
+
+__global__ void morton_to_points_kernel(const uint64_t *__restrict__ m, int16_t *__restrict__ p, int64_t n) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  int16_t x, y, z;
+  to_point(m[t], x, y, z);
+  p[t * 3 + 0] = x;
+  p[t * 3 + 1] = y;
+  p[t * 3 + 2] = z;
+}
+
+// ------------------------------------------------------------------ raytrace
+__device__ __forceinline__ float ray_aabb(const float o_q[3], const float d[3], const float inv[3],
+                                          const float sgn[3], const float org[3], float r) {
+  const float o0 = o_q[0] - org[0], o1 = o_q[1] - org[1], o2 = o_q[2] - org[2];
+  const float cmax = fmaxf(fmaxf(fabsf(o0), fabsf(o1)), fabsf(o2));
+  float winding = cmax < r ? -1.0f : 1.0f;
+  winding *= r;
+  if (winding < 0) return winding;
+  const float d0 = fmaf(winding, sgn[0], -o0) * inv[0];
+  const float d1 = fmaf(winding, sgn[1], -o1) * inv[1];
+  const float d2 = fmaf(winding, sgn[2], -o2) * inv[2];
+  const float ltxy = fmaf(d[1], d0, o1), ltxz = fmaf(d[2], d0, o2);
+  const float ltyx = fmaf(d[0], d1, o0), ltyz = fmaf(d[2], d1, o2);
+  const float ltzx = fmaf(d[0], d2, o0), ltzy = fmaf(d[1], d2, o1);
+  const bool t0 = (d0 >= 0.0f) && (fabsf(ltxy) <= r) && (fabsf(ltxz) <= r);
+  const bool t1 = (d1 >= 0.0f) && (fabsf(ltyx) <= r) && (fabsf(ltyz) <= r);
+  const bool t2 = (d2 >= 0.0f) && (fabsf(ltzx) <= r) && (fabsf(ltzy) <= r);
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+  if (t0) s0 = sgn[0];
+  else if (t1) s1 = sgn[1];
+  else if (t2) s2 = sgn[2];
+  float dd = 0.0f;
+  if (s0 != 0.0f) dd = d0;
+  else if (s1 != 0.0f) dd = d1;
+  else if (s2 != 0.0f) dd = d2;
+  if (dd != 0.0f) return dd;
+  return 0.0f;
+}
+
+struct RayIn {
+  const uint8_t *octree;
+  const int16_t *points;
+  const int32_t *exsum;
+  const float *ro, *rd;
+};
+
+// decide (raytrace_cuda.cu:63-222): info = children count / keep flag; depth at the target level
+__global__ void rt_decide_kernel(RayIn in, int64_t num, const int2 *__restrict__ nug, uint32_t *__restrict__ info,
+                                 float *__restrict__ depth, uint32_t level, int last, int with_depth, int with_exit) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t > num) return;
+  if (t == num) {
+    info[t] = 0;
+    return;
+  }
+  const int ridx = nug[t].x, pidx = nug[t].y;
+  const int16_t *p = in.points + (int64_t)pidx * 3;
+  const float o[3] = {in.ro[ridx * 3], in.ro[ridx * 3 + 1], in.ro[ridx * 3 + 2]};
+  const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
+  const float r = (float)(1.0 / (double)(float)(1u << level));
+  const float vc[3] = {fmaf(r, fmaf(2.0f, (float)p[0], 1.0f), -1.0f), fmaf(r, fmaf(2.0f, (float)p[1], 1.0f), -1.0f),
+                       fmaf(r, fmaf(2.0f, (float)p[2], 1.0f), -1.0f)};
+  const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
+  const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
+  if (last && with_depth) {
+    if (with_exit) {
+      const float xs[3] = {signbit(-d[0]) ? 1.0f : -1.0f, signbit(-d[1]) ? 1.0f : -1.0f,
+                           signbit(-d[2]) ? 1.0f : -1.0f};
+      const float en = ray_aabb(o, d, inv, sgn, vc, r);
+      const float ex = ray_aabb(o, d, inv, xs, vc, r);
+      depth[t * 2] = en;
+      depth[t * 2 + 1] = ex;
+      info[t] = (en > 0.0f && ex > 0.0f) ? 1u : 0u;
+    } else {
+      const float dv = ray_aabb(o, d, inv, sgn, vc, r);
+      depth[t] = dv;
+      info[t] = dv > 0.0f ? 1u : 0u;
+    }
+  } else {
+    const float dv = ray_aabb(o, d, inv, sgn, vc, r);
+    if (!last)
+      info[t] = dv != 0.0f ? (uint32_t)__popc(in.octree[pidx]) : 0u;
+    else
+      info[t] = dv > 0.0f ? 1u : 0u;
+  }
+}
+
+__global__ void rt_subdivide_kernel(RayIn in, int64_t num, const int2 *__restrict__ nin, int2 *__restrict__ nout,
+                                    const uint32_t *__restrict__ info, const uint32_t *__restrict__ psum,
+                                    uint32_t level) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= num || !info[t]) return;
+  const int ridx = nin[t].x, pidx = nin[t].y;
+  const int16_t *p = in.points + (int64_t)pidx * 3;
+  uint32_t base = psum[t];
+  const uint8_t ob = in.octree[pidx];
+  const uint32_t s = (uint32_t)in.exsum[pidx];
+  const float scale = (float)(1.0 / (double)(float)(1u << level));
+  const float *org = in.ro + (int64_t)ridx * 3;
+  const float x = (float)((double)(0.5f * org[0] + 0.5f) - (double)scale * ((double)(float)p[0] + 0.5));
+  const float y = (float)((double)(0.5f * org[1] + 0.5f) - (double)scale * ((double)(float)p[1] + 0.5));
+  const float z = (float)((double)(0.5f * org[2] + 0.5f) - (double)scale * ((double)(float)p[2] + 0.5));
+  uint32_t code = 0;
+  if (x > 0) code = 4;
+  if (y > 0) code += 2;
+  if (z > 0) code += 1;
+  // front-to-back: children by increasing Hamming distance to `code`, then index
+  for (int h = 0; h <= 3; h++)
+    for (uint32_t j = 0; j < 8; j++) {
+      if (__popc(code ^ j) != h || !(ob & (1u << j))) continue;
+      const uint32_t c = (uint32_t)__popc(ob & ((2u << j) - 1));
+      nout[base] = make_int2(ridx, (int)(s + c));
+      base++;
+    }
+}
+
+__global__ void rt_compact_kernel(int64_t num, const int2 *__restrict__ nin, const float *__restrict__ din,
+                                  int2 *__restrict__ nout, float *__restrict__ dout, int dd,
+                                  const uint32_t *__restrict__ info, const uint32_t *__restrict__ psum) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= num || !info[t]) return;
+  const uint32_t o = psum[t];
+  nout[o] = nin[t];
+  if (dout)
+    for (int k = 0; k < dd; k++) dout[(int64_t)o * dd + k] = din[t * dd + k];
+}
+
+__global__ void rt_init_kernel(int64_t n, int2 *__restrict__ nug) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t < n) nug[t] = make_int2((int)t, 0);
+}
+
+template <typename S>
+__global__ void pack_bounds_kernel(int64_t n, const S *__restrict__ ids, int32_t *__restrict__ out) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t < n) out[t] = (t == 0 || ids[t - 1] != ids[t]) ? 1 : 0;
+}
+
+}  // namespace kl
+
+using namespace kl;
+
+extern "C" int kl_mesh_to_spc(int64_t num_faces, const float *fv, uint32_t level, kl_alloc_fn alloc, void *ctx,
+                              uint8_t **octree, int64_t *num_nodes, int64_t **face_idx, float **bary,
+                              int64_t *num_leaves, kl_stream stream) {
+  KL_REQUIRE(level < (uint32_t)SPC_MAX_LEVELS, "mesh_to_spc: level must be < 15");
+  KL_REQUIRE(alloc != nullptr, "mesh_to_spc: allocator required");
+  Scratch sc{alloc, ctx};
+  return mesh_to_spc_impl(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves, S(stream));
+}
+
+extern "C" int kl_morton_to_octree(int64_t n, const uint64_t *morton, uint32_t level, kl_alloc_fn alloc, void *ctx,
+                                   uint8_t **octree, int64_t *num_nodes, kl_stream stream) {
+  KL_REQUIRE(alloc != nullptr, "morton_to_octree: allocator required");
+  Scratch sc{alloc, ctx};
+  return morton_to_octree_impl(n, morton, level, sc, octree, num_nodes, S(stream));
+}
+
+extern "C" int kl_scan_octrees(int batch, const uint8_t *octrees, const int32_t *lengths_host, int32_t *exsum,
+                               int32_t *pyramid_host, int *level, kl_stream stream) {
+  hipStream_t st = S(stream);
+  const int STR = SPC_MAX_LEVELS + 2;
+  int64_t maxlen = 0;
+  for (int b = 0; b < batch; b++) maxlen = std::max<int64_t>(maxlen, lengths_host[b]);
+  uint32_t *cnt = nullptr;
+  int32_t *dpyr = nullptr;
+  void *tmp = nullptr;
+  size_t tb = 0;
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                (int)maxlen + 1, st));
+  KL_CHECK_HIP(hipMallocAsync((void **)&cnt, (maxlen + 1) * sizeof(uint32_t), st));
+  KL_CHECK_HIP(hipMallocAsync((void **)&dpyr, (size_t)batch * (2 * STR + 1) * sizeof(int32_t), st));
+  KL_CHECK_HIP(hipMallocAsync(&tmp, tb > 0 ? tb : 16, st));
+  int64_t off = 0;
+  for (int b = 0; b < batch; b++) {
+    const int64_t osize = lengths_host[b];
+    hipLaunchKernelGGL(popc_kernel, dim3((unsigned)cdiv(osize + 1, 256)), dim3(256), 0, st, osize, octrees + off,
+                       cnt);
+    KL_CHECK_LAUNCH();
+    // exsum segment b: [off + b, off + b + osize] = exclusive sum over osize+1 entries
+    KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, (uint32_t *)(exsum + off + b), (int)osize + 1, st));
+    hipLaunchKernelGGL(pyramid_kernel, dim3(1), dim3(64), 0, st, exsum + off + b, (uint32_t)osize,
+                       dpyr + (size_t)b * (2 * STR + 1), dpyr + (size_t)b * (2 * STR + 1) + 2 * STR);
+    KL_CHECK_LAUNCH();
+    off += osize;
+  }
+  std::vector<int32_t> h((size_t)batch * (2 * STR + 1));
+  KL_CHECK_HIP(hipMemcpyAsync(h.data(), dpyr, h.size() * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  KL_CHECK_HIP(hipStreamSynchronize(st));
+  KL_CHECK_HIP(hipFreeAsync(cnt, st));
+  KL_CHECK_HIP(hipFreeAsync(dpyr, st));
+  KL_CHECK_HIP(hipFreeAsync(tmp, st));
+  int lvl = 0;
+  for (int b = 0; b < batch; b++) {
+    for (int i = 0; i < 2 * STR; i++) pyramid_host[(size_t)b * 2 * STR + i] = h[(size_t)b * (2 * STR + 1) + i];
+    lvl = h[(size_t)b * (2 * STR + 1) + 2 * STR];
+  }
+  *level = lvl;
+  return KL_OK;
+}
+
+extern "C" int kl_generate_points(int batch, int max_level, const uint8_t *octrees, const int32_t *pyramids_host,
+                                  const int32_t *exsum, int16_t *points, kl_stream stream) {
+  hipStream_t st = S(stream);
+  const int L = max_level;
+  int64_t pmax = 1;
+  for (int b = 0; b < batch; b++) pmax = std::max<int64_t>(pmax, pyramids_host[(size_t)b * 2 * (L + 2) + (L + 2) + L + 1]);
+  uint64_t *mort = nullptr;
+  KL_CHECK_HIP(hipMallocAsync((void **)&mort, pmax * sizeof(uint64_t), st));
+  const uint8_t *oct = octrees;
+  const int32_t *ex = exsum;
+  int16_t *pts = points;
+  for (int b = 0; b < batch; b++) {
+    const int32_t *pyr = pyramids_host + (size_t)b * 2 * (L + 2);
+    const int32_t *pyrsum = pyr + L + 2;
+    const int32_t osize = pyrsum[L];
+    const int32_t total = pyrsum[L + 1];
+    KL_CHECK_HIP(hipMemsetAsync(mort, 0, sizeof(uint64_t), st));
+    const uint8_t *co = oct;
+    const int32_t *cs = ex + 1;
+    const uint64_t *cm = mort;
+    for (int l = 0; l < L; l++) {
+      const int n = pyr[l];
+      if (n > 0) {
+        hipLaunchKernelGGL(nodes_to_morton_kernel, dim3((unsigned)cdiv(n, 64)), dim3(64), 0, st, co, cs, cm, mort, n);
+        KL_CHECK_LAUNCH();
+      }
+      co += n;
+      cs += n;
+      cm += n;
+    }
+    if (total > 0) {
+      hipLaunchKernelGGL(morton_to_points_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, mort, pts,
+                         (int64_t)total);
+      KL_CHECK_LAUNCH();
+    }
+    pts += (size_t)total * 3;
+    oct += osize;
+    ex += osize + 1;
+  }
+  KL_CHECK_HIP(hipFreeAsync(mort, st));
+  return KL_OK;
+}
+
+extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int16_t *points, int64_t num_points,
+                           const int32_t *exsum, int max_level, const float *ray_o, const float *ray_d,
+                           int64_t num_rays, uint32_t target_level, int return_depth, int with_exit,
+                           kl_alloc_fn alloc, void *ctx, int32_t **nuggets, float **depth, int64_t *num_hits,
+                           kl_stream stream) {
+  (void)octree_size;
+  (void)num_points;
+  (void)max_level;
+  KL_REQUIRE(alloc != nullptr, "raytrace: allocator required");
+  hipStream_t st = S(stream);
+  Scratch sc{alloc, ctx};
+  RayIn in{octree, points, exsum, ray_o, ray_d};
+  const int dd = with_exit ? 2 : 1;
+  int64_t num = num_rays;
+  int2 *n0 = (int2 *)sc.get(num * sizeof(int2));
+  if (!n0) return KL_E_ALLOC;
+  if (num > 0) {
+    hipLaunchKernelGGL(rt_init_kernel, dim3((unsigned)cdiv(num, 256)), dim3(256), 0, st, num, n0);
+    KL_CHECK_LAUNCH();
+  }
+  *depth = nullptr;
+  for (uint32_t l = 0; l <= target_level; l++) {
+    const int last = l == target_level;
+    uint32_t *info = (uint32_t *)sc.get((num + 1) * sizeof(uint32_t));
+    uint32_t *psum = (uint32_t *)sc.get((num + 2) * sizeof(uint32_t));
+    float *d0 = nullptr;
+    if (last && return_depth) d0 = (float *)sc.get(num * dd * sizeof(float));
+    if (!info || !psum || (last && return_depth && !d0)) return KL_E_ALLOC;
+    hipLaunchKernelGGL(rt_decide_kernel, dim3((unsigned)cdiv(num + 1, 256)), dim3(256), 0, st, in, num, n0, info, d0,
+                       l, last, return_depth, with_exit);
+    KL_CHECK_LAUNCH();
+    uint32_t cnt = 0;
+    int rc = exclusive_scan(info, psum, num, sc, st, &cnt);
+    if (rc) return rc;
+    int2 *n1 = (int2 *)sc.get((size_t)cnt * sizeof(int2));
+    if (!n1) return KL_E_ALLOC;
+    if (cnt == 0) {
+      *nuggets = (int32_t *)n1;
+      if (return_depth) *depth = (float *)sc.get(16);
+      *num_hits = 0;
+      return KL_OK;
+    }
+    if (!last) {
+      hipLaunchKernelGGL(rt_subdivide_kernel, dim3((unsigned)cdiv(num, 256)), dim3(256), 0, st, in, num, n0, n1, info,
+                         psum, l);
+      KL_CHECK_LAUNCH();
+    } else {
+      float *d1 = nullptr;
+      if (return_depth) {
+        d1 = (float *)sc.get((size_t)cnt * dd * sizeof(float));
+        if (!d1) return KL_E_ALLOC;
+        *depth = d1;
+      }
+      hipLaunchKernelGGL(rt_compact_kernel, dim3((unsigned)cdiv(num, 256)), dim3(256), 0, st, num, n0, d0, n1, d1, dd,
+                         info, psum);
+      KL_CHECK_LAUNCH();
+    }
+    n0 = n1;
+    num = cnt;
+  }
+  *nuggets = (int32_t *)n0;
+  *num_hits = num;
+  return KL_OK;
+}
+
+extern "C" int kl_mark_pack_boundaries(kl_dtype dtype, int64_t num, const void *ids, int32_t *out, kl_stream stream) {
+  if (num == 0) return KL_OK;
+  const dim3 g((unsigned)cdiv(num, 256));
+  switch (dtype) {
+    case KL_I32:
+      hipLaunchKernelGGL(pack_bounds_kernel<int32_t>, g, dim3(256), 0, S(stream), num, (const int32_t *)ids, out);
+      break;
+    case KL_I64:
+      hipLaunchKernelGGL(pack_bounds_kernel<int64_t>, g, dim3(256), 0, S(stream), num, (const int64_t *)ids, out);
+      break;
+    case KL_I16:
+      hipLaunchKernelGGL(pack_bounds_kernel<int16_t>, g, dim3(256), 0, S(stream), num, (const int16_t *)ids, out);
+      break;
+    case KL_I8:
+      hipLaunchKernelGGL(pack_bounds_kernel<int8_t>, g, dim3(256), 0, S(stream), num, (const int8_t *)ids, out);
+      break;
+    case KL_U8:
+      hipLaunchKernelGGL(pack_bounds_kernel<uint8_t>, g, dim3(256), 0, S(stream), num, (const uint8_t *)ids, out);
+      break;
+    default:
+      set_error("mark_pack_boundaries: unsupported dtype");
+      return KL_E_INVALID;
+  }
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}

@@ -1,0 +1,455 @@
+"""``kaolin._C`` for MI355X: the reference's pybind registry (bindings.cpp:37-99),
+restricted to the hot path, re-implemented over the C ABI of libkaolin_hip.so.
+
+Same submodule paths, function names, argument order, dtypes, output containers
+(lists, or a tuple for scan_octrees_cuda), in/out-parameter conventions and
+argument-check messages as the reference dispatchers cited on each function.
+Outputs are allocated here with torch (caching allocator, current stream);
+kernels run on ``torch.cuda.current_stream()`` of the input's device.
+"""
+import ctypes
+import types
+
+import torch
+
+from . import _native as N
+from ._checks import (Arg, check_all_same_gpu, check_contiguous, check_dim, check_same_size, check_same_type,
+                      check_size, check_size_dim)
+
+_FLOATS = (torch.float32, torch.float64)
+
+
+def _float_only(func, t):
+    if t.dtype not in _FLOATS:
+        raise RuntimeError(f'"{func}" not implemented for \'{_tname(t.dtype)}\'')
+
+
+def _tname(dtype):
+    return {torch.float16: 'Half', torch.float32: 'Float', torch.float64: 'Double', torch.uint8: 'Byte',
+            torch.int8: 'Char', torch.int16: 'Short', torch.int32: 'Int', torch.int64: 'Long'}.get(dtype, str(dtype))
+
+
+# --------------------------------------------------------------------------- render.mesh
+def packed_rasterize_forward_cuda(height, width, face_vertices_z, face_vertices_image, face_bboxes, face_features,
+                                  first_idx_face_per_mesh, multiplier, eps, max_faces_per_mesh=None):
+    """rasterization.cpp:49-104.  ``max_faces_per_mesh`` (extension, optional) bounds
+    the per-mesh face count for the screen-space bins; default = total packed faces."""
+    func = 'packed_rasterize_forward_cuda'
+    args = [Arg(face_vertices_z, 'face_vertices_z', 3), Arg(face_vertices_image, 'face_vertices_image', 4),
+            Arg(face_bboxes, 'face_bboxes', 5), Arg(face_features, 'face_features', 6),
+            Arg(first_idx_face_per_mesh, 'first_idx_face_per_mesh', 7)]
+    check_all_same_gpu(func, args)
+    check_contiguous(func, args)
+    num_faces = face_vertices_z.shape[0]
+    batch_size = first_idx_face_per_mesh.shape[0] - 1
+    feat_dim = face_features.shape[2]
+    check_size(func, args[0], (num_faces, 3))
+    check_size(func, args[1], (num_faces, 3, 2))
+    check_size(func, args[2], (num_faces, 4))
+    check_size(func, args[3], (num_faces, 3, feat_dim))
+    check_size(func, args[4], (batch_size + 1,))
+    _float_only(func, face_vertices_z)
+    N.require_gpu(func, face_vertices_z)
+    dev = face_vertices_z.device
+    dtype = face_vertices_z.dtype
+    feats = torch.empty((batch_size, height, width, feat_dim), dtype=dtype, device=dev)
+    idx = torch.empty((batch_size, height, width), dtype=torch.long, device=dev)
+    w = torch.empty((batch_size, height, width, 3), dtype=dtype, device=dev)
+    maxf = int(max_faces_per_mesh) if max_faces_per_mesh is not None else max(int(num_faces), 1)
+    lib = N.lib()
+    ws_bytes = lib.kl_rasterize_workspace_bytes(batch_size, height, width, maxf)
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        N.check(lib.kl_packed_rasterize_forward(
+            N.dtype_code(dtype), height, width, batch_size, num_faces, feat_dim, maxf,
+            N.ptr(face_vertices_z), N.ptr(face_vertices_image), N.ptr(face_bboxes), N.ptr(face_features),
+            N.ptr(first_idx_face_per_mesh), float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w),
+            N.ptr(ws), ws_bytes, N.stream_of(dev)), func)
+    return [feats, idx, w]
+
+
+def rasterize_backward_cuda(grad_interpolated_features, interpolated_features, selected_face_idx, output_weights,
+                            face_vertices_image, face_features, eps):
+    """rasterization.cpp:106-168."""
+    func = 'rasterize_backward_cuda'
+    args = [Arg(grad_interpolated_features, 'grad_interpolated_features', 1),
+            Arg(interpolated_features, 'interpolated_features', 2), Arg(selected_face_idx, 'selected_face_idx', 3),
+            Arg(output_weights, 'output_weights', 4), Arg(face_vertices_image, 'face_vertices_image', 5),
+            Arg(face_features, 'face_features', 6)]
+    check_all_same_gpu(func, args)
+    check_contiguous(func, args)
+    B, H, W, D = grad_interpolated_features.shape
+    F = face_vertices_image.shape[1]
+    check_size(func, args[0], (B, H, W, D))
+    check_size(func, args[1], (B, H, W, D))
+    check_size(func, args[2], (B, H, W))
+    check_size(func, args[3], (B, H, W, 3))
+    check_size(func, args[4], (B, F, 3, 2))
+    check_size(func, args[5], (B, F, 3, D))
+    _float_only(func, grad_interpolated_features)
+    N.require_gpu(func, grad_interpolated_features)
+    dev = face_vertices_image.device
+    g_img = torch.empty_like(face_vertices_image)
+    g_feat = torch.empty_like(face_features)
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_rasterize_backward(
+            N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, N.ptr(grad_interpolated_features),
+            N.ptr(selected_face_idx), N.ptr(output_weights), N.ptr(face_vertices_image), N.ptr(face_features),
+            float(eps), N.ptr(g_img), N.ptr(g_feat), N.stream_of(dev)), func)
+    return [g_img, g_feat]
+
+
+def dibr_soft_mask_forward_cuda(face_vertices_image, face_large_bboxes, selected_face_idx, sigmainv, knum,
+                                multiplier):
+    """dibr_soft_mask.cpp:48-108."""
+    func = 'dibr_soft_mask_forward_cuda'
+    args = [Arg(face_vertices_image, 'face_vertices_image', 1), Arg(face_large_bboxes, 'face_bboxes', 2),
+            Arg(selected_face_idx, 'selected_face_idx', 3)]
+    check_all_same_gpu(func, args)
+    check_contiguous(func, args)
+    B, F = face_vertices_image.shape[:2]
+    H, W = selected_face_idx.shape[1:]
+    check_size(func, args[0], (B, F, 3, 2))
+    check_size(func, args[1], (B, F, 4))
+    check_size(func, args[2], (B, H, W))
+    _float_only(func, face_vertices_image)
+    N.require_gpu(func, face_vertices_image)
+    dev = face_vertices_image.device
+    dtype = face_vertices_image.dtype
+    K = int(knum)
+    soft_mask = torch.empty((B, H, W), dtype=dtype, device=dev)
+    prob = torch.empty((B, H, W, K), dtype=dtype, device=dev)
+    cidx = torch.empty((B, H, W, K), dtype=torch.long, device=dev)
+    ctype = torch.empty((B, H, W, K), dtype=torch.uint8, device=dev)
+    lib = N.lib()
+    ws_bytes = lib.kl_soft_mask_workspace_bytes(B, H, W, F)
+    ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        N.check(lib.kl_dibr_soft_mask_forward(
+            N.dtype_code(dtype), B, H, W, F, K, N.ptr(face_vertices_image), N.ptr(face_large_bboxes),
+            N.ptr(selected_face_idx), float(sigmainv), float(multiplier), N.ptr(soft_mask), N.ptr(prob),
+            N.ptr(cidx), N.ptr(ctype), N.ptr(ws), ws_bytes, N.stream_of(dev)), func)
+    return [soft_mask, prob, cidx, ctype]
+
+
+def dibr_soft_mask_backward_cuda(grad_soft_mask, soft_mask, selected_face_idx, close_face_prob, close_face_idx,
+                                 close_face_dist_type, face_vertices_image, sigmainv, multiplier):
+    """dibr_soft_mask.cpp:110-183."""
+    func = 'dibr_soft_mask_backward_cuda'
+    args = [Arg(grad_soft_mask, 'grad_soft_mask', 1), Arg(soft_mask, 'soft_mask', 2),
+            Arg(selected_face_idx, 'selected_face_idx', 3), Arg(close_face_prob, 'close_face_prob', 4),
+            Arg(close_face_idx, 'close_face_idx', 5), Arg(close_face_dist_type, 'close_face_dist_type', 6),
+            Arg(face_vertices_image, 'face_vertices_image', 7)]
+    check_all_same_gpu(func, [args[i] for i in (0, 1, 4, 5, 3, 6)])
+    check_contiguous(func, [args[i] for i in (0, 1, 3, 4, 5, 6)])
+    B, F = face_vertices_image.shape[:2]
+    H, W = selected_face_idx.shape[1:]
+    K = close_face_idx.shape[-1]
+    check_size(func, args[0], (B, H, W))
+    check_size(func, args[1], (B, H, W))
+    check_size(func, args[2], (B, H, W))
+    check_size(func, args[3], (B, H, W, K))
+    check_size(func, args[4], (B, H, W, K))
+    check_size(func, args[5], (B, H, W, K))
+    check_size(func, args[6], (B, F, 3, 2))
+    _float_only(func, face_vertices_image)
+    N.require_gpu(func, face_vertices_image)
+    dev = face_vertices_image.device
+    g = torch.empty_like(face_vertices_image)
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_dibr_soft_mask_backward(
+            N.dtype_code(face_vertices_image.dtype), B, H, W, F, K, N.ptr(grad_soft_mask), N.ptr(soft_mask),
+            N.ptr(selected_face_idx.contiguous()), N.ptr(close_face_prob), N.ptr(close_face_idx),
+            N.ptr(close_face_dist_type), N.ptr(face_vertices_image), float(sigmainv), float(multiplier), N.ptr(g),
+            N.stream_of(dev)), func)
+    return g
+
+
+# ------------------------------------------------------------------------------ metrics
+def unbatched_triangle_distance_forward_cuda(points, face_vertices, dist, face_idx, dist_type):
+    """unbatched_triangle_distance.cpp:43-72 (writes into the caller's tensors)."""
+    func = 'unbatched_triangle_distance_forward_cuda'
+    args = [Arg(points, 'points', 1), Arg(face_vertices, 'face_vertices', 2), Arg(dist, 'dist', 3),
+            Arg(face_idx, 'face_idx', 4), Arg(dist_type, 'dist_type', 5)]
+    check_all_same_gpu(func, args)
+    check_contiguous(func, args)
+    P, F = points.shape[0], face_vertices.shape[0]
+    check_size(func, args[0], (P, 3))
+    check_size(func, args[1], (F, 3, 3))
+    check_size(func, args[2], (P,))
+    check_size(func, args[3], (P,))
+    check_size(func, args[4], (P,))
+    _float_only(func, points)
+    N.require_gpu(func, points)
+    dev = points.device
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_unbatched_triangle_distance_forward(
+            N.dtype_code(points.dtype), P, F, N.ptr(points), N.ptr(face_vertices), N.ptr(dist), N.ptr(face_idx),
+            N.ptr(dist_type), N.stream_of(dev)), func)
+
+
+def unbatched_triangle_distance_backward_cuda(grad_dist, points, face_vertices, face_idx, dist_type, grad_points,
+                                              grad_face_vertices):
+    """unbatched_triangle_distance.cpp:74-114 (writes into the caller's tensors)."""
+    func = 'unbatched_triangle_distance_backward_cuda'
+    args = [Arg(grad_dist, 'grad_dist', 1), Arg(points, 'points', 2), Arg(face_vertices, 'face_vertices', 3),
+            Arg(face_idx, 'face_idx', 4), Arg(dist_type, 'dist_type', 5), Arg(grad_points, 'grad_points', 6),
+            Arg(grad_face_vertices, 'grad_face_vertices', 7)]
+    check_all_same_gpu(func, args)
+    check_contiguous(func, args)
+    P, F = points.shape[0], face_vertices.shape[0]
+    check_size(func, args[0], (P,))
+    check_size(func, args[1], (P, 3))
+    check_size(func, args[2], (F, 3, 3))
+    check_size(func, args[3], (P,))
+    check_size(func, args[4], (P,))
+    check_size(func, args[5], (P, 3))
+    check_size(func, args[6], (F, 3, 3))
+    _float_only(func, points)
+    N.require_gpu(func, points)
+    dev = points.device
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_unbatched_triangle_distance_backward(
+            N.dtype_code(points.dtype), P, F, N.ptr(grad_dist), N.ptr(points), N.ptr(face_vertices),
+            N.ptr(face_idx), N.ptr(dist_type), N.ptr(grad_points), N.ptr(grad_face_vertices), N.stream_of(dev)),
+            func)
+
+
+def sided_distance_forward_cuda(p1, p2):
+    """sided_distance.cpp:65-89."""
+    func = 'sided_distance_forward_cuda'
+    a1, a2 = Arg(p1, 'p1', 1), Arg(p2, 'p2', 2)
+    check_all_same_gpu(func, [a1, a2])
+    check_contiguous(func, [a1, a2])
+    check_same_type(func, a1, a2)
+    B, N1 = p1.shape[0], p1.shape[1]
+    N2 = p2.shape[1]
+    check_size(func, a1, (B, N1, 3))
+    check_size(func, a2, (B, N2, 3))
+    N.require_gpu(func, p1)
+    dev = p1.device
+    dist = torch.empty((B, N1), dtype=p1.dtype, device=dev)
+    idx = torch.empty((B, N1), dtype=torch.long, device=dev)
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_sided_distance_forward(N.dtype_code(p1.dtype), B, N1, N2, N.ptr(p1), N.ptr(p2),
+                                                  N.ptr(dist), N.ptr(idx), N.stream_of(dev)), func)
+    return [dist, idx]
+
+
+def sided_distance_backward_cuda(grad_output, p1, p2, idx):
+    """sided_distance.cpp:91-122."""
+    func = 'sided_distance_backward_cuda'
+    ag, a1, a2, ai = Arg(grad_output, 'grad_output', 1), Arg(p1, 'p1', 2), Arg(p2, 'p2', 3), Arg(idx, 'idx', 4)
+    check_all_same_gpu(func, [ag, a1, a2, ai])
+    check_contiguous(func, [ag, a1, a2, ai])
+    B, N1, N2 = p1.shape[0], p1.shape[1], p2.shape[1]
+    check_size(func, ai, (B, N1))
+    check_size(func, a1, (B, N1, 3))
+    check_size(func, a2, (B, N2, 3))
+    check_same_size(func, ai, ag)
+    N.require_gpu(func, p1)
+    dev = p1.device
+    g1 = torch.empty_like(p1)
+    g2 = torch.empty_like(p2)
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_sided_distance_backward(N.dtype_code(p1.dtype), B, N1, N2, N.ptr(grad_output),
+                                                   N.ptr(p1), N.ptr(p2), N.ptr(idx), N.ptr(g1), N.ptr(g2),
+                                                   N.stream_of(dev)), func)
+    return [g1, g2]
+
+
+# ------------------------------------------------------------------- ops.conversions / spc
+def mesh_to_spc_cuda(face_vertices, target_level):
+    """mesh_to_spc.cpp:28-44."""
+    func = 'mesh_to_spc_cuda'
+    if not face_vertices.is_cuda:
+        raise RuntimeError('face_vertices must be a CUDA tensor')
+    if not face_vertices.is_contiguous():
+        raise RuntimeError('face_vertices must be contiguous')
+    if face_vertices.dim() != 3 or face_vertices.shape[1] != 3 or face_vertices.shape[2] != 3:
+        raise RuntimeError('face_vertices must be of shape (F, 3, 3)')
+    if face_vertices.dtype != torch.float32:
+        raise RuntimeError('face_vertices must be float')
+    N.require_gpu(func, face_vertices)
+    dev = face_vertices.device
+    arena = N.Arena(dev)
+    oct_p, fidx_p, bary_p = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    nn, nl = ctypes.c_int64(), ctypes.c_int64()
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_mesh_to_spc(face_vertices.shape[0], N.ptr(face_vertices), int(target_level), arena.fn,
+                                       None, ctypes.byref(oct_p), ctypes.byref(nn), ctypes.byref(fidx_p),
+                                       ctypes.byref(bary_p), ctypes.byref(nl), N.stream_of(dev)), func)
+    if nl.value == 0:
+        return [torch.empty((0,), dtype=torch.uint8, device=dev), torch.empty((0,), dtype=torch.long, device=dev),
+                torch.zeros((0, 3), dtype=torch.float32, device=dev)]
+    octree = arena.tensor(oct_p.value, nn.value, torch.uint8, (nn.value,))
+    face_idx = arena.tensor(fidx_p.value, nl.value, torch.long, (nl.value,))
+    bary = arena.tensor(bary_p.value, nl.value * 2, torch.float32, (nl.value, 2))
+    return [octree, face_idx, bary]
+
+
+def morton_to_octree(mortons, level):
+    """spc.cpp:55-65 (mortons: sorted unique int64 leaf codes)."""
+    func = 'morton_to_octree'
+    N.require_gpu(func, mortons)
+    dev = mortons.device
+    mortons = mortons.contiguous()
+    arena = N.Arena(dev)
+    oct_p, nn = ctypes.c_void_p(), ctypes.c_int64()
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_morton_to_octree(mortons.shape[0], N.ptr(mortons), int(level), arena.fn, None,
+                                            ctypes.byref(oct_p), ctypes.byref(nn), N.stream_of(dev)), func)
+    return arena.tensor(oct_p.value, nn.value, torch.uint8, (nn.value,))
+
+
+def points_to_octree(points, level):
+    """spc.cpp:67-77: int16 points (N,3) -> octree (via morton codes)."""
+    from .ops.spc.points import points_to_morton
+    morton = torch.sort(points_to_morton(points.contiguous()))[0]
+    return morton_to_octree(morton, level)
+
+
+def _check_octrees(octrees, name='octrees'):
+    if octrees.dtype != torch.uint8:
+        raise RuntimeError(f'{name} must be byte')
+    if not octrees.is_cuda:
+        raise RuntimeError(f'{name} must be a CUDA tensor')
+    if not octrees.is_contiguous():
+        raise RuntimeError(f'{name} must be contiguous')
+
+
+def scan_octrees_cuda(octrees, lengths):
+    """spc.cpp:79-107 -> (level, pyramid (B,2,level+2) CPU int32, exsum int32)."""
+    func = 'scan_octrees_cuda'
+    _check_octrees(octrees)
+    if lengths.is_cuda:
+        raise RuntimeError('lengths must be a cpu tensor')
+    if not lengths.is_contiguous():
+        raise RuntimeError('lengths must be contiguous')
+    N.require_gpu(func, octrees)
+    dev = octrees.device
+    lengths32 = lengths.to(torch.int32).contiguous()
+    B = lengths32.shape[0]
+    total = int(lengths32.sum())
+    exsum = torch.zeros(total + B, dtype=torch.int32, device=dev)
+    pyr = torch.zeros((B, 2, 17), dtype=torch.int32)
+    level = ctypes.c_int()
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_scan_octrees(B, N.ptr(octrees), ctypes.c_void_p(lengths32.data_ptr()), N.ptr(exsum),
+                                        ctypes.c_void_p(pyr.data_ptr()), ctypes.byref(level), N.stream_of(dev)),
+                func)
+    lv = level.value
+    return lv, pyr[:, :, :lv + 2].contiguous(), exsum
+
+
+def generate_points_cuda(octrees, pyramids, exsum):
+    """spc.cpp:109-134."""
+    func = 'generate_points_cuda'
+    _check_octrees(octrees)
+    if pyramids.is_cuda:
+        raise RuntimeError('pyramids must be a cpu tensor')
+    if not pyramids.is_contiguous():
+        raise RuntimeError('pyramids must be contiguous')
+    if not exsum.is_cuda:
+        raise RuntimeError('exsum must be a CUDA tensor')
+    if not exsum.is_contiguous():
+        raise RuntimeError('exsum must be contiguous')
+    N.require_gpu(func, octrees)
+    dev = octrees.device
+    pyr = pyramids.to(torch.int32).contiguous()
+    level = pyr.shape[2] - 2
+    psum = int(pyr[:, 1, level + 1].sum())
+    points = torch.empty((psum, 3), dtype=torch.int16, device=dev)
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_generate_points(pyr.shape[0], level, N.ptr(octrees), ctypes.c_void_p(pyr.data_ptr()),
+                                           N.ptr(exsum), N.ptr(points), N.stream_of(dev)), func)
+    return points
+
+
+# ------------------------------------------------------------------------------ render.spc
+def raytrace_cuda(octree, points, pyramid, exclusive_sum, ray_o, ray_d, target_level, return_depth, with_exit):
+    """raytrace.cpp:170-214."""
+    func = 'raytrace_cuda'
+    args = [Arg(octree, 'octree', 1), Arg(points, 'points', 2), Arg(exclusive_sum, 'exclusive_sum', 4),
+            Arg(ray_o, 'ray_o', 5), Arg(ray_d, 'ray_d', 6)]
+    check_all_same_gpu(func, args)
+    check_contiguous(func, args)
+    if pyramid.is_cuda:
+        raise RuntimeError(f'Expected tensor to have cpu DeviceType, but got tensor with {pyramid.device.type} '
+                           f'DeviceType (while checking arguments for {func})')
+    if points.dtype != torch.int16:
+        raise RuntimeError('points must be short')
+    check_dim(func, Arg(points, 'points', 2), 2)
+    check_size_dim(func, Arg(points, 'points', 2), 1, 3)
+    check_dim(func, Arg(pyramid, 'pyramid', 3), 2)
+    check_size_dim(func, Arg(pyramid, 'pyramid', 3), 0, 2)
+    max_level = pyramid.shape[1] - 2
+    if not max_level < 15:
+        raise RuntimeError('SPC pyramid too big')
+    pyr = pyramid.reshape(-1)
+    osize = int(pyr[2 * max_level + 2])
+    psize = int(pyr[2 * max_level + 3])
+    check_size_dim(func, Arg(octree, 'octree', 1), 0, osize)
+    check_size_dim(func, Arg(points, 'points', 2), 0, psize)
+    if not (int(pyr[max_level + 1]) == 0 and int(pyr[max_level + 2]) == 0):
+        raise RuntimeError('SPC pyramid corrupt, check if the SPC pyramid has been sliced')
+    N.require_gpu(func, octree)
+    dev = octree.device
+    arena = N.Arena(dev)
+    nug_p, dep_p, nh = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_raytrace(N.ptr(octree), octree.shape[0], N.ptr(points), points.shape[0],
+                                    N.ptr(exclusive_sum), max_level, N.ptr(ray_o), N.ptr(ray_d), ray_o.shape[0],
+                                    int(target_level), int(bool(return_depth)), int(bool(with_exit)), arena.fn, None,
+                                    ctypes.byref(nug_p), ctypes.byref(dep_p), ctypes.byref(nh), N.stream_of(dev)),
+                func)
+    n = nh.value
+    nuggets = arena.tensor(nug_p.value, 2 * n, torch.int32, (n, 2))
+    if return_depth:
+        dd = 2 if with_exit else 1
+        depth = arena.tensor(dep_p.value, n * dd, torch.float32, (n, dd))
+        return [nuggets, depth]
+    return [nuggets]
+
+
+def mark_pack_boundaries_cuda(pack_ids):
+    """raytrace.cpp:216-232."""
+    func = 'mark_pack_boundaries_cuda'
+    a = Arg(pack_ids, 'pack_ids', 1)
+    check_dim(func, a, 1)
+    check_all_same_gpu(func, [a])
+    check_contiguous(func, [a])
+    if pack_ids.dtype not in (torch.uint8, torch.int8, torch.int32, torch.int64, torch.int16):
+        raise RuntimeError(f'Expected scalar type of argument #1 \'pack_ids\' to be one of Byte, Char, Int, Long, '
+                           f'Short (while checking arguments for {func})')
+    dev = pack_ids.device
+    out = torch.empty((pack_ids.shape[0],), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_mark_pack_boundaries(N.dtype_code(pack_ids.dtype), pack_ids.shape[0], N.ptr(pack_ids),
+                                                N.ptr(out), N.stream_of(dev)), func)
+    return out
+
+
+# ----------------------------------------------------------------------- module layout
+def _module(name, **fns):
+    m = types.ModuleType(name)
+    for k, v in fns.items():
+        setattr(m, k, v)
+    return m
+
+
+render = _module('kaolin._C.render')
+render.mesh = _module('kaolin._C.render.mesh', packed_rasterize_forward_cuda=packed_rasterize_forward_cuda,
+                      rasterize_backward_cuda=rasterize_backward_cuda,
+                      dibr_soft_mask_forward_cuda=dibr_soft_mask_forward_cuda,
+                      dibr_soft_mask_backward_cuda=dibr_soft_mask_backward_cuda)
+render.spc = _module('kaolin._C.render.spc', raytrace_cuda=raytrace_cuda,
+                     mark_pack_boundaries_cuda=mark_pack_boundaries_cuda)
+metrics = _module('kaolin._C.metrics', sided_distance_forward_cuda=sided_distance_forward_cuda,
+                  sided_distance_backward_cuda=sided_distance_backward_cuda,
+                  unbatched_triangle_distance_forward_cuda=unbatched_triangle_distance_forward_cuda,
+                  unbatched_triangle_distance_backward_cuda=unbatched_triangle_distance_backward_cuda)
+ops = _module('kaolin._C.ops')
+ops.conversions = _module('kaolin._C.ops.conversions', mesh_to_spc_cuda=mesh_to_spc_cuda)
+ops.spc = _module('kaolin._C.ops.spc', morton_to_octree=morton_to_octree, points_to_octree=points_to_octree,
+                  scan_octrees_cuda=scan_octrees_cuda, generate_points_cuda=generate_points_cuda)

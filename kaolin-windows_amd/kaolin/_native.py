@@ -1,0 +1,138 @@
+"""Loader for libkaolin_hip.so, the gfx950 C-ABI library (include/kaolin_hip.h).
+
+There is no fallback: if the library is missing or no HIP device is present, every
+hot-path op raises.  The library is loaded from this package's ``_lib`` directory
+(built in-tree by ``__graft_entry__.build()`` / ``make -C kaolin-windows_amd/csrc``).
+"""
+import ctypes
+import os
+
+import torch
+
+_LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib')
+LIB_PATH = os.path.join(_LIB_DIR, 'libkaolin_hip.so')
+
+KL_F32, KL_F64, KL_F16, KL_U8, KL_I8, KL_I16, KL_I32, KL_I64 = range(8)
+_DTYPES = {
+    torch.float32: KL_F32, torch.float64: KL_F64, torch.float16: KL_F16, torch.uint8: KL_U8,
+    torch.int8: KL_I8, torch.int16: KL_I16, torch.int32: KL_I32, torch.int64: KL_I64,
+}
+
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+_lib = None
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+_SZ = ctypes.c_size_t
+_PP = ctypes.POINTER(ctypes.c_void_p)
+
+_SIGS = {
+    'kl_last_error': (ctypes.c_char_p, []),
+    'kl_abi_version': (_I, []),
+    'kl_rasterize_workspace_bytes': (_SZ, [_I, _I, _I, _I64]),
+    'kl_packed_rasterize_forward': (_I, [_I, _I, _I, _I, _I64, _I, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P,
+                                         _SZ, _P]),
+    'kl_rasterize_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
+    'kl_soft_mask_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
+    'kl_dibr_soft_mask_forward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _SZ, _P]),
+    'kl_dibr_soft_mask_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P]),
+    'kl_unbatched_triangle_distance_forward': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P]),
+    'kl_unbatched_triangle_distance_backward': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
+    'kl_sided_distance_forward': (_I, [_I, _I, _I64, _I64, _P, _P, _P, _P, _P]),
+    'kl_sided_distance_backward': (_I, [_I, _I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    'kl_mesh_to_spc': (_I, [_I64, _P, ctypes.c_uint32, ALLOC_FN, _P, _PP, ctypes.POINTER(_I64), _PP, _PP,
+                            ctypes.POINTER(_I64), _P]),
+    'kl_morton_to_octree': (_I, [_I64, _P, ctypes.c_uint32, ALLOC_FN, _P, _PP, ctypes.POINTER(_I64), _P]),
+    'kl_scan_octrees': (_I, [_I, _P, _P, _P, _P, ctypes.POINTER(_I), _P]),
+    'kl_generate_points': (_I, [_I, _I, _P, _P, _P, _P, _P]),
+    'kl_raytrace': (_I, [_P, _I64, _P, _I64, _P, _I, _P, _P, _I64, ctypes.c_uint32, _I, _I, ALLOC_FN, _P, _PP, _PP,
+                         ctypes.POINTER(_I64), _P]),
+    'kl_mark_pack_boundaries': (_I, [_I, _I64, _P, _P, _P]),
+    'kl_voxelgrid_mark': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
+    'kl_voxelgrid_mark_f64': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
+}
+
+
+def lib():
+    """Load (once) and return the ctypes handle.  Raises if the library is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f'kaolin HIP library not found at {LIB_PATH}; build it with '
+                '`make -C kaolin-windows_amd/csrc` (hipcc --offload-arch=gfx950)')
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def dtype_code(dtype):
+    try:
+        return _DTYPES[dtype]
+    except KeyError:
+        raise RuntimeError(f'dtype {dtype} is not supported by the kaolin HIP library') from None
+
+
+def check(rc, func):
+    if rc != 0:
+        msg = lib().kl_last_error().decode(errors='replace')
+        raise RuntimeError(f'{func}: {msg} (kaolin HIP error {rc})')
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_gpu(func, *tensors):
+    """The HIP path is the only path: CPU tensors or a missing device raise."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(f'In {func}: kaolin-mi355x runs only on GPU tensors '
+                               f'(got a {t.device} tensor); there is no CPU fallback')
+    lib()
+
+
+class Arena:
+    """Device allocator handed to the C ABI for data-dependent outputs: every request
+    becomes a torch uint8 tensor (caching allocator, current stream)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.by_ptr = {}
+        self._cb = ALLOC_FN(self._alloc)
+
+    def _alloc(self, ctx, nbytes):
+        try:
+            t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
+        except Exception:  # pragma: no cover - OOM inside a C callback
+            return None
+        p = t.data_ptr()
+        self.by_ptr[p] = t
+        return p
+
+    @property
+    def fn(self):
+        return self._cb
+
+    def tensor(self, p, numel, dtype, shape):
+        """View of an arena allocation as a typed tensor of `shape` (numel elements)."""
+        if numel == 0:
+            return torch.empty(shape, dtype=dtype, device=self.device)
+        base = self.by_ptr[p]
+        esize = torch.empty((), dtype=dtype).element_size()
+        return base[:numel * esize].view(dtype).reshape(shape)

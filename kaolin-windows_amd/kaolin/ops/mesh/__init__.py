@@ -1,0 +1,2 @@
+from .mesh import index_vertices_by_faces  # noqa: F401
+from .trianglemesh import face_normals  # noqa: F401

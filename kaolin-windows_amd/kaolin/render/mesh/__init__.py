@@ -1,0 +1,2 @@
+from .rasterization import rasterize  # noqa: F401
+from .dibr import dibr_soft_mask, dibr_rasterization  # noqa: F401

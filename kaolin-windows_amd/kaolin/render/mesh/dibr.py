@@ -1,0 +1,56 @@
+"""DIB-R soft mask and dibr_rasterization (kaolin/render/mesh/dibr.py:27-209) over the HIP path."""
+import torch
+from torch.autograd import Function
+
+from ... import _C
+from .rasterization import rasterize
+
+__all__ = ['dibr_soft_mask', 'dibr_rasterization']
+
+
+class DibrSoftMaskCuda(Function):
+    """dibr.py:27-73."""
+
+    @staticmethod
+    def forward(ctx, face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier):
+        face_vertices_image = face_vertices_image.contiguous()
+        face_vertices_image = face_vertices_image * multiplier
+        selected_face_idx = selected_face_idx.contiguous()
+        points_min = torch.min(face_vertices_image, dim=-2)[0]
+        points_max = torch.max(face_vertices_image, dim=-2)[0]
+        face_large_bboxes = torch.cat([points_min - boxlen * multiplier, points_max + boxlen * multiplier], dim=-1)
+        soft_mask, close_face_prob, close_face_idx, close_face_dist_type = \
+            _C.render.mesh.dibr_soft_mask_forward_cuda(face_vertices_image, face_large_bboxes.contiguous(),
+                                                       selected_face_idx, sigmainv, knum, multiplier)
+        ctx.multiplier = multiplier
+        ctx.sigmainv = sigmainv
+        ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, close_face_prob, close_face_idx,
+                              close_face_dist_type)
+        return soft_mask
+
+    @staticmethod
+    def backward(ctx, grad_soft_mask):
+        soft_mask, face_vertices_image, selected_face_idx, close_face_prob, close_face_idx, close_face_dist_type = \
+            ctx.saved_tensors
+        grad_face_vertices_image = _C.render.mesh.dibr_soft_mask_backward_cuda(
+            grad_soft_mask.contiguous(), soft_mask, selected_face_idx, close_face_prob, close_face_idx,
+            close_face_dist_type, face_vertices_image, ctx.sigmainv, ctx.multiplier)
+        return grad_face_vertices_image, None, None, None, None, None
+
+
+def dibr_soft_mask(face_vertices_image, selected_face_idx, sigmainv=7000, boxlen=0.02, knum=30, multiplier=1000.):
+    r"""Soft silhouette of DIB-R (Chen et al., NeurIPS 2019): for every pixel not covered
+    by a rasterized face, 1 - prod(1 - exp(-sigmainv * d^2)) over the first ``knum``
+    faces (index order) whose bbox enlarged by ``boxlen`` contains it; 1 where covered."""
+    return DibrSoftMaskCuda.apply(face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier)
+
+
+def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z,
+                       sigmainv=7000, boxlen=0.02, knum=30, multiplier=None, eps=None, rast_backend='cuda'):
+    r"""DIB-R renderer: rasterize(valid = face_normals_z >= 0) + dibr_soft_mask.
+    Returns (features, soft_mask, face_idx) as dibr.py:119-209."""
+    interpolated_features, face_idx = rasterize(height, width, face_vertices_z, face_vertices_image, face_features,
+                                                face_normals_z >= 0., multiplier, eps, rast_backend)
+    _multiplier = 1000. if multiplier is None else multiplier
+    soft_mask = dibr_soft_mask(face_vertices_image, face_idx, sigmainv, boxlen, knum, _multiplier)
+    return interpolated_features, soft_mask, face_idx

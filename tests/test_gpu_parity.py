@@ -1,0 +1,479 @@
+"""HIP path (through kaolin._C and the front-ends) vs the CPU oracle and the reference goldens.
+
+All tests need an MI355X.  Integer outputs (face indices, distance types, octrees,
+nuggets, voxels) must be bit-identical to the oracle; floating outputs of the forward
+kernels are bit-identical too where no transcendental is involved (same operation
+order, no contraction, IEEE div/sqrt); soft-mask probabilities differ only by expf
+ulps (tolerance 1e-6 relative); gradients accumulate with float atomics in a
+different order (tolerance 1e-5, the north-star bar).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module')
+def kal():
+    import kaolin
+    return kaolin
+
+
+def T(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t.to(dtype) if dtype is not None else t
+
+
+def A(t):
+    return t.detach().cpu().numpy()
+
+
+def _uv_sphere(n_lat, n_lon, radius=1.0):
+    lat = np.linspace(0, math.pi, n_lat + 1)[1:-1]
+    lon = np.arange(n_lon) * (2 * math.pi / n_lon)
+    ring = np.stack([np.sin(lat)[:, None] * np.cos(lon)[None], np.repeat(np.cos(lat)[:, None], n_lon, 1),
+                     np.sin(lat)[:, None] * np.sin(lon)[None]], -1).reshape(-1, 3)
+    verts = np.concatenate([[[0., 1., 0.]], ring, [[0., -1., 0.]]]) * radius
+    faces = []
+    nr = n_lat - 1
+    for j in range(n_lon):
+        faces.append([0, 1 + (j + 1) % n_lon, 1 + j])
+    for i in range(nr - 1):
+        for j in range(n_lon):
+            a, b = 1 + i * n_lon + j, 1 + i * n_lon + (j + 1) % n_lon
+            c, d = 1 + (i + 1) * n_lon + j, 1 + (i + 1) * n_lon + (j + 1) % n_lon
+            faces += [[a, b, d], [a, d, c]]
+    last = 1 + nr * n_lon
+    for j in range(n_lon):
+        faces.append([1 + (nr - 1) * n_lon + j, 1 + (nr - 1) * n_lon + (j + 1) % n_lon, last])
+    return verts, np.array(faces, np.int64)
+
+
+def _render_inputs(kal, n_lat, n_lon, B, dtype=torch.float32, seed=0):
+    v, f = _uv_sphere(n_lat, n_lon, 0.9)
+    g = np.random.default_rng(seed)
+    v = v * (1 + 0.01 * g.standard_normal((v.shape[0], 1)))
+    verts = T(v, dtype).unsqueeze(0).repeat(B, 1, 1)
+    faces = T(f)
+    az = torch.arange(B, dtype=dtype, device=DEV) * (2 * math.pi / B)
+    cam = torch.stack([3 * torch.sin(az), torch.zeros_like(az) + 0.3, 3 * torch.cos(az)], -1)
+    rot, trans = kal.render.camera.generate_rotate_translate_matrices(
+        cam, torch.zeros_like(cam), torch.tensor([[0., 1., 0.]], dtype=dtype, device=DEV).repeat(B, 1))
+    vc = kal.render.camera.rotate_translate_points(verts, rot, trans)
+    proj = kal.render.camera.generate_perspective_projection(math.pi / 4, dtype=dtype).to(DEV)
+    vi = kal.render.camera.perspective_camera(vc, proj)
+    fvc = kal.ops.mesh.index_vertices_by_faces(vc, faces)
+    fvz = fvc[..., -1].contiguous()
+    fvi = kal.ops.mesh.index_vertices_by_faces(vi, faces).contiguous()
+    fnz = kal.ops.mesh.face_normals(fvc, unit=True)[..., -1]
+    uv = torch.stack([torch.atan2(verts[..., 2], verts[..., 0]), verts[..., 1]], -1)
+    feat = kal.ops.mesh.index_vertices_by_faces(torch.cat([uv, torch.ones_like(uv[..., :1])], -1), faces)
+    return fvz, fvi, feat.contiguous(), fnz
+
+
+# ------------------------------------------------------------------ rasterize
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('flip', [0, 1])
+@pytest.mark.parametrize('valid', [0, 1])
+def test_rasterize_sphere_fixture(kal, golden, dname, flip, valid):
+    g = golden('dibr_sphere.npz')
+    p = f'{dname}_flip{flip}_'
+    q = p + f'valid{valid}_'
+    fvz, fvi, uv = T(g[p + 'face_vertices_z']), T(g[p + 'face_vertices_image']), T(g[p + 'face_uvs'])
+    vf = T(g[p + 'valid_faces']) if valid else None
+    fvi_r = fvi.clone().requires_grad_(True)
+    uv_r = uv.clone().requires_grad_(True)
+    feats, fidx = kal.render.mesh.rasterize(35, 31, fvz, fvi_r, uv_r, valid_faces=vf)
+    # reference golden (naive oracle of the reference) with the reference test tolerances
+    assert np.array_equal(A(fidx), g[q + 'face_idx'])
+    np.testing.assert_allclose(A(feats), g[q + 'features'], rtol=1e-5, atol=1e-5)
+    feats.backward(T(g[q + 'grad_out']))
+    np.testing.assert_allclose(A(fvi_r.grad), g[q + 'grad_face_vertices_image'], rtol=1e-3, atol=1e-2)
+    np.testing.assert_allclose(A(uv_r.grad), g[q + 'grad_face_uvs'], rtol=1e-3, atol=1e-3)
+    # our oracle: bit-exact forward, 1e-5 backward
+    of, oi, ow = orc.rasterize(35, 31, g[p + 'face_vertices_z'], g[p + 'face_vertices_image'], g[p + 'face_uvs'],
+                               valid_faces=g[p + 'valid_faces'] if valid else None)
+    assert np.array_equal(A(fidx), oi)
+    assert np.array_equal(A(feats), of)
+    gi, gf = orc.rasterize_backward(g[q + 'grad_out'], oi, ow, g[p + 'face_vertices_image'], g[p + 'face_uvs'], 1e-8)
+    np.testing.assert_allclose(A(fvi_r.grad), gi, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(A(uv_r.grad), gf, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('H,W', [(96, 128), (67, 45)])
+def test_packed_rasterize_vs_oracle(kal, dtype, H, W):
+    fvz, fvi, feat, fnz = _render_inputs(kal, 30, 50, 3, dtype)
+    valid = fnz >= 0
+    feats, fidx = kal.render.mesh.rasterize(H, W, fvz, fvi, feat, valid_faces=valid)
+    of, oi, ow = orc.rasterize(H, W, A(fvz), A(fvi), A(feat), valid_faces=A(valid))
+    assert np.array_equal(A(fidx), oi)
+    assert np.array_equal(A(feats), of)
+    assert (oi >= 0).mean() > 0.2
+
+
+def test_rasterize_backward_vs_oracle(kal):
+    fvz, fvi, feat, fnz = _render_inputs(kal, 30, 50, 2)
+    fvi_r = fvi.clone().requires_grad_(True)
+    feat_r = feat.clone().requires_grad_(True)
+    feats, fidx = kal.render.mesh.rasterize(80, 80, fvz, fvi_r, feat_r, valid_faces=fnz >= 0)
+    go = torch.rand_like(feats)
+    feats.backward(go)
+    of, oi, ow = orc.rasterize(80, 80, A(fvz), A(fvi), A(feat), valid_faces=A(fnz >= 0))
+    gi, gf = orc.rasterize_backward(A(go), oi, ow, A(fvi), A(feat), 1e-8)
+    np.testing.assert_allclose(A(fvi_r.grad), gi, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(A(feat_r.grad), gf, rtol=1e-5, atol=1e-5)
+
+
+def test_packed_rasterize_C_direct(kal):
+    """_C entry point with packed inputs (rasterization.cpp:49-104): packed (per-mesh) index."""
+    fvz, fvi, feat, fnz = _render_inputs(kal, 12, 20, 2)
+    B, F = fvz.shape[:2]
+    m = 1000.
+    vfvi = (fvi * m).reshape(B * F, 3, 2).contiguous()
+    bbox = torch.cat([vfvi.min(1)[0], vfvi.max(1)[0]], 1).contiguous()
+    first = torch.tensor([0, F, 2 * F], dtype=torch.long, device=DEV)
+    out = kal._C.render.mesh.packed_rasterize_forward_cuda(40, 33, fvz.reshape(-1, 3).contiguous(), vfvi, bbox,
+                                                           feat.reshape(-1, 3, 3).contiguous(), first, m, 1e-8)
+    assert isinstance(out, list) and len(out) == 3
+    of, oi, ow = orc.packed_rasterize_forward(40, 33, A(fvz.reshape(-1, 3)), A(vfvi), A(bbox),
+                                              A(feat.reshape(-1, 3, 3)), A(first), m, 1e-8)
+    assert np.array_equal(A(out[1]), oi)
+    assert np.array_equal(A(out[0]), of)
+    assert np.array_equal(A(out[2]), ow)
+
+
+# ------------------------------------------------------------------ soft mask
+def _mask_iou_target(sel):
+    mask = sel != -1
+    return torch.nn.functional.pad(mask, (0, 5))[..., 5:]
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('sig,box', [(7000, 0.02), (7000, 0.2), (70, 0.02), (70, 0.2)])
+@pytest.mark.parametrize('knum', [30, 20])
+@pytest.mark.parametrize('multiplier', [1000, 100, 1])
+def test_soft_mask_simple_golden(kal, golden, dtype, sig, box, knum, multiplier):
+    """test_dibr.py:108-191 on the HIP path."""
+    g = golden('dibr_simple.npz')
+    fvi = T(g['face_vertices_image'], dtype)
+    fvz = T(g['face_vertices_z'], dtype)
+    _, sel = kal.render.mesh.rasterize(35, 31, fvz, fvi, torch.zeros(fvz.shape + (1,), dtype=dtype, device=DEV))
+    assert np.array_equal(A(sel), g['selected_face_idx'])
+    fm = fvi * multiplier
+    bb = torch.cat([fm.min(-2)[0] - box * multiplier, fm.max(-2)[0] + box * multiplier], -1)
+    mask, prob, cidx, ctype = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb.contiguous(), sel, sig, knum,
+                                                                             multiplier)
+    np.testing.assert_allclose(A(mask), g[f'soft_mask_{sig}_{box}'], atol=1e-5, rtol=1e-5)
+    assert np.array_equal(A(cidx), g[f'close_face_idx_{sig}_{box}'][..., :knum])
+    np.testing.assert_allclose(A(prob), g[f'close_face_prob_{sig}_{box}'][..., :knum], atol=1e-5, rtol=1e-5)
+    assert np.array_equal(A(ctype), g[f'close_face_dist_type_{sig}_{box}'][..., :knum])
+    fvi_r = fvi.clone().requires_grad_(True)
+    sm = kal.render.mesh.dibr_soft_mask(fvi_r, sel, sig, box, knum, multiplier)
+    loss = kal.metrics.render.mask_iou(sm, _mask_iou_target(sel))
+    loss.backward()
+    np.testing.assert_allclose(A(fvi_r.grad), g[f'grad_{sig}_{box}'], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('flip', [0, 1])
+@pytest.mark.parametrize('sig,box', [(7000, 0.02), (70, 0.01)])
+@pytest.mark.parametrize('knum', [30, 40])
+def test_soft_mask_sphere_golden(kal, golden, dname, flip, sig, box, knum):
+    """test_dibr.py:297-394 on the HIP path (type <=1% mismatch, grads 1e-1 as the reference)."""
+    g = golden('dibr_sphere.npz')
+    p = f'{dname}_flip{flip}_'
+    fvi, fvz = T(g[p + 'face_vertices_image']), T(g[p + 'face_vertices_z'])
+    _, sel = kal.render.mesh.rasterize(35, 31, fvz, fvi, torch.zeros(fvz.shape + (1,), dtype=fvz.dtype, device=DEV))
+    for multiplier in (1000, 100):
+        fm = fvi * multiplier
+        bb = torch.cat([fm.min(-2)[0] - box * multiplier, fm.max(-2)[0] + box * multiplier], -1).contiguous()
+        mask, prob, cidx, ctype = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, sel, sig, knum, multiplier)
+        np.testing.assert_allclose(A(mask), g[f'soft_mask_{sig}_{box}'], atol=1e-5, rtol=1e-5)
+        assert np.array_equal(A(cidx), g[f'close_face_idx_{sig}_{box}'][..., :knum])
+        np.testing.assert_allclose(A(prob), g[f'close_face_prob_{sig}_{box}'][..., :knum], atol=1e-5, rtol=1e-5)
+        assert np.mean(A(ctype) != g[f'close_face_dist_type_{sig}_{box}'][..., :knum]) <= 0.01
+        fvi_r = fvi.clone().requires_grad_(True)
+        sm = kal.render.mesh.dibr_soft_mask(fvi_r, sel, sig, box, knum, multiplier)
+        kal.metrics.render.mask_iou(sm, _mask_iou_target(sel)).backward()
+        np.testing.assert_allclose(A(fvi_r.grad), g[f'grad_{sig}_{box}'], rtol=1e-1, atol=1e-1)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('knum', [30, 7])
+def test_soft_mask_vs_oracle(kal, dtype, knum):
+    fvz, fvi, feat, fnz = _render_inputs(kal, 30, 50, 3, dtype)
+    H, W = 72, 100
+    _, sel = kal.render.mesh.rasterize(H, W, fvz, fvi, feat, valid_faces=fnz >= 0)
+    m, box, sig = 1000., 0.04, 7000.
+    fm = (fvi * m).contiguous()
+    bb = torch.cat([fm.min(-2)[0] - box * m, fm.max(-2)[0] + box * m], -1).contiguous()
+    mask, prob, cidx, ctype = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, sel, sig, knum, m)
+    om, op, oi, ot = orc.dibr_soft_mask_forward(A(fm), A(bb), A(sel), sig, knum, m)
+    assert np.array_equal(A(cidx), oi)
+    assert np.array_equal(A(ctype), ot)
+    np.testing.assert_allclose(A(prob), op, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(A(mask), om, rtol=1e-6, atol=1e-7)
+    assert (oi[..., 0] >= 0).sum() > 100  # the band is exercised
+    if knum == 7:
+        assert (oi[..., -1] >= 0).sum() > 0  # some pixels saturate knum
+    grad = torch.rand_like(mask)
+    gi = kal._C.render.mesh.dibr_soft_mask_backward_cuda(grad, mask, sel, prob, cidx, ctype, fm, sig, m)
+    ogi = orc.dibr_soft_mask_backward(A(grad), om, A(sel), op, oi, ot, A(fm), sig, m)
+    np.testing.assert_allclose(A(gi), ogi, rtol=1e-5, atol=1e-5)
+
+
+def test_dibr_rasterization_composition(kal):
+    """test_dibr.py:486-529: dibr_rasterization == rasterize + dibr_soft_mask, exactly."""
+    fvz, fvi, feat, fnz = _render_inputs(kal, 20, 30, 2)
+    f1, sm1, i1 = kal.render.mesh.dibr_rasterization(64, 48, fvz, fvi, feat, fnz, 7000, 0.02, 30, 1000)
+    f2, i2 = kal.render.mesh.rasterize(64, 48, fvz, fvi, feat, fnz >= 0., 1000)
+    sm2 = kal.render.mesh.dibr_soft_mask(fvi, i2, 7000, 0.02, 30, 1000.)
+    assert torch.equal(f1, f2) and torch.equal(i1, i2) and torch.equal(sm1, sm2)
+
+
+def test_dibr_deterministic_forward(kal):
+    fvz, fvi, feat, fnz = _render_inputs(kal, 40, 60, 2)
+    r1 = kal.render.mesh.dibr_rasterization(128, 128, fvz, fvi, feat, fnz)
+    r2 = kal.render.mesh.dibr_rasterization(128, 128, fvz, fvi, feat, fnz)
+    for a, b in zip(r1, r2):
+        assert torch.equal(a, b)
+
+
+# ------------------------------------------------------------ point_to_mesh
+def test_p2m_kat(kal, golden):
+    g = golden('p2m.npz')
+    for dtype in (torch.float32, torch.float64):
+        d, i, t = kal.metrics.trianglemesh.point_to_mesh_distance(T(g['kat_points'], dtype).unsqueeze(0),
+                                                                  T(g['kat_face_vertices'], dtype).unsqueeze(0))
+        np.testing.assert_allclose(A(d[0]), g['kat_dist'], rtol=1e-5, atol=1e-8)
+        assert np.array_equal(A(i[0]), g['kat_face_idx'])
+        assert np.array_equal(A(t[0]), g['kat_dist_type'])
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_p2m_random_fixture(kal, golden, dname):
+    g = golden('p2m.npz')
+    p = f'rand_{dname}_'
+    P = T(g[p + 'points']).requires_grad_(True)
+    FV = T(g[p + 'face_vertices']).requires_grad_(True)
+    d, i, t = kal.metrics.trianglemesh.point_to_mesh_distance(P.unsqueeze(0), FV.unsqueeze(0))
+    np.testing.assert_allclose(A(d[0]), g[p + 'dist'], rtol=1e-5, atol=1e-8)
+    assert np.array_equal(A(i[0]), g[p + 'face_idx'])
+    assert np.array_equal(A(t[0]), g[p + 'dist_type'])
+    od, oi, ot = orc.unbatched_triangle_distance_forward(g[p + 'points'], g[p + 'face_vertices'])
+    assert np.array_equal(A(d[0]), od) and np.array_equal(A(i[0]), oi) and np.array_equal(A(t[0]), ot)
+    d.backward(T(g[p + 'grad_out']).unsqueeze(0))
+    np.testing.assert_allclose(A(P.grad), g[p + 'grad_points'], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(A(FV.grad), g[p + 'grad_face_vertices'], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize('P,F', [(3000, 1800), (700, 513), (64, 1)])
+def test_p2m_vs_oracle(kal, P, F):
+    g = torch.Generator(device='cpu').manual_seed(P + F)
+    pts = torch.randn((P, 3), generator=g)
+    fv = torch.randn((F, 3, 3), generator=g)
+    d = torch.empty(P, device=DEV)
+    i = torch.empty(P, dtype=torch.long, device=DEV)
+    t = torch.empty(P, dtype=torch.int32, device=DEV)
+    kal._C.metrics.unbatched_triangle_distance_forward_cuda(pts.to(DEV), fv.to(DEV), d, i, t)
+    od, oi, ot = orc.unbatched_triangle_distance_forward(pts.numpy(), fv.numpy())
+    assert np.array_equal(A(d), od) and np.array_equal(A(i), oi) and np.array_equal(A(t), ot)
+    gr = torch.rand(P, generator=g)
+    gp = torch.empty((P, 3), device=DEV)
+    gf = torch.empty((F, 3, 3), device=DEV)
+    kal._C.metrics.unbatched_triangle_distance_backward_cuda(gr.to(DEV), pts.to(DEV), fv.to(DEV), i, t, gp, gf)
+    ogp, ogf = orc.unbatched_triangle_distance_backward(gr.numpy(), pts.numpy(), fv.numpy(), oi, ot)
+    np.testing.assert_allclose(A(gp), ogp, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(A(gf), ogf, rtol=1e-5, atol=1e-5)
+
+
+# ------------------------------------------------------------ sided distance
+def test_sided_kat_and_ties(kal, golden):
+    g = golden('sided.npz')
+    for dtype in (torch.float16, torch.float32, torch.float64):
+        d, i = kal.metrics.pointcloud.sided_distance(T(g['kat_p1'], dtype), T(g['kat_p2'], dtype))
+        tol = 1e-3 if dtype == torch.float16 else 1e-4
+        np.testing.assert_allclose(A(d.double()), g['kat_dist'], rtol=tol, atol=tol * 10 if dtype == torch.float16 else 1e-5)
+        assert np.array_equal(A(i), g['kat_idx'])
+    d, i = kal.metrics.pointcloud.sided_distance(T(g['large_p1']), T(g['large_p2']))
+    od, oi = orc.sided_distance_forward(g['large_p1'], g['large_p2'])
+    assert np.array_equal(A(d), od) and np.array_equal(A(i), oi)
+    np.testing.assert_allclose(A(d), g['large_dist'])
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+def test_sided_vs_oracle_and_grad(kal, golden, dtype):
+    g = golden('sided.npz')
+    p1 = T(g['rand_p1'], dtype).requires_grad_(True)
+    p2 = T(g['rand_p2'], dtype).requires_grad_(True)
+    d, i = kal.metrics.pointcloud.sided_distance(p1, p2)
+    od, oi = orc.sided_distance_forward(A(p1), A(p2))
+    assert np.array_equal(A(d), od) and np.array_equal(A(i), oi)
+    np.testing.assert_allclose(A(d), g['rand_dist'], rtol=1e-5, atol=1e-6)
+    gr = torch.rand_like(d)
+    d.backward(gr)
+    og1, og2 = orc.sided_distance_backward(A(gr), A(p1), A(p2), oi)
+    np.testing.assert_allclose(A(p1.grad), og1, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(A(p2.grad), og2, rtol=1e-5, atol=1e-5)
+
+
+def test_sided_gradcheck(kal):
+    g = torch.Generator().manual_seed(0)
+    p1 = torch.randn((5, 20, 3), generator=g, dtype=torch.double).to(DEV).requires_grad_(True)
+    p2 = torch.randn((5, 15, 3), generator=g, dtype=torch.double).to(DEV).requires_grad_(True)
+    assert torch.autograd.gradcheck(kal.metrics.pointcloud.sided_distance, (p1, p2), eps=1e-6, atol=1e-6)
+
+
+def test_sided_error_messages(kal):
+    """test_pointcloud.py:124-152: messages matched verbatim."""
+    with pytest.raises(RuntimeError, match=r"Expected tensor of size \[3, 3, 3\], but got tensor of size \[2, 3, 3\] "
+                                           r"for argument #2 'p2' \(while checking arguments for "
+                                           r"sided_distance_forward_cuda\)"):
+        kal.metrics.pointcloud.sided_distance(torch.randint(0, 10, (3, 2, 3), device=DEV).float(),
+                                              torch.randint(0, 10, (2, 3, 3), device=DEV).float())
+    with pytest.raises(RuntimeError, match="Expected 3-dimensional tensor, but got 4-dimensional tensor for "
+                                           r"argument #1 'p1' \(while checking arguments for "
+                                           r"sided_distance_forward_cuda\)"):
+        kal.metrics.pointcloud.sided_distance(torch.rand((3, 2, 3, 4), device=DEV), torch.rand((2, 3, 3), device=DEV))
+
+
+def test_chamfer_and_fscore(kal, golden):
+    g = golden('sided.npz')
+    p1, p2 = T(g['rand_p1']), T(g['rand_p2'])
+    ch = kal.metrics.pointcloud.chamfer_distance(p1, p2)
+    d1, _ = orc.sided_distance_forward(g['rand_p1'], g['rand_p2'])
+    d2, _ = orc.sided_distance_forward(g['rand_p2'], g['rand_p1'])
+    np.testing.assert_allclose(A(ch), d1.mean(-1) + d2.mean(-1), rtol=1e-5)
+    fs = kal.metrics.pointcloud.f_score(p1, p2, radius=0.05)
+    assert fs.shape == (2,) and torch.all((fs >= 0) & (fs <= 1))
+
+
+# ------------------------------------------------------------ voxelgrid
+@pytest.mark.parametrize('name', ['batched', 'origins', 'scale', 'res7', 'default_os', 'sphere32', 'random24'])
+def test_voxelgrid_golden(kal, golden, name):
+    g = golden('voxelgrid.npz')
+    o = T(g[f'{name}_origin']) if f'{name}_origin' in g else None
+    s = T(g[f'{name}_scale']) if f'{name}_scale' in g else None
+    vg = kal.ops.conversions.trianglemeshes_to_voxelgrids(T(g[f'{name}_vertices']), T(g[f'{name}_faces']),
+                                                          int(g[f'{name}_resolution']), o, s)
+    assert np.array_equal(np.argwhere(A(vg)).astype(np.int32), g[f'{name}_occupied'])
+    assert set(np.unique(A(vg))) <= {0.0, 1.0}
+
+
+def test_voxelgrid_sparse(kal, golden):
+    g = golden('voxelgrid.npz')
+    vg = kal.ops.conversions.trianglemeshes_to_voxelgrids(T(g['batched_vertices']), T(g['batched_faces']), 3,
+                                                          T(g['batched_origin']), T(g['batched_scale']),
+                                                          return_sparse=True)
+    assert vg.is_sparse
+    assert np.array_equal(np.argwhere(A(vg.to_dense())).astype(np.int32), g['batched_occupied'])
+
+
+def test_voxelgrid_vs_oracle_sphere(kal):
+    v, f = _uv_sphere(40, 64, 0.95)
+    vg = kal.ops.conversions.trianglemeshes_to_voxelgrids(T(v, torch.float32).unsqueeze(0), T(f), 96)
+    ov = orc.voxelgrid(v[None].astype(np.float32), f, 96)
+    assert np.array_equal(A(vg).astype(np.uint8), ov)
+
+
+# ------------------------------------------------------------------ SPC
+def test_mesh_to_spc_kat(kal, golden):
+    g = golden('spc.npz')
+    octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(T(g['m2s_face_vertices']), int(g['m2s_level']))
+    assert np.array_equal(A(octree), g['m2s_octree'])
+    assert np.array_equal(A(fidx), g['m2s_face_idx'])
+    np.testing.assert_allclose(A(bary), g['m2s_bary'], atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize('level', [1, 4, 6])
+def test_mesh_to_spc_vs_oracle(kal, level):
+    v, f = _uv_sphere(16, 24, 0.9)
+    fv = v[f].astype(np.float32)
+    octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(T(fv), level)
+    oo, of, ob = orc.mesh_to_spc(fv, level)
+    assert np.array_equal(A(octree), oo)
+    assert np.array_equal(A(fidx), of)
+    np.testing.assert_array_equal(A(bary), ob)
+
+
+def test_mesh_to_spc_empty(kal):
+    fv = torch.tensor([[[5., 5., 5.], [6., 5., 5.], [5., 6., 5.]]], device=DEV)
+    octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(fv, 3)
+    assert octree.shape == (0,) and fidx.shape == (0,) and tuple(bary.shape) == (0, 3)
+
+
+def test_scan_generate_kat(kal, golden):
+    g = golden('spc.npz')
+    level, pyr, ex = kal.ops.spc.scan_octrees(T(g['scan_octrees']), torch.from_numpy(g['scan_lengths']))
+    assert level == int(g['scan_max_level'])
+    assert not pyr.is_cuda and np.array_equal(pyr.numpy(), g['scan_pyramids'])
+    assert np.array_equal(A(ex), g['scan_exsum'])
+    pts = kal.ops.spc.generate_points(T(g['scan_octrees']), pyr, ex)
+    assert np.array_equal(A(pts), g['scan_points'])
+
+
+def _rt_setup(kal, octree_np):
+    octree = T(octree_np)
+    level, pyr, ex = kal.ops.spc.scan_octrees(octree, torch.tensor([len(octree_np)], dtype=torch.int32))
+    pts = kal.ops.spc.generate_points(octree, pyr, ex)
+    return octree, pyr[0], ex, pts
+
+
+@pytest.mark.parametrize('name', ['positive', 'negative', 'none', 'coarser', 'depth', 'depth_exit',
+                                  'inside_nodepth', 'inside_depth', 'inside_exit'])
+def test_raytrace_kat(kal, golden, name):
+    g = golden('spc.npz')
+    octree, pyr, ex, pts = _rt_setup(kal, g['rt_octree'])
+    lv, rd, we = (int(x) for x in g[f'rt_{name}_cfg'])
+    out = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(g[f'rt_{name}_origin']),
+                                            T(g[f'rt_{name}_direction']), lv, return_depth=bool(rd),
+                                            with_exit=bool(we))
+    nug = np.stack([A(out[0]), A(out[1])], -1).reshape(-1, 2)
+    assert np.array_equal(nug, g[f'rt_{name}_nuggets'])
+    if rd:
+        np.testing.assert_allclose(A(out[2]), g[f'rt_{name}_depth'], rtol=1e-5, atol=1e-6)
+
+
+def test_raytrace_ambiguous(kal, golden):
+    g = golden('spc.npz')
+    octree, pyr, ex, pts = _rt_setup(kal, g['rt_ambiguous_octree'])
+    r, p, d = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(g['rt_ambiguous_origin']),
+                                                T(g['rt_ambiguous_direction']), 1, return_depth=True)
+    assert np.array_equal(np.stack([A(r), A(p)], -1), g['rt_ambiguous_nuggets'])
+
+
+def test_mark_pack_boundaries_kat(kal, golden):
+    g = golden('spc.npz')
+    octree, pyr, ex, pts = _rt_setup(kal, g['rt_octree'])
+    r, p = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(g['rt_positive_origin']),
+                                             T(g['rt_positive_direction']), 2, return_depth=False)
+    assert np.array_equal(A(kal.render.spc.mark_pack_boundaries(r)), g['rt_positive_first_hits'])
+
+
+@pytest.mark.parametrize('with_exit', [False, True])
+def test_raytrace_vs_oracle_mesh_spc(kal, with_exit):
+    v, f = _uv_sphere(24, 36, 0.8)
+    fv = v[f].astype(np.float32)
+    L = 6
+    octree, _, _ = kal.ops.conversions.unbatched_mesh_to_spc(T(fv), L)
+    octree_np = A(octree)
+    octree, pyr, ex, pts = _rt_setup(kal, octree_np)
+    n = 48
+    ii, jj = np.meshgrid(np.linspace(-0.9, 0.9, n), np.linspace(-0.9, 0.9, n), indexing='ij')
+    origin = np.stack([ii, jj, np.full_like(ii, 3.)], -1).reshape(-1, 3).astype(np.float32)
+    d = np.stack([0.05 * ii, 0.03 * jj, -np.ones_like(ii)], -1).reshape(-1, 3)
+    d = (d / np.linalg.norm(d, axis=-1, keepdims=True)).astype(np.float32)
+    r, p, dep = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(origin), T(d), L, return_depth=True,
+                                                  with_exit=with_exit)
+    onug, odep = orc.raytrace(octree_np, A(pts), pyr.numpy(), A(ex), origin, d, L, True, with_exit)
+    assert np.array_equal(np.stack([A(r), A(p)], -1), onug)
+    assert np.array_equal(A(dep), odep)
+    assert len(onug) > 1000
