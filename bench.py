@@ -1,0 +1,272 @@
+"""bench.py -- DIB-R 512^2 forward+backward throughput (Mpixels/s) on MI355X, plus
+point_to_mesh_distance (Mpairs/s), per BASELINE.json.
+
+Workload (BASELINE.json configs[2]), per rank:
+  UV sphere 126 lat x 200 lon = 50,000 faces, radius 0.9*(1+0.01*N(0,1)) per vertex
+  (seed 0); 4 views (azimuth 90 deg apart, distance 3, look-at 0, up +y, fovy pi/4);
+  features D=3 = [uv, 1]; dibr_rasterization(512, 512, ..., sigmainv=7000,
+  boxlen=0.02, knum=30, multiplier=1000, eps=1e-8); loss = <feat, g_feat> +
+  <soft_mask, g_mask> with g ~ U[0,1] (seed 1); backward to face_vertices_image and
+  face_features.  One step = that forward + backward over the rank's 4 views.
+Multi-GPU: one process per GPU (torchrun); each rank renders its own 4 views of the
+replicated mesh (weak scaling, global batch 4N), per-shard losses are all-gathered
+over RCCL each step; time = max over ranks.
+
+Also reported: p2m (configs[1]: 100k points vs 20k faces, forward) Mpairs/s, the
+roofline of the dominant op (HIP events on its stream over the timed region) and a
+CPU baseline (the C oracle, 1 thread, on a stated row sample of view 0).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'kaolin-windows_amd'))
+sys.path.insert(0, ROOT)
+
+import kaolin as kal  # noqa: E402
+from kaolin import _native  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector peak
+
+
+def uv_sphere(n_lat, n_lon, device, dtype=torch.float32, seed=0):
+    lat = torch.linspace(0, math.pi, n_lat + 1, dtype=torch.float64)[1:-1]
+    lon = torch.arange(n_lon, dtype=torch.float64) * (2 * math.pi / n_lon)
+    ring = torch.stack([torch.sin(lat)[:, None] * torch.cos(lon)[None], torch.cos(lat)[:, None].expand(-1, n_lon),
+                        torch.sin(lat)[:, None] * torch.sin(lon)[None]], -1).reshape(-1, 3)
+    verts = torch.cat([torch.tensor([[0., 1., 0.]], dtype=torch.float64), ring,
+                       torch.tensor([[0., -1., 0.]], dtype=torch.float64)])
+    g = torch.Generator().manual_seed(seed)
+    verts = verts * (0.9 * (1 + 0.01 * torch.randn((verts.shape[0], 1), generator=g, dtype=torch.float64)))
+    nr = n_lat - 1
+    j = torch.arange(n_lon)
+    jn = (j + 1) % n_lon
+    top = torch.stack([torch.zeros_like(j), 1 + jn, 1 + j], -1)
+    i = torch.arange(nr - 1)[:, None]
+    a = 1 + i * n_lon + j
+    b = 1 + i * n_lon + jn
+    c = a + n_lon
+    d = b + n_lon
+    mid = torch.stack([torch.stack([a, b, d], -1), torch.stack([a, d, c], -1)], 2).reshape(-1, 3)
+    last = 1 + nr * n_lon
+    bot = torch.stack([1 + (nr - 1) * n_lon + j, 1 + (nr - 1) * n_lon + jn, torch.full_like(j, last)], -1)
+    faces = torch.cat([top, mid, bot]).to(device)
+    return verts.to(device=device, dtype=dtype), faces
+
+
+def dibr_inputs(views, device, H=512, W=512):
+    verts, faces = uv_sphere(126, 200, device)
+    assert faces.shape[0] == 50000
+    B = len(views)
+    az = torch.tensor(views, dtype=torch.float32, device=device)
+    cam = torch.stack([3 * torch.sin(az), torch.zeros_like(az), 3 * torch.cos(az)], -1)
+    rot, trans = kal.render.camera.generate_rotate_translate_matrices(
+        cam, torch.zeros_like(cam), torch.tensor([[0., 1., 0.]], device=device).repeat(B, 1))
+    v = verts.unsqueeze(0).repeat(B, 1, 1)
+    vc = kal.render.camera.rotate_translate_points(v, rot, trans)
+    proj = kal.render.camera.generate_perspective_projection(math.pi / 4).to(device)
+    vi = kal.render.camera.perspective_camera(vc, proj)
+    fvc = kal.ops.mesh.index_vertices_by_faces(vc, faces)
+    fvz = fvc[..., -1].contiguous()
+    fvi = kal.ops.mesh.index_vertices_by_faces(vi, faces).contiguous()
+    fnz = kal.ops.mesh.face_normals(fvc, unit=True)[..., -1].contiguous()
+    # sphere parametrisation uv + constant 1 (the tutorial's [uv, mask] features)
+    u = torch.atan2(verts[:, 2], verts[:, 0]) / (2 * math.pi) + 0.5
+    vv = torch.acos(torch.clamp(verts[:, 1] / verts.norm(dim=1), -1, 1)) / math.pi
+    vfeat = torch.stack([u, vv, torch.ones_like(u)], -1).unsqueeze(0).repeat(B, 1, 1)
+    feat = kal.ops.mesh.index_vertices_by_faces(vfeat, faces).contiguous()
+    g = torch.Generator(device='cpu').manual_seed(1)
+    g_feat = torch.rand((B, H, W, 3), generator=g).to(device)
+    g_mask = torch.rand((B, H, W), generator=g).to(device)
+    return dict(fvz=fvz, fvi=fvi, feat=feat, fnz=fnz, g_feat=g_feat, g_mask=g_mask, H=H, W=W, F=faces.shape[0])
+
+
+def dibr_step(inp, world):
+    fvi = inp['fvi'].detach().requires_grad_(True)
+    feat = inp['feat'].detach().requires_grad_(True)
+    feats, mask, idx = kal.render.mesh.dibr_rasterization(inp['H'], inp['W'], inp['fvz'], fvi, feat, inp['fnz'],
+                                                          sigmainv=7000, boxlen=0.02, knum=30, multiplier=1000,
+                                                          eps=1e-8)
+    loss = (feats * inp['g_feat']).sum() + (mask * inp['g_mask']).sum()
+    loss.backward()
+    if world > 1:  # per-shard losses all-gathered over RCCL / xGMI
+        out = [torch.empty_like(loss) for _ in range(world)]
+        dist.all_gather(out, loss.detach())
+    return fvi.grad, feat.grad, mask, idx
+
+
+def op_bytes(name, inp, stats):
+    """Algorithmic HBM bytes of one call of each op (SURVEY.md §8d decomposition, fp32)."""
+    B, H, W = inp['fvz'].shape[0], inp['H'], inp['W']
+    F = inp['F']
+    D, K, s = 3, 30, 4
+    px = B * H * W
+    nv = stats['valid_faces']
+    if name == 'dibr_soft_mask_forward_cuda':
+        # read sel (8/px) + faces (fvi 24 + bbox 16) ; write mask + K x (prob 4 + idx 8 + type 1)
+        return px * (8 + s + K * (s + 8 + 1)) + B * F * (6 * s + 4 * s)
+    if name == 'dibr_soft_mask_backward_cuda':
+        # read grad, mask, sel per px + used slots (+ terminator) of uncovered px; write grad (B,F,3,2)
+        return px * (s + s + 8) + stats['slot_reads'] * (8 + s + 1) + B * F * 6 * s * 2
+    if name == 'packed_rasterize_forward_cuda':
+        return px * (8 + 3 * s + D * s) + nv * (3 * s + 6 * s + 4 * s + 3 * D * s)
+    if name == 'rasterize_backward_cuda':
+        return px * (8 + 3 * s + D * s) + B * F * (6 * s + 3 * D * s) * 2
+    return None
+
+
+def timed_loop(fn, steps, world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(inp, row_step):
+    """The C oracle (1 thread) on view 0, every `row_step`-th pixel row: rasterize fwd,
+    soft mask fwd, soft mask bwd, rasterize bwd."""
+    import numpy as np
+    from oracle import oracle as orc
+    A = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    fvz, fvi, feat, fnz = (A(inp[k][:1]) for k in ('fvz', 'fvi', 'feat', 'fnz'))
+    H, W = inp['H'], inp['W']
+    orc.lib().or_set_row_step(row_step)
+    try:
+        t0 = time.perf_counter()
+        of, oi, ow = orc.rasterize(H, W, fvz, fvi, feat, valid_faces=fnz >= 0)
+        fm, bb = orc.soft_mask_bboxes(fvi, 0.02, 1000.)
+        om, op, oci, oct_ = orc.dibr_soft_mask_forward(fm, bb, oi, 7000., 30, 1000.)
+        orc.dibr_soft_mask_backward(np.ones_like(om), om, oi, op, oci, oct_, fm, 7000., 1000.)
+        orc.rasterize_backward(np.ones_like(of), oi, ow, fvi, feat, 1e-8)
+        dt = time.perf_counter() - t0
+    finally:
+        orc.lib().or_set_row_step(1)
+    rows = len(range(0, H, row_step))
+    return rows * W / dt / 1e6, rows * W, dt
+
+
+def p2m_bench(device, steps):
+    g = torch.Generator().manual_seed(0)
+    pts = torch.randn((100000, 3), generator=g).to(device)
+    fv = torch.randn((20000, 3, 3), generator=g).to(device)
+    d = torch.empty(100000, device=device)
+    i = torch.empty(100000, dtype=torch.long, device=device)
+    t = torch.empty(100000, dtype=torch.int32, device=device)
+    f = lambda: kal._C.metrics.unbatched_triangle_distance_forward_cuda(pts, fv, d, i, t)  # noqa: E731
+    f()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(steps):
+        f()
+    e.record()
+    torch.cuda.synchronize()
+    ms = s.elapsed_time(e) / steps
+    return 100000 * 20000 / (ms * 1e-3) / 1e6, ms
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--cpu-row-step', type=int, default=8)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-p2m', action='store_true')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl')
+    device = torch.device('cuda', local if world > 1 else 0)
+    torch.cuda.set_device(device)
+
+    views_per_rank = 4
+    views = [2 * math.pi * (rank * views_per_rank + k) / (views_per_rank * world) for k in range(views_per_rank)]
+    inp = dibr_inputs(views, device)
+    step = lambda: dibr_step(inp, world)  # noqa: E731
+    for _ in range(args.warmup):
+        step()
+    # workload statistics for the algorithmic byte counts
+    with torch.no_grad():
+        _, fidx = kal.render.mesh.rasterize(inp['H'], inp['W'], inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'] >= 0)
+        fm = inp['fvi'] * 1000.
+        bb = torch.cat([fm.min(-2)[0] - 20., fm.max(-2)[0] + 20.], -1).contiguous()
+        _, _, cidx, _ = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, fidx, 7000., 30, 1000.)
+        unc = fidx < 0
+        used = (cidx >= 0).sum(-1)
+        slot_reads = int((torch.clamp(used + 1, max=30) * unc).sum())
+        stats = dict(valid_faces=int((inp['fnz'] >= 0).sum()), slot_reads=slot_reads,
+                     uncovered=float(unc.float().mean()), mean_slots=float(used[unc].float().mean()))
+    timer = _native.OpTimer()
+    _native.set_timer(timer)
+    elapsed = timed_loop(step, args.steps, world)
+    _native.set_timer(None)
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    ops_ms = timer.summary_ms()
+    pixels = views_per_rank * inp['H'] * inp['W'] * world * args.steps
+    value = pixels / elapsed / 1e6
+    result = None
+    if rank == 0:
+        dom = max(ops_ms, key=ops_ms.get)
+        dbytes = op_bytes(dom, inp, stats)
+        achieved = dbytes / (ops_ms[dom] * 1e-3) / 1e9
+        ops_report = {k: {'ms': round(v, 4), 'GB/s': (round(op_bytes(k, inp, stats) / (v * 1e-3) / 1e9, 1)
+                                                     if op_bytes(k, inp, stats) else None)}
+                      for k, v in ops_ms.items()}
+        result = {
+            'metric': 'DIB-R 512^2 fwd+bwd Mpixels/s + point_to_mesh Mpairs/s, 1/2/4/8 GPU',
+            'value': round(value, 2), 'unit': 'Mpixels/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded UV sphere, 4 views/GPU)',
+            'config': {'workload': 'dibr_rasterization fwd+bwd, batch=4/GPU, 50k-face mesh, 512x512, K=30',
+                       'global_batch': views_per_rank * world, 'height': 512, 'width': 512, 'faces': 50000,
+                       'parallelism': f'batch-sharded x{world} (RCCL all_gather of per-shard losses)'},
+            'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'bytes_per_launch': dbytes, 'avg_launch_ms': round(ops_ms[dom], 4)},
+            'ops': ops_report,
+            'workload_stats': stats,
+        }
+    if not args.no_p2m and rank == 0:
+        mp, ms = p2m_bench(device, max(3, args.steps // 4))
+        result['p2m'] = {'metric': 'point_to_mesh Mpairs/s (100k pts x 20k faces, fwd)', 'value': round(mp, 1),
+                         'ms': round(ms, 3),
+                         'roofline': {'bound': 'valu', 'flop_per_pair': 50,
+                                      'achieved_tflops': round(mp * 1e6 * 50 / 1e12, 2),
+                                      'peak_tflops': FP32_PEAK_TFLOPS,
+                                      'frac': round(mp * 1e6 * 50 / 1e12 / FP32_PEAK_TFLOPS, 4)}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rate, npx, dt = cpu_baseline(inp, args.cpu_row_step)
+        result['cpu_baseline'] = {'value': round(rate, 5), 'unit': 'Mpixels/s', 'cores': 1, 'kind': 'port',
+                                  'sample': f'C oracle, view 0, every {args.cpu_row_step}th row of 512x512 '
+                                            f'({npx} px, fwd+bwd, {dt:.1f} s)'}
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -59,7 +59,7 @@ def packed_rasterize_forward_cuda(height, width, face_vertices_z, face_vertices_
     lib = N.lib()
     ws_bytes = lib.kl_rasterize_workspace_bytes(batch_size, height, width, maxf)
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev):
+    with torch.cuda.device(dev), N.timed(func, dev):
         N.check(lib.kl_packed_rasterize_forward(
             N.dtype_code(dtype), height, width, batch_size, num_faces, feat_dim, maxf,
             N.ptr(face_vertices_z), N.ptr(face_vertices_image), N.ptr(face_bboxes), N.ptr(face_features),
@@ -91,7 +91,7 @@ def rasterize_backward_cuda(grad_interpolated_features, interpolated_features, s
     dev = face_vertices_image.device
     g_img = torch.empty_like(face_vertices_image)
     g_feat = torch.empty_like(face_features)
-    with torch.cuda.device(dev):
+    with torch.cuda.device(dev), N.timed(func, dev):
         N.check(N.lib().kl_rasterize_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, N.ptr(grad_interpolated_features),
             N.ptr(selected_face_idx), N.ptr(output_weights), N.ptr(face_vertices_image), N.ptr(face_features),
@@ -124,7 +124,7 @@ def dibr_soft_mask_forward_cuda(face_vertices_image, face_large_bboxes, selected
     lib = N.lib()
     ws_bytes = lib.kl_soft_mask_workspace_bytes(B, H, W, F)
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev):
+    with torch.cuda.device(dev), N.timed(func, dev):
         N.check(lib.kl_dibr_soft_mask_forward(
             N.dtype_code(dtype), B, H, W, F, K, N.ptr(face_vertices_image), N.ptr(face_large_bboxes),
             N.ptr(selected_face_idx), float(sigmainv), float(multiplier), N.ptr(soft_mask), N.ptr(prob),
@@ -156,7 +156,7 @@ def dibr_soft_mask_backward_cuda(grad_soft_mask, soft_mask, selected_face_idx, c
     N.require_gpu(func, face_vertices_image)
     dev = face_vertices_image.device
     g = torch.empty_like(face_vertices_image)
-    with torch.cuda.device(dev):
+    with torch.cuda.device(dev), N.timed(func, dev):
         N.check(N.lib().kl_dibr_soft_mask_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, K, N.ptr(grad_soft_mask), N.ptr(soft_mask),
             N.ptr(selected_face_idx.contiguous()), N.ptr(close_face_prob), N.ptr(close_face_idx),
@@ -182,7 +182,7 @@ def unbatched_triangle_distance_forward_cuda(points, face_vertices, dist, face_i
     _float_only(func, points)
     N.require_gpu(func, points)
     dev = points.device
-    with torch.cuda.device(dev):
+    with torch.cuda.device(dev), N.timed(func, dev):
         N.check(N.lib().kl_unbatched_triangle_distance_forward(
             N.dtype_code(points.dtype), P, F, N.ptr(points), N.ptr(face_vertices), N.ptr(dist), N.ptr(face_idx),
             N.ptr(dist_type), N.stream_of(dev)), func)
@@ -208,7 +208,7 @@ def unbatched_triangle_distance_backward_cuda(grad_dist, points, face_vertices, 
     _float_only(func, points)
     N.require_gpu(func, points)
     dev = points.device
-    with torch.cuda.device(dev):
+    with torch.cuda.device(dev), N.timed(func, dev):
         N.check(N.lib().kl_unbatched_triangle_distance_backward(
             N.dtype_code(points.dtype), P, F, N.ptr(grad_dist), N.ptr(points), N.ptr(face_vertices),
             N.ptr(face_idx), N.ptr(dist_type), N.ptr(grad_points), N.ptr(grad_face_vertices), N.stream_of(dev)),
@@ -230,7 +230,7 @@ def sided_distance_forward_cuda(p1, p2):
     dev = p1.device
     dist = torch.empty((B, N1), dtype=p1.dtype, device=dev)
     idx = torch.empty((B, N1), dtype=torch.long, device=dev)
-    with torch.cuda.device(dev):
+    with torch.cuda.device(dev), N.timed(func, dev):
         N.check(N.lib().kl_sided_distance_forward(N.dtype_code(p1.dtype), B, N1, N2, N.ptr(p1), N.ptr(p2),
                                                   N.ptr(dist), N.ptr(idx), N.stream_of(dev)), func)
     return [dist, idx]
@@ -251,7 +251,7 @@ def sided_distance_backward_cuda(grad_output, p1, p2, idx):
     dev = p1.device
     g1 = torch.empty_like(p1)
     g2 = torch.empty_like(p2)
-    with torch.cuda.device(dev):
+    with torch.cuda.device(dev), N.timed(func, dev):
         N.check(N.lib().kl_sided_distance_backward(N.dtype_code(p1.dtype), B, N1, N2, N.ptr(grad_output),
                                                    N.ptr(p1), N.ptr(p2), N.ptr(idx), N.ptr(g1), N.ptr(g2),
                                                    N.stream_of(dev)), func)

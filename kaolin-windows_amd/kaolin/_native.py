@@ -4,6 +4,7 @@ There is no fallback: if the library is missing or no HIP device is present, eve
 hot-path op raises.  The library is loaded from this package's ``_lib`` directory
 (built in-tree by ``__graft_entry__.build()`` / ``make -C kaolin-windows_amd/csrc``).
 """
+import contextlib
 import ctypes
 import os
 
@@ -136,3 +137,44 @@ class Arena:
         base = self.by_ptr[p]
         esize = torch.empty((), dtype=dtype).element_size()
         return base[:numel * esize].view(dtype).reshape(shape)
+
+
+# ----------------------------------------------------------------- op timing
+class OpTimer:
+    """HIP-event timing of every native op call on the stream it is launched on
+    (enabled by bench.py over its timed region)."""
+
+    def __init__(self):
+        self.records = {}
+
+    def add(self, name, start, end):
+        self.records.setdefault(name, []).append((start, end))
+
+    def summary_ms(self):
+        torch.cuda.synchronize()
+        return {k: sum(s.elapsed_time(e) for s, e in v) / len(v) for k, v in self.records.items()}
+
+    def counts(self):
+        return {k: len(v) for k, v in self.records.items()}
+
+
+_TIMER = None
+
+
+def set_timer(timer):
+    global _TIMER
+    _TIMER = timer
+
+
+@contextlib.contextmanager
+def timed(name, device):
+    if _TIMER is None:
+        yield
+        return
+    st = torch.cuda.current_stream(device)
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record(st)
+    yield
+    e.record(st)
+    _TIMER.add(name, s, e)

@@ -24,6 +24,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* Pixel-row sampling for bench.py's cpu_baseline leg: the DIB-R loops process only
+ * rows j with j % g_row_step == 0 (default 1 = every row). */
+static int g_row_step = 1;
+void or_set_row_step(int s) { g_row_step = s > 0 ? s : 1; }
+
 #define T float
 #define SUF f32
 #include "oracle_typed.inc"
