@@ -81,6 +81,27 @@ int kl_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int 
                           void *grad_face_vertices_image, void *grad_face_features,
                           kl_stream stream);
 
+/* Fused front-end path of rasterize() / RasterizeCuda (rasterization.py:290-388): takes the
+ * UNPACKED (B,F) inputs and the optional (B,F) valid mask (uint8/bool) directly, applies
+ * the multiplier and the bboxes in-kernel with the front-end's own float ops, and writes
+ * the ORIGINAL per-mesh face index (what RasterizeCuda.forward returns after its remap).
+ * face_vertices_image (B,F,3,2) unscaled; outputs as kl_packed_rasterize_forward. */
+size_t kl_dibr_rasterize_workspace_bytes(int batch, int height, int width, int num_faces);
+int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, int batch, int num_faces, int feat_dim,
+                              const void *face_vertices_z, const void *face_vertices_image,
+                              const void *face_features, const uint8_t *valid_faces, float multiplier, float eps,
+                              void *interpolated_features, int64_t *face_idx, void *output_weights,
+                              void *workspace, size_t workspace_bytes, kl_stream stream);
+/* Atomic-free backward of the fused path: one thread per face gathers the pixels of its
+ * conservative screen bbox whose face_idx equals it (deterministic, row-major order).
+ * Requires face_idx produced by the forward (faces are only selected inside their bbox). */
+int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
+                               const void *grad_interpolated_features, const int64_t *face_idx,
+                               const void *output_weights, const void *face_vertices_image,
+                               const void *face_features, float eps, void *grad_face_vertices_image,
+                               void *grad_face_features, void *workspace, size_t workspace_bytes,
+                               kl_stream stream);
+
 size_t kl_soft_mask_workspace_bytes(int batch, int height, int width, int num_faces);
 
 /* dibr_soft_mask.cpp:48-108  dibr_soft_mask_forward_cuda.
@@ -93,6 +114,23 @@ int kl_dibr_soft_mask_forward(kl_dtype dtype, int batch, int height, int width, 
                               void *soft_mask, void *close_face_prob, int64_t *close_face_idx,
                               uint8_t *close_face_dist_type, void *workspace, size_t workspace_bytes,
                               kl_stream stream);
+
+/* Fused front-end path of DibrSoftMaskCuda (dibr.py:27-73): face_vertices_image UNSCALED;
+ * `face_vertices_image * multiplier` and the enlarged bboxes (min/max -/+ bbox_pad) are
+ * evaluated in-kernel with the front-end's float ops.  bbox_pad = boxlen * multiplier as
+ * the caller's double-precision product (the front-end's python-float expression). */
+int kl_dibr_soft_mask_forward_fused(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
+                                    const void *face_vertices_image, const int64_t *selected_face_idx,
+                                    float sigmainv, double bbox_pad, float multiplier, void *soft_mask,
+                                    void *close_face_prob, int64_t *close_face_idx,
+                                    uint8_t *close_face_dist_type, void *workspace, size_t workspace_bytes,
+                                    kl_stream stream);
+int kl_dibr_soft_mask_backward_fused(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
+                                     const void *grad_soft_mask, const void *soft_mask,
+                                     const int64_t *selected_face_idx, const void *close_face_prob,
+                                     const int64_t *close_face_idx, const uint8_t *close_face_dist_type,
+                                     const void *face_vertices_image, float sigmainv, float multiplier,
+                                     void *grad_face_vertices_image, kl_stream stream);
 
 /* dibr_soft_mask.cpp:110-183  dibr_soft_mask_backward_cuda.
  * Output grad_face_vertices_image (B,F,3,2) (fully written). */

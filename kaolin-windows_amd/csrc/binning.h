@@ -10,6 +10,13 @@
 // Bit setting is an idempotent atomicOr, so bins are deterministic.
 //
 // Tiles are TILE_W x TILE_H pixels (one wave = one 64-pixel row segment).
+//
+// Face sources (how a consumer obtains a face's bbox in multiplied coordinates):
+//   BboxSrc     explicit (N,4) bboxes (the reference's packed / soft-mask _C inputs);
+//   RastSrc     min/max of face_vertices_image * m, optional valid mask (fused path);
+//   SoftSrc     min/max of face_vertices_image * m -/+ boxlen*m (fused path).
+// The fused sources evaluate exactly the reference front-end's torch expressions
+// (rasterization.py:337-344, dibr.py:31-39), so bins and walks see identical values.
 #pragma once
 
 #include "common.h"
@@ -39,6 +46,80 @@ inline BinGeom make_bin_geom(int batch, int height, int width, int64_t max_faces
   return g;
 }
 
+template <typename T>
+struct BboxSrc {
+  const T *bbox;  // (N,4)
+  const T *fvi;   // (N,3,2) already x multiplier
+  __device__ __forceinline__ bool valid(int64_t) const { return true; }
+  __device__ __forceinline__ void verts(int64_t f, T v[6]) const {
+#pragma unroll
+    for (int q = 0; q < 6; q++) v[q] = fvi[f * 6 + q];
+  }
+  __device__ __forceinline__ void get(int64_t f, T &x0, T &y0, T &x1, T &y1) const {
+    const T *b = bbox + f * 4;
+    x0 = b[0];
+    y0 = b[1];
+    x1 = b[2];
+    y1 = b[3];
+  }
+};
+
+// min / max over the three vertices as torch.min / torch.max(dim) (NaN propagates)
+template <typename T>
+__device__ __forceinline__ T tmin3(T a, T b, T c) {
+  T r = a;
+  if (b < r || b != b) r = (r != r) ? r : b;
+  if (c < r || c != c) r = (r != r) ? r : c;
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ T tmax3(T a, T b, T c) {
+  T r = a;
+  if (b > r || b != b) r = (r != r) ? r : b;
+  if (c > r || c != c) r = (r != r) ? r : c;
+  return r;
+}
+
+template <typename T>
+struct RastSrc {
+  const T *fvi;          // (B*F,3,2) unscaled
+  const uint8_t *vmask;  // (B*F) valid faces, or nullptr = all valid
+  T m;
+  __device__ __forceinline__ bool valid(int64_t f) const { return vmask == nullptr || vmask[f] != 0; }
+  __device__ __forceinline__ void verts(int64_t f, T v[6]) const {
+#pragma unroll
+    for (int q = 0; q < 6; q++) v[q] = fvi[f * 6 + q] * m;
+  }
+  __device__ __forceinline__ void get(int64_t f, T &x0, T &y0, T &x1, T &y1) const {
+    const T *v = fvi + f * 6;
+    const T ax = v[0] * m, ay = v[1] * m, bx = v[2] * m, by = v[3] * m, cx = v[4] * m, cy = v[5] * m;
+    x0 = tmin3(ax, bx, cx);
+    y0 = tmin3(ay, by, cy);
+    x1 = tmax3(ax, bx, cx);
+    y1 = tmax3(ay, by, cy);
+  }
+};
+
+template <typename T>
+struct SoftSrc {
+  const T *fvi;  // (B*F,3,2) unscaled
+  T m;
+  T pad;         // (T)(boxlen * multiplier), the python-float product cast to the tensor dtype
+  __device__ __forceinline__ bool valid(int64_t) const { return true; }
+  __device__ __forceinline__ void verts(int64_t f, T v[6]) const {
+#pragma unroll
+    for (int q = 0; q < 6; q++) v[q] = fvi[f * 6 + q] * m;
+  }
+  __device__ __forceinline__ void get(int64_t f, T &x0, T &y0, T &x1, T &y1) const {
+    const T *v = fvi + f * 6;
+    const T ax = v[0] * m, ay = v[1] * m, bx = v[2] * m, by = v[3] * m, cx = v[4] * m, cy = v[5] * m;
+    x0 = tmin3(ax, bx, cx) - pad;
+    y0 = tmin3(ay, by, cy) - pad;
+    x1 = tmax3(ax, bx, cx) + pad;
+    y1 = tmax3(ay, by, cy) + pad;
+  }
+};
+
 // Conservative pixel-index interval [lo, hi] whose centres c(i) = s * (2i + 1 - N)
 // (s = m / N, float) may satisfy  vmin <= c(i) < vmax  (x axis; the y axis calls it
 // with the flipped centre formula).  Any NaN bound => the reference's comparisons are
@@ -60,23 +141,27 @@ __device__ __forceinline__ void axis_range(double vmin, double vmax, double s, i
     ia = (n - 1 - b) * 0.5;
     ib = (n - 1 - a) * 0.5;
   }
+  if (!(ib >= -2.0) || !(ia <= (double)n + 1.0)) {  // entirely off screen (also +-inf)
+    lo = 1;
+    hi = 0;
+    return;
+  }
   double l = floor(ia) - 1.0, h = ceil(ib) + 1.0;
   if (l < 0.0) l = 0.0;
   if (h > (double)(n - 1)) h = (double)(n - 1);
-  if (l > h || ib < -2.0 || ia > (double)n + 1.0) {
+  if (l > h) {
     lo = 1;
-    hi = 0;  // empty
+    hi = 0;
     return;
   }
   lo = (int)l;
   hi = (int)h;
 }
 
-// One wave per (mesh b, chunk c).  bboxes: (total,4) [xmin,ymin,xmax,ymax] (x multiplier).
-// Mesh b owns faces [first(b), last(b)).  first_idx == nullptr => uniform meshes of F faces.
-template <typename T>
-__global__ void __launch_bounds__(256) bin_faces_kernel(const T *__restrict__ bboxes,
-                                                        const int64_t *__restrict__ first_idx,
+// One wave per (mesh b, chunk c).  Mesh b owns faces [first(b), last(b)) of the source.
+// first_idx == nullptr => uniform meshes of `faces_per_mesh` faces.
+template <typename T, typename Src>
+__global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *__restrict__ first_idx,
                                                         int faces_per_mesh, BinGeom g, float m,
                                                         uint32_t *__restrict__ bitmap) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -96,12 +181,13 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(const T *__restrict__ bb
   if (base >= f1) return;
   const int64_t f = base + lane;
   int tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
-  if (f < f1) {
-    const T *bb = bboxes + f * 4;
+  if (f < f1 && src.valid(f)) {
+    T bx0, by0, bx1, by1;
+    src.get(f, bx0, by0, bx1, by1);
     int ix0, ix1, iy0, iy1;
     const double sx = (double)(m / (float)g.width), sy = (double)(m / (float)g.height);
-    axis_range((double)bb[0], (double)bb[2], sx, g.width, false, ix0, ix1);
-    axis_range((double)bb[1], (double)bb[3], sy, g.height, true, iy0, iy1);
+    axis_range((double)bx0, (double)bx1, sx, g.width, false, ix0, ix1);
+    axis_range((double)by0, (double)by1, sy, g.height, true, iy0, iy1);
     if (ix0 <= ix1 && iy0 <= iy1) {
       tx0 = ix0 / TILE_W;
       tx1 = ix1 / TILE_W;
@@ -130,12 +216,12 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(const T *__restrict__ bb
   }
 }
 
-template <typename T>
-inline int launch_binning(const T *bboxes, const int64_t *first_idx, int faces_per_mesh, const BinGeom &g,
-                          float m, uint32_t *bitmap, hipStream_t st) {
+template <typename T, typename Src>
+inline int launch_binning(Src src, const int64_t *first_idx, int faces_per_mesh, const BinGeom &g, float m,
+                          uint32_t *bitmap, hipStream_t st) {
   KL_CHECK_HIP(hipMemsetAsync(bitmap, 0, g.bytes(), st));
   dim3 grid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)g.batch);
-  hipLaunchKernelGGL(bin_faces_kernel<T>, grid, dim3(256), 0, st, bboxes, first_idx, faces_per_mesh, g, m,
+  hipLaunchKernelGGL((bin_faces_kernel<T, Src>), grid, dim3(256), 0, st, src, first_idx, faces_per_mesh, g, m,
                      bitmap);
   KL_CHECK_LAUNCH();
   return KL_OK;

@@ -59,9 +59,9 @@ __device__ __forceinline__ void soft_dist(T x0, T y0, const T v[6], float multip
 }
 
 // LDS per wave: code[K][64] (face << 3 | type) + prob[K][64] + kid[64]
-template <typename T>
+template <typename T, typename Src>
 __global__ void __launch_bounds__(128) soft_mask_fwd_kernel(
-    const T *__restrict__ fvi, const T *__restrict__ bboxes, const int64_t *__restrict__ sel,
+    Src src, const int64_t *__restrict__ sel,
     const uint32_t *__restrict__ bitmap, BinGeom g, int F, int K, float sigmainv, float multiplier,
     T *__restrict__ out_mask, T *__restrict__ out_prob, int64_t *__restrict__ out_idx,
     uint8_t *__restrict__ out_type) {
@@ -103,19 +103,12 @@ __global__ void __launch_bounds__(128) soft_mask_fwd_kernel(
       const int fl = c * 64 + lane;  // face index within the mesh
       const bool fv = fl < F;
       T bx0 = 0, by0 = 0, bx1 = 0, by1 = 0;
-      if (fv) {
-        const T *bb = bboxes + (f0 + fl) * 4;
-        bx0 = bb[0]; by0 = bb[1]; bx1 = bb[2]; by1 = bb[3];
-      }
+      if (fv) src.get(f0 + fl, bx0, by0, bx1, by1);
       const bool touch = fv && !(y0 < by0 || y0 >= by1 || sxhi < bx0 || sxlo >= bx1);
       uint64_t mask = ballot(touch);
       if (!mask) continue;
       T v[6] = {0, 0, 0, 0, 0, 0};
-      if (touch) {
-        const T *vv = fvi + (f0 + fl) * 6;
-#pragma unroll
-        for (int q = 0; q < 6; q++) v[q] = vv[q];
-      }
+      if (touch) src.verts(f0 + fl, v);
       while (mask) {
         const int s = __builtin_ctzll(mask);
         mask &= mask - 1;
@@ -167,12 +160,16 @@ __global__ void __launch_bounds__(128) soft_mask_fwd_kernel(
   }
 }
 
-template <typename T>
+template <typename T, bool SCALE>
 __global__ void __launch_bounds__(256) soft_mask_bwd_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const int64_t *__restrict__ sel,
     const T *__restrict__ prob, const int64_t *__restrict__ cidx, const uint8_t *__restrict__ ctype,
     const T *__restrict__ fvi, int B, int H, int W, int F, int K, float sigmainv, float multiplier,
     T *__restrict__ gfvi) {
+  // SCALE: fvi holds unscaled coordinates, multiplied here exactly as the front-end's
+  // `face_vertices_image * multiplier` (dibr.py:31) would have
+  const T ms = (T)multiplier;
+  auto V = [&](size_t k) -> T { return SCALE ? fvi[k] * ms : fvi[k]; };
   const int64_t npix = (int64_t)H * W;
   for (int64_t tp = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; tp < (int64_t)B * npix;
        tp += (int64_t)gridDim.x * blockDim.x) {
@@ -195,14 +192,14 @@ __global__ void __launch_bounds__(256) soft_mask_bwd_kernel(
       const int edgeid = (int)ctype[pk + k] - 1;
       if (edgeid >= 3) {
         const size_t ps = s6 + (edgeid - 3) * 2;
-        const T x1 = fvi[ps], y1 = fvi[ps + 1];
+        const T x1 = V(ps), y1 = V(ps + 1);
         const T dLdx1 = dLdz * (T)2 * (x1 - x0);
         const T dLdy1 = dLdz * (T)2 * (y1 - y0);
         atomicAdd(gfvi + ps + 0, dLdx1 / (T)multiplier);
         atomicAdd(gfvi + ps + 1, dLdy1 / (T)multiplier);
       } else {
         const size_t ps = s6 + edgeid * 2, ps2 = s6 + ((edgeid + 1) % 3) * 2;
-        const T x1 = fvi[ps], y1 = fvi[ps + 1], x2 = fvi[ps2], y2 = fvi[ps2 + 1];
+        const T x1 = V(ps), y1 = V(ps + 1), x2 = V(ps2), y2 = V(ps2 + 1);
         const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
         const T up = A * x0 + Bc * y0 + C;
         const T down = A * A + Bc * Bc;
@@ -228,30 +225,30 @@ static size_t sm_lds_per_wave(int K) {
   return (size_t)K * 64 * (sizeof(uint32_t) + sizeof(T)) + 64 * sizeof(int);
 }
 
-template <typename T>
-static int soft_mask_fwd(int B, int H, int W, int F, int K, const void *fvi, const void *bbox,
-                         const int64_t *sel, float sigmainv, float m, void *mask, void *prob, int64_t *cidx,
-                         uint8_t *ctype, void *ws, size_t ws_bytes, hipStream_t st) {
+template <typename T, typename Src>
+static int soft_mask_fwd(Src src, int B, int H, int W, int F, int K, const int64_t *sel, float sigmainv, float m,
+                         void *mask, void *prob, int64_t *cidx, uint8_t *ctype, void *ws, size_t ws_bytes,
+                         hipStream_t st) {
   BinGeom g = make_bin_geom(B, H, W, F);
   KL_REQUIRE(ws_bytes >= g.bytes(), "dibr_soft_mask_forward: workspace too small");
   KL_REQUIRE(K >= 0, "dibr_soft_mask_forward: knum must be >= 0");
-  KL_REQUIRE((int64_t)F * 64 < (1ll << 29) * 64, "dibr_soft_mask_forward: too many faces");
+  KL_REQUIRE(F < (1 << 28), "dibr_soft_mask_forward: too many faces");
   if (B == 0 || H == 0 || W == 0) return KL_OK;
   uint32_t *bitmap = reinterpret_cast<uint32_t *>(ws);
-  int rc = launch_binning<T>((const T *)bbox, nullptr, F, g, m, bitmap, st);
+  int rc = launch_binning<T, Src>(src, nullptr, F, g, m, bitmap, st);
   if (rc) return rc;
   const size_t pw = sm_lds_per_wave<T>(K);
   int waves = 2;
   if (pw * 2 > 160 * 1024) waves = 1;
   KL_REQUIRE(pw * waves <= 160 * 1024, "dibr_soft_mask_forward: knum too large for the LDS staging buffer");
   dim3 grid(g.tiles_x, (unsigned)cdiv(H, waves), B);
-  hipLaunchKernelGGL(soft_mask_fwd_kernel<T>, grid, dim3(64 * waves), pw * waves, st, (const T *)fvi,
-                     (const T *)bbox, sel, bitmap, g, F, K, sigmainv, m, (T *)mask, (T *)prob, cidx, ctype);
+  hipLaunchKernelGGL((soft_mask_fwd_kernel<T, Src>), grid, dim3(64 * waves), pw * waves, st, src, sel, bitmap, g, F, K,
+                     sigmainv, m, (T *)mask, (T *)prob, cidx, ctype);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
 
-template <typename T>
+template <typename T, bool SCALE>
 static int soft_mask_bwd(int B, int H, int W, int F, int K, const void *grad, const void *mask,
                          const int64_t *sel, const void *prob, const int64_t *cidx, const uint8_t *ctype,
                          const void *fvi, float sigmainv, float m, void *gfvi, hipStream_t st) {
@@ -259,8 +256,9 @@ static int soft_mask_bwd(int B, int H, int W, int F, int K, const void *grad, co
   const int64_t total = (int64_t)B * H * W;
   if (total == 0) return KL_OK;
   const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(total, 256), 65536);
-  hipLaunchKernelGGL(soft_mask_bwd_kernel<T>, dim3(blocks), dim3(256), 0, st, (const T *)grad, (const T *)mask,
-                     sel, (const T *)prob, cidx, ctype, (const T *)fvi, B, H, W, F, K, sigmainv, m, (T *)gfvi);
+  hipLaunchKernelGGL((soft_mask_bwd_kernel<T, SCALE>), dim3(blocks), dim3(256), 0, st, (const T *)grad,
+                     (const T *)mask, sel, (const T *)prob, cidx, ctype, (const T *)fvi, B, H, W, F, K, sigmainv, m,
+                     (T *)gfvi);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
@@ -279,12 +277,31 @@ extern "C" int kl_dibr_soft_mask_forward(kl_dtype dtype, int batch, int height, 
                                          int64_t *cidx, uint8_t *ctype, void *ws, size_t ws_bytes,
                                          kl_stream stream) {
   if (dtype == KL_F32)
-    return soft_mask_fwd<float>(batch, height, width, num_faces, knum, fvi, bbox, sel, sigmainv, multiplier, mask,
-                                prob, cidx, ctype, ws, ws_bytes, S(stream));
+    return soft_mask_fwd<float>(BboxSrc<float>{(const float *)bbox, (const float *)fvi}, batch, height, width,
+                                num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype, ws, ws_bytes,
+                                S(stream));
   if (dtype == KL_F64)
-    return soft_mask_fwd<double>(batch, height, width, num_faces, knum, fvi, bbox, sel, sigmainv, multiplier,
-                                 mask, prob, cidx, ctype, ws, ws_bytes, S(stream));
+    return soft_mask_fwd<double>(BboxSrc<double>{(const double *)bbox, (const double *)fvi}, batch, height, width,
+                                 num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype, ws, ws_bytes,
+                                 S(stream));
   set_error("dibr_soft_mask_forward_cuda not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_dibr_soft_mask_forward_fused(kl_dtype dtype, int batch, int height, int width, int num_faces,
+                                               int knum, const void *fvi, const int64_t *sel, float sigmainv,
+                                               double pad, float multiplier, void *mask, void *prob,
+                                               int64_t *cidx, uint8_t *ctype, void *ws, size_t ws_bytes,
+                                               kl_stream stream) {
+  if (dtype == KL_F32)
+    return soft_mask_fwd<float>(SoftSrc<float>{(const float *)fvi, (float)multiplier, (float)pad}, batch, height,
+                                width, num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype, ws,
+                                ws_bytes, S(stream));
+  if (dtype == KL_F64)
+    return soft_mask_fwd<double>(SoftSrc<double>{(const double *)fvi, (double)multiplier, pad}, batch, height, width,
+                                 num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype, ws, ws_bytes,
+                                 S(stream));
+  set_error("dibr_soft_mask_forward not implemented for this dtype");
   return KL_E_INVALID;
 }
 
@@ -294,11 +311,26 @@ extern "C" int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height,
                                           const void *fvi, float sigmainv, float multiplier, void *gfvi,
                                           kl_stream stream) {
   if (dtype == KL_F32)
-    return soft_mask_bwd<float>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype, fvi,
-                                sigmainv, multiplier, gfvi, S(stream));
+    return soft_mask_bwd<float, false>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype, fvi,
+                                       sigmainv, multiplier, gfvi, S(stream));
   if (dtype == KL_F64)
-    return soft_mask_bwd<double>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype, fvi,
-                                 sigmainv, multiplier, gfvi, S(stream));
+    return soft_mask_bwd<double, false>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype,
+                                        fvi, sigmainv, multiplier, gfvi, S(stream));
   set_error("dibr_soft_mask_backward_cuda not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_dibr_soft_mask_backward_fused(kl_dtype dtype, int batch, int height, int width, int num_faces,
+                                                int knum, const void *grad, const void *mask, const int64_t *sel,
+                                                const void *prob, const int64_t *cidx, const uint8_t *ctype,
+                                                const void *fvi, float sigmainv, float multiplier, void *gfvi,
+                                                kl_stream stream) {
+  if (dtype == KL_F32)
+    return soft_mask_bwd<float, true>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype, fvi,
+                                      sigmainv, multiplier, gfvi, S(stream));
+  if (dtype == KL_F64)
+    return soft_mask_bwd<double, true>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype,
+                                       fvi, sigmainv, multiplier, gfvi, S(stream));
+  set_error("dibr_soft_mask_backward not implemented for this dtype");
   return KL_E_INVALID;
 }

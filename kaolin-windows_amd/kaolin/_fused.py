@@ -1,0 +1,109 @@
+"""Fused DIB-R entry points used by the front-ends (not part of the reference's _C registry).
+
+The reference front-ends run ~10 PyTorch ops around each native call: valid-face
+packing with ``torch.where`` (a host sync), gathers, ``* multiplier``, bbox min/max/cat,
+a cumsum for ``first_idx`` and a packed->original index remap (rasterization.py:309-367,
+dibr.py:31-39).  These entry points take the unpacked inputs and do all of it inside
+the HIP kernels with the same float operations, so the results are identical to the
+unfused chain (tests/test_gpu_parity.py checks both against the oracle).
+"""
+import torch
+
+from . import _native as N
+
+
+def _ws(nbytes, device):
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+
+
+def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_features, valid_faces, multiplier,
+                      eps):
+    """-> interpolated_features (B,H,W,D), face_idx (B,H,W) original index, output_weights (B,H,W,3)."""
+    func = 'rasterize'
+    N.require_gpu(func, face_vertices_z)
+    B, F = face_vertices_z.shape[:2]
+    D = face_features.shape[-1]
+    dev = face_vertices_z.device
+    dtype = face_vertices_z.dtype
+    if dtype not in (torch.float32, torch.float64):
+        raise RuntimeError(f'"{func}" not implemented for {dtype}')
+    fvz = face_vertices_z.contiguous()
+    fvi = face_vertices_image.contiguous()
+    feat = face_features.contiguous()
+    valid = None
+    if valid_faces is not None:
+        valid = valid_faces.contiguous()
+        valid = valid.view(torch.uint8) if valid.dtype == torch.bool else (valid != 0).view(torch.uint8)
+    feats = torch.empty((B, height, width, D), dtype=dtype, device=dev)
+    idx = torch.empty((B, height, width), dtype=torch.long, device=dev)
+    w = torch.empty((B, height, width, 3), dtype=dtype, device=dev)
+    lib = N.lib()
+    nbytes = lib.kl_dibr_rasterize_workspace_bytes(B, height, width, F)
+    ws = _ws(nbytes, dev)
+    with torch.cuda.device(dev), N.timed('dibr_rasterize_forward', dev):
+        N.check(lib.kl_dibr_rasterize_forward(
+            N.dtype_code(dtype), height, width, B, F, D, N.ptr(fvz), N.ptr(fvi), N.ptr(feat), N.ptr(valid),
+            float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w), N.ptr(ws), nbytes, N.stream_of(dev)),
+            func)
+    return feats, idx, w
+
+
+def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_features, eps):
+    func = 'rasterize backward'
+    B, H, W, D = grad.shape
+    F = face_vertices_image.shape[1]
+    dev = face_vertices_image.device
+    g_img = torch.empty_like(face_vertices_image)
+    g_feat = torch.empty_like(face_features)
+    lib = N.lib()
+    nbytes = lib.kl_dibr_rasterize_workspace_bytes(B, H, W, F)
+    ws = _ws(nbytes, dev)
+    with torch.cuda.device(dev), N.timed('dibr_rasterize_backward', dev):
+        N.check(lib.kl_dibr_rasterize_backward(
+            N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, N.ptr(grad.contiguous()), N.ptr(face_idx),
+            N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), float(eps), N.ptr(g_img),
+            N.ptr(g_feat), N.ptr(ws), nbytes, N.stream_of(dev)), func)
+    return g_img, g_feat
+
+
+def soft_mask_forward(face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier):
+    """face_vertices_image UNSCALED -> soft_mask, close_face_prob, close_face_idx, close_face_dist_type."""
+    func = 'dibr_soft_mask'
+    N.require_gpu(func, face_vertices_image)
+    fvi = face_vertices_image.contiguous()
+    sel = selected_face_idx.contiguous()
+    B, F = fvi.shape[:2]
+    H, W = sel.shape[1:]
+    dev = fvi.device
+    dtype = fvi.dtype
+    if dtype not in (torch.float32, torch.float64):
+        raise RuntimeError(f'"{func}" not implemented for {dtype}')
+    K = int(knum)
+    mask = torch.empty((B, H, W), dtype=dtype, device=dev)
+    prob = torch.empty((B, H, W, K), dtype=dtype, device=dev)
+    cidx = torch.empty((B, H, W, K), dtype=torch.long, device=dev)
+    ctype = torch.empty((B, H, W, K), dtype=torch.uint8, device=dev)
+    lib = N.lib()
+    nbytes = lib.kl_soft_mask_workspace_bytes(B, H, W, F)
+    ws = _ws(nbytes, dev)
+    with torch.cuda.device(dev), N.timed('dibr_soft_mask_forward', dev):
+        N.check(lib.kl_dibr_soft_mask_forward_fused(
+            N.dtype_code(dtype), B, H, W, F, K, N.ptr(fvi), N.ptr(sel), float(sigmainv), float(boxlen * multiplier),
+            float(multiplier), N.ptr(mask), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(ws), nbytes,
+            N.stream_of(dev)), func)
+    return mask, prob, cidx, ctype
+
+
+def soft_mask_backward(grad, mask, sel, prob, cidx, ctype, face_vertices_image, sigmainv, multiplier):
+    func = 'dibr_soft_mask backward'
+    B, F = face_vertices_image.shape[:2]
+    H, W = sel.shape[1:]
+    K = cidx.shape[-1]
+    dev = face_vertices_image.device
+    g = torch.empty_like(face_vertices_image)
+    with torch.cuda.device(dev), N.timed('dibr_soft_mask_backward', dev):
+        N.check(N.lib().kl_dibr_soft_mask_backward_fused(
+            N.dtype_code(face_vertices_image.dtype), B, H, W, F, K, N.ptr(grad.contiguous()), N.ptr(mask),
+            N.ptr(sel), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(face_vertices_image), float(sigmainv),
+            float(multiplier), N.ptr(g), N.stream_of(dev)), func)
+    return g

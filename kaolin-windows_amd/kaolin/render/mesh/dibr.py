@@ -2,26 +2,22 @@
 import torch
 from torch.autograd import Function
 
-from ... import _C
+from ... import _fused
 from .rasterization import rasterize
 
 __all__ = ['dibr_soft_mask', 'dibr_rasterization']
 
 
 class DibrSoftMaskCuda(Function):
-    """dibr.py:27-73."""
+    """dibr.py:27-73 on the fused HIP path: ``* multiplier`` and the enlarged bboxes are
+    evaluated in-kernel; the UNSCALED face_vertices_image is saved for backward."""
 
     @staticmethod
     def forward(ctx, face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier):
         face_vertices_image = face_vertices_image.contiguous()
-        face_vertices_image = face_vertices_image * multiplier
         selected_face_idx = selected_face_idx.contiguous()
-        points_min = torch.min(face_vertices_image, dim=-2)[0]
-        points_max = torch.max(face_vertices_image, dim=-2)[0]
-        face_large_bboxes = torch.cat([points_min - boxlen * multiplier, points_max + boxlen * multiplier], dim=-1)
-        soft_mask, close_face_prob, close_face_idx, close_face_dist_type = \
-            _C.render.mesh.dibr_soft_mask_forward_cuda(face_vertices_image, face_large_bboxes.contiguous(),
-                                                       selected_face_idx, sigmainv, knum, multiplier)
+        soft_mask, close_face_prob, close_face_idx, close_face_dist_type = _fused.soft_mask_forward(
+            face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier)
         ctx.multiplier = multiplier
         ctx.sigmainv = sigmainv
         ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, close_face_prob, close_face_idx,
@@ -32,9 +28,9 @@ class DibrSoftMaskCuda(Function):
     def backward(ctx, grad_soft_mask):
         soft_mask, face_vertices_image, selected_face_idx, close_face_prob, close_face_idx, close_face_dist_type = \
             ctx.saved_tensors
-        grad_face_vertices_image = _C.render.mesh.dibr_soft_mask_backward_cuda(
-            grad_soft_mask.contiguous(), soft_mask, selected_face_idx, close_face_prob, close_face_idx,
-            close_face_dist_type, face_vertices_image, ctx.sigmainv, ctx.multiplier)
+        grad_face_vertices_image = _fused.soft_mask_backward(
+            grad_soft_mask, soft_mask, selected_face_idx, close_face_prob, close_face_idx, close_face_dist_type,
+            face_vertices_image, ctx.sigmainv, ctx.multiplier)
         return grad_face_vertices_image, None, None, None, None, None
 
 

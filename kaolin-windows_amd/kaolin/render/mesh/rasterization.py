@@ -9,6 +9,7 @@ import torch
 from torch.autograd import Function
 
 from ... import _C
+from ... import _fused
 
 __all__ = ['rasterize']
 
@@ -38,7 +39,38 @@ def _pack_valid_faces(face_vertices_z, face_vertices_image, face_features, valid
 
 
 class RasterizeCuda(Function):
-    """torch.autograd.Function for ``rasterize`` with backend 'cuda' (rasterization.py:243-388)."""
+    """torch.autograd.Function for ``rasterize`` with backend 'cuda' (rasterization.py:243-388).
+
+    Runs the fused HIP path: the valid-face packing, ``* multiplier``, bboxes and the
+    packed->original index remap of the reference front-end happen inside the kernels
+    (same float operations), and the backward is an atomic-free per-face gather.
+    ``_C.render.mesh.packed_rasterize_forward_cuda`` / ``rasterize_backward_cuda`` keep
+    the reference's packed contract for direct callers.
+    """
+
+    @staticmethod
+    def forward(ctx, height, width, face_vertices_z, face_vertices_image, face_features, valid_faces, multiplier,
+                eps):
+        face_features = face_features.contiguous()
+        face_vertices_image = face_vertices_image.contiguous()
+        interpolated_features, face_idx, output_weights = _fused.rasterize_forward(
+            height, width, face_vertices_z, face_vertices_image, face_features, valid_faces, multiplier, eps)
+        ctx.save_for_backward(interpolated_features, face_idx, output_weights, face_vertices_image, face_features)
+        ctx.mark_non_differentiable(face_idx)
+        ctx.eps = eps
+        return interpolated_features, face_idx
+
+    @staticmethod
+    def backward(ctx, grad_interpolated_features, grad_face_idx):
+        interpolated_features, face_idx, output_weights, face_vertices_image, face_features = ctx.saved_tensors
+        grad_face_vertices_image, grad_face_features = _fused.rasterize_backward(
+            grad_interpolated_features, face_idx, output_weights, face_vertices_image, face_features, ctx.eps)
+        return None, None, None, grad_face_vertices_image, grad_face_features, None, None, None
+
+
+class RasterizeCudaPacked(Function):
+    """The reference's exact chain (rasterization.py:290-388): torch packing + the
+    packed ``_C`` entry points.  Kept for parity checks of the _C contract."""
 
     @staticmethod
     def forward(ctx, height, width, face_vertices_z, face_vertices_image, face_features, valid_faces, multiplier,
@@ -48,7 +80,6 @@ class RasterizeCuda(Function):
         num_faces = face_vertices_z.shape[1]
         valid_faces_idx, vfvi, vfvz, vfeat, first_idx = _pack_valid_faces(
             face_vertices_z, face_vertices_image, face_features, valid_faces)
-        # To avoid numeric error, coordinates are enlarged by the multiplier
         vfvi = vfvi * multiplier
         points_min = torch.min(vfvi, dim=1)[0]
         points_max = torch.max(vfvi, dim=1)[0]
@@ -87,12 +118,13 @@ def rasterize(height, width, face_vertices_z, face_vertices_image, face_features
         multiplier = 1000
     if eps is None:
         eps = 1e-8
-    if backend not in ('cuda', 'hip'):
+    if backend not in ('cuda', 'hip', 'cuda_packed'):
         raise ValueError(f'"{backend}" is not a valid backend for kaolin-mi355x, valid choices are ["cuda", "hip"] '
                          '(the nvdiffrast backends are not available on ROCm)')
     _face_features = torch.cat(face_features, dim=-1) if isinstance(face_features, (list, tuple)) else face_features
-    image_features, face_idx = RasterizeCuda.apply(height, width, face_vertices_z, face_vertices_image,
-                                                   _face_features, valid_faces, multiplier, eps)
+    fn = RasterizeCudaPacked if backend == 'cuda_packed' else RasterizeCuda
+    image_features, face_idx = fn.apply(height, width, face_vertices_z, face_vertices_image, _face_features,
+                                        valid_faces, multiplier, eps)
     if isinstance(face_features, (list, tuple)):
         out = []
         cur = 0

@@ -119,6 +119,35 @@ def test_packed_rasterize_vs_oracle(kal, dtype, H, W):
     assert (oi >= 0).mean() > 0.2
 
 
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('use_valid', [False, True])
+def test_fused_path_matches_packed_C_chain(kal, dtype, use_valid):
+    """The fused front-end path (in-kernel packing / bbox / remap, gather backward) equals
+    the reference's torch-glue + packed _C chain: forward bit-exact, grads 1e-5."""
+    fvz, fvi, feat, fnz = _render_inputs(kal, 30, 50, 3, dtype)
+    valid = (fnz >= 0) if use_valid else None
+    outs = []
+    for backend in ('cuda', 'cuda_packed'):
+        a = fvi.clone().requires_grad_(True)
+        b = feat.clone().requires_grad_(True)
+        f, i = kal.render.mesh.rasterize(70, 90, fvz, a, b, valid_faces=valid, backend=backend)
+        g = torch.Generator(device='cpu').manual_seed(3)
+        f.backward(torch.rand(f.shape, generator=g, dtype=dtype).to(DEV))
+        outs.append((f, i, a.grad, b.grad))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    np.testing.assert_allclose(A(outs[0][2]), A(outs[1][2]), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(A(outs[0][3]), A(outs[1][3]), rtol=1e-5, atol=1e-5)
+    # soft mask: fused (unscaled input, in-kernel bbox) vs the _C contract
+    m, box = 1000., 0.02
+    fm = (fvi * m).contiguous()
+    bb = torch.cat([fm.min(-2)[0] - box * m, fm.max(-2)[0] + box * m], -1).contiguous()
+    r1 = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, outs[0][1], 7000., 30, m)
+    from kaolin import _fused
+    r2 = _fused.soft_mask_forward(fvi, outs[0][1], 7000., box, 30, m)
+    for x, y in zip(r1, r2):
+        assert torch.equal(x, y)
+
+
 def test_rasterize_backward_vs_oracle(kal):
     fvz, fvi, feat, fnz = _render_inputs(kal, 30, 50, 2)
     fvi_r = fvi.clone().requires_grad_(True)
