@@ -118,19 +118,23 @@ int kl_dibr_soft_mask_forward(kl_dtype dtype, int batch, int height, int width, 
 /* Fused front-end path of DibrSoftMaskCuda (dibr.py:27-73): face_vertices_image UNSCALED;
  * `face_vertices_image * multiplier` and the enlarged bboxes (min/max -/+ bbox_pad) are
  * evaluated in-kernel with the front-end's float ops.  bbox_pad = boxlen * multiplier as
- * the caller's double-precision product (the front-end's python-float expression). */
+ * the caller's double-precision product (the front-end's python-float expression).
+ * hits (B,H,W) uint8, optional (NULL = not written; requires knum <= 255): the number of
+ * filled slots per pixel, which lets the fused backward skip the slot scan. */
 int kl_dibr_soft_mask_forward_fused(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
                                     const void *face_vertices_image, const int64_t *selected_face_idx,
                                     float sigmainv, double bbox_pad, float multiplier, void *soft_mask,
                                     void *close_face_prob, int64_t *close_face_idx,
-                                    uint8_t *close_face_dist_type, void *workspace, size_t workspace_bytes,
-                                    kl_stream stream);
+                                    uint8_t *close_face_dist_type, uint8_t *hits, void *workspace,
+                                    size_t workspace_bytes, kl_stream stream);
+/* hits: the forward's per-pixel slot counts, or NULL to scan the slots up to the first -1
+ * as the reference does. */
 int kl_dibr_soft_mask_backward_fused(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
                                      const void *grad_soft_mask, const void *soft_mask,
                                      const int64_t *selected_face_idx, const void *close_face_prob,
                                      const int64_t *close_face_idx, const uint8_t *close_face_dist_type,
-                                     const void *face_vertices_image, float sigmainv, float multiplier,
-                                     void *grad_face_vertices_image, kl_stream stream);
+                                     const uint8_t *hits, const void *face_vertices_image, float sigmainv,
+                                     float multiplier, void *grad_face_vertices_image, kl_stream stream);
 
 /* dibr_soft_mask.cpp:110-183  dibr_soft_mask_backward_cuda.
  * Output grad_face_vertices_image (B,F,3,2) (fully written). */

@@ -160,10 +160,11 @@ __device__ __forceinline__ void axis_range(double vmin, double vmax, double s, i
 
 // One wave per (mesh b, chunk c).  Mesh b owns faces [first(b), last(b)) of the source.
 // first_idx == nullptr => uniform meshes of `faces_per_mesh` faces.
+// bbox_out (optional): the face bboxes of the source, (N,4), for consumers that walk them.
 template <typename T, typename Src>
 __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *__restrict__ first_idx,
                                                         int faces_per_mesh, BinGeom g, float m,
-                                                        uint32_t *__restrict__ bitmap) {
+                                                        uint32_t *__restrict__ bitmap, T *__restrict__ bbox_out) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.y;
@@ -184,6 +185,12 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *
   if (f < f1 && src.valid(f)) {
     T bx0, by0, bx1, by1;
     src.get(f, bx0, by0, bx1, by1);
+    if (bbox_out) {
+      bbox_out[f * 4 + 0] = bx0;
+      bbox_out[f * 4 + 1] = by0;
+      bbox_out[f * 4 + 2] = bx1;
+      bbox_out[f * 4 + 3] = by1;
+    }
     int ix0, ix1, iy0, iy1;
     const double sx = (double)(m / (float)g.width), sy = (double)(m / (float)g.height);
     axis_range((double)bx0, (double)bx1, sx, g.width, false, ix0, ix1);
@@ -218,11 +225,11 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *
 
 template <typename T, typename Src>
 inline int launch_binning(Src src, const int64_t *first_idx, int faces_per_mesh, const BinGeom &g, float m,
-                          uint32_t *bitmap, hipStream_t st) {
+                          uint32_t *bitmap, hipStream_t st, T *bbox_out = nullptr) {
   KL_CHECK_HIP(hipMemsetAsync(bitmap, 0, g.bytes(), st));
   dim3 grid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)g.batch);
   hipLaunchKernelGGL((bin_faces_kernel<T, Src>), grid, dim3(256), 0, st, src, first_idx, faces_per_mesh, g, m,
-                     bitmap);
+                     bitmap, bbox_out);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

@@ -1,17 +1,17 @@
 // raster.hip -- packed_rasterize_forward / rasterize_backward for gfx950.
 //
 // Forward (reference: rasterization_cuda.cu:43-236, a per-pixel walk over ALL faces
-// of the mesh with the batch looped serially in every thread): here faces are first
-// binned to 64x8 pixel tiles (binning.h), then one wave per 64-pixel row segment walks
-// only the candidate 64-face chunks of its tile, in ascending face order.  Per chunk
-// the wave loads the 64 faces once (one per lane, coalesced), ballots which of them can
-// touch its row, and broadcasts each surviving face through the scalar unit
-// (v_readlane) to all 64 pixel lanes.  The per-pixel arithmetic is the reference's,
-// statement for statement (bbox reject, edge functions, copysign(eps) normalisation,
-// strict depth test), so face index / weights / features are bit-identical to the
-// oracle for the same inputs.
+// of the mesh with the batch looped serially in every thread).  Here the work is
+// proportional to what faces actually cover: one thread per face visits the exact
+// pixel-centre range of its bbox, runs the reference's per-(pixel, face) arithmetic
+// (bbox reject, edge functions, copysign(eps) normalisation, sign test) and ranks
+// the hit with a 64-bit atomicMax of (depth, ~face) in a visibility buffer; a
+// per-pixel resolve pass then recomputes the winner's weights and interpolates.
+// "Max depth, lowest index on ties" is exactly the reference's strict `z0 <= max_z0`
+// fold in index order, so face index / weights / features are bit-identical to the
+// oracle (NaN depths, which break that order, are replayed sequentially).
 //
-// Two entry points share that walk:
+// Two entry points share it:
 //   kl_packed_rasterize_forward  -- the reference's _C contract (packed valid faces,
 //                                   coordinates pre-multiplied, explicit bboxes);
 //   kl_dibr_rasterize_forward    -- fused front-end path: unpacked (B,F) faces + valid
@@ -31,105 +31,306 @@
 
 namespace kl {
 
+// ---------------------------------------------------------------- forward
+// A face, as the reference's per-pixel loop sees it (rasterization_cuda.cu:95-133):
+// bbox and vertices in multiplied coordinates, vertex depths.
+template <typename T>
+struct RastFace {
+  T xmin, ymin, xmax, ymax;
+  T v[6];
+  T az, bz, cz;
+};
+
 template <typename T, typename Src>
-__global__ void __launch_bounds__(256) rasterize_fwd_kernel(
-    Src src, const T *__restrict__ fvz, const T *__restrict__ feat, const int64_t *__restrict__ first_idx,
-    int faces_per_mesh, const uint32_t *__restrict__ bitmap, BinGeom g, int D, float multiplier, float eps,
-    T *__restrict__ out_feat, int64_t *__restrict__ out_idx, T *__restrict__ out_w) {
-  const int lane = threadIdx.x & 63;
-  const int j = blockIdx.y * 4 + (threadIdx.x >> 6);
-  const int b = blockIdx.z;
-  const int tx = blockIdx.x;
-  const int H = g.height, W = g.width;
-  if (j >= H) return;
-  const int i = tx * TILE_W + lane;
-  const bool px_valid = i < W;
-  int64_t f0, f1;
-  if (first_idx) {
-    f0 = first_idx[b];
-    f1 = first_idx[b + 1];
-  } else {
-    f0 = (int64_t)b * faces_per_mesh;
-    f1 = f0 + faces_per_mesh;
+__device__ __forceinline__ void load_face(const Src &src, const T *__restrict__ fvz, int64_t f, RastFace<T> &r) {
+  src.get(f, r.xmin, r.ymin, r.xmax, r.ymax);
+  src.verts(f, r.v);
+  r.az = fvz[f * 3 + 0];
+  r.bz = fvz[f * 3 + 1];
+  r.cz = fvz[f * 3 + 2];
+}
+
+// The reference's per-(pixel, face) test, statement for statement: bbox reject, edge
+// functions, copysign(eps) normalisation, barycentric sign test.  true => (w0,w1,w2)
+// are the face's weights at the pixel centre (x0, y0).
+template <typename T>
+__device__ __forceinline__ bool face_weights(const RastFace<T> &r, T x0, T y0, float eps, T &w0, T &w1, T &w2) {
+  if (x0 < r.xmin || x0 >= r.xmax || y0 < r.ymin || y0 >= r.ymax) return false;
+  const T aex = r.v[0] - x0, aey = r.v[1] - y0;
+  const T bex = r.v[2] - x0, bey = r.v[3] - y0;
+  const T cex = r.v[4] - x0, cey = r.v[5] - y0;
+  w0 = bex * cey - bey * cex;
+  w1 = cex * aey - cey * aex;
+  w2 = aex * bey - aey * bex;
+  T norm = w0 + w1 + w2;
+  norm = (T)((double)norm + copysign((double)eps, (double)norm));
+  w0 /= norm;
+  w1 /= norm;
+  w2 /= norm;
+  return !(w0 < (T)0 || w1 < (T)0 || w2 < (T)0);
+}
+
+template <typename T>
+__device__ __forceinline__ T face_depth(const RastFace<T> &r, T w0, T w1, T w2) {
+  return w0 * r.az + w1 * r.bz + w2 * r.cz;
+}
+
+// Exact pixel interval of one axis whose float centres c satisfy  lo <= c < hi  (the
+// reference's bbox test).  Centres are monotone in the index, so the conservative
+// interval of axis_range is trimmed by evaluating the exact centre formula at its ends.
+// NaN bounds never reject: the whole axis.
+template <typename T>
+__device__ __forceinline__ void exact_axis(T lo, T hi, float m, int n, bool flip, int &a, int &b) {
+  axis_range((double)lo, (double)hi, (double)(m / (float)n), n, flip, a, b);
+  if (!(lo == lo) || !(hi == hi)) return;
+  auto c = [&](int k) { return flip ? pix_y<T>(m, n, k) : pix_x<T>(m, n, k); };
+  auto in = [&](int k) { return !(c(k) < lo || c(k) >= hi); };
+  while (a <= b && !in(a)) a++;
+  while (b >= a && !in(b)) b--;
+}
+
+// Depth-ordered visibility through one 64-bit atomicMax per covered (face, pixel):
+//   float : key = order(z0) << 32 | ~local_face   -> max depth, lowest index on ties,
+//           which is exactly the reference's `if (z0 <= max_z0) continue` fold over
+//           faces in index order;
+//   double: pass 0 maxes order(z0) (64 bit), pass 1 mins the index among the faces
+//           that reach it.
+// order() maps floats to unsigned keys monotonically with -0 == +0.  z0 = -inf never
+// wins in the reference (-inf <= -inf), so it is dropped.  A NaN z0 breaks the total
+// order (the reference then keeps the LAST passing face); such pixels are flagged and
+// re-walked sequentially by the resolve kernel.
+__device__ __forceinline__ uint32_t order32(float z) {
+  uint32_t u = __float_as_uint(z == 0.0f ? 0.0f : z);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ uint64_t order64(double z) {
+  uint64_t u = (uint64_t)__double_as_longlong(z == 0.0 ? 0.0 : z);
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+
+struct VisBuf {
+  unsigned long long *key;  // (P) 0 = empty
+  uint32_t *idx;            // (P) double only
+  uint8_t *flag;            // (P) NaN depth seen
+};
+
+template <int PASS>
+__device__ __forceinline__ void vis_update(const VisBuf &vb, int64_t p, float z0, uint32_t local) {
+  if (z0 != z0) {
+    vb.flag[p] = 1;
+    return;
   }
+  if (z0 == -INFINITY) return;
+  atomicMax(vb.key + p, ((unsigned long long)order32(z0) << 32) | (unsigned long long)(~local));
+}
+template <int PASS>
+__device__ __forceinline__ void vis_update(const VisBuf &vb, int64_t p, double z0, uint32_t local) {
+  if (z0 != z0) {
+    if (PASS == 0) vb.flag[p] = 1;
+    return;
+  }
+  if (z0 == -INFINITY) return;
+  if (PASS == 0)
+    atomicMax(vb.key + p, (unsigned long long)order64(z0));
+  else if (vb.key[p] == order64(z0))
+    atomicMin(vb.idx + p, local);
+}
 
-  const T x0 = pix_x<T>(multiplier, W, px_valid ? i : W - 1);
-  const T y0 = pix_y<T>(multiplier, H, j);
-  // pixel-centre extent of this row segment (for the per-chunk ballot)
-  const int ilast = min(tx * TILE_W + 63, W - 1);
-  const T xlo = pix_x<T>(multiplier, W, tx * TILE_W);
-  const T xhi = pix_x<T>(multiplier, W, ilast);
-  const T sxlo = xlo < xhi ? xlo : xhi, sxhi = xlo < xhi ? xhi : xlo;
+// mesh of packed face f (first_idx) or of dense face f (uniform meshes)
+__device__ __forceinline__ void face_mesh(int64_t f, const int64_t *__restrict__ first_idx, int B,
+                                          int faces_per_mesh, int &b, int64_t &f0) {
+  if (first_idx) {
+    int lo = 0, hi = B - 1;  // last b with first_idx[b] <= f
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (first_idx[mid] <= f)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    b = lo;
+    f0 = first_idx[lo];
+  } else {
+    b = (int)(f / faces_per_mesh);
+    f0 = (int64_t)b * faces_per_mesh;
+  }
+}
 
-  T max_z0 = -INFINITY, mw0 = 0, mw1 = 0, mw2 = 0;
-  int64_t max_f = -1;
+constexpr int VIS_SMALL_AREA = 64;  // faces covering more pixel centres go to the WG kernel
 
-  const uint32_t *words = bitmap + ((size_t)(b * g.tiles_y + j / TILE_H) * g.tiles_x + tx) * g.words;
-  for (int wi = 0; wi < g.words; wi++) {
-    uint32_t word = words[wi];
-    while (word) {
-      const int c = wi * 32 + __builtin_ctz(word);
-      word &= word - 1;
-      const int64_t base = f0 + (int64_t)c * 64;
-      const int64_t f = base + lane;
-      const bool fv = f < f1 && src.valid(f);
-      T bx0 = 0, by0 = 0, bx1 = 0, by1 = 0;
-      if (fv) src.get(f, bx0, by0, bx1, by1);
-      // may this face cover some pixel centre of the row segment?  (NaN-safe: NaN never rejects)
-      const bool touch = fv && !(y0 < by0 || y0 >= by1 || sxhi < bx0 || sxlo >= bx1);
-      uint64_t mask = ballot(touch);
-      if (!mask) continue;
-      T v[6] = {0, 0, 0, 0, 0, 0};
-      T az = 0, bz = 0, cz = 0;
-      if (touch) {
-        src.verts(f, v);
-        const T *z = fvz + f * 3;
-        az = z[0];
-        bz = z[1];
-        cz = z[2];
-      }
-      while (mask) {
-        const int s = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const T xmin = bcast(bx0, s), ymin = bcast(by0, s), xmax = bcast(bx1, s), ymax = bcast(by1, s);
-        const T Ax = bcast(v[0], s), Ay = bcast(v[1], s), Bx = bcast(v[2], s), By = bcast(v[3], s);
-        const T Cx = bcast(v[4], s), Cy = bcast(v[5], s);
-        const T Az = bcast(az, s), Bz = bcast(bz, s), Cz = bcast(cz, s);
-        if (x0 < xmin || x0 >= xmax || y0 < ymin || y0 >= ymax) continue;
-        const T aex = Ax - x0, aey = Ay - y0;
-        const T bex = Bx - x0, bey = By - y0;
-        const T cex = Cx - x0, cey = Cy - y0;
-        T w0 = bex * cey - bey * cex;
-        T w1 = cex * aey - cey * aex;
-        T w2 = aex * bey - aey * bex;
-        T norm = w0 + w1 + w2;
-        norm = (T)((double)norm + copysign((double)eps, (double)norm));
-        w0 /= norm;
-        w1 /= norm;
-        w2 /= norm;
-        if (w0 < (T)0 || w1 < (T)0 || w2 < (T)0) continue;
-        const T z0 = w0 * Az + w1 * Bz + w2 * Cz;
-        if (z0 <= max_z0) continue;
-        max_z0 = z0;
-        max_f = base + s;
-        mw0 = w0;
-        mw1 = w1;
-        mw2 = w2;
-      }
+// one thread per face; faces whose exact pixel range exceeds VIS_SMALL_AREA are queued
+template <typename T, typename Src, int PASS>
+__global__ void __launch_bounds__(256) raster_vis_kernel(Src src, const T *__restrict__ fvz,
+                                                         const int64_t *__restrict__ first_idx, int B,
+                                                         int faces_per_mesh, int64_t nfaces, int H, int W, float m,
+                                                         float eps, VisBuf vb, int *__restrict__ big,
+                                                         int *__restrict__ nbig) {
+  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (f >= nfaces || !src.valid(f)) return;
+  RastFace<T> r;
+  load_face(src, fvz, f, r);
+  int ix0, ix1, iy0, iy1;
+  exact_axis(r.xmin, r.xmax, m, W, false, ix0, ix1);
+  if (ix0 > ix1) return;
+  exact_axis(r.ymin, r.ymax, m, H, true, iy0, iy1);
+  if (iy0 > iy1) return;
+  if ((int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) > VIS_SMALL_AREA) {
+    if (PASS == 0) big[atomicAdd(nbig, 1)] = (int)f;
+    return;
+  }
+  int b;
+  int64_t f0;
+  face_mesh(f, first_idx, B, faces_per_mesh, b, f0);
+  const uint32_t local = (uint32_t)(f - f0);
+  for (int j = iy0; j <= iy1; j++) {
+    const T y0 = pix_y<T>(m, H, j);
+    const int64_t row = ((int64_t)b * H + j) * W;
+    for (int i = ix0; i <= ix1; i++) {
+      T w0, w1, w2;
+      if (face_weights(r, pix_x<T>(m, W, i), y0, eps, w0, w1, w2))
+        vis_update<PASS>(vb, row + i, face_depth(r, w0, w1, w2), local);
     }
   }
-  if (!px_valid) return;
-  const size_t pix = ((size_t)b * H + j) * W + i;
-  out_idx[pix] = max_f >= 0 ? max_f - f0 : -1;
-  out_w[pix * 3 + 0] = mw0;
-  out_w[pix * 3 + 1] = mw1;
-  out_w[pix * 3 + 2] = mw2;
-  if (max_f >= 0) {
-    const T *r = feat + (size_t)max_f * 3 * D;
-    for (int d = 0; d < D; d++) out_feat[pix * D + d] = mw0 * r[d] + mw1 * r[D + d] + mw2 * r[2 * D + d];
-  } else {
-    for (int d = 0; d < D; d++) out_feat[pix * D + d] = (T)0;
+}
+
+// one workgroup per queued large face
+template <typename T, typename Src, int PASS>
+__global__ void __launch_bounds__(256) raster_vis_big_kernel(Src src, const T *__restrict__ fvz,
+                                                             const int64_t *__restrict__ first_idx, int B,
+                                                             int faces_per_mesh, int H, int W, float m, float eps,
+                                                             VisBuf vb, const int *__restrict__ big,
+                                                             const int *__restrict__ nbig) {
+  const int n = *nbig;
+  for (int k = blockIdx.x; k < n; k += gridDim.x) {
+    const int64_t f = big[k];
+    RastFace<T> r;
+    load_face(src, fvz, f, r);
+    int ix0, ix1, iy0, iy1;
+    exact_axis(r.xmin, r.xmax, m, W, false, ix0, ix1);
+    exact_axis(r.ymin, r.ymax, m, H, true, iy0, iy1);
+    int b;
+    int64_t f0;
+    face_mesh(f, first_idx, B, faces_per_mesh, b, f0);
+    const uint32_t local = (uint32_t)(f - f0);
+    const int w = ix1 - ix0 + 1;
+    const int64_t area = (int64_t)w * (iy1 - iy0 + 1);
+    for (int64_t e = threadIdx.x; e < area; e += blockDim.x) {
+      const int j = iy0 + (int)(e / w), i = ix0 + (int)(e % w);
+      T w0, w1, w2;
+      if (face_weights(r, pix_x<T>(m, W, i), pix_y<T>(m, H, j), eps, w0, w1, w2))
+        vis_update<PASS>(vb, ((int64_t)b * H + j) * W + i, face_depth(r, w0, w1, w2), local);
+    }
   }
+}
+
+// One thread per pixel: decode the winner, recompute its weights with the same
+// arithmetic (bit-identical to the pass that ranked it) and write the outputs.
+// Flagged pixels (NaN depth) replay the reference's sequential fold over all faces.
+template <typename T, typename Src>
+__global__ void __launch_bounds__(256) raster_resolve_kernel(Src src, const T *__restrict__ fvz,
+                                                             const T *__restrict__ feat,
+                                                             const int64_t *__restrict__ first_idx,
+                                                             int faces_per_mesh, int B, int H, int W, int D,
+                                                             float m, float eps, VisBuf vb, T *__restrict__ out_feat,
+                                                             int64_t *__restrict__ out_idx, T *__restrict__ out_w) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= (int64_t)B * H * W) return;
+  const int b = (int)(p / ((int64_t)H * W));
+  const int rem = (int)(p - (int64_t)b * H * W);
+  const int j = rem / W, i = rem - j * W;
+  const T x0 = pix_x<T>(m, W, i), y0 = pix_y<T>(m, H, j);
+  const int64_t f0 = first_idx ? first_idx[b] : (int64_t)b * faces_per_mesh;
+  int64_t win = -1;
+  T mw0 = 0, mw1 = 0, mw2 = 0;
+  if (vb.flag[p]) {
+    const int64_t f1 = first_idx ? first_idx[b + 1] : f0 + faces_per_mesh;
+    T max_z0 = -INFINITY;
+    for (int64_t f = f0; f < f1; f++) {
+      if (!src.valid(f)) continue;
+      RastFace<T> r;
+      load_face(src, fvz, f, r);
+      T w0, w1, w2;
+      if (!face_weights(r, x0, y0, eps, w0, w1, w2)) continue;
+      const T z0 = face_depth(r, w0, w1, w2);
+      if (z0 <= max_z0) continue;
+      max_z0 = z0;
+      win = f;
+      mw0 = w0;
+      mw1 = w1;
+      mw2 = w2;
+    }
+  } else {
+    const unsigned long long key = vb.key[p];
+    if (key != 0) {
+      win = f0 + (int64_t)(sizeof(T) == 4 ? (uint32_t)~(uint32_t)key : vb.idx[p]);
+      RastFace<T> r;
+      load_face(src, fvz, win, r);
+      face_weights(r, x0, y0, eps, mw0, mw1, mw2);
+    }
+  }
+  out_idx[p] = win >= 0 ? win - f0 : -1;
+  out_w[p * 3 + 0] = mw0;
+  out_w[p * 3 + 1] = mw1;
+  out_w[p * 3 + 2] = mw2;
+  if (win >= 0) {
+    const T *c = feat + (size_t)win * 3 * D;
+    for (int d = 0; d < D; d++) out_feat[p * D + d] = mw0 * c[d] + mw1 * c[D + d] + mw2 * c[2 * D + d];
+  } else {
+    for (int d = 0; d < D; d++) out_feat[p * D + d] = (T)0;
+  }
+}
+
+struct RastWs {
+  size_t P, nf;
+  size_t off_key, off_idx, off_flag, off_big, bytes;
+  RastWs(int B, int H, int W, int64_t nfaces) {
+    P = (size_t)B * H * W;
+    nf = (size_t)(nfaces > 0 ? nfaces : 0);
+    off_key = 0;
+    off_idx = off_key + P * 8;
+    off_flag = off_idx + P * 4;
+    off_big = off_flag + ((P + 15) & ~(size_t)15);
+    bytes = off_big + (nf + 1) * 4;
+  }
+};
+
+template <typename T, typename Src>
+static int launch_rast_fwd(Src src, int H, int W, int B, int D, int64_t nfaces, int64_t ws_faces, const T *fvz,
+                           const T *feat, const int64_t *first_idx, int faces_per_mesh, float m, float eps,
+                           T *out_feat, int64_t *out_idx, T *out_w, void *ws, size_t ws_bytes, hipStream_t st) {
+  const RastWs L(B, H, W, ws_faces);
+  KL_REQUIRE(nfaces <= ws_faces && ws_bytes >= L.bytes, "rasterize forward: workspace too small");
+  KL_REQUIRE(nfaces < ((int64_t)1 << 31), "rasterize forward: too many faces");
+  if (L.P == 0) return KL_OK;
+  char *w = reinterpret_cast<char *>(ws);
+  VisBuf vb{reinterpret_cast<unsigned long long *>(w + L.off_key), reinterpret_cast<uint32_t *>(w + L.off_idx),
+            reinterpret_cast<uint8_t *>(w + L.off_flag)};
+  int *nbig = reinterpret_cast<int *>(w + L.off_big);
+  int *big = nbig + 1;
+  // key | idx | flag | nbig are contiguous: key and flag/nbig zeroed, idx set to ~0
+  KL_CHECK_HIP(hipMemsetAsync(w, 0, L.off_big + 4, st));
+  if (sizeof(T) == 8) KL_CHECK_HIP(hipMemsetAsync(w + L.off_idx, 0xff, L.P * 4, st));
+  if (nfaces > 0) {
+    const unsigned fb = (unsigned)cdiv(nfaces, 256);
+    hipLaunchKernelGGL((raster_vis_kernel<T, Src, 0>), dim3(fb), dim3(256), 0, st, src, fvz, first_idx, B,
+                       faces_per_mesh, nfaces, H, W, m, eps, vb, big, nbig);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL((raster_vis_big_kernel<T, Src, 0>), dim3(512), dim3(256), 0, st, src, fvz, first_idx, B,
+                       faces_per_mesh, H, W, m, eps, vb, big, nbig);
+    KL_CHECK_LAUNCH();
+    if (sizeof(T) == 8) {
+      hipLaunchKernelGGL((raster_vis_kernel<T, Src, 1>), dim3(fb), dim3(256), 0, st, src, fvz, first_idx, B,
+                         faces_per_mesh, nfaces, H, W, m, eps, vb, big, nbig);
+      KL_CHECK_LAUNCH();
+      hipLaunchKernelGGL((raster_vis_big_kernel<T, Src, 1>), dim3(512), dim3(256), 0, st, src, fvz, first_idx, B,
+                         faces_per_mesh, H, W, m, eps, vb, big, nbig);
+      KL_CHECK_LAUNCH();
+    }
+  }
+  hipLaunchKernelGGL((raster_resolve_kernel<T, Src>), dim3((unsigned)cdiv((int64_t)L.P, 256)), dim3(256), 0, st, src,
+                     fvz, feat, first_idx, faces_per_mesh, B, H, W, D, m, eps, vb, out_feat, out_idx, out_w);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
 }
 
 // d(interpolated feature)/d(face vertices) of one pixel (rasterization_cuda.cu:287-399).
@@ -360,23 +561,6 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
   }
 }
 
-template <typename T, typename Src>
-static int launch_rast_fwd(Src src, int H, int W, int B, int D, int64_t maxf, const T *fvz, const T *feat,
-                           const int64_t *first_idx, int faces_per_mesh, float m, float eps, T *out_feat,
-                           int64_t *out_idx, T *out_w, void *ws, size_t ws_bytes, hipStream_t st) {
-  BinGeom g = make_bin_geom(B, H, W, maxf);
-  KL_REQUIRE(ws_bytes >= g.bytes(), "rasterize forward: workspace too small");
-  if (B == 0 || H == 0 || W == 0) return KL_OK;
-  uint32_t *bitmap = reinterpret_cast<uint32_t *>(ws);
-  int rc = launch_binning<T, Src>(src, first_idx, faces_per_mesh, g, m, bitmap, st);
-  if (rc) return rc;
-  dim3 grid(g.tiles_x, (unsigned)cdiv(H, 4), B);
-  hipLaunchKernelGGL((rasterize_fwd_kernel<T, Src>), grid, dim3(256), 0, st, src, fvz, feat, first_idx,
-                     faces_per_mesh, bitmap, g, D, m, eps, out_feat, out_idx, out_w);
-  KL_CHECK_LAUNCH();
-  return KL_OK;
-}
-
 template <typename T>
 static int rasterize_bwd(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
                          const void *w, const void *fvi, const void *feat, float eps, void *gfvi, void *gfeat,
@@ -435,7 +619,7 @@ static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *g
 using namespace kl;
 
 extern "C" size_t kl_rasterize_workspace_bytes(int batch, int height, int width, int64_t max_faces_per_mesh) {
-  return make_bin_geom(batch, height, width, max_faces_per_mesh).bytes();
+  return RastWs(batch, height, width, (int64_t)batch * max_faces_per_mesh).bytes;
 }
 
 extern "C" int kl_packed_rasterize_forward(kl_dtype dtype, int height, int width, int batch, int64_t num_faces,
@@ -444,15 +628,15 @@ extern "C" int kl_packed_rasterize_forward(kl_dtype dtype, int height, int width
                                            const int64_t *first_idx, float multiplier, float eps, void *out_feat,
                                            int64_t *out_idx, void *out_w, void *ws, size_t ws_bytes,
                                            kl_stream stream) {
-  (void)num_faces;
+  const int64_t ws_faces = (int64_t)batch * max_faces_per_mesh;
   if (dtype == KL_F32)
     return launch_rast_fwd<float>(BboxSrc<float>{(const float *)bbox, (const float *)fvi}, height, width, batch,
-                                  feat_dim, max_faces_per_mesh, (const float *)fvz, (const float *)feat, first_idx, 0,
+                                  feat_dim, num_faces, ws_faces, (const float *)fvz, (const float *)feat, first_idx, 0,
                                   multiplier, eps, (float *)out_feat, out_idx, (float *)out_w, ws, ws_bytes,
                                   S(stream));
   if (dtype == KL_F64)
     return launch_rast_fwd<double>(BboxSrc<double>{(const double *)bbox, (const double *)fvi}, height, width, batch,
-                                   feat_dim, max_faces_per_mesh, (const double *)fvz, (const double *)feat, first_idx,
+                                   feat_dim, num_faces, ws_faces, (const double *)fvz, (const double *)feat, first_idx,
                                    0, multiplier, eps, (double *)out_feat, out_idx, (double *)out_w, ws, ws_bytes,
                                    S(stream));
   set_error("packed_rasterize_forward_cuda not implemented for this dtype");
@@ -460,7 +644,7 @@ extern "C" int kl_packed_rasterize_forward(kl_dtype dtype, int height, int width
 }
 
 extern "C" size_t kl_dibr_rasterize_workspace_bytes(int batch, int height, int width, int num_faces) {
-  const size_t fwd = make_bin_geom(batch, height, width, num_faces).bytes();
+  const size_t fwd = RastWs(batch, height, width, (int64_t)batch * num_faces).bytes;
   const size_t bwd = ((size_t)batch * num_faces + 1) * sizeof(int);
   return fwd > bwd ? fwd : bwd;
 }
@@ -470,16 +654,17 @@ extern "C" int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, 
                                          const uint8_t *valid_faces, float multiplier, float eps, void *out_feat,
                                          int64_t *out_idx, void *out_w, void *ws, size_t ws_bytes,
                                          kl_stream stream) {
+  const int64_t nf = (int64_t)batch * num_faces;
   if (dtype == KL_F32)
     return launch_rast_fwd<float>(RastSrc<float>{(const float *)fvi, valid_faces, (float)multiplier}, height, width,
-                                  batch, feat_dim, num_faces, (const float *)fvz, (const float *)feat, nullptr,
+                                  batch, feat_dim, nf, nf, (const float *)fvz, (const float *)feat, nullptr,
                                   num_faces, multiplier, eps, (float *)out_feat, out_idx, (float *)out_w, ws, ws_bytes,
                                   S(stream));
   if (dtype == KL_F64)
     return launch_rast_fwd<double>(RastSrc<double>{(const double *)fvi, valid_faces, (double)multiplier}, height,
-                                   width, batch, feat_dim, num_faces, (const double *)fvz, (const double *)feat,
-                                   nullptr, num_faces, multiplier, eps, (double *)out_feat, out_idx, (double *)out_w,
-                                   ws, ws_bytes, S(stream));
+                                   width, batch, feat_dim, nf, nf, (const double *)fvz, (const double *)feat, nullptr,
+                                   num_faces, multiplier, eps, (double *)out_feat, out_idx, (double *)out_w, ws,
+                                   ws_bytes, S(stream));
   set_error("dibr_rasterize_forward not implemented for this dtype");
   return KL_E_INVALID;
 }

@@ -58,79 +58,192 @@ __device__ __forceinline__ void soft_dist(T x0, T y0, const T v[6], float multip
     }
 }
 
-// LDS per wave: code[K][64] (face << 3 | type) + prob[K][64] + kid[64]
+// Pixel interval [lo, hi] (lane indices of the row segment starting at pixel ibase,
+// clipped to [0, 63]) whose centres c satisfy  x_lo <= c < x_hi  exactly as the
+// reference's float/double comparisons decide it: a float estimate, then corrected
+// against the exact centre formula (monotone in the index).  NaN bounds never reject.
+template <typename T>
+__device__ __forceinline__ void seg_range(T x_lo, T x_hi, float m, int W, int ibase, int &lo, int &hi) {
+  if (!(x_lo == x_lo) || !(x_hi == x_hi)) {
+    lo = 0;
+    hi = 63;
+    return;
+  }
+  const float inv = (float)W / m;  // index = (c / s + W - 1) / 2, s = m / W
+  auto est = [&](T c) -> int {
+    const float t = ((float)c * inv + (float)(W - 1)) * 0.5f - (float)ibase;
+    return t < -1.0f ? -1 : (t > 64.0f ? 64 : (int)ceilf(t));
+  };
+  auto cx = [&](int l) { return pix_x<T>(m, W, ibase + l); };
+  lo = min(max(est(x_lo), 0), 64);  // first lane with c >= x_lo
+  while (lo > 0 && cx(lo - 1) >= x_lo) lo--;
+  while (lo < 64 && !(cx(lo) >= x_lo)) lo++;
+  hi = min(max(est(x_hi) - 1, -1), 63);  // last lane with c < x_hi
+  while (hi < 63 && cx(hi + 1) < x_hi) hi++;
+  while (hi >= 0 && !(cx(hi) < x_hi)) hi--;
+}
+
+// Forward, one wave per 64-pixel row segment, three phases:
+//  1. selection: walk the candidate chunks of the tile in ascending order (the next
+//     chunk's bboxes are loaded while the current one is tested).  Each lane takes one
+//     face of the chunk and computes the exact lane interval its bbox covers on this
+//     row; only faces whose interval meets a still-active pixel (uncovered, < knum
+//     hits) are visited, in lane order, appending their id to the slot list of every
+//     active pixel of the interval ([slot][lane] in LDS);
+//  2. evaluation: the wave's hits, flattened, are evaluated 64 at a time with every
+//     lane busy (distance, probability, type), written straight to their output slots
+//     and the probabilities kept in LDS for the in-order product;
+//  3. the unused slots (-1 / 0 / 0) are written with lane-contiguous stores.
+// LDS per wave: K x 64 slots of sizeof(T) (face id, then its probability) + 2 x 64 ints.
 template <typename T, typename Src>
-__global__ void __launch_bounds__(128) soft_mask_fwd_kernel(
-    Src src, const int64_t *__restrict__ sel,
+__global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
+    Src src, const T *__restrict__ bbox, const int64_t *__restrict__ sel,
     const uint32_t *__restrict__ bitmap, BinGeom g, int F, int K, float sigmainv, float multiplier,
     T *__restrict__ out_mask, T *__restrict__ out_prob, int64_t *__restrict__ out_idx,
-    uint8_t *__restrict__ out_type) {
+    uint8_t *__restrict__ out_type, uint8_t *__restrict__ out_hits, bool bbox_vec4) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int waves = blockDim.x >> 6;
-  const size_t per_wave = (size_t)K * 64 * (sizeof(uint32_t) + sizeof(T)) + 64 * sizeof(int);
+  const size_t per_wave = (size_t)K * 64 * sizeof(T) + 128 * sizeof(int);
   unsigned char *mine = smem + per_wave * wid;
-  T *s_prob = reinterpret_cast<T *>(mine);
-  uint32_t *s_code = reinterpret_cast<uint32_t *>(mine + (size_t)K * 64 * sizeof(T));
-  int *s_kid = reinterpret_cast<int *>(mine + (size_t)K * 64 * (sizeof(T) + sizeof(uint32_t)));
+  T *s_slot = reinterpret_cast<T *>(mine);                                    // [K][64]
+  int *s_kid = reinterpret_cast<int *>(mine + (size_t)K * 64 * sizeof(T));   // [64]
+  int *s_pre = s_kid + 64;                                                    // [64] exclusive prefix
 
   const int j = blockIdx.y * waves + wid;
   const int b = blockIdx.z;
   const int tx = blockIdx.x;
   const int H = g.height, W = g.width;
   if (j >= H) return;
-  const int i = tx * TILE_W + lane;
+  const int ibase = tx * TILE_W;
+  const int i = ibase + lane;
   const bool px_valid = i < W;
   const size_t pix = ((size_t)b * H + j) * W + (px_valid ? i : W - 1);
   const bool covered = px_valid ? (sel[pix] >= 0) : true;
-
-  const T x0 = pix_x<T>(multiplier, W, px_valid ? i : W - 1);
   const T y0 = pix_y<T>(multiplier, H, j);
-  const int ilast = min(tx * TILE_W + 63, W - 1);
-  const T xa = pix_x<T>(multiplier, W, tx * TILE_W), xb = pix_x<T>(multiplier, W, ilast);
-  const T sxlo = xa < xb ? xa : xb, sxhi = xa < xb ? xb : xa;
+  // phase 1 view: the id of slot (k, lane) lives in the first 4 bytes of s_slot[k*64 + lane]
+  uint32_t *s_face = reinterpret_cast<uint32_t *>(s_slot);
+  constexpr int ID_STEP = (int)(sizeof(T) / sizeof(uint32_t));
 
+  // ---- phase 1: selection
   int kid = 0;
   bool active = !covered && K > 0;
+  uint64_t amask = ballot(active);
   const uint32_t *words = bitmap + ((size_t)(b * g.tiles_y + j / TILE_H) * g.tiles_x + tx) * g.words;
   const int64_t f0 = (int64_t)b * F;
-  for (int wi = 0; wi < g.words && ballot(active); wi++) {
-    uint32_t word = words[wi];
-    while (word && ballot(active)) {
-      const int c = wi * 32 + __builtin_ctz(word);
-      word &= word - 1;
-      const int fl = c * 64 + lane;  // face index within the mesh
-      const bool fv = fl < F;
-      T bx0 = 0, by0 = 0, bx1 = 0, by1 = 0;
-      if (fv) src.get(f0 + fl, bx0, by0, bx1, by1);
-      const bool touch = fv && !(y0 < by0 || y0 >= by1 || sxhi < bx0 || sxlo >= bx1);
-      uint64_t mask = ballot(touch);
-      if (!mask) continue;
-      T v[6] = {0, 0, 0, 0, 0, 0};
-      if (touch) src.verts(f0 + fl, v);
-      while (mask) {
-        const int s = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const T xmin = bcast(bx0, s), ymin = bcast(by0, s), xmax = bcast(bx1, s), ymax = bcast(by1, s);
-        T vb[6];
-#pragma unroll
-        for (int q = 0; q < 6; q++) vb[q] = bcast(v[q], s);
-        if (active && !(x0 < xmin || x0 >= xmax || y0 < ymin || y0 >= ymax)) {
-          T dsq;
-          int edgeid;
-          soft_dist<T>(x0, y0, vb, multiplier, dsq, edgeid);
-          const T z = (T)sigmainv * dsq / (T)multiplier / (T)multiplier;
-          const T pr = kl_exp<T>(-z);
-          s_prob[kid * 64 + lane] = pr;
-          s_code[kid * 64 + lane] = ((uint32_t)(c * 64 + s) << 3) | (uint32_t)(edgeid + 1);
-          kid++;
-          if (kid >= K) active = false;
-        }
-        if (!ballot(active)) break;
+  const T *bb = bbox + f0 * 4;
+  // candidate chunks: 64 bitmap words per vector load, non-empty words found by ballot
+  int wg = 0;                 // word group (64 words)
+  uint32_t wv = 0;            // this lane's word of the group
+  uint64_t wmask = 0;         // non-empty words of the group
+  uint32_t word = 0;          // word being consumed (uniform)
+  int wbase = 0;              // chunk index of bit 0 of `word`
+  auto next_chunk = [&]() -> int {
+    while (!word) {
+      while (!wmask) {
+        if (wg * 64 >= g.words) return -1;
+        const int w = wg * 64 + lane;
+        wv = w < g.words ? words[w] : 0u;
+        wmask = ballot(wv != 0);
+        wg++;
+      }
+      const int s = __builtin_ctzll(wmask);
+      wmask &= wmask - 1;
+      word = (uint32_t)__builtin_amdgcn_readlane((int)wv, s);
+      wbase = ((wg - 1) * 64 + s) * 32;
+    }
+    const int c = wbase + __builtin_ctz(word);
+    word &= word - 1;
+    return c;
+  };
+  T nb0 = 0, nb1 = 0, nb2 = 0, nb3 = 0;
+  auto load_chunk = [&](int c) {
+    const int fl = c * 64 + lane;
+    if (fl < F) {
+      if (sizeof(T) == 4 && bbox_vec4) {
+        const float4 q = reinterpret_cast<const float4 *>(bb)[fl];
+        nb0 = (T)q.x;
+        nb1 = (T)q.y;
+        nb2 = (T)q.z;
+        nb3 = (T)q.w;
+      } else {
+        nb0 = bb[fl * 4 + 0];
+        nb1 = bb[fl * 4 + 1];
+        nb2 = bb[fl * 4 + 2];
+        nb3 = bb[fl * 4 + 3];
       }
     }
+  };
+  int cn = -1;
+  if (amask) {
+    cn = next_chunk();
+    if (cn >= 0) load_chunk(cn);
   }
+  while (cn >= 0 && amask) {
+    const int c = cn;
+    const T bx0 = nb0, by0 = nb1, bx1 = nb2, by1 = nb3;
+    cn = next_chunk();
+    if (cn >= 0) load_chunk(cn);  // in flight while chunk c is tested
+    const int fl = c * 64 + lane;
+    int lo = 64, hi = -1;
+    if (fl < F && !(y0 < by0 || y0 >= by1)) seg_range<T>(bx0, bx1, multiplier, W, ibase, lo, hi);
+    const uint64_t rm = lo <= hi ? ((~0ull >> (63 - hi)) & (~0ull << lo)) : 0ull;
+    uint64_t mask = ballot((rm & amask) != 0);
+    while (mask) {
+      const int s = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const int a = __builtin_amdgcn_readlane(lo, s), e = __builtin_amdgcn_readlane(hi, s);
+      if (active && lane >= a && lane <= e) {
+        s_face[(kid * 64 + lane) * ID_STEP] = (uint32_t)(c * 64 + s);
+        kid++;
+        if (kid >= K) active = false;
+      }
+      amask = ballot(active);
+      if (!amask) break;
+      // faces of this chunk whose interval no longer meets an active pixel are skipped
+      mask &= ballot((rm & amask) != 0);
+    }
+  }
+  if (!px_valid) kid = 0;
+  if (out_hits && px_valid) out_hits[pix] = (uint8_t)kid;
+
+  // ---- phase 2: dense evaluation of the wave's hits
+  int pre = kid;  // inclusive scan over lanes
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(pre, o);
+    if (lane >= o) pre += u;
+  }
+  const int total = __shfl(pre, 63);
+  s_kid[lane] = kid;
+  s_pre[lane] = pre - kid;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const size_t rowpix0 = ((size_t)b * H + j) * W + (size_t)ibase;
+  for (int e = lane; e < total; e += 64) {
+    int lo = 0;  // owner lane p: last lane with s_pre[p] <= e (and a hit)
+#pragma unroll
+    for (int st = 32; st > 0; st >>= 1)
+      if (s_pre[lo + st] <= e) lo += st;
+    const int p = lo, k = e - s_pre[p];
+    const uint32_t fl = s_face[(k * 64 + p) * ID_STEP];
+    T v[6];
+    src.verts(f0 + fl, v);
+    T dsq;
+    int edgeid;
+    soft_dist<T>(pix_x<T>(multiplier, W, ibase + p), y0, v, multiplier, dsq, edgeid);
+    const T z = (T)sigmainv * dsq / (T)multiplier / (T)multiplier;
+    const T pr = kl_exp<T>(-z);
+    const size_t o = (rowpix0 + p) * K + k;
+    out_prob[o] = pr;
+    out_idx[o] = (int64_t)fl;
+    out_type[o] = (uint8_t)(edgeid + 1);
+    s_slot[k * 64 + p] = pr;  // overwrites only this hit's own id
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
   // soft mask value: 1 - prod(1 - p) in double, slot order (dibr_soft_mask_cuda.cu:174-182)
   if (px_valid) {
     T res;
@@ -138,112 +251,219 @@ __global__ void __launch_bounds__(128) soft_mask_fwd_kernel(
       res = (T)1.0;
     } else {
       T allprob = (T)1.0;
-      for (int k = 0; k < kid; k++) allprob = (T)((double)allprob * (1.0 - (double)s_prob[k * 64 + lane]));
+      for (int k = 0; k < kid; k++) allprob = (T)((double)allprob * (1.0 - (double)s_slot[k * 64 + lane]));
       res = (T)(1.0 - (double)allprob);
     }
     out_mask[pix] = res;
   }
-  s_kid[lane] = px_valid ? kid : 0;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // write this wave's contiguous slot range [pix0*K, (pix0+n)*K)
-  const int n = min(64, W - tx * TILE_W);
-  const size_t e0 = (((size_t)b * H + j) * W + (size_t)tx * TILE_W) * K;
+
+  // ---- phase 3: the unused slots of this row segment, lane-contiguous
+  if (K == 0) return;
+  const int n = min(64, W - ibase);
   const int ne = n * K;
+  int p = 0, k = lane;  // element e = p*K + k, advanced incrementally (no division)
+  while (k >= K) {
+    k -= K;
+    p++;
+  }
+  const int dp = 64 / K, dk = 64 - dp * K;
   for (int e = lane; e < ne; e += 64) {
-    const int p = e / K, k = e - p * K;
-    const bool hit = k < s_kid[p];
-    const uint32_t code = hit ? s_code[k * 64 + p] : 0u;
-    out_idx[e0 + e] = hit ? (int64_t)(code >> 3) : (int64_t)-1;
-    out_prob[e0 + e] = hit ? s_prob[k * 64 + p] : (T)0;
-    out_type[e0 + e] = (uint8_t)(code & 7u);
+    if (k >= s_kid[p]) {
+      const size_t o = rowpix0 * K + e;
+      out_idx[o] = -1;
+      out_prob[o] = (T)0;
+      out_type[o] = 0;
+    }
+    p += dp;
+    k += dk;
+    if (k >= K) {
+      k -= K;
+      p++;
+    }
   }
 }
 
+// Backward, aggregated: one 512-thread workgroup per 64x8 tile (one wave per row
+// segment).  The wave's hits (the first kid slots of each uncovered pixel) are
+// evaluated densely, 64 at a time, and the per-face vertex-gradient terms -- the
+// reference's expressions, each already divided by the multiplier as it adds them --
+// are summed in an LDS hash table keyed by face (faces of a tile are shared by many
+// of its pixels); the table is flushed with one global atomic per (face, coordinate).
+// Faces that do not fit the table fall back to direct global atomics.
+// kid per pixel: `hits` from the fused forward, or the reference's scan of the slots
+// up to the first -1 (hits == nullptr, the _C contract).
+constexpr int SMB_HCAP = 1024;
+
 template <typename T, bool SCALE>
-__global__ void __launch_bounds__(256) soft_mask_bwd_kernel(
+__global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const int64_t *__restrict__ sel,
     const T *__restrict__ prob, const int64_t *__restrict__ cidx, const uint8_t *__restrict__ ctype,
-    const T *__restrict__ fvi, int B, int H, int W, int F, int K, float sigmainv, float multiplier,
-    T *__restrict__ gfvi) {
-  // SCALE: fvi holds unscaled coordinates, multiplied here exactly as the front-end's
-  // `face_vertices_image * multiplier` (dibr.py:31) would have
+    const uint8_t *__restrict__ hits, const T *__restrict__ fvi, int B, int H, int W, int F, int K,
+    float sigmainv, float multiplier, T *__restrict__ gfvi) {
+  __shared__ int s_key[SMB_HCAP];
+  __shared__ T s_val[SMB_HCAP * 6];
+  __shared__ double s_a[8][64];
+  __shared__ int s_pre[8][64];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  for (int q = threadIdx.x; q < SMB_HCAP; q += blockDim.x) s_key[q] = -1;
+  for (int q = threadIdx.x; q < SMB_HCAP * 6; q += blockDim.x) s_val[q] = (T)0;
+  __syncthreads();
+
+  const int b = blockIdx.z;
+  const int j = blockIdx.y * 8 + wid;
+  const int ibase = blockIdx.x * 64;
+  const int i = ibase + lane;
   const T ms = (T)multiplier;
-  auto V = [&](size_t k) -> T { return SCALE ? fvi[k] * ms : fvi[k]; };
-  const int64_t npix = (int64_t)H * W;
-  for (int64_t tp = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; tp < (int64_t)B * npix;
-       tp += (int64_t)gridDim.x * blockDim.x) {
-    if (sel[tp] >= 0) continue;
-    const int b = (int)(tp / npix);
-    const int rem = (int)(tp - (int64_t)b * npix);
-    const int j = rem / W, i = rem - j * W;
-    const T x0 = pix_x<T>(multiplier, W, i);
-    const T y0 = pix_y<T>(multiplier, H, j);
-    const T dLdp = grad[tp];
-    const T allprob = mask[tp];
-    const size_t pk = (size_t)tp * K;
-    for (int k = 0; k < K; k++) {
-      const int64_t f = cidx[pk + k];
-      if (f < 0) break;
-      const size_t s6 = ((size_t)b * F + f) * 6;
-      const T pr = prob[pk + k];
-      const T dLdz = (T)(-1.0 * (double)sigmainv * (double)dLdp * (1.0 - (double)allprob) /
-                         (1.0 - (double)pr + SM_EPS) * (double)pr);
-      const int edgeid = (int)ctype[pk + k] - 1;
-      if (edgeid >= 3) {
-        const size_t ps = s6 + (edgeid - 3) * 2;
-        const T x1 = V(ps), y1 = V(ps + 1);
-        const T dLdx1 = dLdz * (T)2 * (x1 - x0);
-        const T dLdy1 = dLdz * (T)2 * (y1 - y0);
-        atomicAdd(gfvi + ps + 0, dLdx1 / (T)multiplier);
-        atomicAdd(gfvi + ps + 1, dLdy1 / (T)multiplier);
+  const T *fb = fvi + (size_t)b * F * 6;  // this mesh's face vertices
+  auto V = [&](size_t k) -> T { return SCALE ? fb[k] * ms : fb[k]; };
+  int kid = 0;
+  size_t pk = 0;
+  if (j < H && i < W) {
+    const size_t p = ((size_t)b * H + j) * W + i;
+    pk = p * K;
+    if (sel[p] < 0) {
+      if (hits) {
+        kid = hits[p];
       } else {
-        const size_t ps = s6 + edgeid * 2, ps2 = s6 + ((edgeid + 1) % 3) * 2;
-        const T x1 = V(ps), y1 = V(ps + 1), x2 = V(ps2), y2 = V(ps2 + 1);
-        const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
-        const T up = A * x0 + Bc * y0 + C;
-        const T down = A * A + Bc * Bc;
-        const T dsq = (T)((double)(up * up) / ((double)down + SM_EPS));
-        const T dzdA = (T)((double)((T)2 * (x0 * up - dsq * A)) / ((double)down + SM_EPS));
-        const T dzdB = (T)((double)((T)2 * (y0 * up - dsq * Bc)) / ((double)down + SM_EPS));
-        const T dzdC = (T)((double)((T)2 * up) / ((double)down + SM_EPS));
-        const T dLdx1 = dLdz * (dzdB - y2 * dzdC);
-        const T dLdy1 = dLdz * (x2 * dzdC - dzdA);
-        const T dLdx2 = dLdz * (y1 * dzdC - dzdB);
-        const T dLdy2 = dLdz * (dzdA - x1 * dzdC);
-        atomicAdd(gfvi + ps + 0, dLdx1 / (T)multiplier);
-        atomicAdd(gfvi + ps + 1, dLdy1 / (T)multiplier);
-        atomicAdd(gfvi + ps2 + 0, dLdx2 / (T)multiplier);
-        atomicAdd(gfvi + ps2 + 1, dLdy2 / (T)multiplier);
+        while (kid < K && cidx[pk + kid] >= 0) kid++;
+      }
+      // the reference's  -1.0 * sigmainv * dLdp * (1.0 - allprob), evaluated left to right
+      s_a[wid][lane] = -1.0 * (double)sigmainv * (double)grad[p] * (1.0 - (double)mask[p]);
+    }
+  }
+  int pre = kid;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(pre, o);
+    if (lane >= o) pre += u;
+  }
+  const int total = __shfl(pre, 63);
+  s_pre[wid][lane] = pre - kid;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+  const T y0 = pix_y<T>(multiplier, H, j < H ? j : 0);
+  const size_t rowk = (((size_t)b * H + (j < H ? j : 0)) * W + ibase) * K;
+  T *gb = gfvi + (size_t)b * F * 6;
+  for (int e = lane; e < total; e += 64) {
+    int lo = 0;
+#pragma unroll
+    for (int st = 32; st > 0; st >>= 1)
+      if (s_pre[wid][lo + st] <= e) lo += st;
+    const int p = lo, k = e - s_pre[wid][p];
+    const size_t o = rowk + (size_t)p * K + k;
+    const int f = (int)cidx[o];
+    const T pr = prob[o];
+    const int edgeid = (int)ctype[o] - 1;
+    const T x0 = pix_x<T>(multiplier, W, ibase + p);
+    const T dLdz = (T)(s_a[wid][p] / (1.0 - (double)pr + SM_EPS) * (double)pr);
+    const size_t s6 = (size_t)f * 6;
+    int c0, c1 = -1;  // coordinate pairs touched: vertex c0 (and c1)
+    T g0x, g0y, g1x = 0, g1y = 0;
+    if (edgeid >= 3) {
+      c0 = edgeid - 3;
+      const T x1 = V(s6 + c0 * 2), y1 = V(s6 + c0 * 2 + 1);
+      g0x = dLdz * (T)2 * (x1 - x0) / (T)multiplier;
+      g0y = dLdz * (T)2 * (y1 - y0) / (T)multiplier;
+    } else {
+      c0 = edgeid;
+      c1 = (edgeid + 1) % 3;
+      const size_t ps = s6 + c0 * 2, ps2 = s6 + c1 * 2;
+      const T x1 = V(ps), y1 = V(ps + 1), x2 = V(ps2), y2 = V(ps2 + 1);
+      const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
+      const T up = A * x0 + Bc * y0 + C;
+      const T down = A * A + Bc * Bc;
+      const T dsq = (T)((double)(up * up) / ((double)down + SM_EPS));
+      const T dzdA = (T)((double)((T)2 * (x0 * up - dsq * A)) / ((double)down + SM_EPS));
+      const T dzdB = (T)((double)((T)2 * (y0 * up - dsq * Bc)) / ((double)down + SM_EPS));
+      const T dzdC = (T)((double)((T)2 * up) / ((double)down + SM_EPS));
+      g0x = dLdz * (dzdB - y2 * dzdC) / (T)multiplier;
+      g0y = dLdz * (x2 * dzdC - dzdA) / (T)multiplier;
+      g1x = dLdz * (y1 * dzdC - dzdB) / (T)multiplier;
+      g1y = dLdz * (dzdA - x1 * dzdC) / (T)multiplier;
+    }
+    // LDS hash slot of face f (linear probing, bounded)
+    int slot = -1;
+    unsigned h = ((unsigned)f * 2654435761u) >> 22;  // 10 bits
+#pragma unroll 1
+    for (int t = 0; t < 16; t++) {
+      const int cur = s_key[h];
+      if (cur == f) {
+        slot = (int)h;
+        break;
+      }
+      if (cur == -1) {
+        const int prev = atomicCAS(&s_key[h], -1, f);
+        if (prev == -1 || prev == f) {
+          slot = (int)h;
+          break;
+        }
+      }
+      h = (h + 1) & (SMB_HCAP - 1);
+    }
+    if (slot >= 0) {
+      atomicAdd(&s_val[slot * 6 + c0 * 2], g0x);
+      atomicAdd(&s_val[slot * 6 + c0 * 2 + 1], g0y);
+      if (c1 >= 0) {
+        atomicAdd(&s_val[slot * 6 + c1 * 2], g1x);
+        atomicAdd(&s_val[slot * 6 + c1 * 2 + 1], g1y);
+      }
+    } else {
+      atomicAdd(gb + s6 + c0 * 2, g0x);
+      atomicAdd(gb + s6 + c0 * 2 + 1, g0y);
+      if (c1 >= 0) {
+        atomicAdd(gb + s6 + c1 * 2, g1x);
+        atomicAdd(gb + s6 + c1 * 2 + 1, g1y);
       }
     }
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < SMB_HCAP * 6; q += blockDim.x) {
+    const int key = s_key[q / 6];
+    const T v = s_val[q];
+    if (key >= 0 && v != (T)0) atomicAdd(gb + (size_t)key * 6 + q % 6, v);
   }
 }
 
 template <typename T>
 static size_t sm_lds_per_wave(int K) {
-  return (size_t)K * 64 * (sizeof(uint32_t) + sizeof(T)) + 64 * sizeof(int);
+  return (size_t)K * 64 * sizeof(T) + 128 * sizeof(int);
 }
 
+// workspace: bin bitmap | per-face bboxes (fused path; sized for f64)
+static size_t sm_ws_bbox_off(const BinGeom &g) { return (g.bytes() + 255) & ~(size_t)255; }
+static size_t sm_ws_bytes(int B, int H, int W, int F) {
+  return sm_ws_bbox_off(make_bin_geom(B, H, W, F)) + (size_t)B * F * 4 * sizeof(double);
+}
+
+// bbox == nullptr: the source computes the bboxes (fused path) and binning stores them
 template <typename T, typename Src>
-static int soft_mask_fwd(Src src, int B, int H, int W, int F, int K, const int64_t *sel, float sigmainv, float m,
-                         void *mask, void *prob, int64_t *cidx, uint8_t *ctype, void *ws, size_t ws_bytes,
-                         hipStream_t st) {
+static int soft_mask_fwd(Src src, const T *bbox, int B, int H, int W, int F, int K, const int64_t *sel,
+                         float sigmainv, float m, void *mask, void *prob, int64_t *cidx, uint8_t *ctype,
+                         uint8_t *hits, void *ws, size_t ws_bytes, hipStream_t st) {
   BinGeom g = make_bin_geom(B, H, W, F);
-  KL_REQUIRE(ws_bytes >= g.bytes(), "dibr_soft_mask_forward: workspace too small");
+  KL_REQUIRE(ws_bytes >= (bbox ? g.bytes() : sm_ws_bytes(B, H, W, F)),
+             "dibr_soft_mask_forward: workspace too small");
   KL_REQUIRE(K >= 0, "dibr_soft_mask_forward: knum must be >= 0");
   KL_REQUIRE(F < (1 << 28), "dibr_soft_mask_forward: too many faces");
+  KL_REQUIRE(hits == nullptr || K <= 255, "dibr_soft_mask_forward: per-pixel hit counts need knum <= 255");
   if (B == 0 || H == 0 || W == 0) return KL_OK;
   uint32_t *bitmap = reinterpret_cast<uint32_t *>(ws);
-  int rc = launch_binning<T, Src>(src, nullptr, F, g, m, bitmap, st);
+  T *bbox_out = nullptr;
+  if (!bbox) {
+    bbox_out = reinterpret_cast<T *>(reinterpret_cast<char *>(ws) + sm_ws_bbox_off(g));
+    bbox = bbox_out;
+  }
+  int rc = launch_binning<T, Src>(src, nullptr, F, g, m, bitmap, st, bbox_out);
   if (rc) return rc;
   const size_t pw = sm_lds_per_wave<T>(K);
-  int waves = 2;
-  if (pw * 2 > 160 * 1024) waves = 1;
-  KL_REQUIRE(pw * waves <= 160 * 1024, "dibr_soft_mask_forward: knum too large for the LDS staging buffer");
+  int waves = 4;
+  while (waves > 1 && pw * waves > 64 * 1024) waves--;
+  KL_REQUIRE(pw * waves <= 160 * 1024, "dibr_soft_mask_forward: knum too large for the LDS slot lists");
   dim3 grid(g.tiles_x, (unsigned)cdiv(H, waves), B);
-  hipLaunchKernelGGL((soft_mask_fwd_kernel<T, Src>), grid, dim3(64 * waves), pw * waves, st, src, sel, bitmap, g, F, K,
-                     sigmainv, m, (T *)mask, (T *)prob, cidx, ctype);
+  hipLaunchKernelGGL((soft_mask_fwd_kernel<T, Src>), grid, dim3(64 * waves), pw * waves, st, src, bbox, sel, bitmap,
+                     g, F, K, sigmainv, m, (T *)mask, (T *)prob, cidx, ctype, hits, ((uintptr_t)bbox & 15) == 0);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
@@ -251,14 +471,13 @@ static int soft_mask_fwd(Src src, int B, int H, int W, int F, int K, const int64
 template <typename T, bool SCALE>
 static int soft_mask_bwd(int B, int H, int W, int F, int K, const void *grad, const void *mask,
                          const int64_t *sel, const void *prob, const int64_t *cidx, const uint8_t *ctype,
-                         const void *fvi, float sigmainv, float m, void *gfvi, hipStream_t st) {
+                         const uint8_t *hits, const void *fvi, float sigmainv, float m, void *gfvi, hipStream_t st) {
+  KL_REQUIRE(F < (1 << 28), "dibr_soft_mask_backward: too many faces");
   KL_CHECK_HIP(hipMemsetAsync(gfvi, 0, sizeof(T) * (size_t)B * F * 6, st));
-  const int64_t total = (int64_t)B * H * W;
-  if (total == 0) return KL_OK;
-  const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(total, 256), 65536);
-  hipLaunchKernelGGL((soft_mask_bwd_kernel<T, SCALE>), dim3(blocks), dim3(256), 0, st, (const T *)grad,
-                     (const T *)mask, sel, (const T *)prob, cidx, ctype, (const T *)fvi, B, H, W, F, K, sigmainv, m,
-                     (T *)gfvi);
+  if ((int64_t)B * H * W == 0 || K <= 0) return KL_OK;
+  dim3 grid((unsigned)cdiv(W, 64), (unsigned)cdiv(H, 8), B);
+  hipLaunchKernelGGL((soft_mask_bwd_agg_kernel<T, SCALE>), grid, dim3(512), 0, st, (const T *)grad, (const T *)mask,
+                     sel, (const T *)prob, cidx, ctype, hits, (const T *)fvi, B, H, W, F, K, sigmainv, m, (T *)gfvi);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
@@ -268,7 +487,7 @@ static int soft_mask_bwd(int B, int H, int W, int F, int K, const void *grad, co
 using namespace kl;
 
 extern "C" size_t kl_soft_mask_workspace_bytes(int batch, int height, int width, int num_faces) {
-  return make_bin_geom(batch, height, width, num_faces).bytes();
+  return sm_ws_bytes(batch, height, width, num_faces);
 }
 
 extern "C" int kl_dibr_soft_mask_forward(kl_dtype dtype, int batch, int height, int width, int num_faces,
@@ -277,13 +496,13 @@ extern "C" int kl_dibr_soft_mask_forward(kl_dtype dtype, int batch, int height, 
                                          int64_t *cidx, uint8_t *ctype, void *ws, size_t ws_bytes,
                                          kl_stream stream) {
   if (dtype == KL_F32)
-    return soft_mask_fwd<float>(BboxSrc<float>{(const float *)bbox, (const float *)fvi}, batch, height, width,
-                                num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype, ws, ws_bytes,
-                                S(stream));
+    return soft_mask_fwd<float>(BboxSrc<float>{(const float *)bbox, (const float *)fvi}, (const float *)bbox, batch,
+                                height, width, num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype,
+                                nullptr, ws, ws_bytes, S(stream));
   if (dtype == KL_F64)
-    return soft_mask_fwd<double>(BboxSrc<double>{(const double *)bbox, (const double *)fvi}, batch, height, width,
-                                 num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype, ws, ws_bytes,
-                                 S(stream));
+    return soft_mask_fwd<double>(BboxSrc<double>{(const double *)bbox, (const double *)fvi}, (const double *)bbox,
+                                 batch, height, width, num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx,
+                                 ctype, nullptr, ws, ws_bytes, S(stream));
   set_error("dibr_soft_mask_forward_cuda not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -291,16 +510,16 @@ extern "C" int kl_dibr_soft_mask_forward(kl_dtype dtype, int batch, int height, 
 extern "C" int kl_dibr_soft_mask_forward_fused(kl_dtype dtype, int batch, int height, int width, int num_faces,
                                                int knum, const void *fvi, const int64_t *sel, float sigmainv,
                                                double pad, float multiplier, void *mask, void *prob,
-                                               int64_t *cidx, uint8_t *ctype, void *ws, size_t ws_bytes,
-                                               kl_stream stream) {
+                                               int64_t *cidx, uint8_t *ctype, uint8_t *hits, void *ws,
+                                               size_t ws_bytes, kl_stream stream) {
   if (dtype == KL_F32)
-    return soft_mask_fwd<float>(SoftSrc<float>{(const float *)fvi, (float)multiplier, (float)pad}, batch, height,
-                                width, num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype, ws,
-                                ws_bytes, S(stream));
+    return soft_mask_fwd<float>(SoftSrc<float>{(const float *)fvi, (float)multiplier, (float)pad}, nullptr, batch,
+                                height, width, num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype,
+                                hits, ws, ws_bytes, S(stream));
   if (dtype == KL_F64)
-    return soft_mask_fwd<double>(SoftSrc<double>{(const double *)fvi, (double)multiplier, pad}, batch, height, width,
-                                 num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype, ws, ws_bytes,
-                                 S(stream));
+    return soft_mask_fwd<double>(SoftSrc<double>{(const double *)fvi, (double)multiplier, pad}, nullptr, batch,
+                                 height, width, num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype,
+                                 hits, ws, ws_bytes, S(stream));
   set_error("dibr_soft_mask_forward not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -311,11 +530,11 @@ extern "C" int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height,
                                           const void *fvi, float sigmainv, float multiplier, void *gfvi,
                                           kl_stream stream) {
   if (dtype == KL_F32)
-    return soft_mask_bwd<float, false>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype, fvi,
-                                       sigmainv, multiplier, gfvi, S(stream));
+    return soft_mask_bwd<float, false>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype,
+                                       nullptr, fvi, sigmainv, multiplier, gfvi, S(stream));
   if (dtype == KL_F64)
     return soft_mask_bwd<double, false>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype,
-                                        fvi, sigmainv, multiplier, gfvi, S(stream));
+                                        nullptr, fvi, sigmainv, multiplier, gfvi, S(stream));
   set_error("dibr_soft_mask_backward_cuda not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -323,14 +542,14 @@ extern "C" int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height,
 extern "C" int kl_dibr_soft_mask_backward_fused(kl_dtype dtype, int batch, int height, int width, int num_faces,
                                                 int knum, const void *grad, const void *mask, const int64_t *sel,
                                                 const void *prob, const int64_t *cidx, const uint8_t *ctype,
-                                                const void *fvi, float sigmainv, float multiplier, void *gfvi,
-                                                kl_stream stream) {
+                                                const uint8_t *hits, const void *fvi, float sigmainv,
+                                                float multiplier, void *gfvi, kl_stream stream) {
   if (dtype == KL_F32)
-    return soft_mask_bwd<float, true>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype, fvi,
-                                      sigmainv, multiplier, gfvi, S(stream));
+    return soft_mask_bwd<float, true>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype, hits,
+                                      fvi, sigmainv, multiplier, gfvi, S(stream));
   if (dtype == KL_F64)
     return soft_mask_bwd<double, true>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype,
-                                       fvi, sigmainv, multiplier, gfvi, S(stream));
+                                       hits, fvi, sigmainv, multiplier, gfvi, S(stream));
   set_error("dibr_soft_mask_backward not implemented for this dtype");
   return KL_E_INVALID;
 }

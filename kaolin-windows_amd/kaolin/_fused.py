@@ -66,8 +66,9 @@ def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_featur
     return g_img, g_feat
 
 
-def soft_mask_forward(face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier):
-    """face_vertices_image UNSCALED -> soft_mask, close_face_prob, close_face_idx, close_face_dist_type."""
+def soft_mask_forward(face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier, with_hits=False):
+    """face_vertices_image UNSCALED -> soft_mask, close_face_prob, close_face_idx, close_face_dist_type
+    (+ the per-pixel filled-slot counts, uint8, when ``with_hits``; None if knum > 255)."""
     func = 'dibr_soft_mask'
     N.require_gpu(func, face_vertices_image)
     fvi = face_vertices_image.contiguous()
@@ -83,18 +84,21 @@ def soft_mask_forward(face_vertices_image, selected_face_idx, sigmainv, boxlen, 
     prob = torch.empty((B, H, W, K), dtype=dtype, device=dev)
     cidx = torch.empty((B, H, W, K), dtype=torch.long, device=dev)
     ctype = torch.empty((B, H, W, K), dtype=torch.uint8, device=dev)
+    hits = torch.empty((B, H, W), dtype=torch.uint8, device=dev) if with_hits and K <= 255 else None
     lib = N.lib()
     nbytes = lib.kl_soft_mask_workspace_bytes(B, H, W, F)
     ws = _ws(nbytes, dev)
     with torch.cuda.device(dev), N.timed('dibr_soft_mask_forward', dev):
         N.check(lib.kl_dibr_soft_mask_forward_fused(
             N.dtype_code(dtype), B, H, W, F, K, N.ptr(fvi), N.ptr(sel), float(sigmainv), float(boxlen * multiplier),
-            float(multiplier), N.ptr(mask), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(ws), nbytes,
+            float(multiplier), N.ptr(mask), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(hits), N.ptr(ws), nbytes,
             N.stream_of(dev)), func)
+    if with_hits:
+        return mask, prob, cidx, ctype, hits
     return mask, prob, cidx, ctype
 
 
-def soft_mask_backward(grad, mask, sel, prob, cidx, ctype, face_vertices_image, sigmainv, multiplier):
+def soft_mask_backward(grad, mask, sel, prob, cidx, ctype, face_vertices_image, sigmainv, multiplier, hits=None):
     func = 'dibr_soft_mask backward'
     B, F = face_vertices_image.shape[:2]
     H, W = sel.shape[1:]
@@ -104,6 +108,6 @@ def soft_mask_backward(grad, mask, sel, prob, cidx, ctype, face_vertices_image, 
     with torch.cuda.device(dev), N.timed('dibr_soft_mask_backward', dev):
         N.check(N.lib().kl_dibr_soft_mask_backward_fused(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, K, N.ptr(grad.contiguous()), N.ptr(mask),
-            N.ptr(sel), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(face_vertices_image), float(sigmainv),
+            N.ptr(sel), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(hits), N.ptr(face_vertices_image), float(sigmainv),
             float(multiplier), N.ptr(g), N.stream_of(dev)), func)
     return g

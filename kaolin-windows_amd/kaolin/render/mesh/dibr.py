@@ -16,21 +16,21 @@ class DibrSoftMaskCuda(Function):
     def forward(ctx, face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier):
         face_vertices_image = face_vertices_image.contiguous()
         selected_face_idx = selected_face_idx.contiguous()
-        soft_mask, close_face_prob, close_face_idx, close_face_dist_type = _fused.soft_mask_forward(
-            face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier)
+        soft_mask, close_face_prob, close_face_idx, close_face_dist_type, hits = _fused.soft_mask_forward(
+            face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier, with_hits=True)
         ctx.multiplier = multiplier
         ctx.sigmainv = sigmainv
         ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, close_face_prob, close_face_idx,
-                              close_face_dist_type)
+                              close_face_dist_type, hits)
         return soft_mask
 
     @staticmethod
     def backward(ctx, grad_soft_mask):
-        soft_mask, face_vertices_image, selected_face_idx, close_face_prob, close_face_idx, close_face_dist_type = \
-            ctx.saved_tensors
+        soft_mask, face_vertices_image, selected_face_idx, close_face_prob, close_face_idx, close_face_dist_type, \
+            hits = ctx.saved_tensors
         grad_face_vertices_image = _fused.soft_mask_backward(
             grad_soft_mask, soft_mask, selected_face_idx, close_face_prob, close_face_idx, close_face_dist_type,
-            face_vertices_image, ctx.sigmainv, ctx.multiplier)
+            face_vertices_image, ctx.sigmainv, ctx.multiplier, hits)
         return grad_face_vertices_image, None, None, None, None, None
 
 

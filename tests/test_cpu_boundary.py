@@ -40,9 +40,11 @@ def test_abi_version_and_error_channel():
 def test_workspace_sizes():
     from kaolin import _native
     lib = _native.lib()
-    # 512x512, 4 meshes of 50k faces: 8x64 tiles of 64x8 px, ceil(ceil(50000/64)/32) = 25 words
-    assert lib.kl_rasterize_workspace_bytes(4, 512, 512, 50000) == 4 * 8 * 64 * 25 * 4
-    assert lib.kl_soft_mask_workspace_bytes(4, 512, 512, 50000) == 4 * 8 * 64 * 25 * 4
+    # rasterizer visibility buffer: 8 B key + 4 B index + 1 B flag per pixel, + big-face queue
+    P = 4 * 512 * 512
+    assert lib.kl_rasterize_workspace_bytes(4, 512, 512, 50000) == 13 * P + (4 * 50000 + 1) * 4
+    # soft-mask bins: 8x64 tiles of 64x8 px, ceil(ceil(50000/64)/32) = 25 words, + f64 bboxes
+    assert lib.kl_soft_mask_workspace_bytes(4, 512, 512, 50000) == 4 * 8 * 64 * 25 * 4 + 4 * 50000 * 4 * 8
 
 
 def test_C_registry_layout():

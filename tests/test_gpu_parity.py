@@ -148,6 +148,89 @@ def test_fused_path_matches_packed_C_chain(kal, dtype, use_valid):
         assert torch.equal(x, y)
 
 
+def _adversarial_faces(dtype, seed=5):
+    """Small random faces on a coarse depth grid (exact depth ties between overlapping
+    faces), exact duplicates (same depth -> lowest index must win), -0.0/+0.0 depth ties,
+    faces far larger than 64 pixels, a NaN depth, an infinite and a NaN coordinate, a
+    zero-area face and faces straddling the screen border."""
+    g = np.random.default_rng(seed)
+    n = 400
+    c = g.uniform(-1.1, 1.1, (n, 1, 2))
+    fvi = c + g.uniform(-0.12, 0.12, (n, 3, 2))
+    fvz = -np.round(g.uniform(1, 3, (n, 1)) * 2) / 2 + np.zeros((n, 3))
+    fvi = np.concatenate([fvi, fvi[:60]])                      # duplicates
+    fvz = np.concatenate([fvz, fvz[:60]])
+    big = np.array([[[-0.9, -0.9], [0.9, -0.8], [0.0, 0.95]], [[-1.5, 1.5], [1.5, 1.5], [0.0, -1.5]]])
+    fvi = np.concatenate([fvi, big, big[:1], big[:1]])         # big faces, then a +0/-0 depth pair
+    fvz = np.concatenate([fvz, np.full((2, 3), -1.0), np.zeros((1, 3)), -np.zeros((1, 3))])
+    fvz[7, 0] = np.nan                                         # NaN depth
+    fvi[11, 1, 0] = np.inf                                     # infinite coordinate
+    fvi[13, 2, 1] = np.nan                                     # NaN coordinate
+    fvi[17] = fvi[17, :1]                                      # zero-area face
+    feat = g.uniform(-1, 1, (fvi.shape[0], 3, 2))
+    np_dt = np.float32 if dtype == torch.float32 else np.float64
+    return fvz[None].astype(np_dt), fvi[None].astype(np_dt), feat[None].astype(np_dt)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('backend', ['cuda', 'cuda_packed'])
+def test_rasterize_adversarial_vs_oracle(kal, dtype, backend):
+    z, v, f = _adversarial_faces(dtype)
+    z, v, f = np.concatenate([z, z[:, ::-1]]), np.concatenate([v, v[:, ::-1]]), np.concatenate([f, f[:, ::-1]])
+    valid = np.random.default_rng(1).uniform(size=z.shape[:2]) > 0.1
+    for vf in (None, valid):
+        feats, fidx = kal.render.mesh.rasterize(97, 130, T(z), T(v), T(f), None if vf is None else T(vf),
+                                                backend=backend)
+        of, oi, ow = orc.rasterize(97, 130, z, v, f, valid_faces=vf)
+        assert np.array_equal(A(fidx), oi)
+        assert np.array_equal(A(feats), of, equal_nan=True)
+        assert (oi >= 0).mean() > 0.5
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('K', [30, 8])
+def test_soft_mask_adversarial_vs_oracle(kal, dtype, K):
+    from kaolin import _fused
+    z, v, f = _adversarial_faces(dtype, seed=6)
+    _, sel = kal.render.mesh.rasterize(97, 130, T(z), T(v), T(f))
+    m, box, sig = 1000., 0.03, 7000.
+    mask, prob, cidx, ctype, hits = _fused.soft_mask_forward(T(v), sel, sig, box, K, m, with_hits=True)
+    assert np.array_equal(A(hits), (A(cidx) >= 0).sum(-1))
+    fm = v * v.dtype.type(m)
+    pad = v.dtype.type(box * m)
+    bb = np.concatenate([fm.min(-2) - pad, fm.max(-2) + pad], -1)
+    om, op, oi, ot = orc.dibr_soft_mask_forward(fm, bb, A(sel), sig, K, m)
+    assert np.array_equal(A(cidx), oi)
+    assert np.array_equal(A(ctype), ot)
+    np.testing.assert_allclose(A(prob), op, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(A(mask), om, rtol=1e-6, atol=1e-7)
+    assert (oi[..., -1] >= 0).sum() > (100 if K == 8 else -1)  # K=8: many pixels saturate knum
+    grad = torch.rand_like(mask)
+    ogi = orc.dibr_soft_mask_backward(A(grad), om, A(sel), op, oi, ot, fm, sig, m)
+    g1 = _fused.soft_mask_backward(grad, mask, sel, prob, cidx, ctype, T(v), sig, m, hits)
+    g2 = kal._C.render.mesh.dibr_soft_mask_backward_cuda(grad, mask, sel, prob, cidx, ctype, T(fm), sig, m)
+    fin = np.isfinite(ogi)
+    assert fin.mean() > 0.9
+    np.testing.assert_allclose(A(g1)[fin], ogi[fin], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(A(g2)[fin], ogi[fin], rtol=1e-5, atol=1e-5)
+
+
+def test_dibr_bench_sphere_vs_oracle(kal):
+    """The bench workload's mesh (50k-face UV sphere, heavy pole tiles) at 128x128:
+    rasterizer and soft mask bit-exact / 1e-6 against the oracle."""
+    import bench
+    inp = bench.dibr_inputs([0.3], DEV, H=128, W=128)
+    fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+    feats, mask, idx = kal.render.mesh.dibr_rasterization(128, 128, fvz, fvi, feat, fnz, 7000, 0.02, 30, 1000, 1e-8)
+    of, oi, ow = orc.rasterize(128, 128, A(fvz), A(fvi), A(feat), valid_faces=A(fnz >= 0))
+    assert np.array_equal(A(idx), oi)
+    assert np.array_equal(A(feats), of)
+    fm = A(fvi) * np.float32(1000.)
+    bb = np.concatenate([fm.min(-2) - np.float32(20.), fm.max(-2) + np.float32(20.)], -1)
+    om, op, oi2, ot = orc.dibr_soft_mask_forward(fm, bb, oi, 7000., 30, 1000.)
+    np.testing.assert_allclose(A(mask), om, rtol=1e-6, atol=1e-7)
+
+
 def test_rasterize_backward_vs_oracle(kal):
     fvz, fvi, feat, fnz = _render_inputs(kal, 30, 50, 2)
     fvi_r = fvi.clone().requires_grad_(True)
