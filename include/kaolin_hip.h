@@ -53,8 +53,8 @@ int kl_abi_version(void);
 
 /* ---------------------------------------------------------------- DIB-R */
 
-/* Workspace for the screen-space face bins of packed_rasterize_forward.
- * max_faces_per_mesh: upper bound on (first_idx[b+1] - first_idx[b]). */
+/* Workspace of packed_rasterize_forward: the per-pixel visibility buffer (13 B/px) and a
+ * queue of large faces.  max_faces_per_mesh: upper bound on (first_idx[b+1] - first_idx[b]). */
 size_t kl_rasterize_workspace_bytes(int batch, int height, int width, int64_t max_faces_per_mesh);
 
 /* rasterization.cpp:49-104  packed_rasterize_forward_cuda.
@@ -92,15 +92,16 @@ int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, int batch, 
                               const void *face_features, const uint8_t *valid_faces, float multiplier, float eps,
                               void *interpolated_features, int64_t *face_idx, void *output_weights,
                               void *workspace, size_t workspace_bytes, kl_stream stream);
-/* Atomic-free backward of the fused path: one thread per face gathers the pixels of its
- * conservative screen bbox whose face_idx equals it (deterministic, row-major order).
- * Requires face_idx produced by the forward (faces are only selected inside their bbox). */
+/* Atomic-free backward of the fused path: one thread per face gathers the pixels of the
+ * exact pixel range the forward visited for it (same valid_faces / multiplier) whose
+ * face_idx equals it (deterministic, row-major order).  Requires face_idx produced by
+ * kl_dibr_rasterize_forward with the same valid_faces and multiplier. */
 int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
                                const void *grad_interpolated_features, const int64_t *face_idx,
                                const void *output_weights, const void *face_vertices_image,
-                               const void *face_features, float eps, void *grad_face_vertices_image,
-                               void *grad_face_features, void *workspace, size_t workspace_bytes,
-                               kl_stream stream);
+                               const void *face_features, const uint8_t *valid_faces, float multiplier, float eps,
+                               void *grad_face_vertices_image, void *grad_face_features, void *workspace,
+                               size_t workspace_bytes, kl_stream stream);
 
 size_t kl_soft_mask_workspace_bytes(int batch, int height, int width, int num_faces);
 

@@ -156,16 +156,41 @@ __device__ __forceinline__ void face_mesh(int64_t f, const int64_t *__restrict__
   }
 }
 
-constexpr int VIS_SMALL_AREA = 64;  // faces covering more pixel centres go to the WG kernel
+constexpr int VIS_SMALL_AREA = 1024;  // faces covering more pixel centres go to the WG kernel
+constexpr int LPF = 8;                // lanes per face in the per-face kernels
 
-// one thread per face; faces whose exact pixel range exceeds VIS_SMALL_AREA are queued
+// Walks a face's exact pixel range [ix0,ix1]x[iy0,iy1] in row-major order, lane s of the
+// face's lane group taking elements s, s+LPF, ...  (no divisions in the loop).
+struct RangeWalk {
+  int w, area, e, col, row;
+  __device__ __forceinline__ RangeWalk(int ix0, int ix1, int iy0, int iy1, int s) {
+    w = ix1 - ix0 + 1;
+    area = w * (iy1 - iy0 + 1);
+    e = s;
+    row = s / w;
+    col = s - row * w;
+  }
+  __device__ __forceinline__ bool more() const { return e < area; }
+  __device__ __forceinline__ void next() {
+    e += LPF;
+    col += LPF;
+    while (col >= w) {
+      col -= w;
+      row++;
+    }
+  }
+};
+
+// LPF lanes per face; faces whose exact pixel range exceeds VIS_SMALL_AREA are queued
 template <typename T, typename Src, int PASS>
 __global__ void __launch_bounds__(256) raster_vis_kernel(Src src, const T *__restrict__ fvz,
                                                          const int64_t *__restrict__ first_idx, int B,
                                                          int faces_per_mesh, int64_t nfaces, int H, int W, float m,
                                                          float eps, VisBuf vb, int *__restrict__ big,
                                                          int *__restrict__ nbig) {
-  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t f = t / LPF;
+  const int s = (int)(t % LPF);
   if (f >= nfaces || !src.valid(f)) return;
   RastFace<T> r;
   load_face(src, fvz, f, r);
@@ -175,21 +200,19 @@ __global__ void __launch_bounds__(256) raster_vis_kernel(Src src, const T *__res
   exact_axis(r.ymin, r.ymax, m, H, true, iy0, iy1);
   if (iy0 > iy1) return;
   if ((int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) > VIS_SMALL_AREA) {
-    if (PASS == 0) big[atomicAdd(nbig, 1)] = (int)f;
+    if (PASS == 0 && s == 0) big[atomicAdd(nbig, 1)] = (int)f;
     return;
   }
   int b;
   int64_t f0;
   face_mesh(f, first_idx, B, faces_per_mesh, b, f0);
   const uint32_t local = (uint32_t)(f - f0);
-  for (int j = iy0; j <= iy1; j++) {
-    const T y0 = pix_y<T>(m, H, j);
-    const int64_t row = ((int64_t)b * H + j) * W;
-    for (int i = ix0; i <= ix1; i++) {
-      T w0, w1, w2;
-      if (face_weights(r, pix_x<T>(m, W, i), y0, eps, w0, w1, w2))
-        vis_update<PASS>(vb, row + i, face_depth(r, w0, w1, w2), local);
-    }
+  const int64_t pbase = (int64_t)b * H * W;
+  for (RangeWalk rw(ix0, ix1, iy0, iy1, s); rw.more(); rw.next()) {
+    const int i = ix0 + rw.col, j = iy0 + rw.row;
+    T w0, w1, w2;
+    if (face_weights(r, pix_x<T>(m, W, i), pix_y<T>(m, H, j), eps, w0, w1, w2))
+      vis_update<PASS>(vb, pbase + (int64_t)j * W + i, face_depth(r, w0, w1, w2), local);
   }
 }
 
@@ -311,7 +334,7 @@ static int launch_rast_fwd(Src src, int H, int W, int B, int D, int64_t nfaces, 
   KL_CHECK_HIP(hipMemsetAsync(w, 0, L.off_big + 4, st));
   if (sizeof(T) == 8) KL_CHECK_HIP(hipMemsetAsync(w + L.off_idx, 0xff, L.P * 4, st));
   if (nfaces > 0) {
-    const unsigned fb = (unsigned)cdiv(nfaces, 256);
+    const unsigned fb = (unsigned)cdiv(nfaces * LPF, 256);
     hipLaunchKernelGGL((raster_vis_kernel<T, Src, 0>), dim3(fb), dim3(256), 0, st, src, fvz, first_idx, B,
                        faces_per_mesh, nfaces, H, W, m, eps, vb, big, nbig);
     KL_CHECK_LAUNCH();
@@ -422,76 +445,121 @@ __global__ void __launch_bounds__(256) rasterize_bwd_kernel(
 }
 
 // ---------------------------------------------------------------- gather backward
-constexpr int GATHER_MAX_AREA = 1024;  // faces with larger screen bboxes go to the WG path
+// One thread per face visits exactly the pixel range the forward visited for it (the
+// same in-kernel bbox and exact_axis), so every pixel the face can have won is seen;
+// pixels are taken 8 at a time with their face_idx / weights / grads loads in flight
+// together.  Faces whose range exceeds VIS_SMALL_AREA go to a workgroup per face.
+constexpr int GATHER_BATCH = 4;
 
 template <typename T>
-__device__ __forceinline__ bool conservative_range(const T v[6], int H, int W, int &ix0, int &ix1, int &iy0,
-                                                   int &iy1) {
-  const T xmin = tmin3(v[0], v[2], v[4]), xmax = tmax3(v[0], v[2], v[4]);
-  const T ymin = tmin3(v[1], v[3], v[5]), ymax = tmax3(v[1], v[3], v[5]);
-  // unscaled pixel centres: x(i) = (2i+1-W)/W ; the forward compared in x multiplier
-  // space, which differs by rounding only -> +-1 pixel margin inside axis_range.
-  axis_range((double)xmin, (double)xmax, 1.0 / (double)W, W, false, ix0, ix1);
-  axis_range((double)ymin, (double)ymax, 1.0 / (double)H, H, true, iy0, iy1);
+__device__ __forceinline__ bool face_range(const RastSrc<T> &src, int64_t tf, float m, int H, int W, int &ix0,
+                                           int &ix1, int &iy0, int &iy1) {
+  T x0, y0, x1, y1;
+  src.get(tf, x0, y0, x1, y1);
+  exact_axis(x0, x1, m, W, false, ix0, ix1);
+  exact_axis(y0, y1, m, H, true, iy0, iy1);
   return ix0 <= ix1 && iy0 <= iy1;
 }
 
 template <typename T, int MAXD>
+struct GatherAcc {
+  T gi[6];
+  T gf[3 * MAXD];
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int q = 0; q < 6; q++) gi[q] = (T)0;
+#pragma unroll
+    for (int q = 0; q < 3 * MAXD; q++) gf[q] = (T)0;
+  }
+  // one pixel won by the face: the reference's per-pixel terms (rasterization_cuda.cu:262-399)
+  __device__ __forceinline__ void add(const T v[6], const T *c, int D, T w_a, T w_b, T w_c, const T *g, float eps) {
+    BaryGrad<T> bg;
+    bg.init(v, w_a, w_b, w_c, eps);
+#pragma unroll
+    for (int d = 0; d < MAXD; d++) {
+      if (d < D) {
+        const T gd = g[d];
+        gf[d] += gd * w_a;
+        gf[MAXD + d] += gd * w_b;
+        gf[2 * MAXD + d] += gd * w_c;
+        T o[6];
+        bg.terms(gd, c[d], c[D + d], c[2 * D + d], o);
+#pragma unroll
+        for (int q = 0; q < 6; q++) gi[q] += o[q];
+      }
+    }
+  }
+};
+
+template <typename T, int MAXD>
 __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
-    const T *__restrict__ fvi, const T *__restrict__ feat, int B, int H, int W, int F, int D, float eps,
-    T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig) {
-  const int64_t tf = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (tf >= (int64_t)B * F) return;
-  const int b = (int)(tf / F);
+    const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid, int B, int H, int W,
+    int F, int D, float m, float eps, T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat, int *__restrict__ big,
+    int *__restrict__ nbig) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t tf = t / LPF;  // LPF consecutive lanes per face (whole groups per wave)
+  const int s = (int)(t % LPF);
+  const bool in = tf < (int64_t)B * F;
+  const int b = in ? (int)(tf / F) : 0;
   const int64_t f = tf - (int64_t)b * F;
-  T v[6];
-#pragma unroll
-  for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
+  const RastSrc<T> src{fvi, valid, (T)m};
+  GatherAcc<T, MAXD> acc;
+  acc.zero();
   int ix0, ix1, iy0, iy1;
-  T gi[6] = {0, 0, 0, 0, 0, 0};
-  T gf[3 * MAXD];
+  bool queued = false;
+  if (in && src.valid(tf) && face_range(src, tf, m, H, W, ix0, ix1, iy0, iy1)) {
+    if ((int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) > VIS_SMALL_AREA) {
+      queued = true;
+      if (s == 0) big[atomicAdd(nbig, 1)] = (int)tf;
+    } else {
+      T v[6];
 #pragma unroll
-  for (int q = 0; q < 3 * MAXD; q++) gf[q] = (T)0;
-  if (conservative_range(v, H, W, ix0, ix1, iy0, iy1)) {
-    const int area = (ix1 - ix0 + 1) * (iy1 - iy0 + 1);
-    if (area > GATHER_MAX_AREA) {
-      big[atomicAdd(nbig, 1)] = (int)tf;
-      return;  // the WG kernel writes this face
-    }
-    const T *c = feat + tf * 3 * D;
-    for (int j = iy0; j <= iy1; j++) {
-      for (int i = ix0; i <= ix1; i++) {
-        const int64_t p = ((int64_t)b * H + j) * W + i;
-        if (face_idx[p] != f) continue;
-        const T w_a = wts[p * 3 + 0], w_b = wts[p * 3 + 1], w_c = wts[p * 3 + 2];
-        const T *g = grad_feat + p * D;
-        BaryGrad<T> bg;
-        bg.init(v, w_a, w_b, w_c, eps);
+      for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
+      const T *c = feat + tf * 3 * D;
+      const int64_t pbase = (int64_t)b * H * W;
+      RangeWalk rw(ix0, ix1, iy0, iy1, s);
+      while (rw.more()) {
+        // face_idx of GATHER_BATCH pixels in flight together; the (rare) hits then load
+        // their weights / grads one by one
+        int64_t px[GATHER_BATCH];
+        uint32_t hits = 0;
 #pragma unroll
-        for (int d = 0; d < MAXD; d++) {
-          if (d < D) {
-            const T gd = g[d];
-            gf[d] += gd * w_a;
-            gf[MAXD + d] += gd * w_b;
-            gf[2 * MAXD + d] += gd * w_c;
-            T o[6];
-            bg.terms(gd, c[d], c[D + d], c[2 * D + d], o);
+        for (int u = 0; u < GATHER_BATCH; u++) {
+          px[u] = pbase + (int64_t)(iy0 + rw.row) * W + ix0 + rw.col;
+          if (rw.more() && face_idx[px[u]] == f) hits |= 1u << u;
+          rw.next();
+        }
+#pragma unroll 1
+        for (; hits; hits &= hits - 1) {
+          const int u = __builtin_ctz(hits);
+          int64_t p = px[0];
 #pragma unroll
-            for (int q = 0; q < 6; q++) gi[q] += o[q];
-          }
+          for (int q = 1; q < GATHER_BATCH; q++)
+            if (u == q) p = px[q];
+          acc.add(v, c, D, wts[p * 3 + 0], wts[p * 3 + 1], wts[p * 3 + 2], grad_feat + p * D, eps);
         }
       }
     }
   }
+  // fixed-order butterfly over the face's lane group: every lane ends with the total
 #pragma unroll
-  for (int q = 0; q < 6; q++) grad_fvi[tf * 6 + q] = gi[q];
+  for (int o = 1; o < LPF; o <<= 1) {
 #pragma unroll
-  for (int d = 0; d < MAXD; d++) {
-    if (d < D) {
-      grad_ffeat[tf * 3 * D + d] = gf[d];
-      grad_ffeat[tf * 3 * D + D + d] = gf[MAXD + d];
-      grad_ffeat[tf * 3 * D + 2 * D + d] = gf[2 * MAXD + d];
+    for (int q = 0; q < 6; q++) acc.gi[q] += __shfl_xor(acc.gi[q], o);
+#pragma unroll
+    for (int q = 0; q < 3 * MAXD; q++) acc.gf[q] += __shfl_xor(acc.gf[q], o);
+  }
+  if (!in || queued) return;  // queued faces are written by the workgroup kernel
+  // lane s writes the values q = s, s+LPF, ...
+#pragma unroll
+  for (int q = 0; q < 6 + 3 * MAXD; q++) {
+    if (q % LPF != s) continue;
+    if (q < 6) {
+      grad_fvi[tf * 6 + q] = acc.gi[q];
+    } else {
+      const int r = q - 6, ii = r / MAXD, d = r % MAXD;
+      if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = acc.gf[r];
     }
   }
 }
@@ -500,10 +568,12 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
 template <typename T, int MAXD>
 __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
-    const T *__restrict__ fvi, const T *__restrict__ feat, int H, int W, int F, int D, float eps,
-    T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat, const int *__restrict__ big, const int *__restrict__ nbig) {
+    const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid, int H, int W, int F,
+    int D, float m, float eps, T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat, const int *__restrict__ big,
+    const int *__restrict__ nbig) {
   __shared__ T red[256];
   const int n = *nbig;
+  const RastSrc<T> src{fvi, valid, (T)m};
   for (int k = blockIdx.x; k < n; k += gridDim.x) {
     const int64_t tf = big[k];
     const int b = (int)(tf / F);
@@ -512,37 +582,20 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
 #pragma unroll
     for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
     int ix0, ix1, iy0, iy1;
-    conservative_range(v, H, W, ix0, ix1, iy0, iy1);
+    face_range(src, tf, m, H, W, ix0, ix1, iy0, iy1);
     const int w = ix1 - ix0 + 1;
     const int64_t area = (int64_t)w * (iy1 - iy0 + 1);
-    T acc[6 + 3 * MAXD];
-#pragma unroll
-    for (int q = 0; q < 6 + 3 * MAXD; q++) acc[q] = (T)0;
+    GatherAcc<T, MAXD> acc;
+    acc.zero();
     const T *c = feat + tf * 3 * D;
     for (int64_t e = threadIdx.x; e < area; e += blockDim.x) {
       const int j = iy0 + (int)(e / w), i = ix0 + (int)(e % w);
       const int64_t p = ((int64_t)b * H + j) * W + i;
       if (face_idx[p] != f) continue;
-      const T w_a = wts[p * 3 + 0], w_b = wts[p * 3 + 1], w_c = wts[p * 3 + 2];
-      const T *g = grad_feat + p * D;
-      BaryGrad<T> bg;
-      bg.init(v, w_a, w_b, w_c, eps);
-#pragma unroll
-      for (int d = 0; d < MAXD; d++) {
-        if (d < D) {
-          const T gd = g[d];
-          acc[6 + d] += gd * w_a;
-          acc[6 + MAXD + d] += gd * w_b;
-          acc[6 + 2 * MAXD + d] += gd * w_c;
-          T o[6];
-          bg.terms(gd, c[d], c[D + d], c[2 * D + d], o);
-#pragma unroll
-          for (int q = 0; q < 6; q++) acc[q] += o[q];
-        }
-      }
+      acc.add(v, c, D, wts[p * 3 + 0], wts[p * 3 + 1], wts[p * 3 + 2], grad_feat + p * D, eps);
     }
     for (int q = 0; q < 6 + 3 * MAXD; q++) {
-      red[threadIdx.x] = acc[q];
+      red[threadIdx.x] = q < 6 ? acc.gi[q] : acc.gf[q - 6];
       __syncthreads();
       for (int s = 128; s > 0; s >>= 1) {
         if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
@@ -578,26 +631,27 @@ static int rasterize_bwd(int B, int H, int W, int F, int D, const void *grad, co
 
 template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
-                                     const T *w, const T *fvi, const T *feat, float eps, T *gfvi, T *gfeat,
-                                     int *big, int *nbig, hipStream_t st) {
+                                     const T *w, const T *fvi, const T *feat, const uint8_t *valid, float m, float eps,
+                                     T *gfvi, T *gfeat, int *big, int *nbig, hipStream_t st) {
   KL_CHECK_HIP(hipMemsetAsync(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
-  hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf, 256)), dim3(256), 0, st, grad,
-                     face_idx, w, fvi, feat, B, H, W, F, D, eps, gfvi, gfeat, big, nbig);
+  hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st, grad,
+                     face_idx, w, fvi, feat, valid, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig);
   KL_CHECK_LAUNCH();
   hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(256), dim3(256), 0, st, grad, face_idx, w, fvi,
-                     feat, H, W, F, D, eps, gfvi, gfeat, big, nbig);
+                     feat, valid, H, W, F, D, m, eps, gfvi, gfeat, big, nbig);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
 
 template <typename T>
 static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
-                                const void *w, const void *fvi, const void *feat, float eps, void *gfvi, void *gfeat,
-                                void *ws, size_t ws_bytes, hipStream_t st) {
+                                const void *w, const void *fvi, const void *feat, const uint8_t *valid, float m,
+                                float eps, void *gfvi, void *gfeat, void *ws, size_t ws_bytes, hipStream_t st) {
   const int64_t nf = (int64_t)B * F;
   if (nf == 0) return KL_OK;
   KL_REQUIRE(ws_bytes >= (size_t)(nf + 1) * sizeof(int), "rasterize backward: workspace too small");
+  KL_REQUIRE(nf < ((int64_t)1 << 31), "rasterize backward: too many faces");
   int *nbig = reinterpret_cast<int *>(ws);
   int *big = nbig + 1;
   const T *g = (const T *)grad;
@@ -605,11 +659,11 @@ static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *g
   const T *fv = (const T *)fvi;
   const T *ft = (const T *)feat;
   if (D <= 4)
-    return rasterize_bwd_gather_maxd<T, 4>(B, H, W, F, D, g, face_idx, wt, fv, ft, eps, (T *)gfvi, (T *)gfeat, big,
-                                           nbig, st);
+    return rasterize_bwd_gather_maxd<T, 4>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, m, eps, (T *)gfvi,
+                                           (T *)gfeat, big, nbig, st);
   if (D <= 8)
-    return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, eps, (T *)gfvi, (T *)gfeat, big,
-                                           nbig, st);
+    return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, m, eps, (T *)gfvi,
+                                           (T *)gfeat, big, nbig, st);
   // wide features: the scatter kernel
   return rasterize_bwd<T>(B, H, W, F, D, grad, face_idx, w, fvi, feat, eps, gfvi, gfeat, st);
 }
@@ -685,14 +739,15 @@ extern "C" int kl_rasterize_backward(kl_dtype dtype, int batch, int height, int 
 
 extern "C" int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces,
                                           int feat_dim, const void *grad, const int64_t *face_idx, const void *w,
-                                          const void *fvi, const void *feat, float eps, void *gfvi, void *gfeat,
-                                          void *ws, size_t ws_bytes, kl_stream stream) {
+                                          const void *fvi, const void *feat, const uint8_t *valid_faces,
+                                          float multiplier, float eps, void *gfvi, void *gfeat, void *ws,
+                                          size_t ws_bytes, kl_stream stream) {
   if (dtype == KL_F32)
-    return rasterize_bwd_gather<float>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat, eps,
-                                       gfvi, gfeat, ws, ws_bytes, S(stream));
+    return rasterize_bwd_gather<float>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat,
+                                       valid_faces, multiplier, eps, gfvi, gfeat, ws, ws_bytes, S(stream));
   if (dtype == KL_F64)
-    return rasterize_bwd_gather<double>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat, eps,
-                                        gfvi, gfeat, ws, ws_bytes, S(stream));
+    return rasterize_bwd_gather<double>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat,
+                                        valid_faces, multiplier, eps, gfvi, gfeat, ws, ws_bytes, S(stream));
   set_error("dibr_rasterize_backward not implemented for this dtype");
   return KL_E_INVALID;
 }

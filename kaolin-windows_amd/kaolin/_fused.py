@@ -16,6 +16,13 @@ def _ws(nbytes, device):
     return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
 
 
+def _valid_u8(valid_faces):
+    if valid_faces is None:
+        return None
+    valid = valid_faces.contiguous()
+    return valid.view(torch.uint8) if valid.dtype == torch.bool else (valid != 0).view(torch.uint8)
+
+
 def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_features, valid_faces, multiplier,
                       eps):
     """-> interpolated_features (B,H,W,D), face_idx (B,H,W) original index, output_weights (B,H,W,3)."""
@@ -30,10 +37,7 @@ def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_
     fvz = face_vertices_z.contiguous()
     fvi = face_vertices_image.contiguous()
     feat = face_features.contiguous()
-    valid = None
-    if valid_faces is not None:
-        valid = valid_faces.contiguous()
-        valid = valid.view(torch.uint8) if valid.dtype == torch.bool else (valid != 0).view(torch.uint8)
+    valid = _valid_u8(valid_faces)
     feats = torch.empty((B, height, width, D), dtype=dtype, device=dev)
     idx = torch.empty((B, height, width), dtype=torch.long, device=dev)
     w = torch.empty((B, height, width, 3), dtype=dtype, device=dev)
@@ -48,20 +52,23 @@ def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_
     return feats, idx, w
 
 
-def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_features, eps):
+def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_features, valid_faces, multiplier, eps):
+    """Gather backward; valid_faces / multiplier must be the forward's."""
     func = 'rasterize backward'
     B, H, W, D = grad.shape
     F = face_vertices_image.shape[1]
     dev = face_vertices_image.device
     g_img = torch.empty_like(face_vertices_image)
     g_feat = torch.empty_like(face_features)
+    valid = _valid_u8(valid_faces)
     lib = N.lib()
     nbytes = lib.kl_dibr_rasterize_workspace_bytes(B, H, W, F)
     ws = _ws(nbytes, dev)
     with torch.cuda.device(dev), N.timed('dibr_rasterize_backward', dev):
         N.check(lib.kl_dibr_rasterize_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, N.ptr(grad.contiguous()), N.ptr(face_idx),
-            N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), float(eps), N.ptr(g_img),
+            N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), N.ptr(valid), float(multiplier),
+            float(eps), N.ptr(g_img),
             N.ptr(g_feat), N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return g_img, g_feat
 

@@ -55,16 +55,18 @@ class RasterizeCuda(Function):
         face_vertices_image = face_vertices_image.contiguous()
         interpolated_features, face_idx, output_weights = _fused.rasterize_forward(
             height, width, face_vertices_z, face_vertices_image, face_features, valid_faces, multiplier, eps)
-        ctx.save_for_backward(interpolated_features, face_idx, output_weights, face_vertices_image, face_features)
+        ctx.save_for_backward(face_idx, output_weights, face_vertices_image, face_features, valid_faces)
         ctx.mark_non_differentiable(face_idx)
         ctx.eps = eps
+        ctx.multiplier = multiplier
         return interpolated_features, face_idx
 
     @staticmethod
     def backward(ctx, grad_interpolated_features, grad_face_idx):
-        interpolated_features, face_idx, output_weights, face_vertices_image, face_features = ctx.saved_tensors
+        face_idx, output_weights, face_vertices_image, face_features, valid_faces = ctx.saved_tensors
         grad_face_vertices_image, grad_face_features = _fused.rasterize_backward(
-            grad_interpolated_features, face_idx, output_weights, face_vertices_image, face_features, ctx.eps)
+            grad_interpolated_features, face_idx, output_weights, face_vertices_image, face_features, valid_faces,
+            ctx.multiplier, ctx.eps)
         return None, None, None, grad_face_vertices_image, grad_face_features, None, None, None
 
 
