@@ -89,6 +89,27 @@ def dibr_inputs(views, device, H=512, W=512):
     return dict(fvz=fvz, fvi=fvi, feat=feat, fnz=fnz, g_feat=g_feat, g_mask=g_mask, H=H, W=W, F=faces.shape[0])
 
 
+def views_for_rank(rank, world, per_rank):
+    """Contiguous shard of the world's per_rank*world azimuths (weak scaling: fixed per rank)."""
+    n = per_rank * world
+    return [2 * math.pi * (rank * per_rank + k) / n for k in range(per_rank)]
+
+
+def gather_losses(loss, world):
+    """The step's only collective: all_gather of the per-shard scalar losses."""
+    out = [torch.empty_like(loss) for _ in range(world)]
+    dist.all_gather(out, loss.detach())
+    return torch.stack(out)
+
+
+def max_over_ranks(elapsed, device, world):
+    if world == 1:
+        return elapsed
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t)
+
+
 def dibr_step(inp, world):
     fvi = inp['fvi'].detach().requires_grad_(True)
     feat = inp['feat'].detach().requires_grad_(True)
@@ -98,8 +119,7 @@ def dibr_step(inp, world):
     loss = (feats * inp['g_feat']).sum() + (mask * inp['g_mask']).sum()
     loss.backward()
     if world > 1:  # per-shard losses all-gathered over RCCL / xGMI
-        out = [torch.empty_like(loss) for _ in range(world)]
-        dist.all_gather(out, loss.detach())
+        gather_losses(loss, world)
     return fvi.grad, feat.grad, mask, idx
 
 
@@ -124,6 +144,32 @@ def op_bytes(name, inp, stats):
     if name in ('rasterize_backward_cuda', 'dibr_rasterize_backward'):
         return px * (8 + 3 * s + D * s) + B * F * (6 * s + 3 * D * s) * 2
     return None
+
+
+# kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
+OP_KERNELS = {
+    'dibr_soft_mask_forward': ('bin_faces_kernel<float, kl::SoftSrc', 'soft_mask_fwd_kernel<float, kl::SoftSrc'),
+    'dibr_soft_mask_backward': ('soft_mask_bwd_agg_kernel<float, true>',),
+    'dibr_rasterize_forward': ('raster_vis_kernel<float, kl::RastSrc', 'raster_vis_big_kernel<float, kl::RastSrc',
+                               'raster_resolve_kernel<float, kl::RastSrc'),
+    'dibr_rasterize_backward': ('rasterize_bwd_gather_kernel<float', 'rasterize_bwd_bigface_kernel<float'),
+}
+
+
+def pmc_traffic(op):
+    """HBM bytes per call of `op` from the committed PMC summary (scripts/pmc_traffic.py), or None."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'pmc_traffic.json')
+    if op not in OP_KERNELS or not os.path.exists(path):
+        return None
+    kern = json.load(open(path))['kernels']
+    total, found = 0, 0
+    for pref in OP_KERNELS[op]:
+        for name, v in kern.items():
+            if pref in name:
+                total += v['hbm_bytes']
+                found += 1
+                break
+    return total if found else None
 
 
 def timed_loop(fn, steps, world):
@@ -202,7 +248,7 @@ def main():
     torch.cuda.set_device(device)
 
     views_per_rank = 4
-    views = [2 * math.pi * (rank * views_per_rank + k) / (views_per_rank * world) for k in range(views_per_rank)]
+    views = views_for_rank(rank, world, views_per_rank)
     inp = dibr_inputs(views, device)
     step = lambda: dibr_step(inp, world)  # noqa: E731
     for _ in range(args.warmup):
@@ -222,10 +268,7 @@ def main():
     _native.set_timer(timer)
     elapsed = timed_loop(step, args.steps, world)
     _native.set_timer(None)
-    if world > 1:
-        t = torch.tensor([elapsed], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    elapsed = max_over_ranks(elapsed, device, world)
     ops_ms = timer.summary_ms()
     pixels = views_per_rank * inp['H'] * inp['W'] * world * args.steps
     value = pixels / elapsed / 1e6
@@ -247,7 +290,7 @@ def main():
                        'global_batch': views_per_rank * world, 'height': 512, 'width': 512, 'faces': 50000,
                        'parallelism': f'batch-sharded x{world} (RCCL all_gather of per-shard losses)'},
             'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(dom),
                          'bytes_per_launch': dbytes, 'avg_launch_ms': round(ops_ms[dom], 4)},
             'ops': ops_report,
             'workload_stats': stats,

@@ -149,11 +149,15 @@ int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height, int width,
 /* ------------------------------------------------------------ distances */
 
 /* unbatched_triangle_distance.cpp:43-72.  points (P,3), face_vertices (F,3,3).
- * Outputs dist (P), face_idx (P) int64, dist_type (P) int32. dtype KL_F32 | KL_F64. */
+ * Outputs dist (P), face_idx (P) int64, dist_type (P) int32. dtype KL_F32 | KL_F64.
+ * workspace (optional, NULL allowed): kl_unbatched_triangle_distance_workspace_bytes(P)
+ * bytes, used to process points in Morton order so that whole waves can skip faces
+ * that provably cannot be their nearest (results are unchanged). */
+size_t kl_unbatched_triangle_distance_workspace_bytes(int64_t num_points);
 int kl_unbatched_triangle_distance_forward(kl_dtype dtype, int64_t num_points, int64_t num_faces,
                                            const void *points, const void *face_vertices,
                                            void *dist, int64_t *face_idx, int32_t *dist_type,
-                                           kl_stream stream);
+                                           void *workspace, size_t workspace_bytes, kl_stream stream);
 
 /* unbatched_triangle_distance.cpp:74-114.  grad_points (P,3) fully written;
  * grad_face_vertices (F,3,3) fully written (zero where no point selected the face). */

@@ -17,6 +17,8 @@
 
 #include <hip/hip_fp16.h>
 
+#include <hipcub/hipcub.hpp>
+
 #include <type_traits>
 
 namespace kl {
@@ -51,6 +53,8 @@ template <typename T>
 struct FaceRec {
   V3<T> v1, v2, v3, e12, e23, e31, un, en12, en23, en31;
   T l12, l23, l31;
+  T thick;  // pruning only: max |dot(x - v1, un)| over the triangle (+ rounding slack)
+  T hmax;   // pruning only: max |coordinate| of the vertices
 };
 
 template <typename T>
@@ -70,6 +74,11 @@ __device__ __forceinline__ void make_face(const T *v, FaceRec<T> &r) {
   r.en12 = cross(normal, r.e12);
   r.en23 = cross(normal, r.e23);
   r.en31 = cross(normal, r.e31);
+  const T hm = fmax(fmax(fmax(fabs(r.v1.x), fabs(r.v1.y)), fmax(fabs(r.v1.z), fabs(r.v2.x))),
+                    fmax(fmax(fabs(r.v2.y), fabs(r.v2.z)), fmax(fmax(fabs(r.v3.x), fabs(r.v3.y)), fabs(r.v3.z))));
+  r.hmax = hm;
+  // the triangle lies within +-thick of the computed plane {x : dot(x - v1, un) = 0}
+  r.thick = fmax(fabs(dot(r.e12, r.un)), fabs(dot(r.e31, r.un))) + (T)(64.0 / 16777216.0) * hm;
 }
 
 // squared distance (as float, :302) + type of one point to one face
@@ -102,31 +111,101 @@ __device__ __forceinline__ float point_face(const V3<T> &p, const FaceRec<T> &f,
   return (float)dot(dv, dv);
 }
 
-constexpr int P2M_TILE = 256;  // faces per LDS tile (a divisor of the reference's 512)
+#ifdef KL_P2M_PROBE  // dev probe (scripts/dev/p2m_probe.hip): counts skipped / evaluated (wave, face) pairs
+__device__ unsigned long long g_p2m_skipped, g_p2m_evaluated;
+#define KL_P2M_COUNT(v) v++
+#else
+#define KL_P2M_COUNT(v)
+#endif
 
+constexpr int P2M_TILE = 256;  // faces per LDS tile (a divisor of the reference's 512)
+constexpr float P2M_E = 1.0f / 16777216.0f;  // float unit roundoff (d is stored as float for both dtypes)
+
+// Face skipping.  The reference's fold (first face of each 512-face tile taken
+// unconditionally, then strict '<' inside a tile, strict '<' across tiles) gives every
+// point the minimum float distance over all faces, earliest face on ties (NaN aside).
+// A face whose computed distance d satisfies d >= min(best of earlier tiles, current
+// tile best) can never change the outcome, so it need not be evaluated.  Points are
+// processed in Morton order, so a wave's 64 points form a cluster (centre c, radius
+// R); every triangle lies in the slab |dot(x - v1, un)| <= thick of its computed plane,
+// which bounds every computed distance of the cluster from below:
+//   L = (|dot(c - v1, un)| - R(1 + 16E) - thick - 64 E M)(1 - 4E),  M = |c|inf + R + hmax,
+//   d >= ((L - 64 E M)^2)(1 - 8E)
+// (the 64 E M terms bound the rounding of the plane distance and of the computed closest
+// point, E = 2^-24 as d is truncated to float).  Faces are skipped for the whole wave
+// only when that bound reaches the largest threshold of its lanes; the first face of
+// each reference tile is always evaluated.  Skipped or not, every evaluated value is the
+// reference's, so results are unchanged; non-finite inputs make the bound NaN / -inf and
+// disable skipping.
+// grid: (point blocks, face splits).  A split covers whole 512-face reference tiles
+// [f_begin, f_end); with more than one split each writes its partial (dist, idx, type)
+// at part + split * P (sorted point order) for p2m_combine_kernel.  The reference fold
+// restricted to a split: only split 0 takes its first tile unconditionally; later
+// splits start from +inf, so, as in the global fold, a NaN tile never replaces.
 template <typename T>
 __global__ void __launch_bounds__(256) p2m_fwd_kernel(const T *__restrict__ pts, const T *__restrict__ fv,
-                                                       int64_t P, int64_t F, T *__restrict__ out_dist,
-                                                       int64_t *__restrict__ out_idx, int32_t *__restrict__ out_type) {
+                                                       const int32_t *__restrict__ order, int64_t P, int64_t F,
+                                                       int64_t split_faces, T *__restrict__ out_dist,
+                                                       int64_t *__restrict__ out_idx, int32_t *__restrict__ out_type,
+                                                       T *__restrict__ part_dist, int64_t *__restrict__ part_idx,
+                                                       int32_t *__restrict__ part_type) {
   __shared__ FaceRec<T> sf[P2M_TILE];
-  const int64_t pi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const bool valid = pi < P;
+  const int64_t si = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool valid = si < P;
+  const int64_t pi = valid ? (order ? (int64_t)order[si] : si) : 0;
+  const bool first_split = blockIdx.y == 0;
+  const int64_t f_begin = (int64_t)blockIdx.y * split_faces;
+  const int64_t f_end = min(F, f_begin + split_faces);
   V3<T> p = mk((T)0, (T)0, (T)0);
   if (valid) p = mk(pts[pi * 3], pts[pi * 3 + 1], pts[pi * 3 + 2]);
+  // cluster of the wave's points (padding lanes repeat lane 0's point)
+  const V3<T> p0 = mk(__shfl(p.x, 0), __shfl(p.y, 0), __shfl(p.z, 0));
+  const V3<T> q = valid ? p : p0;
+  const bool fin = isfinite(q.x) && isfinite(q.y) && isfinite(q.z);
+  const bool all_fin = __all(fin);
+  V3<T> c = mk((T)0, (T)0, (T)0);
+  T R = (T)INFINITY, cinf = (T)0;
+  if (all_fin) {
+    c = mk((wave_min(q.x) + wave_max(q.x)) * (T)0.5, (wave_min(q.y) + wave_max(q.y)) * (T)0.5,
+           (wave_min(q.z) + wave_max(q.z)) * (T)0.5);
+    const V3<T> dq = q - c;
+    R = wave_max(kl_sqrt<T>(dot(dq, dq))) * (T)(1.0 + 16.0 * P2M_E);
+    cinf = fmax(fmax(fabs(c.x), fabs(c.y)), fabs(c.z));
+  }
+#ifdef KL_P2M_PROBE
+  unsigned long long g_p2m_skipped = 0, g_p2m_evaluated = 0;
+#endif
   T best = (T)INFINITY, tbest = (T)INFINITY;
   int64_t best_f = 0, tbest_f = 0;
   int best_t = 0, tbest_t = 0;
-  for (int64_t start = 0; start < F; start += P2M_TILE) {
-    const int n = (int)min((int64_t)P2M_TILE, F - start);
+  T thr_max = (T)INFINITY;  // >= max over lanes of min(best, tbest) (refreshed per LDS tile)
+  for (int64_t start = f_begin; start < f_end; start += P2M_TILE) {
+    const int n = (int)min((int64_t)P2M_TILE, f_end - start);
+    if (start > f_begin) {  // thresholds only decrease, so a stale maximum is a safe upper bound
+      T thr = fmin(best, tbest);
+      if (thr != thr || !valid) thr = valid ? (T)INFINITY : (T)0;
+      thr_max = wave_max(thr);
+    }
     __syncthreads();
     for (int s = threadIdx.x; s < n; s += blockDim.x) make_face<T>(fv + (start + s) * 9, sf[s]);
     __syncthreads();
     for (int s = 0; s < n; s++) {
       const int64_t f = start + s;
+      const FaceRec<T> &fr = sf[s];
+      if ((f & 511) != 0) {
+        const T M = cinf + R + fr.hmax;
+        const T slack = (T)(64.0 * P2M_E) * M;
+        const T L = (fabs(dot(c - fr.v1, fr.un)) - R - fr.thick - slack) * (T)(1.0 - 4.0 * P2M_E) - slack;
+        if (L > (T)0 && L * L * (T)(1.0 - 8.0 * P2M_E) >= thr_max) {  // wave-uniform
+          KL_P2M_COUNT(g_p2m_skipped);
+          continue;
+        }
+      }
+      KL_P2M_COUNT(g_p2m_evaluated);
       int t;
-      const float d = point_face<T>(p, sf[s], t);
+      const float d = point_face<T>(p, fr, t);
       if ((f & 511) == 0) {  // a reference tile begins: merge the previous tile, restart
-        if (f > 0 && (f == 512 || best > tbest)) {
+        if (f > f_begin && ((first_split && f == 512) || best > tbest)) {
           best = tbest; best_f = tbest_f; best_t = tbest_t;
         }
         tbest = (T)d; tbest_f = f; tbest_t = t;
@@ -135,14 +214,149 @@ __global__ void __launch_bounds__(256) p2m_fwd_kernel(const T *__restrict__ pts,
       }
     }
   }
+#ifdef KL_P2M_PROBE
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&::kl::g_p2m_skipped, g_p2m_skipped);
+    atomicAdd(&::kl::g_p2m_evaluated, g_p2m_evaluated);
+  }
+#endif
   if (!valid) return;
-  if (F > 0 && (F <= 512 || best > tbest)) {
+  if (f_end > f_begin && ((first_split && f_end <= 512) || best > tbest)) {
     best = tbest; best_f = tbest_f; best_t = tbest_t;
   }
-  out_dist[pi] = best;
-  out_idx[pi] = best_f;
-  out_type[pi] = best_t;
+  if (part_dist) {
+    const int64_t o = (int64_t)blockIdx.y * P + si;
+    part_dist[o] = best;
+    part_idx[o] = best_f;
+    part_type[o] = best_t;
+  } else {
+    out_dist[pi] = best;
+    out_idx[pi] = best_f;
+    out_type[pi] = best_t;
+  }
 }
+
+// folds the splits' partials in face order with the reference's strict '<'
+template <typename T>
+__global__ void __launch_bounds__(256) p2m_combine_kernel(const int32_t *__restrict__ order, int64_t P, int splits,
+                                                           const T *__restrict__ part_dist,
+                                                           const int64_t *__restrict__ part_idx,
+                                                           const int32_t *__restrict__ part_type,
+                                                           T *__restrict__ out_dist, int64_t *__restrict__ out_idx,
+                                                           int32_t *__restrict__ out_type) {
+  const int64_t si = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (si >= P) return;
+  T best = part_dist[si];
+  int64_t bi = part_idx[si];
+  int32_t bt = part_type[si];
+  for (int k = 1; k < splits; k++) {
+    const T d = part_dist[(int64_t)k * P + si];
+    if (best > d) {
+      best = d;
+      bi = part_idx[(int64_t)k * P + si];
+      bt = part_type[(int64_t)k * P + si];
+    }
+  }
+  const int64_t pi = order ? (int64_t)order[si] : si;
+  out_dist[pi] = best;
+  out_idx[pi] = bi;
+  out_type[pi] = bt;
+}
+
+// ---- Morton ordering of the points (the clusters the skipping test works on)
+__device__ __forceinline__ int32_t f2ord(float v) {  // order-preserving float -> int
+  const int32_t b = __float_as_int(v);
+  return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float ord2f(int32_t b) { return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff); }
+
+// one 1024-thread block: per-axis min / max of the finite point coordinates
+template <typename T>
+__global__ void __launch_bounds__(1024) p2m_bounds_kernel(const T *__restrict__ pts, int64_t P, int32_t *bounds) {
+  __shared__ float red[6][16];
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = threadIdx.x; i < P; i += blockDim.x) {
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const float v = (float)pts[i * 3 + a];
+      if (isfinite(v)) {
+        lo[a] = fminf(lo[a], v);
+        hi[a] = fmaxf(hi[a], v);
+      }
+    }
+  }
+  const int w = threadIdx.x >> 6;
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    const float l = wave_min(lo[a]), h = wave_max(hi[a]);
+    if ((threadIdx.x & 63) == 0) {
+      red[a][w] = l;
+      red[3 + a][w] = h;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    const int a = threadIdx.x;
+    float r = red[a][0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); k++) r = a < 3 ? fminf(r, red[a][k]) : fmaxf(r, red[a][k]);
+    bounds[a] = f2ord(r);
+  }
+}
+
+__device__ __forceinline__ uint32_t spread10(uint32_t v) {
+  v &= 0x3ff;
+  v = (v | (v << 16)) & 0x030000ff;
+  v = (v | (v << 8)) & 0x0300f00f;
+  v = (v | (v << 4)) & 0x030c30c3;
+  v = (v | (v << 2)) & 0x09249249;
+  return v;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) p2m_morton_kernel(const T *__restrict__ pts, int64_t P,
+                                                          const int32_t *__restrict__ bounds, uint32_t *keys,
+                                                          int32_t *vals) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= P) return;
+  uint32_t code = 0x3fffffffu;  // non-finite points last
+  const float x = (float)pts[i * 3], y = (float)pts[i * 3 + 1], z = (float)pts[i * 3 + 2];
+  if (isfinite(x) && isfinite(y) && isfinite(z)) {
+    uint32_t g[3];
+    const float v[3] = {x, y, z};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+      const float lo = ord2f(bounds[a]), hi = ord2f(bounds[3 + a]);
+      const float t = hi > lo ? (v[a] - lo) / (hi - lo) : 0.0f;
+      g[a] = (uint32_t)fminf(fmaxf(t * 1024.0f, 0.0f), 1023.0f);
+    }
+    code = (spread10(g[0]) << 2) | (spread10(g[1]) << 1) | spread10(g[2]);
+  }
+  keys[i] = code;
+  vals[i] = (int32_t)i;
+}
+
+constexpr int P2M_MAX_SPLITS = 16;
+
+struct P2MWs {
+  size_t keys_in, keys_out, vals_in, vals_out, temp, temp_bytes, part, bytes;
+  explicit P2MWs(int64_t P) {
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                       (const int32_t *)nullptr, (int32_t *)nullptr, (int)P, 0, 30);
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    keys_in = 256;  // [0, 256): 6 bounds
+    keys_out = keys_in + al(4 * (size_t)P);
+    vals_in = keys_out + al(4 * (size_t)P);
+    vals_out = vals_in + al(4 * (size_t)P);
+    temp = vals_out + al(4 * (size_t)P);
+    temp_bytes = tb;
+    part = temp + al(tb);  // P2M_MAX_SPLITS x P x (dist 8 + idx 8 + type 4)
+    bytes = part + al((size_t)P2M_MAX_SPLITS * P * 20);
+  }
+};
+
+// below this many pairs the Morton sort is not worth its launches
+constexpr int64_t P2M_SORT_MIN_PAIRS = (int64_t)1 << 24;
 
 template <typename T>
 __device__ __forceinline__ void edge_bwd(V3<T> vab, V3<T> pb, T *ga, T *gb, T *gp, T grad) {
@@ -331,12 +545,52 @@ __global__ void __launch_bounds__(256) sided_bwd_kernel(const S *__restrict__ gr
 
 template <typename T>
 static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *dist, int64_t *idx, int32_t *type,
-                   hipStream_t st) {
+                   void *ws, size_t ws_bytes, hipStream_t st) {
   if (P == 0) return KL_OK;
   KL_REQUIRE(F > 0, "unbatched_triangle_distance_forward: face_vertices must not be empty");
-  hipLaunchKernelGGL(p2m_fwd_kernel<T>, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, (const T *)pts,
-                     (const T *)fv, P, F, (T *)dist, idx, type);
+  KL_REQUIRE(P < ((int64_t)1 << 31), "unbatched_triangle_distance_forward: too many points");
+  const int32_t *order = nullptr;
+  T *pd = nullptr;
+  int64_t *pidx = nullptr;
+  int32_t *pt = nullptr;
+  const unsigned pblocks = (unsigned)cdiv(P, 256);
+  int splits = 1;
+  int64_t split_faces = F;
+  if (ws && P * F >= P2M_SORT_MIN_PAIRS) {
+    const P2MWs L(P);
+    KL_REQUIRE(ws_bytes >= L.bytes, "unbatched_triangle_distance_forward: workspace too small");
+    char *w = reinterpret_cast<char *>(ws);
+    int32_t *bounds = reinterpret_cast<int32_t *>(w);
+    hipLaunchKernelGGL(p2m_bounds_kernel<T>, dim3(1), dim3(1024), 0, st, (const T *)pts, P, bounds);
+    KL_CHECK_LAUNCH();
+    uint32_t *kin = reinterpret_cast<uint32_t *>(w + L.keys_in), *kout = reinterpret_cast<uint32_t *>(w + L.keys_out);
+    int32_t *vin = reinterpret_cast<int32_t *>(w + L.vals_in), *vout = reinterpret_cast<int32_t *>(w + L.vals_out);
+    hipLaunchKernelGGL(p2m_morton_kernel<T>, dim3(pblocks), dim3(256), 0, st, (const T *)pts, P, bounds, kin, vin);
+    KL_CHECK_LAUNCH();
+    size_t tb = L.temp_bytes;
+    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.temp, tb, kin, kout, vin, vout, (int)P, 0, 30, st));
+    order = vout;
+    // enough (point block, face split) workgroups to fill the chip several times over;
+    // splits cover whole 512-face reference tiles
+    const int64_t tiles = cdiv(F, 512);
+    const int64_t want = std::max<int64_t>(1, cdiv(2048, pblocks));
+    splits = (int)std::min<int64_t>(std::min<int64_t>(want, tiles), P2M_MAX_SPLITS);
+    split_faces = cdiv(tiles, splits) * 512;
+    splits = (int)cdiv(F, split_faces);
+    if (splits > 1) {
+      pd = reinterpret_cast<T *>(w + L.part);
+      pidx = reinterpret_cast<int64_t *>(w + L.part + (size_t)P2M_MAX_SPLITS * P * 8);
+      pt = reinterpret_cast<int32_t *>(w + L.part + (size_t)P2M_MAX_SPLITS * P * 16);
+    }
+  }
+  hipLaunchKernelGGL(p2m_fwd_kernel<T>, dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
+                     (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt);
   KL_CHECK_LAUNCH();
+  if (splits > 1) {
+    hipLaunchKernelGGL(p2m_combine_kernel<T>, dim3(pblocks), dim3(256), 0, st, order, P, splits, pd, pidx, pt,
+                       (T *)dist, idx, type);
+    KL_CHECK_LAUNCH();
+  }
   return KL_OK;
 }
 
@@ -390,11 +644,13 @@ static int sided_bwd(int B, int64_t N, int64_t M, const void *grad, const void *
 
 using namespace kl;
 
+extern "C" size_t kl_unbatched_triangle_distance_workspace_bytes(int64_t P) { return P2MWs(P > 0 ? P : 1).bytes; }
+
 extern "C" int kl_unbatched_triangle_distance_forward(kl_dtype dtype, int64_t P, int64_t F, const void *pts,
                                                       const void *fv, void *dist, int64_t *idx, int32_t *type,
-                                                      kl_stream stream) {
-  if (dtype == KL_F32) return p2m_fwd<float>(P, F, pts, fv, dist, idx, type, S(stream));
-  if (dtype == KL_F64) return p2m_fwd<double>(P, F, pts, fv, dist, idx, type, S(stream));
+                                                      void *ws, size_t ws_bytes, kl_stream stream) {
+  if (dtype == KL_F32) return p2m_fwd<float>(P, F, pts, fv, dist, idx, type, ws, ws_bytes, S(stream));
+  if (dtype == KL_F64) return p2m_fwd<double>(P, F, pts, fv, dist, idx, type, ws, ws_bytes, S(stream));
   set_error("unbatched_triangle_distance_forward_cuda not implemented for this dtype");
   return KL_E_INVALID;
 }

@@ -18,6 +18,8 @@
 // face-vertex gradient.
 #include "binning.h"
 
+#include <hipcub/hipcub.hpp>
+
 namespace kl {
 
 constexpr double SM_EPS = 1e-7;
@@ -100,7 +102,8 @@ __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
     Src src, const T *__restrict__ bbox, const int64_t *__restrict__ sel,
     const uint32_t *__restrict__ bitmap, BinGeom g, int F, int K, float sigmainv, float multiplier,
     T *__restrict__ out_mask, T *__restrict__ out_prob, int64_t *__restrict__ out_idx,
-    uint8_t *__restrict__ out_type, uint8_t *__restrict__ out_hits, bool bbox_vec4) {
+    uint8_t *__restrict__ out_type, uint8_t *__restrict__ out_hits, bool bbox_vec4,
+    const int32_t *__restrict__ tile_order) {
   extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -111,9 +114,13 @@ __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
   int *s_kid = reinterpret_cast<int *>(mine + (size_t)K * 64 * sizeof(T));   // [64]
   int *s_pre = s_kid + 64;                                                    // [64] exclusive prefix
 
-  const int j = blockIdx.y * waves + wid;
-  const int b = blockIdx.z;
-  const int tx = blockIdx.x;
+  // work unit = (tile, row group): tiles in tile_order (heaviest first), else grid order
+  const int groups = TILE_H / waves;
+  const int tile = tile_order[blockIdx.x / groups];
+  const int tx = tile % g.tiles_x;
+  const int ty = (tile / g.tiles_x) % g.tiles_y;
+  const int b = tile / (g.tiles_x * g.tiles_y);
+  const int j = ty * TILE_H + (blockIdx.x % groups) * waves + wid;
   const int H = g.height, W = g.width;
   if (j >= H) return;
   const int ibase = tx * TILE_W;
@@ -426,16 +433,44 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
   }
 }
 
+// Longest-first order of the tiles for the forward walk: a tile's cost grows with its
+// candidate chunks (set bits of its bitmap words), and the heaviest tiles -- around the
+// silhouette's tight spots -- would otherwise start last and set the kernel's tail.
+__global__ void __launch_bounds__(256) tile_work_kernel(const uint32_t *__restrict__ bitmap, BinGeom g,
+                                                         uint32_t *__restrict__ keys, int32_t *__restrict__ vals) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  if (t >= nt) return;
+  const uint32_t *w = bitmap + (size_t)t * g.words;
+  uint32_t n = 0;
+  for (int k = 0; k < g.words; k++) n += __popc(w[k]);
+  keys[t] = 0xffffu - min(n, 0xffffu);  // ascending sort -> heaviest first
+  vals[t] = t;
+}
+
 template <typename T>
 static size_t sm_lds_per_wave(int K) {
   return (size_t)K * 64 * sizeof(T) + 128 * sizeof(int);
 }
 
-// workspace: bin bitmap | per-face bboxes (fused path; sized for f64)
-static size_t sm_ws_bbox_off(const BinGeom &g) { return (g.bytes() + 255) & ~(size_t)255; }
-static size_t sm_ws_bytes(int B, int H, int W, int F) {
-  return sm_ws_bbox_off(make_bin_geom(B, H, W, F)) + (size_t)B * F * 4 * sizeof(double);
-}
+// workspace: bin bitmap | tile order (keys/vals in/out + sort temp) | per-face bboxes
+// (fused path; sized for f64)
+static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+struct SmWs {
+  size_t order, order_temp, order_temp_bytes, bbox, bytes;
+  SmWs(const BinGeom &g, int F) {
+    const int nt = g.batch * g.tiles_y * g.tiles_x;
+    size_t tb = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                             (const int32_t *)nullptr, (int32_t *)nullptr, nt, 0, 16);
+    order = al256(g.bytes());
+    order_temp = order + 4 * al256((size_t)nt * 4);
+    order_temp_bytes = tb;
+    bbox = order_temp + al256(tb);
+    bytes = bbox + (size_t)g.batch * F * 4 * sizeof(double);
+  }
+};
+static size_t sm_ws_bytes(int B, int H, int W, int F) { return SmWs(make_bin_geom(B, H, W, F), F).bytes; }
 
 // bbox == nullptr: the source computes the bboxes (fused path) and binning stores them
 template <typename T, typename Src>
@@ -443,27 +478,39 @@ static int soft_mask_fwd(Src src, const T *bbox, int B, int H, int W, int F, int
                          float sigmainv, float m, void *mask, void *prob, int64_t *cidx, uint8_t *ctype,
                          uint8_t *hits, void *ws, size_t ws_bytes, hipStream_t st) {
   BinGeom g = make_bin_geom(B, H, W, F);
-  KL_REQUIRE(ws_bytes >= (bbox ? g.bytes() : sm_ws_bytes(B, H, W, F)),
-             "dibr_soft_mask_forward: workspace too small");
+  const SmWs L(g, F);
+  KL_REQUIRE(ws_bytes >= (bbox ? L.bbox : L.bytes), "dibr_soft_mask_forward: workspace too small");
   KL_REQUIRE(K >= 0, "dibr_soft_mask_forward: knum must be >= 0");
   KL_REQUIRE(F < (1 << 28), "dibr_soft_mask_forward: too many faces");
   KL_REQUIRE(hits == nullptr || K <= 255, "dibr_soft_mask_forward: per-pixel hit counts need knum <= 255");
   if (B == 0 || H == 0 || W == 0) return KL_OK;
   uint32_t *bitmap = reinterpret_cast<uint32_t *>(ws);
+  char *w = reinterpret_cast<char *>(ws);
   T *bbox_out = nullptr;
   if (!bbox) {
-    bbox_out = reinterpret_cast<T *>(reinterpret_cast<char *>(ws) + sm_ws_bbox_off(g));
+    bbox_out = reinterpret_cast<T *>(w + L.bbox);
     bbox = bbox_out;
   }
   int rc = launch_binning<T, Src>(src, nullptr, F, g, m, bitmap, st, bbox_out);
   if (rc) return rc;
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  const size_t ob = al256((size_t)nt * 4);
+  uint32_t *kin = reinterpret_cast<uint32_t *>(w + L.order), *kout = reinterpret_cast<uint32_t *>(w + L.order + ob);
+  int32_t *vin = reinterpret_cast<int32_t *>(w + L.order + 2 * ob);
+  int32_t *vout = reinterpret_cast<int32_t *>(w + L.order + 3 * ob);
+  hipLaunchKernelGGL(tile_work_kernel, dim3((unsigned)cdiv(nt, 256)), dim3(256), 0, st, bitmap, g, kin, vin);
+  KL_CHECK_LAUNCH();
+  size_t tb = L.order_temp_bytes;
+  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.order_temp, tb, kin, kout, vin, vout, nt, 0, 16, st));
   const size_t pw = sm_lds_per_wave<T>(K);
   int waves = 4;
   while (waves > 1 && pw * waves > 64 * 1024) waves--;
   KL_REQUIRE(pw * waves <= 160 * 1024, "dibr_soft_mask_forward: knum too large for the LDS slot lists");
-  dim3 grid(g.tiles_x, (unsigned)cdiv(H, waves), B);
-  hipLaunchKernelGGL((soft_mask_fwd_kernel<T, Src>), grid, dim3(64 * waves), pw * waves, st, src, bbox, sel, bitmap,
-                     g, F, K, sigmainv, m, (T *)mask, (T *)prob, cidx, ctype, hits, ((uintptr_t)bbox & 15) == 0);
+  while (TILE_H % waves) waves--;
+  const unsigned units = (unsigned)(nt * (TILE_H / waves));
+  hipLaunchKernelGGL((soft_mask_fwd_kernel<T, Src>), dim3(units), dim3(64 * waves), pw * waves, st, src, bbox, sel,
+                     bitmap, g, F, K, sigmainv, m, (T *)mask, (T *)prob, cidx, ctype, hits,
+                     ((uintptr_t)bbox & 15) == 0, (const int32_t *)vout);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

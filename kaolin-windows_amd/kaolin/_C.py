@@ -182,10 +182,13 @@ def unbatched_triangle_distance_forward_cuda(points, face_vertices, dist, face_i
     _float_only(func, points)
     N.require_gpu(func, points)
     dev = points.device
+    lib = N.lib()
+    nbytes = lib.kl_unbatched_triangle_distance_workspace_bytes(P)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev), N.timed(func, dev):
-        N.check(N.lib().kl_unbatched_triangle_distance_forward(
+        N.check(lib.kl_unbatched_triangle_distance_forward(
             N.dtype_code(points.dtype), P, F, N.ptr(points), N.ptr(face_vertices), N.ptr(dist), N.ptr(face_idx),
-            N.ptr(dist_type), N.stream_of(dev)), func)
+            N.ptr(dist_type), N.ptr(ws), nbytes, N.stream_of(dev)), func)
 
 
 def unbatched_triangle_distance_backward_cuda(grad_dist, points, face_vertices, face_idx, dist_type, grad_points,
