@@ -110,7 +110,8 @@ def max_over_ranks(elapsed, device, world):
     return float(t)
 
 
-def dibr_step(inp, world):
+def dibr_compute(inp):
+    """dibr_rasterization forward + the tutorial's loss + backward (everything but the collective)."""
     fvi = inp['fvi'].detach().requires_grad_(True)
     feat = inp['feat'].detach().requires_grad_(True)
     feats, mask, idx = kal.render.mesh.dibr_rasterization(inp['H'], inp['W'], inp['fvz'], fvi, feat, inp['fnz'],
@@ -118,9 +119,36 @@ def dibr_step(inp, world):
                                                           eps=1e-8)
     loss = (feats * inp['g_feat']).sum() + (mask * inp['g_mask']).sum()
     loss.backward()
+    return loss.detach(), fvi.grad, feat.grad, mask, idx
+
+
+def dibr_step(inp, world):
+    loss, gfvi, gfeat, mask, idx = dibr_compute(inp)
     if world > 1:  # per-shard losses all-gathered over RCCL / xGMI
         gather_losses(loss, world)
-    return fvi.grad, feat.grad, mask, idx
+    return gfvi, gfeat, mask, idx
+
+
+def graphed_step(inp, world):
+    """The same step with dibr_compute captured once in a HIP graph (its ~35 launches
+    replayed as one); the loss all_gather stays an eager RCCL call.  Inputs are static
+    buffers, as in a training loop that copies each batch into them."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            dibr_compute(inp)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        static_out = dibr_compute(inp)
+
+    def step():
+        graph.replay()
+        if world > 1:
+            gather_losses(static_out[0], world)
+        return static_out
+    return step, static_out
 
 
 def op_bytes(name, inp, stats):
@@ -236,6 +264,7 @@ def main():
     ap.add_argument('--cpu-row-step', type=int, default=8)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-p2m', action='store_true')
+    ap.add_argument('--eager', action='store_true', help='time the eager step only (no HIP graph capture)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -264,13 +293,31 @@ def main():
         slot_reads = int((torch.clamp(used + 1, max=30) * unc).sum())
         stats = dict(valid_faces=int((inp['fnz'] >= 0).sum()), slot_reads=slot_reads,
                      uncovered=float(unc.float().mean()), mean_slots=float(used[unc].float().mean()))
+    # eager pass: per-op HIP-event timing for the roofline, and the eager rate
     timer = _native.OpTimer()
     _native.set_timer(timer)
-    elapsed = timed_loop(step, args.steps, world)
+    eager_elapsed = timed_loop(step, args.steps, world)
     _native.set_timer(None)
-    elapsed = max_over_ranks(elapsed, device, world)
+    eager_elapsed = max_over_ranks(eager_elapsed, device, world)
     ops_ms = timer.summary_ms()
     pixels = views_per_rank * inp['H'] * inp['W'] * world * args.steps
+    eager_value = pixels / eager_elapsed / 1e6
+    mode = 'eager'
+    elapsed = eager_elapsed
+    if not args.eager:
+        gstep, gout = graphed_step(inp, world)
+        ref = dibr_step(inp, world)
+        gstep()
+        torch.cuda.synchronize()
+        # the replayed graph must reproduce the eager step (forward bit-exact, grads to float order)
+        ok = torch.equal(gout[4], ref[3]) and torch.equal(gout[3], ref[2]) and \
+            torch.allclose(gout[1], ref[0], rtol=1e-4, atol=1e-5) and torch.allclose(gout[2], ref[1], rtol=1e-4, atol=1e-5)
+        if not ok:
+            raise RuntimeError('graph replay differs from the eager step')
+        for _ in range(args.warmup):
+            gstep()
+        elapsed = max_over_ranks(timed_loop(gstep, args.steps, world), device, world)
+        mode = 'hip_graph'
     value = pixels / elapsed / 1e6
     result = None
     if rank == 0:
@@ -294,6 +341,8 @@ def main():
                          'bytes_per_launch': dbytes, 'avg_launch_ms': round(ops_ms[dom], 4)},
             'ops': ops_report,
             'workload_stats': stats,
+            'mode': mode,
+            'eager': {'value': round(eager_value, 2), 'ms_per_step': round(eager_elapsed / args.steps * 1e3, 4)},
         }
     if not args.no_p2m and rank == 0:
         mp, ms = p2m_bench(device, max(3, args.steps // 4))

@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *
 template <typename T, typename Src>
 inline int launch_binning(Src src, const int64_t *first_idx, int faces_per_mesh, const BinGeom &g, float m,
                           uint32_t *bitmap, hipStream_t st, T *bbox_out = nullptr) {
-  KL_CHECK_HIP(hipMemsetAsync(bitmap, 0, g.bytes(), st));
+  KL_CHECK_RC(fill_async(bitmap, 0, g.bytes(), st));
   dim3 grid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)g.batch);
   hipLaunchKernelGGL((bin_faces_kernel<T, Src>), grid, dim3(256), 0, st, src, first_idx, faces_per_mesh, g, m,
                      bitmap, bbox_out);

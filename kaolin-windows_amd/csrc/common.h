@@ -15,6 +15,9 @@
 namespace kl {
 
 void set_error(const std::string &msg);
+extern int g_dev_flags;  // kl_dev_set_flags (ablation timing only; 0 in the product path)
+// memset as a kernel launch on `st` (graph-capture friendly); returns a kl_status
+int fill_async(void *p, int value, size_t bytes, hipStream_t st);
 
 #define KL_CHECK_HIP(expr)                                                              \
   do {                                                                                  \
@@ -26,6 +29,12 @@ void set_error(const std::string &msg);
   } while (0)
 
 #define KL_CHECK_LAUNCH() KL_CHECK_HIP(hipGetLastError())
+
+#define KL_CHECK_RC(expr)                                                               \
+  do {                                                                                  \
+    const int _rc = (expr);                                                             \
+    if (_rc) return _rc;                                                                \
+  } while (0)
 
 #define KL_REQUIRE(cond, msg)                                                           \
   do {                                                                                  \

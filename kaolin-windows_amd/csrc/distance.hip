@@ -597,7 +597,7 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
 template <typename T>
 static int p2m_bwd(int64_t P, int64_t F, const void *grad, const void *pts, const void *fv, const int64_t *idx,
                    const int32_t *type, void *gp, void *gf, hipStream_t st) {
-  KL_CHECK_HIP(hipMemsetAsync(gf, 0, sizeof(T) * (size_t)F * 9, st));
+  KL_CHECK_RC(fill_async(gf, 0, sizeof(T) * (size_t)F * 9, st));
   if (P == 0) return KL_OK;
   hipLaunchKernelGGL(p2m_bwd_kernel<T>, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, (const T *)grad,
                      (const T *)pts, (const T *)fv, idx, type, P, (T *)gp, (T *)gf);
@@ -619,7 +619,7 @@ static int sided_fwd(int B, int64_t N, int64_t M, const void *p1, const void *p2
 template <typename S>
 static int sided_bwd(int B, int64_t N, int64_t M, const void *grad, const void *p1, const void *p2,
                      const int64_t *idx, void *g1, void *g2, hipStream_t st) {
-  KL_CHECK_HIP(hipMemsetAsync(g2, 0, sizeof(S) * (size_t)B * M * 3, st));
+  KL_CHECK_RC(fill_async(g2, 0, sizeof(S) * (size_t)B * M * 3, st));
   if (B == 0 || N == 0) return KL_OK;
   hipLaunchKernelGGL(sided_bwd_kernel<S>, dim3((unsigned)cdiv(N, 256), B), dim3(256), 0, st, (const S *)grad,
                      (const S *)p1, (const S *)p2, idx, N, M, (S *)g1, (S *)g2);

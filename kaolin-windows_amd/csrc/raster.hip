@@ -331,8 +331,8 @@ static int launch_rast_fwd(Src src, int H, int W, int B, int D, int64_t nfaces, 
   int *nbig = reinterpret_cast<int *>(w + L.off_big);
   int *big = nbig + 1;
   // key | idx | flag | nbig are contiguous: key and flag/nbig zeroed, idx set to ~0
-  KL_CHECK_HIP(hipMemsetAsync(w, 0, L.off_big + 4, st));
-  if (sizeof(T) == 8) KL_CHECK_HIP(hipMemsetAsync(w + L.off_idx, 0xff, L.P * 4, st));
+  KL_CHECK_RC(fill_async(w, 0, L.off_big + 4, st));
+  if (sizeof(T) == 8) KL_CHECK_RC(fill_async(w + L.off_idx, 0xff, L.P * 4, st));
   if (nfaces > 0) {
     const unsigned fb = (unsigned)cdiv(nfaces * LPF, 256);
     hipLaunchKernelGGL((raster_vis_kernel<T, Src, 0>), dim3(fb), dim3(256), 0, st, src, fvz, first_idx, B,
@@ -618,8 +618,8 @@ template <typename T>
 static int rasterize_bwd(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
                          const void *w, const void *fvi, const void *feat, float eps, void *gfvi, void *gfeat,
                          hipStream_t st) {
-  KL_CHECK_HIP(hipMemsetAsync(gfvi, 0, sizeof(T) * (size_t)B * F * 6, st));
-  KL_CHECK_HIP(hipMemsetAsync(gfeat, 0, sizeof(T) * (size_t)B * F * 3 * D, st));
+  KL_CHECK_RC(fill_async(gfvi, 0, sizeof(T) * (size_t)B * F * 6, st));
+  KL_CHECK_RC(fill_async(gfeat, 0, sizeof(T) * (size_t)B * F * 3 * D, st));
   const int64_t total = (int64_t)B * H * W;
   if (total == 0) return KL_OK;
   const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(total, 256), 65536);
@@ -633,7 +633,7 @@ template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
                                      const T *w, const T *fvi, const T *feat, const uint8_t *valid, float m, float eps,
                                      T *gfvi, T *gfeat, int *big, int *nbig, hipStream_t st) {
-  KL_CHECK_HIP(hipMemsetAsync(nbig, 0, sizeof(int), st));
+  KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
   hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st, grad,
                      face_idx, w, fvi, feat, valid, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig);

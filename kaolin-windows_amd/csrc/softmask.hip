@@ -306,7 +306,7 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const int64_t *__restrict__ sel,
     const T *__restrict__ prob, const int64_t *__restrict__ cidx, const uint8_t *__restrict__ ctype,
     const uint8_t *__restrict__ hits, const T *__restrict__ fvi, int B, int H, int W, int F, int K,
-    float sigmainv, float multiplier, T *__restrict__ gfvi) {
+    float sigmainv, float multiplier, T *__restrict__ gfvi, int dev) {
   __shared__ int s_key[SMB_HCAP];
   __shared__ T s_val[SMB_HCAP * 6];
   __shared__ double s_a[8][64];
@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
   const T y0 = pix_y<T>(multiplier, H, j < H ? j : 0);
   const size_t rowk = (((size_t)b * H + (j < H ? j : 0)) * W + ibase) * K;
   T *gb = gfvi + (size_t)b * F * 6;
-  for (int e = lane; e < total; e += 64) {
+  for (int e = lane; e < ((dev & 8) ? 0 : total); e += 64) {
     int lo = 0;
 #pragma unroll
     for (int st = 32; st > 0; st >>= 1)
@@ -390,6 +390,10 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
       g1x = dLdz * (y1 * dzdC - dzdB) / (T)multiplier;
       g1y = dLdz * (dzdA - x1 * dzdC) / (T)multiplier;
     }
+    if (dev & 4) {  // ablation: loads + arithmetic only
+      asm volatile("" : : "v"(g0x), "v"(g0y), "v"(g1x), "v"(g1y));
+      continue;
+    }
     // LDS hash slot of face f (linear probing, bounded)
     int slot = -1;
     unsigned h = ((unsigned)f * 2654435761u) >> 22;  // 10 bits
@@ -409,6 +413,10 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
       }
       h = (h + 1) & (SMB_HCAP - 1);
     }
+    if (dev & 2) {  // ablation: no accumulation
+      asm volatile("" : : "v"(g0x), "v"(g0y), "v"(g1x), "v"(g1y), "v"(slot));
+      continue;
+    }
     if (slot >= 0) {
       atomicAdd(&s_val[slot * 6 + c0 * 2], g0x);
       atomicAdd(&s_val[slot * 6 + c0 * 2 + 1], g0y);
@@ -426,6 +434,7 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
     }
   }
   __syncthreads();
+  if (dev & 1) return;  // ablation: no flush
   for (int q = threadIdx.x; q < SMB_HCAP * 6; q += blockDim.x) {
     const int key = s_key[q / 6];
     const T v = s_val[q];
@@ -520,11 +529,12 @@ static int soft_mask_bwd(int B, int H, int W, int F, int K, const void *grad, co
                          const int64_t *sel, const void *prob, const int64_t *cidx, const uint8_t *ctype,
                          const uint8_t *hits, const void *fvi, float sigmainv, float m, void *gfvi, hipStream_t st) {
   KL_REQUIRE(F < (1 << 28), "dibr_soft_mask_backward: too many faces");
-  KL_CHECK_HIP(hipMemsetAsync(gfvi, 0, sizeof(T) * (size_t)B * F * 6, st));
+  KL_CHECK_RC(fill_async(gfvi, 0, sizeof(T) * (size_t)B * F * 6, st));
   if ((int64_t)B * H * W == 0 || K <= 0) return KL_OK;
   dim3 grid((unsigned)cdiv(W, 64), (unsigned)cdiv(H, 8), B);
   hipLaunchKernelGGL((soft_mask_bwd_agg_kernel<T, SCALE>), grid, dim3(512), 0, st, (const T *)grad, (const T *)mask,
-                     sel, (const T *)prob, cidx, ctype, hits, (const T *)fvi, B, H, W, F, K, sigmainv, m, (T *)gfvi);
+                     sel, (const T *)prob, cidx, ctype, hits, (const T *)fvi, B, H, W, F, K, sigmainv, m, (T *)gfvi,
+                     g_dev_flags);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

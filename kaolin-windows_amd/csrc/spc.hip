@@ -654,7 +654,7 @@ extern "C" int kl_generate_points(int batch, int max_level, const uint8_t *octre
     const int32_t *pyrsum = pyr + L + 2;
     const int32_t osize = pyrsum[L];
     const int32_t total = pyrsum[L + 1];
-    KL_CHECK_HIP(hipMemsetAsync(mort, 0, sizeof(uint64_t), st));
+    KL_CHECK_RC(fill_async(mort, 0, sizeof(uint64_t), st));
     const uint8_t *co = oct;
     const int32_t *cs = ex + 1;
     const uint64_t *cm = mort;

@@ -150,10 +150,8 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
       rc = KL_E_ALLOC;
       break;
     }
-    if (hipMemsetAsync(counter, 0, sizeof(unsigned long long), st) != hipSuccess) {
-      rc = KL_E_HIP;
-      break;
-    }
+    rc = fill_async(counter, 0, sizeof(unsigned long long), st);
+    if (rc) break;
     hipLaunchKernelGGL((subdivide_kernel<T, G>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, n, cur, thr, R, grid,
                        nxt, counter);
     if (hipGetLastError() != hipSuccess ||
