@@ -111,15 +111,20 @@ def max_over_ranks(elapsed, device, world):
 
 
 def dibr_compute(inp):
-    """dibr_rasterization forward + the tutorial's loss + backward (everything but the collective)."""
+    """dibr_rasterization forward + the loss L = <features, g_feat> + <soft_mask, g_mask> + backward
+    (everything but the collective).  dL/dfeatures = g_feat and dL/dsoft_mask = g_mask exactly, so the
+    backward is driven with them directly (torch.autograd.backward) -- the same gradients as
+    L.backward() without the broadcast kernels of the sum's backward; L itself is two dot products."""
     fvi = inp['fvi'].detach().requires_grad_(True)
     feat = inp['feat'].detach().requires_grad_(True)
     feats, mask, idx = kal.render.mesh.dibr_rasterization(inp['H'], inp['W'], inp['fvz'], fvi, feat, inp['fnz'],
                                                           sigmainv=7000, boxlen=0.02, knum=30, multiplier=1000,
                                                           eps=1e-8)
-    loss = (feats * inp['g_feat']).sum() + (mask * inp['g_mask']).sum()
-    loss.backward()
-    return loss.detach(), fvi.grad, feat.grad, mask, idx
+    with torch.no_grad():
+        loss = torch.dot(feats.reshape(-1), inp['g_feat'].reshape(-1)) + \
+            torch.dot(mask.reshape(-1), inp['g_mask'].reshape(-1))
+    torch.autograd.backward([feats, mask], [inp['g_feat'], inp['g_mask']])
+    return loss, fvi.grad, feat.grad, mask, idx
 
 
 def dibr_step(inp, world):
@@ -158,12 +163,19 @@ def op_bytes(name, inp, stats):
     D, K, s = 3, 30, 4
     px = B * H * W
     nv = stats['valid_faces']
-    if name in ('dibr_soft_mask_forward_cuda', 'dibr_soft_mask_forward'):
-        # read sel (8/px) + faces (fvi 24 + bbox 16) ; write mask + K x (prob 4 + idx 8 + type 1)
+    if name == 'dibr_soft_mask_forward_cuda':
+        # the _C contract: read sel (8/px) + faces (fvi 24 + bbox 16); write mask + K x (prob 4 + idx 8 + type 1)
         return px * (8 + s + K * (s + 8 + 1)) + B * F * (6 * s + 4 * s)
-    if name in ('dibr_soft_mask_backward_cuda', 'dibr_soft_mask_backward'):
+    if name == 'dibr_soft_mask_forward':
+        # compact state: read sel (8/px), faces (fvi 24 + bbox write/read 2 x 16); write mask + hits (4 + 1)
+        # per px and one record (face 4 + prob 4) per hit
+        return px * (8 + s + 1) + stats['hits'] * (4 + s) + B * F * (6 * s + 2 * 4 * s)
+    if name == 'dibr_soft_mask_backward_cuda':
         # read grad, mask, sel per px + used slots (+ terminator) of uncovered px; write grad (B,F,3,2)
         return px * (s + s + 8) + stats['slot_reads'] * (8 + s + 1) + B * F * 6 * s * 2
+    if name == 'dibr_soft_mask_backward':
+        # compact state: read grad, mask, hits per px + one record per hit + faces; add into grad (B,F,3,2)
+        return px * (s + s + 1) + stats['hits'] * (4 + s) + B * F * 6 * s * 2
     if name == 'packed_rasterize_forward_cuda':
         return px * (8 + 3 * s + D * s) + nv * (3 * s + 6 * s + 4 * s + 3 * D * s)
     if name == 'dibr_rasterize_forward':
@@ -176,8 +188,9 @@ def op_bytes(name, inp, stats):
 
 # kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
 OP_KERNELS = {
-    'dibr_soft_mask_forward': ('bin_faces_kernel<float, kl::SoftSrc', 'soft_mask_fwd_kernel<float, kl::SoftSrc'),
-    'dibr_soft_mask_backward': ('soft_mask_bwd_agg_kernel<float, true>',),
+    'dibr_soft_mask_forward': ('bin_faces_kernel<float, kl::SoftSrc', 'tile_order_kernel', 'soft_tile_fwd_kernel<float',
+                               'soft_tile_eval_kernel<float'),
+    'dibr_soft_mask_backward': ('soft_tile_bwd_kernel<float',),
     'dibr_rasterize_forward': ('raster_vis_kernel<float, kl::RastSrc', 'raster_vis_big_kernel<float, kl::RastSrc',
                                'raster_resolve_kernel<float, kl::RastSrc'),
     'dibr_rasterize_backward': ('rasterize_bwd_gather_kernel<float', 'rasterize_bwd_bigface_kernel<float'),
@@ -197,7 +210,7 @@ def pmc_traffic(op):
                 total += v['hbm_bytes']
                 found += 1
                 break
-    return total if found else None
+    return total if found == len(OP_KERNELS[op]) else None
 
 
 def timed_loop(fn, steps, world):
@@ -291,7 +304,7 @@ def main():
         unc = fidx < 0
         used = (cidx >= 0).sum(-1)
         slot_reads = int((torch.clamp(used + 1, max=30) * unc).sum())
-        stats = dict(valid_faces=int((inp['fnz'] >= 0).sum()), slot_reads=slot_reads,
+        stats = dict(valid_faces=int((inp['fnz'] >= 0).sum()), slot_reads=slot_reads, hits=int(used.sum()),
                      uncovered=float(unc.float().mean()), mean_slots=float(used[unc].float().mean()))
     # eager pass: per-op HIP-event timing for the roofline, and the eager rate
     timer = _native.OpTimer()

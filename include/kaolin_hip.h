@@ -82,26 +82,32 @@ int kl_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int 
                           kl_stream stream);
 
 /* Fused front-end path of rasterize() / RasterizeCuda (rasterization.py:290-388): takes the
- * UNPACKED (B,F) inputs and the optional (B,F) valid mask (uint8/bool) directly, applies
+ * UNPACKED (B,F) inputs and the optional (B,F) valid mask (uint8/bool) -- or, when it is
+ * NULL, the optional (B,F) face_normals_z of dibr_rasterization, valid = face_normals_z >= 0
+ * (dibr.py:195), evaluated in-kernel -- directly, applies
  * the multiplier and the bboxes in-kernel with the front-end's own float ops, and writes
  * the ORIGINAL per-mesh face index (what RasterizeCuda.forward returns after its remap).
  * face_vertices_image (B,F,3,2) unscaled; outputs as kl_packed_rasterize_forward. */
 size_t kl_dibr_rasterize_workspace_bytes(int batch, int height, int width, int num_faces);
 int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, int batch, int num_faces, int feat_dim,
                               const void *face_vertices_z, const void *face_vertices_image,
-                              const void *face_features, const uint8_t *valid_faces, float multiplier, float eps,
+                              const void *face_features, const uint8_t *valid_faces, const void *face_normals_z,
+                              float multiplier, float eps,
                               void *interpolated_features, int64_t *face_idx, void *output_weights,
                               void *workspace, size_t workspace_bytes, kl_stream stream);
 /* Atomic-free backward of the fused path: one thread per face gathers the pixels of the
  * exact pixel range the forward visited for it (same valid_faces / multiplier) whose
  * face_idx equals it (deterministic, row-major order).  Requires face_idx produced by
- * kl_dibr_rasterize_forward with the same valid_faces and multiplier. */
+ * kl_dibr_rasterize_forward with the same valid_faces and multiplier.  Every face's gradient
+ * is written (zeros where it won no pixel).  scratch: NULL, or a zeroed int32 the call uses
+ * as its big-face counter instead of zeroing one in the workspace (kl_dibr_forward). */
 int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
                                const void *grad_interpolated_features, const int64_t *face_idx,
                                const void *output_weights, const void *face_vertices_image,
-                               const void *face_features, const uint8_t *valid_faces, float multiplier, float eps,
-                               void *grad_face_vertices_image, void *grad_face_features, void *workspace,
-                               size_t workspace_bytes, kl_stream stream);
+                               const void *face_features, const uint8_t *valid_faces, const void *face_normals_z,
+                               float multiplier, float eps, void *grad_face_vertices_image,
+                               void *grad_face_features, int *scratch, void *workspace, size_t workspace_bytes,
+                               kl_stream stream);
 
 size_t kl_soft_mask_workspace_bytes(int batch, int height, int width, int num_faces);
 
@@ -136,6 +142,64 @@ int kl_dibr_soft_mask_backward_fused(kl_dtype dtype, int batch, int height, int 
                                      const int64_t *close_face_idx, const uint8_t *close_face_dist_type,
                                      const uint8_t *hits, const void *face_vertices_image, float sigmainv,
                                      float multiplier, void *grad_face_vertices_image, kl_stream stream);
+
+/* Compact fused path of DibrSoftMaskCuda (dibr.py:27-73), the one the front-end runs
+ * (knum <= 255).  The reference saves four (B,H,W,knum) slot tensors for its backward
+ * (dibr.py:46-49); this path saves instead:
+ *   hits     (B,H,W) uint8   the number of filled slots per pixel;
+ *   rec_face, rec_prob       one record per filled slot: local face index | dist_type << 28
+ *                            (uint32) and the slot's probability (tensor dtype); the records
+ *                            of 64-pixel row segment s = (b*H + j) * ceil(W/64) + i/64 occupy
+ *                            [s*64*knum, ...) in (pixel, slot) order
+ *                            (kl_soft_mask_compact_records() elements to allocate; only the
+ *                            filled slots are written);
+ *   seg_tot  int32 per row segment (kl_soft_mask_compact_segments()): its number of records;
+ *   scratch  one int32 the forward zeroes (see kl_dibr_forward).
+ * face_vertices_image UNSCALED as in the _fused entry.  soft_mask equals
+ * kl_dibr_soft_mask_forward's bit for bit. */
+size_t kl_soft_mask_compact_workspace_bytes(int batch, int height, int width, int num_faces);
+size_t kl_soft_mask_compact_records(int batch, int height, int width, int knum);
+size_t kl_soft_mask_compact_segments(int batch, int height, int width);
+int kl_dibr_soft_mask_forward_compact(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
+                                      const void *face_vertices_image, const int64_t *selected_face_idx,
+                                      float sigmainv, double bbox_pad, float multiplier, void *soft_mask,
+                                      uint8_t *hits, uint32_t *rec_face, void *rec_prob, int *seg_tot, int *scratch,
+                                      void *workspace, size_t workspace_bytes, kl_stream stream);
+/* dibr_soft_mask.cpp:110-183 on the compact state.  accumulate = 0: grad_face_vertices_image
+ * is overwritten; 1: the terms are added onto its contents.  scratch is left zeroed. */
+size_t kl_soft_mask_compact_bwd_workspace_bytes(int batch, int height, int width, int knum);
+int kl_dibr_soft_mask_backward_compact(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
+                                       const void *grad_soft_mask, const void *soft_mask, const uint8_t *hits,
+                                       const uint32_t *rec_face, const void *rec_prob, const int *seg_tot,
+                                       const void *face_vertices_image, float sigmainv, float multiplier,
+                                       void *grad_face_vertices_image, int accumulate, int *scratch,
+                                       void *workspace, size_t workspace_bytes, kl_stream stream);
+
+/* dibr_rasterization (dibr.py:119-209) in one call per direction: rasterize with
+ * valid_faces = face_normals_z >= 0 (evaluated in-kernel), then the compact soft mask on
+ * its face index.  Outputs: interpolated_features (B,H,W,D), face_idx (B,H,W) int64,
+ * output_weights (B,H,W,3), soft_mask (B,H,W), and the compact soft-mask state (hits,
+ * rec_face, rec_prob, seg_tot, scratch as above; the backward uses scratch as the
+ * rasterizer gather's big-face counter and leaves it zeroed, so it needs no fill).  The
+ * backward writes grad_face_vertices_image / grad_face_features (every face): the
+ * rasterizer's gather terms plus the soft-mask terms (grad_soft_mask may be NULL).
+ * feat_dim <= 8.  Workspaces: kl_dibr_workspace_bytes (forward),
+ * kl_dibr_bwd_workspace_bytes (backward). */
+size_t kl_dibr_workspace_bytes(int batch, int height, int width, int num_faces);
+size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum);
+int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim, int knum,
+                    const void *face_vertices_z, const void *face_vertices_image, const void *face_features,
+                    const void *face_normals_z, float sigmainv, double bbox_pad, float multiplier, float eps,
+                    void *interpolated_features, int64_t *face_idx, void *output_weights, void *soft_mask,
+                    uint8_t *hits, uint32_t *rec_face, void *rec_prob, int *seg_tot, int *scratch, void *workspace,
+                    size_t workspace_bytes, kl_stream stream);
+int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim, int knum,
+                     const void *grad_interpolated_features, const void *grad_soft_mask, const int64_t *face_idx,
+                     const void *output_weights, const void *face_vertices_image, const void *face_features,
+                     const void *face_normals_z, const void *soft_mask, const uint8_t *hits,
+                     const uint32_t *rec_face, const void *rec_prob, const int *seg_tot, float sigmainv,
+                     float multiplier, float eps, void *grad_face_vertices_image, void *grad_face_features,
+                     int *scratch, void *workspace, size_t workspace_bytes, kl_stream stream);
 
 /* dibr_soft_mask.cpp:110-183  dibr_soft_mask_backward_cuda.
  * Output grad_face_vertices_image (B,F,3,2) (fully written). */

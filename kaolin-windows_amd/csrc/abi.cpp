@@ -8,12 +8,16 @@ namespace kl {
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 int g_dev_flags = 0;
+void *g_dev_debug = nullptr;
 }  // namespace kl
 
 // Development hook (not part of include/kaolin_hip.h): bit flags that switch parts of
 // some kernels off for ablation timing (scripts/dev/ablate.py).  Results are wrong
 // while any flag is set; 0 (the default) is the product path.
 extern "C" void kl_dev_set_flags(int flags) { kl::g_dev_flags = flags; }
+// Development hook: a device buffer some kernels write per-wave timing stamps into
+// (scripts/dev/stamps.py); nullptr (the default) in the product path.
+extern "C" void kl_dev_set_debug(void *buf) { kl::g_dev_debug = buf; }
 
 namespace kl {
 // Byte fill as an ordinary kernel: 16-byte stores over the aligned body, bytes at the

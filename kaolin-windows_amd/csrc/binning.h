@@ -85,7 +85,11 @@ struct RastSrc {
   const T *fvi;          // (B*F,3,2) unscaled
   const uint8_t *vmask;  // (B*F) valid faces, or nullptr = all valid
   T m;
-  __device__ __forceinline__ bool valid(int64_t f) const { return vmask == nullptr || vmask[f] != 0; }
+  const T *nz;           // (B*F) face_normals_z: valid = nz >= 0 (NaN invalid), used when vmask is null
+  __device__ __forceinline__ bool valid(int64_t f) const {
+    if (vmask) return vmask[f] != 0;
+    return nz == nullptr || nz[f] >= (T)0;
+  }
   __device__ __forceinline__ void verts(int64_t f, T v[6]) const {
 #pragma unroll
     for (int q = 0; q < 6; q++) v[q] = fvi[f * 6 + q] * m;
@@ -223,10 +227,11 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *
   }
 }
 
+// zero_bytes: bytes from `bitmap` zeroed first (0 = the bitmap's own g.bytes()).
 template <typename T, typename Src>
 inline int launch_binning(Src src, const int64_t *first_idx, int faces_per_mesh, const BinGeom &g, float m,
-                          uint32_t *bitmap, hipStream_t st, T *bbox_out = nullptr) {
-  KL_CHECK_RC(fill_async(bitmap, 0, g.bytes(), st));
+                          uint32_t *bitmap, hipStream_t st, T *bbox_out = nullptr, size_t zero_bytes = 0) {
+  KL_CHECK_RC(fill_async(bitmap, 0, zero_bytes ? zero_bytes : g.bytes(), st));
   dim3 grid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)g.batch);
   hipLaunchKernelGGL((bin_faces_kernel<T, Src>), grid, dim3(256), 0, st, src, first_idx, faces_per_mesh, g, m,
                      bitmap, bbox_out);

@@ -15,7 +15,12 @@
 namespace kl {
 
 void set_error(const std::string &msg);
-extern int g_dev_flags;  // kl_dev_set_flags (ablation timing only; 0 in the product path)
+extern int g_dev_flags;    // kl_dev_set_flags (ablation timing only; 0 in the product path)
+extern void *g_dev_debug;  // kl_dev_set_debug (per-wave stamps; nullptr in the product path)
+
+// shader-clock and 100 MHz wall-clock stamps for the dev timing buffer
+__device__ __forceinline__ uint64_t stamp_clk() { return __builtin_readcyclecounter(); }
+__device__ __forceinline__ uint64_t stamp_wall() { return __builtin_amdgcn_s_memrealtime(); }
 // memset as a kernel launch on `st` (graph-capture friendly); returns a kl_status
 int fill_async(void *p, int value, size_t bytes, hipStream_t st);
 

@@ -27,7 +27,7 @@
 //                                   face, in row-major order -- no atomics, deterministic.
 //                                   Valid whenever face_idx came from the forward (a face
 //                                   can only be selected inside its bbox).
-#include "binning.h"
+#include "soft_common.h"
 
 namespace kl {
 
@@ -494,16 +494,16 @@ struct GatherAcc {
 template <typename T, int MAXD>
 __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
-    const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid, int B, int H, int W,
-    int F, int D, float m, float eps, T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat, int *__restrict__ big,
-    int *__restrict__ nbig) {
+    const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
+    const T *__restrict__ nz, int B, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
+    T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t tf = t / LPF;  // LPF consecutive lanes per face (whole groups per wave)
   const int s = (int)(t % LPF);
   const bool in = tf < (int64_t)B * F;
   const int b = in ? (int)(tf / F) : 0;
   const int64_t f = tf - (int64_t)b * F;
-  const RastSrc<T> src{fvi, valid, (T)m};
+  const RastSrc<T> src{fvi, valid, (T)m, nz};
   GatherAcc<T, MAXD> acc;
   acc.zero();
   int ix0, ix1, iy0, iy1;
@@ -568,12 +568,12 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
 template <typename T, int MAXD>
 __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
-    const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid, int H, int W, int F,
-    int D, float m, float eps, T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat, const int *__restrict__ big,
-    const int *__restrict__ nbig) {
+    const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
+    const T *__restrict__ nz, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
+    T *__restrict__ grad_ffeat, const int *__restrict__ big, const int *__restrict__ nbig) {
   __shared__ T red[256];
   const int n = *nbig;
-  const RastSrc<T> src{fvi, valid, (T)m};
+  const RastSrc<T> src{fvi, valid, (T)m, nz};
   for (int k = blockIdx.x; k < n; k += gridDim.x) {
     const int64_t tf = big[k];
     const int b = (int)(tf / F);
@@ -629,41 +629,47 @@ static int rasterize_bwd(int B, int H, int W, int F, int D, const void *grad, co
   return KL_OK;
 }
 
+// nbig: a zeroed int (zero_nbig: this call zeroes it first).
 template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
-                                     const T *w, const T *fvi, const T *feat, const uint8_t *valid, float m, float eps,
-                                     T *gfvi, T *gfeat, int *big, int *nbig, hipStream_t st) {
-  KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
+                                     const T *w, const T *fvi, const T *feat, const uint8_t *valid, const T *nz,
+                                     float m, float eps, T *gfvi, T *gfeat, int *big, int *nbig, bool zero_nbig,
+                                     hipStream_t st) {
+  if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
   hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st, grad,
-                     face_idx, w, fvi, feat, valid, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig);
+                     face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig);
   KL_CHECK_LAUNCH();
   hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(256), dim3(256), 0, st, grad, face_idx, w, fvi,
-                     feat, valid, H, W, F, D, m, eps, gfvi, gfeat, big, nbig);
+                     feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
 
+// The gather backward writes every face's gradient (zeros where nothing was won).
+// nbig == nullptr: the big-face counter lives at the head of the workspace and is zeroed here.
 template <typename T>
 static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
-                                const void *w, const void *fvi, const void *feat, const uint8_t *valid, float m,
-                                float eps, void *gfvi, void *gfeat, void *ws, size_t ws_bytes, hipStream_t st) {
+                                const void *w, const void *fvi, const void *feat, const uint8_t *valid, const T *nz,
+                                float m, float eps, void *gfvi, void *gfeat, void *ws, size_t ws_bytes, int *nbig,
+                                hipStream_t st) {
   const int64_t nf = (int64_t)B * F;
   if (nf == 0) return KL_OK;
   KL_REQUIRE(ws_bytes >= (size_t)(nf + 1) * sizeof(int), "rasterize backward: workspace too small");
   KL_REQUIRE(nf < ((int64_t)1 << 31), "rasterize backward: too many faces");
-  int *nbig = reinterpret_cast<int *>(ws);
-  int *big = nbig + 1;
+  const bool zero = nbig == nullptr;
+  if (zero) nbig = reinterpret_cast<int *>(ws);
+  int *big = reinterpret_cast<int *>(ws) + 1;
   const T *g = (const T *)grad;
   const T *wt = (const T *)w;
   const T *fv = (const T *)fvi;
   const T *ft = (const T *)feat;
   if (D <= 4)
-    return rasterize_bwd_gather_maxd<T, 4>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, st);
+    return rasterize_bwd_gather_maxd<T, 4>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
+                                           (T *)gfeat, big, nbig, zero, st);
   if (D <= 8)
-    return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, st);
+    return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
+                                           (T *)gfeat, big, nbig, zero, st);
   // wide features: the scatter kernel
   return rasterize_bwd<T>(B, H, W, F, D, grad, face_idx, w, fvi, feat, eps, gfvi, gfeat, st);
 }
@@ -705,17 +711,19 @@ extern "C" size_t kl_dibr_rasterize_workspace_bytes(int batch, int height, int w
 
 extern "C" int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, int batch, int num_faces,
                                          int feat_dim, const void *fvz, const void *fvi, const void *feat,
-                                         const uint8_t *valid_faces, float multiplier, float eps, void *out_feat,
-                                         int64_t *out_idx, void *out_w, void *ws, size_t ws_bytes,
+                                         const uint8_t *valid_faces, const void *fnz, float multiplier, float eps,
+                                         void *out_feat, int64_t *out_idx, void *out_w, void *ws, size_t ws_bytes,
                                          kl_stream stream) {
   const int64_t nf = (int64_t)batch * num_faces;
   if (dtype == KL_F32)
-    return launch_rast_fwd<float>(RastSrc<float>{(const float *)fvi, valid_faces, (float)multiplier}, height, width,
+    return launch_rast_fwd<float>(RastSrc<float>{(const float *)fvi, valid_faces, (float)multiplier,
+                                                 (const float *)fnz}, height, width,
                                   batch, feat_dim, nf, nf, (const float *)fvz, (const float *)feat, nullptr,
                                   num_faces, multiplier, eps, (float *)out_feat, out_idx, (float *)out_w, ws, ws_bytes,
                                   S(stream));
   if (dtype == KL_F64)
-    return launch_rast_fwd<double>(RastSrc<double>{(const double *)fvi, valid_faces, (double)multiplier}, height,
+    return launch_rast_fwd<double>(RastSrc<double>{(const double *)fvi, valid_faces, (double)multiplier,
+                                                   (const double *)fnz}, height,
                                    width, batch, feat_dim, nf, nf, (const double *)fvz, (const double *)feat, nullptr,
                                    num_faces, multiplier, eps, (double *)out_feat, out_idx, (double *)out_w, ws,
                                    ws_bytes, S(stream));
@@ -740,14 +748,103 @@ extern "C" int kl_rasterize_backward(kl_dtype dtype, int batch, int height, int 
 extern "C" int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces,
                                           int feat_dim, const void *grad, const int64_t *face_idx, const void *w,
                                           const void *fvi, const void *feat, const uint8_t *valid_faces,
-                                          float multiplier, float eps, void *gfvi, void *gfeat, void *ws,
-                                          size_t ws_bytes, kl_stream stream) {
+                                          const void *fnz, float multiplier, float eps, void *gfvi, void *gfeat,
+                                          int *scratch, void *ws, size_t ws_bytes, kl_stream stream) {
   if (dtype == KL_F32)
     return rasterize_bwd_gather<float>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat,
-                                       valid_faces, multiplier, eps, gfvi, gfeat, ws, ws_bytes, S(stream));
+                                       valid_faces, (const float *)fnz, multiplier, eps, gfvi, gfeat, ws, ws_bytes,
+                                       scratch, S(stream));
   if (dtype == KL_F64)
     return rasterize_bwd_gather<double>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat,
-                                        valid_faces, multiplier, eps, gfvi, gfeat, ws, ws_bytes, S(stream));
+                                        valid_faces, (const double *)fnz, multiplier, eps, gfvi, gfeat, ws, ws_bytes,
+                                        scratch, S(stream));
   set_error("dibr_rasterize_backward not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+// ---------------------------------------------------------------- dibr_rasterization
+// The whole of dibr_rasterization (dibr.py:119-209) in one call per direction: rasterize
+// with valid = face_normals_z >= 0 evaluated in-kernel, then the soft mask of the
+// compact path (softtile.hip) on the rasterizer's face index.  The backward runs the
+// gather (which writes every face's gradient) and adds the soft-mask terms onto it.
+// The state's scratch int is the gather's big-face counter: the forward zeroes it and
+// the soft-mask backward re-zeroes it, so the backward needs no fill of its own.
+namespace kl {
+template <typename T>
+static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, const T *fvi, const T *feat, const T *fnz,
+                    float sigmainv, double pad, float m, float eps, T *out_feat, int64_t *out_idx, T *out_w,
+                    T *out_mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st) {
+  const int64_t nf = (int64_t)B * F;
+  KL_CHECK_RC(launch_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, nf, nf, fvz, feat, nullptr, F, m,
+                                 eps, out_feat, out_idx, out_w, ws, ws_bytes, st));
+  return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, ws, ws_bytes, st);
+}
+
+template <typename T>
+static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat, const T *grad_mask,
+                    const int64_t *face_idx, const T *w, const T *fvi, const T *feat, const T *fnz, const T *mask,
+                    const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *ws,
+                    size_t ws_bytes, hipStream_t st) {
+  KL_REQUIRE(D <= 8, "dibr_rasterization backward: feature dimension > 8 is not supported by the fused path");
+  KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
+                                      gfeat, ws, ws_bytes, s.scratch, st));
+  return soft_tile_backward<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m, gfvi, true, ws, ws_bytes, st);
+}
+}  // namespace kl
+
+extern "C" size_t kl_dibr_workspace_bytes(int batch, int height, int width, int num_faces) {
+  const size_t a = kl_dibr_rasterize_workspace_bytes(batch, height, width, num_faces);
+  const size_t b = soft_tile_ws_bytes(batch, height, width, num_faces);
+  return a > b ? a : b;
+}
+
+extern "C" size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum) {
+  const size_t a = kl_dibr_rasterize_workspace_bytes(batch, height, width, num_faces);
+  const size_t b = soft_tile_bwd_ws_bytes(batch, height, width, knum);
+  return a > b ? a : b;
+}
+
+extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
+                               int knum, const void *fvz, const void *fvi, const void *feat, const void *fnz,
+                               float sigmainv, double bbox_pad, float multiplier, float eps, void *out_feat,
+                               int64_t *out_idx, void *out_w, void *out_mask, uint8_t *hits, uint32_t *rec_face,
+                               void *rec_prob, int *seg_tot, int *scratch, void *ws, size_t ws_bytes,
+                               kl_stream stream) {
+  if (dtype == KL_F32)
+    return dibr_fwd<float>(batch, height, width, num_faces, feat_dim, knum, (const float *)fvz, (const float *)fvi,
+                           (const float *)feat, (const float *)fnz, sigmainv, bbox_pad, multiplier, eps,
+                           (float *)out_feat, out_idx, (float *)out_w, (float *)out_mask,
+                           SoftState<float>{hits, rec_face, (float *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
+                           S(stream));
+  if (dtype == KL_F64)
+    return dibr_fwd<double>(batch, height, width, num_faces, feat_dim, knum, (const double *)fvz, (const double *)fvi,
+                            (const double *)feat, (const double *)fnz, sigmainv, bbox_pad, multiplier, eps,
+                            (double *)out_feat, out_idx, (double *)out_w, (double *)out_mask,
+                            SoftState<double>{hits, rec_face, (double *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
+                            S(stream));
+  set_error("dibr_rasterization not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
+                                int knum, const void *grad_feat, const void *grad_mask, const int64_t *face_idx,
+                                const void *w, const void *fvi, const void *feat, const void *fnz, const void *mask,
+                                const uint8_t *hits, const uint32_t *rec_face, const void *rec_prob,
+                                const int *seg_tot, float sigmainv, float multiplier, float eps, void *gfvi,
+                                void *gfeat, int *scratch, void *ws, size_t ws_bytes, kl_stream stream) {
+  if (dtype == KL_F32)
+    return dibr_bwd<float>(
+        batch, height, width, num_faces, feat_dim, knum, (const float *)grad_feat, (const float *)grad_mask, face_idx,
+        (const float *)w, (const float *)fvi, (const float *)feat, (const float *)fnz, (const float *)mask,
+        SoftState<float>{(uint8_t *)hits, (uint32_t *)rec_face, (float *)rec_prob, (int *)seg_tot, scratch},
+        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream));
+  if (dtype == KL_F64)
+    return dibr_bwd<double>(
+        batch, height, width, num_faces, feat_dim, knum, (const double *)grad_feat, (const double *)grad_mask,
+        face_idx, (const double *)w, (const double *)fvi, (const double *)feat, (const double *)fnz,
+        (const double *)mask,
+        SoftState<double>{(uint8_t *)hits, (uint32_t *)rec_face, (double *)rec_prob, (int *)seg_tot, scratch},
+        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream));
+  set_error("dibr_rasterization backward not implemented for this dtype");
   return KL_E_INVALID;
 }

@@ -16,74 +16,11 @@
 //
 // Backward (dibr_soft_mask_cuda.cu:230-353): one thread per pixel, atomics into the
 // face-vertex gradient.
-#include "binning.h"
+#include "soft_common.h"
 
 #include <hipcub/hipcub.hpp>
 
 namespace kl {
-
-constexpr double SM_EPS = 1e-7;
-
-template <typename T>
-__device__ __forceinline__ void soft_dist(T x0, T y0, const T v[6], float multiplier, T &dsq, int &edgeid) {
-  T pdis[6];
-#pragma unroll
-  for (int e = 0; e < 3; e++) {
-    const int e2 = (e + 1) % 3;
-    const T x1 = v[e * 2], y1 = v[e * 2 + 1];
-    const T x2 = v[e2 * 2], y2 = v[e2 * 2 + 1];
-    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
-    const T up = A * x0 + Bc * y0 + C;
-    const T down = A * A + Bc * Bc;
-    T x3 = Bc * Bc * x0 - A * Bc * y0 - A * C;
-    T y3 = A * A * y0 - A * Bc * x0 - Bc * C;
-    x3 = (T)((double)x3 / ((double)down + SM_EPS));
-    y3 = (T)((double)y3 / ((double)down + SM_EPS));
-    const T direct = (x3 - x1) * (x3 - x2) + (y3 - y1) * (y3 - y2);
-    if (direct > (T)0)
-      pdis[e] = (T)(4 * multiplier * multiplier);
-    else
-      pdis[e] = (T)((double)(up * up) / ((double)down + SM_EPS));
-  }
-#pragma unroll
-  for (int e = 0; e < 3; e++) {
-    const T x1 = v[e * 2], y1 = v[e * 2 + 1];
-    pdis[e + 3] = (x0 - x1) * (x0 - x1) + (y0 - y1) * (y0 - y1);
-  }
-  edgeid = 0;
-  dsq = pdis[0];
-#pragma unroll
-  for (int e = 1; e < 6; e++)
-    if (dsq > pdis[e]) {
-      dsq = pdis[e];
-      edgeid = e;
-    }
-}
-
-// Pixel interval [lo, hi] (lane indices of the row segment starting at pixel ibase,
-// clipped to [0, 63]) whose centres c satisfy  x_lo <= c < x_hi  exactly as the
-// reference's float/double comparisons decide it: a float estimate, then corrected
-// against the exact centre formula (monotone in the index).  NaN bounds never reject.
-template <typename T>
-__device__ __forceinline__ void seg_range(T x_lo, T x_hi, float m, int W, int ibase, int &lo, int &hi) {
-  if (!(x_lo == x_lo) || !(x_hi == x_hi)) {
-    lo = 0;
-    hi = 63;
-    return;
-  }
-  const float inv = (float)W / m;  // index = (c / s + W - 1) / 2, s = m / W
-  auto est = [&](T c) -> int {
-    const float t = ((float)c * inv + (float)(W - 1)) * 0.5f - (float)ibase;
-    return t < -1.0f ? -1 : (t > 64.0f ? 64 : (int)ceilf(t));
-  };
-  auto cx = [&](int l) { return pix_x<T>(m, W, ibase + l); };
-  lo = min(max(est(x_lo), 0), 64);  // first lane with c >= x_lo
-  while (lo > 0 && cx(lo - 1) >= x_lo) lo--;
-  while (lo < 64 && !(cx(lo) >= x_lo)) lo++;
-  hi = min(max(est(x_hi) - 1, -1), 63);  // last lane with c < x_hi
-  while (hi < 63 && cx(hi + 1) < x_hi) hi++;
-  while (hi >= 0 && !(cx(hi) < x_hi)) hi--;
-}
 
 // Forward, one wave per 64-pixel row segment, three phases:
 //  1. selection: walk the candidate chunks of the tile in ascending order (the next
@@ -296,25 +233,22 @@ __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
 // reference's expressions, each already divided by the multiplier as it adds them --
 // are summed in an LDS hash table keyed by face (faces of a tile are shared by many
 // of its pixels); the table is flushed with one global atomic per (face, coordinate).
-// Faces that do not fit the table fall back to direct global atomics.
 // kid per pixel: `hits` from the fused forward, or the reference's scan of the slots
 // up to the first -1 (hits == nullptr, the _C contract).
-constexpr int SMB_HCAP = 1024;
-
 template <typename T, bool SCALE>
 __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const int64_t *__restrict__ sel,
     const T *__restrict__ prob, const int64_t *__restrict__ cidx, const uint8_t *__restrict__ ctype,
     const uint8_t *__restrict__ hits, const T *__restrict__ fvi, int B, int H, int W, int F, int K,
-    float sigmainv, float multiplier, T *__restrict__ gfvi, int dev) {
+    float sigmainv, float multiplier, T *__restrict__ gfvi) {
   __shared__ int s_key[SMB_HCAP];
   __shared__ T s_val[SMB_HCAP * 6];
   __shared__ double s_a[8][64];
   __shared__ int s_pre[8][64];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  for (int q = threadIdx.x; q < SMB_HCAP; q += blockDim.x) s_key[q] = -1;
-  for (int q = threadIdx.x; q < SMB_HCAP * 6; q += blockDim.x) s_val[q] = (T)0;
+  FaceHash<T> hash{s_key, s_val};
+  hash.init(threadIdx.x, blockDim.x);
   __syncthreads();
 
   const int b = blockIdx.z;
@@ -323,7 +257,6 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
   const int i = ibase + lane;
   const T ms = (T)multiplier;
   const T *fb = fvi + (size_t)b * F * 6;  // this mesh's face vertices
-  auto V = [&](size_t k) -> T { return SCALE ? fb[k] * ms : fb[k]; };
   int kid = 0;
   size_t pk = 0;
   if (j < H && i < W) {
@@ -353,7 +286,7 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
   const T y0 = pix_y<T>(multiplier, H, j < H ? j : 0);
   const size_t rowk = (((size_t)b * H + (j < H ? j : 0)) * W + ibase) * K;
   T *gb = gfvi + (size_t)b * F * 6;
-  for (int e = lane; e < ((dev & 8) ? 0 : total); e += 64) {
+  for (int e = lane; e < total; e += 64) {
     int lo = 0;
 #pragma unroll
     for (int st = 32; st > 0; st >>= 1)
@@ -365,81 +298,16 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
     const int edgeid = (int)ctype[o] - 1;
     const T x0 = pix_x<T>(multiplier, W, ibase + p);
     const T dLdz = (T)(s_a[wid][p] / (1.0 - (double)pr + SM_EPS) * (double)pr);
-    const size_t s6 = (size_t)f * 6;
-    int c0, c1 = -1;  // coordinate pairs touched: vertex c0 (and c1)
-    T g0x, g0y, g1x = 0, g1y = 0;
-    if (edgeid >= 3) {
-      c0 = edgeid - 3;
-      const T x1 = V(s6 + c0 * 2), y1 = V(s6 + c0 * 2 + 1);
-      g0x = dLdz * (T)2 * (x1 - x0) / (T)multiplier;
-      g0y = dLdz * (T)2 * (y1 - y0) / (T)multiplier;
-    } else {
-      c0 = edgeid;
-      c1 = (edgeid + 1) % 3;
-      const size_t ps = s6 + c0 * 2, ps2 = s6 + c1 * 2;
-      const T x1 = V(ps), y1 = V(ps + 1), x2 = V(ps2), y2 = V(ps2 + 1);
-      const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
-      const T up = A * x0 + Bc * y0 + C;
-      const T down = A * A + Bc * Bc;
-      const T dsq = (T)((double)(up * up) / ((double)down + SM_EPS));
-      const T dzdA = (T)((double)((T)2 * (x0 * up - dsq * A)) / ((double)down + SM_EPS));
-      const T dzdB = (T)((double)((T)2 * (y0 * up - dsq * Bc)) / ((double)down + SM_EPS));
-      const T dzdC = (T)((double)((T)2 * up) / ((double)down + SM_EPS));
-      g0x = dLdz * (dzdB - y2 * dzdC) / (T)multiplier;
-      g0y = dLdz * (x2 * dzdC - dzdA) / (T)multiplier;
-      g1x = dLdz * (y1 * dzdC - dzdB) / (T)multiplier;
-      g1y = dLdz * (dzdA - x1 * dzdC) / (T)multiplier;
-    }
-    if (dev & 4) {  // ablation: loads + arithmetic only
-      asm volatile("" : : "v"(g0x), "v"(g0y), "v"(g1x), "v"(g1y));
-      continue;
-    }
-    // LDS hash slot of face f (linear probing, bounded)
-    int slot = -1;
-    unsigned h = ((unsigned)f * 2654435761u) >> 22;  // 10 bits
-#pragma unroll 1
-    for (int t = 0; t < 16; t++) {
-      const int cur = s_key[h];
-      if (cur == f) {
-        slot = (int)h;
-        break;
-      }
-      if (cur == -1) {
-        const int prev = atomicCAS(&s_key[h], -1, f);
-        if (prev == -1 || prev == f) {
-          slot = (int)h;
-          break;
-        }
-      }
-      h = (h + 1) & (SMB_HCAP - 1);
-    }
-    if (dev & 2) {  // ablation: no accumulation
-      asm volatile("" : : "v"(g0x), "v"(g0y), "v"(g1x), "v"(g1y), "v"(slot));
-      continue;
-    }
-    if (slot >= 0) {
-      atomicAdd(&s_val[slot * 6 + c0 * 2], g0x);
-      atomicAdd(&s_val[slot * 6 + c0 * 2 + 1], g0y);
-      if (c1 >= 0) {
-        atomicAdd(&s_val[slot * 6 + c1 * 2], g1x);
-        atomicAdd(&s_val[slot * 6 + c1 * 2 + 1], g1y);
-      }
-    } else {
-      atomicAdd(gb + s6 + c0 * 2, g0x);
-      atomicAdd(gb + s6 + c0 * 2 + 1, g0y);
-      if (c1 >= 0) {
-        atomicAdd(gb + s6 + c1 * 2, g1x);
-        atomicAdd(gb + s6 + c1 * 2 + 1, g1y);
-      }
-    }
+    T v[6];
+#pragma unroll
+    for (int q = 0; q < 6; q++) v[q] = SCALE ? fb[(size_t)f * 6 + q] * ms : fb[(size_t)f * 6 + q];
+    int c0, c1;
+    T g0x, g0y, g1x, g1y;
+    soft_hit_grad<T>(v, edgeid, x0, y0, dLdz, multiplier, c0, c1, g0x, g0y, g1x, g1y);
+    hash.add(f, c0, c1, g0x, g0y, g1x, g1y, gb);
   }
   __syncthreads();
-  if (dev & 1) return;  // ablation: no flush
-  for (int q = threadIdx.x; q < SMB_HCAP * 6; q += blockDim.x) {
-    const int key = s_key[q / 6];
-    const T v = s_val[q];
-    if (key >= 0 && v != (T)0) atomicAdd(gb + (size_t)key * 6 + q % 6, v);
-  }
+  hash.flush(threadIdx.x, blockDim.x, gb);
 }
 
 // Longest-first order of the tiles for the forward walk: a tile's cost grows with its
@@ -533,8 +401,7 @@ static int soft_mask_bwd(int B, int H, int W, int F, int K, const void *grad, co
   if ((int64_t)B * H * W == 0 || K <= 0) return KL_OK;
   dim3 grid((unsigned)cdiv(W, 64), (unsigned)cdiv(H, 8), B);
   hipLaunchKernelGGL((soft_mask_bwd_agg_kernel<T, SCALE>), grid, dim3(512), 0, st, (const T *)grad, (const T *)mask,
-                     sel, (const T *)prob, cidx, ctype, hits, (const T *)fvi, B, H, W, F, K, sigmainv, m, (T *)gfvi,
-                     g_dev_flags);
+                     sel, (const T *)prob, cidx, ctype, hits, (const T *)fvi, B, H, W, F, K, sigmainv, m, (T *)gfvi);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

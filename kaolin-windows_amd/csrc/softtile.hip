@@ -1,0 +1,897 @@
+// softtile.hip -- DIB-R soft mask with a compact saved state (the fused front-end path).
+//
+// The reference's dibr_soft_mask returns only the soft mask (dibr.py:27-55); its four
+// (B,H,W,knum) slot tensors -- prob f32, idx int64 (-1 padded), type u8 -- exist only
+// to be saved for its backward (dibr.py:58-73), and at 13 B x knum per pixel they are
+// ~95% of the op's HBM traffic (414 MB at the bench config, almost all padding).  The
+// fused path saves instead, per pixel, the number of filled slots (u8) and, per hit, a
+// record (face | type << 28, prob) packed contiguously per 64-pixel row segment in
+// (pixel, slot) order: the same values as the filled slots, nothing for the padding.
+// The soft mask and the gradients are computed with the reference's arithmetic and
+// hit order, so they equal the _C path's (tests/test_gpu_parity.py).
+//
+// Forward, per 64x8 tile (one workgroup, one wave per pixel row):
+//  1. the tile's candidate 64-face chunks (binning.h bitmap) are expanded cooperatively,
+//     R chunks per step (one per wave, all loads in flight together): each face's exact
+//     lane interval on the tile's columns and the tile rows its bbox spans are computed
+//     ONCE for the tile, and faces that touch it are appended in index order to an LDS
+//     face list (ordered compaction across the waves);
+//  2. each row wave walks the list: faces whose interval meets a still-active pixel
+//     (uncovered, < knum hits) are appended, in index order, to the [slot][lane] lists of
+//     the active pixels they cover -- exactly the reference's "first knum faces whose
+//     enlarged bbox contains the pixel centre";
+//  3. the wave's hits are evaluated densely (64 per step), records written contiguously,
+//     and the mask is 1 - prod(1 - p) in slot order.
+// Tiles run heaviest first (candidate-chunk counts, one counting-sort workgroup).
+//
+// Backward, per tile: each row wave reads its records (coalesced), evaluates the
+// reference's per-hit terms and sums them per face in an LDS hash (soft_common.h),
+// flushed with global atomics -- into a zeroed gradient, or added onto the rasterizer
+// backward's gradient (kl_dibr_backward).
+#include "soft_common.h"
+
+#include <algorithm>
+
+namespace kl {
+
+constexpr int ST_LIST_CAP = 1024;  // face-list entries per workgroup (8 B each)
+constexpr int ORD_BUCKETS = 32;
+
+// Heaviest-first tile order: counting sort of the tiles on floor(log2(count + 1)) of their
+// candidate-chunk counts (set bits of the tile's bitmap words), descending.  One thread
+// per tile counts; the workgroup histograms are summed in `ghist`; the last workgroup to
+// finish (the `gdone` ticket) scans the histogram and scatters the order.  ghist / gdone
+// are zeroed with the bitmap.  The scratch int of the compact state is zeroed here too.
+__global__ void __launch_bounds__(256) tile_order_kernel(const uint32_t *__restrict__ bitmap, int words, int nt,
+                                                         uint8_t *__restrict__ bk, int *__restrict__ ghist,
+                                                         int *__restrict__ gdone, int32_t *__restrict__ order,
+                                                         int *__restrict__ scratch) {
+  __shared__ int hist[ORD_BUCKETS];
+  __shared__ int last;
+  if (threadIdx.x < ORD_BUCKETS) hist[threadIdx.x] = 0;
+  if (threadIdx.x == 0 && blockIdx.x == 0 && scratch) *scratch = 0;
+  __syncthreads();
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nt) {
+    const uint32_t *w = bitmap + (size_t)t * words;
+    unsigned n = 0;
+    int k = 0;
+    for (; k + 4 <= words; k += 4) n += __popc(w[k]) + __popc(w[k + 1]) + __popc(w[k + 2]) + __popc(w[k + 3]);
+    for (; k < words; k++) n += __popc(w[k]);
+    const int b = 31 - __clz(n + 1u);
+    bk[t] = (uint8_t)b;
+    atomicAdd(&hist[b], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x < ORD_BUCKETS && hist[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], hist[threadIdx.x]);
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(gdone, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
+      const int c = atomicAdd(&ghist[q], 0);
+      hist[q] = s;
+      s += c;
+    }
+  }
+  __syncthreads();
+  for (int u = threadIdx.x; u < nt; u += blockDim.x) {
+    const int b = __builtin_nontemporal_load(&bk[u]);
+    order[atomicAdd(&hist[b], 1)] = u;
+  }
+}
+
+// Lane exchange v <- v[lane ^ S] with cross-lane VALU ops (gfx950 permlane swaps, DPP)
+// where they exist and ds_swizzle (no memory access) for xor 4.
+template <int S>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lane) {
+  if constexpr (S == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (lane & 32) ? r[0] : r[1];
+  } else if constexpr (S == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return (lane & 16) ? r[0] : r[1];
+  } else if constexpr (S == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  } else if constexpr (S == 4) {
+    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (4 << 10) | 0x1f);  // bitmask mode, xor 4
+  } else if constexpr (S == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  } else {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  }
+}
+
+template <int S>
+__device__ __forceinline__ uint64_t transpose_stage(uint64_t x, uint64_t m, int lane) {
+  const uint64_t p = ((uint64_t)xor_lane<S>((uint32_t)(x >> 32), lane) << 32) | xor_lane<S>((uint32_t)x, lane);
+  return (lane & S) ? ((x & ~m) | ((p & ~m) >> S)) : ((x & m) | ((p & m) << S));
+}
+
+// 64x64 bit-matrix transpose across the wave: lane i holds row i (bit j = column j) on
+// entry and column i (bit j = row j) on exit.  Six block-swap stages.
+__device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {
+  x = transpose_stage<32>(x, 0x00000000ffffffffull, lane);
+  x = transpose_stage<16>(x, 0x0000ffff0000ffffull, lane);
+  x = transpose_stage<8>(x, 0x00ff00ff00ff00ffull, lane);
+  x = transpose_stage<4>(x, 0x0f0f0f0f0f0f0f0full, lane);
+  x = transpose_stage<2>(x, 0x3333333333333333ull, lane);
+  x = transpose_stage<1>(x, 0x5555555555555555ull, lane);
+  return x;
+}
+
+template <typename T>
+struct SoftTileArgs {
+  SoftSrc<T> src;            // unscaled face_vertices_image, multiplier, bbox pad
+  const T *bbox;             // (B*F,4) enlarged bboxes (stored by the binning pass)
+  const int64_t *sel;        // (B,H,W) rasterized face index
+  const uint32_t *bitmap;
+  const int32_t *order;      // tiles, heaviest first
+  BinGeom g;
+  int F, K;
+  float sigmainv, m;
+  T *mask;                   // (B,H,W)
+  uint8_t *hits;             // (B,H,W)
+  uint32_t *rec_face;        // per row segment s: [s*64*K, s*64*K + hits of the segment)
+  T *rec_prob;
+  int *seg_tot;              // per row segment: its number of hits
+  uint64_t *dbg;             // dev stamps (kl_dev_set_debug), 12 per wave, or nullptr
+};
+
+__host__ __device__ constexpr size_t st_wave_lds(int K) { return (size_t)K * 64 * sizeof(uint32_t) + 128 * sizeof(int); }
+constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int); }
+
+// The candidate chunks of a tile (set bits of its bitmap words, ascending) as a sequence
+// with random access by ordinal: 64 words per group, one per lane, with an exclusive
+// prefix of their bit counts.  Wave-uniform; every wave of the workgroup holds a copy.
+// at(n) must be called with non-decreasing n.
+struct ChunkSeq {
+  const uint32_t *words;
+  int nwords, grp, base, gtot, pc;
+  uint32_t wv;
+  __device__ __forceinline__ void load(int g, int lane) {
+    grp = g;
+    const int w = g * 64 + lane;
+    wv = w < nwords ? words[w] : 0u;
+    const int c = __popc(wv);
+    int inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(inc, o);
+      if (lane >= o) inc += u;
+    }
+    pc = inc - c;
+    gtot = __shfl(inc, 63);
+  }
+  __device__ __forceinline__ void init(const uint32_t *w, int n, int lane) {
+    words = w;
+    nwords = n;
+    base = 0;
+    load(0, lane);
+  }
+  __device__ __forceinline__ int at(int n, int lane) {
+    while (n >= base + gtot) {
+      if ((grp + 1) * 64 >= nwords) return -1;
+      base += gtot;
+      load(grp + 1, lane);
+    }
+    const int t = n - base;
+    const uint64_t le = ballot(pc <= t);
+    const int L = 63 - __builtin_clzll(le);
+    int k = t - __builtin_amdgcn_readlane(pc, L);
+    uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)wv, L);
+    int bit = 0;
+#pragma unroll
+    for (int h = 16; h > 0; h >>= 1) {  // the k-th set bit of w
+      const int c = __popc(w & ((1u << h) - 1u));
+      if (k >= c) {
+        k -= c;
+        w >>= h;
+        bit += h;
+      }
+    }
+    return (grp * 64 + L) * 32 + bit;
+  }
+};
+
+template <typename T>
+__global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int R = blockDim.x >> 6;  // rows (waves) per workgroup, divides TILE_H
+  const int K = a.K;
+  const BinGeom &g = a.g;
+  const int H = g.height, W = g.width;
+  uint32_t *L_face = reinterpret_cast<uint32_t *>(smem);
+  uint32_t *L_pack = L_face + ST_LIST_CAP;
+  int *s_cnt = reinterpret_cast<int *>(L_pack + ST_LIST_CAP);  // [8] per-wave scratch
+  unsigned char *mine = smem + st_head_lds() + st_wave_lds(K) * wid;
+  uint32_t *s_face = reinterpret_cast<uint32_t *>(mine);                           // [K][64] face ids
+  int *s_pre = reinterpret_cast<int *>(mine + (size_t)K * 64 * sizeof(uint32_t));  // [64]
+
+  const int per_tile = TILE_H / R;
+  const int tile = a.order[blockIdx.x / per_tile];
+  const int tx = tile % g.tiles_x;
+  const int ty = (tile / g.tiles_x) % g.tiles_y;
+  const int b = tile / (g.tiles_x * g.tiles_y);
+  const int j0 = ty * TILE_H + (blockIdx.x % per_tile) * R;  // first row of the workgroup
+  const int j = j0 + wid;
+  const bool row_ok = j < H;
+  const int ibase = tx * TILE_W;
+  const int i = ibase + lane;
+  const bool px_valid = row_ok && i < W;
+  const size_t pix = ((size_t)b * H + (row_ok ? j : H - 1)) * W + (i < W ? i : W - 1);
+  const bool covered = px_valid ? (a.sel[pix] >= 0) : true;
+  const float m = a.m;
+  const float sx = m / (float)W, sy = m / (float)H, xinv = (float)W / m;  // pixel pitch as pix_x / pix_y
+  auto py = [&](int jj) { return (T)(sy * (float)(H - 2 * jj - 1)); };   // == pix_y<T>(m, H, jj)
+  auto px = [&](int ii) { return (T)(sx * (float)(2 * ii + 1 - W)); };   // == pix_x<T>(m, W, ii)
+  const T y0 = py(row_ok ? j : H - 1);
+  const int64_t f0 = (int64_t)b * a.F;
+  uint64_t t0 = 0, t1 = 0, w0 = 0, c_fill = 0, c_walk = 0, c_sync = 0, tq = 0;
+  uint64_t c_pf = 0, c_test = 0, c_s1 = 0, tr = 0;
+  int n_entries = 0, n_iters = 0, n_groups = 0;
+  if (a.dbg) {
+    t0 = stamp_clk();
+    w0 = stamp_wall();
+  }
+
+  int kid = 0;
+  bool active = !covered && K > 0;
+  uint64_t amask = ballot(active);
+  if (lane == 0) s_cnt[wid] = amask != 0;
+  __syncthreads();
+  int any = 0;
+  for (int w = 0; w < R; w++) any |= s_cnt[w];
+  __syncthreads();
+
+  if (any) {
+    ChunkSeq seq;
+    seq.init(a.bitmap + ((size_t)(b * g.tiles_y + ty) * g.tiles_x + tx) * g.words, g.words, lane);
+    const T *bb = a.bbox + f0 * 4;
+    // this wave's chunk of the next step (chunk ordinal pos + wid) with its bboxes in flight
+    int pos = 0, nc = -1;
+    bool nexists = false;
+    T nb0 = 0, nb1 = 0, nb2 = 0, nb3 = 0;
+    auto pf_next = [&]() {
+      nexists = seq.at(pos, lane) >= 0;
+      nc = nexists ? seq.at(pos + wid, lane) : -1;
+      pos += R;
+      const int fl = nc * 64 + lane;
+      if (nc >= 0 && fl < a.F) {
+        if (sizeof(T) == 4) {
+          const float4 q4 = reinterpret_cast<const float4 *>(bb)[fl];
+          nb0 = (T)q4.x;
+          nb1 = (T)q4.y;
+          nb2 = (T)q4.z;
+          nb3 = (T)q4.w;
+        } else {
+          nb0 = bb[fl * 4 + 0];
+          nb1 = bb[fl * 4 + 1];
+          nb2 = bb[fl * 4 + 2];
+          nb3 = bb[fl * 4 + 3];
+        }
+      }
+    };
+    pf_next();
+    bool more = nexists;
+    while (true) {
+      // ---- 1. expand candidate chunks into the face list, R chunks per step; the next
+      //         step's bboxes are in flight while this step's are tested
+      int len = 0;
+      if (a.dbg) tq = stamp_clk();
+      while (more && len + R * 64 <= ST_LIST_CAP) {
+        if (a.dbg) tr = stamp_clk();
+        const int c = nc;
+        const T bx0 = nb0, by0 = nb1, bx1 = nb2, by1 = nb3;
+        pf_next();  // consumed by the next step, in this fill or after the drain
+        more = nexists;
+        if (a.dbg) {
+          const uint64_t t = stamp_clk();
+          c_pf += t - tr;
+          tr = t;
+        }
+        bool keep = false;
+        int lo = 64, hi = -1;
+        uint32_t rows = 0;
+        const int fl = c * 64 + lane;
+        if (c >= 0 && fl < a.F) {
+          for (int r = 0; r < R; r++) {
+            const int jr = j0 + r;
+            if (jr < H) {
+              const T yr = py(jr);
+              if (!(yr < by0 || yr >= by1)) rows |= 1u << r;
+            }
+          }
+          if (rows) seg_range_s<T>(bx0, bx1, sx, xinv, W, ibase, lo, hi);
+          keep = rows != 0 && lo <= hi;
+        }
+        const uint64_t km = ballot(keep);
+        if (lane == 0) s_cnt[wid] = __popcll(km);
+        if (a.dbg) {
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          const uint64_t t = stamp_clk();
+          c_test += t - tr;
+          tr = t;
+        }
+        __syncthreads();
+        if (a.dbg) {
+          const uint64_t t = stamp_clk();
+          c_s1 += t - tr;
+          tr = t;
+        }
+        int pre = 0, tot = 0;
+        for (int w = 0; w < R; w++) {
+          const int v = s_cnt[w];
+          pre += w < wid ? v : 0;
+          tot += v;
+        }
+        if (keep) {
+          const int p = len + pre + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
+                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
+          L_face[p] = (uint32_t)fl;
+          L_pack[p] = (uint32_t)lo | ((uint32_t)hi << 6) | (rows << 12);
+        }
+        len += tot;
+        n_groups++;
+        __syncthreads();
+      }
+      n_entries += len;
+      if (a.dbg) {
+        const uint64_t t = stamp_clk();
+        c_fill += t - tq;
+        tq = t;
+      }
+      // ---- 2. this row's walk over the list, 64 entries per step: the entries' pixel
+      //         masks are transposed so that every pixel lane holds the (ordered) entries
+      //         covering it, and appends them until it has knum hits
+      for (int base = 0; base < len && amask; base += 64) {
+        const int e = base + lane;
+        uint64_t rm = 0;
+        if (e < len) {
+          const uint32_t pk = L_pack[e];
+          if ((pk >> (12 + wid)) & 1u) {
+            const int lo = (int)(pk & 63u), hi = (int)((pk >> 6) & 63u);
+            rm = (~0ull >> (63 - hi)) & (~0ull << lo);
+          }
+        }
+        if (!ballot((rm & amask) != 0)) continue;
+        uint64_t cm = transpose64(rm, lane);
+        if (!active) cm = 0;
+        while (cm) {
+          const int q = __builtin_ctzll(cm);
+          cm &= cm - 1;
+          s_face[kid * 64 + lane] = L_face[base + q];
+          kid++;
+          n_iters++;
+          if (kid >= K) {
+            active = false;
+            cm = 0;
+          }
+        }
+        amask = ballot(active);
+      }
+      if (a.dbg) {
+        const uint64_t t = stamp_clk();
+        c_walk += t - tq;
+        tq = t;
+      }
+      if (lane == 0) s_cnt[wid] = amask != 0;
+      __syncthreads();
+      any = 0;
+      for (int w = 0; w < R; w++) any |= s_cnt[w];
+      __syncthreads();
+      if (a.dbg) c_sync += stamp_clk() - tq;
+      if (!any || !more) break;
+    }
+  }
+  if (!px_valid) kid = 0;
+  if (a.dbg) t1 = stamp_clk();
+
+  // ---- 3. the row's hits (face ids, (pixel, slot) order) -> records; the evaluation
+  //         runs in soft_tile_eval_kernel, where heavy rows spread over the whole chip
+  int pre = kid;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(pre, o);
+    if (lane >= o) pre += u;
+  }
+  const int total = __shfl(pre, 63);
+  s_pre[lane] = pre - kid;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const size_t rbase = ((size_t)(b * H + (row_ok ? j : 0)) * g.tiles_x + tx) * 64 * (size_t)K;
+  for (int e = lane; e < total; e += 64) {
+    int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
+#pragma unroll
+    for (int st = 32; st > 0; st >>= 1)
+      if (s_pre[lo + st] <= e) lo += st;
+    a.rec_face[rbase + e] = s_face[(e - s_pre[lo]) * 64 + lo];
+  }
+  if (px_valid) {
+    a.hits[pix] = (uint8_t)kid;
+    if (kid == 0) a.mask[pix] = covered ? (T)1.0 : (T)0.0;  // 1 - prod over no slots = 0
+  }
+  if (row_ok && lane == 0) a.seg_tot[(size_t)(b * H + j) * g.tiles_x + tx] = total;
+  if (a.dbg && lane == 0) {
+    uint64_t *d = a.dbg + ((size_t)blockIdx.x * R + wid) * 12;
+    d[8] = c_fill;
+    d[9] = c_walk;
+    d[10] = c_sync;
+    d[11] = (c_pf << 42) | ((c_test & 0x1fffff) << 21) | (c_s1 & 0x1fffff);
+    d[0] = t0;
+    d[1] = t1;
+    d[2] = stamp_clk();
+    d[3] = w0;
+    d[4] = stamp_wall();
+    d[5] = (uint64_t)total;  // (eval stamps t1..t2 are now the record write-out)
+    d[6] = ((uint64_t)n_entries << 32) | (uint32_t)n_iters;
+    d[7] = ((uint64_t)n_groups << 32) | (uint32_t)tile;
+  }
+}
+
+// Evaluation of the selected hits: one wave per row segment (4 per workgroup, the tile's
+// rows in the heaviest-first tile order), the hits evaluated densely U x 64 at a time with
+// their vertex loads in flight together, the reference's per-(pixel, face) distance and
+// probability, then 1 - prod(1 - p) in slot order for the pixels with hits.
+template <typename T>
+__global__ void __launch_bounds__(256) soft_tile_eval_kernel(SoftTileArgs<T> a) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int R = blockDim.x >> 6;
+  const int K = a.K;
+  const BinGeom &g = a.g;
+  const int H = g.height, W = g.width;
+  unsigned char *mine = smem + ((size_t)K * 64 * sizeof(T) + 64 * sizeof(int)) * wid;
+  T *s_prob = reinterpret_cast<T *>(mine);                                  // [K][64]
+  int *s_pre = reinterpret_cast<int *>(mine + (size_t)K * 64 * sizeof(T));  // [64]
+  const int per_tile = TILE_H / R;
+  const int tile = a.order[blockIdx.x / per_tile];
+  const int tx = tile % g.tiles_x;
+  const int ty = (tile / g.tiles_x) % g.tiles_y;
+  const int b = tile / (g.tiles_x * g.tiles_y);
+  const int j = ty * TILE_H + (blockIdx.x % per_tile) * R + wid;
+  if (j >= H) return;
+  const int ibase = tx * TILE_W;
+  const int i = ibase + lane;
+  const bool px_valid = i < W;
+  const size_t pix = ((size_t)b * H + j) * W + (px_valid ? i : W - 1);
+  const int kid = px_valid ? (int)a.hits[pix] : 0;
+  int pre = kid;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(pre, o);
+    if (lane >= o) pre += u;
+  }
+  const int total = __shfl(pre, 63);
+  if (total == 0) return;
+  s_pre[lane] = pre - kid;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const float m = a.m;
+  const float sx = m / (float)W, sy = m / (float)H;
+  const T y0 = (T)(sy * (float)(H - 2 * j - 1));  // == pix_y
+  const int64_t f0 = (int64_t)b * a.F;
+  const size_t rbase = ((size_t)(b * H + j) * g.tiles_x + tx) * 64 * (size_t)K;
+  constexpr int U = 4;
+  for (int e0 = lane; e0 < total; e0 += 64 * U) {
+    int pp[U], kk[U];
+    uint32_t ff[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int e = e0 + 64 * u;
+      int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (s_pre[lo + st] <= e) lo += st;
+      pp[u] = lo;
+      kk[u] = e - s_pre[lo];
+      ff[u] = e < total ? a.rec_face[rbase + e] : 0u;
+    }
+    T v[U][6];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (e0 + 64 * u < total) a.src.verts(f0 + ff[u], v[u]);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int e = e0 + 64 * u;
+      if (e < total) {
+        T dsq;
+        int edgeid;
+        soft_dist<T>((T)(sx * (float)(2 * (ibase + pp[u]) + 1 - W)), y0, v[u], m, dsq, edgeid);
+        const T z = (T)a.sigmainv * dsq / (T)m / (T)m;
+        const T pr = kl_exp<T>(-z);
+        a.rec_face[rbase + e] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
+        a.rec_prob[rbase + e] = pr;
+        s_prob[kk[u] * 64 + pp[u]] = pr;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (kid > 0) {
+    // 1 - prod(1 - p) in double, slot order (dibr_soft_mask_cuda.cu:174-182)
+    T allprob = (T)1.0;
+    for (int k = 0; k < kid; k++) allprob = (T)((double)allprob * (1.0 - (double)s_prob[k * 64 + lane]));
+    a.mask[pix] = (T)(1.0 - (double)allprob);
+  }
+}
+
+// ---------------------------------------------------------------- backward
+// Work items of the backward: per tile, the hits of its 8 rows taken row-major in pieces
+// of SB_PIECE (one hit per thread of a workgroup), so that the heavy tiles (the silhouette's
+// tight spots, ~10^4 hits) spread over many workgroups.  The plan kernel (one workgroup)
+// lists the items tile by tile from the forward's per-row-segment hit totals and zeroes
+// the item counter; the backward kernel is persistent and claims items in that order.
+constexpr int SB_PIECE = 512;
+
+__global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restrict__ seg_tot, BinGeom g,
+                                                             int2 *__restrict__ items, int *__restrict__ ctl) {
+  __shared__ int s_sum[1024];
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  int carry = 0;
+  for (int t0 = 0; t0 < nt; t0 += blockDim.x) {
+    const int t = t0 + threadIdx.x;
+    int np = 0;
+    if (t < nt) {
+      const int tx = t % g.tiles_x, ty = (t / g.tiles_x) % g.tiles_y, b = t / (g.tiles_x * g.tiles_y);
+      int tot = 0;
+      for (int r = 0; r < TILE_H; r++) {
+        const int j = ty * TILE_H + r;
+        if (j < g.height) tot += seg_tot[((size_t)b * g.height + j) * g.tiles_x + tx];
+      }
+      np = (tot + SB_PIECE - 1) / SB_PIECE;
+    }
+    s_sum[threadIdx.x] = np;
+    __syncthreads();
+    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
+      const int v = (int)threadIdx.x >= o ? s_sum[threadIdx.x - o] : 0;
+      __syncthreads();
+      s_sum[threadIdx.x] += v;
+      __syncthreads();
+    }
+    const int excl = carry + s_sum[threadIdx.x] - np;
+    for (int q = 0; q < np; q++) items[excl + q] = make_int2(t, q);
+    carry += s_sum[blockDim.x - 1];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    ctl[0] = carry;
+    ctl[1] = 0;
+  }
+}
+
+// Per-face accumulation for one work item: LDS hash on the mesh-local face index with
+// the list of used slots, so the flush and the reset touch only those.  HC slots (a power
+// of two): 1024 for f32; 512 for f64, whose workgroup would otherwise need ~64 KB of LDS.
+template <typename T, int HC>
+struct ItemHash {
+  int *key;   // [HC], -1 = empty
+  T *val;     // [HC * 6]
+  int *used;  // [HC]
+  int *nused;
+  __device__ __forceinline__ int slot(int f) {
+    unsigned h = ((unsigned)f * 2654435761u) >> (32 - __builtin_ctz(HC));
+#pragma unroll 1
+    for (int t = 0; t < 32; t++) {
+      const int cur = key[h];
+      if (cur == f) return (int)h;
+      if (cur == -1) {
+        const int prev = atomicCAS(&key[h], -1, f);
+        if (prev == -1) {
+          used[atomicAdd(nused, 1)] = (int)h;
+          return (int)h;
+        }
+        if (prev == f) return (int)h;
+      }
+      h = (h + 1) & (HC - 1);
+    }
+    return -1;
+  }
+  __device__ __forceinline__ void add(int f, int c0, int c1, T g0x, T g0y, T g1x, T g1y, T *gmesh) {
+    const int s = slot(f);
+    if (s >= 0) {
+      atomicAdd(&val[s * 6 + c0 * 2], g0x);
+      atomicAdd(&val[s * 6 + c0 * 2 + 1], g0y);
+      if (c1 >= 0) {
+        atomicAdd(&val[s * 6 + c1 * 2], g1x);
+        atomicAdd(&val[s * 6 + c1 * 2 + 1], g1y);
+      }
+    } else {  // no free slot within the probe bound
+      global_add_pair<T>(gmesh + (size_t)f * 6, c0, c1, g0x, g0y, g1x, g1y);
+    }
+  }
+  // one thread per used slot: add its non-zero coordinates to the mesh gradient, reset it
+  __device__ __forceinline__ void flush_reset(int tid, int nthreads, T *gmesh) {
+    const int n = *nused;
+    for (int u = tid; u < n; u += nthreads) {
+      const int sl = used[u];
+      const int f = key[sl];
+#pragma unroll
+      for (int c = 0; c < 6; c++) {
+        const T v = val[sl * 6 + c];
+        if (v != (T)0) atomicAdd(gmesh + (size_t)f * 6 + c, v);
+        val[sl * 6 + c] = (T)0;
+      }
+      key[sl] = -1;
+    }
+  }
+};
+
+// Backward (persistent): one work item (tile, piece) at a time per 512-thread workgroup;
+// each wave prepares one row of the tile (filled-slot prefix, the reference's
+// a = -sigmainv * dLdp * (1 - allprob)), then every thread takes one hit of the piece:
+// its record, the reference's terms (soft_hit_grad), summed per face in the item hash.
+template <typename T>
+__global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
+    const T *__restrict__ grad, const T *__restrict__ mask, const uint8_t *__restrict__ hits,
+    const uint32_t *__restrict__ rec_face, const T *__restrict__ rec_prob, const T *__restrict__ fvi, BinGeom g,
+    int F, int K, float sigmainv, float multiplier, T *__restrict__ gfvi, const int2 *__restrict__ items,
+    int *__restrict__ ctl, int *__restrict__ scratch, int dev) {
+  constexpr int HC = sizeof(T) == 4 ? 1024 : 512;
+  __shared__ int s_key[HC];
+  __shared__ T s_val[HC * 6];
+  __shared__ int s_used[HC];
+  __shared__ int s_nused, s_item;
+  __shared__ double s_a[TILE_H][64];
+  __shared__ int s_pre[TILE_H][65];
+  __shared__ int s_rowpre[TILE_H + 1];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;  // the item's row
+  const int H = g.height, W = g.width;
+  for (int q = threadIdx.x; q < HC; q += blockDim.x) s_key[q] = -1;
+  for (int q = threadIdx.x; q < HC * 6; q += blockDim.x) s_val[q] = (T)0;
+  if (threadIdx.x == 0) s_nused = 0;
+  if (scratch && threadIdx.x == 0 && blockIdx.x == 0) *scratch = 0;
+  ItemHash<T, HC> hash{s_key, s_val, s_used, &s_nused};
+  const int nitems = ctl[0];
+  const T ms = (T)multiplier;
+  const float sx = multiplier / (float)W, sy = multiplier / (float)H;
+  while (true) {
+    __syncthreads();  // the previous item's hash reset / s_item reads are done
+    if (threadIdx.x == 0) s_item = atomicAdd(&ctl[1], 1);
+    __syncthreads();
+    const int q = s_item;
+    if (q >= nitems) return;
+    const int2 it = items[q];
+    const int tile = it.x;
+    const int tx = tile % g.tiles_x, ty = (tile / g.tiles_x) % g.tiles_y, b = tile / (g.tiles_x * g.tiles_y);
+    const int ibase = tx * TILE_W;
+    {  // row `wid` of the tile
+      const int j = ty * TILE_H + wid, i = ibase + lane;
+      int kid = 0;
+      if (j < H && i < W) {
+        const size_t p = ((size_t)b * H + j) * W + i;
+        kid = hits[p];
+        // the reference's  -1.0 * sigmainv * dLdp * (1.0 - allprob), evaluated left to right
+        if (kid) s_a[wid][lane] = -1.0 * (double)sigmainv * (double)grad[p] * (1.0 - (double)mask[p]);
+      }
+      int pre = kid;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int u = __shfl_up(pre, o);
+        if (lane >= o) pre += u;
+      }
+      s_pre[wid][lane] = pre - kid;
+      if (lane == 63) s_rowpre[wid + 1] = pre;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      s_rowpre[0] = 0;
+      for (int r = 1; r <= TILE_H; r++) s_rowpre[r] += s_rowpre[r - 1];
+    }
+    __syncthreads();
+    const int f = it.y * SB_PIECE + (int)threadIdx.x;
+    if (f < s_rowpre[TILE_H] && !(dev & 8)) {
+      int r = 0;
+#pragma unroll
+      for (int k = 1; k < TILE_H; k++) r += s_rowpre[k] <= f ? 1 : 0;
+      const int e = f - s_rowpre[r];
+      int lo = 0;  // owner lane: last lane with s_pre[r][lo] <= e
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (s_pre[r][lo + st] <= e) lo += st;
+      const int j = ty * TILE_H + r;
+      const size_t o = ((size_t)(b * H + j) * g.tiles_x + tx) * 64 * (size_t)K + e;
+      const uint32_t rr = rec_face[o];
+      const T pr = rec_prob[o];
+      const int face = (int)(rr & 0x0fffffffu);
+      const int edgeid = (int)(rr >> 28) - 1;
+      const T x0 = (T)(sx * (float)(2 * (ibase + lo) + 1 - W));  // == pix_x
+      const T y0 = (T)(sy * (float)(H - 2 * j - 1));               // == pix_y
+      const T dLdz = (T)(s_a[r][lo] / (1.0 - (double)pr + SM_EPS) * (double)pr);
+      const T *fb = fvi + ((size_t)b * F + face) * 6;
+      T v[6];
+#pragma unroll
+      for (int c = 0; c < 6; c++) v[c] = fb[c] * ms;
+      int c0, c1;
+      T g0x, g0y, g1x, g1y;
+      soft_hit_grad<T>(v, edgeid, x0, y0, dLdz, multiplier, c0, c1, g0x, g0y, g1x, g1y);
+      if (dev & 2)
+        asm volatile("" : : "v"(g0x), "v"(g0y), "v"(g1x), "v"(g1y), "v"(c0), "v"(c1));
+      else
+        hash.add(face, c0, c1, g0x, g0y, g1x, g1y, gfvi + (size_t)b * F * 6);
+    }
+    __syncthreads();
+    hash.flush_reset(threadIdx.x, blockDim.x, gfvi + (size_t)b * F * 6);
+    __syncthreads();
+    if (threadIdx.x == 0) s_nused = 0;
+  }
+}
+
+// workspace: bitmap | ghist[32], gdone (zeroed with the bitmap) | tile buckets | tile order |
+// bboxes (sized for f64)
+struct StWs {
+  size_t hist, zero, bk, order, bbox, bytes;
+  StWs(const BinGeom &g, int F) {
+    const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
+    hist = g.bytes();
+    zero = hist + (ORD_BUCKETS + 1) * sizeof(int);
+    bk = (zero + 255) & ~(size_t)255;
+    order = (bk + nt + 255) & ~(size_t)255;
+    bbox = (order + nt * 4 + 255) & ~(size_t)255;
+    bytes = bbox + (size_t)g.batch * F * 4 * sizeof(double);
+  }
+};
+
+static int rows_per_wg(int K) {
+  for (int R = 8; R >= 1; R >>= 1)
+    if (st_head_lds() + st_wave_lds(K) * R <= 150 * 1024) return R;
+  return 0;
+}
+
+template <typename T>
+int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv, double pad,
+                      float m, T *mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st) {
+  uint8_t *hits = s.hits;
+  uint32_t *rec_face = s.rec_face;
+  T *rec_prob = s.rec_prob;
+  int *scratch = s.scratch;
+  const BinGeom g = make_bin_geom(B, H, W, F);
+  const StWs L(g, F);
+  KL_REQUIRE(ws_bytes >= L.bytes, "dibr_soft_mask: workspace too small");
+  KL_REQUIRE(K >= 0 && K <= 255, "dibr_soft_mask: the compact path needs 0 <= knum <= 255");
+  KL_REQUIRE(F < (1 << 28), "dibr_soft_mask: too many faces");
+  if ((int64_t)B * H * W == 0) return scratch ? fill_async(scratch, 0, sizeof(int), st) : KL_OK;
+  int R = rows_per_wg(K);
+  KL_REQUIRE(R > 0, "dibr_soft_mask: knum too large for the LDS slot lists");
+  const int dev_r = (g_dev_flags >> 8) & 15;  // dev override of the rows per workgroup (ablation)
+  if (dev_r && dev_r <= R && TILE_H % dev_r == 0) R = dev_r;
+  char *w = reinterpret_cast<char *>(ws);
+  uint32_t *bitmap = reinterpret_cast<uint32_t *>(w);
+  int *ghist = reinterpret_cast<int *>(w + L.hist);
+  uint8_t *bk = reinterpret_cast<uint8_t *>(w + L.bk);
+  int32_t *order = reinterpret_cast<int32_t *>(w + L.order);
+  T *bbox = reinterpret_cast<T *>(w + L.bbox);
+  const SoftSrc<T> src{fvi, (T)m, (T)pad};
+  const int rc = launch_binning<T, SoftSrc<T>>(src, nullptr, F, g, m, bitmap, st, bbox, L.zero);
+  if (rc) return rc;
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  hipLaunchKernelGGL(tile_order_kernel, dim3((unsigned)cdiv(nt, 256)), dim3(256), 0, st, (const uint32_t *)bitmap,
+                     g.words, nt, bk, ghist, ghist + ORD_BUCKETS, order, scratch);
+  KL_CHECK_LAUNCH();
+  SoftTileArgs<T> args{src,  bbox, sel,  bitmap,   order,    g,        F,         K,
+                       sigmainv, m, mask, hits, rec_face, rec_prob, s.seg_tot, (uint64_t *)g_dev_debug};
+  const size_t lds = st_head_lds() + st_wave_lds(K) * R;
+  hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)(nt * (TILE_H / R))), dim3(64 * R), lds, st, args);
+  KL_CHECK_LAUNCH();
+  if (K > 0) {
+    const size_t ew = (size_t)K * 64 * sizeof(T) + 64 * sizeof(int);
+    int RE = 4;
+    while (RE > 1 && ew * RE > 64 * 1024) RE >>= 1;
+    hipLaunchKernelGGL((soft_tile_eval_kernel<T>), dim3((unsigned)(nt * (TILE_H / RE))), dim3(64 * RE), ew * RE, st,
+                       args);
+    KL_CHECK_LAUNCH();
+  }
+  return KL_OK;
+}
+
+size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int K) {
+  const BinGeom g = make_bin_geom(B, H, W, 1);
+  const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
+  return 256 + nt * (size_t)(K + 2) * sizeof(int2);
+}
+
+template <typename T>
+int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
+                       const T *fvi, float sigmainv, float m, T *gfvi, bool accumulate, void *ws, size_t ws_bytes,
+                       hipStream_t st) {
+  KL_REQUIRE(F < (1 << 28), "dibr_soft_mask backward: too many faces");
+  if (!accumulate) KL_CHECK_RC(fill_async(gfvi, 0, sizeof(T) * (size_t)B * F * 6, st));
+  if ((int64_t)B * H * W == 0 || K <= 0 || grad == nullptr)
+    return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
+  KL_REQUIRE(ws_bytes >= soft_tile_bwd_ws_bytes(B, H, W, K), "dibr_soft_mask backward: workspace too small");
+  const BinGeom g = make_bin_geom(B, H, W, F);
+  int *ctl = reinterpret_cast<int *>(ws);
+  int2 *items = reinterpret_cast<int2 *>(reinterpret_cast<char *>(ws) + 256);
+  hipLaunchKernelGGL(soft_bwd_plan_kernel, dim3(1), dim3(1024), 0, st, (const int *)s.seg_tot, g, items, ctl);
+  KL_CHECK_LAUNCH();
+  int dev_id = 0, ncu = 256;
+  if (hipGetDevice(&dev_id) == hipSuccess)
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_id);
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
+  hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
+                     (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, gfvi,
+                     (const int2 *)items, ctl, s.scratch, g_dev_flags);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+template int soft_tile_forward<float>(int, int, int, int, int, const float *, const int64_t *, float, double, float,
+                                      float *, const SoftState<float> &, void *, size_t, hipStream_t);
+template int soft_tile_forward<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
+                                       float, double *, const SoftState<double> &, void *, size_t, hipStream_t);
+template int soft_tile_backward<float>(int, int, int, int, int, const float *, const float *,
+                                       const SoftState<float> &, const float *, float, float, float *, bool, void *,
+                                       size_t, hipStream_t);
+template int soft_tile_backward<double>(int, int, int, int, int, const double *, const double *,
+                                        const SoftState<double> &, const double *, float, float, double *, bool,
+                                        void *, size_t, hipStream_t);
+
+size_t soft_tile_ws_bytes(int B, int H, int W, int F) { return StWs(make_bin_geom(B, H, W, F), F).bytes; }
+
+}  // namespace kl
+
+using namespace kl;
+
+extern "C" size_t kl_soft_mask_compact_workspace_bytes(int batch, int height, int width, int num_faces) {
+  return soft_tile_ws_bytes(batch, height, width, num_faces);
+}
+
+extern "C" size_t kl_soft_mask_compact_records(int batch, int height, int width, int knum) {
+  return (size_t)batch * height * cdiv(width, TILE_W) * TILE_W * (size_t)(knum > 0 ? knum : 0);
+}
+
+extern "C" size_t kl_soft_mask_compact_segments(int batch, int height, int width) {
+  return (size_t)batch * height * cdiv(width, TILE_W);
+}
+
+extern "C" size_t kl_soft_mask_compact_bwd_workspace_bytes(int batch, int height, int width, int knum) {
+  return soft_tile_bwd_ws_bytes(batch, height, width, knum);
+}
+
+extern "C" int kl_dibr_soft_mask_forward_compact(kl_dtype dtype, int batch, int height, int width, int num_faces,
+                                                 int knum, const void *fvi, const int64_t *sel, float sigmainv,
+                                                 double pad, float multiplier, void *mask, uint8_t *hits,
+                                                 uint32_t *rec_face, void *rec_prob, int *seg_tot, int *scratch,
+                                                 void *ws, size_t ws_bytes, kl_stream stream) {
+  if (dtype == KL_F32)
+    return soft_tile_forward<float>(batch, height, width, num_faces, knum, (const float *)fvi, sel, sigmainv, pad,
+                                    multiplier, (float *)mask,
+                                    SoftState<float>{hits, rec_face, (float *)rec_prob, seg_tot, scratch}, ws,
+                                    ws_bytes, S(stream));
+  if (dtype == KL_F64)
+    return soft_tile_forward<double>(batch, height, width, num_faces, knum, (const double *)fvi, sel, sigmainv, pad,
+                                     multiplier, (double *)mask,
+                                     SoftState<double>{hits, rec_face, (double *)rec_prob, seg_tot, scratch}, ws,
+                                     ws_bytes, S(stream));
+  set_error("dibr_soft_mask not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_dibr_soft_mask_backward_compact(kl_dtype dtype, int batch, int height, int width, int num_faces,
+                                                  int knum, const void *grad, const void *mask, const uint8_t *hits,
+                                                  const uint32_t *rec_face, const void *rec_prob, const int *seg_tot,
+                                                  const void *fvi, float sigmainv, float multiplier, void *gfvi,
+                                                  int accumulate, int *scratch, void *ws, size_t ws_bytes,
+                                                  kl_stream stream) {
+  if (dtype == KL_F32)
+    return soft_tile_backward<float>(
+        batch, height, width, num_faces, knum, (const float *)grad, (const float *)mask,
+        SoftState<float>{(uint8_t *)hits, (uint32_t *)rec_face, (float *)rec_prob, (int *)seg_tot, scratch},
+        (const float *)fvi, sigmainv, multiplier, (float *)gfvi, accumulate != 0, ws, ws_bytes, S(stream));
+  if (dtype == KL_F64)
+    return soft_tile_backward<double>(
+        batch, height, width, num_faces, knum, (const double *)grad, (const double *)mask,
+        SoftState<double>{(uint8_t *)hits, (uint32_t *)rec_face, (double *)rec_prob, (int *)seg_tot, scratch},
+        (const double *)fvi, sigmainv, multiplier, (double *)gfvi, accumulate != 0, ws, ws_bytes, S(stream));
+  set_error("dibr_soft_mask backward not implemented for this dtype");
+  return KL_E_INVALID;
+}

@@ -23,9 +23,19 @@ def _valid_u8(valid_faces):
     return valid.view(torch.uint8) if valid.dtype == torch.bool else (valid != 0).view(torch.uint8)
 
 
+def _validity(valid_faces, face_normals_z, dtype):
+    """(uint8 valid mask, face_normals_z for the in-kernel `>= 0` test): exactly one is used."""
+    if valid_faces is not None or face_normals_z is None:
+        return _valid_u8(valid_faces), None
+    if face_normals_z.dtype != dtype:  # the in-kernel test reads the tensor dtype
+        return _valid_u8(face_normals_z >= 0), None
+    return None, face_normals_z.contiguous()
+
+
 def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_features, valid_faces, multiplier,
-                      eps):
-    """-> interpolated_features (B,H,W,D), face_idx (B,H,W) original index, output_weights (B,H,W,3)."""
+                      eps, face_normals_z=None):
+    """-> interpolated_features (B,H,W,D), face_idx (B,H,W) original index, output_weights (B,H,W,3).
+    With ``valid_faces`` None and ``face_normals_z`` given, valid = face_normals_z >= 0 in-kernel."""
     func = 'rasterize'
     N.require_gpu(func, face_vertices_z)
     B, F = face_vertices_z.shape[:2]
@@ -37,7 +47,7 @@ def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_
     fvz = face_vertices_z.contiguous()
     fvi = face_vertices_image.contiguous()
     feat = face_features.contiguous()
-    valid = _valid_u8(valid_faces)
+    valid, fnz = _validity(valid_faces, face_normals_z, dtype)
     feats = torch.empty((B, height, width, D), dtype=dtype, device=dev)
     idx = torch.empty((B, height, width), dtype=torch.long, device=dev)
     w = torch.empty((B, height, width, 3), dtype=dtype, device=dev)
@@ -47,29 +57,31 @@ def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_
     with torch.cuda.device(dev), N.timed('dibr_rasterize_forward', dev):
         N.check(lib.kl_dibr_rasterize_forward(
             N.dtype_code(dtype), height, width, B, F, D, N.ptr(fvz), N.ptr(fvi), N.ptr(feat), N.ptr(valid),
-            float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w), N.ptr(ws), nbytes, N.stream_of(dev)),
+            N.ptr(fnz), float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w), N.ptr(ws), nbytes, N.stream_of(dev)),
             func)
     return feats, idx, w
 
 
-def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_features, valid_faces, multiplier, eps):
-    """Gather backward; valid_faces / multiplier must be the forward's."""
+def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_features, valid_faces, multiplier, eps,
+                       face_normals_z=None, scratch=None):
+    """Gather backward; valid_faces / face_normals_z / multiplier must be the forward's.
+    ``scratch``: the zeroed int32 of a compact soft-mask state (see soft_mask_forward_compact)."""
     func = 'rasterize backward'
     B, H, W, D = grad.shape
     F = face_vertices_image.shape[1]
     dev = face_vertices_image.device
     g_img = torch.empty_like(face_vertices_image)
     g_feat = torch.empty_like(face_features)
-    valid = _valid_u8(valid_faces)
+    valid, fnz = _validity(valid_faces, face_normals_z, face_vertices_image.dtype)
     lib = N.lib()
     nbytes = lib.kl_dibr_rasterize_workspace_bytes(B, H, W, F)
     ws = _ws(nbytes, dev)
     with torch.cuda.device(dev), N.timed('dibr_rasterize_backward', dev):
         N.check(lib.kl_dibr_rasterize_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, N.ptr(grad.contiguous()), N.ptr(face_idx),
-            N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), N.ptr(valid), float(multiplier),
-            float(eps), N.ptr(g_img),
-            N.ptr(g_feat), N.ptr(ws), nbytes, N.stream_of(dev)), func)
+            N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), N.ptr(valid), N.ptr(fnz),
+            float(multiplier), float(eps), N.ptr(g_img), N.ptr(g_feat), N.ptr(scratch), N.ptr(ws), nbytes,
+            N.stream_of(dev)), func)
     return g_img, g_feat
 
 
@@ -117,4 +129,68 @@ def soft_mask_backward(grad, mask, sel, prob, cidx, ctype, face_vertices_image, 
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, K, N.ptr(grad.contiguous()), N.ptr(mask),
             N.ptr(sel), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(hits), N.ptr(face_vertices_image), float(sigmainv),
             float(multiplier), N.ptr(g), N.stream_of(dev)), func)
+    return g
+
+
+class SoftMaskState:
+    """The compact saved state of the soft mask (softtile.hip): per-pixel filled-slot
+    counts, the per-hit records, the per-row-segment hit totals and the zeroed int32
+    scratch word."""
+    __slots__ = ('hits', 'rec_face', 'rec_prob', 'seg_tot', 'scratch', 'knum')
+
+    def __init__(self, hits, rec_face, rec_prob, seg_tot, scratch, knum):
+        self.hits, self.rec_face, self.rec_prob = hits, rec_face, rec_prob
+        self.seg_tot, self.scratch, self.knum = seg_tot, scratch, knum
+
+    def tensors(self):
+        return self.hits, self.rec_face, self.rec_prob, self.seg_tot, self.scratch
+
+
+def soft_mask_forward_compact(face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier):
+    """face_vertices_image UNSCALED -> soft_mask (B,H,W), SoftMaskState.  knum <= 255."""
+    func = 'dibr_soft_mask'
+    N.require_gpu(func, face_vertices_image, selected_face_idx)
+    fvi = face_vertices_image.contiguous()
+    sel = selected_face_idx.contiguous()
+    B, F = fvi.shape[:2]
+    H, W = sel.shape[1:]
+    dev = fvi.device
+    dtype = fvi.dtype
+    if dtype not in (torch.float32, torch.float64):
+        raise RuntimeError(f'"{func}" not implemented for {dtype}')
+    K = int(knum)
+    lib = N.lib()
+    mask = torch.empty((B, H, W), dtype=dtype, device=dev)
+    hits = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
+    nrec = lib.kl_soft_mask_compact_records(B, H, W, K)
+    rec_face = torch.empty(max(nrec, 1), dtype=torch.int32, device=dev)
+    rec_prob = torch.empty(max(nrec, 1), dtype=dtype, device=dev)
+    seg_tot = torch.empty(max(lib.kl_soft_mask_compact_segments(B, H, W), 1), dtype=torch.int32, device=dev)
+    scratch = torch.empty(1, dtype=torch.int32, device=dev)
+    nbytes = lib.kl_soft_mask_compact_workspace_bytes(B, H, W, F)
+    ws = _ws(nbytes, dev)
+    with torch.cuda.device(dev), N.timed('dibr_soft_mask_forward', dev):
+        N.check(lib.kl_dibr_soft_mask_forward_compact(
+            N.dtype_code(dtype), B, H, W, F, K, N.ptr(fvi), N.ptr(sel), float(sigmainv), float(boxlen * multiplier),
+            float(multiplier), N.ptr(mask), N.ptr(hits), N.ptr(rec_face), N.ptr(rec_prob), N.ptr(seg_tot),
+            N.ptr(scratch), N.ptr(ws), nbytes, N.stream_of(dev)), func)
+    return mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, scratch, K)
+
+
+def soft_mask_backward_compact(grad, mask, state, face_vertices_image, sigmainv, multiplier, out=None):
+    """-> grad_face_vertices_image; with ``out`` the terms are added onto it (returned)."""
+    func = 'dibr_soft_mask backward'
+    B, F = face_vertices_image.shape[:2]
+    H, W = mask.shape[1:]
+    dev = face_vertices_image.device
+    g = out if out is not None else torch.empty_like(face_vertices_image)
+    lib = N.lib()
+    nbytes = lib.kl_soft_mask_compact_bwd_workspace_bytes(B, H, W, state.knum)
+    ws = _ws(nbytes, dev)
+    with torch.cuda.device(dev), N.timed('dibr_soft_mask_backward', dev):
+        N.check(lib.kl_dibr_soft_mask_backward_compact(
+            N.dtype_code(face_vertices_image.dtype), B, H, W, F, state.knum, N.ptr(grad.contiguous()), N.ptr(mask),
+            N.ptr(state.hits), N.ptr(state.rec_face), N.ptr(state.rec_prob), N.ptr(state.seg_tot),
+            N.ptr(face_vertices_image), float(sigmainv), float(multiplier), N.ptr(g), 1 if out is not None else 0,
+            N.ptr(state.scratch), N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return g

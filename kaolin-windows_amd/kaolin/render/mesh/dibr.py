@@ -10,28 +10,86 @@ __all__ = ['dibr_soft_mask', 'dibr_rasterization']
 
 class DibrSoftMaskCuda(Function):
     """dibr.py:27-73 on the fused HIP path: ``* multiplier`` and the enlarged bboxes are
-    evaluated in-kernel; the UNSCALED face_vertices_image is saved for backward."""
+    evaluated in-kernel; the UNSCALED face_vertices_image is saved for backward.
+
+    For knum <= 255 the saved state is compact (softtile.hip): per-pixel filled-slot counts
+    and one record per filled slot, instead of the reference's four (B,H,W,knum) slot
+    tensors -- the returned soft mask and the gradient are the same."""
 
     @staticmethod
     def forward(ctx, face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier):
         face_vertices_image = face_vertices_image.contiguous()
         selected_face_idx = selected_face_idx.contiguous()
-        soft_mask, close_face_prob, close_face_idx, close_face_dist_type, hits = _fused.soft_mask_forward(
-            face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier, with_hits=True)
         ctx.multiplier = multiplier
         ctx.sigmainv = sigmainv
+        ctx.compact = 0 <= int(knum) <= 255
+        if ctx.compact:
+            soft_mask, state = _fused.soft_mask_forward_compact(face_vertices_image, selected_face_idx, sigmainv,
+                                                                boxlen, knum, multiplier)
+            ctx.knum = state.knum
+            ctx.save_for_backward(soft_mask, face_vertices_image, *state.tensors())
+            return soft_mask
+        soft_mask, close_face_prob, close_face_idx, close_face_dist_type, hits = _fused.soft_mask_forward(
+            face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier, with_hits=True)
         ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, close_face_prob, close_face_idx,
                               close_face_dist_type, hits)
         return soft_mask
 
     @staticmethod
     def backward(ctx, grad_soft_mask):
+        if ctx.compact:
+            soft_mask, face_vertices_image, *st = ctx.saved_tensors
+            state = _fused.SoftMaskState(*st, ctx.knum)
+            grad_face_vertices_image = _fused.soft_mask_backward_compact(
+                grad_soft_mask, soft_mask, state, face_vertices_image, ctx.sigmainv, ctx.multiplier)
+            return grad_face_vertices_image, None, None, None, None, None
         soft_mask, face_vertices_image, selected_face_idx, close_face_prob, close_face_idx, close_face_dist_type, \
             hits = ctx.saved_tensors
         grad_face_vertices_image = _fused.soft_mask_backward(
             grad_soft_mask, soft_mask, selected_face_idx, close_face_prob, close_face_idx, close_face_dist_type,
             face_vertices_image, ctx.sigmainv, ctx.multiplier, hits)
         return grad_face_vertices_image, None, None, None, None, None
+
+
+class DibrRasterizationCuda(Function):
+    """dibr_rasterization (dibr.py:119-209) as one autograd node: rasterize with
+    valid = face_normals_z >= 0 evaluated in-kernel, then the compact soft mask on its
+    face index.  The backward runs the rasterizer's gather (which writes every face's
+    gradient) and adds the soft-mask terms onto it -- no zero fill and no separate sum of
+    the two gradients.  Outputs and gradients equal rasterize + dibr_soft_mask's."""
+
+    @staticmethod
+    def forward(ctx, height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z, sigmainv,
+                boxlen, knum, multiplier, eps):
+        face_vertices_image = face_vertices_image.contiguous()
+        face_features = face_features.contiguous()
+        face_normals_z = face_normals_z.detach().contiguous()
+        feats, face_idx, weights = _fused.rasterize_forward(height, width, face_vertices_z, face_vertices_image,
+                                                            face_features, None, multiplier, eps,
+                                                            face_normals_z=face_normals_z)
+        soft_mask, state = _fused.soft_mask_forward_compact(face_vertices_image, face_idx, sigmainv, boxlen, knum,
+                                                            multiplier)
+        ctx.mark_non_differentiable(face_idx)
+        ctx.sigmainv, ctx.multiplier, ctx.eps, ctx.knum = sigmainv, multiplier, eps, state.knum
+        ctx.save_for_backward(face_idx, weights, face_vertices_image, face_features, face_normals_z, soft_mask,
+                              *state.tensors())
+        return feats, soft_mask, face_idx
+
+    @staticmethod
+    def backward(ctx, grad_feats, grad_soft_mask, grad_face_idx):
+        face_idx, weights, fvi, feat, fnz, soft_mask, *st = ctx.saved_tensors
+        state = _fused.SoftMaskState(*st, ctx.knum)
+        scratch = state.scratch
+        if grad_feats is None:
+            grad_feats = torch.zeros(face_idx.shape + (feat.shape[-1],), dtype=feat.dtype, device=feat.device)
+        g_img, g_feat = _fused.rasterize_backward(grad_feats, face_idx, weights, fvi, feat, None, ctx.multiplier,
+                                                  ctx.eps, face_normals_z=fnz, scratch=scratch)
+        if grad_soft_mask is not None:
+            _fused.soft_mask_backward_compact(grad_soft_mask, soft_mask, state, fvi, ctx.sigmainv, ctx.multiplier,
+                                              out=g_img)
+        else:
+            scratch.zero_()
+        return None, None, None, g_img, g_feat, None, None, None, None, None, None
 
 
 def dibr_soft_mask(face_vertices_image, selected_face_idx, sigmainv=7000, boxlen=0.02, knum=30, multiplier=1000.):
@@ -45,8 +103,14 @@ def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face
                        sigmainv=7000, boxlen=0.02, knum=30, multiplier=None, eps=None, rast_backend='cuda'):
     r"""DIB-R renderer: rasterize(valid = face_normals_z >= 0) + dibr_soft_mask.
     Returns (features, soft_mask, face_idx) as dibr.py:119-209."""
+    _multiplier = 1000. if multiplier is None else multiplier
+    _eps = 1e-8 if eps is None else eps
+    if (rast_backend in ('cuda', 'hip') and not isinstance(face_features, (list, tuple))
+            and face_features.shape[-1] <= 8 and 0 <= int(knum) <= 255
+            and face_vertices_image.dtype in (torch.float32, torch.float64)):
+        return DibrRasterizationCuda.apply(height, width, face_vertices_z, face_vertices_image, face_features,
+                                           face_normals_z, sigmainv, boxlen, knum, _multiplier, _eps)
     interpolated_features, face_idx = rasterize(height, width, face_vertices_z, face_vertices_image, face_features,
                                                 face_normals_z >= 0., multiplier, eps, rast_backend)
-    _multiplier = 1000. if multiplier is None else multiplier
     soft_mask = dibr_soft_mask(face_vertices_image, face_idx, sigmainv, boxlen, knum, _multiplier)
     return interpolated_features, soft_mask, face_idx

@@ -35,19 +35,17 @@ def main():
     H, W = inp['H'], inp['W']
     valid = inp['fnz'] >= 0
     feats, idx, w = _fused.rasterize_forward(H, W, inp['fvz'], inp['fvi'], inp['feat'], valid, 1000., 1e-8)
-    mask, prob, cidx, ctype, hits = _fused.soft_mask_forward(inp['fvi'], idx, 7000., 0.02, 30, 1000., with_hits=True)
+    mask, state = _fused.soft_mask_forward_compact(inp['fvi'], idx, 7000., 0.02, 30, 1000.)
     gm = inp['g_mask']
     ops = {
         'rasterize_forward': lambda: _fused.rasterize_forward(H, W, inp['fvz'], inp['fvi'], inp['feat'], valid,
                                                               1000., 1e-8),
-        'soft_mask_forward': lambda: _fused.soft_mask_forward(inp['fvi'], idx, 7000., 0.02, 30, 1000.,
-                                                              with_hits=True),
-        'soft_mask_backward': lambda: _fused.soft_mask_backward(gm, mask, idx, prob, cidx, ctype, inp['fvi'], 7000.,
-                                                                1000., hits),
+        'soft_mask_forward': lambda: _fused.soft_mask_forward_compact(inp['fvi'], idx, 7000., 0.02, 30, 1000.),
+        'soft_mask_backward': lambda: _fused.soft_mask_backward_compact(gm, mask, state, inp['fvi'], 7000., 1000.),
         'rasterize_backward': lambda: _fused.rasterize_backward(inp['g_feat'], idx, w, inp['fvi'], inp['feat'],
                                                                 valid, 1000., 1e-8),
     }
-    flags = [int(f) for f in os.environ.get('ABLATE_FLAGS', '0,1,2,4').split(',')]
+    flags = [int(f) for f in os.environ.get('ABLATE_FLAGS', '0,1,2,4,6,7').split(',')]
     for name, fn in ops.items():
         row = []
         for f in flags:

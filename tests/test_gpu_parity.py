@@ -363,6 +363,127 @@ def test_dibr_deterministic_forward(kal):
         assert torch.equal(a, b)
 
 
+# ------------------------------------------------- compact soft-mask state (fused path)
+def _decode_compact(state, H, W, K):
+    """The compact records back into the reference's (B,H,W,K) slot tensors."""
+    hits = A(state.hits).astype(np.int64)
+    B = hits.shape[0]
+    tx = (W + 63) // 64
+    rf = A(state.rec_face).view(np.uint32)
+    rp = A(state.rec_prob)
+    idx = np.full((B, H, W, K), -1, np.int64)
+    typ = np.zeros((B, H, W, K), np.uint8)
+    prob = np.zeros((B, H, W, K), rp.dtype)
+    for b in range(B):
+        for j in range(H):
+            for t in range(tx):
+                seg = (b * H + j) * tx + t
+                base = seg * 64 * K
+                e = 0
+                for i in range(t * 64, min(W, t * 64 + 64)):
+                    for k in range(hits[b, j, i]):
+                        r = int(rf[base + e])
+                        idx[b, j, i, k] = r & 0x0fffffff
+                        typ[b, j, i, k] = r >> 28
+                        prob[b, j, i, k] = rp[base + e]
+                        e += 1
+    return idx, typ, prob
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('K', [30, 8, 1])
+def test_soft_mask_compact_vs_oracle(kal, dtype, K):
+    """Compact fused state: mask bit-exact to the _C path, the records decode to the
+    oracle's slots exactly (idx, type) / 1e-6 (prob), gradients 1e-5 -- on adversarial faces."""
+    from kaolin import _fused
+    z, v, f = _adversarial_faces(dtype, seed=6)
+    _, sel = kal.render.mesh.rasterize(97, 130, T(z), T(v), T(f))
+    m, box, sig = 1000., 0.03, 7000.
+    mask, state = _fused.soft_mask_forward_compact(T(v), sel, sig, box, K, m)
+    fm = v * v.dtype.type(m)
+    pad = v.dtype.type(box * m)
+    bb = np.concatenate([fm.min(-2) - pad, fm.max(-2) + pad], -1)
+    om, op, oi, ot = orc.dibr_soft_mask_forward(fm, bb, A(sel), sig, K, m)
+    np.testing.assert_allclose(A(mask), om, rtol=1e-6, atol=1e-7)
+    r1 = kal._C.render.mesh.dibr_soft_mask_forward_cuda(T(fm), T(bb), sel, sig, K, m)
+    assert np.array_equal(A(mask), A(r1[0]), equal_nan=True)  # NaN where a face has a NaN vertex
+    assert np.array_equal(A(state.hits), (oi >= 0).sum(-1))
+    idx, typ, prob = _decode_compact(state, 97, 130, K)
+    assert np.array_equal(idx, oi)
+    assert np.array_equal(typ, ot)
+    np.testing.assert_allclose(prob, op, rtol=1e-6, atol=1e-7)
+    grad = torch.rand_like(mask)
+    ogi = orc.dibr_soft_mask_backward(A(grad), om, A(sel), op, oi, ot, fm, sig, m)
+    g1 = _fused.soft_mask_backward_compact(grad, mask, state, T(v), sig, m)
+    fin = np.isfinite(ogi)
+    atol = max(1e-5, 4 * np.finfo(ogi.dtype).eps * np.abs(ogi[fin]).max()) if fin.any() else 1e-5
+    np.testing.assert_allclose(A(g1)[fin], ogi[fin], rtol=1e-5, atol=atol)
+    assert int(state.scratch.item()) == 0
+
+
+@pytest.mark.parametrize('which', ['both', 'features', 'mask'])
+def test_dibr_rasterization_fused_grads_vs_oracle(kal, which):
+    """The single-node dibr_rasterization backward (gather + soft terms added in place)
+    against the oracle's rasterize_backward + dibr_soft_mask_backward, on the bench mesh."""
+    import bench
+    inp = bench.dibr_inputs([0.3, 2.0], DEV, H=96, W=128)
+    fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+    a = fvi.clone().requires_grad_(True)
+    b = feat.clone().requires_grad_(True)
+    feats, mask, idx = kal.render.mesh.dibr_rasterization(96, 128, fvz, a, b, fnz, 7000, 0.02, 30, 1000, 1e-8)
+    gf = torch.rand_like(feats)
+    gm = torch.rand_like(mask)
+    outs, grads = ([feats, mask], [gf, gm]) if which == 'both' else \
+        (([feats], [gf]) if which == 'features' else ([mask], [gm]))
+    torch.autograd.backward(outs, grads, retain_graph=True)
+    of, oi, ow = orc.rasterize(96, 128, A(fvz), A(fvi), A(feat), valid_faces=A(fnz >= 0))
+    assert np.array_equal(A(idx), oi) and np.array_equal(A(feats), of)
+    fm = A(fvi) * np.float32(1000.)
+    bb = np.concatenate([fm.min(-2) - np.float32(20.), fm.max(-2) + np.float32(20.)], -1)
+    om, op, oci, oct_ = orc.dibr_soft_mask_forward(fm, bb, oi, 7000., 30, 1000.)
+    np.testing.assert_allclose(A(mask), om, rtol=1e-6, atol=1e-7)
+    gi = np.zeros(fm.shape, np.float32)
+    gfe = np.zeros(A(feat).shape, np.float32)
+    if which in ('both', 'features'):
+        gi_r, gfe = orc.rasterize_backward(A(gf), oi, ow, A(fvi), A(feat), 1e-8)
+        gi = gi + gi_r
+    if which in ('both', 'mask'):
+        gi = gi + orc.dibr_soft_mask_backward(A(gm), om, oi, op, oci, oct_, fm, 7000., 1000.)
+    atol = max(1e-5, 4 * np.finfo(np.float32).eps * np.abs(gi).max())
+    np.testing.assert_allclose(A(a.grad), gi, rtol=1e-5, atol=atol)
+    np.testing.assert_allclose(A(b.grad), gfe, rtol=1e-5, atol=1e-5)
+    # a second backward through the retained graph gives the same gradients again
+    g1 = a.grad.clone()
+    a.grad = None
+    torch.autograd.backward(outs, grads)
+    np.testing.assert_allclose(A(a.grad), A(g1), rtol=1e-5, atol=atol)
+
+
+def test_dibr_bench_full_size_fused_equals_C_chain(kal):
+    """cfg3 at full size (4 views, 512^2, 50k faces): the fused single-node path's
+    outputs equal the reference-contract chain (packed _C rasterizer + _C soft mask)
+    exactly; gradients agree to float summation order."""
+    import bench
+    inp = bench.dibr_inputs([0.0, 1.5707963, 3.1415927, 4.712389], DEV)
+    fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+    a1, b1 = fvi.clone().requires_grad_(True), feat.clone().requires_grad_(True)
+    f1, m1, i1 = kal.render.mesh.dibr_rasterization(512, 512, fvz, a1, b1, fnz)
+    (f1 * inp['g_feat']).sum().add((m1 * inp['g_mask']).sum()).backward()
+    a2, b2 = fvi.clone().requires_grad_(True), feat.clone().requires_grad_(True)
+    f2, i2 = kal.render.mesh.rasterize(512, 512, fvz, a2, b2, fnz >= 0, backend='cuda_packed')
+    fm = (a2 * 1000.)
+    bb = torch.cat([fm.min(-2)[0] - 20., fm.max(-2)[0] + 20.], -1).contiguous()
+    m2 = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm.detach().contiguous(), bb.detach(), i2, 7000., 30,
+                                                        1000.)[0]
+    assert torch.equal(f1, f2) and torch.equal(i1, i2) and torch.equal(m1, m2)
+    sm = kal.render.mesh.dibr_soft_mask(a2, i2, 7000, 0.02, 30, 1000.)
+    assert torch.equal(sm, m2)
+    (f2 * inp['g_feat']).sum().add((sm * inp['g_mask']).sum()).backward()
+    scale = float(a2.grad.abs().max())
+    torch.testing.assert_close(a1.grad, a2.grad, rtol=1e-4, atol=1e-5 * max(1., scale))
+    torch.testing.assert_close(b1.grad, b2.grad, rtol=1e-4, atol=1e-5)
+
+
 # ------------------------------------------------------------ point_to_mesh
 def test_p2m_kat(kal, golden):
     g = golden('p2m.npz')
