@@ -101,6 +101,30 @@ __device__ __forceinline__ double bcast(double v, int src) {
   return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
 }
 
+// Exclusive prefix sum over a workgroup (<= 1024 threads): wave scans with shuffles, then
+// the wave totals in `s_wave` (>= 16 ints of LDS).  Returns the thread's exclusive prefix;
+// *total gets the workgroup sum.  Every thread must call it (two barriers).
+__device__ __forceinline__ int block_exclusive_scan(int v, int *s_wave, int *total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) s_wave[wid] = inc;
+  __syncthreads();
+  int before = 0, all = 0;
+  for (int w = 0; w < nw; w++) {
+    const int t = s_wave[w];
+    before += w < wid ? t : 0;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + inc - v;
+}
+
 template <typename T>
 __device__ __forceinline__ T kl_exp(T x);
 template <>

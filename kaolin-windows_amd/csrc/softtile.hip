@@ -38,51 +38,52 @@ constexpr int ST_LIST_CAP = 1024;  // face-list entries per workgroup (8 B each)
 constexpr int ORD_BUCKETS = 32;
 
 // Heaviest-first tile order: counting sort of the tiles on floor(log2(count + 1)) of their
-// candidate-chunk counts (set bits of the tile's bitmap words), descending.  One thread
-// per tile counts; the workgroup histograms are summed in `ghist`; the last workgroup to
-// finish (the `gdone` ticket) scans the histogram and scatters the order.  ghist / gdone
-// are zeroed with the bitmap.  The scratch int of the compact state is zeroed here too.
-__global__ void __launch_bounds__(256) tile_order_kernel(const uint32_t *__restrict__ bitmap, int words, int nt,
-                                                         uint8_t *__restrict__ bk, int *__restrict__ ghist,
-                                                         int *__restrict__ gdone, int32_t *__restrict__ order,
-                                                         int *__restrict__ scratch) {
+// candidate-chunk counts (set bits of the tile's bitmap words), descending.  Two kernels:
+// one wave per tile counts and adds to the bucket histogram `ghist` (zeroed with the
+// bitmap); one workgroup then scans the histogram and scatters the order (a kernel
+// boundary instead of a per-workgroup release fence).  The scratch int of the compact
+// state is zeroed here too.
+__global__ void __launch_bounds__(256) tile_bucket_kernel(const uint32_t *__restrict__ bitmap, int words, int nt,
+                                                          uint8_t *__restrict__ bk, int *__restrict__ ghist,
+                                                          int *__restrict__ scratch) {
   __shared__ int hist[ORD_BUCKETS];
-  __shared__ int last;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (threadIdx.x < ORD_BUCKETS) hist[threadIdx.x] = 0;
   if (threadIdx.x == 0 && blockIdx.x == 0 && scratch) *scratch = 0;
   __syncthreads();
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int t = blockIdx.x * (blockDim.x >> 6) + wid;  // one wave per tile
   if (t < nt) {
     const uint32_t *w = bitmap + (size_t)t * words;
     unsigned n = 0;
-    int k = 0;
-    for (; k + 4 <= words; k += 4) n += __popc(w[k]) + __popc(w[k + 1]) + __popc(w[k + 2]) + __popc(w[k + 3]);
-    for (; k < words; k++) n += __popc(w[k]);
-    const int b = 31 - __clz(n + 1u);
-    bk[t] = (uint8_t)b;
-    atomicAdd(&hist[b], 1);
-  }
-  __syncthreads();
-  if (threadIdx.x < ORD_BUCKETS && hist[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], hist[threadIdx.x]);
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(gdone, 1) == (int)gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
-      const int c = atomicAdd(&ghist[q], 0);
-      hist[q] = s;
-      s += c;
+    for (int k = lane; k < words; k += 64) n += __popc(w[k]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+    if (lane == 0) {
+      const int b = 31 - __clz(n + 1u);
+      bk[t] = (uint8_t)b;
+      atomicAdd(&hist[b], 1);
     }
   }
   __syncthreads();
-  for (int u = threadIdx.x; u < nt; u += blockDim.x) {
-    const int b = __builtin_nontemporal_load(&bk[u]);
-    order[atomicAdd(&hist[b], 1)] = u;
+  if (threadIdx.x < ORD_BUCKETS && hist[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], hist[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *__restrict__ bk, const int *__restrict__ ghist,
+                                                          int nt, int32_t *__restrict__ order, int identity) {
+  __shared__ int base[ORD_BUCKETS];
+  if (identity) {  // dev ablation: grid order
+    for (int u = threadIdx.x; u < nt; u += blockDim.x) order[u] = u;
+    return;
   }
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
+      base[q] = s;
+      s += ghist[q];
+    }
+  }
+  __syncthreads();
+  for (int u = threadIdx.x; u < nt; u += blockDim.x) order[atomicAdd(&base[bk[u]], 1)] = u;
 }
 
 // Lane exchange v <- v[lane ^ S] with cross-lane VALU ops (gfx950 permlane swaps, DPP)
@@ -533,7 +534,7 @@ constexpr int SB_PIECE = 512;
 
 __global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restrict__ seg_tot, BinGeom g,
                                                              int2 *__restrict__ items, int *__restrict__ ctl) {
-  __shared__ int s_sum[1024];
+  __shared__ int s_wave[16];
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   int carry = 0;
   for (int t0 = 0; t0 < nt; t0 += blockDim.x) {
@@ -541,25 +542,21 @@ __global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restri
     int np = 0;
     if (t < nt) {
       const int tx = t % g.tiles_x, ty = (t / g.tiles_x) % g.tiles_y, b = t / (g.tiles_x * g.tiles_y);
-      int tot = 0;
-      for (int r = 0; r < TILE_H; r++) {
+      int v[TILE_H];
+#pragma unroll
+      for (int r = 0; r < TILE_H; r++) {  // the tile's row totals, loads in flight together
         const int j = ty * TILE_H + r;
-        if (j < g.height) tot += seg_tot[((size_t)b * g.height + j) * g.tiles_x + tx];
+        v[r] = j < g.height ? seg_tot[((size_t)b * g.height + j) * g.tiles_x + tx] : 0;
       }
+      int tot = 0;
+#pragma unroll
+      for (int r = 0; r < TILE_H; r++) tot += v[r];
       np = (tot + SB_PIECE - 1) / SB_PIECE;
     }
-    s_sum[threadIdx.x] = np;
-    __syncthreads();
-    for (int o = 1; o < (int)blockDim.x; o <<= 1) {
-      const int v = (int)threadIdx.x >= o ? s_sum[threadIdx.x - o] : 0;
-      __syncthreads();
-      s_sum[threadIdx.x] += v;
-      __syncthreads();
-    }
-    const int excl = carry + s_sum[threadIdx.x] - np;
+    int all;
+    const int excl = carry + block_exclusive_scan(np, s_wave, &all);
     for (int q = 0; q < np; q++) items[excl + q] = make_int2(t, q);
-    carry += s_sum[blockDim.x - 1];
-    __syncthreads();
+    carry += all;
   }
   if (threadIdx.x == 0) {
     ctl[0] = carry;
@@ -773,8 +770,16 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
   const int rc = launch_binning<T, SoftSrc<T>>(src, nullptr, F, g, m, bitmap, st, bbox, L.zero);
   if (rc) return rc;
   const int nt = g.batch * g.tiles_y * g.tiles_x;
-  hipLaunchKernelGGL(tile_order_kernel, dim3((unsigned)cdiv(nt, 256)), dim3(256), 0, st, (const uint32_t *)bitmap,
-                     g.words, nt, bk, ghist, ghist + ORD_BUCKETS, order, scratch);
+  const int identity = (g_dev_flags >> 12) & 1;  // dev ablation: no heaviest-first order
+  if (!identity) {
+    hipLaunchKernelGGL(tile_bucket_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)bitmap,
+                       g.words, nt, bk, ghist, scratch);
+    KL_CHECK_LAUNCH();
+  } else if (scratch) {
+    KL_CHECK_RC(fill_async(scratch, 0, sizeof(int), st));
+  }
+  hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt,
+                     order, identity);
   KL_CHECK_LAUNCH();
   SoftTileArgs<T> args{src,  bbox, sel,  bitmap,   order,    g,        F,         K,
                        sigmainv, m, mask, hits, rec_face, rec_prob, s.seg_tot, (uint64_t *)g_dev_debug};
