@@ -188,9 +188,9 @@ def op_bytes(name, inp, stats):
 
 # kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
 OP_KERNELS = {
-    'dibr_soft_mask_forward': ('bin_faces_kernel<float, kl::SoftSrc', 'tile_order_kernel', 'soft_tile_fwd_kernel<float',
-                               'soft_tile_eval_kernel<float'),
-    'dibr_soft_mask_backward': ('soft_tile_bwd_kernel<float',),
+    'dibr_soft_mask_forward': ('bin_faces_kernel<float, kl::SoftSrc', 'tile_bucket_kernel', 'tile_order_kernel',
+                               'soft_tile_fwd_kernel<float', 'soft_tile_eval_kernel<float'),
+    'dibr_soft_mask_backward': ('soft_bwd_plan_kernel', 'soft_tile_bwd_kernel<float'),
     'dibr_rasterize_forward': ('raster_vis_kernel<float, kl::RastSrc', 'raster_vis_big_kernel<float, kl::RastSrc',
                                'raster_resolve_kernel<float, kl::RastSrc'),
     'dibr_rasterize_backward': ('rasterize_bwd_gather_kernel<float', 'rasterize_bwd_bigface_kernel<float'),
@@ -227,12 +227,12 @@ def timed_loop(fn, steps, world):
 
 
 def cpu_baseline(inp, row_step):
-    """The C oracle (1 thread) on view 0, every `row_step`-th pixel row: rasterize fwd,
-    soft mask fwd, soft mask bwd, rasterize bwd."""
+    """The C oracle (1 thread) on all the rank's views, every `row_step`-th pixel row:
+    rasterize fwd, soft mask fwd, soft mask bwd, rasterize bwd."""
     import numpy as np
     from oracle import oracle as orc
     A = lambda t: t.detach().cpu().numpy()  # noqa: E731
-    fvz, fvi, feat, fnz = (A(inp[k][:1]) for k in ('fvz', 'fvi', 'feat', 'fnz'))
+    fvz, fvi, feat, fnz = (A(inp[k]) for k in ('fvz', 'fvi', 'feat', 'fnz'))
     H, W = inp['H'], inp['W']
     orc.lib().or_set_row_step(row_step)
     try:
@@ -245,7 +245,7 @@ def cpu_baseline(inp, row_step):
         dt = time.perf_counter() - t0
     finally:
         orc.lib().or_set_row_step(1)
-    rows = len(range(0, H, row_step))
+    rows = len(range(0, H, row_step)) * fvz.shape[0]
     return rows * W / dt / 1e6, rows * W, dt
 
 
@@ -274,7 +274,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--cpu-row-step', type=int, default=8)
+    ap.add_argument('--cpu-row-step', type=int, default=2)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-p2m', action='store_true')
     ap.add_argument('--eager', action='store_true', help='time the eager step only (no HIP graph capture)')
@@ -351,7 +351,10 @@ def main():
                        'parallelism': f'batch-sharded x{world} (RCCL all_gather of per-shard losses)'},
             'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(dom),
-                         'bytes_per_launch': dbytes, 'avg_launch_ms': round(ops_ms[dom], 4)},
+                         'bytes_per_launch': dbytes, 'avg_launch_ms': round(ops_ms[dom], 4),
+                         'note': 'algorithmic bytes of the compact soft-mask state (the reference layout would '
+                                 'move ' + str(op_bytes('dibr_soft_mask_forward_cuda', inp, stats)) + ' B per call); '
+                                 'the op is latency-bound, not HBM-bound (DESIGN.md section 5)'},
             'ops': ops_report,
             'workload_stats': stats,
             'mode': mode,
@@ -368,8 +371,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rate, npx, dt = cpu_baseline(inp, args.cpu_row_step)
         result['cpu_baseline'] = {'value': round(rate, 5), 'unit': 'Mpixels/s', 'cores': 1, 'kind': 'port',
-                                  'sample': f'C oracle, view 0, every {args.cpu_row_step}th row of 512x512 '
-                                            f'({npx} px, fwd+bwd, {dt:.1f} s)'}
+                                  'sample': f'C oracle, the {views_per_rank} views, every {args.cpu_row_step}th row of '
+                                            f'512x512 ({npx} px, fwd+bwd, {dt:.1f} s)'}
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
