@@ -162,6 +162,32 @@ __device__ __forceinline__ void axis_range(double vmin, double vmax, double s, i
   hi = (int)h;
 }
 
+// Sets chunk c's bit in every tile of mesh b that one of the wave's faces touches (the
+// lane's face covers tiles [tx0,tx1] x [ty0,ty1]; empty when tx0 > tx1).  Small unions
+// are walked by the wave with one atomicOr per tile, large ones per lane.
+__device__ __forceinline__ void bin_mark(const BinGeom &g, int b, int c, int lane, int tx0, int tx1, int ty0,
+                                         int ty1, uint32_t *__restrict__ bitmap) {
+  const bool has = tx0 <= tx1;
+  const int ux0 = wave_min(has ? tx0 : INT32_MAX), ux1 = wave_max(has ? tx1 : -1);
+  const int uy0 = wave_min(has ? ty0 : INT32_MAX), uy1 = wave_max(has ? ty1 : -1);
+  if (ux0 > ux1) return;
+  const uint32_t bit = 1u << (c & 31);
+  const size_t tile_base = (size_t)b * g.tiles_y * g.tiles_x;
+  const int area = (ux1 - ux0 + 1) * (uy1 - uy0 + 1);
+  if (area <= 256) {
+    for (int ty = uy0; ty <= uy1; ty++)
+      for (int tx = ux0; tx <= ux1; tx++) {
+        const uint64_t hit = ballot(has && tx0 <= tx && tx <= tx1 && ty0 <= ty && ty <= ty1);
+        if (hit && lane == 0)
+          atomicOr(&bitmap[(tile_base + (size_t)ty * g.tiles_x + tx) * g.words + (c >> 5)], bit);
+      }
+  } else if (has) {
+    for (int ty = ty0; ty <= ty1; ty++)
+      for (int tx = tx0; tx <= tx1; tx++)
+        atomicOr(&bitmap[(tile_base + (size_t)ty * g.tiles_x + tx) * g.words + (c >> 5)], bit);
+  }
+}
+
 // One wave per (mesh b, chunk c).  Mesh b owns faces [first(b), last(b)) of the source.
 // first_idx == nullptr => uniform meshes of `faces_per_mesh` faces.
 // bbox_out (optional): the face bboxes of the source, (N,4), for consumers that walk them.
@@ -206,25 +232,7 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *
       ty1 = iy1 / TILE_H;
     }
   }
-  const bool has = tx0 <= tx1;
-  const int ux0 = wave_min(has ? tx0 : INT32_MAX), ux1 = wave_max(has ? tx1 : -1);
-  const int uy0 = wave_min(has ? ty0 : INT32_MAX), uy1 = wave_max(has ? ty1 : -1);
-  if (ux0 > ux1) return;
-  const uint32_t bit = 1u << (c & 31);
-  const size_t tile_base = (size_t)b * g.tiles_y * g.tiles_x;
-  const int area = (ux1 - ux0 + 1) * (uy1 - uy0 + 1);
-  if (area <= 256) {
-    for (int ty = uy0; ty <= uy1; ty++)
-      for (int tx = ux0; tx <= ux1; tx++) {
-        const uint64_t hit = ballot(has && tx0 <= tx && tx <= tx1 && ty0 <= ty && ty <= ty1);
-        if (hit && lane == 0)
-          atomicOr(&bitmap[(tile_base + (size_t)ty * g.tiles_x + tx) * g.words + (c >> 5)], bit);
-      }
-  } else if (has) {
-    for (int ty = ty0; ty <= ty1; ty++)
-      for (int tx = tx0; tx <= tx1; tx++)
-        atomicOr(&bitmap[(tile_base + (size_t)ty * g.tiles_x + tx) * g.words + (c >> 5)], bit);
-  }
+  bin_mark(g, b, c, lane, tx0, tx1, ty0, ty1, bitmap);
 }
 
 // zero_bytes: bytes from `bitmap` zeroed first (0 = the bitmap's own g.bytes()).

@@ -19,6 +19,12 @@ extern int g_dev_flags;    // kl_dev_set_flags (ablation timing only; 0 in the p
 extern void *g_dev_debug;  // kl_dev_set_debug (per-wave stamps; nullptr in the product path)
 
 // shader-clock and 100 MHz wall-clock stamps for the dev timing buffer
+// Dev stamps (kl_dev_set_debug) are compiled in only with -DKL_DEV_STAMPS=1 (make STAMPS=1):
+// the bookkeeping costs registers even when the buffer is null.
+#ifndef KL_DEV_STAMPS
+#define KL_DEV_STAMPS 0
+#endif
+constexpr bool kDevStamps = KL_DEV_STAMPS != 0;
 __device__ __forceinline__ uint64_t stamp_clk() { return __builtin_readcyclecounter(); }
 __device__ __forceinline__ uint64_t stamp_wall() { return __builtin_amdgcn_s_memrealtime(); }
 // memset as a kernel launch on `st` (graph-capture friendly); returns a kl_status

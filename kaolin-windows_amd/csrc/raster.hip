@@ -28,6 +28,8 @@
 //                                   Valid whenever face_idx came from the forward (a face
 //                                   can only be selected inside its bbox).
 #include "soft_common.h"
+#include "tileorder.h"
+#include "tilewalk.h"
 
 namespace kl {
 
@@ -52,13 +54,13 @@ __device__ __forceinline__ void load_face(const Src &src, const T *__restrict__ 
 
 // The reference's per-(pixel, face) test, statement for statement: bbox reject, edge
 // functions, copysign(eps) normalisation, barycentric sign test.  true => (w0,w1,w2)
-// are the face's weights at the pixel centre (x0, y0).
+// are the face's weights at the pixel centre (x0, y0).  tri_weights is the part after
+// the bbox reject.
 template <typename T>
-__device__ __forceinline__ bool face_weights(const RastFace<T> &r, T x0, T y0, float eps, T &w0, T &w1, T &w2) {
-  if (x0 < r.xmin || x0 >= r.xmax || y0 < r.ymin || y0 >= r.ymax) return false;
-  const T aex = r.v[0] - x0, aey = r.v[1] - y0;
-  const T bex = r.v[2] - x0, bey = r.v[3] - y0;
-  const T cex = r.v[4] - x0, cey = r.v[5] - y0;
+__device__ __forceinline__ bool tri_weights(const T *v, T x0, T y0, float eps, T &w0, T &w1, T &w2) {
+  const T aex = v[0] - x0, aey = v[1] - y0;
+  const T bex = v[2] - x0, bey = v[3] - y0;
+  const T cex = v[4] - x0, cey = v[5] - y0;
   w0 = bex * cey - bey * cex;
   w1 = cex * aey - cey * aex;
   w2 = aex * bey - aey * bex;
@@ -68,6 +70,12 @@ __device__ __forceinline__ bool face_weights(const RastFace<T> &r, T x0, T y0, f
   w1 /= norm;
   w2 /= norm;
   return !(w0 < (T)0 || w1 < (T)0 || w2 < (T)0);
+}
+
+template <typename T>
+__device__ __forceinline__ bool face_weights(const RastFace<T> &r, T x0, T y0, float eps, T &w0, T &w1, T &w2) {
+  if (x0 < r.xmin || x0 >= r.xmax || y0 < r.ymin || y0 >= r.ymax) return false;
+  return tri_weights<T>(r.v, x0, y0, eps, w0, w1, w2);
 }
 
 template <typename T>
@@ -352,6 +360,490 @@ static int launch_rast_fwd(Src src, int H, int W, int B, int D, int64_t nfaces, 
   }
   hipLaunchKernelGGL((raster_resolve_kernel<T, Src>), dim3((unsigned)cdiv((int64_t)L.P, 256)), dim3(256), 0, st, src,
                      fvz, feat, first_idx, faces_per_mesh, B, H, W, D, m, eps, vb, out_feat, out_idx, out_w);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+// ---------------------------------------------------------------- tile forward (fused path)
+// One 512-thread workgroup per 64x8 pixel tile, one wave per row, one lane per pixel.
+// The tile's candidate chunks (bin bitmap) are expanded 8 chunks (512 faces) per step:
+// each wave loads one chunk's faces (vertices x m, depths, validity) -- the next step's
+// loads in flight while this step's are tested -- rejects invalid faces and those whose
+// bbox misses every pixel centre of the tile (exact row test, exact column interval), and
+// appends the rest in index order to an LDS list.  Each row then transposes the list's
+// pixel masks so that every pixel lane visits its own candidates in index order and runs
+// the reference's per-(pixel, face) loop body (rasterization_cuda.cu:95-171) verbatim:
+// bbox-passing faces, edge weights, sign test, depth, strict `z0 <= max_z0` fold.  So
+// the fold is the reference's, NaN depths included, with no atomics and no resolve pass.
+constexpr int RT_CAP = 512;  // list entries per step: one chunk per wave
+constexpr int RT_VS = 12;    // LDS stride of a list entry: 6 coordinates, 3 depths, pad
+
+// Exact pixel interval of one axis whose centres c pass the reference's bbox test
+// (!(c < vlo) && !(c >= vhi), rasterization_cuda.cu:101-104) in float arithmetic: an
+// index estimate corrected against the exact centre formula (monotone in the index).
+// x: c(k) = (T)(s * (2k + 1 - n)) increasing; y (flip): c(k) = (T)(s * (n - 2k - 1))
+// decreasing.  NaN bounds never reject.  Empty: a > b.
+template <typename T>
+__device__ __forceinline__ void exact_range(T vlo, T vhi, float s, float inv, int n, bool flip, int &a, int &b) {
+  if (!(vlo == vlo)) vlo = (T)-INFINITY;  // a NaN bound passes every centre, as -inf / +inf do
+  if (!(vhi == vhi)) vhi = (T)INFINITY;
+  auto c = [&](int k) -> T { return flip ? (T)(s * (float)(n - 2 * k - 1)) : (T)(s * (float)(2 * k + 1 - n)); };
+  auto est = [&](T v) -> int {  // index whose centre is near v, clamped to [0, n]
+    const float t = flip ? ((float)(n - 1) - (float)v * inv) * 0.5f : ((float)v * inv + (float)(n - 1)) * 0.5f;
+    if (!(t == t)) return 0;
+    return t <= 0.0f ? 0 : (t >= (float)n ? n : (int)t);
+  };
+  // P(k) monotone false -> true in k: first k with P (n if none)
+  auto first = [&](int e, auto P) {
+    while (e > 0 && P(e - 1)) e--;
+    while (e < n && !P(e)) e++;
+    return e;
+  };
+  if (!flip) {
+    a = first(est(vlo), [&](int k) { return !(c(k) < vlo); });
+    b = first(est(vhi), [&](int k) { return c(k) >= vhi; }) - 1;
+  } else {
+    a = first(est(vhi), [&](int k) { return !(c(k) >= vhi); });
+    b = first(est(vlo), [&](int k) { return c(k) < vlo; }) - 1;
+  }
+}
+
+// Face records written by raster_bin_kernel: vertices x m (6), depths (3), pad (3); and
+// the exact pixel ranges of the reference's bbox test (rasterization_cuda.cu:101-104),
+// x0 | x1 << 16 and y0 | y1 << 16, empty (1, 0) for invalid faces.
+constexpr int RT_REC = 12;
+
+// The reference's float pixel pitches (m / W, m / H) and their inverses (estimates only),
+// computed once on the host with the same float division.
+struct PixPitch {
+  float sx, sy, xinv, yinv;
+};
+
+// VMODE: 0 all faces valid, 1 valid mask, 2 face_normals_z >= 0.  All loads are issued
+// up front (clamped index, no branch around them) and the stores come last.
+template <typename T, int VMODE>
+__global__ void __launch_bounds__(256) raster_bin_kernel(RastSrc<T> src, const T *__restrict__ fvz, int F, BinGeom g,
+                                                         PixPitch pp, uint32_t *__restrict__ bitmap,
+                                                         T *__restrict__ rec, uint2 *__restrict__ rng) {
+  const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.y;
+  if (c >= g.chunks || c * 64 >= F) return;
+  const int fl = c * 64 + lane;
+  const bool live = fl < F;
+  const int64_t f = (int64_t)b * F + (live ? fl : F - 1);
+  T v[6], z[3];
+  src.verts(f, v);
+#pragma unroll
+  for (int q = 0; q < 3; q++) z[q] = fvz[f * 3 + q];
+  bool valid = live;
+  if constexpr (VMODE == 1) valid = valid && src.vmask[f] != 0;
+  if constexpr (VMODE == 2) valid = valid && src.nz[f] >= (T)0;
+  int ix0 = 1, ix1 = 0, iy0 = 1, iy1 = 0;
+  if (valid) {
+    const T xmin = tmin3(v[0], v[2], v[4]), ymin = tmin3(v[1], v[3], v[5]);
+    const T xmax = tmax3(v[0], v[2], v[4]), ymax = tmax3(v[1], v[3], v[5]);
+    exact_range(xmin, xmax, pp.sx, pp.xinv, g.width, false, ix0, ix1);
+    exact_range(ymin, ymax, pp.sy, pp.yinv, g.height, true, iy0, iy1);
+    if (ix0 > ix1 || iy0 > iy1) {
+      ix0 = iy0 = 1;
+      ix1 = iy1 = 0;
+    }
+  }
+  if (live) {
+    T *r = rec + f * RT_REC;
+#pragma unroll
+    for (int q = 0; q < 6; q++) r[q] = v[q];
+#pragma unroll
+    for (int q = 0; q < 3; q++) r[6 + q] = z[q];
+    rng[f] = make_uint2((uint32_t)ix0 | ((uint32_t)ix1 << 16), (uint32_t)iy0 | ((uint32_t)iy1 << 16));
+  }
+  const bool has = ix0 <= ix1;
+  bin_mark(g, b, c, lane, has ? ix0 / TILE_W : 1, has ? ix1 / TILE_W : 0, has ? iy0 / TILE_H : 1,
+           has ? iy1 / TILE_H : 0, bitmap);
+}
+
+template <typename T>
+struct RastTileArgs {
+  RastSrc<T> src;
+  const T *fvz;
+  const T *feat;
+  const uint32_t *bitmap;
+  const T *rec;
+  const uint2 *rng;
+  const int32_t *items;  // tileorder.h work items, heaviest first
+  const int *nitems;
+  BinGeom g;
+  int F, D;
+  float eps;
+  T *out_feat;
+  int64_t *out_idx;
+  T *out_w;
+  uint64_t *dbg;  // dev stamps (kl_dev_set_debug), 8 per wave, or nullptr
+};
+
+template <typename T>
+__global__ void __launch_bounds__(512) raster_tile_kernel(RastTileArgs<T> a) {
+  uint64_t *const dbg = kDevStamps ? a.dbg : nullptr;  // compiled out unless KL_DEV_STAMPS
+  constexpr int R = 8;  // waves per workgroup
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const BinGeom &g = a.g;
+  // the item: a tile, or one of 2^lg parts of its rows (heavy tiles); 2^lg waves share a row
+  if ((int)blockIdx.x >= *a.nitems) return;
+  const int32_t item = a.items[blockIdx.x];
+  const int tile = item & 0xffffff;
+  const int part = (item >> 24) & 15;
+  const int lg = (item >> 28) & 7;
+  ChunkSeq seq;
+  seq.init(a.bitmap + (size_t)tile * g.words, g.words, lane);
+  const int RG = R >> lg;     // rows of the workgroup
+  const int WPR = 1 << lg;    // waves per row
+  __shared__ uint32_t L_face[RT_CAP];
+  __shared__ uint32_t L_pack[RT_CAP];
+  __shared__ __align__(16) T L_v[RT_CAP * RT_VS];
+  __shared__ int s_cnt[R];
+  __shared__ int s_pre[R * 64];                   // f32 pair walk: entry width prefix << 8 | lo
+  __shared__ unsigned long long s_key[R * 64];    // f32 pair walk: per-pixel depth key
+  __shared__ unsigned long long s_nan[R];         // f32 pair walk: pixels that saw a NaN depth
+  const int r = wid >> lg;          // this wave's row of the workgroup
+  const int sub = wid & (WPR - 1);  // and its share of that row's pairs
+  if constexpr (sizeof(T) == 4) {
+    if ((int)threadIdx.x < RG * 64) s_key[threadIdx.x] = 0;
+    if ((int)threadIdx.x < RG) s_nan[threadIdx.x] = 0;
+    __syncthreads();
+  }
+  const int H = g.height, W = g.width;
+  const int tx = tile % g.tiles_x;
+  const int ty = (tile / g.tiles_x) % g.tiles_y;
+  const int b = tile / (g.tiles_x * g.tiles_y);
+  const int j0 = ty * TILE_H + part * RG;  // the workgroup's first row
+  const int j = j0 + r;
+  const int ibase = tx * TILE_W;
+  const int i = ibase + lane;
+  const bool px_valid = j < H && i < W;
+  const float m = a.src.m;
+  const float sx = m / (float)W, sy = m / (float)H;
+  const T x0 = (T)(sx * (float)(2 * i + 1 - W));               // == pix_x<T>(m, W, i)
+  const T y0 = (T)(sy * (float)(H - 2 * (j < H ? j : H - 1) - 1));  // == pix_y<T>(m, H, j)
+  const int64_t f0 = (int64_t)b * a.F;
+  const T *rec = a.rec + f0 * RT_REC;
+  const uint2 *rng = a.rng + f0;
+
+  T max_z0 = -INFINITY, mw0 = 0, mw1 = 0, mw2 = 0;
+  int win = -1;
+  uint64_t t0 = 0, w0s = 0, c_fill = 0, c_walk = 0, tq = 0, tr = 0;
+  uint64_t c_ph[5] = {0, 0, 0, 0, 0};
+  auto phase = [&](int k) {
+    if (dbg) {
+      const uint64_t t = stamp_clk();
+      c_ph[k] += t - tr;
+      tr = t;
+    }
+  };
+  int n_entries = 0, n_iters = 0, n_visits = 0;
+  if (dbg) {
+    t0 = stamp_clk();
+    w0s = stamp_wall();
+  }
+
+  // A step = one candidate chunk per wave.  Its face data is loaded a step ahead into
+  // alternating register sets (no copy between them, so the loads stay in flight while
+  // the current step is tested and walked).
+  struct Pref {
+    T v[9];
+    uint2 r;
+    int c;
+  };
+  int pos = 0;
+  bool more = false;
+  auto issue = [&](Pref &P) {
+    more = seq.at(pos, lane) >= 0;
+    P.c = more ? seq.at(pos + wid, lane) : -1;
+    pos += R;
+    // unconditional loads from a clamped index: a guarded load would be waited for at once
+    int fl = P.c * 64 + lane;
+    fl = fl < 0 ? 0 : (fl < a.F ? fl : a.F - 1);
+#pragma unroll
+    for (int q = 0; q < 9; q++) P.v[q] = rec[(size_t)fl * RT_REC + q];
+    P.r = rng[fl];
+  };
+  auto step = [&](Pref &cur, Pref &nxt) {
+    if (dbg) tq = tr = stamp_clk();
+    const int c = cur.c;
+    if (dbg) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      phase(4);
+    }
+    issue(nxt);
+    phase(0);
+    // the face's exact pixel ranges against this tile's rows and columns
+    const int fl = c * 64 + lane;
+    const int ix0 = (int)(cur.r.x & 0xffffu), ix1 = (int)(cur.r.x >> 16);
+    const int iy0 = (int)(cur.r.y & 0xffffu), iy1 = (int)(cur.r.y >> 16);
+    const int ya = max(iy0, j0) - j0, yb = min(iy1, j0 + RG - 1) - j0;
+    const uint32_t rows = ya <= yb ? ((2u << yb) - 1u) & ~((1u << ya) - 1u) : 0u;
+    const int lo = max(ix0 - ibase, 0), hi = min(ix1 - ibase, 63);
+    const bool keep = c >= 0 && fl < a.F && rows != 0 && lo <= hi;
+    const T *v = cur.v;
+    const uint64_t km = ballot(keep);
+    if (lane == 0) s_cnt[wid] = __popcll(km);
+    phase(1);
+    __syncthreads();
+    phase(2);
+    int pre = 0, len = 0;
+#pragma unroll
+    for (int w = 0; w < R; w++) {
+      const int cw = s_cnt[w];
+      pre += w < wid ? cw : 0;
+      len += cw;
+    }
+    if (keep) {
+      const int p = pre + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
+      L_face[p] = (uint32_t)fl;
+      L_pack[p] = (uint32_t)lo | ((uint32_t)hi << 6) | (rows << 12);
+#pragma unroll
+      for (int q = 0; q < 9; q++) L_v[p * RT_VS + q] = v[q];
+    }
+    __syncthreads();
+    phase(3);
+    n_entries += len;
+    if (dbg) {
+      const uint64_t t = stamp_clk();
+      c_fill += t - tq;
+      tq = t;
+    }
+    if constexpr (sizeof(T) == 4) {
+      // this row's (pixel, face) pairs, 64 list entries at a time, evaluated densely: an
+      // entry's pixels are the contiguous run [lo, hi], so pair t belongs to the entry whose
+      // exclusive width prefix is the last <= t.  Each pair ranks its depth in the pixel's
+      // LDS key (max depth, lowest index on ties: the reference's strict fold for non-NaN
+      // depths); a NaN depth flags the pixel for the sequential replay below.
+      for (int base = 0; base < len; base += 64) {
+        const int e = base + lane;
+        int lo = 0, wdt = 0;
+        if (e < len) {
+          const uint32_t pk = L_pack[e];
+          if ((pk >> (12 + r)) & 1u) {
+            lo = (int)(pk & 63u);
+            wdt = (int)((pk >> 6) & 63u) - lo + 1;
+          }
+        }
+        int inc = wdt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int u = __shfl_up(inc, o);
+          if (lane >= o) inc += u;
+        }
+        const int total = __shfl(inc, 63);
+        if (total == 0) continue;
+        s_pre[wid * 64 + lane] = ((inc - wdt) << 8) | lo;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        if (dbg) {
+          n_visits += wdt;
+          n_iters += (total + 63) >> 6;
+        }
+        for (int t = lane + 64 * sub; t < total; t += 64 * WPR) {
+          int q = 0;  // owner entry: last q with prefix <= t
+#pragma unroll
+          for (int stp = 32; stp > 0; stp >>= 1)
+            if ((s_pre[wid * 64 + q + stp] >> 8) <= t) q += stp;
+          const int pq = s_pre[wid * 64 + q];
+          const int pix = (pq & 255) + t - (pq >> 8);
+          const T *v = L_v + (base + q) * RT_VS;
+          const T xp = (T)(sx * (float)(2 * (ibase + pix) + 1 - W));
+          T w0, w1, w2;
+          if (!tri_weights<T>(v, xp, y0, a.eps, w0, w1, w2)) continue;
+          const float z0 = (float)(w0 * v[6] + w1 * v[7] + w2 * v[8]);
+          if (z0 != z0)
+            atomicOr(&s_nan[r], 1ull << pix);
+          else if (z0 != -INFINITY)
+            atomicMax(&s_key[r * 64 + pix],
+                      ((unsigned long long)order32(z0) << 32) | (unsigned long long)(~L_face[base + q]));
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      }
+    } else {
+    // this row's walk: 64 list entries at a time, transposed to per-pixel candidate masks
+    for (int base = 0; base < len; base += 64) {
+      const int e = base + lane;
+      uint64_t rm = 0;
+      if (e < len) {
+        const uint32_t pk = L_pack[e];
+        if ((pk >> (12 + r)) & 1u) {
+          const int lo = (int)(pk & 63u), hi = (int)((pk >> 6) & 63u);
+          rm = (~0ull >> (63 - hi)) & (~0ull << lo);
+        }
+      }
+      if (!ballot(rm != 0)) continue;
+      uint64_t cm = transpose64(rm, lane);
+      if (dbg) {
+        n_visits += __popcll(cm);
+        n_iters += wave_max(__popcll(cm));
+      }
+      while (cm) {
+        const int q = __builtin_ctzll(cm);
+        cm &= cm - 1;
+        const T *v = L_v + (base + q) * RT_VS;
+        T w0, w1, w2;
+        if (!tri_weights<T>(v, x0, y0, a.eps, w0, w1, w2)) continue;
+        const T z0 = w0 * v[6] + w1 * v[7] + w2 * v[8];
+        if (z0 <= max_z0) continue;
+        max_z0 = z0;
+        win = (int)L_face[base + q];
+        mw0 = w0;
+        mw1 = w1;
+        mw2 = w2;
+      }
+    }
+    }
+    if (dbg) c_walk += stamp_clk() - tq;
+    __syncthreads();  // the list is rewritten by the next step
+  };
+  Pref PA, PB;
+  issue(PA);
+  while (more) {
+    step(PA, PB);
+    if (!more) break;
+    step(PB, PA);
+  }
+  if (dbg && lane == 0) {
+    uint64_t *d = dbg + ((size_t)blockIdx.x * R + wid) * 8;
+    d[0] = t0;
+    d[1] = stamp_clk();
+    d[2] = w0s;
+    d[3] = stamp_wall();
+    d[4] = c_fill;
+    d[5] = c_walk;
+    d[6] = ((uint64_t)n_entries << 32) | (uint32_t)n_iters;
+    d[7] = ((uint64_t)(pos / R - 1) << 32) | (uint32_t)tile;
+  }
+  if (dbg) {
+    const int tv = n_visits;
+    const int sv = wave_max(tv);  // max visits of a lane
+    int sum = tv;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    if (lane == 0) dbg[(size_t)gridDim.x * R * 8 + ((size_t)blockIdx.x * R + wid) * 2] = (uint64_t)sum;
+    if (lane == 0) dbg[(size_t)gridDim.x * R * 8 + ((size_t)blockIdx.x * R + wid) * 2 + 1] = (uint64_t)sv;
+    if (lane == 0)
+      for (int k = 0; k < 5; k++) dbg[(size_t)gridDim.x * R * 10 + ((size_t)blockIdx.x * R + wid) * 5 + k] = c_ph[k];
+  }
+  if (!px_valid || sub != 0) return;  // the row's keys are complete: every step ends in a barrier
+  if constexpr (sizeof(T) == 4) {
+    const unsigned long long key = s_key[r * 64 + lane];
+    if ((s_nan[r] >> lane) & 1ull) {
+      // a NaN depth breaks the total order: replay the reference's fold over every face
+      for (int f = 0; f < a.F; f++) {
+        const uint2 rr = rng[f];  // exact bbox test (and validity)
+        if (i < (int)(rr.x & 0xffffu) || i > (int)(rr.x >> 16) || j < (int)(rr.y & 0xffffu) ||
+            j > (int)(rr.y >> 16))
+          continue;
+        const T *v = rec + (size_t)f * RT_REC;
+        T w0, w1, w2;
+        if (!tri_weights<T>(v, x0, y0, a.eps, w0, w1, w2)) continue;
+        const T z0 = w0 * v[6] + w1 * v[7] + w2 * v[8];
+        if (z0 <= max_z0) continue;
+        max_z0 = z0;
+        win = f;
+        mw0 = w0;
+        mw1 = w1;
+        mw2 = w2;
+      }
+    } else if (key != 0) {
+      win = (int)(~(uint32_t)key);
+      tri_weights<T>(rec + (size_t)win * RT_REC, x0, y0, a.eps, mw0, mw1, mw2);  // the arithmetic that ranked it
+    }
+  }
+  const size_t p = ((size_t)b * H + j) * W + i;
+  const int D = a.D;
+  a.out_idx[p] = win;
+  a.out_w[p * 3 + 0] = mw0;
+  a.out_w[p * 3 + 1] = mw1;
+  a.out_w[p * 3 + 2] = mw2;
+  if (win >= 0) {
+    const T *c = a.feat + (size_t)(f0 + win) * 3 * D;
+    for (int d = 0; d < D; d++) a.out_feat[p * D + d] = mw0 * c[d] + mw1 * c[D + d] + mw2 * c[2 * D + d];
+  } else {
+    for (int d = 0; d < D; d++) a.out_feat[p * D + d] = (T)0;
+  }
+}
+
+// workspace: bin bitmap | ghist (zeroed with the bitmap) | face records | pixel ranges |
+// tile buckets | work items | item count  (records sized for sizeof(T) <= 8)
+struct RastTileWs {
+  size_t off_hist, off_rec, off_rng, off_bk, off_items, off_n, bytes;
+  RastTileWs(const BinGeom &g, int B, int F, size_t tsize) {
+    const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
+    off_hist = g.bytes();
+    off_rec = (off_hist + ORD_BUCKETS * sizeof(int) + 255) & ~(size_t)255;
+    off_rng = off_rec + (((size_t)B * F * RT_REC * tsize + 255) & ~(size_t)255);
+    off_bk = (off_rng + (size_t)B * F * sizeof(uint2) + 255) & ~(size_t)255;
+    off_items = (off_bk + nt + 255) & ~(size_t)255;
+    off_n = off_items + nt * TILE_H * sizeof(int32_t);
+    bytes = off_n + sizeof(int);
+  }
+};
+inline size_t rast_tile_ws_bytes(int B, int H, int W, int F) {
+  return RastTileWs(make_bin_geom(B, H, W, F), B, F, sizeof(double)).bytes;
+}
+
+template <typename T>
+static int launch_rast_tile(RastSrc<T> src, int H, int W, int B, int D, int F, const T *fvz, const T *feat, float m,
+                            float eps, T *out_feat, int64_t *out_idx, T *out_w, void *ws, size_t ws_bytes,
+                            hipStream_t st) {
+  const BinGeom g = make_bin_geom(B, H, W, F);
+  const RastTileWs L(g, B, F, sizeof(T));
+  KL_REQUIRE(ws_bytes >= L.bytes, "rasterize forward: workspace too small");
+  KL_REQUIRE(H < 65536 && W < 65536, "rasterize forward: height and width must be < 65536");
+  const size_t P = (size_t)B * H * W;
+  if (P == 0) return KL_OK;
+  if (F == 0) {  // no faces: face_idx -1, zero weights and features (the kernels need F > 0)
+    KL_CHECK_RC(fill_async(out_idx, 0xff, P * sizeof(int64_t), st));
+    KL_CHECK_RC(fill_async(out_w, 0, P * 3 * sizeof(T), st));
+    return fill_async(out_feat, 0, P * D * sizeof(T), st);
+  }
+  char *w = reinterpret_cast<char *>(ws);
+  uint32_t *bitmap = reinterpret_cast<uint32_t *>(w);
+  int *ghist = reinterpret_cast<int *>(w + L.off_hist);
+  T *rec = reinterpret_cast<T *>(w + L.off_rec);
+  uint2 *rng = reinterpret_cast<uint2 *>(w + L.off_rng);
+  uint8_t *bk = reinterpret_cast<uint8_t *>(w + L.off_bk);
+  int32_t *items = reinterpret_cast<int32_t *>(w + L.off_items);
+  int *nitems = reinterpret_cast<int *>(w + L.off_n);
+  KL_CHECK_RC(fill_async(bitmap, 0, L.off_hist + ORD_BUCKETS * sizeof(int), st));
+  const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);
+  const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
+  if (src.vmask)
+    hipLaunchKernelGGL((raster_bin_kernel<T, 1>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, bitmap, rec, rng);
+  else if (src.nz)
+    hipLaunchKernelGGL((raster_bin_kernel<T, 2>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, bitmap, rec, rng);
+  else
+    hipLaunchKernelGGL((raster_bin_kernel<T, 0>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, bitmap, rec, rng);
+  KL_CHECK_LAUNCH();
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  // heaviest tiles first; tiles with >= 2^split_from - 1 candidate chunks are split into
+  // 2^split_log2 row parts (f32 only: the f64 walk is one wave per row).  Dev flag bits
+  // 16-20 / 21-22 override the two (ablation); bit 12 = grid order, no split.
+  int split_from = 5, split_log2 = 2;
+  if ((g_dev_flags >> 16) & 31) split_from = (g_dev_flags >> 16) & 31;
+  if ((g_dev_flags >> 21) & 3) split_log2 = (g_dev_flags >> 21) & 3;
+  if (sizeof(T) != 4) split_log2 = 0;
+  const int identity = (g_dev_flags >> 12) & 1;
+  if (!identity) {
+    hipLaunchKernelGGL(tile_bucket_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)bitmap,
+                       g.words, nt, bk, ghist, nullptr);
+    KL_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt, items,
+                     identity, split_from, split_log2, nitems);
+  KL_CHECK_LAUNCH();
+  const RastTileArgs<T> args{src, fvz, feat, bitmap, rec, rng, items, nitems, g, F, D, eps, out_feat, out_idx, out_w,
+                             reinterpret_cast<uint64_t *>(g_dev_debug)};
+  hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
@@ -674,6 +1166,20 @@ static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *g
   return rasterize_bwd<T>(B, H, W, F, D, grad, face_idx, w, fvi, feat, eps, gfvi, gfeat, st);
 }
 
+// The fused front-end path's forward: the tile rasterizer (dev flag bit 13 selects the
+// per-face visibility-buffer path instead, for ablation timing).
+template <typename T>
+static int dibr_rast_fwd(RastSrc<T> src, int H, int W, int B, int D, int F, const T *fvz, const T *feat, float m,
+                         float eps, T *out_feat, int64_t *out_idx, T *out_w, void *ws, size_t ws_bytes,
+                         hipStream_t st) {
+  if (g_dev_flags & (1 << 13)) {
+    const int64_t nf = (int64_t)B * F;
+    return launch_rast_fwd<T>(src, H, W, B, D, nf, nf, fvz, feat, nullptr, F, m, eps, out_feat, out_idx, out_w, ws,
+                              ws_bytes, st);
+  }
+  return launch_rast_tile<T>(src, H, W, B, D, F, fvz, feat, m, eps, out_feat, out_idx, out_w, ws, ws_bytes, st);
+}
+
 }  // namespace kl
 
 using namespace kl;
@@ -704,7 +1210,9 @@ extern "C" int kl_packed_rasterize_forward(kl_dtype dtype, int height, int width
 }
 
 extern "C" size_t kl_dibr_rasterize_workspace_bytes(int batch, int height, int width, int num_faces) {
-  const size_t fwd = RastWs(batch, height, width, (int64_t)batch * num_faces).bytes;
+  const size_t tile = rast_tile_ws_bytes(batch, height, width, num_faces);
+  const size_t vis = RastWs(batch, height, width, (int64_t)batch * num_faces).bytes;  // dev ablation path
+  const size_t fwd = tile > vis ? tile : vis;
   const size_t bwd = ((size_t)batch * num_faces + 1) * sizeof(int);
   return fwd > bwd ? fwd : bwd;
 }
@@ -714,19 +1222,16 @@ extern "C" int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, 
                                          const uint8_t *valid_faces, const void *fnz, float multiplier, float eps,
                                          void *out_feat, int64_t *out_idx, void *out_w, void *ws, size_t ws_bytes,
                                          kl_stream stream) {
-  const int64_t nf = (int64_t)batch * num_faces;
   if (dtype == KL_F32)
-    return launch_rast_fwd<float>(RastSrc<float>{(const float *)fvi, valid_faces, (float)multiplier,
-                                                 (const float *)fnz}, height, width,
-                                  batch, feat_dim, nf, nf, (const float *)fvz, (const float *)feat, nullptr,
-                                  num_faces, multiplier, eps, (float *)out_feat, out_idx, (float *)out_w, ws, ws_bytes,
-                                  S(stream));
+    return dibr_rast_fwd<float>(RastSrc<float>{(const float *)fvi, valid_faces, (float)multiplier,
+                                               (const float *)fnz}, height, width, batch, feat_dim, num_faces,
+                                (const float *)fvz, (const float *)feat, multiplier, eps, (float *)out_feat, out_idx,
+                                (float *)out_w, ws, ws_bytes, S(stream));
   if (dtype == KL_F64)
-    return launch_rast_fwd<double>(RastSrc<double>{(const double *)fvi, valid_faces, (double)multiplier,
-                                                   (const double *)fnz}, height,
-                                   width, batch, feat_dim, nf, nf, (const double *)fvz, (const double *)feat, nullptr,
-                                   num_faces, multiplier, eps, (double *)out_feat, out_idx, (double *)out_w, ws,
-                                   ws_bytes, S(stream));
+    return dibr_rast_fwd<double>(RastSrc<double>{(const double *)fvi, valid_faces, (double)multiplier,
+                                                 (const double *)fnz}, height, width, batch, feat_dim, num_faces,
+                                 (const double *)fvz, (const double *)feat, multiplier, eps, (double *)out_feat,
+                                 out_idx, (double *)out_w, ws, ws_bytes, S(stream));
   set_error("dibr_rasterize_forward not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -774,9 +1279,8 @@ template <typename T>
 static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, const T *fvi, const T *feat, const T *fnz,
                     float sigmainv, double pad, float m, float eps, T *out_feat, int64_t *out_idx, T *out_w,
                     T *out_mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st) {
-  const int64_t nf = (int64_t)B * F;
-  KL_CHECK_RC(launch_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, nf, nf, fvz, feat, nullptr, F, m,
-                                 eps, out_feat, out_idx, out_w, ws, ws_bytes, st));
+  KL_CHECK_RC(dibr_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, F, fvz, feat, m, eps, out_feat,
+                               out_idx, out_w, ws, ws_bytes, st));
   return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, ws, ws_bytes, st);
 }
 

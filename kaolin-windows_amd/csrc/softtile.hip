@@ -29,102 +29,14 @@
 // flushed with global atomics -- into a zeroed gradient, or added onto the rasterizer
 // backward's gradient (kl_dibr_backward).
 #include "soft_common.h"
+#include "tileorder.h"
+#include "tilewalk.h"
 
 #include <algorithm>
 
 namespace kl {
 
 constexpr int ST_LIST_CAP = 1024;  // face-list entries per workgroup (8 B each)
-constexpr int ORD_BUCKETS = 32;
-
-// Heaviest-first tile order: counting sort of the tiles on floor(log2(count + 1)) of their
-// candidate-chunk counts (set bits of the tile's bitmap words), descending.  Two kernels:
-// one wave per tile counts and adds to the bucket histogram `ghist` (zeroed with the
-// bitmap); one workgroup then scans the histogram and scatters the order (a kernel
-// boundary instead of a per-workgroup release fence).  The scratch int of the compact
-// state is zeroed here too.
-__global__ void __launch_bounds__(256) tile_bucket_kernel(const uint32_t *__restrict__ bitmap, int words, int nt,
-                                                          uint8_t *__restrict__ bk, int *__restrict__ ghist,
-                                                          int *__restrict__ scratch) {
-  __shared__ int hist[ORD_BUCKETS];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x < ORD_BUCKETS) hist[threadIdx.x] = 0;
-  if (threadIdx.x == 0 && blockIdx.x == 0 && scratch) *scratch = 0;
-  __syncthreads();
-  const int t = blockIdx.x * (blockDim.x >> 6) + wid;  // one wave per tile
-  if (t < nt) {
-    const uint32_t *w = bitmap + (size_t)t * words;
-    unsigned n = 0;
-    for (int k = lane; k < words; k += 64) n += __popc(w[k]);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
-    if (lane == 0) {
-      const int b = 31 - __clz(n + 1u);
-      bk[t] = (uint8_t)b;
-      atomicAdd(&hist[b], 1);
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < ORD_BUCKETS && hist[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], hist[threadIdx.x]);
-}
-
-__global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *__restrict__ bk, const int *__restrict__ ghist,
-                                                          int nt, int32_t *__restrict__ order, int identity) {
-  __shared__ int base[ORD_BUCKETS];
-  if (identity) {  // dev ablation: grid order
-    for (int u = threadIdx.x; u < nt; u += blockDim.x) order[u] = u;
-    return;
-  }
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
-      base[q] = s;
-      s += ghist[q];
-    }
-  }
-  __syncthreads();
-  for (int u = threadIdx.x; u < nt; u += blockDim.x) order[atomicAdd(&base[bk[u]], 1)] = u;
-}
-
-// Lane exchange v <- v[lane ^ S] with cross-lane VALU ops (gfx950 permlane swaps, DPP)
-// where they exist and ds_swizzle (no memory access) for xor 4.
-template <int S>
-__device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lane) {
-  if constexpr (S == 32) {
-    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-    return (lane & 32) ? r[0] : r[1];
-  } else if constexpr (S == 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-    return (lane & 16) ? r[0] : r[1];
-  } else if constexpr (S == 8) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
-  } else if constexpr (S == 4) {
-    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (4 << 10) | 0x1f);  // bitmask mode, xor 4
-  } else if constexpr (S == 2) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
-  } else {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
-  }
-}
-
-template <int S>
-__device__ __forceinline__ uint64_t transpose_stage(uint64_t x, uint64_t m, int lane) {
-  const uint64_t p = ((uint64_t)xor_lane<S>((uint32_t)(x >> 32), lane) << 32) | xor_lane<S>((uint32_t)x, lane);
-  return (lane & S) ? ((x & ~m) | ((p & ~m) >> S)) : ((x & m) | ((p & m) << S));
-}
-
-// 64x64 bit-matrix transpose across the wave: lane i holds row i (bit j = column j) on
-// entry and column i (bit j = row j) on exit.  Six block-swap stages.
-__device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {
-  x = transpose_stage<32>(x, 0x00000000ffffffffull, lane);
-  x = transpose_stage<16>(x, 0x0000ffff0000ffffull, lane);
-  x = transpose_stage<8>(x, 0x00ff00ff00ff00ffull, lane);
-  x = transpose_stage<4>(x, 0x0f0f0f0f0f0f0f0full, lane);
-  x = transpose_stage<2>(x, 0x3333333333333333ull, lane);
-  x = transpose_stage<1>(x, 0x5555555555555555ull, lane);
-  return x;
-}
-
 template <typename T>
 struct SoftTileArgs {
   SoftSrc<T> src;            // unscaled face_vertices_image, multiplier, bbox pad
@@ -146,61 +58,9 @@ struct SoftTileArgs {
 __host__ __device__ constexpr size_t st_wave_lds(int K) { return (size_t)K * 64 * sizeof(uint32_t) + 128 * sizeof(int); }
 constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int); }
 
-// The candidate chunks of a tile (set bits of its bitmap words, ascending) as a sequence
-// with random access by ordinal: 64 words per group, one per lane, with an exclusive
-// prefix of their bit counts.  Wave-uniform; every wave of the workgroup holds a copy.
-// at(n) must be called with non-decreasing n.
-struct ChunkSeq {
-  const uint32_t *words;
-  int nwords, grp, base, gtot, pc;
-  uint32_t wv;
-  __device__ __forceinline__ void load(int g, int lane) {
-    grp = g;
-    const int w = g * 64 + lane;
-    wv = w < nwords ? words[w] : 0u;
-    const int c = __popc(wv);
-    int inc = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(inc, o);
-      if (lane >= o) inc += u;
-    }
-    pc = inc - c;
-    gtot = __shfl(inc, 63);
-  }
-  __device__ __forceinline__ void init(const uint32_t *w, int n, int lane) {
-    words = w;
-    nwords = n;
-    base = 0;
-    load(0, lane);
-  }
-  __device__ __forceinline__ int at(int n, int lane) {
-    while (n >= base + gtot) {
-      if ((grp + 1) * 64 >= nwords) return -1;
-      base += gtot;
-      load(grp + 1, lane);
-    }
-    const int t = n - base;
-    const uint64_t le = ballot(pc <= t);
-    const int L = 63 - __builtin_clzll(le);
-    int k = t - __builtin_amdgcn_readlane(pc, L);
-    uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)wv, L);
-    int bit = 0;
-#pragma unroll
-    for (int h = 16; h > 0; h >>= 1) {  // the k-th set bit of w
-      const int c = __popc(w & ((1u << h) - 1u));
-      if (k >= c) {
-        k -= c;
-        w >>= h;
-        bit += h;
-      }
-    }
-    return (grp * 64 + L) * 32 + bit;
-  }
-};
-
 template <typename T>
 __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
+  uint64_t *const dbg = kDevStamps ? a.dbg : nullptr;  // compiled out unless KL_DEV_STAMPS
   extern __shared__ __align__(16) unsigned char smem[];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -231,13 +91,11 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   const float m = a.m;
   const float sx = m / (float)W, sy = m / (float)H, xinv = (float)W / m;  // pixel pitch as pix_x / pix_y
   auto py = [&](int jj) { return (T)(sy * (float)(H - 2 * jj - 1)); };   // == pix_y<T>(m, H, jj)
-  auto px = [&](int ii) { return (T)(sx * (float)(2 * ii + 1 - W)); };   // == pix_x<T>(m, W, ii)
-  const T y0 = py(row_ok ? j : H - 1);
   const int64_t f0 = (int64_t)b * a.F;
   uint64_t t0 = 0, t1 = 0, w0 = 0, c_fill = 0, c_walk = 0, c_sync = 0, tq = 0;
   uint64_t c_pf = 0, c_test = 0, c_s1 = 0, tr = 0;
   int n_entries = 0, n_iters = 0, n_groups = 0;
-  if (a.dbg) {
+  if (dbg) {
     t0 = stamp_clk();
     w0 = stamp_wall();
   }
@@ -285,14 +143,14 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
       // ---- 1. expand candidate chunks into the face list, R chunks per step; the next
       //         step's bboxes are in flight while this step's are tested
       int len = 0;
-      if (a.dbg) tq = stamp_clk();
+      if (dbg) tq = stamp_clk();
       while (more && len + R * 64 <= ST_LIST_CAP) {
-        if (a.dbg) tr = stamp_clk();
+        if (dbg) tr = stamp_clk();
         const int c = nc;
         const T bx0 = nb0, by0 = nb1, bx1 = nb2, by1 = nb3;
         pf_next();  // consumed by the next step, in this fill or after the drain
         more = nexists;
-        if (a.dbg) {
+        if (dbg) {
           const uint64_t t = stamp_clk();
           c_pf += t - tr;
           tr = t;
@@ -314,14 +172,14 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
         }
         const uint64_t km = ballot(keep);
         if (lane == 0) s_cnt[wid] = __popcll(km);
-        if (a.dbg) {
+        if (dbg) {
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
           const uint64_t t = stamp_clk();
           c_test += t - tr;
           tr = t;
         }
         __syncthreads();
-        if (a.dbg) {
+        if (dbg) {
           const uint64_t t = stamp_clk();
           c_s1 += t - tr;
           tr = t;
@@ -343,7 +201,7 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
         __syncthreads();
       }
       n_entries += len;
-      if (a.dbg) {
+      if (dbg) {
         const uint64_t t = stamp_clk();
         c_fill += t - tq;
         tq = t;
@@ -377,7 +235,7 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
         }
         amask = ballot(active);
       }
-      if (a.dbg) {
+      if (dbg) {
         const uint64_t t = stamp_clk();
         c_walk += t - tq;
         tq = t;
@@ -387,12 +245,12 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
       any = 0;
       for (int w = 0; w < R; w++) any |= s_cnt[w];
       __syncthreads();
-      if (a.dbg) c_sync += stamp_clk() - tq;
+      if (dbg) c_sync += stamp_clk() - tq;
       if (!any || !more) break;
     }
   }
   if (!px_valid) kid = 0;
-  if (a.dbg) t1 = stamp_clk();
+  if (dbg) t1 = stamp_clk();
 
   // ---- 3. the row's hits (face ids, (pixel, slot) order) -> records; the evaluation
   //         runs in soft_tile_eval_kernel, where heavy rows spread over the whole chip
@@ -419,8 +277,8 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
     if (kid == 0) a.mask[pix] = covered ? (T)1.0 : (T)0.0;  // 1 - prod over no slots = 0
   }
   if (row_ok && lane == 0) a.seg_tot[(size_t)(b * H + j) * g.tiles_x + tx] = total;
-  if (a.dbg && lane == 0) {
-    uint64_t *d = a.dbg + ((size_t)blockIdx.x * R + wid) * 12;
+  if (dbg && lane == 0) {
+    uint64_t *d = dbg + ((size_t)blockIdx.x * R + wid) * 12;
     d[8] = c_fill;
     d[9] = c_walk;
     d[10] = c_sync;
@@ -779,7 +637,7 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
     KL_CHECK_RC(fill_async(scratch, 0, sizeof(int), st));
   }
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt,
-                     order, identity);
+                     order, identity, ORD_BUCKETS, 0, nullptr);
   KL_CHECK_LAUNCH();
   SoftTileArgs<T> args{src,  bbox, sel,  bitmap,   order,    g,        F,         K,
                        sigmainv, m, mask, hits, rec_face, rec_prob, s.seg_tot, (uint64_t *)g_dev_debug};

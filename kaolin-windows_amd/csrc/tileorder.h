@@ -1,0 +1,74 @@
+// tileorder.h -- heaviest-first order of the 64x8 tiles of a bin bitmap (binning.h), shared
+// by the soft mask (softtile.hip) and the tile rasterizer (raster.hip).
+#pragma once
+
+#include "common.h"
+
+namespace kl {
+
+constexpr int ORD_BUCKETS = 32;
+
+// Counting sort of the tiles on floor(log2(count + 1)) of their candidate-chunk counts
+// (set bits of the tile's bitmap words), descending.  Two kernels: one wave per tile
+// counts and adds to the bucket histogram `ghist` (zeroed with the bitmap); one
+// workgroup then scans the histogram and scatters the order (a kernel boundary instead
+// of a per-workgroup release fence).  `scratch` (optional) is zeroed here too.
+static __global__ void __launch_bounds__(256) tile_bucket_kernel(const uint32_t *__restrict__ bitmap, int words, int nt,
+                                                          uint8_t *__restrict__ bk, int *__restrict__ ghist,
+                                                          int *__restrict__ scratch) {
+  __shared__ int hist[ORD_BUCKETS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x < ORD_BUCKETS) hist[threadIdx.x] = 0;
+  if (threadIdx.x == 0 && blockIdx.x == 0 && scratch) *scratch = 0;
+  __syncthreads();
+  const int t = blockIdx.x * (blockDim.x >> 6) + wid;  // one wave per tile
+  if (t < nt) {
+    const uint32_t *w = bitmap + (size_t)t * words;
+    unsigned n = 0;
+    for (int k = lane; k < words; k += 64) n += __popc(w[k]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+    if (lane == 0) {
+      const int b = 31 - __clz(n + 1u);
+      bk[t] = (uint8_t)b;
+      atomicAdd(&hist[b], 1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < ORD_BUCKETS && hist[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], hist[threadIdx.x]);
+}
+
+// Work items, heaviest first: tile | part << 24 | log2(parts) << 28.  Tiles of bucket
+// >= split_from become 2^split_log2 items (parts of the tile's rows), the others one.
+// nitems (optional) receives the item count.  identity: grid order, no split (dev ablation).
+static __global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *__restrict__ bk, const int *__restrict__ ghist,
+                                                          int nt, int32_t *__restrict__ order, int identity,
+                                                          int split_from, int split_log2, int *__restrict__ nitems) {
+  __shared__ int base[ORD_BUCKETS];
+  if (identity) {
+    for (int u = threadIdx.x; u < nt; u += blockDim.x) order[u] = u;
+    if (nitems && threadIdx.x == 0) *nitems = nt;
+    return;
+  }
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
+      base[q] = s;
+      s += ghist[q] << (q >= split_from ? split_log2 : 0);
+    }
+    if (nitems) *nitems = s;
+  }
+  __syncthreads();
+  for (int u = threadIdx.x; u < nt; u += blockDim.x) {
+    const int q = bk[u];
+    if (q >= split_from) {
+      const int np = 1 << split_log2;
+      const int o = atomicAdd(&base[q], np);
+      for (int k = 0; k < np; k++) order[o + k] = u | (k << 24) | (split_log2 << 28);
+    } else {
+      order[atomicAdd(&base[q], 1)] = u;
+    }
+  }
+}
+
+}  // namespace kl
