@@ -181,6 +181,10 @@ def op_bytes(name, inp, stats):
     if name == 'dibr_rasterize_forward':
         # write idx/weights/features; read (valid mask + z + image coords) of all faces + features of valid ones
         return px * (8 + 3 * s + D * s) + B * F * (1 + 3 * s + 6 * s) + nv * 3 * D * s
+    if name == 'dibr_forward':
+        # both of the above in one call: the faces are read once for both
+        return (op_bytes('dibr_rasterize_forward', inp, stats) + op_bytes('dibr_soft_mask_forward', inp, stats)
+                - B * F * 6 * s)
     if name in ('rasterize_backward_cuda', 'dibr_rasterize_backward'):
         return px * (8 + 3 * s + D * s) + B * F * (6 * s + 3 * D * s) * 2
     return None
@@ -191,8 +195,10 @@ OP_KERNELS = {
     'dibr_soft_mask_forward': ('bin_faces_kernel<float, kl::SoftSrc', 'tile_bucket_kernel', 'tile_order_kernel',
                                'soft_tile_fwd_kernel<float', 'soft_tile_eval_kernel<float'),
     'dibr_soft_mask_backward': ('soft_bwd_plan_kernel', 'soft_tile_bwd_kernel<float'),
-    'dibr_rasterize_forward': ('raster_vis_kernel<float, kl::RastSrc', 'raster_vis_big_kernel<float, kl::RastSrc',
-                               'raster_resolve_kernel<float, kl::RastSrc'),
+    'dibr_rasterize_forward': ('raster_bin_kernel<float, 2>', 'tile_bucket_kernel', 'tile_order_kernel',
+                               'raster_tile_kernel<float'),
+    'dibr_forward': ('raster_bin_kernel<float, 2>', 'tile_bucket2_kernel', 'tile_order2_kernel', 'raster_tile_kernel<float',
+                     'soft_tile_fwd_kernel<float', 'soft_tile_eval_kernel<float'),
     'dibr_rasterize_backward': ('rasterize_bwd_gather_kernel<float', 'rasterize_bwd_bigface_kernel<float'),
 }
 

@@ -27,6 +27,8 @@
 //                                   face, in row-major order -- no atomics, deterministic.
 //                                   Valid whenever face_idx came from the forward (a face
 //                                   can only be selected inside its bbox).
+#include <algorithm>
+
 #include "soft_common.h"
 #include "tileorder.h"
 #include "tilewalk.h"
@@ -424,7 +426,9 @@ struct PixPitch {
 template <typename T, int VMODE>
 __global__ void __launch_bounds__(256) raster_bin_kernel(RastSrc<T> src, const T *__restrict__ fvz, int F, BinGeom g,
                                                          PixPitch pp, uint32_t *__restrict__ bitmap,
-                                                         T *__restrict__ rec, uint2 *__restrict__ rng) {
+                                                         T *__restrict__ rec, uint2 *__restrict__ rng,
+                                                         uint32_t *__restrict__ sbitmap = nullptr,
+                                                         T *__restrict__ sbbox = nullptr, T spad = 0) {
   const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.y;
@@ -461,6 +465,30 @@ __global__ void __launch_bounds__(256) raster_bin_kernel(RastSrc<T> src, const T
   const bool has = ix0 <= ix1;
   bin_mark(g, b, c, lane, has ? ix0 / TILE_W : 1, has ? ix1 / TILE_W : 0, has ? iy0 / TILE_H : 1,
            has ? iy1 / TILE_H : 0, bitmap);
+  if (sbitmap) {
+    // the soft mask's bins of the same faces (kl_dibr_forward): every face, bbox enlarged
+    // by boxlen * multiplier as SoftSrc / dibr.py:31-39, conservative tiles as bin_faces_kernel
+    int tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
+    if (live) {
+      const T bx0 = tmin3(v[0], v[2], v[4]) - spad, by0 = tmin3(v[1], v[3], v[5]) - spad;
+      const T bx1 = tmax3(v[0], v[2], v[4]) + spad, by1 = tmax3(v[1], v[3], v[5]) + spad;
+      T *q = sbbox + f * 4;
+      q[0] = bx0;
+      q[1] = by0;
+      q[2] = bx1;
+      q[3] = by1;
+      int jx0, jx1, jy0, jy1;
+      axis_range((double)bx0, (double)bx1, (double)pp.sx, g.width, false, jx0, jx1);
+      axis_range((double)by0, (double)by1, (double)pp.sy, g.height, true, jy0, jy1);
+      if (jx0 <= jx1 && jy0 <= jy1) {
+        tx0 = jx0 / TILE_W;
+        tx1 = jx1 / TILE_W;
+        ty0 = jy0 / TILE_H;
+        ty1 = jy1 / TILE_H;
+      }
+    }
+    bin_mark(g, b, c, lane, tx0, tx1, ty0, ty1, sbitmap);
+  }
 }
 
 template <typename T>
@@ -1275,13 +1303,89 @@ extern "C" int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height,
 // The state's scratch int is the gather's big-face counter: the forward zeroes it and
 // the soft-mask backward re-zeroes it, so the backward needs no fill of its own.
 namespace kl {
+// Workspace of kl_dibr_forward: the rasterizer's and the soft mask's bins are built by one
+// pass over the faces, counted by one bucket kernel and ordered by one order kernel.
+//   zeroed: raster bitmap | soft bitmap | raster ghist | soft ghist
+//   then:   face records | pixel ranges | raster buckets | soft buckets | raster items |
+//           item count | soft order | soft bboxes     (records and bboxes sized for f64)
+struct DibrFwdWs {
+  size_t off_sbm, off_rgh, off_sgh, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder, off_sbbox,
+      bytes;
+  DibrFwdWs(int B, int H, int W, int F) {
+    const BinGeom g = make_bin_geom(B, H, W, F);
+    const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    off_sbm = g.bytes();
+    off_rgh = off_sbm + g.bytes();
+    off_sgh = off_rgh + ORD_BUCKETS * sizeof(int);
+    zero = off_sgh + ORD_BUCKETS * sizeof(int);
+    off_rec = up(zero);
+    off_rng = up(off_rec + (size_t)B * F * RT_REC * sizeof(double));
+    off_rbk = up(off_rng + (size_t)B * F * sizeof(uint2));
+    off_sbk = up(off_rbk + nt);
+    off_items = up(off_sbk + nt);
+    off_n = off_items + nt * TILE_H * sizeof(int32_t);
+    off_sorder = up(off_n + sizeof(int));
+    off_sbbox = up(off_sorder + nt * sizeof(int32_t));
+    bytes = off_sbbox + (size_t)B * F * 4 * sizeof(double);
+  }
+};
+
 template <typename T>
 static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, const T *fvi, const T *feat, const T *fnz,
                     float sigmainv, double pad, float m, float eps, T *out_feat, int64_t *out_idx, T *out_w,
                     T *out_mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st) {
-  KL_CHECK_RC(dibr_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, F, fvz, feat, m, eps, out_feat,
-                               out_idx, out_w, ws, ws_bytes, st));
-  return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, ws, ws_bytes, st);
+  const DibrFwdWs L(B, H, W, F);
+  KL_REQUIRE(ws_bytes >= L.bytes, "dibr_rasterization forward: workspace too small");
+  KL_REQUIRE(H < 65536 && W < 65536, "dibr_rasterization forward: height and width must be < 65536");
+  KL_REQUIRE(K >= 0 && K <= 255, "dibr_rasterization forward: the compact soft mask needs 0 <= knum <= 255");
+  KL_REQUIRE(F < (1 << 28), "dibr_rasterization forward: too many faces");
+  const size_t P = (size_t)B * H * W;
+  if (P == 0) return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
+  if (F == 0 || (g_dev_flags & (1 << 13))) {  // no faces (or dev: the separate pipelines)
+    KL_CHECK_RC(dibr_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, F, fvz, feat, m, eps, out_feat,
+                                 out_idx, out_w, ws, ws_bytes, st));
+    return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, ws, ws_bytes, st);
+  }
+  const BinGeom g = make_bin_geom(B, H, W, F);
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  char *w = reinterpret_cast<char *>(ws);
+  uint32_t *rbm = reinterpret_cast<uint32_t *>(w);
+  uint32_t *sbm = reinterpret_cast<uint32_t *>(w + L.off_sbm);
+  int *rgh = reinterpret_cast<int *>(w + L.off_rgh);
+  int *sgh = reinterpret_cast<int *>(w + L.off_sgh);
+  T *rec = reinterpret_cast<T *>(w + L.off_rec);
+  uint2 *rng = reinterpret_cast<uint2 *>(w + L.off_rng);
+  uint8_t *rbk = reinterpret_cast<uint8_t *>(w + L.off_rbk);
+  uint8_t *sbk = reinterpret_cast<uint8_t *>(w + L.off_sbk);
+  int32_t *items = reinterpret_cast<int32_t *>(w + L.off_items);
+  int *nitems = reinterpret_cast<int *>(w + L.off_n);
+  int32_t *sorder = reinterpret_cast<int32_t *>(w + L.off_sorder);
+  T *sbbox = reinterpret_cast<T *>(w + L.off_sbbox);
+  KL_CHECK_RC(fill_async(w, 0, L.zero, st));
+  const RastSrc<T> src{fvi, nullptr, (T)m, fnz};
+  const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
+  const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);
+  if (fnz)
+    hipLaunchKernelGGL((raster_bin_kernel<T, 2>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, rbm, rec, rng, sbm,
+                       sbbox, (T)pad);
+  else
+    hipLaunchKernelGGL((raster_bin_kernel<T, 0>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, rbm, rec, rng, sbm,
+                       sbbox, (T)pad);
+  KL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(tile_bucket2_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)rbm,
+                     (const uint32_t *)sbm, g.words, nt, rbk, sbk, rgh, sgh, s.scratch);
+  KL_CHECK_LAUNCH();
+  const int split_from = 5, split_log2 = sizeof(T) == 4 ? 2 : 0;
+  hipLaunchKernelGGL(tile_order2_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh, items,
+                     split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt);
+  KL_CHECK_LAUNCH();
+  const RastTileArgs<T> args{src, fvz, feat, rbm, rec, rng, items, nitems, g, F, D, eps, out_feat, out_idx, out_w,
+                             reinterpret_cast<uint64_t *>(g_dev_debug)};
+  hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
+  KL_CHECK_LAUNCH();
+  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, sbm, sorder, sbbox,
+                                   st);
 }
 
 template <typename T>
@@ -1297,9 +1401,10 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
 }  // namespace kl
 
 extern "C" size_t kl_dibr_workspace_bytes(int batch, int height, int width, int num_faces) {
-  const size_t a = kl_dibr_rasterize_workspace_bytes(batch, height, width, num_faces);
+  const size_t a = kl_dibr_rasterize_workspace_bytes(batch, height, width, num_faces);  // F == 0 / dev path
   const size_t b = soft_tile_ws_bytes(batch, height, width, num_faces);
-  return a > b ? a : b;
+  const size_t c = DibrFwdWs(batch, height, width, num_faces).bytes;
+  return std::max(a, std::max(b, c));
 }
 
 extern "C" size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum) {

@@ -604,9 +604,6 @@ static int rows_per_wg(int K) {
 template <typename T>
 int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv, double pad,
                       float m, T *mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st) {
-  uint8_t *hits = s.hits;
-  uint32_t *rec_face = s.rec_face;
-  T *rec_prob = s.rec_prob;
   int *scratch = s.scratch;
   const BinGeom g = make_bin_geom(B, H, W, F);
   const StWs L(g, F);
@@ -614,10 +611,7 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
   KL_REQUIRE(K >= 0 && K <= 255, "dibr_soft_mask: the compact path needs 0 <= knum <= 255");
   KL_REQUIRE(F < (1 << 28), "dibr_soft_mask: too many faces");
   if ((int64_t)B * H * W == 0) return scratch ? fill_async(scratch, 0, sizeof(int), st) : KL_OK;
-  int R = rows_per_wg(K);
-  KL_REQUIRE(R > 0, "dibr_soft_mask: knum too large for the LDS slot lists");
-  const int dev_r = (g_dev_flags >> 8) & 15;  // dev override of the rows per workgroup (ablation)
-  if (dev_r && dev_r <= R && TILE_H % dev_r == 0) R = dev_r;
+  KL_REQUIRE(rows_per_wg(K) > 0, "dibr_soft_mask: knum too large for the LDS slot lists");
   char *w = reinterpret_cast<char *>(ws);
   uint32_t *bitmap = reinterpret_cast<uint32_t *>(w);
   int *ghist = reinterpret_cast<int *>(w + L.hist);
@@ -639,8 +633,25 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt,
                      order, identity, ORD_BUCKETS, 0, nullptr);
   KL_CHECK_LAUNCH();
-  SoftTileArgs<T> args{src,  bbox, sel,  bitmap,   order,    g,        F,         K,
-                       sigmainv, m, mask, hits, rec_face, rec_prob, s.seg_tot, (uint64_t *)g_dev_debug};
+  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, sel, sigmainv, pad, m, mask, s, bitmap, order, bbox, st);
+}
+
+// The selection and evaluation kernels on bins made by the caller: bitmap (SoftSrc bins),
+// heaviest-first tile order and the enlarged bboxes; s.scratch already zeroed.
+template <typename T>
+int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv,
+                           double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
+                           const int32_t *order, const T *bbox, hipStream_t st) {
+  const BinGeom g = make_bin_geom(B, H, W, F);
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  if (nt == 0) return KL_OK;
+  int R = rows_per_wg(K);
+  KL_REQUIRE(R > 0, "dibr_soft_mask: knum too large for the LDS slot lists");
+  const int dev_r = (g_dev_flags >> 8) & 15;  // dev override of the rows per workgroup (ablation)
+  if (dev_r && dev_r <= R && TILE_H % dev_r == 0) R = dev_r;
+  const SoftSrc<T> src{fvi, (T)m, (T)pad};
+  SoftTileArgs<T> args{src,      bbox, sel,  bitmap,  order,      g,          F,          K,
+                       sigmainv, m,    mask, s.hits, s.rec_face, s.rec_prob, s.seg_tot, (uint64_t *)g_dev_debug};
   const size_t lds = st_head_lds() + st_wave_lds(K) * R;
   hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)(nt * (TILE_H / R))), dim3(64 * R), lds, st, args);
   KL_CHECK_LAUNCH();
@@ -691,6 +702,12 @@ template int soft_tile_forward<float>(int, int, int, int, int, const float *, co
                                       float *, const SoftState<float> &, void *, size_t, hipStream_t);
 template int soft_tile_forward<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
                                        float, double *, const SoftState<double> &, void *, size_t, hipStream_t);
+template int soft_tile_forward_main<float>(int, int, int, int, int, const float *, const int64_t *, float, double,
+                                           float, float *, const SoftState<float> &, const uint32_t *,
+                                           const int32_t *, const float *, hipStream_t);
+template int soft_tile_forward_main<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
+                                            float, double *, const SoftState<double> &, const uint32_t *,
+                                            const int32_t *, const double *, hipStream_t);
 template int soft_tile_backward<float>(int, int, int, int, int, const float *, const float *,
                                        const SoftState<float> &, const float *, float, float, float *, bool, void *,
                                        size_t, hipStream_t);

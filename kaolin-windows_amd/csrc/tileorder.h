@@ -41,10 +41,10 @@ static __global__ void __launch_bounds__(256) tile_bucket_kernel(const uint32_t 
 // Work items, heaviest first: tile | part << 24 | log2(parts) << 28.  Tiles of bucket
 // >= split_from become 2^split_log2 items (parts of the tile's rows), the others one.
 // nitems (optional) receives the item count.  identity: grid order, no split (dev ablation).
-static __global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *__restrict__ bk, const int *__restrict__ ghist,
-                                                          int nt, int32_t *__restrict__ order, int identity,
-                                                          int split_from, int split_log2, int *__restrict__ nitems) {
-  __shared__ int base[ORD_BUCKETS];
+// `base` is a workgroup-shared [ORD_BUCKETS] array.
+__device__ __forceinline__ void order_items(int *base, const uint8_t *__restrict__ bk, const int *__restrict__ ghist,
+                                            int nt, int32_t *__restrict__ order, int identity, int split_from,
+                                            int split_log2, int *__restrict__ nitems) {
   if (identity) {
     for (int u = threadIdx.x; u < nt; u += blockDim.x) order[u] = u;
     if (nitems && threadIdx.x == 0) *nitems = nt;
@@ -69,6 +69,66 @@ static __global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *
       order[atomicAdd(&base[q], 1)] = u;
     }
   }
+}
+
+static __global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *__restrict__ bk,
+                                                                 const int *__restrict__ ghist, int nt,
+                                                                 int32_t *__restrict__ order, int identity,
+                                                                 int split_from, int split_log2,
+                                                                 int *__restrict__ nitems) {
+  __shared__ int base[ORD_BUCKETS];
+  order_items(base, bk, ghist, nt, order, identity, split_from, split_log2, nitems);
+}
+
+// Two bitmaps over the same tiles at once (kl_dibr_forward: the rasterizer's and the soft
+// mask's bins): one wave per tile counts both.
+static __global__ void __launch_bounds__(256) tile_bucket2_kernel(const uint32_t *__restrict__ bm0,
+                                                                  const uint32_t *__restrict__ bm1, int words, int nt,
+                                                                  uint8_t *__restrict__ bk0, uint8_t *__restrict__ bk1,
+                                                                  int *__restrict__ gh0, int *__restrict__ gh1,
+                                                                  int *__restrict__ scratch) {
+  __shared__ int hist[2][ORD_BUCKETS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x < 2 * ORD_BUCKETS) hist[threadIdx.x / ORD_BUCKETS][threadIdx.x % ORD_BUCKETS] = 0;
+  if (threadIdx.x == 0 && blockIdx.x == 0 && scratch) *scratch = 0;
+  __syncthreads();
+  const int t = blockIdx.x * (blockDim.x >> 6) + wid;
+  if (t < nt) {
+    unsigned n0 = 0, n1 = 0;
+    for (int k = lane; k < words; k += 64) {
+      n0 += __popc(bm0[(size_t)t * words + k]);
+      n1 += __popc(bm1[(size_t)t * words + k]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      n0 += __shfl_xor(n0, o);
+      n1 += __shfl_xor(n1, o);
+    }
+    if (lane == 0) {
+      const int b0 = 31 - __clz(n0 + 1u), b1 = 31 - __clz(n1 + 1u);
+      bk0[t] = (uint8_t)b0;
+      bk1[t] = (uint8_t)b1;
+      atomicAdd(&hist[0][b0], 1);
+      atomicAdd(&hist[1][b1], 1);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * ORD_BUCKETS) {
+    const int h = hist[threadIdx.x / ORD_BUCKETS][threadIdx.x % ORD_BUCKETS];
+    if (h) atomicAdd((threadIdx.x < ORD_BUCKETS ? gh0 : gh1) + threadIdx.x % ORD_BUCKETS, h);
+  }
+}
+
+static __global__ void __launch_bounds__(1024) tile_order2_kernel(const uint8_t *__restrict__ bk0,
+                                                                  const int *__restrict__ gh0,
+                                                                  int32_t *__restrict__ order0, int split_from,
+                                                                  int split_log2, int *__restrict__ nitems0,
+                                                                  const uint8_t *__restrict__ bk1,
+                                                                  const int *__restrict__ gh1,
+                                                                  int32_t *__restrict__ order1, int nt) {
+  __shared__ int base[2][ORD_BUCKETS];
+  order_items(base[0], bk0, gh0, nt, order0, 0, split_from, split_log2, nitems0);
+  order_items(base[1], bk1, gh1, nt, order1, 0, ORD_BUCKETS, 0, nullptr);
 }
 
 }  // namespace kl

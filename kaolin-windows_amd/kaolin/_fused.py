@@ -194,3 +194,44 @@ def soft_mask_backward_compact(grad, mask, state, face_vertices_image, sigmainv,
             N.ptr(face_vertices_image), float(sigmainv), float(multiplier), N.ptr(g), 1 if out is not None else 0,
             N.ptr(state.scratch), N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return g
+
+
+def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z, sigmainv, boxlen,
+                 knum, multiplier, eps):
+    """dibr_rasterization's forward in one call (kl_dibr_forward): rasterize with valid =
+    face_normals_z >= 0 and the compact soft mask, sharing one binning pass.
+    -> features (B,H,W,D), face_idx (B,H,W), weights (B,H,W,3), soft_mask (B,H,W), SoftMaskState.
+    face_normals_z must have the dtype of face_vertices_image."""
+    func = 'dibr_rasterization'
+    N.require_gpu(func, face_vertices_z, face_vertices_image, face_normals_z)
+    B, F = face_vertices_z.shape[:2]
+    D = face_features.shape[-1]
+    dev = face_vertices_z.device
+    dtype = face_vertices_z.dtype
+    if dtype not in (torch.float32, torch.float64) or face_normals_z.dtype != dtype:
+        raise RuntimeError(f'"{func}" fused forward needs f32/f64 inputs of one dtype')
+    H, W, K = int(height), int(width), int(knum)
+    fvz = face_vertices_z.contiguous()
+    fvi = face_vertices_image.contiguous()
+    feat = face_features.contiguous()
+    fnz = face_normals_z.contiguous()
+    lib = N.lib()
+    feats = torch.empty((B, H, W, D), dtype=dtype, device=dev)
+    idx = torch.empty((B, H, W), dtype=torch.long, device=dev)
+    w = torch.empty((B, H, W, 3), dtype=dtype, device=dev)
+    mask = torch.empty((B, H, W), dtype=dtype, device=dev)
+    hits = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
+    nrec = lib.kl_soft_mask_compact_records(B, H, W, K)
+    rec_face = torch.empty(max(nrec, 1), dtype=torch.int32, device=dev)
+    rec_prob = torch.empty(max(nrec, 1), dtype=dtype, device=dev)
+    seg_tot = torch.empty(max(lib.kl_soft_mask_compact_segments(B, H, W), 1), dtype=torch.int32, device=dev)
+    scratch = torch.empty(1, dtype=torch.int32, device=dev)
+    nbytes = lib.kl_dibr_workspace_bytes(B, H, W, F)
+    ws = _ws(nbytes, dev)
+    with torch.cuda.device(dev), N.timed('dibr_forward', dev):
+        N.check(lib.kl_dibr_forward(
+            N.dtype_code(dtype), B, H, W, F, D, K, N.ptr(fvz), N.ptr(fvi), N.ptr(feat), N.ptr(fnz), float(sigmainv),
+            float(boxlen * multiplier), float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w),
+            N.ptr(mask), N.ptr(hits), N.ptr(rec_face), N.ptr(rec_prob), N.ptr(seg_tot), N.ptr(scratch), N.ptr(ws),
+            nbytes, N.stream_of(dev)), func)
+    return feats, idx, w, mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, scratch, K)

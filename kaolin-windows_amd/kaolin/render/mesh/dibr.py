@@ -64,11 +64,16 @@ class DibrRasterizationCuda(Function):
         face_vertices_image = face_vertices_image.contiguous()
         face_features = face_features.contiguous()
         face_normals_z = face_normals_z.detach().contiguous()
-        feats, face_idx, weights = _fused.rasterize_forward(height, width, face_vertices_z, face_vertices_image,
-                                                            face_features, None, multiplier, eps,
-                                                            face_normals_z=face_normals_z)
-        soft_mask, state = _fused.soft_mask_forward_compact(face_vertices_image, face_idx, sigmainv, boxlen, knum,
-                                                            multiplier)
+        if face_normals_z.dtype == face_vertices_image.dtype:  # one call, one shared binning pass
+            feats, face_idx, weights, soft_mask, state = _fused.dibr_forward(
+                height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z, sigmainv, boxlen,
+                knum, multiplier, eps)
+        else:
+            feats, face_idx, weights = _fused.rasterize_forward(height, width, face_vertices_z, face_vertices_image,
+                                                                face_features, None, multiplier, eps,
+                                                                face_normals_z=face_normals_z)
+            soft_mask, state = _fused.soft_mask_forward_compact(face_vertices_image, face_idx, sigmainv, boxlen, knum,
+                                                                multiplier)
         ctx.mark_non_differentiable(face_idx)
         ctx.sigmainv, ctx.multiplier, ctx.eps, ctx.knum = sigmainv, multiplier, eps, state.knum
         ctx.save_for_backward(face_idx, weights, face_vertices_image, face_features, face_normals_z, soft_mask,
