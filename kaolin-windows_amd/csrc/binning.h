@@ -188,13 +188,50 @@ __device__ __forceinline__ void bin_mark(const BinGeom &g, int b, int c, int lan
   }
 }
 
+// The reference's float pixel pitches (m / W, m / H) and their inverses (estimates only),
+// computed once on the host with the same float division.
+struct PixPitch {
+  float sx, sy, xinv, yinv;
+};
+
+// Exact pixel interval of one axis whose centres c pass the reference's bbox test
+// (!(c < vlo) && !(c >= vhi), rasterization_cuda.cu:101-104) in float arithmetic: an
+// index estimate corrected against the exact centre formula (monotone in the index).
+// x: c(k) = (T)(s * (2k + 1 - n)) increasing; y (flip): c(k) = (T)(s * (n - 2k - 1))
+// decreasing.  NaN bounds never reject.  Empty: a > b.
+template <typename T>
+__device__ __forceinline__ void exact_range(T vlo, T vhi, float s, float inv, int n, bool flip, int &a, int &b) {
+  if (!(vlo == vlo)) vlo = (T)-INFINITY;  // a NaN bound passes every centre, as -inf / +inf do
+  if (!(vhi == vhi)) vhi = (T)INFINITY;
+  auto c = [&](int k) -> T { return flip ? (T)(s * (float)(n - 2 * k - 1)) : (T)(s * (float)(2 * k + 1 - n)); };
+  auto est = [&](T v) -> int {  // index whose centre is near v, clamped to [0, n]
+    const float t = flip ? ((float)(n - 1) - (float)v * inv) * 0.5f : ((float)v * inv + (float)(n - 1)) * 0.5f;
+    if (!(t == t)) return 0;
+    return t <= 0.0f ? 0 : (t >= (float)n ? n : (int)t);
+  };
+  // P(k) monotone false -> true in k: first k with P (n if none)
+  auto first = [&](int e, auto P) {
+    while (e > 0 && P(e - 1)) e--;
+    while (e < n && !P(e)) e++;
+    return e;
+  };
+  if (!flip) {
+    a = first(est(vlo), [&](int k) { return !(c(k) < vlo); });
+    b = first(est(vhi), [&](int k) { return c(k) >= vhi; }) - 1;
+  } else {
+    a = first(est(vhi), [&](int k) { return !(c(k) >= vhi); });
+    b = first(est(vlo), [&](int k) { return c(k) < vlo; }) - 1;
+  }
+}
+
 // One wave per (mesh b, chunk c).  Mesh b owns faces [first(b), last(b)) of the source.
 // first_idx == nullptr => uniform meshes of `faces_per_mesh` faces.
 // bbox_out (optional): the face bboxes of the source, (N,4), for consumers that walk them.
 template <typename T, typename Src>
 __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *__restrict__ first_idx,
                                                         int faces_per_mesh, BinGeom g, float m,
-                                                        uint32_t *__restrict__ bitmap, T *__restrict__ bbox_out) {
+                                                        uint32_t *__restrict__ bitmap, T *__restrict__ bbox_out,
+                                                        uint2 *__restrict__ rng_out) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.y;
@@ -222,9 +259,18 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *
       bbox_out[f * 4 + 3] = by1;
     }
     int ix0, ix1, iy0, iy1;
-    const double sx = (double)(m / (float)g.width), sy = (double)(m / (float)g.height);
-    axis_range((double)bx0, (double)bx1, sx, g.width, false, ix0, ix1);
-    axis_range((double)by0, (double)by1, sy, g.height, true, iy0, iy1);
+    if (rng_out) {  // exact pixel ranges (the consumer's bbox test), tiles from them
+      const float sx = m / (float)g.width, sy = m / (float)g.height;
+      exact_range(bx0, bx1, sx, (float)g.width / m, g.width, false, ix0, ix1);
+      exact_range(by0, by1, sy, (float)g.height / m, g.height, true, iy0, iy1);
+      const bool e = ix0 > ix1 || iy0 > iy1;
+      rng_out[f] = e ? make_uint2(1u, 1u)
+                     : make_uint2((uint32_t)ix0 | ((uint32_t)ix1 << 16), (uint32_t)iy0 | ((uint32_t)iy1 << 16));
+    } else {
+      const double sx = (double)(m / (float)g.width), sy = (double)(m / (float)g.height);
+      axis_range((double)bx0, (double)bx1, sx, g.width, false, ix0, ix1);
+      axis_range((double)by0, (double)by1, sy, g.height, true, iy0, iy1);
+    }
     if (ix0 <= ix1 && iy0 <= iy1) {
       tx0 = ix0 / TILE_W;
       tx1 = ix1 / TILE_W;
@@ -238,11 +284,12 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *
 // zero_bytes: bytes from `bitmap` zeroed first (0 = the bitmap's own g.bytes()).
 template <typename T, typename Src>
 inline int launch_binning(Src src, const int64_t *first_idx, int faces_per_mesh, const BinGeom &g, float m,
-                          uint32_t *bitmap, hipStream_t st, T *bbox_out = nullptr, size_t zero_bytes = 0) {
+                          uint32_t *bitmap, hipStream_t st, T *bbox_out = nullptr, size_t zero_bytes = 0,
+                          uint2 *rng_out = nullptr) {
   KL_CHECK_RC(fill_async(bitmap, 0, zero_bytes ? zero_bytes : g.bytes(), st));
   dim3 grid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)g.batch);
   hipLaunchKernelGGL((bin_faces_kernel<T, Src>), grid, dim3(256), 0, st, src, first_idx, faces_per_mesh, g, m,
-                     bitmap, bbox_out);
+                     bitmap, bbox_out, rng_out);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

@@ -380,46 +380,10 @@ static int launch_rast_fwd(Src src, int H, int W, int B, int D, int64_t nfaces, 
 constexpr int RT_CAP = 512;  // list entries per step: one chunk per wave
 constexpr int RT_VS = 12;    // LDS stride of a list entry: 6 coordinates, 3 depths, pad
 
-// Exact pixel interval of one axis whose centres c pass the reference's bbox test
-// (!(c < vlo) && !(c >= vhi), rasterization_cuda.cu:101-104) in float arithmetic: an
-// index estimate corrected against the exact centre formula (monotone in the index).
-// x: c(k) = (T)(s * (2k + 1 - n)) increasing; y (flip): c(k) = (T)(s * (n - 2k - 1))
-// decreasing.  NaN bounds never reject.  Empty: a > b.
-template <typename T>
-__device__ __forceinline__ void exact_range(T vlo, T vhi, float s, float inv, int n, bool flip, int &a, int &b) {
-  if (!(vlo == vlo)) vlo = (T)-INFINITY;  // a NaN bound passes every centre, as -inf / +inf do
-  if (!(vhi == vhi)) vhi = (T)INFINITY;
-  auto c = [&](int k) -> T { return flip ? (T)(s * (float)(n - 2 * k - 1)) : (T)(s * (float)(2 * k + 1 - n)); };
-  auto est = [&](T v) -> int {  // index whose centre is near v, clamped to [0, n]
-    const float t = flip ? ((float)(n - 1) - (float)v * inv) * 0.5f : ((float)v * inv + (float)(n - 1)) * 0.5f;
-    if (!(t == t)) return 0;
-    return t <= 0.0f ? 0 : (t >= (float)n ? n : (int)t);
-  };
-  // P(k) monotone false -> true in k: first k with P (n if none)
-  auto first = [&](int e, auto P) {
-    while (e > 0 && P(e - 1)) e--;
-    while (e < n && !P(e)) e++;
-    return e;
-  };
-  if (!flip) {
-    a = first(est(vlo), [&](int k) { return !(c(k) < vlo); });
-    b = first(est(vhi), [&](int k) { return c(k) >= vhi; }) - 1;
-  } else {
-    a = first(est(vhi), [&](int k) { return !(c(k) >= vhi); });
-    b = first(est(vlo), [&](int k) { return c(k) < vlo; }) - 1;
-  }
-}
-
 // Face records written by raster_bin_kernel: vertices x m (6), depths (3), pad (3); and
 // the exact pixel ranges of the reference's bbox test (rasterization_cuda.cu:101-104),
 // x0 | x1 << 16 and y0 | y1 << 16, empty (1, 0) for invalid faces.
 constexpr int RT_REC = 12;
-
-// The reference's float pixel pitches (m / W, m / H) and their inverses (estimates only),
-// computed once on the host with the same float division.
-struct PixPitch {
-  float sx, sy, xinv, yinv;
-};
 
 // VMODE: 0 all faces valid, 1 valid mask, 2 face_normals_z >= 0.  All loads are issued
 // up front (clamped index, no branch around them) and the stores come last.
@@ -428,7 +392,7 @@ __global__ void __launch_bounds__(256) raster_bin_kernel(RastSrc<T> src, const T
                                                          PixPitch pp, uint32_t *__restrict__ bitmap,
                                                          T *__restrict__ rec, uint2 *__restrict__ rng,
                                                          uint32_t *__restrict__ sbitmap = nullptr,
-                                                         T *__restrict__ sbbox = nullptr, T spad = 0) {
+                                                         uint2 *__restrict__ srng = nullptr, T spad = 0) {
   const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.y;
@@ -467,25 +431,24 @@ __global__ void __launch_bounds__(256) raster_bin_kernel(RastSrc<T> src, const T
            has ? iy1 / TILE_H : 0, bitmap);
   if (sbitmap) {
     // the soft mask's bins of the same faces (kl_dibr_forward): every face, bbox enlarged
-    // by boxlen * multiplier as SoftSrc / dibr.py:31-39, conservative tiles as bin_faces_kernel
+    // by boxlen * multiplier as SoftSrc / dibr.py:31-39, and its exact pixel ranges
     int tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
     if (live) {
       const T bx0 = tmin3(v[0], v[2], v[4]) - spad, by0 = tmin3(v[1], v[3], v[5]) - spad;
       const T bx1 = tmax3(v[0], v[2], v[4]) + spad, by1 = tmax3(v[1], v[3], v[5]) + spad;
-      T *q = sbbox + f * 4;
-      q[0] = bx0;
-      q[1] = by0;
-      q[2] = bx1;
-      q[3] = by1;
       int jx0, jx1, jy0, jy1;
-      axis_range((double)bx0, (double)bx1, (double)pp.sx, g.width, false, jx0, jx1);
-      axis_range((double)by0, (double)by1, (double)pp.sy, g.height, true, jy0, jy1);
-      if (jx0 <= jx1 && jy0 <= jy1) {
+      exact_range(bx0, bx1, pp.sx, pp.xinv, g.width, false, jx0, jx1);
+      exact_range(by0, by1, pp.sy, pp.yinv, g.height, true, jy0, jy1);
+      if (jx0 > jx1 || jy0 > jy1) {
+        jx0 = jy0 = 1;
+        jx1 = jy1 = 0;
+      } else {
         tx0 = jx0 / TILE_W;
         tx1 = jx1 / TILE_W;
         ty0 = jy0 / TILE_H;
         ty1 = jy1 / TILE_H;
       }
+      srng[f] = make_uint2((uint32_t)jx0 | ((uint32_t)jx1 << 16), (uint32_t)jy0 | ((uint32_t)jy1 << 16));
     }
     bin_mark(g, b, c, lane, tx0, tx1, ty0, ty1, sbitmap);
   }
@@ -1307,9 +1270,9 @@ namespace kl {
 // pass over the faces, counted by one bucket kernel and ordered by one order kernel.
 //   zeroed: raster bitmap | soft bitmap | raster ghist | soft ghist
 //   then:   face records | pixel ranges | raster buckets | soft buckets | raster items |
-//           item count | soft order | soft bboxes     (records and bboxes sized for f64)
+//           item count | soft order | soft pixel ranges     (records sized for f64)
 struct DibrFwdWs {
-  size_t off_sbm, off_rgh, off_sgh, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder, off_sbbox,
+  size_t off_sbm, off_rgh, off_sgh, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder, off_srng,
       bytes;
   DibrFwdWs(int B, int H, int W, int F) {
     const BinGeom g = make_bin_geom(B, H, W, F);
@@ -1326,8 +1289,8 @@ struct DibrFwdWs {
     off_items = up(off_sbk + nt);
     off_n = off_items + nt * TILE_H * sizeof(int32_t);
     off_sorder = up(off_n + sizeof(int));
-    off_sbbox = up(off_sorder + nt * sizeof(int32_t));
-    bytes = off_sbbox + (size_t)B * F * 4 * sizeof(double);
+    off_srng = up(off_sorder + nt * sizeof(int32_t));
+    bytes = off_srng + (size_t)B * F * sizeof(uint2);
   }
 };
 
@@ -1361,17 +1324,17 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   int32_t *items = reinterpret_cast<int32_t *>(w + L.off_items);
   int *nitems = reinterpret_cast<int *>(w + L.off_n);
   int32_t *sorder = reinterpret_cast<int32_t *>(w + L.off_sorder);
-  T *sbbox = reinterpret_cast<T *>(w + L.off_sbbox);
+  uint2 *srng = reinterpret_cast<uint2 *>(w + L.off_srng);
   KL_CHECK_RC(fill_async(w, 0, L.zero, st));
   const RastSrc<T> src{fvi, nullptr, (T)m, fnz};
   const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
   const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);
   if (fnz)
     hipLaunchKernelGGL((raster_bin_kernel<T, 2>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, rbm, rec, rng, sbm,
-                       sbbox, (T)pad);
+                       srng, (T)pad);
   else
     hipLaunchKernelGGL((raster_bin_kernel<T, 0>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, rbm, rec, rng, sbm,
-                       sbbox, (T)pad);
+                       srng, (T)pad);
   KL_CHECK_LAUNCH();
   hipLaunchKernelGGL(tile_bucket2_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)rbm,
                      (const uint32_t *)sbm, g.words, nt, rbk, sbk, rgh, sgh, s.scratch);
@@ -1384,7 +1347,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
                              reinterpret_cast<uint64_t *>(g_dev_debug)};
   hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
   KL_CHECK_LAUNCH();
-  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, sbm, sorder, sbbox,
+  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, sbm, sorder, srng,
                                    st);
 }
 

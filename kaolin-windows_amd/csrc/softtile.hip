@@ -40,7 +40,7 @@ constexpr int ST_LIST_CAP = 1024;  // face-list entries per workgroup (8 B each)
 template <typename T>
 struct SoftTileArgs {
   SoftSrc<T> src;            // unscaled face_vertices_image, multiplier, bbox pad
-  const T *bbox;             // (B*F,4) enlarged bboxes (stored by the binning pass)
+  const uint2 *rng;          // (B*F) exact pixel ranges of the enlarged bboxes (binning pass)
   const int64_t *sel;        // (B,H,W) rasterized face index
   const uint32_t *bitmap;
   const int32_t *order;      // tiles, heaviest first
@@ -88,9 +88,6 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   const bool px_valid = row_ok && i < W;
   const size_t pix = ((size_t)b * H + (row_ok ? j : H - 1)) * W + (i < W ? i : W - 1);
   const bool covered = px_valid ? (a.sel[pix] >= 0) : true;
-  const float m = a.m;
-  const float sx = m / (float)W, sy = m / (float)H, xinv = (float)W / m;  // pixel pitch as pix_x / pix_y
-  auto py = [&](int jj) { return (T)(sy * (float)(H - 2 * jj - 1)); };   // == pix_y<T>(m, H, jj)
   const int64_t f0 = (int64_t)b * a.F;
   uint64_t t0 = 0, t1 = 0, w0 = 0, c_fill = 0, c_walk = 0, c_sync = 0, tq = 0;
   uint64_t c_pf = 0, c_test = 0, c_s1 = 0, tr = 0;
@@ -112,64 +109,47 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   if (any) {
     ChunkSeq seq;
     seq.init(a.bitmap + ((size_t)(b * g.tiles_y + ty) * g.tiles_x + tx) * g.words, g.words, lane);
-    const T *bb = a.bbox + f0 * 4;
-    // this wave's chunk of the next step (chunk ordinal pos + wid) with its bboxes in flight
+    const uint2 *rg = a.rng + f0;
+    // this wave's chunk of the next step (chunk ordinal pos + wid) with its pixel ranges in
+    // flight: an unconditional load from a clamped index (a guarded load would be waited
+    // for at once), issued after the current step's ranges are tested so that no copy of
+    // the loaded registers is needed
     int pos = 0, nc = -1;
     bool nexists = false;
-    T nb0 = 0, nb1 = 0, nb2 = 0, nb3 = 0;
+    uint2 nr = make_uint2(1u, 1u);
     auto pf_next = [&]() {
       nexists = seq.at(pos, lane) >= 0;
       nc = nexists ? seq.at(pos + wid, lane) : -1;
       pos += R;
-      const int fl = nc * 64 + lane;
-      if (nc >= 0 && fl < a.F) {
-        if (sizeof(T) == 4) {
-          const float4 q4 = reinterpret_cast<const float4 *>(bb)[fl];
-          nb0 = (T)q4.x;
-          nb1 = (T)q4.y;
-          nb2 = (T)q4.z;
-          nb3 = (T)q4.w;
-        } else {
-          nb0 = bb[fl * 4 + 0];
-          nb1 = bb[fl * 4 + 1];
-          nb2 = bb[fl * 4 + 2];
-          nb3 = bb[fl * 4 + 3];
-        }
-      }
+      int fl = nc * 64 + lane;
+      fl = fl < 0 ? 0 : (fl < a.F ? fl : a.F - 1);
+      nr = rg[fl];
     };
     pf_next();
     bool more = nexists;
     while (true) {
       // ---- 1. expand candidate chunks into the face list, R chunks per step; the next
-      //         step's bboxes are in flight while this step's are tested
+      //         step's ranges are in flight while this step's entries are stored and walked
       int len = 0;
       if (dbg) tq = stamp_clk();
       while (more && len + R * 64 <= ST_LIST_CAP) {
         if (dbg) tr = stamp_clk();
         const int c = nc;
-        const T bx0 = nb0, by0 = nb1, bx1 = nb2, by1 = nb3;
-        pf_next();  // consumed by the next step, in this fill or after the drain
-        more = nexists;
+        const int fl = c * 64 + lane;
+        // the face's exact pixel ranges (bin pass) against the workgroup's rows / columns
+        const int ix0 = (int)(nr.x & 0xffffu), ix1 = (int)(nr.x >> 16);
+        const int iy0 = (int)(nr.y & 0xffffu), iy1 = (int)(nr.y >> 16);
+        const int ya = max(iy0, j0) - j0, yb = min(iy1, j0 + R - 1) - j0;
+        const uint32_t rows = ya <= yb ? ((2u << yb) - 1u) & ~((1u << ya) - 1u) : 0u;
+        const int lo = max(ix0 - ibase, 0), hi = min(ix1 - ibase, 63);
+        const bool keep = c >= 0 && fl < a.F && rows != 0 && lo <= hi;
         if (dbg) {
           const uint64_t t = stamp_clk();
           c_pf += t - tr;
           tr = t;
         }
-        bool keep = false;
-        int lo = 64, hi = -1;
-        uint32_t rows = 0;
-        const int fl = c * 64 + lane;
-        if (c >= 0 && fl < a.F) {
-          for (int r = 0; r < R; r++) {
-            const int jr = j0 + r;
-            if (jr < H) {
-              const T yr = py(jr);
-              if (!(yr < by0 || yr >= by1)) rows |= 1u << r;
-            }
-          }
-          if (rows) seg_range_s<T>(bx0, bx1, sx, xinv, W, ibase, lo, hi);
-          keep = rows != 0 && lo <= hi;
-        }
+        pf_next();  // consumed by the next step, in this fill or after the drain
+        more = nexists;
         const uint64_t km = ballot(keep);
         if (lane == 0) s_cnt[wid] = __popcll(km);
         if (dbg) {
@@ -581,17 +561,17 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
 }
 
 // workspace: bitmap | ghist[32], gdone (zeroed with the bitmap) | tile buckets | tile order |
-// bboxes (sized for f64)
+// pixel ranges
 struct StWs {
-  size_t hist, zero, bk, order, bbox, bytes;
+  size_t hist, zero, bk, order, rng, bytes;
   StWs(const BinGeom &g, int F) {
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
     hist = g.bytes();
     zero = hist + (ORD_BUCKETS + 1) * sizeof(int);
     bk = (zero + 255) & ~(size_t)255;
     order = (bk + nt + 255) & ~(size_t)255;
-    bbox = (order + nt * 4 + 255) & ~(size_t)255;
-    bytes = bbox + (size_t)g.batch * F * 4 * sizeof(double);
+    rng = (order + nt * 4 + 255) & ~(size_t)255;
+    bytes = rng + (size_t)g.batch * F * sizeof(uint2);
   }
 };
 
@@ -617,9 +597,9 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
   int *ghist = reinterpret_cast<int *>(w + L.hist);
   uint8_t *bk = reinterpret_cast<uint8_t *>(w + L.bk);
   int32_t *order = reinterpret_cast<int32_t *>(w + L.order);
-  T *bbox = reinterpret_cast<T *>(w + L.bbox);
+  uint2 *rng = reinterpret_cast<uint2 *>(w + L.rng);
   const SoftSrc<T> src{fvi, (T)m, (T)pad};
-  const int rc = launch_binning<T, SoftSrc<T>>(src, nullptr, F, g, m, bitmap, st, bbox, L.zero);
+  const int rc = launch_binning<T, SoftSrc<T>>(src, nullptr, F, g, m, bitmap, st, nullptr, L.zero, rng);
   if (rc) return rc;
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   const int identity = (g_dev_flags >> 12) & 1;  // dev ablation: no heaviest-first order
@@ -633,15 +613,16 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt,
                      order, identity, ORD_BUCKETS, 0, nullptr);
   KL_CHECK_LAUNCH();
-  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, sel, sigmainv, pad, m, mask, s, bitmap, order, bbox, st);
+  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, sel, sigmainv, pad, m, mask, s, bitmap, order, rng, st);
 }
 
 // The selection and evaluation kernels on bins made by the caller: bitmap (SoftSrc bins),
-// heaviest-first tile order and the enlarged bboxes; s.scratch already zeroed.
+// heaviest-first tile order and the exact pixel ranges of the enlarged bboxes; s.scratch
+// already zeroed.
 template <typename T>
 int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv,
                            double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
-                           const int32_t *order, const T *bbox, hipStream_t st) {
+                           const int32_t *order, const uint2 *rng, hipStream_t st) {
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   if (nt == 0) return KL_OK;
@@ -650,7 +631,7 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   const int dev_r = (g_dev_flags >> 8) & 15;  // dev override of the rows per workgroup (ablation)
   if (dev_r && dev_r <= R && TILE_H % dev_r == 0) R = dev_r;
   const SoftSrc<T> src{fvi, (T)m, (T)pad};
-  SoftTileArgs<T> args{src,      bbox, sel,  bitmap,  order,      g,          F,          K,
+  SoftTileArgs<T> args{src,      rng,  sel,  bitmap,  order,      g,          F,          K,
                        sigmainv, m,    mask, s.hits, s.rec_face, s.rec_prob, s.seg_tot, (uint64_t *)g_dev_debug};
   const size_t lds = st_head_lds() + st_wave_lds(K) * R;
   hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)(nt * (TILE_H / R))), dim3(64 * R), lds, st, args);
@@ -704,10 +685,10 @@ template int soft_tile_forward<double>(int, int, int, int, int, const double *, 
                                        float, double *, const SoftState<double> &, void *, size_t, hipStream_t);
 template int soft_tile_forward_main<float>(int, int, int, int, int, const float *, const int64_t *, float, double,
                                            float, float *, const SoftState<float> &, const uint32_t *,
-                                           const int32_t *, const float *, hipStream_t);
+                                           const int32_t *, const uint2 *, hipStream_t);
 template int soft_tile_forward_main<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
                                             float, double *, const SoftState<double> &, const uint32_t *,
-                                            const int32_t *, const double *, hipStream_t);
+                                            const int32_t *, const uint2 *, hipStream_t);
 template int soft_tile_backward<float>(int, int, int, int, int, const float *, const float *,
                                        const SoftState<float> &, const float *, float, float, float *, bool, void *,
                                        size_t, hipStream_t);
