@@ -366,8 +366,8 @@ __global__ void __launch_bounds__(256) soft_tile_eval_kernel(SoftTileArgs<T> a) 
 // Work items of the backward: per tile, the hits of its 8 rows taken row-major in pieces
 // of SB_PIECE (one hit per thread of a workgroup), so that the heavy tiles (the silhouette's
 // tight spots, ~10^4 hits) spread over many workgroups.  The plan kernel (one workgroup)
-// lists the items tile by tile from the forward's per-row-segment hit totals and zeroes
-// the item counter; the backward kernel is persistent and claims items in that order.
+// lists the items tile by tile from the forward's per-row-segment hit totals and writes
+// the item count; the backward kernel is persistent and takes the items round-robin.
 constexpr int SB_PIECE = 512;
 
 __global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restrict__ seg_tot, BinGeom g,
@@ -396,10 +396,7 @@ __global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restri
     for (int q = 0; q < np; q++) items[excl + q] = make_int2(t, q);
     carry += all;
   }
-  if (threadIdx.x == 0) {
-    ctl[0] = carry;
-    ctl[1] = 0;
-  }
+  if (threadIdx.x == 0) ctl[0] = carry;
 }
 
 // Per-face accumulation for one work item: LDS hash on the mesh-local face index with
@@ -473,7 +470,7 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
   __shared__ int s_key[HC];
   __shared__ T s_val[HC * 6];
   __shared__ int s_used[HC];
-  __shared__ int s_nused, s_item;
+  __shared__ int s_nused;
   __shared__ double s_a[TILE_H][64];
   __shared__ int s_pre[TILE_H][65];
   __shared__ int s_rowpre[TILE_H + 1];
@@ -488,11 +485,10 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
   const int nitems = ctl[0];
   const T ms = (T)multiplier;
   const float sx = multiplier / (float)W, sy = multiplier / (float)H;
-  while (true) {
-    __syncthreads();  // the previous item's hash reset / s_item reads are done
-    if (threadIdx.x == 0) s_item = atomicAdd(&ctl[1], 1);
-    __syncthreads();
-    const int q = s_item;
+  // items are taken round-robin (a claim counter's returning atomic costs more than the
+  // imbalance it removes: the items are pieces of at most SB_PIECE hits)
+  for (int q = (int)blockIdx.x;; q += (int)gridDim.x) {
+    __syncthreads();  // the previous item's hash reset is done
     if (q >= nitems) return;
     const int2 it = items[q];
     const int tile = it.x;
