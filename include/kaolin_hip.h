@@ -95,19 +95,20 @@ int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, int batch, 
                               float multiplier, float eps,
                               void *interpolated_features, int64_t *face_idx, void *output_weights,
                               void *workspace, size_t workspace_bytes, kl_stream stream);
-/* Atomic-free backward of the fused path: one thread per face gathers the pixels of the
- * exact pixel range the forward visited for it (same valid_faces / multiplier) whose
- * face_idx equals it (deterministic, row-major order).  Requires face_idx produced by
- * kl_dibr_rasterize_forward with the same valid_faces and multiplier.  Every face's gradient
- * is written (zeros where it won no pixel).  scratch: NULL, or a zeroed int32 the call uses
- * as its big-face counter instead of zeroing one in the workspace (kl_dibr_forward). */
+/* Atomic-free backward of the fused path: 8 lanes per face gather the pixels of the face's
+ * exact pixel range (the reference's bbox test, same valid_faces / multiplier as the forward)
+ * whose face_idx equals it (deterministic, row-major order).  Requires face_idx produced by
+ * the fused forward with the same valid_faces and multiplier.  Every face's gradient is
+ * written (zeros where it won no pixel).  scratch: NULL, or a zeroed int32 the call uses as
+ * its big-face counter instead of zeroing one in the workspace (kl_dibr_forward).
+ * face_ranges: NULL, or kl_dibr_forward's per-face ranges (then the ranges are not recomputed). */
 int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
                                const void *grad_interpolated_features, const int64_t *face_idx,
                                const void *output_weights, const void *face_vertices_image,
                                const void *face_features, const uint8_t *valid_faces, const void *face_normals_z,
                                float multiplier, float eps, void *grad_face_vertices_image,
-                               void *grad_face_features, int *scratch, void *workspace, size_t workspace_bytes,
-                               kl_stream stream);
+                               void *grad_face_features, int *scratch, const uint32_t *face_ranges,
+                               void *workspace, size_t workspace_bytes, kl_stream stream);
 
 size_t kl_soft_mask_workspace_bytes(int batch, int height, int width, int num_faces);
 
@@ -183,6 +184,8 @@ int kl_dibr_soft_mask_backward_compact(kl_dtype dtype, int batch, int height, in
  * rasterizer gather's big-face counter and leaves it zeroed, so it needs no fill).  The
  * backward writes grad_face_vertices_image / grad_face_features (every face): the
  * rasterizer's gather terms plus the soft-mask terms (grad_soft_mask may be NULL).
+ * face_ranges: NULL, or (B*F) x 2 uint32 the forward fills with each face's exact pixel
+ * ranges (x0 | x1 << 16, y0 | y1 << 16; empty for invalid faces) for the backward to reuse.
  * feat_dim <= 8.  Workspaces: kl_dibr_workspace_bytes (forward),
  * kl_dibr_bwd_workspace_bytes (backward). */
 size_t kl_dibr_workspace_bytes(int batch, int height, int width, int num_faces);
@@ -191,15 +194,16 @@ int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_fa
                     const void *face_vertices_z, const void *face_vertices_image, const void *face_features,
                     const void *face_normals_z, float sigmainv, double bbox_pad, float multiplier, float eps,
                     void *interpolated_features, int64_t *face_idx, void *output_weights, void *soft_mask,
-                    uint8_t *hits, uint32_t *rec_face, void *rec_prob, int *seg_tot, int *scratch, void *workspace,
-                    size_t workspace_bytes, kl_stream stream);
+                    uint8_t *hits, uint32_t *rec_face, void *rec_prob, int *seg_tot, int *scratch,
+                    uint32_t *face_ranges, void *workspace, size_t workspace_bytes, kl_stream stream);
 int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim, int knum,
                      const void *grad_interpolated_features, const void *grad_soft_mask, const int64_t *face_idx,
                      const void *output_weights, const void *face_vertices_image, const void *face_features,
                      const void *face_normals_z, const void *soft_mask, const uint8_t *hits,
                      const uint32_t *rec_face, const void *rec_prob, const int *seg_tot, float sigmainv,
                      float multiplier, float eps, void *grad_face_vertices_image, void *grad_face_features,
-                     int *scratch, void *workspace, size_t workspace_bytes, kl_stream stream);
+                     int *scratch, const uint32_t *face_ranges, void *workspace, size_t workspace_bytes,
+                     kl_stream stream);
 
 /* dibr_soft_mask.cpp:110-183  dibr_soft_mask_backward_cuda.
  * Output grad_face_vertices_image (B,F,3,2) (fully written). */

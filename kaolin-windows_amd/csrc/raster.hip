@@ -944,6 +944,16 @@ __device__ __forceinline__ bool face_range(const RastSrc<T> &src, int64_t tf, fl
   return ix0 <= ix1 && iy0 <= iy1;
 }
 
+// The forward's exact pixel ranges of a face (kl_dibr_forward's face_ranges), empty = invalid.
+__device__ __forceinline__ bool rng_range(const uint2 *rng, int64_t tf, int &ix0, int &ix1, int &iy0, int &iy1) {
+  const uint2 r = rng[tf];
+  ix0 = (int)(r.x & 0xffffu);
+  ix1 = (int)(r.x >> 16);
+  iy0 = (int)(r.y & 0xffffu);
+  iy1 = (int)(r.y >> 16);
+  return ix0 <= ix1 && iy0 <= iy1;
+}
+
 template <typename T, int MAXD>
 struct GatherAcc {
   T gi[6];
@@ -979,7 +989,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
     const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
     const T *__restrict__ nz, int B, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
-    T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig) {
+    T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig, const uint2 *__restrict__ rng) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t tf = t / LPF;  // LPF consecutive lanes per face (whole groups per wave)
   const int s = (int)(t % LPF);
@@ -991,7 +1001,8 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
   acc.zero();
   int ix0, ix1, iy0, iy1;
   bool queued = false;
-  if (in && src.valid(tf) && face_range(src, tf, m, H, W, ix0, ix1, iy0, iy1)) {
+  if (in && (rng ? rng_range(rng, tf, ix0, ix1, iy0, iy1)
+                 : (src.valid(tf) && face_range(src, tf, m, H, W, ix0, ix1, iy0, iy1)))) {
     if ((int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) > VIS_SMALL_AREA) {
       queued = true;
       if (s == 0) big[atomicAdd(nbig, 1)] = (int)tf;
@@ -1053,7 +1064,8 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
     const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
     const T *__restrict__ nz, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
-    T *__restrict__ grad_ffeat, const int *__restrict__ big, const int *__restrict__ nbig) {
+    T *__restrict__ grad_ffeat, const int *__restrict__ big, const int *__restrict__ nbig,
+    const uint2 *__restrict__ rng) {
   __shared__ T red[256];
   const int n = *nbig;
   const RastSrc<T> src{fvi, valid, (T)m, nz};
@@ -1065,7 +1077,10 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
 #pragma unroll
     for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
     int ix0, ix1, iy0, iy1;
-    face_range(src, tf, m, H, W, ix0, ix1, iy0, iy1);
+    if (rng)
+      rng_range(rng, tf, ix0, ix1, iy0, iy1);
+    else
+      face_range(src, tf, m, H, W, ix0, ix1, iy0, iy1);
     const int w = ix1 - ix0 + 1;
     const int64_t area = (int64_t)w * (iy1 - iy0 + 1);
     GatherAcc<T, MAXD> acc;
@@ -1117,14 +1132,14 @@ template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
                                      const T *w, const T *fvi, const T *feat, const uint8_t *valid, const T *nz,
                                      float m, float eps, T *gfvi, T *gfeat, int *big, int *nbig, bool zero_nbig,
-                                     hipStream_t st) {
+                                     const uint2 *rng, hipStream_t st) {
   if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
   hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st, grad,
-                     face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig);
+                     face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng);
   KL_CHECK_LAUNCH();
   hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(256), dim3(256), 0, st, grad, face_idx, w, fvi,
-                     feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig);
+                     feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
@@ -1135,7 +1150,7 @@ template <typename T>
 static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
                                 const void *w, const void *fvi, const void *feat, const uint8_t *valid, const T *nz,
                                 float m, float eps, void *gfvi, void *gfeat, void *ws, size_t ws_bytes, int *nbig,
-                                hipStream_t st) {
+                                hipStream_t st, const uint2 *rng = nullptr) {
   const int64_t nf = (int64_t)B * F;
   if (nf == 0) return KL_OK;
   KL_REQUIRE(ws_bytes >= (size_t)(nf + 1) * sizeof(int), "rasterize backward: workspace too small");
@@ -1149,10 +1164,10 @@ static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *g
   const T *ft = (const T *)feat;
   if (D <= 4)
     return rasterize_bwd_gather_maxd<T, 4>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, st);
+                                           (T *)gfeat, big, nbig, zero, rng, st);
   if (D <= 8)
     return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, st);
+                                           (T *)gfeat, big, nbig, zero, rng, st);
   // wide features: the scatter kernel
   return rasterize_bwd<T>(B, H, W, F, D, grad, face_idx, w, fvi, feat, eps, gfvi, gfeat, st);
 }
@@ -1245,15 +1260,17 @@ extern "C" int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height,
                                           int feat_dim, const void *grad, const int64_t *face_idx, const void *w,
                                           const void *fvi, const void *feat, const uint8_t *valid_faces,
                                           const void *fnz, float multiplier, float eps, void *gfvi, void *gfeat,
-                                          int *scratch, void *ws, size_t ws_bytes, kl_stream stream) {
+                                          int *scratch, const uint32_t *face_ranges, void *ws, size_t ws_bytes,
+                                          kl_stream stream) {
+  const uint2 *fr = reinterpret_cast<const uint2 *>(face_ranges);
   if (dtype == KL_F32)
     return rasterize_bwd_gather<float>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat,
                                        valid_faces, (const float *)fnz, multiplier, eps, gfvi, gfeat, ws, ws_bytes,
-                                       scratch, S(stream));
+                                       scratch, S(stream), fr);
   if (dtype == KL_F64)
     return rasterize_bwd_gather<double>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat,
                                         valid_faces, (const double *)fnz, multiplier, eps, gfvi, gfeat, ws, ws_bytes,
-                                        scratch, S(stream));
+                                        scratch, S(stream), fr);
   set_error("dibr_rasterize_backward not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -1297,7 +1314,8 @@ struct DibrFwdWs {
 template <typename T>
 static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, const T *fvi, const T *feat, const T *fnz,
                     float sigmainv, double pad, float m, float eps, T *out_feat, int64_t *out_idx, T *out_w,
-                    T *out_mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st) {
+                    T *out_mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st,
+                    uint2 *face_ranges) {
   const DibrFwdWs L(B, H, W, F);
   KL_REQUIRE(ws_bytes >= L.bytes, "dibr_rasterization forward: workspace too small");
   KL_REQUIRE(H < 65536 && W < 65536, "dibr_rasterization forward: height and width must be < 65536");
@@ -1306,6 +1324,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const size_t P = (size_t)B * H * W;
   if (P == 0) return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
   if (F == 0 || (g_dev_flags & (1 << 13))) {  // no faces (or dev: the separate pipelines)
+    KL_REQUIRE(face_ranges == nullptr || F == 0, "dibr_rasterization forward: face_ranges needs the combined path");
     KL_CHECK_RC(dibr_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, F, fvz, feat, m, eps, out_feat,
                                  out_idx, out_w, ws, ws_bytes, st));
     return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, ws, ws_bytes, st);
@@ -1318,7 +1337,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   int *rgh = reinterpret_cast<int *>(w + L.off_rgh);
   int *sgh = reinterpret_cast<int *>(w + L.off_sgh);
   T *rec = reinterpret_cast<T *>(w + L.off_rec);
-  uint2 *rng = reinterpret_cast<uint2 *>(w + L.off_rng);
+  uint2 *rng = face_ranges ? face_ranges : reinterpret_cast<uint2 *>(w + L.off_rng);
   uint8_t *rbk = reinterpret_cast<uint8_t *>(w + L.off_rbk);
   uint8_t *sbk = reinterpret_cast<uint8_t *>(w + L.off_sbk);
   int32_t *items = reinterpret_cast<int32_t *>(w + L.off_items);
@@ -1355,10 +1374,10 @@ template <typename T>
 static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat, const T *grad_mask,
                     const int64_t *face_idx, const T *w, const T *fvi, const T *feat, const T *fnz, const T *mask,
                     const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *ws,
-                    size_t ws_bytes, hipStream_t st) {
+                    size_t ws_bytes, hipStream_t st, const uint2 *face_ranges) {
   KL_REQUIRE(D <= 8, "dibr_rasterization backward: feature dimension > 8 is not supported by the fused path");
   KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
-                                      gfeat, ws, ws_bytes, s.scratch, st));
+                                      gfeat, ws, ws_bytes, s.scratch, st, face_ranges));
   return soft_tile_backward<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m, gfvi, true, ws, ws_bytes, st);
 }
 }  // namespace kl
@@ -1380,20 +1399,21 @@ extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width,
                                int knum, const void *fvz, const void *fvi, const void *feat, const void *fnz,
                                float sigmainv, double bbox_pad, float multiplier, float eps, void *out_feat,
                                int64_t *out_idx, void *out_w, void *out_mask, uint8_t *hits, uint32_t *rec_face,
-                               void *rec_prob, int *seg_tot, int *scratch, void *ws, size_t ws_bytes,
-                               kl_stream stream) {
+                               void *rec_prob, int *seg_tot, int *scratch, uint32_t *face_ranges, void *ws,
+                               size_t ws_bytes, kl_stream stream) {
+  uint2 *fr = reinterpret_cast<uint2 *>(face_ranges);
   if (dtype == KL_F32)
     return dibr_fwd<float>(batch, height, width, num_faces, feat_dim, knum, (const float *)fvz, (const float *)fvi,
                            (const float *)feat, (const float *)fnz, sigmainv, bbox_pad, multiplier, eps,
                            (float *)out_feat, out_idx, (float *)out_w, (float *)out_mask,
                            SoftState<float>{hits, rec_face, (float *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
-                           S(stream));
+                           S(stream), fr);
   if (dtype == KL_F64)
     return dibr_fwd<double>(batch, height, width, num_faces, feat_dim, knum, (const double *)fvz, (const double *)fvi,
                             (const double *)feat, (const double *)fnz, sigmainv, bbox_pad, multiplier, eps,
                             (double *)out_feat, out_idx, (double *)out_w, (double *)out_mask,
                             SoftState<double>{hits, rec_face, (double *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
-                            S(stream));
+                            S(stream), fr);
   set_error("dibr_rasterization not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -1403,20 +1423,22 @@ extern "C" int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width
                                 const void *w, const void *fvi, const void *feat, const void *fnz, const void *mask,
                                 const uint8_t *hits, const uint32_t *rec_face, const void *rec_prob,
                                 const int *seg_tot, float sigmainv, float multiplier, float eps, void *gfvi,
-                                void *gfeat, int *scratch, void *ws, size_t ws_bytes, kl_stream stream) {
+                                void *gfeat, int *scratch, const uint32_t *face_ranges, void *ws, size_t ws_bytes,
+                                kl_stream stream) {
+  const uint2 *fr = reinterpret_cast<const uint2 *>(face_ranges);
   if (dtype == KL_F32)
     return dibr_bwd<float>(
         batch, height, width, num_faces, feat_dim, knum, (const float *)grad_feat, (const float *)grad_mask, face_idx,
         (const float *)w, (const float *)fvi, (const float *)feat, (const float *)fnz, (const float *)mask,
         SoftState<float>{(uint8_t *)hits, (uint32_t *)rec_face, (float *)rec_prob, (int *)seg_tot, scratch},
-        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream));
+        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream), fr);
   if (dtype == KL_F64)
     return dibr_bwd<double>(
         batch, height, width, num_faces, feat_dim, knum, (const double *)grad_feat, (const double *)grad_mask,
         face_idx, (const double *)w, (const double *)fvi, (const double *)feat, (const double *)fnz,
         (const double *)mask,
         SoftState<double>{(uint8_t *)hits, (uint32_t *)rec_face, (double *)rec_prob, (int *)seg_tot, scratch},
-        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream));
+        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream), fr);
   set_error("dibr_rasterization backward not implemented for this dtype");
   return KL_E_INVALID;
 }

@@ -63,9 +63,10 @@ def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_
 
 
 def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_features, valid_faces, multiplier, eps,
-                       face_normals_z=None, scratch=None):
+                       face_normals_z=None, scratch=None, face_ranges=None):
     """Gather backward; valid_faces / face_normals_z / multiplier must be the forward's.
-    ``scratch``: the zeroed int32 of a compact soft-mask state (see soft_mask_forward_compact)."""
+    ``scratch``: the zeroed int32 of a compact soft-mask state (see soft_mask_forward_compact).
+    ``face_ranges``: the per-face pixel ranges dibr_forward returned (reused, not recomputed)."""
     func = 'rasterize backward'
     B, H, W, D = grad.shape
     F = face_vertices_image.shape[1]
@@ -80,8 +81,8 @@ def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_featur
         N.check(lib.kl_dibr_rasterize_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, N.ptr(grad.contiguous()), N.ptr(face_idx),
             N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), N.ptr(valid), N.ptr(fnz),
-            float(multiplier), float(eps), N.ptr(g_img), N.ptr(g_feat), N.ptr(scratch), N.ptr(ws), nbytes,
-            N.stream_of(dev)), func)
+            float(multiplier), float(eps), N.ptr(g_img), N.ptr(g_feat), N.ptr(scratch), N.ptr(face_ranges), N.ptr(ws),
+            nbytes, N.stream_of(dev)), func)
     return g_img, g_feat
 
 
@@ -200,7 +201,8 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
                  knum, multiplier, eps):
     """dibr_rasterization's forward in one call (kl_dibr_forward): rasterize with valid =
     face_normals_z >= 0 and the compact soft mask, sharing one binning pass.
-    -> features (B,H,W,D), face_idx (B,H,W), weights (B,H,W,3), soft_mask (B,H,W), SoftMaskState.
+    -> features (B,H,W,D), face_idx (B,H,W), weights (B,H,W,3), soft_mask (B,H,W), SoftMaskState,
+    face_ranges (B,F,2) int32 (each face's exact pixel ranges, for rasterize_backward).
     face_normals_z must have the dtype of face_vertices_image."""
     func = 'dibr_rasterization'
     N.require_gpu(func, face_vertices_z, face_vertices_image, face_normals_z)
@@ -226,12 +228,13 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     rec_prob = torch.empty(max(nrec, 1), dtype=dtype, device=dev)
     seg_tot = torch.empty(max(lib.kl_soft_mask_compact_segments(B, H, W), 1), dtype=torch.int32, device=dev)
     scratch = torch.empty(1, dtype=torch.int32, device=dev)
+    ranges = torch.empty((B, F, 2), dtype=torch.int32, device=dev)
     nbytes = lib.kl_dibr_workspace_bytes(B, H, W, F)
     ws = _ws(nbytes, dev)
     with torch.cuda.device(dev), N.timed('dibr_forward', dev):
         N.check(lib.kl_dibr_forward(
             N.dtype_code(dtype), B, H, W, F, D, K, N.ptr(fvz), N.ptr(fvi), N.ptr(feat), N.ptr(fnz), float(sigmainv),
             float(boxlen * multiplier), float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w),
-            N.ptr(mask), N.ptr(hits), N.ptr(rec_face), N.ptr(rec_prob), N.ptr(seg_tot), N.ptr(scratch), N.ptr(ws),
-            nbytes, N.stream_of(dev)), func)
-    return feats, idx, w, mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, scratch, K)
+            N.ptr(mask), N.ptr(hits), N.ptr(rec_face), N.ptr(rec_prob), N.ptr(seg_tot), N.ptr(scratch),
+            N.ptr(ranges if F > 0 else None), N.ptr(ws), nbytes, N.stream_of(dev)), func)
+    return feats, idx, w, mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, scratch, K), ranges

@@ -65,10 +65,11 @@ class DibrRasterizationCuda(Function):
         face_features = face_features.contiguous()
         face_normals_z = face_normals_z.detach().contiguous()
         if face_normals_z.dtype == face_vertices_image.dtype:  # one call, one shared binning pass
-            feats, face_idx, weights, soft_mask, state = _fused.dibr_forward(
+            feats, face_idx, weights, soft_mask, state, ranges = _fused.dibr_forward(
                 height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z, sigmainv, boxlen,
                 knum, multiplier, eps)
         else:
+            ranges = None
             feats, face_idx, weights = _fused.rasterize_forward(height, width, face_vertices_z, face_vertices_image,
                                                                 face_features, None, multiplier, eps,
                                                                 face_normals_z=face_normals_z)
@@ -76,19 +77,20 @@ class DibrRasterizationCuda(Function):
                                                                 multiplier)
         ctx.mark_non_differentiable(face_idx)
         ctx.sigmainv, ctx.multiplier, ctx.eps, ctx.knum = sigmainv, multiplier, eps, state.knum
+        ctx.has_ranges = ranges is not None and ranges.numel() > 0
         ctx.save_for_backward(face_idx, weights, face_vertices_image, face_features, face_normals_z, soft_mask,
-                              *state.tensors())
+                              ranges if ctx.has_ranges else None, *state.tensors())
         return feats, soft_mask, face_idx
 
     @staticmethod
     def backward(ctx, grad_feats, grad_soft_mask, grad_face_idx):
-        face_idx, weights, fvi, feat, fnz, soft_mask, *st = ctx.saved_tensors
+        face_idx, weights, fvi, feat, fnz, soft_mask, ranges, *st = ctx.saved_tensors
         state = _fused.SoftMaskState(*st, ctx.knum)
         scratch = state.scratch
         if grad_feats is None:
             grad_feats = torch.zeros(face_idx.shape + (feat.shape[-1],), dtype=feat.dtype, device=feat.device)
         g_img, g_feat = _fused.rasterize_backward(grad_feats, face_idx, weights, fvi, feat, None, ctx.multiplier,
-                                                  ctx.eps, face_normals_z=fnz, scratch=scratch)
+                                                  ctx.eps, face_normals_z=fnz, scratch=scratch, face_ranges=ranges)
         if grad_soft_mask is not None:
             _fused.soft_mask_backward_compact(grad_soft_mask, soft_mask, state, fvi, ctx.sigmainv, ctx.multiplier,
                                               out=g_img)
