@@ -1290,7 +1290,7 @@ namespace kl {
 //           item count | soft order | soft pixel ranges     (records sized for f64)
 struct DibrFwdWs {
   size_t off_sbm, off_rgh, off_sgh, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder, off_srng,
-      bytes;
+      off_defer, bytes;
   DibrFwdWs(int B, int H, int W, int F) {
     const BinGeom g = make_bin_geom(B, H, W, F);
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
@@ -1307,7 +1307,8 @@ struct DibrFwdWs {
     off_n = off_items + nt * TILE_H * sizeof(int32_t);
     off_sorder = up(off_n + sizeof(int));
     off_srng = up(off_sorder + nt * sizeof(int32_t));
-    bytes = off_srng + (size_t)B * F * sizeof(uint2);
+    off_defer = up(off_srng + (size_t)B * F * sizeof(uint2));
+    bytes = off_defer + (size_t)B * H * g.tiles_x;
   }
 };
 
@@ -1366,8 +1367,9 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
                              reinterpret_cast<uint64_t *>(g_dev_debug)};
   hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
   KL_CHECK_LAUNCH();
+  uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.off_defer);
   return soft_tile_forward_main<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, sbm, sorder, srng,
-                                   st);
+                                   defer, st);
 }
 
 template <typename T>

@@ -37,6 +37,9 @@
 namespace kl {
 
 constexpr int ST_LIST_CAP = 1024;  // face-list entries per workgroup (8 B each)
+#ifndef ST_EVAL_INLINE
+#define ST_EVAL_INLINE (1 << 30)  // workgroups with at most this many hits evaluate them inline
+#endif
 template <typename T>
 struct SoftTileArgs {
   SoftSrc<T> src;            // unscaled face_vertices_image, multiplier, bbox pad
@@ -52,7 +55,9 @@ struct SoftTileArgs {
   uint32_t *rec_face;        // per row segment s: [s*64*K, s*64*K + hits of the segment)
   T *rec_prob;
   int *seg_tot;              // per row segment: its number of hits
+  uint8_t *defer;            // per row segment: its hits are left to soft_tile_eval_kernel
   uint64_t *dbg;             // dev stamps (kl_dev_set_debug), 12 per wave, or nullptr
+  int dev;                   // dev ablation flags (kl_dev_set_flags), 0 in the product path
 };
 
 __host__ __device__ constexpr size_t st_wave_lds(int K) { return (size_t)K * 64 * sizeof(uint32_t) + 128 * sizeof(int); }
@@ -232,8 +237,9 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   if (!px_valid) kid = 0;
   if (dbg) t1 = stamp_clk();
 
-  // ---- 3. the row's hits (face ids, (pixel, slot) order) -> records; the evaluation
-  //         runs in soft_tile_eval_kernel, where heavy rows spread over the whole chip
+  // ---- 3. the row's hits ((pixel, slot) order) -> records.  Workgroups with few hits
+  //         evaluate them here (f32); the others leave face ids for soft_tile_eval_kernel,
+  //         where the heavy rows spread over the whole chip, and flag their rows for it.
   int pre = kid;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -242,21 +248,78 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   }
   const int total = __shfl(pre, 63);
   s_pre[lane] = pre - kid;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (lane == 0) s_cnt[wid] = total;
+  __syncthreads();
+  int wg_total = 0;
+  for (int w = 0; w < R; w++) wg_total += s_cnt[w];
+  const bool inline_eval = sizeof(T) == 4 && K > 0 && wg_total <= ST_EVAL_INLINE;
   const size_t rbase = ((size_t)(b * H + (row_ok ? j : 0)) * g.tiles_x + tx) * 64 * (size_t)K;
-  for (int e = lane; e < total; e += 64) {
-    int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
+  if (inline_eval) {
+    // the eval kernel's arithmetic, face ids straight from the slot lists; each slot's
+    // probability replaces its face id in place (same lane, same slot)
+    T *s_prob = reinterpret_cast<T *>(s_face);
+    const float m = a.m;
+    const float sx = m / (float)W, sy = m / (float)H;
+    const T y0 = (T)(sy * (float)(H - 2 * (row_ok ? j : 0) - 1));  // == pix_y
+    constexpr int U = 4;
+    for (int e0 = lane; e0 < total; e0 += 64 * U) {
+      int pp[U], kk[U];
+      uint32_t ff[U];
 #pragma unroll
-    for (int st = 32; st > 0; st >>= 1)
-      if (s_pre[lo + st] <= e) lo += st;
-    a.rec_face[rbase + e] = s_face[(e - s_pre[lo]) * 64 + lo];
+      for (int u = 0; u < U; u++) {
+        const int e = e0 + 64 * u;
+        int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+          if (s_pre[lo + st] <= e) lo += st;
+        pp[u] = lo;
+        kk[u] = e - s_pre[lo];
+        ff[u] = e < total ? s_face[kk[u] * 64 + lo] : 0u;
+      }
+      T v[U][6];
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (e0 + 64 * u < total) a.src.verts(f0 + ff[u], v[u]);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int e = e0 + 64 * u;
+        if (e < total) {
+          T dsq;
+          int edgeid;
+          soft_dist<T>((T)(sx * (float)(2 * (ibase + pp[u]) + 1 - W)), y0, v[u], m, dsq, edgeid);
+          const T z = (T)a.sigmainv * dsq / (T)m / (T)m;
+          const T pr = kl_exp<T>(-z);
+          a.rec_face[rbase + e] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
+          a.rec_prob[rbase + e] = pr;
+          s_prob[kk[u] * 64 + pp[u]] = pr;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (px_valid && kid > 0) {
+      // 1 - prod(1 - p) in double, slot order (dibr_soft_mask_cuda.cu:174-182)
+      T allprob = (T)1.0;
+      for (int k = 0; k < kid; k++) allprob = (T)((double)allprob * (1.0 - (double)s_prob[k * 64 + lane]));
+      a.mask[pix] = (T)(1.0 - (double)allprob);
+    }
+  } else {
+    for (int e = lane; e < total; e += 64) {
+      int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (s_pre[lo + st] <= e) lo += st;
+      a.rec_face[rbase + e] = s_face[(e - s_pre[lo]) * 64 + lo];
+    }
   }
   if (px_valid) {
     a.hits[pix] = (uint8_t)kid;
     if (kid == 0) a.mask[pix] = covered ? (T)1.0 : (T)0.0;  // 1 - prod over no slots = 0
   }
-  if (row_ok && lane == 0) a.seg_tot[(size_t)(b * H + j) * g.tiles_x + tx] = total;
+  if (row_ok && lane == 0) {
+    a.seg_tot[(size_t)(b * H + j) * g.tiles_x + tx] = total;
+    a.defer[(size_t)(b * H + j) * g.tiles_x + tx] = inline_eval ? 0 : 1;
+  }
   if (dbg && lane == 0) {
     uint64_t *d = dbg + ((size_t)blockIdx.x * R + wid) * 12;
     d[8] = c_fill;
@@ -297,6 +360,7 @@ __global__ void __launch_bounds__(256) soft_tile_eval_kernel(SoftTileArgs<T> a) 
   const int b = tile / (g.tiles_x * g.tiles_y);
   const int j = ty * TILE_H + (blockIdx.x % per_tile) * R + wid;
   if (j >= H) return;
+  if (!a.defer[(size_t)(b * H + j) * g.tiles_x + tx]) return;  // evaluated by the selection kernel
   const int ibase = tx * TILE_W;
   const int i = ibase + lane;
   const bool px_valid = i < W;
@@ -341,9 +405,12 @@ __global__ void __launch_bounds__(256) soft_tile_eval_kernel(SoftTileArgs<T> a) 
     for (int u = 0; u < U; u++) {
       const int e = e0 + 64 * u;
       if (e < total) {
-        T dsq;
-        int edgeid;
-        soft_dist<T>((T)(sx * (float)(2 * (ibase + pp[u]) + 1 - W)), y0, v[u], m, dsq, edgeid);
+        T dsq = (T)0;
+        int edgeid = 0;
+        if (!(a.dev & (1 << 20)))
+          soft_dist<T>((T)(sx * (float)(2 * (ibase + pp[u]) + 1 - W)), y0, v[u], m, dsq, edgeid);
+        else
+          dsq = v[u][0] + v[u][1] + v[u][2] + v[u][3] + v[u][4] + v[u][5];
         const T z = (T)a.sigmainv * dsq / (T)m / (T)m;
         const T pr = kl_exp<T>(-z);
         a.rec_face[rbase + e] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
@@ -559,7 +626,7 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
 // workspace: bitmap | ghist[32], gdone (zeroed with the bitmap) | tile buckets | tile order |
 // pixel ranges
 struct StWs {
-  size_t hist, zero, bk, order, rng, bytes;
+  size_t hist, zero, bk, order, rng, defer, bytes;
   StWs(const BinGeom &g, int F) {
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
     hist = g.bytes();
@@ -567,7 +634,8 @@ struct StWs {
     bk = (zero + 255) & ~(size_t)255;
     order = (bk + nt + 255) & ~(size_t)255;
     rng = (order + nt * 4 + 255) & ~(size_t)255;
-    bytes = rng + (size_t)g.batch * F * sizeof(uint2);
+    defer = (rng + (size_t)g.batch * F * sizeof(uint2) + 255) & ~(size_t)255;
+    bytes = defer + (size_t)g.batch * g.height * g.tiles_x;
   }
 };
 
@@ -609,7 +677,8 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt,
                      order, identity, ORD_BUCKETS, 0, nullptr);
   KL_CHECK_LAUNCH();
-  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, sel, sigmainv, pad, m, mask, s, bitmap, order, rng, st);
+  uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.defer);
+  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, sel, sigmainv, pad, m, mask, s, bitmap, order, rng, defer, st);
 }
 
 // The selection and evaluation kernels on bins made by the caller: bitmap (SoftSrc bins),
@@ -618,7 +687,7 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
 template <typename T>
 int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv,
                            double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
-                           const int32_t *order, const uint2 *rng, hipStream_t st) {
+                           const int32_t *order, const uint2 *rng, uint8_t *defer, hipStream_t st) {
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   if (nt == 0) return KL_OK;
@@ -628,11 +697,12 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   if (dev_r && dev_r <= R && TILE_H % dev_r == 0) R = dev_r;
   const SoftSrc<T> src{fvi, (T)m, (T)pad};
   SoftTileArgs<T> args{src,      rng,  sel,  bitmap,  order,      g,          F,          K,
-                       sigmainv, m,    mask, s.hits, s.rec_face, s.rec_prob, s.seg_tot, (uint64_t *)g_dev_debug};
+                       sigmainv, m,    mask, s.hits, s.rec_face, s.rec_prob, s.seg_tot, defer,
+                       (uint64_t *)g_dev_debug, g_dev_flags};
   const size_t lds = st_head_lds() + st_wave_lds(K) * R;
   hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)(nt * (TILE_H / R))), dim3(64 * R), lds, st, args);
   KL_CHECK_LAUNCH();
-  if (K > 0) {
+  if (K > 0 && (sizeof(T) != 4 || ST_EVAL_INLINE < (1 << 30))) {  // rows left for the eval kernel
     const size_t ew = (size_t)K * 64 * sizeof(T) + 64 * sizeof(int);
     int RE = 4;
     while (RE > 1 && ew * RE > 64 * 1024) RE >>= 1;
@@ -681,10 +751,10 @@ template int soft_tile_forward<double>(int, int, int, int, int, const double *, 
                                        float, double *, const SoftState<double> &, void *, size_t, hipStream_t);
 template int soft_tile_forward_main<float>(int, int, int, int, int, const float *, const int64_t *, float, double,
                                            float, float *, const SoftState<float> &, const uint32_t *,
-                                           const int32_t *, const uint2 *, hipStream_t);
+                                           const int32_t *, const uint2 *, uint8_t *, hipStream_t);
 template int soft_tile_forward_main<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
                                             float, double *, const SoftState<double> &, const uint32_t *,
-                                            const int32_t *, const uint2 *, hipStream_t);
+                                            const int32_t *, const uint2 *, uint8_t *, hipStream_t);
 template int soft_tile_backward<float>(int, int, int, int, int, const float *, const float *,
                                        const SoftState<float> &, const float *, float, float, float *, bool, void *,
                                        size_t, hipStream_t);
