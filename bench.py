@@ -193,12 +193,12 @@ def op_bytes(name, inp, stats):
 # kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
 OP_KERNELS = {
     'dibr_soft_mask_forward': ('bin_faces_kernel<float, kl::SoftSrc', 'tile_bucket_kernel', 'tile_order_kernel',
-                               'soft_tile_fwd_kernel<float', 'soft_tile_eval_kernel<float'),
+                               'soft_tile_fwd_kernel<float'),
     'dibr_soft_mask_backward': ('soft_bwd_plan_kernel', 'soft_tile_bwd_kernel<float'),
     'dibr_rasterize_forward': ('raster_bin_kernel<float, 2>', 'tile_bucket_kernel', 'tile_order_kernel',
                                'raster_tile_kernel<float'),
     'dibr_forward': ('raster_bin_kernel<float, 2>', 'tile_bucket2_kernel', 'tile_order2_kernel', 'raster_tile_kernel<float',
-                     'soft_tile_fwd_kernel<float', 'soft_tile_eval_kernel<float'),
+                     'soft_tile_fwd_kernel<float'),
     'dibr_rasterize_backward': ('rasterize_bwd_gather_kernel<float', 'rasterize_bwd_bigface_kernel<float'),
 }
 

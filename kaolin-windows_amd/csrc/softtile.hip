@@ -37,9 +37,6 @@
 namespace kl {
 
 constexpr int ST_LIST_CAP = 1024;  // face-list entries per workgroup (8 B each)
-#ifndef ST_EVAL_INLINE
-#define ST_EVAL_INLINE (1 << 30)  // workgroups with at most this many hits evaluate them inline
-#endif
 template <typename T>
 struct SoftTileArgs {
   SoftSrc<T> src;            // unscaled face_vertices_image, multiplier, bbox pad
@@ -237,9 +234,10 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   if (!px_valid) kid = 0;
   if (dbg) t1 = stamp_clk();
 
-  // ---- 3. the row's hits ((pixel, slot) order) -> records.  Workgroups with few hits
-  //         evaluate them here (f32); the others leave face ids for soft_tile_eval_kernel,
-  //         where the heavy rows spread over the whole chip, and flag their rows for it.
+  // ---- 3. the row's hits ((pixel, slot) order) -> records, evaluated here (f32: the heavy
+  //         tiles run first, so their evaluation overlaps the light tiles' selection -- a
+  //         separate evaluation kernel measured 32 us against 10 us added here); f64 leaves
+  //         face ids for soft_tile_eval_kernel and flags its rows for it.
   int pre = kid;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -248,11 +246,9 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   }
   const int total = __shfl(pre, 63);
   s_pre[lane] = pre - kid;
-  if (lane == 0) s_cnt[wid] = total;
-  __syncthreads();
-  int wg_total = 0;
-  for (int w = 0; w < R; w++) wg_total += s_cnt[w];
-  const bool inline_eval = sizeof(T) == 4 && K > 0 && wg_total <= ST_EVAL_INLINE;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  const bool inline_eval = sizeof(T) == 4 && K > 0;
   const size_t rbase = ((size_t)(b * H + (row_ok ? j : 0)) * g.tiles_x + tx) * 64 * (size_t)K;
   if (inline_eval) {
     // the eval kernel's arithmetic, face ids straight from the slot lists; each slot's
@@ -702,7 +698,7 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   const size_t lds = st_head_lds() + st_wave_lds(K) * R;
   hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)(nt * (TILE_H / R))), dim3(64 * R), lds, st, args);
   KL_CHECK_LAUNCH();
-  if (K > 0 && (sizeof(T) != 4 || ST_EVAL_INLINE < (1 << 30))) {  // rows left for the eval kernel
+  if (K > 0 && sizeof(T) != 4) {  // f64: the rows left for the evaluation kernel
     const size_t ew = (size_t)K * 64 * sizeof(T) + 64 * sizeof(int);
     int RE = 4;
     while (RE > 1 && ew * RE > 64 * 1024) RE >>= 1;
