@@ -110,19 +110,33 @@ def max_over_ranks(elapsed, device, world):
     return float(t)
 
 
+def loss_dot2(a, ga, b, gb, inp):
+    """L = <a, ga> + <b, gb> in one launch (kl_loss_dot2: fp64 accumulation, deterministic; two
+    torch.dot calls plus their add were four launches, ~25 us per step)."""
+    if os.environ.get('KL_BENCH_TORCH_LOSS'):  # dev A/B: the two-torch.dot loss
+        with torch.no_grad():
+            return torch.dot(a.reshape(-1), ga.reshape(-1)) + torch.dot(b.reshape(-1), gb.reshape(-1))
+    if 'loss_ws' not in inp:
+        inp['loss_ws'] = torch.zeros(_native.lib().kl_loss_dot2_workspace_bytes(), dtype=torch.uint8, device=a.device)
+    out = torch.empty(1, dtype=torch.float32, device=a.device)
+    _native.check(_native.lib().kl_loss_dot2(_native.ptr(a), _native.ptr(ga), a.numel(), _native.ptr(b),
+                                             _native.ptr(gb), b.numel(), _native.ptr(inp['loss_ws']),
+                                             _native.ptr(out), _native.stream_of(a.device)), 'kl_loss_dot2')
+    return out[0]
+
+
 def dibr_compute(inp):
     """dibr_rasterization forward + the loss L = <features, g_feat> + <soft_mask, g_mask> + backward
     (everything but the collective).  dL/dfeatures = g_feat and dL/dsoft_mask = g_mask exactly, so the
     backward is driven with them directly (torch.autograd.backward) -- the same gradients as
-    L.backward() without the broadcast kernels of the sum's backward; L itself is two dot products."""
+    L.backward() without the broadcast kernels of the sum's backward; L itself is two dot products
+    (one fused launch, loss_dot2)."""
     fvi = inp['fvi'].detach().requires_grad_(True)
     feat = inp['feat'].detach().requires_grad_(True)
     feats, mask, idx = kal.render.mesh.dibr_rasterization(inp['H'], inp['W'], inp['fvz'], fvi, feat, inp['fnz'],
                                                           sigmainv=7000, boxlen=0.02, knum=30, multiplier=1000,
                                                           eps=1e-8)
-    with torch.no_grad():
-        loss = torch.dot(feats.reshape(-1), inp['g_feat'].reshape(-1)) + \
-            torch.dot(mask.reshape(-1), inp['g_mask'].reshape(-1))
+    loss = loss_dot2(feats.detach(), inp['g_feat'], mask.detach(), inp['g_mask'], inp)
     torch.autograd.backward([feats, mask], [inp['g_feat'], inp['g_mask']])
     return loss, fvi.grad, feat.grad, mask, idx
 

@@ -51,6 +51,14 @@ typedef void *(*kl_alloc_fn)(void *ctx, size_t bytes);
 const char *kl_last_error(void);
 int kl_abi_version(void);
 
+/* Training-loop helper, not a reference op (bench.py's loss):
+ *   out[0] = <a, ga> + <b, gb>   (fp32 inputs, fp64 accumulation, deterministic order).
+ * ws: kl_loss_dot2_workspace_bytes() bytes of scratch (no initialisation needed).
+ * Two launches (per-block partials, then their ordered sum). */
+size_t kl_loss_dot2_workspace_bytes(void);
+int kl_loss_dot2(const float *a, const float *ga, int64_t na, const float *b, const float *gb, int64_t nb, void *ws,
+                 float *out, kl_stream stream);
+
 /* ---------------------------------------------------------------- DIB-R */
 
 /* Workspace of packed_rasterize_forward: the per-pixel visibility buffer (13 B/px) and a
@@ -284,6 +292,37 @@ int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int16_t *point
 /* raytrace.cpp:216-240 mark_pack_boundaries_cuda: boundaries (N) int32 (1 at pack starts). */
 int kl_mark_pack_boundaries(kl_dtype dtype, int64_t num, const void *pack_ids, int32_t *boundaries,
                             kl_stream stream);
+
+/* Packed ray ops (render/spc/raytrace.py:86-296).  feats (num_feats, feat_dim) row-major in
+ * f16 / f32 / f64; a pack is the run of rows [pack_indices[p], pack_indices[p+1]), the last
+ * one ending at num_feats.  Rows before the first pack keep the reference's initial value
+ * (0; 1 for cumprod), which these calls write.  Every output element is written. */
+
+/* raytrace.cpp:285-309 diff_cuda (pack_indices int64): out[i] = feats[i+1] - feats[i]
+ * inside a pack, 0 on a pack's last row. */
+int kl_pack_diff(kl_dtype dtype, int64_t num_feats, int64_t feat_dim, const void *feats,
+                 const int64_t *pack_indices, int64_t num_packs, void *out, kl_stream stream);
+
+/* raytrace.cpp:354-377 cumsum_cuda / :380-402 cumprod_cuda (pack_indices int32), with the
+ * reference kernels' exclusive / reverse semantics (raytrace_cuda.cu:391-483). */
+int kl_pack_cumsum(kl_dtype dtype, int64_t num_feats, int64_t feat_dim, const void *feats,
+                   const int32_t *pack_indices, int64_t num_packs, int exclusive, int reverse, void *out,
+                   kl_stream stream);
+int kl_pack_cumprod(kl_dtype dtype, int64_t num_feats, int64_t feat_dim, const void *feats,
+                    const int32_t *pack_indices, int64_t num_packs, int exclusive, int reverse, void *out,
+                    kl_stream stream);
+
+/* raytrace.cpp:311-325 inclusive_sum_cuda: out = inclusive prefix sum of info (int32).
+ * ws: kl_inclusive_sum_workspace_bytes(num) bytes of scratch. */
+size_t kl_inclusive_sum_workspace_bytes(int64_t num);
+int kl_inclusive_sum_i32(int64_t num, const int32_t *info, int32_t *out, void *ws, size_t ws_bytes,
+                         kl_stream stream);
+
+/* raytrace.cpp:328-351 sum_reduce_cuda: out (num_out, feat_dim), row r = the sum of the rows i
+ * with inclusive_sum[i] == r + 1, added in row order (deterministic; the reference used
+ * unordered atomics).  num_out = inclusive_sum[num_feats - 1] in the reference. */
+int kl_sum_reduce(kl_dtype dtype, int64_t num_feats, int64_t feat_dim, const void *feats,
+                  const int32_t *inclusive_sum, int64_t num_out, void *out, kl_stream stream);
 
 /* ------------------------------------------------------------ voxelgrid */
 

@@ -33,6 +33,8 @@ _PP = ctypes.POINTER(ctypes.c_void_p)
 _SIGS = {
     'kl_last_error': (ctypes.c_char_p, []),
     'kl_abi_version': (_I, []),
+    'kl_loss_dot2_workspace_bytes': (ctypes.c_size_t, []),
+    'kl_loss_dot2': (_I, [_P, _P, _I64, _P, _P, _I64, _P, _P, _P]),
     'kl_rasterize_workspace_bytes': (_SZ, [_I, _I, _I, _I64]),
     'kl_packed_rasterize_forward': (_I, [_I, _I, _I, _I, _I64, _I, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P,
                                          _SZ, _P]),
@@ -76,6 +78,12 @@ _SIGS = {
     'kl_raytrace': (_I, [_P, _I64, _P, _I64, _P, _I, _P, _P, _I64, ctypes.c_uint32, _I, _I, ALLOC_FN, _P, _PP, _PP,
                          ctypes.POINTER(_I64), _P]),
     'kl_mark_pack_boundaries': (_I, [_I, _I64, _P, _P, _P]),
+    'kl_pack_diff': (_I, [_I, _I64, _I64, _P, _P, _I64, _P, _P]),
+    'kl_pack_cumsum': (_I, [_I, _I64, _I64, _P, _P, _I64, _I, _I, _P, _P]),
+    'kl_pack_cumprod': (_I, [_I, _I64, _I64, _P, _P, _I64, _I, _I, _P, _P]),
+    'kl_inclusive_sum_workspace_bytes': (_SZ, [_I64]),
+    'kl_inclusive_sum_i32': (_I, [_I64, _P, _P, _P, _SZ, _P]),
+    'kl_sum_reduce': (_I, [_I, _I64, _I64, _P, _P, _I64, _P, _P]),
     'kl_voxelgrid_mark': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
     'kl_voxelgrid_mark_f64': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
 }

@@ -757,3 +757,19 @@ def test_raytrace_vs_oracle_mesh_spc(kal, with_exit):
     assert np.array_equal(np.stack([A(r), A(p)], -1), onug)
     assert np.array_equal(A(dep), odep)
     assert len(onug) > 1000
+
+
+@pytest.mark.parametrize('na,nb', [(0, 5), (7, 0), (3145728, 1048576), (1001, 333)])
+def test_loss_dot2(kal, na, nb):
+    """bench.py's fused loss helper (kl_loss_dot2) vs an fp64 torch dot; replays reuse the workspace."""
+    from kaolin import _native
+    g = torch.Generator(device='cpu').manual_seed(3)
+    a, ga, b, gb = (torch.rand(n, generator=g).to(DEV) for n in (na, na, nb, nb))
+    ws = torch.zeros(_native.lib().kl_loss_dot2_workspace_bytes(), dtype=torch.uint8, device=DEV)
+    ref = float(a.double() @ ga.double() + b.double() @ gb.double())
+    for _ in range(3):
+        out = torch.full((1,), float('nan'), device=DEV)
+        _native.check(_native.lib().kl_loss_dot2(_native.ptr(a), _native.ptr(ga), na, _native.ptr(b), _native.ptr(gb),
+                                                 nb, _native.ptr(ws), _native.ptr(out), _native.stream_of(a.device)),
+                      'kl_loss_dot2')
+        assert abs(float(out) - ref) <= 1e-6 * max(1.0, abs(ref))
