@@ -433,6 +433,95 @@ def mark_pack_boundaries_cuda(pack_ids):
     return out
 
 
+_HALF_FLOATS = (torch.float16, torch.float32, torch.float64)
+
+
+def _check_scalar_types(func, a, allowed):
+    """at::checkScalarTypes / at::checkScalarType message."""
+    if a.t.dtype not in allowed:
+        names = ', '.join(_tname(d) for d in allowed)
+        what = f'one of {names}' if len(allowed) > 1 else names
+        raise RuntimeError(f"Expected scalar type of argument #{a.pos} '{a.name}' to be {what}; but got "
+                           f"{_tname(a.t.dtype)} (while checking arguments for {func})")
+
+
+def _pack_args(func, feats, idx, idx_name, idx_dtype):
+    a, b = Arg(feats, 'feats', 1), Arg(idx, idx_name, 2)
+    check_dim(func, a, 2)
+    check_dim(func, b, 1)
+    check_all_same_gpu(func, [a, b])
+    check_contiguous(func, [a, b])
+    _check_scalar_types(func, a, _HALF_FLOATS)
+    _check_scalar_types(func, b, (idx_dtype,))
+
+
+def diff_cuda(feats, pack_indices):
+    """raytrace.cpp:285-309."""
+    func = 'diff_cuda'
+    _pack_args(func, feats, pack_indices, 'pack_indices', torch.int64)
+    out = torch.empty_like(feats)
+    dev = feats.device
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_pack_diff(N.dtype_code(feats.dtype), feats.shape[0], feats.shape[1], N.ptr(feats),
+                                     N.ptr(pack_indices), pack_indices.shape[0], N.ptr(out), N.stream_of(dev)), func)
+    return out
+
+
+def inclusive_sum_cuda(info):
+    """raytrace.cpp:311-325."""
+    func = 'inclusive_sum_cuda'
+    a = Arg(info, 'info', 1)
+    check_dim(func, a, 1)
+    check_all_same_gpu(func, [a])
+    check_contiguous(func, [a])
+    _check_scalar_types(func, a, (torch.int32,))
+    n = info.shape[0]
+    dev = info.device
+    out = torch.empty((n,), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        ws = torch.empty((N.lib().kl_inclusive_sum_workspace_bytes(n),), dtype=torch.uint8, device=dev)
+        N.check(N.lib().kl_inclusive_sum_i32(n, N.ptr(info), N.ptr(out), N.ptr(ws), ws.numel(), N.stream_of(dev)),
+                func)
+    return out
+
+
+def sum_reduce_cuda(feats, inclusive_sum):
+    """raytrace.cpp:328-351: (cnt, feat_dim) with cnt = inclusive_sum[-1] (a device->host read,
+    as the reference's cudaMemcpyAsync at raytrace_cuda.cu:677)."""
+    func = 'sum_reduce_cuda'
+    _pack_args(func, feats, inclusive_sum, 'inclusive_sum', torch.int32)
+    nf, dim = feats.shape
+    dev = feats.device
+    cnt = int(inclusive_sum[-1]) if nf > 0 else 0
+    cnt = max(0, min(cnt, nf))  # the reference allocated num_feats rows and sliced [:cnt]
+    out = torch.empty((cnt, dim), dtype=feats.dtype, device=dev)
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_sum_reduce(N.dtype_code(feats.dtype), nf, dim, N.ptr(feats), N.ptr(inclusive_sum), cnt,
+                                      N.ptr(out), N.stream_of(dev)), func)
+    return out
+
+
+def _pack_scan(func, entry, feats, pack_indices, exclusive, reverse):
+    _pack_args(func, feats, pack_indices, 'pack_indices', torch.int32)
+    out = torch.empty_like(feats)
+    dev = feats.device
+    with torch.cuda.device(dev):
+        N.check(getattr(N.lib(), entry)(N.dtype_code(feats.dtype), feats.shape[0], feats.shape[1], N.ptr(feats),
+                                        N.ptr(pack_indices), pack_indices.shape[0], int(bool(exclusive)),
+                                        int(bool(reverse)), N.ptr(out), N.stream_of(dev)), func)
+    return out
+
+
+def cumsum_cuda(feats, pack_indices, exclusive, reverse):
+    """raytrace.cpp:354-377."""
+    return _pack_scan('cumsum_cuda', 'kl_pack_cumsum', feats, pack_indices, exclusive, reverse)
+
+
+def cumprod_cuda(feats, pack_indices, exclusive, reverse):
+    """raytrace.cpp:380-402."""
+    return _pack_scan('cumprod_cuda', 'kl_pack_cumprod', feats, pack_indices, exclusive, reverse)
+
+
 # ----------------------------------------------------------------------- module layout
 def _module(name, **fns):
     m = types.ModuleType(name)
@@ -447,7 +536,9 @@ render.mesh = _module('kaolin._C.render.mesh', packed_rasterize_forward_cuda=pac
                       dibr_soft_mask_forward_cuda=dibr_soft_mask_forward_cuda,
                       dibr_soft_mask_backward_cuda=dibr_soft_mask_backward_cuda)
 render.spc = _module('kaolin._C.render.spc', raytrace_cuda=raytrace_cuda,
-                     mark_pack_boundaries_cuda=mark_pack_boundaries_cuda)
+                     mark_pack_boundaries_cuda=mark_pack_boundaries_cuda, diff_cuda=diff_cuda,
+                     inclusive_sum_cuda=inclusive_sum_cuda, sum_reduce_cuda=sum_reduce_cuda,
+                     cumsum_cuda=cumsum_cuda, cumprod_cuda=cumprod_cuda)
 metrics = _module('kaolin._C.metrics', sided_distance_forward_cuda=sided_distance_forward_cuda,
                   sided_distance_backward_cuda=sided_distance_backward_cuda,
                   unbatched_triangle_distance_forward_cuda=unbatched_triangle_distance_forward_cuda,

@@ -1,1 +1,2 @@
-from .raytrace import unbatched_raytrace, mark_pack_boundaries, mark_first_hit  # noqa: F401
+from .raytrace import (unbatched_raytrace, mark_pack_boundaries, mark_first_hit, diff, sum_reduce,  # noqa: F401
+                       cumsum, cumprod, exponential_integration)

@@ -289,3 +289,69 @@ def voxelgrid(vertices, faces, resolution, origin=None, scale=None):
     s = _c(scale, np.float32) if scale is not None else None
     lib().or_voxelgrid_f32(_p(v), B, V, _p(f), f.shape[0], R, _p(o), _p(s), _p(grid))
     return grid
+
+
+# ---------------------------------------------------------------------------------------------
+# Packed ray ops (render/spc/raytrace.py:86-296; kernels raytrace_cuda.cu:309-483).  numpy
+# restatement: each pack is walked row by row in the reference kernels' order, operand order
+# `in op prev`, arithmetic in the feature dtype (float16 rounds after every step).
+def pack_starts(boundaries):
+    """torch.nonzero(boundaries)[..., 0] (raytrace.py:176,199)."""
+    return np.nonzero(np.asarray(boundaries))[0]
+
+
+def _pack_ranges(starts, n):
+    starts = [int(s) for s in starts]
+    ends = starts[1:] + [n]
+    return list(zip(starts, ends))
+
+
+def pack_diff(feats, starts):
+    """diff_cuda_kernel (raytrace_cuda.cu:309-325): zeros outside packs and on each pack's last row."""
+    feats = np.asarray(feats)
+    out = np.zeros_like(feats)
+    for b, e in _pack_ranges(starts, feats.shape[0]):
+        for i in range(b, e - 1):
+            out[i] = feats[i + 1] - feats[i]
+    return out
+
+
+def inclusive_sum(info):
+    """cub::DeviceScan::InclusiveSum over int32 (raytrace_cuda.cu:650-663)."""
+    return np.cumsum(np.asarray(info, dtype=np.int64)).astype(np.int32)
+
+
+def sum_reduce(feats, isum):
+    """sum_reduce_cuda_kernel (raytrace_cuda.cu:327-346) with the adds in row order (the
+    reference's atomics are unordered); out has isum[-1] rows."""
+    feats = np.asarray(feats)
+    cnt = int(isum[-1]) if len(isum) else 0
+    out = np.zeros((cnt,) + feats.shape[1:], dtype=feats.dtype)
+    for i in range(feats.shape[0]):
+        r = int(isum[i]) - 1
+        if 0 <= r < cnt:
+            out[r] = out[r] + feats[i]
+    return out
+
+
+def pack_scan(feats, starts, exclusive, reverse, op):
+    """cumsum / cumprod kernels (raytrace_cuda.cu:391-483); op 'sum' or 'prod'.  Output
+    initialised as the reference's at::zeros / at::ones."""
+    feats = np.asarray(feats)
+    f = (lambda a, b: a + b) if op == 'sum' else (lambda a, b: a * b)
+    out = (np.zeros_like(feats) if op == 'sum' else np.ones_like(feats))
+    off = 1 if exclusive else 0
+    for b, e in _pack_ranges(starts, feats.shape[0]):
+        if b >= e:
+            continue
+        if not reverse:
+            if not off:
+                out[b] = feats[b]
+            for i in range(b + 1, e):
+                out[i] = f(feats[i - off], out[i - 1])
+        else:
+            if not off:
+                out[e - 1] = feats[e - 1]
+            for i in range(e - 2, b - 1, -1):
+                out[i] = f(feats[i + off], out[i + 1])
+    return out

@@ -441,6 +441,33 @@ def spc():
     save('spc.npz', **arrays)
 
 
+def rayops():
+    """Packed ray-op KATs transcribed from render/spc/test_rayops.py:20-208 (data only):
+    feats (6,2), tau (6,1), boundaries [1,0,1,0,0,1], and every expected output there."""
+    f = np.array([[1, 1], [1, 1], [1, 1], [2, 2], [3, 3], [5, 5]], dtype=np.float32)
+    arrays = {
+        'feats': f,
+        'tau': np.array([[0], [0], [0], [1], [0], [1]], dtype=np.float32),
+        'boundaries': np.array([1, 0, 1, 0, 0, 1], dtype=np.bool_),
+        'ridx': np.array([1, 1, 1, 1, 2, 2, 3, 3, 3], dtype=np.int32),
+        'ridx_boundaries': np.array([1, 0, 0, 0, 1, 0, 1, 0, 0], dtype=np.bool_),
+        'diff': np.array([[0, 0], [0, 0], [1, 1], [1, 1], [0, 0], [0, 0]], dtype=np.float32),
+        'sum_reduce': np.array([[2, 2], [6, 6], [5, 5]], dtype=np.float32),
+        'cumsum': np.array([[1, 1], [2, 2], [1, 1], [3, 3], [6, 6], [5, 5]], dtype=np.float32),
+        'cumsum_reverse': np.array([[2, 2], [1, 1], [6, 6], [5, 5], [3, 3], [5, 5]], dtype=np.float32),
+        'cumsum_exclusive': np.array([[0, 0], [1, 1], [0, 0], [1, 1], [3, 3], [0, 0]], dtype=np.float32),
+        'cumsum_exclusive_reverse': np.array([[1, 1], [0, 0], [5, 5], [3, 3], [0, 0], [0, 0]], dtype=np.float32),
+        'cumprod': np.array([[1, 1], [1, 1], [1, 1], [2, 2], [6, 6], [5, 5]], dtype=np.float32),
+        'cumprod_reverse': np.array([[1, 1], [1, 1], [6, 6], [6, 6], [3, 3], [5, 5]], dtype=np.float32),
+        'cumprod_exclusive': np.array([[1, 1], [1, 1], [1, 1], [1, 1], [2, 2], [1, 1]], dtype=np.float32),
+        'cumprod_exclusive_reverse': np.array([[1, 1], [1, 1], [6, 6], [3, 3], [1, 1], [1, 1]], dtype=np.float32),
+        # exponential_integration(exclusive=False), atol 1e-4 in the reference test
+        'expint_feats': np.array([[0, 0], [0.4651, 0.4651], [1.1627, 1.1627]], dtype=np.float32),
+        'expint_transmittance': np.array([[0.0], [0.0], [0.0], [0.2325], [0.0], [0.2325]], dtype=np.float32),
+    }
+    save('rayops.npz', **arrays)
+
+
 if __name__ == '__main__':
     torch.set_num_threads(8)
     dibr_simple()
@@ -449,3 +476,4 @@ if __name__ == '__main__':
     sided()
     voxelgrid()
     spc()
+    rayops()

@@ -57,7 +57,9 @@ def test_C_registry_layout():
                  'metrics.unbatched_triangle_distance_forward_cuda',
                  'metrics.unbatched_triangle_distance_backward_cuda', 'ops.conversions.mesh_to_spc_cuda',
                  'ops.spc.morton_to_octree', 'ops.spc.scan_octrees_cuda', 'ops.spc.generate_points_cuda',
-                 'render.spc.raytrace_cuda', 'render.spc.mark_pack_boundaries_cuda']:
+                 'render.spc.raytrace_cuda', 'render.spc.mark_pack_boundaries_cuda', 'render.spc.diff_cuda',
+                 'render.spc.inclusive_sum_cuda', 'render.spc.sum_reduce_cuda', 'render.spc.cumsum_cuda',
+                 'render.spc.cumprod_cuda']:
         obj = C
         for part in path.split('.'):
             obj = getattr(obj, part)
@@ -88,6 +90,11 @@ def test_cpu_tensors_fail_loudly():
         kaolin.render.mesh.rasterize(8, 8, torch.rand(1, 2, 3), torch.rand(1, 2, 3, 2), torch.rand(1, 2, 3, 1))
     with pytest.raises(RuntimeError, match='no CPU fallback'):
         kaolin.ops.conversions.trianglemeshes_to_voxelgrids(torch.rand(1, 3, 3), torch.tensor([[0, 1, 2]]), 4)
+    bnd = torch.tensor([True, False, True])
+    for fn in (kaolin.render.spc.cumsum, kaolin.render.spc.cumprod, kaolin.render.spc.sum_reduce,
+               kaolin.render.spc.diff):
+        with pytest.raises(RuntimeError, match='on CPU'):
+            fn(torch.rand(3, 2), bnd)
 
 
 def test_voxelgrid_resolution_type():

@@ -773,3 +773,103 @@ def test_loss_dot2(kal, na, nb):
                                                  nb, _native.ptr(ws), _native.ptr(out), _native.stream_of(a.device)),
                       'kl_loss_dot2')
         assert abs(float(out) - ref) <= 1e-6 * max(1.0, abs(ref))
+
+
+# ---------------------------------------------------------------- packed ray ops (§8f rank 1)
+def _rand_packs(rng, n, dim, dtype, lead_gap=True):
+    """n rows in random packs (lengths 1..40); with lead_gap the first rows belong to no pack."""
+    b = np.zeros(n, dtype=bool)
+    i = int(rng.integers(1, 5)) if lead_gap else 0
+    while i < n:
+        b[i] = True
+        i += int(rng.integers(1, 41))
+    x = (rng.random((n, dim)) * 1.5 + 0.25).astype(dtype)
+    return x, b
+
+
+def test_rayops_kat(kal, golden):
+    g = golden('rayops.npz')
+    spc = kal.render.spc
+    f, bnd, tau = T(g['feats']), T(g['boundaries']), T(g['tau'])
+    assert torch.equal(spc.mark_pack_boundaries(T(g['ridx'])).cpu(), torch.from_numpy(g['ridx_boundaries']))
+    assert np.array_equal(A(spc.diff(f, bnd)), g['diff'])
+    assert np.array_equal(A(spc.sum_reduce(f, bnd)), g['sum_reduce'])
+    for op, fn in (('sum', spc.cumsum), ('prod', spc.cumprod)):
+        for ex in (False, True):
+            for rev in (False, True):
+                key = 'cum' + op + ('_exclusive' if ex else '') + ('_reverse' if rev else '')
+                assert np.array_equal(A(fn(f, bnd, exclusive=ex, reverse=rev)), g[key]), key
+    feats_out, trans = spc.exponential_integration(f, tau, bnd, exclusive=False)
+    assert np.allclose(A(feats_out), g['expint_feats'], atol=1e-4)
+    assert np.allclose(A(trans), g['expint_transmittance'], atol=1e-4)
+
+
+@pytest.mark.parametrize('dtype', [np.float32, np.float64, np.float16])
+@pytest.mark.parametrize('dim', [1, 3, 32])
+def test_rayops_vs_oracle(kal, dtype, dim):
+    """Bit-exact vs the oracle's sequential walks, rows before the first pack included."""
+    rng = np.random.default_rng(dim)
+    x, b = _rand_packs(rng, 3000, dim, dtype)
+    spc = kal.render.spc
+    xt, bt = T(x), T(b)
+    st = orc.pack_starts(b)
+    for ex in (False, True):
+        for rev in (False, True):
+            assert np.array_equal(A(spc.cumsum(xt, bt, exclusive=ex, reverse=rev)),
+                                  orc.pack_scan(x, st, ex, rev, 'sum')), (ex, rev)
+            assert np.array_equal(A(spc.cumprod(xt, bt, exclusive=ex, reverse=rev)),
+                                  orc.pack_scan(x, st, ex, rev, 'prod')), (ex, rev)
+    assert np.array_equal(A(spc.diff(xt, bt)), orc.pack_diff(x, st))
+    isum = orc.inclusive_sum(b)
+    assert np.array_equal(A(kal._C.render.spc.inclusive_sum_cuda(bt.int())), isum)
+    assert np.array_equal(A(spc.sum_reduce(xt, bt)), orc.sum_reduce(x, isum))
+
+
+def test_rayops_edge_cases(kal):
+    spc = kal.render.spc
+    x = T(np.arange(12, dtype=np.float32).reshape(6, 2))
+    none = T(np.zeros(6, dtype=bool))
+    assert torch.equal(spc.cumsum(x, none), torch.zeros_like(x))      # no pack: at::zeros untouched
+    assert torch.equal(spc.cumprod(x, none), torch.ones_like(x))      # at::ones untouched
+    assert torch.equal(spc.diff(x, none), torch.zeros_like(x))
+    assert spc.sum_reduce(x, none).shape == (0, 2)
+    one = T(np.array([1, 0, 0, 0, 0, 0], dtype=bool))
+    assert torch.equal(spc.sum_reduce(x, one), x.sum(0, keepdim=True))
+    empty = torch.zeros((0, 2), device=DEV)
+    eb = torch.zeros((0,), dtype=torch.bool, device=DEV)
+    assert spc.cumsum(empty, eb).shape == (0, 2)
+    assert spc.sum_reduce(empty, eb).shape == (0, 2)
+
+
+def test_rayops_big_and_backward(kal):
+    """test_rayops.py's big cases: 10000 packs x 100 rows x 32 features vs torch along dim 1."""
+    spc = kal.render.spc
+    g = torch.Generator(device='cpu').manual_seed(0)
+    fb = torch.rand((10000, 100, 32), generator=g).to(DEV)
+    bnd = torch.zeros((10000, 100), dtype=torch.bool, device=DEV)
+    bnd[:, 0] = True
+    bnd = bnd.reshape(-1)
+    flat = fb.reshape(-1, 32)
+    assert torch.allclose(spc.sum_reduce(flat, bnd), fb.sum(1), atol=1e-5)
+    assert torch.allclose(spc.cumsum(flat, bnd), torch.cumsum(fb, 1).reshape(-1, 32), atol=1e-5)
+    assert torch.allclose(spc.cumprod(flat, bnd), torch.cumprod(fb, 1).reshape(-1, 32), atol=1e-4)
+    for fn, ref, atol in ((spc.sum_reduce, lambda t: t.sum(1), 1e-5), (spc.cumsum, lambda t: torch.cumsum(t, 1), 1e-4),
+                          (spc.cumprod, lambda t: torch.cumprod(t, 1), 1e-2)):
+        x = (fb + 1e-3).detach().requires_grad_(True)
+        fn(x.reshape(-1, 32), bnd).sum().backward()
+        g0 = x.grad.clone()
+        x.grad = None
+        ref(x).sum().backward()
+        assert torch.allclose(g0, x.grad, atol=atol), fn.__name__
+
+
+def test_rayops_error_messages(kal):
+    C = kal._C.render.spc
+    with pytest.raises(RuntimeError, match=r"Expected 2-dimensional tensor, but got 1-dimensional tensor for "
+                                           r"argument #1 'feats' \(while checking arguments for cumsum_cuda\)"):
+        C.cumsum_cuda(torch.zeros(4, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV), False, False)
+    with pytest.raises(RuntimeError, match=r"argument #2 'pack_indices' to be Long"):
+        C.diff_cuda(torch.zeros(4, 2, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV))
+    with pytest.raises(RuntimeError, match=r"argument #1 'feats' to be one of Half, Float, Double"):
+        C.cumprod_cuda(torch.zeros(4, 2, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32,
+                                                                                      device=DEV), False, False)

@@ -238,3 +238,45 @@ def test_voxel_order_matches_front_to_back_rule():
     assert list(o[0]) == [0, 1, 2, 4, 3, 5, 6, 7]
     assert list(o[5]) == [5, 1, 4, 7, 0, 3, 6, 2]
     assert list(o[7]) == [7, 3, 5, 6, 1, 2, 4, 0]
+
+
+# ---- packed ray ops (render/spc/test_rayops.py KATs)
+@pytest.mark.parametrize('op', ['sum', 'prod'])
+@pytest.mark.parametrize('exclusive', [False, True])
+@pytest.mark.parametrize('reverse', [False, True])
+def test_rayops_scan_kat(golden, op, exclusive, reverse):
+    g = golden('rayops.npz')
+    key = 'cum' + op + ('_exclusive' if exclusive else '') + ('_reverse' if reverse else '')
+    out = orc.pack_scan(g['feats'], orc.pack_starts(g['boundaries']), exclusive, reverse, op)
+    assert np.array_equal(out, g[key])
+
+
+def test_rayops_diff_sum_reduce_kat(golden):
+    g = golden('rayops.npz')
+    st = orc.pack_starts(g['boundaries'])
+    assert np.array_equal(orc.pack_diff(g['feats'], st), g['diff'])
+    assert np.array_equal(orc.sum_reduce(g['feats'], orc.inclusive_sum(g['boundaries'])), g['sum_reduce'])
+    r = g['ridx']
+    assert np.array_equal(np.concatenate([[True], r[1:] != r[:-1]]), g['ridx_boundaries'])
+
+
+def test_rayops_exponential_integration_kat(golden):
+    """The reference's composition (raytrace.py:322-330) over the oracle scans, vs its KAT (atol 1e-4)."""
+    g = golden('rayops.npz')
+    st = orc.pack_starts(g['boundaries'])
+    tau = g['tau']
+    alpha = 1.0 - np.exp(-tau)
+    trans = np.exp(-orc.pack_scan(tau, st, False, False, 'sum')) * alpha
+    out = orc.sum_reduce(trans * g['feats'], orc.inclusive_sum(g['boundaries']))
+    assert np.allclose(out, g['expint_feats'], atol=1e-4)
+    assert np.allclose(trans, g['expint_transmittance'], atol=1e-4)
+
+
+def test_rayops_scan_matches_numpy_accumulate():
+    """Sequential scans: the oracle equals numpy's (strictly sequential) accumulate per pack."""
+    rng = np.random.default_rng(0)
+    x = rng.random((50, 3), dtype=np.float32)
+    st = np.array([0, 7, 8, 30])
+    out = orc.pack_scan(x, st, False, False, 'sum')
+    for b, e in zip(st, list(st[1:]) + [50]):
+        assert np.array_equal(out[b:e], np.add.accumulate(x[b:e], axis=0))
