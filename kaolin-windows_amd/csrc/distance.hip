@@ -118,44 +118,91 @@ __device__ unsigned long long g_p2m_skipped, g_p2m_evaluated;
 #define KL_P2M_COUNT(v)
 #endif
 
-constexpr int P2M_TILE = 256;  // faces per LDS tile (a divisor of the reference's 512)
+constexpr int P2M_TILE = 128;  // faces per LDS tile (a divisor of the reference's 512)
 constexpr float P2M_E = 1.0f / 16777216.0f;  // float unit roundoff (d is stored as float for both dtypes)
+
+// Lane-parallel pruning record of one face (LDS, structure of arrays): unit normal un and
+// the plane offset dv = dot(v1, un) with the slab half-thickness thick (FaceRec), plus, per
+// edge e, a unit vector o_e in the plane pointing away from the triangle and the offset
+// off_e such that dot(x, o_e) <= off_e for every point x of the triangle (max over the
+// three vertices, plus rounding slack).
+template <typename T>
+struct PruneTile {
+  T o[9][P2M_TILE];
+  T off[3][P2M_TILE];
+  T dv[P2M_TILE];
+};
+
+template <typename T>
+__device__ __forceinline__ void make_prune(const FaceRec<T> &r, PruneTile<T> &pt, int s) {
+  const V3<T> e[3] = {r.e12, r.e23, r.e31};
+  const V3<T> a[3] = {r.v1, r.v2, r.v3};
+  const V3<T> b[3] = {r.v2, r.v3, r.v1};
+  const V3<T> opp[3] = {r.v3, r.v1, r.v2};
+  const T slack = (T)(64.0 / 16777216.0) * r.hmax;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    V3<T> o = cross(r.un, e[k]);
+    const T inv = (T)1 / kl_sqrt<T>(dot(o, o));
+    o = o * inv;
+    if (dot(opp[k] - a[k], o) > (T)0) o = mk(-o.x, -o.y, -o.z);
+    const T d0 = dot(a[k], o), d1 = dot(b[k], o), d2 = dot(opp[k], o);
+    pt.o[3 * k][s] = o.x;
+    pt.o[3 * k + 1][s] = o.y;
+    pt.o[3 * k + 2][s] = o.z;
+    pt.off[k][s] = fmax(fmax(d0, d1), d2) + slack;
+  }
+  pt.dv[s] = dot(r.v1, r.un);
+}
 
 // Face skipping.  The reference's fold (first face of each 512-face tile taken
 // unconditionally, then strict '<' inside a tile, strict '<' across tiles) gives every
 // point the minimum float distance over all faces, earliest face on ties (NaN aside).
 // A face whose computed distance d satisfies d >= min(best of earlier tiles, current
 // tile best) can never change the outcome, so it need not be evaluated.  Points are
-// processed in Morton order, so a wave's 64 points form a cluster (centre c, radius
-// R); every triangle lies in the slab |dot(x - v1, un)| <= thick of its computed plane,
-// which bounds every computed distance of the cluster from below:
-//   L = (|dot(c - v1, un)| - R(1 + 16E) - thick - 64 E M)(1 - 4E),  M = |c|inf + R + hmax,
-//   d >= ((L - 64 E M)^2)(1 - 8E)
-// (the 64 E M terms bound the rounding of the plane distance and of the computed closest
-// point, E = 2^-24 as d is truncated to float).  Faces are skipped for the whole wave
-// only when that bound reaches the largest threshold of its lanes; the first face of
-// each reference tile is always evaluated.  Skipped or not, every evaluated value is the
-// reference's, so results are unchanged; non-finite inputs make the bound NaN / -inf and
-// disable skipping.
+// processed in Morton order, so a wave's 64 points form a cluster (centre c, radius R).
+// Every point x of a triangle satisfies |dot(x, un) - dv| <= thick (its plane slab) and
+// dot(x, o_e) <= off_e for each edge (its in-plane edge half-planes); with
+//   A = |dot(c, un) - dv| - thick,  B = max_e dot(c, o_e) - off_e   (each clamped at 0)
+// un _|_ o_e gives |p - x| >= sqrt(A^2 + B^2) - R for every point p of the cluster.  The
+// computed d is within 64 E M of the true squared-distance geometry (M = |c|inf + R +
+// hmax, E = 2^-24 as d is truncated to float) and A, B within 16 E M of their exact
+// values, so with s = 256 E M subtracted from A and B and the (1 +- 32 E) factors for the
+// float evaluation and the near-orthogonality of the computed unit vectors,
+//   (A^2 + B^2)(1 - 32E) > ((R + sqrt(thr))(1 + 16E) + s)^2 (1 + 32E)
+// proves d > thr.  The test runs lane-parallel: each lane bounds one face of a 64-face
+// chunk against the wave's cluster, a ballot gives the chunk's faces to evaluate, and the
+// wave walks them in face order.  The first face of each reference tile is always
+// evaluated.  Skipped or not, every evaluated value is the reference's, so results are
+// unchanged; non-finite inputs give NaN / infinite bounds, which never skip (the
+// comparisons are false, and a non-finite cluster disables the test).
 // grid: (point blocks, face splits).  A split covers whole 512-face reference tiles
 // [f_begin, f_end); with more than one split each writes its partial (dist, idx, type)
 // at part + split * P (sorted point order) for p2m_combine_kernel.  The reference fold
 // restricted to a split: only split 0 takes its first tile unconditionally; later
 // splits start from +inf, so, as in the global fold, a NaN tile never replaces.
+#ifndef KL_P2M_WAVES_PER_EU
+#define KL_P2M_WAVES_PER_EU 5
+#endif
+// occupancy: the float kernel is latency-bound at 4 waves per SIMD (113 VGPRs); asking
+// for 5 (96 VGPRs, 4 spilled) measured 3-5 % faster on cfg2, 6 (22 spills) no better
 template <typename T>
-__global__ void __launch_bounds__(256) p2m_fwd_kernel(const T *__restrict__ pts, const T *__restrict__ fv,
+__global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1)) p2m_fwd_kernel(const T *__restrict__ pts, const T *__restrict__ fv,
                                                        const int32_t *__restrict__ order, int64_t P, int64_t F,
                                                        int64_t split_faces, T *__restrict__ out_dist,
                                                        int64_t *__restrict__ out_idx, int32_t *__restrict__ out_type,
                                                        T *__restrict__ part_dist, int64_t *__restrict__ part_idx,
-                                                       int32_t *__restrict__ part_type) {
+                                                       int32_t *__restrict__ part_type,
+                                                       const int32_t *__restrict__ bounds, uint32_t *gbest) {
   __shared__ FaceRec<T> sf[P2M_TILE];
+  __shared__ PruneTile<T> sp;
   const int64_t si = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const bool valid = si < P;
   const int64_t pi = valid ? (order ? (int64_t)order[si] : si) : 0;
   const bool first_split = blockIdx.y == 0;
   const int64_t f_begin = (int64_t)blockIdx.y * split_faces;
   const int64_t f_end = min(F, f_begin + split_faces);
+  const int lane = threadIdx.x & 63;
   V3<T> p = mk((T)0, (T)0, (T)0);
   if (valid) p = mk(pts[pi * 3], pts[pi * 3 + 1], pts[pi * 3 + 2]);
   // cluster of the wave's points (padding lanes repeat lane 0's point)
@@ -172,50 +219,84 @@ __global__ void __launch_bounds__(256) p2m_fwd_kernel(const T *__restrict__ pts,
     R = wave_max(kl_sqrt<T>(dot(dq, dq))) * (T)(1.0 + 16.0 * P2M_E);
     cinf = fmax(fmax(fabs(c.x), fabs(c.y)), fabs(c.z));
   }
+  // Shared thresholds (all faces proper, finite bounded cluster): the fold is then the plain
+  // (distance, index) minimum, so the best distance any split has found for a point bounds
+  // its result and is as good a threshold as this split's own.  gbest holds them as float
+  // bits (distances are >= +0, so integer order is float order); reads may be stale, which
+  // only weakens the bound.
+  const bool share = gbest != nullptr && all_fin && bounds[6] != 0 && cinf + R < (T)1e15;
+  float published = INFINITY;
 #ifdef KL_P2M_PROBE
   unsigned long long g_p2m_skipped = 0, g_p2m_evaluated = 0;
 #endif
   T best = (T)INFINITY, tbest = (T)INFINITY;
   int64_t best_f = 0, tbest_f = 0;
   int best_t = 0, tbest_t = 0;
-  T thr_max = (T)INFINITY;  // >= max over lanes of min(best, tbest) (refreshed per LDS tile)
   for (int64_t start = f_begin; start < f_end; start += P2M_TILE) {
     const int n = (int)min((int64_t)P2M_TILE, f_end - start);
-    if (start > f_begin) {  // thresholds only decrease, so a stale maximum is a safe upper bound
-      T thr = fmin(best, tbest);
-      if (thr != thr || !valid) thr = valid ? (T)INFINITY : (T)0;
-      thr_max = wave_max(thr);
+    float shared_thr = INFINITY;
+    if (share && valid)
+      shared_thr = __uint_as_float(__hip_atomic_load(gbest + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();
+    for (int s = threadIdx.x; s < n; s += blockDim.x) {
+      make_face<T>(fv + (start + s) * 9, sf[s]);
+      make_prune<T>(sf[s], sp, s);
     }
     __syncthreads();
-    for (int s = threadIdx.x; s < n; s += blockDim.x) make_face<T>(fv + (start + s) * 9, sf[s]);
-    __syncthreads();
-    for (int s = 0; s < n; s++) {
-      const int64_t f = start + s;
-      const FaceRec<T> &fr = sf[s];
-      if ((f & 511) != 0) {
+    for (int s0 = 0; s0 < n; s0 += 64) {
+      // thresholds only decrease, so a stale maximum over the lanes is a safe upper bound
+      T thr = fmin(best, tbest);
+      if (thr != thr || !valid) thr = valid ? (T)INFINITY : (T)0;
+      if (share) thr = fmin(thr, (T)shared_thr);
+      const T thr_max = wave_max(thr);
+      const int s = s0 + lane;
+      bool eval = s < n;
+      if (eval && all_fin && ((start + s) & 511) != 0 && thr_max < (T)INFINITY) {
+        const FaceRec<T> &fr = sf[s];
         const T M = cinf + R + fr.hmax;
-        const T slack = (T)(64.0 * P2M_E) * M;
-        const T L = (fabs(dot(c - fr.v1, fr.un)) - R - fr.thick - slack) * (T)(1.0 - 4.0 * P2M_E) - slack;
-        if (L > (T)0 && L * L * (T)(1.0 - 8.0 * P2M_E) >= thr_max) {  // wave-uniform
-          KL_P2M_COUNT(g_p2m_skipped);
-          continue;
-        }
+        const T sl = (T)(256.0 * P2M_E) * M;
+        const T A = fmax(fabs(dot(c, fr.un) - sp.dv[s]) - fr.thick - sl, (T)0);
+        T b = dot(c, mk(sp.o[0][s], sp.o[1][s], sp.o[2][s])) - sp.off[0][s];
+        b = fmax(b, dot(c, mk(sp.o[3][s], sp.o[4][s], sp.o[5][s])) - sp.off[1][s]);
+        b = fmax(b, dot(c, mk(sp.o[6][s], sp.o[7][s], sp.o[8][s])) - sp.off[2][s]);
+        const T B = fmax(b - sl, (T)0);
+        const T K = (R + kl_sqrt<T>(thr_max)) * (T)(1.0 + 16.0 * P2M_E) + sl;
+        if ((A * A + B * B) * (T)(1.0 - 32.0 * P2M_E) > K * K * (T)(1.0 + 32.0 * P2M_E)) eval = false;
       }
-      KL_P2M_COUNT(g_p2m_evaluated);
-      int t;
-      const float d = point_face<T>(p, fr, t);
-      if ((f & 511) == 0) {  // a reference tile begins: merge the previous tile, restart
-        if (f > f_begin && ((first_split && f == 512) || best > tbest)) {
-          best = tbest; best_f = tbest_f; best_t = tbest_t;
+      uint64_t mask = __ballot(eval);
+#ifdef KL_P2M_PROBE
+      g_p2m_evaluated += __popcll(mask);
+      g_p2m_skipped += (uint64_t)min(64, n - s0) - __popcll(mask);
+#endif
+      // fold one evaluated face into the reference's tile-wise running minimum
+      auto fold = [&](int64_t f, float d, int t) {
+        if ((f & 511) == 0) {  // a reference tile begins: merge the previous tile, restart
+          if (f > f_begin && ((first_split && f == 512) || best > tbest)) {
+            best = tbest; best_f = tbest_f; best_t = tbest_t;
+          }
+          tbest = (T)d; tbest_f = f; tbest_t = t;
+        } else if (tbest > (T)d) {
+          tbest = (T)d; tbest_f = f; tbest_t = t;
         }
-        tbest = (T)d; tbest_f = f; tbest_t = t;
-      } else if (tbest > (T)d) {
-        tbest = (T)d; tbest_f = f; tbest_t = t;
+      };
+      while (mask) {
+        const int sj = s0 + __builtin_ctzll(mask);
+        mask &= mask - 1;
+        int t;
+        const float d = point_face<T>(p, sf[sj], t);
+        fold(start + sj, d, t);
+      }
+    }
+    if (share && valid) {
+      const float cur = (float)fmin(best, tbest);
+      if (cur < published) {
+        atomicMin(gbest + si, __float_as_uint(cur));
+        published = cur;
       }
     }
   }
 #ifdef KL_P2M_PROBE
-  if ((threadIdx.x & 63) == 0) {
+  if (lane == 0) {
     atomicAdd(&::kl::g_p2m_skipped, g_p2m_skipped);
     atomicAdd(&::kl::g_p2m_evaluated, g_p2m_evaluated);
   }
@@ -271,11 +352,32 @@ __device__ __forceinline__ int32_t f2ord(float v) {  // order-preserving float -
 __device__ __forceinline__ float ord2f(int32_t b) { return __int_as_float(b >= 0 ? b : b ^ 0x7fffffff); }
 
 // one 1024-thread block: per-axis min / max of the finite point coordinates
+// bounds[6] = 1 iff every face is proper (finite, |coordinates| < 1e15, edges and normal of
+// nonzero length as make_face computes them): then no point--face distance of a finite,
+// bounded point is NaN, the reference fold is the plain (distance, index) minimum, and any
+// computed distance is an upper bound of the result (p2m_fwd_kernel's shared thresholds).
 template <typename T>
-__global__ void __launch_bounds__(1024) p2m_bounds_kernel(const T *__restrict__ pts, int64_t P, int32_t *bounds) {
+__global__ void __launch_bounds__(1024) p2m_bounds_kernel(const T *__restrict__ pts, int64_t P,
+                                                          const T *__restrict__ fv, int64_t F, int32_t *partial) {
   __shared__ float red[6][16];
+  __shared__ int proper;
+  if (threadIdx.x == 0) proper = 1;
+  __syncthreads();
+  bool ok = true;
+  for (int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; f < F; f += (int64_t)gridDim.x * blockDim.x) {
+    const T *v = fv + f * 9;
+    const V3<T> v1 = mk(v[0], v[1], v[2]), v2 = mk(v[3], v[4], v[5]), v3 = mk(v[6], v[7], v[8]);
+    const V3<T> e12 = v2 - v1, e23 = v3 - v2, e31 = v1 - v3;
+    const V3<T> normal = cross(v1 - v2, e31);
+    const T nn = dot(normal, normal), l12 = dot(e12, e12), l23 = dot(e23, e23), l31 = dot(e31, e31);
+    const T hm = fmax(fmax(fmax(fabs(v1.x), fabs(v1.y)), fmax(fabs(v1.z), fabs(v2.x))),
+                      fmax(fmax(fabs(v2.y), fabs(v2.z)), fmax(fmax(fabs(v3.x), fabs(v3.y)), fabs(v3.z))));
+    ok = ok && hm < (T)1e15 && nn > (T)1e-30 && l12 > (T)1e-30 && l23 > (T)1e-30 && l31 > (T)1e-30 &&
+         nn < (T)1e36;  // (hm < 1e15 also rejects NaN / inf)
+  }
+  if (!ok) proper = 0;
   float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (int64_t i = threadIdx.x; i < P; i += blockDim.x) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < P; i += (int64_t)gridDim.x * blockDim.x) {
 #pragma unroll
     for (int a = 0; a < 3; a++) {
       const float v = (float)pts[i * 3 + a];
@@ -299,26 +401,71 @@ __global__ void __launch_bounds__(1024) p2m_bounds_kernel(const T *__restrict__ 
     const int a = threadIdx.x;
     float r = red[a][0];
     for (int k = 1; k < (int)(blockDim.x >> 6); k++) r = a < 3 ? fminf(r, red[a][k]) : fmaxf(r, red[a][k]);
-    bounds[a] = f2ord(r);
+    partial[blockIdx.x * 8 + a] = f2ord(r);
   }
+  if (threadIdx.x == 6) partial[blockIdx.x * 8 + 6] = proper;
 }
 
-__device__ __forceinline__ uint32_t spread10(uint32_t v) {
-  v &= 0x3ff;
-  v = (v | (v << 16)) & 0x030000ff;
-  v = (v | (v << 8)) & 0x0300f00f;
-  v = (v | (v << 4)) & 0x030c30c3;
-  v = (v | (v << 2)) & 0x09249249;
-  return v;
+// folds the bound kernel's per-block partials (every block of the Morton kernel does it, into
+// LDS; block 0 also stores the result for p2m_fwd_kernel)
+__device__ __forceinline__ void fold_bounds(const int32_t *__restrict__ partial, int nblk, int32_t *sb,
+                                            int32_t *bounds) {
+  if (threadIdx.x < 7) {
+    const int a = threadIdx.x;
+    int32_t r = partial[a];
+    for (int k = 1; k < nblk; k++) {
+      const int32_t v = partial[k * 8 + a];
+      r = a < 3 ? min(r, v) : a < 6 ? max(r, v) : (r & v);
+    }
+    sb[a] = r;
+    if (blockIdx.x == 0) bounds[a] = r;
+  }
+  __syncthreads();
 }
+
+// 3-D Hilbert index of a 10-bit-per-axis grid cell (Skilling's transpose transform, then
+// bit interleave).  Hilbert order keeps every run of 64 consecutive points spatially
+// compact (no Morton jumps across octant boundaries): on cfg2 the mean cluster radius is
+// 0.39 against 0.50 for Morton order, and the faces a wave must evaluate shrink with it.
+__device__ __forceinline__ uint32_t hilbert3(uint32_t x0, uint32_t x1, uint32_t x2) {
+  uint32_t X[3] = {x0, x1, x2};
+  for (uint32_t Q = 1u << 9; Q > 1; Q >>= 1) {
+    const uint32_t P = Q - 1;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+      if (X[i] & Q) {
+        X[0] ^= P;
+      } else {
+        const uint32_t t = (X[0] ^ X[i]) & P;
+        X[0] ^= t;
+        X[i] ^= t;
+      }
+    }
+  }
+  X[1] ^= X[0];
+  X[2] ^= X[1];
+  uint32_t t = 0;
+  for (uint32_t Q = 1u << 9; Q > 1; Q >>= 1)
+    if (X[2] & Q) t ^= Q - 1;
+  X[0] ^= t;
+  X[1] ^= t;
+  X[2] ^= t;
+  uint32_t h = 0;
+  for (int b = 9; b >= 0; b--) h = (h << 3) | (((X[0] >> b) & 1) << 2) | (((X[1] >> b) & 1) << 1) | ((X[2] >> b) & 1);
+  return h;
+}
+
+constexpr uint32_t P2M_KEY_BITS = 31;  // 30-bit Hilbert keys; non-finite points get 2^30 (last)
 
 template <typename T>
 __global__ void __launch_bounds__(256) p2m_morton_kernel(const T *__restrict__ pts, int64_t P,
-                                                          const int32_t *__restrict__ bounds, uint32_t *keys,
-                                                          int32_t *vals) {
+                                                          const int32_t *__restrict__ partial, int nblk,
+                                                          int32_t *out_bounds, uint32_t *keys, int32_t *vals) {
+  __shared__ int32_t bounds[8];
+  fold_bounds(partial, nblk, bounds, out_bounds);
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= P) return;
-  uint32_t code = 0x3fffffffu;  // non-finite points last
+  uint32_t code = 1u << 30;  // non-finite points last
   const float x = (float)pts[i * 3], y = (float)pts[i * 3 + 1], z = (float)pts[i * 3 + 2];
   if (isfinite(x) && isfinite(y) && isfinite(z)) {
     uint32_t g[3];
@@ -329,29 +476,36 @@ __global__ void __launch_bounds__(256) p2m_morton_kernel(const T *__restrict__ p
       const float t = hi > lo ? (v[a] - lo) / (hi - lo) : 0.0f;
       g[a] = (uint32_t)fminf(fmaxf(t * 1024.0f, 0.0f), 1023.0f);
     }
-    code = (spread10(g[0]) << 2) | (spread10(g[1]) << 1) | spread10(g[2]);
+    code = hilbert3(g[0], g[1], g[2]);
   }
   keys[i] = code;
   vals[i] = (int32_t)i;
 }
 
-constexpr int P2M_MAX_SPLITS = 16;
+#ifndef KL_P2M_MAX_SPLITS
+#define KL_P2M_MAX_SPLITS 32
+#endif
+constexpr int P2M_MAX_SPLITS = KL_P2M_MAX_SPLITS;
+// workgroups the (point block, face split) grid aims for (scripts/dev/p2m_probe.hip sweeps it)
+static int g_p2m_target_blocks = 10240;
+constexpr int P2M_BOUND_BLOCKS = 64;  // blocks of p2m_bounds_kernel
 
 struct P2MWs {
-  size_t keys_in, keys_out, vals_in, vals_out, temp, temp_bytes, part, bytes;
+  size_t keys_in, keys_out, vals_in, vals_out, temp, temp_bytes, part, gbest, bytes;
   explicit P2MWs(int64_t P) {
     size_t tb = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                       (const int32_t *)nullptr, (int32_t *)nullptr, (int)P, 0, 30);
+                                       (const int32_t *)nullptr, (int32_t *)nullptr, (int)P, 0, P2M_KEY_BITS);
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
-    keys_in = 256;  // [0, 256): 6 bounds
+    keys_in = 256 + 32 * P2M_BOUND_BLOCKS;  // [0, 28): bounds + flag; [256, ...): per-block partials
     keys_out = keys_in + al(4 * (size_t)P);
     vals_in = keys_out + al(4 * (size_t)P);
     vals_out = vals_in + al(4 * (size_t)P);
     temp = vals_out + al(4 * (size_t)P);
     temp_bytes = tb;
     part = temp + al(tb);  // P2M_MAX_SPLITS x P x (dist 8 + idx 8 + type 4)
-    bytes = part + al((size_t)P2M_MAX_SPLITS * P * 20);
+    gbest = part + al((size_t)P2M_MAX_SPLITS * P * 20);  // P x float bits (shared thresholds)
+    bytes = gbest + al(4 * (size_t)P);
   }
 };
 
@@ -553,6 +707,8 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
   T *pd = nullptr;
   int64_t *pidx = nullptr;
   int32_t *pt = nullptr;
+  const int32_t *bounds_c = nullptr;
+  uint32_t *gbest = nullptr;
   const unsigned pblocks = (unsigned)cdiv(P, 256);
   int splits = 1;
   int64_t split_faces = F;
@@ -561,19 +717,27 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
     KL_REQUIRE(ws_bytes >= L.bytes, "unbatched_triangle_distance_forward: workspace too small");
     char *w = reinterpret_cast<char *>(ws);
     int32_t *bounds = reinterpret_cast<int32_t *>(w);
-    hipLaunchKernelGGL(p2m_bounds_kernel<T>, dim3(1), dim3(1024), 0, st, (const T *)pts, P, bounds);
+    int32_t *partial = bounds + 64;  // [256, 256 + 32 * nblk) bytes
+    const int nblk = (int)std::min<int64_t>(P2M_BOUND_BLOCKS, std::max<int64_t>(1, cdiv(std::max(P, F), 4096)));
+    hipLaunchKernelGGL(p2m_bounds_kernel<T>, dim3(nblk), dim3(1024), 0, st, (const T *)pts, P, (const T *)fv, F,
+                       partial);
     KL_CHECK_LAUNCH();
     uint32_t *kin = reinterpret_cast<uint32_t *>(w + L.keys_in), *kout = reinterpret_cast<uint32_t *>(w + L.keys_out);
     int32_t *vin = reinterpret_cast<int32_t *>(w + L.vals_in), *vout = reinterpret_cast<int32_t *>(w + L.vals_out);
-    hipLaunchKernelGGL(p2m_morton_kernel<T>, dim3(pblocks), dim3(256), 0, st, (const T *)pts, P, bounds, kin, vin);
+    hipLaunchKernelGGL(p2m_morton_kernel<T>, dim3(pblocks), dim3(256), 0, st, (const T *)pts, P, partial, nblk,
+                       bounds, kin, vin);
     KL_CHECK_LAUNCH();
     size_t tb = L.temp_bytes;
-    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.temp, tb, kin, kout, vin, vout, (int)P, 0, 30, st));
+    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.temp, tb, kin, kout, vin, vout, (int)P, 0, P2M_KEY_BITS, st));
     order = vout;
-    // enough (point block, face split) workgroups to fill the chip several times over;
+    bounds_c = bounds;
+    gbest = reinterpret_cast<uint32_t *>(w + L.gbest);
+    KL_CHECK_RC(fill_async(gbest, 0x7f, 4 * (size_t)P, st));  // 0x7f7f7f7f = 3.4e38, above any proper distance
+    // enough (point block, face split) workgroups to fill the chip ~10 times over (cfg2:
+    // 20 splits of 1024 faces, 1.6 ms; 14 of 1536: 2.0 ms; 40 of 512: 2.1 ms);
     // splits cover whole 512-face reference tiles
     const int64_t tiles = cdiv(F, 512);
-    const int64_t want = std::max<int64_t>(1, cdiv(2048, pblocks));
+    const int64_t want = std::max<int64_t>(1, cdiv(g_p2m_target_blocks, pblocks));
     splits = (int)std::min<int64_t>(std::min<int64_t>(want, tiles), P2M_MAX_SPLITS);
     split_faces = cdiv(tiles, splits) * 512;
     splits = (int)cdiv(F, split_faces);
@@ -584,7 +748,7 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
     }
   }
   hipLaunchKernelGGL(p2m_fwd_kernel<T>, dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
-                     (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt);
+                     (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
   KL_CHECK_LAUNCH();
   if (splits > 1) {
     hipLaunchKernelGGL(p2m_combine_kernel<T>, dim3(pblocks), dim3(256), 0, st, order, P, splits, pd, pidx, pt,

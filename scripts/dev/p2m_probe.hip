@@ -10,6 +10,7 @@
 
 namespace kl {
 void set_error(const std::string &msg) { fprintf(stderr, "error: %s\n", msg.c_str()); }
+int fill_async(void *p, int value, size_t bytes, hipStream_t st) { return hipMemsetAsync(p, value, bytes, st) == hipSuccess ? 0 : -2; }
 }  // namespace kl
 
 #define CK(x)                                                        \
@@ -44,13 +45,15 @@ int main(int argc, char **argv) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int mode = 0; mode < 2; mode++) {
+  const int targets[] = {6144, 8192, 10240, 12288, 16384, 20480};
+  for (int mode = 1; mode < 2 + 5; mode++) {
     unsigned long long z = 0;
-    for (int rep = 0; rep < 3; rep++) {
+    if (mode >= 1) g_p2m_target_blocks = targets[mode - 1];
+    for (int rep = 0; rep < 2; rep++) {
       CK(hipMemcpyToSymbol(HIP_SYMBOL(g_p2m_skipped), &z, 8));
       CK(hipMemcpyToSymbol(HIP_SYMBOL(g_p2m_evaluated), &z, 8));
       CK(hipEventRecord(a, 0));
-      int rc = p2m_fwd<float>(P, F, dp, df, dd, di, dt, mode ? ws : nullptr, mode ? L.bytes : 0, 0);
+      int rc = p2m_fwd<float>(P, F, dp, df, dd, di, dt, ws, L.bytes, 0);
       CK(hipEventRecord(b, 0));
       CK(hipEventSynchronize(b));
       if (rc) return 1;
@@ -59,7 +62,7 @@ int main(int argc, char **argv) {
       unsigned long long sk, ev;
       CK(hipMemcpyFromSymbol(&sk, HIP_SYMBOL(g_p2m_skipped), 8));
       CK(hipMemcpyFromSymbol(&ev, HIP_SYMBOL(g_p2m_evaluated), 8));
-      printf("mode=%s rep=%d  %.3f ms  skipped=%llu evaluated=%llu (%.1f%% skipped)\n", mode ? "morton" : "plain", rep,
+      printf("target=%d mode=%s rep=%d  %.3f ms  skipped=%llu evaluated=%llu (%.1f%% skipped)\n", g_p2m_target_blocks, mode ? "morton" : "plain", rep,
              ms, sk, ev, 100.0 * sk / (double)(sk + ev + 1));
     }
   }
