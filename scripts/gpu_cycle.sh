@@ -6,7 +6,7 @@ set -e
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 ROOT=$(pwd)
-timeout -k 10 500 python -m pytest tests -m gpu -x -q > "$OUT/gpu_tests.log" 2>&1
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
 timeout -k 10 240 python bench.py ${BENCH_ARGS:---no-cpu-baseline} > "$OUT/bench.log" 2>&1
 cd /tmp
 export TMPDIR=/tmp
