@@ -222,6 +222,41 @@ int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height, int width,
                                const void *face_vertices_image, float sigmainv, float multiplier,
                                void *grad_face_vertices_image, kl_stream stream);
 
+/* ------------------------------------------------------------ DefTet sparse render */
+
+/* deftet.cpp:49-111  deftet_sparse_render_forward_cuda (kernel deftet_cuda.cu:32-190).
+ * face_vertices_z (B,F,3), face_vertices_image (B,F,3,2), face_bboxes (B,F,4) [xmin ymin xmax ymax]
+ * or NULL (then min / max over the three vertices in-kernel, as deftet.py:290-292 computes them),
+ * pixel_coords (B,P,2), pixel_depth_ranges (B,P,2) [lo, hi).  dtype KL_F32 | KL_F64.
+ * Outputs (B,P,K), fully written: face_idx int64 (first K hits in mesh order, then -1),
+ * pixel_depths (-inf pad), w0, w1 (0 pad). */
+int kl_deftet_sparse_render_forward(kl_dtype dtype, int64_t batch_size, int64_t num_faces, int64_t num_pixels,
+                                    int64_t knum, const void *face_vertices_z, const void *face_vertices_image,
+                                    const void *face_bboxes, const void *pixel_coords,
+                                    const void *pixel_depth_ranges, float eps, int64_t *face_idx,
+                                    void *pixel_depths, void *w0, void *w1, kl_stream stream);
+
+/* deftet.py:294-306 (the torch glue of DeftetSparseRenderer.forward) in one pass: per pixel the
+ * hits of kl_deftet_sparse_render_forward ranked by depth, descending (stable), then
+ * sorted_face_idx (B,P,K) int64, weights (B,P,K,3) = (w0, w1, 1 - (w0 + w1)) and
+ * interpolated_features (B,P,K,D) = (w0 f0 + w1 f1) + w2 f2 from face_features (B,F,3,D). */
+int kl_deftet_sparse_render_resolve(kl_dtype dtype, int64_t batch_size, int64_t num_faces, int64_t num_pixels,
+                                    int64_t knum, int64_t feat_dim, const int64_t *face_idx,
+                                    const void *pixel_depths, const void *w0, const void *w1,
+                                    const void *face_features, int64_t *sorted_face_idx, void *weights,
+                                    void *interpolated_features, kl_stream stream);
+
+/* deftet.cpp:113-163  deftet_sparse_render_backward_cuda (kernel deftet_cuda.cu:240-420).
+ * grad_interpolated_features (B,P,K,D), face_idx (B,P,K) int64, weights (B,P,K,3),
+ * face_vertices_image (B,F,3,2), face_features (B,F,3,D) -> grad_face_vertices_image (B,F,3,2),
+ * grad_face_features (B,F,3,D), fully written (zeroed, then float atomics as the reference). */
+int kl_deftet_sparse_render_backward(kl_dtype dtype, int64_t batch_size, int64_t num_faces, int64_t num_pixels,
+                                     int64_t knum, int64_t feat_dim, const void *grad_interpolated_features,
+                                     const int64_t *face_idx, const void *weights,
+                                     const void *face_vertices_image, const void *face_features, float eps,
+                                     void *grad_face_vertices_image, void *grad_face_features,
+                                     kl_stream stream);
+
 /* ------------------------------------------------------------ distances */
 
 /* unbatched_triangle_distance.cpp:43-72.  points (P,3), face_vertices (F,3,3).

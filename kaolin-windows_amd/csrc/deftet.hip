@@ -1,0 +1,374 @@
+// deftet.hip -- DefTet sparse volumetric render: every face a pixel's
+// ray crosses inside its depth range, not only the nearest one.
+//
+// Reference: kaolin/render/mesh/deftet.py:269-417 (DeftetSparseRenderer, deftet_sparse_render)
+// over deftet.cpp:49-163 (bindings) and deftet_cuda.cu (forward kernel :32-190, backward
+// kernel :240-420).
+//
+// Forward (the reference kernel's semantics): for pixel (x0, y0) with depth range [lo, hi),
+// walk the mesh's faces in mesh order.  Face f is a hit when (x0, y0) is inside its
+// [min, max) bbox, its three barycentrics (cross-product form, normalised by
+// norm + copysignf(eps, norm)) are all >= 0, and the interpolated depth d = w0 az + w1 bz + w2 cz
+// satisfies lo <= d < hi.  The first knum hits in mesh order fill slots 0..n-1 of the pixel's
+// row; the other slots hold -1 / -inf / 0 / 0 (the reference's at::full / at::zeros).
+//
+// MI355X mapping: one lane per pixel (the reference spends a 32-lane warp per pixel and
+// ballots the insertion slot).  A workgroup owns 256 pixels of one mesh.  Faces stream
+// through LDS in tiles of 256; each tile is first culled against the workgroup's pixel bbox
+// with an order-preserving compaction (block scan), so the per-lane walk (LDS broadcast
+// reads, no bank conflicts) only visits faces that can touch one of its pixels.  For
+// image-grid pixels (DefTet's use) a workgroup covers a thin strip of the image and the walk
+// is a small fraction of F.  Each lane appends its own hits in mesh order: no ballots, no
+// atomics, every slot written once.
+//
+// Resolve (deftet.py:294-306, the torch glue of the forward): per pixel the n hits are ranked
+// by depth, descending (stable: equal depths keep mesh order; the reference's argsort leaves
+// ties unspecified), and the sorted face ids, weights (w0, w1, w2 = 1 - (w0 + w1)) and the
+// interpolated features (w0 f0 + w1 f1) + w2 f2 are written in one pass.
+//
+// Backward (deftet_cuda.cu:240-420): one lane per (pixel, slot) item that holds a face; the
+// reference's k1/k2/k3 derivative form term by term; hardware float atomics into the
+// per-face gradients (unordered, like the reference's atomicAdd).  The six vertex-gradient
+// terms are summed over the feature dimension in registers first (D times fewer atomics).
+#include <cmath>
+
+#include "common.h"
+
+namespace kl {
+
+constexpr int kDtTile = 256;  // pixels per workgroup == faces per LDS tile
+
+template <typename T>
+__device__ __forceinline__ T dt_copysign_eps_f(float eps, T v) {
+  // copysignf(double eps, double v) of the reference: both operands rounded to float
+  return (T)copysignf(eps, (float)v);
+}
+
+// deftet_cuda.cu:32-190
+template <typename T>
+__global__ void __launch_bounds__(kDtTile)
+    deftet_fwd_kernel(int64_t F, int64_t P, int K, const T *__restrict__ fvz, const T *__restrict__ fvi,
+                      const T *__restrict__ bboxes, const T *__restrict__ pix, const T *__restrict__ ranges,
+                      float eps, int64_t *__restrict__ out_idx, T *__restrict__ out_depth, T *__restrict__ out_w0,
+                      T *__restrict__ out_w1) {
+  __shared__ T s_f[13][kDtTile];  // ax ay bx by cx cy az bz cz xmin ymin xmax ymax
+  __shared__ int s_id[kDtTile];
+  __shared__ int s_wave[16];
+  __shared__ T s_box[4][kDtTile / 64];
+
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y;
+  const int64_t p = (int64_t)blockIdx.x * kDtTile + tid;
+  const bool active = p < P;
+  const int64_t prow = b * P + p;
+
+  T x0 = 0, y0 = 0, lo = 0, hi = 0;
+  if (active) {
+    x0 = pix[prow * 2 + 0];
+    y0 = pix[prow * 2 + 1];
+    lo = ranges[prow * 2 + 0];
+    hi = ranges[prow * 2 + 1];
+  }
+  // workgroup pixel bbox (NaN pixels never hit, so they may be left out of it)
+  {
+    T bxmin = INFINITY, bymin = INFINITY, bxmax = -INFINITY, bymax = -INFINITY;
+    if (active && x0 == x0 && y0 == y0) {
+      bxmin = x0; bxmax = x0; bymin = y0; bymax = y0;
+    }
+    bxmin = wave_min(bxmin); bymin = wave_min(bymin);
+    bxmax = wave_max(bxmax); bymax = wave_max(bymax);
+    if ((tid & 63) == 0) {
+      s_box[0][tid >> 6] = bxmin; s_box[1][tid >> 6] = bymin;
+      s_box[2][tid >> 6] = bxmax; s_box[3][tid >> 6] = bymax;
+    }
+  }
+  __syncthreads();
+  T gxmin = s_box[0][0], gymin = s_box[1][0], gxmax = s_box[2][0], gymax = s_box[3][0];
+#pragma unroll
+  for (int w = 1; w < kDtTile / 64; w++) {
+    gxmin = s_box[0][w] < gxmin ? s_box[0][w] : gxmin;
+    gymin = s_box[1][w] < gymin ? s_box[1][w] : gymin;
+    gxmax = s_box[2][w] > gxmax ? s_box[2][w] : gxmax;
+    gymax = s_box[3][w] > gymax ? s_box[3][w] : gymax;
+  }
+
+  int n = 0;
+  int64_t *row_idx = out_idx + prow * K;
+  T *row_d = out_depth + prow * K;
+  T *row_w0 = out_w0 + prow * K;
+  T *row_w1 = out_w1 + prow * K;
+  const T *mz = fvz + b * F * 3;
+  const T *mi = fvi + b * F * 6;
+  const T *mb = bboxes ? bboxes + b * F * 4 : nullptr;
+
+  for (int64_t t0 = 0; t0 < F; t0 += kDtTile) {
+    if (!__syncthreads_or(active && n < K)) break;  // every pixel of the workgroup is full
+    const int64_t f = t0 + tid;
+    T v[13];
+    bool keep = false;
+    if (f < F) {
+#pragma unroll
+      for (int c = 0; c < 6; c++) v[c] = mi[f * 6 + c];
+#pragma unroll
+      for (int c = 0; c < 3; c++) v[6 + c] = mz[f * 3 + c];
+      if (mb) {
+#pragma unroll
+        for (int c = 0; c < 4; c++) v[9 + c] = mb[f * 4 + c];
+      } else {  // deftet.py:290-292: min / max over the three vertices
+        v[9] = fmin(fmin(v[0], v[2]), v[4]);
+        v[10] = fmin(fmin(v[1], v[3]), v[5]);
+        v[11] = fmax(fmax(v[0], v[2]), v[4]);
+        v[12] = fmax(fmax(v[1], v[3]), v[5]);
+      }
+      // some pixel x of the workgroup can satisfy xmin <= x < xmax (same for y)
+      keep = v[9] <= gxmax && v[11] > gxmin && v[10] <= gymax && v[12] > gymin;
+    }
+    int total;
+    const int pos = block_exclusive_scan(keep ? 1 : 0, s_wave, &total);
+    if (keep) {
+#pragma unroll
+      for (int c = 0; c < 13; c++) s_f[c][pos] = v[c];
+      s_id[pos] = (int)f;
+    }
+    __syncthreads();
+    if (active && n < K) {
+      for (int j = 0; j < total; j++) {
+        const T xmin = s_f[9][j], ymin = s_f[10][j], xmax = s_f[11][j], ymax = s_f[12][j];
+        if (!(x0 >= xmin && x0 < xmax && y0 >= ymin && y0 < ymax)) continue;
+        const T aex = s_f[0][j] - x0, aey = s_f[1][j] - y0;
+        const T bex = s_f[2][j] - x0, bey = s_f[3][j] - y0;
+        const T cex = s_f[4][j] - x0, cey = s_f[5][j] - y0;
+        const T _w0 = bex * cey - bey * cex;
+        const T _w1 = cex * aey - cey * aex;
+        const T _w2 = aex * bey - aey * bex;
+        const T norm = _w0 + _w1 + _w2;
+        const T den = norm + dt_copysign_eps_f(eps, norm);
+        const T w0 = _w0 / den, w1 = _w1 / den, w2 = _w2 / den;
+        if (w0 >= (T)0 && w1 >= (T)0 && w2 >= (T)0) {
+          const T d = w0 * s_f[6][j] + w1 * s_f[7][j] + w2 * s_f[8][j];
+          if (d < hi && d >= lo) {
+            row_idx[n] = s_id[j];
+            row_d[n] = d;
+            row_w0[n] = w0;
+            row_w1[n] = w1;
+            if (++n == K) break;
+          }
+        }
+      }
+    }
+  }
+  if (active) {
+    for (int k = n; k < K; k++) {
+      row_idx[k] = -1;
+      row_d[k] = -INFINITY;
+      row_w0[k] = 0;
+      row_w1[k] = 0;
+    }
+  }
+}
+
+// deftet.py:294-306
+template <typename T>
+__global__ void __launch_bounds__(256)
+    deftet_resolve_kernel(int64_t F, int64_t P, int K, int D, const int64_t *__restrict__ idx,
+                          const T *__restrict__ depth, const T *__restrict__ w0a, const T *__restrict__ w1a,
+                          const T *__restrict__ feat, int64_t *__restrict__ sidx, T *__restrict__ weights,
+                          T *__restrict__ interp, int64_t rows) {
+  const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const int64_t b = r / P;
+  const int64_t base = r * K;
+  int n = 0;
+  while (n < K && idx[base + n] >= 0) n++;
+  const T *mf = feat + b * F * 3 * D;
+  for (int i = 0; i < n; i++) {
+    const T di = depth[base + i];
+    int rank = 0;
+    for (int j = 0; j < n; j++) {
+      const T dj = depth[base + j];
+      rank += (dj > di || (dj == di && j < i)) ? 1 : 0;
+    }
+    const int64_t o = base + rank;
+    const int64_t fid = idx[base + i];
+    const T w0 = w0a[base + i], w1 = w1a[base + i];
+    const T w2 = (T)1 - (w0 + w1);
+    sidx[o] = fid;
+    weights[o * 3 + 0] = w0;
+    weights[o * 3 + 1] = w1;
+    weights[o * 3 + 2] = w2;
+    const T *f0 = mf + fid * 3 * D;
+    for (int c = 0; c < D; c++) interp[o * D + c] = w0 * f0[c] + w1 * f0[D + c] + w2 * f0[2 * D + c];
+  }
+  for (int k = n; k < K; k++) {
+    const int64_t o = base + k;
+    sidx[o] = -1;
+    weights[o * 3 + 0] = 0;
+    weights[o * 3 + 1] = 0;
+    weights[o * 3 + 2] = 0;
+    for (int c = 0; c < D; c++) interp[o * D + c] = 0;
+  }
+}
+
+__device__ __forceinline__ void dt_atomic_add(float *p, float v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void dt_atomic_add(double *p, double v) { unsafeAtomicAdd(p, v); }
+
+// deftet_cuda.cu:240-420
+template <typename T>
+__global__ void __launch_bounds__(256)
+    deftet_bwd_kernel(int64_t F, int64_t PK, int D, const T *__restrict__ grad, const int64_t *__restrict__ idx,
+                      const T *__restrict__ weights, const T *__restrict__ fvi, const T *__restrict__ feat, float eps,
+                      T *__restrict__ g_img, T *__restrict__ g_feat, int64_t items) {
+  const int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (it >= items) return;
+  const int64_t fid = idx[it];
+  if (fid < 0) return;
+  const int64_t b = it / PK;
+  const int64_t face = b * F + fid;
+  const T *g = grad + it * D;
+  const T aw = weights[it * 3 + 0], bw = weights[it * 3 + 1], cw = weights[it * 3 + 2];
+  const T wv[3] = {aw, bw, cw};
+  T *gf = g_feat + face * 3 * D;
+  for (int ii = 0; ii < 3; ii++)
+    for (int c = 0; c < D; c++) dt_atomic_add(gf + ii * D + c, g[c] * wv[ii]);
+
+  const T *im = fvi + face * 6;
+  const T ax = im[0], ay = im[1], bx = im[2], by = im[3], cx = im[4], cy = im[5];
+  const T x0 = aw * ax + bw * bx + cw * cx;
+  const T y0 = aw * ay + bw * by + cw * cy;
+  const T m = bx - ax, p = by - ay, n = cx - ax, q = cy - ay, s = x0 - ax, t = y0 - ay;
+  const T k1 = s * q - n * t;
+  const T k2 = m * t - s * p;
+  T k3 = m * q - n * p;
+  k3 += copysign((double)eps, (double)k3);  // evaluated in double, rounded to T (as the reference)
+
+  const T zero = 0;
+  const T dk1dm = zero, dk1dn = -t, dk1dp = zero, dk1dq = s, dk1ds = q, dk1dt = -n;
+  const T dk2dm = t, dk2dn = zero, dk2dp = -s, dk2dq = zero, dk2ds = -p, dk2dt = m;
+  const T dk3dm = q, dk3dn = -p, dk3dp = -n, dk3dq = m, dk3ds = zero, dk3dt = zero;
+
+  const T dw1dm = dk1dm * k3 - dk3dm * k1, dw1dn = dk1dn * k3 - dk3dn * k1;
+  const T dw1dp = dk1dp * k3 - dk3dp * k1, dw1dq = dk1dq * k3 - dk3dq * k1;
+  const T dw1ds = dk1ds * k3 - dk3ds * k1, dw1dt = dk1dt * k3 - dk3dt * k1;
+  const T dw2dm = dk2dm * k3 - dk3dm * k2, dw2dn = dk2dn * k3 - dk3dn * k2;
+  const T dw2dp = dk2dp * k3 - dk3dp * k2, dw2dq = dk2dq * k3 - dk3dq * k2;
+  const T dw2ds = dk2ds * k3 - dk3ds * k2, dw2dt = dk2dt * k3 - dk3dt * k2;
+
+  const T dw1dax = -(dw1dm + dw1dn + dw1ds), dw1day = -(dw1dp + dw1dq + dw1dt);
+  const T dw1dbx = dw1dm, dw1dby = dw1dp, dw1dcx = dw1dn, dw1dcy = dw1dq;
+  const T dw2dax = -(dw2dm + dw2dn + dw2ds), dw2day = -(dw2dp + dw2dq + dw2dt);
+  const T dw2dbx = dw2dm, dw2dby = dw2dp, dw2dcx = dw2dn, dw2dcy = dw2dq;
+
+  T acc[6] = {0, 0, 0, 0, 0, 0};
+  const T *fa = feat + face * 3 * D;
+  const T kk = k3 * k3;
+  for (int c = 0; c < D; c++) {
+    const T c0 = fa[c], c1 = fa[D + c], c2 = fa[2 * D + c];
+    const T dIdax = (c1 - c0) * dw1dax + (c2 - c0) * dw2dax;
+    const T dIday = (c1 - c0) * dw1day + (c2 - c0) * dw2day;
+    const T dIdbx = (c1 - c0) * dw1dbx + (c2 - c0) * dw2dbx;
+    const T dIdby = (c1 - c0) * dw1dby + (c2 - c0) * dw2dby;
+    const T dIdcx = (c1 - c0) * dw1dcx + (c2 - c0) * dw2dcx;
+    const T dIdcy = (c1 - c0) * dw1dcy + (c2 - c0) * dw2dcy;
+    const T dldI = g[c] / kk;
+    acc[0] += dldI * dIdax; acc[1] += dldI * dIday;
+    acc[2] += dldI * dIdbx; acc[3] += dldI * dIdby;
+    acc[4] += dldI * dIdcx; acc[5] += dldI * dIdcy;
+  }
+  T *gi = g_img + face * 6;
+#pragma unroll
+  for (int c = 0; c < 6; c++) dt_atomic_add(gi + c, acc[c]);
+}
+
+template <typename T>
+static int deftet_forward(int64_t B, int64_t F, int64_t P, int64_t K, const void *fvz, const void *fvi,
+                          const void *bboxes, const void *pix, const void *ranges, float eps, int64_t *idx, void *depth,
+                          void *w0, void *w1, hipStream_t st) {
+  hipLaunchKernelGGL(deftet_fwd_kernel<T>, dim3((unsigned)cdiv(P, kDtTile), (unsigned)B), dim3(kDtTile), 0, st, F, P,
+                     (int)K, (const T *)fvz, (const T *)fvi, (const T *)bboxes, (const T *)pix, (const T *)ranges, eps,
+                     idx, (T *)depth, (T *)w0, (T *)w1);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+template <typename T>
+static int deftet_resolve(int64_t B, int64_t F, int64_t P, int64_t K, int64_t D, const int64_t *idx, const void *depth,
+                          const void *w0, const void *w1, const void *feat, int64_t *sidx, void *weights, void *interp,
+                          hipStream_t st) {
+  const int64_t rows = B * P;
+  hipLaunchKernelGGL(deftet_resolve_kernel<T>, dim3((unsigned)cdiv(rows, 256)), dim3(256), 0, st, F, P, (int)K, (int)D,
+                     idx, (const T *)depth, (const T *)w0, (const T *)w1, (const T *)feat, sidx, (T *)weights,
+                     (T *)interp, rows);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+template <typename T>
+static int deftet_backward(int64_t B, int64_t F, int64_t P, int64_t K, int64_t D, const void *grad, const int64_t *idx,
+                           const void *weights, const void *fvi, const void *feat, float eps, void *g_img,
+                           void *g_feat, hipStream_t st) {
+  KL_CHECK_RC(fill_async(g_img, 0, (size_t)(B * F * 6) * sizeof(T), st));
+  KL_CHECK_RC(fill_async(g_feat, 0, (size_t)(B * F * 3 * D) * sizeof(T), st));
+  const int64_t items = B * P * K;
+  if (items == 0) return KL_OK;
+  hipLaunchKernelGGL(deftet_bwd_kernel<T>, dim3((unsigned)cdiv(items, 256)), dim3(256), 0, st, F, P * K, (int)D,
+                     (const T *)grad, idx, (const T *)weights, (const T *)fvi, (const T *)feat, eps, (T *)g_img,
+                     (T *)g_feat, items);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+}  // namespace kl
+
+using namespace kl;
+
+static int check_deftet_sizes(int64_t B, int64_t F, int64_t P, int64_t K, int64_t D) {
+  KL_REQUIRE(B >= 0 && F >= 0 && P >= 0 && K >= 0 && D >= 0, "deftet_sparse_render: negative size");
+  KL_REQUIRE(B < 65536, "deftet_sparse_render: batch_size must be < 65536");
+  KL_REQUIRE(F < ((int64_t)1 << 31), "deftet_sparse_render: num_faces must be < 2^31");
+  KL_REQUIRE(K < ((int64_t)1 << 31) && D < ((int64_t)1 << 20), "deftet_sparse_render: knum / feature_dim too large");
+  KL_REQUIRE(P < ((int64_t)1 << 40), "deftet_sparse_render: num_pixels too large");
+  return KL_OK;
+}
+
+#define KL_DT_DISPATCH(dtype, FN, ...)                          \
+  switch (dtype) {                                              \
+    case KL_F32: return FN<float>(__VA_ARGS__);                 \
+    case KL_F64: return FN<double>(__VA_ARGS__);                \
+    default: set_error("expected a Float or Double tensor");    \
+      return KL_E_INVALID;                                      \
+  }
+
+extern "C" int kl_deftet_sparse_render_forward(kl_dtype dtype, int64_t batch_size, int64_t num_faces,
+                                               int64_t num_pixels, int64_t knum, const void *face_vertices_z,
+                                               const void *face_vertices_image, const void *face_bboxes,
+                                               const void *pixel_coords, const void *pixel_depth_ranges, float eps,
+                                               int64_t *face_idx, void *pixel_depths, void *w0, void *w1,
+                                               kl_stream stream) {
+  KL_CHECK_RC(check_deftet_sizes(batch_size, num_faces, num_pixels, knum, 0));
+  if (batch_size == 0 || num_pixels == 0 || knum == 0) return KL_OK;
+  KL_DT_DISPATCH(dtype, deftet_forward, batch_size, num_faces, num_pixels, knum, face_vertices_z, face_vertices_image,
+                 face_bboxes, pixel_coords, pixel_depth_ranges, eps, face_idx, pixel_depths, w0, w1, S(stream));
+}
+
+extern "C" int kl_deftet_sparse_render_resolve(kl_dtype dtype, int64_t batch_size, int64_t num_faces,
+                                               int64_t num_pixels, int64_t knum, int64_t feat_dim,
+                                               const int64_t *face_idx, const void *pixel_depths, const void *w0,
+                                               const void *w1, const void *face_features, int64_t *sorted_face_idx,
+                                               void *weights, void *interpolated_features, kl_stream stream) {
+  KL_CHECK_RC(check_deftet_sizes(batch_size, num_faces, num_pixels, knum, feat_dim));
+  if (batch_size == 0 || num_pixels == 0 || knum == 0) return KL_OK;
+  KL_DT_DISPATCH(dtype, deftet_resolve, batch_size, num_faces, num_pixels, knum, feat_dim, face_idx, pixel_depths, w0,
+                 w1, face_features, sorted_face_idx, weights, interpolated_features, S(stream));
+}
+
+extern "C" int kl_deftet_sparse_render_backward(kl_dtype dtype, int64_t batch_size, int64_t num_faces,
+                                                int64_t num_pixels, int64_t knum, int64_t feat_dim,
+                                                const void *grad_interpolated_features, const int64_t *face_idx,
+                                                const void *weights, const void *face_vertices_image,
+                                                const void *face_features, float eps, void *grad_face_vertices_image,
+                                                void *grad_face_features, kl_stream stream) {
+  KL_CHECK_RC(check_deftet_sizes(batch_size, num_faces, num_pixels, knum, feat_dim));
+  KL_DT_DISPATCH(dtype, deftet_backward, batch_size, num_faces, num_pixels, knum, feat_dim, grad_interpolated_features,
+                 face_idx, weights, face_vertices_image, face_features, eps, grad_face_vertices_image,
+                 grad_face_features, S(stream));
+}

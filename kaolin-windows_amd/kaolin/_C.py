@@ -165,6 +165,93 @@ def dibr_soft_mask_backward_cuda(grad_soft_mask, soft_mask, selected_face_idx, c
     return g
 
 
+# ------------------------------------------------------------------------ render.mesh.deftet
+def deftet_sparse_render_forward_cuda(face_vertices_z, face_vertices_image, face_bboxes, pixel_coords,
+                                      pixel_depth_ranges, knum, eps):
+    """deftet.cpp:49-111: [face_idx (B,P,K) i64 (mesh order, -1 pad), pixel_depths (-inf pad), w0, w1]."""
+    func = 'deftet_sparse_render_forward_cuda'
+    args = [Arg(face_vertices_z, 'face_vertices_z', 1), Arg(face_vertices_image, 'face_vertices_image', 2),
+            Arg(face_bboxes, 'face_bboxes', 3), Arg(pixel_coords, 'pixel_coords', 4),
+            Arg(pixel_depth_ranges, 'pixel_depth_ranges', 5)]
+    check_all_same_gpu(func, args)
+    check_contiguous(func, args)
+    B, F = face_vertices_z.shape[:2]
+    P = pixel_coords.shape[1]
+    check_size(func, args[0], (B, F, 3))
+    check_size(func, args[1], (B, F, 3, 2))
+    check_size(func, args[2], (B, F, 4))
+    check_size(func, args[3], (B, P, 2))
+    check_size(func, args[4], (B, P, 2))
+    _float_only(func, face_vertices_z)
+    N.require_gpu(func, face_vertices_z)
+    return deftet_forward(func, face_vertices_z, face_vertices_image, face_bboxes, pixel_coords, pixel_depth_ranges,
+                          knum, eps)
+
+
+def deftet_forward(func, fvz, fvi, bboxes, pix, ranges, knum, eps):
+    """The forward kernel on checked, contiguous inputs; ``bboxes`` may be None (computed in-kernel
+    with the same min / max as deftet.py:290-292)."""
+    B, F = fvz.shape[:2]
+    P = pix.shape[1]
+    K = int(knum)
+    dev, dtype = fvz.device, fvz.dtype
+    idx = torch.empty((B, P, K), dtype=torch.long, device=dev)
+    depth = torch.empty((B, P, K), dtype=dtype, device=dev)
+    w0 = torch.empty((B, P, K), dtype=dtype, device=dev)
+    w1 = torch.empty((B, P, K), dtype=dtype, device=dev)
+    with torch.cuda.device(dev), N.timed(func, dev):
+        N.check(N.lib().kl_deftet_sparse_render_forward(
+            N.dtype_code(dtype), B, F, P, K, N.ptr(fvz), N.ptr(fvi), N.ptr(bboxes), N.ptr(pix), N.ptr(ranges),
+            float(eps), N.ptr(idx), N.ptr(depth), N.ptr(w0), N.ptr(w1), N.stream_of(dev)), func)
+    return [idx, depth, w0, w1]
+
+
+def deftet_resolve(face_idx, pixel_depths, w0, w1, face_features):
+    """deftet.py:294-306 (DeftetSparseRenderer.forward's torch glue) as one kernel (not a reference
+    _C name): (sorted_face_idx (B,P,K), weights (B,P,K,3), interpolated_features (B,P,K,D))."""
+    func = 'deftet_sparse_render_resolve'
+    B, P, K = face_idx.shape
+    F, D = face_features.shape[1], face_features.shape[3]
+    dev, dtype = face_features.device, face_features.dtype
+    sidx = torch.empty((B, P, K), dtype=torch.long, device=dev)
+    weights = torch.empty((B, P, K, 3), dtype=dtype, device=dev)
+    interp = torch.empty((B, P, K, D), dtype=dtype, device=dev)
+    with torch.cuda.device(dev), N.timed(func, dev):
+        N.check(N.lib().kl_deftet_sparse_render_resolve(
+            N.dtype_code(dtype), B, F, P, K, D, N.ptr(face_idx), N.ptr(pixel_depths), N.ptr(w0), N.ptr(w1),
+            N.ptr(face_features), N.ptr(sidx), N.ptr(weights), N.ptr(interp), N.stream_of(dev)), func)
+    return sidx, weights, interp
+
+
+def deftet_sparse_render_backward_cuda(grad_interpolated_features, face_idx, weights, face_vertices_image,
+                                       face_features, eps):
+    """deftet.cpp:113-163: [grad_face_vertices_image, grad_face_features]."""
+    func = 'deftet_sparse_render_backward_cuda'
+    args = [Arg(grad_interpolated_features, 'grad_interpolated_features', 1), Arg(face_idx, 'face_idx', 2),
+            Arg(weights, 'weights', 3), Arg(face_vertices_image, 'face_vertices_image', 4),
+            Arg(face_features, 'face_features', 5)]
+    check_all_same_gpu(func, args)
+    check_contiguous(func, args)
+    B, P, K, D = grad_interpolated_features.shape
+    F = face_vertices_image.shape[1]
+    check_size(func, args[0], (B, P, K, D))
+    check_size(func, args[1], (B, P, K))
+    check_size(func, args[2], (B, P, K, 3))
+    check_size(func, args[3], (B, F, 3, 2))
+    check_size(func, args[4], (B, F, 3, D))
+    _float_only(func, grad_interpolated_features)
+    N.require_gpu(func, grad_interpolated_features)
+    dev = face_vertices_image.device
+    g_img = torch.empty_like(face_vertices_image)
+    g_feat = torch.empty_like(face_features)
+    with torch.cuda.device(dev), N.timed(func, dev):
+        N.check(N.lib().kl_deftet_sparse_render_backward(
+            N.dtype_code(face_vertices_image.dtype), B, F, P, K, D, N.ptr(grad_interpolated_features),
+            N.ptr(face_idx), N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), float(eps),
+            N.ptr(g_img), N.ptr(g_feat), N.stream_of(dev)), func)
+    return [g_img, g_feat]
+
+
 # ------------------------------------------------------------------------------ metrics
 def unbatched_triangle_distance_forward_cuda(points, face_vertices, dist, face_idx, dist_type):
     """unbatched_triangle_distance.cpp:43-72 (writes into the caller's tensors)."""
@@ -534,7 +621,9 @@ render = _module('kaolin._C.render')
 render.mesh = _module('kaolin._C.render.mesh', packed_rasterize_forward_cuda=packed_rasterize_forward_cuda,
                       rasterize_backward_cuda=rasterize_backward_cuda,
                       dibr_soft_mask_forward_cuda=dibr_soft_mask_forward_cuda,
-                      dibr_soft_mask_backward_cuda=dibr_soft_mask_backward_cuda)
+                      dibr_soft_mask_backward_cuda=dibr_soft_mask_backward_cuda,
+                      deftet_sparse_render_forward_cuda=deftet_sparse_render_forward_cuda,
+                      deftet_sparse_render_backward_cuda=deftet_sparse_render_backward_cuda)
 render.spc = _module('kaolin._C.render.spc', raytrace_cuda=raytrace_cuda,
                      mark_pack_boundaries_cuda=mark_pack_boundaries_cuda, diff_cuda=diff_cuda,
                      inclusive_sum_cuda=inclusive_sum_cuda, sum_reduce_cuda=sum_reduce_cuda,

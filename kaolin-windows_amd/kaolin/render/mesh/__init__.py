@@ -1,2 +1,3 @@
 from .rasterization import rasterize  # noqa: F401
 from .dibr import dibr_soft_mask, dibr_rasterization  # noqa: F401
+from .deftet import deftet_sparse_render  # noqa: F401

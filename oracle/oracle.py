@@ -355,3 +355,128 @@ def pack_scan(feats, starts, exclusive, reverse, op):
             for i in range(e - 2, b - 1, -1):
                 out[i] = f(feats[i + off], out[i + 1])
     return out
+
+
+# ---------------------------------------------------------------------------------------------
+# DefTet sparse render (render/mesh/deftet.py:269-417; kernels deftet_cuda.cu:32-190, 240-420).
+# numpy restatement in the input dtype, no fused multiply-add (every product and sum rounded,
+# as the HIP build with -ffp-contract=off).  Loops over pixels, vectorised over faces.
+def _copysign_eps_f(eps, v, dtype):
+    # copysignf((double)eps, (double)v): both operands rounded to float (deftet_cuda.cu fwd)
+    return np.copysign(np.float32(eps), v.astype(np.float32)).astype(dtype)
+
+
+def deftet_sparse_render_forward(fvz, fvi, bboxes, pix, ranges, knum, eps=1e-8):
+    """deftet_sparse_render_forward_cuda (deftet.cpp:49-111): the first knum hits in MESH order.
+    bboxes may be None (min / max over the vertices, deftet.py:290-292).
+    Returns face_idx (B,P,K) int64 (-1 pad), depth (-inf pad), w0, w1 (0 pad)."""
+    dt = fvz.dtype
+    B, F = fvz.shape[:2]
+    P = pix.shape[1]
+    K = int(knum)
+    if bboxes is None:
+        bboxes = np.concatenate([fvi.min(axis=2), fvi.max(axis=2)], axis=-1)
+    idx = np.full((B, P, K), -1, np.int64)
+    depth = np.full((B, P, K), -np.inf, dt)
+    w0o = np.zeros((B, P, K), dt)
+    w1o = np.zeros((B, P, K), dt)
+    for b in range(B):
+        ax, ay, bx, by, cx, cy = (fvi[b, :, v // 2, v % 2] for v in range(6))
+        az, bz, cz = fvz[b, :, 0], fvz[b, :, 1], fvz[b, :, 2]
+        bb = bboxes[b]
+        for p in range(P):
+            x0, y0 = pix[b, p, 0], pix[b, p, 1]
+            lo, hi = ranges[b, p, 0], ranges[b, p, 1]
+            f = np.nonzero((x0 >= bb[:, 0]) & (x0 < bb[:, 2]) & (y0 >= bb[:, 1]) & (y0 < bb[:, 3]))[0]
+            if f.size == 0:
+                continue
+            aex, aey = ax[f] - x0, ay[f] - y0
+            bex, bey = bx[f] - x0, by[f] - y0
+            cex, cey = cx[f] - x0, cy[f] - y0
+            _w0 = bex * cey - bey * cex
+            _w1 = cex * aey - cey * aex
+            _w2 = aex * bey - aey * bex
+            norm = _w0 + _w1 + _w2
+            den = norm + _copysign_eps_f(eps, norm, dt)
+            w0, w1, w2 = _w0 / den, _w1 / den, _w2 / den
+            d = w0 * az[f] + w1 * bz[f] + w2 * cz[f]
+            ok = (w0 >= 0) & (w1 >= 0) & (w2 >= 0) & (d < hi) & (d >= lo)
+            sel = np.nonzero(ok)[0][:K]
+            n = sel.size
+            idx[b, p, :n] = f[sel]
+            depth[b, p, :n] = d[sel]
+            w0o[b, p, :n] = w0[sel]
+            w1o[b, p, :n] = w1[sel]
+    return idx, depth, w0o, w1o
+
+
+def deftet_resolve(idx, depth, w0, w1, feat):
+    """deftet.py:294-306: stable descending depth order, weights (w0, w1, 1 - (w0 + w1)) and
+    interpolated features (w0 f0 + w1 f1) + w2 f2.  Returns (sorted_idx, weights, features)."""
+    dt = feat.dtype
+    B, P, K = idx.shape
+    order = np.argsort(-depth, axis=-1, kind='stable')
+    sidx = np.take_along_axis(idx, order, -1)
+    sw0 = np.take_along_axis(w0, order, -1)
+    sw1 = np.take_along_axis(w1, order, -1)
+    sw2 = (sidx != -1).astype(dt) - (sw0 + sw1)
+    weights = np.stack([sw0, sw1, sw2], axis=-1)
+    padded = np.concatenate([np.zeros_like(feat[:, :1]), feat], axis=1)  # (B,F+1,3,D)
+    sel = np.stack([padded[b][sidx[b] + 1] for b in range(B)])  # (B,P,K,3,D)
+    interp = sw0[..., None] * sel[..., 0, :] + sw1[..., None] * sel[..., 1, :] + sw2[..., None] * sel[..., 2, :]
+    return sidx, weights, interp
+
+
+def deftet_sparse_render(pix, ranges, fvz, fvi, feat, knum=300, eps=1e-8):
+    """DeftetSparseRenderer.forward: (interpolated_features, sorted_face_idx, weights)."""
+    idx, depth, w0, w1 = deftet_sparse_render_forward(fvz, fvi, None, pix, ranges, knum, eps)
+    sidx, weights, interp = deftet_resolve(idx, depth, w0, w1, feat)
+    return interp, sidx, weights
+
+
+def deftet_sparse_render_backward(grad, idx, weights, fvi, feat, eps=1e-8):
+    """deftet_sparse_render_backward_cuda (deftet_cuda.cu:240-420), per (pixel, slot) item with a
+    face, accumulated in item order (the reference's atomics are unordered)."""
+    dt = fvi.dtype
+    B, P, K, D = grad.shape
+    F = fvi.shape[1]
+    g_img = np.zeros_like(fvi)
+    g_feat = np.zeros_like(feat)
+    bi, pi, ki = np.nonzero(idx >= 0)
+    if bi.size == 0:
+        return g_img, g_feat
+    fid = idx[bi, pi, ki]
+    g = grad[bi, pi, ki]  # (N,D)
+    w = weights[bi, pi, ki]  # (N,3)
+    for ii in range(3):
+        np.add.at(g_feat, (bi, fid, ii), g * w[:, ii:ii + 1])
+    im = fvi[bi, fid].reshape(-1, 6)
+    ax, ay, bx, by, cx, cy = (im[:, c] for c in range(6))
+    aw, bw, cw = w[:, 0], w[:, 1], w[:, 2]
+    x0 = aw * ax + bw * bx + cw * cx
+    y0 = aw * ay + bw * by + cw * cy
+    m, p, n, q, s, t = bx - ax, by - ay, cx - ax, cy - ay, x0 - ax, y0 - ay
+    k1 = s * q - n * t
+    k2 = m * t - s * p
+    k3 = m * q - n * p
+    k3 = (k3.astype(np.float64) + np.copysign(np.float64(np.float32(eps)), k3.astype(np.float64))).astype(dt)
+    z = np.zeros_like(k3)
+    dk1 = dict(m=z, n=-t, p=z, q=s, s=q, t=-n)
+    dk2 = dict(m=t, n=z, p=-s, q=z, s=-p, t=m)
+    dk3 = dict(m=q, n=-p, p=-n, q=m, s=z, t=z)
+    dw1 = {v: dk1[v] * k3 - dk3[v] * k1 for v in 'mnpqst'}
+    dw2 = {v: dk2[v] * k3 - dk3[v] * k2 for v in 'mnpqst'}
+    d1 = [-(dw1['m'] + dw1['n'] + dw1['s']), -(dw1['p'] + dw1['q'] + dw1['t']), dw1['m'], dw1['p'], dw1['n'],
+          dw1['q']]
+    d2 = [-(dw2['m'] + dw2['n'] + dw2['s']), -(dw2['p'] + dw2['q'] + dw2['t']), dw2['m'], dw2['p'], dw2['n'],
+          dw2['q']]
+    fa = feat[bi, fid]  # (N,3,D)
+    c0, c1, c2 = fa[:, 0], fa[:, 1], fa[:, 2]
+    dldI = g / (k3 * k3)[:, None]
+    acc = np.zeros((bi.size, 6), dt)
+    for c in range(D):
+        for v in range(6):
+            dI = (c1[:, c] - c0[:, c]) * d1[v] + (c2[:, c] - c0[:, c]) * d2[v]
+            acc[:, v] = acc[:, v] + dldI[:, c] * dI
+    np.add.at(g_img.reshape(B, F, 6), (bi, fid), acc)
+    return g_img, g_feat

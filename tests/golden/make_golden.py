@@ -468,8 +468,86 @@ def rayops():
     save('rayops.npz', **arrays)
 
 
+# --------------------------------------------------------------------------
+# DefTet sparse render (tests/python/kaolin/render/mesh/test_deftet.py)
+# --------------------------------------------------------------------------
+def deftet():
+    """Simple-case KATs transcribed from test_deftet.py:36-230 (data only), and the model.obj
+    case of test_deftet.py:335-551 run through the reference's _naive_deftet_sparse_render
+    (forward + autograd backward) in f32 and f64."""
+    arrays = {
+        'simple_fvi': np.array(
+            [[[[-1., 0.], [0., -1.], [0., 1.]], [[-1., 0.], [0., 1.], [0., -1.]], [[0., -1.], [0., 1.], [1., 0.]]],
+             [[[-1., -1.], [1., -1.], [-1., 1.]], [[-1., -1.], [1., -1.], [-1., 1.]],
+              [[-1., -1.], [1., -1.], [-1., 1.]]]]),
+        'simple_fvz': np.array([[[-2., -1., -1.], [-2.5, -3., -3.], [-2., -2., -2.]],
+                                [[-2., -1., -3.], [-2., -2., -2.], [-2., -3., -1.]]]),
+        'simple_feat_face': np.array([[[[0.]] * 3, [[1.]] * 3, [[2.]] * 3], [[[3.]] * 3, [[4.]] * 3, [[5.]] * 3]]),
+        'simple_feat_vert': np.arange(18, dtype=np.float64).reshape(2, 3, 3, 1),
+        'simple_pix': np.array(
+            [[[-0.999, 0.], [-0.001, -0.998], [0.001, 0.998], [0.999, 0.], [-0.45, 0.], [0.45, 0.], [-0.999, -0.999]],
+             [[-0.998, -0.999], [0.998, -0.999], [-0.999, 0.998], [-0.001, -0.], [0., -0.999], [-0.999, 0.],
+              [0.001, 0.001]]]),
+        # test_full_render (range [-4, 0), knum=5)
+        'simple_full_idx': np.array(
+            [[[0, 1, -1, -1, -1], [0, 1, -1, -1, -1], [2, -1, -1, -1, -1], [2, -1, -1, -1, -1],
+              [0, 1, -1, -1, -1], [2, -1, -1, -1, -1], [-1, -1, -1, -1, -1]],
+             [[0, 1, 2, -1, -1], [0, 1, 2, -1, -1], [2, 1, 0, -1, -1], [2, 1, 0, -1, -1],
+              [0, 1, 2, -1, -1], [2, 1, 0, -1, -1], [-1, -1, -1, -1, -1]]], dtype=np.int64),
+        'simple_full_feat_vert': np.array(
+            [[[0., 3., 0., 0., 0.], [1., 5., 0., 0., 0.], [7., 0., 0., 0., 0.], [8., 0., 0., 0., 0.],
+              [0.825, 3.825, 0., 0., 0.], [7.175, 0., 0., 0., 0.], [0., 0., 0., 0., 0.]],
+             [[9., 12., 15., 0., 0.], [10., 13., 16., 0., 0.], [17., 14., 11., 0., 0.], [16.5, 13.5, 10.5, 0., 0.],
+              [9.5, 12.5, 15.5, 0., 0.], [16., 13., 10., 0., 0.], [0., 0., 0., 0., 0.]]]),
+        # test_restricted_range (range [-2.1, 0), knum=5)
+        'simple_restricted_idx': np.array(
+            [[[0, -1, -1, -1, -1], [0, -1, -1, -1, -1], [2, -1, -1, -1, -1], [2, -1, -1, -1, -1],
+              [0, -1, -1, -1, -1], [2, -1, -1, -1, -1], [-1, -1, -1, -1, -1]],
+             [[0, 1, 2, -1, -1], [0, 1, -1, -1, -1], [2, 1, -1, -1, -1], [2, 1, 0, -1, -1],
+              [0, 1, -1, -1, -1], [2, 1, -1, -1, -1], [-1, -1, -1, -1, -1]]], dtype=np.int64),
+        'simple_restricted_feat_vert': np.array(
+            [[[0., 0., 0., 0., 0.], [1., 0., 0., 0., 0.], [7., 0., 0., 0., 0.], [8., 0., 0., 0., 0.],
+              [0.825, 0., 0., 0., 0.], [7.175, 0., 0., 0., 0.], [0., 0., 0., 0., 0.]],
+             [[9., 12., 15., 0., 0.], [10., 13., 0., 0., 0.], [17., 14., 0., 0., 0.], [16.5, 13.5, 10.5, 0., 0.],
+              [9.5, 12.5, 0., 0., 0.], [16., 13., 0., 0., 0.], [0., 0., 0., 0., 0.]]]),
+    }
+    P, K = 128, 20
+    for dname, dtype in (('f32', torch.float), ('f64', torch.double)):
+        inp = _sphere_inputs(dtype, False)
+        fvz, fvi, fuv = inp['face_vertices_z'], inp['face_vertices_image'], inp['face_uvs']
+        vz = inp['vertices_camera_z']
+        B = fvz.shape[0]
+        g = torch.Generator().manual_seed(77)
+        pix = torch.rand((B, P, 2), generator=g, dtype=dtype) * 2. - 1.
+        arrays[f'{dname}_fvz'] = fvz
+        arrays[f'{dname}_fvi'] = fvi
+        arrays[f'{dname}_fuv'] = fuv
+        arrays[f'{dname}_pix'] = pix
+        for up in (0, 1):
+            min_z, max_z = vz.min(dim=1)[0], vz.max(dim=1)[0]
+            lo = (min_z + max_z) / 2. if up else min_z
+            rr = torch.nn.functional.pad(lo.unsqueeze(-1), (0, 1), value=0.).unsqueeze(1).repeat(1, P, 1)
+            fvi_r = fvi.clone().requires_grad_(True)
+            fuv_r = fuv.clone().requires_grad_(True)
+            feats, idx = _naive_deftet_sparse_render(pix, rr, fvz, fvi_r, fuv_r, K)
+            grad_out = torch.rand(feats.shape, generator=g, dtype=dtype)
+            feats.backward(grad_out)
+            q = f'{dname}_up{up}_'
+            arrays[q + 'ranges'] = rr
+            arrays[q + 'features'] = feats.detach()
+            arrays[q + 'face_idx'] = idx
+            arrays[q + 'grad_out'] = grad_out
+            arrays[q + 'grad_fvi'] = fvi_r.grad
+            arrays[q + 'grad_fuv'] = fuv_r.grad
+    save('deftet.npz', **arrays)
+
+
 if __name__ == '__main__':
     torch.set_num_threads(8)
+    if len(sys.argv) > 1:  # regenerate only the named fixtures
+        for name in sys.argv[1:]:
+            globals()[name]()
+        sys.exit(0)
     dibr_simple()
     dibr_sphere()
     p2m()
