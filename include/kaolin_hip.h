@@ -359,6 +359,23 @@ int kl_inclusive_sum_i32(int64_t num, const int32_t *info, int32_t *out, void *w
 int kl_sum_reduce(kl_dtype dtype, int64_t num_feats, int64_t feat_dim, const void *feats,
                   const int32_t *inclusive_sum, int64_t num_out, void *out, kl_stream stream);
 
+/* ------------------------------------------------------------ check_sign */
+
+/* mesh_intersection.cpp:33-68  unbatched_mesh_intersection_cuda (kernel
+ * mesh_intersection_cuda.cu:100-210).  points (P,3), verts_1/2/3 (F,3) face corners, dtype
+ * KL_F32 | KL_F64 -> result (P) in the same dtype: the number of faces the ray from each point
+ * toward +x crosses (edge / vertex hits counted once).  Fully written. */
+int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points, int64_t num_faces, const void *points,
+                                   const void *verts_1, const void *verts_2, const void *verts_3, void *result,
+                                   kl_stream stream);
+
+/* check_sign (ops/mesh/check_sign.py:25-154) for a batch in one launch: verts (B,V,3),
+ * faces (F,3) int64, points (B,P,3), maxlen (B) the per-mesh divisor check_sign.py:140-146
+ * applies to verts and points (NULL: none) -> contains (B,P) bool bytes (odd crossing count). */
+int kl_check_sign(kl_dtype dtype, int64_t batch_size, int64_t num_vertices, int64_t num_faces, int64_t num_points,
+                  const void *verts, const int64_t *faces, const void *points, const void *maxlen,
+                  uint8_t *contains, kl_stream stream);
+
 /* ------------------------------------------------------------ voxelgrid */
 
 /* trianglemeshes_to_voxelgrids (ops/conversions/trianglemesh.py:29-110) for ONE batch

@@ -1,0 +1,269 @@
+// checksign.hip -- point-in-mesh test by ray-crossing parity.
+//
+// Reference: kaolin/ops/mesh/check_sign.py:25-154 (check_sign, _unbatched_check_sign_cuda) over
+// mesh_intersection.cpp:33-68 (unbatched_mesh_intersection_cuda) and
+// mesh_intersection_cuda.cu:40-233 (kernel and helpers).
+//
+// Per (point q, face p1 p2 p3): skip when q's (y, z) lies outside the face's (y, z) bbox (the
+// bounds rounded to float, as the reference's `float y_min = min(...)`); the face separates q
+// from q + (10, 0, 0) when the signed volumes of the two ends differ in sign; then q's (y, z)
+// projection must be inside the projected triangle (three edge signed areas, each computed in
+// a direction-independent way), and a projection on an edge or a vertex counts only for the
+// face "below" it (mesh_intersection_cuda.cu:150-200), so that one crossing is one count.
+// `contains` = odd count.  Every operation in the reference's order, no contraction: the
+// counts are bit-identical.
+//
+// MI355X mapping: one lane per point, a register count per lane (the reference adds 1.0 with
+// a global atomicAdd per crossing).  A workgroup owns 256 points; faces stream through LDS in
+// tiles of 256 and each tile is culled against the workgroup's (y, z) point bbox with an
+// order-preserving block compaction, so lanes walk (LDS broadcast reads) only faces whose
+// bbox can hold one of the workgroup's points.  The batched entry gathers the face corners
+// from (vertices, faces) and applies check_sign's 1 / maxlen normalisation on load (the same
+// IEEE division the reference does in torch), so neither the normalised vertices nor the
+// (F, 3, 3) corner arrays are materialised.
+#include "common.h"
+
+namespace kl {
+
+constexpr int kCsTile = 256;
+
+struct CsV2 {
+  double x, y;
+};
+
+template <typename T>
+struct CsFaces {
+  const T *v1, *v2, *v3;   // (F,3) corner arrays (unbatched _C entry), or
+  const T *verts;          // (B,V,3) vertices with
+  const int64_t *faces;    // (F,3) indices (batched entry)
+  const T *maxlen;         // (B) divisor applied on load, or null
+  int64_t V;
+};
+
+// mesh_intersection_cuda.cu:71-82 (signed_area on the (y, z) projection)
+template <typename T>
+__device__ __forceinline__ T cs_signed_area(T ax, T ay, T bx, T by, T cx, T cy) {
+  if (cx > bx || (bx == cx && cy < by)) return -((by - cy) * (ax - cx) + (cx - bx) * (ay - cy));
+  return (cy - by) * (ax - bx) + (bx - cx) * (ay - by);
+}
+
+// mesh_intersection_cuda.cu:84-98
+template <typename T>
+__device__ __forceinline__ bool cs_above(T vx, T vy, T lx, T ly, T rx, T ry) {
+  const T v1x = rx - lx, v1y = ry - ly;
+  const T v2x = vx - lx, v2y = vy - ly;
+  return (v1x * v2y - v1y * v2x) > (T)0;
+}
+
+// mesh_intersection_cuda.cu:60-66: dot(cross(b - a, c - a), d - a)
+template <typename T>
+__device__ __forceinline__ T cs_signed_volume(T ax, T ay, T az, const T *b, const T *c, const T *d) {
+  const T ux = b[0] - ax, uy = b[1] - ay, uz = b[2] - az;
+  const T vx = c[0] - ax, vy = c[1] - ay, vz = c[2] - az;
+  const T nx = uy * vz - uz * vy, ny = uz * vx - ux * vz, nz = ux * vy - uy * vx;
+  return nx * (d[0] - ax) + ny * (d[1] - ay) + nz * (d[2] - az);
+}
+
+// one (point, face) pair: 1 when the ray from q crosses the face once (mesh_intersection_cuda.cu:120-205)
+template <typename T>
+__device__ __forceinline__ int cs_cross(T qx, T qy, T qz, const T *p1, const T *p2, const T *p3, const float *bb) {
+  // bbox_check (:45-55): the bounds are float
+  if (qy < (T)bb[0] || (T)bb[1] < qy || qz < (T)bb[2] || (T)bb[3] < qz) return 0;
+  const bool c1 = cs_signed_volume(qx, qy, qz, p1, p2, p3) > (T)0;
+  const bool c2 = cs_signed_volume(qx + (T)10., qy, qz, p1, p2, p3) > (T)0;
+  if (c1 == c2) return 0;
+  const T d1 = cs_signed_area(qy, qz, p1[1], p1[2], p2[1], p2[2]);
+  const T d2 = cs_signed_area(qy, qz, p2[1], p2[2], p3[1], p3[2]);
+  if (!(d1 * d2 >= (T)0)) return 0;
+  const T d3 = cs_signed_area(qy, qz, p3[1], p3[2], p1[1], p1[2]);
+  if (!(d3 * d1 >= (T)0 && d2 * d3 >= (T)0)) return 0;
+  bool on_edge = false, on_vertex = false;
+  T v1x = 0, v1y = 0, v2x = 0, v2y = 0, ox = 0, oy = 0;
+  if (qy == p1[1] && qz == p1[2]) {
+    on_vertex = true; v1x = p2[1]; v1y = p2[2]; v2x = p3[1]; v2y = p3[2];
+  } else if (qy == p2[1] && qz == p2[2]) {
+    on_vertex = true; v1x = p1[1]; v1y = p1[2]; v2x = p3[1]; v2y = p3[2];
+  } else if (qy == p3[1] && qz == p3[2]) {
+    on_vertex = true; v1x = p1[1]; v1y = p1[2]; v2x = p2[1]; v2y = p2[2];
+  } else if (d1 == (T)0) {
+    on_edge = true; v1x = p1[1]; v1y = p1[2]; v2x = p2[1]; v2y = p2[2]; ox = p3[1]; oy = p3[2];
+  } else if (d2 == (T)0) {
+    on_edge = true; v1x = p2[1]; v1y = p2[2]; v2x = p3[1]; v2y = p3[2]; ox = p1[1]; oy = p1[2];
+  } else if (d3 == (T)0) {
+    on_edge = true; v1x = p3[1]; v1y = p3[2]; v2x = p1[1]; v2y = p1[2]; ox = p2[1]; oy = p2[2];
+  }
+  if (!on_edge && !on_vertex) return 1;
+  if (v1x > v2x || (v1x == v2x && v1y > v2y)) {
+    T tx = v1x, ty = v1y;
+    v1x = v2x; v1y = v2y; v2x = tx; v2y = ty;
+  }
+  if (on_edge) return cs_above(ox, oy, v1x, v1y, v2x, v2y) ? 0 : 1;
+  // is_valid_overlap_vertice (:93-98)
+  return (cs_above(qy, qz, v1x, v1y, v2x, v2y) && (v1x < qy) && (v2x >= qy)) ? 1 : 0;
+}
+
+template <typename T>
+__device__ __forceinline__ void cs_load_face(const CsFaces<T> &src, int64_t b, int64_t f, T *v) {
+  if (src.faces) {
+    const T *vb = src.verts + b * src.V * 3;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const int64_t vi = src.faces[f * 3 + c];
+#pragma unroll
+      for (int k = 0; k < 3; k++) v[c * 3 + k] = vb[vi * 3 + k];
+    }
+    if (src.maxlen) {
+      const T m = src.maxlen[b];
+#pragma unroll
+      for (int k = 0; k < 9; k++) v[k] = v[k] / m;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      v[k] = src.v1[f * 3 + k];
+      v[3 + k] = src.v2[f * 3 + k];
+      v[6 + k] = src.v3[f * 3 + k];
+    }
+  }
+}
+
+// grid (cdiv(P, 256), B); counts (B,P) in T (the _C contract) and/or contains (B,P) bool
+template <typename T>
+__global__ void __launch_bounds__(kCsTile)
+    check_sign_kernel(int64_t P, int64_t F, const T *__restrict__ points, CsFaces<T> src, T *__restrict__ counts,
+                      uint8_t *__restrict__ contains) {
+  __shared__ T s_v[9][kCsTile];
+  __shared__ float s_bb[4][kCsTile];
+  __shared__ int s_wave[16];
+  __shared__ T s_box[4][kCsTile / 64];
+
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y;
+  const int64_t p = (int64_t)blockIdx.x * kCsTile + tid;
+  const bool active = p < P;
+  const int64_t row = b * P + p;
+  T qx = 0, qy = 0, qz = 0;
+  if (active) {
+    const T *q = points + row * 3;
+    qx = q[0]; qy = q[1]; qz = q[2];
+    if (src.maxlen) {  // check_sign.py:146: points / maxlen
+      const T m = src.maxlen[b];
+      qx = qx / m; qy = qy / m; qz = qz / m;
+    }
+  }
+  {
+    T ymn = INFINITY, zmn = INFINITY, ymx = -INFINITY, zmx = -INFINITY;
+    if (active && qy == qy && qz == qz) {
+      ymn = qy; ymx = qy; zmn = qz; zmx = qz;
+    }
+    ymn = wave_min(ymn); zmn = wave_min(zmn);
+    ymx = wave_max(ymx); zmx = wave_max(zmx);
+    if ((tid & 63) == 0) {
+      s_box[0][tid >> 6] = ymn; s_box[1][tid >> 6] = ymx;
+      s_box[2][tid >> 6] = zmn; s_box[3][tid >> 6] = zmx;
+    }
+  }
+  __syncthreads();
+  T gymn = s_box[0][0], gymx = s_box[1][0], gzmn = s_box[2][0], gzmx = s_box[3][0];
+#pragma unroll
+  for (int w = 1; w < kCsTile / 64; w++) {
+    gymn = s_box[0][w] < gymn ? s_box[0][w] : gymn;
+    gymx = s_box[1][w] > gymx ? s_box[1][w] : gymx;
+    gzmn = s_box[2][w] < gzmn ? s_box[2][w] : gzmn;
+    gzmx = s_box[3][w] > gzmx ? s_box[3][w] : gzmx;
+  }
+
+  int count = 0;
+  for (int64_t t0 = 0; t0 < F; t0 += kCsTile) {
+    const int64_t f = t0 + tid;
+    T v[9];
+    float bb[4];
+    bool keep = false;
+    if (f < F) {
+      cs_load_face(src, b, f, v);
+      // float y_min = min(b.y, min(c.y, d.y)) etc. (:47-50)
+      bb[0] = (float)fmin(v[1], fmin(v[4], v[7]));
+      bb[1] = (float)fmax(v[1], fmax(v[4], v[7]));
+      bb[2] = (float)fmin(v[2], fmin(v[5], v[8]));
+      bb[3] = (float)fmax(v[2], fmax(v[5], v[8]));
+      // some point of the workgroup can pass bbox_check (NaN bounds never pass it)
+      keep = (T)bb[0] <= gymx && (T)bb[1] >= gymn && (T)bb[2] <= gzmx && (T)bb[3] >= gzmn;
+    }
+    int total;
+    const int pos = block_exclusive_scan(keep ? 1 : 0, s_wave, &total);
+    if (keep) {
+#pragma unroll
+      for (int k = 0; k < 9; k++) s_v[k][pos] = v[k];
+#pragma unroll
+      for (int k = 0; k < 4; k++) s_bb[k][pos] = bb[k];
+    }
+    __syncthreads();
+    if (active) {
+      for (int j = 0; j < total; j++) {
+        const T p1[3] = {s_v[0][j], s_v[1][j], s_v[2][j]};
+        const T p2[3] = {s_v[3][j], s_v[4][j], s_v[5][j]};
+        const T p3[3] = {s_v[6][j], s_v[7][j], s_v[8][j]};
+        const float bbj[4] = {s_bb[0][j], s_bb[1][j], s_bb[2][j], s_bb[3][j]};
+        count += cs_cross(qx, qy, qz, p1, p2, p3, bbj);
+      }
+    }
+    __syncthreads();
+  }
+  if (active) {
+    if (counts) counts[row] = (T)count;
+    if (contains) contains[row] = (uint8_t)(count & 1);
+  }
+}
+
+template <typename T>
+static int check_sign_launch(int64_t B, int64_t P, int64_t F, const void *points, const CsFaces<T> &src, void *counts,
+                             uint8_t *contains, hipStream_t st) {
+  if (B == 0 || P == 0) return KL_OK;
+  hipLaunchKernelGGL(check_sign_kernel<T>, dim3((unsigned)cdiv(P, kCsTile), (unsigned)B), dim3(kCsTile), 0, st, P, F,
+                     (const T *)points, src, (T *)counts, contains);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+template <typename T>
+static int mesh_intersection_unbatched(int64_t P, int64_t F, const void *points, const void *v1, const void *v2,
+                                       const void *v3, void *counts, hipStream_t st) {
+  CsFaces<T> src{(const T *)v1, (const T *)v2, (const T *)v3, nullptr, nullptr, nullptr, 0};
+  return check_sign_launch<T>(1, P, F, points, src, counts, nullptr, st);
+}
+
+template <typename T>
+static int check_sign_batched(int64_t B, int64_t V, int64_t F, int64_t P, const void *verts, const int64_t *faces,
+                              const void *points, const void *maxlen, uint8_t *contains, hipStream_t st) {
+  CsFaces<T> src{nullptr, nullptr, nullptr, (const T *)verts, faces, (const T *)maxlen, V};
+  return check_sign_launch<T>(B, P, F, points, src, nullptr, contains, st);
+}
+
+}  // namespace kl
+
+using namespace kl;
+
+#define KL_CS_DISPATCH(dtype, FN, ...)                          \
+  switch (dtype) {                                              \
+    case KL_F32: return FN<float>(__VA_ARGS__);                 \
+    case KL_F64: return FN<double>(__VA_ARGS__);                \
+    default: set_error("expected a Float or Double tensor");    \
+      return KL_E_INVALID;                                      \
+  }
+
+extern "C" int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points, int64_t num_faces, const void *points,
+                                              const void *verts_1, const void *verts_2, const void *verts_3,
+                                              void *result, kl_stream stream) {
+  KL_REQUIRE(num_points >= 0 && num_faces >= 0, "unbatched_mesh_intersection: negative size");
+  KL_CS_DISPATCH(dtype, mesh_intersection_unbatched, num_points, num_faces, points, verts_1, verts_2, verts_3, result,
+                 S(stream));
+}
+
+extern "C" int kl_check_sign(kl_dtype dtype, int64_t batch_size, int64_t num_vertices, int64_t num_faces,
+                             int64_t num_points, const void *verts, const int64_t *faces, const void *points,
+                             const void *maxlen, uint8_t *contains, kl_stream stream) {
+  KL_REQUIRE(batch_size >= 0 && num_vertices >= 0 && num_faces >= 0 && num_points >= 0, "check_sign: negative size");
+  KL_REQUIRE(batch_size < 65536, "check_sign: batch_size must be < 65536");
+  KL_CS_DISPATCH(dtype, check_sign_batched, batch_size, num_vertices, num_faces, num_points, verts, faces, points,
+                 maxlen, contains, S(stream));
+}

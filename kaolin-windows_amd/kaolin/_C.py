@@ -348,6 +348,47 @@ def sided_distance_backward_cuda(grad_output, p1, p2, idx):
     return [g1, g2]
 
 
+# ----------------------------------------------------------------------------- ops.mesh
+def unbatched_mesh_intersection_cuda(points, verts_1, verts_2, verts_3):
+    """mesh_intersection.cpp:33-68: crossing counts (P,) in the points dtype."""
+    func = 'unbatched_mesh_intersection_cuda'
+    args = [Arg(points, 'points', 1), Arg(verts_1, 'verts_1', 2), Arg(verts_2, 'verts_2', 3),
+            Arg(verts_3, 'verts_3', 4)]
+    check_all_same_gpu(func, args)
+    check_contiguous(func, args)
+    for a in args[1:]:
+        check_same_type(func, args[0], a)
+    P = points.shape[0]
+    F = verts_1.shape[0]
+    check_size(func, args[0], (P, 3))
+    for a in args[1:]:
+        check_size(func, a, (F, 3))
+    if points.dtype not in _FLOATS:
+        raise RuntimeError(f'unbatched_mesh_intersection_cuda not implemented for \'{_tname(points.dtype)}\'')
+    N.require_gpu(func, points)
+    dev = points.device
+    out = torch.empty((P,), dtype=points.dtype, device=dev)
+    with torch.cuda.device(dev), N.timed(func, dev):
+        N.check(N.lib().kl_unbatched_mesh_intersection(N.dtype_code(points.dtype), P, F, N.ptr(points), N.ptr(verts_1),
+                                                       N.ptr(verts_2), N.ptr(verts_3), N.ptr(out),
+                                                       N.stream_of(dev)), func)
+    return out
+
+
+def check_sign_batched(verts, faces, points, maxlen):
+    """check_sign.py:140-154 for the whole batch in one launch (not a reference _C name):
+    contains (B,P) bool, faces gathered and 1 / maxlen applied in-kernel."""
+    func = 'check_sign'
+    B, V = verts.shape[:2]
+    F, P = faces.shape[0], points.shape[1]
+    dev = points.device
+    out = torch.empty((B, P), dtype=torch.bool, device=dev)
+    with torch.cuda.device(dev), N.timed(func, dev):
+        N.check(N.lib().kl_check_sign(N.dtype_code(verts.dtype), B, V, F, P, N.ptr(verts), N.ptr(faces), N.ptr(points),
+                                      N.ptr(maxlen), N.ptr(out), N.stream_of(dev)), func)
+    return out
+
+
 # ------------------------------------------------------------------- ops.conversions / spc
 def mesh_to_spc_cuda(face_vertices, target_level):
     """mesh_to_spc.cpp:28-44."""
@@ -633,6 +674,7 @@ metrics = _module('kaolin._C.metrics', sided_distance_forward_cuda=sided_distanc
                   unbatched_triangle_distance_forward_cuda=unbatched_triangle_distance_forward_cuda,
                   unbatched_triangle_distance_backward_cuda=unbatched_triangle_distance_backward_cuda)
 ops = _module('kaolin._C.ops')
+ops.mesh = _module('kaolin._C.ops.mesh', unbatched_mesh_intersection_cuda=unbatched_mesh_intersection_cuda)
 ops.conversions = _module('kaolin._C.ops.conversions', mesh_to_spc_cuda=mesh_to_spc_cuda)
 ops.spc = _module('kaolin._C.ops.spc', morton_to_octree=morton_to_octree, points_to_octree=points_to_octree,
                   scan_octrees_cuda=scan_octrees_cuda, generate_points_cuda=generate_points_cuda)

@@ -480,3 +480,91 @@ def deftet_sparse_render_backward(grad, idx, weights, fvi, feat, eps=1e-8):
             acc[:, v] = acc[:, v] + dldI[:, c] * dI
     np.add.at(g_img.reshape(B, F, 6), (bi, fid), acc)
     return g_img, g_feat
+
+
+# ---------------------------------------------------------------------------------------------
+# check_sign (ops/mesh/check_sign.py:25-154; kernel mesh_intersection_cuda.cu:40-210).  numpy
+# restatement in the input dtype, per point vectorised over the faces, operations in the
+# kernel's order (crossing counts are integers: bit-exact).
+def _cs_signed_area(ax, ay, bx, by, cx, cy):
+    flip = (cx > bx) | ((bx == cx) & (cy < by))
+    a = -((by - cy) * (ax - cx) + (cx - bx) * (ay - cy))
+    b = (cy - by) * (ax - bx) + (bx - cx) * (ay - by)
+    return np.where(flip, a, b)
+
+
+def _cs_above(vx, vy, lx, ly, rx, ry):
+    v1x, v1y = rx - lx, ry - ly
+    v2x, v2y = vx - lx, vy - ly
+    return (v1x * v2y - v1y * v2x) > 0
+
+
+def _cs_signed_volume(ax, ay, az, b, c, d):
+    """signed_volume(a, b, c, d) = dot(cross(b - a, c - a), d - a) (mesh_intersection_cuda.cu:60-66)."""
+    ux, uy, uz = b[:, 0] - ax, b[:, 1] - ay, b[:, 2] - az
+    vx, vy, vz = c[:, 0] - ax, c[:, 1] - ay, c[:, 2] - az
+    nx, ny, nz = uy * vz - uz * vy, uz * vx - ux * vz, ux * vy - uy * vx
+    return nx * (d[:, 0] - ax) + ny * (d[:, 1] - ay) + nz * (d[:, 2] - az)
+
+
+def mesh_intersection_counts(points, v1, v2, v3):
+    """unbatched_mesh_intersection_cuda: (P,) crossing counts (as int64)."""
+    dt = points.dtype
+    f32 = np.float32
+    ymin = np.minimum(v1[:, 1], np.minimum(v2[:, 1], v3[:, 1])).astype(f32).astype(dt)
+    ymax = np.maximum(v1[:, 1], np.maximum(v2[:, 1], v3[:, 1])).astype(f32).astype(dt)
+    zmin = np.minimum(v1[:, 2], np.minimum(v2[:, 2], v3[:, 2])).astype(f32).astype(dt)
+    zmax = np.maximum(v1[:, 2], np.maximum(v2[:, 2], v3[:, 2])).astype(f32).astype(dt)
+    out = np.zeros(points.shape[0], np.int64)
+    ten = dt.type(10.)
+    for i, (qx, qy, qz) in enumerate(points):
+        f = np.nonzero(~((qy < ymin) | (ymax < qy) | (qz < zmin) | (zmax < qz)))[0]
+        if f.size == 0:
+            continue
+        a, b, c = v1[f], v2[f], v3[f]
+        c1 = _cs_signed_volume(qx, qy, qz, a, b, c) > 0
+        c2 = _cs_signed_volume(qx + ten, qy, qz, a, b, c) > 0
+        d1 = _cs_signed_area(qy, qz, a[:, 1], a[:, 2], b[:, 1], b[:, 2])
+        d2 = _cs_signed_area(qy, qz, b[:, 1], b[:, 2], c[:, 1], c[:, 2])
+        d3 = _cs_signed_area(qy, qz, c[:, 1], c[:, 2], a[:, 1], a[:, 2])
+        inside = (c1 != c2) & (d1 * d2 >= 0) & (d3 * d1 >= 0) & (d2 * d3 >= 0)
+        cnt = 0
+        for j in np.nonzero(inside)[0]:
+            p = [(a[j, 1], a[j, 2]), (b[j, 1], b[j, 2]), (c[j, 1], c[j, 2])]
+            on_v = on_e = False
+            if (qy, qz) == p[0]:
+                on_v, v1_, v2_ = True, p[1], p[2]
+            elif (qy, qz) == p[1]:
+                on_v, v1_, v2_ = True, p[0], p[2]
+            elif (qy, qz) == p[2]:
+                on_v, v1_, v2_ = True, p[0], p[1]
+            elif d1[j] == 0:
+                on_e, v1_, v2_, o = True, p[0], p[1], p[2]
+            elif d2[j] == 0:
+                on_e, v1_, v2_, o = True, p[1], p[2], p[0]
+            elif d3[j] == 0:
+                on_e, v1_, v2_, o = True, p[2], p[0], p[1]
+            if not (on_v or on_e):
+                cnt += 1
+                continue
+            if v1_[0] > v2_[0] or (v1_[0] == v2_[0] and v1_[1] > v2_[1]):
+                v1_, v2_ = v2_, v1_
+            if on_e:
+                cnt += 0 if _cs_above(o[0], o[1], v1_[0], v1_[1], v2_[0], v2_[1]) else 1
+            else:
+                cnt += 1 if (_cs_above(qy, qz, v1_[0], v1_[1], v2_[0], v2_[1]) and v1_[0] < qy
+                             and v2_[0] >= qy) else 0
+        out[i] = cnt
+    return out
+
+
+def check_sign(verts, faces, points):
+    """check_sign.py:140-154 (GPU branch): (B,P) bool."""
+    res = []
+    for b in range(verts.shape[0]):
+        maxlen = (verts[b].max(0) - verts[b].min(0)).max()
+        v = verts[b] / maxlen
+        p = points[b] / maxlen
+        cnt = mesh_intersection_counts(p, v[faces[:, 0]], v[faces[:, 1]], v[faces[:, 2]])
+        res.append(cnt % 2 == 1)
+    return np.stack(res)

@@ -542,6 +542,27 @@ def deftet():
     save('deftet.npz', **arrays)
 
 
+# --------------------------------------------------------------------------
+# check_sign (tests/python/kaolin/ops/mesh/test_check_sign.py:26-186): transcribed data
+# --------------------------------------------------------------------------
+def check_sign():
+    v = np.array([[1., 0., 0.], [1., 0., 1.], [1., -1., -1.], [1., 1., -1.],
+                  [-1., 0., 0.], [-1., 0., -4.], [-1., -4., 4.], [-1., 4., 4.]])
+    faces = np.array([[0, 1, 2], [0, 2, 3], [0, 3, 1], [1, 2, 6], [2, 3, 5], [3, 1, 7],
+                      [5, 6, 2], [6, 7, 1], [7, 5, 3], [4, 6, 5], [4, 7, 6], [4, 5, 7]], np.int64)
+    p = np.array([[0.9, 0., 0.], [0.9, 0., -1.], [0.9, 0., -0.9], [0.9, 0.1, -1.0], [0.9, 0., 1.],
+                  [0.9, -1., -1.], [0.9, 1., -1.], [-0.99, 0., -3.9], [-0.99, -3.9, 3.9], [-0.99, 3.9, 3.9],
+                  [0.9, 0., -4.], [0.9, -4., 4.], [0.9, 4., 4.], [0.9, 0., 4.], [-0.9, 0., -3.9],
+                  [-0.9, -3.9, 3.9], [-0.9, 3.9, 3.9], [0.5, 0., 5.], [0.5, -5., 4.], [1.1, 0., 0.],
+                  [1.1, 0., -1.], [1.1, 0., -0.9], [1.1, 0.1, -1.0], [1.1, 0., 1.], [1.1, -1., -1.],
+                  [1.1, 1., -1.], [-1.1, 0., 0.], [-1.1, 0., -1.], [-1.1, 0., -0.9], [-1.1, 0.1, -1.0],
+                  [-1.1, 0., 1.], [-1.1, -1., -1.], [-1.1, 1., -1.]])
+    e = np.array([True] * 10 + [False] * 23)
+    save('check_sign.npz', verts=np.stack([v, -v]), faces=faces,
+         zero_area_faces=np.array([[1, 1, 1], [0, 0, 0], [2, 2, 2], [3, 3, 3]], np.int64),
+         points=np.stack([p, -p[::-1]]), expected=np.stack([e, e[::-1]]))
+
+
 if __name__ == '__main__':
     torch.set_num_threads(8)
     if len(sys.argv) > 1:  # regenerate only the named fixtures

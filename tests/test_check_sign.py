@@ -1,0 +1,135 @@
+"""check_sign (reference ops/mesh/check_sign.py:25-154, test_check_sign.py).
+
+CPU: the numpy oracle (oracle/oracle.py, mesh_intersection_counts / check_sign) against the
+reference's known answers (test_check_sign.py:26-186: points overlapping vertices and edges in
+projection, in front of / behind the mesh, zero-area faces), transcribed in
+tests/golden/check_sign.npz.  Argument errors of the front-end (no device needed).
+
+GPU: kaolin.ops.mesh.check_sign (one batched launch) and
+kaolin._C.ops.mesh.unbatched_mesh_intersection_cuda against the oracle, bit-exact (integer
+crossing counts), and inside/outside of a closed sphere at a size the oracle does not reach.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+
+@pytest.mark.parametrize('dtype', [np.float32, np.float64])
+@pytest.mark.parametrize('zero_area', [False, True])
+def test_oracle_kat(golden, dtype, zero_area):
+    g = golden('check_sign.npz')
+    faces = np.concatenate([g['faces'], g['zero_area_faces']]) if zero_area else g['faces']
+    out = orc.check_sign(g['verts'].astype(dtype), faces, g['points'].astype(dtype))
+    np.testing.assert_array_equal(out, g['expected'])
+
+
+@pytest.fixture(scope='module')
+def kal():
+    import kaolin
+    return kaolin
+
+
+@pytest.mark.parametrize('mutate,exc,msg', [
+    (lambda v, f, p: (v, f.int(), p), TypeError, r'Expected faces entries to be torch.int64 but got torch.int32.'),
+    (lambda v, f, p: (v.unsqueeze(-1), f, p), ValueError, r'Expected verts to have 3 dimensions but got 4 dimensions.'),
+    (lambda v, f, p: (v, f.unsqueeze(-1), p), ValueError, r'Expected faces to have 2 dimensions but got 3 dimensions.'),
+    (lambda v, f, p: (v, f, p.unsqueeze(-1)), ValueError,
+     r'Expected points to have 3 dimensions but got 4 dimensions.'),
+    (lambda v, f, p: (v[..., :2], f, p), ValueError, r'Expected verts to have 3 coordinates but got 2 coordinates.'),
+    (lambda v, f, p: (v, f[:, :2], p), ValueError, r'Expected faces to have 3 vertices but got 2 vertices.'),
+    (lambda v, f, p: (v, f, p[..., :2]), ValueError, r'Expected points to have 3 coordinates but got 2 coordinates.'),
+])
+def test_argument_errors(kal, golden, mutate, exc, msg):
+    g = golden('check_sign.npz')
+    v, f, p = torch.from_numpy(g['verts']), torch.from_numpy(g['faces']), torch.from_numpy(g['points'])
+    with pytest.raises(exc, match=msg):
+        kal.ops.mesh.check_sign(*mutate(v, f, p))
+    with pytest.raises(TypeError, match=r"Expected hash_resolution to be int but got <class 'float'>."):
+        kal.ops.mesh.check_sign(v, f, p, 512.0)
+
+
+def test_cpu_tensors_raise(kal, golden):
+    g = golden('check_sign.npz')
+    with pytest.raises(RuntimeError, match='CPU fallback|GPU tensors'):
+        kal.ops.mesh.check_sign(torch.from_numpy(g['verts']), torch.from_numpy(g['faces']),
+                                torch.from_numpy(g['points']))
+
+
+# ------------------------------------------------------------------------------- GPU parity
+DEV = 'cuda'
+
+
+def _T(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def _uv_sphere(n_lat, n_lon, radius=1.0):
+    lat = np.linspace(0, math.pi, n_lat + 1)[1:-1]
+    lon = np.arange(n_lon) * (2 * math.pi / n_lon)
+    ring = np.stack([np.sin(lat)[:, None] * np.cos(lon)[None], np.cos(lat)[:, None] * np.ones_like(lon)[None],
+                     np.sin(lat)[:, None] * np.sin(lon)[None]], -1).reshape(-1, 3)
+    verts = np.concatenate([[[0, 1, 0]], ring, [[0, -1, 0]]]) * radius
+    faces = []
+    R = len(lat)
+    for j in range(n_lon):
+        j1 = (j + 1) % n_lon
+        faces.append([0, 1 + j1, 1 + j])
+        faces.append([1 + (R - 1) * n_lon + j, 1 + (R - 1) * n_lon + j1, len(verts) - 1])
+        for i in range(R - 1):
+            a, b = 1 + i * n_lon + j, 1 + i * n_lon + j1
+            c, d = a + n_lon, b + n_lon
+            faces += [[a, b, d], [a, d, c]]
+    return verts, np.array(faces, np.int64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('zero_area', [False, True])
+def test_gpu_kat(kal, golden, dtype, zero_area):
+    g = golden('check_sign.npz')
+    faces = np.concatenate([g['faces'], g['zero_area_faces']]) if zero_area else g['faces']
+    out = kal.ops.mesh.check_sign(_T(g['verts']).to(dtype), _T(faces), _T(g['points']).to(dtype))
+    assert out.dtype == torch.bool
+    np.testing.assert_array_equal(out.cpu().numpy(), g['expected'])
+    out1 = kal.ops.mesh.check_sign(_T(g['verts'][:1]).to(dtype), _T(faces), _T(g['points'][:1]).to(dtype))
+    np.testing.assert_array_equal(out1.cpu().numpy(), g['expected'][:1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [np.float32, np.float64])
+def test_gpu_vs_oracle(kal, dtype):
+    """Grid points on the sphere's own vertex coordinates (vertex / edge overlaps in projection)
+    plus random points; raw _C counts and the batched front-end, both bit-exact."""
+    verts, faces = _uv_sphere(12, 18, 0.8)
+    verts = verts.astype(dtype)
+    rng = np.random.default_rng(3)
+    grid = np.stack(np.meshgrid(np.linspace(-1, 1, 9), verts[:40:3, 1], verts[:40:5, 2]), -1).reshape(-1, 3)
+    pts = np.concatenate([grid, rng.uniform(-1, 1, (700, 3))]).astype(dtype)
+    v1, v2, v3 = verts[faces[:, 0]], verts[faces[:, 1]], verts[faces[:, 2]]
+    cnt = kal._C.ops.mesh.unbatched_mesh_intersection_cuda(_T(pts), _T(v1), _T(v2), _T(v3))
+    assert cnt.dtype == torch.from_numpy(pts).dtype and cnt.shape == (len(pts),)
+    ref = orc.mesh_intersection_counts(pts, v1, v2, v3)
+    np.testing.assert_array_equal(cnt.cpu().numpy().astype(np.int64), ref)
+    B = 2
+    vb = np.stack([verts, verts * dtype(1.5) + dtype(0.1)])
+    pb = np.stack([pts, pts * dtype(1.2)])
+    out = kal.ops.mesh.check_sign(_T(vb), _T(faces), _T(pb))
+    np.testing.assert_array_equal(out.cpu().numpy(), orc.check_sign(vb, faces, pb))
+    assert out.shape == (B, len(pts))
+
+
+@pytest.mark.gpu
+def test_gpu_sphere_inside_property(kal):
+    """20k-face sphere, 200k points: inside <=> |p| < r away from the surface."""
+    verts, faces = _uv_sphere(101, 100, 1.0)
+    rng = np.random.default_rng(0)
+    pts = rng.uniform(-1.3, 1.3, (1, 200000, 3)).astype(np.float32)
+    out = kal.ops.mesh.check_sign(_T(verts[None].astype(np.float32)), _T(faces), _T(pts)).cpu().numpy()[0]
+    r = np.linalg.norm(pts[0], axis=-1)
+    far = np.abs(r - 1.0) > 0.01  # the tessellation is within 1e-3 of the sphere
+    np.testing.assert_array_equal(out[far], (r < 1.0)[far])
+    assert out[far].sum() > 10000
