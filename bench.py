@@ -12,7 +12,8 @@ Multi-GPU: one process per GPU (torchrun); each rank renders its own 4 views of 
 replicated mesh (weak scaling, global batch 4N), per-shard losses are all-gathered
 over RCCL each step; time = max over ranks.
 
-Also reported: p2m (configs[1]: 100k points vs 20k faces, forward) Mpairs/s, the
+Also reported: p2m (configs[1]: 100k points vs 20k faces, forward) Mpairs/s, the §8f
+sub-benches (deftet_sparse_render fwd+bwd on the same views, check_sign 1M points), the
 roofline of the dominant op (HIP events on its stream over the timed region) and a
 CPU baseline (the C oracle, 1 thread, on a stated row sample of view 0).
 """
@@ -289,6 +290,63 @@ def p2m_bench(device, steps):
     return 100000 * 20000 / (ms * 1e-3) / 1e6, ms
 
 
+def _event_ms(fn, steps):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(steps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / steps
+
+
+def deftet_bench(inp, steps, knum=8):
+    """deftet_sparse_render fwd+bwd on the cfg3 mesh and views: every
+    pixel centre of the 512x512 grid, depth range = the mesh's z span, knum=8 (a covered pixel
+    of the sphere holds its front and back faces)."""
+    fvz, fvi, feat, H, W = inp['fvz'], inp['fvi'], inp['feat'], inp['H'], inp['W']
+    B, dev = fvz.shape[0], fvz.device
+    x = (2 * torch.arange(W, device=dev, dtype=torch.float32) + 1 - W) / W
+    y = (H - 2 * torch.arange(H, device=dev, dtype=torch.float32) - 1.) / H
+    pix = torch.stack([x.view(1, -1).expand(H, W), y.view(-1, 1).expand(H, W)], -1).reshape(1, -1, 2)
+    pix = pix.expand(B, -1, -1).contiguous()
+    zmin, zmax = fvz.reshape(B, -1).min(1)[0], fvz.reshape(B, -1).max(1)[0]
+    rr = torch.stack([zmin - 1e-2, zmax + 1e-2], -1).unsqueeze(1).expand(-1, H * W, -1).contiguous()
+    fvi_r = fvi.detach().clone().requires_grad_(True)
+    feat_r = feat.detach().clone().requires_grad_(True)
+    g = torch.rand((B, H * W, knum, feat.shape[-1]), generator=torch.Generator().manual_seed(2)).to(dev)
+    render = kal.render.mesh.deftet_sparse_render
+
+    def fwd():
+        return render(pix, rr, fvz, fvi_r, feat_r, knum)
+
+    def step():
+        out, _ = fwd()
+        torch.autograd.grad(out, [fvi_r, feat_r], g)
+
+    ms_fwd = _event_ms(lambda: fwd(), steps)
+    ms = _event_ms(step, steps)
+    _, idx = fwd()
+    hits = int((idx >= 0).sum())
+    return {'metric': 'deftet_sparse_render fwd+bwd Mpixels/s (4 views, 512x512, 50k faces, knum=8, f32)',
+            'value': round(B * H * W / (ms * 1e-3) / 1e6, 1), 'ms': round(ms, 3), 'fwd_ms': round(ms_fwd, 3),
+            'hits': hits}
+
+
+def check_sign_bench(device, steps, n_points=1000000):
+    """check_sign: the cfg3 sphere (50k faces) vs 1M points in [-1,1]^3."""
+    verts, faces = uv_sphere(126, 200, device)
+    g = torch.Generator().manual_seed(3)
+    pts = (torch.rand((1, n_points, 3), generator=g) * 2 - 1).to(device)
+    v = verts.unsqueeze(0).contiguous()
+    ms = _event_ms(lambda: kal.ops.mesh.check_sign(v, faces, pts), steps)
+    return {'metric': 'check_sign Mpoints/s (1M points vs 50k-face sphere, f32)',
+            'value': round(n_points / (ms * 1e-3) / 1e6, 1), 'ms': round(ms, 3),
+            'nominal_mpairs_per_s': round(n_points * faces.shape[0] / (ms * 1e-3) / 1e6, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -297,6 +355,7 @@ def main():
     ap.add_argument('--cpu-row-step', type=int, default=2)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-p2m', action='store_true')
+    ap.add_argument('--no-extra', action='store_true', help='skip the deftet / check_sign sub-benches')
     ap.add_argument('--eager', action='store_true', help='time the eager step only (no HIP graph capture)')
     args = ap.parse_args()
 
@@ -388,6 +447,9 @@ def main():
                                       'achieved_tflops': round(mp * 1e6 * 50 / 1e12, 2),
                                       'peak_tflops': FP32_PEAK_TFLOPS,
                                       'frac': round(mp * 1e6 * 50 / 1e12 / FP32_PEAK_TFLOPS, 4)}}
+    if not args.no_extra and rank == 0:
+        result['deftet'] = deftet_bench(inp, max(3, args.steps // 4))
+        result['check_sign'] = check_sign_bench(device, max(3, args.steps // 4))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rate, npx, dt = cpu_baseline(inp, args.cpu_row_step)
         result['cpu_baseline'] = {'value': round(rate, 5), 'unit': 'Mpixels/s', 'cores': 1, 'kind': 'port',

@@ -229,12 +229,15 @@ int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height, int width,
  * or NULL (then min / max over the three vertices in-kernel, as deftet.py:290-292 computes them),
  * pixel_coords (B,P,2), pixel_depth_ranges (B,P,2) [lo, hi).  dtype KL_F32 | KL_F64.
  * Outputs (B,P,K), fully written: face_idx int64 (first K hits in mesh order, then -1),
- * pixel_depths (-inf pad), w0, w1 (0 pad). */
+ * pixel_depths (-inf pad), w0, w1 (0 pad).  workspace: kl_deftet_workspace_bytes(B, F) bytes
+ * (per-tile face bboxes, no initialisation needed). */
+size_t kl_deftet_workspace_bytes(int64_t batch_size, int64_t num_faces);
 int kl_deftet_sparse_render_forward(kl_dtype dtype, int64_t batch_size, int64_t num_faces, int64_t num_pixels,
                                     int64_t knum, const void *face_vertices_z, const void *face_vertices_image,
                                     const void *face_bboxes, const void *pixel_coords,
                                     const void *pixel_depth_ranges, float eps, int64_t *face_idx,
-                                    void *pixel_depths, void *w0, void *w1, kl_stream stream);
+                                    void *pixel_depths, void *w0, void *w1, void *workspace,
+                                    size_t workspace_bytes, kl_stream stream);
 
 /* deftet.py:294-306 (the torch glue of DeftetSparseRenderer.forward) in one pass: per pixel the
  * hits of kl_deftet_sparse_render_forward ranked by depth, descending (stable), then
@@ -369,12 +372,15 @@ int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points, int64_t n
                                    const void *verts_1, const void *verts_2, const void *verts_3, void *result,
                                    kl_stream stream);
 
-/* check_sign (ops/mesh/check_sign.py:25-154) for a batch in one launch: verts (B,V,3),
- * faces (F,3) int64, points (B,P,3), maxlen (B) the per-mesh divisor check_sign.py:140-146
- * applies to verts and points (NULL: none) -> contains (B,P) bool bytes (odd crossing count). */
+/* check_sign (ops/mesh/check_sign.py:25-154) for a batch: verts (B,V,3), faces (F,3) int64,
+ * points (B,P,3), maxlen (B) the per-mesh divisor check_sign.py:140-146 applies to verts and
+ * points (NULL: none) -> contains (B,P) bool bytes (odd crossing count).  workspace:
+ * kl_check_sign_workspace_bytes(B, F, P) bytes (point order keys, per-tile face bounds, sort
+ * scratch; no initialisation needed). */
+size_t kl_check_sign_workspace_bytes(int64_t batch_size, int64_t num_faces, int64_t num_points);
 int kl_check_sign(kl_dtype dtype, int64_t batch_size, int64_t num_vertices, int64_t num_faces, int64_t num_points,
                   const void *verts, const int64_t *faces, const void *points, const void *maxlen,
-                  uint8_t *contains, kl_stream stream);
+                  uint8_t *contains, void *workspace, size_t workspace_bytes, kl_stream stream);
 
 /* ------------------------------------------------------------ voxelgrid */
 

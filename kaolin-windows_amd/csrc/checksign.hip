@@ -21,15 +21,13 @@
 // from (vertices, faces) and applies check_sign's 1 / maxlen normalisation on load (the same
 // IEEE division the reference does in torch), so neither the normalised vertices nor the
 // (F, 3, 3) corner arrays are materialised.
+#include <hipcub/hipcub.hpp>
+
 #include "common.h"
 
 namespace kl {
 
 constexpr int kCsTile = 256;
-
-struct CsV2 {
-  double x, y;
-};
 
 template <typename T>
 struct CsFaces {
@@ -127,11 +125,78 @@ __device__ __forceinline__ void cs_load_face(const CsFaces<T> &src, int64_t b, i
   }
 }
 
-// grid (cdiv(P, 256), B); counts (B,P) in T (the _C contract) and/or contains (B,P) bool
+// Float-bit order key of v (monotone), for the point ordering below.
+__device__ __forceinline__ uint32_t cs_order_bits(float v) {
+  const uint32_t u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ uint32_t cs_spread16(uint32_t x) {
+  x &= 0xffffu;
+  x = (x | (x << 8)) & 0x00ff00ffu;
+  x = (x | (x << 4)) & 0x0f0f0f0fu;
+  x = (x | (x << 2)) & 0x33333333u;
+  x = (x | (x << 1)) & 0x55555555u;
+  return x;
+}
+
+// Sort keys: 2D Morton code of the top 16 order bits of (y, z), so that the 256 points of a
+// workgroup share a small (y, z) box and the face culling below removes most of the mesh.
+// The order only changes which lane tests which point; every count is unchanged.
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cs_key_kernel(int64_t n, int64_t P, const T *__restrict__ points, uint32_t *__restrict__ keys,
+                  int32_t *__restrict__ vals) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t ky = cs_order_bits((float)points[i * 3 + 1]) >> 16;
+  const uint32_t kz = cs_order_bits((float)points[i * 3 + 2]) >> 16;
+  keys[i] = (cs_spread16(ky) << 1) | cs_spread16(kz);
+  vals[i] = (int32_t)(i % P);  // point index within its mesh
+}
+
+// Union of the (float) (y, z) face bounds per tile of kCsTile faces (grid (ntiles, B)).
+template <typename T>
+__global__ void __launch_bounds__(kCsTile) cs_tilebox_kernel(int64_t F, CsFaces<T> src, float *__restrict__ tbox) {
+  __shared__ float s_r[4][kCsTile / 64];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * kCsTile + tid;
+  float r0 = INFINITY, r1 = -INFINITY, r2 = INFINITY, r3 = -INFINITY;
+  if (f < F) {
+    T v[9];
+    cs_load_face(src, b, f, v);
+    r0 = (float)fmin(v[1], fmin(v[4], v[7]));
+    r1 = (float)fmax(v[1], fmax(v[4], v[7]));
+    r2 = (float)fmin(v[2], fmin(v[5], v[8]));
+    r3 = (float)fmax(v[2], fmax(v[5], v[8]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    r0 = fminf(r0, __shfl_xor(r0, o));
+    r1 = fmaxf(r1, __shfl_xor(r1, o));
+    r2 = fminf(r2, __shfl_xor(r2, o));
+    r3 = fmaxf(r3, __shfl_xor(r3, o));
+  }
+  if ((tid & 63) == 0) {
+    s_r[0][tid >> 6] = r0; s_r[1][tid >> 6] = r1; s_r[2][tid >> 6] = r2; s_r[3][tid >> 6] = r3;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < kCsTile / 64; w++) {
+      r0 = fminf(r0, s_r[0][w]); r1 = fmaxf(r1, s_r[1][w]); r2 = fminf(r2, s_r[2][w]); r3 = fmaxf(r3, s_r[3][w]);
+    }
+    float *o = tbox + (b * gridDim.x + blockIdx.x) * 4;
+    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = r3;
+  }
+}
+
+// grid (cdiv(P, 256), B); counts (B,P) in T (the _C contract) and/or contains (B,P) bool.
+// perm (B,P) int32 or null: lane i of the batch handles point perm[i].
+// tbox (B, ntiles, 4) float or null.
 template <typename T>
 __global__ void __launch_bounds__(kCsTile)
     check_sign_kernel(int64_t P, int64_t F, const T *__restrict__ points, CsFaces<T> src, T *__restrict__ counts,
-                      uint8_t *__restrict__ contains) {
+                      uint8_t *__restrict__ contains, const int32_t *__restrict__ perm,
+                      const float *__restrict__ tbox) {
   __shared__ T s_v[9][kCsTile];
   __shared__ float s_bb[4][kCsTile];
   __shared__ int s_wave[16];
@@ -139,8 +204,9 @@ __global__ void __launch_bounds__(kCsTile)
 
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.y;
-  const int64_t p = (int64_t)blockIdx.x * kCsTile + tid;
-  const bool active = p < P;
+  const int64_t i = (int64_t)blockIdx.x * kCsTile + tid;
+  const bool active = i < P;
+  const int64_t p = (active && perm) ? (int64_t)perm[b * P + i] : i;
   const int64_t row = b * P + p;
   T qx = 0, qy = 0, qz = 0;
   if (active) {
@@ -174,7 +240,12 @@ __global__ void __launch_bounds__(kCsTile)
   }
 
   int count = 0;
+  const int64_t ntiles = (F + kCsTile - 1) / kCsTile;
   for (int64_t t0 = 0; t0 < F; t0 += kCsTile) {
+    if (tbox) {  // workgroup-uniform skip of a tile no point of the workgroup can use
+      const float *tb = tbox + (b * ntiles + t0 / kCsTile) * 4;
+      if (!((T)tb[0] <= gymx && (T)tb[1] >= gymn && (T)tb[2] <= gzmx && (T)tb[3] >= gzmn)) continue;
+    }
     const int64_t f = t0 + tid;
     T v[9];
     float bb[4];
@@ -217,26 +288,68 @@ __global__ void __launch_bounds__(kCsTile)
 
 template <typename T>
 static int check_sign_launch(int64_t B, int64_t P, int64_t F, const void *points, const CsFaces<T> &src, void *counts,
-                             uint8_t *contains, hipStream_t st) {
+                             uint8_t *contains, const int32_t *perm, const float *tbox, hipStream_t st) {
   if (B == 0 || P == 0) return KL_OK;
   hipLaunchKernelGGL(check_sign_kernel<T>, dim3((unsigned)cdiv(P, kCsTile), (unsigned)B), dim3(kCsTile), 0, st, P, F,
-                     (const T *)points, src, (T *)counts, contains);
+                     (const T *)points, src, (T *)counts, contains, perm, tbox);
   KL_CHECK_LAUNCH();
   return KL_OK;
+}
+
+// workspace layout of the batched entry (byte offsets, 256-aligned)
+struct CsWs {
+  size_t keys_in, keys_out, vals_in, vals_out, tbox, temp, temp_bytes, total;
+};
+static size_t cs_align(size_t x) { return (x + 255) & ~(size_t)255; }
+static CsWs cs_ws_layout(int64_t B, int64_t F, int64_t P) {
+  CsWs w{};
+  size_t tb = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (const int32_t *)nullptr, (int32_t *)nullptr, (int)(P > 0 ? P : 1));
+  size_t o = 0;
+  w.keys_in = o; o += cs_align((size_t)(B * P) * 4);
+  w.keys_out = o; o += cs_align((size_t)(B * P) * 4);
+  w.vals_in = o; o += cs_align((size_t)(B * P) * 4);
+  w.vals_out = o; o += cs_align((size_t)(B * P) * 4);
+  w.tbox = o; o += cs_align((size_t)(B * cdiv(F, kCsTile)) * 16);
+  w.temp = o; w.temp_bytes = cs_align(tb > 0 ? tb : 1); o += w.temp_bytes;
+  w.total = o;
+  return w;
 }
 
 template <typename T>
 static int mesh_intersection_unbatched(int64_t P, int64_t F, const void *points, const void *v1, const void *v2,
                                        const void *v3, void *counts, hipStream_t st) {
   CsFaces<T> src{(const T *)v1, (const T *)v2, (const T *)v3, nullptr, nullptr, nullptr, 0};
-  return check_sign_launch<T>(1, P, F, points, src, counts, nullptr, st);
+  return check_sign_launch<T>(1, P, F, points, src, counts, nullptr, nullptr, nullptr, st);
 }
 
 template <typename T>
 static int check_sign_batched(int64_t B, int64_t V, int64_t F, int64_t P, const void *verts, const int64_t *faces,
-                              const void *points, const void *maxlen, uint8_t *contains, hipStream_t st) {
+                              const void *points, const void *maxlen, uint8_t *contains, void *ws, size_t ws_bytes,
+                              hipStream_t st) {
   CsFaces<T> src{nullptr, nullptr, nullptr, (const T *)verts, faces, (const T *)maxlen, V};
-  return check_sign_launch<T>(B, P, F, points, src, nullptr, contains, st);
+  if (B == 0 || P == 0) return KL_OK;
+  const CsWs L = cs_ws_layout(B, F, P);
+  KL_REQUIRE(ws && ws_bytes >= L.total, "check_sign: workspace too small");
+  uint8_t *w = (uint8_t *)ws;
+  uint32_t *kin = (uint32_t *)(w + L.keys_in), *kout = (uint32_t *)(w + L.keys_out);
+  int32_t *vin = (int32_t *)(w + L.vals_in), *vout = (int32_t *)(w + L.vals_out);
+  float *tbox = (float *)(w + L.tbox);
+  const int64_t ntiles = cdiv(F, kCsTile);
+  if (ntiles > 0) {
+    hipLaunchKernelGGL(cs_tilebox_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kCsTile), 0, st, F, src, tbox);
+    KL_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(cs_key_kernel<T>, dim3((unsigned)cdiv(B * P, 256)), dim3(256), 0, st, B * P, P,
+                     (const T *)points, kin, vin);
+  KL_CHECK_LAUNCH();
+  for (int64_t b = 0; b < B; b++) {  // each mesh's points sorted on their own
+    size_t tb = L.temp_bytes;
+    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.temp, tb, kin + b * P, kout + b * P, vin + b * P,
+                                                    vout + b * P, (int)P, 0, 32, st));
+  }
+  return check_sign_launch<T>(B, P, F, points, src, nullptr, contains, vout, tbox, st);
 }
 
 }  // namespace kl
@@ -259,11 +372,17 @@ extern "C" int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points
                  S(stream));
 }
 
+extern "C" size_t kl_check_sign_workspace_bytes(int64_t batch_size, int64_t num_faces, int64_t num_points) {
+  return cs_ws_layout(batch_size, num_faces, num_points).total;
+}
+
 extern "C" int kl_check_sign(kl_dtype dtype, int64_t batch_size, int64_t num_vertices, int64_t num_faces,
                              int64_t num_points, const void *verts, const int64_t *faces, const void *points,
-                             const void *maxlen, uint8_t *contains, kl_stream stream) {
+                             const void *maxlen, uint8_t *contains, void *workspace, size_t workspace_bytes,
+                             kl_stream stream) {
   KL_REQUIRE(batch_size >= 0 && num_vertices >= 0 && num_faces >= 0 && num_points >= 0, "check_sign: negative size");
   KL_REQUIRE(batch_size < 65536, "check_sign: batch_size must be < 65536");
+  KL_REQUIRE(num_points < ((int64_t)1 << 31), "check_sign: num_points must be < 2^31");
   KL_CS_DISPATCH(dtype, check_sign_batched, batch_size, num_vertices, num_faces, num_points, verts, faces, points,
-                 maxlen, contains, S(stream));
+                 maxlen, contains, workspace, workspace_bytes, S(stream));
 }

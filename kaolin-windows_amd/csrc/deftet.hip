@@ -44,13 +44,59 @@ __device__ __forceinline__ T dt_copysign_eps_f(float eps, T v) {
   return (T)copysignf(eps, (float)v);
 }
 
+template <typename T>
+__device__ __forceinline__ void dt_face_bbox(const T *__restrict__ mi, const T *__restrict__ mb, int64_t f, T *bb) {
+  if (mb) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) bb[c] = mb[f * 4 + c];
+  } else {  // deftet.py:290-292: min / max over the three vertices
+    const T *v = mi + f * 6;
+    bb[0] = fmin(fmin(v[0], v[2]), v[4]);
+    bb[1] = fmin(fmin(v[1], v[3]), v[5]);
+    bb[2] = fmax(fmax(v[0], v[2]), v[4]);
+    bb[3] = fmax(fmax(v[1], v[3]), v[5]);
+  }
+}
+
+// Union bbox of each tile of kDtTile consecutive faces (grid (ntiles, B)): lets a workgroup
+// skip a whole tile, without loading it, when no face of it can reach its pixels.
+template <typename T>
+__global__ void __launch_bounds__(kDtTile)
+    deftet_tilebox_kernel(int64_t F, const T *__restrict__ fvi, const T *__restrict__ bboxes, T *__restrict__ tbox) {
+  __shared__ T s_r[4][kDtTile / 64];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * kDtTile + tid;
+  T bb[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
+  if (f < F) dt_face_bbox(fvi + b * F * 6, bboxes ? bboxes + b * F * 4 : nullptr, f, bb);
+  // fmin / fmax drop NaN bounds: a face with one never passes the per-face test anyway
+  T r0 = bb[0], r1 = bb[1], r2 = bb[2], r3 = bb[3];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    r0 = fmin(r0, (T)__shfl_xor(r0, o));
+    r1 = fmin(r1, (T)__shfl_xor(r1, o));
+    r2 = fmax(r2, (T)__shfl_xor(r2, o));
+    r3 = fmax(r3, (T)__shfl_xor(r3, o));
+  }
+  if ((tid & 63) == 0) {
+    s_r[0][tid >> 6] = r0; s_r[1][tid >> 6] = r1; s_r[2][tid >> 6] = r2; s_r[3][tid >> 6] = r3;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < kDtTile / 64; w++) {
+      r0 = fmin(r0, s_r[0][w]); r1 = fmin(r1, s_r[1][w]); r2 = fmax(r2, s_r[2][w]); r3 = fmax(r3, s_r[3][w]);
+    }
+    T *o = tbox + (b * gridDim.x + blockIdx.x) * 4;
+    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = r3;
+  }
+}
+
 // deftet_cuda.cu:32-190
 template <typename T>
 __global__ void __launch_bounds__(kDtTile)
     deftet_fwd_kernel(int64_t F, int64_t P, int K, const T *__restrict__ fvz, const T *__restrict__ fvi,
                       const T *__restrict__ bboxes, const T *__restrict__ pix, const T *__restrict__ ranges,
                       float eps, int64_t *__restrict__ out_idx, T *__restrict__ out_depth, T *__restrict__ out_w0,
-                      T *__restrict__ out_w1) {
+                      T *__restrict__ out_w1, const T *__restrict__ tbox) {
   __shared__ T s_f[13][kDtTile];  // ax ay bx by cx cy az bz cz xmin ymin xmax ymax
   __shared__ int s_id[kDtTile];
   __shared__ int s_wave[16];
@@ -101,7 +147,12 @@ __global__ void __launch_bounds__(kDtTile)
   const T *mi = fvi + b * F * 6;
   const T *mb = bboxes ? bboxes + b * F * 4 : nullptr;
 
+  const int64_t ntiles = (F + kDtTile - 1) / kDtTile;
   for (int64_t t0 = 0; t0 < F; t0 += kDtTile) {
+    {  // workgroup-uniform: skip a tile whose union bbox misses the workgroup's pixels
+      const T *tb = tbox + (b * ntiles + t0 / kDtTile) * 4;
+      if (!(tb[0] <= gxmax && tb[2] > gxmin && tb[1] <= gymax && tb[3] > gymin)) continue;
+    }
     if (!__syncthreads_or(active && n < K)) break;  // every pixel of the workgroup is full
     const int64_t f = t0 + tid;
     T v[13];
@@ -111,15 +162,7 @@ __global__ void __launch_bounds__(kDtTile)
       for (int c = 0; c < 6; c++) v[c] = mi[f * 6 + c];
 #pragma unroll
       for (int c = 0; c < 3; c++) v[6 + c] = mz[f * 3 + c];
-      if (mb) {
-#pragma unroll
-        for (int c = 0; c < 4; c++) v[9 + c] = mb[f * 4 + c];
-      } else {  // deftet.py:290-292: min / max over the three vertices
-        v[9] = fmin(fmin(v[0], v[2]), v[4]);
-        v[10] = fmin(fmin(v[1], v[3]), v[5]);
-        v[11] = fmax(fmax(v[0], v[2]), v[4]);
-        v[12] = fmax(fmax(v[1], v[3]), v[5]);
-      }
+      dt_face_bbox(mi, mb, f, v + 9);
       // some pixel x of the workgroup can satisfy xmin <= x < xmax (same for y)
       keep = v[9] <= gxmax && v[11] > gxmin && v[10] <= gymax && v[12] > gymin;
     }
@@ -282,10 +325,17 @@ __global__ void __launch_bounds__(256)
 template <typename T>
 static int deftet_forward(int64_t B, int64_t F, int64_t P, int64_t K, const void *fvz, const void *fvi,
                           const void *bboxes, const void *pix, const void *ranges, float eps, int64_t *idx, void *depth,
-                          void *w0, void *w1, hipStream_t st) {
+                          void *w0, void *w1, void *ws, size_t ws_bytes, hipStream_t st) {
+  const int64_t ntiles = cdiv(F, kDtTile);
+  KL_REQUIRE(ws_bytes >= (size_t)(B * ntiles * 4) * sizeof(T), "deftet_sparse_render_forward: workspace too small");
+  if (ntiles > 0) {
+    hipLaunchKernelGGL(deftet_tilebox_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kDtTile), 0, st, F,
+                       (const T *)fvi, (const T *)bboxes, (T *)ws);
+    KL_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(deftet_fwd_kernel<T>, dim3((unsigned)cdiv(P, kDtTile), (unsigned)B), dim3(kDtTile), 0, st, F, P,
                      (int)K, (const T *)fvz, (const T *)fvi, (const T *)bboxes, (const T *)pix, (const T *)ranges, eps,
-                     idx, (T *)depth, (T *)w0, (T *)w1);
+                     idx, (T *)depth, (T *)w0, (T *)w1, (const T *)ws);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
@@ -343,11 +393,16 @@ extern "C" int kl_deftet_sparse_render_forward(kl_dtype dtype, int64_t batch_siz
                                                const void *face_vertices_image, const void *face_bboxes,
                                                const void *pixel_coords, const void *pixel_depth_ranges, float eps,
                                                int64_t *face_idx, void *pixel_depths, void *w0, void *w1,
-                                               kl_stream stream) {
+                                               void *workspace, size_t workspace_bytes, kl_stream stream) {
   KL_CHECK_RC(check_deftet_sizes(batch_size, num_faces, num_pixels, knum, 0));
   if (batch_size == 0 || num_pixels == 0 || knum == 0) return KL_OK;
   KL_DT_DISPATCH(dtype, deftet_forward, batch_size, num_faces, num_pixels, knum, face_vertices_z, face_vertices_image,
-                 face_bboxes, pixel_coords, pixel_depth_ranges, eps, face_idx, pixel_depths, w0, w1, S(stream));
+                 face_bboxes, pixel_coords, pixel_depth_ranges, eps, face_idx, pixel_depths, w0, w1, workspace,
+                 workspace_bytes, S(stream));
+}
+
+extern "C" size_t kl_deftet_workspace_bytes(int64_t batch_size, int64_t num_faces) {
+  return (size_t)(batch_size * cdiv(num_faces, kDtTile) * 4) * sizeof(double) + 16;
 }
 
 extern "C" int kl_deftet_sparse_render_resolve(kl_dtype dtype, int64_t batch_size, int64_t num_faces,

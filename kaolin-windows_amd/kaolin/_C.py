@@ -199,10 +199,13 @@ def deftet_forward(func, fvz, fvi, bboxes, pix, ranges, knum, eps):
     depth = torch.empty((B, P, K), dtype=dtype, device=dev)
     w0 = torch.empty((B, P, K), dtype=dtype, device=dev)
     w1 = torch.empty((B, P, K), dtype=dtype, device=dev)
+    lib = N.lib()
+    ws_bytes = lib.kl_deftet_workspace_bytes(B, F)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev), N.timed(func, dev):
-        N.check(N.lib().kl_deftet_sparse_render_forward(
+        N.check(lib.kl_deftet_sparse_render_forward(
             N.dtype_code(dtype), B, F, P, K, N.ptr(fvz), N.ptr(fvi), N.ptr(bboxes), N.ptr(pix), N.ptr(ranges),
-            float(eps), N.ptr(idx), N.ptr(depth), N.ptr(w0), N.ptr(w1), N.stream_of(dev)), func)
+            float(eps), N.ptr(idx), N.ptr(depth), N.ptr(w0), N.ptr(w1), N.ptr(ws), ws_bytes, N.stream_of(dev)), func)
     return [idx, depth, w0, w1]
 
 
@@ -383,9 +386,12 @@ def check_sign_batched(verts, faces, points, maxlen):
     F, P = faces.shape[0], points.shape[1]
     dev = points.device
     out = torch.empty((B, P), dtype=torch.bool, device=dev)
+    lib = N.lib()
+    ws_bytes = lib.kl_check_sign_workspace_bytes(B, F, P)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev), N.timed(func, dev):
-        N.check(N.lib().kl_check_sign(N.dtype_code(verts.dtype), B, V, F, P, N.ptr(verts), N.ptr(faces), N.ptr(points),
-                                      N.ptr(maxlen), N.ptr(out), N.stream_of(dev)), func)
+        N.check(lib.kl_check_sign(N.dtype_code(verts.dtype), B, V, F, P, N.ptr(verts), N.ptr(faces), N.ptr(points),
+                                  N.ptr(maxlen), N.ptr(out), N.ptr(ws), ws_bytes, N.stream_of(dev)), func)
     return out
 
 

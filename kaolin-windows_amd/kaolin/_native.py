@@ -84,14 +84,16 @@ _SIGS = {
     'kl_inclusive_sum_workspace_bytes': (_SZ, [_I64]),
     'kl_inclusive_sum_i32': (_I, [_I64, _P, _P, _P, _SZ, _P]),
     'kl_sum_reduce': (_I, [_I, _I64, _I64, _P, _P, _I64, _P, _P]),
+    'kl_deftet_workspace_bytes': (_SZ, [_I64, _I64]),
     'kl_deftet_sparse_render_forward': (_I, [_I, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P,
-                                             _P]),
+                                             _P, _SZ, _P]),
     'kl_deftet_sparse_render_resolve': (_I, [_I, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
                                              _P]),
     'kl_deftet_sparse_render_backward': (_I, [_I, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _F, _P, _P,
                                               _P]),
     'kl_unbatched_mesh_intersection': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P]),
-    'kl_check_sign': (_I, [_I, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P]),
+    'kl_check_sign_workspace_bytes': (_SZ, [_I64, _I64, _I64]),
+    'kl_check_sign': (_I, [_I, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_voxelgrid_mark': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
     'kl_voxelgrid_mark_f64': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
 }
