@@ -252,13 +252,17 @@ int kl_deftet_sparse_render_resolve(kl_dtype dtype, int64_t batch_size, int64_t 
 /* deftet.cpp:113-163  deftet_sparse_render_backward_cuda (kernel deftet_cuda.cu:240-420).
  * grad_interpolated_features (B,P,K,D), face_idx (B,P,K) int64, weights (B,P,K,3),
  * face_vertices_image (B,F,3,2), face_features (B,F,3,D) -> grad_face_vertices_image (B,F,3,2),
- * grad_face_features (B,F,3,D), fully written (zeroed, then float atomics as the reference). */
+ * grad_face_features (B,F,3,D), fully written.  With a workspace of
+ * kl_deftet_bwd_workspace_bytes(B, F, P, K) bytes the items are radix-sorted by face and each
+ * face sums its items in item order (deterministic, no atomics); with NULL (or sizes past
+ * 2^31 items) the reference's float atomics are used. */
+size_t kl_deftet_bwd_workspace_bytes(int64_t batch_size, int64_t num_faces, int64_t num_pixels, int64_t knum);
 int kl_deftet_sparse_render_backward(kl_dtype dtype, int64_t batch_size, int64_t num_faces, int64_t num_pixels,
                                      int64_t knum, int64_t feat_dim, const void *grad_interpolated_features,
                                      const int64_t *face_idx, const void *weights,
                                      const void *face_vertices_image, const void *face_features, float eps,
-                                     void *grad_face_vertices_image, void *grad_face_features,
-                                     kl_stream stream);
+                                     void *grad_face_vertices_image, void *grad_face_features, void *workspace,
+                                     size_t workspace_bytes, kl_stream stream);
 
 /* ------------------------------------------------------------ distances */
 

@@ -32,6 +32,8 @@
 // terms are summed over the feature dimension in registers first (D times fewer atomics).
 #include <cmath>
 
+#include <hipcub/hipcub.hpp>
+
 #include "common.h"
 
 namespace kl {
@@ -255,26 +257,12 @@ __global__ void __launch_bounds__(256)
 __device__ __forceinline__ void dt_atomic_add(float *p, float v) { unsafeAtomicAdd(p, v); }
 __device__ __forceinline__ void dt_atomic_add(double *p, double v) { unsafeAtomicAdd(p, v); }
 
-// deftet_cuda.cu:240-420
+// deftet_cuda.cu:290-410: one item's contribution to its face's six image-coordinate
+// gradients, the reference's terms in the reference's order, summed over the features.
 template <typename T>
-__global__ void __launch_bounds__(256)
-    deftet_bwd_kernel(int64_t F, int64_t PK, int D, const T *__restrict__ grad, const int64_t *__restrict__ idx,
-                      const T *__restrict__ weights, const T *__restrict__ fvi, const T *__restrict__ feat, float eps,
-                      T *__restrict__ g_img, T *__restrict__ g_feat, int64_t items) {
-  const int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (it >= items) return;
-  const int64_t fid = idx[it];
-  if (fid < 0) return;
-  const int64_t b = it / PK;
-  const int64_t face = b * F + fid;
-  const T *g = grad + it * D;
-  const T aw = weights[it * 3 + 0], bw = weights[it * 3 + 1], cw = weights[it * 3 + 2];
-  const T wv[3] = {aw, bw, cw};
-  T *gf = g_feat + face * 3 * D;
-  for (int ii = 0; ii < 3; ii++)
-    for (int c = 0; c < D; c++) dt_atomic_add(gf + ii * D + c, g[c] * wv[ii]);
-
-  const T *im = fvi + face * 6;
+__device__ __forceinline__ void dt_item_img_grad(const T *__restrict__ g, int D, T aw, T bw, T cw,
+                                                 const T *__restrict__ im, const T *__restrict__ fa, float eps,
+                                                 T acc[6]) {
   const T ax = im[0], ay = im[1], bx = im[2], by = im[3], cx = im[4], cy = im[5];
   const T x0 = aw * ax + bw * bx + cw * cx;
   const T y0 = aw * ay + bw * by + cw * cy;
@@ -301,8 +289,8 @@ __global__ void __launch_bounds__(256)
   const T dw2dax = -(dw2dm + dw2dn + dw2ds), dw2day = -(dw2dp + dw2dq + dw2dt);
   const T dw2dbx = dw2dm, dw2dby = dw2dp, dw2dcx = dw2dn, dw2dcy = dw2dq;
 
-  T acc[6] = {0, 0, 0, 0, 0, 0};
-  const T *fa = feat + face * 3 * D;
+#pragma unroll
+  for (int v = 0; v < 6; v++) acc[v] = 0;
   const T kk = k3 * k3;
   for (int c = 0; c < D; c++) {
     const T c0 = fa[c], c1 = fa[D + c], c2 = fa[2 * D + c];
@@ -317,9 +305,122 @@ __global__ void __launch_bounds__(256)
     acc[2] += dldI * dIdbx; acc[3] += dldI * dIdby;
     acc[4] += dldI * dIdcx; acc[5] += dldI * dIdcy;
   }
+}
+
+// deftet_cuda.cu:240-420 with atomics: one lane per (pixel, slot) item that holds a face.
+// Used only when the item count does not fit the sorted gather below.
+template <typename T>
+__global__ void __launch_bounds__(256)
+    deftet_bwd_kernel(int64_t F, int64_t PK, int D, const T *__restrict__ grad, const int64_t *__restrict__ idx,
+                      const T *__restrict__ weights, const T *__restrict__ fvi, const T *__restrict__ feat, float eps,
+                      T *__restrict__ g_img, T *__restrict__ g_feat, int64_t items) {
+  const int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (it >= items) return;
+  const int64_t fid = idx[it];
+  if (fid < 0) return;
+  const int64_t face = (it / PK) * F + fid;
+  const T *g = grad + it * D;
+  const T wv[3] = {weights[it * 3 + 0], weights[it * 3 + 1], weights[it * 3 + 2]};
+  T *gf = g_feat + face * 3 * D;
+  for (int ii = 0; ii < 3; ii++)
+    for (int c = 0; c < D; c++) dt_atomic_add(gf + ii * D + c, g[c] * wv[ii]);
+  T acc[6];
+  dt_item_img_grad(g, D, wv[0], wv[1], wv[2], fvi + face * 6, feat + face * 3 * D, eps, acc);
   T *gi = g_img + face * 6;
 #pragma unroll
   for (int c = 0; c < 6; c++) dt_atomic_add(gi + c, acc[c]);
+}
+
+// Sort keys of the gather backward: the item's global face id (b*F + fid), or B*F for an empty
+// slot (sorted last; the sort then needs only the bits of B*F).  The radix sort is stable, so each face's items stay in item order.
+__global__ void __launch_bounds__(256)
+    deftet_bwd_keys_kernel(int64_t F, int64_t PK, uint32_t empty, const int64_t *__restrict__ idx,
+                           uint32_t *__restrict__ keys, int32_t *__restrict__ vals, int64_t items) {
+  const int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (it >= items) return;
+  const int64_t fid = idx[it];
+  keys[it] = fid >= 0 ? (uint32_t)((it / PK) * F + fid) : empty;
+  vals[it] = (int32_t)it;
+}
+
+__device__ __forceinline__ int64_t dt_lower_bound(const uint32_t *__restrict__ a, int64_t n, uint32_t key) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Gather backward: one lane per face; its items (a contiguous run of the sorted keys) are
+// summed in item order.  No atomics, deterministic, and the same summation order as the
+// oracle's ordered accumulation, so the gradients are bit-identical to it.
+template <typename T>
+__global__ void __launch_bounds__(256)
+    deftet_bwd_gather_kernel(int64_t BF, int D, const uint32_t *__restrict__ skeys, const int32_t *__restrict__ svals,
+                             int64_t items, const T *__restrict__ grad, const T *__restrict__ weights,
+                             const T *__restrict__ fvi, const T *__restrict__ feat, float eps, T *__restrict__ g_img,
+                             T *__restrict__ g_feat) {
+  const int64_t face = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (face >= BF) return;
+  const int64_t lo = dt_lower_bound(skeys, items, (uint32_t)face);
+  const int64_t hi = dt_lower_bound(skeys, items, (uint32_t)(face + 1));
+  const T *im = fvi + face * 6;
+  const T *fa = feat + face * 3 * D;
+  T sum[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t i = lo; i < hi; i++) {
+    const int64_t it = svals[i];
+    T acc[6];
+    dt_item_img_grad(grad + it * D, D, weights[it * 3 + 0], weights[it * 3 + 1], weights[it * 3 + 2], im, fa, eps,
+                     acc);
+#pragma unroll
+    for (int v = 0; v < 6; v++) sum[v] += acc[v];
+  }
+#pragma unroll
+  for (int v = 0; v < 6; v++) g_img[face * 6 + v] = sum[v];
+  for (int ii = 0; ii < 3; ii++) {
+    for (int c = 0; c < D; c++) {
+      T s = 0;
+      for (int64_t i = lo; i < hi; i++) {
+        const int64_t it = svals[i];
+        s += grad[it * D + c] * weights[it * 3 + ii];
+      }
+      g_feat[(face * 3 + ii) * D + c] = s;
+    }
+  }
+}
+
+// workspace of the gather backward (byte offsets, 256-aligned)
+struct DtBwdWs {
+  size_t keys_in, keys_out, vals_in, vals_out, temp, temp_bytes, total;
+  bool gather;  // false: sizes out of range for the 32-bit sort, use the atomic kernel
+};
+static size_t dt_align(size_t x) { return (x + 255) & ~(size_t)255; }
+static DtBwdWs dt_bwd_layout(int64_t B, int64_t F, int64_t P, int64_t K) {
+  DtBwdWs w{};
+  const int64_t n = B * P * K;
+  w.gather = n > 0 && n < ((int64_t)1 << 31) && B * F < ((int64_t)1 << 31);
+  if (!w.gather) {
+    w.total = 16;
+    return w;
+  }
+  size_t tb = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (const int32_t *)nullptr, (int32_t *)nullptr, (int)n);
+  size_t o = 0;
+  w.keys_in = o; o += dt_align((size_t)n * 4);
+  w.keys_out = o; o += dt_align((size_t)n * 4);
+  w.vals_in = o; o += dt_align((size_t)n * 4);
+  w.vals_out = o; o += dt_align((size_t)n * 4);
+  w.temp = o; w.temp_bytes = dt_align(tb > 0 ? tb : 1); o += w.temp_bytes;
+  w.total = o;
+  return w;
+}
+
+static int dt_key_bits(int64_t BF) {  // bits of the largest key (BF, the empty-slot key)
+  int bits = 1;
+  while (bits < 32 && ((int64_t)1 << bits) <= BF) bits++;
+  return bits;
 }
 
 template <typename T>
@@ -355,14 +456,32 @@ static int deftet_resolve(int64_t B, int64_t F, int64_t P, int64_t K, int64_t D,
 template <typename T>
 static int deftet_backward(int64_t B, int64_t F, int64_t P, int64_t K, int64_t D, const void *grad, const int64_t *idx,
                            const void *weights, const void *fvi, const void *feat, float eps, void *g_img,
-                           void *g_feat, hipStream_t st) {
-  KL_CHECK_RC(fill_async(g_img, 0, (size_t)(B * F * 6) * sizeof(T), st));
-  KL_CHECK_RC(fill_async(g_feat, 0, (size_t)(B * F * 3 * D) * sizeof(T), st));
-  const int64_t items = B * P * K;
-  if (items == 0) return KL_OK;
-  hipLaunchKernelGGL(deftet_bwd_kernel<T>, dim3((unsigned)cdiv(items, 256)), dim3(256), 0, st, F, P * K, (int)D,
-                     (const T *)grad, idx, (const T *)weights, (const T *)fvi, (const T *)feat, eps, (T *)g_img,
-                     (T *)g_feat, items);
+                           void *g_feat, void *ws, size_t ws_bytes, hipStream_t st) {
+  const int64_t items = B * P * K, BF = B * F;
+  const DtBwdWs L = dt_bwd_layout(B, F, P, K);
+  if (!L.gather || ws == nullptr || ws_bytes < L.total) {
+    KL_CHECK_RC(fill_async(g_img, 0, (size_t)(BF * 6) * sizeof(T), st));
+    KL_CHECK_RC(fill_async(g_feat, 0, (size_t)(BF * 3 * D) * sizeof(T), st));
+    if (items == 0) return KL_OK;
+    hipLaunchKernelGGL(deftet_bwd_kernel<T>, dim3((unsigned)cdiv(items, 256)), dim3(256), 0, st, F, P * K, (int)D,
+                       (const T *)grad, idx, (const T *)weights, (const T *)fvi, (const T *)feat, eps, (T *)g_img,
+                       (T *)g_feat, items);
+    KL_CHECK_LAUNCH();
+    return KL_OK;
+  }
+  if (BF == 0) return KL_OK;
+  uint8_t *w = (uint8_t *)ws;
+  uint32_t *kin = (uint32_t *)(w + L.keys_in), *kout = (uint32_t *)(w + L.keys_out);
+  int32_t *vin = (int32_t *)(w + L.vals_in), *vout = (int32_t *)(w + L.vals_out);
+  hipLaunchKernelGGL(deftet_bwd_keys_kernel, dim3((unsigned)cdiv(items, 256)), dim3(256), 0, st, F, P * K,
+                     (uint32_t)BF, idx, kin, vin, items);
+  KL_CHECK_LAUNCH();
+  size_t tb = L.temp_bytes;
+  const int bits = dt_key_bits(BF);
+  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.temp, tb, kin, kout, vin, vout, (int)items, 0, bits, st));
+  hipLaunchKernelGGL(deftet_bwd_gather_kernel<T>, dim3((unsigned)cdiv(BF, 256)), dim3(256), 0, st, BF, (int)D, kout,
+                     vout, items, (const T *)grad, (const T *)weights, (const T *)fvi, (const T *)feat, eps,
+                     (T *)g_img, (T *)g_feat);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
@@ -421,9 +540,15 @@ extern "C" int kl_deftet_sparse_render_backward(kl_dtype dtype, int64_t batch_si
                                                 const void *grad_interpolated_features, const int64_t *face_idx,
                                                 const void *weights, const void *face_vertices_image,
                                                 const void *face_features, float eps, void *grad_face_vertices_image,
-                                                void *grad_face_features, kl_stream stream) {
+                                                void *grad_face_features, void *workspace, size_t workspace_bytes,
+                                                kl_stream stream) {
   KL_CHECK_RC(check_deftet_sizes(batch_size, num_faces, num_pixels, knum, feat_dim));
   KL_DT_DISPATCH(dtype, deftet_backward, batch_size, num_faces, num_pixels, knum, feat_dim, grad_interpolated_features,
                  face_idx, weights, face_vertices_image, face_features, eps, grad_face_vertices_image,
-                 grad_face_features, S(stream));
+                 grad_face_features, workspace, workspace_bytes, S(stream));
+}
+
+extern "C" size_t kl_deftet_bwd_workspace_bytes(int64_t batch_size, int64_t num_faces, int64_t num_pixels,
+                                                int64_t knum) {
+  return dt_bwd_layout(batch_size, num_faces, num_pixels, knum).total;
 }

@@ -247,11 +247,14 @@ def deftet_sparse_render_backward_cuda(grad_interpolated_features, face_idx, wei
     dev = face_vertices_image.device
     g_img = torch.empty_like(face_vertices_image)
     g_feat = torch.empty_like(face_features)
+    lib = N.lib()
+    ws_bytes = lib.kl_deftet_bwd_workspace_bytes(B, F, P, K)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev), N.timed(func, dev):
-        N.check(N.lib().kl_deftet_sparse_render_backward(
+        N.check(lib.kl_deftet_sparse_render_backward(
             N.dtype_code(face_vertices_image.dtype), B, F, P, K, D, N.ptr(grad_interpolated_features),
             N.ptr(face_idx), N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), float(eps),
-            N.ptr(g_img), N.ptr(g_feat), N.stream_of(dev)), func)
+            N.ptr(g_img), N.ptr(g_feat), N.ptr(ws), ws_bytes, N.stream_of(dev)), func)
     return [g_img, g_feat]
 
 

@@ -89,8 +89,9 @@ _SIGS = {
                                              _P, _SZ, _P]),
     'kl_deftet_sparse_render_resolve': (_I, [_I, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
                                              _P]),
+    'kl_deftet_bwd_workspace_bytes': (_SZ, [_I64, _I64, _I64, _I64]),
     'kl_deftet_sparse_render_backward': (_I, [_I, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _F, _P, _P,
-                                              _P]),
+                                              _P, _SZ, _P]),
     'kl_unbatched_mesh_intersection': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P]),
     'kl_check_sign_workspace_bytes': (_SZ, [_I64, _I64, _I64]),
     'kl_check_sign': (_I, [_I, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P]),

@@ -10,8 +10,9 @@ no depth on a bound, so both agree there.
 
 GPU tests run the HIP path through kaolin.render.mesh.deftet_sparse_render and
 kaolin._C.render.mesh.deftet_sparse_render_{forward,backward}_cuda and compare with the
-oracle: face indices bit-exact; depths, weights and features bit-exact (same operation order,
-no contraction); gradients within 1e-5 (float atomics in another order).
+oracle: face indices, depths, weights, features and gradients bit-exact (same operation order,
+no contraction; the backward sums each face's items in item order, as the oracle does).  The
+atomic fallback of the ABI (no workspace) is checked to 1e-5.
 """
 import numpy as np
 import pytest
@@ -134,10 +135,31 @@ def test_gpu_render_fwd_bwd_vs_oracle(kal, dtype):
     grad = np.random.default_rng(5).uniform(0, 1, interp.shape).astype(dtype)
     interp.backward(_T(grad))
     g_img, g_feat = orc.deftet_sparse_render_backward(grad, r_idx, r_w, fvi, feat)
-    tol = 1e-5 if dtype == np.float32 else 1e-10
-    scale_i = max(np.abs(g_img).max(), 1.0)
-    np.testing.assert_allclose(_A(fvi_t.grad), g_img, rtol=tol, atol=tol * scale_i)
-    np.testing.assert_allclose(_A(feat_t.grad), g_feat, rtol=tol, atol=tol)
+    # the gather backward sums each face's items in item order, as the oracle: bit-exact
+    np.testing.assert_array_equal(_A(fvi_t.grad), g_img)
+    np.testing.assert_array_equal(_A(feat_t.grad), g_feat)
+
+
+@pytest.mark.gpu
+def test_gpu_backward_atomic_fallback(kal):
+    """Without a workspace the ABI falls back to the reference's float atomics (rounding-level)."""
+    import ctypes
+    from kaolin import _native as N
+    pix, ranges, fvz, fvi, feat, K = _grid_case(np.float32, F=1500, H=20, W=24)
+    r_interp, r_idx, r_w = orc.deftet_sparse_render(pix, ranges, fvz, fvi, feat, K)
+    grad = np.random.default_rng(6).uniform(0, 1, r_interp.shape).astype(np.float32)
+    B, P, _, D = grad.shape
+    F = fvi.shape[1]
+    g_img = torch.empty(fvi.shape, device=DEV)
+    g_feat = torch.empty(feat.shape, device=DEV)
+    gt, it, wt, ft, fet = _T(grad), _T(r_idx), _T(r_w), _T(fvi), _T(feat)
+    N.check(N.lib().kl_deftet_sparse_render_backward(
+        N.KL_F32, B, F, P, K, D, N.ptr(gt), N.ptr(it), N.ptr(wt), N.ptr(ft), N.ptr(fet), 1e-8, N.ptr(g_img),
+        N.ptr(g_feat), None, 0, N.stream_of(torch.device(DEV))), 'deftet bwd')
+    torch.cuda.synchronize()
+    e_img, e_feat = orc.deftet_sparse_render_backward(grad, r_idx, r_w, fvi, feat)
+    np.testing.assert_allclose(_A(g_img), e_img, rtol=1e-5, atol=1e-5 * max(np.abs(e_img).max(), 1.0))
+    np.testing.assert_allclose(_A(g_feat), e_feat, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.gpu
