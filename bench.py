@@ -205,6 +205,16 @@ def op_bytes(name, inp, stats):
     return None
 
 
+def survey_step_bytes(inp, stats):
+    """SURVEY.md §8d cfg3 figure for one fwd+bwd step, in the reference's data layout:
+    B*H*W*(60 + 8D + 13K + u*(8 + 13*kbar)) + B*F*(164 + 36D), u = uncovered fraction and
+    kbar = mean used soft-mask slots (+ terminator) over uncovered pixels, both measured."""
+    B, H, W, F = inp['fvz'].shape[0], inp['H'], inp['W'], inp['F']
+    D, K = 3, 30
+    u, kbar = stats['uncovered'], stats['mean_slots']
+    return int(B * H * W * (60 + 8 * D + 13 * K + u * (8 + 13 * kbar)) + B * F * (164 + 36 * D))
+
+
 # kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
 OP_KERNELS = {
     'dibr_soft_mask_forward': ('bin_faces_kernel<float, kl::SoftSrc', 'tile_bucket_kernel', 'tile_order_kernel',
@@ -433,7 +443,13 @@ def main():
                          'bytes_per_launch': dbytes, 'avg_launch_ms': round(ops_ms[dom], 4),
                          'note': 'algorithmic bytes of the compact soft-mask state (the reference layout would '
                                  'move ' + str(op_bytes('dibr_soft_mask_forward_cuda', inp, stats)) + ' B per call); '
-                                 'the op is latency-bound, not HBM-bound (DESIGN.md section 5)'},
+                                 'the op is latency-bound, not HBM-bound (DESIGN.md section 5)',
+                         'survey_formula': {
+                             'scope': 'whole fwd+bwd step, SURVEY.md 8d cfg3 bytes (reference layout)',
+                             'bytes_per_step': survey_step_bytes(inp, stats),
+                             'achieved': round(survey_step_bytes(inp, stats) / (elapsed / args.steps) / 1e9, 1),
+                             'frac': round(survey_step_bytes(inp, stats) / (elapsed / args.steps) / 1e9
+                                           / HBM_PEAK_GBS, 4)}},
             'ops': ops_report,
             'workload_stats': stats,
             'mode': mode,

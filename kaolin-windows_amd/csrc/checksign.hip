@@ -199,6 +199,7 @@ __global__ void __launch_bounds__(kCsTile)
                       const float *__restrict__ tbox) {
   __shared__ T s_v[9][kCsTile];
   __shared__ float s_bb[4][kCsTile];
+  __shared__ int s_tiles[kCsTile];
   __shared__ int s_wave[16];
   __shared__ T s_box[4][kCsTile / 64];
 
@@ -240,45 +241,57 @@ __global__ void __launch_bounds__(kCsTile)
   }
 
   int count = 0;
+  // Tiles whose union (y, z) bounds reach the workgroup's points, listed 256 tile ids at a
+  // time with one coalesced pass over the tile boxes (all tiles when there are no boxes).
   const int64_t ntiles = (F + kCsTile - 1) / kCsTile;
-  for (int64_t t0 = 0; t0 < F; t0 += kCsTile) {
-    if (tbox) {  // workgroup-uniform skip of a tile no point of the workgroup can use
-      const float *tb = tbox + (b * ntiles + t0 / kCsTile) * 4;
-      if (!((T)tb[0] <= gymx && (T)tb[1] >= gymn && (T)tb[2] <= gzmx && (T)tb[3] >= gzmn)) continue;
+  for (int64_t tc = 0; tc < ntiles; tc += kCsTile) {
+    const int64_t tt = tc + tid;
+    bool tok = tt < ntiles;
+    if (tok && tbox) {
+      const float *tb = tbox + (b * ntiles + tt) * 4;
+      tok = (T)tb[0] <= gymx && (T)tb[1] >= gymn && (T)tb[2] <= gzmx && (T)tb[3] >= gzmn;
     }
-    const int64_t f = t0 + tid;
-    T v[9];
-    float bb[4];
-    bool keep = false;
-    if (f < F) {
-      cs_load_face(src, b, f, v);
-      // float y_min = min(b.y, min(c.y, d.y)) etc. (:47-50)
-      bb[0] = (float)fmin(v[1], fmin(v[4], v[7]));
-      bb[1] = (float)fmax(v[1], fmax(v[4], v[7]));
-      bb[2] = (float)fmin(v[2], fmin(v[5], v[8]));
-      bb[3] = (float)fmax(v[2], fmax(v[5], v[8]));
-      // some point of the workgroup can pass bbox_check (NaN bounds never pass it)
-      keep = (T)bb[0] <= gymx && (T)bb[1] >= gymn && (T)bb[2] <= gzmx && (T)bb[3] >= gzmn;
-    }
-    int total;
-    const int pos = block_exclusive_scan(keep ? 1 : 0, s_wave, &total);
-    if (keep) {
-#pragma unroll
-      for (int k = 0; k < 9; k++) s_v[k][pos] = v[k];
-#pragma unroll
-      for (int k = 0; k < 4; k++) s_bb[k][pos] = bb[k];
-    }
+    int ntl;
+    const int tpos = block_exclusive_scan(tok ? 1 : 0, s_wave, &ntl);
+    if (tok) s_tiles[tpos] = (int)tt;
     __syncthreads();
-    if (active) {
-      for (int j = 0; j < total; j++) {
-        const T p1[3] = {s_v[0][j], s_v[1][j], s_v[2][j]};
-        const T p2[3] = {s_v[3][j], s_v[4][j], s_v[5][j]};
-        const T p3[3] = {s_v[6][j], s_v[7][j], s_v[8][j]};
-        const float bbj[4] = {s_bb[0][j], s_bb[1][j], s_bb[2][j], s_bb[3][j]};
-        count += cs_cross(qx, qy, qz, p1, p2, p3, bbj);
+    for (int kt = 0; kt < ntl; kt++) {
+      const int64_t t0 = (int64_t)s_tiles[kt] * kCsTile;
+      const int64_t f = t0 + tid;
+      T v[9];
+      float bb[4];
+      bool keep = false;
+      if (f < F) {
+        cs_load_face(src, b, f, v);
+        // float y_min = min(b.y, min(c.y, d.y)) etc. (:47-50)
+        bb[0] = (float)fmin(v[1], fmin(v[4], v[7]));
+        bb[1] = (float)fmax(v[1], fmax(v[4], v[7]));
+        bb[2] = (float)fmin(v[2], fmin(v[5], v[8]));
+        bb[3] = (float)fmax(v[2], fmax(v[5], v[8]));
+        // some point of the workgroup can pass bbox_check (NaN bounds never pass it)
+        keep = (T)bb[0] <= gymx && (T)bb[1] >= gymn && (T)bb[2] <= gzmx && (T)bb[3] >= gzmn;
       }
+      int total;
+      const int pos = block_exclusive_scan(keep ? 1 : 0, s_wave, &total);
+      if (keep) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) s_v[k][pos] = v[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) s_bb[k][pos] = bb[k];
+      }
+      __syncthreads();
+      if (active) {
+        for (int j = 0; j < total; j++) {
+          const T p1[3] = {s_v[0][j], s_v[1][j], s_v[2][j]};
+          const T p2[3] = {s_v[3][j], s_v[4][j], s_v[5][j]};
+          const T p3[3] = {s_v[6][j], s_v[7][j], s_v[8][j]};
+          const float bbj[4] = {s_bb[0][j], s_bb[1][j], s_bb[2][j], s_bb[3][j]};
+          count += cs_cross(qx, qy, qz, p1, p2, p3, bbj);
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
+    __syncthreads();  // s_tiles is rewritten by the next chunk
   }
   if (active) {
     if (counts) counts[row] = (T)count;

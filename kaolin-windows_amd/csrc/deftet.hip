@@ -101,6 +101,7 @@ __global__ void __launch_bounds__(kDtTile)
                       T *__restrict__ out_w1, const T *__restrict__ tbox) {
   __shared__ T s_f[13][kDtTile];  // ax ay bx by cx cy az bz cz xmin ymin xmax ymax
   __shared__ int s_id[kDtTile];
+  __shared__ int s_tiles[kDtTile];
   __shared__ int s_wave[16];
   __shared__ T s_box[4][kDtTile / 64];
 
@@ -149,58 +150,75 @@ __global__ void __launch_bounds__(kDtTile)
   const T *mi = fvi + b * F * 6;
   const T *mb = bboxes ? bboxes + b * F * 4 : nullptr;
 
+  // Tiles whose union bbox reaches the workgroup's pixels, listed (in mesh order) 256 tile ids
+  // at a time with one coalesced pass over the tile boxes, instead of a dependent global load
+  // per tile inside the walk.
   const int64_t ntiles = (F + kDtTile - 1) / kDtTile;
-  for (int64_t t0 = 0; t0 < F; t0 += kDtTile) {
-    {  // workgroup-uniform: skip a tile whose union bbox misses the workgroup's pixels
-      const T *tb = tbox + (b * ntiles + t0 / kDtTile) * 4;
-      if (!(tb[0] <= gxmax && tb[2] > gxmin && tb[1] <= gymax && tb[3] > gymin)) continue;
+  bool full = false;
+  for (int64_t tc = 0; tc < ntiles && !full; tc += kDtTile) {
+    const int64_t tt = tc + tid;
+    bool tok = false;
+    if (tt < ntiles) {
+      const T *tb = tbox + (b * ntiles + tt) * 4;
+      tok = tb[0] <= gxmax && tb[2] > gxmin && tb[1] <= gymax && tb[3] > gymin;
     }
-    if (!__syncthreads_or(active && n < K)) break;  // every pixel of the workgroup is full
-    const int64_t f = t0 + tid;
-    T v[13];
-    bool keep = false;
-    if (f < F) {
-#pragma unroll
-      for (int c = 0; c < 6; c++) v[c] = mi[f * 6 + c];
-#pragma unroll
-      for (int c = 0; c < 3; c++) v[6 + c] = mz[f * 3 + c];
-      dt_face_bbox(mi, mb, f, v + 9);
-      // some pixel x of the workgroup can satisfy xmin <= x < xmax (same for y)
-      keep = v[9] <= gxmax && v[11] > gxmin && v[10] <= gymax && v[12] > gymin;
-    }
-    int total;
-    const int pos = block_exclusive_scan(keep ? 1 : 0, s_wave, &total);
-    if (keep) {
-#pragma unroll
-      for (int c = 0; c < 13; c++) s_f[c][pos] = v[c];
-      s_id[pos] = (int)f;
-    }
+    int ntl;
+    const int tpos = block_exclusive_scan(tok ? 1 : 0, s_wave, &ntl);
+    if (tok) s_tiles[tpos] = (int)tt;
     __syncthreads();
-    if (active && n < K) {
-      for (int j = 0; j < total; j++) {
-        const T xmin = s_f[9][j], ymin = s_f[10][j], xmax = s_f[11][j], ymax = s_f[12][j];
-        if (!(x0 >= xmin && x0 < xmax && y0 >= ymin && y0 < ymax)) continue;
-        const T aex = s_f[0][j] - x0, aey = s_f[1][j] - y0;
-        const T bex = s_f[2][j] - x0, bey = s_f[3][j] - y0;
-        const T cex = s_f[4][j] - x0, cey = s_f[5][j] - y0;
-        const T _w0 = bex * cey - bey * cex;
-        const T _w1 = cex * aey - cey * aex;
-        const T _w2 = aex * bey - aey * bex;
-        const T norm = _w0 + _w1 + _w2;
-        const T den = norm + dt_copysign_eps_f(eps, norm);
-        const T w0 = _w0 / den, w1 = _w1 / den, w2 = _w2 / den;
-        if (w0 >= (T)0 && w1 >= (T)0 && w2 >= (T)0) {
-          const T d = w0 * s_f[6][j] + w1 * s_f[7][j] + w2 * s_f[8][j];
-          if (d < hi && d >= lo) {
-            row_idx[n] = s_id[j];
-            row_d[n] = d;
-            row_w0[n] = w0;
-            row_w1[n] = w1;
-            if (++n == K) break;
+    for (int k = 0; k < ntl; k++) {
+      if (!__syncthreads_or(active && n < K)) {  // every pixel of the workgroup is full
+        full = true;
+        break;
+      }
+      const int64_t t0 = (int64_t)s_tiles[k] * kDtTile;
+      const int64_t f = t0 + tid;
+      T v[13];
+      bool keep = false;
+      if (f < F) {
+#pragma unroll
+        for (int c = 0; c < 6; c++) v[c] = mi[f * 6 + c];
+#pragma unroll
+        for (int c = 0; c < 3; c++) v[6 + c] = mz[f * 3 + c];
+        dt_face_bbox(mi, mb, f, v + 9);
+        // some pixel x of the workgroup can satisfy xmin <= x < xmax (same for y)
+        keep = v[9] <= gxmax && v[11] > gxmin && v[10] <= gymax && v[12] > gymin;
+      }
+      int total;
+      const int pos = block_exclusive_scan(keep ? 1 : 0, s_wave, &total);
+      if (keep) {
+#pragma unroll
+        for (int c = 0; c < 13; c++) s_f[c][pos] = v[c];
+        s_id[pos] = (int)f;
+      }
+      __syncthreads();
+      if (active && n < K) {
+        for (int j = 0; j < total; j++) {
+          const T xmin = s_f[9][j], ymin = s_f[10][j], xmax = s_f[11][j], ymax = s_f[12][j];
+          if (!(x0 >= xmin && x0 < xmax && y0 >= ymin && y0 < ymax)) continue;
+          const T aex = s_f[0][j] - x0, aey = s_f[1][j] - y0;
+          const T bex = s_f[2][j] - x0, bey = s_f[3][j] - y0;
+          const T cex = s_f[4][j] - x0, cey = s_f[5][j] - y0;
+          const T _w0 = bex * cey - bey * cex;
+          const T _w1 = cex * aey - cey * aex;
+          const T _w2 = aex * bey - aey * bex;
+          const T norm = _w0 + _w1 + _w2;
+          const T den = norm + dt_copysign_eps_f(eps, norm);
+          const T w0 = _w0 / den, w1 = _w1 / den, w2 = _w2 / den;
+          if (w0 >= (T)0 && w1 >= (T)0 && w2 >= (T)0) {
+            const T d = w0 * s_f[6][j] + w1 * s_f[7][j] + w2 * s_f[8][j];
+            if (d < hi && d >= lo) {
+              row_idx[n] = s_id[j];
+              row_d[n] = d;
+              row_w0[n] = w0;
+              row_w1[n] = w1;
+              if (++n == K) break;
+            }
           }
         }
       }
     }
+    __syncthreads();  // s_tiles is rewritten by the next chunk
   }
   if (active) {
     for (int k = n; k < K; k++) {
