@@ -379,12 +379,14 @@ int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points, int64_t n
 /* check_sign (ops/mesh/check_sign.py:25-154) for a batch: verts (B,V,3), faces (F,3) int64,
  * points (B,P,3), maxlen (B) the per-mesh divisor check_sign.py:140-146 applies to verts and
  * points (NULL: none) -> contains (B,P) bool bytes (odd crossing count).  workspace:
- * kl_check_sign_workspace_bytes(B, F, P) bytes (point order keys, per-tile face bounds, sort
- * scratch; no initialisation needed). */
-size_t kl_check_sign_workspace_bytes(int64_t batch_size, int64_t num_faces, int64_t num_points);
+ * kl_check_sign_workspace_bytes(dtype, B, F, P) bytes (no initialisation needed); the (y, z)
+ * grid's face lists are allocated through `alloc` once their length is known (one 8-byte
+ * device-to-host read and a stream synchronisation). */
+size_t kl_check_sign_workspace_bytes(kl_dtype dtype, int64_t batch_size, int64_t num_faces, int64_t num_points);
 int kl_check_sign(kl_dtype dtype, int64_t batch_size, int64_t num_vertices, int64_t num_faces, int64_t num_points,
                   const void *verts, const int64_t *faces, const void *points, const void *maxlen,
-                  uint8_t *contains, void *workspace, size_t workspace_bytes, kl_stream stream);
+                  uint8_t *contains, void *workspace, size_t workspace_bytes, kl_alloc_fn alloc, void *alloc_ctx,
+                  kl_stream stream);
 
 /* ------------------------------------------------------------ voxelgrid */
 

@@ -14,13 +14,14 @@
 // counts are bit-identical.
 //
 // MI355X mapping: one lane per point, a register count per lane (the reference adds 1.0 with
-// a global atomicAdd per crossing).  A workgroup owns 256 points; faces stream through LDS in
-// tiles of 256 and each tile is culled against the workgroup's (y, z) point bbox with an
-// order-preserving block compaction, so lanes walk (LDS broadcast reads) only faces whose
-// bbox can hold one of the workgroup's points.  The batched entry gathers the face corners
-// from (vertices, faces) and applies check_sign's 1 / maxlen normalisation on load (the same
-// IEEE division the reference does in torch), so neither the normalised vertices nor the
-// (F, 3, 3) corner arrays are materialised.
+// a global atomicAdd per crossing).
+// * Batched entry (check_sign): the faces are binned into a G x G grid over the mesh's (y, z)
+//   box (count, scan, fill), and each lane walks only its point's cell list.  Points are
+//   visited in the Morton order of their (y, z) so that a wave's lanes share cells.  Face
+//   corners are gathered from (vertices, faces) once, with check_sign's 1 / maxlen
+//   normalisation applied on load (the IEEE division the reference does in torch).
+// * Unbatched _C entry: faces stream through LDS in tiles of 256, compacted per tile against
+//   the workgroup's (y, z) point box, and lanes walk them with LDS broadcast reads.
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -154,41 +155,6 @@ __global__ void __launch_bounds__(256)
   vals[i] = (int32_t)(i % P);  // point index within its mesh
 }
 
-// Union of the (float) (y, z) face bounds per tile of kCsTile faces (grid (ntiles, B)).
-template <typename T>
-__global__ void __launch_bounds__(kCsTile) cs_tilebox_kernel(int64_t F, CsFaces<T> src, float *__restrict__ tbox) {
-  __shared__ float s_r[4][kCsTile / 64];
-  const int tid = threadIdx.x;
-  const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * kCsTile + tid;
-  float r0 = INFINITY, r1 = -INFINITY, r2 = INFINITY, r3 = -INFINITY;
-  if (f < F) {
-    T v[9];
-    cs_load_face(src, b, f, v);
-    r0 = (float)fmin(v[1], fmin(v[4], v[7]));
-    r1 = (float)fmax(v[1], fmax(v[4], v[7]));
-    r2 = (float)fmin(v[2], fmin(v[5], v[8]));
-    r3 = (float)fmax(v[2], fmax(v[5], v[8]));
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    r0 = fminf(r0, __shfl_xor(r0, o));
-    r1 = fmaxf(r1, __shfl_xor(r1, o));
-    r2 = fminf(r2, __shfl_xor(r2, o));
-    r3 = fmaxf(r3, __shfl_xor(r3, o));
-  }
-  if ((tid & 63) == 0) {
-    s_r[0][tid >> 6] = r0; s_r[1][tid >> 6] = r1; s_r[2][tid >> 6] = r2; s_r[3][tid >> 6] = r3;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    for (int w = 1; w < kCsTile / 64; w++) {
-      r0 = fminf(r0, s_r[0][w]); r1 = fmaxf(r1, s_r[1][w]); r2 = fminf(r2, s_r[2][w]); r3 = fmaxf(r3, s_r[3][w]);
-    }
-    float *o = tbox + (b * gridDim.x + blockIdx.x) * 4;
-    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = r3;
-  }
-}
-
 // grid (cdiv(P, 256), B); counts (B,P) in T (the _C contract) and/or contains (B,P) bool.
 // perm (B,P) int32 or null: lane i of the batch handles point perm[i].
 // tbox (B, ntiles, 4) float or null.
@@ -309,23 +275,186 @@ static int check_sign_launch(int64_t B, int64_t P, int64_t F, const void *points
   return KL_OK;
 }
 
-// workspace layout of the batched entry (byte offsets, 256-aligned)
+// ---- batched entry: a (y, z) grid of face lists ------------------------------------------
+// A ray toward +x can only cross faces whose (y, z) bounds hold the point, so the mesh's (y, z)
+// box is cut into G x G cells and every face is listed in the cells its float bounds overlap.
+// The cell of a value is a monotone function of it (the same float expression for faces and
+// points), so every face that passes a point's bbox_check is in the point's cell list.  The
+// counts do not depend on the order of a list.  Points outside the box cross nothing.
+
+// Per face: normalised corners (9 x T) and float (y, z) bounds (4), written once; plus the
+// per-tile union bounds (reduced to the mesh box below).
+template <typename T>
+__global__ void __launch_bounds__(kCsTile)
+    cs_prep_kernel(int64_t F, CsFaces<T> src, T *__restrict__ fc, float *__restrict__ fb, float *__restrict__ tbox) {
+  __shared__ float s_r[4][kCsTile / 64];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * kCsTile + tid;
+  float r0 = INFINITY, r1 = -INFINITY, r2 = INFINITY, r3 = -INFINITY;
+  if (f < F) {
+    T v[9];
+    cs_load_face(src, b, f, v);
+    const int64_t o = b * F + f;
+#pragma unroll
+    for (int k = 0; k < 9; k++) fc[o * 9 + k] = v[k];
+    const float bb[4] = {(float)fmin(v[1], fmin(v[4], v[7])), (float)fmax(v[1], fmax(v[4], v[7])),
+                         (float)fmin(v[2], fmin(v[5], v[8])), (float)fmax(v[2], fmax(v[5], v[8]))};
+#pragma unroll
+    for (int k = 0; k < 4; k++) fb[o * 4 + k] = bb[k];
+    r0 = bb[0]; r1 = bb[1]; r2 = bb[2]; r3 = bb[3];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    r0 = fminf(r0, __shfl_xor(r0, o));
+    r1 = fmaxf(r1, __shfl_xor(r1, o));
+    r2 = fminf(r2, __shfl_xor(r2, o));
+    r3 = fmaxf(r3, __shfl_xor(r3, o));
+  }
+  if ((tid & 63) == 0) {
+    s_r[0][tid >> 6] = r0; s_r[1][tid >> 6] = r1; s_r[2][tid >> 6] = r2; s_r[3][tid >> 6] = r3;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < kCsTile / 64; w++) {
+      r0 = fminf(r0, s_r[0][w]); r1 = fmaxf(r1, s_r[1][w]); r2 = fminf(r2, s_r[2][w]); r3 = fmaxf(r3, s_r[3][w]);
+    }
+    float *o = tbox + (b * gridDim.x + blockIdx.x) * 4;
+    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = r3;
+  }
+}
+
+// mesh box (y0, y1, z0, z1) and cell scales (G / extent, 0 for an empty or infinite extent);
+// one workgroup per mesh
+__global__ void __launch_bounds__(256)
+    cs_meshbox_kernel(int64_t ntiles, int G, const float *__restrict__ tbox, float *__restrict__ mbox) {
+  __shared__ float s_r[4][4];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  float r0 = INFINITY, r1 = -INFINITY, r2 = INFINITY, r3 = -INFINITY;
+  for (int64_t t = tid; t < ntiles; t += 256) {
+    const float *tb = tbox + (b * ntiles + t) * 4;
+    r0 = fminf(r0, tb[0]); r1 = fmaxf(r1, tb[1]); r2 = fminf(r2, tb[2]); r3 = fmaxf(r3, tb[3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    r0 = fminf(r0, __shfl_xor(r0, o));
+    r1 = fmaxf(r1, __shfl_xor(r1, o));
+    r2 = fminf(r2, __shfl_xor(r2, o));
+    r3 = fmaxf(r3, __shfl_xor(r3, o));
+  }
+  if ((tid & 63) == 0) {
+    s_r[0][tid >> 6] = r0; s_r[1][tid >> 6] = r1; s_r[2][tid >> 6] = r2; s_r[3][tid >> 6] = r3;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; w++) {
+      r0 = fminf(r0, s_r[0][w]); r1 = fmaxf(r1, s_r[1][w]); r2 = fminf(r2, s_r[2][w]); r3 = fmaxf(r3, s_r[3][w]);
+    }
+    const float ey = r1 - r0, ez = r3 - r2;
+    float *o = mbox + b * 8;
+    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = r3;
+    o[4] = (ey > 0.f && ey < INFINITY) ? (float)G / ey : 0.f;
+    o[5] = (ez > 0.f && ez < INFINITY) ? (float)G / ez : 0.f;
+  }
+}
+
+// monotone cell coordinate of v in [0, G)
+__device__ __forceinline__ int cs_cell(float v, float v0, float inv, int G) {
+  const float c = fminf(fmaxf((v - v0) * inv, 0.f), (float)(G - 1));
+  return (int)c;
+}
+
+// fill == false: count the list entries of each cell; fill == true: write them
+template <bool FILL>
+__global__ void __launch_bounds__(256)
+    cs_bin_kernel(int64_t F, int G, const float *__restrict__ fb, const float *__restrict__ mbox,
+                  int *__restrict__ cnt, const int *__restrict__ offs, int *__restrict__ list) {
+  const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (f >= F) return;
+  const float *bb = fb + (b * F + f) * 4;
+  const float y0 = bb[0], y1 = bb[1], z0 = bb[2], z1 = bb[3];
+  if (!(y0 <= y1 && z0 <= z1)) return;  // NaN bounds never pass bbox_check
+  const float *m = mbox + b * 8;
+  const int cy0 = cs_cell(y0, m[0], m[4], G), cy1 = cs_cell(y1, m[0], m[4], G);
+  const int cz0 = cs_cell(z0, m[2], m[5], G), cz1 = cs_cell(z1, m[2], m[5], G);
+  int *c = cnt + b * (int64_t)G * G;
+  for (int cz = cz0; cz <= cz1; cz++)
+    for (int cy = cy0; cy <= cy1; cy++) {
+      const int64_t cell = (int64_t)cz * G + cy;
+      const int slot = atomicAdd(c + cell, 1);
+      if (FILL) list[offs[b * (int64_t)G * G + cell] + slot] = (int)f;
+    }
+}
+
+// one lane per point (Morton order through perm): walk the point's cell list
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cs_grid_check_kernel(int64_t P, int64_t F, int G, const T *__restrict__ points, const T *__restrict__ maxlen,
+                         const int32_t *__restrict__ perm, const float *__restrict__ mbox, const int *__restrict__ cnt,
+                         const int *__restrict__ offs, const int *__restrict__ list, const T *__restrict__ fc,
+                         const float *__restrict__ fb, uint8_t *__restrict__ contains) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t b = blockIdx.y;
+  if (i >= P) return;
+  const int64_t p = perm ? (int64_t)perm[b * P + i] : i;
+  const int64_t row = b * P + p;
+  T qx = points[row * 3 + 0], qy = points[row * 3 + 1], qz = points[row * 3 + 2];
+  if (maxlen) {
+    const T m = maxlen[b];
+    qx = qx / m; qy = qy / m; qz = qz / m;
+  }
+  const float *mb = mbox + b * 8;
+  int count = 0;
+  // outside the union of the face bounds (or NaN): no face passes bbox_check
+  if (qy >= (T)mb[0] && qy <= (T)mb[1] && qz >= (T)mb[2] && qz <= (T)mb[3]) {
+    const int cy = cs_cell((float)qy, mb[0], mb[4], G), cz = cs_cell((float)qz, mb[2], mb[5], G);
+    const int64_t cell = b * (int64_t)G * G + (int64_t)cz * G + cy;
+    const int n = cnt[cell], o = offs[cell];
+    for (int k = 0; k < n; k++) {
+      const int64_t f = b * F + list[o + k];
+      const T *v = fc + f * 9;
+      const T p1[3] = {v[0], v[1], v[2]}, p2[3] = {v[3], v[4], v[5]}, p3[3] = {v[6], v[7], v[8]};
+      const float *bb = fb + f * 4;
+      const float bbj[4] = {bb[0], bb[1], bb[2], bb[3]};
+      count += cs_cross(qx, qy, qz, p1, p2, p3, bbj);
+    }
+  }
+  contains[row] = (uint8_t)(count & 1);
+}
+
+static int cs_grid_dim(int64_t F) {
+  int G = 1;
+  while (G < 1024 && (int64_t)G * G < F) G++;
+  return G;
+}
+
+// workspace layout of the batched entry (byte offsets, 256-aligned); the face lists come from
+// the allocator callback once their total is known
 struct CsWs {
-  size_t keys_in, keys_out, vals_in, vals_out, tbox, temp, temp_bytes, total;
+  size_t keys_in, keys_out, vals_in, vals_out, tbox, mbox, fc, fb, cnt, offs, temp, temp_bytes, total;
+  int G;
 };
 static size_t cs_align(size_t x) { return (x + 255) & ~(size_t)255; }
-static CsWs cs_ws_layout(int64_t B, int64_t F, int64_t P) {
+static CsWs cs_ws_layout(int64_t B, int64_t F, int64_t P, size_t tsize) {
   CsWs w{};
-  size_t tb = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+  w.G = cs_grid_dim(F);
+  const int64_t cells = B * (int64_t)w.G * w.G;
+  size_t t1 = 0, t2 = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                            (const int32_t *)nullptr, (int32_t *)nullptr, (int)(P > 0 ? P : 1));
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (const int *)nullptr, (int *)nullptr, (int)cells);
   size_t o = 0;
   w.keys_in = o; o += cs_align((size_t)(B * P) * 4);
   w.keys_out = o; o += cs_align((size_t)(B * P) * 4);
   w.vals_in = o; o += cs_align((size_t)(B * P) * 4);
   w.vals_out = o; o += cs_align((size_t)(B * P) * 4);
   w.tbox = o; o += cs_align((size_t)(B * cdiv(F, kCsTile)) * 16);
-  w.temp = o; w.temp_bytes = cs_align(tb > 0 ? tb : 1); o += w.temp_bytes;
+  w.mbox = o; o += cs_align((size_t)B * 32);
+  w.fc = o; o += cs_align((size_t)(B * F) * 9 * tsize);
+  w.fb = o; o += cs_align((size_t)(B * F) * 16);
+  w.cnt = o; o += cs_align((size_t)cells * 4);
+  w.offs = o; o += cs_align((size_t)cells * 4);
+  w.temp = o; w.temp_bytes = cs_align(t1 > t2 ? t1 : (t2 > 0 ? t2 : 1)); o += w.temp_bytes;
   w.total = o;
   return w;
 }
@@ -340,29 +469,63 @@ static int mesh_intersection_unbatched(int64_t P, int64_t F, const void *points,
 template <typename T>
 static int check_sign_batched(int64_t B, int64_t V, int64_t F, int64_t P, const void *verts, const int64_t *faces,
                               const void *points, const void *maxlen, uint8_t *contains, void *ws, size_t ws_bytes,
-                              hipStream_t st) {
+                              kl_alloc_fn alloc, void *alloc_ctx, hipStream_t st) {
   CsFaces<T> src{nullptr, nullptr, nullptr, (const T *)verts, faces, (const T *)maxlen, V};
   if (B == 0 || P == 0) return KL_OK;
-  const CsWs L = cs_ws_layout(B, F, P);
+  if (F == 0) return fill_async(contains, 0, (size_t)(B * P), st);
+  const CsWs L = cs_ws_layout(B, F, P, sizeof(T));
   KL_REQUIRE(ws && ws_bytes >= L.total, "check_sign: workspace too small");
+  KL_REQUIRE(alloc != nullptr, "check_sign: allocator callback required");
+  const int G = L.G;
+  const int64_t cells = B * (int64_t)G * G;
   uint8_t *w = (uint8_t *)ws;
   uint32_t *kin = (uint32_t *)(w + L.keys_in), *kout = (uint32_t *)(w + L.keys_out);
   int32_t *vin = (int32_t *)(w + L.vals_in), *vout = (int32_t *)(w + L.vals_out);
-  float *tbox = (float *)(w + L.tbox);
+  float *tbox = (float *)(w + L.tbox), *mbox = (float *)(w + L.mbox), *fb = (float *)(w + L.fb);
+  T *fc = (T *)(w + L.fc);
+  int *cnt = (int *)(w + L.cnt), *offs = (int *)(w + L.offs);
   const int64_t ntiles = cdiv(F, kCsTile);
-  if (ntiles > 0) {
-    hipLaunchKernelGGL(cs_tilebox_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kCsTile), 0, st, F, src, tbox);
-    KL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cs_prep_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kCsTile), 0, st, F, src, fc, fb,
+                     tbox);
+  KL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(cs_meshbox_kernel, dim3((unsigned)B), dim3(256), 0, st, ntiles, G, (const float *)tbox, mbox);
+  KL_CHECK_LAUNCH();
+  KL_CHECK_RC(fill_async(cnt, 0, (size_t)cells * 4, st));
+  const dim3 fgrid((unsigned)cdiv(F, 256), (unsigned)B);
+  hipLaunchKernelGGL(cs_bin_kernel<false>, fgrid, dim3(256), 0, st, F, G, (const float *)fb, (const float *)mbox, cnt,
+                     (const int *)nullptr, (int *)nullptr);
+  KL_CHECK_LAUNCH();
+  size_t tb = L.temp_bytes;
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, cnt, offs, (int)cells, st));
+  int last[2] = {0, 0};
+  KL_CHECK_HIP(hipMemcpyAsync(&last[0], offs + cells - 1, 4, hipMemcpyDeviceToHost, st));
+  KL_CHECK_HIP(hipMemcpyAsync(&last[1], cnt + cells - 1, 4, hipMemcpyDeviceToHost, st));
+  KL_CHECK_HIP(hipStreamSynchronize(st));
+  const int64_t total = (int64_t)last[0] + last[1];
+  KL_REQUIRE(total >= 0 && total < ((int64_t)1 << 31), "check_sign: face lists too long");
+  int *list = (int *)alloc(alloc_ctx, (size_t)(total > 0 ? total : 1) * 4);
+  if (!list) {
+    set_error("check_sign: allocator returned NULL");
+    return KL_E_ALLOC;
   }
+  KL_CHECK_RC(fill_async(cnt, 0, (size_t)cells * 4, st));
+  hipLaunchKernelGGL(cs_bin_kernel<true>, fgrid, dim3(256), 0, st, F, G, (const float *)fb, (const float *)mbox, cnt,
+                     (const int *)offs, list);
+  KL_CHECK_LAUNCH();
   hipLaunchKernelGGL(cs_key_kernel<T>, dim3((unsigned)cdiv(B * P, 256)), dim3(256), 0, st, B * P, P,
                      (const T *)points, kin, vin);
   KL_CHECK_LAUNCH();
   for (int64_t b = 0; b < B; b++) {  // each mesh's points sorted on their own
-    size_t tb = L.temp_bytes;
-    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.temp, tb, kin + b * P, kout + b * P, vin + b * P,
+    size_t ts = L.temp_bytes;
+    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.temp, ts, kin + b * P, kout + b * P, vin + b * P,
                                                     vout + b * P, (int)P, 0, 32, st));
   }
-  return check_sign_launch<T>(B, P, F, points, src, nullptr, contains, vout, tbox, st);
+  hipLaunchKernelGGL(cs_grid_check_kernel<T>, dim3((unsigned)cdiv(P, 256), (unsigned)B), dim3(256), 0, st, P, F, G,
+                     (const T *)points, (const T *)maxlen, (const int32_t *)vout, (const float *)mbox,
+                     (const int *)cnt, (const int *)offs, (const int *)list, (const T *)fc, (const float *)fb,
+                     contains);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
 }
 
 }  // namespace kl
@@ -385,17 +548,19 @@ extern "C" int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points
                  S(stream));
 }
 
-extern "C" size_t kl_check_sign_workspace_bytes(int64_t batch_size, int64_t num_faces, int64_t num_points) {
-  return cs_ws_layout(batch_size, num_faces, num_points).total;
+extern "C" size_t kl_check_sign_workspace_bytes(kl_dtype dtype, int64_t batch_size, int64_t num_faces,
+                                                int64_t num_points) {
+  return cs_ws_layout(batch_size, num_faces, num_points, dtype == KL_F64 ? 8 : 4).total;
 }
 
 extern "C" int kl_check_sign(kl_dtype dtype, int64_t batch_size, int64_t num_vertices, int64_t num_faces,
                              int64_t num_points, const void *verts, const int64_t *faces, const void *points,
                              const void *maxlen, uint8_t *contains, void *workspace, size_t workspace_bytes,
-                             kl_stream stream) {
+                             kl_alloc_fn alloc, void *alloc_ctx, kl_stream stream) {
   KL_REQUIRE(batch_size >= 0 && num_vertices >= 0 && num_faces >= 0 && num_points >= 0, "check_sign: negative size");
   KL_REQUIRE(batch_size < 65536, "check_sign: batch_size must be < 65536");
-  KL_REQUIRE(num_points < ((int64_t)1 << 31), "check_sign: num_points must be < 2^31");
+  KL_REQUIRE(num_points < ((int64_t)1 << 31) && num_faces < ((int64_t)1 << 31),
+             "check_sign: num_points and num_faces must be < 2^31");
   KL_CS_DISPATCH(dtype, check_sign_batched, batch_size, num_vertices, num_faces, num_points, verts, faces, points,
-                 maxlen, contains, workspace, workspace_bytes, S(stream));
+                 maxlen, contains, workspace, workspace_bytes, alloc, alloc_ctx, S(stream));
 }

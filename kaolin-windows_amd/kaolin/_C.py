@@ -390,11 +390,13 @@ def check_sign_batched(verts, faces, points, maxlen):
     dev = points.device
     out = torch.empty((B, P), dtype=torch.bool, device=dev)
     lib = N.lib()
-    ws_bytes = lib.kl_check_sign_workspace_bytes(B, F, P)
+    code = N.dtype_code(verts.dtype)
+    ws_bytes = lib.kl_check_sign_workspace_bytes(code, B, F, P)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    arena = N.Arena(dev)
     with torch.cuda.device(dev), N.timed(func, dev):
-        N.check(lib.kl_check_sign(N.dtype_code(verts.dtype), B, V, F, P, N.ptr(verts), N.ptr(faces), N.ptr(points),
-                                  N.ptr(maxlen), N.ptr(out), N.ptr(ws), ws_bytes, N.stream_of(dev)), func)
+        N.check(lib.kl_check_sign(code, B, V, F, P, N.ptr(verts), N.ptr(faces), N.ptr(points), N.ptr(maxlen),
+                                  N.ptr(out), N.ptr(ws), ws_bytes, arena.fn, None, N.stream_of(dev)), func)
     return out
 
 
