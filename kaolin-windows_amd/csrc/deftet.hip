@@ -353,36 +353,30 @@ __global__ void __launch_bounds__(256)
 // slot (sorted last; the sort then needs only the bits of B*F).  The radix sort is stable, so each face's items stay in item order.
 __global__ void __launch_bounds__(256)
     deftet_bwd_keys_kernel(int64_t F, int64_t PK, uint32_t empty, const int64_t *__restrict__ idx,
-                           uint32_t *__restrict__ keys, int32_t *__restrict__ vals, int64_t items) {
+                           uint32_t *__restrict__ keys, int32_t *__restrict__ vals, int *__restrict__ cnt,
+                           int64_t items) {
   const int64_t it = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (it >= items) return;
   const int64_t fid = idx[it];
-  keys[it] = fid >= 0 ? (uint32_t)((it / PK) * F + fid) : empty;
+  const uint32_t key = fid >= 0 ? (uint32_t)((it / PK) * F + fid) : empty;
+  keys[it] = key;
   vals[it] = (int32_t)it;
+  if (fid >= 0) atomicAdd(cnt + key, 1);  // per-face item counts -> run offsets (exclusive scan)
 }
 
-__device__ __forceinline__ int64_t dt_lower_bound(const uint32_t *__restrict__ a, int64_t n, uint32_t key) {
-  int64_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (a[mid] < key) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-// Gather backward: one lane per face; its items (a contiguous run of the sorted keys) are
-// summed in item order.  No atomics, deterministic, and the same summation order as the
+// Gather backward: one lane per face; its items (the run [offs, offs + cnt) of the sorted keys)
+// are summed in item order.  No atomics, deterministic, and the same summation order as the
 // oracle's ordered accumulation, so the gradients are bit-identical to it.
 template <typename T>
 __global__ void __launch_bounds__(256)
-    deftet_bwd_gather_kernel(int64_t BF, int D, const uint32_t *__restrict__ skeys, const int32_t *__restrict__ svals,
-                             int64_t items, const T *__restrict__ grad, const T *__restrict__ weights,
+    deftet_bwd_gather_kernel(int64_t BF, int D, const int *__restrict__ offs, const int *__restrict__ cnt,
+                             const int32_t *__restrict__ svals, const T *__restrict__ grad, const T *__restrict__ weights,
                              const T *__restrict__ fvi, const T *__restrict__ feat, float eps, T *__restrict__ g_img,
                              T *__restrict__ g_feat) {
   const int64_t face = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (face >= BF) return;
-  const int64_t lo = dt_lower_bound(skeys, items, (uint32_t)face);
-  const int64_t hi = dt_lower_bound(skeys, items, (uint32_t)(face + 1));
+  const int64_t lo = offs[face];
+  const int64_t hi = lo + cnt[face];
   const T *im = fvi + face * 6;
   const T *fa = feat + face * 3 * D;
   T sum[6] = {0, 0, 0, 0, 0, 0};
@@ -410,7 +404,7 @@ __global__ void __launch_bounds__(256)
 
 // workspace of the gather backward (byte offsets, 256-aligned)
 struct DtBwdWs {
-  size_t keys_in, keys_out, vals_in, vals_out, temp, temp_bytes, total;
+  size_t keys_in, keys_out, vals_in, vals_out, cnt, offs, temp, temp_bytes, total;
   bool gather;  // false: sizes out of range for the 32-bit sort, use the atomic kernel
 };
 static size_t dt_align(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -422,14 +416,18 @@ static DtBwdWs dt_bwd_layout(int64_t B, int64_t F, int64_t P, int64_t K) {
     w.total = 16;
     return w;
   }
-  size_t tb = 0;
+  size_t tb = 0, ts = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                            (const int32_t *)nullptr, (int32_t *)nullptr, (int)n);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, ts, (const int *)nullptr, (int *)nullptr, (int)(B * F));
+  if (ts > tb) tb = ts;
   size_t o = 0;
   w.keys_in = o; o += dt_align((size_t)n * 4);
   w.keys_out = o; o += dt_align((size_t)n * 4);
   w.vals_in = o; o += dt_align((size_t)n * 4);
   w.vals_out = o; o += dt_align((size_t)n * 4);
+  w.cnt = o; o += dt_align((size_t)(B * F) * 4);
+  w.offs = o; o += dt_align((size_t)(B * F) * 4);
   w.temp = o; w.temp_bytes = dt_align(tb > 0 ? tb : 1); o += w.temp_bytes;
   w.total = o;
   return w;
@@ -491,15 +489,19 @@ static int deftet_backward(int64_t B, int64_t F, int64_t P, int64_t K, int64_t D
   uint8_t *w = (uint8_t *)ws;
   uint32_t *kin = (uint32_t *)(w + L.keys_in), *kout = (uint32_t *)(w + L.keys_out);
   int32_t *vin = (int32_t *)(w + L.vals_in), *vout = (int32_t *)(w + L.vals_out);
+  int *cnt = (int *)(w + L.cnt), *offs = (int *)(w + L.offs);
+  KL_CHECK_RC(fill_async(cnt, 0, (size_t)BF * 4, st));
   hipLaunchKernelGGL(deftet_bwd_keys_kernel, dim3((unsigned)cdiv(items, 256)), dim3(256), 0, st, F, P * K,
-                     (uint32_t)BF, idx, kin, vin, items);
+                     (uint32_t)BF, idx, kin, vin, cnt, items);
   KL_CHECK_LAUNCH();
   size_t tb = L.temp_bytes;
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, cnt, offs, (int)BF, st));
+  tb = L.temp_bytes;
   const int bits = dt_key_bits(BF);
   KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.temp, tb, kin, kout, vin, vout, (int)items, 0, bits, st));
-  hipLaunchKernelGGL(deftet_bwd_gather_kernel<T>, dim3((unsigned)cdiv(BF, 256)), dim3(256), 0, st, BF, (int)D, kout,
-                     vout, items, (const T *)grad, (const T *)weights, (const T *)fvi, (const T *)feat, eps,
-                     (T *)g_img, (T *)g_feat);
+  hipLaunchKernelGGL(deftet_bwd_gather_kernel<T>, dim3((unsigned)cdiv(BF, 256)), dim3(256), 0, st, BF, (int)D,
+                     (const int *)offs, (const int *)cnt, vout, (const T *)grad, (const T *)weights, (const T *)fvi,
+                     (const T *)feat, eps, (T *)g_img, (T *)g_feat);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
