@@ -39,6 +39,7 @@
 namespace kl {
 
 constexpr int kDtTile = 256;  // pixels per workgroup == faces per LDS tile
+constexpr int kDtRegD = 8;    // feature widths the gather backward keeps in registers
 
 template <typename T>
 __device__ __forceinline__ T dt_copysign_eps_f(float eps, T v) {
@@ -380,6 +381,35 @@ __global__ void __launch_bounds__(256)
   const T *im = fvi + face * 6;
   const T *fa = feat + face * 3 * D;
   T sum[6] = {0, 0, 0, 0, 0, 0};
+  if (D <= kDtRegD) {  // one pass over the items, feature sums in registers
+    T fs[3][kDtRegD];
+#pragma unroll
+    for (int ii = 0; ii < 3; ii++)
+#pragma unroll
+      for (int c = 0; c < kDtRegD; c++) fs[ii][c] = 0;
+    for (int64_t i = lo; i < hi; i++) {
+      const int64_t it = svals[i];
+      const T *g = grad + it * D;
+      const T wv[3] = {weights[it * 3 + 0], weights[it * 3 + 1], weights[it * 3 + 2]};
+      T acc[6];
+      dt_item_img_grad(g, D, wv[0], wv[1], wv[2], im, fa, eps, acc);
+#pragma unroll
+      for (int v = 0; v < 6; v++) sum[v] += acc[v];
+#pragma unroll
+      for (int ii = 0; ii < 3; ii++)
+#pragma unroll
+        for (int c = 0; c < kDtRegD; c++)
+          if (c < D) fs[ii][c] += g[c] * wv[ii];
+    }
+#pragma unroll
+    for (int v = 0; v < 6; v++) g_img[face * 6 + v] = sum[v];
+#pragma unroll
+    for (int ii = 0; ii < 3; ii++)
+#pragma unroll
+      for (int c = 0; c < kDtRegD; c++)
+        if (c < D) g_feat[(face * 3 + ii) * D + c] = fs[ii][c];
+    return;
+  }
   for (int64_t i = lo; i < hi; i++) {
     const int64_t it = svals[i];
     T acc[6];
