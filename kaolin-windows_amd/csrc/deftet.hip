@@ -273,6 +273,67 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Slot-parallel resolve for knum <= 256: a workgroup owns floor(256 / K) consecutive pixels and
+// one lane per (pixel, slot).  The slots are staged through LDS with coalesced loads; lane
+// (p, i) ranks its hit among pixel p's hits (the same stable rule as deftet_resolve_kernel)
+// and records it in the inverse permutation; lane (p, k) then writes output slot k, so every
+// output array is written with consecutive lanes on consecutive addresses.
+template <typename T>
+__global__ void __launch_bounds__(256)
+    deftet_resolve_slots_kernel(int64_t F, int64_t P, int K, int D, const int64_t *__restrict__ idx,
+                                const T *__restrict__ depth, const T *__restrict__ w0a, const T *__restrict__ w1a,
+                                const T *__restrict__ feat, int64_t *__restrict__ sidx, T *__restrict__ weights,
+                                T *__restrict__ interp, int64_t rows) {
+  __shared__ int64_t s_id[256];
+  __shared__ T s_d[256], s_w0[256], s_w1[256];
+  __shared__ short s_inv[256];
+  const int ppb = 256 / K;
+  const int t = threadIdx.x;
+  const int pl = t / K, k = t - (t / K) * K;
+  const int64_t r = (int64_t)blockIdx.x * ppb + pl;  // pixel row (b * P + p)
+  const bool active = pl < ppb && r < rows;
+  const int64_t o = r * K + k;
+  if (active) {
+    s_id[t] = idx[o];
+    s_d[t] = depth[o];
+    s_w0[t] = w0a[o];
+    s_w1[t] = w1a[o];
+  }
+  s_inv[t] = -1;
+  __syncthreads();
+  const int base = pl * K;
+  if (active && s_id[t] >= 0) {
+    const T di = s_d[t];
+    int rank = 0;
+    for (int j = 0; j < K; j++) {
+      if (s_id[base + j] < 0) continue;
+      const T dj = s_d[base + j];
+      rank += (dj > di || (dj == di && j < k)) ? 1 : 0;
+    }
+    s_inv[base + rank] = (short)k;
+  }
+  __syncthreads();
+  if (!active) return;
+  const int i = s_inv[t];
+  if (i < 0) {
+    sidx[o] = -1;
+    weights[o * 3 + 0] = 0;
+    weights[o * 3 + 1] = 0;
+    weights[o * 3 + 2] = 0;
+    for (int c = 0; c < D; c++) interp[o * D + c] = 0;
+    return;
+  }
+  const int64_t fid = s_id[base + i];
+  const T w0 = s_w0[base + i], w1 = s_w1[base + i];
+  const T w2 = (T)1 - (w0 + w1);
+  sidx[o] = fid;
+  weights[o * 3 + 0] = w0;
+  weights[o * 3 + 1] = w1;
+  weights[o * 3 + 2] = w2;
+  const T *f0 = feat + ((r / P) * F + fid) * 3 * D;
+  for (int c = 0; c < D; c++) interp[o * D + c] = w0 * f0[c] + w1 * f0[D + c] + w2 * f0[2 * D + c];
+}
+
 __device__ __forceinline__ void dt_atomic_add(float *p, float v) { unsafeAtomicAdd(p, v); }
 __device__ __forceinline__ void dt_atomic_add(double *p, double v) { unsafeAtomicAdd(p, v); }
 
@@ -492,9 +553,16 @@ static int deftet_resolve(int64_t B, int64_t F, int64_t P, int64_t K, int64_t D,
                           const void *w0, const void *w1, const void *feat, int64_t *sidx, void *weights, void *interp,
                           hipStream_t st) {
   const int64_t rows = B * P;
-  hipLaunchKernelGGL(deftet_resolve_kernel<T>, dim3((unsigned)cdiv(rows, 256)), dim3(256), 0, st, F, P, (int)K, (int)D,
-                     idx, (const T *)depth, (const T *)w0, (const T *)w1, (const T *)feat, sidx, (T *)weights,
-                     (T *)interp, rows);
+  if (K <= 256) {
+    const int64_t ppb = 256 / K;
+    hipLaunchKernelGGL(deftet_resolve_slots_kernel<T>, dim3((unsigned)cdiv(rows, ppb)), dim3(256), 0, st, F, P, (int)K,
+                       (int)D, idx, (const T *)depth, (const T *)w0, (const T *)w1, (const T *)feat, sidx,
+                       (T *)weights, (T *)interp, rows);
+  } else {
+    hipLaunchKernelGGL(deftet_resolve_kernel<T>, dim3((unsigned)cdiv(rows, 256)), dim3(256), 0, st, F, P, (int)K,
+                       (int)D, idx, (const T *)depth, (const T *)w0, (const T *)w1, (const T *)feat, sidx,
+                       (T *)weights, (T *)interp, rows);
+  }
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

@@ -227,3 +227,14 @@ def test_gpu_edge_cases(kal):
             fvz, fvi, torch.zeros((1, 1, 4), dtype=dt, device=DEV), pix, rr, 3, 1e-8)
     with pytest.raises(RuntimeError, match='CPU fallback|GPU tensors'):
         kal.render.mesh.deftet_sparse_render(pix.cpu(), rr.cpu(), fvz.cpu(), fvi.cpu(), feat.cpu(), 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('knum', [1, 7, 300])
+def test_gpu_knum_paths(kal, knum):
+    """knum <= 256 takes the slot-parallel resolve, the default 300 the per-pixel one; both vs oracle."""
+    pix, ranges, fvz, fvi, feat, _ = _grid_case(np.float32, B=1, F=600, H=12, W=10, seed=4)
+    interp, idx = kal.render.mesh.deftet_sparse_render(_T(pix), _T(ranges), _T(fvz), _T(fvi), _T(feat), knum)
+    r_interp, r_idx, _ = orc.deftet_sparse_render(pix, ranges, fvz, fvi, feat, knum)
+    np.testing.assert_array_equal(_A(idx), r_idx)
+    np.testing.assert_array_equal(_A(interp), r_interp)
