@@ -61,6 +61,30 @@ __device__ __forceinline__ void dt_face_bbox(const T *__restrict__ mi, const T *
   }
 }
 
+// bbox from the face's image coordinates already in registers (deftet.py:290-292)
+template <typename T>
+__device__ __forceinline__ void dt_face_bbox_regs(const T *v, T *bb) {
+  bb[0] = fmin(fmin(v[0], v[2]), v[4]);
+  bb[1] = fmin(fmin(v[1], v[3]), v[5]);
+  bb[2] = fmax(fmax(v[0], v[2]), v[4]);
+  bb[3] = fmax(fmax(v[1], v[3]), v[5]);
+}
+
+// raw loads of face f (image coords, z, and the given bboxes if any) into v[0..12]
+template <typename T>
+__device__ __forceinline__ void dt_load_face(const T *__restrict__ mi, const T *__restrict__ mz,
+                                             const T *__restrict__ mb, int64_t f, int64_t F, T *v) {
+  if (f >= F) return;
+#pragma unroll
+  for (int c = 0; c < 6; c++) v[c] = mi[f * 6 + c];
+#pragma unroll
+  for (int c = 0; c < 3; c++) v[6 + c] = mz[f * 3 + c];
+  if (mb) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) v[9 + c] = mb[f * 4 + c];
+  }
+}
+
 // Union bbox of each tile of kDtTile consecutive faces (grid (ntiles, B)): lets a workgroup
 // skip a whole tile, without loading it, when no face of it can reach its pixels.
 template <typename T>
@@ -167,21 +191,19 @@ __global__ void __launch_bounds__(kDtTile)
     const int tpos = block_exclusive_scan(tok ? 1 : 0, s_wave, &ntl);
     if (tok) s_tiles[tpos] = (int)tt;
     __syncthreads();
+    // The next tile's faces are loaded into registers before the current tile's walk, so the
+    // global latency overlaps the walk; the bbox min / max waits until the next iteration.
+    T v[13];
+    if (ntl > 0) dt_load_face(mi, mz, mb, (int64_t)s_tiles[0] * kDtTile + tid, F, v);
     for (int k = 0; k < ntl; k++) {
       if (!__syncthreads_or(active && n < K)) {  // every pixel of the workgroup is full
         full = true;
         break;
       }
-      const int64_t t0 = (int64_t)s_tiles[k] * kDtTile;
-      const int64_t f = t0 + tid;
-      T v[13];
+      const int64_t f = (int64_t)s_tiles[k] * kDtTile + tid;
       bool keep = false;
       if (f < F) {
-#pragma unroll
-        for (int c = 0; c < 6; c++) v[c] = mi[f * 6 + c];
-#pragma unroll
-        for (int c = 0; c < 3; c++) v[6 + c] = mz[f * 3 + c];
-        dt_face_bbox(mi, mb, f, v + 9);
+        if (!mb) dt_face_bbox_regs(v, v + 9);
         // some pixel x of the workgroup can satisfy xmin <= x < xmax (same for y)
         keep = v[9] <= gxmax && v[11] > gxmin && v[10] <= gymax && v[12] > gymin;
       }
@@ -193,6 +215,7 @@ __global__ void __launch_bounds__(kDtTile)
         s_id[pos] = (int)f;
       }
       __syncthreads();
+      if (k + 1 < ntl) dt_load_face(mi, mz, mb, (int64_t)s_tiles[k + 1] * kDtTile + tid, F, v);
       if (active && n < K) {
         for (int j = 0; j < total; j++) {
           const T xmin = s_f[9][j], ymin = s_f[10][j], xmax = s_f[11][j], ymax = s_f[12][j];
