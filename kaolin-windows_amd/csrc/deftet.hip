@@ -13,23 +13,21 @@
 // row; the other slots hold -1 / -inf / 0 / 0 (the reference's at::full / at::zeros).
 //
 // MI355X mapping: one lane per pixel (the reference spends a 32-lane warp per pixel and
-// ballots the insertion slot).  A workgroup owns 256 pixels of one mesh.  Faces stream
-// through LDS in tiles of 256; each tile is first culled against the workgroup's pixel bbox
-// with an order-preserving compaction (block scan), so the per-lane walk (LDS broadcast
-// reads, no bank conflicts) only visits faces that can touch one of its pixels.  For
-// image-grid pixels (DefTet's use) a workgroup covers a thin strip of the image and the walk
-// is a small fraction of F.  Each lane appends its own hits in mesh order: no ballots, no
-// atomics, every slot written once.
+// ballots the insertion slot).  A workgroup owns 256 pixels of one mesh.  A pre-pass writes
+// each 256-face tile's union bbox; a workgroup lists the tiles that can reach its pixel box in
+// one coalesced pass, streams only those through LDS, and culls each against its pixel box with
+// an order-preserving compaction (block scan), so the per-lane walk (LDS broadcast reads, no
+// bank conflicts) only visits faces that can touch one of its pixels.  Each lane appends its
+// own hits in mesh order: no ballots, no atomics, every slot written once.
 //
 // Resolve (deftet.py:294-306, the torch glue of the forward): per pixel the n hits are ranked
 // by depth, descending (stable: equal depths keep mesh order; the reference's argsort leaves
 // ties unspecified), and the sorted face ids, weights (w0, w1, w2 = 1 - (w0 + w1)) and the
-// interpolated features (w0 f0 + w1 f1) + w2 f2 are written in one pass.
+// interpolated features (w0 f0 + w1 f1) + w2 f2 are written, one lane per output slot.
 //
-// Backward (deftet_cuda.cu:240-420): one lane per (pixel, slot) item that holds a face; the
-// reference's k1/k2/k3 derivative form term by term; hardware float atomics into the
-// per-face gradients (unordered, like the reference's atomicAdd).  The six vertex-gradient
-// terms are summed over the feature dimension in registers first (D times fewer atomics).
+// Backward (deftet_cuda.cu:240-420): the (pixel, slot) items are radix-sorted by face (stable)
+// and one lane per face sums its items in item order with the reference's k1/k2/k3 derivative
+// terms: deterministic, no atomics.  Without a workspace the reference's float atomics are used.
 #include <cmath>
 
 #include <hipcub/hipcub.hpp>
