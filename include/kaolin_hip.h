@@ -230,14 +230,18 @@ int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height, int width,
  * pixel_coords (B,P,2), pixel_depth_ranges (B,P,2) [lo, hi).  dtype KL_F32 | KL_F64.
  * Outputs (B,P,K), fully written: face_idx int64 (first K hits in mesh order, then -1),
  * pixel_depths (-inf pad), w0, w1 (0 pad).  workspace: kl_deftet_workspace_bytes(B, F) bytes
- * (per-tile face bboxes, no initialisation needed). */
+ * (no initialisation needed).  With `alloc` the faces are binned into a screen grid of
+ * mesh-ordered lists (their length is read back: one 8-byte device-to-host copy and a stream
+ * synchronisation; the lists come from `alloc`); with NULL each workgroup walks the face tiles
+ * that reach its pixels.  Both give the same outputs. */
 size_t kl_deftet_workspace_bytes(int64_t batch_size, int64_t num_faces);
 int kl_deftet_sparse_render_forward(kl_dtype dtype, int64_t batch_size, int64_t num_faces, int64_t num_pixels,
                                     int64_t knum, const void *face_vertices_z, const void *face_vertices_image,
                                     const void *face_bboxes, const void *pixel_coords,
                                     const void *pixel_depth_ranges, float eps, int64_t *face_idx,
                                     void *pixel_depths, void *w0, void *w1, void *workspace,
-                                    size_t workspace_bytes, kl_stream stream);
+                                    size_t workspace_bytes, kl_alloc_fn alloc, void *alloc_ctx,
+                                    kl_stream stream);
 
 /* deftet.py:294-306 (the torch glue of DeftetSparseRenderer.forward) in one pass: per pixel the
  * hits of kl_deftet_sparse_render_forward ranked by depth, descending (stable), then

@@ -38,6 +38,7 @@ namespace kl {
 
 constexpr int kDtTile = 256;  // pixels per workgroup == faces per LDS tile
 constexpr int kDtRegD = 8;    // feature widths the gather backward keeps in registers
+constexpr int kDtStageK = 8;  // knum up to which the binned forward stages its hits in LDS
 
 template <typename T>
 __device__ __forceinline__ T dt_copysign_eps_f(float eps, T v) {
@@ -249,6 +250,202 @@ __global__ void __launch_bounds__(kDtTile)
       row_w0[k] = 0;
       row_w1[k] = 0;
     }
+  }
+}
+
+// ---- binned forward: a screen grid of face lists in mesh order --------------------------------
+// The faces are listed in every cell of a G x G grid over the mesh's screen box that their bbox
+// overlaps; a stable radix sort by cell keeps each list in mesh order.  The cell of a value is
+// one monotone float expression for faces and pixels, so every face that can pass a pixel's
+// [min, max) bbox test is in the pixel's list, and walking the list in order finds the same
+// first-knum hits as walking all faces.
+
+// mesh screen box (T) and cell scales (float; 0 for an empty or infinite extent), one
+// workgroup per mesh, from the per-tile boxes
+template <typename T>
+__global__ void __launch_bounds__(256)
+    deftet_meshbox_kernel(int64_t ntiles, int G, const T *__restrict__ tbox, T *__restrict__ mbox,
+                          float *__restrict__ mscale) {
+  __shared__ T s_r[4][4];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  T r0 = INFINITY, r1 = INFINITY, r2 = -INFINITY, r3 = -INFINITY;
+  for (int64_t t = tid; t < ntiles; t += 256) {
+    const T *tb = tbox + (b * ntiles + t) * 4;
+    r0 = fmin(r0, tb[0]); r1 = fmin(r1, tb[1]); r2 = fmax(r2, tb[2]); r3 = fmax(r3, tb[3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    r0 = fmin(r0, (T)__shfl_xor(r0, o));
+    r1 = fmin(r1, (T)__shfl_xor(r1, o));
+    r2 = fmax(r2, (T)__shfl_xor(r2, o));
+    r3 = fmax(r3, (T)__shfl_xor(r3, o));
+  }
+  if ((tid & 63) == 0) {
+    s_r[0][tid >> 6] = r0; s_r[1][tid >> 6] = r1; s_r[2][tid >> 6] = r2; s_r[3][tid >> 6] = r3;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; w++) {
+      r0 = fmin(r0, s_r[0][w]); r1 = fmin(r1, s_r[1][w]); r2 = fmax(r2, s_r[2][w]); r3 = fmax(r3, s_r[3][w]);
+    }
+    T *o = mbox + b * 4;
+    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = r3;
+    const float ex = (float)r2 - (float)r0, ey = (float)r3 - (float)r1;
+    mscale[b * 4 + 0] = (float)r0;
+    mscale[b * 4 + 1] = (float)r1;
+    mscale[b * 4 + 2] = (ex > 0.f && ex < INFINITY) ? (float)G / ex : 0.f;
+    mscale[b * 4 + 3] = (ey > 0.f && ey < INFINITY) ? (float)G / ey : 0.f;
+  }
+}
+
+// monotone cell coordinate of v in [0, G)
+template <typename T>
+__device__ __forceinline__ int dt_cell(T v, float v0, float inv, int G) {
+  const float c = fminf(fmaxf(((float)v - v0) * inv, 0.f), (float)(G - 1));
+  return (int)c;
+}
+
+// cells covered by face f's bbox (0 when it has a NaN bound: it never passes the bbox test)
+template <typename T>
+__device__ __forceinline__ int dt_face_cells(const T *bb, const float *ms, int G, int &cx0, int &cy0, int &nx) {
+  if (!(bb[0] <= bb[2] && bb[1] <= bb[3])) return 0;
+  cx0 = dt_cell(bb[0], ms[0], ms[2], G);
+  cy0 = dt_cell(bb[1], ms[1], ms[3], G);
+  const int cx1 = dt_cell(bb[2], ms[0], ms[2], G), cy1 = dt_cell(bb[3], ms[1], ms[3], G);
+  nx = cx1 - cx0 + 1;
+  return nx * (cy1 - cy0 + 1);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+    deftet_bin_count_kernel(int64_t F, int G, const T *__restrict__ fvi, const T *__restrict__ bboxes,
+                            const float *__restrict__ mscale, int *__restrict__ fcnt) {
+  const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (f >= F) return;
+  T bb[4];
+  dt_face_bbox(fvi + b * F * 6, bboxes ? bboxes + b * F * 4 : nullptr, f, bb);
+  int cx0, cy0, nx;
+  fcnt[b * F + f] = dt_face_cells(bb, mscale + b * 4, G, cx0, cy0, nx);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+    deftet_bin_fill_kernel(int64_t F, int G, const T *__restrict__ fvi, const T *__restrict__ bboxes,
+                           const float *__restrict__ mscale, const int *__restrict__ foff, uint32_t *__restrict__ keys,
+                           int32_t *__restrict__ vals, int *__restrict__ ccnt) {
+  const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (f >= F) return;
+  T bb[4];
+  dt_face_bbox(fvi + b * F * 6, bboxes ? bboxes + b * F * 4 : nullptr, f, bb);
+  int cx0, cy0, nx;
+  const int n = dt_face_cells(bb, mscale + b * 4, G, cx0, cy0, nx);
+  int64_t o = foff[b * F + f];
+  const uint32_t kb = (uint32_t)(b * G * G);
+  for (int i = 0; i < n; i++) {
+    const uint32_t cell = (uint32_t)((cy0 + i / nx) * G + (cx0 + i % nx));
+    keys[o + i] = kb + cell;
+    vals[o + i] = (int32_t)f;
+    atomicAdd(ccnt + kb + cell, 1);
+  }
+}
+
+// one lane per pixel: walk the pixel's cell list (mesh order) with the reference's test.
+// STAGE (knum <= kDtStageK): the hits go to LDS rows and the workgroup writes each output array
+// as one contiguous range (coalesced) instead of per-lane strided stores.
+template <typename T, bool STAGE>
+__global__ void __launch_bounds__(256)
+    deftet_fwd_binned_kernel(int64_t F, int64_t P, int K, int G, const T *__restrict__ fvz, const T *__restrict__ fvi,
+                             const T *__restrict__ bboxes, const T *__restrict__ pix, const T *__restrict__ ranges,
+                             float eps, const T *__restrict__ mbox, const float *__restrict__ mscale,
+                             const int *__restrict__ coff, const int *__restrict__ ccnt, const int32_t *__restrict__ list,
+                             int64_t *__restrict__ out_idx, T *__restrict__ out_depth, T *__restrict__ out_w0,
+                             T *__restrict__ out_w1) {
+  __shared__ int s_hid[STAGE ? 256 * kDtStageK : 1];
+  __shared__ T s_hd[STAGE ? 256 * kDtStageK : 1], s_hw0[STAGE ? 256 * kDtStageK : 1], s_hw1[STAGE ? 256 * kDtStageK : 1];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y, p = (int64_t)blockIdx.x * 256 + tid;
+  if (!STAGE && p >= P) return;
+  const bool active = p < P;
+  const int64_t prow = b * P + (active ? p : 0);
+  T x0 = 0, y0 = 0, lo = 0, hi = 0;
+  if (active) {
+    x0 = pix[prow * 2 + 0]; y0 = pix[prow * 2 + 1];
+    lo = ranges[prow * 2 + 0]; hi = ranges[prow * 2 + 1];
+  }
+  int64_t *row_idx = out_idx + prow * K;
+  T *row_d = out_depth + prow * K;
+  T *row_w0 = out_w0 + prow * K;
+  T *row_w1 = out_w1 + prow * K;
+  int n = 0;
+  const T *mb = mbox + b * 4;
+  // outside the union of the face bboxes no face's [min, max) test can pass
+  if (active && x0 >= mb[0] && x0 < mb[2] && y0 >= mb[1] && y0 < mb[3]) {
+    const float *ms = mscale + b * 4;
+    const int64_t cell = b * (int64_t)G * G + (int64_t)dt_cell(y0, ms[1], ms[3], G) * G + dt_cell(x0, ms[0], ms[2], G);
+    const int c0 = coff[cell], cn = ccnt[cell];
+    const T *mi = fvi + b * F * 6;
+    const T *mz = fvz + b * F * 3;
+    const T *mbb = bboxes ? bboxes + b * F * 4 : nullptr;
+    for (int e = 0; e < cn; e++) {
+      const int64_t f = list[c0 + e];
+      T bb[4];
+      dt_face_bbox(mi, mbb, f, bb);
+      if (!(x0 >= bb[0] && x0 < bb[2] && y0 >= bb[1] && y0 < bb[3])) continue;
+      const T *v = mi + f * 6;
+      const T aex = v[0] - x0, aey = v[1] - y0;
+      const T bex = v[2] - x0, bey = v[3] - y0;
+      const T cex = v[4] - x0, cey = v[5] - y0;
+      const T _w0 = bex * cey - bey * cex;
+      const T _w1 = cex * aey - cey * aex;
+      const T _w2 = aex * bey - aey * bex;
+      const T norm = _w0 + _w1 + _w2;
+      const T den = norm + dt_copysign_eps_f(eps, norm);
+      const T w0 = _w0 / den, w1 = _w1 / den, w2 = _w2 / den;
+      if (w0 >= (T)0 && w1 >= (T)0 && w2 >= (T)0) {
+        const T d = w0 * mz[f * 3 + 0] + w1 * mz[f * 3 + 1] + w2 * mz[f * 3 + 2];
+        if (d < hi && d >= lo) {
+          if constexpr (STAGE) {
+            s_hid[tid * K + n] = (int)f;
+            s_hd[tid * K + n] = d;
+            s_hw0[tid * K + n] = w0;
+            s_hw1[tid * K + n] = w1;
+          } else {
+            row_idx[n] = f;
+            row_d[n] = d;
+            row_w0[n] = w0;
+            row_w1[n] = w1;
+          }
+          if (++n == K) break;
+        }
+      }
+    }
+  }
+  if constexpr (STAGE) {
+    for (int k = n; k < K; k++) {
+      s_hid[tid * K + k] = -1;
+      s_hd[tid * K + k] = -INFINITY;
+      s_hw0[tid * K + k] = 0;
+      s_hw1[tid * K + k] = 0;
+    }
+    __syncthreads();
+    const int64_t r0 = b * P + (int64_t)blockIdx.x * 256;
+    const int64_t nrows = min((int64_t)256, P - (int64_t)blockIdx.x * 256);
+    const int cnt = (int)(nrows * K);
+    for (int e = tid; e < cnt; e += 256) {
+      const int64_t o = r0 * K + e;
+      out_idx[o] = (int64_t)s_hid[e];
+      out_depth[o] = s_hd[e];
+      out_w0[o] = s_hw0[e];
+      out_w1[o] = s_hw1[e];
+    }
+    return;
+  }
+  for (int k = n; k < K; k++) {
+    row_idx[k] = -1;
+    row_d[k] = -INFINITY;
+    row_w0[k] = 0;
+    row_w1[k] = 0;
   }
 }
 
@@ -551,17 +748,120 @@ static int dt_key_bits(int64_t BF) {  // bits of the largest key (BF, the empty-
   return bits;
 }
 
+static size_t dt_falign(size_t x) { return (x + 255) & ~(size_t)255; }
+static int dt_grid_dim(int64_t F) {  // ~4 faces per cell per layer
+  int G = 1;
+  while (G < 1024 && (int64_t)(G + 1) * (G + 1) * 4 <= F) G++;
+  return G;
+}
+// forward workspace: tile boxes, then (binned path) mesh boxes, per-face counts / offsets,
+// per-cell counts / offsets and the scan scratch
+struct DtFwdWs {
+  size_t tbox, mbox, mscale, fcnt, foff, ccnt, coff, temp, temp_bytes, total;
+  int G;
+};
+static DtFwdWs dt_fwd_layout(int64_t B, int64_t F, size_t tsize) {
+  DtFwdWs w{};
+  w.G = dt_grid_dim(F);
+  const int64_t cells = B * (int64_t)w.G * w.G;
+  size_t t1 = 0, t2 = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, (const int *)nullptr, (int *)nullptr, (int)(B * F > 0 ? B * F : 1));
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (const int *)nullptr, (int *)nullptr, (int)cells);
+  size_t o = 0;
+  w.tbox = o; o += dt_falign((size_t)(B * cdiv(F, kDtTile)) * 4 * tsize);
+  w.mbox = o; o += dt_falign((size_t)B * 4 * tsize);
+  w.mscale = o; o += dt_falign((size_t)B * 16);
+  w.fcnt = o; o += dt_falign((size_t)(B * F) * 4);
+  w.foff = o; o += dt_falign((size_t)(B * F) * 4);
+  w.ccnt = o; o += dt_falign((size_t)cells * 4);
+  w.coff = o; o += dt_falign((size_t)cells * 4);
+  w.temp = o; w.temp_bytes = dt_falign(t1 > t2 ? t1 : (t2 > 0 ? t2 : 1)); o += w.temp_bytes;
+  w.total = o;
+  return w;
+}
+
+template <typename T>
+static int deftet_forward_binned(int64_t B, int64_t F, int64_t P, int64_t K, const void *fvz, const void *fvi,
+                                 const void *bboxes, const void *pix, const void *ranges, float eps, int64_t *idx,
+                                 void *depth, void *w0, void *w1, const DtFwdWs &L, uint8_t *w, kl_alloc_fn alloc,
+                                 void *alloc_ctx, hipStream_t st) {
+  const int G = L.G;
+  const int64_t cells = B * (int64_t)G * G, BF = B * F, ntiles = cdiv(F, kDtTile);
+  T *tbox = (T *)(w + L.tbox), *mbox = (T *)(w + L.mbox);
+  float *mscale = (float *)(w + L.mscale);
+  int *fcnt = (int *)(w + L.fcnt), *foff = (int *)(w + L.foff), *ccnt = (int *)(w + L.ccnt), *coff = (int *)(w + L.coff);
+  hipLaunchKernelGGL(deftet_meshbox_kernel<T>, dim3((unsigned)B), dim3(256), 0, st, ntiles, G, (const T *)tbox, mbox,
+                     mscale);
+  KL_CHECK_LAUNCH();
+  const dim3 fgrid((unsigned)cdiv(F, 256), (unsigned)B);
+  hipLaunchKernelGGL(deftet_bin_count_kernel<T>, fgrid, dim3(256), 0, st, F, G, (const T *)fvi, (const T *)bboxes,
+                     (const float *)mscale, fcnt);
+  KL_CHECK_LAUNCH();
+  size_t tb = L.temp_bytes;
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, fcnt, foff, (int)BF, st));
+  int last[2] = {0, 0};
+  KL_CHECK_HIP(hipMemcpyAsync(&last[0], foff + BF - 1, 4, hipMemcpyDeviceToHost, st));
+  KL_CHECK_HIP(hipMemcpyAsync(&last[1], fcnt + BF - 1, 4, hipMemcpyDeviceToHost, st));
+  KL_CHECK_HIP(hipStreamSynchronize(st));
+  const int64_t total = (int64_t)last[0] + last[1];
+  KL_REQUIRE(total >= 0 && total < ((int64_t)1 << 31), "deftet_sparse_render_forward: face lists too long");
+  const int64_t ne = total > 0 ? total : 1;
+  size_t ts = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, ts, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (const int32_t *)nullptr, (int32_t *)nullptr, (int)ne);
+  uint8_t *lw = (uint8_t *)alloc(alloc_ctx, dt_falign((size_t)ne * 4) * 4 + dt_falign(ts > 0 ? ts : 1));
+  if (!lw) {
+    set_error("deftet_sparse_render_forward: allocator returned NULL");
+    return KL_E_ALLOC;
+  }
+  uint32_t *kin = (uint32_t *)lw, *kout = (uint32_t *)(lw + dt_falign((size_t)ne * 4));
+  int32_t *vin = (int32_t *)(lw + 2 * dt_falign((size_t)ne * 4)), *vout = (int32_t *)(lw + 3 * dt_falign((size_t)ne * 4));
+  KL_CHECK_RC(fill_async(ccnt, 0, (size_t)cells * 4, st));
+  hipLaunchKernelGGL(deftet_bin_fill_kernel<T>, fgrid, dim3(256), 0, st, F, G, (const T *)fvi, (const T *)bboxes,
+                     (const float *)mscale, (const int *)foff, kin, vin, ccnt);
+  KL_CHECK_LAUNCH();
+  int bits = 1;
+  while (bits < 32 && ((int64_t)1 << bits) < cells) bits++;
+  if (total > 0) {
+    ts = ts > 0 ? ts : 1;
+    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(lw + 4 * dt_falign((size_t)ne * 4), ts, kin, kout, vin, vout,
+                                                    (int)total, 0, bits, st));
+  }
+  tb = L.temp_bytes;
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, ccnt, coff, (int)cells, st));
+  const dim3 pgrid((unsigned)cdiv(P, 256), (unsigned)B);
+  if (K <= kDtStageK)
+    hipLaunchKernelGGL((deftet_fwd_binned_kernel<T, true>), pgrid, dim3(256), 0, st, F, P, (int)K, G, (const T *)fvz,
+                       (const T *)fvi, (const T *)bboxes, (const T *)pix, (const T *)ranges, eps, (const T *)mbox,
+                       (const float *)mscale, (const int *)coff, (const int *)ccnt, (const int32_t *)vout, idx,
+                       (T *)depth, (T *)w0, (T *)w1);
+  else
+    hipLaunchKernelGGL((deftet_fwd_binned_kernel<T, false>), pgrid, dim3(256), 0, st, F, P, (int)K, G, (const T *)fvz,
+                       (const T *)fvi, (const T *)bboxes, (const T *)pix, (const T *)ranges, eps, (const T *)mbox,
+                       (const float *)mscale, (const int *)coff, (const int *)ccnt, (const int32_t *)vout, idx,
+                       (T *)depth, (T *)w0, (T *)w1);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
 template <typename T>
 static int deftet_forward(int64_t B, int64_t F, int64_t P, int64_t K, const void *fvz, const void *fvi,
                           const void *bboxes, const void *pix, const void *ranges, float eps, int64_t *idx, void *depth,
-                          void *w0, void *w1, void *ws, size_t ws_bytes, hipStream_t st) {
+                          void *w0, void *w1, void *ws, size_t ws_bytes, kl_alloc_fn alloc, void *alloc_ctx,
+                          hipStream_t st) {
   const int64_t ntiles = cdiv(F, kDtTile);
-  KL_REQUIRE(ws_bytes >= (size_t)(B * ntiles * 4) * sizeof(T), "deftet_sparse_render_forward: workspace too small");
+  const DtFwdWs L = dt_fwd_layout(B, F, sizeof(T));
+  KL_REQUIRE(ws && ws_bytes >= (size_t)(B * ntiles * 4) * sizeof(T),
+             "deftet_sparse_render_forward: workspace too small");
   if (ntiles > 0) {
     hipLaunchKernelGGL(deftet_tilebox_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kDtTile), 0, st, F,
-                       (const T *)fvi, (const T *)bboxes, (T *)ws);
+                       (const T *)fvi, (const T *)bboxes, (T *)((uint8_t *)ws + L.tbox));
     KL_CHECK_LAUNCH();
   }
+  if (alloc && F > 0 && ws_bytes >= L.total && B * F < ((int64_t)1 << 31) &&
+      B * (int64_t)L.G * L.G < ((int64_t)1 << 31))
+    return deftet_forward_binned<T>(B, F, P, K, fvz, fvi, bboxes, pix, ranges, eps, idx, depth, w0, w1, L,
+                                    (uint8_t *)ws, alloc, alloc_ctx, st);
   hipLaunchKernelGGL(deftet_fwd_kernel<T>, dim3((unsigned)cdiv(P, kDtTile), (unsigned)B), dim3(kDtTile), 0, st, F, P,
                      (int)K, (const T *)fvz, (const T *)fvi, (const T *)bboxes, (const T *)pix, (const T *)ranges, eps,
                      idx, (T *)depth, (T *)w0, (T *)w1, (const T *)ws);
@@ -651,16 +951,17 @@ extern "C" int kl_deftet_sparse_render_forward(kl_dtype dtype, int64_t batch_siz
                                                const void *face_vertices_image, const void *face_bboxes,
                                                const void *pixel_coords, const void *pixel_depth_ranges, float eps,
                                                int64_t *face_idx, void *pixel_depths, void *w0, void *w1,
-                                               void *workspace, size_t workspace_bytes, kl_stream stream) {
+                                               void *workspace, size_t workspace_bytes, kl_alloc_fn alloc,
+                                               void *alloc_ctx, kl_stream stream) {
   KL_CHECK_RC(check_deftet_sizes(batch_size, num_faces, num_pixels, knum, 0));
   if (batch_size == 0 || num_pixels == 0 || knum == 0) return KL_OK;
   KL_DT_DISPATCH(dtype, deftet_forward, batch_size, num_faces, num_pixels, knum, face_vertices_z, face_vertices_image,
                  face_bboxes, pixel_coords, pixel_depth_ranges, eps, face_idx, pixel_depths, w0, w1, workspace,
-                 workspace_bytes, S(stream));
+                 workspace_bytes, alloc, alloc_ctx, S(stream));
 }
 
 extern "C" size_t kl_deftet_workspace_bytes(int64_t batch_size, int64_t num_faces) {
-  return (size_t)(batch_size * cdiv(num_faces, kDtTile) * 4) * sizeof(double) + 16;
+  return dt_fwd_layout(batch_size, num_faces, sizeof(double)).total;
 }
 
 extern "C" int kl_deftet_sparse_render_resolve(kl_dtype dtype, int64_t batch_size, int64_t num_faces,

@@ -188,9 +188,11 @@ def deftet_sparse_render_forward_cuda(face_vertices_z, face_vertices_image, face
                           knum, eps)
 
 
-def deftet_forward(func, fvz, fvi, bboxes, pix, ranges, knum, eps):
+def deftet_forward(func, fvz, fvi, bboxes, pix, ranges, knum, eps, binned=False):
     """The forward kernel on checked, contiguous inputs; ``bboxes`` may be None (computed in-kernel
-    with the same min / max as deftet.py:290-292)."""
+    with the same min / max as deftet.py:290-292).  ``binned`` selects the screen-grid path
+    (faster kernel, but one host synchronisation to size the lists); the default tile walk needs
+    none and is faster end to end at the bench sizes.  Same outputs."""
     B, F = fvz.shape[:2]
     P = pix.shape[1]
     K = int(knum)
@@ -202,10 +204,13 @@ def deftet_forward(func, fvz, fvi, bboxes, pix, ranges, knum, eps):
     lib = N.lib()
     ws_bytes = lib.kl_deftet_workspace_bytes(B, F)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    arena = N.Arena(dev)
+    alloc = arena.fn if binned else N.ALLOC_FN()
     with torch.cuda.device(dev), N.timed(func, dev):
         N.check(lib.kl_deftet_sparse_render_forward(
             N.dtype_code(dtype), B, F, P, K, N.ptr(fvz), N.ptr(fvi), N.ptr(bboxes), N.ptr(pix), N.ptr(ranges),
-            float(eps), N.ptr(idx), N.ptr(depth), N.ptr(w0), N.ptr(w1), N.ptr(ws), ws_bytes, N.stream_of(dev)), func)
+            float(eps), N.ptr(idx), N.ptr(depth), N.ptr(w0), N.ptr(w1), N.ptr(ws), ws_bytes, alloc, None,
+            N.stream_of(dev)), func)
     return [idx, depth, w0, w1]
 
 

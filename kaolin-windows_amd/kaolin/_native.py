@@ -86,7 +86,7 @@ _SIGS = {
     'kl_sum_reduce': (_I, [_I, _I64, _I64, _P, _P, _I64, _P, _P]),
     'kl_deftet_workspace_bytes': (_SZ, [_I64, _I64]),
     'kl_deftet_sparse_render_forward': (_I, [_I, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P,
-                                             _P, _SZ, _P]),
+                                             _P, _SZ, ALLOC_FN, _P, _P]),
     'kl_deftet_sparse_render_resolve': (_I, [_I, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P,
                                              _P]),
     'kl_deftet_bwd_workspace_bytes': (_SZ, [_I64, _I64, _I64, _I64]),

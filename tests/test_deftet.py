@@ -238,3 +238,22 @@ def test_gpu_knum_paths(kal, knum):
     r_interp, r_idx, _ = orc.deftet_sparse_render(pix, ranges, fvz, fvi, feat, knum)
     np.testing.assert_array_equal(_A(idx), r_idx)
     np.testing.assert_array_equal(_A(interp), r_interp)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [np.float32, np.float64])
+def test_gpu_binned_and_tile_forward_agree(kal, dtype):
+    """The screen-grid forward (with an allocator) and the tile-walk forward (without) give the
+    same slots, both equal to the oracle; includes NaN / inf faces and pixels off the mesh."""
+    pix, ranges, fvz, fvi, feat, K = _grid_case(dtype, B=2, F=2500, H=30, W=26, seed=9)
+    fvi = fvi.copy()
+    fvi[0, 5, 1, 0] = np.nan
+    fvi[1, 7, 2, 1] = np.inf
+    pix = pix * dtype(1.3)  # some pixels outside every face's bbox
+    args = [_T(fvz), _T(fvi), None, _T(pix), _T(ranges), K, 1e-8]
+    a = kal._C.deftet_forward('deftet', *args, binned=True)
+    b = kal._C.deftet_forward('deftet', *args, binned=False)
+    ref = orc.deftet_sparse_render_forward(fvz, fvi, None, pix, ranges, K, 1e-8)
+    for x, y, r in zip(a, b, ref):
+        np.testing.assert_array_equal(_A(x), _A(y))
+        np.testing.assert_array_equal(_A(x), r)
