@@ -370,6 +370,11 @@ def deftet_sparse_render_forward(fvz, fvi, bboxes, pix, ranges, knum, eps=1e-8):
     """deftet_sparse_render_forward_cuda (deftet.cpp:49-111): the first knum hits in MESH order.
     bboxes may be None (min / max over the vertices, deftet.py:290-292).
     Returns face_idx (B,P,K) int64 (-1 pad), depth (-inf pad), w0, w1 (0 pad)."""
+    with np.errstate(invalid='ignore', divide='ignore'):  # NaN / inf faces give NaN weights, as on the GPU
+        return _deftet_sparse_render_forward(fvz, fvi, bboxes, pix, ranges, knum, eps)
+
+
+def _deftet_sparse_render_forward(fvz, fvi, bboxes, pix, ranges, knum, eps):
     dt = fvz.dtype
     B, F = fvz.shape[:2]
     P = pix.shape[1]
