@@ -375,9 +375,11 @@ int kl_sum_reduce(kl_dtype dtype, int64_t num_feats, int64_t feat_dim, const voi
 /* mesh_intersection.cpp:33-68  unbatched_mesh_intersection_cuda (kernel
  * mesh_intersection_cuda.cu:100-210).  points (P,3), verts_1/2/3 (F,3) face corners, dtype
  * KL_F32 | KL_F64 -> result (P) in the same dtype: the number of faces the ray from each point
- * toward +x crosses (edge / vertex hits counted once).  Fully written. */
+ * toward +x crosses (edge / vertex hits counted once).  Fully written.  workspace:
+ * kl_check_sign_workspace_bytes(dtype, 1, F, P) bytes; `alloc` as for kl_check_sign below. */
 int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points, int64_t num_faces, const void *points,
                                    const void *verts_1, const void *verts_2, const void *verts_3, void *result,
+                                   void *workspace, size_t workspace_bytes, kl_alloc_fn alloc, void *alloc_ctx,
                                    kl_stream stream);
 
 /* check_sign (ops/mesh/check_sign.py:25-154) for a batch: verts (B,V,3), faces (F,3) int64,

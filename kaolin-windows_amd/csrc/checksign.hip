@@ -20,8 +20,8 @@
 //   visited in the Morton order of their (y, z) so that a wave's lanes share cells.  Face
 //   corners are gathered from (vertices, faces) once, with check_sign's 1 / maxlen
 //   normalisation applied on load (the IEEE division the reference does in torch).
-// * Unbatched _C entry: faces stream through LDS in tiles of 256, compacted per tile against
-//   the workgroup's (y, z) point box, and lanes walk them with LDS broadcast reads.
+// * Unbatched _C entry (unbatched_mesh_intersection_cuda): the same grid path on the given
+//   corner arrays, writing the crossing counts.
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -155,126 +155,6 @@ __global__ void __launch_bounds__(256)
   vals[i] = (int32_t)(i % P);  // point index within its mesh
 }
 
-// grid (cdiv(P, 256), B); counts (B,P) in T (the _C contract) and/or contains (B,P) bool.
-// perm (B,P) int32 or null: lane i of the batch handles point perm[i].
-// tbox (B, ntiles, 4) float or null.
-template <typename T>
-__global__ void __launch_bounds__(kCsTile)
-    check_sign_kernel(int64_t P, int64_t F, const T *__restrict__ points, CsFaces<T> src, T *__restrict__ counts,
-                      uint8_t *__restrict__ contains, const int32_t *__restrict__ perm,
-                      const float *__restrict__ tbox) {
-  __shared__ T s_v[9][kCsTile];
-  __shared__ float s_bb[4][kCsTile];
-  __shared__ int s_tiles[kCsTile];
-  __shared__ int s_wave[16];
-  __shared__ T s_box[4][kCsTile / 64];
-
-  const int tid = threadIdx.x;
-  const int64_t b = blockIdx.y;
-  const int64_t i = (int64_t)blockIdx.x * kCsTile + tid;
-  const bool active = i < P;
-  const int64_t p = (active && perm) ? (int64_t)perm[b * P + i] : i;
-  const int64_t row = b * P + p;
-  T qx = 0, qy = 0, qz = 0;
-  if (active) {
-    const T *q = points + row * 3;
-    qx = q[0]; qy = q[1]; qz = q[2];
-    if (src.maxlen) {  // check_sign.py:146: points / maxlen
-      const T m = src.maxlen[b];
-      qx = qx / m; qy = qy / m; qz = qz / m;
-    }
-  }
-  {
-    T ymn = INFINITY, zmn = INFINITY, ymx = -INFINITY, zmx = -INFINITY;
-    if (active && qy == qy && qz == qz) {
-      ymn = qy; ymx = qy; zmn = qz; zmx = qz;
-    }
-    ymn = wave_min(ymn); zmn = wave_min(zmn);
-    ymx = wave_max(ymx); zmx = wave_max(zmx);
-    if ((tid & 63) == 0) {
-      s_box[0][tid >> 6] = ymn; s_box[1][tid >> 6] = ymx;
-      s_box[2][tid >> 6] = zmn; s_box[3][tid >> 6] = zmx;
-    }
-  }
-  __syncthreads();
-  T gymn = s_box[0][0], gymx = s_box[1][0], gzmn = s_box[2][0], gzmx = s_box[3][0];
-#pragma unroll
-  for (int w = 1; w < kCsTile / 64; w++) {
-    gymn = s_box[0][w] < gymn ? s_box[0][w] : gymn;
-    gymx = s_box[1][w] > gymx ? s_box[1][w] : gymx;
-    gzmn = s_box[2][w] < gzmn ? s_box[2][w] : gzmn;
-    gzmx = s_box[3][w] > gzmx ? s_box[3][w] : gzmx;
-  }
-
-  int count = 0;
-  // Tiles whose union (y, z) bounds reach the workgroup's points, listed 256 tile ids at a
-  // time with one coalesced pass over the tile boxes (all tiles when there are no boxes).
-  const int64_t ntiles = (F + kCsTile - 1) / kCsTile;
-  for (int64_t tc = 0; tc < ntiles; tc += kCsTile) {
-    const int64_t tt = tc + tid;
-    bool tok = tt < ntiles;
-    if (tok && tbox) {
-      const float *tb = tbox + (b * ntiles + tt) * 4;
-      tok = (T)tb[0] <= gymx && (T)tb[1] >= gymn && (T)tb[2] <= gzmx && (T)tb[3] >= gzmn;
-    }
-    int ntl;
-    const int tpos = block_exclusive_scan(tok ? 1 : 0, s_wave, &ntl);
-    if (tok) s_tiles[tpos] = (int)tt;
-    __syncthreads();
-    for (int kt = 0; kt < ntl; kt++) {
-      const int64_t t0 = (int64_t)s_tiles[kt] * kCsTile;
-      const int64_t f = t0 + tid;
-      T v[9];
-      float bb[4];
-      bool keep = false;
-      if (f < F) {
-        cs_load_face(src, b, f, v);
-        // float y_min = min(b.y, min(c.y, d.y)) etc. (:47-50)
-        bb[0] = (float)fmin(v[1], fmin(v[4], v[7]));
-        bb[1] = (float)fmax(v[1], fmax(v[4], v[7]));
-        bb[2] = (float)fmin(v[2], fmin(v[5], v[8]));
-        bb[3] = (float)fmax(v[2], fmax(v[5], v[8]));
-        // some point of the workgroup can pass bbox_check (NaN bounds never pass it)
-        keep = (T)bb[0] <= gymx && (T)bb[1] >= gymn && (T)bb[2] <= gzmx && (T)bb[3] >= gzmn;
-      }
-      int total;
-      const int pos = block_exclusive_scan(keep ? 1 : 0, s_wave, &total);
-      if (keep) {
-#pragma unroll
-        for (int k = 0; k < 9; k++) s_v[k][pos] = v[k];
-#pragma unroll
-        for (int k = 0; k < 4; k++) s_bb[k][pos] = bb[k];
-      }
-      __syncthreads();
-      if (active) {
-        for (int j = 0; j < total; j++) {
-          const T p1[3] = {s_v[0][j], s_v[1][j], s_v[2][j]};
-          const T p2[3] = {s_v[3][j], s_v[4][j], s_v[5][j]};
-          const T p3[3] = {s_v[6][j], s_v[7][j], s_v[8][j]};
-          const float bbj[4] = {s_bb[0][j], s_bb[1][j], s_bb[2][j], s_bb[3][j]};
-          count += cs_cross(qx, qy, qz, p1, p2, p3, bbj);
-        }
-      }
-      __syncthreads();
-    }
-    __syncthreads();  // s_tiles is rewritten by the next chunk
-  }
-  if (active) {
-    if (counts) counts[row] = (T)count;
-    if (contains) contains[row] = (uint8_t)(count & 1);
-  }
-}
-
-template <typename T>
-static int check_sign_launch(int64_t B, int64_t P, int64_t F, const void *points, const CsFaces<T> &src, void *counts,
-                             uint8_t *contains, const int32_t *perm, const float *tbox, hipStream_t st) {
-  if (B == 0 || P == 0) return KL_OK;
-  hipLaunchKernelGGL(check_sign_kernel<T>, dim3((unsigned)cdiv(P, kCsTile), (unsigned)B), dim3(kCsTile), 0, st, P, F,
-                     (const T *)points, src, (T *)counts, contains, perm, tbox);
-  KL_CHECK_LAUNCH();
-  return KL_OK;
-}
-
 // ---- batched entry: a (y, z) grid of face lists ------------------------------------------
 // A ray toward +x can only cross faces whose (y, z) bounds hold the point, so the mesh's (y, z)
 // box is cut into G x G cells and every face is listed in the cells its float bounds overlap.
@@ -392,7 +272,7 @@ __global__ void __launch_bounds__(256)
     cs_grid_check_kernel(int64_t P, int64_t F, int G, const T *__restrict__ points, const T *__restrict__ maxlen,
                          const int32_t *__restrict__ perm, const float *__restrict__ mbox, const int *__restrict__ cnt,
                          const int *__restrict__ offs, const int *__restrict__ list, const T *__restrict__ fc,
-                         const float *__restrict__ fb, uint8_t *__restrict__ contains) {
+                         const float *__restrict__ fb, T *__restrict__ counts, uint8_t *__restrict__ contains) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t b = blockIdx.y;
   if (i >= P) return;
@@ -419,7 +299,8 @@ __global__ void __launch_bounds__(256)
       count += cs_cross(qx, qy, qz, p1, p2, p3, bbj);
     }
   }
-  contains[row] = (uint8_t)(count & 1);
+  if (counts) counts[row] = (T)count;
+  if (contains) contains[row] = (uint8_t)(count & 1);
 }
 
 static int cs_grid_dim(int64_t F) {
@@ -459,20 +340,17 @@ static CsWs cs_ws_layout(int64_t B, int64_t F, int64_t P, size_t tsize) {
   return w;
 }
 
+// counts (B,P) in T (the _C contract) and/or contains (B,P) bool bytes
 template <typename T>
-static int mesh_intersection_unbatched(int64_t P, int64_t F, const void *points, const void *v1, const void *v2,
-                                       const void *v3, void *counts, hipStream_t st) {
-  CsFaces<T> src{(const T *)v1, (const T *)v2, (const T *)v3, nullptr, nullptr, nullptr, 0};
-  return check_sign_launch<T>(1, P, F, points, src, counts, nullptr, nullptr, nullptr, st);
-}
-
-template <typename T>
-static int check_sign_batched(int64_t B, int64_t V, int64_t F, int64_t P, const void *verts, const int64_t *faces,
-                              const void *points, const void *maxlen, uint8_t *contains, void *ws, size_t ws_bytes,
-                              kl_alloc_fn alloc, void *alloc_ctx, hipStream_t st) {
-  CsFaces<T> src{nullptr, nullptr, nullptr, (const T *)verts, faces, (const T *)maxlen, V};
+static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, const CsFaces<T> &src,
+                           const void *maxlen, void *counts, uint8_t *contains, void *ws, size_t ws_bytes,
+                           kl_alloc_fn alloc, void *alloc_ctx, hipStream_t st) {
   if (B == 0 || P == 0) return KL_OK;
-  if (F == 0) return fill_async(contains, 0, (size_t)(B * P), st);
+  if (F == 0) {
+    if (counts) KL_CHECK_RC(fill_async(counts, 0, (size_t)(B * P) * sizeof(T), st));
+    if (contains) KL_CHECK_RC(fill_async(contains, 0, (size_t)(B * P), st));
+    return KL_OK;
+  }
   const CsWs L = cs_ws_layout(B, F, P, sizeof(T));
   KL_REQUIRE(ws && ws_bytes >= L.total, "check_sign: workspace too small");
   KL_REQUIRE(alloc != nullptr, "check_sign: allocator callback required");
@@ -523,9 +401,25 @@ static int check_sign_batched(int64_t B, int64_t V, int64_t F, int64_t P, const 
   hipLaunchKernelGGL(cs_grid_check_kernel<T>, dim3((unsigned)cdiv(P, 256), (unsigned)B), dim3(256), 0, st, P, F, G,
                      (const T *)points, (const T *)maxlen, (const int32_t *)vout, (const float *)mbox,
                      (const int *)cnt, (const int *)offs, (const int *)list, (const T *)fc, (const float *)fb,
-                     contains);
+                     (T *)counts, contains);
   KL_CHECK_LAUNCH();
   return KL_OK;
+}
+
+template <typename T>
+static int mesh_intersection_unbatched(int64_t P, int64_t F, const void *points, const void *v1, const void *v2,
+                                       const void *v3, void *counts, void *ws, size_t ws_bytes, kl_alloc_fn alloc,
+                                       void *alloc_ctx, hipStream_t st) {
+  CsFaces<T> src{(const T *)v1, (const T *)v2, (const T *)v3, nullptr, nullptr, nullptr, 0};
+  return check_sign_grid<T>(1, F, P, points, src, nullptr, counts, nullptr, ws, ws_bytes, alloc, alloc_ctx, st);
+}
+
+template <typename T>
+static int check_sign_batched(int64_t B, int64_t V, int64_t F, int64_t P, const void *verts, const int64_t *faces,
+                              const void *points, const void *maxlen, uint8_t *contains, void *ws, size_t ws_bytes,
+                              kl_alloc_fn alloc, void *alloc_ctx, hipStream_t st) {
+  CsFaces<T> src{nullptr, nullptr, nullptr, (const T *)verts, faces, (const T *)maxlen, V};
+  return check_sign_grid<T>(B, F, P, points, src, maxlen, nullptr, contains, ws, ws_bytes, alloc, alloc_ctx, st);
 }
 
 }  // namespace kl
@@ -542,10 +436,13 @@ using namespace kl;
 
 extern "C" int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points, int64_t num_faces, const void *points,
                                               const void *verts_1, const void *verts_2, const void *verts_3,
-                                              void *result, kl_stream stream) {
+                                              void *result, void *workspace, size_t workspace_bytes,
+                                              kl_alloc_fn alloc, void *alloc_ctx, kl_stream stream) {
   KL_REQUIRE(num_points >= 0 && num_faces >= 0, "unbatched_mesh_intersection: negative size");
+  KL_REQUIRE(num_points < ((int64_t)1 << 31) && num_faces < ((int64_t)1 << 31),
+             "unbatched_mesh_intersection: num_points and num_faces must be < 2^31");
   KL_CS_DISPATCH(dtype, mesh_intersection_unbatched, num_points, num_faces, points, verts_1, verts_2, verts_3, result,
-                 S(stream));
+                 workspace, workspace_bytes, alloc, alloc_ctx, S(stream));
 }
 
 extern "C" size_t kl_check_sign_workspace_bytes(kl_dtype dtype, int64_t batch_size, int64_t num_faces,

@@ -379,10 +379,15 @@ def unbatched_mesh_intersection_cuda(points, verts_1, verts_2, verts_3):
     N.require_gpu(func, points)
     dev = points.device
     out = torch.empty((P,), dtype=points.dtype, device=dev)
+    lib = N.lib()
+    code = N.dtype_code(points.dtype)
+    ws_bytes = lib.kl_check_sign_workspace_bytes(code, 1, F, P)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    arena = N.Arena(dev)
     with torch.cuda.device(dev), N.timed(func, dev):
-        N.check(N.lib().kl_unbatched_mesh_intersection(N.dtype_code(points.dtype), P, F, N.ptr(points), N.ptr(verts_1),
-                                                       N.ptr(verts_2), N.ptr(verts_3), N.ptr(out),
-                                                       N.stream_of(dev)), func)
+        N.check(lib.kl_unbatched_mesh_intersection(code, P, F, N.ptr(points), N.ptr(verts_1), N.ptr(verts_2),
+                                                   N.ptr(verts_3), N.ptr(out), N.ptr(ws), ws_bytes, arena.fn, None,
+                                                   N.stream_of(dev)), func)
     return out
 
 

@@ -92,7 +92,7 @@ _SIGS = {
     'kl_deftet_bwd_workspace_bytes': (_SZ, [_I64, _I64, _I64, _I64]),
     'kl_deftet_sparse_render_backward': (_I, [_I, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _F, _P, _P,
                                               _P, _SZ, _P]),
-    'kl_unbatched_mesh_intersection': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P]),
+    'kl_unbatched_mesh_intersection': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, ALLOC_FN, _P, _P]),
     'kl_check_sign_workspace_bytes': (_SZ, [_I, _I64, _I64, _I64]),
     'kl_check_sign': (_I, [_I, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, ALLOC_FN, _P, _P]),
     'kl_voxelgrid_mark': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
