@@ -316,6 +316,14 @@ int kl_morton_to_octree(int64_t num_points, const uint64_t *morton, uint32_t lev
                         kl_alloc_fn alloc, void *alloc_ctx, uint8_t **octree, int64_t *num_nodes,
                         kl_stream stream);
 
+/* point_utils.cpp:52-64 points_to_morton_cuda (caller ops/spc/points.py:105):
+ * points (N,3) int16 -> morton (N) int64, bit 3i+2 = x_i, 3i+1 = y_i, 3i = z_i (spc_math.h:93-107). */
+int kl_points_to_morton(int64_t num_points, const int16_t *points, int64_t *morton, kl_stream stream);
+
+/* point_utils.cpp:36-50 morton_to_points_cuda (caller ops/spc/points.py:131):
+ * morton (N) int64 -> points (N,3) int16 (spc_math.h:110-121). */
+int kl_morton_to_points(int64_t num_points, const int64_t *morton, int16_t *points, kl_stream stream);
+
 /* spc.cpp:79-107 scan_octrees_cuda.  lengths_host (B) int32 on the host.
  * exsum (sum(lengths) + B) int32 device output; pyramid_host (B,2,17) int32 host output
  * (zero-filled by the callee); returns the level through *level. */

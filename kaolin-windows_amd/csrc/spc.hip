@@ -447,6 +447,15 @@ __global__ void morton_to_points_kernel(const uint64_t *__restrict__ m, int16_t 
   p[t * 3 + 2] = z;
 }
 
+// points_to_morton (point_utils_cuda.cu, spc_math.h:93-107): one lane per point; the 6 B
+// point is read as three int16 loads (rows of 6 B are not 4-B aligned) and the code is
+// written as one 8-B store, so a wave moves 384 B in and 512 B out.
+__global__ void points_to_morton_kernel(const int16_t *__restrict__ p, int64_t *__restrict__ m, int64_t n) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  m[t] = (int64_t)to_morton(p[t * 3 + 0], p[t * 3 + 1], p[t * 3 + 2]);
+}
+
 // ------------------------------------------------------------------ raytrace
 __device__ __forceinline__ float ray_aabb(const float o_q[3], const float d[3], const float inv[3],
                                           const float sgn[3], const float org[3], float r) {
@@ -743,6 +752,24 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
   }
   *nuggets = (int32_t *)n0;
   *num_hits = num;
+  return KL_OK;
+}
+
+extern "C" int kl_points_to_morton(int64_t num_points, const int16_t *points, int64_t *morton, kl_stream stream) {
+  KL_REQUIRE(num_points >= 0, "points_to_morton: negative size");
+  if (num_points == 0) return KL_OK;
+  hipLaunchKernelGGL(points_to_morton_kernel, dim3((unsigned)cdiv(num_points, 256)), dim3(256), 0, S(stream), points,
+                     morton, num_points);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
+extern "C" int kl_morton_to_points(int64_t num_points, const int64_t *morton, int16_t *points, kl_stream stream) {
+  KL_REQUIRE(num_points >= 0, "morton_to_points: negative size");
+  if (num_points == 0) return KL_OK;
+  hipLaunchKernelGGL(morton_to_points_kernel, dim3((unsigned)cdiv(num_points, 256)), dim3(256), 0, S(stream),
+                     (const uint64_t *)morton, points, num_points);
+  KL_CHECK_LAUNCH();
   return KL_OK;
 }
 

@@ -455,10 +455,41 @@ def morton_to_octree(mortons, level):
 
 
 def points_to_octree(points, level):
-    """spc.cpp:67-77: int16 points (N,3) -> octree (via morton codes)."""
-    from .ops.spc.points import points_to_morton
-    morton = torch.sort(points_to_morton(points.contiguous()))[0]
-    return morton_to_octree(morton, level)
+    """spc.cpp:67-77 -> spc_cuda.cu:166-178: int16 points (N,3), unique and in morton order
+    (the caller's contract, as in the reference) -> morton codes -> octree."""
+    return morton_to_octree(points_to_morton_cuda(points.contiguous()), level)
+
+
+def points_to_morton_cuda(points):
+    """point_utils.cpp:52-64."""
+    func = 'points_to_morton_cuda'
+    a = Arg(points, 'points', 1)
+    check_all_same_gpu(func, [a])
+    check_contiguous(func, [a])
+    _check_scalar_types(func, a, (torch.int16,))
+    if points.dim() != 2 or points.shape[1] != 3:
+        raise RuntimeError('points must be Nx3')
+    n = points.shape[0]
+    dev = points.device
+    morton = torch.empty((n,), dtype=torch.long, device=dev)
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_points_to_morton(n, N.ptr(points), N.ptr(morton), N.stream_of(dev)), func)
+    return morton
+
+
+def morton_to_points_cuda(morton_codes):
+    """point_utils.cpp:36-50."""
+    func = 'morton_to_points_cuda'
+    a = Arg(morton_codes, 'morton_codes', 1)
+    check_all_same_gpu(func, [a])
+    check_contiguous(func, [a])
+    _check_scalar_types(func, a, (torch.int64,))
+    n = morton_codes.shape[0]
+    dev = morton_codes.device
+    points = torch.empty((n, 3), dtype=torch.int16, device=dev)
+    with torch.cuda.device(dev):
+        N.check(N.lib().kl_morton_to_points(n, N.ptr(morton_codes), N.ptr(points), N.stream_of(dev)), func)
+    return points
 
 
 def _check_octrees(octrees, name='octrees'):
@@ -698,4 +729,5 @@ ops = _module('kaolin._C.ops')
 ops.mesh = _module('kaolin._C.ops.mesh', unbatched_mesh_intersection_cuda=unbatched_mesh_intersection_cuda)
 ops.conversions = _module('kaolin._C.ops.conversions', mesh_to_spc_cuda=mesh_to_spc_cuda)
 ops.spc = _module('kaolin._C.ops.spc', morton_to_octree=morton_to_octree, points_to_octree=points_to_octree,
+                  points_to_morton_cuda=points_to_morton_cuda, morton_to_points_cuda=morton_to_points_cuda,
                   scan_octrees_cuda=scan_octrees_cuda, generate_points_cuda=generate_points_cuda)

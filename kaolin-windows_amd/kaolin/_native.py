@@ -75,6 +75,8 @@ _SIGS = {
     'kl_morton_to_octree': (_I, [_I64, _P, ctypes.c_uint32, ALLOC_FN, _P, _PP, ctypes.POINTER(_I64), _P]),
     'kl_scan_octrees': (_I, [_I, _P, _P, _P, _P, ctypes.POINTER(_I), _P]),
     'kl_generate_points': (_I, [_I, _I, _P, _P, _P, _P, _P]),
+    'kl_points_to_morton': (_I, [_I64, _P, _P, _P]),
+    'kl_morton_to_points': (_I, [_I64, _P, _P, _P]),
     'kl_raytrace': (_I, [_P, _I64, _P, _I64, _P, _I, _P, _P, _I64, ctypes.c_uint32, _I, _I, ALLOC_FN, _P, _PP, _PP,
                          ctypes.POINTER(_I64), _P]),
     'kl_mark_pack_boundaries': (_I, [_I, _I64, _P, _P, _P]),

@@ -84,12 +84,12 @@ def test_cpu_tensors_fail_loudly():
     import kaolin
     with pytest.raises(RuntimeError, match='on CPU'):
         kaolin.metrics.pointcloud.sided_distance(torch.rand(1, 4, 3), torch.rand(1, 5, 3))
-    with pytest.raises(RuntimeError, match='no CPU'):
-        kaolin.metrics.trianglemesh.point_to_mesh_distance(torch.rand(1, 4, 3), torch.rand(1, 5, 3, 3))
     with pytest.raises(RuntimeError):
         kaolin.render.mesh.rasterize(8, 8, torch.rand(1, 2, 3), torch.rand(1, 2, 3, 2), torch.rand(1, 2, 3, 1))
-    with pytest.raises(RuntimeError, match='no CPU fallback'):
-        kaolin.ops.conversions.trianglemeshes_to_voxelgrids(torch.rand(1, 3, 3), torch.tensor([[0, 1, 2]]), 4)
+    with pytest.raises(RuntimeError, match='on CPU'):
+        kaolin.ops.spc.points_to_morton(torch.zeros(4, 3, dtype=torch.int16))
+    with pytest.raises(RuntimeError, match='on CPU'):
+        kaolin.ops.spc.morton_to_points(torch.zeros(4, dtype=torch.long))
     bnd = torch.tensor([True, False, True])
     for fn in (kaolin.render.spc.cumsum, kaolin.render.spc.cumprod, kaolin.render.spc.sum_reduce,
                kaolin.render.spc.diff):
