@@ -1,44 +1,94 @@
-"""bench.py -- DIB-R 512^2 forward+backward throughput (Mpixels/s) on MI355X, plus
-point_to_mesh_distance (Mpairs/s), per BASELINE.json.
+"""bench.py -- DIB-R fwd+bwd throughput (Mpixels/s) on MI355X, plus point_to_mesh_distance
+(Mpairs/s) and the other BASELINE.json configs as sub-lines.
 
-Workload (BASELINE.json configs[2]), per rank:
-  UV sphere 126 lat x 200 lon = 50,000 faces, radius 0.9*(1+0.01*N(0,1)) per vertex
-  (seed 0); 4 views (azimuth 90 deg apart, distance 3, look-at 0, up +y, fovy pi/4);
-  features D=3 = [uv, 1]; dibr_rasterization(512, 512, ..., sigmainv=7000,
-  boxlen=0.02, knum=30, multiplier=1000, eps=1e-8); loss = <feat, g_feat> +
-  <soft_mask, g_mask> with g ~ U[0,1] (seed 1); backward to face_vertices_image and
-  face_features.  One step = that forward + backward over the rank's 4 views.
-Multi-GPU: one process per GPU (torchrun); each rank renders its own 4 views of the
-replicated mesh (weak scaling, global batch 4N), per-shard losses are all-gathered
-over RCCL each step; time = max over ranks.
+Headline (``--config cfg3``, the default; BASELINE.json configs[2]),
+per rank: UV sphere 126 lat x 200 lon = 50,000 faces, radius 0.9*(1+0.01*N(0,1)) per vertex
+(seed 0); 4 views (azimuth 2*pi*i/(4N), distance 3, look-at 0, up +y, fovy pi/4); features
+D=3 = [uv, 1]; dibr_rasterization(512, 512, ..., sigmainv=7000, boxlen=0.02, knum=30,
+multiplier=1000, eps=1e-8); loss = <feat, g_feat> + <soft_mask, g_mask> with g ~ U[0,1]
+(seed 1); backward to face_vertices_image and face_features.  One step = that forward +
+backward over the rank's views.  ``--config cfg5`` (configs[4]): 8 views per rank at
+1024x1024, 64 views over 8 GPUs.
 
-Also reported: p2m (configs[1]: 100k points vs 20k faces, forward) Mpairs/s, the §8f
-sub-benches (deftet_sparse_render fwd+bwd on the same views, check_sign 1M points), the
-roofline of the dominant op (HIP events on its stream over the timed region) and a
-CPU baseline (the C oracle, 1 thread, on a stated row sample of view 0).
+Multi-GPU: one process per GPU.  Under torchrun (the driver's N>1 launch) the ranks come
+from the environment and WORLD_SIZE must equal --gpus.  Run directly with --gpus N > 1, this
+script starts the N rank processes itself (before anything touches the GPU) and exits with
+their status.  Views are sharded contiguously (weak scaling), per-shard losses are
+all-gathered over RCCL each step; time = max over ranks.
+
+Sub-lines: p2m (configs[1], points split over the ranks, faces replicated,
+outputs all-gathered, face gradient all-reduced), cfg4 (voxelgrid R=512 + mesh_to_spc L=9
+on a 200k-face sphere), raytrace (the cfg4 SPC, 512^2 rays), cfg1 (sided_distance 2k x 2k),
+deftet and check_sign; a full-size parity block (the GPU step against the C oracle on a row
+sample) and CPU baselines (1 thread and all threads, median of 5, samples stated).
 """
 import argparse
 import json
 import math
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
-
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'kaolin-windows_amd'))
 sys.path.insert(0, ROOT)
 
-import kaolin as kal  # noqa: E402
-from kaolin import _native  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector peak
+METRIC = 'DIB-R 512^2 fwd+bwd Mpixels/s + point_to_mesh Mpairs/s, 1/2/4/8 GPU'
+CONFIGS = {
+    'cfg3': dict(views=4, H=512, W=512, row_step=2,
+                 workload='dibr_rasterization fwd+bwd, batch=4/GPU, 50k-face mesh, 512x512, K=30'),
+    'cfg5': dict(views=8, H=1024, W=1024, row_step=16,
+                 workload='dibr_rasterization fwd+bwd, batch=8/GPU (64 @ 8 GPUs), 50k-face mesh, 1024x1024, K=30'),
+}
 
 
-def uv_sphere(n_lat, n_lon, device, dtype=torch.float32, seed=0):
+# ----------------------------------------------------------------------------- launcher
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', choices=sorted(CONFIGS), default='cfg3')
+    ap.add_argument('--device', choices=['cuda', 'cpu'], default='cuda',
+                    help='cpu: gloo self-test of the launcher and the sharded p2m path (no GPU)')
+    ap.add_argument('--cpu-row-step', type=int, default=None, help='oracle row sample (default per config)')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-p2m', action='store_true')
+    ap.add_argument('--no-extra', action='store_true', help='skip the cfg4 / raytrace / cfg1 / deftet / check_sign legs')
+    ap.add_argument('--eager', action='store_true', help='time the eager step only (no HIP graph capture)')
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """Start n rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+    rendezvous on 127.0.0.1) and return the worst exit status.  The parent makes no GPU call:
+    each child is a fresh interpreter."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    codes = [p.wait() for p in procs]
+    bad = [c for c in codes if c != 0]
+    return bad[0] if bad else 0
+
+
+# ----------------------------------------------------------------------------- workloads
+def uv_sphere(n_lat, n_lon, device, dtype=None, seed=0, radius=0.9, noise=0.01):
+    import torch
+    dtype = dtype or torch.float32
     lat = torch.linspace(0, math.pi, n_lat + 1, dtype=torch.float64)[1:-1]
     lon = torch.arange(n_lon, dtype=torch.float64) * (2 * math.pi / n_lon)
     ring = torch.stack([torch.sin(lat)[:, None] * torch.cos(lon)[None], torch.cos(lat)[:, None].expand(-1, n_lon),
@@ -46,7 +96,7 @@ def uv_sphere(n_lat, n_lon, device, dtype=torch.float32, seed=0):
     verts = torch.cat([torch.tensor([[0., 1., 0.]], dtype=torch.float64), ring,
                        torch.tensor([[0., -1., 0.]], dtype=torch.float64)])
     g = torch.Generator().manual_seed(seed)
-    verts = verts * (0.9 * (1 + 0.01 * torch.randn((verts.shape[0], 1), generator=g, dtype=torch.float64)))
+    verts = verts * (radius * (1 + noise * torch.randn((verts.shape[0], 1), generator=g, dtype=torch.float64)))
     nr = n_lat - 1
     j = torch.arange(n_lon)
     jn = (j + 1) % n_lon
@@ -64,6 +114,8 @@ def uv_sphere(n_lat, n_lon, device, dtype=torch.float32, seed=0):
 
 
 def dibr_inputs(views, device, H=512, W=512):
+    import torch
+    import kaolin as kal
     verts, faces = uv_sphere(126, 200, device)
     assert faces.shape[0] == 50000
     B = len(views)
@@ -98,25 +150,85 @@ def views_for_rank(rank, world, per_rank):
 
 def gather_losses(loss, world):
     """The step's only collective: all_gather of the per-shard scalar losses."""
-    out = [torch.empty_like(loss) for _ in range(world)]
-    dist.all_gather(out, loss.detach())
-    return torch.stack(out)
+    from kaolin.distributed import gather_losses as gl
+    return gl(loss) if world > 1 else loss.detach().reshape(1)
 
 
 def max_over_ranks(elapsed, device, world):
     if world == 1:
         return elapsed
+    import torch
+    import torch.distributed as dist
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t)
 
 
+def _sync(device):
+    import torch
+    if device.type == 'cuda':
+        torch.cuda.synchronize(device)
+
+
+def timed_loop(fn, steps, world, device=None):
+    import torch
+    import torch.distributed as dist
+    device = device or torch.device('cuda', torch.cuda.current_device())
+    if world > 1:
+        dist.barrier()
+    _sync(device)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    _sync(device)
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def cpu_info():
+    model = None
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    all_threads = int(os.environ.get('OMP_NUM_THREADS') or os.cpu_count() or 1)
+    return {'model': model, 'visible_cpus': os.cpu_count(), 'threads_used_for_nproc_leg': all_threads}
+
+
+def median_time(fn, reps=5):
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts)
+
+
+def torch_cpu_legs(fn, units, unit_scale, reps=5):
+    """Median of `reps` runs of fn on 1 thread and on all threads -> {threads: rate}."""
+    import torch
+    prev = torch.get_num_threads()
+    out = {}
+    try:
+        for nt in sorted({1, cpu_info()['threads_used_for_nproc_leg']}):
+            torch.set_num_threads(nt)
+            fn()  # warm
+            out[str(nt)] = round(units / median_time(fn, reps) / unit_scale, 4)
+    finally:
+        torch.set_num_threads(prev)
+    return out
+
+
+# ----------------------------------------------------------------------------- DIB-R step
 def loss_dot2(a, ga, b, gb, inp):
     """L = <a, ga> + <b, gb> in one launch (kl_loss_dot2: fp64 accumulation, deterministic; two
     torch.dot calls plus their add were four launches, ~25 us per step)."""
-    if os.environ.get('KL_BENCH_TORCH_LOSS'):  # dev A/B: the two-torch.dot loss
-        with torch.no_grad():
-            return torch.dot(a.reshape(-1), ga.reshape(-1)) + torch.dot(b.reshape(-1), gb.reshape(-1))
+    import torch
+    from kaolin import _native
     if 'loss_ws' not in inp:
         inp['loss_ws'] = torch.zeros(_native.lib().kl_loss_dot2_workspace_bytes(), dtype=torch.uint8, device=a.device)
     out = torch.empty(1, dtype=torch.float32, device=a.device)
@@ -126,33 +238,38 @@ def loss_dot2(a, ga, b, gb, inp):
     return out[0]
 
 
-def dibr_compute(inp):
+def dibr_compute(inp, g_feat=None, g_mask=None):
     """dibr_rasterization forward + the loss L = <features, g_feat> + <soft_mask, g_mask> + backward
     (everything but the collective).  dL/dfeatures = g_feat and dL/dsoft_mask = g_mask exactly, so the
     backward is driven with them directly (torch.autograd.backward) -- the same gradients as
     L.backward() without the broadcast kernels of the sum's backward; L itself is two dot products
     (one fused launch, loss_dot2)."""
+    import torch
+    import kaolin as kal
+    g_feat = inp['g_feat'] if g_feat is None else g_feat
+    g_mask = inp['g_mask'] if g_mask is None else g_mask
     fvi = inp['fvi'].detach().requires_grad_(True)
     feat = inp['feat'].detach().requires_grad_(True)
     feats, mask, idx = kal.render.mesh.dibr_rasterization(inp['H'], inp['W'], inp['fvz'], fvi, feat, inp['fnz'],
                                                           sigmainv=7000, boxlen=0.02, knum=30, multiplier=1000,
                                                           eps=1e-8)
-    loss = loss_dot2(feats.detach(), inp['g_feat'], mask.detach(), inp['g_mask'], inp)
-    torch.autograd.backward([feats, mask], [inp['g_feat'], inp['g_mask']])
-    return loss, fvi.grad, feat.grad, mask, idx
+    loss = loss_dot2(feats.detach(), g_feat, mask.detach(), g_mask, inp)
+    torch.autograd.backward([feats, mask], [g_feat, g_mask])
+    return loss, fvi.grad, feat.grad, mask, idx, feats
 
 
 def dibr_step(inp, world):
-    loss, gfvi, gfeat, mask, idx = dibr_compute(inp)
+    out = dibr_compute(inp)
     if world > 1:  # per-shard losses all-gathered over RCCL / xGMI
-        gather_losses(loss, world)
-    return gfvi, gfeat, mask, idx
+        gather_losses(out[0], world)
+    return out
 
 
 def graphed_step(inp, world):
-    """The same step with dibr_compute captured once in a HIP graph (its ~35 launches
-    replayed as one); the loss all_gather stays an eager RCCL call.  Inputs are static
-    buffers, as in a training loop that copies each batch into them."""
+    """The same step with dibr_compute captured once in a HIP graph (its launches replayed as
+    one); the loss all_gather stays an eager RCCL call.  Inputs are static buffers, as in a
+    training loop that copies each batch into them."""
+    import torch
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(side):
@@ -185,14 +302,9 @@ def op_bytes(name, inp, stats):
         # compact state: read sel (8/px), faces (fvi 24 + bbox write/read 2 x 16); write mask + hits (4 + 1)
         # per px and one record (face 4 + prob 4) per hit
         return px * (8 + s + 1) + stats['hits'] * (4 + s) + B * F * (6 * s + 2 * 4 * s)
-    if name == 'dibr_soft_mask_backward_cuda':
-        # read grad, mask, sel per px + used slots (+ terminator) of uncovered px; write grad (B,F,3,2)
-        return px * (s + s + 8) + stats['slot_reads'] * (8 + s + 1) + B * F * 6 * s * 2
     if name == 'dibr_soft_mask_backward':
         # compact state: read grad, mask, hits per px + one record per hit + faces; add into grad (B,F,3,2)
         return px * (s + s + 1) + stats['hits'] * (4 + s) + B * F * 6 * s * 2
-    if name == 'packed_rasterize_forward_cuda':
-        return px * (8 + 3 * s + D * s) + nv * (3 * s + 6 * s + 4 * s + 3 * D * s)
     if name == 'dibr_rasterize_forward':
         # write idx/weights/features; read (valid mask + z + image coords) of all faces + features of valid ones
         return px * (8 + 3 * s + D * s) + B * F * (1 + 3 * s + 6 * s) + nv * 3 * D * s
@@ -202,6 +314,9 @@ def op_bytes(name, inp, stats):
                 - B * F * 6 * s)
     if name in ('rasterize_backward_cuda', 'dibr_rasterize_backward'):
         return px * (8 + 3 * s + D * s) + B * F * (6 * s + 3 * D * s) * 2
+    if name == 'dibr_backward':
+        return (op_bytes('dibr_rasterize_backward', inp, stats) + op_bytes('dibr_soft_mask_backward', inp, stats)
+                - B * F * 6 * s * 2)
     return None
 
 
@@ -217,21 +332,18 @@ def survey_step_bytes(inp, stats):
 
 # kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
 OP_KERNELS = {
-    'dibr_soft_mask_forward': ('bin_faces_kernel<float, kl::SoftSrc', 'tile_bucket_kernel', 'tile_order_kernel',
-                               'soft_tile_fwd_kernel<float'),
-    'dibr_soft_mask_backward': ('soft_bwd_plan_kernel', 'soft_tile_bwd_kernel<float'),
-    'dibr_rasterize_forward': ('raster_bin_kernel<float, 2>', 'tile_bucket_kernel', 'tile_order_kernel',
-                               'raster_tile_kernel<float'),
     'dibr_forward': ('raster_bin_kernel<float, 2>', 'tile_bucket2_kernel', 'tile_order2_kernel', 'raster_tile_kernel<float',
                      'soft_tile_fwd_kernel<float'),
-    'dibr_rasterize_backward': ('rasterize_bwd_gather_kernel<float', 'rasterize_bwd_bigface_kernel<float'),
+    'dibr_backward': ('rasterize_bwd_gather_kernel<float', 'rasterize_bwd_bigface_kernel<float', 'soft_bwd_plan_kernel',
+                      'soft_tile_bwd_kernel<float'),
 }
 
 
-def pmc_traffic(op):
-    """HBM bytes per call of `op` from the committed PMC summary (scripts/pmc_traffic.py), or None."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'profiles', 'pmc_traffic.json')
-    if op not in OP_KERNELS or not os.path.exists(path):
+def pmc_traffic(op, config):
+    """HBM bytes per call of `op` from the committed PMC summary (scripts/pmc_traffic.py), or None
+    (the summary was measured on the cfg3 workload only)."""
+    path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    if config != 'cfg3' or op not in OP_KERNELS or not os.path.exists(path):
         return None
     kern = json.load(open(path))['kernels']
     total, found = 0, 0
@@ -244,26 +356,37 @@ def pmc_traffic(op):
     return total if found == len(OP_KERNELS[op]) else None
 
 
-def timed_loop(fn, steps, world):
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        fn()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    return time.perf_counter() - t0
+def workload_stats(inp):
+    """Per-run counts for the algorithmic byte model: valid faces, soft-mask hits, uncovered
+    fraction and mean used slots (from the _C contract's slot tensors, outside the timed region)."""
+    import torch
+    import kaolin as kal
+    with torch.no_grad():
+        _, fidx = kal.render.mesh.rasterize(inp['H'], inp['W'], inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'] >= 0)
+        fm = inp['fvi'] * 1000.
+        bb = torch.cat([fm.min(-2)[0] - 20., fm.max(-2)[0] + 20.], -1).contiguous()
+        _, _, cidx, _ = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, fidx, 7000., 30, 1000.)
+        unc = fidx < 0
+        used = (cidx >= 0).sum(-1)
+        stats = dict(valid_faces=int((inp['fnz'] >= 0).sum()), hits=int(used.sum()),
+                     uncovered=float(unc.float().mean()), mean_slots=float(used[unc].float().mean()))
+        del cidx
+    torch.cuda.empty_cache()
+    return stats
 
 
-def cpu_baseline(inp, row_step):
-    """The C oracle (1 thread) on all the rank's views, every `row_step`-th pixel row:
-    rasterize fwd, soft mask fwd, soft mask bwd, rasterize bwd."""
+def dibr_parity_and_cpu(inp, row_step):
+    """The C oracle (1 thread) on every `row_step`-th pixel row of all the rank's views: rasterize
+    fwd, soft mask fwd, soft mask bwd, rasterize bwd with the bench's own upstream gradients.  Timed
+    as the CPU baseline, then compared with the GPU step: forward rows bit-exact / max-abs, and the
+    GPU backward driven by the same gradients restricted to the sampled rows (a pixel's gradient
+    terms depend only on that pixel) against the oracle's gradients."""
     import numpy as np
+    import torch
     from oracle import oracle as orc
     A = lambda t: t.detach().cpu().numpy()  # noqa: E731
     fvz, fvi, feat, fnz = (A(inp[k]) for k in ('fvz', 'fvi', 'feat', 'fnz'))
+    gf, gm = A(inp['g_feat']), A(inp['g_mask'])
     H, W = inp['H'], inp['W']
     orc.lib().or_set_row_step(row_step)
     try:
@@ -271,36 +394,309 @@ def cpu_baseline(inp, row_step):
         of, oi, ow = orc.rasterize(H, W, fvz, fvi, feat, valid_faces=fnz >= 0)
         fm, bb = orc.soft_mask_bboxes(fvi, 0.02, 1000.)
         om, op, oci, oct_ = orc.dibr_soft_mask_forward(fm, bb, oi, 7000., 30, 1000.)
-        orc.dibr_soft_mask_backward(np.ones_like(om), om, oi, op, oci, oct_, fm, 7000., 1000.)
-        orc.rasterize_backward(np.ones_like(of), oi, ow, fvi, feat, 1e-8)
+        gi_s = orc.dibr_soft_mask_backward(gm, om, oi, op, oci, oct_, fm, 7000., 1000.)
+        gi_r, gf_r = orc.rasterize_backward(gf, oi, ow, fvi, feat, 1e-8)
         dt = time.perf_counter() - t0
     finally:
         orc.lib().or_set_row_step(1)
-    rows = len(range(0, H, row_step)) * fvz.shape[0]
-    return rows * W / dt / 1e6, rows * W, dt
+    rows = np.arange(0, H, row_step)
+    npx = len(rows) * W * fvz.shape[0]
+    # GPU: full forward, backward restricted to the sampled rows
+    rmask = torch.zeros((1, H, 1), device=inp['fvz'].device)
+    rmask[:, rows] = 1
+    _, gfvi, gfeat, mask, idx, feats = dibr_compute(inp, inp['g_feat'] * rmask.unsqueeze(-1), inp['g_mask'] * rmask)
+    torch.cuda.synchronize()
+    gi_o, gfe_o = gi_r + gi_s, gf_r
+    gi_g, gfe_g = A(gfvi), A(gfeat)
+    scale_i = float(np.abs(gi_o).max())
+    parity = {
+        'sample': f'every {row_step}th row of {fvz.shape[0]} views at {H}x{W} ({npx} px), oracle = C restatement',
+        'face_idx_equal': bool(np.array_equal(A(idx)[:, rows], oi[:, rows])),
+        'max_abs_feat': float(np.abs(A(feats)[:, rows] - of[:, rows]).max()),
+        'max_abs_mask': float(np.abs(A(mask)[:, rows] - om[:, rows]).max()),
+        'max_abs_grad_fvi': float(np.abs(gi_g - gi_o).max()),
+        'max_abs_grad_feat': float(np.abs(gfe_g - gfe_o).max()),
+        'max_abs_grad_fvi_reference_magnitude': scale_i,
+        'grad_fvi_elems_over_1e-5': int((np.abs(gi_g - gi_o) > 1e-5).sum()),
+    }
+    cpu = {'value': round(npx / dt / 1e6, 5), 'unit': 'Mpixels/s', 'cores': 1, 'kind': 'port',
+           'sample': f'C oracle (restatement of the reference CUDA path), {fvz.shape[0]} views, every {row_step}th '
+                     f'row of {H}x{W} ({npx} px), fwd+bwd, {dt:.1f} s'}
+    return parity, cpu
 
 
-def p2m_bench(device, steps):
+def dibr_headline(args, world, rank, device):
+    import torch
+    import kaolin as kal  # noqa: F401
+    from kaolin import _native
+    cfg = CONFIGS[args.config]
+    inp = dibr_inputs(views_for_rank(rank, world, cfg['views']), device, cfg['H'], cfg['W'])
+    step = lambda: dibr_step(inp, world)  # noqa: E731
+    for _ in range(args.warmup):
+        step()
+    stats = workload_stats(inp)
+    # eager pass: per-op HIP-event timing for the roofline, and the eager rate
+    timer = _native.OpTimer()
+    _native.set_timer(timer)
+    eager_elapsed = timed_loop(step, args.steps, world, device)
+    _native.set_timer(None)
+    eager_elapsed = max_over_ranks(eager_elapsed, device, world)
+    ops_ms = timer.summary_ms()
+    pixels = cfg['views'] * cfg['H'] * cfg['W'] * world * args.steps
+    mode, elapsed = 'eager', eager_elapsed
+    if not args.eager:
+        gstep, gout = graphed_step(inp, world)
+        ref = dibr_step(inp, world)
+        gstep()
+        torch.cuda.synchronize()
+        # the replayed graph must reproduce the eager step (forward bit-exact, grads to float order)
+        ok = torch.equal(gout[4], ref[4]) and torch.equal(gout[3], ref[3]) and \
+            torch.allclose(gout[1], ref[1], rtol=1e-4, atol=1e-5) and torch.allclose(gout[2], ref[2], rtol=1e-4, atol=1e-5)
+        if not ok:
+            raise RuntimeError('graph replay differs from the eager step')
+        for _ in range(args.warmup):
+            gstep()
+        elapsed = max_over_ranks(timed_loop(gstep, args.steps, world, device), device, world)
+        mode = 'hip_graph'
+    value = pixels / elapsed / 1e6
+    if rank != 0:
+        return None, inp
+    ops_ms = {k: v for k, v in ops_ms.items() if op_bytes(k, inp, stats)}
+    dom = max(ops_ms, key=ops_ms.get)
+    dbytes = op_bytes(dom, inp, stats)
+    achieved = dbytes / (ops_ms[dom] * 1e-3) / 1e9
+    ops_report = {k: {'ms': round(v, 4), 'bytes': op_bytes(k, inp, stats),
+                      'GB/s': round(op_bytes(k, inp, stats) / (v * 1e-3) / 1e9, 1)} for k, v in ops_ms.items()}
+    sb = survey_step_bytes(inp, stats)
+    result = {
+        'metric': METRIC, 'value': round(value, 2), 'unit': 'Mpixels/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
+        'data': f'synthetic (seeded UV sphere, {cfg["views"]} views/GPU)',
+        'config': {'workload': cfg['workload'], 'config': args.config, 'global_batch': cfg['views'] * world,
+                   'height': cfg['H'], 'width': cfg['W'], 'faces': 50000,
+                   'parallelism': f'batch-sharded x{world} (RCCL all_gather of per-shard losses)'},
+        'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
+                     'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(dom, args.config),
+                     'bytes_per_launch': dbytes, 'avg_launch_ms': round(ops_ms[dom], 4),
+                     'note': 'algorithmic bytes of the compact soft-mask state (the reference layout would move '
+                             + str(op_bytes('dibr_soft_mask_forward_cuda', inp, stats)) + ' B per call in the soft '
+                             'mask alone); the op is latency-bound, not HBM-bound (DESIGN.md section 5)',
+                     'survey_formula': {
+                         'scope': 'whole fwd+bwd step, SURVEY.md 8d cfg3 bytes (reference layout)',
+                         'bytes_per_step': sb, 'achieved': round(sb / (elapsed / args.steps) / 1e9, 1),
+                         'frac': round(sb / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}},
+        'ops': ops_report, 'workload_stats': stats, 'mode': mode,
+        'eager': {'value': round(pixels / eager_elapsed / 1e6, 2),
+                  'ms_per_step': round(eager_elapsed / args.steps * 1e3, 4)},
+    }
+    return result, inp
+
+
+# ----------------------------------------------------------------------------- p2m (cfg2)
+def p2m_inputs(device):
+    import torch
     g = torch.Generator().manual_seed(0)
-    pts = torch.randn((100000, 3), generator=g).to(device)
-    fv = torch.randn((20000, 3, 3), generator=g).to(device)
-    d = torch.empty(100000, device=device)
-    i = torch.empty(100000, dtype=torch.long, device=device)
-    t = torch.empty(100000, dtype=torch.int32, device=device)
-    f = lambda: kal._C.metrics.unbatched_triangle_distance_forward_cuda(pts, fv, d, i, t)  # noqa: E731
-    f()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(steps):
-        f()
-    e.record()
-    torch.cuda.synchronize()
-    ms = s.elapsed_time(e) / steps
-    return 100000 * 20000 / (ms * 1e-3) / 1e6, ms
+    pts = torch.randn((100000, 3), generator=g)
+    fv = torch.randn((20000, 3, 3), generator=g)
+    gd = torch.rand((100000,), generator=torch.Generator().manual_seed(1))
+    return pts.to(device), fv.to(device), gd.to(device)
 
 
+def p2m_leg(device, world, rank, steps, points=None, face_vertices=None, grad=None):
+    """cfg2: 100k points vs 20k faces, points split contiguously over the ranks, faces
+    replicated, outputs all-gathered (kaolin.distributed.sharded_point_to_mesh_distance).
+    Timed: forward (+ gather), and forward + backward (+ face-gradient all_reduce)."""
+    import torch
+    from kaolin.distributed import shard_bounds, sharded_point_to_mesh_distance
+    if points is None:
+        points, face_vertices, grad = p2m_inputs(device)
+    P, F = points.shape[0], face_vertices.shape[0]
+    lo, hi = shard_bounds(P, rank, world)
+    local = points[lo:hi].contiguous()
+
+    def fwd():
+        with torch.no_grad():
+            return sharded_point_to_mesh_distance(local, face_vertices)
+
+    lp = local.detach().requires_grad_(True)
+    fvr = face_vertices.detach().requires_grad_(True)
+
+    def fwd_bwd():
+        lp.grad = None
+        fvr.grad = None
+        d, _, _ = sharded_point_to_mesh_distance(lp, fvr)
+        d.backward(grad)
+
+    out = fwd()
+    fwd_bwd()
+    t_f = max_over_ranks(timed_loop(fwd, steps, world, device), device, world) / steps
+    t_fb = max_over_ranks(timed_loop(fwd_bwd, steps, world, device), device, world) / steps
+    res = {'metric': 'point_to_mesh Mpairs/s (100k pts x 20k faces, fwd; points sharded over ranks)',
+           'value': round(P * F / t_f / 1e6, 1), 'ms': round(t_f * 1e3, 4),
+           'fwd_bwd': {'value': round(P * F / t_fb / 1e6, 1), 'ms': round(t_fb * 1e3, 4)},
+           'n_ranks': world, 'points_per_rank': hi - lo, 'faces': F,
+           'roofline': {'bound': 'valu', 'flop_per_pair': 50, 'note': 'nominal pairs (P*F); pruned pairs are not evaluated',
+                        'achieved_tflops': round(P * F / t_f * 50 / 1e12, 2), 'peak_tflops': FP32_PEAK_TFLOPS,
+                        'frac': round(P * F / t_f * 50 / 1e12 / FP32_PEAK_TFLOPS, 4)}}
+    return res, out, (lp.grad, fvr.grad)
+
+
+def p2m_parity(points, face_vertices, out, n_sample=2000):
+    """Oracle check of the sharded result on a point sample (C restatement of the reference
+    CUDA kernel): forward bit-exact; face gradient of the sample via the oracle backward."""
+    import numpy as np
+    from oracle import oracle as orc
+    A = lambda t: t.detach().cpu().numpy()  # noqa: E731
+    P = points.shape[0]
+    sel = np.linspace(0, P - 1, n_sample).astype(np.int64)
+    od, oi, ot = orc.unbatched_triangle_distance_forward(A(points)[sel], A(face_vertices))
+    d, i, t = (A(x) for x in out)
+    return {'sample': f'{n_sample} evenly spaced points of {P} vs all {face_vertices.shape[0]} faces',
+            'dist_equal': bool(np.array_equal(d[sel], od)), 'face_idx_equal': bool(np.array_equal(i[sel], oi)),
+            'dist_type_equal': bool(np.array_equal(t[sel], ot))}
+
+
+def p2m_cpu_legs(points, face_vertices, n_points=200):
+    """The reference's CPU path for point_to_mesh_distance (its naive torch evaluation, restated in
+    kaolin.metrics.trianglemesh) on the first n_points points vs all faces, fwd, 1 and all threads."""
+    import torch
+    from kaolin.metrics.trianglemesh import _unbatched_naive_point_to_mesh_distance as naive
+    p = points[:n_points].cpu()
+    fv = face_vertices.cpu()
+
+    def run():
+        with torch.no_grad():
+            naive(p, fv)
+    rates = torch_cpu_legs(run, n_points * fv.shape[0], 1e6)
+    return {'unit': 'Mpairs/s', 'kind': 'port', 'by_threads': rates,
+            'sample': f'first {n_points} points x {fv.shape[0]} faces (fwd, median of 5; rate extrapolates linearly '
+                      'in points)'}
+
+
+# ----------------------------------------------------------------------------- cfg1 sided
+def sided_leg(device, steps):
+    """cfg1: sided_distance on two random 2k-point clouds: the HIP kernel, and the reference's
+    CPU path (its torch `_sided_distance`, restated in kaolin.metrics.pointcloud) on the host."""
+    import torch
+    import kaolin as kal
+    from kaolin.metrics.pointcloud import _sided_distance
+    g = torch.Generator().manual_seed(0)
+    p1, p2 = torch.rand((1, 2048, 3), generator=g), torch.rand((1, 2048, 3), generator=g)
+    d1, d2 = p1.to(device), p2.to(device)
+    ms = _event_ms(lambda: kal.metrics.pointcloud.sided_distance(d1, d2), steps)
+    dist, _ = kal.metrics.pointcloud.sided_distance(d1, d2)
+    ref = _sided_distance(p1, p2)
+    rates = torch_cpu_legs(lambda: _sided_distance(p1, p2), 2048 * 2048, 1e6)
+    return {'metric': 'sided_distance Mpairs/s (2048 x 2048, f32, fwd)', 'value': round(2048 * 2048 / (ms * 1e-3) / 1e6, 1),
+            'ms': round(ms, 4), 'parity_vs_cpu_reference_path': {'max_abs': float((dist.cpu() - ref).abs().max())},
+            'cpu': {'unit': 'Mpairs/s', 'kind': 'port', 'by_threads': rates,
+                    'sample': 'full 2048 x 2048 (median of 5)', 'survey_reference_8_threads': 152.0}}
+
+
+# ----------------------------------------------------------------------------- cfg4
+def cfg4_inputs(device):
+    verts, faces = uv_sphere(251, 400, device, radius=0.95, noise=0.0)
+    assert faces.shape[0] == 200000
+    return verts, faces
+
+
+def cfg4_leg(device, steps):
+    """cfg4: trianglemeshes_to_voxelgrids at R=512 and unbatched_mesh_to_spc at L=9 on the
+    200k-face sphere (radius 0.95), with the SURVEY.md §8d byte counts."""
+    import torch
+    import kaolin as kal
+    from kaolin import _native
+    verts, faces = cfg4_inputs(device)
+    V, F, R, L = verts.shape[0], faces.shape[0], 512, 9
+    vb = verts.unsqueeze(0).contiguous()
+    fv = kal.ops.mesh.index_vertices_by_faces(vb, faces)[0].contiguous()
+    vox = lambda: kal.ops.conversions.trianglemeshes_to_voxelgrids(vb, faces, R)  # noqa: E731
+    spc = lambda: kal.ops.conversions.unbatched_mesh_to_spc(fv, L)  # noqa: E731
+    grid = vox()
+    n_occ = int(grid.count_nonzero())
+    del grid
+    octree, fidx, bary = spc()
+    counts = (torch.zeros(16, dtype=torch.int64)).numpy()
+    import ctypes
+    nlev = _native.lib().kl_mesh_to_spc_level_counts(ctypes.c_void_p(counts.ctypes.data), 16)
+    N = [int(x) for x in counts[:nlev]]
+    nodes = int(octree.shape[0])
+    leaves = int(fidx.shape[0])
+    n_steps = max(3, steps // 4)
+    ms_vox = _wall_ms(vox, n_steps)
+    ms_spc = _wall_ms(spc, n_steps)
+    vox_bytes = 4 * R ** 3 + 12 * V + 24 * F
+    # SURVEY.md §8d: sum_l 28 N_l + sum_{l>=1} 16 N_l + N_L (32 + 36 + 8) + 9 * nodes
+    spc_bytes = sum(28 * n for n in N) + sum(16 * n for n in N[1:]) + N[-1] * (32 + 36 + 8) + 9 * nodes
+    return {'metric': 'cfg4: trianglemeshes_to_voxelgrids R=512 + unbatched_mesh_to_spc L=9, 200k-face sphere (f32)',
+            'voxelgrid': {'ms': round(ms_vox, 3), 'occupied': n_occ, 'bytes': vox_bytes,
+                          'roofline': {'bound': 'hbm', 'achieved': round(vox_bytes / (ms_vox * 1e-3) / 1e9, 1),
+                                       'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                                       'frac': round(vox_bytes / (ms_vox * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
+            'mesh_to_spc': {'ms': round(ms_spc, 3), 'nodes': nodes, 'leaves': leaves, 'proposals_per_level': N,
+                            'bytes': spc_bytes,
+                            'roofline': {'bound': 'hbm', 'achieved': round(spc_bytes / (ms_spc * 1e-3) / 1e9, 1),
+                                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                                         'frac': round(spc_bytes / (ms_spc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
+            'timing': 'wall clock per call incl. the per-level host count reads (median of runs)',
+            'spc': (octree, fidx, bary)}
+
+
+def cfg4_cpu_leg(device, stride=32):
+    """The reference's voxelgrid algorithm on the host (its torch subdivision, restated in
+    kaolin.ops.conversions as the CPU path) on every `stride`-th face of the cfg4 mesh at R=512,
+    extrapolated linearly to all faces."""
+    import torch
+    import kaolin as kal
+    verts, faces = cfg4_inputs('cpu')
+    sub = faces[::stride].contiguous()
+    vb = verts.unsqueeze(0)
+    o = torch.min(vb, dim=1)[0]
+    s = torch.max(torch.max(vb, dim=1)[0] - o, dim=1)[0]
+    run = lambda: kal.ops.conversions.trianglemeshes_to_voxelgrids(vb, sub, 512, o, s)  # noqa: E731
+    rates = torch_cpu_legs(run, 1.0, 1.0, reps=3)
+    return {'unit': 'meshes/s (extrapolated)', 'kind': 'port',
+            'by_threads': {k: round(v / stride, 6) for k, v in rates.items()},
+            'sample': f'every {stride}th face ({sub.shape[0]} of {faces.shape[0]}) at R=512, median of 3, time x{stride} '
+                      '(extrapolated); the reference itself took 55.9 s per mesh on 8 threads (BASELINE.md)'}
+
+
+# ----------------------------------------------------------------------------- raytrace
+def raytrace_leg(device, steps, spc_tuple):
+    """North-star raytrace row: the cfg4 SPC (level 9), 512x512 pinhole rays from z=+3 toward
+    the z=0 square [-1,1]^2 (SURVEY.md §8d byte model with the per-level hit counts)."""
+    import torch
+    import kaolin as kal
+    octree = spc_tuple[0]
+    lengths = torch.tensor([octree.shape[0]], dtype=torch.int32)
+    L, pyr, exsum = kal.ops.spc.scan_octrees(octree, lengths)
+    pts = kal.ops.spc.generate_points(octree, pyr, exsum)
+    n = 512
+    xs = (torch.arange(n, device=device, dtype=torch.float32) + 0.5) / n * 2 - 1
+    tgt = torch.stack([xs.view(1, -1).expand(n, n), xs.view(-1, 1).expand(n, n), torch.zeros(n, n, device=device)], -1)
+    o = torch.tensor([0., 0., 3.], device=device).expand(n * n, 3).contiguous()
+    d = tgt.reshape(-1, 3) - o
+    d = (d / d.norm(dim=-1, keepdim=True)).contiguous()
+    rt = lambda: kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], exsum, o, d, L)  # noqa: E731
+    ridx, pidx, depth = rt()
+    hits = int(ridx.shape[0])
+    per_level = [int(kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], exsum, o, d, lv,
+                                                        return_depth=False)[0].shape[0]) for lv in range(L + 1)]
+    ms = _wall_ms(rt, max(3, steps // 4))
+    R = n * n
+    nbytes = 24 * R + sum(31 * per_level[lv] + 8 * (per_level[lv + 1] if lv + 1 <= L else 0)
+                          for lv in range(L + 1)) + per_level[L] * (16 + 4)
+    return {'metric': 'unbatched_raytrace Mrays/s (cfg4 SPC level 9, 512x512 rays, depth)',
+            'value': round(R / (ms * 1e-3) / 1e6, 2), 'ms': round(ms, 4), 'hits': hits, 'hits_per_level': per_level,
+            'bytes': nbytes, 'timing': 'wall clock per call incl. the per-level host count reads',
+            'roofline': {'bound': 'hbm', 'achieved': round(nbytes / (ms * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+
+
+# ----------------------------------------------------------------------------- deftet / check_sign
 def _event_ms(fn, steps):
+    import torch
     fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -312,10 +708,25 @@ def _event_ms(fn, steps):
     return s.elapsed_time(e) / steps
 
 
+def _wall_ms(fn, steps):
+    import torch
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts) * 1e3
+
+
 def deftet_bench(inp, steps, knum=8):
     """deftet_sparse_render fwd+bwd on the cfg3 mesh and views: every
     pixel centre of the 512x512 grid, depth range = the mesh's z span, knum=8 (a covered pixel
     of the sphere holds its front and back faces)."""
+    import torch
+    import kaolin as kal
     fvz, fvi, feat, H, W = inp['fvz'], inp['fvi'], inp['feat'], inp['H'], inp['W']
     B, dev = fvz.shape[0], fvz.device
     x = (2 * torch.arange(W, device=dev, dtype=torch.float32) + 1 - W) / W
@@ -340,13 +751,15 @@ def deftet_bench(inp, steps, knum=8):
     ms = _event_ms(step, steps)
     _, idx = fwd()
     hits = int((idx >= 0).sum())
-    return {'metric': 'deftet_sparse_render fwd+bwd Mpixels/s (4 views, 512x512, 50k faces, knum=8, f32)',
+    return {'metric': f'deftet_sparse_render fwd+bwd Mpixels/s ({B} views, {H}x{W}, 50k faces, knum=8, f32)',
             'value': round(B * H * W / (ms * 1e-3) / 1e6, 1), 'ms': round(ms, 3), 'fwd_ms': round(ms_fwd, 3),
             'hits': hits}
 
 
 def check_sign_bench(device, steps, n_points=1000000):
     """check_sign: the cfg3 sphere (50k faces) vs 1M points in [-1,1]^3."""
+    import torch
+    import kaolin as kal
     verts, faces = uv_sphere(126, 200, device)
     g = torch.Generator().manual_seed(3)
     pts = (torch.rand((1, n_points, 3), generator=g) * 2 - 1).to(device)
@@ -357,126 +770,98 @@ def check_sign_bench(device, steps, n_points=1000000):
             'nominal_mpairs_per_s': round(n_points * faces.shape[0] / (ms * 1e-3) / 1e6, 1)}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--cpu-row-step', type=int, default=2)
-    ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--no-p2m', action='store_true')
-    ap.add_argument('--no-extra', action='store_true', help='skip the deftet / check_sign sub-benches')
-    ap.add_argument('--eager', action='store_true', help='time the eager step only (no HIP graph capture)')
-    args = ap.parse_args()
+# ----------------------------------------------------------------------------- CPU self-test
+def cpu_selftest(args, world, rank):
+    """--device cpu: the launcher, the rendezvous, the sharded p2m leg (CPU path of
+    point_to_mesh_distance) with its gather / all_reduce, and the max-over-ranks timing, on
+    gloo.  The gathered result is checked against the unsharded op on every rank."""
+    import torch
+    import kaolin as kal
+    dev = torch.device('cpu')
+    g = torch.Generator().manual_seed(0)
+    pts, fv = torch.randn((203, 3), generator=g), torch.randn((37, 3, 3), generator=g)
+    grad = torch.rand((203,), generator=g)
+    res, out, (gl, gfv) = p2m_leg(dev, world, rank, max(1, args.steps), pts, fv, grad)
+    p = pts.clone().requires_grad_(True)
+    f = fv.clone().requires_grad_(True)
+    d, i, t = kal.metrics.trianglemesh.point_to_mesh_distance(p[None], f[None])
+    d.backward(grad[None])
+    from kaolin.distributed import shard_bounds
+    lo, hi = shard_bounds(pts.shape[0], rank, world)
+    ok = (torch.equal(out[0], d[0].detach()) and torch.equal(out[1], i[0]) and torch.equal(out[2], t[0])
+          and torch.equal(gl, p.grad[lo:hi]) and torch.allclose(gfv, f.grad, rtol=1e-5, atol=1e-6))
+    flags = [None] * world if world > 1 else [ok]
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_gather_object(flags, ok)
+    if rank == 0:
+        res['parity_all_ranks'] = all(flags)
+        print(json.dumps({'metric': 'cpu self-test (sharded point_to_mesh_distance over gloo)', 'n_ranks': world,
+                          'steps': args.steps, 'p2m': res}))
+    return 0 if all(flags) else 1
 
+
+# ----------------------------------------------------------------------------- main
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        return launch_ranks(args.gpus, argv)
     world = int(os.environ.get('WORLD_SIZE', '1'))
+    if world != args.gpus:
+        print(f'bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing to time a different job',
+              file=sys.stderr)
+        return 2
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    import torch
+    import torch.distributed as dist
+    if args.device == 'cpu':
+        if world > 1:
+            dist.init_process_group('gloo')
+        try:
+            return cpu_selftest(args, world, rank)
+        finally:
+            if world > 1:
+                dist.destroy_process_group()
+    torch.cuda.set_device(local)
+    device = torch.device('cuda', local)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl')
-    device = torch.device('cuda', local if world > 1 else 0)
-    torch.cuda.set_device(device)
-
-    views_per_rank = 4
-    views = views_for_rank(rank, world, views_per_rank)
-    inp = dibr_inputs(views, device)
-    step = lambda: dibr_step(inp, world)  # noqa: E731
-    for _ in range(args.warmup):
-        step()
-    # workload statistics for the algorithmic byte counts
-    with torch.no_grad():
-        _, fidx = kal.render.mesh.rasterize(inp['H'], inp['W'], inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'] >= 0)
-        fm = inp['fvi'] * 1000.
-        bb = torch.cat([fm.min(-2)[0] - 20., fm.max(-2)[0] + 20.], -1).contiguous()
-        _, _, cidx, _ = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, fidx, 7000., 30, 1000.)
-        unc = fidx < 0
-        used = (cidx >= 0).sum(-1)
-        slot_reads = int((torch.clamp(used + 1, max=30) * unc).sum())
-        stats = dict(valid_faces=int((inp['fnz'] >= 0).sum()), slot_reads=slot_reads, hits=int(used.sum()),
-                     uncovered=float(unc.float().mean()), mean_slots=float(used[unc].float().mean()))
-    # eager pass: per-op HIP-event timing for the roofline, and the eager rate
-    timer = _native.OpTimer()
-    _native.set_timer(timer)
-    eager_elapsed = timed_loop(step, args.steps, world)
-    _native.set_timer(None)
-    eager_elapsed = max_over_ranks(eager_elapsed, device, world)
-    ops_ms = timer.summary_ms()
-    pixels = views_per_rank * inp['H'] * inp['W'] * world * args.steps
-    eager_value = pixels / eager_elapsed / 1e6
-    mode = 'eager'
-    elapsed = eager_elapsed
-    if not args.eager:
-        gstep, gout = graphed_step(inp, world)
-        ref = dibr_step(inp, world)
-        gstep()
-        torch.cuda.synchronize()
-        # the replayed graph must reproduce the eager step (forward bit-exact, grads to float order)
-        ok = torch.equal(gout[4], ref[3]) and torch.equal(gout[3], ref[2]) and \
-            torch.allclose(gout[1], ref[0], rtol=1e-4, atol=1e-5) and torch.allclose(gout[2], ref[1], rtol=1e-4, atol=1e-5)
-        if not ok:
-            raise RuntimeError('graph replay differs from the eager step')
-        for _ in range(args.warmup):
-            gstep()
-        elapsed = max_over_ranks(timed_loop(gstep, args.steps, world), device, world)
-        mode = 'hip_graph'
-    value = pixels / elapsed / 1e6
-    result = None
-    if rank == 0:
-        ops_ms = {k: v for k, v in ops_ms.items() if op_bytes(k, inp, stats)}
-        dom = max(ops_ms, key=ops_ms.get)
-        dbytes = op_bytes(dom, inp, stats)
-        achieved = dbytes / (ops_ms[dom] * 1e-3) / 1e9
-        ops_report = {k: {'ms': round(v, 4), 'GB/s': (round(op_bytes(k, inp, stats) / (v * 1e-3) / 1e9, 1)
-                                                     if op_bytes(k, inp, stats) else None)}
-                      for k, v in ops_ms.items()}
-        result = {
-            'metric': 'DIB-R 512^2 fwd+bwd Mpixels/s + point_to_mesh Mpairs/s, 1/2/4/8 GPU',
-            'value': round(value, 2), 'unit': 'Mpixels/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic (seeded UV sphere, 4 views/GPU)',
-            'config': {'workload': 'dibr_rasterization fwd+bwd, batch=4/GPU, 50k-face mesh, 512x512, K=30',
-                       'global_batch': views_per_rank * world, 'height': 512, 'width': 512, 'faces': 50000,
-                       'parallelism': f'batch-sharded x{world} (RCCL all_gather of per-shard losses)'},
-            'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(dom),
-                         'bytes_per_launch': dbytes, 'avg_launch_ms': round(ops_ms[dom], 4),
-                         'note': 'algorithmic bytes of the compact soft-mask state (the reference layout would '
-                                 'move ' + str(op_bytes('dibr_soft_mask_forward_cuda', inp, stats)) + ' B per call); '
-                                 'the op is latency-bound, not HBM-bound (DESIGN.md section 5)',
-                         'survey_formula': {
-                             'scope': 'whole fwd+bwd step, SURVEY.md 8d cfg3 bytes (reference layout)',
-                             'bytes_per_step': survey_step_bytes(inp, stats),
-                             'achieved': round(survey_step_bytes(inp, stats) / (elapsed / args.steps) / 1e9, 1),
-                             'frac': round(survey_step_bytes(inp, stats) / (elapsed / args.steps) / 1e9
-                                           / HBM_PEAK_GBS, 4)}},
-            'ops': ops_report,
-            'workload_stats': stats,
-            'mode': mode,
-            'eager': {'value': round(eager_value, 2), 'ms_per_step': round(eager_elapsed / args.steps * 1e3, 4)},
-        }
-    if not args.no_p2m and rank == 0:
-        mp, ms = p2m_bench(device, max(3, args.steps // 4))
-        result['p2m'] = {'metric': 'point_to_mesh Mpairs/s (100k pts x 20k faces, fwd)', 'value': round(mp, 1),
-                         'ms': round(ms, 3),
-                         'roofline': {'bound': 'valu', 'flop_per_pair': 50,
-                                      'achieved_tflops': round(mp * 1e6 * 50 / 1e12, 2),
-                                      'peak_tflops': FP32_PEAK_TFLOPS,
-                                      'frac': round(mp * 1e6 * 50 / 1e12 / FP32_PEAK_TFLOPS, 4)}}
-    if not args.no_extra and rank == 0:
-        result['deftet'] = deftet_bench(inp, max(3, args.steps // 4))
+        dist.init_process_group('nccl', device_id=device)
+    result, inp = dibr_headline(args, world, rank, device)
+    if not args.no_p2m:
+        p2m_res, p2m_out, p2m_grads = p2m_leg(device, world, rank, max(5, args.steps // 2))
+        if rank == 0:
+            result['p2m'] = p2m_res
+            pts, fv, _ = p2m_inputs(device)
+            result['p2m']['parity'] = p2m_parity(pts, fv, p2m_out)
+            if world == 1 and not args.no_cpu_baseline:
+                result['p2m']['cpu'] = p2m_cpu_legs(pts, fv)
+    if rank == 0 and not args.no_extra:
+        c4 = cfg4_leg(device, args.steps)
+        spc_tuple = c4.pop('spc')
+        result['cfg4'] = c4
+        result['raytrace'] = raytrace_leg(device, args.steps, spc_tuple)
+        del spc_tuple
+        result['cfg1_sided'] = sided_leg(device, max(5, args.steps))
+        if world == 1 and not args.no_cpu_baseline:
+            result['cfg4']['cpu'] = cfg4_cpu_leg(device)
+        if args.config == 'cfg3':
+            result['deftet'] = deftet_bench(inp, max(3, args.steps // 4))
         result['check_sign'] = check_sign_bench(device, max(3, args.steps // 4))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rate, npx, dt = cpu_baseline(inp, args.cpu_row_step)
-        result['cpu_baseline'] = {'value': round(rate, 5), 'unit': 'Mpixels/s', 'cores': 1, 'kind': 'port',
-                                  'sample': f'C oracle, the {views_per_rank} views, every {args.cpu_row_step}th row of '
-                                            f'512x512 ({npx} px, fwd+bwd, {dt:.1f} s)'}
+        row_step = args.cpu_row_step or CONFIGS[args.config]['row_step']
+        parity, cpu = dibr_parity_and_cpu(inp, row_step)
+        result['parity'] = parity
+        result['cpu_baseline'] = cpu
+        result['cpu_host'] = cpu_info()
     if rank == 0:
         print(json.dumps(result))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

@@ -311,6 +311,11 @@ int kl_mesh_to_spc(int64_t num_faces, const float *face_vertices, uint32_t level
                    uint8_t **octree, int64_t *num_nodes, int64_t **face_idx, float **bary,
                    int64_t *num_leaves, kl_stream stream);
 
+/* Measurement helper, not a reference op: the number of (face, voxel) proposals tested at
+ * each level 0..L by the last kl_mesh_to_spc call on the calling thread (N_0 = F).  Copies
+ * min(capacity, L+1) counts and returns L+1 (0 before any call). */
+int kl_mesh_to_spc_level_counts(int64_t *counts, int capacity);
+
 /* spc.cpp:55-65 morton_to_octree: sorted unique leaf morton codes -> octree bytes. */
 int kl_morton_to_octree(int64_t num_points, const uint64_t *morton, uint32_t level,
                         kl_alloc_fn alloc, void *alloc_ctx, uint8_t **octree, int64_t *num_nodes,

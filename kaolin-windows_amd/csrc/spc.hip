@@ -324,9 +324,15 @@ __global__ void iota_kernel(int64_t n, int64_t *__restrict__ t, uint64_t *__rest
   }
 }
 
+// proposals (face, voxel) tested per level by the last mesh_to_spc call on this thread
+// (N_l of SURVEY.md §8d's cfg4 byte count; read by kl_mesh_to_spc_level_counts)
+static thread_local int64_t t_m2s_counts[SPC_MAX_LEVELS + 1];
+static thread_local int t_m2s_levels = 0;
+
 static int mesh_to_spc_impl(int64_t F, const float *fv, uint32_t L, Scratch &sc, uint8_t **octree,
                             int64_t *num_nodes, int64_t **face_idx, float **bary, int64_t *num_leaves,
                             hipStream_t st) {
+  t_m2s_levels = 0;
   *num_nodes = 0;
   *num_leaves = 0;
   *octree = nullptr;
@@ -341,6 +347,8 @@ static int mesh_to_spc_impl(int64_t F, const float *fv, uint32_t L, Scratch &sc,
     KL_CHECK_LAUNCH();
   }
   for (uint32_t l = 0; l <= L; l++) {
+    t_m2s_counts[l] = cnt;
+    t_m2s_levels = (int)l + 1;
     uint32_t *occ = (uint32_t *)sc.get((cnt + 1) * sizeof(uint32_t));
     uint32_t *psum = (uint32_t *)sc.get((cnt + 2) * sizeof(uint32_t));
     if (!occ || !psum) return KL_E_ALLOC;
@@ -595,6 +603,12 @@ extern "C" int kl_mesh_to_spc(int64_t num_faces, const float *fv, uint32_t level
   KL_REQUIRE(alloc != nullptr, "mesh_to_spc: allocator required");
   Scratch sc{alloc, ctx};
   return mesh_to_spc_impl(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves, S(stream));
+}
+
+extern "C" int kl_mesh_to_spc_level_counts(int64_t *counts, int capacity) {
+  const int n = t_m2s_levels < capacity ? t_m2s_levels : capacity;
+  for (int i = 0; i < n; i++) counts[i] = t_m2s_counts[i];
+  return t_m2s_levels;
 }
 
 extern "C" int kl_morton_to_octree(int64_t n, const uint64_t *morton, uint32_t level, kl_alloc_fn alloc, void *ctx,

@@ -57,3 +57,11 @@ def f_score(gt_points, pred_points, radius=0.01, eps=1e-8):
     precision = tp / (tp + fp)
     recall = tp / (tp + fn)
     return 2 * (precision * recall) / (precision + recall + eps)
+
+
+def _sided_distance(p1, p2):
+    """The reference's pure-torch sided distance (pointcloud.py:186-197; used by its tests and as
+    the CPU path timed beside the HIP kernel): min_j |p1_i - p2_j|^2 over a (B,N,M) difference."""
+    b = p1.shape[0]
+    diff = (p1.reshape(b, -1, 1, 3) - p2.reshape(b, 1, -1, 3)) ** 2
+    return torch.min(torch.sum(diff, dim=-1), dim=-1).values

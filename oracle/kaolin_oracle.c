@@ -2,7 +2,10 @@
  *
  * This library is the parity checker for the HIP product path.  Only tests/,
  * __graft_entry__.smoke() and bench.py's cpu_baseline leg load it.  It is plain C,
- * single-threaded, compiled with -O2 -ffp-contract=off (see oracle/Makefile).
+ * compiled with -O2 -ffp-contract=off (see oracle/Makefile).  Single-threaded except two
+ * loops over independent items (p2m forward per point, mesh_to_spc barycentrics per leaf),
+ * which are OpenMP-parallel so that full-size parity checks finish in seconds; each item
+ * writes only its own outputs, so results do not depend on the thread count.
  *
  * Floating-point kernels (rasterize, soft mask, point->triangle distance, sided
  * distance) live in oracle_typed.inc, instantiated for float and double.  This
@@ -164,6 +167,13 @@ void or_bary(const float *fv, uint64_t m, unsigned level, float *out2)
   float s = (float)(1. / (double)(bx + by + bz));
   bx *= s; by *= s;
   out2[0] = bx; out2[1] = by;
+}
+
+/* or_bary over n leaves (face index per leaf into fv (F,3,3)); independent per leaf */
+void or_bary_batch(const float *fv, const uint64_t *m, const int64_t *face, int64_t n, unsigned level, float *out)
+{
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; i++) or_bary(fv + face[i] * 9, m[i], level, out + 2 * i);
 }
 
 typedef struct { uint64_t m; int64_t t; } mt_pair;

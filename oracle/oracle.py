@@ -34,6 +34,10 @@ def lib():
         _lib.or_raytrace.restype = ctypes.c_int64
         _lib.or_scan_octrees.restype = ctypes.c_int
         _lib.or_to_morton.restype = ctypes.c_uint64
+        _lib.or_mesh_to_spc_leaves.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint, ctypes.c_void_p,
+                                               ctypes.c_void_p]
+        _lib.or_bary_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                       ctypes.c_uint, ctypes.c_void_p]
     return _lib
 
 
@@ -229,10 +233,7 @@ def mesh_to_spc(face_vertices, level):
     lib().or_free(pm)
     lib().or_free(pf)
     bary = np.zeros((n, 2), np.float32)
-    flat = fv.reshape(-1, 9)
-    for i in range(n):
-        lib().or_bary(_p(np.ascontiguousarray(flat[face[i]])), ctypes.c_uint64(int(mort[i])), level,
-                      bary[i].ctypes.data_as(_P))
+    lib().or_bary_batch(_p(fv), _p(mort), _p(face), n, level, _p(bary))
     return morton_to_octree(mort, level), face, bary
 
 

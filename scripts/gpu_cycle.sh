@@ -6,9 +6,9 @@ set -e
 OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 ROOT=$(pwd)
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
-timeout -k 10 240 python bench.py ${BENCH_ARGS:---no-cpu-baseline} > "$OUT/bench.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 180 --timeout-method thread ${TESTS_ARGS:-} > "$OUT/gpu_tests.log" 2>&1
+timeout -k 10 480 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof" -o run \
-  -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 10 > "$ROOT/$OUT/prof_bench.log" 2>&1
+  -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-extra --no-p2m --steps 10 > "$ROOT/$OUT/prof_bench.log" 2>&1

@@ -71,3 +71,50 @@ def test_single_rank_is_identity():
     import bench
     assert bench.views_for_rank(0, 1, 4) == pytest.approx([0, math.pi / 2, math.pi, 3 * math.pi / 2])
     assert bench.max_over_ranks(2.5, torch.device('cpu'), 1) == 2.5
+
+
+# ------------------------------------------------------------------ launcher + point sharding
+import json  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_bench(args, env_extra=None, timeout=300):
+    env = dict(os.environ)
+    for k in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py')] + args, env=env, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_bench_launcher_spawns_ranks_and_shards_p2m(world):
+    """bench.py --gpus N (no torchrun) starts N rank processes itself; over gloo the sharded
+    point_to_mesh_distance (points split, faces replicated, outputs all-gathered, face gradient
+    all-reduced) equals the unsharded op on every rank."""
+    r = _run_bench(['--device', 'cpu', '--gpus', str(world), '--steps', '1'])
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line['n_ranks'] == world
+    assert line['p2m']['parity_all_ranks'] is True
+    assert line['p2m']['points_per_rank'] == -(-203 // world)
+
+
+def test_bench_refuses_world_size_mismatch():
+    r = _run_bench(['--gpus', '2'], env_extra={'WORLD_SIZE': '3', 'RANK': '0'})
+    assert r.returncode == 2
+    assert 'refusing' in r.stderr
+
+
+def test_shard_bounds_cover_in_order():
+    from kaolin.distributed import shard_bounds
+    for n in (0, 1, 7, 100, 101):
+        for world in (1, 2, 3, 8):
+            spans = [shard_bounds(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [hi - lo for lo, hi in spans]
+            assert max(sizes) - min(sizes) <= 1

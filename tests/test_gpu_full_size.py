@@ -1,0 +1,196 @@
+"""BASELINE.json configs at (or as one GPU shard of) their full size, against the oracle.
+
+* cfg5: one rank's shard of the 64-view 1024^2 job (8 views), forward rows bit-exact and
+  gradients of the sampled rows, on a row sample;
+* cfg4: trianglemeshes_to_voxelgrids at R=512 and unbatched_mesh_to_spc at L=9 on the
+  200k-face sphere, bit-exact; the level-9 SPC ray-marched by 512^2 rays (sampled);
+* cfg2: point_to_mesh_distance on 100k points x 20k faces, bit-exact forward, gradients;
+* morton helpers and the single-rank sharded p2m path.
+The oracle's p2m forward and barycentric loops are OpenMP-parallel over independent items
+(results do not depend on the thread count).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def A(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.fixture(scope='module')
+def kal():
+    import kaolin
+    return kaolin
+
+
+# ------------------------------------------------------------------ cfg5 shard
+def test_cfg5_shard_vs_oracle(kal):
+    """BASELINE.json configs[4]: rank 0's shard (views 0..7 of 64) at 1024x1024, K=30.  Every
+    32nd pixel row of the 8 views: face_idx and features bit-exact, soft mask to expf ulps; the
+    backward driven by upstream gradients on those rows only, against the oracle's."""
+    import bench
+    step = 32
+    inp = bench.dibr_inputs(bench.views_for_rank(0, 8, 8), DEV, 1024, 1024)
+    fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+    rows = np.arange(0, 1024, step)
+    rmask = torch.zeros((1, 1024, 1), device=DEV)
+    rmask[:, rows] = 1
+    gf, gm = inp['g_feat'] * rmask.unsqueeze(-1), inp['g_mask'] * rmask
+    a, b = fvi.clone().requires_grad_(True), feat.clone().requires_grad_(True)
+    feats, mask, idx = kal.render.mesh.dibr_rasterization(1024, 1024, fvz, a, b, fnz, 7000, 0.02, 30, 1000, 1e-8)
+    torch.autograd.backward([feats, mask], [gf, gm])
+    orc.lib().or_set_row_step(step)
+    try:
+        of, oi, ow = orc.rasterize(1024, 1024, A(fvz), A(fvi), A(feat), valid_faces=A(fnz >= 0))
+        fm, bb = orc.soft_mask_bboxes(A(fvi), 0.02, 1000.)
+        om, op, oci, oct_ = orc.dibr_soft_mask_forward(fm, bb, oi, 7000., 30, 1000.)
+        gi_s = orc.dibr_soft_mask_backward(A(gm), om, oi, op, oci, oct_, fm, 7000., 1000.)
+        gi_r, gf_r = orc.rasterize_backward(A(gf), oi, ow, A(fvi), A(feat), 1e-8)
+    finally:
+        orc.lib().or_set_row_step(1)
+    assert np.array_equal(A(idx)[:, rows], oi[:, rows])
+    assert np.array_equal(A(feats)[:, rows], of[:, rows])
+    np.testing.assert_allclose(A(mask)[:, rows], om[:, rows], rtol=1e-6, atol=1e-7)
+    assert (oi[:, rows] >= 0).sum() > 100000 and (om[:, rows] > 0).sum() > 100000
+    gi = gi_r + gi_s
+    np.testing.assert_allclose(A(b.grad), gf_r, rtol=1e-5, atol=1e-5)
+    atol = max(1e-5, 4 * np.finfo(np.float32).eps * np.abs(gi).max())
+    np.testing.assert_allclose(A(a.grad), gi, rtol=1e-5, atol=atol)
+
+
+# ------------------------------------------------------------------ cfg4
+@pytest.fixture(scope='module')
+def cfg4():
+    import bench
+    v, f = bench.cfg4_inputs('cpu')
+    return v.numpy(), f.numpy()
+
+
+def test_cfg4_voxelgrid_r512_vs_oracle(kal, cfg4):
+    """BASELINE.json configs[3]: 200k-face sphere at R=512, default origin / scale: the
+    occupied voxel set is bit-equal to the oracle's (1M voxels)."""
+    v, f = cfg4
+    grid = kal.ops.conversions.trianglemeshes_to_voxelgrids(torch.from_numpy(v).to(DEV).unsqueeze(0),
+                                                            torch.from_numpy(f).to(DEV), 512)
+    og = torch.from_numpy(orc.voxelgrid(v[None], f, 512)).to(DEV)
+    assert grid.shape == (1, 512, 512, 512) and grid.dtype == torch.float32
+    assert torch.equal(grid != 0, og != 0)
+    assert int(og.sum()) > 500000
+    assert torch.all((grid == 0) | (grid == 1))
+
+
+def test_cfg4_mesh_to_spc_l9_and_raytrace_vs_oracle(kal, cfg4):
+    """unbatched_mesh_to_spc at level 9 on the same mesh: octree and face_idx bit-equal,
+    barycentrics within 1e-5; then the north-star raytrace of that SPC (512^2 pinhole rays from
+    z=+3, every 16th ray checked): nuggets and depths bit-equal."""
+    v, f = cfg4
+    fv = v[f].astype(np.float32)
+    octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(torch.from_numpy(fv).to(DEV), 9)
+    oo, of, ob = orc.mesh_to_spc(fv, 9)
+    assert np.array_equal(A(octree), oo)
+    assert np.array_equal(A(fidx), of)
+    np.testing.assert_allclose(A(bary), ob, rtol=0, atol=1e-5)
+    assert len(of) > 1000000
+    lengths = torch.tensor([octree.shape[0]], dtype=torch.int32)
+    L, pyr, ex = kal.ops.spc.scan_octrees(octree, lengths)
+    assert L == 9
+    pts = kal.ops.spc.generate_points(octree, pyr, ex)
+    n = 512
+    xs = (np.arange(n) + 0.5) / n * 2 - 1
+    tgt = np.stack([np.tile(xs[None], (n, 1)), np.tile(xs[:, None], (1, n)), np.zeros((n, n))], -1).reshape(-1, 3)
+    o = np.tile(np.array([[0., 0., 3.]]), (n * n, 1))
+    d = tgt - o
+    d = d / np.linalg.norm(d, axis=-1, keepdims=True)
+    o, d = o[::16].astype(np.float32), d[::16].astype(np.float32)
+    r, p, dep = kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], ex, torch.from_numpy(o).to(DEV),
+                                                  torch.from_numpy(d).to(DEV), 9, return_depth=True)
+    onug, odep = orc.raytrace(A(octree), A(pts), pyr.numpy()[0], A(ex), o, d, 9, True, False)
+    assert np.array_equal(np.stack([A(r), A(p)], -1), onug)
+    assert np.array_equal(A(dep), odep)
+    assert len(onug) > 10000
+
+
+# ------------------------------------------------------------------ cfg2
+def test_cfg2_full_size_vs_oracle(kal):
+    """BASELINE.json configs[1] at full size (100k points x 20k faces, the bench's seeded
+    inputs): dist, face_idx and dist_type bit-exact against the oracle over every point (this
+    is the 20 x 1024-face-split, shared-threshold path the bench times); the backward: grad
+    of the points bit-exact, face gradient to 1e-5."""
+    import bench
+    pts, fv, gd = bench.p2m_inputs(DEV)
+    p = pts.clone().requires_grad_(True)
+    f = fv.clone().requires_grad_(True)
+    d, i, t = kal.metrics.trianglemesh.point_to_mesh_distance(p[None], f[None])
+    od, oi, ot = orc.unbatched_triangle_distance_forward(A(pts), A(fv))
+    assert np.array_equal(A(i[0]), oi)
+    assert np.array_equal(A(t[0]), ot)
+    assert np.array_equal(A(d[0]), od)
+    d.backward(gd[None])
+    ogp, ogf = orc.unbatched_triangle_distance_backward(A(gd), A(pts), A(fv), oi, ot)
+    assert np.array_equal(A(p.grad), ogp)
+    np.testing.assert_allclose(A(f.grad), ogf, rtol=1e-5, atol=1e-5)
+
+
+def test_sharded_p2m_single_rank_equals_op(kal):
+    """kaolin.distributed.sharded_point_to_mesh_distance with no process group is the op."""
+    import bench
+    from kaolin.distributed import sharded_point_to_mesh_distance
+    pts, fv, _ = bench.p2m_inputs(DEV)
+    pts, fv = pts[:5000].contiguous(), fv[:3000].contiguous()
+    d1, i1, t1 = sharded_point_to_mesh_distance(pts, fv)
+    d2, i2, t2 = kal.metrics.trianglemesh.point_to_mesh_distance(pts[None], fv[None])
+    assert torch.equal(d1, d2[0]) and torch.equal(i1, i2[0]) and torch.equal(t1, t2[0])
+
+
+# ------------------------------------------------------------------ morton helpers
+def _np_morton(p):
+    p = p.astype(np.int64) & 0xFFFF
+    m = np.zeros(p.shape[0], np.int64)
+    for i in range(15):
+        m |= ((p[:, 2] >> i) & 1) << (3 * i)
+        m |= ((p[:, 1] >> i) & 1) << (3 * i + 1)
+        m |= ((p[:, 0] >> i) & 1) << (3 * i + 2)
+    return m
+
+
+def test_points_to_morton_and_back(kal):
+    """_C.ops.spc.points_to_morton_cuda / morton_to_points_cuda (point_utils.cpp:36-64): the
+    reference docstring example, 1M random 15-bit points vs the bit formula of spc_math.h:93-121,
+    and the round trip."""
+    ex = torch.tensor([[0, 0, 0], [0, 0, 1], [0, 0, 2], [0, 0, 3], [0, 1, 0]], device=DEV, dtype=torch.int16)
+    assert kal.ops.spc.points_to_morton(ex).tolist() == [0, 1, 8, 9, 2]
+    assert torch.equal(kal.ops.spc.morton_to_points(torch.tensor([0, 1, 8, 9, 2], device=DEV)), ex)
+    g = np.random.default_rng(0)
+    p = g.integers(0, 1 << 15, (1000000, 3)).astype(np.int16)
+    m = kal.ops.spc.points_to_morton(torch.from_numpy(p).to(DEV))
+    assert m.dtype == torch.int64 and np.array_equal(A(m), _np_morton(p))
+    back = kal.ops.spc.morton_to_points(m)
+    assert back.dtype == torch.int16 and np.array_equal(A(back), p)
+    # batched shapes are kept (points.py:105,131)
+    assert kal.ops.spc.points_to_morton(torch.from_numpy(p[:12].reshape(2, 6, 3)).to(DEV)).shape == (2, 6)
+    assert kal.ops.spc.morton_to_points(m[:12].reshape(3, 4)).shape == (3, 4, 3)
+    assert kal.ops.spc.points_to_morton(torch.zeros((0, 3), dtype=torch.int16, device=DEV)).shape == (0,)
+    with pytest.raises(RuntimeError, match="Expected scalar type of argument #1 'points' to be Short"):
+        kal._C.ops.spc.points_to_morton_cuda(torch.zeros((4, 3), dtype=torch.int32, device=DEV))
+
+
+def test_unbatched_points_to_octree_vs_oracle(kal):
+    """points.py:50-77 (dedup + morton sort on the unsorted path) against the oracle's
+    morton_to_octree of the sorted unique codes."""
+    g = np.random.default_rng(1)
+    level = 6
+    p = g.integers(0, 1 << level, (5000, 3)).astype(np.int16)
+    octree = kal.ops.spc.unbatched_points_to_octree(torch.from_numpy(p).to(DEV), level)
+    codes = np.unique(_np_morton(p)).astype(np.uint64)
+    assert np.array_equal(A(octree), orc.morton_to_octree(codes, level))
+    srt = kal.ops.spc.morton_to_points(torch.from_numpy(codes.astype(np.int64)).to(DEV))
+    assert torch.equal(kal.ops.spc.unbatched_points_to_octree(srt, level, sorted=True), octree)
