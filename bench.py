@@ -186,6 +186,11 @@ def timed_loop(fn, steps, world, device=None):
     return time.perf_counter() - t0
 
 
+def progress(msg):
+    """One line per leg on stderr (a long run keeps showing signs of life)."""
+    print(f'[bench {time.strftime("%H:%M:%S")}] {msg}', file=sys.stderr, flush=True)
+
+
 def cpu_info():
     model = None
     try:
@@ -828,29 +833,38 @@ def main(argv=None):
     device = torch.device('cuda', local)
     if world > 1:
         dist.init_process_group('nccl', device_id=device)
+    progress(f'rank {rank}/{world}: DIB-R {args.config} headline')
     result, inp = dibr_headline(args, world, rank, device)
     if not args.no_p2m:
+        progress('p2m leg')
         p2m_res, p2m_out, p2m_grads = p2m_leg(device, world, rank, max(5, args.steps // 2))
         if rank == 0:
             result['p2m'] = p2m_res
             pts, fv, _ = p2m_inputs(device)
             result['p2m']['parity'] = p2m_parity(pts, fv, p2m_out)
             if world == 1 and not args.no_cpu_baseline:
+                progress('p2m cpu leg')
                 result['p2m']['cpu'] = p2m_cpu_legs(pts, fv)
     if rank == 0 and not args.no_extra:
+        progress('cfg4 leg')
         c4 = cfg4_leg(device, args.steps)
         spc_tuple = c4.pop('spc')
         result['cfg4'] = c4
+        progress('raytrace leg')
         result['raytrace'] = raytrace_leg(device, args.steps, spc_tuple)
         del spc_tuple
+        progress('cfg1 sided leg')
         result['cfg1_sided'] = sided_leg(device, max(5, args.steps))
         if world == 1 and not args.no_cpu_baseline:
+            progress('cfg4 cpu leg')
             result['cfg4']['cpu'] = cfg4_cpu_leg(device)
+        progress('deftet / check_sign legs')
         if args.config == 'cfg3':
             result['deftet'] = deftet_bench(inp, max(3, args.steps // 4))
         result['check_sign'] = check_sign_bench(device, max(3, args.steps // 4))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         row_step = args.cpu_row_step or CONFIGS[args.config]['row_step']
+        progress(f'DIB-R parity + cpu baseline (oracle, every {row_step}th row)')
         parity, cpu = dibr_parity_and_cpu(inp, row_step)
         result['parity'] = parity
         result['cpu_baseline'] = cpu
