@@ -37,6 +37,7 @@ struct CsFaces {
   const int64_t *faces;    // (F,3) indices (batched entry)
   const T *maxlen;         // (B) divisor applied on load, or null
   int64_t V;
+  int *bad;                // set to 1 when a face index is outside [0, V) (batched entry)
 };
 
 // mesh_intersection_cuda.cu:71-82 (signed_area on the (y, z) projection)
@@ -107,7 +108,11 @@ __device__ __forceinline__ void cs_load_face(const CsFaces<T> &src, int64_t b, i
     const T *vb = src.verts + b * src.V * 3;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
-      const int64_t vi = src.faces[f * 3 + c];
+      int64_t vi = src.faces[f * 3 + c];
+      if (vi < 0 || vi >= src.V) {  // torch.index_select raises here (check_sign.py:29-31)
+        *src.bad = 1;
+        vi = 0;
+      }
 #pragma unroll
       for (int k = 0; k < 3; k++) v[c * 3 + k] = vb[vi * 3 + k];
     }
@@ -244,19 +249,27 @@ __device__ __forceinline__ int cs_cell(float v, float v0, float inv, int G) {
   return (int)c;
 }
 
-// fill == false: count the list entries of each cell; fill == true: write them
+// fill == false: count the list entries of each cell, and their total in 64 bits (the int32
+// scan below is used only when that total is < 2^31); fill == true: write them
 template <bool FILL>
 __global__ void __launch_bounds__(256)
     cs_bin_kernel(int64_t F, int G, const float *__restrict__ fb, const float *__restrict__ mbox,
-                  int *__restrict__ cnt, const int *__restrict__ offs, int *__restrict__ list) {
+                  int *__restrict__ cnt, const int *__restrict__ offs, int *__restrict__ list,
+                  unsigned long long *__restrict__ total) {
   const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (f >= F) return;
-  const float *bb = fb + (b * F + f) * 4;
-  const float y0 = bb[0], y1 = bb[1], z0 = bb[2], z1 = bb[3];
-  if (!(y0 <= y1 && z0 <= z1)) return;  // NaN bounds never pass bbox_check
-  const float *m = mbox + b * 8;
-  const int cy0 = cs_cell(y0, m[0], m[4], G), cy1 = cs_cell(y1, m[0], m[4], G);
-  const int cz0 = cs_cell(z0, m[2], m[5], G), cz1 = cs_cell(z1, m[2], m[5], G);
+  int cy0 = 0, cy1 = -1, cz0 = 0, cz1 = -1;
+  if (f < F) {
+    const float *bb = fb + (b * F + f) * 4;
+    const float y0 = bb[0], y1 = bb[1], z0 = bb[2], z1 = bb[3];
+    if (y0 <= y1 && z0 <= z1) {  // NaN bounds never pass bbox_check
+      const float *m = mbox + b * 8;
+      cy0 = cs_cell(y0, m[0], m[4], G);
+      cy1 = cs_cell(y1, m[0], m[4], G);
+      cz0 = cs_cell(z0, m[2], m[5], G);
+      cz1 = cs_cell(z1, m[2], m[5], G);
+    }
+  }
+  if (!FILL) wave_add_u64(total, (unsigned long long)(cy1 - cy0 + 1) * (unsigned long long)(cz1 - cz0 + 1));
   int *c = cnt + b * (int64_t)G * G;
   for (int cz = cz0; cz <= cz1; cz++)
     for (int cy = cy0; cy <= cy1; cy++) {
@@ -312,7 +325,7 @@ static int cs_grid_dim(int64_t F) {
 // workspace layout of the batched entry (byte offsets, 256-aligned); the face lists come from
 // the allocator callback once their total is known
 struct CsWs {
-  size_t keys_in, keys_out, vals_in, vals_out, tbox, mbox, fc, fb, cnt, offs, temp, temp_bytes, total;
+  size_t keys_in, keys_out, vals_in, vals_out, tbox, mbox, ctl, fc, fb, cnt, offs, temp, temp_bytes, total;
   int G;
 };
 static size_t cs_align(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -331,6 +344,7 @@ static CsWs cs_ws_layout(int64_t B, int64_t F, int64_t P, size_t tsize) {
   w.vals_out = o; o += cs_align((size_t)(B * P) * 4);
   w.tbox = o; o += cs_align((size_t)(B * cdiv(F, kCsTile)) * 16);
   w.mbox = o; o += cs_align((size_t)B * 32);
+  w.ctl = o; o += cs_align(16);  // u64 list total, int bad-index flag
   w.fc = o; o += cs_align((size_t)(B * F) * 9 * tsize);
   w.fb = o; o += cs_align((size_t)(B * F) * 16);
   w.cnt = o; o += cs_align((size_t)cells * 4);
@@ -354,41 +368,57 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   const CsWs L = cs_ws_layout(B, F, P, sizeof(T));
   KL_REQUIRE(ws && ws_bytes >= L.total, "check_sign: workspace too small");
   KL_REQUIRE(alloc != nullptr, "check_sign: allocator callback required");
-  const int G = L.G;
-  const int64_t cells = B * (int64_t)G * G;
+  int G = L.G;
   uint8_t *w = (uint8_t *)ws;
   uint32_t *kin = (uint32_t *)(w + L.keys_in), *kout = (uint32_t *)(w + L.keys_out);
   int32_t *vin = (int32_t *)(w + L.vals_in), *vout = (int32_t *)(w + L.vals_out);
   float *tbox = (float *)(w + L.tbox), *mbox = (float *)(w + L.mbox), *fb = (float *)(w + L.fb);
   T *fc = (T *)(w + L.fc);
   int *cnt = (int *)(w + L.cnt), *offs = (int *)(w + L.offs);
+  unsigned long long *d_total = (unsigned long long *)(w + L.ctl);
+  CsFaces<T> fsrc = src;
+  fsrc.bad = (int *)(w + L.ctl + 8);
   const int64_t ntiles = cdiv(F, kCsTile);
-  hipLaunchKernelGGL(cs_prep_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kCsTile), 0, st, F, src, fc, fb,
+  KL_CHECK_RC(fill_async(w + L.ctl, 0, 16, st));
+  hipLaunchKernelGGL(cs_prep_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kCsTile), 0, st, F, fsrc, fc, fb,
                      tbox);
   KL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(cs_meshbox_kernel, dim3((unsigned)B), dim3(256), 0, st, ntiles, G, (const float *)tbox, mbox);
-  KL_CHECK_LAUNCH();
-  KL_CHECK_RC(fill_async(cnt, 0, (size_t)cells * 4, st));
   const dim3 fgrid((unsigned)cdiv(F, 256), (unsigned)B);
-  hipLaunchKernelGGL(cs_bin_kernel<false>, fgrid, dim3(256), 0, st, F, G, (const float *)fb, (const float *)mbox, cnt,
-                     (const int *)nullptr, (int *)nullptr);
-  KL_CHECK_LAUNCH();
+  // The list total is F * (cells per face); many large faces can take it past the int32 scan.
+  // Then the grid is coarsened (G = 1 lists every face once: total <= F < 2^31).
+  struct {
+    unsigned long long total;
+    int bad, pad;
+  } ctl{};
+  for (;;) {
+    hipLaunchKernelGGL(cs_meshbox_kernel, dim3((unsigned)B), dim3(256), 0, st, ntiles, G, (const float *)tbox, mbox);
+    KL_CHECK_LAUNCH();
+    KL_CHECK_RC(fill_async(cnt, 0, (size_t)B * G * G * 4, st));
+    hipLaunchKernelGGL(cs_bin_kernel<false>, fgrid, dim3(256), 0, st, F, G, (const float *)fb, (const float *)mbox,
+                       cnt, (const int *)nullptr, (int *)nullptr, d_total);
+    KL_CHECK_LAUNCH();
+    KL_CHECK_HIP(hipMemcpyAsync(&ctl, d_total, 16, hipMemcpyDeviceToHost, st));
+    KL_CHECK_HIP(hipStreamSynchronize(st));
+    KL_REQUIRE(!ctl.bad, "check_sign: index out of range in self (a face index is outside [0, num_vertices))");
+    // (dev flag 1 << 24: a 2^10 cap, so that tests reach the coarsening on small meshes)
+    const unsigned long long cap = (g_dev_flags & (1 << 24)) ? (1ull << 10) : (1ull << 31);
+    if (ctl.total < cap || G == 1) break;
+    G = G / 2 > 1 ? G / 2 : 1;
+    KL_CHECK_RC(fill_async(d_total, 0, 8, st));
+  }
+  const int64_t total = (int64_t)ctl.total;
+  KL_REQUIRE(total < ((int64_t)1 << 31), "check_sign: face lists too long");
+  const int64_t ncells = B * (int64_t)G * G;
   size_t tb = L.temp_bytes;
-  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, cnt, offs, (int)cells, st));
-  int last[2] = {0, 0};
-  KL_CHECK_HIP(hipMemcpyAsync(&last[0], offs + cells - 1, 4, hipMemcpyDeviceToHost, st));
-  KL_CHECK_HIP(hipMemcpyAsync(&last[1], cnt + cells - 1, 4, hipMemcpyDeviceToHost, st));
-  KL_CHECK_HIP(hipStreamSynchronize(st));
-  const int64_t total = (int64_t)last[0] + last[1];
-  KL_REQUIRE(total >= 0 && total < ((int64_t)1 << 31), "check_sign: face lists too long");
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, cnt, offs, (int)ncells, st));
   int *list = (int *)alloc(alloc_ctx, (size_t)(total > 0 ? total : 1) * 4);
   if (!list) {
     set_error("check_sign: allocator returned NULL");
     return KL_E_ALLOC;
   }
-  KL_CHECK_RC(fill_async(cnt, 0, (size_t)cells * 4, st));
+  KL_CHECK_RC(fill_async(cnt, 0, (size_t)ncells * 4, st));
   hipLaunchKernelGGL(cs_bin_kernel<true>, fgrid, dim3(256), 0, st, F, G, (const float *)fb, (const float *)mbox, cnt,
-                     (const int *)offs, list);
+                     (const int *)offs, list, (unsigned long long *)nullptr);
   KL_CHECK_LAUNCH();
   hipLaunchKernelGGL(cs_key_kernel<T>, dim3((unsigned)cdiv(B * P, 256)), dim3(256), 0, st, B * P, P,
                      (const T *)points, kin, vin);
@@ -410,7 +440,7 @@ template <typename T>
 static int mesh_intersection_unbatched(int64_t P, int64_t F, const void *points, const void *v1, const void *v2,
                                        const void *v3, void *counts, void *ws, size_t ws_bytes, kl_alloc_fn alloc,
                                        void *alloc_ctx, hipStream_t st) {
-  CsFaces<T> src{(const T *)v1, (const T *)v2, (const T *)v3, nullptr, nullptr, nullptr, 0};
+  CsFaces<T> src{(const T *)v1, (const T *)v2, (const T *)v3, nullptr, nullptr, nullptr, 0, nullptr};
   return check_sign_grid<T>(1, F, P, points, src, nullptr, counts, nullptr, ws, ws_bytes, alloc, alloc_ctx, st);
 }
 
@@ -418,7 +448,7 @@ template <typename T>
 static int check_sign_batched(int64_t B, int64_t V, int64_t F, int64_t P, const void *verts, const int64_t *faces,
                               const void *points, const void *maxlen, uint8_t *contains, void *ws, size_t ws_bytes,
                               kl_alloc_fn alloc, void *alloc_ctx, hipStream_t st) {
-  CsFaces<T> src{nullptr, nullptr, nullptr, (const T *)verts, faces, (const T *)maxlen, V};
+  CsFaces<T> src{nullptr, nullptr, nullptr, (const T *)verts, faces, (const T *)maxlen, V, nullptr};
   return check_sign_grid<T>(B, F, P, points, src, maxlen, nullptr, contains, ws, ws_bytes, alloc, alloc_ctx, st);
 }
 

@@ -131,6 +131,14 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int *s_wave, int *tot
   return before + inc - v;
 }
 
+// Adds v of every lane into *dst (64-bit): a wave sum, then one vector atomic per wave.
+// Every lane of the wave must call it (lanes with nothing to add pass 0).
+__device__ __forceinline__ void wave_add_u64(unsigned long long *dst, unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
+}
+
 template <typename T>
 __device__ __forceinline__ T kl_exp(T x);
 template <>

@@ -320,13 +320,19 @@ __device__ __forceinline__ int dt_face_cells(const T *bb, const float *ms, int G
 template <typename T>
 __global__ void __launch_bounds__(256)
     deftet_bin_count_kernel(int64_t F, int G, const T *__restrict__ fvi, const T *__restrict__ bboxes,
-                            const float *__restrict__ mscale, int *__restrict__ fcnt) {
+                            const float *__restrict__ mscale, int *__restrict__ fcnt,
+                            unsigned long long *__restrict__ total) {
   const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (f >= F) return;
-  T bb[4];
-  dt_face_bbox(fvi + b * F * 6, bboxes ? bboxes + b * F * 4 : nullptr, f, bb);
-  int cx0, cy0, nx;
-  fcnt[b * F + f] = dt_face_cells(bb, mscale + b * 4, G, cx0, cy0, nx);
+  int n = 0;
+  if (f < F) {
+    T bb[4];
+    dt_face_bbox(fvi + b * F * 6, bboxes ? bboxes + b * F * 4 : nullptr, f, bb);
+    int cx0, cy0, nx;
+    n = dt_face_cells(bb, mscale + b * 4, G, cx0, cy0, nx);
+    fcnt[b * F + f] = n;
+  }
+  // the list total in 64 bits: the int32 offset scan is used only below 2^31
+  wave_add_u64(total, (unsigned long long)n);
 }
 
 template <typename T>
@@ -757,7 +763,7 @@ static int dt_grid_dim(int64_t F) {  // ~4 faces per cell per layer
 // forward workspace: tile boxes, then (binned path) mesh boxes, per-face counts / offsets,
 // per-cell counts / offsets and the scan scratch
 struct DtFwdWs {
-  size_t tbox, mbox, mscale, fcnt, foff, ccnt, coff, temp, temp_bytes, total;
+  size_t tbox, mbox, mscale, ctl, fcnt, foff, ccnt, coff, temp, temp_bytes, total;
   int G;
 };
 static DtFwdWs dt_fwd_layout(int64_t B, int64_t F, size_t tsize) {
@@ -771,6 +777,7 @@ static DtFwdWs dt_fwd_layout(int64_t B, int64_t F, size_t tsize) {
   w.tbox = o; o += dt_falign((size_t)(B * cdiv(F, kDtTile)) * 4 * tsize);
   w.mbox = o; o += dt_falign((size_t)B * 4 * tsize);
   w.mscale = o; o += dt_falign((size_t)B * 16);
+  w.ctl = o; o += dt_falign(8);  // u64 list total
   w.fcnt = o; o += dt_falign((size_t)(B * F) * 4);
   w.foff = o; o += dt_falign((size_t)(B * F) * 4);
   w.ccnt = o; o += dt_falign((size_t)cells * 4);
@@ -784,7 +791,7 @@ template <typename T>
 static int deftet_forward_binned(int64_t B, int64_t F, int64_t P, int64_t K, const void *fvz, const void *fvi,
                                  const void *bboxes, const void *pix, const void *ranges, float eps, int64_t *idx,
                                  void *depth, void *w0, void *w1, const DtFwdWs &L, uint8_t *w, kl_alloc_fn alloc,
-                                 void *alloc_ctx, hipStream_t st) {
+                                 void *alloc_ctx, hipStream_t st, bool *too_long) {
   const int G = L.G;
   const int64_t cells = B * (int64_t)G * G, BF = B * F, ntiles = cdiv(F, kDtTile);
   T *tbox = (T *)(w + L.tbox), *mbox = (T *)(w + L.mbox);
@@ -794,17 +801,23 @@ static int deftet_forward_binned(int64_t B, int64_t F, int64_t P, int64_t K, con
                      mscale);
   KL_CHECK_LAUNCH();
   const dim3 fgrid((unsigned)cdiv(F, 256), (unsigned)B);
+  unsigned long long *d_total = (unsigned long long *)(w + L.ctl);
+  KL_CHECK_RC(fill_async(d_total, 0, 8, st));
   hipLaunchKernelGGL(deftet_bin_count_kernel<T>, fgrid, dim3(256), 0, st, F, G, (const T *)fvi, (const T *)bboxes,
-                     (const float *)mscale, fcnt);
+                     (const float *)mscale, fcnt, d_total);
   KL_CHECK_LAUNCH();
+  unsigned long long htotal = 0;
+  KL_CHECK_HIP(hipMemcpyAsync(&htotal, d_total, 8, hipMemcpyDeviceToHost, st));
+  KL_CHECK_HIP(hipStreamSynchronize(st));
+  // (dev flag 1 << 24: a 2^10 cap, so that tests reach the fallback on small meshes)
+  const unsigned long long cap = (g_dev_flags & (1 << 24)) ? (1ull << 10) : (1ull << 31);
+  if (htotal >= cap) {  // too many (face, cell) entries: the tile walk
+    *too_long = true;
+    return KL_OK;
+  }
+  const int64_t total = (int64_t)htotal;
   size_t tb = L.temp_bytes;
   KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, fcnt, foff, (int)BF, st));
-  int last[2] = {0, 0};
-  KL_CHECK_HIP(hipMemcpyAsync(&last[0], foff + BF - 1, 4, hipMemcpyDeviceToHost, st));
-  KL_CHECK_HIP(hipMemcpyAsync(&last[1], fcnt + BF - 1, 4, hipMemcpyDeviceToHost, st));
-  KL_CHECK_HIP(hipStreamSynchronize(st));
-  const int64_t total = (int64_t)last[0] + last[1];
-  KL_REQUIRE(total >= 0 && total < ((int64_t)1 << 31), "deftet_sparse_render_forward: face lists too long");
   const int64_t ne = total > 0 ? total : 1;
   size_t ts = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, ts, (const uint32_t *)nullptr, (uint32_t *)nullptr,
@@ -859,9 +872,12 @@ static int deftet_forward(int64_t B, int64_t F, int64_t P, int64_t K, const void
     KL_CHECK_LAUNCH();
   }
   if (alloc && F > 0 && ws_bytes >= L.total && B * F < ((int64_t)1 << 31) &&
-      B * (int64_t)L.G * L.G < ((int64_t)1 << 31))
-    return deftet_forward_binned<T>(B, F, P, K, fvz, fvi, bboxes, pix, ranges, eps, idx, depth, w0, w1, L,
-                                    (uint8_t *)ws, alloc, alloc_ctx, st);
+      B * (int64_t)L.G * L.G < ((int64_t)1 << 31)) {
+    bool too_long = false;
+    const int rc = deftet_forward_binned<T>(B, F, P, K, fvz, fvi, bboxes, pix, ranges, eps, idx, depth, w0, w1, L,
+                                            (uint8_t *)ws, alloc, alloc_ctx, st, &too_long);
+    if (rc || !too_long) return rc;
+  }
   hipLaunchKernelGGL(deftet_fwd_kernel<T>, dim3((unsigned)cdiv(P, kDtTile), (unsigned)B), dim3(kDtTile), 0, st, F, P,
                      (int)K, (const T *)fvz, (const T *)fvi, (const T *)bboxes, (const T *)pix, (const T *)ranges, eps,
                      idx, (T *)depth, (T *)w0, (T *)w1, (const T *)ws);

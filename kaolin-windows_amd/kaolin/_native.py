@@ -11,7 +11,9 @@ import os
 import torch
 
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib')
-LIB_PATH = os.path.join(_LIB_DIR, 'libkaolin_hip.so')
+# KAOLIN_HIP_LIB points at another build of the same library (development builds, e.g.
+# `make STAMPS=1 OUT=...`); the default is the in-tree build
+LIB_PATH = os.environ.get('KAOLIN_HIP_LIB') or os.path.join(_LIB_DIR, 'libkaolin_hip.so')
 
 KL_F32, KL_F64, KL_F16, KL_U8, KL_I8, KL_I16, KL_I32, KL_I64 = range(8)
 _DTYPES = {

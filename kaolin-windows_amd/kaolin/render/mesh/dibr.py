@@ -95,7 +95,7 @@ class DibrRasterizationCuda(Function):
             _fused.soft_mask_backward_compact(grad_soft_mask, soft_mask, state, fvi, ctx.sigmainv, ctx.multiplier,
                                               out=g_img)
         else:
-            scratch.zero_()
+            scratch.data.zero_()  # .data: no version bump of the saved tensor (retain_graph)
         return None, None, None, g_img, g_feat, None, None, None, None, None, None
 
 

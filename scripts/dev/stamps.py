@@ -39,6 +39,8 @@ def main():
     lib.kl_dev_set_debug(None)
     lib.kl_dev_set_flags(0)
     d = dbg.view(nwaves, 12).cpu().numpy().astype(np.uint64)
+    if os.environ.get('STAMPS_DUMP'):
+        np.save(os.environ['STAMPS_DUMP'], d)
     t0, t1, t2, w0, w1 = (d[:, k].astype(np.float64) for k in range(5))
     hits = d[:, 5].astype(np.int64)
     entries = (d[:, 6] >> np.uint64(32)).astype(np.int64)

@@ -133,3 +133,46 @@ def test_gpu_sphere_inside_property(kal):
     far = np.abs(r - 1.0) > 0.01  # the tessellation is within 1e-3 of the sphere
     np.testing.assert_array_equal(out[far], (r < 1.0)[far])
     assert out[far].sum() > 10000
+
+
+def _dev_flags(kal, flags):
+    import ctypes
+    lib = kal._native.lib()
+    lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
+    lib.kl_dev_set_flags(flags)
+
+
+@pytest.mark.gpu
+def test_gpu_list_total_coarsens_grid(kal):
+    """The (y, z) cell lists' total is counted in 64 bits; past the int32 scan's range the grid
+    is coarsened (here forced with a 2^10 test cap, dev flag 1 << 24).  Large faces spanning the
+    whole box plus the sphere: counts still bit-exact."""
+    verts, faces = _uv_sphere(12, 18, 0.8)
+    big = np.array([[-2., -1., -1.], [2., 1.1, -0.9], [0.5, -0.9, 1.2], [0.1, 1., 1.]])
+    verts = np.concatenate([verts, big]).astype(np.float32)
+    n = len(verts) - 4
+    faces = np.concatenate([faces, np.array([[n, n + 1, n + 2], [n + 1, n + 2, n + 3]] * 20)])
+    pts = np.random.default_rng(5).uniform(-1, 1, (3000, 3)).astype(np.float32)
+    v1, v2, v3 = verts[faces[:, 0]], verts[faces[:, 1]], verts[faces[:, 2]]
+    ref = orc.mesh_intersection_counts(pts, v1, v2, v3)
+    _dev_flags(kal, 1 << 24)
+    try:
+        cnt = kal._C.ops.mesh.unbatched_mesh_intersection_cuda(_T(pts), _T(v1), _T(v2), _T(v3))
+        out = kal.ops.mesh.check_sign(_T(verts[None]), _T(faces), _T(pts[None]))
+    finally:
+        _dev_flags(kal, 0)
+    np.testing.assert_array_equal(cnt.cpu().numpy().astype(np.int64), ref)
+    np.testing.assert_array_equal(out.cpu().numpy(), orc.check_sign(verts[None], faces, pts[None]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('bad', [-1, 10 ** 6])
+def test_gpu_face_index_out_of_range_raises(kal, bad):
+    """The reference's index_select raises on an index outside the vertices; so does the batched
+    kernel (a device flag read back with the list total), instead of reading out of bounds."""
+    verts, faces = _uv_sphere(6, 8, 0.8)
+    faces = faces.copy()
+    faces[3, 1] = bad
+    pts = np.zeros((1, 10, 3), np.float32)
+    with pytest.raises(RuntimeError, match='index out of range'):
+        kal.ops.mesh.check_sign(_T(verts[None].astype(np.float32)), _T(faces), _T(pts))

@@ -257,3 +257,22 @@ def test_gpu_binned_and_tile_forward_agree(kal, dtype):
     for x, y, r in zip(a, b, ref):
         np.testing.assert_array_equal(_A(x), _A(y))
         np.testing.assert_array_equal(_A(x), r)
+
+
+@pytest.mark.gpu
+def test_gpu_binned_list_cap_falls_back_to_tile_walk(kal):
+    """The screen-grid lists' total is counted in 64 bits; past the int32 scan's range the forward
+    takes the tile walk (forced here with a 2^10 test cap, dev flag 1 << 24): same slots."""
+    import ctypes
+    pix, ranges, fvz, fvi, feat, K = _grid_case(np.float32, B=2, F=2500, H=30, W=26, seed=9)
+    args = [_T(fvz), _T(fvi), None, _T(pix), _T(ranges), K, 1e-8]
+    lib = kal._native.lib()
+    lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
+    lib.kl_dev_set_flags(1 << 24)
+    try:
+        a = kal._C.deftet_forward('deftet', *args, binned=True)
+    finally:
+        lib.kl_dev_set_flags(0)
+    ref = orc.deftet_sparse_render_forward(fvz, fvi, None, pix, ranges, K, 1e-8)
+    for x, r in zip(a, ref):
+        np.testing.assert_array_equal(_A(x), r)
