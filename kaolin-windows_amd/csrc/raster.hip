@@ -1289,8 +1289,8 @@ namespace kl {
 //   then:   face records | pixel ranges | raster buckets | soft buckets | raster items |
 //           item count | soft order | soft pixel ranges     (records sized for f64)
 struct DibrFwdWs {
-  size_t off_sbm, off_rgh, off_sgh, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder, off_srng,
-      off_defer, bytes;
+  size_t off_sbm, off_rgh, off_sgh, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder, off_sn,
+      off_srng, off_defer, bytes;
   DibrFwdWs(int B, int H, int W, int F) {
     const BinGeom g = make_bin_geom(B, H, W, F);
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
@@ -1306,7 +1306,8 @@ struct DibrFwdWs {
     off_items = up(off_sbk + nt);
     off_n = off_items + nt * TILE_H * sizeof(int32_t);
     off_sorder = up(off_n + sizeof(int));
-    off_srng = up(off_sorder + nt * sizeof(int32_t));
+    off_sn = off_sorder + nt * TILE_H * sizeof(int32_t);
+    off_srng = up(off_sn + sizeof(int));
     off_defer = up(off_srng + (size_t)B * F * sizeof(uint2));
     bytes = off_defer + (size_t)B * H * g.tiles_x;
   }
@@ -1344,6 +1345,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   int32_t *items = reinterpret_cast<int32_t *>(w + L.off_items);
   int *nitems = reinterpret_cast<int *>(w + L.off_n);
   int32_t *sorder = reinterpret_cast<int32_t *>(w + L.off_sorder);
+  int *snitems = reinterpret_cast<int *>(w + L.off_sn);
   uint2 *srng = reinterpret_cast<uint2 *>(w + L.off_srng);
   KL_CHECK_RC(fill_async(w, 0, L.zero, st));
   const RastSrc<T> src{fvi, nullptr, (T)m, fnz};
@@ -1361,15 +1363,16 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   KL_CHECK_LAUNCH();
   const int split_from = 5, split_log2 = sizeof(T) == 4 ? 2 : 0;
   hipLaunchKernelGGL(tile_order2_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh, items,
-                     split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt);
+                     split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt,
+                     soft_lp_min(K), snitems);
   KL_CHECK_LAUNCH();
   const RastTileArgs<T> args{src, fvz, feat, rbm, rec, rng, items, nitems, g, F, D, eps, out_feat, out_idx, out_w,
                              reinterpret_cast<uint64_t *>(g_dev_debug)};
   hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
   KL_CHECK_LAUNCH();
   uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.off_defer);
-  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, sbm, sorder, srng,
-                                   defer, st);
+  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, sbm, sorder, snitems,
+                                   srng, defer, st);
 }
 
 template <typename T>

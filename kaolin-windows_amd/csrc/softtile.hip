@@ -36,14 +36,18 @@
 
 namespace kl {
 
-constexpr int ST_LIST_CAP = 1024;  // face-list entries per workgroup (8 B each)
+// Forward work items (tileorder.h, order_soft_items): a 4-wave workgroup takes 8 >> lp rows of
+// a tile with Q = 4 / (8 >> lp) waves per row.
+constexpr int ST_WAVES = 4;
+
 template <typename T>
 struct SoftTileArgs {
   SoftSrc<T> src;            // unscaled face_vertices_image, multiplier, bbox pad
   const uint2 *rng;          // (B*F) exact pixel ranges of the enlarged bboxes (binning pass)
   const int64_t *sel;        // (B,H,W) rasterized face index
   const uint32_t *bitmap;
-  const int32_t *order;      // tiles, heaviest first
+  const int32_t *order;      // work items, heaviest first
+  const int *nitems;         // their number
   BinGeom g;
   int F, K;
   float sigmainv, m;
@@ -53,37 +57,58 @@ struct SoftTileArgs {
   T *rec_prob;
   int *seg_tot;              // per row segment: its number of hits
   uint8_t *defer;            // per row segment: its hits are left to soft_tile_eval_kernel
-  uint64_t *dbg;             // dev stamps (kl_dev_set_debug), 12 per wave, or nullptr
+  uint64_t *dbg;             // dev stamps (kl_dev_set_debug), 10 per wave, or nullptr
   int dev;                   // dev ablation flags (kl_dev_set_flags), 0 in the product path
 };
 
-__host__ __device__ constexpr size_t st_wave_lds(int K) { return (size_t)K * 64 * sizeof(uint32_t) + 128 * sizeof(int); }
+// LDS of one row: its [K][64] slot lists (face ids, then probabilities in place), the
+// filled-slot prefix and the hit total
+__host__ __device__ constexpr size_t st_row_lds(int K) {
+  return (size_t)K * 64 * sizeof(uint32_t) + 72 * sizeof(int);  // slots | prefix, total
+}
+
+// The workgroup's face list: the candidate chunks' faces touching its rows, in index order
+// (face id; lane interval lo | hi << 6 and row bits << 12), refilled when full.
+constexpr int ST_LIST_CAP = 1024;
 constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int); }
 
+// Forward, one work item (a part of a tile's rows) per 4-wave workgroup.
+//  1. walk (one wave per row): the tile's candidate chunks are read straight from the bin
+//     bitmap, their faces' exact pixel ranges (binning pass) loaded four chunks ahead; each
+//     chunk's 64 faces are tested against the row and, if one of them covers a still-active
+//     pixel (uncovered, < knum hits), their pixel masks are transposed across the wave
+//     (transpose64) so that every active pixel lane appends the covering faces in index order
+//     -- the reference's "first knum faces whose enlarged bbox contains the pixel centre";
+//  2. evaluation: the row's hits, densely, by the Q waves of the row (the reference's distance
+//     and probability), records written contiguously in (pixel, slot) order;
+//  3. the mask, 1 - prod(1 - p) in double in slot order, by the row's first wave.
+// Rows are independent: no workgroup barrier unless Q > 1.
 template <typename T>
-__global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
-  uint64_t *const dbg = kDevStamps ? a.dbg : nullptr;  // compiled out unless KL_DEV_STAMPS
+__global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
+  if ((int)blockIdx.x >= *a.nitems) return;
+  uint64_t *const dbg = kDevStamps ? a.dbg : nullptr;  // compiled out unless KL_DEV_STAMPS
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
-  const int R = blockDim.x >> 6;  // rows (waves) per workgroup, divides TILE_H
   const int K = a.K;
   const BinGeom &g = a.g;
   const int H = g.height, W = g.width;
+  const int item = a.order[blockIdx.x];
+  const int tile = item & 0xffffff, part = (item >> 24) & 15, lp = (item >> 28) & 7;
+  if (kDevStamps && (a.dev & (1 << 16)) && lp < 2) return;  // dev: the heavy items alone
+  const int RP = TILE_H >> lp;      // rows of this part
+  const int Q = ST_WAVES / RP;      // waves per row (lp >= 1: RP <= 4)
+  const int r = wid / Q, qi = wid - r * Q;
   uint32_t *L_face = reinterpret_cast<uint32_t *>(smem);
   uint32_t *L_pack = L_face + ST_LIST_CAP;
-  int *s_cnt = reinterpret_cast<int *>(L_pack + ST_LIST_CAP);  // [8] per-wave scratch
-  unsigned char *mine = smem + st_head_lds() + st_wave_lds(K) * wid;
-  uint32_t *s_face = reinterpret_cast<uint32_t *>(mine);                           // [K][64] face ids
-  int *s_pre = reinterpret_cast<int *>(mine + (size_t)K * 64 * sizeof(uint32_t));  // [64]
-
-  const int per_tile = TILE_H / R;
-  const int tile = a.order[blockIdx.x / per_tile];
+  int *s_wcnt = reinterpret_cast<int *>(L_pack + ST_LIST_CAP);  // [ST_WAVES] per-wave scratch
+  unsigned char *rowmem = smem + st_head_lds() + st_row_lds(K) * r;
+  uint32_t *s_face = reinterpret_cast<uint32_t *>(rowmem);                          // [K][64]
+  int *s_pre = reinterpret_cast<int *>(rowmem + (size_t)K * 64 * sizeof(uint32_t));  // [64], then total
   const int tx = tile % g.tiles_x;
   const int ty = (tile / g.tiles_x) % g.tiles_y;
   const int b = tile / (g.tiles_x * g.tiles_y);
-  const int j0 = ty * TILE_H + (blockIdx.x % per_tile) * R;  // first row of the workgroup
-  const int j = j0 + wid;
+  const int j = ty * TILE_H + part * RP + r;
   const bool row_ok = j < H;
   const int ibase = tx * TILE_W;
   const int i = ibase + lane;
@@ -91,84 +116,66 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   const size_t pix = ((size_t)b * H + (row_ok ? j : H - 1)) * W + (i < W ? i : W - 1);
   const bool covered = px_valid ? (a.sel[pix] >= 0) : true;
   const int64_t f0 = (int64_t)b * a.F;
-  uint64_t t0 = 0, t1 = 0, w0 = 0, c_fill = 0, c_walk = 0, c_sync = 0, tq = 0;
-  uint64_t c_pf = 0, c_test = 0, c_s1 = 0, tr = 0;
-  int n_entries = 0, n_iters = 0, n_groups = 0;
+  const int F = a.F;
+  uint64_t t0 = 0, w0 = 0, t1 = 0, c_fill = 0, tf = 0;
+  int nchunks = 0;
   if (dbg) {
     t0 = stamp_clk();
     w0 = stamp_wall();
   }
 
   int kid = 0;
-  bool active = !covered && K > 0;
+  bool active = !covered && K > 0;  // (every wave of a row tracks its pixels' state)
   uint64_t amask = ballot(active);
-  if (lane == 0) s_cnt[wid] = amask != 0;
+  const int j0 = ty * TILE_H + part * RP;  // the workgroup's first row
+  // any active pixel in the workgroup's rows? (workgroup-uniform)
+  if (lane == 0) s_wcnt[wid] = amask != 0;
   __syncthreads();
   int any = 0;
-  for (int w = 0; w < R; w++) any |= s_cnt[w];
+  for (int w = 0; w < ST_WAVES; w++) any |= s_wcnt[w];
   __syncthreads();
-
   if (any) {
     ChunkSeq seq;
     seq.init(a.bitmap + ((size_t)(b * g.tiles_y + ty) * g.tiles_x + tx) * g.words, g.words, lane);
     const uint2 *rg = a.rng + f0;
-    // this wave's chunk of the next step (chunk ordinal pos + wid) with its pixel ranges in
-    // flight: an unconditional load from a clamped index (a guarded load would be waited
-    // for at once), issued after the current step's ranges are tested so that no copy of
-    // the loaded registers is needed
+    // this wave's chunk of the next fill step (ordinal pos + wid) with its pixel ranges in
+    // flight: an unconditional load from a clamped index (a guarded load is waited for at
+    // once), issued after the current step's ranges are tested
     int pos = 0, nc = -1;
     bool nexists = false;
     uint2 nr = make_uint2(1u, 1u);
     auto pf_next = [&]() {
       nexists = seq.at(pos, lane) >= 0;
       nc = nexists ? seq.at(pos + wid, lane) : -1;
-      pos += R;
+      pos += ST_WAVES;
       int fl = nc * 64 + lane;
-      fl = fl < 0 ? 0 : (fl < a.F ? fl : a.F - 1);
+      fl = fl < 0 ? 0 : (fl < F ? fl : F - 1);
       nr = rg[fl];
     };
     pf_next();
     bool more = nexists;
     while (true) {
-      // ---- 1. expand candidate chunks into the face list, R chunks per step; the next
-      //         step's ranges are in flight while this step's entries are stored and walked
+      // ---- 1a. fill: the candidate chunks' faces that touch the workgroup's rows, in index
+      //          order, with their lane interval and row bits, ST_WAVES chunks per step
       int len = 0;
-      if (dbg) tq = stamp_clk();
-      while (more && len + R * 64 <= ST_LIST_CAP) {
-        if (dbg) tr = stamp_clk();
+      if (dbg) tf = stamp_clk();
+      while (more && len + ST_WAVES * 64 <= ST_LIST_CAP) {
         const int c = nc;
         const int fl = c * 64 + lane;
-        // the face's exact pixel ranges (bin pass) against the workgroup's rows / columns
         const int ix0 = (int)(nr.x & 0xffffu), ix1 = (int)(nr.x >> 16);
         const int iy0 = (int)(nr.y & 0xffffu), iy1 = (int)(nr.y >> 16);
-        const int ya = max(iy0, j0) - j0, yb = min(iy1, j0 + R - 1) - j0;
+        const int ya = max(iy0, j0) - j0, yb = min(iy1, j0 + RP - 1) - j0;
         const uint32_t rows = ya <= yb ? ((2u << yb) - 1u) & ~((1u << ya) - 1u) : 0u;
         const int lo = max(ix0 - ibase, 0), hi = min(ix1 - ibase, 63);
-        const bool keep = c >= 0 && fl < a.F && rows != 0 && lo <= hi;
-        if (dbg) {
-          const uint64_t t = stamp_clk();
-          c_pf += t - tr;
-          tr = t;
-        }
-        pf_next();  // consumed by the next step, in this fill or after the drain
+        const bool keep = c >= 0 && fl < F && rows != 0 && lo <= hi;
+        pf_next();  // consumed by the next step, in this fill or after the walk
         more = nexists;
         const uint64_t km = ballot(keep);
-        if (lane == 0) s_cnt[wid] = __popcll(km);
-        if (dbg) {
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-          const uint64_t t = stamp_clk();
-          c_test += t - tr;
-          tr = t;
-        }
+        if (lane == 0) s_wcnt[wid] = __popcll(km);
         __syncthreads();
-        if (dbg) {
-          const uint64_t t = stamp_clk();
-          c_s1 += t - tr;
-          tr = t;
-        }
         int pre = 0, tot = 0;
-        for (int w = 0; w < R; w++) {
-          const int v = s_cnt[w];
+        for (int w = 0; w < ST_WAVES; w++) {
+          const int v = s_wcnt[w];
           pre += w < wid ? v : 0;
           tot += v;
         }
@@ -179,91 +186,127 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
           L_pack[p] = (uint32_t)lo | ((uint32_t)hi << 6) | (rows << 12);
         }
         len += tot;
-        n_groups++;
         __syncthreads();
       }
-      n_entries += len;
       if (dbg) {
-        const uint64_t t = stamp_clk();
-        c_fill += t - tq;
-        tq = t;
+        nchunks += len;
+        c_fill += stamp_clk() - tf;
       }
-      // ---- 2. this row's walk over the list, 64 entries per step: the entries' pixel
-      //         masks are transposed so that every pixel lane holds the (ordered) entries
-      //         covering it, and appends them until it has knum hits
-      for (int base = 0; base < len && amask; base += 64) {
-        const int e = base + lane;
+      // ---- 1b. walk: per row, the list in blocks of 64 entries; the entries' pixel masks are
+      //          transposed so that every pixel lane holds the (ordered) entries covering it,
+      //          and appends them until it has knum hits.  The Q waves of a row take the
+      //          blocks round-robin, a prefix of their per-pixel counts giving each its slots.
+      const int nb = (len + 63) >> 6;
+      auto block_mask = [&](int blk) -> uint64_t {
+        const int e = blk * 64 + lane;
         uint64_t rm = 0;
         if (e < len) {
           const uint32_t pk = L_pack[e];
-          if ((pk >> (12 + wid)) & 1u) {
+          if ((pk >> (12 + r)) & 1u) {
             const int lo = (int)(pk & 63u), hi = (int)((pk >> 6) & 63u);
             rm = (~0ull >> (63 - hi)) & (~0ull << lo);
           }
         }
-        if (!ballot((rm & amask) != 0)) continue;
-        uint64_t cm = transpose64(rm, lane);
-        if (!active) cm = 0;
-        while (cm) {
-          const int q = __builtin_ctzll(cm);
-          cm &= cm - 1;
-          s_face[kid * 64 + lane] = L_face[base + q];
-          kid++;
-          n_iters++;
-          if (kid >= K) {
-            active = false;
-            cm = 0;
+        return rm;
+      };
+      if (Q == 1) {
+        for (int blk = 0; blk < nb && amask; blk++) {
+          const uint64_t rm = block_mask(blk);
+          if (!ballot((rm & amask) != 0)) continue;
+          uint64_t cm = transpose64(rm, lane);
+          if (!active) cm = 0;
+          const int base = blk * 64;
+          while (cm) {
+            const int q = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            s_face[kid * 64 + lane] = L_face[base + q];
+            if (++kid >= K) {
+              active = false;
+              cm = 0;
+            }
           }
+          amask = ballot(active);
         }
-        amask = ballot(active);
+      } else {
+        // per-wave counts of this round, in the LDS of an unused row (RP <= 2)
+        int *s_cnt = reinterpret_cast<int *>(smem + st_head_lds() + st_row_lds(K) * (RP + r));
+        for (int b0 = 0; b0 < nb; b0 += Q) {  // workgroup-uniform rounds
+          const int blk = b0 + qi;
+          uint64_t cm = 0;
+          if (amask && blk < nb) {
+            const uint64_t rm = block_mask(blk);
+            if (ballot((rm & amask) != 0)) {
+              cm = transpose64(rm, lane);
+              if (!active) cm = 0;
+            }
+          }
+          s_cnt[qi * 64 + lane] = __popcll(cm);
+          __syncthreads();
+          int slot = kid, all = 0;
+          for (int q = 0; q < Q; q++) {
+            const int v = s_cnt[q * 64 + lane];
+            slot += q < qi ? v : 0;
+            all += v;
+          }
+          const int base = blk * 64;
+          while (cm && slot < K) {
+            s_face[slot * 64 + lane] = L_face[base + __builtin_ctzll(cm)];
+            cm &= cm - 1;
+            slot++;
+          }
+          kid = min(K, kid + all);
+          active = active && kid < K;
+          amask = ballot(active);
+          __syncthreads();  // s_cnt is rewritten by the next round
+        }
       }
-      if (dbg) {
-        const uint64_t t = stamp_clk();
-        c_walk += t - tq;
-        tq = t;
-      }
-      if (lane == 0) s_cnt[wid] = amask != 0;
+      if (lane == 0) s_wcnt[wid] = amask != 0;
       __syncthreads();
       any = 0;
-      for (int w = 0; w < R; w++) any |= s_cnt[w];
+      for (int w = 0; w < ST_WAVES; w++) any |= s_wcnt[w];
       __syncthreads();
-      if (dbg) c_sync += stamp_clk() - tq;
       if (!any || !more) break;
     }
   }
-  if (!px_valid) kid = 0;
-  if (dbg) t1 = stamp_clk();
-
-  // ---- 3. the row's hits ((pixel, slot) order) -> records, evaluated here (f32: the heavy
-  //         tiles run first, so their evaluation overlaps the light tiles' selection -- a
-  //         separate evaluation kernel measured 32 us against 10 us added here); f64 leaves
-  //         face ids for soft_tile_eval_kernel and flags its rows for it.
-  int pre = kid;
+  if (qi == 0) {
+    if (!px_valid) kid = 0;
+    int pre = kid;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(pre, o);
-    if (lane >= o) pre += u;
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(pre, o);
+      if (lane >= o) pre += u;
+    }
+    s_pre[lane] = pre - kid;
+    if (lane == 63) s_pre[64] = pre;
   }
-  const int total = __shfl(pre, 63);
-  s_pre[lane] = pre - kid;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (dbg) t1 = stamp_clk();
+  if (Q > 1) {
+    __syncthreads();
+  } else {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  const int total = s_pre[64];
+
+  // ---- 2. the row's hits ((pixel, slot) order) -> records, evaluated here for f32; f64 leaves
+  //         face ids for soft_tile_eval_kernel and flags its rows for it.
   const bool inline_eval = sizeof(T) == 4 && K > 0;
   const size_t rbase = ((size_t)(b * H + (row_ok ? j : 0)) * g.tiles_x + tx) * 64 * (size_t)K;
   if (inline_eval) {
-    // the eval kernel's arithmetic, face ids straight from the slot lists; each slot's
-    // probability replaces its face id in place (same lane, same slot)
+    // face ids straight from the slot lists; each slot's probability replaces its face id in
+    // place (the same thread reads and writes a slot)
     T *s_prob = reinterpret_cast<T *>(s_face);
     const float m = a.m;
     const float sx = m / (float)W, sy = m / (float)H;
     const T y0 = (T)(sy * (float)(H - 2 * (row_ok ? j : 0) - 1));  // == pix_y
     constexpr int U = 4;
-    for (int e0 = lane; e0 < total; e0 += 64 * U) {
+    const int S = 64 * Q;
+    for (int e0 = qi * 64 + lane; e0 < total; e0 += S * U) {
       int pp[U], kk[U];
       uint32_t ff[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int e = e0 + 64 * u;
+        const int e = e0 + S * u;
         int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
 #pragma unroll
         for (int st = 32; st > 0; st >>= 1)
@@ -271,14 +314,14 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
         pp[u] = lo;
         kk[u] = e - s_pre[lo];
         ff[u] = e < total ? s_face[kk[u] * 64 + lo] : 0u;
+        if (kDevStamps && a.dev) ff[u] = min(ff[u], (uint32_t)(F - 1));  // dev ablations leave no face ids
       }
       T v[U][6];
 #pragma unroll
-      for (int u = 0; u < U; u++)
-        if (e0 + 64 * u < total) a.src.verts(f0 + ff[u], v[u]);
+      for (int u = 0; u < U; u++) a.src.verts(f0 + ff[u], v[u]);  // all in flight (ff = 0 past the end)
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int e = e0 + 64 * u;
+        const int e = e0 + S * u;
         if (e < total) {
           T dsq;
           int edgeid;
@@ -291,15 +334,27 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    if (px_valid && kid > 0) {
-      // 1 - prod(1 - p) in double, slot order (dibr_soft_mask_cuda.cu:174-182)
+    if (Q > 1) {
+      __syncthreads();
+    } else {
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
+    if (qi == 0 && px_valid && kid > 0) {
+      // 1 - prod(1 - p) in double, slot order (dibr_soft_mask_cuda.cu:174-182); slots read
+      // eight at a time so that their LDS reads overlap
       T allprob = (T)1.0;
-      for (int k = 0; k < kid; k++) allprob = (T)((double)allprob * (1.0 - (double)s_prob[k * 64 + lane]));
+      for (int k0 = 0; k0 < kid; k0 += 8) {
+        T pk[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) pk[u] = s_prob[min(k0 + u, kid - 1) * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+          if (k0 + u < kid) allprob = (T)((double)allprob * (1.0 - (double)pk[u]));
+      }
       a.mask[pix] = (T)(1.0 - (double)allprob);
     }
-  } else {
+  } else if (qi == 0) {
     for (int e = lane; e < total; e += 64) {
       int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
 #pragma unroll
@@ -308,33 +363,32 @@ __global__ void __launch_bounds__(512) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
       a.rec_face[rbase + e] = s_face[(e - s_pre[lo]) * 64 + lo];
     }
   }
-  if (px_valid) {
-    a.hits[pix] = (uint8_t)kid;
-    if (kid == 0) a.mask[pix] = covered ? (T)1.0 : (T)0.0;  // 1 - prod over no slots = 0
-  }
-  if (row_ok && lane == 0) {
-    a.seg_tot[(size_t)(b * H + j) * g.tiles_x + tx] = total;
-    a.defer[(size_t)(b * H + j) * g.tiles_x + tx] = inline_eval ? 0 : 1;
+  if (qi == 0) {
+    if (px_valid) {
+      a.hits[pix] = (uint8_t)kid;
+      if (kid == 0) a.mask[pix] = covered ? (T)1.0 : (T)0.0;  // 1 - prod over no slots = 0
+    }
+    if (row_ok && lane == 0) {
+      a.seg_tot[(size_t)(b * H + j) * g.tiles_x + tx] = total;
+      a.defer[(size_t)(b * H + j) * g.tiles_x + tx] = inline_eval ? 0 : 1;
+    }
   }
   if (dbg && lane == 0) {
-    uint64_t *d = dbg + ((size_t)blockIdx.x * R + wid) * 12;
+    uint64_t *d = dbg + ((size_t)blockIdx.x * ST_WAVES + wid) * 10;
     d[8] = c_fill;
-    d[9] = c_walk;
-    d[10] = c_sync;
-    d[11] = (c_pf << 42) | ((c_test & 0x1fffff) << 21) | (c_s1 & 0x1fffff);
     d[0] = t0;
     d[1] = t1;
     d[2] = stamp_clk();
     d[3] = w0;
     d[4] = stamp_wall();
-    d[5] = (uint64_t)total;  // (eval stamps t1..t2 are now the record write-out)
-    d[6] = ((uint64_t)n_entries << 32) | (uint32_t)n_iters;
-    d[7] = ((uint64_t)n_groups << 32) | (uint32_t)tile;
+    d[5] = (uint64_t)total;
+    d[6] = ((uint64_t)nchunks << 32) | (uint32_t)(qi | (Q << 8));
+    d[7] = ((uint64_t)(uint32_t)j << 32) | (uint32_t)tile;
   }
 }
 
-// Evaluation of the selected hits: one wave per row segment (4 per workgroup, the tile's
-// rows in the heaviest-first tile order), the hits evaluated densely U x 64 at a time with
+// Evaluation of the selected hits (f64): one wave per row segment (4 per workgroup, tiles in
+// grid order), the hits evaluated densely U x 64 at a time with
 // their vertex loads in flight together, the reference's per-(pixel, face) distance and
 // probability, then 1 - prod(1 - p) in slot order for the pixels with hits.
 template <typename T>
@@ -350,7 +404,7 @@ __global__ void __launch_bounds__(256) soft_tile_eval_kernel(SoftTileArgs<T> a) 
   T *s_prob = reinterpret_cast<T *>(mine);                                  // [K][64]
   int *s_pre = reinterpret_cast<int *>(mine + (size_t)K * 64 * sizeof(T));  // [64]
   const int per_tile = TILE_H / R;
-  const int tile = a.order[blockIdx.x / per_tile];
+  const int tile = blockIdx.x / per_tile;
   const int tx = tile % g.tiles_x;
   const int ty = (tile / g.tiles_x) % g.tiles_y;
   const int b = tile / (g.tiles_x * g.tiles_y);
@@ -401,12 +455,9 @@ __global__ void __launch_bounds__(256) soft_tile_eval_kernel(SoftTileArgs<T> a) 
     for (int u = 0; u < U; u++) {
       const int e = e0 + 64 * u;
       if (e < total) {
-        T dsq = (T)0;
-        int edgeid = 0;
-        if (!(a.dev & (1 << 20)))
-          soft_dist<T>((T)(sx * (float)(2 * (ibase + pp[u]) + 1 - W)), y0, v[u], m, dsq, edgeid);
-        else
-          dsq = v[u][0] + v[u][1] + v[u][2] + v[u][3] + v[u][4] + v[u][5];
+        T dsq;
+        int edgeid;
+        soft_dist<T>((T)(sx * (float)(2 * (ibase + pp[u]) + 1 - W)), y0, v[u], m, dsq, edgeid);
         const T z = (T)a.sigmainv * dsq / (T)m / (T)m;
         const T pr = kl_exp<T>(-z);
         a.rec_face[rbase + e] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
@@ -619,26 +670,29 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
   }
 }
 
-// workspace: bitmap | ghist[32], gdone (zeroed with the bitmap) | tile buckets | tile order |
-// pixel ranges
+// workspace: bitmap | ghist[32], gdone (zeroed with the bitmap) | tile buckets | work items |
+// item count | pixel ranges | defer flags
 struct StWs {
-  size_t hist, zero, bk, order, rng, defer, bytes;
+  size_t hist, zero, bk, order, nitems, rng, defer, bytes;
   StWs(const BinGeom &g, int F) {
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
     hist = g.bytes();
     zero = hist + (ORD_BUCKETS + 1) * sizeof(int);
     bk = (zero + 255) & ~(size_t)255;
     order = (bk + nt + 255) & ~(size_t)255;
-    rng = (order + nt * 4 + 255) & ~(size_t)255;
+    nitems = order + nt * TILE_H * sizeof(int32_t);
+    rng = (nitems + sizeof(int) + 255) & ~(size_t)255;
     defer = (rng + (size_t)g.batch * F * sizeof(uint2) + 255) & ~(size_t)255;
     bytes = defer + (size_t)g.batch * g.height * g.tiles_x;
   }
 };
 
-static int rows_per_wg(int K) {
-  for (int R = 8; R >= 1; R >>= 1)
-    if (st_head_lds() + st_wave_lds(K) * R <= 150 * 1024) return R;
-  return 0;
+// Fewest parts per tile (lp_min >= 1: at most 4 rows per workgroup) whose slot lists fit in
+// 64 KB of LDS (two workgroups per CU); knum near 255 takes one row per workgroup.
+int soft_lp_min(int K) {
+  int lp = 1;
+  while (lp < 3 && st_head_lds() + (size_t)(TILE_H >> lp) * st_row_lds(K) > 64 * 1024) lp++;
+  return lp;
 }
 
 template <typename T>
@@ -651,7 +705,6 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
   KL_REQUIRE(K >= 0 && K <= 255, "dibr_soft_mask: the compact path needs 0 <= knum <= 255");
   KL_REQUIRE(F < (1 << 28), "dibr_soft_mask: too many faces");
   if ((int64_t)B * H * W == 0) return scratch ? fill_async(scratch, 0, sizeof(int), st) : KL_OK;
-  KL_REQUIRE(rows_per_wg(K) > 0, "dibr_soft_mask: knum too large for the LDS slot lists");
   char *w = reinterpret_cast<char *>(ws);
   uint32_t *bitmap = reinterpret_cast<uint32_t *>(w);
   int *ghist = reinterpret_cast<int *>(w + L.hist);
@@ -662,41 +715,38 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
   const int rc = launch_binning<T, SoftSrc<T>>(src, nullptr, F, g, m, bitmap, st, nullptr, L.zero, rng);
   if (rc) return rc;
   const int nt = g.batch * g.tiles_y * g.tiles_x;
-  const int identity = (g_dev_flags >> 12) & 1;  // dev ablation: no heaviest-first order
-  if (!identity) {
-    hipLaunchKernelGGL(tile_bucket_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)bitmap,
-                       g.words, nt, bk, ghist, scratch);
-    KL_CHECK_LAUNCH();
-  } else if (scratch) {
-    KL_CHECK_RC(fill_async(scratch, 0, sizeof(int), st));
-  }
-  hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt,
-                     order, identity, ORD_BUCKETS, 0, nullptr);
+  int *nitems = reinterpret_cast<int *>(w + L.nitems);
+  hipLaunchKernelGGL(tile_bucket_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)bitmap,
+                     g.words, nt, bk, ghist, scratch);
+  KL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(soft_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt, order,
+                     soft_lp_min(K), nitems);
   KL_CHECK_LAUNCH();
   uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.defer);
-  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, sel, sigmainv, pad, m, mask, s, bitmap, order, rng, defer, st);
+  return soft_tile_forward_main<T>(B, H, W, F, K, fvi, sel, sigmainv, pad, m, mask, s, bitmap, order, nitems, rng,
+                                   defer, st);
 }
 
 // The selection and evaluation kernels on bins made by the caller: bitmap (SoftSrc bins),
-// heaviest-first tile order and the exact pixel ranges of the enlarged bboxes; s.scratch
-// already zeroed.
+// work items (order_soft_items with lp_min = soft_lp_min(K)) and their count, and the exact
+// pixel ranges of the enlarged bboxes; s.scratch already zeroed.
 template <typename T>
 int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv,
                            double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
-                           const int32_t *order, const uint2 *rng, uint8_t *defer, hipStream_t st) {
+                           const int32_t *order, const int *nitems, const uint2 *rng, uint8_t *defer,
+                           hipStream_t st) {
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   if (nt == 0) return KL_OK;
-  int R = rows_per_wg(K);
-  KL_REQUIRE(R > 0, "dibr_soft_mask: knum too large for the LDS slot lists");
-  const int dev_r = (g_dev_flags >> 8) & 15;  // dev override of the rows per workgroup (ablation)
-  if (dev_r && dev_r <= R && TILE_H % dev_r == 0) R = dev_r;
+  const int lp_min = soft_lp_min(K);
+  const size_t lds = st_head_lds() + (size_t)(TILE_H >> lp_min) * st_row_lds(K);
+  KL_REQUIRE(lds <= 160 * 1024, "dibr_soft_mask: knum too large for the LDS slot lists");
   const SoftSrc<T> src{fvi, (T)m, (T)pad};
-  SoftTileArgs<T> args{src,      rng,  sel,  bitmap,  order,      g,          F,          K,
-                       sigmainv, m,    mask, s.hits, s.rec_face, s.rec_prob, s.seg_tot, defer,
-                       (uint64_t *)g_dev_debug, g_dev_flags};
-  const size_t lds = st_head_lds() + st_wave_lds(K) * R;
-  hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)(nt * (TILE_H / R))), dim3(64 * R), lds, st, args);
+  SoftTileArgs<T> args{src, rng,  sel,    bitmap, order,      nitems,     g,         F,     K,
+                       sigmainv, m, mask, s.hits, s.rec_face, s.rec_prob, s.seg_tot, defer, (uint64_t *)g_dev_debug,
+                       g_dev_flags};
+  hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)soft_items_bound(nt, lp_min)), dim3(64 * ST_WAVES), lds,
+                     st, args);
   KL_CHECK_LAUNCH();
   if (K > 0 && sizeof(T) != 4) {  // f64: the rows left for the evaluation kernel
     const size_t ew = (size_t)K * 64 * sizeof(T) + 64 * sizeof(int);
@@ -747,10 +797,10 @@ template int soft_tile_forward<double>(int, int, int, int, int, const double *, 
                                        float, double *, const SoftState<double> &, void *, size_t, hipStream_t);
 template int soft_tile_forward_main<float>(int, int, int, int, int, const float *, const int64_t *, float, double,
                                            float, float *, const SoftState<float> &, const uint32_t *,
-                                           const int32_t *, const uint2 *, uint8_t *, hipStream_t);
+                                           const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t);
 template int soft_tile_forward_main<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
                                             float, double *, const SoftState<double> &, const uint32_t *,
-                                            const int32_t *, const uint2 *, uint8_t *, hipStream_t);
+                                            const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t);
 template int soft_tile_backward<float>(int, int, int, int, int, const float *, const float *,
                                        const SoftState<float> &, const float *, float, float, float *, bool, void *,
                                        size_t, hipStream_t);

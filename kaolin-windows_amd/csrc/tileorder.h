@@ -71,6 +71,53 @@ __device__ __forceinline__ void order_items(int *base, const uint8_t *__restrict
   }
 }
 
+// Soft-mask work items (softtile.hip), heaviest first: tile | part << 24 | lp << 28.  A tile's
+// 8 rows are cut into 2^lp parts of 8 >> lp rows, one 4-wave workgroup per part.  lp is lp_min
+// (set by the LDS the slot lists need) except for the heaviest buckets: >= ST_B8 candidate-chunk
+// bucket -> 8 parts (one row, 4 waves sharing its evaluation), >= ST_B4 -> 4 parts (2 rows,
+// 2 waves each), at most ST_CAP8 / ST_CAP4 tiles each, so that soft_items_bound() holds.
+constexpr int ST_B4 = 5, ST_B8 = 6, ST_CAP4 = 256, ST_CAP8 = 128;
+inline int soft_items_bound(int nt, int lp_min) {
+  auto extra = [&](int lp, int cap) { return lp > lp_min ? cap * ((1 << lp) - (1 << lp_min)) : 0; };
+  return (nt << lp_min) + extra(2, ST_CAP4) + extra(3, ST_CAP8);
+}
+__device__ __forceinline__ void order_soft_items(int *base, int *lpb, const uint8_t *__restrict__ bk,
+                                                 const int *__restrict__ ghist, int nt, int32_t *__restrict__ order,
+                                                 int lp_min, int *__restrict__ nitems) {
+  if (threadIdx.x == 0) {
+    int s = 0, n4 = 0, n8 = 0;
+    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
+      const int h = ghist[q];
+      int lp = lp_min;
+      if (q >= ST_B8 && n8 + h <= ST_CAP8) {
+        lp = lp > 3 ? lp : 3;
+        n8 += h;
+      } else if (q >= ST_B4 && n4 + h <= ST_CAP4) {
+        lp = lp > 2 ? lp : 2;
+        n4 += h;
+      }
+      lpb[q] = lp;
+      base[q] = s;
+      s += h << lp;
+    }
+    *nitems = s;
+  }
+  __syncthreads();
+  for (int u = threadIdx.x; u < nt; u += blockDim.x) {
+    const int q = bk[u], lp = lpb[q], np = 1 << lp;
+    const int o = atomicAdd(&base[q], np);
+    for (int k = 0; k < np; k++) order[o + k] = u | (k << 24) | (lp << 28);
+  }
+}
+
+static __global__ void __launch_bounds__(1024) soft_order_kernel(const uint8_t *__restrict__ bk,
+                                                                 const int *__restrict__ ghist, int nt,
+                                                                 int32_t *__restrict__ order, int lp_min,
+                                                                 int *__restrict__ nitems) {
+  __shared__ int base[ORD_BUCKETS], lpb[ORD_BUCKETS];
+  order_soft_items(base, lpb, bk, ghist, nt, order, lp_min, nitems);
+}
+
 static __global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *__restrict__ bk,
                                                                  const int *__restrict__ ghist, int nt,
                                                                  int32_t *__restrict__ order, int identity,
@@ -81,7 +128,8 @@ static __global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *
 }
 
 // Two bitmaps over the same tiles at once (kl_dibr_forward: the rasterizer's and the soft
-// mask's bins): one wave per tile counts both.
+// mask's bins): one wave per tile counts both; the order kernel writes the rasterizer's items
+// and the soft mask's (order_soft_items).
 static __global__ void __launch_bounds__(256) tile_bucket2_kernel(const uint32_t *__restrict__ bm0,
                                                                   const uint32_t *__restrict__ bm1, int words, int nt,
                                                                   uint8_t *__restrict__ bk0, uint8_t *__restrict__ bk1,
@@ -125,10 +173,11 @@ static __global__ void __launch_bounds__(1024) tile_order2_kernel(const uint8_t 
                                                                   int split_log2, int *__restrict__ nitems0,
                                                                   const uint8_t *__restrict__ bk1,
                                                                   const int *__restrict__ gh1,
-                                                                  int32_t *__restrict__ order1, int nt) {
-  __shared__ int base[2][ORD_BUCKETS];
+                                                                  int32_t *__restrict__ order1, int nt, int lp_min1,
+                                                                  int *__restrict__ nitems1) {
+  __shared__ int base[2][ORD_BUCKETS], lpb[ORD_BUCKETS];
   order_items(base[0], bk0, gh0, nt, order0, 0, split_from, split_log2, nitems0);
-  order_items(base[1], bk1, gh1, nt, order1, 0, ORD_BUCKETS, 0, nullptr);
+  order_soft_items(base[1], lpb, bk1, gh1, nt, order1, lp_min1, nitems1);
 }
 
 }  // namespace kl

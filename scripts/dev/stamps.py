@@ -1,10 +1,12 @@
 """Per-wave timing stamps of the compact soft-mask forward (development aid).
 
 Runs soft_mask_forward_compact on the bench workload with the library's dev stamp buffer
-(kl_dev_set_debug) and prints where the waves spend their cycles: selection (steps 1-2)
-and evaluation (step 3), the slowest waves and the wall-clock span.
-usage: python scripts/dev/stamps.py [knum] [rows per workgroup]
+(kl_dev_set_debug; a `make STAMPS=1` build, loaded through KAOLIN_HIP_LIB) and prints where
+the waves spend their cycles: walk (step 1) and evaluation + mask (steps 2-3), the slowest
+rows and the wall-clock span.  10 stamps per wave (softtile.hip, soft_tile_fwd_kernel).
+usage: python scripts/dev/stamps.py [knum]      (STAMPS_DUMP=path.npy saves the raw stamps)
 """
+import collections
 import ctypes
 import os
 import sys
@@ -20,61 +22,58 @@ from kaolin import _fused, _native as N  # noqa: E402
 
 def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 30
-    rows = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     lib = N.lib()
     lib.kl_dev_set_debug.argtypes = [ctypes.c_void_p]
     lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
-    lib.kl_dev_set_flags(rows << 8)
+    flags = int(os.environ.get('STAMPS_FLAGS', '0'), 0)
     inp = bench.dibr_inputs([0.0, 1.5707963, 3.1415927, 4.712389], 'cuda')
     H, W = inp['H'], inp['W']
     valid = inp['fnz'] >= 0
     _, idx, _ = _fused.rasterize_forward(H, W, inp['fvz'], inp['fvi'], inp['feat'], valid, 1000., 1e-8)
-    nwaves = 4 * H * (W // 64)
-    dbg = torch.zeros(nwaves * 12, dtype=torch.int64, device='cuda')
+    nwaves = 4 * (H // 8) * (W // 64) * 8 * 4  # grid bound (tiles x 8 parts x 4 waves)
+    dbg = torch.zeros(nwaves * 10, dtype=torch.int64, device='cuda')
     for _ in range(3):
         _fused.soft_mask_forward_compact(inp['fvi'], idx, 7000., 0.02, K, 1000.)
     lib.kl_dev_set_debug(ctypes.c_void_p(dbg.data_ptr()))
+    lib.kl_dev_set_flags(flags)
     _fused.soft_mask_forward_compact(inp['fvi'], idx, 7000., 0.02, K, 1000.)
     torch.cuda.synchronize()
-    lib.kl_dev_set_debug(None)
     lib.kl_dev_set_flags(0)
-    d = dbg.view(nwaves, 12).cpu().numpy().astype(np.uint64)
+    lib.kl_dev_set_debug(None)
+    d = dbg.view(nwaves, 10).cpu().numpy().astype(np.uint64)
+    d = d[d[:, 3] != 0]
     if os.environ.get('STAMPS_DUMP'):
         np.save(os.environ['STAMPS_DUMP'], d)
     t0, t1, t2, w0, w1 = (d[:, k].astype(np.float64) for k in range(5))
     hits = d[:, 5].astype(np.int64)
-    entries = (d[:, 6] >> np.uint64(32)).astype(np.int64)
-    iters = (d[:, 6] & np.uint64(0xffffffff)).astype(np.int64)
-    groups = (d[:, 7] >> np.uint64(32)).astype(np.int64)
+    nch = (d[:, 6] >> np.uint64(32)).astype(np.int64)
+    qi = (d[:, 6] & np.uint64(0xff)).astype(np.int64)
+    Q = ((d[:, 6] >> np.uint64(8)) & np.uint64(0xff)).astype(np.int64)
+    row = (d[:, 7] >> np.uint64(32)).astype(np.int64)
     tile = (d[:, 7] & np.uint64(0xffffffff)).astype(np.int64)
-    c_fill, c_walk, c_sync = (d[:, k].astype(np.float64) for k in (8, 9, 10))
-    c_pf = (d[:, 11] >> np.uint64(42)).astype(np.float64)
-    c_test = ((d[:, 11] >> np.uint64(21)) & np.uint64(0x1fffff)).astype(np.float64)
-    c_s1 = (d[:, 11] & np.uint64(0x1fffff)).astype(np.float64)
-    sel = t1 - t0
-    ev = t2 - t1
-    span_us = (w1.max() - w0.min()) / 100.0
-    print(f'knum={K} rows/WG={rows or "default"} waves={nwaves} wall span {span_us:.1f} us')
-    print(f'cycles/wave: selection mean {sel.mean():.0f} max {sel.max():.0f} | eval mean {ev.mean():.0f} '
-          f'max {ev.max():.0f} | sum over waves {(sel.sum() + ev.sum()) / 1e6:.1f} Mcyc')
-    print(f'totals: hits {hits.sum()} list entries {entries.sum()} face iterations {iters.sum()} '
-          f'groups {groups.sum()}')
+    walk, ev = t1 - t0, t2 - t1
+    fill = d[:, 8].astype(np.float64)
     start_us = (w0 - w0.min()) / 100.0
     end_us = (w1 - w0.min()) / 100.0
+    span = end_us.max()
+    print(f'knum={K} waves={len(d)} wall span {span:.1f} us; waves by Q: '
+          f'{dict(collections.Counter(Q.tolist()))}')
+    lead = qi == 0
+    hot = lead & (hits > 0)
+    print(f'rows with hits: {hot.sum()}  walk cycles mean {walk[hot].mean():.0f} max {walk[hot].max():.0f} | '
+          f'eval+mask mean {ev[hot].mean():.0f} max {ev[hot].max():.0f} | fill (in walk) mean {fill[hot].mean():.0f} '
+          f'max {fill[hot].max():.0f} | list entries mean {nch[hot].mean():.1f}')
+    print(f'rows without hits: {(lead & (hits == 0)).sum()}  duration mean '
+          f'{(end_us - start_us)[lead & (hits == 0)].mean():.2f} us')
     for q in (0.5, 0.9, 0.99, 1.0):
         print(f'  wave end quantile {q}: {np.quantile(end_us, q):.1f} us, start {np.quantile(start_us, q):.1f} us')
-    order = np.argsort(-(sel + ev))[:12]
-    print(f'selection split (mean cycles): fill {c_fill.mean():.0f} walk {c_walk.mean():.0f} sync {c_sync.mean():.0f}')
-    print(f'fill split (mean cycles): prefetch {c_pf.mean():.0f} test(+load wait) {c_test.mean():.0f} '
-          f'sync1 {c_s1.mean():.0f}; heaviest wave: {c_pf[np.argmax(c_fill)]:.0f} {c_test[np.argmax(c_fill)]:.0f} '
-          f'{c_s1[np.argmax(c_fill)]:.0f} of {c_fill.max():.0f}')
-    print('slowest waves: tile  start_us end_us  sel_cyc (fill walk sync) eval_cyc  hits entries iters groups')
+    order = np.argsort(-(end_us - start_us) * lead)[:12]
+    print('slowest rows: tile row Q start_us end_us walk_cyc eval_cyc hits chunks')
     for k in order:
-        print(f'  {tile[k]:6d} {start_us[k]:7.1f} {end_us[k]:7.1f} {sel[k]:8.0f} ({c_fill[k]:7.0f} {c_walk[k]:7.0f} '
-              f'{c_sync[k]:6.0f}) {ev[k]:8.0f} {hits[k]:5d} {entries[k]:6d} {iters[k]:5d} {groups[k]:4d}')
-    # busy-wave histogram over time (concurrency)
-    bins = np.linspace(0, span_us, 21)
-    busy = [((start_us <= b) & (end_us > b)).sum() for b in bins[:-1]]
+        print(f'  {tile[k]:6d} {row[k]:4d} {Q[k]} {start_us[k]:7.1f} {end_us[k]:7.1f} {walk[k]:8.0f} {ev[k]:8.0f} '
+              f'{hits[k]:5d} {nch[k]:4d}')
+    bins = np.linspace(0, span, 21)
+    busy = [int(((start_us <= b) & (end_us > b)).sum()) for b in bins[:-1]]
     print('waves in flight every 5% of the span:', busy)
 
 
