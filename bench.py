@@ -411,6 +411,16 @@ def dibr_parity_and_cpu(inp, row_step):
     rmask[:, rows] = 1
     _, gfvi, gfeat, mask, idx, feats = dibr_compute(inp, inp['g_feat'] * rmask.unsqueeze(-1), inp['g_mask'] * rmask)
     torch.cuda.synchronize()
+    # the soft-mask backward's parity on identical saved values: the GPU forward's mask and
+    # probabilities (equal to the oracle's to expf ulps, reported as max_abs_mask)
+    from kaolin import _fused
+    _, state = _fused.soft_mask_forward_compact(inp['fvi'], idx, 7000., 0.02, 30, 1000.)
+    _, _, gp = orc.decode_compact(A(state.hits), A(state.rec_face), A(state.rec_prob), 30, rows=rows)
+    orc.lib().or_set_row_step(row_step)
+    try:
+        gi_s = orc.dibr_soft_mask_backward(gm, A(mask), oi, gp, oci, oct_, fm, 7000., 1000.)
+    finally:
+        orc.lib().or_set_row_step(1)
     gi_o, gfe_o = gi_r + gi_s, gf_r
     gi_g, gfe_g = A(gfvi), A(gfeat)
     scale_i = float(np.abs(gi_o).max())
@@ -423,6 +433,10 @@ def dibr_parity_and_cpu(inp, row_step):
         'max_abs_grad_feat': float(np.abs(gfe_g - gfe_o).max()),
         'max_abs_grad_fvi_reference_magnitude': scale_i,
         'grad_fvi_elems_over_1e-5': int((np.abs(gi_g - gi_o) > 1e-5).sum()),
+        'grad_fvi_equal': bool(np.array_equal(gi_g, gi_o)),
+        'grad_feat_equal': bool(np.array_equal(gfe_g, gfe_o)),
+        'grad_note': 'both sides sum the float terms in double and round once; the soft-mask '
+                     'backward runs on the GPU forward\'s saved mask / probabilities',
     }
     cpu = {'value': round(npx / dt / 1e6, 5), 'unit': 'Mpixels/s', 'cores': 1, 'kind': 'port',
            'sample': f'C oracle (restatement of the reference CUDA path), {fvz.shape[0]} views, every {row_step}th '

@@ -81,13 +81,17 @@ int kl_packed_rasterize_forward(kl_dtype dtype, int height, int width, int batch
 
 /* rasterization.cpp:106-168  rasterize_backward_cuda.
  * face_idx: (B,H,W) ORIGINAL face index per mesh; face_vertices_image (B,F,3,2) unscaled.
- * Outputs (fully written): grad_face_vertices_image (B,F,3,2), grad_face_features (B,F,3,D). */
+ * Outputs (fully written): grad_face_vertices_image (B,F,3,2), grad_face_features (B,F,3,D).
+ * The reference's per-pixel float terms are summed in double (workspace:
+ * kl_rasterize_backward_workspace_bytes) and rounded once, so the result does not depend on the
+ * order of the atomics (the reference's float atomics make it run-to-run nondeterministic). */
+size_t kl_rasterize_backward_workspace_bytes(int batch, int num_faces, int feat_dim);
 int kl_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
                           const void *grad_interpolated_features, const int64_t *face_idx,
                           const void *output_weights, const void *face_vertices_image,
                           const void *face_features, float eps,
                           void *grad_face_vertices_image, void *grad_face_features,
-                          kl_stream stream);
+                          void *workspace, size_t workspace_bytes, kl_stream stream);
 
 /* Fused front-end path of rasterize() / RasterizeCuda (rasterization.py:290-388): takes the
  * UNPACKED (B,F) inputs and the optional (B,F) valid mask (uint8/bool) -- or, when it is
@@ -105,11 +109,14 @@ int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, int batch, 
                               void *workspace, size_t workspace_bytes, kl_stream stream);
 /* Atomic-free backward of the fused path: 8 lanes per face gather the pixels of the face's
  * exact pixel range (the reference's bbox test, same valid_faces / multiplier as the forward)
- * whose face_idx equals it (deterministic, row-major order).  Requires face_idx produced by
- * the fused forward with the same valid_faces and multiplier.  Every face's gradient is
- * written (zeros where it won no pixel).  scratch: NULL, or a zeroed int32 the call uses as
- * its big-face counter instead of zeroing one in the workspace (kl_dibr_forward).
- * face_ranges: NULL, or kl_dibr_forward's per-face ranges (then the ranges are not recomputed). */
+ * whose face_idx equals it, summing the reference's float terms in double (rounded once:
+ * deterministic and order-independent).  Requires face_idx produced by the fused forward with
+ * the same valid_faces and multiplier.  Every face's gradient is written (zeros where it won no
+ * pixel).  scratch: NULL, or a zeroed int32 the call uses as its big-face counter instead of
+ * zeroing one in the workspace (kl_dibr_forward).  face_ranges: NULL, or kl_dibr_forward's
+ * per-face ranges (then the ranges are not recomputed).  feat_dim > 8 takes the scatter path
+ * of kl_rasterize_backward.  workspace: kl_dibr_rasterize_bwd_workspace_bytes. */
+size_t kl_dibr_rasterize_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int feat_dim);
 int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
                                const void *grad_interpolated_features, const int64_t *face_idx,
                                const void *output_weights, const void *face_vertices_image,
@@ -144,13 +151,15 @@ int kl_dibr_soft_mask_forward_fused(kl_dtype dtype, int batch, int height, int w
                                     uint8_t *close_face_dist_type, uint8_t *hits, void *workspace,
                                     size_t workspace_bytes, kl_stream stream);
 /* hits: the forward's per-pixel slot counts, or NULL to scan the slots up to the first -1
- * as the reference does. */
+ * as the reference does.  workspace: kl_soft_mask_backward_workspace_bytes (see
+ * kl_dibr_soft_mask_backward). */
 int kl_dibr_soft_mask_backward_fused(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
                                      const void *grad_soft_mask, const void *soft_mask,
                                      const int64_t *selected_face_idx, const void *close_face_prob,
                                      const int64_t *close_face_idx, const uint8_t *close_face_dist_type,
                                      const uint8_t *hits, const void *face_vertices_image, float sigmainv,
-                                     float multiplier, void *grad_face_vertices_image, kl_stream stream);
+                                     float multiplier, void *grad_face_vertices_image, void *workspace,
+                                     size_t workspace_bytes, kl_stream stream);
 
 /* Compact fused path of DibrSoftMaskCuda (dibr.py:27-73), the one the front-end runs
  * (knum <= 255).  The reference saves four (B,H,W,knum) slot tensors for its backward
@@ -174,9 +183,11 @@ int kl_dibr_soft_mask_forward_compact(kl_dtype dtype, int batch, int height, int
                                       float sigmainv, double bbox_pad, float multiplier, void *soft_mask,
                                       uint8_t *hits, uint32_t *rec_face, void *rec_prob, int *seg_tot, int *scratch,
                                       void *workspace, size_t workspace_bytes, kl_stream stream);
-/* dibr_soft_mask.cpp:110-183 on the compact state.  accumulate = 0: grad_face_vertices_image
- * is overwritten; 1: the terms are added onto its contents.  scratch is left zeroed. */
-size_t kl_soft_mask_compact_bwd_workspace_bytes(int batch, int height, int width, int knum);
+/* dibr_soft_mask.cpp:110-183 on the compact state.  The terms are summed in double and
+ * rounded once (order-independent); accumulate = 0: grad_face_vertices_image is overwritten
+ * with that sum; 1: the rounded sum is added onto its contents (one float add, as autograd
+ * adds the soft-mask gradient to the rasterizer's).  scratch is left zeroed. */
+size_t kl_soft_mask_compact_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum);
 int kl_dibr_soft_mask_backward_compact(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
                                        const void *grad_soft_mask, const void *soft_mask, const uint8_t *hits,
                                        const uint32_t *rec_face, const void *rec_prob, const int *seg_tot,
@@ -188,10 +199,12 @@ int kl_dibr_soft_mask_backward_compact(kl_dtype dtype, int batch, int height, in
  * valid_faces = face_normals_z >= 0 (evaluated in-kernel), then the compact soft mask on
  * its face index.  Outputs: interpolated_features (B,H,W,D), face_idx (B,H,W) int64,
  * output_weights (B,H,W,3), soft_mask (B,H,W), and the compact soft-mask state (hits,
- * rec_face, rec_prob, seg_tot, scratch as above; the backward uses scratch as the
- * rasterizer gather's big-face counter and leaves it zeroed, so it needs no fill).  The
- * backward writes grad_face_vertices_image / grad_face_features (every face): the
- * rasterizer's gather terms plus the soft-mask terms (grad_soft_mask may be NULL).
+ * rec_face, rec_prob, seg_tot, scratch as above; the backward's soft-mask stage zeroes scratch
+ * and the rasterizer gather then uses it as its big-face counter).  The backward writes
+ * grad_face_vertices_image / grad_face_features (every face): the soft-mask terms are summed in
+ * double first, then the gather writes each face's gradient as the rounded sum of its own
+ * terms (double) plus the soft mask's rounded sum -- autograd's add of the two gradients in
+ * the reference (grad_soft_mask may be NULL).
  * face_ranges: NULL, or (B*F) x 2 uint32 the forward fills with each face's exact pixel
  * ranges (x0 | x1 << 16, y0 | y1 << 16; empty for invalid faces) for the backward to reuse.
  * feat_dim <= 8.  Workspaces: kl_dibr_workspace_bytes (forward),
@@ -214,13 +227,17 @@ int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width, int num_f
                      kl_stream stream);
 
 /* dibr_soft_mask.cpp:110-183  dibr_soft_mask_backward_cuda.
- * Output grad_face_vertices_image (B,F,3,2) (fully written). */
+ * Output grad_face_vertices_image (B,F,3,2) (fully written): the reference's per-hit float
+ * terms summed in double (workspace: kl_soft_mask_backward_workspace_bytes) and rounded once,
+ * independent of the order of the atomics. */
+size_t kl_soft_mask_backward_workspace_bytes(int batch, int num_faces);
 int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int knum,
                                const void *grad_soft_mask, const void *soft_mask,
                                const int64_t *selected_face_idx, const void *close_face_prob,
                                const int64_t *close_face_idx, const uint8_t *close_face_dist_type,
                                const void *face_vertices_image, float sigmainv, float multiplier,
-                               void *grad_face_vertices_image, kl_stream stream);
+                               void *grad_face_vertices_image, void *workspace, size_t workspace_bytes,
+                               kl_stream stream);
 
 /* ------------------------------------------------------------ DefTet sparse render */
 

@@ -29,6 +29,11 @@ __device__ __forceinline__ uint64_t stamp_clk() { return __builtin_readcyclecoun
 __device__ __forceinline__ uint64_t stamp_wall() { return __builtin_amdgcn_s_memrealtime(); }
 // memset as a kernel launch on `st` (graph-capture friendly); returns a kl_status
 int fill_async(void *p, int value, size_t bytes, hipStream_t st);
+// out[i] = (T)acc[i], or out[i] + (T)acc[i] with accumulate: the single rounding of a gradient
+// summed in double (raster.hip)
+template <typename T>
+int acc_finalize(const double *acc, T *out, size_t n, bool accumulate, hipStream_t st);
+inline size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 #define KL_CHECK_HIP(expr)                                                              \
   do {                                                                                  \

@@ -891,11 +891,33 @@ struct BaryGrad {
   }
 };
 
+// The single rounding of a gradient summed in double (common.h).
+template <typename T>
+__global__ void __launch_bounds__(256) acc_finalize_kernel(const double *__restrict__ acc, T *__restrict__ out,
+                                                           size_t n, int accumulate) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    out[i] = accumulate ? out[i] + (T)acc[i] : (T)acc[i];
+}
+template <typename T>
+int acc_finalize(const double *acc, T *out, size_t n, bool accumulate, hipStream_t st) {
+  if (n == 0) return KL_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>(cdiv((int64_t)n, 256), 8192);
+  hipLaunchKernelGGL((acc_finalize_kernel<T>), dim3(blocks), dim3(256), 0, st, acc, out, n, accumulate ? 1 : 0);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+template int acc_finalize<float>(const double *, float *, size_t, bool, hipStream_t);
+template int acc_finalize<double>(const double *, double *, size_t, bool, hipStream_t);
+
+// The _C contract's scatter backward (rasterize_backward_cuda takes no multiplier, so the
+// faces' pixel ranges are unknown): one thread per pixel, the reference's terms added with
+// global atomics into double accumulators, rounded once (acc_finalize) -- the order of the
+// atomics does not change the result (the float terms sum exactly in double).
 template <typename T>
 __global__ void __launch_bounds__(256) rasterize_bwd_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
     const T *__restrict__ fvi, const T *__restrict__ feat, int B, int H, int W, int F, int D, float eps,
-    T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat) {
+    double *__restrict__ grad_fvi, double *__restrict__ grad_ffeat) {
   const int64_t npix = (int64_t)H * W;
   for (int64_t tp = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; tp < (int64_t)B * npix;
        tp += (int64_t)gridDim.x * blockDim.x) {
@@ -907,9 +929,9 @@ __global__ void __launch_bounds__(256) rasterize_bwd_kernel(
     const T w_a = wts[tp * 3 + 0], w_b = wts[tp * 3 + 1], w_c = wts[tp * 3 + 2];
     for (int d = 0; d < D; d++) {
       const T gd = g[d];
-      atomicAdd(grad_ffeat + tf * 3 * D + d, gd * w_a);
-      atomicAdd(grad_ffeat + tf * 3 * D + D + d, gd * w_b);
-      atomicAdd(grad_ffeat + tf * 3 * D + 2 * D + d, gd * w_c);
+      atomicAdd(grad_ffeat + tf * 3 * D + d, (double)(gd * w_a));
+      atomicAdd(grad_ffeat + tf * 3 * D + D + d, (double)(gd * w_b));
+      atomicAdd(grad_ffeat + tf * 3 * D + 2 * D + d, (double)(gd * w_c));
     }
     T v[6];
 #pragma unroll
@@ -917,12 +939,12 @@ __global__ void __launch_bounds__(256) rasterize_bwd_kernel(
     BaryGrad<T> bg;
     bg.init(v, w_a, w_b, w_c, eps);
     const T *c = feat + tf * 3 * D;
-    T *gv = grad_fvi + tf * 6;
+    double *gv = grad_fvi + tf * 6;
     for (int d = 0; d < D; d++) {
       T o[6];
       bg.terms(g[d], c[d], c[D + d], c[2 * D + d], o);
 #pragma unroll
-      for (int q = 0; q < 6; q++) atomicAdd(gv + q, o[q]);
+      for (int q = 0; q < 6; q++) atomicAdd(gv + q, (double)o[q]);
     }
   }
 }
@@ -954,15 +976,18 @@ __device__ __forceinline__ bool rng_range(const uint2 *rng, int64_t tf, int &ix0
   return ix0 <= ix1 && iy0 <= iy1;
 }
 
+// Per-face sums of the reference's float terms, in double: they are exact whenever the terms'
+// magnitudes span less than ~2^29, so the rounded result does not depend on the order of the
+// adds (lanes, butterfly) -- it equals the oracle's, which sums the same terms in pixel order.
 template <typename T, int MAXD>
 struct GatherAcc {
-  T gi[6];
-  T gf[3 * MAXD];
+  double gi[6];
+  double gf[3 * MAXD];
   __device__ __forceinline__ void zero() {
 #pragma unroll
-    for (int q = 0; q < 6; q++) gi[q] = (T)0;
+    for (int q = 0; q < 6; q++) gi[q] = 0.0;
 #pragma unroll
-    for (int q = 0; q < 3 * MAXD; q++) gf[q] = (T)0;
+    for (int q = 0; q < 3 * MAXD; q++) gf[q] = 0.0;
   }
   // one pixel won by the face: the reference's per-pixel terms (rasterization_cuda.cu:262-399)
   __device__ __forceinline__ void add(const T v[6], const T *c, int D, T w_a, T w_b, T w_c, const T *g, float eps) {
@@ -972,13 +997,13 @@ struct GatherAcc {
     for (int d = 0; d < MAXD; d++) {
       if (d < D) {
         const T gd = g[d];
-        gf[d] += gd * w_a;
-        gf[MAXD + d] += gd * w_b;
-        gf[2 * MAXD + d] += gd * w_c;
+        gf[d] += (double)(gd * w_a);
+        gf[MAXD + d] += (double)(gd * w_b);
+        gf[2 * MAXD + d] += (double)(gd * w_c);
         T o[6];
         bg.terms(gd, c[d], c[D + d], c[2 * D + d], o);
 #pragma unroll
-        for (int q = 0; q < 6; q++) gi[q] += o[q];
+        for (int q = 0; q < 6; q++) gi[q] += (double)o[q];
       }
     }
   }
@@ -989,7 +1014,8 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
     const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
     const T *__restrict__ nz, int B, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
-    T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig, const uint2 *__restrict__ rng) {
+    T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig, const uint2 *__restrict__ rng,
+    const double *__restrict__ soft) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t tf = t / LPF;  // LPF consecutive lanes per face (whole groups per wave)
   const int s = (int)(t % LPF);
@@ -997,6 +1023,10 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
   const int b = in ? (int)(tf / F) : 0;
   const int64_t f = tf - (int64_t)b * F;
   const RastSrc<T> src{fvi, valid, (T)m, nz};
+  // the soft mask's sum of coordinate s (written by lane s below), loaded now so that its
+  // latency hides behind the walk: an unconditional load from a clamped index
+  double sv = 0.0;
+  if (soft) sv = soft[(in ? tf : 0) * 6 + (s < 6 ? s : 5)];
   GatherAcc<T, MAXD> acc;
   acc.zero();
   int ix0, ix1, iy0, iy1;
@@ -1049,11 +1079,11 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
 #pragma unroll
   for (int q = 0; q < 6 + 3 * MAXD; q++) {
     if (q % LPF != s) continue;
-    if (q < 6) {
-      grad_fvi[tf * 6 + q] = acc.gi[q];
+    if (q < 6) {  // (q == s) + the soft mask's sum, rounded on its own: autograd's add of the two
+      grad_fvi[tf * 6 + q] = soft ? (T)acc.gi[q] + (T)sv : (T)acc.gi[q];
     } else {
       const int r = q - 6, ii = r / MAXD, d = r % MAXD;
-      if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = acc.gf[r];
+      if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)acc.gf[r];
     }
   }
 }
@@ -1065,8 +1095,8 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
     const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
     const T *__restrict__ nz, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
     T *__restrict__ grad_ffeat, const int *__restrict__ big, const int *__restrict__ nbig,
-    const uint2 *__restrict__ rng) {
-  __shared__ T red[256];
+    const uint2 *__restrict__ rng, const double *__restrict__ soft) {
+  __shared__ double red[256];
   const int n = *nbig;
   const RastSrc<T> src{fvi, valid, (T)m, nz};
   for (int k = blockIdx.x; k < n; k += gridDim.x) {
@@ -1101,10 +1131,10 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
       }
       if (threadIdx.x == 0) {
         if (q < 6) {
-          grad_fvi[tf * 6 + q] = red[0];
+          grad_fvi[tf * 6 + q] = soft ? (T)red[0] + (T)soft[tf * 6 + q] : (T)red[0];
         } else {
           const int r = q - 6, ii = r / MAXD, d = r % MAXD;
-          if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = red[0];
+          if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)red[0];
         }
       }
       __syncthreads();
@@ -1112,19 +1142,31 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
   }
 }
 
+// workspace of the scatter backward: the double accumulators of both gradients
+static size_t rast_scatter_ws_bytes(int B, int F, int D) {
+  return al256((size_t)B * F * 6 * sizeof(double)) + al256((size_t)B * F * 3 * D * sizeof(double));
+}
+
 template <typename T>
 static int rasterize_bwd(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
                          const void *w, const void *fvi, const void *feat, float eps, void *gfvi, void *gfeat,
-                         hipStream_t st) {
-  KL_CHECK_RC(fill_async(gfvi, 0, sizeof(T) * (size_t)B * F * 6, st));
-  KL_CHECK_RC(fill_async(gfeat, 0, sizeof(T) * (size_t)B * F * 3 * D, st));
+                         void *ws, size_t ws_bytes, hipStream_t st) {
+  const size_t ni = (size_t)B * F * 6, nf = (size_t)B * F * 3 * D;
   const int64_t total = (int64_t)B * H * W;
-  if (total == 0) return KL_OK;
+  if (total == 0 || ni == 0) {
+    KL_CHECK_RC(fill_async(gfvi, 0, sizeof(T) * ni, st));
+    return fill_async(gfeat, 0, sizeof(T) * nf, st);
+  }
+  KL_REQUIRE(ws && ws_bytes >= rast_scatter_ws_bytes(B, F, D), "rasterize_backward: workspace too small");
+  double *ai = reinterpret_cast<double *>(ws);
+  double *af = reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + al256(ni * sizeof(double)));
+  KL_CHECK_RC(fill_async(ws, 0, rast_scatter_ws_bytes(B, F, D), st));
   const unsigned blocks = (unsigned)std::min<int64_t>(cdiv(total, 256), 65536);
   hipLaunchKernelGGL(rasterize_bwd_kernel<T>, dim3(blocks), dim3(256), 0, st, (const T *)grad, face_idx,
-                     (const T *)w, (const T *)fvi, (const T *)feat, B, H, W, F, D, eps, (T *)gfvi, (T *)gfeat);
+                     (const T *)w, (const T *)fvi, (const T *)feat, B, H, W, F, D, eps, ai, af);
   KL_CHECK_LAUNCH();
-  return KL_OK;
+  KL_CHECK_RC(acc_finalize<T>(ai, (T *)gfvi, ni, false, st));
+  return acc_finalize<T>(af, (T *)gfeat, nf, false, st);
 }
 
 // nbig: a zeroed int (zero_nbig: this call zeroes it first).
@@ -1132,14 +1174,14 @@ template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
                                      const T *w, const T *fvi, const T *feat, const uint8_t *valid, const T *nz,
                                      float m, float eps, T *gfvi, T *gfeat, int *big, int *nbig, bool zero_nbig,
-                                     const uint2 *rng, hipStream_t st) {
+                                     const uint2 *rng, const double *soft, hipStream_t st) {
   if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
   hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st, grad,
-                     face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng);
+                     face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
   KL_CHECK_LAUNCH();
   hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(256), dim3(256), 0, st, grad, face_idx, w, fvi,
-                     feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng);
+                     feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
@@ -1150,9 +1192,13 @@ template <typename T>
 static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
                                 const void *w, const void *fvi, const void *feat, const uint8_t *valid, const T *nz,
                                 float m, float eps, void *gfvi, void *gfeat, void *ws, size_t ws_bytes, int *nbig,
-                                hipStream_t st, const uint2 *rng = nullptr) {
+                                hipStream_t st, const uint2 *rng = nullptr, const double *soft = nullptr) {
   const int64_t nf = (int64_t)B * F;
   if (nf == 0) return KL_OK;
+  if (D > 8) {  // wide features: the scatter kernel
+    KL_REQUIRE(soft == nullptr, "rasterize backward: the soft-mask sum needs feat_dim <= 8");
+    return rasterize_bwd<T>(B, H, W, F, D, grad, face_idx, w, fvi, feat, eps, gfvi, gfeat, ws, ws_bytes, st);
+  }
   KL_REQUIRE(ws_bytes >= (size_t)(nf + 1) * sizeof(int), "rasterize backward: workspace too small");
   KL_REQUIRE(nf < ((int64_t)1 << 31), "rasterize backward: too many faces");
   const bool zero = nbig == nullptr;
@@ -1162,14 +1208,18 @@ static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *g
   const T *wt = (const T *)w;
   const T *fv = (const T *)fvi;
   const T *ft = (const T *)feat;
+  // MAXD = D where it is small (the accumulators are doubles: registers set the occupancy)
+  if (D <= 2)
+    return rasterize_bwd_gather_maxd<T, 2>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
+                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
+  if (D == 3)
+    return rasterize_bwd_gather_maxd<T, 3>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
+                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
   if (D <= 4)
     return rasterize_bwd_gather_maxd<T, 4>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, st);
-  if (D <= 8)
-    return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, st);
-  // wide features: the scatter kernel
-  return rasterize_bwd<T>(B, H, W, F, D, grad, face_idx, w, fvi, feat, eps, gfvi, gfeat, st);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
+  return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
+                                         (T *)gfeat, big, nbig, zero, rng, soft, st);
 }
 
 // The fused front-end path's forward: the tile rasterizer (dev flag bit 13 selects the
@@ -1242,18 +1292,28 @@ extern "C" int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, 
   return KL_E_INVALID;
 }
 
+extern "C" size_t kl_rasterize_backward_workspace_bytes(int batch, int num_faces, int feat_dim) {
+  return rast_scatter_ws_bytes(batch, num_faces, feat_dim);
+}
+
 extern "C" int kl_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces,
                                      int feat_dim, const void *grad, const int64_t *face_idx, const void *w,
                                      const void *fvi, const void *feat, float eps, void *gfvi, void *gfeat,
-                                     kl_stream stream) {
+                                     void *ws, size_t ws_bytes, kl_stream stream) {
   if (dtype == KL_F32)
     return rasterize_bwd<float>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat, eps,
-                                gfvi, gfeat, S(stream));
+                                gfvi, gfeat, ws, ws_bytes, S(stream));
   if (dtype == KL_F64)
     return rasterize_bwd<double>(batch, height, width, num_faces, feat_dim, grad, face_idx, w, fvi, feat, eps,
-                                 gfvi, gfeat, S(stream));
+                                 gfvi, gfeat, ws, ws_bytes, S(stream));
   set_error("rasterize_backward_cuda not implemented for this dtype");
   return KL_E_INVALID;
+}
+
+extern "C" size_t kl_dibr_rasterize_bwd_workspace_bytes(int batch, int height, int width, int num_faces,
+                                                        int feat_dim) {
+  const size_t gather = ((size_t)batch * num_faces + 1) * sizeof(int);
+  return feat_dim > 8 ? std::max(gather, rast_scatter_ws_bytes(batch, num_faces, feat_dim)) : gather;
 }
 
 extern "C" int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces,
@@ -1381,9 +1441,18 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
                     const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *ws,
                     size_t ws_bytes, hipStream_t st, const uint2 *face_ranges) {
   KL_REQUIRE(D <= 8, "dibr_rasterization backward: feature dimension > 8 is not supported by the fused path");
-  KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
-                                      gfeat, ws, ws_bytes, s.scratch, st, face_ranges));
-  return soft_tile_backward<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m, gfvi, true, ws, ws_bytes, st);
+  // workspace: the soft mask's double sums | (its items, then the gather's big-face list)
+  const size_t acc_bytes = al256((size_t)B * F * 6 * sizeof(double));
+  KL_REQUIRE(ws_bytes >= acc_bytes, "dibr_rasterization backward: workspace too small");
+  double *acc = reinterpret_cast<double *>(ws);
+  void *rest = reinterpret_cast<char *>(ws) + acc_bytes;
+  bool has_soft = false;
+  // the soft-mask sums first (left in double); the gather then writes every face's gradient as
+  // its own rounded sum + the soft mask's rounded sum (no zero fill, no separate finalize)
+  KL_CHECK_RC(soft_tile_backward<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m, gfvi, true, rest,
+                                    ws_bytes - acc_bytes, st, acc, &has_soft));
+  return rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi, gfeat,
+                                 rest, ws_bytes - acc_bytes, s.scratch, st, face_ranges, has_soft ? acc : nullptr);
 }
 }  // namespace kl
 
@@ -1395,9 +1464,9 @@ extern "C" size_t kl_dibr_workspace_bytes(int batch, int height, int width, int 
 }
 
 extern "C" size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum) {
-  const size_t a = kl_dibr_rasterize_workspace_bytes(batch, height, width, num_faces);
-  const size_t b = soft_tile_bwd_ws_bytes(batch, height, width, knum);
-  return a > b ? a : b;
+  const size_t a = kl_dibr_rasterize_bwd_workspace_bytes(batch, height, width, num_faces, 8);
+  const size_t b = soft_tile_bwd_items_bytes(batch, height, width, knum);
+  return al256((size_t)batch * num_faces * 6 * sizeof(double)) + (a > b ? a : b);
 }
 
 extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,

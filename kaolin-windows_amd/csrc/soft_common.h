@@ -120,17 +120,20 @@ __device__ __attribute__((noinline)) void global_add_pair(T *g, int c0, int c1, 
 }
 
 // Per-face accumulation of (face, coordinate) gradient terms in an LDS hash table
-// (linear probing, bounded), flushed with one global atomic per non-zero entry; terms
-// of faces that find no slot go straight to global atomics.
+// (linear probing, bounded), flushed with one global atomic per non-zero entry into a
+// double accumulator; terms of faces that find no slot go straight to global atomics.
+// Every accumulation is in double: the reference's float terms (each rounded as it computes
+// them) sum exactly whenever their magnitudes span less than ~2^29, so the rounded result
+// does not depend on the order of the atomics (acc_finalize rounds once).
 constexpr int SMB_HCAP = 1024;
 
 template <typename T>
 struct FaceHash {
-  int *key;  // [SMB_HCAP], -1 = empty
-  T *val;    // [SMB_HCAP * 6]
+  int *key;     // [SMB_HCAP], -1 = empty
+  double *val;  // [SMB_HCAP * 6]
   __device__ __forceinline__ void init(int tid, int nthreads) {
     for (int q = tid; q < SMB_HCAP; q += nthreads) key[q] = -1;
-    for (int q = tid; q < SMB_HCAP * 6; q += nthreads) val[q] = (T)0;
+    for (int q = tid; q < SMB_HCAP * 6; q += nthreads) val[q] = 0.0;
   }
   __device__ __forceinline__ int slot(int f) {
     unsigned h = ((unsigned)f * 2654435761u) >> 22;  // 10 bits
@@ -147,24 +150,24 @@ struct FaceHash {
     return -1;
   }
   // add the hit's terms (coordinate pairs c0 and, if c1 >= 0, c1) of face f
-  __device__ __forceinline__ void add(int f, int c0, int c1, T g0x, T g0y, T g1x, T g1y, T *gface) {
+  __device__ __forceinline__ void add(int f, int c0, int c1, T g0x, T g0y, T g1x, T g1y, double *gface) {
     const int s = slot(f);
     if (s >= 0) {
-      atomicAdd(&val[s * 6 + c0 * 2], g0x);
-      atomicAdd(&val[s * 6 + c0 * 2 + 1], g0y);
+      atomicAdd(&val[s * 6 + c0 * 2], (double)g0x);
+      atomicAdd(&val[s * 6 + c0 * 2 + 1], (double)g0y);
       if (c1 >= 0) {
-        atomicAdd(&val[s * 6 + c1 * 2], g1x);
-        atomicAdd(&val[s * 6 + c1 * 2 + 1], g1y);
+        atomicAdd(&val[s * 6 + c1 * 2], (double)g1x);
+        atomicAdd(&val[s * 6 + c1 * 2 + 1], (double)g1y);
       }
     } else {
-      global_add_pair<T>(gface + (size_t)f * 6, c0, c1, g0x, g0y, g1x, g1y);
+      global_add_pair<double>(gface + (size_t)f * 6, c0, c1, g0x, g0y, g1x, g1y);
     }
   }
-  __device__ __forceinline__ void flush(int tid, int nthreads, T *gmesh) {
+  __device__ __forceinline__ void flush(int tid, int nthreads, double *gmesh) {
     for (int q = tid; q < SMB_HCAP * 6; q += nthreads) {
       const int k = key[q / 6];
-      const T v = val[q];
-      if (k >= 0 && v != (T)0) atomicAdd(gmesh + (size_t)k * 6 + q % 6, v);
+      const double v = val[q];
+      if (k >= 0 && v != 0.0) atomicAdd(gmesh + (size_t)k * 6 + q % 6, v);
     }
   }
 };
@@ -193,8 +196,9 @@ int soft_lp_min(int K);
 template <typename T>
 int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
                        const T *fvi, float sigmainv, float m, T *gfvi, bool accumulate, void *ws, size_t ws_bytes,
-                       hipStream_t st);
-size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int K);
+                       hipStream_t st, double *acc_out = nullptr, bool *has_sum = nullptr);
+size_t soft_tile_bwd_items_bytes(int B, int H, int W, int K);
+size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int F, int K);
 size_t soft_tile_ws_bytes(int B, int H, int W, int F);
 
 }  // namespace kl

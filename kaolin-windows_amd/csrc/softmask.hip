@@ -231,8 +231,9 @@ __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
 // segment).  The wave's hits (the first kid slots of each uncovered pixel) are
 // evaluated densely, 64 at a time, and the per-face vertex-gradient terms -- the
 // reference's expressions, each already divided by the multiplier as it adds them --
-// are summed in an LDS hash table keyed by face (faces of a tile are shared by many
-// of its pixels); the table is flushed with one global atomic per (face, coordinate).
+// are summed in double in an LDS hash table keyed by face (faces of a tile are shared by
+// many of its pixels); the table is flushed with one global double atomic per (face,
+// coordinate) into a double accumulator, rounded once afterwards (acc_finalize).
 // kid per pixel: `hits` from the fused forward, or the reference's scan of the slots
 // up to the first -1 (hits == nullptr, the _C contract).
 template <typename T, bool SCALE>
@@ -240,9 +241,9 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const int64_t *__restrict__ sel,
     const T *__restrict__ prob, const int64_t *__restrict__ cidx, const uint8_t *__restrict__ ctype,
     const uint8_t *__restrict__ hits, const T *__restrict__ fvi, int B, int H, int W, int F, int K,
-    float sigmainv, float multiplier, T *__restrict__ gfvi) {
+    float sigmainv, float multiplier, double *__restrict__ gacc) {
   __shared__ int s_key[SMB_HCAP];
-  __shared__ T s_val[SMB_HCAP * 6];
+  __shared__ double s_val[SMB_HCAP * 6];
   __shared__ double s_a[8][64];
   __shared__ int s_pre[8][64];
   const int lane = threadIdx.x & 63;
@@ -285,7 +286,7 @@ __global__ void __launch_bounds__(512) soft_mask_bwd_agg_kernel(
 
   const T y0 = pix_y<T>(multiplier, H, j < H ? j : 0);
   const size_t rowk = (((size_t)b * H + (j < H ? j : 0)) * W + ibase) * K;
-  T *gb = gfvi + (size_t)b * F * 6;
+  double *gb = gacc + (size_t)b * F * 6;
   for (int e = lane; e < total; e += 64) {
     int lo = 0;
 #pragma unroll
@@ -332,7 +333,6 @@ static size_t sm_lds_per_wave(int K) {
 
 // workspace: bin bitmap | tile order (keys/vals in/out + sort temp) | per-face bboxes
 // (fused path; sized for f64)
-static size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 struct SmWs {
   size_t order, order_temp, order_temp_bytes, bbox, bytes;
   SmWs(const BinGeom &g, int F) {
@@ -392,18 +392,25 @@ static int soft_mask_fwd(Src src, const T *bbox, int B, int H, int W, int F, int
   return KL_OK;
 }
 
+// workspace: the (B,F,3,2) double accumulator
+static size_t sm_bwd_ws_bytes(int B, int F) { return al256((size_t)B * F * 6 * sizeof(double)); }
+
 template <typename T, bool SCALE>
 static int soft_mask_bwd(int B, int H, int W, int F, int K, const void *grad, const void *mask,
                          const int64_t *sel, const void *prob, const int64_t *cidx, const uint8_t *ctype,
-                         const uint8_t *hits, const void *fvi, float sigmainv, float m, void *gfvi, hipStream_t st) {
+                         const uint8_t *hits, const void *fvi, float sigmainv, float m, void *gfvi, void *ws,
+                         size_t ws_bytes, hipStream_t st) {
   KL_REQUIRE(F < (1 << 28), "dibr_soft_mask_backward: too many faces");
-  KL_CHECK_RC(fill_async(gfvi, 0, sizeof(T) * (size_t)B * F * 6, st));
-  if ((int64_t)B * H * W == 0 || K <= 0) return KL_OK;
+  const size_t n = (size_t)B * F * 6;
+  if ((int64_t)B * H * W == 0 || K <= 0 || n == 0) return fill_async(gfvi, 0, sizeof(T) * n, st);
+  KL_REQUIRE(ws && ws_bytes >= sm_bwd_ws_bytes(B, F), "dibr_soft_mask_backward: workspace too small");
+  double *acc = reinterpret_cast<double *>(ws);
+  KL_CHECK_RC(fill_async(acc, 0, n * sizeof(double), st));
   dim3 grid((unsigned)cdiv(W, 64), (unsigned)cdiv(H, 8), B);
   hipLaunchKernelGGL((soft_mask_bwd_agg_kernel<T, SCALE>), grid, dim3(512), 0, st, (const T *)grad, (const T *)mask,
-                     sel, (const T *)prob, cidx, ctype, hits, (const T *)fvi, B, H, W, F, K, sigmainv, m, (T *)gfvi);
+                     sel, (const T *)prob, cidx, ctype, hits, (const T *)fvi, B, H, W, F, K, sigmainv, m, acc);
   KL_CHECK_LAUNCH();
-  return KL_OK;
+  return acc_finalize<T>(acc, (T *)gfvi, n, false, st);
 }
 
 }  // namespace kl
@@ -448,17 +455,21 @@ extern "C" int kl_dibr_soft_mask_forward_fused(kl_dtype dtype, int batch, int he
   return KL_E_INVALID;
 }
 
+extern "C" size_t kl_soft_mask_backward_workspace_bytes(int batch, int num_faces) {
+  return sm_bwd_ws_bytes(batch, num_faces);
+}
+
 extern "C" int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height, int width, int num_faces,
                                           int knum, const void *grad, const void *mask, const int64_t *sel,
                                           const void *prob, const int64_t *cidx, const uint8_t *ctype,
-                                          const void *fvi, float sigmainv, float multiplier, void *gfvi,
-                                          kl_stream stream) {
+                                          const void *fvi, float sigmainv, float multiplier, void *gfvi, void *ws,
+                                          size_t ws_bytes, kl_stream stream) {
   if (dtype == KL_F32)
     return soft_mask_bwd<float, false>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype,
-                                       nullptr, fvi, sigmainv, multiplier, gfvi, S(stream));
+                                       nullptr, fvi, sigmainv, multiplier, gfvi, ws, ws_bytes, S(stream));
   if (dtype == KL_F64)
     return soft_mask_bwd<double, false>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype,
-                                        nullptr, fvi, sigmainv, multiplier, gfvi, S(stream));
+                                        nullptr, fvi, sigmainv, multiplier, gfvi, ws, ws_bytes, S(stream));
   set_error("dibr_soft_mask_backward_cuda not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -467,13 +478,14 @@ extern "C" int kl_dibr_soft_mask_backward_fused(kl_dtype dtype, int batch, int h
                                                 int knum, const void *grad, const void *mask, const int64_t *sel,
                                                 const void *prob, const int64_t *cidx, const uint8_t *ctype,
                                                 const uint8_t *hits, const void *fvi, float sigmainv,
-                                                float multiplier, void *gfvi, kl_stream stream) {
+                                                float multiplier, void *gfvi, void *ws, size_t ws_bytes,
+                                                kl_stream stream) {
   if (dtype == KL_F32)
     return soft_mask_bwd<float, true>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype, hits,
-                                      fvi, sigmainv, multiplier, gfvi, S(stream));
+                                      fvi, sigmainv, multiplier, gfvi, ws, ws_bytes, S(stream));
   if (dtype == KL_F64)
     return soft_mask_bwd<double, true>(batch, height, width, num_faces, knum, grad, mask, sel, prob, cidx, ctype,
-                                       hits, fvi, sigmainv, multiplier, gfvi, S(stream));
+                                       hits, fvi, sigmainv, multiplier, gfvi, ws, ws_bytes, S(stream));
   set_error("dibr_soft_mask_backward not implemented for this dtype");
   return KL_E_INVALID;
 }

@@ -10,19 +10,21 @@
 // The soft mask and the gradients are computed with the reference's arithmetic and
 // hit order, so they equal the _C path's (tests/test_gpu_parity.py).
 //
-// Forward, per 64x8 tile (one workgroup, one wave per pixel row):
+// Forward, per work item = a part of a 64x8 tile's rows (one 4-wave workgroup):
 //  1. the tile's candidate 64-face chunks (binning.h bitmap) are expanded cooperatively,
-//     R chunks per step (one per wave, all loads in flight together): each face's exact
-//     lane interval on the tile's columns and the tile rows its bbox spans are computed
-//     ONCE for the tile, and faces that touch it are appended in index order to an LDS
-//     face list (ordered compaction across the waves);
-//  2. each row wave walks the list: faces whose interval meets a still-active pixel
-//     (uncovered, < knum hits) are appended, in index order, to the [slot][lane] lists of
-//     the active pixels they cover -- exactly the reference's "first knum faces whose
-//     enlarged bbox contains the pixel centre";
-//  3. the wave's hits are evaluated densely (64 per step), records written contiguously,
-//     and the mask is 1 - prod(1 - p) in slot order.
-// Tiles run heaviest first (candidate-chunk counts, one counting-sort workgroup).
+//     one chunk per wave and step: each face's exact lane interval on the tile's columns and
+//     the item's rows its bbox spans, and faces that touch them are appended in index order
+//     to an LDS face list (ordered compaction across the waves);
+//  2. each row walks the list: faces whose interval meets a still-active pixel (uncovered,
+//     < knum hits) are appended, in index order, to the [slot][lane] lists of the active
+//     pixels they cover -- exactly the reference's "first knum faces whose enlarged bbox
+//     contains the pixel centre";
+//  3. the row's hits are evaluated densely, records written contiguously, and the mask is
+//     1 - prod(1 - p) in slot order.
+// Items run heaviest first (candidate-chunk counts, one counting-sort workgroup); the
+// heaviest tiles (the silhouette's tight spots) are split into 4 or 8 items whose rows get
+// 2 or 4 waves each, for the walk (blocks of the list round-robin, a per-pixel count prefix
+// giving each wave its slots) and the evaluation.
 //
 // Backward, per tile: each row wave reads its records (coalesced), evaluates the
 // reference's per-hit terms and sums them per face in an LDS hash (soft_common.h),
@@ -72,17 +74,8 @@ __host__ __device__ constexpr size_t st_row_lds(int K) {
 constexpr int ST_LIST_CAP = 1024;
 constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int); }
 
-// Forward, one work item (a part of a tile's rows) per 4-wave workgroup.
-//  1. walk (one wave per row): the tile's candidate chunks are read straight from the bin
-//     bitmap, their faces' exact pixel ranges (binning pass) loaded four chunks ahead; each
-//     chunk's 64 faces are tested against the row and, if one of them covers a still-active
-//     pixel (uncovered, < knum hits), their pixel masks are transposed across the wave
-//     (transpose64) so that every active pixel lane appends the covering faces in index order
-//     -- the reference's "first knum faces whose enlarged bbox contains the pixel centre";
-//  2. evaluation: the row's hits, densely, by the Q waves of the row (the reference's distance
-//     and probability), records written contiguously in (pixel, slot) order;
-//  3. the mask, 1 - prod(1 - p) in double in slot order, by the row's first wave.
-// Rows are independent: no workgroup barrier unless Q > 1.
+// Forward, one work item (a part of a tile's rows) per 4-wave workgroup: fill and walk (1a,
+// 1b below), the dense evaluation by the row's Q waves, the mask by its first wave.
 template <typename T>
 __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
@@ -514,13 +507,13 @@ __global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restri
 }
 
 // Per-face accumulation for one work item: LDS hash on the mesh-local face index with
-// the list of used slots, so the flush and the reset touch only those.  HC slots (a power
-// of two): 1024 for f32; 512 for f64, whose workgroup would otherwise need ~64 KB of LDS.
+// the list of used slots, so the flush and the reset touch only those.  Sums are in
+// double (see FaceHash, soft_common.h): HC = 512 slots keep the workgroup near 34 KB of LDS.
 template <typename T, int HC>
 struct ItemHash {
-  int *key;   // [HC], -1 = empty
-  T *val;     // [HC * 6]
-  int *used;  // [HC]
+  int *key;     // [HC], -1 = empty
+  double *val;  // [HC * 6]
+  int *used;    // [HC]
   int *nused;
   __device__ __forceinline__ int slot(int f) {
     unsigned h = ((unsigned)f * 2654435761u) >> (32 - __builtin_ctz(HC));
@@ -540,30 +533,30 @@ struct ItemHash {
     }
     return -1;
   }
-  __device__ __forceinline__ void add(int f, int c0, int c1, T g0x, T g0y, T g1x, T g1y, T *gmesh) {
+  __device__ __forceinline__ void add(int f, int c0, int c1, T g0x, T g0y, T g1x, T g1y, double *gmesh) {
     const int s = slot(f);
     if (s >= 0) {
-      atomicAdd(&val[s * 6 + c0 * 2], g0x);
-      atomicAdd(&val[s * 6 + c0 * 2 + 1], g0y);
+      atomicAdd(&val[s * 6 + c0 * 2], (double)g0x);
+      atomicAdd(&val[s * 6 + c0 * 2 + 1], (double)g0y);
       if (c1 >= 0) {
-        atomicAdd(&val[s * 6 + c1 * 2], g1x);
-        atomicAdd(&val[s * 6 + c1 * 2 + 1], g1y);
+        atomicAdd(&val[s * 6 + c1 * 2], (double)g1x);
+        atomicAdd(&val[s * 6 + c1 * 2 + 1], (double)g1y);
       }
     } else {  // no free slot within the probe bound
-      global_add_pair<T>(gmesh + (size_t)f * 6, c0, c1, g0x, g0y, g1x, g1y);
+      global_add_pair<double>(gmesh + (size_t)f * 6, c0, c1, g0x, g0y, g1x, g1y);
     }
   }
-  // one thread per used slot: add its non-zero coordinates to the mesh gradient, reset it
-  __device__ __forceinline__ void flush_reset(int tid, int nthreads, T *gmesh) {
+  // one thread per used slot: add its non-zero coordinates to the mesh accumulator, reset it
+  __device__ __forceinline__ void flush_reset(int tid, int nthreads, double *gmesh) {
     const int n = *nused;
     for (int u = tid; u < n; u += nthreads) {
       const int sl = used[u];
       const int f = key[sl];
 #pragma unroll
       for (int c = 0; c < 6; c++) {
-        const T v = val[sl * 6 + c];
-        if (v != (T)0) atomicAdd(gmesh + (size_t)f * 6 + c, v);
-        val[sl * 6 + c] = (T)0;
+        const double v = val[sl * 6 + c];
+        if (v != 0.0) atomicAdd(gmesh + (size_t)f * 6 + c, v);
+        val[sl * 6 + c] = 0.0;
       }
       key[sl] = -1;
     }
@@ -578,11 +571,11 @@ template <typename T>
 __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const uint8_t *__restrict__ hits,
     const uint32_t *__restrict__ rec_face, const T *__restrict__ rec_prob, const T *__restrict__ fvi, BinGeom g,
-    int F, int K, float sigmainv, float multiplier, T *__restrict__ gfvi, const int2 *__restrict__ items,
+    int F, int K, float sigmainv, float multiplier, double *__restrict__ gacc, const int2 *__restrict__ items,
     int *__restrict__ ctl, int *__restrict__ scratch, int dev) {
-  constexpr int HC = sizeof(T) == 4 ? 1024 : 512;
+  constexpr int HC = 512;
   __shared__ int s_key[HC];
-  __shared__ T s_val[HC * 6];
+  __shared__ double s_val[HC * 6];
   __shared__ int s_used[HC];
   __shared__ int s_nused;
   __shared__ double s_a[TILE_H][64];
@@ -592,7 +585,7 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
   const int wid = threadIdx.x >> 6;  // the item's row
   const int H = g.height, W = g.width;
   for (int q = threadIdx.x; q < HC; q += blockDim.x) s_key[q] = -1;
-  for (int q = threadIdx.x; q < HC * 6; q += blockDim.x) s_val[q] = (T)0;
+  for (int q = threadIdx.x; q < HC * 6; q += blockDim.x) s_val[q] = 0.0;
   if (threadIdx.x == 0) s_nused = 0;
   if (scratch && threadIdx.x == 0 && blockIdx.x == 0) *scratch = 0;
   ItemHash<T, HC> hash{s_key, s_val, s_used, &s_nused};
@@ -661,10 +654,10 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
       if (dev & 2)
         asm volatile("" : : "v"(g0x), "v"(g0y), "v"(g1x), "v"(g1y), "v"(c0), "v"(c1));
       else
-        hash.add(face, c0, c1, g0x, g0y, g1x, g1y, gfvi + (size_t)b * F * 6);
+        hash.add(face, c0, c1, g0x, g0y, g1x, g1y, gacc + (size_t)b * F * 6);
     }
     __syncthreads();
-    hash.flush_reset(threadIdx.x, blockDim.x, gfvi + (size_t)b * F * 6);
+    hash.flush_reset(threadIdx.x, blockDim.x, gacc + (size_t)b * F * 6);
     __syncthreads();
     if (threadIdx.x == 0) s_nused = 0;
   }
@@ -759,24 +752,38 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   return KL_OK;
 }
 
-size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int K) {
+// workspace: item count | items | the (B,F,3,2) double accumulator
+static size_t soft_bwd_acc_offset(int B, int H, int W, int K) {
   const BinGeom g = make_bin_geom(B, H, W, 1);
   const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
-  return 256 + nt * (size_t)(K + 2) * sizeof(int2);
+  return al256(256 + nt * (size_t)(K + 2) * sizeof(int2));
+}
+size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int F, int K) {
+  return soft_bwd_acc_offset(B, H, W, K) + al256((size_t)B * F * 6 * sizeof(double));
 }
 
+// acc_out == nullptr: the sums are rounded into gfvi (overwritten, or added with accumulate);
+// otherwise they are left in acc_out (B*F*6 doubles, zeroed here; gfvi unused) for a caller
+// that rounds them itself (kl_dibr_backward's gather) -- *has_sum tells whether any was made.
 template <typename T>
 int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
                        const T *fvi, float sigmainv, float m, T *gfvi, bool accumulate, void *ws, size_t ws_bytes,
-                       hipStream_t st) {
+                       hipStream_t st, double *acc_out, bool *has_sum) {
   KL_REQUIRE(F < (1 << 28), "dibr_soft_mask backward: too many faces");
-  if (!accumulate) KL_CHECK_RC(fill_async(gfvi, 0, sizeof(T) * (size_t)B * F * 6, st));
-  if ((int64_t)B * H * W == 0 || K <= 0 || grad == nullptr)
+  const size_t n = (size_t)B * F * 6;
+  if (has_sum) *has_sum = false;
+  if ((int64_t)B * H * W == 0 || K <= 0 || grad == nullptr || n == 0) {
+    if (!accumulate && !acc_out) KL_CHECK_RC(fill_async(gfvi, 0, sizeof(T) * n, st));
     return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
-  KL_REQUIRE(ws_bytes >= soft_tile_bwd_ws_bytes(B, H, W, K), "dibr_soft_mask backward: workspace too small");
+  }
+  KL_REQUIRE(ws_bytes >= (acc_out ? soft_bwd_acc_offset(B, H, W, K) : soft_tile_bwd_ws_bytes(B, H, W, F, K)),
+             "dibr_soft_mask backward: workspace too small");
   const BinGeom g = make_bin_geom(B, H, W, F);
   int *ctl = reinterpret_cast<int *>(ws);
   int2 *items = reinterpret_cast<int2 *>(reinterpret_cast<char *>(ws) + 256);
+  double *acc = acc_out ? acc_out
+                        : reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + soft_bwd_acc_offset(B, H, W, K));
+  KL_CHECK_RC(fill_async(acc, 0, n * sizeof(double), st));
   hipLaunchKernelGGL(soft_bwd_plan_kernel, dim3(1), dim3(1024), 0, st, (const int *)s.seg_tot, g, items, ctl);
   KL_CHECK_LAUNCH();
   int dev_id = 0, ncu = 256;
@@ -785,11 +792,16 @@ int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
   hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
-                     (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, gfvi,
+                     (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, acc,
                      (const int2 *)items, ctl, s.scratch, g_dev_flags);
   KL_CHECK_LAUNCH();
-  return KL_OK;
+  if (acc_out) {
+    if (has_sum) *has_sum = true;
+    return KL_OK;
+  }
+  return acc_finalize<T>(acc, gfvi, n, accumulate, st);
 }
+size_t soft_tile_bwd_items_bytes(int B, int H, int W, int K) { return soft_bwd_acc_offset(B, H, W, K); }
 
 template int soft_tile_forward<float>(int, int, int, int, int, const float *, const int64_t *, float, double, float,
                                       float *, const SoftState<float> &, void *, size_t, hipStream_t);
@@ -803,10 +815,10 @@ template int soft_tile_forward_main<double>(int, int, int, int, int, const doubl
                                             const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t);
 template int soft_tile_backward<float>(int, int, int, int, int, const float *, const float *,
                                        const SoftState<float> &, const float *, float, float, float *, bool, void *,
-                                       size_t, hipStream_t);
+                                       size_t, hipStream_t, double *, bool *);
 template int soft_tile_backward<double>(int, int, int, int, int, const double *, const double *,
                                         const SoftState<double> &, const double *, float, float, double *, bool,
-                                        void *, size_t, hipStream_t);
+                                        void *, size_t, hipStream_t, double *, bool *);
 
 size_t soft_tile_ws_bytes(int B, int H, int W, int F) { return StWs(make_bin_geom(B, H, W, F), F).bytes; }
 
@@ -826,8 +838,9 @@ extern "C" size_t kl_soft_mask_compact_segments(int batch, int height, int width
   return (size_t)batch * height * cdiv(width, TILE_W);
 }
 
-extern "C" size_t kl_soft_mask_compact_bwd_workspace_bytes(int batch, int height, int width, int knum) {
-  return soft_tile_bwd_ws_bytes(batch, height, width, knum);
+extern "C" size_t kl_soft_mask_compact_bwd_workspace_bytes(int batch, int height, int width, int num_faces,
+                                                         int knum) {
+  return soft_tile_bwd_ws_bytes(batch, height, width, num_faces, knum);
 }
 
 extern "C" int kl_dibr_soft_mask_forward_compact(kl_dtype dtype, int batch, int height, int width, int num_faces,

@@ -91,11 +91,13 @@ def rasterize_backward_cuda(grad_interpolated_features, interpolated_features, s
     dev = face_vertices_image.device
     g_img = torch.empty_like(face_vertices_image)
     g_feat = torch.empty_like(face_features)
+    nbytes = N.lib().kl_rasterize_backward_workspace_bytes(B, F, D)
+    ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev), N.timed(func, dev):
         N.check(N.lib().kl_rasterize_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, N.ptr(grad_interpolated_features),
             N.ptr(selected_face_idx), N.ptr(output_weights), N.ptr(face_vertices_image), N.ptr(face_features),
-            float(eps), N.ptr(g_img), N.ptr(g_feat), N.stream_of(dev)), func)
+            float(eps), N.ptr(g_img), N.ptr(g_feat), N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return [g_img, g_feat]
 
 
@@ -156,12 +158,14 @@ def dibr_soft_mask_backward_cuda(grad_soft_mask, soft_mask, selected_face_idx, c
     N.require_gpu(func, face_vertices_image)
     dev = face_vertices_image.device
     g = torch.empty_like(face_vertices_image)
+    nbytes = N.lib().kl_soft_mask_backward_workspace_bytes(B, F)
+    ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
     with torch.cuda.device(dev), N.timed(func, dev):
         N.check(N.lib().kl_dibr_soft_mask_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, K, N.ptr(grad_soft_mask), N.ptr(soft_mask),
             N.ptr(selected_face_idx.contiguous()), N.ptr(close_face_prob), N.ptr(close_face_idx),
             N.ptr(close_face_dist_type), N.ptr(face_vertices_image), float(sigmainv), float(multiplier), N.ptr(g),
-            N.stream_of(dev)), func)
+            N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return g
 
 

@@ -75,7 +75,7 @@ def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_featur
     g_feat = torch.empty_like(face_features)
     valid, fnz = _validity(valid_faces, face_normals_z, face_vertices_image.dtype)
     lib = N.lib()
-    nbytes = lib.kl_dibr_rasterize_workspace_bytes(B, H, W, F)
+    nbytes = lib.kl_dibr_rasterize_bwd_workspace_bytes(B, H, W, F, D)
     ws = _ws(nbytes, dev)
     with torch.cuda.device(dev), N.timed('dibr_rasterize_backward', dev):
         N.check(lib.kl_dibr_rasterize_backward(
@@ -125,11 +125,13 @@ def soft_mask_backward(grad, mask, sel, prob, cidx, ctype, face_vertices_image, 
     K = cidx.shape[-1]
     dev = face_vertices_image.device
     g = torch.empty_like(face_vertices_image)
+    nbytes = N.lib().kl_soft_mask_backward_workspace_bytes(B, F)
+    ws = _ws(nbytes, dev)
     with torch.cuda.device(dev), N.timed('dibr_soft_mask_backward', dev):
         N.check(N.lib().kl_dibr_soft_mask_backward_fused(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, K, N.ptr(grad.contiguous()), N.ptr(mask),
             N.ptr(sel), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(hits), N.ptr(face_vertices_image), float(sigmainv),
-            float(multiplier), N.ptr(g), N.stream_of(dev)), func)
+            float(multiplier), N.ptr(g), N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return g
 
 
@@ -179,14 +181,15 @@ def soft_mask_forward_compact(face_vertices_image, selected_face_idx, sigmainv, 
 
 
 def soft_mask_backward_compact(grad, mask, state, face_vertices_image, sigmainv, multiplier, out=None):
-    """-> grad_face_vertices_image; with ``out`` the terms are added onto it (returned)."""
+    """-> grad_face_vertices_image (the terms summed in double, rounded once); with ``out`` that
+    rounded sum is added onto it (returned), as autograd adds it to the rasterizer's gradient."""
     func = 'dibr_soft_mask backward'
     B, F = face_vertices_image.shape[:2]
     H, W = mask.shape[1:]
     dev = face_vertices_image.device
     g = out if out is not None else torch.empty_like(face_vertices_image)
     lib = N.lib()
-    nbytes = lib.kl_soft_mask_compact_bwd_workspace_bytes(B, H, W, state.knum)
+    nbytes = lib.kl_soft_mask_compact_bwd_workspace_bytes(B, H, W, F, state.knum)
     ws = _ws(nbytes, dev)
     with torch.cuda.device(dev), N.timed('dibr_soft_mask_backward', dev):
         N.check(lib.kl_dibr_soft_mask_backward_compact(
@@ -195,6 +198,32 @@ def soft_mask_backward_compact(grad, mask, state, face_vertices_image, sigmainv,
             N.ptr(face_vertices_image), float(sigmainv), float(multiplier), N.ptr(g), 1 if out is not None else 0,
             N.ptr(state.scratch), N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return g
+
+
+def dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, face_vertices_image, face_features, face_normals_z,
+                  soft_mask, state, sigmainv, multiplier, eps, face_ranges=None):
+    """dibr_rasterization's backward in one call (kl_dibr_backward): the soft-mask terms summed in
+    double first, then the rasterizer's gather writes every face's gradient as its own rounded
+    sum plus the soft mask's (as autograd adds the two).  grad_soft_mask may be None.
+    -> grad_face_vertices_image, grad_face_features."""
+    func = 'dibr_rasterization backward'
+    B, H, W, D = grad_feats.shape
+    F = face_vertices_image.shape[1]
+    dev = face_vertices_image.device
+    g_img = torch.empty_like(face_vertices_image)
+    g_feat = torch.empty_like(face_features)
+    lib = N.lib()
+    nbytes = lib.kl_dibr_bwd_workspace_bytes(B, H, W, F, state.knum)
+    ws = _ws(nbytes, dev)
+    gm = grad_soft_mask.contiguous() if grad_soft_mask is not None else None
+    with torch.cuda.device(dev), N.timed('dibr_backward', dev):
+        N.check(lib.kl_dibr_backward(
+            N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, state.knum, N.ptr(grad_feats.contiguous()),
+            N.ptr(gm), N.ptr(face_idx), N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features),
+            N.ptr(face_normals_z), N.ptr(soft_mask), N.ptr(state.hits), N.ptr(state.rec_face), N.ptr(state.rec_prob),
+            N.ptr(state.seg_tot), float(sigmainv), float(multiplier), float(eps), N.ptr(g_img), N.ptr(g_feat),
+            N.ptr(state.scratch), N.ptr(face_ranges), N.ptr(ws), nbytes, N.stream_of(dev)), func)
+    return g_img, g_feat
 
 
 def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z, sigmainv, boxlen,

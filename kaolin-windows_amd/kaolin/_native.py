@@ -40,7 +40,10 @@ _SIGS = {
     'kl_rasterize_workspace_bytes': (_SZ, [_I, _I, _I, _I64]),
     'kl_packed_rasterize_forward': (_I, [_I, _I, _I, _I, _I64, _I, _I64, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P,
                                          _SZ, _P]),
-    'kl_rasterize_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _P, _P, _P]),
+    'kl_rasterize_backward_workspace_bytes': (_SZ, [_I, _I, _I]),
+    'kl_rasterize_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _P, _P, _P, _SZ, _P]),
+    'kl_dibr_rasterize_bwd_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
+    'kl_soft_mask_backward_workspace_bytes': (_SZ, [_I, _I]),
     'kl_dibr_rasterize_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'kl_dibr_rasterize_forward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _SZ,
                                        _P]),
@@ -50,11 +53,11 @@ _SIGS = {
     'kl_dibr_soft_mask_forward_fused': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _F, ctypes.c_double, _F, _P, _P, _P,
                                              _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_backward_fused': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P,
-                                              _P]),
+                                              _P, _SZ, _P]),
     'kl_soft_mask_compact_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'kl_soft_mask_compact_records': (_SZ, [_I, _I, _I, _I]),
     'kl_soft_mask_compact_segments': (_SZ, [_I, _I, _I]),
-    'kl_soft_mask_compact_bwd_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
+    'kl_soft_mask_compact_bwd_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'kl_dibr_soft_mask_forward_compact': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _F, ctypes.c_double, _F, _P, _P, _P,
                                                _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_backward_compact': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, _I,
@@ -66,7 +69,8 @@ _SIGS = {
     'kl_dibr_backward': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F,
                               _F, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_forward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _SZ, _P]),
-    'kl_dibr_soft_mask_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P]),
+    'kl_dibr_soft_mask_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _SZ,
+                                        _P]),
     'kl_unbatched_triangle_distance_workspace_bytes': (_SZ, [_I64]),
     'kl_unbatched_triangle_distance_forward': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_unbatched_triangle_distance_backward': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),

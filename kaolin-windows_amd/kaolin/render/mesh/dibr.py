@@ -54,9 +54,10 @@ class DibrSoftMaskCuda(Function):
 class DibrRasterizationCuda(Function):
     """dibr_rasterization (dibr.py:119-209) as one autograd node: rasterize with
     valid = face_normals_z >= 0 evaluated in-kernel, then the compact soft mask on its
-    face index.  The backward runs the rasterizer's gather (which writes every face's
-    gradient) and adds the soft-mask terms onto it -- no zero fill and no separate sum of
-    the two gradients.  Outputs and gradients equal rasterize + dibr_soft_mask's."""
+    face index.  The backward is one call: the soft-mask terms summed in double, then the
+    rasterizer's gather, which writes every face's gradient as its rounded sum plus the soft
+    mask's -- no zero fill and no separate sum of the two gradients.  Outputs and gradients
+    equal rasterize + dibr_soft_mask's."""
 
     @staticmethod
     def forward(ctx, height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z, sigmainv,
@@ -86,16 +87,17 @@ class DibrRasterizationCuda(Function):
     def backward(ctx, grad_feats, grad_soft_mask, grad_face_idx):
         face_idx, weights, fvi, feat, fnz, soft_mask, ranges, *st = ctx.saved_tensors
         state = _fused.SoftMaskState(*st, ctx.knum)
-        scratch = state.scratch
         if grad_feats is None:
             grad_feats = torch.zeros(face_idx.shape + (feat.shape[-1],), dtype=feat.dtype, device=feat.device)
-        g_img, g_feat = _fused.rasterize_backward(grad_feats, face_idx, weights, fvi, feat, None, ctx.multiplier,
-                                                  ctx.eps, face_normals_z=fnz, scratch=scratch, face_ranges=ranges)
-        if grad_soft_mask is not None:
-            _fused.soft_mask_backward_compact(grad_soft_mask, soft_mask, state, fvi, ctx.sigmainv, ctx.multiplier,
-                                              out=g_img)
-        else:
-            scratch.data.zero_()  # .data: no version bump of the saved tensor (retain_graph)
+        if fnz.dtype == fvi.dtype:
+            g_img, g_feat = _fused.dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, fvi, feat, fnz,
+                                                 soft_mask, state, ctx.sigmainv, ctx.multiplier, ctx.eps, ranges)
+        else:  # face_normals_z of another dtype: the two stages (the rasterizer's reads a valid mask)
+            g_img, g_feat = _fused.rasterize_backward(grad_feats, face_idx, weights, fvi, feat, None, ctx.multiplier,
+                                                      ctx.eps, face_normals_z=fnz, face_ranges=ranges)
+            if grad_soft_mask is not None:
+                _fused.soft_mask_backward_compact(grad_soft_mask, soft_mask, state, fvi, ctx.sigmainv,
+                                                  ctx.multiplier, out=g_img)
         return None, None, None, g_img, g_feat, None, None, None, None, None, None
 
 

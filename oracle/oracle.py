@@ -83,12 +83,13 @@ def rasterize_backward(grad_feat, face_idx, weights, fvi, feat, eps):
     face_idx = _c(face_idx, np.int64)
     B, H, W, D = grad_feat.shape
     F = fvi.shape[1]
-    g_img = np.zeros_like(fvi)
-    g_feat = np.zeros_like(feat)
+    # the reference's float terms summed in double, rounded once (its atomics have no order)
+    g_img = np.zeros(fvi.shape, np.float64)
+    g_feat = np.zeros(feat.shape, np.float64)
     getattr(lib(), f'or_rasterize_bwd_{sfx}')(
         B, H, W, F, D, _p(grad_feat), _p(face_idx), _p(weights), _p(fvi), _p(feat),
         ctypes.c_float(eps), _p(g_img), _p(g_feat))
-    return g_img, g_feat
+    return g_img.astype(dt), g_feat.astype(dt)
 
 
 def rasterize(height, width, fvz, fvi, feat, valid_faces=None, multiplier=1000, eps=1e-8):
@@ -140,11 +141,11 @@ def dibr_soft_mask_backward(grad, mask, sel, prob, cidx, ctype, fvi_m, sigmainv,
     B, F = fvi_m.shape[:2]
     H, W = sel.shape[1:]
     K = cidx.shape[-1]
-    g = np.zeros_like(fvi_m)
+    g = np.zeros(fvi_m.shape, np.float64)  # float terms summed in double, rounded once
     getattr(lib(), f'or_soft_mask_bwd_{sfx}')(
         B, H, W, F, K, _p(grad), _p(mask), _p(sel), _p(prob), _p(cidx), _p(ctype), _p(fvi_m),
         ctypes.c_float(sigmainv), ctypes.c_float(multiplier), _p(g))
-    return g
+    return g.astype(dt)
 
 
 def soft_mask_bboxes(fvi, boxlen, multiplier):
@@ -574,3 +575,46 @@ def check_sign(verts, faces, points):
         cnt = mesh_intersection_counts(p, v[faces[:, 0]], v[faces[:, 1]], v[faces[:, 2]])
         res.append(cnt % 2 == 1)
     return np.stack(res)
+
+
+# ------------------------------------------------------------ compact soft-mask state (GPU)
+# The checker's view of the GPU forward's saved state (softtile.hip layout, kaolin_hip.h):
+# decode_compact() rebuilds the reference's (B,H,W,K) slot tensors from it, so that the oracle's
+# soft-mask backward can run on the GPU forward's own saved values.
+def decode_compact(hits, rec_face, rec_prob, K, rows=None):
+    """(hits (B,H,W) u8, rec_face u32, rec_prob) -> idx (B,H,W,K) int64 (-1 pad), type u8 (0 pad),
+    prob (0 pad), for all rows or only `rows` (the others left as padding)."""
+    hits = np.asarray(hits).astype(np.int64)
+    rf = np.asarray(rec_face).view(np.uint32)
+    rp = np.asarray(rec_prob)
+    B, H, W = hits.shape
+    tx = (W + 63) // 64
+    rows = np.arange(H) if rows is None else np.asarray(rows)
+    idx = np.full((B, H, W, K), -1, np.int64)
+    typ = np.zeros((B, H, W, K), np.uint8)
+    prob = np.zeros((B, H, W, K), rp.dtype)
+    if K == 0 or len(rows) == 0:
+        return idx, typ, prob
+    h = np.zeros((B, len(rows), tx * 64), np.int64)
+    h[:, :, :W] = hits[:, rows]
+    h = h.reshape(B, len(rows), tx, 64)
+    pre = np.cumsum(h, -1) - h                                  # filled slots before the pixel
+    seg = (np.arange(B)[:, None, None] * H + rows[None, :, None]) * tx + np.arange(tx)[None, None, :]
+    base = (seg * 64 * K)[..., None] + pre                      # (B, R, tx, 64)
+    R = len(rows)
+    bi = np.full((B, R, W, K), -1, np.int64)
+    bt = np.zeros((B, R, W, K), np.uint8)
+    bp = np.zeros((B, R, W, K), rp.dtype)
+    for k in range(K):
+        sel = k < h
+        pos = np.where(sel, base + k, 0)
+        f = np.where(sel, rf[pos], 0).reshape(B, R, tx * 64)[:, :, :W]
+        p = np.where(sel, rp[pos], 0).reshape(B, R, tx * 64)[:, :, :W]
+        s = sel.reshape(B, R, tx * 64)[:, :, :W]
+        bi[..., k] = np.where(s, (f & 0x0fffffff).astype(np.int64), -1)
+        bt[..., k] = np.where(s, (f >> 28).astype(np.uint8), 0)
+        bp[..., k] = np.where(s, p, 0)
+    idx[:, rows] = bi
+    typ[:, rows] = bt
+    prob[:, rows] = bp
+    return idx, typ, prob

@@ -14,6 +14,7 @@ import pytest
 import torch
 
 from oracle import oracle as orc
+from dibr_util import assert_grads_equal
 
 pytestmark = pytest.mark.gpu
 
@@ -103,8 +104,8 @@ def test_rasterize_sphere_fixture(kal, golden, dname, flip, valid):
     assert np.array_equal(A(fidx), oi)
     assert np.array_equal(A(feats), of)
     gi, gf = orc.rasterize_backward(g[q + 'grad_out'], oi, ow, g[p + 'face_vertices_image'], g[p + 'face_uvs'], 1e-8)
-    np.testing.assert_allclose(A(fvi_r.grad), gi, rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(A(uv_r.grad), gf, rtol=1e-5, atol=1e-5)
+    assert_grads_equal(A(fvi_r.grad), gi)
+    assert_grads_equal(A(uv_r.grad), gf)
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
@@ -123,7 +124,7 @@ def test_packed_rasterize_vs_oracle(kal, dtype, H, W):
 @pytest.mark.parametrize('use_valid', [False, True])
 def test_fused_path_matches_packed_C_chain(kal, dtype, use_valid):
     """The fused front-end path (in-kernel packing / bbox / remap, gather backward) equals
-    the reference's torch-glue + packed _C chain: forward bit-exact, grads 1e-5."""
+    the reference's torch-glue + packed _C chain: forward and gradients bit-exact."""
     fvz, fvi, feat, fnz = _render_inputs(kal, 30, 50, 3, dtype)
     valid = (fnz >= 0) if use_valid else None
     outs = []
@@ -135,8 +136,8 @@ def test_fused_path_matches_packed_C_chain(kal, dtype, use_valid):
         f.backward(torch.rand(f.shape, generator=g, dtype=dtype).to(DEV))
         outs.append((f, i, a.grad, b.grad))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    np.testing.assert_allclose(A(outs[0][2]), A(outs[1][2]), rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(A(outs[0][3]), A(outs[1][3]), rtol=1e-5, atol=1e-5)
+    assert_grads_equal(A(outs[0][2]), A(outs[1][2]))
+    assert_grads_equal(A(outs[0][3]), A(outs[1][3]))
     # soft mask: fused (unscaled input, in-kernel bbox) vs the _C contract
     m, box = 1000., 0.02
     fm = (fvi * m).contiguous()
@@ -206,17 +207,13 @@ def test_soft_mask_adversarial_vs_oracle(kal, dtype, K):
     np.testing.assert_allclose(A(mask), om, rtol=1e-6, atol=1e-7)
     assert (oi[..., -1] >= 0).sum() > (100 if K == 8 else -1)  # K=8: many pixels saturate knum
     grad = torch.rand_like(mask)
-    ogi = orc.dibr_soft_mask_backward(A(grad), om, A(sel), op, oi, ot, fm, sig, m)
+    # the backward on identical saved values: the GPU forward's mask and probabilities
+    ogi = orc.dibr_soft_mask_backward(A(grad), A(mask), A(sel), A(prob), oi, ot, fm, sig, m)
     g1 = _fused.soft_mask_backward(grad, mask, sel, prob, cidx, ctype, T(v), sig, m, hits)
     g2 = kal._C.render.mesh.dibr_soft_mask_backward_cuda(grad, mask, sel, prob, cidx, ctype, T(fm), sig, m)
-    fin = np.isfinite(ogi)
-    assert fin.mean() > 0.9
-    # gradients are sums of per-pixel terms in an unspecified (atomic) order, as in the
-    # reference; with |terms| ~1e2 here, near-cancelling sums carry float32 order error
-    # ~eps * magnitude, so the absolute tolerance scales with the gradient magnitude
-    atol = max(1e-5, 4 * np.finfo(ogi.dtype).eps * np.abs(ogi[fin]).max())
-    np.testing.assert_allclose(A(g1)[fin], ogi[fin], rtol=1e-5, atol=atol)
-    np.testing.assert_allclose(A(g2)[fin], ogi[fin], rtol=1e-5, atol=atol)
+    assert np.isfinite(ogi).mean() > 0.9
+    assert_grads_equal(A(g1), ogi)
+    assert_grads_equal(A(g2), ogi)
 
 
 def test_dibr_bench_sphere_vs_oracle(kal):
@@ -244,8 +241,13 @@ def test_rasterize_backward_vs_oracle(kal):
     feats.backward(go)
     of, oi, ow = orc.rasterize(80, 80, A(fvz), A(fvi), A(feat), valid_faces=A(fnz >= 0))
     gi, gf = orc.rasterize_backward(A(go), oi, ow, A(fvi), A(feat), 1e-8)
-    np.testing.assert_allclose(A(fvi_r.grad), gi, rtol=1e-5, atol=1e-5)
-    np.testing.assert_allclose(A(feat_r.grad), gf, rtol=1e-5, atol=1e-5)
+    assert_grads_equal(A(fvi_r.grad), gi)
+    assert_grads_equal(A(feat_r.grad), gf)
+    # the _C contract's scatter backward (rasterize_backward_cuda), directly against the oracle
+    w = torch.from_numpy(ow).to(DEV)
+    g_img, g_feat = kal._C.render.mesh.rasterize_backward_cuda(go, feats, fidx, w, fvi, feat, 1e-8)
+    assert_grads_equal(A(g_img), gi)
+    assert_grads_equal(A(g_feat), gf)
 
 
 def test_packed_rasterize_C_direct(kal):
@@ -342,8 +344,8 @@ def test_soft_mask_vs_oracle(kal, dtype, knum):
         assert (oi[..., -1] >= 0).sum() > 0  # some pixels saturate knum
     grad = torch.rand_like(mask)
     gi = kal._C.render.mesh.dibr_soft_mask_backward_cuda(grad, mask, sel, prob, cidx, ctype, fm, sig, m)
-    ogi = orc.dibr_soft_mask_backward(A(grad), om, A(sel), op, oi, ot, A(fm), sig, m)
-    np.testing.assert_allclose(A(gi), ogi, rtol=1e-5, atol=1e-5)
+    ogi = orc.dibr_soft_mask_backward(A(grad), A(mask), A(sel), A(prob), oi, ot, A(fm), sig, m)
+    assert_grads_equal(A(gi), ogi)
 
 
 def test_dibr_rasterization_composition(kal):
@@ -366,28 +368,8 @@ def test_dibr_deterministic_forward(kal):
 # ------------------------------------------------- compact soft-mask state (fused path)
 def _decode_compact(state, H, W, K):
     """The compact records back into the reference's (B,H,W,K) slot tensors."""
-    hits = A(state.hits).astype(np.int64)
-    B = hits.shape[0]
-    tx = (W + 63) // 64
-    rf = A(state.rec_face).view(np.uint32)
-    rp = A(state.rec_prob)
-    idx = np.full((B, H, W, K), -1, np.int64)
-    typ = np.zeros((B, H, W, K), np.uint8)
-    prob = np.zeros((B, H, W, K), rp.dtype)
-    for b in range(B):
-        for j in range(H):
-            for t in range(tx):
-                seg = (b * H + j) * tx + t
-                base = seg * 64 * K
-                e = 0
-                for i in range(t * 64, min(W, t * 64 + 64)):
-                    for k in range(hits[b, j, i]):
-                        r = int(rf[base + e])
-                        idx[b, j, i, k] = r & 0x0fffffff
-                        typ[b, j, i, k] = r >> 28
-                        prob[b, j, i, k] = rp[base + e]
-                        e += 1
-    return idx, typ, prob
+    from dibr_util import decode_compact, state_arrays
+    return decode_compact(*state_arrays(state), K)
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
@@ -413,11 +395,9 @@ def test_soft_mask_compact_vs_oracle(kal, dtype, K):
     assert np.array_equal(typ, ot)
     np.testing.assert_allclose(prob, op, rtol=1e-6, atol=1e-7)
     grad = torch.rand_like(mask)
-    ogi = orc.dibr_soft_mask_backward(A(grad), om, A(sel), op, oi, ot, fm, sig, m)
+    ogi = orc.dibr_soft_mask_backward(A(grad), A(mask), A(sel), prob, oi, ot, fm, sig, m)  # GPU's saved values
     g1 = _fused.soft_mask_backward_compact(grad, mask, state, T(v), sig, m)
-    fin = np.isfinite(ogi)
-    atol = max(1e-5, 4 * np.finfo(ogi.dtype).eps * np.abs(ogi[fin]).max()) if fin.any() else 1e-5
-    np.testing.assert_allclose(A(g1)[fin], ogi[fin], rtol=1e-5, atol=atol)
+    assert_grads_equal(A(g1), ogi)
     assert int(state.scratch.item()) == 0
 
 
@@ -448,15 +428,19 @@ def test_dibr_rasterization_fused_grads_vs_oracle(kal, which):
         gi_r, gfe = orc.rasterize_backward(A(gf), oi, ow, A(fvi), A(feat), 1e-8)
         gi = gi + gi_r
     if which in ('both', 'mask'):
-        gi = gi + orc.dibr_soft_mask_backward(A(gm), om, oi, op, oci, oct_, fm, 7000., 1000.)
-    atol = max(1e-5, 4 * np.finfo(np.float32).eps * np.abs(gi).max())
-    np.testing.assert_allclose(A(a.grad), gi, rtol=1e-5, atol=atol)
-    np.testing.assert_allclose(A(b.grad), gfe, rtol=1e-5, atol=1e-5)
+        # the soft-mask backward on the GPU forward's saved values (its mask and probabilities,
+        # which equal the oracle's to expf ulps)
+        from kaolin import _fused
+        _, state = _fused.soft_mask_forward_compact(fvi, idx, 7000., 0.02, 30, 1000.)
+        _, _, gp = _decode_compact(state, 96, 128, 30)
+        gi = gi + orc.dibr_soft_mask_backward(A(gm), A(mask), oi, gp, oci, oct_, fm, 7000., 1000.)
+    assert_grads_equal(A(a.grad), gi)
+    assert_grads_equal(A(b.grad), gfe)
     # a second backward through the retained graph gives the same gradients again
     g1 = a.grad.clone()
     a.grad = None
     torch.autograd.backward(outs, grads)
-    np.testing.assert_allclose(A(a.grad), A(g1), rtol=1e-5, atol=atol)
+    assert torch.equal(a.grad, g1)
 
 
 def test_dibr_bench_full_size_fused_equals_C_chain(kal):
@@ -479,9 +463,8 @@ def test_dibr_bench_full_size_fused_equals_C_chain(kal):
     sm = kal.render.mesh.dibr_soft_mask(a2, i2, 7000, 0.02, 30, 1000.)
     assert torch.equal(sm, m2)
     (f2 * inp['g_feat']).sum().add((sm * inp['g_mask']).sum()).backward()
-    scale = float(a2.grad.abs().max())
-    torch.testing.assert_close(a1.grad, a2.grad, rtol=1e-4, atol=1e-5 * max(1., scale))
-    torch.testing.assert_close(b1.grad, b2.grad, rtol=1e-4, atol=1e-5)
+    assert torch.equal(a1.grad, a2.grad)  # both sum in double and round once
+    assert torch.equal(b1.grad, b2.grad)
 
 
 # ------------------------------------------------------------ point_to_mesh
