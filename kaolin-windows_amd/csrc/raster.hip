@@ -770,7 +770,7 @@ struct RastTileWs {
   RastTileWs(const BinGeom &g, int B, int F, size_t tsize) {
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
     off_hist = g.bytes();
-    off_rec = (off_hist + ORD_BUCKETS * sizeof(int) + 255) & ~(size_t)255;
+    off_rec = (off_hist + ORD_HIST * sizeof(int) + 255) & ~(size_t)255;
     off_rng = off_rec + (((size_t)B * F * RT_REC * tsize + 255) & ~(size_t)255);
     off_bk = (off_rng + (size_t)B * F * sizeof(uint2) + 255) & ~(size_t)255;
     off_items = (off_bk + nt + 255) & ~(size_t)255;
@@ -805,7 +805,7 @@ static int launch_rast_tile(RastSrc<T> src, int H, int W, int B, int D, int F, c
   uint8_t *bk = reinterpret_cast<uint8_t *>(w + L.off_bk);
   int32_t *items = reinterpret_cast<int32_t *>(w + L.off_items);
   int *nitems = reinterpret_cast<int *>(w + L.off_n);
-  KL_CHECK_RC(fill_async(bitmap, 0, L.off_hist + ORD_BUCKETS * sizeof(int), st));
+  KL_CHECK_RC(fill_async(bitmap, 0, L.off_hist + ORD_HIST * sizeof(int), st));
   const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);
   const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
   if (src.vmask)
@@ -1357,8 +1357,8 @@ struct DibrFwdWs {
     auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
     off_sbm = g.bytes();
     off_rgh = off_sbm + g.bytes();
-    off_sgh = off_rgh + ORD_BUCKETS * sizeof(int);
-    zero = off_sgh + ORD_BUCKETS * sizeof(int);
+    off_sgh = off_rgh + ORD_HIST * sizeof(int);
+    zero = off_sgh + ORD_HIST * sizeof(int);
     off_rec = up(zero);
     off_rng = up(off_rec + (size_t)B * F * RT_REC * sizeof(double));
     off_rbk = up(off_rng + (size_t)B * F * sizeof(uint2));

@@ -670,7 +670,7 @@ struct StWs {
   StWs(const BinGeom &g, int F) {
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
     hist = g.bytes();
-    zero = hist + (ORD_BUCKETS + 1) * sizeof(int);
+    zero = hist + (ORD_HIST + 1) * sizeof(int);
     bk = (zero + 255) & ~(size_t)255;
     order = (bk + nt + 255) & ~(size_t)255;
     nitems = order + nt * TILE_H * sizeof(int32_t);

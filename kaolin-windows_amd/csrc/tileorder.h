@@ -7,6 +7,10 @@
 namespace kl {
 
 constexpr int ORD_BUCKETS = 32;
+constexpr int ORD_HIST = 8 * ORD_BUCKETS;  // histogram ints: (band, bucket) tile counts (tile_band below)
+
+// Tiles are cut into 8 bands of consecutive tiles (XCD-aware placement, see place_items).
+__device__ __forceinline__ int tile_band(int u, int nt) { return (int)((int64_t)u * 8 / nt); }
 
 // Counting sort of the tiles on floor(log2(count + 1)) of their candidate-chunk counts
 // (set bits of the tile's bitmap words), descending.  Two kernels: one wave per tile
@@ -16,9 +20,9 @@ constexpr int ORD_BUCKETS = 32;
 static __global__ void __launch_bounds__(256) tile_bucket_kernel(const uint32_t *__restrict__ bitmap, int words, int nt,
                                                           uint8_t *__restrict__ bk, int *__restrict__ ghist,
                                                           int *__restrict__ scratch) {
-  __shared__ int hist[ORD_BUCKETS];
+  __shared__ int hist[ORD_HIST];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x < ORD_BUCKETS) hist[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < ORD_HIST; i += blockDim.x) hist[i] = 0;
   if (threadIdx.x == 0 && blockIdx.x == 0 && scratch) *scratch = 0;
   __syncthreads();
   const int t = blockIdx.x * (blockDim.x >> 6) + wid;  // one wave per tile
@@ -31,63 +35,122 @@ static __global__ void __launch_bounds__(256) tile_bucket_kernel(const uint32_t 
     if (lane == 0) {
       const int b = 31 - __clz(n + 1u);
       bk[t] = (uint8_t)b;
-      atomicAdd(&hist[b], 1);
+      atomicAdd(&hist[tile_band(t, nt) * ORD_BUCKETS + b], 1);
     }
   }
   __syncthreads();
-  if (threadIdx.x < ORD_BUCKETS && hist[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], hist[threadIdx.x]);
+  for (int i = threadIdx.x; i < ORD_HIST; i += blockDim.x)
+    if (hist[i]) atomicAdd(&ghist[i], hist[i]);
 }
 
-// Work items, heaviest first: tile | part << 24 | log2(parts) << 28.  Tiles of bucket
-// >= split_from become 2^split_log2 items (parts of the tile's rows), the others one.
-// nitems (optional) receives the item count.  identity: grid order, no split (dev ablation).
-// `base` is a workgroup-shared [ORD_BUCKETS] array.
-__device__ __forceinline__ void order_items(int *base, const uint8_t *__restrict__ bk, const int *__restrict__ ghist,
-                                            int nt, int32_t *__restrict__ order, int identity, int split_from,
-                                            int split_log2, int *__restrict__ nitems) {
+// Work items: tile | part << 24 | lp << 28, a tile's rows cut into 2^lp parts.
+//
+// XCD-aware placement.  Workgroups are dealt round-robin over the 8 XCDs (block b and b + 8
+// share one; MI355X_MICROARCH.md, "Workgroup dispatch"), and each XCD has its own L2.  A
+// tile's work reads the face records / ranges of the faces over it, chunk by chunk, so tiles
+// far apart on different XCDs fetch the same lines from HBM once per XCD.  The tiles are cut
+// into 8 bands of consecutive tiles (tile rows of one view); band g's items go to positions
+// p = 8 r + g (r = the item's rank in the band, heaviest first), so each XCD walks one
+// band's faces.  Bands with more items than their share of positions (N / 8) place the
+// rest, lightest last, in the other classes' free positions.  For speed only: the results do
+// not depend on the placement.
+// The order kernels keep the tiles' buckets in LDS (one global read) up to this many tiles.
+constexpr int ORD_LDS_TILES = 16384;
+
+// lpb[q]: parts (log2) of a tile of bucket q; ghist: tiles per (band, bucket) (bucket kernels);
+// bk: the buckets, in LDS when nt <= ORD_LDS_TILES.  Shared scratch: sb[8*32], sx[32].  All
+// threads of the (single) workgroup call it.
+__device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, const int *__restrict__ ghist,
+                                            const uint8_t *__restrict__ bk, int nt, int32_t *__restrict__ order,
+                                            int *__restrict__ nitems) {
+  __syncthreads();  // lpb / staged buckets written
+  // per band, the exclusive prefix over buckets, heaviest first: one lane per (band, bucket),
+  // a 32-lane segmented scan (two bands per wave)
+  if (threadIdx.x < 8 * ORD_BUCKETS) {
+    const int t = threadIdx.x, g = t / ORD_BUCKETS, q = ORD_BUCKETS - 1 - t % ORD_BUCKETS;
+    const int v = ghist[g * ORD_BUCKETS + q] << lpb[q];  // items of (band g, bucket q)
+    int inc = v;
+#pragma unroll
+    for (int o = 1; o < ORD_BUCKETS; o <<= 1) {
+      const int w = __shfl_up(inc, o);
+      if (t % ORD_BUCKETS >= o) inc += w;
+    }
+    sb[g * ORD_BUCKETS + q] = inc - v;
+    if (q == 0) sx[8 + g] = inc;  // items of band g
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int n[8], N = 0;
+    for (int g = 0; g < 8; g++) {
+      n[g] = sx[8 + g];
+      N += n[g];
+    }
+    int ob = 0, fp = 0;
+    for (int g = 0; g < 8; g++) {
+      const int cap = N / 8 + (g < N % 8 ? 1 : 0);
+      sx[g] = cap;                 // positions of class g
+      sx[8 + g] = n[g];            // items of band g
+      sx[16 + g] = ob;             // first overflow index of band g
+      sx[24 + g] = fp;             // first free-slot index of class g
+      ob += n[g] > cap ? n[g] - cap : 0;
+      fp += cap > n[g] ? cap - n[g] : 0;
+    }
+    if (nitems) *nitems = N;
+  }
+  __syncthreads();
+  for (int u = threadIdx.x; u < nt; u += blockDim.x) {
+    const int q = bk[u], g = tile_band(u, nt), lp = lpb[q], np = 1 << lp;
+    const int r0 = atomicAdd(&sb[g * ORD_BUCKETS + q], np);
+    for (int k = 0; k < np; k++) {
+      const int r = r0 + k;
+      int pos;
+      if (r < sx[g]) {
+        pos = r * 8 + g;
+      } else {  // the j-th overflow item takes the j-th free position
+        const int j = sx[16 + g] + r - sx[g];
+        int x = 0;
+        while (x < 7 && sx[24 + x + 1] <= j) x++;
+        pos = (sx[8 + x] + j - sx[24 + x]) * 8 + x;
+      }
+      order[pos] = u | (k << 24) | (lp << 28);
+    }
+  }
+}
+
+// The rasterizer's items: tiles of bucket >= split_from become 2^split_log2 items (parts of
+// the tile's rows), the others one.  nitems (optional) receives the item count.  identity:
+// grid order, no split (dev ablation).
+__device__ __forceinline__ void order_items(int *sb, int *sx, int *lpb, const int *__restrict__ ghist,
+                                            const uint8_t *__restrict__ bk, int nt, int32_t *__restrict__ order,
+                                            int identity, int split_from, int split_log2,
+                                            int *__restrict__ nitems) {
   if (identity) {
     for (int u = threadIdx.x; u < nt; u += blockDim.x) order[u] = u;
     if (nitems && threadIdx.x == 0) *nitems = nt;
     return;
   }
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
-      base[q] = s;
-      s += ghist[q] << (q >= split_from ? split_log2 : 0);
-    }
-    if (nitems) *nitems = s;
-  }
-  __syncthreads();
-  for (int u = threadIdx.x; u < nt; u += blockDim.x) {
-    const int q = bk[u];
-    if (q >= split_from) {
-      const int np = 1 << split_log2;
-      const int o = atomicAdd(&base[q], np);
-      for (int k = 0; k < np; k++) order[o + k] = u | (k << 24) | (split_log2 << 28);
-    } else {
-      order[atomicAdd(&base[q], 1)] = u;
-    }
-  }
+  if (threadIdx.x < ORD_BUCKETS) lpb[threadIdx.x] = (int)threadIdx.x >= split_from ? split_log2 : 0;
+  place_items(sb, sx, lpb, ghist, bk, nt, order, nitems);
 }
 
-// Soft-mask work items (softtile.hip), heaviest first: tile | part << 24 | lp << 28.  A tile's
-// 8 rows are cut into 2^lp parts of 8 >> lp rows, one 4-wave workgroup per part.  lp is lp_min
-// (set by the LDS the slot lists need) except for the heaviest buckets: >= ST_B8 candidate-chunk
-// bucket -> 8 parts (one row, 4 waves sharing its evaluation), >= ST_B4 -> 4 parts (2 rows,
-// 2 waves each), at most ST_CAP8 / ST_CAP4 tiles each, so that soft_items_bound() holds.
+// Soft-mask work items (softtile.hip).  A 4-wave workgroup takes one part.  lp is lp_min (set
+// by the LDS the slot lists need) except for the heaviest buckets: >= ST_B8 candidate-chunk
+// bucket -> 8 parts (one row, 4 waves sharing its walk and evaluation), >= ST_B4 -> 4 parts
+// (2 rows, 2 waves each), at most ST_CAP8 / ST_CAP4 tiles each, so that soft_items_bound()
+// holds.
 constexpr int ST_B4 = 5, ST_B8 = 6, ST_CAP4 = 256, ST_CAP8 = 128;
 inline int soft_items_bound(int nt, int lp_min) {
   auto extra = [&](int lp, int cap) { return lp > lp_min ? cap * ((1 << lp) - (1 << lp_min)) : 0; };
   return (nt << lp_min) + extra(2, ST_CAP4) + extra(3, ST_CAP8);
 }
-__device__ __forceinline__ void order_soft_items(int *base, int *lpb, const uint8_t *__restrict__ bk,
+__device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, const uint8_t *__restrict__ bk,
                                                  const int *__restrict__ ghist, int nt, int32_t *__restrict__ order,
                                                  int lp_min, int *__restrict__ nitems) {
   if (threadIdx.x == 0) {
-    int s = 0, n4 = 0, n8 = 0;
+    int n4 = 0, n8 = 0;
     for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
-      const int h = ghist[q];
+      int h = 0;  // tiles of bucket q over the bands
+      for (int g = 0; g < 8; g++) h += ghist[g * ORD_BUCKETS + q];
       int lp = lp_min;
       if (q >= ST_B8 && n8 + h <= ST_CAP8) {
         lp = lp > 3 ? lp : 3;
@@ -97,25 +160,26 @@ __device__ __forceinline__ void order_soft_items(int *base, int *lpb, const uint
         n4 += h;
       }
       lpb[q] = lp;
-      base[q] = s;
-      s += h << lp;
     }
-    *nitems = s;
   }
-  __syncthreads();
-  for (int u = threadIdx.x; u < nt; u += blockDim.x) {
-    const int q = bk[u], lp = lpb[q], np = 1 << lp;
-    const int o = atomicAdd(&base[q], np);
-    for (int k = 0; k < np; k++) order[o + k] = u | (k << 24) | (lp << 28);
-  }
+  place_items(sb, sx, lpb, ghist, bk, nt, order, nitems);
+}
+
+// the buckets of tiles [0, nt) into LDS when they fit (else the global array is used)
+__device__ __forceinline__ const uint8_t *stage_buckets(uint8_t *lds, const uint8_t *__restrict__ bk, int nt) {
+  if (nt > ORD_LDS_TILES) return bk;
+  for (int u = threadIdx.x; u < nt; u += blockDim.x) lds[u] = bk[u];
+  return lds;  // (the first barrier of place_items orders these writes)
 }
 
 static __global__ void __launch_bounds__(1024) soft_order_kernel(const uint8_t *__restrict__ bk,
                                                                  const int *__restrict__ ghist, int nt,
                                                                  int32_t *__restrict__ order, int lp_min,
                                                                  int *__restrict__ nitems) {
-  __shared__ int base[ORD_BUCKETS], lpb[ORD_BUCKETS];
-  order_soft_items(base, lpb, bk, ghist, nt, order, lp_min, nitems);
+  __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS];
+  __shared__ uint8_t sbk[ORD_LDS_TILES];
+  const uint8_t *b = stage_buckets(sbk, bk, nt);
+  order_soft_items(sb, sx, lpb, b, ghist, nt, order, lp_min, nitems);
 }
 
 static __global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *__restrict__ bk,
@@ -123,8 +187,10 @@ static __global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *
                                                                  int32_t *__restrict__ order, int identity,
                                                                  int split_from, int split_log2,
                                                                  int *__restrict__ nitems) {
-  __shared__ int base[ORD_BUCKETS];
-  order_items(base, bk, ghist, nt, order, identity, split_from, split_log2, nitems);
+  __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS];
+  __shared__ uint8_t sbk[ORD_LDS_TILES];
+  const uint8_t *b = identity ? bk : stage_buckets(sbk, bk, nt);
+  order_items(sb, sx, lpb, ghist, b, nt, order, identity, split_from, split_log2, nitems);
 }
 
 // Two bitmaps over the same tiles at once (kl_dibr_forward: the rasterizer's and the soft
@@ -135,9 +201,9 @@ static __global__ void __launch_bounds__(256) tile_bucket2_kernel(const uint32_t
                                                                   uint8_t *__restrict__ bk0, uint8_t *__restrict__ bk1,
                                                                   int *__restrict__ gh0, int *__restrict__ gh1,
                                                                   int *__restrict__ scratch) {
-  __shared__ int hist[2][ORD_BUCKETS];
+  __shared__ int hist[2][ORD_HIST];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x < 2 * ORD_BUCKETS) hist[threadIdx.x / ORD_BUCKETS][threadIdx.x % ORD_BUCKETS] = 0;
+  for (int i = threadIdx.x; i < 2 * ORD_HIST; i += blockDim.x) hist[i / ORD_HIST][i % ORD_HIST] = 0;
   if (threadIdx.x == 0 && blockIdx.x == 0 && scratch) *scratch = 0;
   __syncthreads();
   const int t = blockIdx.x * (blockDim.x >> 6) + wid;
@@ -153,17 +219,17 @@ static __global__ void __launch_bounds__(256) tile_bucket2_kernel(const uint32_t
       n1 += __shfl_xor(n1, o);
     }
     if (lane == 0) {
-      const int b0 = 31 - __clz(n0 + 1u), b1 = 31 - __clz(n1 + 1u);
+      const int b0 = 31 - __clz(n0 + 1u), b1 = 31 - __clz(n1 + 1u), band = tile_band(t, nt);
       bk0[t] = (uint8_t)b0;
       bk1[t] = (uint8_t)b1;
-      atomicAdd(&hist[0][b0], 1);
-      atomicAdd(&hist[1][b1], 1);
+      atomicAdd(&hist[0][band * ORD_BUCKETS + b0], 1);
+      atomicAdd(&hist[1][band * ORD_BUCKETS + b1], 1);
     }
   }
   __syncthreads();
-  if (threadIdx.x < 2 * ORD_BUCKETS) {
-    const int h = hist[threadIdx.x / ORD_BUCKETS][threadIdx.x % ORD_BUCKETS];
-    if (h) atomicAdd((threadIdx.x < ORD_BUCKETS ? gh0 : gh1) + threadIdx.x % ORD_BUCKETS, h);
+  for (int i = threadIdx.x; i < 2 * ORD_HIST; i += blockDim.x) {
+    const int h = hist[i / ORD_HIST][i % ORD_HIST];
+    if (h) atomicAdd((i < ORD_HIST ? gh0 : gh1) + i % ORD_HIST, h);
   }
 }
 
@@ -175,9 +241,22 @@ static __global__ void __launch_bounds__(1024) tile_order2_kernel(const uint8_t 
                                                                   const int *__restrict__ gh1,
                                                                   int32_t *__restrict__ order1, int nt, int lp_min1,
                                                                   int *__restrict__ nitems1) {
-  __shared__ int base[2][ORD_BUCKETS], lpb[ORD_BUCKETS];
-  order_items(base[0], bk0, gh0, nt, order0, 0, split_from, split_log2, nitems0);
-  order_soft_items(base[1], lpb, bk1, gh1, nt, order1, lp_min1, nitems1);
+  __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS];
+  __shared__ uint8_t sbk[2][ORD_LDS_TILES];
+  // both bitmaps' buckets read at once (their loads in flight together)
+  const uint8_t *b0 = bk0, *b1 = bk1;
+  if (nt <= ORD_LDS_TILES) {
+    for (int u = threadIdx.x; u < nt; u += blockDim.x) {
+      const uint8_t q0 = bk0[u], q1 = bk1[u];
+      sbk[0][u] = q0;
+      sbk[1][u] = q1;
+    }
+    b0 = sbk[0];
+    b1 = sbk[1];
+  }
+  order_items(sb, sx, lpb, gh0, b0, nt, order0, 0, split_from, split_log2, nitems0);
+  __syncthreads();
+  order_soft_items(sb, sx, lpb, b1, gh1, nt, order1, lp_min1, nitems1);
 }
 
 }  // namespace kl
