@@ -555,10 +555,29 @@ def p2m_leg(device, world, rank, steps, points=None, face_vertices=None, grad=No
            'value': round(P * F / t_f / 1e6, 1), 'ms': round(t_f * 1e3, 4),
            'fwd_bwd': {'value': round(P * F / t_fb / 1e6, 1), 'ms': round(t_fb * 1e3, 4)},
            'n_ranks': world, 'points_per_rank': hi - lo, 'faces': F,
-           'roofline': {'bound': 'valu', 'flop_per_pair': 50, 'note': 'nominal pairs (P*F); pruned pairs are not evaluated',
-                        'achieved_tflops': round(P * F / t_f * 50 / 1e12, 2), 'peak_tflops': FP32_PEAK_TFLOPS,
-                        'frac': round(P * F / t_f * 50 / 1e12 / FP32_PEAK_TFLOPS, 4)}}
+           'roofline': p2m_roofline(P, F, t_f)}
     return res, out, (lp.grad, fvr.grad)
+
+
+def p2m_roofline(P, F, t_f):
+    """p2m forward against the FP32 VALU peak.  `frac` prices the NOMINAL pairs (P*F x 50 flop,
+    SURVEY.md 8d); the kernel evaluates only the (wave, face) pairs its bounds cannot skip, so the
+    committed counter profile (profiles/r02c_p2m_pmc.json: probe + SQ_INSTS_VALU*_F32 passes) gives
+    the executed share, executed FP32 rate and VALU issue occupancy beside it."""
+    nominal = P * F * 50 / t_f / 1e12
+    r = {'bound': 'valu', 'flop_per_pair': 50, 'note': 'nominal pairs (P*F); pruned pairs are not evaluated',
+         'achieved_tflops': round(nominal, 2), 'peak_tflops': FP32_PEAK_TFLOPS,
+         'frac': round(nominal / FP32_PEAK_TFLOPS, 4)}
+    path = os.path.join(ROOT, 'profiles', 'r02c_p2m_pmc.json')
+    if P == 100000 and F == 20000 and os.path.exists(path):
+        pm = json.load(open(path))
+        r['measured'] = {'source': 'profiles/r02c_p2m_pmc.json (cfg2, one rank)',
+                         'evaluated_pair_fraction': pm['wave_face_pairs']['evaluated_fraction'],
+                         'executed_fp32_tflops': pm['executed_tflops'],
+                         'executed_frac': round(pm['executed_tflops'] / FP32_PEAK_TFLOPS, 4),
+                         'valu_issue_busy': pm['valu_issue_busy_est'],
+                         'wait_any_fraction': pm['wait_any_fraction_of_wave_cycles']}
+    return r
 
 
 def p2m_parity(points, face_vertices, out, n_sample=2000):
