@@ -29,10 +29,27 @@ __device__ __forceinline__ uint64_t stamp_clk() { return __builtin_readcyclecoun
 __device__ __forceinline__ uint64_t stamp_wall() { return __builtin_amdgcn_s_memrealtime(); }
 // memset as a kernel launch on `st` (graph-capture friendly); returns a kl_status
 int fill_async(void *p, int value, size_t bytes, hipStream_t st);
+// Fork/join of one side stream of the current device inside one ABI call (event record +
+// wait, so it is captured into a HIP graph as two parallel branches).  SideFork's
+// constructor locks the device's side stream and makes it wait for `st`; side() is that
+// stream, or `st` itself when none could be made (the work then runs in order); join()
+// makes `st` wait for the side work.  The destructor joins if join() was not called.
+class SideFork {
+ public:
+  explicit SideFork(hipStream_t st);
+  ~SideFork();
+  hipStream_t side() const { return side_; }
+  int join();
+ private:
+  hipStream_t st_, side_;
+  void *slot_;
+  bool joined_;
+};
 // out[i] = (T)acc[i], or out[i] + (T)acc[i] with accumulate: the single rounding of a gradient
 // summed in double (raster.hip)
+// `reset` (optional): an int zeroed by the same launch.
 template <typename T>
-int acc_finalize(const double *acc, T *out, size_t n, bool accumulate, hipStream_t st);
+int acc_finalize(const double *acc, T *out, size_t n, bool accumulate, hipStream_t st, int *reset = nullptr);
 inline size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 #define KL_CHECK_HIP(expr)                                                              \

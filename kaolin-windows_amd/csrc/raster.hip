@@ -894,20 +894,22 @@ struct BaryGrad {
 // The single rounding of a gradient summed in double (common.h).
 template <typename T>
 __global__ void __launch_bounds__(256) acc_finalize_kernel(const double *__restrict__ acc, T *__restrict__ out,
-                                                           size_t n, int accumulate) {
+                                                           size_t n, int accumulate, int *__restrict__ reset) {
+  if (reset && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     out[i] = accumulate ? out[i] + (T)acc[i] : (T)acc[i];
 }
 template <typename T>
-int acc_finalize(const double *acc, T *out, size_t n, bool accumulate, hipStream_t st) {
-  if (n == 0) return KL_OK;
+int acc_finalize(const double *acc, T *out, size_t n, bool accumulate, hipStream_t st, int *reset) {
+  if (n == 0) return reset ? fill_async(reset, 0, sizeof(int), st) : KL_OK;
   const unsigned blocks = (unsigned)std::min<int64_t>(cdiv((int64_t)n, 256), 8192);
-  hipLaunchKernelGGL((acc_finalize_kernel<T>), dim3(blocks), dim3(256), 0, st, acc, out, n, accumulate ? 1 : 0);
+  hipLaunchKernelGGL((acc_finalize_kernel<T>), dim3(blocks), dim3(256), 0, st, acc, out, n, accumulate ? 1 : 0,
+                     reset);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
-template int acc_finalize<float>(const double *, float *, size_t, bool, hipStream_t);
-template int acc_finalize<double>(const double *, double *, size_t, bool, hipStream_t);
+template int acc_finalize<float>(const double *, float *, size_t, bool, hipStream_t, int *);
+template int acc_finalize<double>(const double *, double *, size_t, bool, hipStream_t, int *);
 
 // The _C contract's scatter backward (rasterize_backward_cuda takes no multiplier, so the
 // faces' pixel ranges are unknown): one thread per pixel, the reference's terms added with
@@ -1341,7 +1343,7 @@ extern "C" int kl_dibr_rasterize_backward(kl_dtype dtype, int batch, int height,
 // compact path (softtile.hip) on the rasterizer's face index.  The backward runs the
 // gather (which writes every face's gradient) and adds the soft-mask terms onto it.
 // The state's scratch int is the gather's big-face counter: the forward zeroes it and
-// the soft-mask backward re-zeroes it, so the backward needs no fill of its own.
+// the backward's final add re-zeroes it (retain_graph), so the backward needs no fill of it.
 namespace kl {
 // Workspace of kl_dibr_forward: the rasterizer's and the soft mask's bins are built by one
 // pass over the faces, counted by one bucket kernel and ordered by one order kernel.
@@ -1422,7 +1424,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
                      (const uint32_t *)sbm, g.words, nt, rbk, sbk, rgh, sgh, s.scratch);
   KL_CHECK_LAUNCH();
   const int split_from = 5, split_log2 = sizeof(T) == 4 ? 2 : 0;
-  hipLaunchKernelGGL(tile_order2_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh, items,
+  hipLaunchKernelGGL(tile_order2_kernel, dim3(2), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh, items,
                      split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt,
                      soft_lp_min(K), snitems);
   KL_CHECK_LAUNCH();
@@ -1441,18 +1443,31 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
                     const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *ws,
                     size_t ws_bytes, hipStream_t st, const uint2 *face_ranges) {
   KL_REQUIRE(D <= 8, "dibr_rasterization backward: feature dimension > 8 is not supported by the fused path");
-  // workspace: the soft mask's double sums | (its items, then the gather's big-face list)
+  // workspace: the soft mask's double sums | its items | the gather's big-face list
   const size_t acc_bytes = al256((size_t)B * F * 6 * sizeof(double));
-  KL_REQUIRE(ws_bytes >= acc_bytes, "dibr_rasterization backward: workspace too small");
+  const size_t soft_bytes = al256(soft_tile_bwd_items_bytes(B, H, W, K));
+  KL_REQUIRE(ws_bytes >= acc_bytes + soft_bytes, "dibr_rasterization backward: workspace too small");
   double *acc = reinterpret_cast<double *>(ws);
-  void *rest = reinterpret_cast<char *>(ws) + acc_bytes;
+  void *soft_ws = reinterpret_cast<char *>(ws) + acc_bytes;
+  void *gath_ws = reinterpret_cast<char *>(soft_ws) + soft_bytes;
   bool has_soft = false;
-  // the soft-mask sums first (left in double); the gather then writes every face's gradient as
-  // its own rounded sum + the soft mask's rounded sum (no zero fill, no separate finalize)
-  KL_CHECK_RC(soft_tile_backward<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m, gfvi, true, rest,
-                                    ws_bytes - acc_bytes, st, acc, &has_soft));
-  return rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi, gfeat,
-                                 rest, ws_bytes - acc_bytes, s.scratch, st, face_ranges, has_soft ? acc : nullptr);
+  // The two halves are independent until the final add, so they run concurrently: the
+  // soft-mask sums (fill, plan, backward; left in double) on the side stream, the
+  // rasterizer's gather (every face's own rounded gradient) on `st`; after the join each
+  // coordinate gets the soft sum rounded on its own and added, as autograd adds the two
+  // gradients.  The gather's big-face counter is the state's scratch int (zeroed by the
+  // forward), re-zeroed by that final add; the soft half does not touch it.
+  SideFork fork(st);
+  SoftState<T> ss = s;
+  ss.scratch = nullptr;
+  KL_CHECK_RC(soft_tile_backward<T>(B, H, W, F, K, grad_mask, mask, ss, fvi, sigmainv, m, gfvi, true, soft_ws,
+                                    soft_bytes, fork.side(), acc, &has_soft));
+  KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
+                                      gfeat, gath_ws, ws_bytes - acc_bytes - soft_bytes, s.scratch, st, face_ranges,
+                                      nullptr));
+  KL_CHECK_RC(fork.join());
+  return has_soft ? acc_finalize<T>(acc, gfvi, (size_t)B * F * 6, true, st, s.scratch)
+                  : (s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK);
 }
 }  // namespace kl
 
@@ -1466,7 +1481,7 @@ extern "C" size_t kl_dibr_workspace_bytes(int batch, int height, int width, int 
 extern "C" size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum) {
   const size_t a = kl_dibr_rasterize_bwd_workspace_bytes(batch, height, width, num_faces, 8);
   const size_t b = soft_tile_bwd_items_bytes(batch, height, width, knum);
-  return al256((size_t)batch * num_faces * 6 * sizeof(double)) + (a > b ? a : b);
+  return al256((size_t)batch * num_faces * 6 * sizeof(double)) + al256(b) + a;
 }
 
 extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,

@@ -146,11 +146,19 @@ inline int soft_items_bound(int nt, int lp_min) {
 __device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, const uint8_t *__restrict__ bk,
                                                  const int *__restrict__ ghist, int nt, int32_t *__restrict__ order,
                                                  int lp_min, int *__restrict__ nitems) {
+  // tiles per bucket summed over the bands (one lane per bucket), then the caps walked
+  // serially from the heaviest bucket down on LDS values
+  if (threadIdx.x < ORD_BUCKETS) {
+    int h = 0;
+#pragma unroll
+    for (int g = 0; g < 8; g++) h += ghist[g * ORD_BUCKETS + threadIdx.x];
+    sx[threadIdx.x] = h;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     int n4 = 0, n8 = 0;
     for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
-      int h = 0;  // tiles of bucket q over the bands
-      for (int g = 0; g < 8; g++) h += ghist[g * ORD_BUCKETS + q];
+      const int h = sx[q];
       int lp = lp_min;
       if (q >= ST_B8 && n8 + h <= ST_CAP8) {
         lp = lp > 3 ? lp : 3;
@@ -162,6 +170,7 @@ __device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, con
       lpb[q] = lp;
     }
   }
+  __syncthreads();  // sx is reused by place_items
   place_items(sb, sx, lpb, ghist, bk, nt, order, nitems);
 }
 
@@ -242,21 +251,14 @@ static __global__ void __launch_bounds__(1024) tile_order2_kernel(const uint8_t 
                                                                   int32_t *__restrict__ order1, int nt, int lp_min1,
                                                                   int *__restrict__ nitems1) {
   __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS];
-  __shared__ uint8_t sbk[2][ORD_LDS_TILES];
-  // both bitmaps' buckets read at once (their loads in flight together)
-  const uint8_t *b0 = bk0, *b1 = bk1;
-  if (nt <= ORD_LDS_TILES) {
-    for (int u = threadIdx.x; u < nt; u += blockDim.x) {
-      const uint8_t q0 = bk0[u], q1 = bk1[u];
-      sbk[0][u] = q0;
-      sbk[1][u] = q1;
-    }
-    b0 = sbk[0];
-    b1 = sbk[1];
-  }
-  order_items(sb, sx, lpb, gh0, b0, nt, order0, 0, split_from, split_log2, nitems0);
-  __syncthreads();
-  order_soft_items(sb, sx, lpb, b1, gh1, nt, order1, lp_min1, nitems1);
+  __shared__ uint8_t sbk[ORD_LDS_TILES];
+  // two workgroups: block 0 orders the rasterizer's items, block 1 the soft mask's
+  const bool soft = blockIdx.x == 1;
+  const uint8_t *b = stage_buckets(sbk, soft ? bk1 : bk0, nt);
+  if (soft)
+    order_soft_items(sb, sx, lpb, b, gh1, nt, order1, lp_min1, nitems1);
+  else
+    order_items(sb, sx, lpb, gh0, b, nt, order0, 0, split_from, split_log2, nitems0);
 }
 
 }  // namespace kl
