@@ -59,7 +59,7 @@ def packed_rasterize_forward_cuda(height, width, face_vertices_z, face_vertices_
     lib = N.lib()
     ws_bytes = lib.kl_rasterize_workspace_bytes(batch_size, height, width, maxf)
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_packed_rasterize_forward(
             N.dtype_code(dtype), height, width, batch_size, num_faces, feat_dim, maxf,
             N.ptr(face_vertices_z), N.ptr(face_vertices_image), N.ptr(face_bboxes), N.ptr(face_features),
@@ -93,7 +93,7 @@ def rasterize_backward_cuda(grad_interpolated_features, interpolated_features, s
     g_feat = torch.empty_like(face_features)
     nbytes = N.lib().kl_rasterize_backward_workspace_bytes(B, F, D)
     ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(N.lib().kl_rasterize_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, N.ptr(grad_interpolated_features),
             N.ptr(selected_face_idx), N.ptr(output_weights), N.ptr(face_vertices_image), N.ptr(face_features),
@@ -126,7 +126,7 @@ def dibr_soft_mask_forward_cuda(face_vertices_image, face_large_bboxes, selected
     lib = N.lib()
     ws_bytes = lib.kl_soft_mask_workspace_bytes(B, H, W, F)
     ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_dibr_soft_mask_forward(
             N.dtype_code(dtype), B, H, W, F, K, N.ptr(face_vertices_image), N.ptr(face_large_bboxes),
             N.ptr(selected_face_idx), float(sigmainv), float(multiplier), N.ptr(soft_mask), N.ptr(prob),
@@ -160,7 +160,7 @@ def dibr_soft_mask_backward_cuda(grad_soft_mask, soft_mask, selected_face_idx, c
     g = torch.empty_like(face_vertices_image)
     nbytes = N.lib().kl_soft_mask_backward_workspace_bytes(B, F)
     ws = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(N.lib().kl_dibr_soft_mask_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, K, N.ptr(grad_soft_mask), N.ptr(soft_mask),
             N.ptr(selected_face_idx.contiguous()), N.ptr(close_face_prob), N.ptr(close_face_idx),
@@ -210,7 +210,7 @@ def deftet_forward(func, fvz, fvi, bboxes, pix, ranges, knum, eps, binned=False)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     arena = N.Arena(dev)
     alloc = arena.fn if binned else N.ALLOC_FN()
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_deftet_sparse_render_forward(
             N.dtype_code(dtype), B, F, P, K, N.ptr(fvz), N.ptr(fvi), N.ptr(bboxes), N.ptr(pix), N.ptr(ranges),
             float(eps), N.ptr(idx), N.ptr(depth), N.ptr(w0), N.ptr(w1), N.ptr(ws), ws_bytes, alloc, None,
@@ -228,7 +228,7 @@ def deftet_resolve(face_idx, pixel_depths, w0, w1, face_features):
     sidx = torch.empty((B, P, K), dtype=torch.long, device=dev)
     weights = torch.empty((B, P, K, 3), dtype=dtype, device=dev)
     interp = torch.empty((B, P, K, D), dtype=dtype, device=dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(N.lib().kl_deftet_sparse_render_resolve(
             N.dtype_code(dtype), B, F, P, K, D, N.ptr(face_idx), N.ptr(pixel_depths), N.ptr(w0), N.ptr(w1),
             N.ptr(face_features), N.ptr(sidx), N.ptr(weights), N.ptr(interp), N.stream_of(dev)), func)
@@ -259,7 +259,7 @@ def deftet_sparse_render_backward_cuda(grad_interpolated_features, face_idx, wei
     lib = N.lib()
     ws_bytes = lib.kl_deftet_bwd_workspace_bytes(B, F, P, K)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_deftet_sparse_render_backward(
             N.dtype_code(face_vertices_image.dtype), B, F, P, K, D, N.ptr(grad_interpolated_features),
             N.ptr(face_idx), N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), float(eps),
@@ -287,7 +287,7 @@ def unbatched_triangle_distance_forward_cuda(points, face_vertices, dist, face_i
     lib = N.lib()
     nbytes = lib.kl_unbatched_triangle_distance_workspace_bytes(P)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_unbatched_triangle_distance_forward(
             N.dtype_code(points.dtype), P, F, N.ptr(points), N.ptr(face_vertices), N.ptr(dist), N.ptr(face_idx),
             N.ptr(dist_type), N.ptr(ws), nbytes, N.stream_of(dev)), func)
@@ -313,7 +313,7 @@ def unbatched_triangle_distance_backward_cuda(grad_dist, points, face_vertices, 
     _float_only(func, points)
     N.require_gpu(func, points)
     dev = points.device
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(N.lib().kl_unbatched_triangle_distance_backward(
             N.dtype_code(points.dtype), P, F, N.ptr(grad_dist), N.ptr(points), N.ptr(face_vertices),
             N.ptr(face_idx), N.ptr(dist_type), N.ptr(grad_points), N.ptr(grad_face_vertices), N.stream_of(dev)),
@@ -335,7 +335,7 @@ def sided_distance_forward_cuda(p1, p2):
     dev = p1.device
     dist = torch.empty((B, N1), dtype=p1.dtype, device=dev)
     idx = torch.empty((B, N1), dtype=torch.long, device=dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(N.lib().kl_sided_distance_forward(N.dtype_code(p1.dtype), B, N1, N2, N.ptr(p1), N.ptr(p2),
                                                   N.ptr(dist), N.ptr(idx), N.stream_of(dev)), func)
     return [dist, idx]
@@ -356,7 +356,7 @@ def sided_distance_backward_cuda(grad_output, p1, p2, idx):
     dev = p1.device
     g1 = torch.empty_like(p1)
     g2 = torch.empty_like(p2)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(N.lib().kl_sided_distance_backward(N.dtype_code(p1.dtype), B, N1, N2, N.ptr(grad_output),
                                                    N.ptr(p1), N.ptr(p2), N.ptr(idx), N.ptr(g1), N.ptr(g2),
                                                    N.stream_of(dev)), func)
@@ -388,7 +388,7 @@ def unbatched_mesh_intersection_cuda(points, verts_1, verts_2, verts_3):
     ws_bytes = lib.kl_check_sign_workspace_bytes(code, 1, F, P)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     arena = N.Arena(dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_unbatched_mesh_intersection(code, P, F, N.ptr(points), N.ptr(verts_1), N.ptr(verts_2),
                                                    N.ptr(verts_3), N.ptr(out), N.ptr(ws), ws_bytes, arena.fn, None,
                                                    N.stream_of(dev)), func)
@@ -408,7 +408,7 @@ def check_sign_batched(verts, faces, points, maxlen):
     ws_bytes = lib.kl_check_sign_workspace_bytes(code, B, F, P)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     arena = N.Arena(dev)
-    with torch.cuda.device(dev), N.timed(func, dev):
+    with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_check_sign(code, B, V, F, P, N.ptr(verts), N.ptr(faces), N.ptr(points), N.ptr(maxlen),
                                   N.ptr(out), N.ptr(ws), ws_bytes, arena.fn, None, N.stream_of(dev)), func)
     return out
@@ -431,7 +431,7 @@ def mesh_to_spc_cuda(face_vertices, target_level):
     arena = N.Arena(dev)
     oct_p, fidx_p, bary_p = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
     nn, nl = ctypes.c_int64(), ctypes.c_int64()
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_mesh_to_spc(face_vertices.shape[0], N.ptr(face_vertices), int(target_level), arena.fn,
                                        None, ctypes.byref(oct_p), ctypes.byref(nn), ctypes.byref(fidx_p),
                                        ctypes.byref(bary_p), ctypes.byref(nl), N.stream_of(dev)), func)
@@ -452,7 +452,7 @@ def morton_to_octree(mortons, level):
     mortons = mortons.contiguous()
     arena = N.Arena(dev)
     oct_p, nn = ctypes.c_void_p(), ctypes.c_int64()
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_morton_to_octree(mortons.shape[0], N.ptr(mortons), int(level), arena.fn, None,
                                             ctypes.byref(oct_p), ctypes.byref(nn), N.stream_of(dev)), func)
     return arena.tensor(oct_p.value, nn.value, torch.uint8, (nn.value,))
@@ -476,7 +476,7 @@ def points_to_morton_cuda(points):
     n = points.shape[0]
     dev = points.device
     morton = torch.empty((n,), dtype=torch.long, device=dev)
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_points_to_morton(n, N.ptr(points), N.ptr(morton), N.stream_of(dev)), func)
     return morton
 
@@ -491,7 +491,7 @@ def morton_to_points_cuda(morton_codes):
     n = morton_codes.shape[0]
     dev = morton_codes.device
     points = torch.empty((n, 3), dtype=torch.int16, device=dev)
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_morton_to_points(n, N.ptr(morton_codes), N.ptr(points), N.stream_of(dev)), func)
     return points
 
@@ -521,7 +521,7 @@ def scan_octrees_cuda(octrees, lengths):
     exsum = torch.zeros(total + B, dtype=torch.int32, device=dev)
     pyr = torch.zeros((B, 2, 17), dtype=torch.int32)
     level = ctypes.c_int()
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_scan_octrees(B, N.ptr(octrees), ctypes.c_void_p(lengths32.data_ptr()), N.ptr(exsum),
                                         ctypes.c_void_p(pyr.data_ptr()), ctypes.byref(level), N.stream_of(dev)),
                 func)
@@ -547,7 +547,7 @@ def generate_points_cuda(octrees, pyramids, exsum):
     level = pyr.shape[2] - 2
     psum = int(pyr[:, 1, level + 1].sum())
     points = torch.empty((psum, 3), dtype=torch.int16, device=dev)
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_generate_points(pyr.shape[0], level, N.ptr(octrees), ctypes.c_void_p(pyr.data_ptr()),
                                            N.ptr(exsum), N.ptr(points), N.stream_of(dev)), func)
     return points
@@ -584,7 +584,7 @@ def raytrace_cuda(octree, points, pyramid, exclusive_sum, ray_o, ray_d, target_l
     dev = octree.device
     arena = N.Arena(dev)
     nug_p, dep_p, nh = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_raytrace(N.ptr(octree), octree.shape[0], N.ptr(points), points.shape[0],
                                     N.ptr(exclusive_sum), max_level, N.ptr(ray_o), N.ptr(ray_d), ray_o.shape[0],
                                     int(target_level), int(bool(return_depth)), int(bool(with_exit)), arena.fn, None,
@@ -611,7 +611,7 @@ def mark_pack_boundaries_cuda(pack_ids):
                            f'Short (while checking arguments for {func})')
     dev = pack_ids.device
     out = torch.empty((pack_ids.shape[0],), dtype=torch.int32, device=dev)
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_mark_pack_boundaries(N.dtype_code(pack_ids.dtype), pack_ids.shape[0], N.ptr(pack_ids),
                                                 N.ptr(out), N.stream_of(dev)), func)
     return out
@@ -645,7 +645,7 @@ def diff_cuda(feats, pack_indices):
     _pack_args(func, feats, pack_indices, 'pack_indices', torch.int64)
     out = torch.empty_like(feats)
     dev = feats.device
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_pack_diff(N.dtype_code(feats.dtype), feats.shape[0], feats.shape[1], N.ptr(feats),
                                      N.ptr(pack_indices), pack_indices.shape[0], N.ptr(out), N.stream_of(dev)), func)
     return out
@@ -662,7 +662,7 @@ def inclusive_sum_cuda(info):
     n = info.shape[0]
     dev = info.device
     out = torch.empty((n,), dtype=torch.int32, device=dev)
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         ws = torch.empty((N.lib().kl_inclusive_sum_workspace_bytes(n),), dtype=torch.uint8, device=dev)
         N.check(N.lib().kl_inclusive_sum_i32(n, N.ptr(info), N.ptr(out), N.ptr(ws), ws.numel(), N.stream_of(dev)),
                 func)
@@ -679,7 +679,7 @@ def sum_reduce_cuda(feats, inclusive_sum):
     cnt = int(inclusive_sum[-1]) if nf > 0 else 0
     cnt = max(0, min(cnt, nf))  # the reference allocated num_feats rows and sliced [:cnt]
     out = torch.empty((cnt, dim), dtype=feats.dtype, device=dev)
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(N.lib().kl_sum_reduce(N.dtype_code(feats.dtype), nf, dim, N.ptr(feats), N.ptr(inclusive_sum), cnt,
                                       N.ptr(out), N.stream_of(dev)), func)
     return out
@@ -689,7 +689,7 @@ def _pack_scan(func, entry, feats, pack_indices, exclusive, reverse):
     _pack_args(func, feats, pack_indices, 'pack_indices', torch.int32)
     out = torch.empty_like(feats)
     dev = feats.device
-    with torch.cuda.device(dev):
+    with N.on_device(dev):
         N.check(getattr(N.lib(), entry)(N.dtype_code(feats.dtype), feats.shape[0], feats.shape[1], N.ptr(feats),
                                         N.ptr(pack_indices), pack_indices.shape[0], int(bool(exclusive)),
                                         int(bool(reverse)), N.ptr(out), N.stream_of(dev)), func)

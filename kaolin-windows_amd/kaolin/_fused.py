@@ -54,7 +54,7 @@ def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_
     lib = N.lib()
     nbytes = lib.kl_dibr_rasterize_workspace_bytes(B, height, width, F)
     ws = _ws(nbytes, dev)
-    with torch.cuda.device(dev), N.timed('dibr_rasterize_forward', dev):
+    with N.on_device(dev), N.timed('dibr_rasterize_forward', dev):
         N.check(lib.kl_dibr_rasterize_forward(
             N.dtype_code(dtype), height, width, B, F, D, N.ptr(fvz), N.ptr(fvi), N.ptr(feat), N.ptr(valid),
             N.ptr(fnz), float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w), N.ptr(ws), nbytes, N.stream_of(dev)),
@@ -77,7 +77,7 @@ def rasterize_backward(grad, face_idx, weights, face_vertices_image, face_featur
     lib = N.lib()
     nbytes = lib.kl_dibr_rasterize_bwd_workspace_bytes(B, H, W, F, D)
     ws = _ws(nbytes, dev)
-    with torch.cuda.device(dev), N.timed('dibr_rasterize_backward', dev):
+    with N.on_device(dev), N.timed('dibr_rasterize_backward', dev):
         N.check(lib.kl_dibr_rasterize_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, N.ptr(grad.contiguous()), N.ptr(face_idx),
             N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features), N.ptr(valid), N.ptr(fnz),
@@ -108,7 +108,7 @@ def soft_mask_forward(face_vertices_image, selected_face_idx, sigmainv, boxlen, 
     lib = N.lib()
     nbytes = lib.kl_soft_mask_workspace_bytes(B, H, W, F)
     ws = _ws(nbytes, dev)
-    with torch.cuda.device(dev), N.timed('dibr_soft_mask_forward', dev):
+    with N.on_device(dev), N.timed('dibr_soft_mask_forward', dev):
         N.check(lib.kl_dibr_soft_mask_forward_fused(
             N.dtype_code(dtype), B, H, W, F, K, N.ptr(fvi), N.ptr(sel), float(sigmainv), float(boxlen * multiplier),
             float(multiplier), N.ptr(mask), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(hits), N.ptr(ws), nbytes,
@@ -127,7 +127,7 @@ def soft_mask_backward(grad, mask, sel, prob, cidx, ctype, face_vertices_image, 
     g = torch.empty_like(face_vertices_image)
     nbytes = N.lib().kl_soft_mask_backward_workspace_bytes(B, F)
     ws = _ws(nbytes, dev)
-    with torch.cuda.device(dev), N.timed('dibr_soft_mask_backward', dev):
+    with N.on_device(dev), N.timed('dibr_soft_mask_backward', dev):
         N.check(N.lib().kl_dibr_soft_mask_backward_fused(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, K, N.ptr(grad.contiguous()), N.ptr(mask),
             N.ptr(sel), N.ptr(prob), N.ptr(cidx), N.ptr(ctype), N.ptr(hits), N.ptr(face_vertices_image), float(sigmainv),
@@ -172,7 +172,7 @@ def soft_mask_forward_compact(face_vertices_image, selected_face_idx, sigmainv, 
     scratch = torch.empty(1, dtype=torch.int32, device=dev)
     nbytes = lib.kl_soft_mask_compact_workspace_bytes(B, H, W, F)
     ws = _ws(nbytes, dev)
-    with torch.cuda.device(dev), N.timed('dibr_soft_mask_forward', dev):
+    with N.on_device(dev), N.timed('dibr_soft_mask_forward', dev):
         N.check(lib.kl_dibr_soft_mask_forward_compact(
             N.dtype_code(dtype), B, H, W, F, K, N.ptr(fvi), N.ptr(sel), float(sigmainv), float(boxlen * multiplier),
             float(multiplier), N.ptr(mask), N.ptr(hits), N.ptr(rec_face), N.ptr(rec_prob), N.ptr(seg_tot),
@@ -191,7 +191,7 @@ def soft_mask_backward_compact(grad, mask, state, face_vertices_image, sigmainv,
     lib = N.lib()
     nbytes = lib.kl_soft_mask_compact_bwd_workspace_bytes(B, H, W, F, state.knum)
     ws = _ws(nbytes, dev)
-    with torch.cuda.device(dev), N.timed('dibr_soft_mask_backward', dev):
+    with N.on_device(dev), N.timed('dibr_soft_mask_backward', dev):
         N.check(lib.kl_dibr_soft_mask_backward_compact(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, state.knum, N.ptr(grad.contiguous()), N.ptr(mask),
             N.ptr(state.hits), N.ptr(state.rec_face), N.ptr(state.rec_prob), N.ptr(state.seg_tot),
@@ -216,7 +216,7 @@ def dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, face_vertices_i
     nbytes = lib.kl_dibr_bwd_workspace_bytes(B, H, W, F, state.knum)
     ws = _ws(nbytes, dev)
     gm = grad_soft_mask.contiguous() if grad_soft_mask is not None else None
-    with torch.cuda.device(dev), N.timed('dibr_backward', dev):
+    with N.on_device(dev), N.timed('dibr_backward', dev):
         N.check(lib.kl_dibr_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, state.knum, N.ptr(grad_feats.contiguous()),
             N.ptr(gm), N.ptr(face_idx), N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features),
@@ -260,7 +260,7 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     ranges = torch.empty((B, F, 2), dtype=torch.int32, device=dev)
     nbytes = lib.kl_dibr_workspace_bytes(B, H, W, F)
     ws = _ws(nbytes, dev)
-    with torch.cuda.device(dev), N.timed('dibr_forward', dev):
+    with N.on_device(dev), N.timed('dibr_forward', dev):
         N.check(lib.kl_dibr_forward(
             N.dtype_code(dtype), B, H, W, F, D, K, N.ptr(fvz), N.ptr(fvi), N.ptr(feat), N.ptr(fnz), float(sigmainv),
             float(boxlen * multiplier), float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w),

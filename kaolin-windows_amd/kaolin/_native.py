@@ -4,7 +4,6 @@ There is no fallback: if the library is missing or no HIP device is present, eve
 hot-path op raises.  The library is loaded from this package's ``_lib`` directory
 (built in-tree by ``__graft_entry__.build()`` / ``make -C kaolin-windows_amd/csrc``).
 """
-import contextlib
 import ctypes
 import os
 
@@ -218,15 +217,45 @@ def set_timer(timer):
     _TIMER = timer
 
 
-@contextlib.contextmanager
+class _NullCtx:
+    __slots__ = ()
+
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL = _NullCtx()
+
+
+class _Timed:
+    __slots__ = ('name', 'st', 'e')
+
+    def __init__(self, name, device):
+        self.name, self.st = name, torch.cuda.current_stream(device)
+
+    def __enter__(self):
+        s = torch.cuda.Event(enable_timing=True)
+        self.e = (s, torch.cuda.Event(enable_timing=True))
+        s.record(self.st)
+
+    def __exit__(self, *exc):
+        self.e[1].record(self.st)
+        _TIMER.add(self.name, *self.e)
+        return False
+
+
 def timed(name, device):
-    if _TIMER is None:
-        yield
-        return
-    st = torch.cuda.current_stream(device)
-    s = torch.cuda.Event(enable_timing=True)
-    e = torch.cuda.Event(enable_timing=True)
-    s.record(st)
-    yield
-    e.record(st)
-    _TIMER.add(name, s, e)
+    """HIP-event timing of the op on its stream while bench.py's timer is set; a shared no-op
+    context otherwise (the per-call cost of the eager path)."""
+    return _NULL if _TIMER is None else _Timed(name, device)
+
+
+def on_device(device):
+    """torch.cuda.device(device), skipped when it is already the current device."""
+    idx = device.index
+    if idx is None or idx == torch.cuda.current_device():
+        return _NULL
+    return torch.cuda.device(device)

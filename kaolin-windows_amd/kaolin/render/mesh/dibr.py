@@ -77,6 +77,7 @@ class DibrRasterizationCuda(Function):
             soft_mask, state = _fused.soft_mask_forward_compact(face_vertices_image, face_idx, sigmainv, boxlen, knum,
                                                                 multiplier)
         ctx.mark_non_differentiable(face_idx)
+        ctx.set_materialize_grads(False)  # no zero-filled grads for face_idx (or unused outputs)
         ctx.sigmainv, ctx.multiplier, ctx.eps, ctx.knum = sigmainv, multiplier, eps, state.knum
         ctx.has_ranges = ranges is not None and ranges.numel() > 0
         ctx.save_for_backward(face_idx, weights, face_vertices_image, face_features, face_normals_z, soft_mask,
@@ -87,6 +88,8 @@ class DibrRasterizationCuda(Function):
     def backward(ctx, grad_feats, grad_soft_mask, grad_face_idx):
         face_idx, weights, fvi, feat, fnz, soft_mask, ranges, *st = ctx.saved_tensors
         state = _fused.SoftMaskState(*st, ctx.knum)
+        if grad_feats is None and grad_soft_mask is None:
+            return None, None, None, None, None, None, None, None, None, None, None
         if grad_feats is None:
             grad_feats = torch.zeros(face_idx.shape + (feat.shape[-1],), dtype=feat.dtype, device=feat.device)
         if fnz.dtype == fvi.dtype:

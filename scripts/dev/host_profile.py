@@ -49,6 +49,41 @@ def main():
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     print(f'backward call: {(t1 - t0) / reps * 1e6:.1f} us host')
+    from kaolin import _fused, _native as N
+    f = _fused.dibr_forward(inp['H'], inp['W'], inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'], 7000., 0.02, 30,
+                            1000., 1e-8)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        f = _fused.dibr_forward(inp['H'], inp['W'], inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'], 7000., 0.02,
+                                30, 1000., 1e-8)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    print(f'_fused.dibr_forward: {(t1 - t0) / reps * 1e6:.1f} us host')
+    feats, idx, w, mask, state, ranges = f
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        _fused.dibr_backward(inp['g_feat'], inp['g_mask'], idx, w, inp['fvi'], inp['feat'], inp['fnz'], mask, state,
+                             7000., 1000., 1e-8, ranges)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    print(f'_fused.dibr_backward: {(t1 - t0) / reps * 1e6:.1f} us host')
+    x = torch.empty(16, device='cuda')
+    ws = torch.zeros(N.lib().kl_loss_dot2_workspace_bytes(), dtype=torch.uint8, device='cuda')
+    out = torch.empty(1, device='cuda')
+    args = (N.ptr(x), N.ptr(x), 16, N.ptr(x), N.ptr(x), 16, N.ptr(ws), N.ptr(out), N.stream_of(x.device))
+    lib = N.lib()
+    t0 = time.perf_counter()
+    for _ in range(1000):
+        lib.kl_loss_dot2(*args)
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    print(f'kl_loss_dot2 (2 launches, prebuilt args): {(t1 - t0) / 1000 * 1e6:.1f} us host')
+    t0 = time.perf_counter()
+    for _ in range(1000):
+        torch.empty((4, 512, 512, 3), device='cuda')
+    t1 = time.perf_counter()
+    print(f'torch.empty: {(t1 - t0) / 1000 * 1e6:.2f} us host')
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(n):
