@@ -165,22 +165,41 @@ __device__ __forceinline__ void axis_range(double vmin, double vmax, double s, i
 // Sets chunk c's bit in every tile of mesh b that one of the wave's faces touches (the
 // lane's face covers tiles [tx0,tx1] x [ty0,ty1]; empty when tx0 > tx1).  Small unions
 // are walked by the wave with one atomicOr per tile, large ones per lane.
+// Marks chunk c's bit in every tile of the lanes' tile ranges.  The chunk's union rectangle
+// (<= 256 tiles) is flagged in the wave's LDS scratch `wf` (256 bytes) by every lane for its own
+// tiles, then the flagged tiles are OR-ed in lane-parallel: one atomic per touched tile, no
+// serial walk of the rectangle.  Larger rectangles: per-lane atomics.
 __device__ __forceinline__ void bin_mark(const BinGeom &g, int b, int c, int lane, int tx0, int tx1, int ty0,
-                                         int ty1, uint32_t *__restrict__ bitmap) {
+                                         int ty1, uint32_t *__restrict__ bitmap, uint8_t *wf) {
   const bool has = tx0 <= tx1;
   const int ux0 = wave_min(has ? tx0 : INT32_MAX), ux1 = wave_max(has ? tx1 : -1);
   const int uy0 = wave_min(has ? ty0 : INT32_MAX), uy1 = wave_max(has ? ty1 : -1);
   if (ux0 > ux1) return;
   const uint32_t bit = 1u << (c & 31);
   const size_t tile_base = (size_t)b * g.tiles_y * g.tiles_x;
-  const int area = (ux1 - ux0 + 1) * (uy1 - uy0 + 1);
+  const int uw = ux1 - ux0 + 1;
+  const int area = uw * (uy1 - uy0 + 1);
   if (area <= 256) {
-    for (int ty = uy0; ty <= uy1; ty++)
-      for (int tx = ux0; tx <= ux1; tx++) {
-        const uint64_t hit = ballot(has && tx0 <= tx && tx <= tx1 && ty0 <= ty && ty <= ty1);
-        if (hit && lane == 0)
-          atomicOr(&bitmap[(tile_base + (size_t)ty * g.tiles_x + tx) * g.words + (c >> 5)], bit);
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (q * 64 + lane < area) wf[q * 64 + lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if (has)
+      for (int ty = ty0; ty <= ty1; ty++)
+        for (int tx = tx0; tx <= tx1; tx++) wf[(ty - uy0) * uw + (tx - ux0)] = 1;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int e = q * 64 + lane;
+      if (e < area && wf[e]) {
+        const int ty = uy0 + e / uw, tx = ux0 + e % uw;
+        atomicOr(&bitmap[(tile_base + (size_t)ty * g.tiles_x + tx) * g.words + (c >> 5)], bit);
       }
+    }
+    __builtin_amdgcn_wave_barrier();  // wf is reused by the wave's next call
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   } else if (has) {
     for (int ty = ty0; ty <= ty1; ty++)
       for (int tx = tx0; tx <= tx1; tx++)
@@ -232,6 +251,7 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *
                                                         int faces_per_mesh, BinGeom g, float m,
                                                         uint32_t *__restrict__ bitmap, T *__restrict__ bbox_out,
                                                         uint2 *__restrict__ rng_out) {
+  __shared__ uint8_t s_bm[4][256];  // bin_mark scratch, one per wave
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.y;
@@ -278,7 +298,7 @@ __global__ void __launch_bounds__(256) bin_faces_kernel(Src src, const int64_t *
       ty1 = iy1 / TILE_H;
     }
   }
-  bin_mark(g, b, c, lane, tx0, tx1, ty0, ty1, bitmap);
+  bin_mark(g, b, c, lane, tx0, tx1, ty0, ty1, bitmap, s_bm[threadIdx.x >> 6]);
 }
 
 // zero_bytes: bytes from `bitmap` zeroed first (0 = the bitmap's own g.bytes()).

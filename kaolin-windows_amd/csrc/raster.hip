@@ -393,6 +393,7 @@ __global__ void __launch_bounds__(256) raster_bin_kernel(RastSrc<T> src, const T
                                                          T *__restrict__ rec, uint2 *__restrict__ rng,
                                                          uint32_t *__restrict__ sbitmap = nullptr,
                                                          uint2 *__restrict__ srng = nullptr, T spad = 0) {
+  __shared__ uint8_t s_bm[4][256];  // bin_mark scratch, one per wave
   const int c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.y;
@@ -428,7 +429,7 @@ __global__ void __launch_bounds__(256) raster_bin_kernel(RastSrc<T> src, const T
   }
   const bool has = ix0 <= ix1;
   bin_mark(g, b, c, lane, has ? ix0 / TILE_W : 1, has ? ix1 / TILE_W : 0, has ? iy0 / TILE_H : 1,
-           has ? iy1 / TILE_H : 0, bitmap);
+           has ? iy1 / TILE_H : 0, bitmap, s_bm[threadIdx.x >> 6]);
   if (sbitmap) {
     // the soft mask's bins of the same faces (kl_dibr_forward): every face, bbox enlarged
     // by boxlen * multiplier as SoftSrc / dibr.py:31-39, and its exact pixel ranges
@@ -450,7 +451,7 @@ __global__ void __launch_bounds__(256) raster_bin_kernel(RastSrc<T> src, const T
       }
       srng[f] = make_uint2((uint32_t)jx0 | ((uint32_t)jx1 << 16), (uint32_t)jy0 | ((uint32_t)jy1 << 16));
     }
-    bin_mark(g, b, c, lane, tx0, tx1, ty0, ty1, sbitmap);
+    bin_mark(g, b, c, lane, tx0, tx1, ty0, ty1, sbitmap, s_bm[threadIdx.x >> 6]);
   }
 }
 
@@ -471,6 +472,13 @@ struct RastTileArgs {
   int64_t *out_idx;
   T *out_w;
   uint64_t *dbg;  // dev stamps (kl_dev_set_debug), 8 per wave, or nullptr
+  // kl_dibr_forward: the soft mask's outputs for pixels / row segments without hits, written
+  // here (mask = covered, hits = 0, seg_tot = defer = 0) so that the soft-mask kernel only
+  // touches the ones with hits (nullptr: not written)
+  T *soft_mask = nullptr;
+  uint8_t *soft_hits = nullptr;
+  int *soft_seg = nullptr;
+  uint8_t *soft_defer = nullptr;
 };
 
 template <typename T>
@@ -751,6 +759,14 @@ __global__ void __launch_bounds__(512) raster_tile_kernel(RastTileArgs<T> a) {
   }
   const size_t p = ((size_t)b * H + j) * W + i;
   const int D = a.D;
+  if (a.soft_hits) {
+    a.soft_hits[p] = 0;
+    a.soft_mask[p] = win >= 0 ? (T)1.0 : (T)0.0;
+    if (lane == 0) {
+      a.soft_seg[(size_t)(b * H + j) * g.tiles_x + tx] = 0;
+      a.soft_defer[(size_t)(b * H + j) * g.tiles_x + tx] = 0;
+    }
+  }
   a.out_idx[p] = win;
   a.out_w[p * 3 + 0] = mw0;
   a.out_w[p * 3 + 1] = mw1;
@@ -1426,15 +1442,19 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const int split_from = 5, split_log2 = sizeof(T) == 4 ? 2 : 0;
   hipLaunchKernelGGL(tile_order2_kernel, dim3(2), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh, items,
                      split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt,
-                     soft_lp_min(K), snitems);
-  KL_CHECK_LAUNCH();
-  const RastTileArgs<T> args{src, fvz, feat, rbm, rec, rng, items, nitems, g, F, D, eps, out_feat, out_idx, out_w,
-                             reinterpret_cast<uint64_t *>(g_dev_debug)};
-  hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
+                     soft_lp_min(K), snitems, soft_split(), 1);
   KL_CHECK_LAUNCH();
   uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.off_defer);
+  RastTileArgs<T> args{src, fvz, feat, rbm, rec, rng, items, nitems, g, F, D, eps, out_feat, out_idx, out_w,
+                       reinterpret_cast<uint64_t *>(g_dev_debug)};
+  args.soft_mask = out_mask;
+  args.soft_hits = s.hits;
+  args.soft_seg = s.seg_tot;
+  args.soft_defer = defer;
+  hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
+  KL_CHECK_LAUNCH();
   return soft_tile_forward_main<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, sbm, sorder, snitems,
-                                   srng, defer, st);
+                                   srng, defer, st, true);
 }
 
 template <typename T>

@@ -191,7 +191,7 @@ template <typename T>
 int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv,
                            double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
                            const int32_t *order, const int *nitems, const uint2 *rng, uint8_t *defer,
-                           hipStream_t st);
+                           hipStream_t st, bool prefilled);
 int soft_lp_min(int K);
 template <typename T>
 int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,

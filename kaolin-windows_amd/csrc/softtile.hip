@@ -61,6 +61,8 @@ struct SoftTileArgs {
   uint8_t *defer;            // per row segment: its hits are left to soft_tile_eval_kernel
   uint64_t *dbg;             // dev stamps (kl_dev_set_debug), 10 per wave, or nullptr
   int dev;                   // dev ablation flags (kl_dev_set_flags), 0 in the product path
+  int prefilled;             // mask / hits / seg_tot / defer already written for pixels and rows
+                             // without hits (kl_dibr_forward's rasterizer): only hits are written
 };
 
 // LDS of one row: its [K][64] slot lists (face ids, then probabilities in place), the
@@ -127,6 +129,7 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   int any = 0;
   for (int w = 0; w < ST_WAVES; w++) any |= s_wcnt[w];
   __syncthreads();
+  if (!any && a.prefilled) return;  // no uncovered pixel: its outputs are written (workgroup-uniform)
   if (any) {
     ChunkSeq seq;
     seq.init(a.bitmap + ((size_t)(b * g.tiles_y + ty) * g.tiles_x + tx) * g.words, g.words, lane);
@@ -356,8 +359,8 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
       a.rec_face[rbase + e] = s_face[(e - s_pre[lo]) * 64 + lo];
     }
   }
-  if (qi == 0) {
-    if (px_valid) {
+  if (qi == 0 && (!a.prefilled || total > 0)) {
+    if (px_valid && (!a.prefilled || kid > 0)) {
       a.hits[pix] = (uint8_t)kid;
       if (kid == 0) a.mask[pix] = covered ? (T)1.0 : (T)0.0;  // 1 - prod over no slots = 0
     }
@@ -682,6 +685,15 @@ struct StWs {
 
 // Fewest parts per tile (lp_min >= 1: at most 4 rows per workgroup) whose slot lists fit in
 // 64 KB of LDS (two workgroups per CU); knum near 255 takes one row per workgroup.
+SoftSplit soft_split() {
+  SoftSplit sp = ST_SPLIT;
+  if (g_dev_param[0]) sp.b4 = g_dev_param[0];
+  if (g_dev_param[1]) sp.b8 = g_dev_param[1];
+  if (g_dev_param[2]) sp.cap4 = g_dev_param[2];
+  if (g_dev_param[3]) sp.cap8 = g_dev_param[3];
+  return sp;
+}
+
 int soft_lp_min(int K) {
   int lp = 1;
   while (lp < 3 && st_head_lds() + (size_t)(TILE_H >> lp) * st_row_lds(K) > 64 * 1024) lp++;
@@ -713,11 +725,11 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
                      g.words, nt, bk, ghist, scratch);
   KL_CHECK_LAUNCH();
   hipLaunchKernelGGL(soft_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt, order,
-                     soft_lp_min(K), nitems);
+                     soft_lp_min(K), nitems, soft_split());
   KL_CHECK_LAUNCH();
   uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.defer);
   return soft_tile_forward_main<T>(B, H, W, F, K, fvi, sel, sigmainv, pad, m, mask, s, bitmap, order, nitems, rng,
-                                   defer, st);
+                                   defer, st, false);
 }
 
 // The selection and evaluation kernels on bins made by the caller: bitmap (SoftSrc bins),
@@ -727,7 +739,7 @@ template <typename T>
 int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv,
                            double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
                            const int32_t *order, const int *nitems, const uint2 *rng, uint8_t *defer,
-                           hipStream_t st) {
+                           hipStream_t st, bool prefilled) {
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   if (nt == 0) return KL_OK;
@@ -737,8 +749,8 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   const SoftSrc<T> src{fvi, (T)m, (T)pad};
   SoftTileArgs<T> args{src, rng,  sel,    bitmap, order,      nitems,     g,         F,     K,
                        sigmainv, m, mask, s.hits, s.rec_face, s.rec_prob, s.seg_tot, defer, (uint64_t *)g_dev_debug,
-                       g_dev_flags};
-  hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)soft_items_bound(nt, lp_min)), dim3(64 * ST_WAVES), lds,
+                       g_dev_flags, prefilled ? 1 : 0};
+  hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)soft_items_bound(nt, lp_min, soft_split())), dim3(64 * ST_WAVES), lds,
                      st, args);
   KL_CHECK_LAUNCH();
   if (K > 0 && sizeof(T) != 4) {  // f64: the rows left for the evaluation kernel
@@ -809,10 +821,12 @@ template int soft_tile_forward<double>(int, int, int, int, int, const double *, 
                                        float, double *, const SoftState<double> &, void *, size_t, hipStream_t);
 template int soft_tile_forward_main<float>(int, int, int, int, int, const float *, const int64_t *, float, double,
                                            float, float *, const SoftState<float> &, const uint32_t *,
-                                           const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t);
+                                           const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t,
+                                           bool);
 template int soft_tile_forward_main<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
                                             float, double *, const SoftState<double> &, const uint32_t *,
-                                            const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t);
+                                            const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t,
+                                            bool);
 template int soft_tile_backward<float>(int, int, int, int, int, const float *, const float *,
                                        const SoftState<float> &, const float *, float, float, float *, bool, void *,
                                        size_t, hipStream_t, double *, bool *);

@@ -68,7 +68,7 @@ __device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, co
   // a 32-lane segmented scan (two bands per wave)
   if (threadIdx.x < 8 * ORD_BUCKETS) {
     const int t = threadIdx.x, g = t / ORD_BUCKETS, q = ORD_BUCKETS - 1 - t % ORD_BUCKETS;
-    const int v = ghist[g * ORD_BUCKETS + q] << lpb[q];  // items of (band g, bucket q)
+    const int v = lpb[q] < 0 ? 0 : ghist[g * ORD_BUCKETS + q] << lpb[q];  // items of (band g, bucket q)
     int inc = v;
 #pragma unroll
     for (int o = 1; o < ORD_BUCKETS; o <<= 1) {
@@ -99,7 +99,9 @@ __device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, co
   }
   __syncthreads();
   for (int u = threadIdx.x; u < nt; u += blockDim.x) {
-    const int q = bk[u], g = tile_band(u, nt), lp = lpb[q], np = 1 << lp;
+    const int q = bk[u], g = tile_band(u, nt), lp = lpb[q];
+    if (lp < 0) continue;  // bucket without items
+    const int np = 1 << lp;
     const int r0 = atomicAdd(&sb[g * ORD_BUCKETS + q], np);
     for (int k = 0; k < np; k++) {
       const int r = r0 + k;
@@ -134,18 +136,23 @@ __device__ __forceinline__ void order_items(int *sb, int *sx, int *lpb, const in
 }
 
 // Soft-mask work items (softtile.hip).  A 4-wave workgroup takes one part.  lp is lp_min (set
-// by the LDS the slot lists need) except for the heaviest buckets: >= ST_B8 candidate-chunk
-// bucket -> 8 parts (one row, 4 waves sharing its walk and evaluation), >= ST_B4 -> 4 parts
-// (2 rows, 2 waves each), at most ST_CAP8 / ST_CAP4 tiles each, so that soft_items_bound()
+// by the LDS the slot lists need) except for the heaviest buckets: >= b8 candidate-chunk
+// bucket -> 8 parts (one row, 4 waves sharing its walk and evaluation), >= b4 -> 4 parts
+// (2 rows, 2 waves each), at most cap8 / cap4 tiles each (SoftSplit), so that soft_items_bound()
 // holds.
-constexpr int ST_B4 = 5, ST_B8 = 6, ST_CAP4 = 256, ST_CAP8 = 128;
-inline int soft_items_bound(int nt, int lp_min) {
+struct SoftSplit {
+  int b4, b8, cap4, cap8;
+};
+constexpr SoftSplit ST_SPLIT{5, 6, 256, 128};
+SoftSplit soft_split();  // ST_SPLIT, or the dev parameters' override (softtile.hip)
+inline int soft_items_bound(int nt, int lp_min, SoftSplit sp) {
   auto extra = [&](int lp, int cap) { return lp > lp_min ? cap * ((1 << lp) - (1 << lp_min)) : 0; };
-  return (nt << lp_min) + extra(2, ST_CAP4) + extra(3, ST_CAP8);
+  return (nt << lp_min) + extra(2, sp.cap4) + extra(3, sp.cap8);
 }
 __device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, const uint8_t *__restrict__ bk,
                                                  const int *__restrict__ ghist, int nt, int32_t *__restrict__ order,
-                                                 int lp_min, int *__restrict__ nitems) {
+                                                 int lp_min, int *__restrict__ nitems, SoftSplit sp,
+                                                 int skip_empty = 0) {
   // tiles per bucket summed over the bands (one lane per bucket), then the caps walked
   // serially from the heaviest bucket down on LDS values
   if (threadIdx.x < ORD_BUCKETS) {
@@ -160,14 +167,14 @@ __device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, con
     for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
       const int h = sx[q];
       int lp = lp_min;
-      if (q >= ST_B8 && n8 + h <= ST_CAP8) {
+      if (q >= sp.b8 && n8 + h <= sp.cap8) {
         lp = lp > 3 ? lp : 3;
         n8 += h;
-      } else if (q >= ST_B4 && n4 + h <= ST_CAP4) {
+      } else if (q >= sp.b4 && n4 + h <= sp.cap4) {
         lp = lp > 2 ? lp : 2;
         n4 += h;
       }
-      lpb[q] = lp;
+      lpb[q] = q == 0 && skip_empty ? -1 : lp;  // skip_empty: tiles without candidate faces get no item
     }
   }
   __syncthreads();  // sx is reused by place_items
@@ -184,11 +191,11 @@ __device__ __forceinline__ const uint8_t *stage_buckets(uint8_t *lds, const uint
 static __global__ void __launch_bounds__(1024) soft_order_kernel(const uint8_t *__restrict__ bk,
                                                                  const int *__restrict__ ghist, int nt,
                                                                  int32_t *__restrict__ order, int lp_min,
-                                                                 int *__restrict__ nitems) {
+                                                                 int *__restrict__ nitems, SoftSplit sp) {
   __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS];
   __shared__ uint8_t sbk[ORD_LDS_TILES];
   const uint8_t *b = stage_buckets(sbk, bk, nt);
-  order_soft_items(sb, sx, lpb, b, ghist, nt, order, lp_min, nitems);
+  order_soft_items(sb, sx, lpb, b, ghist, nt, order, lp_min, nitems, sp);
 }
 
 static __global__ void __launch_bounds__(1024) tile_order_kernel(const uint8_t *__restrict__ bk,
@@ -249,14 +256,15 @@ static __global__ void __launch_bounds__(1024) tile_order2_kernel(const uint8_t 
                                                                   const uint8_t *__restrict__ bk1,
                                                                   const int *__restrict__ gh1,
                                                                   int32_t *__restrict__ order1, int nt, int lp_min1,
-                                                                  int *__restrict__ nitems1) {
+                                                                  int *__restrict__ nitems1, SoftSplit sp,
+                                                                  int skip_empty1) {
   __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS];
   __shared__ uint8_t sbk[ORD_LDS_TILES];
   // two workgroups: block 0 orders the rasterizer's items, block 1 the soft mask's
   const bool soft = blockIdx.x == 1;
   const uint8_t *b = stage_buckets(sbk, soft ? bk1 : bk0, nt);
   if (soft)
-    order_soft_items(sb, sx, lpb, b, gh1, nt, order1, lp_min1, nitems1);
+    order_soft_items(sb, sx, lpb, b, gh1, nt, order1, lp_min1, nitems1, sp, skip_empty1);
   else
     order_items(sb, sx, lpb, gh0, b, nt, order0, 0, split_from, split_log2, nitems0);
 }

@@ -26,6 +26,10 @@ def main():
     lib.kl_dev_set_debug.argtypes = [ctypes.c_void_p]
     lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
     flags = int(os.environ.get('STAMPS_FLAGS', '0'), 0)
+    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
+    params = [int(x) for x in os.environ.get('STAMPS_PARAMS', '').split(',') if x]
+    for k, v in enumerate(params):  # SoftSplit b4, b8, cap4, cap8 (tileorder.h)
+        lib.kl_dev_set_param(k, v)
     inp = bench.dibr_inputs([0.0, 1.5707963, 3.1415927, 4.712389], 'cuda')
     H, W = inp['H'], inp['W']
     valid = inp['fnz'] >= 0
