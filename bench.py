@@ -454,13 +454,14 @@ def dibr_headline(args, world, rank, device):
     for _ in range(args.warmup):
         step()
     stats = workload_stats(inp)
-    # eager pass: per-op HIP-event timing for the roofline, and the eager rate
+    # eager pass with per-op HIP events (the roofline's op durations), then the eager rate
+    # without them (the events and their Python cost are not part of the step)
     timer = _native.OpTimer()
     _native.set_timer(timer)
-    eager_elapsed = timed_loop(step, args.steps, world, device)
+    timed_loop(step, args.steps, world, device)
     _native.set_timer(None)
-    eager_elapsed = max_over_ranks(eager_elapsed, device, world)
     ops_ms = timer.summary_ms()
+    eager_elapsed = max_over_ranks(timed_loop(step, args.steps, world, device), device, world)
     pixels = cfg['views'] * cfg['H'] * cfg['W'] * world * args.steps
     mode, elapsed = 'eager', eager_elapsed
     if not args.eager:
@@ -510,6 +511,47 @@ def dibr_headline(args, world, rank, device):
                   'ms_per_step': round(eager_elapsed / args.steps * 1e3, 4)},
     }
     return result, inp
+
+
+# ----------------------------------------------------------------------------- prepare_vertices
+def prepare_leg(device, steps, views=4):
+    """prepare_vertices (render/mesh/utils.py:128-175) fwd + bwd on the
+    cfg3 mesh and views, vertices and camera requiring grad: the fused HIP path
+    (csrc/prepare.hip) against the reference's torch chain of ops on the same GPU."""
+    import torch
+    import kaolin as kal
+    from kaolin.render.mesh.utils import _prepare_vertices_torch
+    verts, faces = uv_sphere(126, 200, device)
+    B, V, F = views, verts.shape[0], faces.shape[0]
+    az = torch.tensor(views_for_rank(0, 1, views), dtype=torch.float32, device=device)
+    cam = torch.stack([3 * torch.sin(az), torch.zeros_like(az), 3 * torch.cos(az)], -1)
+    rot, trans = kal.render.camera.generate_rotate_translate_matrices(
+        cam, torch.zeros_like(cam), torch.tensor([[0., 1., 0.]], device=device).repeat(B, 1))
+    proj = kal.render.camera.generate_perspective_projection(math.pi / 4).to(device)
+    v = verts.unsqueeze(0).repeat(B, 1, 1).requires_grad_(True)
+    rot, trans = rot.requires_grad_(True), trans.requires_grad_(True)
+    g = torch.Generator().manual_seed(3)
+    grads = [torch.rand(s, generator=g).to(device) for s in ((B, F, 3, 3), (B, F, 3, 2), (B, F, 3))]
+
+    def run(fn):
+        out = fn(v, faces, proj, rot, trans, None)
+        torch.autograd.backward(out, grads)
+        v.grad = rot.grad = trans.grad = None
+    fused = lambda: run(lambda *a: kal.render.mesh.prepare_vertices(*a[:5]))  # noqa: E731
+    chain = lambda: run(_prepare_vertices_torch)  # noqa: E731
+    ms_f = _wall_ms(fused, max(5, steps))
+    ms_t = _wall_ms(chain, max(5, steps))
+    # forward: vertices + faces read, three outputs written; backward: the three grads read,
+    # the per-vertex double sums (5 x 8 B, atomics), the vertices re-read, grad_vertices written
+    fwd_bytes = B * V * 12 + F * 24 + B * F * (36 + 24 + 12)
+    bwd_bytes = B * F * (36 + 24 + 12) + F * 24 + B * V * 12 + B * V * 40 * 2 + B * V * 12
+    nb = fwd_bytes + bwd_bytes
+    return {'metric': 'prepare_vertices fwd+bwd ms (4 views, 50k-face mesh, vertices + camera grads, f32)',
+            'ms': round(ms_f, 4), 'torch_chain_ms': round(ms_t, 4), 'speedup': round(ms_t / ms_f, 2),
+            'bytes': nb, 'roofline': {'bound': 'hbm', 'achieved': round(nb / (ms_f * 1e-3) / 1e9, 1),
+                                      'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                                      'frac': round(nb / (ms_f * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+            'timing': 'wall clock per fwd+bwd incl. Python / autograd (median of runs)'}
 
 
 # ----------------------------------------------------------------------------- p2m (cfg2)
@@ -895,6 +937,8 @@ def main(argv=None):
         if args.config == 'cfg3':
             result['deftet'] = deftet_bench(inp, max(3, args.steps // 4))
         result['check_sign'] = check_sign_bench(device, max(3, args.steps // 4))
+        progress('prepare_vertices leg')
+        result['prepare_vertices'] = prepare_leg(device, args.steps)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         row_step = args.cpu_row_step or CONFIGS[args.config]['row_step']
         progress(f'DIB-R parity + cpu baseline (oracle, every {row_step}th row)')

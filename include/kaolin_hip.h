@@ -239,6 +239,35 @@ int kl_dibr_soft_mask_backward(kl_dtype dtype, int batch, int height, int width,
                                void *grad_face_vertices_image, void *workspace, size_t workspace_bytes,
                                kl_stream stream);
 
+/* ------------------------------------------------------ DIB-R input preparation */
+
+/* render/mesh/utils.py:128-175  prepare_vertices (+ camera/legacy.py:22-37 rotate_translate_points,
+ * :120-139 perspective_camera, ops/mesh/mesh.py:25-46 index_vertices_by_faces,
+ * ops/mesh/trianglemesh.py:313-336 face_normals(unit=True)) -- pure PyTorch in the reference,
+ * one launch here.  vertices (Bv,V,3); faces (F,3) int64; camera_rot (Bc,3,3) + camera_trans
+ * (Bc,3), or camera_transform (Bc,4,3) (then rot / trans NULL); camera_proj (Bp,3).  Bv, Bc, Bp
+ * are 1 or B (broadcast as torch does).  Outputs face_vertices_camera (B,F,3,3),
+ * face_vertices_image (B,F,3,2), face_normals (B,F,3).  f32 / f64.  A face index outside
+ * [0, V) reads nothing and yields NaN for that face. */
+int kl_prepare_vertices_forward(kl_dtype dtype, int B, int Bv, int Bc, int Bp, int64_t V, int64_t F,
+                                const void *vertices, const int64_t *faces, const void *camera_rot,
+                                const void *camera_trans, const void *camera_transform, const void *camera_proj,
+                                void *face_vertices_camera, void *face_vertices_image, void *face_normals,
+                                kl_stream stream);
+
+/* Backward of the above (autograd's chain for the reference's ops; per-vertex and per-camera
+ * sums in double, rounded once).  Any grad_face_* may be NULL (zero).  Outputs (NULL = not
+ * wanted): grad_vertices (Bv,V,3); grad_camera (Bc,12): per camera rot (9, row-major) then
+ * trans (3), or transform (4,3) row-major; grad_camera_proj (Bp,3).
+ * ws: kl_prepare_vertices_bwd_workspace_bytes(B, V) bytes (zeroed by the call). */
+size_t kl_prepare_vertices_bwd_workspace_bytes(int B, int64_t V);
+int kl_prepare_vertices_backward(kl_dtype dtype, int B, int Bv, int Bc, int Bp, int64_t V, int64_t F,
+                                 const void *vertices, const int64_t *faces, const void *camera_rot,
+                                 const void *camera_trans, const void *camera_transform, const void *camera_proj,
+                                 const void *grad_face_vertices_camera, const void *grad_face_vertices_image,
+                                 const void *grad_face_normals, void *grad_vertices, void *grad_camera,
+                                 void *grad_camera_proj, void *ws, size_t ws_bytes, kl_stream stream);
+
 /* ------------------------------------------------------------ DefTet sparse render */
 
 /* deftet.cpp:49-111  deftet_sparse_render_forward_cuda (kernel deftet_cuda.cu:32-190).

@@ -8,8 +8,9 @@
 //
 // The occupied set is the union over faces of an independent recursion, so here:
 //   * original vertices are marked directly;
-//   * triangles expand breadth-first, one launch per subdivision level, children
-//     appended through a device counter (order is irrelevant for a set);
+//   * triangles expand breadth-first, one launch per subdivision level; only children that
+//     need a further split are appended (device counter; order is irrelevant for a set), so
+//     the last round writes nothing;
 //   * every midpoint is rounded and stored straight into the dense output grid with
 //     a plain (idempotent) store -- no unique(), no sparse tensor, no sort.
 // Midpoints, edge lengths and rounding use the reference's arithmetic in the input
@@ -68,29 +69,46 @@ __device__ __forceinline__ T edge2(const T *a, const T *b) {
   return dx * dx + dy * dy + dz * dz;
 }
 
+template <typename T>
+__device__ __forceinline__ bool needs_split(const T *v, T thr) {
+  const T e1 = edge2(v + 0, v + 3), e2 = edge2(v + 3, v + 6), e3 = edge2(v + 6, v + 0);
+  T mx = e1;
+  if (e2 > mx) mx = e2;  // torch.max over the three (NaN-free inputs)
+  if (e3 > mx) mx = e3;
+  return mx > thr;
+}
+
+// Appends the triangles of `kids` that need a further split to `out` (one atomic per wave).
+template <typename T>
+__device__ __forceinline__ void append_kept(const Tri<T> &t, bool live, T thr, Tri<T> *__restrict__ out,
+                                            unsigned long long *__restrict__ counter) {
+  const bool keep = live && needs_split(t.v, thr);
+  const uint64_t km = ballot(keep);
+  if (!km) return;
+  const int lane = lane_id();
+  const int leader = __builtin_ctzll(km);
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(km));
+  base = __shfl(base, leader);
+  if (keep) out[base + __popcll(km & ((1ull << lane) - 1))] = t;
+}
+
+// One subdivision round over triangles that need a split (level 0: every face, tested
+// here).  The three midpoints are marked; of the four children only those that need a
+// split themselves (the reference's next-round test on their own coordinates) are written:
+// the others add no vertex the grid does not already hold.
 template <typename T, typename G>
-__global__ void subdivide_kernel(int64_t n, const Tri<T> *__restrict__ in, T thr, int R, G *__restrict__ grid,
-                                 Tri<T> *__restrict__ out, unsigned long long *__restrict__ counter) {
+__global__ void subdivide_kernel(int64_t n, const Tri<T> *__restrict__ in, bool test_input, T thr, int R,
+                                 G *__restrict__ grid, Tri<T> *__restrict__ out,
+                                 unsigned long long *__restrict__ counter) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  bool keep = false;
+  bool live = false;
   Tri<T> t;
   if (i < n) {
     t = in[i];
-    const T e1 = edge2(t.v + 0, t.v + 3), e2 = edge2(t.v + 3, t.v + 6), e3 = edge2(t.v + 6, t.v + 0);
-    T mx = e1;
-    if (e2 > mx) mx = e2;  // torch.max over the three (NaN-free inputs)
-    if (e3 > mx) mx = e3;
-    keep = mx > thr;
+    live = !test_input || needs_split(t.v, thr);
   }
-  // one atomic per wave for the child slots
-  const uint64_t km = ballot(keep);
-  unsigned long long base = 0;
-  const int lane = lane_id();
-  const int leader = km ? __builtin_ctzll(km) : 0;
-  if (km && lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(km) * 4ull);
-  base = __shfl(base, leader);
-  if (!keep) return;
-  const int rank = __popcll(km & ((1ull << lane) - 1));
+  if (!__any(live)) return;
   T v4[3], v5[3], v6[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -98,31 +116,32 @@ __global__ void subdivide_kernel(int64_t n, const Tri<T> *__restrict__ in, T thr
     v5[k] = (t.v[k] + t.v[3 + k]) / (T)2;
     v6[k] = (t.v[3 + k] + t.v[6 + k]) / (T)2;
   }
-  mark_point<T, G>(v4[0], v4[1], v4[2], R, grid);
-  mark_point<T, G>(v5[0], v5[1], v5[2], R, grid);
-  mark_point<T, G>(v6[0], v6[1], v6[2], R, grid);
-  Tri<T> *o = out + base + (unsigned long long)rank * 4;
+  if (live) {
+    mark_point<T, G>(v4[0], v4[1], v4[2], R, grid);
+    mark_point<T, G>(v5[0], v5[1], v5[2], R, grid);
+    mark_point<T, G>(v6[0], v6[1], v6[2], R, grid);
+  }
   Tri<T> c;
 #pragma unroll
   for (int k = 0; k < 3; k++) {  // (v1,v4,v5),(v2,v5,v6),(v4,v5,v6),(v3,v4,v6)
     c.v[k] = t.v[k]; c.v[3 + k] = v4[k]; c.v[6 + k] = v5[k];
   }
-  o[0] = c;
+  append_kept(c, live, thr, out, counter);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     c.v[k] = t.v[3 + k]; c.v[3 + k] = v5[k]; c.v[6 + k] = v6[k];
   }
-  o[1] = c;
+  append_kept(c, live, thr, out, counter);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     c.v[k] = v4[k]; c.v[3 + k] = v5[k]; c.v[6 + k] = v6[k];
   }
-  o[2] = c;
+  append_kept(c, live, thr, out, counter);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     c.v[k] = t.v[6 + k]; c.v[3 + k] = v4[k]; c.v[6 + k] = v6[k];
   }
-  o[3] = c;
+  append_kept(c, live, thr, out, counter);
 }
 
 template <typename T, typename G>
@@ -137,9 +156,12 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
   const T thr = (T)(thr_d * thr_d);  // python float, compared in the tensor dtype
   Tri<T> *cur = (Tri<T> *)alloc(ctx, (size_t)F * sizeof(Tri<T>));
   unsigned long long *counter = (unsigned long long *)alloc(ctx, 64);
+  if (!cur || !counter) {
+    set_error("trianglemeshes_to_voxelgrids: allocation failed");
+    return KL_E_ALLOC;
+  }
   unsigned long long *hcount = nullptr;
   KL_CHECK_HIP(hipHostMalloc((void **)&hcount, sizeof(unsigned long long), hipHostMallocDefault));
-  if (!cur || !counter) return KL_E_ALLOC;
   hipLaunchKernelGGL(gather_tris_kernel<T>, dim3((unsigned)cdiv(F, 256)), dim3(256), 0, st, F, pts, faces, cur);
   KL_CHECK_LAUNCH();
   int64_t n = F;
@@ -147,13 +169,14 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
   for (int level = 0; n > 0 && level < 64; level++) {
     Tri<T> *nxt = (Tri<T> *)alloc(ctx, (size_t)n * 4 * sizeof(Tri<T>));
     if (!nxt) {
+      set_error("trianglemeshes_to_voxelgrids: allocation failed");
       rc = KL_E_ALLOC;
       break;
     }
     rc = fill_async(counter, 0, sizeof(unsigned long long), st);
     if (rc) break;
-    hipLaunchKernelGGL((subdivide_kernel<T, G>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, n, cur, thr, R, grid,
-                       nxt, counter);
+    hipLaunchKernelGGL((subdivide_kernel<T, G>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, n, cur, level == 0,
+                       thr, R, grid, nxt, counter);
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(hcount, counter, sizeof(unsigned long long), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess) {

@@ -70,6 +70,10 @@ _SIGS = {
     'kl_dibr_soft_mask_forward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _SZ,
                                         _P]),
+    'kl_prepare_vertices_forward': (_I, [_I, _I, _I, _I, _I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    'kl_prepare_vertices_bwd_workspace_bytes': (_SZ, [_I, _I64]),
+    'kl_prepare_vertices_backward': (_I, [_I, _I, _I, _I, _I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                          _P, _P, _P, _SZ, _P]),
     'kl_unbatched_triangle_distance_workspace_bytes': (_SZ, [_I64]),
     'kl_unbatched_triangle_distance_forward': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_unbatched_triangle_distance_backward': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -1,0 +1,147 @@
+"""prepare_vertices (kaolin/render/mesh/utils.py:128-175): camera transform, perspective
+projection, index_vertices_by_faces and unit face normals -- the inputs of every DIB-R call.
+
+GPU f32 / f64 tensors run one HIP launch forward and one backward call (csrc/prepare.hip,
+``kl_prepare_vertices_forward`` / ``_backward``), with gradients to the vertices and to every
+camera tensor that requires one.  Other devices and dtypes run the reference's torch chain, as
+the reference does on every device.
+"""
+import torch
+from torch.autograd import Function
+
+from ... import _native as N
+from ...ops.mesh import face_normals as _face_normals
+from ...ops.mesh import index_vertices_by_faces
+from ..camera import perspective_camera, rotate_translate_points
+
+__all__ = ['prepare_vertices']
+
+
+def _prepare_vertices_torch(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform):
+    """The reference's chain (utils.py:160-175), for devices / dtypes the HIP path does not take."""
+    if camera_transform is None:
+        vertices_camera = rotate_translate_points(vertices, camera_rot, camera_trans)
+    else:
+        padded_vertices = torch.nn.functional.pad(vertices, (0, 1), mode='constant', value=1.)
+        vertices_camera = padded_vertices @ camera_transform
+    vertices_image = perspective_camera(vertices_camera, camera_proj)
+    face_vertices_camera = index_vertices_by_faces(vertices_camera, faces)
+    face_vertices_image = index_vertices_by_faces(vertices_image, faces)
+    face_normals = _face_normals(face_vertices_camera, unit=True)
+    return face_vertices_camera, face_vertices_image, face_normals
+
+
+def _batches(vertices, camera_proj, camera_rot, camera_trans, camera_transform):
+    """(B, Bv, Bc, Bp) as torch's broadcasting forms them, or None when the shapes fall outside
+    what the kernel takes (the torch chain then runs and raises / broadcasts as the reference)."""
+    if vertices.ndim != 3 or vertices.shape[-1] != 3:
+        return None
+    Bv = vertices.shape[0]
+    if camera_transform is None:
+        if camera_rot.ndim != 3 or camera_rot.shape[1:] != (3, 3) or camera_trans.numel() % 3:
+            return None
+        Bc = camera_rot.shape[0]
+        if camera_trans.numel() // 3 != Bc:
+            return None
+    else:
+        if camera_transform.ndim != 3 or camera_transform.shape[1:] != (4, 3):
+            return None
+        Bc = camera_transform.shape[0]
+    if camera_proj.numel() % 3:
+        return None
+    Bp = camera_proj.numel() // 3
+    B = max(Bv, Bc, Bp)
+    if any(x not in (1, B) for x in (Bv, Bc, Bp)):
+        return None
+    return B, Bv, Bc, Bp
+
+
+class PrepareVerticesHip(Function):
+    """One autograd node for prepare_vertices on the HIP path (csrc/prepare.hip)."""
+
+    @staticmethod
+    def forward(ctx, vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform, batches):
+        B, Bv, Bc, Bp = batches
+        dtype, dev = vertices.dtype, vertices.device
+        V, F = vertices.shape[1], faces.shape[0]
+        verts = vertices.contiguous()
+        fc = faces.contiguous()
+        proj = camera_proj.contiguous()
+        rot = camera_rot.contiguous() if camera_transform is None else None
+        trans = camera_trans.contiguous() if camera_transform is None else None
+        xf = camera_transform.contiguous() if camera_transform is not None else None
+        fvc = torch.empty((B, F, 3, 3), dtype=dtype, device=dev)
+        fvi = torch.empty((B, F, 3, 2), dtype=dtype, device=dev)
+        fn = torch.empty((B, F, 3), dtype=dtype, device=dev)
+        with N.on_device(dev), N.timed('prepare_vertices_forward', dev):
+            N.check(N.lib().kl_prepare_vertices_forward(
+                N.dtype_code(dtype), B, Bv, Bc, Bp, V, F, N.ptr(verts), N.ptr(fc), N.ptr(rot), N.ptr(trans), N.ptr(xf),
+                N.ptr(proj), N.ptr(fvc), N.ptr(fvi), N.ptr(fn), N.stream_of(dev)), 'prepare_vertices')
+        ctx.batches = batches
+        ctx.shapes = (camera_proj.shape, None if camera_trans is None else camera_trans.shape)
+        ctx.save_for_backward(verts, fc, proj, rot, trans, xf)
+        ctx.set_materialize_grads(False)
+        return fvc, fvi, fn
+
+    @staticmethod
+    def backward(ctx, g_fvc, g_fvi, g_fn):
+        verts, fc, proj, rot, trans, xf = ctx.saved_tensors
+        B, Bv, Bc, Bp = ctx.batches
+        need_v, _, need_p, need_r, need_t, need_x, _ = ctx.needs_input_grad
+        if g_fvc is None and g_fvi is None and g_fn is None:
+            return None, None, None, None, None, None, None
+        dtype, dev = verts.dtype, verts.device
+        V, F = verts.shape[1], fc.shape[0]
+        g_v = torch.empty_like(verts) if need_v else None
+        g_cam = torch.empty((Bc, 12), dtype=dtype, device=dev) if (need_r or need_t or need_x) else None
+        g_proj = torch.empty((Bp, 3), dtype=dtype, device=dev) if need_p else None
+        lib = N.lib()
+        nbytes = lib.kl_prepare_vertices_bwd_workspace_bytes(B, V)
+        ws = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
+        with N.on_device(dev), N.timed('prepare_vertices_backward', dev):
+            N.check(lib.kl_prepare_vertices_backward(
+                N.dtype_code(dtype), B, Bv, Bc, Bp, V, F, N.ptr(verts), N.ptr(fc), N.ptr(rot), N.ptr(trans), N.ptr(xf),
+                N.ptr(proj), N.ptr(None if g_fvc is None else g_fvc.contiguous()),
+                N.ptr(None if g_fvi is None else g_fvi.contiguous()), N.ptr(None if g_fn is None else g_fn.contiguous()),
+                N.ptr(g_v), N.ptr(g_cam), N.ptr(g_proj), N.ptr(ws), nbytes, N.stream_of(dev)),
+                'prepare_vertices backward')
+        proj_shape, trans_shape = ctx.shapes
+        g_r = g_cam[:, :9].reshape(Bc, 3, 3) if need_r else None
+        g_t = g_cam[:, 9:].reshape(trans_shape) if need_t else None
+        g_x = g_cam.reshape(Bc, 4, 3) if need_x else None
+        g_p = g_proj.reshape(proj_shape) if need_p else None
+        return g_v, None, g_p, g_r, g_t, g_x, None
+
+
+def prepare_vertices(vertices, faces, camera_proj, camera_rot=None, camera_trans=None, camera_transform=None):
+    r"""Move and project vertices to the cameras, then index them by faces (utils.py:128-175).
+
+    Args:
+        vertices (torch.Tensor): (batch_size, num_vertices, 3).
+        faces (torch.LongTensor): (num_faces, 3).
+        camera_proj (torch.Tensor): (3, 1).
+        camera_rot (torch.Tensor, optional): (batch_size, 3, 3).
+        camera_trans (torch.Tensor, optional): (batch_size, 3).
+        camera_transform (torch.Tensor, optional): (batch_size, 4, 3); replaces rot and trans.
+    Returns:
+        face_vertices_camera (B, F, 3, 3), face_vertices_image (B, F, 3, 2),
+        face_normals (B, F, 3) (unit).
+    """
+    if camera_transform is None:
+        assert camera_trans is not None and camera_rot is not None, \
+            "camera_transform or camera_trans and camera_rot must be defined"
+        cams = (camera_rot, camera_trans)
+    else:
+        assert camera_trans is None and camera_rot is None, \
+            "camera_trans and camera_rot must be None when camera_transform is defined"
+        cams = (camera_transform,)
+    tensors = (vertices, faces, camera_proj) + cams
+    batches = None
+    if (all(t.is_cuda for t in tensors) and len({t.device for t in tensors}) == 1
+            and vertices.dtype in (torch.float32, torch.float64)
+            and all(t.dtype == vertices.dtype for t in (camera_proj,) + cams)
+            and faces.dtype == torch.long and faces.ndim == 2 and faces.shape[-1] == 3):
+        batches = _batches(vertices, camera_proj, camera_rot, camera_trans, camera_transform)
+    if batches is None:
+        return _prepare_vertices_torch(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform)
+    return PrepareVerticesHip.apply(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform, batches)

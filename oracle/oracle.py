@@ -618,3 +618,27 @@ def decode_compact(hits, rec_face, rec_prob, K, rows=None):
     typ[:, rows] = bt
     prob[:, rows] = bp
     return idx, typ, prob
+
+
+# ------------------------------------------------------------ prepare_vertices (§8f rank 3)
+def prepare_vertices(vertices, faces, camera_proj, camera_rot=None, camera_trans=None, camera_transform=None):
+    """numpy restatement of render/mesh/utils.py:128-175 (float64 arithmetic on the given values):
+    camera/legacy.py:35-36 (P - T) @ R^T or utils.py:163-167 [P, 1] @ M; legacy.py:136-137
+    projection; ops/mesh/mesh.py:44-46 gather; ops/mesh/trianglemesh.py:328-334 unit normals.
+    Broadcasts a batch of 1 as torch does.  -> (fvc (B,F,3,3), fvi (B,F,3,2), fn (B,F,3))."""
+    v = np.asarray(vertices, np.float64)
+    if camera_transform is None:
+        t = np.asarray(camera_trans, np.float64).reshape(-1, 1, 3)
+        r = np.asarray(camera_rot, np.float64)
+        vc = np.matmul(v - t, np.transpose(r, (0, 2, 1)))
+    else:
+        m = np.asarray(camera_transform, np.float64)
+        vc = np.matmul(np.concatenate([v, np.ones(v.shape[:-1] + (1,))], -1), m)
+    pp = vc * np.asarray(camera_proj, np.float64).reshape(-1, 1, 3)
+    vi = pp[:, :, :2] / pp[:, :, 2:3]
+    f = np.asarray(faces, np.int64)
+    fvc = vc[:, f]
+    fvi = vi[:, f]
+    n = np.cross(fvc[:, :, 1] - fvc[:, :, 0], fvc[:, :, 2] - fvc[:, :, 0])
+    fn = n / (np.linalg.norm(n, axis=2, keepdims=True) + 1e-10)
+    return fvc, fvi, fn
