@@ -171,9 +171,10 @@ constexpr int LPF = 8;                // lanes per face in the per-face kernels
 
 // Walks a face's exact pixel range [ix0,ix1]x[iy0,iy1] in row-major order, lane s of the
 // face's lane group taking elements s, s+LPF, ...  (no divisions in the loop).
-struct RangeWalk {
+template <int STEP = LPF>
+struct RangeWalkN {
   int w, area, e, col, row;
-  __device__ __forceinline__ RangeWalk(int ix0, int ix1, int iy0, int iy1, int s) {
+  __device__ __forceinline__ RangeWalkN(int ix0, int ix1, int iy0, int iy1, int s) {
     w = ix1 - ix0 + 1;
     area = w * (iy1 - iy0 + 1);
     e = s;
@@ -182,14 +183,15 @@ struct RangeWalk {
   }
   __device__ __forceinline__ bool more() const { return e < area; }
   __device__ __forceinline__ void next() {
-    e += LPF;
-    col += LPF;
+    e += STEP;
+    col += STEP;
     while (col >= w) {
       col -= w;
       row++;
     }
   }
 };
+using RangeWalk = RangeWalkN<LPF>;
 
 // LPF lanes per face; faces whose exact pixel range exceeds VIS_SMALL_AREA are queued
 template <typename T, typename Src, int PASS>
@@ -453,6 +455,113 @@ __global__ void __launch_bounds__(256) raster_bin_kernel(RastSrc<T> src, const T
     }
     bin_mark(g, b, c, lane, tx0, tx1, ty0, ty1, sbitmap, s_bm[threadIdx.x >> 6]);
   }
+}
+
+// raster_bin_kernel's per-face part as a function: the face's record and exact ranges, and its
+// tile rectangles (raster; soft when `soft`), empty = tx0 > tx1.
+template <typename T, int VMODE>
+__device__ __forceinline__ void bin_face(const RastSrc<T> &src, const T *__restrict__ fvz, const BinGeom &g,
+                                         const PixPitch &pp, int64_t f, T *__restrict__ rec, uint2 *__restrict__ rng,
+                                         bool soft, uint2 *__restrict__ srng, T spad, int4 &rt, int4 &st) {
+  T v[6], z[3];
+  src.verts(f, v);
+#pragma unroll
+  for (int q = 0; q < 3; q++) z[q] = fvz[f * 3 + q];
+  bool valid = true;
+  if constexpr (VMODE == 1) valid = src.vmask[f] != 0;
+  if constexpr (VMODE == 2) valid = src.nz[f] >= (T)0;
+  int ix0 = 1, ix1 = 0, iy0 = 1, iy1 = 0;
+  if (valid) {
+    const T xmin = tmin3(v[0], v[2], v[4]), ymin = tmin3(v[1], v[3], v[5]);
+    const T xmax = tmax3(v[0], v[2], v[4]), ymax = tmax3(v[1], v[3], v[5]);
+    exact_range(xmin, xmax, pp.sx, pp.xinv, g.width, false, ix0, ix1);
+    exact_range(ymin, ymax, pp.sy, pp.yinv, g.height, true, iy0, iy1);
+    if (ix0 > ix1 || iy0 > iy1) {
+      ix0 = iy0 = 1;
+      ix1 = iy1 = 0;
+    }
+  }
+  T *r = rec + f * RT_REC;
+#pragma unroll
+  for (int q = 0; q < 6; q++) r[q] = v[q];
+#pragma unroll
+  for (int q = 0; q < 3; q++) r[6 + q] = z[q];
+  rng[f] = make_uint2((uint32_t)ix0 | ((uint32_t)ix1 << 16), (uint32_t)iy0 | ((uint32_t)iy1 << 16));
+  rt = ix0 <= ix1 ? make_int4(ix0 / TILE_W, ix1 / TILE_W, iy0 / TILE_H, iy1 / TILE_H) : make_int4(1, 0, 1, 0);
+  st = make_int4(1, 0, 1, 0);
+  if (soft) {
+    const T bx0 = tmin3(v[0], v[2], v[4]) - spad, by0 = tmin3(v[1], v[3], v[5]) - spad;
+    const T bx1 = tmax3(v[0], v[2], v[4]) + spad, by1 = tmax3(v[1], v[3], v[5]) + spad;
+    int jx0, jx1, jy0, jy1;
+    exact_range(bx0, bx1, pp.sx, pp.xinv, g.width, false, jx0, jx1);
+    exact_range(by0, by1, pp.sy, pp.yinv, g.height, true, jy0, jy1);
+    if (jx0 > jx1 || jy0 > jy1) {
+      jx0 = jy0 = 1;
+      jx1 = jy1 = 0;
+    } else {
+      st = make_int4(jx0 / TILE_W, jx1 / TILE_W, jy0 / TILE_H, jy1 / TILE_H);
+    }
+    srng[f] = make_uint2((uint32_t)jx0 | ((uint32_t)jx1 << 16), (uint32_t)jy0 | ((uint32_t)jy1 << 16));
+  }
+}
+
+// Bins without global atomics: one workgroup per (byte of a bitmap word, mesh), i.e. the 512
+// faces of 8 chunks, marks its chunks' bits in an LDS byte per tile of the view (LDS
+// atomicOr), then stores that byte of every tile's word -- every byte of the bitmaps is
+// written, so the bitmaps need no zero fill and take no global atomics.
+// LDS: one uint32 per tile and bitmap (bin_word_lds_ok).
+constexpr int BIN_WORD_THREADS = 512;  // one face per thread: 8 chunks
+inline bool bin_word_lds_ok(const BinGeom &g) { return (size_t)g.tiles_x * g.tiles_y * 2 * 4 <= 64 * 1024; }
+
+template <typename T, int VMODE>
+__global__ void __launch_bounds__(BIN_WORD_THREADS) raster_bin_word_kernel(
+    RastSrc<T> src, const T *__restrict__ fvz, int F, BinGeom g, PixPitch pp, uint32_t *__restrict__ bitmap,
+    T *__restrict__ rec, uint2 *__restrict__ rng, uint32_t *__restrict__ sbitmap, uint2 *__restrict__ srng, T spad) {
+  extern __shared__ uint32_t s_words[];
+  const int ntv = g.tiles_x * g.tiles_y;
+  const int grp = blockIdx.x, b = blockIdx.y;  // chunks [8 grp, 8 grp + 8)
+  uint32_t *sr = s_words, *ss = s_words + ntv;
+  const bool soft = sbitmap != nullptr;
+  for (int t = threadIdx.x; t < 2 * ntv; t += blockDim.x) s_words[t] = 0;
+  __syncthreads();
+  const int fl = grp * 512 + (int)threadIdx.x;
+  if (fl < F) {
+    int4 rt, st;
+    bin_face<T, VMODE>(src, fvz, g, pp, (int64_t)b * F + fl, rec, rng, soft, srng, spad, rt, st);
+    const uint32_t bit = 1u << ((fl >> 6) & 7);
+    for (int ty = rt.z; ty <= rt.w; ty++)
+      for (int tx = rt.x; tx <= rt.y; tx++) atomicOr(&sr[ty * g.tiles_x + tx], bit);
+    for (int ty = st.z; ty <= st.w; ty++)
+      for (int tx = st.x; tx <= st.y; tx++) atomicOr(&ss[ty * g.tiles_x + tx], bit);
+  }
+  __syncthreads();
+  const size_t base = (size_t)b * ntv;
+  const int word = grp >> 2, byte = grp & 3;  // little-endian: chunk bits 8 byte .. 8 byte + 7
+  uint8_t *rb = reinterpret_cast<uint8_t *>(bitmap), *sb = reinterpret_cast<uint8_t *>(sbitmap);
+  for (int t = threadIdx.x; t < ntv; t += blockDim.x) {
+    const size_t o = ((base + t) * g.words + word) * 4 + byte;
+    rb[o] = (uint8_t)sr[t];
+    if (soft) sb[o] = (uint8_t)ss[t];
+  }
+}
+
+template <typename T>
+static int launch_bin_word(const RastSrc<T> &src, const T *fvz, int F, const BinGeom &g, const PixPitch &pp,
+                           uint32_t *bitmap, T *rec, uint2 *rng, uint32_t *sbitmap, uint2 *srng, T spad,
+                           hipStream_t st) {
+  const dim3 grid((unsigned)(g.words * 4), (unsigned)g.batch);  // every byte of every word
+  const size_t lds = (size_t)g.tiles_x * g.tiles_y * 2 * sizeof(uint32_t);
+  if (src.vmask)
+    hipLaunchKernelGGL((raster_bin_word_kernel<T, 1>), grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp,
+                       bitmap, rec, rng, sbitmap, srng, spad);
+  else if (src.nz)
+    hipLaunchKernelGGL((raster_bin_word_kernel<T, 2>), grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp,
+                       bitmap, rec, rng, sbitmap, srng, spad);
+  else
+    hipLaunchKernelGGL((raster_bin_word_kernel<T, 0>), grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp,
+                       bitmap, rec, rng, sbitmap, srng, spad);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
 }
 
 template <typename T>
@@ -821,9 +930,13 @@ static int launch_rast_tile(RastSrc<T> src, int H, int W, int B, int D, int F, c
   uint8_t *bk = reinterpret_cast<uint8_t *>(w + L.off_bk);
   int32_t *items = reinterpret_cast<int32_t *>(w + L.off_items);
   int *nitems = reinterpret_cast<int *>(w + L.off_n);
+  const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
+  if (bin_word_lds_ok(g) && !(g_dev_flags & (1 << 14))) {  // dev bit 14: the atomic binning
+    KL_CHECK_RC(fill_async(ghist, 0, ORD_HIST * sizeof(int), st));
+    KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, bitmap, rec, rng, nullptr, nullptr, (T)0, st));
+  } else {
   KL_CHECK_RC(fill_async(bitmap, 0, L.off_hist + ORD_HIST * sizeof(int), st));
   const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);
-  const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
   if (src.vmask)
     hipLaunchKernelGGL((raster_bin_kernel<T, 1>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, bitmap, rec, rng);
   else if (src.nz)
@@ -831,6 +944,7 @@ static int launch_rast_tile(RastSrc<T> src, int H, int W, int B, int D, int F, c
   else
     hipLaunchKernelGGL((raster_bin_kernel<T, 0>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, bitmap, rec, rng);
   KL_CHECK_LAUNCH();
+  }
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   // heaviest tiles first; tiles with >= 2^split_from - 1 candidate chunks are split into
   // 2^split_log2 row parts (f32 only: the f64 walk is one wave per row).  Dev flag bits
@@ -1027,7 +1141,7 @@ struct GatherAcc {
   }
 };
 
-template <typename T, int MAXD>
+template <typename T, int MAXD, int LPF_ = LPF>
 __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
     const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
@@ -1035,8 +1149,8 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
     T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig, const uint2 *__restrict__ rng,
     const double *__restrict__ soft) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t tf = t / LPF;  // LPF consecutive lanes per face (whole groups per wave)
-  const int s = (int)(t % LPF);
+  const int64_t tf = t / LPF_;  // LPF_ consecutive lanes per face (whole groups per wave)
+  const int s = (int)(t % LPF_);
   const bool in = tf < (int64_t)B * F;
   const int b = in ? (int)(tf / F) : 0;
   const int64_t f = tf - (int64_t)b * F;
@@ -1049,8 +1163,25 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
   acc.zero();
   int ix0, ix1, iy0, iy1;
   bool queued = false;
-  if (in && (rng ? rng_range(rng, tf, ix0, ix1, iy0, iy1)
-                 : (src.valid(tf) && face_range(src, tf, m, H, W, ix0, ix1, iy0, iy1)))) {
+  const bool has = in && (rng ? rng_range(rng, tf, ix0, ix1, iy0, iy1)
+                              : (src.valid(tf) && face_range(src, tf, m, H, W, ix0, ix1, iy0, iy1)));
+  if (!__any(has)) {
+    // no face of the wave covers a pixel (culled / off-screen runs of the mesh): zero gradients
+    // (+ the soft sums), no walk and no butterfly
+    if (!in) return;
+#pragma unroll
+    for (int q = 0; q < 6 + 3 * MAXD; q++) {
+      if (q % LPF_ != s) continue;
+      if (q < 6) {
+        grad_fvi[tf * 6 + q] = soft ? (T)0 + (T)sv : (T)0;
+      } else {
+        const int r = q - 6, ii = r / MAXD, d = r % MAXD;
+        if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)0;
+      }
+    }
+    return;
+  }
+  if (has) {
     if ((int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) > VIS_SMALL_AREA) {
       queued = true;
       if (s == 0) big[atomicAdd(nbig, 1)] = (int)tf;
@@ -1060,7 +1191,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
       for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
       const T *c = feat + tf * 3 * D;
       const int64_t pbase = (int64_t)b * H * W;
-      RangeWalk rw(ix0, ix1, iy0, iy1, s);
+      RangeWalkN<LPF_> rw(ix0, ix1, iy0, iy1, s);
       while (rw.more()) {
         // face_idx of GATHER_BATCH pixels in flight together; the (rare) hits then load
         // their weights / grads one by one
@@ -1086,17 +1217,17 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
   }
   // fixed-order butterfly over the face's lane group: every lane ends with the total
 #pragma unroll
-  for (int o = 1; o < LPF; o <<= 1) {
+  for (int o = 1; o < LPF_; o <<= 1) {
 #pragma unroll
     for (int q = 0; q < 6; q++) acc.gi[q] += __shfl_xor(acc.gi[q], o);
 #pragma unroll
     for (int q = 0; q < 3 * MAXD; q++) acc.gf[q] += __shfl_xor(acc.gf[q], o);
   }
   if (!in || queued) return;  // queued faces are written by the workgroup kernel
-  // lane s writes the values q = s, s+LPF, ...
+  // lane s writes the values q = s, s+LPF_, ...
 #pragma unroll
   for (int q = 0; q < 6 + 3 * MAXD; q++) {
-    if (q % LPF != s) continue;
+    if (q % LPF_ != s) continue;
     if (q < 6) {  // (q == s) + the soft mask's sum, rounded on its own: autograd's add of the two
       grad_fvi[tf * 6 + q] = soft ? (T)acc.gi[q] + (T)sv : (T)acc.gi[q];
     } else {
@@ -1195,8 +1326,9 @@ static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T 
                                      const uint2 *rng, const double *soft, hipStream_t st) {
   if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
-  hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st, grad,
-                     face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
+  // 8 lanes per face (measured: 4 lanes 62.7 us, 8 lanes 58 us, 16 lanes 91 us at cfg3)
+  hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st,
+                     grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
   KL_CHECK_LAUNCH();
   hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(256), dim3(256), 0, st, grad, face_idx, w, fvi,
                      feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
@@ -1425,9 +1557,13 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   int32_t *sorder = reinterpret_cast<int32_t *>(w + L.off_sorder);
   int *snitems = reinterpret_cast<int *>(w + L.off_sn);
   uint2 *srng = reinterpret_cast<uint2 *>(w + L.off_srng);
-  KL_CHECK_RC(fill_async(w, 0, L.zero, st));
   const RastSrc<T> src{fvi, nullptr, (T)m, fnz};
   const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
+  if (bin_word_lds_ok(g) && !(g_dev_flags & (1 << 14))) {  // dev bit 14: the atomic binning
+    KL_CHECK_RC(fill_async(w + L.off_rgh, 0, L.zero - L.off_rgh, st));  // histograms only
+    KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, rbm, rec, rng, sbm, srng, (T)pad, st));
+  } else {
+  KL_CHECK_RC(fill_async(w, 0, L.zero, st));
   const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);
   if (fnz)
     hipLaunchKernelGGL((raster_bin_kernel<T, 2>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, rbm, rec, rng, sbm,
@@ -1436,6 +1572,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     hipLaunchKernelGGL((raster_bin_kernel<T, 0>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, rbm, rec, rng, sbm,
                        srng, (T)pad);
   KL_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(tile_bucket2_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)rbm,
                      (const uint32_t *)sbm, g.words, nt, rbk, sbk, rgh, sgh, s.scratch);
   KL_CHECK_LAUNCH();

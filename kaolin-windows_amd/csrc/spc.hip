@@ -12,10 +12,11 @@
 // Differences in structure (not in results):
 //   * every kernel runs on the caller's stream (the reference used the legacy default
 //     stream with synchronous cudaMemcpy);
-//   * per level the only host round-trip is ONE 4-byte count read (needed to size the
-//     next level's buffers through the caller's allocator); octree level sizes in
-//     morton_to_octree and the whole pyramid of scan_octrees are computed on device
-//     and read back once;
+//   * mesh_to_spc sizes its per-level buffers on device (capacity + device counters, see
+//     mesh_to_spc_async) and builds every octree level with one scan: three host reads per
+//     call; the per-level path (one 4-byte count read per level) remains the fallback and
+//     the standalone morton_to_octree; the whole pyramid of scan_octrees is computed on
+//     device and read back once;
 //   * the child order of the ray march (VOXEL_ORDER) is derived, not tabulated:
 //     children sorted by (popcount(code ^ j), j).
 #include "common.h"
@@ -403,6 +404,361 @@ static int mesh_to_spc_impl(int64_t F, const float *fv, uint32_t L, Scratch &sc,
   return KL_OK;
 }
 
+// ------------------------------------------------------------------ mesh_to_spc, device-sized
+// The same per-level proposals without a host round-trip per level: each level is ONE launch
+// that tests its proposals (the same SAT) and appends the survivors' children through a
+// device counter (one atomic per wave) into a buffer of capacity `cap`; the next level reads
+// its count from device memory (grid-stride).  Appending loses the generation order, which
+// the reference's stable sort kept among equal mortons -- that order is ascending face id
+// (level 0 is the faces in order; every level keeps its parents' order), so the final sort
+// is on the key (morton << FB) | face: same (morton, face) sequence, same leaves.  Host
+// round-trips: the final proposal count (+ overflow flag and the per-level counts), the
+// unique-leaf count and the octree size -- 3 instead of one per level and per octree level.
+// Overflow of `cap` (or a key wider than 64 bits) falls back to the per-level path.
+__global__ void m2s_init_kernel(int64_t n, uint64_t *__restrict__ m, uint32_t *__restrict__ t,
+                                unsigned long long *__restrict__ counts) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) {  // level 0: every face, in shard 0
+    m[i] = 0;
+    t[i] = (uint32_t)i;
+  }
+  if (i == 0) counts[0] = (unsigned long long)n;
+}
+
+// One workgroup takes chunks of M2S_PER * 256 proposals, tests them, and reserves the
+// chunk's output with ONE atomic.  A returning atomic on one word saturates at ~88 per us
+// (MI355X_MICROARCH.md), so the counters and the output are sharded M2S_SHARDS ways by
+// workgroup (blockIdx % M2S_SHARDS, which also keeps a shard on one XCD): shard g of a
+// level is the region [g * seg, (g + 1) * seg) of the buffer with its own counter.  A
+// level's input is the previous level's shards, indexed as one sequence (their counts'
+// prefix).  (4 proposals per thread, serially, took 49 us at level 0 against ~12 us.)
+constexpr int M2S_PER = 1;
+constexpr int M2S_SHARDS = 32;
+
+// The shards' counts as one sequence: prefix sums in LDS (filled by the workgroup), item i's
+// buffer position by a binary search over them.
+struct ShardIn {
+  unsigned long long *pre;  // LDS, M2S_SHARDS + 1
+  __device__ __forceinline__ void load(unsigned long long *lds, const unsigned long long *c, unsigned long long seg) {
+    pre = lds;
+    if (threadIdx.x == 0) {
+      unsigned long long a = 0;
+      pre[0] = 0;
+      for (int g = 0; g < M2S_SHARDS; g++) {
+        a += c[g] < seg ? c[g] : seg;
+        pre[g + 1] = a;
+      }
+    }
+    __syncthreads();
+  }
+  __device__ __forceinline__ unsigned long long total() const { return pre[M2S_SHARDS]; }
+  // buffer position of logical item i (< total)
+  __device__ __forceinline__ unsigned long long pos(unsigned long long i, unsigned long long seg) const {
+    int lo = 0, hi = M2S_SHARDS - 1;  // last g with pre[g] <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (pre[mid] <= i)
+        lo = mid;
+      else
+        hi = mid - 1;
+    }
+    return (unsigned long long)lo * seg + (i - pre[lo]);
+  }
+};
+
+__global__ void __launch_bounds__(256) m2s_level_kernel(const float *__restrict__ fv, const uint64_t *__restrict__ min_,
+                                                        const uint32_t *__restrict__ tin,
+                                                        const unsigned long long *__restrict__ cnt_in,
+                                                        uint64_t *__restrict__ mout, uint32_t *__restrict__ tout,
+                                                        unsigned long long *__restrict__ cnt_out,
+                                                        unsigned long long seg, int *__restrict__ overflow,
+                                                        uint32_t level, uint32_t not_done) {
+  __shared__ int s_wave[16];
+  __shared__ unsigned long long s_base;
+  __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
+  ShardIn in;
+  in.load(s_pre, cnt_in, seg);  // an overflowed shard is clamped (flagged, the result is discarded)
+  const unsigned long long n = in.total();
+  const int g = blockIdx.x % M2S_SHARDS;
+  const uint32_t kids = not_done ? 8u : 1u;
+  const unsigned long long chunk = (unsigned long long)M2S_PER * blockDim.x;
+  for (unsigned long long base = (unsigned long long)blockIdx.x * chunk; base < n;
+       base += (unsigned long long)gridDim.x * chunk) {
+    uint64_t m[M2S_PER];
+    uint32_t tr[M2S_PER];
+    uint32_t pass = 0;
+#pragma unroll
+    for (int k = 0; k < M2S_PER; k++) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      m[k] = 0;
+      tr[k] = 0;
+      if (i < n) {
+        const unsigned long long p = in.pos(i, seg);
+        m[k] = min_[p];
+        tr[k] = tin[p];
+      }
+    }
+#pragma unroll 1
+    for (int k = 0; k < M2S_PER; k++) {
+      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
+      if (i >= n) continue;
+      float cx, cy, cz, h;
+      voxel_center(m[k], level, cx, cy, cz, h);
+      const float *v = fv + (int64_t)tr[k] * 9;
+      if (tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h)) pass |= 1u << k;
+    }
+    int total = 0;
+    const int pre = block_exclusive_scan(__popc(pass) * (int)kids, s_wave, &total);
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(cnt_out + g, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    unsigned long long o = s_base + (unsigned long long)pre;
+    __syncthreads();  // s_base is rewritten by the next chunk
+    if (!pass) continue;
+    if (o + (unsigned long long)__popc(pass) * kids > seg) {
+      *overflow = 1;
+      continue;
+    }
+    o += (unsigned long long)g * seg;
+#pragma unroll 1
+    for (int k = 0; k < M2S_PER; k++) {
+      if (!(pass >> k & 1)) continue;
+      if (!not_done) {
+        mout[o] = m[k];
+        tout[o] = tr[k];
+        o++;
+        continue;
+      }
+      int16_t px, py, pz;
+      to_point(m[k], px, py, pz);
+      for (uint32_t c = 0; c < 8; c++) {
+        mout[o + c] = to_morton(2 * px + (c >> 2), 2 * py + ((c >> 1) & 1), 2 * pz + (c & 1));
+        tout[o + c] = tr[k];
+      }
+      o += 8;
+    }
+  }
+}
+
+__global__ void m2s_key_kernel(int64_t n, const uint64_t *__restrict__ m, const uint32_t *__restrict__ t,
+                               const unsigned long long *__restrict__ cnt, unsigned long long seg, int fb,
+                               uint64_t *__restrict__ key) {
+  __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  ShardIn in;
+  in.load(s_pre, cnt, seg);
+  if (i >= n) return;
+  const unsigned long long p = in.pos((unsigned long long)i, seg);
+  key[i] = (m[p] << fb) | (uint64_t)t[p];
+}
+
+__global__ void m2s_key_unique_kernel(int64_t n, const uint64_t *__restrict__ key, int fb, uint32_t *__restrict__ flag) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t > n) return;
+  flag[t] = (t == n) ? 0u : ((t == 0 || (key[t - 1] >> fb) != (key[t] >> fb)) ? 1u : 0u);
+}
+
+// the first (lowest face) entry of every morton: the leaf, its face and barycentrics
+__global__ void m2s_key_leaves_kernel(int64_t n, const uint64_t *__restrict__ key, int fb,
+                                      const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
+                                      const float *__restrict__ fv, uint32_t level, uint64_t *__restrict__ mout,
+                                      int64_t *__restrict__ fout, float *__restrict__ bary) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= n || !flag[t]) return;
+  const uint32_t o = psum[t];
+  const uint64_t m = key[t] >> fb;
+  const int64_t f = (int64_t)(key[t] & ((1ull << fb) - 1));
+  mout[o] = m;
+  fout[o] = f;
+  float cx, cy, cz, h;
+  voxel_center(m, level, cx, cy, cz, h);
+  const float *v = fv + f * 9;
+  const F3 v1 = f3(v[0], v[1], v[2]), v2 = f3(v[3], v[4], v[5]), v3 = f3(v[6], v[7], v[8]);
+  const F3 cp = tri_closest(v1, v2, v3, f3(cx, cy, cz));
+  const F3 cr = fcross(fsub(v1, v2), fsub(v1, v3));
+  const float delta = fdot(cr, cr);
+  const F3 d1 = fsub(cp, v1), d2 = fsub(cp, v2), d3v = fsub(cp, v3);
+  F3 q = fcross(d2, d3v);
+  const float da = sqrtf(fdot(q, q));
+  q = fcross(d1, d3v);
+  const float db = sqrtf(fdot(q, q));
+  q = fcross(d1, d2);
+  const float dc = sqrtf(fdot(q, q));
+  const float rs = 1.0f / sqrtf(delta);
+  float bx = da * rs, by = db * rs, bz = dc * rs;
+  if (bx < 0.0f) bx = 0.f;
+  if (by < 0.0f) by = 0.f;
+  if (bz < 0.0f) bz = 0.f;
+  const float sc = (float)(1. / (double)(bx + by + bz));
+  bary[o * 2 + 0] = bx * sc;
+  bary[o * 2 + 1] = by * sc;
+}
+
+// Octree of sorted unique leaf mortons, all levels at once: row j (0..L-1) of `flag` marks
+// the first leaf under each level-j node (row stride n+1, a zero sentinel per row), so ONE
+// exclusive scan over the rows numbers the nodes level by level -- the octree's own order --
+// and each node's byte is the OR of its children's bits, gathered from their first leaves.
+__global__ void oct_flags_kernel(int64_t n, const uint64_t *__restrict__ m, uint32_t L, uint32_t *__restrict__ flag) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const uint32_t j = blockIdx.y;
+  if (t > n) return;
+  const int sh = 3 * (int)(L - j);
+  flag[(int64_t)j * (n + 1) + t] = (t == n) ? 0u : ((t == 0 || (m[t - 1] >> sh) != (m[t] >> sh)) ? 1u : 0u);
+}
+
+// first leaf of every node (the flagged (row, leaf) positions, numbered by the scan)
+__global__ void oct_first_kernel(int64_t n, const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
+                                 uint32_t *__restrict__ first) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t q = (int64_t)blockIdx.y * (n + 1) + t;
+  if (t < n && flag[q]) first[psum[q]] = (uint32_t)t;
+}
+
+// node p's byte: its children are the next level's nodes whose first leaves lie in p's leaf
+// range [first(p), first(p + 1) or n) -- numbered by the scan at those two positions -- or,
+// under the last level, the leaves themselves
+__global__ void oct_byte_kernel(int64_t n, const uint64_t *__restrict__ m, uint32_t L, uint32_t total,
+                                const uint32_t *__restrict__ psum, const uint32_t *__restrict__ first,
+                                uint8_t *__restrict__ out) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (p >= total) return;
+  uint32_t j = 0;
+  while (j + 1 < L && (int64_t)psum[(int64_t)(j + 1) * (n + 1)] <= p) j++;
+  const uint32_t lend = (j + 1 < L) ? psum[(int64_t)(j + 1) * (n + 1)] : total;  // level j's node end
+  const int64_t t0 = first[p];
+  const int64_t t1 = (p + 1 < (int64_t)lend) ? (int64_t)first[p + 1] : n;
+  const int sh = 3 * (int)(L - j - 1);
+  uint32_t code = 0;
+  if (j + 1 == L) {
+    for (int64_t t = t0; t < t1; t++) code |= 1u << (uint32_t)(m[t] & 7);
+  } else {
+    const int64_t r = (int64_t)(j + 1) * (n + 1);
+    const uint32_t c0 = psum[r + t0], c1 = psum[r + t1];
+    for (uint32_t c = c0; c < c1; c++) code |= 1u << (uint32_t)((m[first[c]] >> sh) & 7);
+  }
+  out[p] = (uint8_t)code;
+}
+
+static int morton_to_octree_rows(int64_t n, const uint64_t *morton, uint32_t L, Scratch &sc, uint8_t **octree,
+                                 int64_t *num_nodes, hipStream_t st) {
+  *octree = nullptr;
+  *num_nodes = 0;
+  if (L == 0 || n == 0) return morton_to_octree_impl(n, morton, L, sc, octree, num_nodes, st);
+  const int64_t len = (int64_t)L * (n + 1);
+  if (len + 1 >= ((int64_t)1 << 31)) return morton_to_octree_impl(n, morton, L, sc, octree, num_nodes, st);
+  uint32_t *flag = (uint32_t *)sc.get((size_t)len * sizeof(uint32_t));
+  uint32_t *psum = (uint32_t *)sc.get((size_t)(len + 1) * sizeof(uint32_t));
+  if (!flag || !psum) return KL_E_ALLOC;
+  hipLaunchKernelGGL(oct_flags_kernel, dim3((unsigned)cdiv(n + 1, 256), L), dim3(256), 0, st, n, morton, L, flag);
+  KL_CHECK_LAUNCH();
+  uint32_t total = 0;
+  KL_CHECK_RC(exclusive_scan(flag, psum, len - 1, sc, st, &total));  // psum[len - 1] = nodes (last sentinel 0)
+  uint32_t *first = (uint32_t *)sc.get((size_t)total * sizeof(uint32_t));
+  uint8_t *out = (uint8_t *)sc.get((size_t)total);
+  if (!first || !out) return KL_E_ALLOC;
+  hipLaunchKernelGGL(oct_first_kernel, dim3((unsigned)cdiv(n, 256), L), dim3(256), 0, st, n, flag, psum, first);
+  KL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(oct_byte_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, n, morton, L, total, psum,
+                     first, out);
+  KL_CHECK_LAUNCH();
+  *octree = out;
+  *num_nodes = total;
+  return KL_OK;
+}
+
+// returns KL_OK, an error, or 1 = not taken (capacity / key width): the caller runs the
+// per-level path
+static int mesh_to_spc_async(int64_t F, const float *fv, uint32_t L, Scratch &sc, uint8_t **octree,
+                             int64_t *num_nodes, int64_t **face_idx, float **bary, int64_t *num_leaves,
+                             hipStream_t st) {
+  int fb = 1;
+  while (fb < 32 && ((int64_t)1 << fb) < F) fb++;
+  if (F <= 0 || F >= ((int64_t)1 << 31) || 3 * (int)L + fb > 64 || L == 0) return 1;
+  // capacity per level buffer: 96 proposals per face (cfg4: 9.4 M of 19.2 M at L = 9), in shards
+  const unsigned long long cap = (unsigned long long)std::max<int64_t>(F * 96, (int64_t)1 << 20);
+  if (cap >= (1ull << 31)) return 1;
+  uint64_t *mb[2];
+  uint32_t *tb[2];
+  for (int k = 0; k < 2; k++) {
+    mb[k] = (uint64_t *)sc.get((size_t)cap * sizeof(uint64_t));
+    tb[k] = (uint32_t *)sc.get((size_t)cap * sizeof(uint32_t));
+    if (!mb[k] || !tb[k]) return KL_E_ALLOC;
+  }
+  // counts[l][shard] for l = 0 .. L+1 (proposals per level, then the final pairs), overflow flag
+  const int NC = (SPC_MAX_LEVELS + 2) * M2S_SHARDS;
+  const size_t cbytes = sizeof(unsigned long long) * (NC + 1);
+  unsigned long long *counts = (unsigned long long *)sc.get(cbytes);
+  if (!counts) return KL_E_ALLOC;
+  int *overflow = (int *)(counts + NC);
+  const unsigned long long seg = cap / M2S_SHARDS;
+  KL_CHECK_RC(fill_async(counts, 0, cbytes, st));
+  hipLaunchKernelGGL(m2s_init_kernel, dim3((unsigned)cdiv(F, 256)), dim3(256), 0, st, F, mb[0], tb[0], counts);
+  KL_CHECK_LAUNCH();
+  const unsigned grid = 16384;  // grid-stride over chunks of M2S_PER * 256 proposals (4.2 M per pass)
+  for (uint32_t l = 0; l <= L; l++) {
+    const int a = l & 1;
+    hipLaunchKernelGGL(m2s_level_kernel, dim3(grid), dim3(256), 0, st, fv, mb[a], tb[a], counts + l * M2S_SHARDS,
+                       mb[a ^ 1], tb[a ^ 1], counts + (l + 1) * M2S_SHARDS, seg, overflow, l, L - l);
+    KL_CHECK_LAUNCH();
+  }
+  unsigned long long *h = nullptr;
+  KL_CHECK_HIP(hipHostMalloc((void **)&h, cbytes, hipHostMallocDefault));
+  int rc = KL_OK;
+  if (hipMemcpyAsync(h, counts, cbytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    set_error("mesh_to_spc: count read failed");
+    rc = KL_E_HIP;
+  }
+  const bool over = rc == KL_OK && *(int *)(h + NC) != 0;
+  auto level_total = [&](uint32_t l) {
+    unsigned long long t = 0;
+    for (int g = 0; g < M2S_SHARDS; g++) t += h[l * M2S_SHARDS + g];
+    return (int64_t)t;
+  };
+  const int64_t cnt = rc == KL_OK ? level_total(L + 1) : 0;
+  if (rc == KL_OK && !over) {
+    for (uint32_t l = 0; l <= L; l++) t_m2s_counts[l] = level_total(l);
+    t_m2s_levels = (int)L + 1;
+  }
+  (void)hipHostFree(h);
+  if (rc) return rc;
+  if (over) return 1;
+  if (cnt == 0) return KL_OK;  // empty: (0,) u8, (0,) i64, (0,3) f32 built by the caller
+  const uint32_t *fin_t = tb[(L + 1) & 1];
+  const uint64_t *fin_m = mb[(L + 1) & 1];
+  // keys into the free buffer pair's morton array, sorted into the other pair's
+  uint64_t *key = mb[L & 1];
+  hipLaunchKernelGGL(m2s_key_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, fin_m, fin_t,
+                     counts + (L + 1) * M2S_SHARDS, seg, fb, key);
+  KL_CHECK_LAUNCH();
+  uint64_t *ks = (uint64_t *)sc.get((size_t)cnt * sizeof(uint64_t));
+  if (!ks) return KL_E_ALLOC;
+  size_t tbytes = 0;
+  const int end_bit = 3 * (int)L + fb;
+  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tbytes, key, ks, (int)cnt, 0, end_bit, st));
+  void *tmp = sc.get(tbytes);
+  if (!tmp) return KL_E_ALLOC;
+  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tbytes, key, ks, (int)cnt, 0, end_bit, st));
+  uint32_t *flag = (uint32_t *)sc.get((cnt + 1) * sizeof(uint32_t));
+  uint32_t *psum = (uint32_t *)sc.get((cnt + 2) * sizeof(uint32_t));
+  if (!flag || !psum) return KL_E_ALLOC;
+  hipLaunchKernelGGL(m2s_key_unique_kernel, dim3((unsigned)cdiv(cnt + 1, 256)), dim3(256), 0, st, cnt, ks, fb, flag);
+  KL_CHECK_LAUNCH();
+  uint32_t uniq = 0;
+  KL_CHECK_RC(exclusive_scan(flag, psum, cnt, sc, st, &uniq));
+  uint64_t *mu = (uint64_t *)sc.get((size_t)uniq * sizeof(uint64_t));
+  int64_t *fu = (int64_t *)sc.get((size_t)uniq * sizeof(int64_t));
+  float *bu = (float *)sc.get((size_t)uniq * 2 * sizeof(float));
+  if (!mu || !fu || !bu) return KL_E_ALLOC;
+  hipLaunchKernelGGL(m2s_key_leaves_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, ks, fb, flag, psum,
+                     fv, L, mu, fu, bu);
+  KL_CHECK_LAUNCH();
+  KL_CHECK_RC(morton_to_octree_rows(uniq, mu, L, sc, octree, num_nodes, st));
+  *face_idx = fu;
+  *bary = bu;
+  *num_leaves = uniq;
+  return KL_OK;
+}
+
 // ------------------------------------------------------------------ scan_octrees
 __global__ void popc_kernel(int64_t n, const uint8_t *__restrict__ o, uint32_t *__restrict__ c) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -602,6 +958,11 @@ extern "C" int kl_mesh_to_spc(int64_t num_faces, const float *fv, uint32_t level
   KL_REQUIRE(level < (uint32_t)SPC_MAX_LEVELS, "mesh_to_spc: level must be < 15");
   KL_REQUIRE(alloc != nullptr, "mesh_to_spc: allocator required");
   Scratch sc{alloc, ctx};
+  if (!(g_dev_flags & (1 << 10))) {  // dev bit 10: the per-level path
+    const int rc = mesh_to_spc_async(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves,
+                                     S(stream));
+    if (rc != 1) return rc;
+  }
   return mesh_to_spc_impl(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves, S(stream));
 }
 
