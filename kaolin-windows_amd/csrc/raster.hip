@@ -516,10 +516,14 @@ inline bool bin_word_lds_ok(const BinGeom &g) { return (size_t)g.tiles_x * g.til
 template <typename T, int VMODE>
 __global__ void __launch_bounds__(BIN_WORD_THREADS) raster_bin_word_kernel(
     RastSrc<T> src, const T *__restrict__ fvz, int F, BinGeom g, PixPitch pp, uint32_t *__restrict__ bitmap,
-    T *__restrict__ rec, uint2 *__restrict__ rng, uint32_t *__restrict__ sbitmap, uint2 *__restrict__ srng, T spad) {
+    T *__restrict__ rec, uint2 *__restrict__ rng, uint32_t *__restrict__ sbitmap, uint2 *__restrict__ srng, T spad,
+    int *__restrict__ zero, int nzero) {
   extern __shared__ uint32_t s_words[];
   const int ntv = g.tiles_x * g.tiles_y;
   const int grp = blockIdx.x, b = blockIdx.y;  // chunks [8 grp, 8 grp + 8)
+  // the bucket kernel's histograms, zeroed here instead of by a fill launch
+  if (grp == 0 && b == 0)
+    for (int t = threadIdx.x; t < nzero; t += blockDim.x) zero[t] = 0;
   uint32_t *sr = s_words, *ss = s_words + ntv;
   const bool soft = sbitmap != nullptr;
   for (int t = threadIdx.x; t < 2 * ntv; t += blockDim.x) s_words[t] = 0;
@@ -548,18 +552,18 @@ __global__ void __launch_bounds__(BIN_WORD_THREADS) raster_bin_word_kernel(
 template <typename T>
 static int launch_bin_word(const RastSrc<T> &src, const T *fvz, int F, const BinGeom &g, const PixPitch &pp,
                            uint32_t *bitmap, T *rec, uint2 *rng, uint32_t *sbitmap, uint2 *srng, T spad,
-                           hipStream_t st) {
+                           int *zero, int nzero, hipStream_t st) {
   const dim3 grid((unsigned)(g.words * 4), (unsigned)g.batch);  // every byte of every word
   const size_t lds = (size_t)g.tiles_x * g.tiles_y * 2 * sizeof(uint32_t);
   if (src.vmask)
     hipLaunchKernelGGL((raster_bin_word_kernel<T, 1>), grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp,
-                       bitmap, rec, rng, sbitmap, srng, spad);
+                       bitmap, rec, rng, sbitmap, srng, spad, zero, nzero);
   else if (src.nz)
     hipLaunchKernelGGL((raster_bin_word_kernel<T, 2>), grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp,
-                       bitmap, rec, rng, sbitmap, srng, spad);
+                       bitmap, rec, rng, sbitmap, srng, spad, zero, nzero);
   else
     hipLaunchKernelGGL((raster_bin_word_kernel<T, 0>), grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp,
-                       bitmap, rec, rng, sbitmap, srng, spad);
+                       bitmap, rec, rng, sbitmap, srng, spad, zero, nzero);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
@@ -932,8 +936,8 @@ static int launch_rast_tile(RastSrc<T> src, int H, int W, int B, int D, int F, c
   int *nitems = reinterpret_cast<int *>(w + L.off_n);
   const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
   if (bin_word_lds_ok(g) && !(g_dev_flags & (1 << 14))) {  // dev bit 14: the atomic binning
-    KL_CHECK_RC(fill_async(ghist, 0, ORD_HIST * sizeof(int), st));
-    KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, bitmap, rec, rng, nullptr, nullptr, (T)0, st));
+    KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, bitmap, rec, rng, nullptr, nullptr, (T)0, ghist, ORD_HIST,
+                                   st));
   } else {
   KL_CHECK_RC(fill_async(bitmap, 0, L.off_hist + ORD_HIST * sizeof(int), st));
   const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);
@@ -1560,8 +1564,8 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const RastSrc<T> src{fvi, nullptr, (T)m, fnz};
   const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
   if (bin_word_lds_ok(g) && !(g_dev_flags & (1 << 14))) {  // dev bit 14: the atomic binning
-    KL_CHECK_RC(fill_async(w + L.off_rgh, 0, L.zero - L.off_rgh, st));  // histograms only
-    KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, rbm, rec, rng, sbm, srng, (T)pad, st));
+    KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, rbm, rec, rng, sbm, srng, (T)pad, rgh,
+                                   (int)((L.zero - L.off_rgh) / sizeof(int)), st));  // + histograms zeroed
   } else {
   KL_CHECK_RC(fill_async(w, 0, L.zero, st));
   const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);

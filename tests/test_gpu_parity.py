@@ -619,6 +619,40 @@ def test_chamfer_and_fscore(kal, golden):
     assert fs.shape == (2,) and torch.all((fs >= 0) & (fs <= 1))
 
 
+# reference tests/python/kaolin/metrics/test_pointcloud.py:305-346 (TestFScore) and the
+# f_score docstring example (metrics/pointcloud.py:158-169): inputs and expected values as data
+_FS_GT = [[[8.8977, 4.1709, 1.2839], [8.5640, 7.7767, 9.4214]],
+          [[0.5431, 6.4495, 11.4914], [3.2126, 8.0865, 3.1018]]]
+_FS_PRED = [[[8.8914, 4.1788, 1.2176], [8.5291, 7.5513, 9.5412]],
+            [[0.4010, 6.4602, 11.5183], [3.2977, 8.0325, 3.1180]]]
+_FS_PRED3 = [[[8.8914, 4.1788, 1.2176], [8.5291, 7.5513, 9.5412], [3.7831, 6.0182, 4.1208]],
+             [[0.4010, 6.4602, 11.5183], [3.2977, 8.0325, 3.1180], [2.4987, 5.8763, 3.1987]]]
+_FS_TOL = {torch.half: (1e-3, 1e-3), torch.float32: (1e-5, 1e-4), torch.float64: (1e-6, 1e-5)}
+
+
+@pytest.mark.parametrize('dtype', [torch.half, torch.float32, torch.float64])
+def test_fscore_reference_kats(kal, dtype):
+    atol, rtol = _FS_TOL[dtype]
+    gt = torch.tensor(_FS_GT, dtype=dtype, device=DEV)
+    for pred, e1, e2 in ((_FS_PRED, [0.5, 1.0], [0.5, 0.5]), (_FS_PRED3, [0.4, 0.8], [0.4, 0.4])):
+        pr = torch.tensor(pred, dtype=dtype, device=DEV)
+        o1 = kal.metrics.pointcloud.f_score(gt, pr, radius=0.2)
+        o2 = kal.metrics.pointcloud.f_score(gt, pr, radius=0.12)
+        assert o1.dtype == dtype
+        assert torch.allclose(o1, torch.tensor(e1, dtype=dtype, device=DEV), atol=atol, rtol=rtol)
+        assert torch.allclose(o2, torch.tensor(e2, dtype=dtype, device=DEV), atol=atol, rtol=rtol)
+    if dtype == torch.half:  # the docstring example is f32; in half eps=1e-8 underflows (0/0 in both)
+        return
+    p1 = torch.tensor([[[8.8977, 4.1709, 1.2839], [8.5640, 7.7767, 9.4214]],
+                       [[0.5431, 6.4495, 11.4914], [3.2126, 8.0865, 3.1018]]], device=DEV, dtype=dtype)
+    p2 = torch.tensor([[[9.4863, 4.2249, 0.1712], [8.1783, 8.5310, 8.5119]],
+                       [[-0.0020699, 6.4429, 12.3], [3.8386, 8.3585, 4.7662]]], device=DEV, dtype=dtype)
+    assert torch.allclose(kal.metrics.pointcloud.f_score(p1, p2, radius=1),
+                          torch.tensor([0.0, 0.5], device=DEV, dtype=dtype), atol=atol, rtol=rtol)
+    assert torch.allclose(kal.metrics.pointcloud.f_score(p1, p2, radius=1.5),
+                          torch.tensor([1.0, 0.5], device=DEV, dtype=dtype), atol=atol, rtol=rtol)
+
+
 # ------------------------------------------------------------ voxelgrid
 @pytest.mark.parametrize('name', ['batched', 'origins', 'scale', 'res7', 'default_os', 'sphere32', 'random24'])
 def test_voxelgrid_golden(kal, golden, name):
