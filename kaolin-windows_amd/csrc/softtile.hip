@@ -549,20 +549,21 @@ struct ItemHash {
       global_add_pair<double>(gmesh + (size_t)f * 6, c0, c1, g0x, g0y, g1x, g1y);
     }
   }
-  // one thread per used slot: add its non-zero coordinates to the mesh accumulator, reset it
+  // one thread per (used slot, coordinate), coordinate fastest: a face's 6 sums go out from 6
+  // consecutive lanes to 48 contiguous bytes, so a wave's double atomics leave L2 as a few
+  // 64-B requests per face instead of one request per lane (memory-side atomics,
+  // MI355X_MICROARCH.md: one lane per row is an order of magnitude slower).  Every thread of the
+  // workgroup calls it (barrier before the key reset).
   __device__ __forceinline__ void flush_reset(int tid, int nthreads, double *gmesh) {
     const int n = *nused;
-    for (int u = tid; u < n; u += nthreads) {
-      const int sl = used[u];
-      const int f = key[sl];
-#pragma unroll
-      for (int c = 0; c < 6; c++) {
-        const double v = val[sl * 6 + c];
-        if (v != 0.0) atomicAdd(gmesh + (size_t)f * 6 + c, v);
-        val[sl * 6 + c] = 0.0;
-      }
-      key[sl] = -1;
+    for (int u = tid; u < n * 6; u += nthreads) {
+      const int sl = used[u / 6], c = u % 6;
+      const double v = val[sl * 6 + c];
+      if (v != 0.0) atomicAdd(gmesh + (size_t)key[sl] * 6 + c, v);
+      val[sl * 6 + c] = 0.0;
     }
+    __syncthreads();
+    for (int u = tid; u < n; u += nthreads) key[used[u]] = -1;
   }
 };
 
