@@ -425,14 +425,11 @@ __global__ void m2s_init_kernel(int64_t n, uint64_t *__restrict__ m, uint32_t *_
   if (i == 0) counts[0] = (unsigned long long)n;
 }
 
-// One workgroup takes chunks of M2S_PER * 256 proposals, tests them, and reserves the
-// chunk's output with ONE atomic.  A returning atomic on one word saturates at ~88 per us
-// (MI355X_MICROARCH.md), so the counters and the output are sharded M2S_SHARDS ways by
-// workgroup (blockIdx % M2S_SHARDS, which also keeps a shard on one XCD): shard g of a
-// level is the region [g * seg, (g + 1) * seg) of the buffer with its own counter.  A
-// level's input is the previous level's shards, indexed as one sequence (their counts'
-// prefix).  (4 proposals per thread, serially, took 49 us at level 0 against ~12 us.)
-constexpr int M2S_PER = 1;
+// A returning atomic on one word saturates at ~88 per us (MI355X_MICROARCH.md), so the level
+// counters and the output are sharded M2S_SHARDS ways by workgroup (blockIdx % M2S_SHARDS,
+// which also keeps a shard on one XCD): shard g of a level is the region [g * seg,
+// (g + 1) * seg) of the buffer with its own counter.  A level's input is the previous
+// level's shards, indexed as one sequence (their counts' prefix).
 constexpr int M2S_SHARDS = 32;
 
 // The shards' counts as one sequence: prefix sums in LDS (filled by the workgroup), item i's
@@ -466,6 +463,15 @@ struct ShardIn {
   }
 };
 
+// Each workgroup owns a contiguous span of the level's proposals (n / gridDim, up to 64
+// chunks of 256): it tests them all first (pass bits in a register per thread), reserves the
+// span's whole output with ONE atomic, then writes the survivors' children chunk by chunk
+// (block scans for the positions).  One round of workgroups per launch, one returning atomic
+// per workgroup and level.  (A grid-stride version with one chunk per pass paid a returning
+// atomic per chunk and its 16,384 mostly idle workgroups ~25 us per level.)
+constexpr int M2S_GRID = 2048;
+constexpr int M2S_MAX_CHUNKS = 64;
+
 __global__ void __launch_bounds__(256) m2s_level_kernel(const float *__restrict__ fv, const uint64_t *__restrict__ min_,
                                                         const uint32_t *__restrict__ tin,
                                                         const unsigned long long *__restrict__ cnt_in,
@@ -481,61 +487,64 @@ __global__ void __launch_bounds__(256) m2s_level_kernel(const float *__restrict_
   const unsigned long long n = in.total();
   const int g = blockIdx.x % M2S_SHARDS;
   const uint32_t kids = not_done ? 8u : 1u;
-  const unsigned long long chunk = (unsigned long long)M2S_PER * blockDim.x;
-  for (unsigned long long base = (unsigned long long)blockIdx.x * chunk; base < n;
-       base += (unsigned long long)gridDim.x * chunk) {
-    uint64_t m[M2S_PER];
-    uint32_t tr[M2S_PER];
-    uint32_t pass = 0;
-#pragma unroll
-    for (int k = 0; k < M2S_PER; k++) {
-      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
-      m[k] = 0;
-      tr[k] = 0;
-      if (i < n) {
-        const unsigned long long p = in.pos(i, seg);
-        m[k] = min_[p];
-        tr[k] = tin[p];
-      }
-    }
+  const unsigned long long span = (n + gridDim.x - 1) / gridDim.x;
+  const unsigned long long lo = (unsigned long long)blockIdx.x * span;
+  const unsigned long long hi = lo + span < n ? lo + span : n;
+  if (lo >= hi) return;
+  const int nch = (int)((hi - lo + blockDim.x - 1) / blockDim.x);
+  if (nch > M2S_MAX_CHUNKS) {  // the host sizes the grid so that this does not happen
+    if (threadIdx.x == 0) *overflow = 1;
+    return;
+  }
+  // 1. test every proposal of the span
+  uint64_t pass = 0;
 #pragma unroll 1
-    for (int k = 0; k < M2S_PER; k++) {
-      const unsigned long long i = base + (unsigned long long)k * blockDim.x + threadIdx.x;
-      if (i >= n) continue;
-      float cx, cy, cz, h;
-      voxel_center(m[k], level, cx, cy, cz, h);
-      const float *v = fv + (int64_t)tr[k] * 9;
-      if (tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h)) pass |= 1u << k;
-    }
-    int total = 0;
-    const int pre = block_exclusive_scan(__popc(pass) * (int)kids, s_wave, &total);
-    if (threadIdx.x == 0) s_base = total ? atomicAdd(cnt_out + g, (unsigned long long)total) : 0ull;
-    __syncthreads();
-    unsigned long long o = s_base + (unsigned long long)pre;
-    __syncthreads();  // s_base is rewritten by the next chunk
-    if (!pass) continue;
-    if (o + (unsigned long long)__popc(pass) * kids > seg) {
-      *overflow = 1;
-      continue;
-    }
-    o += (unsigned long long)g * seg;
+  for (int k = 0; k < nch; k++) {
+    const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
+    if (i >= hi) continue;
+    const unsigned long long p = in.pos(i, seg);
+    float cx, cy, cz, h;
+    voxel_center(min_[p], level, cx, cy, cz, h);
+    const float *v = fv + (int64_t)tin[p] * 9;
+    if (tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h)) pass |= 1ull << k;
+  }
+  // 2. one reservation for the span
+  int total = 0;
+  (void)block_exclusive_scan(__popcll(pass) * (int)kids, s_wave, &total);
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(cnt_out + g, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  unsigned long long o0 = s_base;
+  if (total == 0) return;
+  if (o0 + (unsigned long long)total > seg) {
+    if (threadIdx.x == 0) *overflow = 1;
+    return;
+  }
+  o0 += (unsigned long long)g * seg;
+  // 3. the survivors' children, chunk by chunk in order
 #pragma unroll 1
-    for (int k = 0; k < M2S_PER; k++) {
-      if (!(pass >> k & 1)) continue;
+  for (int k = 0; k < nch; k++) {
+    const bool ps = (pass >> k) & 1;
+    int ctot = 0;
+    const int pre = block_exclusive_scan(ps ? (int)kids : 0, s_wave, &ctot);
+    if (ps) {
+      const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
+      const unsigned long long p = in.pos(i, seg);
+      const uint64_t m = min_[p];
+      const uint32_t tr = tin[p];
+      const unsigned long long o = o0 + (unsigned long long)pre;
       if (!not_done) {
-        mout[o] = m[k];
-        tout[o] = tr[k];
-        o++;
-        continue;
+        mout[o] = m;
+        tout[o] = tr;
+      } else {
+        int16_t px, py, pz;
+        to_point(m, px, py, pz);
+        for (uint32_t c = 0; c < 8; c++) {
+          mout[o + c] = to_morton(2 * px + (c >> 2), 2 * py + ((c >> 1) & 1), 2 * pz + (c & 1));
+          tout[o + c] = tr;
+        }
       }
-      int16_t px, py, pz;
-      to_point(m[k], px, py, pz);
-      for (uint32_t c = 0; c < 8; c++) {
-        mout[o + c] = to_morton(2 * px + (c >> 2), 2 * py + ((c >> 1) & 1), 2 * pz + (c & 1));
-        tout[o + c] = tr[k];
-      }
-      o += 8;
     }
+    o0 += (unsigned long long)ctot;
   }
 }
 
@@ -693,7 +702,8 @@ static int mesh_to_spc_async(int64_t F, const float *fv, uint32_t L, Scratch &sc
   KL_CHECK_RC(fill_async(counts, 0, cbytes, st));
   hipLaunchKernelGGL(m2s_init_kernel, dim3((unsigned)cdiv(F, 256)), dim3(256), 0, st, F, mb[0], tb[0], counts);
   KL_CHECK_LAUNCH();
-  const unsigned grid = 16384;  // grid-stride over chunks of M2S_PER * 256 proposals (4.2 M per pass)
+  // one round of workgroups, each a span of at most M2S_MAX_CHUNKS chunks of 256 proposals
+  const unsigned grid = (unsigned)std::max<int64_t>(M2S_GRID, cdiv((int64_t)cap, 256 * M2S_MAX_CHUNKS));
   for (uint32_t l = 0; l <= L; l++) {
     const int a = l & 1;
     hipLaunchKernelGGL(m2s_level_kernel, dim3(grid), dim3(256), 0, st, fv, mb[a], tb[a], counts + l * M2S_SHARDS,
