@@ -14,6 +14,15 @@ import bench  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    if len(sys.argv) > 2:  # dev parameter overrides "IDX=V,IDX=V"
+        import ctypes
+        from kaolin import _native
+        lib = _native.lib()
+        lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
+        for kv in sys.argv[2].split(','):
+            i, v = (int(x) for x in kv.split('='))
+            lib.kl_dev_set_param(i, v)
+        print('params', sys.argv[2], flush=True)
     import kaolin as kal
     verts, faces = bench.cfg4_inputs('cuda')
     vb = verts.unsqueeze(0).contiguous()
