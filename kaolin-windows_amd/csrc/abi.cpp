@@ -128,13 +128,13 @@ extern "C" int kl_abi_version(void) { return 1; }
 // order: deterministic, and the kernel boundary orders the partials (a last-block ticket
 // needs a device-scope release per block, which measured 29 us here).
 namespace kl {
-constexpr int DOT2_BLOCKS = 1024;
+constexpr int DOT2_BLOCKS = 2048;
 
 __device__ __forceinline__ double dot_strip(const float *__restrict__ a, const float *__restrict__ g, size_t n,
                                             size_t t, size_t nt) {
   double s = 0.0;
   const size_t n4 = ((uintptr_t)a % 16 == 0 && (uintptr_t)g % 16 == 0) ? n / 4 : 0;
-#pragma unroll 4
+#pragma unroll 8
   for (size_t i = t; i < n4; i += nt) {
     const float4 x = reinterpret_cast<const float4 *>(a)[i], y = reinterpret_cast<const float4 *>(g)[i];
     s += (double)(x.x * y.x) + (double)(x.y * y.y) + (double)(x.z * y.z) + (double)(x.w * y.w);
@@ -180,7 +180,7 @@ extern "C" int kl_loss_dot2(const float *a, const float *ga, int64_t na, const f
   }
   double *partial = (double *)ws;
   const int64_t vec = (na + nb) / 4;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kl::DOT2_BLOCKS, (vec + 1023) / 1024));
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kl::DOT2_BLOCKS, (vec + 511) / 512));
   hipLaunchKernelGGL(kl::dot2_partial_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, ga, (size_t)na, b,
                      gb, (size_t)nb, partial);
   KL_CHECK_LAUNCH();
