@@ -328,12 +328,17 @@ int kl_unbatched_triangle_distance_forward(kl_dtype dtype, int64_t num_points, i
                                            void *workspace, size_t workspace_bytes, kl_stream stream);
 
 /* unbatched_triangle_distance.cpp:74-114.  grad_points (P,3) fully written;
- * grad_face_vertices (F,3,3) fully written (zero where no point selected the face). */
+ * grad_face_vertices (F,3,3) fully written (zero where no point selected the face).
+ * workspace: kl_unbatched_triangle_distance_bwd_workspace_bytes(F) bytes -- the per-point terms
+ * are then summed per face coordinate in double and rounded once (deterministic); NULL: the
+ * reference's float atomics (order-dependent last bits). */
+size_t kl_unbatched_triangle_distance_bwd_workspace_bytes(int64_t num_faces);
 int kl_unbatched_triangle_distance_backward(kl_dtype dtype, int64_t num_points, int64_t num_faces,
                                             const void *grad_dist, const void *points,
                                             const void *face_vertices, const int64_t *face_idx,
                                             const int32_t *dist_type, void *grad_points,
-                                            void *grad_face_vertices, kl_stream stream);
+                                            void *grad_face_vertices, void *workspace, size_t workspace_bytes,
+                                            kl_stream stream);
 
 /* sided_distance.cpp:65-89.  p1 (B,N,3), p2 (B,M,3) -> dist (B,N), idx (B,N) int64.
  * dtype: any kl_dtype (half/float/double and the integer types of DISPATCH_NUM_TYPES). */

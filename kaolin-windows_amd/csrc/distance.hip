@@ -512,8 +512,8 @@ struct P2MWs {
 // below this many pairs the Morton sort is not worth its launches
 constexpr int64_t P2M_SORT_MIN_PAIRS = (int64_t)1 << 24;
 
-template <typename T>
-__device__ __forceinline__ void edge_bwd(V3<T> vab, V3<T> pb, T *ga, T *gb, T *gp, T grad) {
+template <typename T, typename A>
+__device__ __forceinline__ void edge_bwd(V3<T> vab, V3<T> pb, A *ga, A *gb, T *gp, T grad) {
   const T l = dot(vab, pb);
   const T m = dot(vab, vab);
   const T k = l / m;
@@ -532,15 +532,18 @@ __device__ __forceinline__ void edge_bwd(V3<T> vab, V3<T> pb, T *ga, T *gb, T *g
   const V3<T> vab_bar = (dm_dvab * m_bar + pb * l_bar) + di_dvab;
   const V3<T> vb_bar = mk(-vab_bar.x - pb_bar.x, -vab_bar.y - pb_bar.y, -vab_bar.z - pb_bar.z);
   gp[0] = pb_bar.x; gp[1] = pb_bar.y; gp[2] = pb_bar.z;
-  atomicAdd(ga + 0, vab_bar.x); atomicAdd(ga + 1, vab_bar.y); atomicAdd(ga + 2, vab_bar.z);
-  atomicAdd(gb + 0, vb_bar.x); atomicAdd(gb + 1, vb_bar.y); atomicAdd(gb + 2, vb_bar.z);
+  atomicAdd(ga + 0, (A)vab_bar.x); atomicAdd(ga + 1, (A)vab_bar.y); atomicAdd(ga + 2, (A)vab_bar.z);
+  atomicAdd(gb + 0, (A)vb_bar.x); atomicAdd(gb + 1, (A)vb_bar.y); atomicAdd(gb + 2, (A)vb_bar.z);
 }
 
-template <typename T>
+// A = double: the per-point terms summed per face coordinate in double (rounded once by
+// acc_finalize), so the gradient does not depend on the atomics' order; A = T: the reference's
+// float atomics (no workspace).
+template <typename T, typename A>
 __global__ void __launch_bounds__(256) p2m_bwd_kernel(const T *__restrict__ grad_dist, const T *__restrict__ pts,
                                                        const T *__restrict__ fv, const int64_t *__restrict__ fidx,
                                                        const int32_t *__restrict__ ftype, int64_t P,
-                                                       T *__restrict__ gpts, T *__restrict__ gfv) {
+                                                       T *__restrict__ gpts, A *__restrict__ gfv) {
   const int64_t pi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (pi >= P) return;
   const int type = ftype[pi];
@@ -550,7 +553,7 @@ __global__ void __launch_bounds__(256) p2m_bwd_kernel(const T *__restrict__ grad
   const V3<T> v1 = mk(v[0], v[1], v[2]), v2 = mk(v[3], v[4], v[5]), v3 = mk(v[6], v[7], v[8]);
   const V3<T> e12 = v2 - v1, e23 = v3 - v2, e31 = v1 - v3;
   const T go = (T)(2. * (double)grad_dist[pi]);
-  T *g = gfv + f * 9;
+  A *g = gfv + f * 9;
   T *gp = gpts + pi * 3;
   if (type == 0) {
     const V3<T> pv = p - v1;
@@ -570,21 +573,21 @@ __global__ void __launch_bounds__(256) p2m_bwd_kernel(const T *__restrict__ grad
     const V3<T> ge21 = cross(e31, gn);
     gp[0] = gpv.x; gp[1] = gpv.y; gp[2] = gpv.z;
     const V3<T> tmp = (ge31 + ge21) - gpv;
-    atomicAdd(g + 0, tmp.x); atomicAdd(g + 1, tmp.y); atomicAdd(g + 2, tmp.z);
-    atomicAdd(g + 3, -ge21.x); atomicAdd(g + 4, -ge21.y); atomicAdd(g + 5, -ge21.z);
-    atomicAdd(g + 6, -ge31.x); atomicAdd(g + 7, -ge31.y); atomicAdd(g + 8, -ge31.z);
+    atomicAdd(g + 0, (A)tmp.x); atomicAdd(g + 1, (A)tmp.y); atomicAdd(g + 2, (A)tmp.z);
+    atomicAdd(g + 3, (A)-ge21.x); atomicAdd(g + 4, (A)-ge21.y); atomicAdd(g + 5, (A)-ge21.z);
+    atomicAdd(g + 6, (A)-ge31.x); atomicAdd(g + 7, (A)-ge31.y); atomicAdd(g + 8, (A)-ge31.z);
   } else if (type >= 1 && type <= 3) {
     const V3<T> vv = type == 1 ? v1 : (type == 2 ? v2 : v3);
     const V3<T> gdv = (p - vv) * go;
-    T *gg = g + (type - 1) * 3;
-    atomicAdd(gg + 0, -gdv.x); atomicAdd(gg + 1, -gdv.y); atomicAdd(gg + 2, -gdv.z);
+    A *gg = g + (type - 1) * 3;
+    atomicAdd(gg + 0, (A)-gdv.x); atomicAdd(gg + 1, (A)-gdv.y); atomicAdd(gg + 2, (A)-gdv.z);
     gp[0] = gdv.x; gp[1] = gdv.y; gp[2] = gdv.z;
   } else if (type == 4) {
-    edge_bwd<T>(e12, p - v1, g + 3, g + 0, gp, go);
+    edge_bwd<T, A>(e12, p - v1, g + 3, g + 0, gp, go);
   } else if (type == 5) {
-    edge_bwd<T>(e23, p - v2, g + 6, g + 3, gp, go);
+    edge_bwd<T, A>(e23, p - v2, g + 6, g + 3, gp, go);
   } else {
-    edge_bwd<T>(e31, p - v3, g + 0, g + 6, gp, go);
+    edge_bwd<T, A>(e31, p - v3, g + 0, g + 6, gp, go);
   }
 }
 
@@ -760,13 +763,25 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
 
 template <typename T>
 static int p2m_bwd(int64_t P, int64_t F, const void *grad, const void *pts, const void *fv, const int64_t *idx,
-                   const int32_t *type, void *gp, void *gf, hipStream_t st) {
-  KL_CHECK_RC(fill_async(gf, 0, sizeof(T) * (size_t)F * 9, st));
-  if (P == 0) return KL_OK;
-  hipLaunchKernelGGL(p2m_bwd_kernel<T>, dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, (const T *)grad,
-                     (const T *)pts, (const T *)fv, idx, type, P, (T *)gp, (T *)gf);
-  KL_CHECK_LAUNCH();
-  return KL_OK;
+                   const int32_t *type, void *gp, void *gf, void *ws, size_t ws_bytes, hipStream_t st) {
+  const size_t n = (size_t)F * 9;
+  if (ws == nullptr) {  // the reference's float atomics into the zeroed output
+    KL_CHECK_RC(fill_async(gf, 0, sizeof(T) * n, st));
+    if (P == 0) return KL_OK;
+    hipLaunchKernelGGL((p2m_bwd_kernel<T, T>), dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, (const T *)grad,
+                       (const T *)pts, (const T *)fv, idx, type, P, (T *)gp, (T *)gf);
+    KL_CHECK_LAUNCH();
+    return KL_OK;
+  }
+  KL_REQUIRE(ws_bytes >= n * sizeof(double), "unbatched_triangle_distance_backward: workspace too small");
+  double *acc = reinterpret_cast<double *>(ws);
+  KL_CHECK_RC(fill_async(acc, 0, n * sizeof(double), st));
+  if (P > 0) {
+    hipLaunchKernelGGL((p2m_bwd_kernel<T, double>), dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, (const T *)grad,
+                       (const T *)pts, (const T *)fv, idx, type, P, (T *)gp, acc);
+    KL_CHECK_LAUNCH();
+  }
+  return acc_finalize<T>(acc, (T *)gf, n, false, st);
 }
 
 template <typename S>
@@ -819,11 +834,16 @@ extern "C" int kl_unbatched_triangle_distance_forward(kl_dtype dtype, int64_t P,
   return KL_E_INVALID;
 }
 
+extern "C" size_t kl_unbatched_triangle_distance_bwd_workspace_bytes(int64_t F) {
+  return (size_t)(F > 0 ? F : 1) * 9 * sizeof(double);
+}
+
 extern "C" int kl_unbatched_triangle_distance_backward(kl_dtype dtype, int64_t P, int64_t F, const void *grad,
                                                        const void *pts, const void *fv, const int64_t *idx,
-                                                       const int32_t *type, void *gp, void *gf, kl_stream stream) {
-  if (dtype == KL_F32) return p2m_bwd<float>(P, F, grad, pts, fv, idx, type, gp, gf, S(stream));
-  if (dtype == KL_F64) return p2m_bwd<double>(P, F, grad, pts, fv, idx, type, gp, gf, S(stream));
+                                                       const int32_t *type, void *gp, void *gf, void *ws,
+                                                       size_t ws_bytes, kl_stream stream) {
+  if (dtype == KL_F32) return p2m_bwd<float>(P, F, grad, pts, fv, idx, type, gp, gf, ws, ws_bytes, S(stream));
+  if (dtype == KL_F64) return p2m_bwd<double>(P, F, grad, pts, fv, idx, type, gp, gf, ws, ws_bytes, S(stream));
   set_error("unbatched_triangle_distance_backward_cuda not implemented for this dtype");
   return KL_E_INVALID;
 }

@@ -313,11 +313,14 @@ def unbatched_triangle_distance_backward_cuda(grad_dist, points, face_vertices, 
     _float_only(func, points)
     N.require_gpu(func, points)
     dev = points.device
+    # the per-point terms summed per face coordinate in double, rounded once (deterministic)
+    nbytes = N.lib().kl_unbatched_triangle_distance_bwd_workspace_bytes(F)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     with N.on_device(dev), N.timed(func, dev):
         N.check(N.lib().kl_unbatched_triangle_distance_backward(
             N.dtype_code(points.dtype), P, F, N.ptr(grad_dist), N.ptr(points), N.ptr(face_vertices),
-            N.ptr(face_idx), N.ptr(dist_type), N.ptr(grad_points), N.ptr(grad_face_vertices), N.stream_of(dev)),
-            func)
+            N.ptr(face_idx), N.ptr(dist_type), N.ptr(grad_points), N.ptr(grad_face_vertices), N.ptr(ws), nbytes,
+            N.stream_of(dev)), func)
 
 
 def sided_distance_forward_cuda(p1, p2):
