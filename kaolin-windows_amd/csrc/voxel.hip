@@ -78,29 +78,29 @@ __device__ __forceinline__ bool needs_split(const T *v, T thr) {
   return mx > thr;
 }
 
-// Appends the triangles of `kids` that need a further split to `out` (one atomic per wave).
-template <typename T>
-__device__ __forceinline__ void append_kept(const Tri<T> &t, bool live, T thr, Tri<T> *__restrict__ out,
-                                            unsigned long long *__restrict__ counter) {
-  const bool keep = live && needs_split(t.v, thr);
-  const uint64_t km = ballot(keep);
-  if (!km) return;
-  const int lane = lane_id();
-  const int leader = __builtin_ctzll(km);
-  unsigned long long base = 0;
-  if (lane == leader) base = atomicAdd(counter, (unsigned long long)__popcll(km));
-  base = __shfl(base, leader);
-  if (keep) out[base + __popcll(km & ((1ull << lane) - 1))] = t;
-}
-
 // One subdivision round over triangles that need a split (level 0: every face, tested
 // here).  The three midpoints are marked; of the four children only those that need a
 // split themselves (the reference's next-round test on their own coordinates) are written:
-// the others add no vertex the grid does not already hold.
+// the others add no vertex the grid does not already hold.  The workgroup's kept children
+// are counted first and reserved with ONE returning atomic (one per wave and child took 156 /
+// 365 us at cfg4's first two rounds: a returning atomic on one word saturates near 88 per us).
+template <typename T>
+__device__ __forceinline__ void make_child(const Tri<T> &t, const T *v4, const T *v5, const T *v6, int c, Tri<T> &o) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {  // (v1,v4,v5),(v2,v5,v6),(v4,v5,v6),(v3,v4,v6)
+    if (c == 0) { o.v[k] = t.v[k]; o.v[3 + k] = v4[k]; o.v[6 + k] = v5[k]; }
+    if (c == 1) { o.v[k] = t.v[3 + k]; o.v[3 + k] = v5[k]; o.v[6 + k] = v6[k]; }
+    if (c == 2) { o.v[k] = v4[k]; o.v[3 + k] = v5[k]; o.v[6 + k] = v6[k]; }
+    if (c == 3) { o.v[k] = t.v[6 + k]; o.v[3 + k] = v4[k]; o.v[6 + k] = v6[k]; }
+  }
+}
+
 template <typename T, typename G>
-__global__ void subdivide_kernel(int64_t n, const Tri<T> *__restrict__ in, bool test_input, T thr, int R,
-                                 G *__restrict__ grid, Tri<T> *__restrict__ out,
-                                 unsigned long long *__restrict__ counter) {
+__global__ void __launch_bounds__(256) subdivide_kernel(int64_t n, const Tri<T> *__restrict__ in, bool test_input,
+                                                        T thr, int R, G *__restrict__ grid, Tri<T> *__restrict__ out,
+                                                        unsigned long long *__restrict__ counter) {
+  __shared__ int s_wave[16];
+  __shared__ unsigned long long s_base;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   bool live = false;
   Tri<T> t;
@@ -108,7 +108,6 @@ __global__ void subdivide_kernel(int64_t n, const Tri<T> *__restrict__ in, bool 
     t = in[i];
     live = !test_input || needs_split(t.v, thr);
   }
-  if (!__any(live)) return;
   T v4[3], v5[3], v6[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
@@ -116,32 +115,30 @@ __global__ void subdivide_kernel(int64_t n, const Tri<T> *__restrict__ in, bool 
     v5[k] = (t.v[k] + t.v[3 + k]) / (T)2;
     v6[k] = (t.v[3 + k] + t.v[6 + k]) / (T)2;
   }
+  uint32_t keep = 0;
   if (live) {
     mark_point<T, G>(v4[0], v4[1], v4[2], R, grid);
     mark_point<T, G>(v5[0], v5[1], v5[2], R, grid);
     mark_point<T, G>(v6[0], v6[1], v6[2], R, grid);
-  }
-  Tri<T> c;
 #pragma unroll
-  for (int k = 0; k < 3; k++) {  // (v1,v4,v5),(v2,v5,v6),(v4,v5,v6),(v3,v4,v6)
-    c.v[k] = t.v[k]; c.v[3 + k] = v4[k]; c.v[6 + k] = v5[k];
+    for (int c = 0; c < 4; c++) {
+      Tri<T> o;
+      make_child(t, v4, v5, v6, c, o);
+      if (needs_split(o.v, thr)) keep |= 1u << c;
+    }
   }
-  append_kept(c, live, thr, out, counter);
+  int total = 0;
+  const int pre = block_exclusive_scan(__popc(keep), s_wave, &total);
+  if (total == 0) return;  // uniform: every thread saw the same total
+  if (threadIdx.x == 0) s_base = atomicAdd(counter, (unsigned long long)total);
+  __syncthreads();
+  unsigned long long o = s_base + (unsigned long long)pre;
 #pragma unroll
-  for (int k = 0; k < 3; k++) {
-    c.v[k] = t.v[3 + k]; c.v[3 + k] = v5[k]; c.v[6 + k] = v6[k];
+  for (int c = 0; c < 4; c++) {
+    if (!(keep >> c & 1)) continue;
+    make_child(t, v4, v5, v6, c, out[o]);
+    o++;
   }
-  append_kept(c, live, thr, out, counter);
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    c.v[k] = v4[k]; c.v[3 + k] = v5[k]; c.v[6 + k] = v6[k];
-  }
-  append_kept(c, live, thr, out, counter);
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    c.v[k] = t.v[6 + k]; c.v[3 + k] = v4[k]; c.v[6 + k] = v6[k];
-  }
-  append_kept(c, live, thr, out, counter);
 }
 
 template <typename T, typename G>
