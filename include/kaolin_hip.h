@@ -468,6 +468,14 @@ int kl_voxelgrid_mark(int64_t num_vertices, const float *points, int64_t num_fac
                       int resolution, kl_dtype grid_dtype, void *grid, kl_alloc_fn alloc, void *alloc_ctx,
                       kl_stream stream);
 
+/* The default origin / scale of trianglemeshes_to_voxelgrids (trianglemesh.py:74-77) for B
+ * meshes of V vertices (B,V,3): origin (B,3) = torch.min(vertices, dim=1), scale (B) =
+ * torch.max(torch.max(vertices, dim=1) - origin, dim=1), exactly (NaN propagated per
+ * coordinate).  f32 / f64.  ws: kl_voxelgrid_bounds_workspace_bytes(B) bytes. */
+size_t kl_voxelgrid_bounds_workspace_bytes(int batch);
+int kl_voxelgrid_bounds(kl_dtype dtype, int batch, int64_t num_vertices, const void *vertices, void *origin,
+                        void *scale, void *workspace, size_t workspace_bytes, kl_stream stream);
+
 /* Same for float64 vertices (the reference subdivides in the vertex dtype). */
 int kl_voxelgrid_mark_f64(int64_t num_vertices, const double *points, int64_t num_faces, const int64_t *faces,
                           int resolution, kl_dtype grid_dtype, void *grid, kl_alloc_fn alloc, void *alloc_ctx,

@@ -19,6 +19,8 @@
 
 #include <hip/hip_fp16.h>
 
+#include <algorithm>
+
 namespace kl {
 
 template <typename T>
@@ -202,9 +204,137 @@ static int voxel_dispatch_grid(int64_t V, const void *pts, int64_t F, const int6
   return KL_E_INVALID;
 }
 
+// ---- default origin / scale (trianglemesh.py:74-77): per mesh, origin = min over the
+// vertices of each coordinate, scale = max over the coordinates of (max - origin).  Min / max
+// are order-independent, so a block reduction plus atomicMin / atomicMax on order-preserving
+// integer keys gives torch.min / torch.max's values exactly; a NaN coordinate makes the mesh's
+// results NaN, as torch's reductions propagate it.  (torch's two dim=1 reductions over the
+// 100k x 3 vertices took ~100 us at cfg4: three outputs per mesh parallelise poorly.)
+template <typename T>
+struct OKey;
+template <>
+struct OKey<float> {
+  using U = unsigned int;
+  __device__ static U key(float f) {
+    const U b = __float_as_uint(f);
+    return (b >> 31) ? ~b : (b | 0x80000000u);
+  }
+  __device__ static float val(U k) { return __uint_as_float((k >> 31) ? (k & 0x7fffffffu) : ~k); }
+};
+template <>
+struct OKey<double> {
+  using U = unsigned long long;
+  __device__ static U key(double f) {
+    const U b = (U)__double_as_longlong(f);
+    return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+  }
+  __device__ static double val(U k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffull) : ~k));
+  }
+};
+
+// acc per mesh: [min x, y, z, max x, y, z, nan x, y, z]
+template <typename T>
+__global__ void __launch_bounds__(256) bounds_init_kernel(int B, typename OKey<T>::U *__restrict__ acc) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B * 9) acc[i] = (i % 9) < 3 ? ~(typename OKey<T>::U)0 : (typename OKey<T>::U)0;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bounds_reduce_kernel(int64_t V, const T *__restrict__ pts,
+                                                            typename OKey<T>::U *__restrict__ acc) {
+  using U = typename OKey<T>::U;
+  __shared__ U s_r[4][9];
+  const int b = blockIdx.y;
+  U mn[3] = {~(U)0, ~(U)0, ~(U)0}, mx[3] = {0, 0, 0};
+  U nan[3] = {0, 0, 0};
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < V; i += (int64_t)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      const T v = pts[((int64_t)b * V + i) * 3 + c];
+      if (v != v) nan[c] = 1;
+      const U k = OKey<T>::key(v);
+      mn[c] = k < mn[c] ? k : mn[c];
+      mx[c] = k > mx[c] ? k : mx[c];
+    }
+  }
+  U r[9] = {mn[0], mn[1], mn[2], mx[0], mx[1], mx[2], nan[0], nan[1], nan[2]};
+#pragma unroll
+  for (int q = 0; q < 9; q++)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const U u = __shfl_xor(r[q], o);
+      r[q] = q < 3 ? (u < r[q] ? u : r[q]) : (u > r[q] ? u : r[q]);
+    }
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < 9; q++) s_r[wid][q] = r[q];
+  __syncthreads();
+  if (threadIdx.x < 9) {
+    const int q = threadIdx.x;
+    U a = s_r[0][q];
+    for (int w = 1; w < 4; w++) a = q < 3 ? (s_r[w][q] < a ? s_r[w][q] : a) : (s_r[w][q] > a ? s_r[w][q] : a);
+    if (q < 3)
+      atomicMin(acc + b * 9 + q, a);
+    else
+      atomicMax(acc + b * 9 + q, a);
+  }
+}
+
+template <typename T>
+__global__ void bounds_final_kernel(int B, const typename OKey<T>::U *__restrict__ acc, T *__restrict__ origin,
+                                    T *__restrict__ scale) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const typename OKey<T>::U *a = acc + b * 9;
+  T s = (T)0;
+  for (int c = 0; c < 3; c++) {
+    const bool nan = a[6 + c] != 0;  // torch's min / max propagate a NaN of the coordinate
+    const T lo = nan ? (T)NAN : OKey<T>::val(a[c]), hi = nan ? (T)NAN : OKey<T>::val(a[3 + c]);
+    origin[b * 3 + c] = lo;
+    const T d = hi - lo;  // torch.max(dim=1): NaN propagates
+    if (c == 0 || d > s || d != d) s = (s != s) ? s : d;
+  }
+  scale[b] = s;
+}
+
+template <typename T>
+static int voxel_bounds(int B, int64_t V, const T *pts, T *origin, T *scale, void *ws, size_t ws_bytes,
+                        hipStream_t st) {
+  using U = typename OKey<T>::U;
+  KL_REQUIRE(ws_bytes >= (size_t)B * 9 * sizeof(U), "voxelgrid bounds: workspace too small");
+  KL_REQUIRE(V > 0, "voxelgrid bounds: no vertices");
+  if (B == 0) return KL_OK;
+  U *acc = reinterpret_cast<U *>(ws);
+  hipLaunchKernelGGL(bounds_init_kernel<T>, dim3((unsigned)cdiv(B * 9, 256)), dim3(256), 0, st, B, acc);
+  KL_CHECK_LAUNCH();
+  const unsigned gx = (unsigned)std::min<int64_t>(cdiv(V, 256), 256);
+  hipLaunchKernelGGL(bounds_reduce_kernel<T>, dim3(gx, B), dim3(256), 0, st, V, pts, acc);
+  KL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bounds_final_kernel<T>, dim3((unsigned)cdiv(B, 64)), dim3(64), 0, st, B, (const U *)acc, origin,
+                     scale);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
 }  // namespace kl
 
 using namespace kl;
+
+extern "C" size_t kl_voxelgrid_bounds_workspace_bytes(int batch) { return (size_t)(batch > 0 ? batch : 1) * 9 * 8; }
+
+extern "C" int kl_voxelgrid_bounds(kl_dtype dtype, int batch, int64_t num_vertices, const void *vertices,
+                                   void *origin, void *scale, void *ws, size_t ws_bytes, kl_stream stream) {
+  if (dtype == KL_F32)
+    return voxel_bounds<float>(batch, num_vertices, (const float *)vertices, (float *)origin, (float *)scale, ws,
+                               ws_bytes, S(stream));
+  if (dtype == KL_F64)
+    return voxel_bounds<double>(batch, num_vertices, (const double *)vertices, (double *)origin, (double *)scale, ws,
+                                ws_bytes, S(stream));
+  set_error("trianglemeshes_to_voxelgrids bounds: f32 / f64 only");
+  return KL_E_INVALID;
+}
 
 extern "C" int kl_voxelgrid_mark(int64_t V, const float *pts, int64_t F, const int64_t *faces, int R,
                                  kl_dtype grid_dtype, void *grid, kl_alloc_fn alloc, void *ctx, kl_stream stream) {

@@ -109,6 +109,8 @@ _SIGS = {
     'kl_check_sign_workspace_bytes': (_SZ, [_I, _I64, _I64, _I64]),
     'kl_check_sign': (_I, [_I, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, ALLOC_FN, _P, _P]),
     'kl_voxelgrid_mark': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
+    'kl_voxelgrid_bounds_workspace_bytes': (_SZ, [_I]),
+    'kl_voxelgrid_bounds': (_I, [_I, _I, _I64, _P, _P, _P, _P, _SZ, _P]),
     'kl_voxelgrid_mark_f64': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
 }
 

@@ -666,6 +666,30 @@ def test_voxelgrid_golden(kal, golden, name):
     assert set(np.unique(A(vg))) <= {0.0, 1.0}
 
 
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+def test_voxelgrid_default_bounds_equal_torch(kal, dtype):
+    """kl_voxelgrid_bounds: the default origin / scale (trianglemesh.py:74-77) equal torch's
+    min / max reductions exactly, NaN propagated per coordinate."""
+    from kaolin import _native as N
+    g = torch.Generator().manual_seed(11)
+    v = (torch.randn((3, 5000, 3), generator=g, dtype=torch.float64) * 3 - 1).to(dtype)
+    v[1, 17, 2] = float('nan')
+    v[2, :, 0] = -0.0
+    vd = v.to(DEV)
+    o = torch.empty((3, 3), dtype=dtype, device=DEV)
+    sc = torch.empty((3,), dtype=dtype, device=DEV)
+    nb = N.lib().kl_voxelgrid_bounds_workspace_bytes(3)
+    ws = torch.empty(nb, dtype=torch.uint8, device=DEV)
+    N.check(N.lib().kl_voxelgrid_bounds(N.dtype_code(dtype), 3, 5000, N.ptr(vd), N.ptr(o), N.ptr(sc), N.ptr(ws), nb,
+                                        N.stream_of(vd.device)), 'bounds')
+    ro = torch.min(v, dim=1)[0]
+    rs = torch.max(torch.max(v, dim=1)[0] - ro, dim=1)[0]
+    assert torch.equal(torch.isnan(o.cpu()), torch.isnan(ro)) and torch.equal(torch.isnan(sc.cpu()), torch.isnan(rs))
+    fin = ~torch.isnan(ro)
+    assert torch.equal(o.cpu()[fin], ro[fin])
+    assert torch.equal(sc.cpu()[~torch.isnan(rs)], rs[~torch.isnan(rs)])
+
+
 def test_voxelgrid_sparse(kal, golden):
     g = golden('voxelgrid.npz')
     vg = kal.ops.conversions.trianglemeshes_to_voxelgrids(T(g['batched_vertices']), T(g['batched_faces']), 3,
