@@ -448,7 +448,8 @@ int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points, int64_t n
 
 /* check_sign (ops/mesh/check_sign.py:25-154) for a batch: verts (B,V,3), faces (F,3) int64,
  * points (B,P,3), maxlen (B) the per-mesh divisor check_sign.py:140-146 applies to verts and
- * points (NULL: none) -> contains (B,P) bool bytes (odd crossing count).  workspace:
+ * points (NULL: computed here from verts as check_sign.py:140-146 does, exactly; V > 0)
+ * -> contains (B,P) bool bytes (odd crossing count).  workspace:
  * kl_check_sign_workspace_bytes(dtype, B, F, P) bytes (no initialisation needed); the (y, z)
  * grid's face lists are allocated through `alloc` once their length is known (one 8-byte
  * device-to-host read and a stream synchronisation). */

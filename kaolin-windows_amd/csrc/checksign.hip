@@ -131,62 +131,49 @@ __device__ __forceinline__ void cs_load_face(const CsFaces<T> &src, int64_t b, i
   }
 }
 
-// Float-bit order key of v (monotone), for the point ordering below.
-__device__ __forceinline__ uint32_t cs_order_bits(float v) {
-  const uint32_t u = __float_as_uint(v);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ uint32_t cs_spread16(uint32_t x) {
-  x &= 0xffffu;
-  x = (x | (x << 8)) & 0x00ff00ffu;
-  x = (x | (x << 4)) & 0x0f0f0f0fu;
-  x = (x | (x << 2)) & 0x33333333u;
-  x = (x | (x << 1)) & 0x55555555u;
-  return x;
-}
-
-// Sort keys: 2D Morton code of the top 16 order bits of (y, z), so that the 256 points of a
-// workgroup share a small (y, z) box and the face culling below removes most of the mesh.
-// The order only changes which lane tests which point; every count is unchanged.
-template <typename T>
-__global__ void __launch_bounds__(256)
-    cs_key_kernel(int64_t n, int64_t P, const T *__restrict__ points, uint32_t *__restrict__ keys,
-                  int32_t *__restrict__ vals) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t ky = cs_order_bits((float)points[i * 3 + 1]) >> 16;
-  const uint32_t kz = cs_order_bits((float)points[i * 3 + 2]) >> 16;
-  keys[i] = (cs_spread16(ky) << 1) | cs_spread16(kz);
-  vals[i] = (int32_t)(i % P);  // point index within its mesh
-}
-
 // ---- batched entry: a (y, z) grid of face lists ------------------------------------------
 // A ray toward +x can only cross faces whose (y, z) bounds hold the point, so the mesh's (y, z)
 // box is cut into G x G cells and every face is listed in the cells its float bounds overlap.
 // The cell of a value is a monotone function of it (the same float expression for faces and
 // points), so every face that passes a point's bbox_check is in the point's cell list.  The
 // counts do not depend on the order of a list.  Points outside the box cross nothing.
+//
+// The lists hold the face records themselves (no index to chase), and the points are put in
+// cell order by a counting sort over the same grid, so that the lanes of a wave walk the same
+// list: every count is unchanged by either.
 
-// Per face: normalised corners (9 x T) and float (y, z) bounds (4), written once; plus the
-// per-tile union bounds (reduced to the mesh box below).
+// Face record: float (y, z) bounds first (one 16-byte load), then the normalised corners.
+template <typename T>
+struct alignas(16) CsRec {
+  float bb[4];
+  T p[9];
+};
+// A point in cell order: normalised coordinates and its index within its mesh.
+template <typename T>
+struct alignas(16) CsPt {
+  T q[3];
+  int32_t p;
+};
+
+// Per face: the record, written once; plus the per-tile union bounds (reduced to the mesh box
+// below).
 template <typename T>
 __global__ void __launch_bounds__(kCsTile)
-    cs_prep_kernel(int64_t F, CsFaces<T> src, T *__restrict__ fc, float *__restrict__ fb, float *__restrict__ tbox) {
+    cs_prep_kernel(int64_t F, CsFaces<T> src, CsRec<T> *__restrict__ rec, float *__restrict__ tbox) {
   __shared__ float s_r[4][kCsTile / 64];
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * kCsTile + tid;
   float r0 = INFINITY, r1 = -INFINITY, r2 = INFINITY, r3 = -INFINITY;
   if (f < F) {
-    T v[9];
-    cs_load_face(src, b, f, v);
-    const int64_t o = b * F + f;
-#pragma unroll
-    for (int k = 0; k < 9; k++) fc[o * 9 + k] = v[k];
-    const float bb[4] = {(float)fmin(v[1], fmin(v[4], v[7])), (float)fmax(v[1], fmax(v[4], v[7])),
-                         (float)fmin(v[2], fmin(v[5], v[8])), (float)fmax(v[2], fmax(v[5], v[8]))};
-#pragma unroll
-    for (int k = 0; k < 4; k++) fb[o * 4 + k] = bb[k];
-    r0 = bb[0]; r1 = bb[1]; r2 = bb[2]; r3 = bb[3];
+    CsRec<T> r;
+    cs_load_face(src, b, f, r.p);
+    const T *v = r.p;
+    r.bb[0] = (float)fmin(v[1], fmin(v[4], v[7]));
+    r.bb[1] = (float)fmax(v[1], fmax(v[4], v[7]));
+    r.bb[2] = (float)fmin(v[2], fmin(v[5], v[8]));
+    r.bb[3] = (float)fmax(v[2], fmax(v[5], v[8]));
+    rec[b * F + f] = r;
+    r0 = r.bb[0]; r1 = r.bb[1]; r2 = r.bb[2]; r3 = r.bb[3];
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -249,71 +236,252 @@ __device__ __forceinline__ int cs_cell(float v, float v0, float inv, int G) {
   return (int)c;
 }
 
-// fill == false: count the list entries of each cell, and their total in 64 bits (the int32
-// scan below is used only when that total is < 2^31); fill == true: write them
-template <bool FILL>
+// fill == false: count the list entries of each cell, and their total in 64 bits (the grid is
+// coarsened when it passes 2^31); fill == true: write the records.  A workgroup's faces are
+// neighbours in a mesh, so their cells usually fit one LDS window: the entries are counted
+// there and each touched cell takes one global atomic per workgroup (device atomics to
+// scattered words run at ~20 per ns chip-wide, a few hundred thousand of them were the cost);
+// a workgroup whose window is larger takes one global atomic per entry.
+constexpr int kCsWin = 4096;
+template <bool FILL, typename T>
 __global__ void __launch_bounds__(256)
-    cs_bin_kernel(int64_t F, int G, const float *__restrict__ fb, const float *__restrict__ mbox,
-                  int *__restrict__ cnt, const int *__restrict__ offs, int *__restrict__ list,
+    cs_bin_kernel(int64_t F, int G, const CsRec<T> *__restrict__ rec, const float *__restrict__ mbox,
+                  int *__restrict__ cnt, const int64_t *__restrict__ offs, CsRec<T> *__restrict__ list,
                   unsigned long long *__restrict__ total) {
-  const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ int s_c[kCsWin];
+  __shared__ int s_r[4][4];
+  const int tid = threadIdx.x;
+  const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * 256 + tid;
   int cy0 = 0, cy1 = -1, cz0 = 0, cz1 = -1;
+  CsRec<T> r;
   if (f < F) {
-    const float *bb = fb + (b * F + f) * 4;
-    const float y0 = bb[0], y1 = bb[1], z0 = bb[2], z1 = bb[3];
-    if (y0 <= y1 && z0 <= z1) {  // NaN bounds never pass bbox_check
+    const float4 bb = *reinterpret_cast<const float4 *>(rec[b * F + f].bb);
+    if (FILL) r = rec[b * F + f];
+    if (bb.x <= bb.y && bb.z <= bb.w) {  // NaN bounds never pass bbox_check
       const float *m = mbox + b * 8;
-      cy0 = cs_cell(y0, m[0], m[4], G);
-      cy1 = cs_cell(y1, m[0], m[4], G);
-      cz0 = cs_cell(z0, m[2], m[5], G);
-      cz1 = cs_cell(z1, m[2], m[5], G);
+      cy0 = cs_cell(bb.x, m[0], m[4], G);
+      cy1 = cs_cell(bb.y, m[0], m[4], G);
+      cz0 = cs_cell(bb.z, m[2], m[5], G);
+      cz1 = cs_cell(bb.w, m[2], m[5], G);
     }
   }
   if (!FILL) wave_add_u64(total, (unsigned long long)(cy1 - cy0 + 1) * (unsigned long long)(cz1 - cz0 + 1));
-  int *c = cnt + b * (int64_t)G * G;
+  // the workgroup's cell window
+  const bool any = cy1 >= cy0;
+  int w0 = any ? cy0 : INT_MAX, w1 = any ? cy1 : INT_MIN, w2 = any ? cz0 : INT_MAX, w3 = any ? cz1 : INT_MIN;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    w0 = min(w0, __shfl_xor(w0, o));
+    w1 = max(w1, __shfl_xor(w1, o));
+    w2 = min(w2, __shfl_xor(w2, o));
+    w3 = max(w3, __shfl_xor(w3, o));
+  }
+  if ((tid & 63) == 0) {
+    s_r[tid >> 6][0] = w0; s_r[tid >> 6][1] = w1; s_r[tid >> 6][2] = w2; s_r[tid >> 6][3] = w3;
+  }
+  __syncthreads();
+  w0 = min(min(s_r[0][0], s_r[1][0]), min(s_r[2][0], s_r[3][0]));
+  w1 = max(max(s_r[0][1], s_r[1][1]), max(s_r[2][1], s_r[3][1]));
+  w2 = min(min(s_r[0][2], s_r[1][2]), min(s_r[2][2], s_r[3][2]));
+  w3 = max(max(s_r[0][3], s_r[1][3]), max(s_r[2][3], s_r[3][3]));
+  if (w1 < w0) return;  // no face of the workgroup is listed (uniform)
+  const int64_t base = b * (int64_t)G * G;
+  const int ww = w1 - w0 + 1;
+  const int64_t area = (int64_t)ww * (w3 - w2 + 1);
+  if (area > kCsWin) {
+    for (int cz = cz0; cz <= cz1; cz++)
+      for (int cy = cy0; cy <= cy1; cy++) {
+        const int64_t cell = base + (int64_t)cz * G + cy;
+        if (FILL) {
+          const int slot = atomicAdd(cnt + cell, 1);
+          list[offs[cell] + slot] = r;
+        } else {
+          atomicAdd(cnt + cell, 1);
+        }
+      }
+    return;
+  }
+  const int na = (int)area;
+  for (int i = tid; i < na; i += 256) s_c[i] = 0;
+  __syncthreads();
+  for (int cz = cz0; cz <= cz1; cz++)
+    for (int cy = cy0; cy <= cy1; cy++) atomicAdd(s_c + (cz - w2) * ww + (cy - w0), 1);
+  __syncthreads();
+  for (int i = tid; i < na; i += 256) {
+    const int c = s_c[i];
+    if (!c) continue;
+    const int64_t cell = base + (int64_t)(w2 + i / ww) * G + (w0 + i % ww);
+    if (FILL)
+      s_c[i] = atomicAdd(cnt + cell, c);  // the workgroup's first slot in the cell
+    else
+      atomicAdd(cnt + cell, c);
+  }
+  if (!FILL) return;
+  __syncthreads();
   for (int cz = cz0; cz <= cz1; cz++)
     for (int cy = cy0; cy <= cy1; cy++) {
-      const int64_t cell = (int64_t)cz * G + cy;
-      const int slot = atomicAdd(c + cell, 1);
-      if (FILL) list[offs[b * (int64_t)G * G + cell] + slot] = (int)f;
+      const int slot = atomicAdd(s_c + (cz - w2) * ww + (cy - w0), 1);
+      list[offs[base + (int64_t)cz * G + cy] + slot] = r;
     }
 }
 
-// one lane per point (Morton order through perm): walk the point's cell list
+// a point's normalised coordinates (check_sign.py:146: points / maxlen)
 template <typename T>
-__global__ void __launch_bounds__(256)
-    cs_grid_check_kernel(int64_t P, int64_t F, int G, const T *__restrict__ points, const T *__restrict__ maxlen,
-                         const int32_t *__restrict__ perm, const float *__restrict__ mbox, const int *__restrict__ cnt,
-                         const int *__restrict__ offs, const int *__restrict__ list, const T *__restrict__ fc,
-                         const float *__restrict__ fb, T *__restrict__ counts, uint8_t *__restrict__ contains) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t b = blockIdx.y;
-  if (i >= P) return;
-  const int64_t p = perm ? (int64_t)perm[b * P + i] : i;
-  const int64_t row = b * P + p;
-  T qx = points[row * 3 + 0], qy = points[row * 3 + 1], qz = points[row * 3 + 2];
+__device__ __forceinline__ void cs_load_point(const T *__restrict__ points, const T *__restrict__ maxlen, int64_t b,
+                                              int64_t row, T *q) {
+  q[0] = points[row * 3 + 0]; q[1] = points[row * 3 + 1]; q[2] = points[row * 3 + 2];
   if (maxlen) {
     const T m = maxlen[b];
-    qx = qx / m; qy = qy / m; qz = qz / m;
+    q[0] = q[0] / m; q[1] = q[1] / m; q[2] = q[2] / m;
   }
+}
+
+// inside the union of the face bounds (a point outside it, or NaN, passes no bbox_check)
+template <typename T>
+__device__ __forceinline__ bool cs_in_box(const T *q, const float *mb) {
+  return q[1] >= (T)mb[0] && q[1] <= (T)mb[1] && q[2] >= (T)mb[2] && q[2] <= (T)mb[3];
+}
+template <typename T>
+__device__ __forceinline__ int cs_point_cell(const T *q, const float *mb, int G) {
+  return cs_cell((float)q[2], mb[2], mb[5], G) * G + cs_cell((float)q[1], mb[0], mb[4], G);
+}
+
+// Counting sort of the points by cell, pass 1: each in-box point takes a slot in its cell;
+// the others are answered here (no crossing).
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cs_pcount_kernel(int64_t P, int G, const T *__restrict__ points, const T *__restrict__ maxlen,
+                     const float *__restrict__ mbox, int *__restrict__ pcnt, int32_t *__restrict__ pslot,
+                     T *__restrict__ counts, uint8_t *__restrict__ contains) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (i >= P) return;
+  const int64_t row = b * P + i;
+  T q[3];
+  cs_load_point(points, maxlen, b, row, q);
   const float *mb = mbox + b * 8;
+  int slot = -1;
+  if (cs_in_box(q, mb)) {
+    slot = atomicAdd(pcnt + b * (int64_t)G * G + cs_point_cell(q, mb, G), 1);
+  } else {
+    if (counts) counts[row] = (T)0;
+    if (contains) contains[row] = 0;
+  }
+  pslot[row] = slot;
+}
+
+// pass 2: the in-box points to their cell-ordered places.  poffs: per cell, the scan of the
+// point counts (offset by poffs[0], the face list total that precedes them in the same scan).
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cs_pscatter_kernel(int64_t P, int G, const T *__restrict__ points, const T *__restrict__ maxlen,
+                       const float *__restrict__ mbox, const int32_t *__restrict__ pslot,
+                       const int64_t *__restrict__ poffs, CsPt<T> *__restrict__ sorted) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (i >= P) return;
+  const int64_t row = b * P + i;
+  const int slot = pslot[row];
+  if (slot < 0) return;
+  CsPt<T> pt;
+  cs_load_point(points, maxlen, b, row, pt.q);
+  const int64_t cell = b * (int64_t)G * G + cs_point_cell(pt.q, mbox + b * 8, G);
+  pt.p = (int32_t)i;
+  sorted[poffs[cell] - poffs[0] + slot] = pt;
+}
+
+// (dev flag 1 << 25) one lane per point in input order: walk the point's cell list, eight
+// records' bounds loaded together, the corners only of the faces whose bounds hold the point
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cs_grid_check_kernel(int64_t P, int G, const T *__restrict__ points, const T *__restrict__ maxlen,
+                         const float *__restrict__ mbox, const int *__restrict__ cnt, const int64_t *__restrict__ offs,
+                         const CsRec<T> *__restrict__ list, T *__restrict__ counts, uint8_t *__restrict__ contains) {
+  const int64_t b = blockIdx.y, GG = (int64_t)G * G;
+  const float *mb = mbox + b * 8;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= P) return;
+  const int64_t row = b * P + i;
+  T q[3];
+  cs_load_point(points, maxlen, b, row, q);
   int count = 0;
-  // outside the union of the face bounds (or NaN): no face passes bbox_check
-  if (qy >= (T)mb[0] && qy <= (T)mb[1] && qz >= (T)mb[2] && qz <= (T)mb[3]) {
-    const int cy = cs_cell((float)qy, mb[0], mb[4], G), cz = cs_cell((float)qz, mb[2], mb[5], G);
-    const int64_t cell = b * (int64_t)G * G + (int64_t)cz * G + cy;
-    const int n = cnt[cell], o = offs[cell];
-    for (int k = 0; k < n; k++) {
-      const int64_t f = b * F + list[o + k];
-      const T *v = fc + f * 9;
-      const T p1[3] = {v[0], v[1], v[2]}, p2[3] = {v[3], v[4], v[5]}, p3[3] = {v[6], v[7], v[8]};
-      const float *bb = fb + f * 4;
-      const float bbj[4] = {bb[0], bb[1], bb[2], bb[3]};
-      count += cs_cross(qx, qy, qz, p1, p2, p3, bbj);
+  if (cs_in_box(q, mb)) {
+    const int64_t cell = b * GG + cs_point_cell(q, mb, G);
+    const int n = cnt[cell];
+    const CsRec<T> *L = list + offs[cell];
+    const T qx = q[0], qy = q[1], qz = q[2];
+    for (int k0 = 0; k0 < n; k0 += 8) {
+      float4 bb[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        bb[u] = (k0 + u < n) ? *reinterpret_cast<const float4 *>(L[k0 + u].bb)
+                             : make_float4(INFINITY, -INFINITY, INFINITY, -INFINITY);
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const float b4[4] = {bb[u].x, bb[u].y, bb[u].z, bb[u].w};
+        if (qy < (T)b4[0] || (T)b4[1] < qy || qz < (T)b4[2] || (T)b4[3] < qz) continue;
+        const T *v = L[k0 + u].p;
+        const T p1[3] = {v[0], v[1], v[2]}, p2[3] = {v[3], v[4], v[5]}, p3[3] = {v[6], v[7], v[8]};
+        count += cs_cross(qx, qy, qz, p1, p2, p3, b4);
+      }
     }
   }
   if (counts) counts[row] = (T)count;
   if (contains) contains[row] = (uint8_t)(count & 1);
+}
+
+// One wave per cell: the cell's points (cell order, 64 a pass) against the cell's list.  The
+// list is staged through LDS 64 records at a time -- one coalesced load per lane, so a long
+// list costs one memory round trip per 64 faces -- and every lane then reads the same record
+// (an LDS broadcast).  Per-lane gathers of records, or scalar loads of them, measured 1.1-1.8x
+// slower.
+constexpr int kCsStage = 64;
+__device__ __forceinline__ void cs_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cs_cell_check_kernel(int64_t ncells, int64_t P, int64_t GG, const int64_t *__restrict__ poffs,
+                         const CsPt<T> *__restrict__ sorted, const int *__restrict__ cnt,
+                         const int64_t *__restrict__ offs, const CsRec<T> *__restrict__ list, T *__restrict__ counts,
+                         uint8_t *__restrict__ contains) {
+  __shared__ CsRec<T> s_rec[4][kCsStage];
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t c = (int64_t)blockIdx.x * 4 + w;
+  if (c >= ncells) return;
+  const int64_t np = poffs[c + 1] - poffs[c];
+  if (np == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t s0 = poffs[c] - poffs[0], b = c / GG;
+  const int n = cnt[c];
+  const CsRec<T> *L = list + offs[c];
+  CsRec<T> *S = s_rec[w];
+  for (int64_t p0 = 0; p0 < np; p0 += 64) {
+    const bool act = p0 + lane < np;
+    T qx = (T)INFINITY, qy = (T)INFINITY, qz = (T)INFINITY;  // an idle lane passes no bbox_check
+    int32_t p = 0;
+    if (act) {
+      const CsPt<T> pt = sorted[s0 + p0 + lane];
+      qx = pt.q[0]; qy = pt.q[1]; qz = pt.q[2];
+      p = pt.p;
+    }
+    int count = 0;
+    for (int k0 = 0; k0 < n; k0 += kCsStage) {
+      const int m = min(kCsStage, n - k0);
+      cs_wave_sync();  // the previous chunk's reads are done
+      if (lane < m) S[lane] = L[k0 + lane];
+      cs_wave_sync();
+      for (int j = 0; j < m; j++) {
+        const CsRec<T> r = S[j];
+        count += cs_cross(qx, qy, qz, r.p, r.p + 3, r.p + 6, r.bb);
+      }
+    }
+    if (act) {
+      const int64_t row = b * P + p;
+      if (counts) counts[row] = (T)count;
+      if (contains) contains[row] = (uint8_t)(count & 1);
+    }
+  }
 }
 
 static int cs_grid_dim(int64_t F) {
@@ -322,10 +490,16 @@ static int cs_grid_dim(int64_t F) {
   return G;
 }
 
+struct CsToI64 {
+  __host__ __device__ int64_t operator()(int v) const { return (int64_t)v; }
+};
+using CsCountIt = hipcub::TransformInputIterator<int64_t, CsToI64, const int *>;
+
 // workspace layout of the batched entry (byte offsets, 256-aligned); the face lists come from
-// the allocator callback once their total is known
+// the allocator callback once their total is known.  cnt / offs: [face counts per cell |
+// point counts per cell | 0] and their exclusive scan in 64 bits.
 struct CsWs {
-  size_t keys_in, keys_out, vals_in, vals_out, tbox, mbox, ctl, fc, fb, cnt, offs, temp, temp_bytes, total;
+  size_t pslot, sorted, tbox, mbox, ctl, rec, cnt, offs, macc, morg, mlen, temp, temp_bytes, list, list_cap, total;
   int G;
 };
 static size_t cs_align(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -333,28 +507,51 @@ static CsWs cs_ws_layout(int64_t B, int64_t F, int64_t P, size_t tsize) {
   CsWs w{};
   w.G = cs_grid_dim(F);
   const int64_t cells = B * (int64_t)w.G * w.G;
-  size_t t1 = 0, t2 = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t1, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                           (const int32_t *)nullptr, (int32_t *)nullptr, (int)(P > 0 ? P : 1));
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t2, (const int *)nullptr, (int *)nullptr, (int)cells);
+  size_t t1 = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, CsCountIt((const int *)nullptr, CsToI64()), (int64_t *)nullptr,
+                                         (int)(2 * cells + 1));
+  const size_t psz = tsize == 8 ? sizeof(CsPt<double>) : sizeof(CsPt<float>);
+  const size_t rsz = tsize == 8 ? sizeof(CsRec<double>) : sizeof(CsRec<float>);
   size_t o = 0;
-  w.keys_in = o; o += cs_align((size_t)(B * P) * 4);
-  w.keys_out = o; o += cs_align((size_t)(B * P) * 4);
-  w.vals_in = o; o += cs_align((size_t)(B * P) * 4);
-  w.vals_out = o; o += cs_align((size_t)(B * P) * 4);
+  w.pslot = o; o += cs_align((size_t)(B * P) * 4);
+  w.sorted = o; o += cs_align((size_t)(B * P) * psz);
   w.tbox = o; o += cs_align((size_t)(B * cdiv(F, kCsTile)) * 16);
   w.mbox = o; o += cs_align((size_t)B * 32);
   w.ctl = o; o += cs_align(16);  // u64 list total, int bad-index flag
-  w.fc = o; o += cs_align((size_t)(B * F) * 9 * tsize);
-  w.fb = o; o += cs_align((size_t)(B * F) * 16);
-  w.cnt = o; o += cs_align((size_t)cells * 4);
-  w.offs = o; o += cs_align((size_t)cells * 4);
-  w.temp = o; w.temp_bytes = cs_align(t1 > t2 ? t1 : (t2 > 0 ? t2 : 1)); o += w.temp_bytes;
+  w.rec = o; o += cs_align((size_t)(B * F) * rsz);
+  w.cnt = o; o += cs_align((size_t)(2 * cells + 1) * 4);
+  w.offs = o; o += cs_align((size_t)(2 * cells + 1) * 8);
+  w.macc = o; o += cs_align((size_t)B * 9 * 8);  // maxlen from the vertices (kl_voxelgrid_bounds)
+  w.morg = o; o += cs_align((size_t)B * 3 * tsize);
+  w.mlen = o; o += cs_align((size_t)B * tsize);
+  w.temp = o; w.temp_bytes = cs_align(t1 > 0 ? t1 : 1); o += w.temp_bytes;
+  // room for 16 list entries per face (up to 256 MiB), so that a typical mesh's lists need no
+  // allocator call (a host round trip); longer lists come from the callback
+  w.list = o; w.list_cap = std::min<size_t>((size_t)(16 * B * F), ((size_t)256 << 20) / rsz); o += w.list_cap * rsz;
   w.total = o;
   return w;
 }
 
-// counts (B,P) in T (the _C contract) and/or contains (B,P) bool bytes
+struct CsCtl {
+  unsigned long long total;
+  int bad, pad;
+};
+// pinned, so that the list-total read is one small DMA (one per host thread)
+static CsCtl *cs_host_ctl() {
+  thread_local CsCtl *p = nullptr;
+  thread_local bool tried = false;
+  if (!tried) {
+    tried = true;
+    if (hipHostMalloc((void **)&p, sizeof(CsCtl), hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+    }
+  }
+  return p;
+}
+
+// counts (B,P) in T (the _C contract) and/or contains (B,P) bool bytes.  The batched entry with
+// maxlen == null takes check_sign.py:140-146's maxlen from the vertices on the device.
 template <typename T>
 static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, const CsFaces<T> &src,
                            const void *maxlen, void *counts, uint8_t *contains, void *ws, size_t ws_bytes,
@@ -370,68 +567,88 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   KL_REQUIRE(alloc != nullptr, "check_sign: allocator callback required");
   int G = L.G;
   uint8_t *w = (uint8_t *)ws;
-  uint32_t *kin = (uint32_t *)(w + L.keys_in), *kout = (uint32_t *)(w + L.keys_out);
-  int32_t *vin = (int32_t *)(w + L.vals_in), *vout = (int32_t *)(w + L.vals_out);
-  float *tbox = (float *)(w + L.tbox), *mbox = (float *)(w + L.mbox), *fb = (float *)(w + L.fb);
-  T *fc = (T *)(w + L.fc);
-  int *cnt = (int *)(w + L.cnt), *offs = (int *)(w + L.offs);
+  int32_t *pslot = (int32_t *)(w + L.pslot);
+  CsPt<T> *sorted = (CsPt<T> *)(w + L.sorted);
+  float *tbox = (float *)(w + L.tbox), *mbox = (float *)(w + L.mbox);
+  CsRec<T> *rec = (CsRec<T> *)(w + L.rec);
+  int *cnt = (int *)(w + L.cnt);
+  int64_t *offs = (int64_t *)(w + L.offs);
   unsigned long long *d_total = (unsigned long long *)(w + L.ctl);
   CsFaces<T> fsrc = src;
   fsrc.bad = (int *)(w + L.ctl + 8);
+  const T *ml = (const T *)maxlen;
+  if (src.faces && !maxlen) {
+    KL_REQUIRE(src.V > 0, "check_sign: verts has no vertices");
+    T *mlen = (T *)(w + L.mlen);
+    KL_CHECK_RC(kl_voxelgrid_bounds(sizeof(T) == 8 ? KL_F64 : KL_F32, (int)B, src.V, src.verts, w + L.morg, mlen,
+                                    w + L.macc, (size_t)B * 9 * 8, (kl_stream)st));
+    ml = mlen;
+  }
+  if (src.faces) fsrc.maxlen = ml;
   const int64_t ntiles = cdiv(F, kCsTile);
+  // (dev flag 1 << 25: points in input order, no counting sort)
+  const bool sort_points = !(g_dev_flags & (1 << 25));
   KL_CHECK_RC(fill_async(w + L.ctl, 0, 16, st));
-  hipLaunchKernelGGL(cs_prep_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kCsTile), 0, st, F, fsrc, fc, fb,
+  hipLaunchKernelGGL(cs_prep_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kCsTile), 0, st, F, fsrc, rec,
                      tbox);
   KL_CHECK_LAUNCH();
-  const dim3 fgrid((unsigned)cdiv(F, 256), (unsigned)B);
-  // The list total is F * (cells per face); many large faces can take it past the int32 scan.
+  const dim3 fgrid((unsigned)cdiv(F, 256), (unsigned)B), pgrid((unsigned)cdiv(P, 256), (unsigned)B);
+  // The list total is F * (cells per face); many large faces can take it past 2^31 entries.
   // Then the grid is coarsened (G = 1 lists every face once: total <= F < 2^31).
-  struct {
-    unsigned long long total;
-    int bad, pad;
-  } ctl{};
+  CsCtl local{}, *ctl = cs_host_ctl();
+  if (!ctl) ctl = &local;
   for (;;) {
+    const int64_t ncells = B * (int64_t)G * G;
     hipLaunchKernelGGL(cs_meshbox_kernel, dim3((unsigned)B), dim3(256), 0, st, ntiles, G, (const float *)tbox, mbox);
     KL_CHECK_LAUNCH();
-    KL_CHECK_RC(fill_async(cnt, 0, (size_t)B * G * G * 4, st));
-    hipLaunchKernelGGL(cs_bin_kernel<false>, fgrid, dim3(256), 0, st, F, G, (const float *)fb, (const float *)mbox,
-                       cnt, (const int *)nullptr, (int *)nullptr, d_total);
+    KL_CHECK_RC(fill_async(cnt, 0, (size_t)(2 * ncells + 1) * 4, st));
+    hipLaunchKernelGGL((cs_bin_kernel<false, T>), fgrid, dim3(256), 0, st, F, G, (const CsRec<T> *)rec,
+                       (const float *)mbox, cnt, (const int64_t *)nullptr, (CsRec<T> *)nullptr, d_total);
     KL_CHECK_LAUNCH();
-    KL_CHECK_HIP(hipMemcpyAsync(&ctl, d_total, 16, hipMemcpyDeviceToHost, st));
+    if (sort_points) {
+      hipLaunchKernelGGL(cs_pcount_kernel<T>, pgrid, dim3(256), 0, st, P, G, (const T *)points, ml,
+                         (const float *)mbox, cnt + ncells, pslot, (T *)counts, contains);
+      KL_CHECK_LAUNCH();
+    }
+    KL_CHECK_HIP(hipMemcpyAsync(ctl, d_total, 16, hipMemcpyDeviceToHost, st));
     KL_CHECK_HIP(hipStreamSynchronize(st));
-    KL_REQUIRE(!ctl.bad, "check_sign: index out of range in self (a face index is outside [0, num_vertices))");
+    KL_REQUIRE(!ctl->bad, "check_sign: index out of range in self (a face index is outside [0, num_vertices))");
     // (dev flag 1 << 24: a 2^10 cap, so that tests reach the coarsening on small meshes)
     const unsigned long long cap = (g_dev_flags & (1 << 24)) ? (1ull << 10) : (1ull << 31);
-    if (ctl.total < cap || G == 1) break;
+    if (ctl->total < cap || G == 1) break;
     G = G / 2 > 1 ? G / 2 : 1;
     KL_CHECK_RC(fill_async(d_total, 0, 8, st));
   }
-  const int64_t total = (int64_t)ctl.total;
+  const int64_t total = (int64_t)ctl->total;
   KL_REQUIRE(total < ((int64_t)1 << 31), "check_sign: face lists too long");
   const int64_t ncells = B * (int64_t)G * G;
   size_t tb = L.temp_bytes;
-  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, cnt, offs, (int)ncells, st));
-  int *list = (int *)alloc(alloc_ctx, (size_t)(total > 0 ? total : 1) * 4);
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, CsCountIt(cnt, CsToI64()), offs, (int)(2 * ncells + 1),
+                                                st));
+  CsRec<T> *list = (size_t)total <= L.list_cap
+                       ? (CsRec<T> *)(w + L.list)
+                       : (CsRec<T> *)alloc(alloc_ctx, (size_t)(total > 0 ? total : 1) * sizeof(CsRec<T>));
   if (!list) {
     set_error("check_sign: allocator returned NULL");
     return KL_E_ALLOC;
   }
   KL_CHECK_RC(fill_async(cnt, 0, (size_t)ncells * 4, st));
-  hipLaunchKernelGGL(cs_bin_kernel<true>, fgrid, dim3(256), 0, st, F, G, (const float *)fb, (const float *)mbox, cnt,
-                     (const int *)offs, list, (unsigned long long *)nullptr);
+  hipLaunchKernelGGL((cs_bin_kernel<true, T>), fgrid, dim3(256), 0, st, F, G, (const CsRec<T> *)rec,
+                     (const float *)mbox, cnt, (const int64_t *)offs, list, (unsigned long long *)nullptr);
   KL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(cs_key_kernel<T>, dim3((unsigned)cdiv(B * P, 256)), dim3(256), 0, st, B * P, P,
-                     (const T *)points, kin, vin);
-  KL_CHECK_LAUNCH();
-  for (int64_t b = 0; b < B; b++) {  // each mesh's points sorted on their own
-    size_t ts = L.temp_bytes;
-    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(w + L.temp, ts, kin + b * P, kout + b * P, vin + b * P,
-                                                    vout + b * P, (int)P, 0, 32, st));
+  if (sort_points) {
+    hipLaunchKernelGGL(cs_pscatter_kernel<T>, pgrid, dim3(256), 0, st, P, G, (const T *)points, ml,
+                       (const float *)mbox, (const int32_t *)pslot, (const int64_t *)(offs + ncells), sorted);
+    KL_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(cs_grid_check_kernel<T>, dim3((unsigned)cdiv(P, 256), (unsigned)B), dim3(256), 0, st, P, F, G,
-                     (const T *)points, (const T *)maxlen, (const int32_t *)vout, (const float *)mbox,
-                     (const int *)cnt, (const int *)offs, (const int *)list, (const T *)fc, (const float *)fb,
-                     (T *)counts, contains);
+  if (sort_points)
+    hipLaunchKernelGGL(cs_cell_check_kernel<T>, dim3((unsigned)cdiv(ncells, 4)), dim3(256), 0, st, ncells, P,
+                       (int64_t)G * G, (const int64_t *)(offs + ncells), (const CsPt<T> *)sorted, (const int *)cnt,
+                       (const int64_t *)offs, (const CsRec<T> *)list, (T *)counts, contains);
+  else
+    hipLaunchKernelGGL(cs_grid_check_kernel<T>, pgrid, dim3(256), 0, st, P, G, (const T *)points, ml,
+                       (const float *)mbox, (const int *)cnt, (const int64_t *)offs, (const CsRec<T> *)list,
+                       (T *)counts, contains);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

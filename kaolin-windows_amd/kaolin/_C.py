@@ -400,7 +400,8 @@ def unbatched_mesh_intersection_cuda(points, verts_1, verts_2, verts_3):
 
 def check_sign_batched(verts, faces, points, maxlen):
     """check_sign.py:140-154 for the whole batch in one launch (not a reference _C name):
-    contains (B,P) bool, faces gathered and 1 / maxlen applied in-kernel."""
+    contains (B,P) bool, faces gathered and 1 / maxlen applied in-kernel (maxlen None: taken
+    from the vertices on the device)."""
     func = 'check_sign'
     B, V = verts.shape[:2]
     F, P = faces.shape[0], points.shape[1]

@@ -59,8 +59,12 @@ def check_sign(verts, faces, points, hash_resolution=512):
     if verts.dtype not in (torch.float32, torch.float64) or points.dtype != verts.dtype:
         raise RuntimeError(f'check_sign: expected float or double verts and points of the same dtype, '
                            f'got {verts.dtype} and {points.dtype}')
-    # check_sign.py:140-146: the largest bbox extent of each mesh
-    vmax = verts.max(dim=1)[0]
-    vmin = verts.min(dim=1)[0]
-    maxlen = (vmax - vmin).max(dim=1)[0].contiguous()
+    # check_sign.py:140-146: the largest bbox extent of each mesh, taken by the library on the
+    # device (kl_voxelgrid_bounds: exact min / max, NaN propagated as torch's reductions do);
+    # torch's reductions only for a mesh without vertices, where they raise as the reference's
+    maxlen = None
+    if verts.shape[1] == 0:
+        vmax = verts.max(dim=1)[0]
+        vmin = verts.min(dim=1)[0]
+        maxlen = (vmax - vmin).max(dim=1)[0].contiguous()
     return _C.check_sign_batched(verts.contiguous(), faces.contiguous(), points.contiguous(), maxlen)

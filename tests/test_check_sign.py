@@ -176,3 +176,26 @@ def test_gpu_face_index_out_of_range_raises(kal, bad):
     pts = np.zeros((1, 10, 3), np.float32)
     with pytest.raises(RuntimeError, match='index out of range'):
         kal.ops.mesh.check_sign(_T(verts[None].astype(np.float32)), _T(faces), _T(pts))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [np.float32, np.float64])
+def test_gpu_batch_nan_and_outside_points(kal, dtype):
+    """maxlen taken on the device (check_sign.py:140-146, NaN propagated as torch's max / min):
+    a NaN vertex that no face uses still makes its mesh's maxlen NaN (every point outside);
+    NaN points, points outside the face box, duplicated points (one cell gets many) and a point
+    count that is not a multiple of the workgroup -- every answer as the oracle's."""
+    verts, faces = _uv_sphere(10, 14, 0.7)
+    verts = np.concatenate([verts, np.zeros((1, 3))]).astype(dtype)
+    rng = np.random.default_rng(11)
+    P = 1237
+    pts = rng.uniform(-1.5, 1.5, (3, P, 3)).astype(dtype)
+    pts[0, :50] = np.nan
+    pts[1, 100:400] = pts[1, 99]
+    pts[2, :30, 1] = np.inf
+    vb = np.stack([verts, verts * dtype(0.5), verts + dtype(0.2)])
+    vb[1, -1, 2] = np.nan
+    out = kal.ops.mesh.check_sign(_T(vb), _T(faces), _T(pts)).cpu().numpy()
+    ref = orc.check_sign(vb, faces, pts)
+    np.testing.assert_array_equal(out, ref)
+    assert not out[1].any() and out[0].any() and out[2].any()
