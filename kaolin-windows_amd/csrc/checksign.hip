@@ -265,7 +265,8 @@ __global__ void __launch_bounds__(256)
       cz1 = cs_cell(bb.w, m[2], m[5], G);
     }
   }
-  if (!FILL) wave_add_u64(total, (unsigned long long)(cy1 - cy0 + 1) * (unsigned long long)(cz1 - cz0 + 1));
+  __shared__ unsigned long long s_t[4];
+  if (!FILL) block_add_u64(total, (unsigned long long)(cy1 - cy0 + 1) * (unsigned long long)(cz1 - cz0 + 1), s_t);
   // the workgroup's cell window
   const bool any = cy1 >= cy0;
   int w0 = any ? cy0 : INT_MAX, w1 = any ? cy1 : INT_MIN, w2 = any ? cz0 : INT_MAX, w3 = any ? cz1 : INT_MIN;
@@ -428,12 +429,40 @@ __global__ void __launch_bounds__(256)
   if (contains) contains[row] = (uint8_t)(count & 1);
 }
 
-// One wave per cell: the cell's points (cell order, 64 a pass) against the cell's list.  The
-// list is staged through LDS 64 records at a time -- one coalesced load per lane, so a long
-// list costs one memory round trip per 64 faces -- and every lane then reads the same record
-// (an LDS broadcast).  Per-lane gathers of records, or scalar loads of them, measured 1.1-1.8x
-// slower.
+// Work units of the cell check: a cell with points takes one unit per 64 records of its list
+// (at least one), so that no wave walks a long list alone (a few cells of the bench's sphere
+// hold ~350 faces: walking them took half the check's time).  ucnt per cell, their total in
+// ctl.
 constexpr int kCsStage = 64;
+__global__ void __launch_bounds__(256)
+    cs_units_kernel(int64_t ncells, const int *__restrict__ cnt, int *__restrict__ ucnt,
+                    unsigned long long *__restrict__ units) {
+  __shared__ unsigned long long s_t[4];
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int u = 0;
+  if (c < ncells) {
+    u = cnt[ncells + c] > 0 ? max(1, (cnt[c] + kCsStage - 1) / kCsStage) : 0;
+    ucnt[c] = u;
+  }
+  block_add_u64(units, (unsigned long long)u, s_t);
+}
+// unit -> cell (uoffs: the units' scan, offset by uoffs[0])
+__global__ void __launch_bounds__(256)
+    cs_unitmap_kernel(int64_t ncells, const int *__restrict__ ucnt, const int64_t *__restrict__ uoffs,
+                      int64_t *__restrict__ unit_cell) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= ncells) return;
+  const int u = ucnt[c];
+  const int64_t o = uoffs[c] - uoffs[0];
+  for (int s = 0; s < u; s++) unit_cell[o + s] = c;
+}
+
+// One wave per unit: the cell's points (cell order, 64 a pass) against the unit's <= 64
+// records, staged through LDS with one coalesced load per lane; every lane then reads the same
+// record (an LDS broadcast).  Per-lane gathers of records, or scalar loads of them, measured
+// 1.1-1.8x slower; two cells per wave (fewer idle lanes) 1.15x slower.  A one-unit cell writes
+// its points' answers; the units of a longer list add their counts into acc, answered by
+// cs_finalize_kernel.
 __device__ __forceinline__ void cs_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -441,21 +470,27 @@ __device__ __forceinline__ void cs_wave_sync() {
 }
 template <typename T>
 __global__ void __launch_bounds__(256)
-    cs_cell_check_kernel(int64_t ncells, int64_t P, int64_t GG, const int64_t *__restrict__ poffs,
-                         const CsPt<T> *__restrict__ sorted, const int *__restrict__ cnt,
-                         const int64_t *__restrict__ offs, const CsRec<T> *__restrict__ list, T *__restrict__ counts,
+    cs_cell_check_kernel(int64_t nunits, int64_t P, int64_t GG, const int64_t *__restrict__ unit_cell,
+                         const int64_t *__restrict__ uoffs, const int *__restrict__ ucnt,
+                         const int64_t *__restrict__ poffs, const CsPt<T> *__restrict__ sorted,
+                         const int *__restrict__ cnt, const int64_t *__restrict__ offs,
+                         const CsRec<T> *__restrict__ list, int *__restrict__ acc, T *__restrict__ counts,
                          uint8_t *__restrict__ contains) {
   __shared__ CsRec<T> s_rec[4][kCsStage];
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t c = (int64_t)blockIdx.x * 4 + w;
-  if (c >= ncells) return;
+  const int64_t u = (int64_t)blockIdx.x * 4 + w;
+  if (u >= nunits) return;
+  const int64_t c = unit_cell[u];
+  const int seg = (int)(u - (uoffs[c] - uoffs[0]));
+  const bool whole = ucnt[c] == 1;
   const int64_t np = poffs[c + 1] - poffs[c];
-  if (np == 0) return;
   const int lane = threadIdx.x & 63;
   const int64_t s0 = poffs[c] - poffs[0], b = c / GG;
-  const int n = cnt[c];
-  const CsRec<T> *L = list + offs[c];
+  const int k0 = seg * kCsStage, m = min(kCsStage, cnt[c] - k0);
+  const CsRec<T> *L = list + offs[c] + k0;
   CsRec<T> *S = s_rec[w];
+  if (lane < m) S[lane] = L[lane];
+  cs_wave_sync();
   for (int64_t p0 = 0; p0 < np; p0 += 64) {
     const bool act = p0 + lane < np;
     T qx = (T)INFINITY, qy = (T)INFINITY, qz = (T)INFINITY;  // an idle lane passes no bbox_check
@@ -466,22 +501,38 @@ __global__ void __launch_bounds__(256)
       p = pt.p;
     }
     int count = 0;
-    for (int k0 = 0; k0 < n; k0 += kCsStage) {
-      const int m = min(kCsStage, n - k0);
-      cs_wave_sync();  // the previous chunk's reads are done
-      if (lane < m) S[lane] = L[k0 + lane];
-      cs_wave_sync();
-      for (int j = 0; j < m; j++) {
-        const CsRec<T> r = S[j];
-        count += cs_cross(qx, qy, qz, r.p, r.p + 3, r.p + 6, r.bb);
-      }
+    for (int j = 0; j < m; j++) {
+      const CsRec<T> r = S[j];
+      count += cs_cross(qx, qy, qz, r.p, r.p + 3, r.p + 6, r.bb);
     }
     if (act) {
       const int64_t row = b * P + p;
-      if (counts) counts[row] = (T)count;
-      if (contains) contains[row] = (uint8_t)(count & 1);
+      if (whole) {
+        if (counts) counts[row] = (T)count;
+        if (contains) contains[row] = (uint8_t)(count & 1);
+      } else if (count) {
+        atomicAdd(acc + row, count);
+      }
     }
   }
+}
+
+// the answers of the points of multi-unit cells (one lane per in-box point, cell order)
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cs_finalize_kernel(int64_t P, int G, const int64_t *__restrict__ poffs, const CsPt<T> *__restrict__ sorted,
+                       const float *__restrict__ mbox, const int *__restrict__ ucnt, const int *__restrict__ acc,
+                       T *__restrict__ counts, uint8_t *__restrict__ contains) {
+  const int64_t b = blockIdx.y, GG = (int64_t)G * G;
+  const int64_t s0 = poffs[b * GG] - poffs[0], s1 = poffs[(b + 1) * GG] - poffs[0];
+  const int64_t j = s0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= s1) return;
+  const CsPt<T> pt = sorted[j];
+  if (ucnt[b * GG + cs_point_cell(pt.q, mbox + b * 8, G)] <= 1) return;
+  const int64_t row = b * P + pt.p;
+  const int count = acc[row];
+  if (counts) counts[row] = (T)count;
+  if (contains) contains[row] = (uint8_t)(count & 1);
 }
 
 static int cs_grid_dim(int64_t F) {
@@ -497,9 +548,9 @@ using CsCountIt = hipcub::TransformInputIterator<int64_t, CsToI64, const int *>;
 
 // workspace layout of the batched entry (byte offsets, 256-aligned); the face lists come from
 // the allocator callback once their total is known.  cnt / offs: [face counts per cell |
-// point counts per cell | 0] and their exclusive scan in 64 bits.
+// point counts per cell | check units per cell | 0] and their exclusive scan in 64 bits.
 struct CsWs {
-  size_t pslot, sorted, tbox, mbox, ctl, rec, cnt, offs, macc, morg, mlen, temp, temp_bytes, list, list_cap, total;
+  size_t pslot, acc, sorted, tbox, mbox, ctl, rec, cnt, offs, macc, morg, mlen, temp, temp_bytes, list, list_cap, total;
   int G;
 };
 static size_t cs_align(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -509,31 +560,33 @@ static CsWs cs_ws_layout(int64_t B, int64_t F, int64_t P, size_t tsize) {
   const int64_t cells = B * (int64_t)w.G * w.G;
   size_t t1 = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t1, CsCountIt((const int *)nullptr, CsToI64()), (int64_t *)nullptr,
-                                         (int)(2 * cells + 1));
+                                         (int)(3 * cells + 1));
   const size_t psz = tsize == 8 ? sizeof(CsPt<double>) : sizeof(CsPt<float>);
   const size_t rsz = tsize == 8 ? sizeof(CsRec<double>) : sizeof(CsRec<float>);
   size_t o = 0;
   w.pslot = o; o += cs_align((size_t)(B * P) * 4);
+  w.acc = o; o += cs_align((size_t)(B * P) * 4);
   w.sorted = o; o += cs_align((size_t)(B * P) * psz);
   w.tbox = o; o += cs_align((size_t)(B * cdiv(F, kCsTile)) * 16);
   w.mbox = o; o += cs_align((size_t)B * 32);
-  w.ctl = o; o += cs_align(16);  // u64 list total, int bad-index flag
+  w.ctl = o; o += cs_align(32);  // u64 list total, u64 check units, int bad-index flag
   w.rec = o; o += cs_align((size_t)(B * F) * rsz);
-  w.cnt = o; o += cs_align((size_t)(2 * cells + 1) * 4);
-  w.offs = o; o += cs_align((size_t)(2 * cells + 1) * 8);
+  w.cnt = o; o += cs_align((size_t)(3 * cells + 1) * 4);
+  w.offs = o; o += cs_align((size_t)(3 * cells + 1) * 8);
   w.macc = o; o += cs_align((size_t)B * 9 * 8);  // maxlen from the vertices (kl_voxelgrid_bounds)
   w.morg = o; o += cs_align((size_t)B * 3 * tsize);
   w.mlen = o; o += cs_align((size_t)B * tsize);
   w.temp = o; w.temp_bytes = cs_align(t1 > 0 ? t1 : 1); o += w.temp_bytes;
-  // room for 16 list entries per face (up to 256 MiB), so that a typical mesh's lists need no
-  // allocator call (a host round trip); longer lists come from the callback
+  // room for 16 list entries per face (up to 256 MiB) and a unit per cell, so that a typical
+  // mesh's lists need no allocator call (a host round trip); longer lists come from the callback
   w.list = o; w.list_cap = std::min<size_t>((size_t)(16 * B * F), ((size_t)256 << 20) / rsz); o += w.list_cap * rsz;
+  o += cs_align((size_t)(2 * cells) * 8);
   w.total = o;
   return w;
 }
 
 struct CsCtl {
-  unsigned long long total;
+  unsigned long long total, units;
   int bad, pad;
 };
 // pinned, so that the list-total read is one small DMA (one per host thread)
@@ -575,7 +628,8 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   int64_t *offs = (int64_t *)(w + L.offs);
   unsigned long long *d_total = (unsigned long long *)(w + L.ctl);
   CsFaces<T> fsrc = src;
-  fsrc.bad = (int *)(w + L.ctl + 8);
+  fsrc.bad = (int *)(w + L.ctl + 16);
+  int *acc = (int *)(w + L.acc);
   const T *ml = (const T *)maxlen;
   if (src.faces && !maxlen) {
     KL_REQUIRE(src.V > 0, "check_sign: verts has no vertices");
@@ -588,7 +642,7 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   const int64_t ntiles = cdiv(F, kCsTile);
   // (dev flag 1 << 25: points in input order, no counting sort)
   const bool sort_points = !(g_dev_flags & (1 << 25));
-  KL_CHECK_RC(fill_async(w + L.ctl, 0, 16, st));
+  KL_CHECK_RC(fill_async(w + L.ctl, 0, 32, st));
   hipLaunchKernelGGL(cs_prep_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kCsTile), 0, st, F, fsrc, rec,
                      tbox);
   KL_CHECK_LAUNCH();
@@ -601,7 +655,7 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
     const int64_t ncells = B * (int64_t)G * G;
     hipLaunchKernelGGL(cs_meshbox_kernel, dim3((unsigned)B), dim3(256), 0, st, ntiles, G, (const float *)tbox, mbox);
     KL_CHECK_LAUNCH();
-    KL_CHECK_RC(fill_async(cnt, 0, (size_t)(2 * ncells + 1) * 4, st));
+    KL_CHECK_RC(fill_async(cnt, 0, (size_t)(3 * ncells + 1) * 4, st));
     hipLaunchKernelGGL((cs_bin_kernel<false, T>), fgrid, dim3(256), 0, st, F, G, (const CsRec<T> *)rec,
                        (const float *)mbox, cnt, (const int64_t *)nullptr, (CsRec<T> *)nullptr, d_total);
     KL_CHECK_LAUNCH();
@@ -610,45 +664,67 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
                          (const float *)mbox, cnt + ncells, pslot, (T *)counts, contains);
       KL_CHECK_LAUNCH();
     }
-    KL_CHECK_HIP(hipMemcpyAsync(ctl, d_total, 16, hipMemcpyDeviceToHost, st));
+    if (sort_points) {
+      hipLaunchKernelGGL(cs_units_kernel, dim3((unsigned)cdiv(ncells, 256)), dim3(256), 0, st, ncells,
+                         (const int *)cnt, cnt + 2 * ncells, d_total + 1);
+      KL_CHECK_LAUNCH();
+    }
+    KL_CHECK_HIP(hipMemcpyAsync(ctl, d_total, sizeof(CsCtl), hipMemcpyDeviceToHost, st));
     KL_CHECK_HIP(hipStreamSynchronize(st));
     KL_REQUIRE(!ctl->bad, "check_sign: index out of range in self (a face index is outside [0, num_vertices))");
     // (dev flag 1 << 24: a 2^10 cap, so that tests reach the coarsening on small meshes)
     const unsigned long long cap = (g_dev_flags & (1 << 24)) ? (1ull << 10) : (1ull << 31);
     if (ctl->total < cap || G == 1) break;
     G = G / 2 > 1 ? G / 2 : 1;
-    KL_CHECK_RC(fill_async(d_total, 0, 8, st));
+    KL_CHECK_RC(fill_async(d_total, 0, 16, st));
   }
   const int64_t total = (int64_t)ctl->total;
   KL_REQUIRE(total < ((int64_t)1 << 31), "check_sign: face lists too long");
   const int64_t ncells = B * (int64_t)G * G;
   size_t tb = L.temp_bytes;
-  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, CsCountIt(cnt, CsToI64()), offs, (int)(2 * ncells + 1),
+  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, CsCountIt(cnt, CsToI64()), offs, (int)(3 * ncells + 1),
                                                 st));
-  CsRec<T> *list = (size_t)total <= L.list_cap
-                       ? (CsRec<T> *)(w + L.list)
-                       : (CsRec<T> *)alloc(alloc_ctx, (size_t)(total > 0 ? total : 1) * sizeof(CsRec<T>));
-  if (!list) {
+  const int64_t nunits = sort_points ? (int64_t)ctl->units : 0;
+  // the lists, then the unit -> cell map (in the workspace when they fit: ncells + total / 64
+  // units <= 2 ncells there)
+  const size_t list_bytes = (size_t)(total > 0 ? total : 1) * sizeof(CsRec<T>);
+  uint8_t *lbuf = (size_t)total <= L.list_cap
+                      ? w + L.list
+                      : (uint8_t *)alloc(alloc_ctx, cs_align(list_bytes) + (size_t)(nunits > 0 ? nunits : 1) * 8);
+  if (!lbuf) {
     set_error("check_sign: allocator returned NULL");
     return KL_E_ALLOC;
   }
+  CsRec<T> *list = (CsRec<T> *)lbuf;
+  int64_t *unit_cell = (int64_t *)(lbuf + ((size_t)total <= L.list_cap ? L.list_cap * sizeof(CsRec<T>)
+                                                                         : cs_align(list_bytes)));
   KL_CHECK_RC(fill_async(cnt, 0, (size_t)ncells * 4, st));
   hipLaunchKernelGGL((cs_bin_kernel<true, T>), fgrid, dim3(256), 0, st, F, G, (const CsRec<T> *)rec,
                      (const float *)mbox, cnt, (const int64_t *)offs, list, (unsigned long long *)nullptr);
   KL_CHECK_LAUNCH();
   if (sort_points) {
+    const int64_t *poffs = offs + ncells, *uoffs = offs + 2 * ncells;
+    const int *ucnt = cnt + 2 * ncells;
     hipLaunchKernelGGL(cs_pscatter_kernel<T>, pgrid, dim3(256), 0, st, P, G, (const T *)points, ml,
-                       (const float *)mbox, (const int32_t *)pslot, (const int64_t *)(offs + ncells), sorted);
+                       (const float *)mbox, (const int32_t *)pslot, poffs, sorted);
     KL_CHECK_LAUNCH();
-  }
-  if (sort_points)
-    hipLaunchKernelGGL(cs_cell_check_kernel<T>, dim3((unsigned)cdiv(ncells, 4)), dim3(256), 0, st, ncells, P,
-                       (int64_t)G * G, (const int64_t *)(offs + ncells), (const CsPt<T> *)sorted, (const int *)cnt,
-                       (const int64_t *)offs, (const CsRec<T> *)list, (T *)counts, contains);
-  else
+    hipLaunchKernelGGL(cs_unitmap_kernel, dim3((unsigned)cdiv(ncells, 256)), dim3(256), 0, st, ncells, ucnt, uoffs,
+                       unit_cell);
+    KL_CHECK_LAUNCH();
+    KL_CHECK_RC(fill_async(acc, 0, (size_t)(B * P) * 4, st));
+    if (nunits > 0) {
+      hipLaunchKernelGGL(cs_cell_check_kernel<T>, dim3((unsigned)cdiv(nunits, 4)), dim3(256), 0, st, nunits, P,
+                         (int64_t)G * G, (const int64_t *)unit_cell, uoffs, ucnt, poffs, (const CsPt<T> *)sorted,
+                         (const int *)cnt, (const int64_t *)offs, (const CsRec<T> *)list, acc, (T *)counts, contains);
+      KL_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(cs_finalize_kernel<T>, pgrid, dim3(256), 0, st, P, G, poffs, (const CsPt<T> *)sorted,
+                       (const float *)mbox, ucnt, (const int *)acc, (T *)counts, contains);
+  } else {
     hipLaunchKernelGGL(cs_grid_check_kernel<T>, pgrid, dim3(256), 0, st, P, G, (const T *)points, ml,
                        (const float *)mbox, (const int *)cnt, (const int64_t *)offs, (const CsRec<T> *)list,
                        (T *)counts, contains);
+  }
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

@@ -162,6 +162,22 @@ __device__ __forceinline__ void wave_add_u64(unsigned long long *dst, unsigned l
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
 }
 
+// Adds v of every thread into *dst: wave sums, then one atomic per workgroup (one returning
+// word takes ~90 atomics per us, so a wave each from a large grid queues behind it).  Every
+// thread of the workgroup must call it (one barrier); s_w: one word of LDS per wave.
+__device__ __forceinline__ void block_add_u64(unsigned long long *dst, unsigned long long v,
+                                              unsigned long long *s_w) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < (int)((blockDim.x + 63) >> 6); w++) t += s_w[w];
+    if (t) atomicAdd(dst, t);
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T kl_exp(T x);
 template <>
