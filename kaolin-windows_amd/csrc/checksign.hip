@@ -26,6 +26,13 @@
 
 #include "common.h"
 
+#ifndef KCS_STAGE
+#define KCS_STAGE 32
+#endif
+#ifndef KCS_GROUP
+#define KCS_GROUP 32
+#endif
+
 namespace kl {
 
 constexpr int kCsTile = 256;
@@ -429,11 +436,11 @@ __global__ void __launch_bounds__(256)
   if (contains) contains[row] = (uint8_t)(count & 1);
 }
 
-// Work units of the cell check: a cell with points takes one unit per 64 records of its list
-// (at least one), so that no wave walks a long list alone (a few cells of the bench's sphere
-// hold ~350 faces: walking them took half the check's time).  ucnt per cell, their total in
-// ctl.
-constexpr int kCsStage = 64;
+// Work units of the cell check: a cell with points takes one unit per kCsStage records of its
+// list (at least one), so that no wave walks a long list alone (a few cells of the bench's
+// sphere hold ~350 faces: walking them took half the check's time).  ucnt per cell, their
+// total in ctl.  (KCS_STAGE / KCS_GROUP: compile-time overrides for A/B runs.)
+constexpr int kCsStage = KCS_STAGE, kCsGroup = KCS_GROUP;  // records per unit, lanes per unit
 __global__ void __launch_bounds__(256)
     cs_units_kernel(int64_t ncells, const int *__restrict__ cnt, int *__restrict__ ucnt,
                     unsigned long long *__restrict__ units) {
@@ -457,12 +464,15 @@ __global__ void __launch_bounds__(256)
   for (int s = 0; s < u; s++) unit_cell[o + s] = c;
 }
 
-// One wave per unit: the cell's points (cell order, 64 a pass) against the unit's <= 64
-// records, staged through LDS with one coalesced load per lane; every lane then reads the same
-// record (an LDS broadcast).  Per-lane gathers of records, or scalar loads of them, measured
-// 1.1-1.8x slower; two cells per wave (fewer idle lanes) 1.15x slower.  A one-unit cell writes
-// its points' answers; the units of a longer list add their counts into acc, answered by
-// cs_finalize_kernel.
+// Two units per wave, 32 lanes each: the unit's cell's points (cell order, 32 a pass) against
+// the unit's <= 32 records, staged through LDS with coalesced loads; the lanes of a unit then
+// read the same record (an LDS broadcast).  The kernel is VALU-bound (counters: ~1000 VALU
+// instructions per 64-lane wave at 64-record units, ~27 % of lanes busy since a cell holds
+// ~17 points), so lanes are what to save: 64-record units one per wave took 112 us, two per
+// wave (twice the LDS per wave, half the occupancy) 113, 32-record units two per wave 85.
+// Per-lane gathers of records, or scalar loads of them, measured 1.1-1.8x slower.  A one-unit
+// cell writes its points' answers; the units of a longer list add their counts into acc,
+// answered by cs_finalize_kernel.
 __device__ __forceinline__ void cs_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -476,27 +486,35 @@ __global__ void __launch_bounds__(256)
                          const int *__restrict__ cnt, const int64_t *__restrict__ offs,
                          const CsRec<T> *__restrict__ list, int *__restrict__ acc, T *__restrict__ counts,
                          uint8_t *__restrict__ contains) {
-  __shared__ CsRec<T> s_rec[4][kCsStage];
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t u = (int64_t)blockIdx.x * 4 + w;
-  if (u >= nunits) return;
-  const int64_t c = unit_cell[u];
-  const int seg = (int)(u - (uoffs[c] - uoffs[0]));
-  const bool whole = ucnt[c] == 1;
-  const int64_t np = poffs[c + 1] - poffs[c];
-  const int lane = threadIdx.x & 63;
-  const int64_t s0 = poffs[c] - poffs[0], b = c / GG;
-  const int k0 = seg * kCsStage, m = min(kCsStage, cnt[c] - k0);
-  const CsRec<T> *L = list + offs[c] + k0;
-  CsRec<T> *S = s_rec[w];
-  if (lane < m) S[lane] = L[lane];
+  constexpr int NG = 256 / kCsGroup;
+  __shared__ CsRec<T> s_rec[NG][kCsStage];
+  const int g = threadIdx.x / kCsGroup, gl = threadIdx.x % kCsGroup;
+  const int64_t u = (int64_t)blockIdx.x * NG + g;
+  int64_t np = 0, s0 = 0, b = 0, c = 0;
+  int m = 0;
+  bool whole = true;
+  CsRec<T> *S = s_rec[g];
+  if (u < nunits) {
+    c = unit_cell[u];
+    const int seg = (int)(u - (uoffs[c] - uoffs[0]));
+    whole = ucnt[c] == 1;
+    np = poffs[c + 1] - poffs[c];
+    s0 = poffs[c] - poffs[0];
+    b = c / GG;
+    const int k0 = seg * kCsStage;
+    m = min(kCsStage, cnt[c] - k0);
+    const CsRec<T> *L = list + offs[c] + k0;
+#pragma unroll
+    for (int v = 0; v < kCsStage / kCsGroup; v++)
+      if (gl + v * kCsGroup < m) S[gl + v * kCsGroup] = L[gl + v * kCsGroup];
+  }
   cs_wave_sync();
-  for (int64_t p0 = 0; p0 < np; p0 += 64) {
-    const bool act = p0 + lane < np;
+  for (int64_t p0 = 0; p0 < np; p0 += kCsGroup) {
+    const bool act = p0 + gl < np;
     T qx = (T)INFINITY, qy = (T)INFINITY, qz = (T)INFINITY;  // an idle lane passes no bbox_check
     int32_t p = 0;
     if (act) {
-      const CsPt<T> pt = sorted[s0 + p0 + lane];
+      const CsPt<T> pt = sorted[s0 + p0 + gl];
       qx = pt.q[0]; qy = pt.q[1]; qz = pt.q[2];
       p = pt.p;
     }
@@ -685,7 +703,7 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, CsCountIt(cnt, CsToI64()), offs, (int)(3 * ncells + 1),
                                                 st));
   const int64_t nunits = sort_points ? (int64_t)ctl->units : 0;
-  // the lists, then the unit -> cell map (in the workspace when they fit: ncells + total / 64
+  // the lists, then the unit -> cell map (in the workspace when they fit: ncells + total / kCsStage
   // units <= 2 ncells there)
   const size_t list_bytes = (size_t)(total > 0 ? total : 1) * sizeof(CsRec<T>);
   uint8_t *lbuf = (size_t)total <= L.list_cap
@@ -713,7 +731,7 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
     KL_CHECK_LAUNCH();
     KL_CHECK_RC(fill_async(acc, 0, (size_t)(B * P) * 4, st));
     if (nunits > 0) {
-      hipLaunchKernelGGL(cs_cell_check_kernel<T>, dim3((unsigned)cdiv(nunits, 4)), dim3(256), 0, st, nunits, P,
+      hipLaunchKernelGGL(cs_cell_check_kernel<T>, dim3((unsigned)cdiv(nunits, 256 / kCsGroup)), dim3(256), 0, st, nunits, P,
                          (int64_t)G * G, (const int64_t *)unit_cell, uoffs, ucnt, poffs, (const CsPt<T> *)sorted,
                          (const int *)cnt, (const int64_t *)offs, (const CsRec<T> *)list, acc, (T *)counts, contains);
       KL_CHECK_LAUNCH();
