@@ -504,9 +504,7 @@ __global__ void __launch_bounds__(256)
     const int k0 = seg * kCsStage;
     m = min(kCsStage, cnt[c] - k0);
     const CsRec<T> *L = list + offs[c] + k0;
-#pragma unroll
-    for (int v = 0; v < kCsStage / kCsGroup; v++)
-      if (gl + v * kCsGroup < m) S[gl + v * kCsGroup] = L[gl + v * kCsGroup];
+    for (int v = gl; v < m; v += kCsGroup) S[v] = L[v];
   }
   cs_wave_sync();
   for (int64_t p0 = 0; p0 < np; p0 += kCsGroup) {
