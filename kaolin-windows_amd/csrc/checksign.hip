@@ -27,7 +27,7 @@
 #include "common.h"
 
 #ifndef KCS_STAGE
-#define KCS_STAGE 32
+#define KCS_STAGE 16
 #endif
 #ifndef KCS_GROUP
 #define KCS_GROUP 32
@@ -465,11 +465,12 @@ __global__ void __launch_bounds__(256)
 }
 
 // Two units per wave, 32 lanes each: the unit's cell's points (cell order, 32 a pass) against
-// the unit's <= 32 records, staged through LDS with coalesced loads; the lanes of a unit then
+// the unit's <= 16 records, staged through LDS with coalesced loads; the lanes of a unit then
 // read the same record (an LDS broadcast).  The kernel is VALU-bound (counters: ~1000 VALU
 // instructions per 64-lane wave at 64-record units, ~27 % of lanes busy since a cell holds
 // ~17 points), so lanes are what to save: 64-record units one per wave took 112 us, two per
-// wave (twice the LDS per wave, half the occupancy) 113, 32-record units two per wave 85.
+// wave (twice the LDS per wave, half the occupancy) 113, 32-record units two per wave 85,
+// 16-record units two per wave 75.
 // Per-lane gathers of records, or scalar loads of them, measured 1.1-1.8x slower.  A one-unit
 // cell writes its points' answers; the units of a longer list add their counts into acc,
 // answered by cs_finalize_kernel.
