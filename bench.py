@@ -155,13 +155,27 @@ def gather_losses(loss, world):
 
 
 def max_over_ranks(elapsed, device, world):
+    return max(per_rank(elapsed, device, world))
+
+
+def per_rank(elapsed, device, world):
+    """Every rank's elapsed time (all_gather over the initialised process group)."""
     if world == 1:
-        return elapsed
+        return [elapsed]
     import torch
     import torch.distributed as dist
     t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x) for x in out]
+
+
+def process_group_info(world):
+    """What the initialised process group says (not the environment): world size, backend."""
+    import torch.distributed as dist
+    if world == 1 or not dist.is_initialized():
+        return {'initialized': dist.is_available() and dist.is_initialized(), 'world_size': 1, 'backend': None}
+    return {'initialized': True, 'world_size': dist.get_world_size(), 'backend': str(dist.get_backend())}
 
 
 def _sync(device):
@@ -461,7 +475,8 @@ def dibr_headline(args, world, rank, device):
     timed_loop(step, args.steps, world, device)
     _native.set_timer(None)
     ops_ms = timer.summary_ms()
-    eager_elapsed = max_over_ranks(timed_loop(step, args.steps, world, device), device, world)
+    eager_times = per_rank(timed_loop(step, args.steps, world, device), device, world)
+    eager_elapsed = max(eager_times)
     pixels = cfg['views'] * cfg['H'] * cfg['W'] * world * args.steps
     mode, elapsed = 'eager', eager_elapsed
     if not args.eager:
@@ -476,8 +491,14 @@ def dibr_headline(args, world, rank, device):
             raise RuntimeError('graph replay differs from the eager step')
         for _ in range(args.warmup):
             gstep()
-        elapsed = max_over_ranks(timed_loop(gstep, args.steps, world, device), device, world)
+        rank_times = per_rank(timed_loop(gstep, args.steps, world, device), device, world)
+        elapsed = max(rank_times)
         mode = 'hip_graph'
+    else:
+        rank_times = eager_times
+    pg = process_group_info(world)
+    if pg['world_size'] != world:
+        raise RuntimeError(f'process group has {pg["world_size"]} ranks, WORLD_SIZE says {world}')
     value = pixels / elapsed / 1e6
     if rank != 0:
         return None, inp
@@ -489,7 +510,7 @@ def dibr_headline(args, world, rank, device):
                       'GB/s': round(op_bytes(k, inp, stats) / (v * 1e-3) / 1e9, 1)} for k, v in ops_ms.items()}
     sb = survey_step_bytes(inp, stats)
     result = {
-        'metric': METRIC, 'value': round(value, 2), 'unit': 'Mpixels/s', 'n_gpus': world, 'steps': args.steps,
+        'metric': METRIC, 'value': round(value, 2), 'unit': 'Mpixels/s', 'n_gpus': pg['world_size'], 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
         'data': f'synthetic (seeded UV sphere, {cfg["views"]} views/GPU)',
@@ -507,6 +528,8 @@ def dibr_headline(args, world, rank, device):
                          'bytes_per_step': sb, 'achieved': round(sb / (elapsed / args.steps) / 1e9, 1),
                          'frac': round(sb / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}},
         'ops': ops_report, 'workload_stats': stats, 'mode': mode,
+        'process_group': dict(pg, per_rank_ms_per_step=[round(t / args.steps * 1e3, 4) for t in rank_times],
+                              devices_visible=torch.cuda.device_count()),
         'eager': {'value': round(pixels / eager_elapsed / 1e6, 2),
                   'ms_per_step': round(eager_elapsed / args.steps * 1e3, 4)},
     }
@@ -552,6 +575,91 @@ def prepare_leg(device, steps, views=4):
                                       'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                                       'frac': round(nb / (ms_f * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             'timing': 'wall clock per fwd+bwd incl. Python / autograd (median of runs)'}
+
+
+# ----------------------------------------------------------------------------- tutorial loop
+def tutorial_setup(device, views=4, H=512, W=512, tex=512):
+    """The reference's own caller (examples/tutorial/dibr_tutorial.ipynb cells 8-14) at cfg3 size:
+    the cfg3 sphere (50k faces) as the optimised mesh, 4 cameras (camera_transform form), a
+    (1,3,tex,tex) texture map, Adam on the vertices + centre shift and on the texture.  Ground
+    truth: a synthetic seeded image and a silhouette (no dataset on the box)."""
+    import torch
+    import kaolin as kal
+    verts, faces = uv_sphere(126, 200, device)
+    F = faces.shape[0]
+    u = torch.atan2(verts[:, 2], verts[:, 0]) / (2 * math.pi) + 0.5
+    vv = torch.acos(torch.clamp(verts[:, 1] / verts.norm(dim=1), -1, 1)) / math.pi
+    face_uvs = kal.ops.mesh.index_vertices_by_faces(torch.stack([u, vv], -1)[None], faces).contiguous()
+    az = torch.tensor(views_for_rank(0, 1, views), dtype=torch.float32, device=device)
+    cam = torch.stack([3 * torch.sin(az), torch.zeros_like(az), 3 * torch.cos(az)], -1)
+    rot, trans = kal.render.camera.generate_rotate_translate_matrices(
+        cam, torch.zeros_like(cam), torch.tensor([[0., 1., 0.]], device=device).repeat(views, 1))
+    cam_transform = torch.cat([rot.transpose(1, 2), -(trans[:, None] @ rot.transpose(1, 2))], 1).contiguous()
+    cam_proj = kal.render.camera.generate_perspective_projection(math.pi / 4).to(device)
+    g = torch.Generator().manual_seed(4)
+    st = dict(
+        faces=faces, face_uvs=face_uvs, cam_transform=cam_transform, cam_proj=cam_proj, B=views, H=H, W=W, F=F,
+        vertices=verts[None].clone().requires_grad_(True),
+        shift=torch.zeros((3,), dtype=torch.float32, device=device, requires_grad=True),
+        texture=torch.rand((1, 3, tex, tex), generator=g).to(device).requires_grad_(True),
+        gt_image=torch.rand((views, H, W, 3), generator=g).to(device),
+        gt_mask=(torch.rand((views, H, W), generator=g) > 0.5).float().to(device))
+    st['vopt'] = torch.optim.Adam([st['vertices'], st['shift']], lr=5e-4)
+    st['topt'] = torch.optim.Adam([st['texture']], lr=1e-2)
+    return st
+
+
+def tutorial_step(st):
+    """One iteration of dibr_tutorial.ipynb cell 14 (render() of cell 12 inlined): zero_grad,
+    center_points + shift, prepare_vertices(camera_transform=...), dibr_rasterization with the
+    feature LIST [face_uvs, ones], texture_mapping (bilinear), clamp(image * mask), L1 image loss
+    + mask_iou, backward, both Adam steps.  The tutorial's laplacian regulariser (a dense V x V
+    matmul, off the rendering path) is left out."""
+    import torch
+    import kaolin as kal
+    B = st['B']
+    st['vopt'].zero_grad()
+    st['topt'].zero_grad()
+    vb = kal.ops.pointcloud.center_points(st['vertices']) + st['shift']
+    fvc, fvi, fn = kal.render.mesh.prepare_vertices(vb.repeat(B, 1, 1), st['faces'], st['cam_proj'],
+                                                    camera_transform=st['cam_transform'])
+    attrs = [st['face_uvs'].repeat(B, 1, 1, 1), torch.ones((B, st['F'], 3, 1), device=fvc.device)]
+    (coords, mask), soft_mask, _ = kal.render.mesh.dibr_rasterization(
+        st['H'], st['W'], fvc[:, :, :, -1], fvi, attrs, fn[:, :, -1], rast_backend='cuda')
+    image = kal.render.mesh.texture_mapping(coords, st['texture'].repeat(B, 1, 1, 1), mode='bilinear')
+    image = torch.clamp(image * mask, 0., 1.)
+    image_loss = torch.mean(torch.abs(image - st['gt_image']))
+    mask_loss = kal.metrics.render.mask_iou(soft_mask, st['gt_mask'])
+    loss = image_loss * 1. + mask_loss * 1.
+    loss.backward()
+    st['vopt'].step()
+    st['topt'].step()
+    return loss
+
+
+def tutorial_leg(device, steps, warmup=3):
+    """The tutorial loop's eager rate (the caller the reference's users run), with the share of
+    its time in the DIB-R fwd+bwd (HIP events on the two native ops) beside it."""
+    import torch
+    from kaolin import _native
+    st = tutorial_setup(device)
+    for _ in range(warmup):
+        tutorial_step(st)
+    ms = _wall_ms(lambda: tutorial_step(st), steps)
+    timer = _native.OpTimer()
+    _native.set_timer(timer)
+    for _ in range(5):
+        tutorial_step(st)
+    _native.set_timer(None)
+    ops = {k: round(v, 4) for k, v in timer.summary_ms().items()}
+    torch.cuda.synchronize()
+    px = st['B'] * st['H'] * st['W']
+    return {'metric': 'DIB-R tutorial loop (dibr_tutorial.ipynb cells 12/14) Mpixels/s, eager, 4 views x 512^2, '
+                      '50k faces, feature list [uv, ones], texture 512^2, Adam',
+            'value': round(px / (ms * 1e-3) / 1e6, 2), 'ms_per_step': round(ms, 4),
+            'native_op_ms': ops,
+            'timing': 'wall clock per iteration (median), eager autograd, everything the tutorial iteration runs '
+                      'except its laplacian regulariser and the dataloader'}
 
 
 # ----------------------------------------------------------------------------- p2m (cfg2)
@@ -939,6 +1047,9 @@ def main(argv=None):
         result['check_sign'] = check_sign_bench(device, max(3, args.steps // 4))
         progress('prepare_vertices leg')
         result['prepare_vertices'] = prepare_leg(device, args.steps)
+        if args.config == 'cfg3':
+            progress('tutorial loop leg')
+            result['tutorial'] = tutorial_leg(device, max(10, args.steps))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         row_step = args.cpu_row_step or CONFIGS[args.config]['row_step']
         progress(f'DIB-R parity + cpu baseline (oracle, every {row_step}th row)')

@@ -48,6 +48,12 @@ typedef void *kl_stream;
  * caller releases `ctx`'s allocations (after the call returns). */
 typedef void *(*kl_alloc_fn)(void *ctx, size_t bytes);
 
+/* ABI version of this header: a caller checks kl_abi_version() == KL_ABI_VERSION at load time.
+ * 2: the workspace arguments moved before the stream (kl_rasterize_backward,
+ *    kl_dibr_soft_mask_backward(_fused), kl_unbatched_triangle_distance_backward) and
+ *    kl_soft_mask_compact_bwd_workspace_bytes gained num_faces. */
+#define KL_ABI_VERSION 2
+
 const char *kl_last_error(void);
 int kl_abi_version(void);
 
@@ -83,8 +89,10 @@ int kl_packed_rasterize_forward(kl_dtype dtype, int height, int width, int batch
  * face_idx: (B,H,W) ORIGINAL face index per mesh; face_vertices_image (B,F,3,2) unscaled.
  * Outputs (fully written): grad_face_vertices_image (B,F,3,2), grad_face_features (B,F,3,D).
  * The reference's per-pixel float terms are summed in double (workspace:
- * kl_rasterize_backward_workspace_bytes) and rounded once, so the result does not depend on the
- * order of the atomics (the reference's float atomics make it run-to-run nondeterministic). */
+ * kl_rasterize_backward_workspace_bytes) and rounded once, so for f32 the result does not depend
+ * on the order of the atomics (the reference's float atomics make it run-to-run
+ * nondeterministic).  f64 terms are added with double atomics: rounded per add, order-dependent
+ * in the last bits. */
 size_t kl_rasterize_backward_workspace_bytes(int batch, int num_faces, int feat_dim);
 int kl_rasterize_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
                           const void *grad_interpolated_features, const int64_t *face_idx,
@@ -109,8 +117,8 @@ int kl_dibr_rasterize_forward(kl_dtype dtype, int height, int width, int batch, 
                               void *workspace, size_t workspace_bytes, kl_stream stream);
 /* Atomic-free backward of the fused path: 8 lanes per face gather the pixels of the face's
  * exact pixel range (the reference's bbox test, same valid_faces / multiplier as the forward)
- * whose face_idx equals it, summing the reference's float terms in double (rounded once:
- * deterministic and order-independent).  Requires face_idx produced by the fused forward with
+ * whose face_idx equals it, summing the reference's terms in double in a fixed lane order
+ * (rounded once: deterministic for f32 and f64).  Requires face_idx produced by the fused forward with
  * the same valid_faces and multiplier.  Every face's gradient is written (zeros where it won no
  * pixel).  scratch: NULL, or a zeroed int32 the call uses as its big-face counter instead of
  * zeroing one in the workspace (kl_dibr_forward).  face_ranges: NULL, or kl_dibr_forward's
@@ -330,7 +338,8 @@ int kl_unbatched_triangle_distance_forward(kl_dtype dtype, int64_t num_points, i
 /* unbatched_triangle_distance.cpp:74-114.  grad_points (P,3) fully written;
  * grad_face_vertices (F,3,3) fully written (zero where no point selected the face).
  * workspace: kl_unbatched_triangle_distance_bwd_workspace_bytes(F) bytes -- the per-point terms
- * are then summed per face coordinate in double and rounded once (deterministic); NULL: the
+ * are then summed per face coordinate in double and rounded once (deterministic for f32; f64
+ * terms are added with double atomics, order-dependent in the last bits); NULL: the
  * reference's float atomics (order-dependent last bits). */
 size_t kl_unbatched_triangle_distance_bwd_workspace_bytes(int64_t num_faces);
 int kl_unbatched_triangle_distance_backward(kl_dtype dtype, int64_t num_points, int64_t num_faces,

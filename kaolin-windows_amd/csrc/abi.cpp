@@ -119,7 +119,9 @@ SideFork::~SideFork() { (void)join(); }
 }  // namespace kl
 
 extern "C" const char *kl_last_error(void) { return kl::g_last_error.c_str(); }
-extern "C" int kl_abi_version(void) { return 1; }
+// 2: workspace arguments before the stream in kl_rasterize_backward, kl_dibr_soft_mask_backward(_fused),
+//    kl_unbatched_triangle_distance_backward; num_faces in kl_soft_mask_compact_bwd_workspace_bytes
+extern "C" int kl_abi_version(void) { return KL_ABI_VERSION; }
 
 // ---- Training-loop helper (not a reference op): L = <a, ga> + <b, gb>.
 // A loss of this shape is what bench.py's step computes; two torch.dot calls plus their

@@ -702,19 +702,20 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, CsCountIt(cnt, CsToI64()), offs, (int)(3 * ncells + 1),
                                                 st));
   const int64_t nunits = sort_points ? (int64_t)ctl->units : 0;
-  // the lists, then the unit -> cell map (in the workspace when they fit: ncells + total / kCsStage
-  // units <= 2 ncells there)
+  // the lists, then the unit -> cell map: in the workspace when both fit (its unit room is
+  // 2 * ncells of the initial grid: units <= ncells + total / kCsStage, and total <= list_cap =
+  // 16 entries per face <= kCsStage * ncells when kCsStage >= 16), else from the allocator
+  static_assert(kCsStage >= 16, "check_sign: the workspace's unit room assumes >= 16 records per unit");
   const size_t list_bytes = (size_t)(total > 0 ? total : 1) * sizeof(CsRec<T>);
-  uint8_t *lbuf = (size_t)total <= L.list_cap
-                      ? w + L.list
-                      : (uint8_t *)alloc(alloc_ctx, cs_align(list_bytes) + (size_t)(nunits > 0 ? nunits : 1) * 8);
+  const bool in_ws = (size_t)total <= L.list_cap && nunits <= 2 * B * (int64_t)L.G * L.G;
+  uint8_t *lbuf = in_ws ? w + L.list
+                        : (uint8_t *)alloc(alloc_ctx, cs_align(list_bytes) + (size_t)(nunits > 0 ? nunits : 1) * 8);
   if (!lbuf) {
     set_error("check_sign: allocator returned NULL");
     return KL_E_ALLOC;
   }
   CsRec<T> *list = (CsRec<T> *)lbuf;
-  int64_t *unit_cell = (int64_t *)(lbuf + ((size_t)total <= L.list_cap ? L.list_cap * sizeof(CsRec<T>)
-                                                                         : cs_align(list_bytes)));
+  int64_t *unit_cell = (int64_t *)(lbuf + (in_ws ? L.list_cap * sizeof(CsRec<T>) : cs_align(list_bytes)));
   KL_CHECK_RC(fill_async(cnt, 0, (size_t)ncells * 4, st));
   hipLaunchKernelGGL((cs_bin_kernel<true, T>), fgrid, dim3(256), 0, st, F, G, (const CsRec<T> *)rec,
                      (const float *)mbox, cnt, (const int64_t *)offs, list, (unsigned long long *)nullptr);

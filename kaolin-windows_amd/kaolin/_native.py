@@ -14,6 +14,8 @@ _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib')
 # `make STAMPS=1 OUT=...`); the default is the in-tree build
 LIB_PATH = os.environ.get('KAOLIN_HIP_LIB') or os.path.join(_LIB_DIR, 'libkaolin_hip.so')
 
+ABI_VERSION = 2  # include/kaolin_hip.h KL_ABI_VERSION: the signatures below
+
 KL_F32, KL_F64, KL_F16, KL_U8, KL_I8, KL_I16, KL_I32, KL_I64 = range(8)
 _DTYPES = {
     torch.float32: KL_F32, torch.float64: KL_F64, torch.float16: KL_F16, torch.uint8: KL_U8,
@@ -128,6 +130,10 @@ def lib():
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        got = handle.kl_abi_version()
+        if got != ABI_VERSION:
+            raise RuntimeError(f'kaolin HIP library at {LIB_PATH} has ABI version {got}, this package expects '
+                               f'{ABI_VERSION}; rebuild it with `make -C kaolin-windows_amd/csrc`')
         _lib = handle
     return _lib
 

@@ -114,14 +114,26 @@ def dibr_soft_mask(face_vertices_image, selected_face_idx, sigmainv=7000, boxlen
 def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z,
                        sigmainv=7000, boxlen=0.02, knum=30, multiplier=None, eps=None, rast_backend='cuda'):
     r"""DIB-R renderer: rasterize(valid = face_normals_z >= 0) + dibr_soft_mask.
-    Returns (features, soft_mask, face_idx) as dibr.py:119-209."""
+    Returns (features, soft_mask, face_idx) as dibr.py:119-209; ``face_features`` may be a
+    list, then features is a tuple of per-element views."""
     _multiplier = 1000. if multiplier is None else multiplier
     _eps = 1e-8 if eps is None else eps
-    if (rast_backend in ('cuda', 'hip') and not isinstance(face_features, (list, tuple))
-            and face_features.shape[-1] <= 8 and 0 <= int(knum) <= 255
+    is_list = isinstance(face_features, (list, tuple))
+    # a feature list (the tutorial's [face_uvs, ones]) is concatenated and the outputs split as
+    # rasterize does (rasterization.py:480-481,498-505); the single node serves both shapes
+    _face_features = torch.cat(face_features, dim=-1) if is_list else face_features
+    if (rast_backend in ('cuda', 'hip') and _face_features.shape[-1] <= 8 and 0 <= int(knum) <= 255
             and face_vertices_image.dtype in (torch.float32, torch.float64)):
-        return DibrRasterizationCuda.apply(height, width, face_vertices_z, face_vertices_image, face_features,
-                                           face_normals_z, sigmainv, boxlen, knum, _multiplier, _eps)
+        feats, soft_mask, face_idx = DibrRasterizationCuda.apply(
+            height, width, face_vertices_z, face_vertices_image, _face_features, face_normals_z, sigmainv, boxlen,
+            knum, _multiplier, _eps)
+        if is_list:
+            out, cur = [], 0
+            for ff in face_features:
+                out.append(feats[..., cur:cur + ff.shape[-1]])
+                cur += ff.shape[-1]
+            feats = tuple(out)
+        return feats, soft_mask, face_idx
     interpolated_features, face_idx = rasterize(height, width, face_vertices_z, face_vertices_image, face_features,
                                                 face_normals_z >= 0., multiplier, eps, rast_backend)
     soft_mask = dibr_soft_mask(face_vertices_image, face_idx, sigmainv, boxlen, knum, _multiplier)

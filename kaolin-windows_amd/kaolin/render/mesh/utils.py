@@ -6,6 +6,8 @@ GPU f32 / f64 tensors run one HIP launch forward and one backward call (csrc/pre
 camera tensor that requires one.  Other devices and dtypes run the reference's torch chain, as
 the reference does on every device.
 """
+import weakref
+
 import torch
 from torch.autograd import Function
 
@@ -14,7 +16,7 @@ from ...ops.mesh import face_normals as _face_normals
 from ...ops.mesh import index_vertices_by_faces
 from ..camera import perspective_camera, rotate_translate_points
 
-__all__ = ['prepare_vertices']
+__all__ = ['prepare_vertices', 'texture_mapping']
 
 
 def _prepare_vertices_torch(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform):
@@ -53,7 +55,32 @@ def _batches(vertices, camera_proj, camera_rot, camera_trans, camera_transform):
     B = max(Bv, Bc, Bp)
     if any(x not in (1, B) for x in (Bv, Bc, Bp)):
         return None
+    if max(Bv, Bc) == 1 < Bp:  # torch gives face_vertices_camera / face_normals a batch of 1 here
+        return None
     return B, Bv, Bc, Bp
+
+
+_CHECKED_FACES = {}  # id(faces) -> (weakref to faces, (version, shape, V) checked)
+
+
+def _check_faces(faces, num_vertices):
+    """index_vertices_by_faces' gather raises on an index outside [0, V); the kernel
+    would give NaN outputs instead.  A faces tensor is checked once (one host read) and
+    remembered (weakly) with its version, shape and V: the meshes of a training loop are fixed, so the
+    steady state reads nothing back.  Skipped under graph capture (no host reads there)."""
+    key = (faces._version, tuple(faces.shape), int(num_vertices))
+    hit = _CHECKED_FACES.get(id(faces))
+    if (hit is not None and hit[0]() is faces and hit[1] == key) or (faces.is_cuda and torch.cuda.is_current_stream_capturing()):
+        return
+    if faces.numel() > 0:
+        lo, hi = torch.aminmax(faces)
+        lo, hi = int(lo), int(hi)
+        if lo < 0 or hi >= num_vertices:  # torch.gather's check (index_vertices_by_faces)
+            bad = lo if lo < 0 else hi
+            raise RuntimeError(f'index {bad} is out of bounds for dimension 1 with size {num_vertices}')
+    for k in [k for k, (r, _) in _CHECKED_FACES.items() if r() is None]:
+        del _CHECKED_FACES[k]
+    _CHECKED_FACES[id(faces)] = (weakref.ref(faces), key)
 
 
 class PrepareVerticesHip(Function):
@@ -144,4 +171,23 @@ def prepare_vertices(vertices, faces, camera_proj, camera_rot=None, camera_trans
         batches = _batches(vertices, camera_proj, camera_rot, camera_trans, camera_transform)
     if batches is None:
         return _prepare_vertices_torch(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform)
+    _check_faces(faces, vertices.shape[1])
     return PrepareVerticesHip.apply(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform, batches)
+
+
+def texture_mapping(texture_coordinates, texture_maps, mode='nearest'):
+    r"""Sample ``texture_maps`` (B, C, h', w') at ``texture_coordinates`` (B, h, w, 2) or (B, N, 2)
+    in OpenGL convention ([0, 1], y up) -> (B, h, w, C) / (B, N, C) (render/mesh/utils.py:23-75).
+
+    The caller-side step after dibr_rasterization in the reference's tutorial loop
+    (dibr_tutorial.ipynb cell 12): coordinates clamped to [0, 1], mapped to grid_sample's
+    [-1, 1] with y reversed, border padding, align_corners=False -- torch's grid_sample, as the
+    reference (not part of the HIP path)."""
+    batch_size = texture_coordinates.shape[0]
+    num_channels = texture_maps.shape[1]
+    coords = texture_coordinates.reshape(batch_size, -1, 1, 2)
+    coords = torch.clamp(coords, 0., 1.) * 2 - 1
+    coords[..., 1] = -coords[..., 1]
+    out = torch.nn.functional.grid_sample(texture_maps, coords, mode=mode, align_corners=False,
+                                          padding_mode='border')
+    return out.permute(0, 2, 3, 1).reshape(batch_size, *texture_coordinates.shape[1:-1], num_channels)

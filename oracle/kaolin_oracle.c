@@ -244,6 +244,93 @@ int64_t or_mesh_to_spc_leaves(const float *fv, int64_t F, unsigned L,
   return (int64_t)u;
 }
 
+/* Sensitivity of mesh_to_spc's separating-axis decisions to the normalisation's rounding
+ * (measurement, not a restatement).  The reference normalises the edges with CUDA's double
+ * rsqrt (mesh_to_spc_cuda.cu:123-125 -> spc_math.h:240-243), which is not correctly rounded
+ * (1 ulp); this restatement and the HIP kernel use 1.0 / sqrt.  For every proposal of the
+ * level recursion (following the 1/sqrt decisions) this counts:
+ *   counts[0] proposals tested, counts[1] proposals with some axis whose float-rounded
+ *   |fd - fr| is at most one float ulp of fr (near the threshold), counts[2] proposals whose
+ *   decision changes when every 1/sqrt is moved 1 ulp up, counts[3] ... 1 ulp down,
+ *   counts[4] of those flips at the leaf level L. */
+static d3 d3norm_ulp(d3 v, int dir)
+{
+  double inv = 1.0 / sqrt(d3dot(v, v));
+  if (dir) inv = nextafter(inv, dir > 0 ? INFINITY : 0.0);
+  return d3mk(inv * v.x, inv * v.y, inv * v.z);
+}
+
+static int tri_voxel_test_ulp(const float *fa, const float *fb, const float *fc, const float *c, float h, int dir,
+                              int *near)
+{
+  d3 va = d3mk((double)(fa[0] - c[0]), (double)(fa[1] - c[1]), (double)(fa[2] - c[2]));
+  d3 vb = d3mk((double)(fb[0] - c[0]), (double)(fb[1] - c[1]), (double)(fb[2] - c[2]));
+  d3 vc = d3mk((double)(fc[0] - c[0]), (double)(fc[1] - c[1]), (double)(fc[2] - c[2]));
+  d3 ab = d3norm_ulp(d3sub(vb, va), dir), bc = d3norm_ulp(d3sub(vc, vb), dir), ca = d3norm_ulp(d3sub(va, vc), dir);
+  d3 axes[13] = {
+    d3mk(0.0, -ab.z, ab.y), d3mk(0.0, -bc.z, bc.y), d3mk(0.0, -ca.z, ca.y),
+    d3mk(ab.z, 0.0, -ab.x), d3mk(bc.z, 0.0, -bc.x), d3mk(ca.z, 0.0, -ca.x),
+    d3mk(-ab.y, ab.x, 0.0), d3mk(-bc.y, bc.x, 0.0), d3mk(-ca.y, ca.x, 0.0),
+    d3mk(1, 0, 0), d3mk(0, 1, 0), d3mk(0, 0, 1), d3cross(ab, bc)};
+  int ok = 1;
+  for (int a = 0; a < 13 && (ok || near); a++) {
+    const d3 axis = axes[a];
+    double d0 = d3dot(va, axis), d1 = d3dot(vb, axis), d2 = d3dot(vc, axis);
+    double maxd = fmax(d0, fmax(d1, d2)), mind = fmin(d0, fmin(d1, d2));
+    double r = (double)h * (fabs(axis.x) + fabs(axis.y) + fabs(axis.z));
+    float fd = (float)fmax(-maxd, mind), fr = (float)r;
+    if (near && fabsf(fd - fr) <= nextafterf(fabsf(fr), INFINITY) - fabsf(fr)) *near = 1;
+    if (!(fd <= fr)) ok = 0;
+    if (!ok && !near) break;
+  }
+  return ok;
+}
+
+void or_m2s_rsqrt_sensitivity(const float *fv, int64_t F, unsigned L, int64_t *counts)
+{
+  size_t cnt = (size_t)F;
+  mt_pair *cur = (mt_pair *)malloc((cnt ? cnt : 1) * sizeof(mt_pair));
+  for (size_t i = 0; i < cnt; i++) { cur[i].m = 0; cur[i].t = (int64_t)i; }
+  for (int k = 0; k < 5; k++) counts[k] = 0;
+  for (unsigned l = 0; l <= L && cnt; l++) {
+    unsigned char *hit = (unsigned char *)malloc(cnt);
+    int64_t c1 = 0, c2 = 0, c3 = 0;
+#pragma omp parallel for schedule(dynamic, 4096) reduction(+ : c1, c2, c3)
+    for (size_t i = 0; i < cnt; i++) {
+      float c[3], h;
+      voxel_center(cur[i].m, l, c, &h);
+      const float *v = fv + cur[i].t * 9;
+      int near = 0;
+      const int base = tri_voxel_test_ulp(v, v + 3, v + 6, c, h, 0, &near);
+      hit[i] = (unsigned char)base;
+      c1 += near;
+      if (near) {
+        c2 += tri_voxel_test_ulp(v, v + 3, v + 6, c, h, 1, NULL) != base;
+        c3 += tri_voxel_test_ulp(v, v + 3, v + 6, c, h, -1, NULL) != base;
+      }
+    }
+    counts[0] += (int64_t)cnt; counts[1] += c1; counts[2] += c2; counts[3] += c3;
+    if (l == L) counts[4] += c2 + c3;
+    size_t nxt = 0;
+    for (size_t i = 0; i < cnt; i++) nxt += hit[i] ? (l < L ? 8 : 0) : 0;
+    mt_pair *n2 = (mt_pair *)malloc((nxt ? nxt : 1) * sizeof(mt_pair));
+    size_t o = 0;
+    for (size_t i = 0; i < cnt && l < L; i++) {
+      if (!hit[i]) continue;
+      int16_t p[3];
+      or_to_point(cur[i].m, p);
+      for (unsigned cc = 0; cc < 8; cc++) {
+        n2[o].m = or_to_morton(2 * p[0] + (cc >> 2), 2 * p[1] + ((cc >> 1) & 1), 2 * p[2] + (cc & 1));
+        n2[o].t = cur[i].t;
+        o++;
+      }
+    }
+    free(hit); free(cur);
+    cur = n2; cnt = nxt;
+  }
+  free(cur);
+}
+
 /* morton_to_octree: level-major bytes, top-down.  Returns octree size; *out malloc'd. */
 int64_t or_morton_to_octree(const uint64_t *mortons, int64_t n, unsigned L, uint8_t **out)
 {

@@ -238,6 +238,17 @@ def mesh_to_spc(face_vertices, level):
     return morton_to_octree(mort, level), face, bary
 
 
+def m2s_rsqrt_sensitivity(face_vertices, level):
+    """Counts of mesh_to_spc SAT decisions sensitive to the edge normalisation's rounding
+    (kaolin_oracle.c:or_m2s_rsqrt_sensitivity): proposals, near-threshold proposals, flips
+    with every 1/sqrt one ulp up, one ulp down, flips at the leaf level."""
+    fv = _c(face_vertices, np.float32)
+    out = np.zeros(5, np.int64)
+    lib().or_m2s_rsqrt_sensitivity(_p(fv), ctypes.c_int64(fv.shape[0]), ctypes.c_uint(level), _p(out))
+    return dict(zip(('proposals', 'near_threshold', 'flips_ulp_up', 'flips_ulp_down', 'flips_at_leaf_level'),
+                    (int(x) for x in out)))
+
+
 def scan_octrees(octrees, lengths):
     o = _c(octrees, np.uint8)
     ln = _c(lengths, np.int32)

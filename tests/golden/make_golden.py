@@ -191,6 +191,56 @@ def dibr_sphere():
     save('dibr_sphere.npz', **arrays)
 
 
+def dibr_sphere_scaled_eps():
+    """The sphere case through the reference's naive renderer in float64, set up to compute
+    what the CUDA kernel computes, so these vectors pin the restatement's arithmetic and not
+    just the reference tests' tolerance band.  Two differences of the naive oracle are undone:
+    * pixel centres: the kernel forms them in float, ``multiplier / W * (2i + 1 - W)``
+      (rasterization_cuda.cu:85-86), also for f64 inputs; here they are those float values
+      divided by the multiplier (in float64);
+    * eps: the naive oracle normalises by k3 + eps in UNSCALED coordinates; the kernel's
+      forward by k3 + copysign(eps) in coordinates x multiplier, where k3 is multiplier^2
+      larger (rasterization_cuda.cu:96-99): the forward fixtures use eps = 1e-8 / 1000^2.  The
+      kernel's backward works in unscaled coordinates with eps itself
+      (rasterization_cuda.cu:262-275): the gradient fixtures use eps = 1e-8."""
+    H, W = 35, 31
+    m = 1000.
+    arrays = {}
+    for dname, dtype in (('f32', torch.float), ('f64', torch.double)):
+        for flip in (0, 1):
+            inp = _sphere_inputs(dtype, bool(flip))
+            p = f'{dname}_flip{flip}_'
+            B = 3
+            fvz64 = inp['face_vertices_z'].double()
+            _, rr = _pixel_coords_ranges(fvz64, H, W, vertices_z=inp['vertices_camera_z'].double())
+            mf = torch.tensor(m, dtype=torch.float32)
+            x = ((mf / W) * (2 * torch.arange(W) + 1 - W).float()).double() / m
+            y = ((mf / H) * (H - 2 * torch.arange(H) - 1).float()).double() / m
+            pix = torch.stack([x.reshape(1, 1, -1).repeat(B, H, 1), y.reshape(1, -1, 1).repeat(B, 1, W)],
+                              dim=-1).reshape(B, -1, 2)
+            for use_valid in (0, 1):
+                kw = {'valid_faces': inp['valid_faces']} if use_valid else {}
+                q = p + f'valid{use_valid}_'
+                fvi = inp['face_vertices_image'].double()
+                fuv = inp['face_uvs'].double()
+                g = torch.Generator().manual_seed(1234 + use_valid)
+                grad_out = torch.rand((B, H, W, fuv.shape[-1]), generator=g, dtype=dtype).double()
+                # forward eps: features, and the feature gradient (sum of grad x forward weights)
+                fuv_r = fuv.clone().requires_grad_(True)
+                feats, idx = _naive_deftet_sparse_render(pix, rr, fvz64, fvi, fuv_r, 1, eps=1e-8 / m ** 2, **kw)
+                feats = feats.reshape(B, H, W, -1)
+                feats.backward(grad_out)
+                arrays[q + 'features'] = feats.detach()
+                arrays[q + 'face_idx'] = idx.reshape(B, H, W)
+                arrays[q + 'grad_face_uvs'] = fuv_r.grad
+                # backward eps: the vertex gradient
+                fvi_r = fvi.clone().requires_grad_(True)
+                feats, _ = _naive_deftet_sparse_render(pix, rr, fvz64, fvi_r, fuv, 1, eps=1e-8, **kw)
+                feats.reshape(B, H, W, -1).backward(grad_out)
+                arrays[q + 'grad_face_vertices_image'] = fvi_r.grad
+    save('dibr_sphere_scaled_eps.npz', **arrays)
+
+
 # --------------------------------------------------------------------------
 # point_to_mesh_distance (tests/python/kaolin/metrics/test_trianglemesh.py)
 # --------------------------------------------------------------------------
@@ -571,6 +621,7 @@ if __name__ == '__main__':
         sys.exit(0)
     dibr_simple()
     dibr_sphere()
+    dibr_sphere_scaled_eps()
     p2m()
     sided()
     voxelgrid()

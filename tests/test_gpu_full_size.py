@@ -205,3 +205,29 @@ def test_unbatched_points_to_octree_vs_oracle(kal):
     assert np.array_equal(A(octree), orc.morton_to_octree(codes, level))
     srt = kal.ops.spc.morton_to_points(torch.from_numpy(codes.astype(np.int64)).to(DEV))
     assert torch.equal(kal.ops.spc.unbatched_points_to_octree(srt, level, sorted=True), octree)
+
+
+# ------------------------------------------------------------------ cfg1
+def test_cfg1_sided_2048_vs_oracle(kal):
+    """BASELINE.json configs[0] at its full size: sided_distance on two seeded U[0,1]^3 clouds of
+    2048 points (the bench's cfg1 inputs).  dist / idx bit-exact against the C oracle (the
+    reference CUDA kernel's order: 512-point tiles, strict < on the squared distance); dist equal
+    to the reference's pure-torch `_sided_distance` to its own summation order (1e-7), idx the
+    argmin with the lowest index on ties; gradients to the oracle's."""
+    from kaolin.metrics.pointcloud import _sided_distance
+    g = torch.Generator().manual_seed(0)
+    p1, p2 = torch.rand((1, 2048, 3), generator=g), torch.rand((1, 2048, 3), generator=g)
+    a = p1.to(DEV).requires_grad_(True)
+    b = p2.to(DEV).requires_grad_(True)
+    d, i = kal.metrics.pointcloud.sided_distance(a, b)
+    od, oi = orc.sided_distance_forward(p1.numpy(), p2.numpy())
+    assert np.array_equal(A(d), od) and np.array_equal(A(i), oi)
+    ref = _sided_distance(p1, p2)
+    np.testing.assert_allclose(A(d), ref.numpy(), rtol=0, atol=1e-7)
+    full = ((p1.reshape(1, -1, 1, 3).double() - p2.reshape(1, 1, -1, 3).double()) ** 2).sum(-1)
+    assert torch.equal(full.gather(2, torch.from_numpy(oi)[..., None])[..., 0], full.min(-1).values)
+    gr = torch.rand(d.shape, generator=torch.Generator().manual_seed(1)).to(DEV)
+    d.backward(gr)
+    og1, og2 = orc.sided_distance_backward(A(gr), p1.numpy(), p2.numpy(), oi)
+    np.testing.assert_allclose(A(a.grad), og1, rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(A(b.grad), og2, rtol=1e-5, atol=1e-5)

@@ -108,6 +108,85 @@ def test_rasterize_sphere_fixture(kal, golden, dname, flip, valid):
     assert_grads_equal(A(uv_r.grad), gf)
 
 
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('flip', [0, 1])
+@pytest.mark.parametrize('valid', [0, 1])
+@pytest.mark.parametrize('backend', ['cuda', 'cuda_packed'])
+def test_rasterize_list_sphere_fixture(kal, golden, dname, flip, valid, backend):
+    """test_rasterization.py:158-200,240-290 (test_cuda_{forward,backward}_with_list): features
+    as the list [face_uvs, face_mask]; the outputs are a tuple of per-element views and each
+    element gets its own gradient.  Golden features at the reference tolerance, the oracle
+    bit-exact on the concatenated features."""
+    g = golden('dibr_sphere.npz')
+    p = f'{dname}_flip{flip}_'
+    q = p + f'valid{valid}_'
+    fvz, fvi, uv = T(g[p + 'face_vertices_z']), T(g[p + 'face_vertices_image']), T(g[p + 'face_uvs'])
+    vf = T(g[p + 'valid_faces']) if valid else None
+    fvi_r = fvi.clone().requires_grad_(True)
+    uv_r = uv.clone().requires_grad_(True)
+    mask_r = torch.ones_like(uv[..., :1]).requires_grad_(True)
+    (uvs_map, mask_map), fidx = kal.render.mesh.rasterize(35, 31, fvz, fvi_r, [uv_r, mask_r], valid_faces=vf,
+                                                          backend=backend)
+    assert uvs_map.shape == uv.shape[:1] + (35, 31, 2) and mask_map.shape == uv.shape[:1] + (35, 31, 1)
+    assert np.array_equal(A(fidx), g[q + 'face_idx'])
+    np.testing.assert_allclose(A(uvs_map), g[q + 'features'], rtol=1e-5, atol=1e-5)
+    cat = np.concatenate([g[p + 'face_uvs'], np.ones_like(g[p + 'face_uvs'][..., :1])], -1)
+    of, oi, ow = orc.rasterize(35, 31, g[p + 'face_vertices_z'], g[p + 'face_vertices_image'], cat,
+                               valid_faces=g[p + 'valid_faces'] if valid else None)
+    assert np.array_equal(A(fidx), oi)
+    assert np.array_equal(A(uvs_map), of[..., :2]) and np.array_equal(A(mask_map), of[..., 2:])
+    go = np.concatenate([g[q + 'grad_out'], np.random.default_rng(2).uniform(size=of[..., 2:].shape)], -1)
+    go = go.astype(of.dtype)
+    torch.autograd.backward([uvs_map, mask_map], [T(go[..., :2]), T(go[..., 2:])])
+    gi, gf = orc.rasterize_backward(go, oi, ow, g[p + 'face_vertices_image'], cat, 1e-8)
+    assert_grads_equal(A(fvi_r.grad), gi)
+    assert_grads_equal(A(uv_r.grad), gf[..., :2])
+    assert_grads_equal(A(mask_r.grad), gf[..., 2:])
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+def test_dibr_rasterization_list_vs_oracle(kal, dtype):
+    """dibr_rasterization with the tutorial's feature list [face_uvs, ones] (dibr_tutorial.ipynb
+    cell 12) runs the single fused node: outputs and per-element gradients equal the tensor
+    call's bit for bit, and the oracle's (rasterize + soft-mask backward on the same values)."""
+    fvz, fvi, feat, fnz = _render_inputs(kal, 30, 50, 3, dtype)
+    H, W = 72, 100
+    uv, ones = feat[..., :2].contiguous(), torch.ones_like(feat[..., 2:])
+    a = fvi.clone().requires_grad_(True)
+    u = uv.clone().requires_grad_(True)
+    o = ones.clone().requires_grad_(True)
+    (fu, fo), mask, idx = kal.render.mesh.dibr_rasterization(H, W, fvz, a, [u, o], fnz)
+    assert fu.shape == (3, H, W, 2) and fo.shape == (3, H, W, 1)
+    gu, go, gm = torch.rand_like(fu), torch.rand_like(fo), torch.rand_like(mask)
+    torch.autograd.backward([fu, fo, mask], [gu, go, gm])
+    # the tensor call on the concatenated features
+    a2 = fvi.clone().requires_grad_(True)
+    f2 = torch.cat([uv, ones], -1).requires_grad_(True)
+    ft, mask2, idx2 = kal.render.mesh.dibr_rasterization(H, W, fvz, a2, f2, fnz)
+    torch.autograd.backward([ft, mask2], [torch.cat([gu, go], -1), gm])
+    assert torch.equal(idx, idx2) and torch.equal(mask, mask2)
+    assert torch.equal(fu, ft[..., :2]) and torch.equal(fo, ft[..., 2:])
+    assert torch.equal(a.grad, a2.grad)
+    assert torch.equal(u.grad, f2.grad[..., :2]) and torch.equal(o.grad, f2.grad[..., 2:])
+    # the oracle
+    cat = A(torch.cat([uv, ones], -1))
+    of, oi, ow = orc.rasterize(H, W, A(fvz), A(fvi), cat, valid_faces=A(fnz >= 0))
+    assert np.array_equal(A(idx), oi) and np.array_equal(A(fu), of[..., :2]) and np.array_equal(A(fo), of[..., 2:])
+    fm = A(fvi) * A(fvi).dtype.type(1000.)
+    pad = fm.dtype.type(0.02 * 1000.)
+    bb = np.concatenate([fm.min(-2) - pad, fm.max(-2) + pad], -1)
+    om, op, oci, oct_ = orc.dibr_soft_mask_forward(fm, bb, oi, 7000., 30, 1000.)
+    np.testing.assert_allclose(A(mask), om, rtol=1e-6, atol=1e-7)
+    from kaolin import _fused
+    _, state = _fused.soft_mask_forward_compact(fvi, idx, 7000., 0.02, 30, 1000.)
+    _, _, gp = _decode_compact(state, H, W, 30)
+    gi_r, gfe = orc.rasterize_backward(A(torch.cat([gu, go], -1)), oi, ow, A(fvi), cat, 1e-8)
+    gi = gi_r + orc.dibr_soft_mask_backward(A(gm), A(mask), oi, gp, oci, oct_, fm, 7000., 1000.)
+    assert_grads_equal(A(a.grad), gi)
+    assert_grads_equal(A(u.grad), gfe[..., :2])
+    assert_grads_equal(A(o.grad), gfe[..., 2:])
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
 @pytest.mark.parametrize('H,W', [(96, 128), (67, 45)])
 def test_packed_rasterize_vs_oracle(kal, dtype, H, W):

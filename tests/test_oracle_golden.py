@@ -48,13 +48,15 @@ def test_soft_mask_simple(golden, dtype, sig, box, knum, multiplier):
     assert np.array_equal(sel, g['selected_face_idx'])
     fm, bb = orc.soft_mask_bboxes(fvi, box, multiplier)
     mask, prob, cidx, ctype = orc.dibr_soft_mask_forward(fm, bb, sel, sig, knum, multiplier)
-    np.testing.assert_allclose(mask, g[f'soft_mask_{sig}_{box}'], atol=1e-5, rtol=1e-5)
+    # the reference's tolerance is 1e-5; the restatement is within 3.4e-6 of the reference's own
+    # CUDA outputs (the .pt goldens) on every case -- asserted at 5e-6 absolute
+    np.testing.assert_allclose(mask, g[f'soft_mask_{sig}_{box}'], atol=5e-6, rtol=0)
     assert np.array_equal(cidx, g[f'close_face_idx_{sig}_{box}'][..., :knum])
-    np.testing.assert_allclose(prob, g[f'close_face_prob_{sig}_{box}'][..., :knum], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(prob, g[f'close_face_prob_{sig}_{box}'][..., :knum], atol=5e-6, rtol=0)
     assert np.array_equal(ctype, g[f'close_face_dist_type_{sig}_{box}'][..., :knum])
     gmask = _mask_iou_grad(mask, _shifted_mask(sel))
     gimg = orc.dibr_soft_mask_backward(gmask, mask, sel, prob, cidx, ctype, fm, sig, multiplier)
-    np.testing.assert_allclose(gimg, g[f'grad_{sig}_{box}'], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(gimg, g[f'grad_{sig}_{box}'], atol=5e-6, rtol=0)
 
 
 # ------------------------------------------------------------ DIB-R sphere
@@ -62,8 +64,15 @@ def test_soft_mask_simple(golden, dtype, sig, box, knum, multiplier):
 @pytest.mark.parametrize('flip', [0, 1])
 @pytest.mark.parametrize('valid', [0, 1])
 def test_rasterize_sphere(golden, dname, flip, valid):
-    """test_rasterization.py:133-232: face_idx exact, features 1e-5,
-    grads rtol 1e-3 / atol 1e-2 (vertices), 1e-3 (features)."""
+    """test_rasterization.py:133-232 against the reference's naive oracle: face_idx exact.  The
+    reference tests allow 1e-5 (features) and rtol 1e-3 / atol 1e-2 (vertex grads), 1e-3
+    (feature grads); the restatement is asserted at its measured distance plus margin: 1.5e-6
+    features, 3e-5 vertex grads, 4e-5 feature grads (measured 9.2e-7, 2.1e-5, 2.7e-5).  The
+    residual is the naive oracle's own arithmetic, not rounding: it normalises by k3 + eps in
+    unscaled coordinates (4e-6 relative on these faces) where the CUDA kernel does it in
+    coordinates x multiplier (negligible there), and it uses exact pixel centres where the
+    kernel forms them in float.  test_rasterize_sphere_pinned removes both and pins the
+    arithmetic itself."""
     g = golden('dibr_sphere.npz')
     p = f'{dname}_flip{flip}_'
     q = p + f'valid{valid}_'
@@ -71,11 +80,36 @@ def test_rasterize_sphere(golden, dname, flip, valid):
     feat, fidx, w = orc.rasterize(35, 31, g[p + 'face_vertices_z'], g[p + 'face_vertices_image'],
                                   g[p + 'face_uvs'], valid_faces=vf)
     assert np.array_equal(fidx, g[q + 'face_idx'])
-    np.testing.assert_allclose(feat, g[q + 'features'], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(feat, g[q + 'features'], rtol=0, atol=1.5e-6)
     gimg, gfeat = orc.rasterize_backward(g[q + 'grad_out'], fidx, w, g[p + 'face_vertices_image'],
                                          g[p + 'face_uvs'], 1e-8)
-    np.testing.assert_allclose(gimg, g[q + 'grad_face_vertices_image'], rtol=1e-3, atol=1e-2)
-    np.testing.assert_allclose(gfeat, g[q + 'grad_face_uvs'], rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(gimg, g[q + 'grad_face_vertices_image'], rtol=0, atol=3e-5)
+    np.testing.assert_allclose(gfeat, g[q + 'grad_face_uvs'], rtol=0, atol=4e-5)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('flip', [0, 1])
+@pytest.mark.parametrize('valid', [0, 1])
+def test_rasterize_sphere_pinned(golden, dname, flip, valid):
+    """The same cases against the reference's naive oracle run in float64 with the CUDA
+    kernel's pixel centres and eps scaling (tests/golden/make_golden.py:dibr_sphere_scaled_eps).
+    f64: features and feature grads 1e-10, vertex grads 2e-8 (measured 2.0e-11, 2.5e-11,
+    6.3e-9 on magnitudes up to 3.6 -- the vertex gradient's k3 cancellation); f32: the
+    restatement's own float rounding, 3e-7 / 3e-6 / 2.5e-5 (measured 1.6e-7, 1.4e-6, 1.2e-5)."""
+    g = golden('dibr_sphere.npz')
+    s = golden('dibr_sphere_scaled_eps.npz')
+    p = f'{dname}_flip{flip}_'
+    q = p + f'valid{valid}_'
+    vf = g[p + 'valid_faces'] if valid else None
+    feat, fidx, w = orc.rasterize(35, 31, g[p + 'face_vertices_z'], g[p + 'face_vertices_image'],
+                                  g[p + 'face_uvs'], valid_faces=vf)
+    assert np.array_equal(fidx, s[q + 'face_idx'])
+    gimg, gfeat = orc.rasterize_backward(g[q + 'grad_out'], fidx, w, g[p + 'face_vertices_image'],
+                                         g[p + 'face_uvs'], 1e-8)
+    tol = (1e-10, 1e-10, 2e-8) if dname == 'f64' else (3e-7, 3e-6, 2.5e-5)
+    np.testing.assert_allclose(feat, s[q + 'features'], rtol=0, atol=tol[0])
+    np.testing.assert_allclose(gfeat, s[q + 'grad_face_uvs'], rtol=0, atol=tol[1])
+    np.testing.assert_allclose(gimg, s[q + 'grad_face_vertices_image'], rtol=0, atol=tol[2])
 
 
 @pytest.mark.parametrize('dname', ['f32', 'f64'])
@@ -280,3 +314,18 @@ def test_rayops_scan_matches_numpy_accumulate():
     out = orc.pack_scan(x, st, False, False, 'sum')
     for b, e in zip(st, list(st[1:]) + [50]):
         assert np.array_equal(out[b:e], np.add.accumulate(x[b:e], axis=0))
+
+
+def test_mesh_to_spc_rsqrt_substitution_cfg4():
+    """The reference normalises the SAT edges with CUDA's double rsqrt (1 ulp, not correctly
+    rounded: mesh_to_spc_cuda.cu:123-125 -> spc_math.h:240-243); the oracle and the HIP kernel
+    use 1.0 / sqrt.  At cfg4 (200k-face sphere, L=9) no decision of the 28.8M proposals flips
+    when every normalisation moves one ulp up or down (512,800 proposals have an axis within a
+    float ulp of the threshold), so the substitution cannot change the cfg4 octree.  Beyond
+    this mesh and the level-3 KAT the octree's equality with the reference is unpinned."""
+    import bench
+    verts, faces = bench.cfg4_inputs('cpu')
+    res = orc.m2s_rsqrt_sensitivity(verts[faces].numpy(), 9)
+    assert res['proposals'] == 28828416
+    assert res['near_threshold'] > 0
+    assert res['flips_ulp_up'] == 0 and res['flips_ulp_down'] == 0

@@ -189,18 +189,52 @@ def test_partial_grads_and_missing_outputs():
 
 
 @pytest.mark.gpu
-def test_out_of_range_face_index_gives_nan_not_a_fault():
+def test_out_of_range_face_index():
+    """The front-end raises torch.gather's error (index_vertices_by_faces) once per faces
+    tensor; the kernel itself, called past that check, gives NaN rows, never a fault."""
     import kaolin as kal
+    from kaolin.render.mesh.utils import PrepareVerticesHip
     verts, faces, proj, rot, trans = _scene(2, 2, seed=4, n_lat=6, n_lon=8)
     bad = faces.clone()
     bad[3, 1] = verts.shape[1] + 100
     bad[5, 0] = -1
-    fvc, fvi, fn = kal.render.mesh.prepare_vertices(verts.float().to(DEV), bad.to(DEV), proj.float().to(DEV),
-                                                    rot.float().to(DEV), trans.float().to(DEV))
+    args = [t.float().to(DEV) for t in (verts, proj, rot, trans)]
+    with pytest.raises(RuntimeError, match='out of bounds for dimension 1'):
+        kal.render.mesh.prepare_vertices(args[0], bad.to(DEV), *args[1:])
+    hi = faces.clone()
+    hi[0, 0] = verts.shape[1]
+    with pytest.raises(RuntimeError, match=f'index {verts.shape[1]} is out of bounds'):
+        kal.render.mesh.prepare_vertices(args[0], hi.to(DEV), *args[1:])
+    fvc, fvi, fn = PrepareVerticesHip.apply(args[0], bad.to(DEV), args[1], args[2], args[3], None, (2, 2, 2, 1))
     assert torch.isnan(fvc[:, 3]).all() and torch.isnan(fvc[:, 5]).all()
     good = torch.ones(faces.shape[0], dtype=torch.bool)
     good[[3, 5]] = False
     assert torch.isfinite(fvc[:, good]).all() and torch.isfinite(fn[:, good]).all()
+    # a valid faces tensor passes, and is not re-read on the next call
+    f_ok = faces.to(DEV)
+    kal.render.mesh.prepare_vertices(args[0], f_ok, *args[1:])
+    kal.render.mesh.prepare_vertices(args[0], f_ok, *args[1:])
+
+
+@pytest.mark.gpu
+def test_batch_one_vertices_and_camera_with_batched_projection():
+    """Bv == Bc == 1 < Bp: torch gives face_vertices_camera and face_normals a batch of 1 and
+    face_vertices_image a batch of Bp; the front-end returns the same shapes and gradients."""
+    import kaolin as kal
+    verts, faces, proj, rot, trans = _scene(1, 1, seed=9)
+    proj = proj.reshape(1, 3).repeat(4, 1) * (1 + 0.1 * torch.arange(4, dtype=torch.float64))[:, None]
+    leaves = [t.to(DEV).requires_grad_(True) for t in (verts, proj, rot, trans)]
+    out = kal.render.mesh.prepare_vertices(leaves[0], faces.to(DEV), *leaves[1:])
+    ref_in = [t.clone().requires_grad_(True) for t in (verts, proj, rot, trans)]
+    ref = _ref_chain(ref_in[0], faces, *ref_in[1:])
+    assert [tuple(o.shape) for o in out] == [tuple(r.shape) for r in ref]
+    assert out[0].shape[0] == 1 and out[1].shape[0] == 4 and out[2].shape[0] == 1
+    g = torch.Generator().manual_seed(3)
+    grads = [torch.rand(r.shape, generator=g, dtype=torch.float64) for r in ref]
+    torch.autograd.backward(out, [x.to(DEV) for x in grads])
+    torch.autograd.backward(ref, grads)
+    for a, b in zip(leaves, ref_in):
+        _close(a.grad, b.grad, 1e-11)
 
 
 @pytest.mark.gpu
