@@ -1143,6 +1143,26 @@ struct GatherAcc {
       }
     }
   }
+  // the same with the face's features (cf, [corner][d], stride MAXD) and the pixel's incoming
+  // gradient (g) in registers
+  __device__ __forceinline__ void add_regs(const T v[6], const T cf[3 * MAXD], int D, T w_a, T w_b, T w_c,
+                                           const T g[MAXD], float eps) {
+    BaryGrad<T> bg;
+    bg.init(v, w_a, w_b, w_c, eps);
+#pragma unroll
+    for (int d = 0; d < MAXD; d++) {
+      if (d < D) {
+        const T gd = g[d];
+        gf[d] += (double)(gd * w_a);
+        gf[MAXD + d] += (double)(gd * w_b);
+        gf[2 * MAXD + d] += (double)(gd * w_c);
+        T o[6];
+        bg.terms(gd, cf[d], cf[MAXD + d], cf[2 * MAXD + d], o);
+#pragma unroll
+        for (int q = 0; q < 6; q++) gi[q] += (double)o[q];
+      }
+    }
+  }
 };
 
 template <typename T, int MAXD, int LPF_ = LPF>
@@ -1241,6 +1261,167 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
   }
 }
 
+// ---------------------------------------------------------------- tile-owner gather
+// The same per-face sums as rasterize_bwd_gather_kernel, organised by screen tile so that the
+// pixel data comes from LDS instead of a chain of dependent global loads per face.
+//   * A face is OWNED by the 64x8 tile holding the top-left corner (ix0, iy0) of its exact pixel
+//     range (the forward's face_ranges): exactly one tile per face with a non-empty range.
+//   * One 256-thread workgroup per tile stages the tile's face index (as int32), weights and
+//     incoming gradients in LDS with coalesced loads, then walks the tile's candidate chunks
+//     (the forward's rasterizer bin bitmap, saved with the state), keeps the faces it owns and
+//     sums each over its whole range, 8 lanes per face: pixels inside the tile from LDS, the
+//     few outside it (faces reaching into the tile below / to the right) from global memory.
+//   * Each face has one writer and a fixed lane order (the butterfly), so the sums are the
+//     gather kernel's exactly (double, rounded once); no atomics.
+//   * Faces without a range (culled, off screen) get zero gradients from the workgroups'
+//     slices of the face list; ranges over VIS_SMALL_AREA pixels are queued for the workgroup-
+//     per-face kernel as before.
+// Tiles are placed XCD-banded: block k runs on XCD k % 8 and takes tile (k % 8) * per + k / 8,
+// so one XCD's L2 serves a band of neighbouring tiles (the out-of-tile reads hit their data).
+constexpr int BT_THREADS = 256;
+constexpr int BT_PX = TILE_W * TILE_H;  // 512 pixels per tile, 2 per thread
+
+template <typename T, int MAXD>
+__global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
+    const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
+    const T *__restrict__ fvi, const T *__restrict__ feat, BinGeom g, int F, int D, float eps,
+    T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig,
+    const uint2 *__restrict__ rng, const uint32_t *__restrict__ bins, int per_band, int faces_per_block) {
+  __shared__ int s_idx[BT_PX];
+  __shared__ T s_w[BT_PX * 3];
+  __shared__ T s_g[BT_PX * MAXD];
+  __shared__ int s_own[BT_THREADS / 64][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int H = g.height, W = g.width;
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  const int64_t nf = (int64_t)g.batch * F;
+  // faces without a range: zero gradients (this block's slice of the face list)
+  for (int64_t k = (int64_t)blockIdx.x * faces_per_block + threadIdx.x;
+       k < min(nf, (int64_t)(blockIdx.x + 1) * faces_per_block); k += BT_THREADS) {
+    int a0, a1, b0, b1;
+    if (rng_range(rng, k, a0, a1, b0, b1)) continue;
+#pragma unroll
+    for (int q = 0; q < 6; q++) grad_fvi[k * 6 + q] = (T)0;
+    for (int q = 0; q < 3 * D; q++) grad_ffeat[k * 3 * D + q] = (T)0;
+  }
+  const int tile = (int)(blockIdx.x % 8) * per_band + (int)(blockIdx.x / 8);
+  if (tile >= nt) return;
+  const int tx = tile % g.tiles_x;
+  const int ty = (tile / g.tiles_x) % g.tiles_y;
+  const int b = tile / (g.tiles_x * g.tiles_y);
+  const int i0 = tx * TILE_W, j0 = ty * TILE_H;
+  const int64_t pbase = (int64_t)b * H * W;
+  // ---- stage the tile's pixels (2 per thread; rows of 64 are contiguous in memory)
+  for (int p = threadIdx.x; p < BT_PX; p += BT_THREADS) {
+    const int j = j0 + p / TILE_W, i = i0 + p % TILE_W;
+    int id = -1;
+    if (j < H && i < W) {
+      const int64_t px = pbase + (int64_t)j * W + i;
+      id = (int)face_idx[px];
+      if (id >= 0) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) s_w[p * 3 + q] = wts[px * 3 + q];
+#pragma unroll
+        for (int d = 0; d < MAXD; d++)
+          if (d < D) s_g[p * MAXD + d] = grad_feat[px * D + d];
+      }
+    }
+    s_idx[p] = id;
+  }
+  __syncthreads();
+  // ---- owned faces: the tile's candidate chunks, one per wave and step
+  ChunkSeq seq;
+  seq.init(bins + (size_t)tile * g.words, g.words, lane);
+  const int64_t f0 = (int64_t)b * F;
+  const int grp = lane >> 3, s = lane & 7;  // 8 faces per wave at a time, 8 lanes each
+  for (int pos = wid;; pos += BT_THREADS / 64) {
+    const int c = seq.at(pos, lane);  // wave-uniform; chunks ascend with pos
+    if (c < 0) break;
+    const int fl = c * 64 + lane;
+    int ix0 = 1, ix1 = 0, iy0 = 1, iy1 = 0;
+    const bool owned = fl < F && rng_range(rng, f0 + fl, ix0, ix1, iy0, iy1) && ix0 / TILE_W == tx &&
+                       iy0 / TILE_H == ty;
+    const uint64_t om = ballot(owned);
+    const int n = __popcll(om);
+    if (owned)
+      s_own[wid][(int)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u))] =
+          fl;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    for (int k0 = 0; k0 < n; k0 += 8) {
+      const int k = k0 + grp;
+      const bool act = k < n;
+      const int f = act ? s_own[wid][k] : 0;
+      const int64_t tf = f0 + f;
+      int a0 = 1, a1 = 0, b0 = 1, b1 = 0;
+      if (act) rng_range(rng, tf, a0, a1, b0, b1);
+      GatherAcc<T, MAXD> acc;
+      acc.zero();
+      const bool is_big = act && (int64_t)(a1 - a0 + 1) * (b1 - b0 + 1) > VIS_SMALL_AREA;
+      if (is_big && s == 0) big[atomicAdd(nbig, 1)] = (int)tf;
+      if (act && !is_big) {
+        T v[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
+        T cf[3 * MAXD];  // the face's features, [corner][d] with stride MAXD
+#pragma unroll
+        for (int q = 0; q < 3 * MAXD; q++) cf[q] = (q % MAXD) < D ? feat[tf * 3 * D + (q / MAXD) * D + q % MAXD] : (T)0;
+        RangeWalkN<8> rw(a0, a1, b0, b1, s);
+        while (rw.more()) {
+          const int j = b0 + rw.row, i = a0 + rw.col;
+          T wa, wb, wc, gl[MAXD];
+          bool hit;
+          if (i < i0 + TILE_W && j < j0 + TILE_H) {
+            const int p = (j - j0) * TILE_W + (i - i0);
+            hit = s_idx[p] == f;
+            if (hit) {
+              wa = s_w[p * 3];
+              wb = s_w[p * 3 + 1];
+              wc = s_w[p * 3 + 2];
+#pragma unroll
+              for (int d = 0; d < MAXD; d++) gl[d] = s_g[p * MAXD + d];
+            }
+          } else {
+            const int64_t px = pbase + (int64_t)j * W + i;
+            hit = face_idx[px] == f;
+            if (hit) {
+              wa = wts[px * 3];
+              wb = wts[px * 3 + 1];
+              wc = wts[px * 3 + 2];
+#pragma unroll
+              for (int d = 0; d < MAXD; d++) gl[d] = d < D ? grad_feat[px * D + d] : (T)0;
+            }
+          }
+          if (hit) acc.add_regs(v, cf, D, wa, wb, wc, gl, eps);
+          rw.next();
+        }
+      }
+      // fixed-order butterfly over the face's 8 lanes
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+#pragma unroll
+        for (int q = 0; q < 6; q++) acc.gi[q] += __shfl_xor(acc.gi[q], o);
+#pragma unroll
+        for (int q = 0; q < 3 * MAXD; q++) acc.gf[q] += __shfl_xor(acc.gf[q], o);
+      }
+      if (act && !is_big) {
+#pragma unroll
+        for (int q = 0; q < 6 + 3 * MAXD; q++) {
+          if (q % 8 != s) continue;
+          if (q < 6) {
+            grad_fvi[tf * 6 + q] = (T)acc.gi[q];
+          } else {
+            const int r = q - 6, ii = r / MAXD, d = r % MAXD;
+            if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)acc.gf[r];
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // s_own is rewritten by the wave's next chunk
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+}
+
 // one 256-thread workgroup per large face; block reduction of the per-thread partials
 template <typename T, int MAXD>
 __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
@@ -1327,9 +1508,24 @@ template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
                                      const T *w, const T *fvi, const T *feat, const uint8_t *valid, const T *nz,
                                      float m, float eps, T *gfvi, T *gfeat, int *big, int *nbig, bool zero_nbig,
-                                     const uint2 *rng, const double *soft, hipStream_t st) {
+                                     const uint2 *rng, const double *soft, hipStream_t st,
+                                     const uint32_t *bins = nullptr) {
   if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
+  if (bins && rng && !soft && !(g_dev_flags & (1 << 17))) {  // tile-owner gather (dev bit 17: the per-face one)
+    const BinGeom g = make_bin_geom(B, H, W, F);
+    const int nt = g.batch * g.tiles_y * g.tiles_x;
+    const int per_band = (int)cdiv(nt, 8);
+    const int grid = 8 * per_band;
+    const int fpb = (int)cdiv(nf, grid);
+    hipLaunchKernelGGL((rasterize_bwd_tile_kernel<T, MAXD>), dim3((unsigned)grid), dim3(BT_THREADS), 0, st, grad,
+                       face_idx, w, fvi, feat, g, F, D, eps, gfvi, gfeat, big, nbig, rng, bins, per_band, fpb);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(256), dim3(256), 0, st, grad, face_idx, w, fvi,
+                       feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
+    KL_CHECK_LAUNCH();
+    return KL_OK;
+  }
   // 8 lanes per face (measured: 4 lanes 62.7 us, 8 lanes 58 us, 16 lanes 91 us at cfg3)
   hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st,
                      grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
@@ -1346,7 +1542,8 @@ template <typename T>
 static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
                                 const void *w, const void *fvi, const void *feat, const uint8_t *valid, const T *nz,
                                 float m, float eps, void *gfvi, void *gfeat, void *ws, size_t ws_bytes, int *nbig,
-                                hipStream_t st, const uint2 *rng = nullptr, const double *soft = nullptr) {
+                                hipStream_t st, const uint2 *rng = nullptr, const double *soft = nullptr,
+                                const uint32_t *bins = nullptr) {
   const int64_t nf = (int64_t)B * F;
   if (nf == 0) return KL_OK;
   if (D > 8) {  // wide features: the scatter kernel
@@ -1365,15 +1562,15 @@ static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *g
   // MAXD = D where it is small (the accumulators are doubles: registers set the occupancy)
   if (D <= 2)
     return rasterize_bwd_gather_maxd<T, 2>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, st, bins);
   if (D == 3)
     return rasterize_bwd_gather_maxd<T, 3>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, st, bins);
   if (D <= 4)
     return rasterize_bwd_gather_maxd<T, 4>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, st, bins);
   return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                         (T *)gfeat, big, nbig, zero, rng, soft, st);
+                                         (T *)gfeat, big, nbig, zero, rng, soft, st, bins);
 }
 
 // The fused front-end path's forward: the tile rasterizer (dev flag bit 13 selects the
@@ -1531,7 +1728,7 @@ template <typename T>
 static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, const T *fvi, const T *feat, const T *fnz,
                     float sigmainv, double pad, float m, float eps, T *out_feat, int64_t *out_idx, T *out_w,
                     T *out_mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st,
-                    uint2 *face_ranges) {
+                    uint2 *face_ranges, uint32_t *raster_bins) {
   const DibrFwdWs L(B, H, W, F);
   KL_REQUIRE(ws_bytes >= L.bytes, "dibr_rasterization forward: workspace too small");
   KL_REQUIRE(H < 65536 && W < 65536, "dibr_rasterization forward: height and width must be < 65536");
@@ -1540,7 +1737,8 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const size_t P = (size_t)B * H * W;
   if (P == 0) return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
   if (F == 0 || (g_dev_flags & (1 << 13))) {  // no faces (or dev: the separate pipelines)
-    KL_REQUIRE(face_ranges == nullptr || F == 0, "dibr_rasterization forward: face_ranges needs the combined path");
+    KL_REQUIRE((face_ranges == nullptr && raster_bins == nullptr) || F == 0,
+               "dibr_rasterization forward: face_ranges / raster_bins need the combined path");
     KL_CHECK_RC(dibr_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, F, fvz, feat, m, eps, out_feat,
                                  out_idx, out_w, ws, ws_bytes, st));
     return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, ws, ws_bytes, st);
@@ -1548,7 +1746,9 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   char *w = reinterpret_cast<char *>(ws);
-  uint32_t *rbm = reinterpret_cast<uint32_t *>(w);
+  // the rasterizer's bins go to the caller's buffer when given (kept for the backward's
+  // tile-owner gather), else to the workspace
+  uint32_t *rbm = raster_bins ? raster_bins : reinterpret_cast<uint32_t *>(w);
   uint32_t *sbm = reinterpret_cast<uint32_t *>(w + L.off_sbm);
   int *rgh = reinterpret_cast<int *>(w + L.off_rgh);
   int *sgh = reinterpret_cast<int *>(w + L.off_sgh);
@@ -1568,6 +1768,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
                                    (int)((L.zero - L.off_rgh) / sizeof(int)), st));  // + histograms zeroed
   } else {
   KL_CHECK_RC(fill_async(w, 0, L.zero, st));
+  if (raster_bins) KL_CHECK_RC(fill_async(raster_bins, 0, g.bytes(), st));
   const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);
   if (fnz)
     hipLaunchKernelGGL((raster_bin_kernel<T, 2>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, rbm, rec, rng, sbm,
@@ -1602,7 +1803,7 @@ template <typename T>
 static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat, const T *grad_mask,
                     const int64_t *face_idx, const T *w, const T *fvi, const T *feat, const T *fnz, const T *mask,
                     const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *ws,
-                    size_t ws_bytes, hipStream_t st, const uint2 *face_ranges) {
+                    size_t ws_bytes, hipStream_t st, const uint2 *face_ranges, const uint32_t *raster_bins) {
   KL_REQUIRE(D <= 8, "dibr_rasterization backward: feature dimension > 8 is not supported by the fused path");
   // workspace: the soft mask's double sums | its items | the gather's big-face list
   const size_t acc_bytes = al256((size_t)B * F * 6 * sizeof(double));
@@ -1625,7 +1826,7 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
                                     soft_bytes, fork.side(), acc, &has_soft));
   KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
                                       gfeat, gath_ws, ws_bytes - acc_bytes - soft_bytes, s.scratch, st, face_ranges,
-                                      nullptr));
+                                      nullptr, face_ranges ? raster_bins : nullptr));
   KL_CHECK_RC(fork.join());
   return has_soft ? acc_finalize<T>(acc, gfvi, (size_t)B * F * 6, true, st, s.scratch)
                   : (s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK);
@@ -1639,6 +1840,10 @@ extern "C" size_t kl_dibr_workspace_bytes(int batch, int height, int width, int 
   return std::max(a, std::max(b, c));
 }
 
+extern "C" size_t kl_dibr_bins_bytes(int batch, int height, int width, int num_faces) {
+  return make_bin_geom(batch, height, width, num_faces).bytes();
+}
+
 extern "C" size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum) {
   const size_t a = kl_dibr_rasterize_bwd_workspace_bytes(batch, height, width, num_faces, 8);
   const size_t b = soft_tile_bwd_items_bytes(batch, height, width, knum);
@@ -1649,21 +1854,21 @@ extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width,
                                int knum, const void *fvz, const void *fvi, const void *feat, const void *fnz,
                                float sigmainv, double bbox_pad, float multiplier, float eps, void *out_feat,
                                int64_t *out_idx, void *out_w, void *out_mask, uint8_t *hits, uint32_t *rec_face,
-                               void *rec_prob, int *seg_tot, int *scratch, uint32_t *face_ranges, void *ws,
-                               size_t ws_bytes, kl_stream stream) {
+                               void *rec_prob, int *seg_tot, int *scratch, uint32_t *face_ranges,
+                               uint32_t *raster_bins, void *ws, size_t ws_bytes, kl_stream stream) {
   uint2 *fr = reinterpret_cast<uint2 *>(face_ranges);
   if (dtype == KL_F32)
     return dibr_fwd<float>(batch, height, width, num_faces, feat_dim, knum, (const float *)fvz, (const float *)fvi,
                            (const float *)feat, (const float *)fnz, sigmainv, bbox_pad, multiplier, eps,
                            (float *)out_feat, out_idx, (float *)out_w, (float *)out_mask,
                            SoftState<float>{hits, rec_face, (float *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
-                           S(stream), fr);
+                           S(stream), fr, raster_bins);
   if (dtype == KL_F64)
     return dibr_fwd<double>(batch, height, width, num_faces, feat_dim, knum, (const double *)fvz, (const double *)fvi,
                             (const double *)feat, (const double *)fnz, sigmainv, bbox_pad, multiplier, eps,
                             (double *)out_feat, out_idx, (double *)out_w, (double *)out_mask,
                             SoftState<double>{hits, rec_face, (double *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
-                            S(stream), fr);
+                            S(stream), fr, raster_bins);
   set_error("dibr_rasterization not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -1673,22 +1878,22 @@ extern "C" int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width
                                 const void *w, const void *fvi, const void *feat, const void *fnz, const void *mask,
                                 const uint8_t *hits, const uint32_t *rec_face, const void *rec_prob,
                                 const int *seg_tot, float sigmainv, float multiplier, float eps, void *gfvi,
-                                void *gfeat, int *scratch, const uint32_t *face_ranges, void *ws, size_t ws_bytes,
-                                kl_stream stream) {
+                                void *gfeat, int *scratch, const uint32_t *face_ranges, const uint32_t *raster_bins,
+                                void *ws, size_t ws_bytes, kl_stream stream) {
   const uint2 *fr = reinterpret_cast<const uint2 *>(face_ranges);
   if (dtype == KL_F32)
     return dibr_bwd<float>(
         batch, height, width, num_faces, feat_dim, knum, (const float *)grad_feat, (const float *)grad_mask, face_idx,
         (const float *)w, (const float *)fvi, (const float *)feat, (const float *)fnz, (const float *)mask,
         SoftState<float>{(uint8_t *)hits, (uint32_t *)rec_face, (float *)rec_prob, (int *)seg_tot, scratch},
-        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream), fr);
+        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream), fr, raster_bins);
   if (dtype == KL_F64)
     return dibr_bwd<double>(
         batch, height, width, num_faces, feat_dim, knum, (const double *)grad_feat, (const double *)grad_mask,
         face_idx, (const double *)w, (const double *)fvi, (const double *)feat, (const double *)fnz,
         (const double *)mask,
         SoftState<double>{(uint8_t *)hits, (uint32_t *)rec_face, (double *)rec_prob, (int *)seg_tot, scratch},
-        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream), fr);
+        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream), fr, raster_bins);
   set_error("dibr_rasterization backward not implemented for this dtype");
   return KL_E_INVALID;
 }

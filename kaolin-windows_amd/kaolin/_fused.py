@@ -12,8 +12,7 @@ import torch
 from . import _native as N
 
 
-def _ws(nbytes, device):
-    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=device)
+_ws = N.workspace
 
 
 def _valid_u8(valid_faces):
@@ -201,7 +200,7 @@ def soft_mask_backward_compact(grad, mask, state, face_vertices_image, sigmainv,
 
 
 def dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, face_vertices_image, face_features, face_normals_z,
-                  soft_mask, state, sigmainv, multiplier, eps, face_ranges=None):
+                  soft_mask, state, sigmainv, multiplier, eps, face_ranges=None, raster_bins=None):
     """dibr_rasterization's backward in one call (kl_dibr_backward): the soft-mask terms summed in
     double first, then the rasterizer's gather writes every face's gradient as its own rounded
     sum plus the soft mask's (as autograd adds the two).  grad_soft_mask may be None.
@@ -222,7 +221,7 @@ def dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, face_vertices_i
             N.ptr(gm), N.ptr(face_idx), N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features),
             N.ptr(face_normals_z), N.ptr(soft_mask), N.ptr(state.hits), N.ptr(state.rec_face), N.ptr(state.rec_prob),
             N.ptr(state.seg_tot), float(sigmainv), float(multiplier), float(eps), N.ptr(g_img), N.ptr(g_feat),
-            N.ptr(state.scratch), N.ptr(face_ranges), N.ptr(ws), nbytes, N.stream_of(dev)), func)
+            N.ptr(state.scratch), N.ptr(face_ranges), N.ptr(raster_bins), N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return g_img, g_feat
 
 
@@ -231,7 +230,8 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     """dibr_rasterization's forward in one call (kl_dibr_forward): rasterize with valid =
     face_normals_z >= 0 and the compact soft mask, sharing one binning pass.
     -> features (B,H,W,D), face_idx (B,H,W), weights (B,H,W,3), soft_mask (B,H,W), SoftMaskState,
-    face_ranges (B,F,2) int32 (each face's exact pixel ranges, for rasterize_backward).
+    face_ranges (B,F,2) int32 (each face's exact pixel ranges, for rasterize_backward), raster_bins
+    (uint8, the rasterizer's screen bins: with face_ranges, the backward's gather runs per tile).
     face_normals_z must have the dtype of face_vertices_image."""
     func = 'dibr_rasterization'
     N.require_gpu(func, face_vertices_z, face_vertices_image, face_normals_z)
@@ -258,6 +258,7 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     seg_tot = torch.empty(max(lib.kl_soft_mask_compact_segments(B, H, W), 1), dtype=torch.int32, device=dev)
     scratch = torch.empty(1, dtype=torch.int32, device=dev)
     ranges = torch.empty((B, F, 2), dtype=torch.int32, device=dev)
+    bins = torch.empty(max(lib.kl_dibr_bins_bytes(B, H, W, F), 4), dtype=torch.uint8, device=dev)
     nbytes = lib.kl_dibr_workspace_bytes(B, H, W, F)
     ws = _ws(nbytes, dev)
     with N.on_device(dev), N.timed('dibr_forward', dev):
@@ -265,5 +266,6 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
             N.dtype_code(dtype), B, H, W, F, D, K, N.ptr(fvz), N.ptr(fvi), N.ptr(feat), N.ptr(fnz), float(sigmainv),
             float(boxlen * multiplier), float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w),
             N.ptr(mask), N.ptr(hits), N.ptr(rec_face), N.ptr(rec_prob), N.ptr(seg_tot), N.ptr(scratch),
-            N.ptr(ranges if F > 0 else None), N.ptr(ws), nbytes, N.stream_of(dev)), func)
-    return feats, idx, w, mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, scratch, K), ranges
+            N.ptr(ranges if F > 0 else None), N.ptr(bins if F > 0 else None), N.ptr(ws), nbytes, N.stream_of(dev)),
+            func)
+    return feats, idx, w, mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, scratch, K), ranges, bins

@@ -14,7 +14,7 @@ _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib')
 # `make STAMPS=1 OUT=...`); the default is the in-tree build
 LIB_PATH = os.environ.get('KAOLIN_HIP_LIB') or os.path.join(_LIB_DIR, 'libkaolin_hip.so')
 
-ABI_VERSION = 2  # include/kaolin_hip.h KL_ABI_VERSION: the signatures below
+ABI_VERSION = 3  # include/kaolin_hip.h KL_ABI_VERSION: the signatures below
 
 KL_F32, KL_F64, KL_F16, KL_U8, KL_I8, KL_I16, KL_I32, KL_I64 = range(8)
 _DTYPES = {
@@ -65,10 +65,11 @@ _SIGS = {
                                                 _P, _P, _SZ, _P]),
     'kl_dibr_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'kl_dibr_bwd_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
+    'kl_dibr_bins_bytes': (_SZ, [_I, _I, _I, _I]),
     'kl_dibr_forward': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, ctypes.c_double, _F, _F, _P, _P, _P,
-                             _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+                             _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_backward': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F,
-                              _F, _P, _P, _P, _P, _P, _SZ, _P]),
+                              _F, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_forward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _SZ,
                                         _P]),
@@ -156,11 +157,34 @@ def check(rc, func):
 
 
 def ptr(t):
-    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+    """Device pointer of a tensor for a c_void_p argument (a plain int: ctypes converts it)."""
+    return t.data_ptr() if t is not None else None
+
+
+_raw_stream = torch._C._cuda_getCurrentRawStream
 
 
 def stream_of(device):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The current HIP stream of `device` as a pointer-sized int (the raw handle: no Stream object)."""
+    idx = device.index
+    return _raw_stream(torch.cuda.current_device() if idx is None else idx)
+
+
+_WS = {}
+
+
+def workspace(nbytes, device):
+    """Scratch for one library call, reused across calls on the same (device, stream): every entry
+    point treats its workspace as uninitialised and is done with it when the stream reaches the
+    call's end, so stream order makes reuse safe.  Grows to the largest request; the current
+    stream is part of the key (graph capture has its own stream, hence its own buffer)."""
+    nbytes = max(int(nbytes), 16)
+    key = (device.index, stream_of(device))
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        _WS[key] = t
+    return t
 
 
 def require_gpu(func, *tensors):
