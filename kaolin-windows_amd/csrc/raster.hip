@@ -1728,7 +1728,7 @@ template <typename T>
 static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, const T *fvi, const T *feat, const T *fnz,
                     float sigmainv, double pad, float m, float eps, T *out_feat, int64_t *out_idx, T *out_w,
                     T *out_mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st,
-                    uint2 *face_ranges, uint32_t *raster_bins) {
+                    uint2 *face_ranges, uint32_t *raster_bins, uint2 *soft_ranges) {
   const DibrFwdWs L(B, H, W, F);
   KL_REQUIRE(ws_bytes >= L.bytes, "dibr_rasterization forward: workspace too small");
   KL_REQUIRE(H < 65536 && W < 65536, "dibr_rasterization forward: height and width must be < 65536");
@@ -1737,8 +1737,8 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const size_t P = (size_t)B * H * W;
   if (P == 0) return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
   if (F == 0 || (g_dev_flags & (1 << 13))) {  // no faces (or dev: the separate pipelines)
-    KL_REQUIRE((face_ranges == nullptr && raster_bins == nullptr) || F == 0,
-               "dibr_rasterization forward: face_ranges / raster_bins need the combined path");
+    KL_REQUIRE((face_ranges == nullptr && raster_bins == nullptr && soft_ranges == nullptr) || F == 0,
+               "dibr_rasterization forward: face_ranges / raster_bins / soft_ranges need the combined path");
     KL_CHECK_RC(dibr_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, F, fvz, feat, m, eps, out_feat,
                                  out_idx, out_w, ws, ws_bytes, st));
     return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, ws, ws_bytes, st);
@@ -1760,7 +1760,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   int *nitems = reinterpret_cast<int *>(w + L.off_n);
   int32_t *sorder = reinterpret_cast<int32_t *>(w + L.off_sorder);
   int *snitems = reinterpret_cast<int *>(w + L.off_sn);
-  uint2 *srng = reinterpret_cast<uint2 *>(w + L.off_srng);
+  uint2 *srng = soft_ranges ? soft_ranges : reinterpret_cast<uint2 *>(w + L.off_srng);
   const RastSrc<T> src{fvi, nullptr, (T)m, fnz};
   const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
   if (bin_word_lds_ok(g) && !(g_dev_flags & (1 << 14))) {  // dev bit 14: the atomic binning
@@ -1803,8 +1803,35 @@ template <typename T>
 static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat, const T *grad_mask,
                     const int64_t *face_idx, const T *w, const T *fvi, const T *feat, const T *fnz, const T *mask,
                     const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *ws,
-                    size_t ws_bytes, hipStream_t st, const uint2 *face_ranges, const uint32_t *raster_bins) {
+                    size_t ws_bytes, hipStream_t st, const uint2 *face_ranges, const uint32_t *raster_bins,
+                    const uint2 *soft_ranges) {
   KL_REQUIRE(D <= 8, "dibr_rasterization backward: feature dimension > 8 is not supported by the fused path");
+  if (soft_ranges && !(g_dev_flags & (1 << 18))) {  // dev bit 18: the atomic soft flush below
+    // The two halves are independent until the final add, so they run concurrently: the
+    // soft-mask sums (zero fill, per-tile slot kernel; left in double) on the side stream, the
+    // rasterizer's gather (every face's own rounded gradient) on `st`; after the join each
+    // coordinate gets the soft sum rounded on its own and added, as autograd adds the two
+    // gradients.  The gather's big-face counter is the state's scratch int (zeroed by the
+    // forward), re-zeroed by that final add.
+    const size_t slot_bytes = al256(soft_slots_ws_bytes(B, F));
+    KL_REQUIRE(ws_bytes >= slot_bytes, "dibr_rasterization backward: workspace too small");
+    void *gath_ws = reinterpret_cast<char *>(ws) + slot_bytes;
+    const bool has_soft = grad_mask != nullptr && K > 0 && (int64_t)B * H * W > 0;
+    if (has_soft) {
+      SideFork fork(st);
+      KL_CHECK_RC(soft_tile_backward_slots<T>(B, H, W, F, K, grad_mask, mask, s, fvi, soft_ranges, sigmainv, m, ws,
+                                              slot_bytes, fork.side()));
+      KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps,
+                                          gfvi, gfeat, gath_ws, ws_bytes - slot_bytes, s.scratch, st, face_ranges,
+                                          nullptr, face_ranges ? raster_bins : nullptr));
+      KL_CHECK_RC(fork.join());
+      return soft_slots_combine<T>(B, F, gfvi, ws, s.scratch, st);
+    }
+    KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
+                                        gfeat, gath_ws, ws_bytes - slot_bytes, s.scratch, st, face_ranges, nullptr,
+                                        face_ranges ? raster_bins : nullptr));
+    return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
+  }
   // workspace: the soft mask's double sums | its items | the gather's big-face list
   const size_t acc_bytes = al256((size_t)B * F * 6 * sizeof(double));
   const size_t soft_bytes = al256(soft_tile_bwd_items_bytes(B, H, W, K));
@@ -1813,12 +1840,6 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
   void *soft_ws = reinterpret_cast<char *>(ws) + acc_bytes;
   void *gath_ws = reinterpret_cast<char *>(soft_ws) + soft_bytes;
   bool has_soft = false;
-  // The two halves are independent until the final add, so they run concurrently: the
-  // soft-mask sums (fill, plan, backward; left in double) on the side stream, the
-  // rasterizer's gather (every face's own rounded gradient) on `st`; after the join each
-  // coordinate gets the soft sum rounded on its own and added, as autograd adds the two
-  // gradients.  The gather's big-face counter is the state's scratch int (zeroed by the
-  // forward), re-zeroed by that final add; the soft half does not touch it.
   SideFork fork(st);
   SoftState<T> ss = s;
   ss.scratch = nullptr;
@@ -1847,7 +1868,9 @@ extern "C" size_t kl_dibr_bins_bytes(int batch, int height, int width, int num_f
 extern "C" size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum) {
   const size_t a = kl_dibr_rasterize_bwd_workspace_bytes(batch, height, width, num_faces, 8);
   const size_t b = soft_tile_bwd_items_bytes(batch, height, width, knum);
-  return al256((size_t)batch * num_faces * 6 * sizeof(double)) + al256(b) + a;
+  const size_t atomic_path = al256((size_t)batch * num_faces * 6 * sizeof(double)) + al256(b) + a;
+  const size_t slot_path = al256(soft_slots_ws_bytes(batch, num_faces)) + a;
+  return std::max(atomic_path, slot_path);
 }
 
 extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
@@ -1855,20 +1878,22 @@ extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width,
                                float sigmainv, double bbox_pad, float multiplier, float eps, void *out_feat,
                                int64_t *out_idx, void *out_w, void *out_mask, uint8_t *hits, uint32_t *rec_face,
                                void *rec_prob, int *seg_tot, int *scratch, uint32_t *face_ranges,
-                               uint32_t *raster_bins, void *ws, size_t ws_bytes, kl_stream stream) {
+                               uint32_t *raster_bins, uint32_t *soft_ranges, void *ws, size_t ws_bytes,
+                               kl_stream stream) {
   uint2 *fr = reinterpret_cast<uint2 *>(face_ranges);
+  uint2 *sr = reinterpret_cast<uint2 *>(soft_ranges);
   if (dtype == KL_F32)
     return dibr_fwd<float>(batch, height, width, num_faces, feat_dim, knum, (const float *)fvz, (const float *)fvi,
                            (const float *)feat, (const float *)fnz, sigmainv, bbox_pad, multiplier, eps,
                            (float *)out_feat, out_idx, (float *)out_w, (float *)out_mask,
                            SoftState<float>{hits, rec_face, (float *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
-                           S(stream), fr, raster_bins);
+                           S(stream), fr, raster_bins, sr);
   if (dtype == KL_F64)
     return dibr_fwd<double>(batch, height, width, num_faces, feat_dim, knum, (const double *)fvz, (const double *)fvi,
                             (const double *)feat, (const double *)fnz, sigmainv, bbox_pad, multiplier, eps,
                             (double *)out_feat, out_idx, (double *)out_w, (double *)out_mask,
                             SoftState<double>{hits, rec_face, (double *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
-                            S(stream), fr, raster_bins);
+                            S(stream), fr, raster_bins, sr);
   set_error("dibr_rasterization not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -1879,21 +1904,22 @@ extern "C" int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width
                                 const uint8_t *hits, const uint32_t *rec_face, const void *rec_prob,
                                 const int *seg_tot, float sigmainv, float multiplier, float eps, void *gfvi,
                                 void *gfeat, int *scratch, const uint32_t *face_ranges, const uint32_t *raster_bins,
-                                void *ws, size_t ws_bytes, kl_stream stream) {
+                                const uint32_t *soft_ranges, void *ws, size_t ws_bytes, kl_stream stream) {
   const uint2 *fr = reinterpret_cast<const uint2 *>(face_ranges);
+  const uint2 *sr = reinterpret_cast<const uint2 *>(soft_ranges);
   if (dtype == KL_F32)
     return dibr_bwd<float>(
         batch, height, width, num_faces, feat_dim, knum, (const float *)grad_feat, (const float *)grad_mask, face_idx,
         (const float *)w, (const float *)fvi, (const float *)feat, (const float *)fnz, (const float *)mask,
         SoftState<float>{(uint8_t *)hits, (uint32_t *)rec_face, (float *)rec_prob, (int *)seg_tot, scratch},
-        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream), fr, raster_bins);
+        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream), fr, raster_bins, sr);
   if (dtype == KL_F64)
     return dibr_bwd<double>(
         batch, height, width, num_faces, feat_dim, knum, (const double *)grad_feat, (const double *)grad_mask,
         face_idx, (const double *)w, (const double *)fvi, (const double *)feat, (const double *)fnz,
         (const double *)mask,
         SoftState<double>{(uint8_t *)hits, (uint32_t *)rec_face, (double *)rec_prob, (int *)seg_tot, scratch},
-        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream), fr, raster_bins);
+        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream), fr, raster_bins, sr);
   set_error("dibr_rasterization backward not implemented for this dtype");
   return KL_E_INVALID;
 }

@@ -67,9 +67,9 @@ _SIGS = {
     'kl_dibr_bwd_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'kl_dibr_bins_bytes': (_SZ, [_I, _I, _I, _I]),
     'kl_dibr_forward': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, ctypes.c_double, _F, _F, _P, _P, _P,
-                             _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+                             _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_backward': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F,
-                              _F, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+                              _F, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_forward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _SZ,
                                         _P]),

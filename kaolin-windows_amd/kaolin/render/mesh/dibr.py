@@ -98,7 +98,8 @@ class DibrRasterizationCuda(Function):
                                                  soft_mask, state, ctx.sigmainv, ctx.multiplier, ctx.eps, ranges, bins)
         else:  # face_normals_z of another dtype: the two stages (the rasterizer's reads a valid mask)
             g_img, g_feat = _fused.rasterize_backward(grad_feats, face_idx, weights, fvi, feat, None, ctx.multiplier,
-                                                      ctx.eps, face_normals_z=fnz, face_ranges=ranges)
+                                                      ctx.eps, face_normals_z=fnz,
+                                                      face_ranges=None if ranges is None else ranges[0])
             if grad_soft_mask is not None:
                 _fused.soft_mask_backward_compact(grad_soft_mask, soft_mask, state, fvi, ctx.sigmainv,
                                                   ctx.multiplier, out=g_img)

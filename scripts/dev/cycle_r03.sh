@@ -1,11 +1,11 @@
 #!/bin/bash
 # r03 development cycle: selected GPU tests, a short bench line, rocprofv3 kernel stats of it.
-# usage: TESTS='-k expr' OUT=gpurun_out/x bash scripts/dev/cycle_r03.sh
+# usage: TESTS='tests/x.py' TESTK='expr' OUT=gpurun_out/x bash scripts/dev/cycle_r03.sh
 set -e
 OUT=${OUT:-gpurun_out/r03}
 mkdir -p "$OUT"
 ROOT=$(pwd)
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${TESTS:-} > "$OUT/tests.log" 2>&1
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 120 --timeout-method thread ${TESTK:+-k "$TESTK"} > "$OUT/tests.log" 2>&1
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra --no-p2m ${BENCH_ARGS:-} > "$OUT/bench.json" 2> "$OUT/bench.err"
 cd /tmp
 export TMPDIR=/tmp

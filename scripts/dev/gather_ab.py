@@ -41,7 +41,7 @@ def main():
     for fl in flags:
         lib.kl_dev_set_flags(fl)
         g = lambda: _fused.rasterize_backward(inp['g_feat'], idx, w, inp['fvi'], inp['feat'], None, 1000., 1e-8,  # noqa
-                                             face_normals_z=inp['fnz'], face_ranges=ranges)
+                                             face_normals_z=inp["fnz"], face_ranges=ranges[0])
         d = lambda: _fused.dibr_backward(inp['g_feat'], inp['g_mask'], idx, w, inp['fvi'], inp['feat'],  # noqa
                                          inp["fnz"], mask, state, 7000., 1000., 1e-8, ranges, bins)
         tg, td = timeit(g), timeit(d)
