@@ -1266,20 +1266,26 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
 // pixel data comes from LDS instead of a chain of dependent global loads per face.
 //   * A face is OWNED by the 64x8 tile holding the top-left corner (ix0, iy0) of its exact pixel
 //     range (the forward's face_ranges): exactly one tile per face with a non-empty range.
-//   * One 256-thread workgroup per tile stages the tile's face index (as int32), weights and
-//     incoming gradients in LDS with coalesced loads, then walks the tile's candidate chunks
-//     (the forward's rasterizer bin bitmap, saved with the state), keeps the faces it owns and
-//     sums each over its whole range, 8 lanes per face: pixels inside the tile from LDS, the
-//     few outside it (faces reaching into the tile below / to the right) from global memory.
+//   * BT_NP 256-thread workgroups per tile each stage the tile's face index (as int32), weights
+//     and incoming gradients in LDS with coalesced loads, then walk their share of the tile's
+//     candidate chunks (the forward's rasterizer bin bitmap, saved with the state; chunk
+//     ordinals interleaved over the parts, so the heavy tiles at the silhouette's poles spread
+//     over BT_NP workgroups), keep the faces the tile owns and sum each over its whole range,
+//     4 lanes per face: pixels inside the tile from LDS, the few outside it (faces reaching
+//     into the tile below / to the right) from global memory.  Parts without a chunk exit
+//     before staging.
 //   * Each face has one writer and a fixed lane order (the butterfly), so the sums are the
 //     gather kernel's exactly (double, rounded once); no atomics.
 //   * Faces without a range (culled, off screen) get zero gradients from the workgroups'
 //     slices of the face list; ranges over VIS_SMALL_AREA pixels are queued for the workgroup-
 //     per-face kernel as before.
-// Tiles are placed XCD-banded: block k runs on XCD k % 8 and takes tile (k % 8) * per + k / 8,
-// so one XCD's L2 serves a band of neighbouring tiles (the out-of-tile reads hit their data).
+// Tiles are placed XCD-banded: block k runs on XCD k % 8 and takes part (k / 8) % NP of tile
+// (k % 8) * per + k / 8 / NP, so one XCD's L2 serves a band of neighbouring tiles (the parts of a
+// tile and the out-of-tile reads hit the same lines).
 constexpr int BT_THREADS = 256;
 constexpr int BT_PX = TILE_W * TILE_H;  // 512 pixels per tile, 2 per thread
+constexpr int BT_NP = 4;                // parts per tile: part p's waves take candidate chunks p, p + NP, ...
+constexpr int BT_LPF = 4;               // lanes per face
 
 template <typename T, int MAXD>
 __global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
@@ -1287,10 +1293,12 @@ __global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
     const T *__restrict__ fvi, const T *__restrict__ feat, BinGeom g, int F, int D, float eps,
     T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig,
     const uint2 *__restrict__ rng, const uint32_t *__restrict__ bins, int per_band, int faces_per_block) {
+  constexpr int NW = BT_THREADS / 64;
+  constexpr int GPW = 64 / BT_LPF;  // faces per wave at a time
   __shared__ int s_idx[BT_PX];
   __shared__ T s_w[BT_PX * 3];
   __shared__ T s_g[BT_PX * MAXD];
-  __shared__ int s_own[BT_THREADS / 64][64];
+  __shared__ int s_own[NW][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int H = g.height, W = g.width;
   const int nt = g.batch * g.tiles_y * g.tiles_x;
@@ -1304,8 +1312,13 @@ __global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
     for (int q = 0; q < 6; q++) grad_fvi[k * 6 + q] = (T)0;
     for (int q = 0; q < 3 * D; q++) grad_ffeat[k * 3 * D + q] = (T)0;
   }
-  const int tile = (int)(blockIdx.x % 8) * per_band + (int)(blockIdx.x / 8);
+  const int xcd = (int)(blockIdx.x % 8), rk = (int)(blockIdx.x / 8);
+  const int part = rk % BT_NP;
+  const int tile = xcd * per_band + rk / BT_NP;
   if (tile >= nt) return;
+  ChunkSeq seq;
+  seq.init(bins + (size_t)tile * g.words, g.words, lane);
+  if (seq.at(part * NW, lane) < 0) return;  // no candidate chunk for this part (workgroup-uniform)
   const int tx = tile % g.tiles_x;
   const int ty = (tile / g.tiles_x) % g.tiles_y;
   const int b = tile / (g.tiles_x * g.tiles_y);
@@ -1329,13 +1342,11 @@ __global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
     s_idx[p] = id;
   }
   __syncthreads();
-  // ---- owned faces: the tile's candidate chunks, one per wave and step
-  ChunkSeq seq;
-  seq.init(bins + (size_t)tile * g.words, g.words, lane);
+  // ---- owned faces of this part's candidate chunks, one chunk per wave and step
   const int64_t f0 = (int64_t)b * F;
-  const int grp = lane >> 3, s = lane & 7;  // 8 faces per wave at a time, 8 lanes each
-  for (int pos = wid;; pos += BT_THREADS / 64) {
-    const int c = seq.at(pos, lane);  // wave-uniform; chunks ascend with pos
+  const int grp = lane / BT_LPF, s = lane % BT_LPF;
+  for (int step = 0;; step++) {
+    const int c = seq.at((step * BT_NP + part) * NW + wid, lane);  // wave-uniform, ascending
     if (c < 0) break;
     const int fl = c * 64 + lane;
     int ix0 = 1, ix1 = 0, iy0 = 1, iy1 = 0;
@@ -1348,7 +1359,7 @@ __global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
           fl;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (int k0 = 0; k0 < n; k0 += 8) {
+    for (int k0 = 0; k0 < n; k0 += GPW) {
       const int k = k0 + grp;
       const bool act = k < n;
       const int f = act ? s_own[wid][k] : 0;
@@ -1366,7 +1377,7 @@ __global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
         T cf[3 * MAXD];  // the face's features, [corner][d] with stride MAXD
 #pragma unroll
         for (int q = 0; q < 3 * MAXD; q++) cf[q] = (q % MAXD) < D ? feat[tf * 3 * D + (q / MAXD) * D + q % MAXD] : (T)0;
-        RangeWalkN<8> rw(a0, a1, b0, b1, s);
+        RangeWalkN<BT_LPF> rw(a0, a1, b0, b1, s);
         while (rw.more()) {
           const int j = b0 + rw.row, i = a0 + rw.col;
           T wa, wb, wc, gl[MAXD];
@@ -1396,9 +1407,9 @@ __global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
           rw.next();
         }
       }
-      // fixed-order butterfly over the face's 8 lanes
+      // fixed-order butterfly over the face's lanes
 #pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
+      for (int o = 1; o < BT_LPF; o <<= 1) {
 #pragma unroll
         for (int q = 0; q < 6; q++) acc.gi[q] += __shfl_xor(acc.gi[q], o);
 #pragma unroll
@@ -1407,7 +1418,7 @@ __global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
       if (act && !is_big) {
 #pragma unroll
         for (int q = 0; q < 6 + 3 * MAXD; q++) {
-          if (q % 8 != s) continue;
+          if (q % BT_LPF != s) continue;
           if (q < 6) {
             grad_fvi[tf * 6 + q] = (T)acc.gi[q];
           } else {
@@ -1516,7 +1527,7 @@ static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T 
     const BinGeom g = make_bin_geom(B, H, W, F);
     const int nt = g.batch * g.tiles_y * g.tiles_x;
     const int per_band = (int)cdiv(nt, 8);
-    const int grid = 8 * per_band;
+    const int grid = 8 * per_band * BT_NP;
     const int fpb = (int)cdiv(nf, grid);
     hipLaunchKernelGGL((rasterize_bwd_tile_kernel<T, MAXD>), dim3((unsigned)grid), dim3(BT_THREADS), 0, st, grad,
                        face_idx, w, fvi, feat, g, F, D, eps, gfvi, gfeat, big, nbig, rng, bins, per_band, fpb);

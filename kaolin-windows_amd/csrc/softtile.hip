@@ -668,29 +668,32 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
 }
 
 // ---------------------------------------------------------------- backward, per-face slots
-// kl_dibr_backward's soft half without the flush's memory-side atomics.  One 512-thread
-// workgroup per tile (all its rows; XCD-banded like the gather), the hits summed per face in
-// the LDS hash as above; then each face's six sums are STORED (not added) into one of the face's
-// slots: slot k = the tile's position in the face's enlarged-bbox tile rectangle (the forward's
-// soft pixel ranges), so every (face, tile) pair has exactly one writer.  A slot's flag byte
-// marks it written.  Faces whose rectangle has more than SB_SLOTS tiles (and hash overflow)
-// add into a zeroed double accumulator instead.  soft_slot_combine_kernel then sums a face's
-// written slots in slot order plus its accumulator, rounds once and adds the result to the
-// rasterizer's gradient -- the same exact double sums as the atomic flush, with one writer per
-// slot.
-constexpr int SB_SLOTS = 8;
+// kl_dibr_backward's soft half without the flush's memory-side atomics.  One 256-thread
+// workgroup per (tile, row pair) (XCD-banded like the gather; the heavy tiles at the
+// silhouette's poles spread over 4 workgroups), the hits summed per face in the LDS hash as
+// above; then each face's six sums are STORED (not added) into one of the face's slots:
+// slot k = 4 x the tile's position in the face's enlarged-bbox tile rectangle (the forward's soft
+// pixel ranges) + the row pair, so every (face, tile, row pair) has exactly one writer.  A slot's
+// flag byte marks it written.  Faces whose rectangle has more than SB_TPOS tiles (and hash
+// overflow) add into a zeroed double accumulator instead.  soft_slot_combine_kernel then sums a
+// face's written slots in slot order plus its accumulator, rounds once and adds the result to
+// the rasterizer's gradient -- the same exact double sums as the atomic flush, one writer per slot.
+constexpr int SB_TPOS = 8;                 // tile positions per face
+constexpr int SB_RP = 2;                   // rows per workgroup
+constexpr int SB_NP = TILE_H / SB_RP;      // workgroups (row pairs) per tile
+constexpr int SB_SLOTS = SB_TPOS * SB_NP;  // slots per face
 constexpr int SB_HC = 1024;
 
-__device__ __forceinline__ int soft_slot_of(uint2 r, int tx, int ty) {
+__device__ __forceinline__ int soft_slot_of(uint2 r, int tx, int ty, int part) {
   const int jx0 = (int)(r.x & 0xffffu), jx1 = (int)(r.x >> 16), jy0 = (int)(r.y & 0xffffu), jy1 = (int)(r.y >> 16);
   if (jx0 > jx1 || jy0 > jy1) return -1;
   const int ntx = jx1 / TILE_W - jx0 / TILE_W + 1, nty = jy1 / TILE_H - jy0 / TILE_H + 1;
-  if (ntx * nty > SB_SLOTS) return -1;
-  return (ty - jy0 / TILE_H) * ntx + (tx - jx0 / TILE_W);
+  if (ntx * nty > SB_TPOS) return -1;
+  return ((ty - jy0 / TILE_H) * ntx + (tx - jx0 / TILE_W)) * SB_NP + part;
 }
 
 template <typename T>
-__global__ void __launch_bounds__(512) soft_tile_bwd_slots_kernel(
+__global__ void __launch_bounds__(256) soft_tile_bwd_slots_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const uint8_t *__restrict__ hits,
     const uint32_t *__restrict__ rec_face, const T *__restrict__ rec_prob, const int *__restrict__ seg_tot,
     const T *__restrict__ fvi, const uint2 *__restrict__ srng, BinGeom g, int F, int K, float sigmainv,
@@ -700,36 +703,38 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_slots_kernel(
   __shared__ double s_val[SB_HC * 6];
   __shared__ int s_used[SB_HC];
   __shared__ int s_nused;
-  __shared__ double s_a[TILE_H][64];
-  __shared__ int s_pre[TILE_H][65];
-  __shared__ int s_rowpre[TILE_H + 1];
+  __shared__ double s_a[SB_RP][64];
+  __shared__ int s_pre[SB_RP][65];
+  __shared__ int s_rowpre[SB_RP + 1];
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;  // the tile's row
+  const int wid = threadIdx.x >> 6;
   const int H = g.height, W = g.width;
   const int nt = g.batch * g.tiles_y * g.tiles_x;
-  const int tile = (int)(blockIdx.x % 8) * per_band + (int)(blockIdx.x / 8);
+  const int xcd = (int)(blockIdx.x % 8), rk = (int)(blockIdx.x / 8);
+  const int part = rk % SB_NP;
+  const int tile = xcd * per_band + rk / SB_NP;
   if (tile >= nt) return;
   const int tx = tile % g.tiles_x, ty = (tile / g.tiles_x) % g.tiles_y, b = tile / (g.tiles_x * g.tiles_y);
-  {  // the tile's hit total first: most tiles have none
-    const int j = ty * TILE_H + wid;
-    const int tot = j < H ? seg_tot[((size_t)b * H + j) * g.tiles_x + tx] : 0;
-    if (lane == 0) s_rowpre[wid + 1] = tot;
+  const int jr0 = ty * TILE_H + part * SB_RP;  // the workgroup's first row
+  if (threadIdx.x < SB_RP) {  // the rows' hit totals first: most row pairs have none
+    const int j = jr0 + (int)threadIdx.x;
+    s_rowpre[threadIdx.x + 1] = j < H ? seg_tot[((size_t)b * H + j) * g.tiles_x + tx] : 0;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     s_rowpre[0] = 0;
-    for (int r = 1; r <= TILE_H; r++) s_rowpre[r] += s_rowpre[r - 1];
+    for (int r = 1; r <= SB_RP; r++) s_rowpre[r] += s_rowpre[r - 1];
     s_nused = 0;
   }
   __syncthreads();
-  const int total = s_rowpre[TILE_H];
+  const int total = s_rowpre[SB_RP];
   if (total == 0) return;
   for (int q = threadIdx.x; q < SB_HC; q += blockDim.x) s_key[q] = -1;
   for (int q = threadIdx.x; q < SB_HC * 6; q += blockDim.x) s_val[q] = 0.0;
   ItemHash<T, SB_HC> hash{s_key, s_val, s_used, &s_nused};
   const int ibase = tx * TILE_W;
-  {  // row `wid`: the filled-slot prefix and the reference's -sigmainv * dLdp * (1 - allprob)
-    const int j = ty * TILE_H + wid, i = ibase + lane;
+  if (wid < SB_RP) {  // row `wid`: the filled-slot prefix and -sigmainv * dLdp * (1 - allprob)
+    const int j = jr0 + wid, i = ibase + lane;
     int kid = 0;
     if (j < H && i < W) {
       const size_t p = ((size_t)b * H + j) * W + i;
@@ -751,13 +756,13 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_slots_kernel(
   for (int f = (int)threadIdx.x; f < total; f += blockDim.x) {
     int r = 0;
 #pragma unroll
-    for (int k = 1; k < TILE_H; k++) r += s_rowpre[k] <= f ? 1 : 0;
+    for (int k = 1; k < SB_RP; k++) r += s_rowpre[k] <= f ? 1 : 0;
     const int e = f - s_rowpre[r];
     int lo = 0;  // owner lane: last lane with s_pre[r][lo] <= e
 #pragma unroll
     for (int st = 32; st > 0; st >>= 1)
       if (s_pre[r][lo + st] <= e) lo += st;
-    const int j = ty * TILE_H + r;
+    const int j = jr0 + r;
     const size_t o = ((size_t)(b * H + j) * g.tiles_x + tx) * 64 * (size_t)K + e;
     const uint32_t rr = rec_face[o];
     const T pr = rec_prob[o];
@@ -776,7 +781,7 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_slots_kernel(
     hash.add(face, c0, c1, g0x, g0y, g1x, g1y, gmesh);
   }
   __syncthreads();
-  // one thread per (used slot, coordinate): store into the face's tile slot, or add into the
+  // one thread per (used slot, coordinate): store into the face's slot, or add into the
   // accumulator when the face has no slot for this tile
   const int n = s_nused;
   const size_t fb0 = (size_t)b * F;
@@ -784,7 +789,7 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_slots_kernel(
     const int sl = s_used[u / 6], c = u % 6;
     const int face = s_key[sl];
     const double v = s_val[sl * 6 + c];
-    const int k = soft_slot_of(srng[fb0 + face], tx, ty);
+    const int k = soft_slot_of(srng[fb0 + face], tx, ty, part);
     if (k >= 0) {
       slots[((fb0 + face) * SB_SLOTS + k) * 6 + c] = v;
       if (c == 0) flags[(fb0 + face) * SB_SLOTS + k] = 1;
@@ -806,14 +811,16 @@ __global__ void __launch_bounds__(256) soft_slot_combine_kernel(const double *__
   if (t >= n) return;
   const int64_t tf = t / 6;
   const int c = (int)(t % 6);
-  uint64_t fl = 0;
-  const uint8_t *fp = flags + tf * SB_SLOTS;
-#pragma unroll
-  for (int k = 0; k < SB_SLOTS; k++) fl |= (uint64_t)fp[k] << (8 * k);
+  const uint64_t *fp = reinterpret_cast<const uint64_t *>(flags + tf * SB_SLOTS);
   double sum = 0.0;
 #pragma unroll
-  for (int k = 0; k < SB_SLOTS; k++)
-    if ((fl >> (8 * k)) & 0xff) sum += slots[(tf * SB_SLOTS + k) * 6 + c];
+  for (int q = 0; q < SB_SLOTS / 8; q++) {
+    const uint64_t fl = fp[q];
+    if (!fl) continue;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+      if ((fl >> (8 * k)) & 0xff) sum += slots[(tf * SB_SLOTS + q * 8 + k) * 6 + c];
+  }
   sum += ovf[t];
   out[t] = out[t] + (T)sum;
 }
@@ -838,7 +845,8 @@ int soft_tile_backward_slots(int B, int H, int W, int F, int K, const T *grad, c
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   const int per_band = (int)cdiv(nt, 8);
-  hipLaunchKernelGGL((soft_tile_bwd_slots_kernel<T>), dim3((unsigned)(8 * per_band)), dim3(512), 0, st, grad, mask,
+  hipLaunchKernelGGL((soft_tile_bwd_slots_kernel<T>), dim3((unsigned)(8 * per_band * SB_NP)), dim3(256), 0, st, grad,
+                     mask,
                      (const uint8_t *)s.hits, (const uint32_t *)s.rec_face, (const T *)s.rec_prob,
                      (const int *)s.seg_tot, fvi, srng, g, F, K, sigmainv, m,
                      reinterpret_cast<double *>(w + nacc + nflag), reinterpret_cast<uint8_t *>(w + nacc),

@@ -166,7 +166,9 @@ def test_dibr_rasterization_list_vs_oracle(kal, dtype):
     torch.autograd.backward([ft, mask2], [torch.cat([gu, go], -1), gm])
     assert torch.equal(idx, idx2) and torch.equal(mask, mask2)
     assert torch.equal(fu, ft[..., :2]) and torch.equal(fo, ft[..., 2:])
-    assert torch.equal(a.grad, a2.grad)
+    # f32: the terms sum exactly in double, bit-equal run to run; f64: the soft-mask hash adds
+    # double terms in LDS-atomic order, equal to ~1e-15 relative
+    assert_grads_equal(A(a.grad), A(a2.grad))
     assert torch.equal(u.grad, f2.grad[..., :2]) and torch.equal(o.grad, f2.grad[..., 2:])
     # the oracle
     cat = A(torch.cat([uv, ones], -1))
