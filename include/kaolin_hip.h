@@ -51,9 +51,8 @@ typedef void *(*kl_alloc_fn)(void *ctx, size_t bytes);
 /* ABI version of this header: a caller checks kl_abi_version() == KL_ABI_VERSION at load time.
  * 2: the workspace arguments moved before the stream (kl_rasterize_backward,
  *    kl_dibr_soft_mask_backward(_fused), kl_unbatched_triangle_distance_backward) and
- *    kl_soft_mask_compact_bwd_workspace_bytes gained num_faces.
- * 3: kl_dibr_forward / kl_dibr_backward take raster_bins and soft_ranges after face_ranges. */
-#define KL_ABI_VERSION 3
+ *    kl_soft_mask_compact_bwd_workspace_bytes gained num_faces. */
+#define KL_ABI_VERSION 2
 
 const char *kl_last_error(void);
 int kl_abi_version(void);
@@ -216,33 +215,24 @@ int kl_dibr_soft_mask_backward_compact(kl_dtype dtype, int batch, int height, in
  * the reference (grad_soft_mask may be NULL).
  * face_ranges: NULL, or (B*F) x 2 uint32 the forward fills with each face's exact pixel
  * ranges (x0 | x1 << 16, y0 | y1 << 16; empty for invalid faces) for the backward to reuse.
- * raster_bins: NULL, or kl_dibr_bins_bytes() bytes the forward fills with the rasterizer's
- * screen bins (per 64x8 tile, a bitmap over 64-face chunks); given with face_ranges to the
- * backward, its gather runs per tile (each face summed by the tile holding its range's top-left
- * pixel, the tile's pixels staged in LDS) instead of per face.
- * soft_ranges: NULL, or (B*F) x 2 uint32 the forward fills with each face's exact pixel ranges
- * of the soft mask's enlarged bbox; given to the backward, the soft-mask sums are stored into
- * per-(face, tile) slots and combined per face in slot order (no memory-side atomics).
  * feat_dim <= 8.  Workspaces: kl_dibr_workspace_bytes (forward),
  * kl_dibr_bwd_workspace_bytes (backward). */
 size_t kl_dibr_workspace_bytes(int batch, int height, int width, int num_faces);
-size_t kl_dibr_bins_bytes(int batch, int height, int width, int num_faces);
 size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum);
 int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim, int knum,
                     const void *face_vertices_z, const void *face_vertices_image, const void *face_features,
                     const void *face_normals_z, float sigmainv, double bbox_pad, float multiplier, float eps,
                     void *interpolated_features, int64_t *face_idx, void *output_weights, void *soft_mask,
                     uint8_t *hits, uint32_t *rec_face, void *rec_prob, int *seg_tot, int *scratch,
-                    uint32_t *face_ranges, uint32_t *raster_bins, uint32_t *soft_ranges, void *workspace,
-                    size_t workspace_bytes, kl_stream stream);
+                    uint32_t *face_ranges, void *workspace, size_t workspace_bytes, kl_stream stream);
 int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim, int knum,
                      const void *grad_interpolated_features, const void *grad_soft_mask, const int64_t *face_idx,
                      const void *output_weights, const void *face_vertices_image, const void *face_features,
                      const void *face_normals_z, const void *soft_mask, const uint8_t *hits,
                      const uint32_t *rec_face, const void *rec_prob, const int *seg_tot, float sigmainv,
                      float multiplier, float eps, void *grad_face_vertices_image, void *grad_face_features,
-                     int *scratch, const uint32_t *face_ranges, const uint32_t *raster_bins,
-                     const uint32_t *soft_ranges, void *workspace, size_t workspace_bytes, kl_stream stream);
+                     int *scratch, const uint32_t *face_ranges, void *workspace, size_t workspace_bytes,
+                     kl_stream stream);
 
 /* dibr_soft_mask.cpp:110-183  dibr_soft_mask_backward_cuda.
  * Output grad_face_vertices_image (B,F,3,2) (fully written): the reference's per-hit float

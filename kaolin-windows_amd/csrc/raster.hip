@@ -1144,7 +1144,7 @@ struct GatherAcc {
     }
   }
   // the same with the face's features (cf, [corner][d], stride MAXD) and the pixel's incoming
-  // gradient (g) in registers
+  // gradient (g) already in registers
   __device__ __forceinline__ void add_regs(const T v[6], const T cf[3 * MAXD], int D, T w_a, T w_b, T w_c,
                                            const T g[MAXD], float eps) {
     BaryGrad<T> bg;
@@ -1183,6 +1183,15 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
   // latency hides behind the walk: an unconditional load from a clamped index
   double sv = 0.0;
   if (soft) sv = soft[(in ? tf : 0) * 6 + (s < 6 ? s : 5)];
+  // the face's vertices and features, loaded with its range (unconditional loads from a clamped
+  // index: one round trip for all of them instead of a chain)
+  const int64_t tfc = in ? tf : 0;
+  T v[6];
+#pragma unroll
+  for (int q = 0; q < 6; q++) v[q] = fvi[tfc * 6 + q];
+  T cf[3 * MAXD];  // [corner][d], stride MAXD
+#pragma unroll
+  for (int q = 0; q < 3 * MAXD; q++) cf[q] = (q % MAXD) < D ? feat[tfc * 3 * D + (q / MAXD) * D + q % MAXD] : (T)0;
   GatherAcc<T, MAXD> acc;
   acc.zero();
   int ix0, ix1, iy0, iy1;
@@ -1210,32 +1219,29 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
       queued = true;
       if (s == 0) big[atomicAdd(nbig, 1)] = (int)tf;
     } else {
-      T v[6];
-#pragma unroll
-      for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
-      const T *c = feat + tf * 3 * D;
       const int64_t pbase = (int64_t)b * H * W;
       RangeWalkN<LPF_> rw(ix0, ix1, iy0, iy1, s);
       while (rw.more()) {
-        // face_idx of GATHER_BATCH pixels in flight together; the (rare) hits then load
-        // their weights / grads one by one
-        int64_t px[GATHER_BATCH];
-        uint32_t hits = 0;
+        // GATHER_BATCH pixels: face index, weights and incoming gradients all in flight together
+        // (unconditional loads; pixels past the range read the face's first pixel and are not
+        // counted)
+        int64_t fid[GATHER_BATCH];
+        T wv[GATHER_BATCH][3], gv[GATHER_BATCH][MAXD];
+        uint32_t live = 0;
 #pragma unroll
         for (int u = 0; u < GATHER_BATCH; u++) {
-          px[u] = pbase + (int64_t)(iy0 + rw.row) * W + ix0 + rw.col;
-          if (rw.more() && face_idx[px[u]] == f) hits |= 1u << u;
+          if (rw.more()) live |= 1u << u;
+          const int64_t px = pbase + (int64_t)(iy0 + (rw.more() ? rw.row : 0)) * W + ix0 + (rw.more() ? rw.col : 0);
+          fid[u] = face_idx[px];
+#pragma unroll
+          for (int q = 0; q < 3; q++) wv[u][q] = wts[px * 3 + q];
+#pragma unroll
+          for (int d = 0; d < MAXD; d++) gv[u][d] = d < D ? grad_feat[px * D + d] : (T)0;
           rw.next();
         }
-#pragma unroll 1
-        for (; hits; hits &= hits - 1) {
-          const int u = __builtin_ctz(hits);
-          int64_t p = px[0];
 #pragma unroll
-          for (int q = 1; q < GATHER_BATCH; q++)
-            if (u == q) p = px[q];
-          acc.add(v, c, D, wts[p * 3 + 0], wts[p * 3 + 1], wts[p * 3 + 2], grad_feat + p * D, eps);
-        }
+        for (int u = 0; u < GATHER_BATCH; u++)
+          if (((live >> u) & 1u) && fid[u] == f) acc.add_regs(v, cf, D, wv[u][0], wv[u][1], wv[u][2], gv[u], eps);
       }
     }
   }
@@ -1258,178 +1264,6 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
       const int r = q - 6, ii = r / MAXD, d = r % MAXD;
       if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)acc.gf[r];
     }
-  }
-}
-
-// ---------------------------------------------------------------- tile-owner gather
-// The same per-face sums as rasterize_bwd_gather_kernel, organised by screen tile so that the
-// pixel data comes from LDS instead of a chain of dependent global loads per face.
-//   * A face is OWNED by the 64x8 tile holding the top-left corner (ix0, iy0) of its exact pixel
-//     range (the forward's face_ranges): exactly one tile per face with a non-empty range.
-//   * BT_NP 256-thread workgroups per tile each stage the tile's face index (as int32), weights
-//     and incoming gradients in LDS with coalesced loads, then walk their share of the tile's
-//     candidate chunks (the forward's rasterizer bin bitmap, saved with the state; chunk
-//     ordinals interleaved over the parts, so the heavy tiles at the silhouette's poles spread
-//     over BT_NP workgroups), keep the faces the tile owns and sum each over its whole range,
-//     4 lanes per face: pixels inside the tile from LDS, the few outside it (faces reaching
-//     into the tile below / to the right) from global memory.  Parts without a chunk exit
-//     before staging.
-//   * Each face has one writer and a fixed lane order (the butterfly), so the sums are the
-//     gather kernel's exactly (double, rounded once); no atomics.
-//   * Faces without a range (culled, off screen) get zero gradients from the workgroups'
-//     slices of the face list; ranges over VIS_SMALL_AREA pixels are queued for the workgroup-
-//     per-face kernel as before.
-// Tiles are placed XCD-banded: block k runs on XCD k % 8 and takes part (k / 8) % NP of tile
-// (k % 8) * per + k / 8 / NP, so one XCD's L2 serves a band of neighbouring tiles (the parts of a
-// tile and the out-of-tile reads hit the same lines).
-constexpr int BT_THREADS = 256;
-constexpr int BT_PX = TILE_W * TILE_H;  // 512 pixels per tile, 2 per thread
-constexpr int BT_NP = 4;                // parts per tile: part p's waves take candidate chunks p, p + NP, ...
-constexpr int BT_LPF = 4;               // lanes per face
-
-template <typename T, int MAXD>
-__global__ void __launch_bounds__(BT_THREADS) rasterize_bwd_tile_kernel(
-    const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
-    const T *__restrict__ fvi, const T *__restrict__ feat, BinGeom g, int F, int D, float eps,
-    T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig,
-    const uint2 *__restrict__ rng, const uint32_t *__restrict__ bins, int per_band, int faces_per_block) {
-  constexpr int NW = BT_THREADS / 64;
-  constexpr int GPW = 64 / BT_LPF;  // faces per wave at a time
-  __shared__ int s_idx[BT_PX];
-  __shared__ T s_w[BT_PX * 3];
-  __shared__ T s_g[BT_PX * MAXD];
-  __shared__ int s_own[NW][64];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int H = g.height, W = g.width;
-  const int nt = g.batch * g.tiles_y * g.tiles_x;
-  const int64_t nf = (int64_t)g.batch * F;
-  // faces without a range: zero gradients (this block's slice of the face list)
-  for (int64_t k = (int64_t)blockIdx.x * faces_per_block + threadIdx.x;
-       k < min(nf, (int64_t)(blockIdx.x + 1) * faces_per_block); k += BT_THREADS) {
-    int a0, a1, b0, b1;
-    if (rng_range(rng, k, a0, a1, b0, b1)) continue;
-#pragma unroll
-    for (int q = 0; q < 6; q++) grad_fvi[k * 6 + q] = (T)0;
-    for (int q = 0; q < 3 * D; q++) grad_ffeat[k * 3 * D + q] = (T)0;
-  }
-  const int xcd = (int)(blockIdx.x % 8), rk = (int)(blockIdx.x / 8);
-  const int part = rk % BT_NP;
-  const int tile = xcd * per_band + rk / BT_NP;
-  if (tile >= nt) return;
-  ChunkSeq seq;
-  seq.init(bins + (size_t)tile * g.words, g.words, lane);
-  if (seq.at(part * NW, lane) < 0) return;  // no candidate chunk for this part (workgroup-uniform)
-  const int tx = tile % g.tiles_x;
-  const int ty = (tile / g.tiles_x) % g.tiles_y;
-  const int b = tile / (g.tiles_x * g.tiles_y);
-  const int i0 = tx * TILE_W, j0 = ty * TILE_H;
-  const int64_t pbase = (int64_t)b * H * W;
-  // ---- stage the tile's pixels (2 per thread; rows of 64 are contiguous in memory)
-  for (int p = threadIdx.x; p < BT_PX; p += BT_THREADS) {
-    const int j = j0 + p / TILE_W, i = i0 + p % TILE_W;
-    int id = -1;
-    if (j < H && i < W) {
-      const int64_t px = pbase + (int64_t)j * W + i;
-      id = (int)face_idx[px];
-      if (id >= 0) {
-#pragma unroll
-        for (int q = 0; q < 3; q++) s_w[p * 3 + q] = wts[px * 3 + q];
-#pragma unroll
-        for (int d = 0; d < MAXD; d++)
-          if (d < D) s_g[p * MAXD + d] = grad_feat[px * D + d];
-      }
-    }
-    s_idx[p] = id;
-  }
-  __syncthreads();
-  // ---- owned faces of this part's candidate chunks, one chunk per wave and step
-  const int64_t f0 = (int64_t)b * F;
-  const int grp = lane / BT_LPF, s = lane % BT_LPF;
-  for (int step = 0;; step++) {
-    const int c = seq.at((step * BT_NP + part) * NW + wid, lane);  // wave-uniform, ascending
-    if (c < 0) break;
-    const int fl = c * 64 + lane;
-    int ix0 = 1, ix1 = 0, iy0 = 1, iy1 = 0;
-    const bool owned = fl < F && rng_range(rng, f0 + fl, ix0, ix1, iy0, iy1) && ix0 / TILE_W == tx &&
-                       iy0 / TILE_H == ty;
-    const uint64_t om = ballot(owned);
-    const int n = __popcll(om);
-    if (owned)
-      s_own[wid][(int)__builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0u))] =
-          fl;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (int k0 = 0; k0 < n; k0 += GPW) {
-      const int k = k0 + grp;
-      const bool act = k < n;
-      const int f = act ? s_own[wid][k] : 0;
-      const int64_t tf = f0 + f;
-      int a0 = 1, a1 = 0, b0 = 1, b1 = 0;
-      if (act) rng_range(rng, tf, a0, a1, b0, b1);
-      GatherAcc<T, MAXD> acc;
-      acc.zero();
-      const bool is_big = act && (int64_t)(a1 - a0 + 1) * (b1 - b0 + 1) > VIS_SMALL_AREA;
-      if (is_big && s == 0) big[atomicAdd(nbig, 1)] = (int)tf;
-      if (act && !is_big) {
-        T v[6];
-#pragma unroll
-        for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
-        T cf[3 * MAXD];  // the face's features, [corner][d] with stride MAXD
-#pragma unroll
-        for (int q = 0; q < 3 * MAXD; q++) cf[q] = (q % MAXD) < D ? feat[tf * 3 * D + (q / MAXD) * D + q % MAXD] : (T)0;
-        RangeWalkN<BT_LPF> rw(a0, a1, b0, b1, s);
-        while (rw.more()) {
-          const int j = b0 + rw.row, i = a0 + rw.col;
-          T wa, wb, wc, gl[MAXD];
-          bool hit;
-          if (i < i0 + TILE_W && j < j0 + TILE_H) {
-            const int p = (j - j0) * TILE_W + (i - i0);
-            hit = s_idx[p] == f;
-            if (hit) {
-              wa = s_w[p * 3];
-              wb = s_w[p * 3 + 1];
-              wc = s_w[p * 3 + 2];
-#pragma unroll
-              for (int d = 0; d < MAXD; d++) gl[d] = s_g[p * MAXD + d];
-            }
-          } else {
-            const int64_t px = pbase + (int64_t)j * W + i;
-            hit = face_idx[px] == f;
-            if (hit) {
-              wa = wts[px * 3];
-              wb = wts[px * 3 + 1];
-              wc = wts[px * 3 + 2];
-#pragma unroll
-              for (int d = 0; d < MAXD; d++) gl[d] = d < D ? grad_feat[px * D + d] : (T)0;
-            }
-          }
-          if (hit) acc.add_regs(v, cf, D, wa, wb, wc, gl, eps);
-          rw.next();
-        }
-      }
-      // fixed-order butterfly over the face's lanes
-#pragma unroll
-      for (int o = 1; o < BT_LPF; o <<= 1) {
-#pragma unroll
-        for (int q = 0; q < 6; q++) acc.gi[q] += __shfl_xor(acc.gi[q], o);
-#pragma unroll
-        for (int q = 0; q < 3 * MAXD; q++) acc.gf[q] += __shfl_xor(acc.gf[q], o);
-      }
-      if (act && !is_big) {
-#pragma unroll
-        for (int q = 0; q < 6 + 3 * MAXD; q++) {
-          if (q % BT_LPF != s) continue;
-          if (q < 6) {
-            grad_fvi[tf * 6 + q] = (T)acc.gi[q];
-          } else {
-            const int r = q - 6, ii = r / MAXD, d = r % MAXD;
-            if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)acc.gf[r];
-          }
-        }
-      }
-    }
-    __builtin_amdgcn_wave_barrier();  // s_own is rewritten by the wave's next chunk
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
 }
 
@@ -1519,24 +1353,9 @@ template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
                                      const T *w, const T *fvi, const T *feat, const uint8_t *valid, const T *nz,
                                      float m, float eps, T *gfvi, T *gfeat, int *big, int *nbig, bool zero_nbig,
-                                     const uint2 *rng, const double *soft, hipStream_t st,
-                                     const uint32_t *bins = nullptr) {
+                                     const uint2 *rng, const double *soft, hipStream_t st) {
   if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
-  if (bins && rng && !soft && !(g_dev_flags & (1 << 17))) {  // tile-owner gather (dev bit 17: the per-face one)
-    const BinGeom g = make_bin_geom(B, H, W, F);
-    const int nt = g.batch * g.tiles_y * g.tiles_x;
-    const int per_band = (int)cdiv(nt, 8);
-    const int grid = 8 * per_band * BT_NP;
-    const int fpb = (int)cdiv(nf, grid);
-    hipLaunchKernelGGL((rasterize_bwd_tile_kernel<T, MAXD>), dim3((unsigned)grid), dim3(BT_THREADS), 0, st, grad,
-                       face_idx, w, fvi, feat, g, F, D, eps, gfvi, gfeat, big, nbig, rng, bins, per_band, fpb);
-    KL_CHECK_LAUNCH();
-    hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(256), dim3(256), 0, st, grad, face_idx, w, fvi,
-                       feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
-    KL_CHECK_LAUNCH();
-    return KL_OK;
-  }
   // 8 lanes per face (measured: 4 lanes 62.7 us, 8 lanes 58 us, 16 lanes 91 us at cfg3)
   hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st,
                      grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
@@ -1553,8 +1372,7 @@ template <typename T>
 static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
                                 const void *w, const void *fvi, const void *feat, const uint8_t *valid, const T *nz,
                                 float m, float eps, void *gfvi, void *gfeat, void *ws, size_t ws_bytes, int *nbig,
-                                hipStream_t st, const uint2 *rng = nullptr, const double *soft = nullptr,
-                                const uint32_t *bins = nullptr) {
+                                hipStream_t st, const uint2 *rng = nullptr, const double *soft = nullptr) {
   const int64_t nf = (int64_t)B * F;
   if (nf == 0) return KL_OK;
   if (D > 8) {  // wide features: the scatter kernel
@@ -1573,15 +1391,15 @@ static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *g
   // MAXD = D where it is small (the accumulators are doubles: registers set the occupancy)
   if (D <= 2)
     return rasterize_bwd_gather_maxd<T, 2>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, soft, st, bins);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
   if (D == 3)
     return rasterize_bwd_gather_maxd<T, 3>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, soft, st, bins);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
   if (D <= 4)
     return rasterize_bwd_gather_maxd<T, 4>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, soft, st, bins);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
   return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                         (T *)gfeat, big, nbig, zero, rng, soft, st, bins);
+                                         (T *)gfeat, big, nbig, zero, rng, soft, st);
 }
 
 // The fused front-end path's forward: the tile rasterizer (dev flag bit 13 selects the
@@ -1739,7 +1557,7 @@ template <typename T>
 static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, const T *fvi, const T *feat, const T *fnz,
                     float sigmainv, double pad, float m, float eps, T *out_feat, int64_t *out_idx, T *out_w,
                     T *out_mask, const SoftState<T> &s, void *ws, size_t ws_bytes, hipStream_t st,
-                    uint2 *face_ranges, uint32_t *raster_bins, uint2 *soft_ranges) {
+                    uint2 *face_ranges) {
   const DibrFwdWs L(B, H, W, F);
   KL_REQUIRE(ws_bytes >= L.bytes, "dibr_rasterization forward: workspace too small");
   KL_REQUIRE(H < 65536 && W < 65536, "dibr_rasterization forward: height and width must be < 65536");
@@ -1748,8 +1566,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const size_t P = (size_t)B * H * W;
   if (P == 0) return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
   if (F == 0 || (g_dev_flags & (1 << 13))) {  // no faces (or dev: the separate pipelines)
-    KL_REQUIRE((face_ranges == nullptr && raster_bins == nullptr && soft_ranges == nullptr) || F == 0,
-               "dibr_rasterization forward: face_ranges / raster_bins / soft_ranges need the combined path");
+    KL_REQUIRE(face_ranges == nullptr || F == 0, "dibr_rasterization forward: face_ranges needs the combined path");
     KL_CHECK_RC(dibr_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, F, fvz, feat, m, eps, out_feat,
                                  out_idx, out_w, ws, ws_bytes, st));
     return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, ws, ws_bytes, st);
@@ -1757,9 +1574,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   char *w = reinterpret_cast<char *>(ws);
-  // the rasterizer's bins go to the caller's buffer when given (kept for the backward's
-  // tile-owner gather), else to the workspace
-  uint32_t *rbm = raster_bins ? raster_bins : reinterpret_cast<uint32_t *>(w);
+  uint32_t *rbm = reinterpret_cast<uint32_t *>(w);
   uint32_t *sbm = reinterpret_cast<uint32_t *>(w + L.off_sbm);
   int *rgh = reinterpret_cast<int *>(w + L.off_rgh);
   int *sgh = reinterpret_cast<int *>(w + L.off_sgh);
@@ -1771,7 +1586,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   int *nitems = reinterpret_cast<int *>(w + L.off_n);
   int32_t *sorder = reinterpret_cast<int32_t *>(w + L.off_sorder);
   int *snitems = reinterpret_cast<int *>(w + L.off_sn);
-  uint2 *srng = soft_ranges ? soft_ranges : reinterpret_cast<uint2 *>(w + L.off_srng);
+  uint2 *srng = reinterpret_cast<uint2 *>(w + L.off_srng);
   const RastSrc<T> src{fvi, nullptr, (T)m, fnz};
   const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
   if (bin_word_lds_ok(g) && !(g_dev_flags & (1 << 14))) {  // dev bit 14: the atomic binning
@@ -1779,7 +1594,6 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
                                    (int)((L.zero - L.off_rgh) / sizeof(int)), st));  // + histograms zeroed
   } else {
   KL_CHECK_RC(fill_async(w, 0, L.zero, st));
-  if (raster_bins) KL_CHECK_RC(fill_async(raster_bins, 0, g.bytes(), st));
   const dim3 bgrid((unsigned)cdiv((int64_t)g.chunks * 64, 256), (unsigned)B);
   if (fnz)
     hipLaunchKernelGGL((raster_bin_kernel<T, 2>), bgrid, dim3(256), 0, st, src, fvz, F, g, pp, rbm, rec, rng, sbm,
@@ -1814,35 +1628,8 @@ template <typename T>
 static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat, const T *grad_mask,
                     const int64_t *face_idx, const T *w, const T *fvi, const T *feat, const T *fnz, const T *mask,
                     const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *ws,
-                    size_t ws_bytes, hipStream_t st, const uint2 *face_ranges, const uint32_t *raster_bins,
-                    const uint2 *soft_ranges) {
+                    size_t ws_bytes, hipStream_t st, const uint2 *face_ranges) {
   KL_REQUIRE(D <= 8, "dibr_rasterization backward: feature dimension > 8 is not supported by the fused path");
-  if (soft_ranges && !(g_dev_flags & (1 << 18))) {  // dev bit 18: the atomic soft flush below
-    // The two halves are independent until the final add, so they run concurrently: the
-    // soft-mask sums (zero fill, per-tile slot kernel; left in double) on the side stream, the
-    // rasterizer's gather (every face's own rounded gradient) on `st`; after the join each
-    // coordinate gets the soft sum rounded on its own and added, as autograd adds the two
-    // gradients.  The gather's big-face counter is the state's scratch int (zeroed by the
-    // forward), re-zeroed by that final add.
-    const size_t slot_bytes = al256(soft_slots_ws_bytes(B, F));
-    KL_REQUIRE(ws_bytes >= slot_bytes, "dibr_rasterization backward: workspace too small");
-    void *gath_ws = reinterpret_cast<char *>(ws) + slot_bytes;
-    const bool has_soft = grad_mask != nullptr && K > 0 && (int64_t)B * H * W > 0;
-    if (has_soft) {
-      SideFork fork(st);
-      KL_CHECK_RC(soft_tile_backward_slots<T>(B, H, W, F, K, grad_mask, mask, s, fvi, soft_ranges, sigmainv, m, ws,
-                                              slot_bytes, fork.side()));
-      KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps,
-                                          gfvi, gfeat, gath_ws, ws_bytes - slot_bytes, s.scratch, st, face_ranges,
-                                          nullptr, face_ranges ? raster_bins : nullptr));
-      KL_CHECK_RC(fork.join());
-      return soft_slots_combine<T>(B, F, gfvi, ws, s.scratch, st);
-    }
-    KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
-                                        gfeat, gath_ws, ws_bytes - slot_bytes, s.scratch, st, face_ranges, nullptr,
-                                        face_ranges ? raster_bins : nullptr));
-    return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
-  }
   // workspace: the soft mask's double sums | its items | the gather's big-face list
   const size_t acc_bytes = al256((size_t)B * F * 6 * sizeof(double));
   const size_t soft_bytes = al256(soft_tile_bwd_items_bytes(B, H, W, K));
@@ -1851,6 +1638,12 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
   void *soft_ws = reinterpret_cast<char *>(ws) + acc_bytes;
   void *gath_ws = reinterpret_cast<char *>(soft_ws) + soft_bytes;
   bool has_soft = false;
+  // The two halves are independent until the final add, so they run concurrently: the
+  // soft-mask sums (fill, plan, backward; left in double) on the side stream, the
+  // rasterizer's gather (every face's own rounded gradient) on `st`; after the join each
+  // coordinate gets the soft sum rounded on its own and added, as autograd adds the two
+  // gradients.  The gather's big-face counter is the state's scratch int (zeroed by the
+  // forward), re-zeroed by that final add; the soft half does not touch it.
   SideFork fork(st);
   SoftState<T> ss = s;
   ss.scratch = nullptr;
@@ -1858,7 +1651,7 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
                                     soft_bytes, fork.side(), acc, &has_soft));
   KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
                                       gfeat, gath_ws, ws_bytes - acc_bytes - soft_bytes, s.scratch, st, face_ranges,
-                                      nullptr, face_ranges ? raster_bins : nullptr));
+                                      nullptr));
   KL_CHECK_RC(fork.join());
   return has_soft ? acc_finalize<T>(acc, gfvi, (size_t)B * F * 6, true, st, s.scratch)
                   : (s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK);
@@ -1872,39 +1665,31 @@ extern "C" size_t kl_dibr_workspace_bytes(int batch, int height, int width, int 
   return std::max(a, std::max(b, c));
 }
 
-extern "C" size_t kl_dibr_bins_bytes(int batch, int height, int width, int num_faces) {
-  return make_bin_geom(batch, height, width, num_faces).bytes();
-}
-
 extern "C" size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum) {
   const size_t a = kl_dibr_rasterize_bwd_workspace_bytes(batch, height, width, num_faces, 8);
   const size_t b = soft_tile_bwd_items_bytes(batch, height, width, knum);
-  const size_t atomic_path = al256((size_t)batch * num_faces * 6 * sizeof(double)) + al256(b) + a;
-  const size_t slot_path = al256(soft_slots_ws_bytes(batch, num_faces)) + a;
-  return std::max(atomic_path, slot_path);
+  return al256((size_t)batch * num_faces * 6 * sizeof(double)) + al256(b) + a;
 }
 
 extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
                                int knum, const void *fvz, const void *fvi, const void *feat, const void *fnz,
                                float sigmainv, double bbox_pad, float multiplier, float eps, void *out_feat,
                                int64_t *out_idx, void *out_w, void *out_mask, uint8_t *hits, uint32_t *rec_face,
-                               void *rec_prob, int *seg_tot, int *scratch, uint32_t *face_ranges,
-                               uint32_t *raster_bins, uint32_t *soft_ranges, void *ws, size_t ws_bytes,
-                               kl_stream stream) {
+                               void *rec_prob, int *seg_tot, int *scratch, uint32_t *face_ranges, void *ws,
+                               size_t ws_bytes, kl_stream stream) {
   uint2 *fr = reinterpret_cast<uint2 *>(face_ranges);
-  uint2 *sr = reinterpret_cast<uint2 *>(soft_ranges);
   if (dtype == KL_F32)
     return dibr_fwd<float>(batch, height, width, num_faces, feat_dim, knum, (const float *)fvz, (const float *)fvi,
                            (const float *)feat, (const float *)fnz, sigmainv, bbox_pad, multiplier, eps,
                            (float *)out_feat, out_idx, (float *)out_w, (float *)out_mask,
                            SoftState<float>{hits, rec_face, (float *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
-                           S(stream), fr, raster_bins, sr);
+                           S(stream), fr);
   if (dtype == KL_F64)
     return dibr_fwd<double>(batch, height, width, num_faces, feat_dim, knum, (const double *)fvz, (const double *)fvi,
                             (const double *)feat, (const double *)fnz, sigmainv, bbox_pad, multiplier, eps,
                             (double *)out_feat, out_idx, (double *)out_w, (double *)out_mask,
                             SoftState<double>{hits, rec_face, (double *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
-                            S(stream), fr, raster_bins, sr);
+                            S(stream), fr);
   set_error("dibr_rasterization not implemented for this dtype");
   return KL_E_INVALID;
 }
@@ -1914,23 +1699,22 @@ extern "C" int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width
                                 const void *w, const void *fvi, const void *feat, const void *fnz, const void *mask,
                                 const uint8_t *hits, const uint32_t *rec_face, const void *rec_prob,
                                 const int *seg_tot, float sigmainv, float multiplier, float eps, void *gfvi,
-                                void *gfeat, int *scratch, const uint32_t *face_ranges, const uint32_t *raster_bins,
-                                const uint32_t *soft_ranges, void *ws, size_t ws_bytes, kl_stream stream) {
+                                void *gfeat, int *scratch, const uint32_t *face_ranges, void *ws, size_t ws_bytes,
+                                kl_stream stream) {
   const uint2 *fr = reinterpret_cast<const uint2 *>(face_ranges);
-  const uint2 *sr = reinterpret_cast<const uint2 *>(soft_ranges);
   if (dtype == KL_F32)
     return dibr_bwd<float>(
         batch, height, width, num_faces, feat_dim, knum, (const float *)grad_feat, (const float *)grad_mask, face_idx,
         (const float *)w, (const float *)fvi, (const float *)feat, (const float *)fnz, (const float *)mask,
         SoftState<float>{(uint8_t *)hits, (uint32_t *)rec_face, (float *)rec_prob, (int *)seg_tot, scratch},
-        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream), fr, raster_bins, sr);
+        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream), fr);
   if (dtype == KL_F64)
     return dibr_bwd<double>(
         batch, height, width, num_faces, feat_dim, knum, (const double *)grad_feat, (const double *)grad_mask,
         face_idx, (const double *)w, (const double *)fvi, (const double *)feat, (const double *)fnz,
         (const double *)mask,
         SoftState<double>{(uint8_t *)hits, (uint32_t *)rec_face, (double *)rec_prob, (int *)seg_tot, scratch},
-        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream), fr, raster_bins, sr);
+        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream), fr);
   set_error("dibr_rasterization backward not implemented for this dtype");
   return KL_E_INVALID;
 }

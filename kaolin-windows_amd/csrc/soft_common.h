@@ -198,15 +198,6 @@ int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T
                        const T *fvi, float sigmainv, float m, T *gfvi, bool accumulate, void *ws, size_t ws_bytes,
                        hipStream_t st, double *acc_out = nullptr, bool *has_sum = nullptr);
 size_t soft_tile_bwd_items_bytes(int B, int H, int W, int K);
-// kl_dibr_backward's soft half with per-face tile slots (no flush atomics): srng = the forward's
-// exact pixel ranges of the enlarged bboxes; soft_slots_combine adds the sums onto gfvi after it.
-template <typename T>
-int soft_tile_backward_slots(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
-                             const T *fvi, const uint2 *srng, float sigmainv, float m, void *ws, size_t ws_bytes,
-                             hipStream_t st);
-template <typename T>
-int soft_slots_combine(int B, int F, T *gfvi, const void *ws, int *reset, hipStream_t st);
-size_t soft_slots_ws_bytes(int B, int F);
 size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int F, int K);
 size_t soft_tile_ws_bytes(int B, int H, int W, int F);
 

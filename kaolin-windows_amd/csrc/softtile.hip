@@ -667,216 +667,6 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
   }
 }
 
-// ---------------------------------------------------------------- backward, per-face slots
-// kl_dibr_backward's soft half without the flush's memory-side atomics.  One 256-thread
-// workgroup per (tile, row pair) (XCD-banded like the gather; the heavy tiles at the
-// silhouette's poles spread over 4 workgroups), the hits summed per face in the LDS hash as
-// above; then each face's six sums are STORED (not added) into one of the face's slots:
-// slot k = 4 x the tile's position in the face's enlarged-bbox tile rectangle (the forward's soft
-// pixel ranges) + the row pair, so every (face, tile, row pair) has exactly one writer.  A slot's
-// flag byte marks it written.  Faces whose rectangle has more than SB_TPOS tiles (and hash
-// overflow) add into a zeroed double accumulator instead.  soft_slot_combine_kernel then sums a
-// face's written slots in slot order plus its accumulator, rounds once and adds the result to
-// the rasterizer's gradient -- the same exact double sums as the atomic flush, one writer per slot.
-constexpr int SB_TPOS = 8;                 // tile positions per face
-constexpr int SB_RP = 2;                   // rows per workgroup
-constexpr int SB_NP = TILE_H / SB_RP;      // workgroups (row pairs) per tile
-constexpr int SB_SLOTS = SB_TPOS * SB_NP;  // slots per face
-constexpr int SB_HC = 1024;
-
-__device__ __forceinline__ int soft_slot_of(uint2 r, int tx, int ty, int part) {
-  const int jx0 = (int)(r.x & 0xffffu), jx1 = (int)(r.x >> 16), jy0 = (int)(r.y & 0xffffu), jy1 = (int)(r.y >> 16);
-  if (jx0 > jx1 || jy0 > jy1) return -1;
-  const int ntx = jx1 / TILE_W - jx0 / TILE_W + 1, nty = jy1 / TILE_H - jy0 / TILE_H + 1;
-  if (ntx * nty > SB_TPOS) return -1;
-  return ((ty - jy0 / TILE_H) * ntx + (tx - jx0 / TILE_W)) * SB_NP + part;
-}
-
-template <typename T>
-__global__ void __launch_bounds__(256) soft_tile_bwd_slots_kernel(
-    const T *__restrict__ grad, const T *__restrict__ mask, const uint8_t *__restrict__ hits,
-    const uint32_t *__restrict__ rec_face, const T *__restrict__ rec_prob, const int *__restrict__ seg_tot,
-    const T *__restrict__ fvi, const uint2 *__restrict__ srng, BinGeom g, int F, int K, float sigmainv,
-    float multiplier, double *__restrict__ slots, uint8_t *__restrict__ flags, double *__restrict__ ovf,
-    int per_band) {
-  __shared__ int s_key[SB_HC];
-  __shared__ double s_val[SB_HC * 6];
-  __shared__ int s_used[SB_HC];
-  __shared__ int s_nused;
-  __shared__ double s_a[SB_RP][64];
-  __shared__ int s_pre[SB_RP][65];
-  __shared__ int s_rowpre[SB_RP + 1];
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int H = g.height, W = g.width;
-  const int nt = g.batch * g.tiles_y * g.tiles_x;
-  const int xcd = (int)(blockIdx.x % 8), rk = (int)(blockIdx.x / 8);
-  const int part = rk % SB_NP;
-  const int tile = xcd * per_band + rk / SB_NP;
-  if (tile >= nt) return;
-  const int tx = tile % g.tiles_x, ty = (tile / g.tiles_x) % g.tiles_y, b = tile / (g.tiles_x * g.tiles_y);
-  const int jr0 = ty * TILE_H + part * SB_RP;  // the workgroup's first row
-  if (threadIdx.x < SB_RP) {  // the rows' hit totals first: most row pairs have none
-    const int j = jr0 + (int)threadIdx.x;
-    s_rowpre[threadIdx.x + 1] = j < H ? seg_tot[((size_t)b * H + j) * g.tiles_x + tx] : 0;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    s_rowpre[0] = 0;
-    for (int r = 1; r <= SB_RP; r++) s_rowpre[r] += s_rowpre[r - 1];
-    s_nused = 0;
-  }
-  __syncthreads();
-  const int total = s_rowpre[SB_RP];
-  if (total == 0) return;
-  for (int q = threadIdx.x; q < SB_HC; q += blockDim.x) s_key[q] = -1;
-  for (int q = threadIdx.x; q < SB_HC * 6; q += blockDim.x) s_val[q] = 0.0;
-  ItemHash<T, SB_HC> hash{s_key, s_val, s_used, &s_nused};
-  const int ibase = tx * TILE_W;
-  if (wid < SB_RP) {  // row `wid`: the filled-slot prefix and -sigmainv * dLdp * (1 - allprob)
-    const int j = jr0 + wid, i = ibase + lane;
-    int kid = 0;
-    if (j < H && i < W) {
-      const size_t p = ((size_t)b * H + j) * W + i;
-      kid = hits[p];
-      if (kid) s_a[wid][lane] = -1.0 * (double)sigmainv * (double)grad[p] * (1.0 - (double)mask[p]);
-    }
-    int pre = kid;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(pre, o);
-      if (lane >= o) pre += u;
-    }
-    s_pre[wid][lane] = pre - kid;
-  }
-  __syncthreads();
-  const T ms = (T)multiplier;
-  const float sx = multiplier / (float)W, sy = multiplier / (float)H;
-  double *const gmesh = ovf + (size_t)b * F * 6;
-  for (int f = (int)threadIdx.x; f < total; f += blockDim.x) {
-    int r = 0;
-#pragma unroll
-    for (int k = 1; k < SB_RP; k++) r += s_rowpre[k] <= f ? 1 : 0;
-    const int e = f - s_rowpre[r];
-    int lo = 0;  // owner lane: last lane with s_pre[r][lo] <= e
-#pragma unroll
-    for (int st = 32; st > 0; st >>= 1)
-      if (s_pre[r][lo + st] <= e) lo += st;
-    const int j = jr0 + r;
-    const size_t o = ((size_t)(b * H + j) * g.tiles_x + tx) * 64 * (size_t)K + e;
-    const uint32_t rr = rec_face[o];
-    const T pr = rec_prob[o];
-    const int face = (int)(rr & 0x0fffffffu);
-    const int edgeid = (int)(rr >> 28) - 1;
-    const T x0 = (T)(sx * (float)(2 * (ibase + lo) + 1 - W));  // == pix_x
-    const T y0 = (T)(sy * (float)(H - 2 * j - 1));               // == pix_y
-    const T dLdz = (T)(s_a[r][lo] / (1.0 - (double)pr + SM_EPS) * (double)pr);
-    const T *fb = fvi + ((size_t)b * F + face) * 6;
-    T v[6];
-#pragma unroll
-    for (int c = 0; c < 6; c++) v[c] = fb[c] * ms;
-    int c0, c1;
-    T g0x, g0y, g1x, g1y;
-    soft_hit_grad<T>(v, edgeid, x0, y0, dLdz, multiplier, c0, c1, g0x, g0y, g1x, g1y);
-    hash.add(face, c0, c1, g0x, g0y, g1x, g1y, gmesh);
-  }
-  __syncthreads();
-  // one thread per (used slot, coordinate): store into the face's slot, or add into the
-  // accumulator when the face has no slot for this tile
-  const int n = s_nused;
-  const size_t fb0 = (size_t)b * F;
-  for (int u = threadIdx.x; u < n * 6; u += blockDim.x) {
-    const int sl = s_used[u / 6], c = u % 6;
-    const int face = s_key[sl];
-    const double v = s_val[sl * 6 + c];
-    const int k = soft_slot_of(srng[fb0 + face], tx, ty, part);
-    if (k >= 0) {
-      slots[((fb0 + face) * SB_SLOTS + k) * 6 + c] = v;
-      if (c == 0) flags[(fb0 + face) * SB_SLOTS + k] = 1;
-    } else if (v != 0.0) {
-      atomicAdd(gmesh + (size_t)face * 6 + c, v);
-    }
-  }
-}
-
-// out[f, c] = rasterizer's rounded sum (already in out) + (T)(written slots of f in slot order
-// + its accumulator); one thread per (face, coordinate).  `reset` (optional) is zeroed.
-template <typename T>
-__global__ void __launch_bounds__(256) soft_slot_combine_kernel(const double *__restrict__ slots,
-                                                                const uint8_t *__restrict__ flags,
-                                                                const double *__restrict__ ovf, T *__restrict__ out,
-                                                                int64_t n, int *__restrict__ reset) {
-  if (reset && blockIdx.x == 0 && threadIdx.x == 0) *reset = 0;
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= n) return;
-  const int64_t tf = t / 6;
-  const int c = (int)(t % 6);
-  const uint64_t *fp = reinterpret_cast<const uint64_t *>(flags + tf * SB_SLOTS);
-  double sum = 0.0;
-#pragma unroll
-  for (int q = 0; q < SB_SLOTS / 8; q++) {
-    const uint64_t fl = fp[q];
-    if (!fl) continue;
-#pragma unroll
-    for (int k = 0; k < 8; k++)
-      if ((fl >> (8 * k)) & 0xff) sum += slots[(tf * SB_SLOTS + q * 8 + k) * 6 + c];
-  }
-  sum += ovf[t];
-  out[t] = out[t] + (T)sum;
-}
-
-size_t soft_slots_ws_bytes(int B, int F) {
-  return al256((size_t)B * F * 6 * sizeof(double)) + al256((size_t)B * F * SB_SLOTS) +
-         al256((size_t)B * F * SB_SLOTS * 6 * sizeof(double));
-}
-
-// The soft half of kl_dibr_backward on `st`: zero the accumulator and flags (one fill), the
-// per-tile slot kernel.  soft_slots_combine() finishes it (after the rasterizer's gather).
-template <typename T>
-int soft_tile_backward_slots(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
-                             const T *fvi, const uint2 *srng, float sigmainv, float m, void *ws, size_t ws_bytes,
-                             hipStream_t st) {
-  KL_REQUIRE(ws_bytes >= soft_slots_ws_bytes(B, F), "dibr_rasterization backward: workspace too small");
-  KL_REQUIRE(F < (1 << 28), "dibr_rasterization backward: too many faces");
-  const size_t nacc = al256((size_t)B * F * 6 * sizeof(double)), nflag = al256((size_t)B * F * SB_SLOTS);
-  char *w = reinterpret_cast<char *>(ws);
-  KL_CHECK_RC(fill_async(w, 0, nacc + nflag, st));
-  if ((int64_t)B * H * W == 0 || K <= 0 || grad == nullptr) return KL_OK;
-  const BinGeom g = make_bin_geom(B, H, W, F);
-  const int nt = g.batch * g.tiles_y * g.tiles_x;
-  const int per_band = (int)cdiv(nt, 8);
-  hipLaunchKernelGGL((soft_tile_bwd_slots_kernel<T>), dim3((unsigned)(8 * per_band * SB_NP)), dim3(256), 0, st, grad,
-                     mask,
-                     (const uint8_t *)s.hits, (const uint32_t *)s.rec_face, (const T *)s.rec_prob,
-                     (const int *)s.seg_tot, fvi, srng, g, F, K, sigmainv, m,
-                     reinterpret_cast<double *>(w + nacc + nflag), reinterpret_cast<uint8_t *>(w + nacc),
-                     reinterpret_cast<double *>(w), per_band);
-  KL_CHECK_LAUNCH();
-  return KL_OK;
-}
-
-template <typename T>
-int soft_slots_combine(int B, int F, T *gfvi, const void *ws, int *reset, hipStream_t st) {
-  const int64_t n = (int64_t)B * F * 6;
-  if (n == 0) return reset ? fill_async(reset, 0, sizeof(int), st) : KL_OK;
-  const size_t nacc = al256((size_t)B * F * 6 * sizeof(double)), nflag = al256((size_t)B * F * SB_SLOTS);
-  const char *w = reinterpret_cast<const char *>(ws);
-  hipLaunchKernelGGL((soft_slot_combine_kernel<T>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st,
-                     reinterpret_cast<const double *>(w + nacc + nflag), reinterpret_cast<const uint8_t *>(w + nacc),
-                     reinterpret_cast<const double *>(w), gfvi, n, reset);
-  KL_CHECK_LAUNCH();
-  return KL_OK;
-}
-
-template int soft_tile_backward_slots<float>(int, int, int, int, int, const float *, const float *,
-                                             const SoftState<float> &, const float *, const uint2 *, float, float,
-                                             void *, size_t, hipStream_t);
-template int soft_tile_backward_slots<double>(int, int, int, int, int, const double *, const double *,
-                                              const SoftState<double> &, const double *, const uint2 *, float, float,
-                                              void *, size_t, hipStream_t);
-template int soft_slots_combine<float>(int, int, float *, const void *, int *, hipStream_t);
-template int soft_slots_combine<double>(int, int, double *, const void *, int *, hipStream_t);
-
 // workspace: bitmap | ghist[32], gdone (zeroed with the bitmap) | tile buckets | work items |
 // item count | pixel ranges | defer flags
 struct StWs {

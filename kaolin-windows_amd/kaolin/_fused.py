@@ -200,16 +200,13 @@ def soft_mask_backward_compact(grad, mask, state, face_vertices_image, sigmainv,
 
 
 def dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, face_vertices_image, face_features, face_normals_z,
-                  soft_mask, state, sigmainv, multiplier, eps, face_ranges=None, raster_bins=None):
+                  soft_mask, state, sigmainv, multiplier, eps, face_ranges=None):
     """dibr_rasterization's backward in one call (kl_dibr_backward): the soft-mask terms summed in
     double first, then the rasterizer's gather writes every face's gradient as its own rounded
     sum plus the soft mask's (as autograd adds the two).  grad_soft_mask may be None.
     -> grad_face_vertices_image, grad_face_features."""
     func = 'dibr_rasterization backward'
     B, H, W, D = grad_feats.shape
-    # dibr_forward's (2,B,F,2) ranges: the rasterizer's and the soft mask's
-    rr, sr = (face_ranges[0], face_ranges[1]) if face_ranges is not None and face_ranges.dim() == 4 else \
-        (face_ranges, None)
     F = face_vertices_image.shape[1]
     dev = face_vertices_image.device
     g_img = torch.empty_like(face_vertices_image)
@@ -224,8 +221,7 @@ def dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, face_vertices_i
             N.ptr(gm), N.ptr(face_idx), N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features),
             N.ptr(face_normals_z), N.ptr(soft_mask), N.ptr(state.hits), N.ptr(state.rec_face), N.ptr(state.rec_prob),
             N.ptr(state.seg_tot), float(sigmainv), float(multiplier), float(eps), N.ptr(g_img), N.ptr(g_feat),
-            N.ptr(state.scratch), N.ptr(rr), N.ptr(raster_bins), N.ptr(sr), N.ptr(ws), nbytes,
-            N.stream_of(dev)), func)
+            N.ptr(state.scratch), N.ptr(face_ranges), N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return g_img, g_feat
 
 
@@ -234,9 +230,7 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     """dibr_rasterization's forward in one call (kl_dibr_forward): rasterize with valid =
     face_normals_z >= 0 and the compact soft mask, sharing one binning pass.
     -> features (B,H,W,D), face_idx (B,H,W), weights (B,H,W,3), soft_mask (B,H,W), SoftMaskState,
-    face_ranges (2,B,F,2) int32 (each face's exact pixel ranges of the rasterizer [0] and of the soft
-    mask's enlarged bbox [1], for the backward), raster_bins
-    (uint8, the rasterizer's screen bins: with face_ranges, the backward's gather runs per tile).
+    face_ranges (B,F,2) int32 (each face's exact pixel ranges, for rasterize_backward).
     face_normals_z must have the dtype of face_vertices_image."""
     func = 'dibr_rasterization'
     N.require_gpu(func, face_vertices_z, face_vertices_image, face_normals_z)
@@ -262,8 +256,7 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     rec_prob = torch.empty(max(nrec, 1), dtype=dtype, device=dev)
     seg_tot = torch.empty(max(lib.kl_soft_mask_compact_segments(B, H, W), 1), dtype=torch.int32, device=dev)
     scratch = torch.empty(1, dtype=torch.int32, device=dev)
-    ranges = torch.empty((2, B, F, 2), dtype=torch.int32, device=dev)  # [0] raster, [1] soft-mask ranges
-    bins = torch.empty(max(lib.kl_dibr_bins_bytes(B, H, W, F), 4), dtype=torch.uint8, device=dev)
+    ranges = torch.empty((B, F, 2), dtype=torch.int32, device=dev)
     nbytes = lib.kl_dibr_workspace_bytes(B, H, W, F)
     ws = _ws(nbytes, dev)
     with N.on_device(dev), N.timed('dibr_forward', dev):
@@ -271,6 +264,5 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
             N.dtype_code(dtype), B, H, W, F, D, K, N.ptr(fvz), N.ptr(fvi), N.ptr(feat), N.ptr(fnz), float(sigmainv),
             float(boxlen * multiplier), float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w),
             N.ptr(mask), N.ptr(hits), N.ptr(rec_face), N.ptr(rec_prob), N.ptr(seg_tot), N.ptr(scratch),
-            N.ptr(ranges[0] if F > 0 else None), N.ptr(bins if F > 0 else None),
-            N.ptr(ranges[1] if F > 0 else None), N.ptr(ws), nbytes, N.stream_of(dev)), func)
-    return feats, idx, w, mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, scratch, K), ranges, bins
+            N.ptr(ranges if F > 0 else None), N.ptr(ws), nbytes, N.stream_of(dev)), func)
+    return feats, idx, w, mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, scratch, K), ranges

@@ -66,11 +66,11 @@ class DibrRasterizationCuda(Function):
         face_features = face_features.contiguous()
         face_normals_z = face_normals_z.detach().contiguous()
         if face_normals_z.dtype == face_vertices_image.dtype:  # one call, one shared binning pass
-            feats, face_idx, weights, soft_mask, state, ranges, bins = _fused.dibr_forward(
+            feats, face_idx, weights, soft_mask, state, ranges = _fused.dibr_forward(
                 height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z, sigmainv, boxlen,
                 knum, multiplier, eps)
         else:
-            ranges = bins = None
+            ranges = None
             feats, face_idx, weights = _fused.rasterize_forward(height, width, face_vertices_z, face_vertices_image,
                                                                 face_features, None, multiplier, eps,
                                                                 face_normals_z=face_normals_z)
@@ -81,13 +81,12 @@ class DibrRasterizationCuda(Function):
         ctx.sigmainv, ctx.multiplier, ctx.eps, ctx.knum = sigmainv, multiplier, eps, state.knum
         ctx.has_ranges = ranges is not None and ranges.numel() > 0
         ctx.save_for_backward(face_idx, weights, face_vertices_image, face_features, face_normals_z, soft_mask,
-                              ranges if ctx.has_ranges else None, bins if ctx.has_ranges else None,
-                              *state.tensors())
+                              ranges if ctx.has_ranges else None, *state.tensors())
         return feats, soft_mask, face_idx
 
     @staticmethod
     def backward(ctx, grad_feats, grad_soft_mask, grad_face_idx):
-        face_idx, weights, fvi, feat, fnz, soft_mask, ranges, bins, *st = ctx.saved_tensors
+        face_idx, weights, fvi, feat, fnz, soft_mask, ranges, *st = ctx.saved_tensors
         state = _fused.SoftMaskState(*st, ctx.knum)
         if grad_feats is None and grad_soft_mask is None:
             return None, None, None, None, None, None, None, None, None, None, None
@@ -95,11 +94,10 @@ class DibrRasterizationCuda(Function):
             grad_feats = torch.zeros(face_idx.shape + (feat.shape[-1],), dtype=feat.dtype, device=feat.device)
         if fnz.dtype == fvi.dtype:
             g_img, g_feat = _fused.dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, fvi, feat, fnz,
-                                                 soft_mask, state, ctx.sigmainv, ctx.multiplier, ctx.eps, ranges, bins)
+                                                 soft_mask, state, ctx.sigmainv, ctx.multiplier, ctx.eps, ranges)
         else:  # face_normals_z of another dtype: the two stages (the rasterizer's reads a valid mask)
             g_img, g_feat = _fused.rasterize_backward(grad_feats, face_idx, weights, fvi, feat, None, ctx.multiplier,
-                                                      ctx.eps, face_normals_z=fnz,
-                                                      face_ranges=None if ranges is None else ranges[0])
+                                                      ctx.eps, face_normals_z=fnz, face_ranges=ranges)
             if grad_soft_mask is not None:
                 _fused.soft_mask_backward_compact(grad_soft_mask, soft_mask, state, fvi, ctx.sigmainv,
                                                   ctx.multiplier, out=g_img)

@@ -35,15 +35,15 @@ def main():
     lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
     inp = bench.dibr_inputs([0.0, 1.5707963, 3.1415927, 4.712389], 'cuda')
     H, W = inp['H'], inp['W']
-    feats, idx, w, mask, state, ranges, bins = _fused.dibr_forward(H, W, inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'],
+    feats, idx, w, mask, state, ranges = _fused.dibr_forward(H, W, inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'],
                                                              7000., 0.02, 30, 1000., 1e-8)
     ref = None
     for fl in flags:
         lib.kl_dev_set_flags(fl)
         g = lambda: _fused.rasterize_backward(inp['g_feat'], idx, w, inp['fvi'], inp['feat'], None, 1000., 1e-8,  # noqa
-                                             face_normals_z=inp["fnz"], face_ranges=ranges[0])
+                                             face_normals_z=inp['fnz'], face_ranges=ranges)
         d = lambda: _fused.dibr_backward(inp['g_feat'], inp['g_mask'], idx, w, inp['fvi'], inp['feat'],  # noqa
-                                         inp["fnz"], mask, state, 7000., 1000., 1e-8, ranges, bins)
+                                         inp['fnz'], mask, state, 7000., 1000., 1e-8, ranges)
         tg, td = timeit(g), timeit(d)
         out = d()
         torch.cuda.synchronize()

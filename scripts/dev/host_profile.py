@@ -60,11 +60,11 @@ def main():
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     print(f'_fused.dibr_forward: {(t1 - t0) / reps * 1e6:.1f} us host')
-    feats, idx, w, mask, state, ranges, bins = f
+    feats, idx, w, mask, state, ranges = f
     t0 = time.perf_counter()
     for _ in range(reps):
         _fused.dibr_backward(inp['g_feat'], inp['g_mask'], idx, w, inp['fvi'], inp['feat'], inp['fnz'], mask, state,
-                             7000., 1000., 1e-8, ranges, bins)
+                             7000., 1000., 1e-8, ranges)
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     print(f'_fused.dibr_backward: {(t1 - t0) / reps * 1e6:.1f} us host')

@@ -43,9 +43,9 @@ def main():
         idx, v = combo[0][0], ','.join(f'{i}={x}' for i, x in combo)
         fw = lambda: _fused.dibr_forward(H, W, inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'], 7000., 0.02, 30,  # noqa
                                          1000., 1e-8)
-        feats, idx_, w, mask, state, ranges, bins = fw()
+        feats, idx_, w, mask, state, ranges = fw()
         d = lambda: _fused.dibr_backward(inp['g_feat'], inp['g_mask'], idx_, w, inp['fvi'], inp['feat'],  # noqa
-                                         inp["fnz"], mask, state, 7000., 1000., 1e-8, ranges, bins)
+                                         inp['fnz'], mask, state, 7000., 1000., 1e-8, ranges)
         print(f'params {v}: dibr_forward {timeit(fw):.1f} us, dibr_backward {timeit(d):.1f} us', flush=True)
     for i in range(8):
         lib.kl_dev_set_param(i, 0)
