@@ -1143,26 +1143,6 @@ struct GatherAcc {
       }
     }
   }
-  // the same with the face's features (cf, [corner][d], stride MAXD) and the pixel's incoming
-  // gradient (g) already in registers
-  __device__ __forceinline__ void add_regs(const T v[6], const T cf[3 * MAXD], int D, T w_a, T w_b, T w_c,
-                                           const T g[MAXD], float eps) {
-    BaryGrad<T> bg;
-    bg.init(v, w_a, w_b, w_c, eps);
-#pragma unroll
-    for (int d = 0; d < MAXD; d++) {
-      if (d < D) {
-        const T gd = g[d];
-        gf[d] += (double)(gd * w_a);
-        gf[MAXD + d] += (double)(gd * w_b);
-        gf[2 * MAXD + d] += (double)(gd * w_c);
-        T o[6];
-        bg.terms(gd, cf[d], cf[MAXD + d], cf[2 * MAXD + d], o);
-#pragma unroll
-        for (int q = 0; q < 6; q++) gi[q] += (double)o[q];
-      }
-    }
-  }
 };
 
 template <typename T, int MAXD, int LPF_ = LPF>
@@ -1183,15 +1163,6 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
   // latency hides behind the walk: an unconditional load from a clamped index
   double sv = 0.0;
   if (soft) sv = soft[(in ? tf : 0) * 6 + (s < 6 ? s : 5)];
-  // the face's vertices and features, loaded with its range (unconditional loads from a clamped
-  // index: one round trip for all of them instead of a chain)
-  const int64_t tfc = in ? tf : 0;
-  T v[6];
-#pragma unroll
-  for (int q = 0; q < 6; q++) v[q] = fvi[tfc * 6 + q];
-  T cf[3 * MAXD];  // [corner][d], stride MAXD
-#pragma unroll
-  for (int q = 0; q < 3 * MAXD; q++) cf[q] = (q % MAXD) < D ? feat[tfc * 3 * D + (q / MAXD) * D + q % MAXD] : (T)0;
   GatherAcc<T, MAXD> acc;
   acc.zero();
   int ix0, ix1, iy0, iy1;
@@ -1219,29 +1190,32 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
       queued = true;
       if (s == 0) big[atomicAdd(nbig, 1)] = (int)tf;
     } else {
+      T v[6];
+#pragma unroll
+      for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
+      const T *c = feat + tf * 3 * D;
       const int64_t pbase = (int64_t)b * H * W;
       RangeWalkN<LPF_> rw(ix0, ix1, iy0, iy1, s);
       while (rw.more()) {
-        // GATHER_BATCH pixels: face index, weights and incoming gradients all in flight together
-        // (unconditional loads; pixels past the range read the face's first pixel and are not
-        // counted)
-        int64_t fid[GATHER_BATCH];
-        T wv[GATHER_BATCH][3], gv[GATHER_BATCH][MAXD];
-        uint32_t live = 0;
+        // face_idx of GATHER_BATCH pixels in flight together; the (rare) hits then load
+        // their weights / grads one by one
+        int64_t px[GATHER_BATCH];
+        uint32_t hits = 0;
 #pragma unroll
         for (int u = 0; u < GATHER_BATCH; u++) {
-          if (rw.more()) live |= 1u << u;
-          const int64_t px = pbase + (int64_t)(iy0 + (rw.more() ? rw.row : 0)) * W + ix0 + (rw.more() ? rw.col : 0);
-          fid[u] = face_idx[px];
-#pragma unroll
-          for (int q = 0; q < 3; q++) wv[u][q] = wts[px * 3 + q];
-#pragma unroll
-          for (int d = 0; d < MAXD; d++) gv[u][d] = d < D ? grad_feat[px * D + d] : (T)0;
+          px[u] = pbase + (int64_t)(iy0 + rw.row) * W + ix0 + rw.col;
+          if (rw.more() && face_idx[px[u]] == f) hits |= 1u << u;
           rw.next();
         }
+#pragma unroll 1
+        for (; hits; hits &= hits - 1) {
+          const int u = __builtin_ctz(hits);
+          int64_t p = px[0];
 #pragma unroll
-        for (int u = 0; u < GATHER_BATCH; u++)
-          if (((live >> u) & 1u) && fid[u] == f) acc.add_regs(v, cf, D, wv[u][0], wv[u][1], wv[u][2], gv[u], eps);
+          for (int q = 1; q < GATHER_BATCH; q++)
+            if (u == q) p = px[q];
+          acc.add(v, c, D, wts[p * 3 + 0], wts[p * 3 + 1], wts[p * 3 + 2], grad_feat + p * D, eps);
+        }
       }
     }
   }

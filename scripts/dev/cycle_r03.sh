@@ -11,3 +11,7 @@ cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/prof" -o run \
   -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-extra --no-p2m --steps 10 > "$ROOT/$OUT/prof_bench.log" 2>&1
+if [ -n "$HOSTPROF" ]; then
+  cd "$ROOT"
+  timeout -k 10 240 python scripts/dev/host_profile.py 200 > "$OUT/host_profile.txt" 2>&1
+fi
