@@ -165,8 +165,19 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
   KL_CHECK_LAUNCH();
   int64_t n = F;
   int rc = KL_OK;
+  // two buffers, ping-pong: a level's children overwrite the level before its parents (each
+  // level only reads the previous one); a buffer is re-allocated only when a level needs more
+  // room than it has, so the allocations are the growth steps, not one per level
+  Tri<T> *buf[2] = {cur, nullptr};
+  size_t cap[2] = {(size_t)F, 0};
+  int ci = 0;
   for (int level = 0; n > 0 && level < 64; level++) {
-    Tri<T> *nxt = (Tri<T> *)alloc(ctx, (size_t)n * 4 * sizeof(Tri<T>));
+    const int ni = 1 - ci;
+    if (cap[ni] < (size_t)n * 4) {
+      buf[ni] = (Tri<T> *)alloc(ctx, (size_t)n * 4 * sizeof(Tri<T>));
+      cap[ni] = (size_t)n * 4;
+    }
+    Tri<T> *nxt = buf[ni];
     if (!nxt) {
       set_error("trianglemeshes_to_voxelgrids: allocation failed");
       rc = KL_E_ALLOC;
@@ -174,8 +185,8 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
     }
     rc = fill_async(counter, 0, sizeof(unsigned long long), st);
     if (rc) break;
-    hipLaunchKernelGGL((subdivide_kernel<T, G>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, n, cur, level == 0,
-                       thr, R, grid, nxt, counter);
+    hipLaunchKernelGGL((subdivide_kernel<T, G>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, n, buf[ci],
+                       level == 0, thr, R, grid, nxt, counter);
     if (hipGetLastError() != hipSuccess ||
         hipMemcpyAsync(hcount, counter, sizeof(unsigned long long), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess) {
@@ -184,7 +195,7 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
       break;
     }
     n = (int64_t)*hcount;
-    cur = nxt;
+    ci = ni;
   }
   (void)hipHostFree(hcount);
   return rc;

@@ -5,7 +5,8 @@
  * compiled with -O2 -ffp-contract=off (see oracle/Makefile).  Single-threaded except two
  * loops over independent items (p2m forward per point, mesh_to_spc barycentrics per leaf),
  * which are OpenMP-parallel so that full-size parity checks finish in seconds; each item
- * writes only its own outputs, so results do not depend on the thread count.
+ * writes only its own outputs, so results do not depend on the thread count.  The DIB-R loops
+ * run on or_set_threads() threads (1 unless bench.py's all-threads CPU leg sets more).
  *
  * Floating-point kernels (rasterize, soft mask, point->triangle distance, sided
  * distance) live in oracle_typed.inc, instantiated for float and double.  This
@@ -31,6 +32,11 @@
  * rows j with j % g_row_step == 0 (default 1 = every row). */
 static int g_row_step = 1;
 void or_set_row_step(int s) { g_row_step = s > 0 ? s : 1; }
+/* Threads of the DIB-R loops (bench.py's all-threads cpu_baseline leg; default 1, the checker).
+ * The forward loops write only their own pixels; the backward's double accumulators are then
+ * added with OpenMP atomics, so only the order of exact double sums changes. */
+static int g_threads = 1;
+void or_set_threads(int n) { g_threads = n > 0 ? n : 1; }
 
 #define T float
 #define SUF f32
