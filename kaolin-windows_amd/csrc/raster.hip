@@ -1240,24 +1240,17 @@ __device__ __forceinline__ void gather_one(
   }
 }
 
-// One thread per (face, lane) of the LPF-lane groups; PERSIST: a grid-stride loop over the same
-// threads from a grid sized to the resident waves (dev bit 19, A/B timing).
-template <typename T, int MAXD, int LPF_ = LPF, bool PERSIST = false>
+// One thread per (face, lane) of the LPF-lane groups.  (A persistent grid-stride version, sized
+// to the resident waves, measured 82 us against 62 at cfg3: the waves are not dispatch-bound.)
+template <typename T, int MAXD, int LPF_ = LPF>
 __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
     const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
     const T *__restrict__ nz, int B, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
     T *__restrict__ grad_ffeat, int *__restrict__ big, int *__restrict__ nbig, const uint2 *__restrict__ rng,
     const double *__restrict__ soft) {
-  if (!PERSIST) {
-    gather_one<T, MAXD, LPF_>(blockIdx.x * (int64_t)blockDim.x + threadIdx.x, grad_feat, face_idx, wts, fvi, feat,
-                              valid, nz, B, H, W, F, D, m, eps, grad_fvi, grad_ffeat, big, nbig, rng, soft);
-    return;
-  }
-  const int64_t total = (int64_t)B * F * LPF_;
-  for (int64_t t0 = blockIdx.x * (int64_t)blockDim.x; t0 < total; t0 += (int64_t)gridDim.x * blockDim.x)
-    gather_one<T, MAXD, LPF_>(t0 + threadIdx.x, grad_feat, face_idx, wts, fvi, feat, valid, nz, B, H, W, F, D, m, eps,
-                              grad_fvi, grad_ffeat, big, nbig, rng, soft);
+  gather_one<T, MAXD, LPF_>(blockIdx.x * (int64_t)blockDim.x + threadIdx.x, grad_feat, face_idx, wts, fvi, feat,
+                            valid, nz, B, H, W, F, D, m, eps, grad_fvi, grad_ffeat, big, nbig, rng, soft);
 }
 
 // one 256-thread workgroup per large face; block reduction of the per-thread partials
@@ -1350,18 +1343,8 @@ static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T 
   if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
   // 8 lanes per face (measured: 4 lanes 62.7 us, 8 lanes 58 us, 16 lanes 91 us at cfg3)
-  if (g_dev_flags & (1 << 19)) {
-    int dev_id = 0, ncu = 256;
-    if (hipGetDevice(&dev_id) == hipSuccess)
-      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_id);
-    const unsigned grid = (unsigned)std::min<int64_t>(cdiv(nf * LPF, 256), (int64_t)ncu * 4);
-    hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD, LPF, true>), dim3(grid), dim3(256), 0, st, grad,
-                       face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
-  } else {
-    hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0,
-                       st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig,
-                       rng, soft);
-  }
+  hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st,
+                     grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
   KL_CHECK_LAUNCH();
   hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(256), dim3(256), 0, st, grad, face_idx, w, fvi,
                      feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
