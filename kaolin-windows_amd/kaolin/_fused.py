@@ -212,7 +212,7 @@ def dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, face_vertices_i
     g_img = torch.empty_like(face_vertices_image)
     g_feat = torch.empty_like(face_features)
     lib = N.lib()
-    nbytes = lib.kl_dibr_bwd_workspace_bytes(B, H, W, F, state.knum)
+    nbytes = N.size('kl_dibr_bwd_workspace_bytes', B, H, W, F, state.knum)
     ws = _ws(nbytes, dev)
     gm = grad_soft_mask.contiguous() if grad_soft_mask is not None else None
     with N.on_device(dev), N.timed('dibr_backward', dev):
@@ -251,13 +251,13 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     w = torch.empty((B, H, W, 3), dtype=dtype, device=dev)
     mask = torch.empty((B, H, W), dtype=dtype, device=dev)
     hits = torch.empty((B, H, W), dtype=torch.uint8, device=dev)
-    nrec = lib.kl_soft_mask_compact_records(B, H, W, K)
+    nrec = N.size('kl_soft_mask_compact_records', B, H, W, K)
     rec_face = torch.empty(max(nrec, 1), dtype=torch.int32, device=dev)
     rec_prob = torch.empty(max(nrec, 1), dtype=dtype, device=dev)
-    seg_tot = torch.empty(max(lib.kl_soft_mask_compact_segments(B, H, W), 1), dtype=torch.int32, device=dev)
+    seg_tot = torch.empty(max(N.size('kl_soft_mask_compact_segments', B, H, W), 1), dtype=torch.int32, device=dev)
     scratch = torch.empty(1, dtype=torch.int32, device=dev)
     ranges = torch.empty((B, F, 2), dtype=torch.int32, device=dev)
-    nbytes = lib.kl_dibr_workspace_bytes(B, H, W, F)
+    nbytes = N.size('kl_dibr_workspace_bytes', B, H, W, F)
     ws = _ws(nbytes, dev)
     with N.on_device(dev), N.timed('dibr_forward', dev):
         N.check(lib.kl_dibr_forward(

@@ -169,6 +169,19 @@ def stream_of(device):
     return _raw_stream(torch.cuda.current_device() if idx is None else idx)
 
 
+_SIZES = {}
+
+
+def size(name, *args):
+    """A `kl_*_bytes` / `kl_*_records` size query, memoised by its arguments (pure functions of the
+    shapes: the eager step asks the same ones every call)."""
+    key = (name,) + args
+    v = _SIZES.get(key)
+    if v is None:
+        v = _SIZES[key] = int(getattr(lib(), name)(*args))
+    return v
+
+
 _WS = {}
 
 
