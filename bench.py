@@ -625,29 +625,54 @@ def tutorial_setup(device, views=4, H=512, W=512, tex=512):
         shift=torch.zeros((3,), dtype=torch.float32, device=device, requires_grad=True),
         texture=torch.rand((1, 3, tex, tex), generator=g).to(device).requires_grad_(True),
         gt_image=torch.rand((views, H, W, 3), generator=g).to(device),
+        gt_uv=torch.rand((views, H, W, 2), generator=g).to(device),
         gt_mask=(torch.rand((views, H, W), generator=g) > 0.5).float().to(device))
     st['vopt'] = torch.optim.Adam([st['vertices'], st['shift']], lr=5e-4)
     st['topt'] = torch.optim.Adam([st['texture']], lr=1e-2)
     return st
 
 
-def tutorial_step(st):
-    """One iteration of dibr_tutorial.ipynb cell 14 (render() of cell 12 inlined): zero_grad,
-    center_points + shift, prepare_vertices(camera_transform=...), dibr_rasterization with the
-    feature LIST [face_uvs, ones], texture_mapping (bilinear), clamp(image * mask), L1 image loss
-    + mask_iou, backward, both Adam steps.  The tutorial's laplacian regulariser (a dense V x V
-    matmul, off the rendering path) is left out."""
+def _tutorial_render(st):
+    """render() of dibr_tutorial.ipynb cell 12 up to the rasterizer: center_points + shift,
+    prepare_vertices(camera_transform=...), dibr_rasterization with the feature LIST
+    [face_uvs, ones] -> (uv map, hard mask), soft mask."""
     import torch
     import kaolin as kal
     B = st['B']
-    st['vopt'].zero_grad()
-    st['topt'].zero_grad()
     vb = kal.ops.pointcloud.center_points(st['vertices']) + st['shift']
     fvc, fvi, fn = kal.render.mesh.prepare_vertices(vb.repeat(B, 1, 1), st['faces'], st['cam_proj'],
                                                     camera_transform=st['cam_transform'])
     attrs = [st['face_uvs'].repeat(B, 1, 1, 1), torch.ones((B, st['F'], 3, 1), device=fvc.device)]
     (coords, mask), soft_mask, _ = kal.render.mesh.dibr_rasterization(
         st['H'], st['W'], fvc[:, :, :, -1], fvi, attrs, fn[:, :, -1], rast_backend='cuda')
+    return coords, mask, soft_mask
+
+
+def tutorial_shape_step(st):
+    """The tutorial's call shape: prepare_vertices -> dibr_rasterization(list
+    [uv, ones]) -> L1 + mask_iou -> backward, eager.  L1 is on the rasterized features (uv map x
+    hard mask against a target); the texture lookup and the optimiser are in tutorial_step."""
+    import torch
+    import kaolin as kal
+    coords, mask, soft_mask = _tutorial_render(st)
+    l1 = torch.mean(torch.abs(coords * mask - st['gt_uv']))
+    loss = l1 + kal.metrics.render.mask_iou(soft_mask, st['gt_mask'])
+    loss.backward()
+    st['vertices'].grad = st['shift'].grad = None
+    return loss
+
+
+def tutorial_step(st):
+    """One whole iteration of dibr_tutorial.ipynb cell 14 (render() of cell 12 inlined): zero_grad,
+    the render above, texture_mapping (bilinear), clamp(image * mask), L1 image loss + mask_iou,
+    backward, both Adam steps.  The tutorial's laplacian regulariser (a dense V x V matmul, off the
+    rendering path) is left out."""
+    import torch
+    import kaolin as kal
+    B = st['B']
+    st['vopt'].zero_grad()
+    st['topt'].zero_grad()
+    coords, mask, soft_mask = _tutorial_render(st)
     image = kal.render.mesh.texture_mapping(coords, st['texture'].repeat(B, 1, 1, 1), mode='bilinear')
     image = torch.clamp(image * mask, 0., 1.)
     image_loss = torch.mean(torch.abs(image - st['gt_image']))
@@ -660,28 +685,41 @@ def tutorial_step(st):
 
 
 def tutorial_leg(device, steps, warmup=3):
-    """The tutorial loop's eager rate (the caller the reference's users run), with the share of
-    its time in the DIB-R fwd+bwd (HIP events on the two native ops) beside it."""
+    """The tutorial's call shape, eager (the caller the reference's users run): `value`; with the
+    DIB-R fwd+bwd's own HIP-event time beside it, and the whole tutorial iteration (texture lookup,
+    optimiser) as `full_iteration`."""
     import torch
     from kaolin import _native
     st = tutorial_setup(device)
+    px = st['B'] * st['H'] * st['W']
     for _ in range(warmup):
-        tutorial_step(st)
-    ms = _wall_ms(lambda: tutorial_step(st), steps)
+        tutorial_shape_step(st)
+    ms = _wall_ms(lambda: tutorial_shape_step(st), steps)
+    # steady-state throughput: the loop without a sync per step (as bench's eager line)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tutorial_shape_step(st)
+    torch.cuda.synchronize()
+    ms_loop = (time.perf_counter() - t0) / steps * 1e3
     timer = _native.OpTimer()
     _native.set_timer(timer)
     for _ in range(5):
-        tutorial_step(st)
+        tutorial_shape_step(st)
     _native.set_timer(None)
     ops = {k: round(v, 4) for k, v in timer.summary_ms().items()}
-    torch.cuda.synchronize()
-    px = st['B'] * st['H'] * st['W']
-    return {'metric': 'DIB-R tutorial loop (dibr_tutorial.ipynb cells 12/14) Mpixels/s, eager, 4 views x 512^2, '
-                      '50k faces, feature list [uv, ones], texture 512^2, Adam',
-            'value': round(px / (ms * 1e-3) / 1e6, 2), 'ms_per_step': round(ms, 4),
-            'native_op_ms': ops,
-            'timing': 'wall clock per iteration (median), eager autograd, everything the tutorial iteration runs '
-                      'except its laplacian regulariser and the dataloader'}
+    for _ in range(warmup):
+        tutorial_step(st)
+    ms_full = _wall_ms(lambda: tutorial_step(st), max(3, steps // 2))
+    return {'metric': 'DIB-R tutorial call shape Mpixels/s, eager: prepare_vertices -> dibr_rasterization([uv, ones]) '
+                      '-> L1 + mask_iou -> backward (4 views x 512^2, 50k faces)',
+            'value': round(px / (ms_loop * 1e-3) / 1e6, 2), 'ms_per_step': round(ms_loop, 4),
+            'ms_per_step_synced': round(ms, 4), 'native_op_ms': ops,
+            'full_iteration': {'ms': round(ms_full, 4), 'value': round(px / (ms_full * 1e-3) / 1e6, 2),
+                               'what': 'dibr_tutorial.ipynb cell 14 minus the laplacian term: + texture_mapping '
+                                       '(bilinear, 512^2 texture), clamp, L1 image loss, both Adam steps'},
+            'timing': 'value: back-to-back eager steps between two synchronizes (as the headline eager line); '
+                      'ms_per_step_synced: median with a synchronize per step'}
 
 
 # ----------------------------------------------------------------------------- p2m (cfg2)

@@ -491,6 +491,21 @@ int kl_voxelgrid_mark_f64(int64_t num_vertices, const double *points, int64_t nu
                           int resolution, kl_dtype grid_dtype, void *grid, kl_alloc_fn alloc, void *alloc_ctx,
                           kl_stream stream);
 
+/* texture_mapping (kaolin/render/mesh/utils.py:23-75): coords (B, N, 2) in [0, 1] (OpenGL, y up;
+ * clamped), texture (B, C, TH, TW) -> out (B, N, C), as torch.nn.functional.grid_sample with
+ * align_corners=False and padding_mode='border' after the reference's [-1, 1] / y mapping.
+ * mode 0 = 'nearest', 1 = 'bilinear'.  Backward: grad_coords (B, N, 2) and/or grad_texture
+ * (B, C, TH, TW) (either may be NULL); the texture terms are summed in double (workspace:
+ * kl_texture_mapping_bwd_workspace_bytes) and rounded once; terms of a zero incoming gradient
+ * are skipped (torch's grid_sample adds them with float atomics). */
+int kl_texture_mapping_forward(kl_dtype dtype, int mode, int batch, int64_t num_points, int channels, int tex_height,
+                               int tex_width, const void *coords, const void *texture, void *out, kl_stream stream);
+size_t kl_texture_mapping_bwd_workspace_bytes(int batch, int channels, int tex_height, int tex_width);
+int kl_texture_mapping_backward(kl_dtype dtype, int mode, int batch, int64_t num_points, int channels,
+                                int tex_height, int tex_width, const void *grad_out, const void *coords,
+                                const void *texture, void *grad_coords, void *grad_texture, void *workspace,
+                                size_t workspace_bytes, kl_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

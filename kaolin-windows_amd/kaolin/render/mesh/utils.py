@@ -175,16 +175,63 @@ def prepare_vertices(vertices, faces, camera_proj, camera_rot=None, camera_trans
     return PrepareVerticesHip.apply(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform, batches)
 
 
+class TextureMappingHip(Function):
+    """texture_mapping's clamp -> [-1, 1] (y reversed) -> grid_sample(border, align_corners=False)
+    chain as one HIP launch each way (csrc/texture.hip): the forward and the coordinate gradient
+    with grid_sample's own arithmetic; the texture gradient summed in double (deterministic), with
+    the terms of zero incoming gradients skipped."""
+
+    @staticmethod
+    def forward(ctx, coords, texture_maps, mode):
+        B, C, TH, TW = texture_maps.shape
+        c = coords.contiguous()
+        tex = texture_maps.contiguous()
+        n = c.numel() // (2 * B) if B else 0
+        out = torch.empty((B, n, C), dtype=tex.dtype, device=tex.device)
+        with N.on_device(tex.device):
+            N.check(N.lib().kl_texture_mapping_forward(N.dtype_code(tex.dtype), mode, B, n, C, TH, TW, N.ptr(c),
+                                                       N.ptr(tex), N.ptr(out), N.stream_of(tex.device)),
+                    'texture_mapping')
+        ctx.mode, ctx.n = mode, n
+        ctx.save_for_backward(c, tex)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        c, tex = ctx.saved_tensors
+        B, C, TH, TW = tex.shape
+        need_c, need_t, _ = ctx.needs_input_grad
+        gc = torch.empty_like(c) if need_c else None
+        gt = torch.empty_like(tex) if need_t else None
+        if gc is None and gt is None:
+            return None, None, None
+        nbytes = N.size('kl_texture_mapping_bwd_workspace_bytes', B, C, TH, TW) if need_t else 0
+        ws = N.workspace(nbytes, tex.device) if need_t else None
+        with N.on_device(tex.device):
+            N.check(N.lib().kl_texture_mapping_backward(
+                N.dtype_code(tex.dtype), ctx.mode, B, ctx.n, C, TH, TW, N.ptr(grad_out.contiguous()), N.ptr(c),
+                N.ptr(tex), N.ptr(gc), N.ptr(gt), N.ptr(ws), nbytes, N.stream_of(tex.device)),
+                'texture_mapping backward')
+        return gc, gt, None
+
+
 def texture_mapping(texture_coordinates, texture_maps, mode='nearest'):
     r"""Sample ``texture_maps`` (B, C, h', w') at ``texture_coordinates`` (B, h, w, 2) or (B, N, 2)
     in OpenGL convention ([0, 1], y up) -> (B, h, w, C) / (B, N, C) (render/mesh/utils.py:23-75).
 
     The caller-side step after dibr_rasterization in the reference's tutorial loop
     (dibr_tutorial.ipynb cell 12): coordinates clamped to [0, 1], mapped to grid_sample's
-    [-1, 1] with y reversed, border padding, align_corners=False -- torch's grid_sample, as the
-    reference (not part of the HIP path)."""
+    [-1, 1] with y reversed, border padding, align_corners=False.  GPU f32 / f64 tensors with
+    mode 'nearest' or 'bilinear' run one HIP launch each way (TextureMappingHip); anything else
+    runs the reference's torch chain."""
     batch_size = texture_coordinates.shape[0]
     num_channels = texture_maps.shape[1]
+    if (texture_coordinates.is_cuda and texture_maps.is_cuda and texture_coordinates.device == texture_maps.device
+            and mode in ('nearest', 'bilinear') and texture_maps.dtype in (torch.float32, torch.float64)
+            and texture_coordinates.dtype == texture_maps.dtype and texture_maps.dim() == 4
+            and texture_coordinates.shape[-1] == 2 and texture_maps.shape[0] == batch_size):
+        out = TextureMappingHip.apply(texture_coordinates, texture_maps, 1 if mode == 'bilinear' else 0)
+        return out.reshape(batch_size, *texture_coordinates.shape[1:-1], num_channels)
     coords = texture_coordinates.reshape(batch_size, -1, 1, 2)
     coords = torch.clamp(coords, 0., 1.) * 2 - 1
     coords[..., 1] = -coords[..., 1]

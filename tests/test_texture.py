@@ -1,0 +1,97 @@
+"""texture_mapping (render/mesh/utils.py:23-75) -- the tutorial's uv lookup after dibr_rasterization.
+
+GPU tensors run csrc/texture.hip; the oracle is the reference's own chain (clamp, [-1, 1] with y
+reversed, torch grid_sample with border padding), run with torch on the same device in float64
+and in the input dtype.  Forward and coordinate gradient follow grid_sample's arithmetic; the
+texture gradient is a double sum of the same float terms (torch adds them with float atomics),
+so it is compared with the float64 chain at the dtype's resolution.
+"""
+import numpy as np
+import pytest
+import torch
+
+DEV = 'cuda'
+
+
+def _ref_chain(coords, tex, mode):
+    b = coords.shape[0]
+    c = torch.clamp(coords.reshape(b, -1, 1, 2), 0., 1.) * 2 - 1
+    c = torch.stack([c[..., 0], -c[..., 1]], -1)
+    out = torch.nn.functional.grid_sample(tex, c, mode=mode, align_corners=False, padding_mode='border')
+    return out.permute(0, 2, 3, 1).reshape(b, *coords.shape[1:-1], tex.shape[1])
+
+
+def _inputs(dtype, dev, B=2, H=37, W=53, C=3, TH=29, TW=41, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    coords = torch.rand((B, H, W, 2), generator=g, dtype=torch.float64) * 1.2 - 0.1
+    coords[0, 0, :6, 0] = torch.tensor([0., 1., 0.5, 0.25, 1. / TW, 0.5 / TW], dtype=torch.float64)
+    coords[0, 1, :4, 1] = torch.tensor([0., 1., 0.5, 0.5 / TH], dtype=torch.float64)
+    coords[1, :3] = 0.  # uncovered pixels of a rasterized uv map: all on one corner texel
+    tex = torch.rand((B, C, TH, TW), generator=g, dtype=torch.float64)
+    return coords.to(dtype).to(dev), tex.to(dtype).to(dev)
+
+
+def test_cpu_tensors_take_the_reference_chain():
+    import kaolin as kal
+    coords, tex = _inputs(torch.float32, 'cpu')
+    for mode in ('nearest', 'bilinear'):
+        assert torch.equal(kal.render.mesh.texture_mapping(coords, tex, mode), _ref_chain(coords, tex, mode))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('mode', ['bilinear', 'nearest'])
+def test_forward_and_grads_vs_reference_chain(dtype, mode):
+    import kaolin as kal
+    from kaolin.render.mesh.utils import TextureMappingHip
+    coords, tex = _inputs(dtype, DEV)
+    c1, t1 = coords.clone().requires_grad_(True), tex.clone().requires_grad_(True)
+    out = kal.render.mesh.texture_mapping(c1, t1, mode)
+    assert out.grad_fn is not None and 'TextureMappingHip' in type(out.grad_fn).__name__ or \
+        any('TextureMappingHip' in type(n[0]).__name__ for n in out.grad_fn.next_functions if n[0] is not None)
+    c2, t2 = coords.clone().requires_grad_(True), tex.clone().requires_grad_(True)
+    ref = _ref_chain(c2, t2, mode)
+    assert out.shape == ref.shape
+    # forward: grid_sample's own operations
+    tol = 1e-6 if dtype == torch.float32 else 1e-14
+    torch.testing.assert_close(out, ref, rtol=tol, atol=tol)
+    g = torch.rand(out.shape, generator=torch.Generator().manual_seed(1), dtype=torch.float64).to(dtype).to(DEV)
+    g[1, :3] = 0.  # zero incoming gradient on the corner-texel pixels (the masked-out uv of the tutorial)
+    out.backward(g)
+    ref.backward(g)
+    torch.testing.assert_close(c1.grad, c2.grad, rtol=tol * 10, atol=tol * 10)
+    # texture: double sum vs torch's float atomics; both against the float64 chain
+    c3, t3 = coords.double().clone().requires_grad_(True), tex.double().clone().requires_grad_(True)
+    _ref_chain(c3, t3, mode).backward(g.double())
+    scale = float(t3.grad.abs().max())
+    err_ours = float((t1.grad.double() - t3.grad).abs().max())
+    err_torch = float((t2.grad.double() - t3.grad).abs().max())
+    assert err_ours <= max(err_torch, 1e-15 * scale, (2e-7 if dtype == torch.float32 else 1e-15) * scale), \
+        (err_ours, err_torch, scale)
+    # deterministic: a second backward gives the same bits
+    t4 = tex.clone().requires_grad_(True)
+    TextureMappingHip.apply(coords, t4, 1 if mode == 'bilinear' else 0).backward(g)
+    assert torch.equal(t4.grad, t1.grad)
+
+
+@pytest.mark.gpu
+def test_tutorial_shape_texture_grad_flows_to_vertices():
+    """The tutorial's chain: dibr_rasterization's uv map -> texture_mapping -> image loss: the
+    HIP lookup's coordinate gradient reaches face_vertices_image as torch's does."""
+    import kaolin as kal
+    import bench
+    inp = bench.dibr_inputs([0.3, 2.0], DEV, H=64, W=96)
+    tex = torch.rand((2, 3, 64, 64), generator=torch.Generator().manual_seed(2)).to(DEV)
+    grads = []
+    for use_hip in (True, False):
+        fvi = inp['fvi'].clone().requires_grad_(True)
+        t = tex.clone().requires_grad_(True)
+        (uv, m), soft, idx = kal.render.mesh.dibr_rasterization(64, 96, inp['fvz'], fvi,
+                                                                [inp['feat'][..., :2].contiguous(),
+                                                                 inp['feat'][..., 2:].contiguous()], inp['fnz'])
+        img = kal.render.mesh.texture_mapping(uv, t, 'bilinear') if use_hip else _ref_chain(uv, t, 'bilinear')
+        torch.clamp(img * m, 0., 1.).sum().backward()
+        grads.append((fvi.grad, t.grad))
+    torch.testing.assert_close(grads[0][0], grads[1][0], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(grads[0][1], grads[1][1], rtol=1e-5, atol=1e-5)
+    assert np.isfinite(grads[0][0].cpu().numpy()).all()
