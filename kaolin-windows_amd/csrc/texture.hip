@@ -5,8 +5,9 @@
 // torch.nn.functional.grid_sample(..., align_corners=False, padding_mode='border').  Here the
 // whole chain is one launch forward and one backward, with grid_sample's own arithmetic
 // (aten/src/ATen/native/cuda/GridSampler.cu: unnormalize, border clip, the four bilinear corner
-// weights and their accumulation order), so the forward equals the torch chain's and the
-// coordinate gradient equals autograd's through it.
+// weights and their accumulation order, and the multiply-adds torch's ROCm build contracts into
+// fma -- written as explicit fma here, since this library compiles with -ffp-contract=off), so
+// the forward equals the torch chain's and the coordinate gradient equals autograd's through it.
 //
 // The texture gradient is where the torch chain spends its time: grid_sample's backward adds
 // every (pixel, channel, corner) term with a float atomic, zero incoming gradients included --
@@ -24,7 +25,7 @@ namespace kl {
 // clipped to 0 as fmax does), safe_downgrade_to_int_range (non-finite -> -100: out of bounds)
 template <typename T>
 __device__ __forceinline__ T tex_source(T c, int size) {
-  T x = ((c + (T)1) * (T)size - (T)1) / (T)2;
+  T x = fma(c + (T)1, (T)size, (T)-1) / (T)2;  // torch's build contracts a * b - 1
   x = fmin((T)(size - 1), fmax(x, (T)0));
   return isfinite(x) ? x : (T)-100;
 }
@@ -33,7 +34,7 @@ __device__ __forceinline__ T tex_source(T c, int size) {
 // times the clip gradient
 template <typename T>
 __device__ __forceinline__ T tex_source_grad(T c, int size, T &mult) {
-  T x = ((c + (T)1) * (T)size - (T)1) / (T)2;
+  T x = fma(c + (T)1, (T)size, (T)-1) / (T)2;
   const T lim = (T)(size - 1);
   T gclip = (T)1;
   if (x <= (T)0) {
@@ -94,10 +95,11 @@ __global__ void __launch_bounds__(256) texture_fwd_kernel(int B, int64_t N, int 
   for (int c = 0; c < C; c++) {
     const T *p = tb + c * plane;
     T o = (T)0;
-    if (b_nw) o += p[(size_t)y0 * TW + x0] * nw;
-    if (b_ne) o += p[(size_t)y0 * TW + x0 + 1] * ne;
-    if (b_sw) o += p[(size_t)(y0 + 1) * TW + x0] * sw;
-    if (b_se) o += p[(size_t)(y0 + 1) * TW + x0 + 1] * se;
+    // out += value * weight as the contracted fma of torch's build
+    if (b_nw) o = fma(p[(size_t)y0 * TW + x0], nw, o);
+    if (b_ne) o = fma(p[(size_t)y0 * TW + x0 + 1], ne, o);
+    if (b_sw) o = fma(p[(size_t)(y0 + 1) * TW + x0], sw, o);
+    if (b_se) o = fma(p[(size_t)(y0 + 1) * TW + x0 + 1], se, o);
     out[t * C + c] = o;
   }
 }
@@ -150,26 +152,26 @@ __global__ void __launch_bounds__(256) texture_bwd_kernel(int B, int64_t N, int 
     double *a = ab ? ab + c * plane : nullptr;
     if (b_nw) {
       const T val = p[o_nw];
-      gix -= val * (iy_se - iy) * g;
-      giy -= val * (ix_se - ix) * g;
+      gix = fma(-(val * (iy_se - iy)), g, gix);
+      giy = fma(-(val * (ix_se - ix)), g, giy);
       if (a && g != (T)0) atomicAdd(a + o_nw, (double)(nw * g));
     }
     if (b_ne) {
       const T val = p[o_nw + 1];
-      gix += val * (iy_sw - iy) * g;
-      giy -= val * (ix - ix_sw) * g;
+      gix = fma(val * (iy_sw - iy), g, gix);
+      giy = fma(-(val * (ix - ix_sw)), g, giy);
       if (a && g != (T)0) atomicAdd(a + o_nw + 1, (double)(ne * g));
     }
     if (b_sw) {
       const T val = p[o_nw + TW];
-      gix -= val * (iy - iy_ne) * g;
-      giy += val * (ix_ne - ix) * g;
+      gix = fma(-(val * (iy - iy_ne)), g, gix);
+      giy = fma(val * (ix_ne - ix), g, giy);
       if (a && g != (T)0) atomicAdd(a + o_nw + TW, (double)(sw * g));
     }
     if (b_se) {
       const T val = p[o_nw + TW + 1];
-      gix += val * (iy - iy_nw) * g;
-      giy += val * (ix - ix_nw) * g;
+      gix = fma(val * (iy - iy_nw), g, gix);
+      giy = fma(val * (ix - ix_nw), g, giy);
       if (a && g != (T)0) atomicAdd(a + o_nw + TW + 1, (double)(se * g));
     }
   }
