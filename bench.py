@@ -586,6 +586,23 @@ def prepare_leg(device, steps, views=4):
     chain = lambda: run(_prepare_vertices_torch)  # noqa: E731
     ms_f = _wall_ms(fused, max(5, steps))
     ms_t = _wall_ms(chain, max(5, steps))
+    # parity at bench size: max-abs of the fused path against the reference's own f32 chain
+    # (torch ops on the same GPU) and of both against float64, outputs and vertex / camera grads
+    res = {}
+    for name, fn, dt in (('fused', lambda *a: kal.render.mesh.prepare_vertices(*a[:5]), torch.float32),
+                         ('chain', _prepare_vertices_torch, torch.float32),
+                         ('f64', _prepare_vertices_torch, torch.float64)):
+        lv = [x.detach().to(dt).requires_grad_(True) for x in (v, rot, trans)]
+        out = fn(lv[0], faces, proj.to(dt), lv[1], lv[2], None)
+        torch.autograd.backward(out, [g.to(dt) for g in grads])
+        res[name] = [o.detach().double() for o in out] + [x.grad.double() for x in lv]
+    names = ['face_vertices_camera', 'face_vertices_image', 'face_normals', 'grad_vertices', 'grad_rot',
+             'grad_trans']
+    mx = lambda a, b: float((a - b).abs().max())  # noqa: E731
+    parity = {n: {'fused_vs_f32_chain': mx(res['fused'][k], res['chain'][k]),
+                  'fused_vs_f64': mx(res['fused'][k], res['f64'][k]),
+                  'f32_chain_vs_f64': mx(res['chain'][k], res['f64'][k])} for k, n in enumerate(names)}
+    v.grad = rot.grad = trans.grad = None
     # forward: vertices + faces read, three outputs written; backward: the three grads read,
     # the per-vertex double sums (5 x 8 B, atomics), the vertices re-read, grad_vertices written
     fwd_bytes = B * V * 12 + F * 24 + B * F * (36 + 24 + 12)
@@ -596,7 +613,8 @@ def prepare_leg(device, steps, views=4):
             'bytes': nb, 'roofline': {'bound': 'hbm', 'achieved': round(nb / (ms_f * 1e-3) / 1e9, 1),
                                       'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                                       'frac': round(nb / (ms_f * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-            'timing': 'wall clock per fwd+bwd incl. Python / autograd (median of runs)'}
+            'timing': 'wall clock per fwd+bwd incl. Python / autograd (median of runs)',
+            'parity_max_abs': parity}
 
 
 # ----------------------------------------------------------------------------- tutorial loop

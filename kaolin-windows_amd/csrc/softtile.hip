@@ -212,27 +212,11 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
           uint64_t cm = transpose64(rm, lane);
           if (!active) cm = 0;
           const int base = blk * 64;
-          // the lane's covering entries in index order, four at a time: their face ids are read
-          // from LDS together, then written to the next slots (no read-write chain per slot)
           while (cm) {
-            int qs[4], n = 0;
-            const int room = K - kid;
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-              if (cm && u < room) {
-                qs[u] = __builtin_ctzll(cm);
-                cm &= cm - 1;
-                n++;
-              }
-            uint32_t fv[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-              if (u < n) fv[u] = L_face[base + qs[u]];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-              if (u < n) s_face[(kid + u) * 64 + lane] = fv[u];
-            kid += n;
-            if (kid >= K) {
+            const int q = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            s_face[kid * 64 + lane] = L_face[base + q];
+            if (++kid >= K) {
               active = false;
               cm = 0;
             }
@@ -261,24 +245,10 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
             all += v;
           }
           const int base = blk * 64;
-          while (cm && slot < K) {  // four at a time, as above
-            int qs[4], n = 0;
-            const int room = K - slot;
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-              if (cm && u < room) {
-                qs[u] = __builtin_ctzll(cm);
-                cm &= cm - 1;
-                n++;
-              }
-            uint32_t fv[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-              if (u < n) fv[u] = L_face[base + qs[u]];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-              if (u < n) s_face[(slot + u) * 64 + lane] = fv[u];
-            slot += n;
+          while (cm && slot < K) {
+            s_face[slot * 64 + lane] = L_face[base + __builtin_ctzll(cm)];
+            cm &= cm - 1;
+            slot++;
           }
           kid = min(K, kid + all);
           active = active && kid < K;
