@@ -524,6 +524,37 @@ def test_dibr_rasterization_fused_grads_vs_oracle(kal, which):
     assert torch.equal(a.grad, g1)
 
 
+def test_compiled_node_equals_python_node(kal, monkeypatch):
+    """csrc/torch_ops.cpp's compiled autograd node (the eager default) against the ctypes / Python
+    node (kaolin/_fused.py): forward and gradients bit-equal, features as a list, a retained
+    second backward included."""
+    from kaolin import _ext
+    assert _ext.get() is not None, 'the compiled node is not built (kaolin/_lib/ext)'
+    import bench
+    inp = bench.dibr_inputs([0.3, 2.0], DEV, H=96, W=128)
+    fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+    runs = []
+    for use_ext in (True, False):
+        if not use_ext:
+            monkeypatch.setattr(_ext, '_mod', None)
+        a = fvi.clone().requires_grad_(True)
+        u = feat[..., :2].contiguous().requires_grad_(True)
+        o = feat[..., 2:].contiguous().requires_grad_(True)
+        (fu, fo), mask, idx = kal.render.mesh.dibr_rasterization(96, 128, fvz, a, [u, o], fnz)
+        name = type(mask.grad_fn).__name__
+        assert ('CppNode' in name or 'DibrRasterization' in name) if use_ext else 'DibrRasterizationCuda' in name
+        g = torch.Generator(device='cpu').manual_seed(5)
+        grads = [torch.rand(t.shape, generator=g).to(DEV) for t in (fu, fo, mask)]
+        torch.autograd.backward([fu, fo, mask], grads, retain_graph=True)
+        first = (a.grad.clone(), u.grad.clone(), o.grad.clone())
+        a.grad = u.grad = o.grad = None
+        torch.autograd.backward([fu, fo, mask], grads)
+        assert torch.equal(a.grad, first[0]) and torch.equal(u.grad, first[1]) and torch.equal(o.grad, first[2])
+        runs.append((fu, fo, mask, idx) + first)
+    for x, y in zip(runs[0], runs[1]):
+        assert torch.equal(x, y)
+
+
 def test_dibr_bench_full_size_fused_equals_C_chain(kal):
     """cfg3 at full size (4 views, 512^2, 50k faces): the fused single-node path's
     outputs equal the reference-contract chain (packed _C rasterizer + _C soft mask)
