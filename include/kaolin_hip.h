@@ -408,6 +408,35 @@ int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int16_t *point
                 kl_alloc_fn alloc, void *alloc_ctx, int32_t **nuggets, float **depth,
                 int64_t *num_hits, kl_stream stream);
 
+/* Fixed-capacity raytrace (no reference counterpart: raytrace_cuda.cu:557-560 reads each level's
+ * count back to size the next).  The same levels with every count kept on the device: nothing is
+ * read back, so the call can be captured into a HIP graph.  nuggets (capacity,2) int32 and depth
+ * (capacity, with_exit?2:1) f32 are caller-allocated; result (2) int64 device output = (rows
+ * written, 1 if some level held more than `capacity` nuggets).  When truncated, the rows are the
+ * first rows of kl_raytrace's output (ray-major, front-to-back order is kept).  Rows past
+ * result[0]: nugget (-1, -1), depth 0.  num_rays and capacity < 2^28. */
+size_t kl_raytrace_fixed_workspace_bytes(int64_t num_rays, int64_t capacity, int with_exit);
+int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, const int32_t *exsum,
+                      const float *ray_o, const float *ray_d, int64_t num_rays, uint32_t target_level,
+                      int return_depth, int with_exit, int64_t capacity, int32_t *nuggets, float *depth,
+                      int64_t *result, void *workspace, size_t workspace_bytes, kl_stream stream);
+
+/* raytrace.cpp:111-166 generate_primary_rays_cuda (deprecated upstream; bindings.cpp:86).
+ * eye / at / up (3) and world (4x4 row-major) float on the host; ray_o, ray_d (height*width, 3)
+ * f32 device outputs.  The reference's pixel of row t is (t % width, t / height). */
+int kl_generate_primary_rays(uint32_t height, uint32_t width, const float *eye, const float *at,
+                             const float *up, float fov, const float *world, float *ray_o, float *ray_d,
+                             kl_stream stream);
+
+/* raytrace.cpp:234-283 generate_shadow_rays_cuda (deprecated upstream; bindings.cpp:88).
+ * ray_o, ray_d (num,3) f32 device; light (3) and plane (4) float on the host; src, dst (num,3)
+ * f32 and map (num) int32 device outputs, of which the first *count rows are the answer
+ * (*count on the host: one device-to-host read, as the reference's cudaMemcpy). */
+size_t kl_generate_shadow_rays_workspace_bytes(int64_t num);
+int kl_generate_shadow_rays(int64_t num, const float *ray_o, const float *ray_d, const float *light,
+                            const float *plane, float *src, float *dst, int32_t *map, int64_t *count,
+                            void *workspace, size_t workspace_bytes, kl_stream stream);
+
 /* raytrace.cpp:216-240 mark_pack_boundaries_cuda: boundaries (N) int32 (1 at pack starts). */
 int kl_mark_pack_boundaries(kl_dtype dtype, int64_t num, const void *pack_ids, int32_t *boundaries,
                             kl_stream stream);
@@ -461,7 +490,10 @@ int kl_unbatched_mesh_intersection(kl_dtype dtype, int64_t num_points, int64_t n
  * -> contains (B,P) bool bytes (odd crossing count).  workspace:
  * kl_check_sign_workspace_bytes(dtype, B, F, P) bytes (no initialisation needed); the (y, z)
  * grid's face lists are allocated through `alloc` once their length is known (one 8-byte
- * device-to-host read and a stream synchronisation). */
+ * device-to-host read and a stream synchronisation).  alloc == NULL: the capturable form --
+ * nothing is read back; the lists use the workspace's fixed room, and when they do not fit
+ * every point is tested against every face on the device (same answers, O(P F)); a face
+ * index outside [0, V) is then clamped, not reported.  Same for kl_unbatched_mesh_intersection. */
 size_t kl_check_sign_workspace_bytes(kl_dtype dtype, int64_t batch_size, int64_t num_faces, int64_t num_points);
 int kl_check_sign(kl_dtype dtype, int64_t batch_size, int64_t num_vertices, int64_t num_faces, int64_t num_points,
                   const void *verts, const int64_t *faces, const void *points, const void *maxlen,

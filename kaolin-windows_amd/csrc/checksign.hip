@@ -254,9 +254,10 @@ template <bool FILL, typename T>
 __global__ void __launch_bounds__(256)
     cs_bin_kernel(int64_t F, int G, const CsRec<T> *__restrict__ rec, const float *__restrict__ mbox,
                   int *__restrict__ cnt, const int64_t *__restrict__ offs, CsRec<T> *__restrict__ list,
-                  unsigned long long *__restrict__ total) {
+                  unsigned long long *__restrict__ total, const int *__restrict__ ovf) {
   __shared__ int s_c[kCsWin];
   __shared__ int s_r[4][4];
+  if (FILL && ovf && *ovf) return;  // capturable entry: the lists did not fit (cs_brute_kernel answers)
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.y, f = (int64_t)blockIdx.x * 256 + tid;
   int cy0 = 0, cy1 = -1, cz0 = 0, cz1 = -1;
@@ -456,9 +457,9 @@ __global__ void __launch_bounds__(256)
 // unit -> cell (uoffs: the units' scan, offset by uoffs[0])
 __global__ void __launch_bounds__(256)
     cs_unitmap_kernel(int64_t ncells, const int *__restrict__ ucnt, const int64_t *__restrict__ uoffs,
-                      int64_t *__restrict__ unit_cell) {
+                      int64_t *__restrict__ unit_cell, const int *__restrict__ ovf) {
   const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= ncells) return;
+  if (c >= ncells || (ovf && *ovf)) return;
   const int u = ucnt[c];
   const int64_t o = uoffs[c] - uoffs[0];
   for (int s = 0; s < u; s++) unit_cell[o + s] = c;
@@ -486,8 +487,14 @@ __global__ void __launch_bounds__(256)
                          const int64_t *__restrict__ poffs, const CsPt<T> *__restrict__ sorted,
                          const int *__restrict__ cnt, const int64_t *__restrict__ offs,
                          const CsRec<T> *__restrict__ list, int *__restrict__ acc, T *__restrict__ counts,
-                         uint8_t *__restrict__ contains) {
+                         uint8_t *__restrict__ contains, const unsigned long long *__restrict__ dunits,
+                         const int *__restrict__ ovf) {
   constexpr int NG = 256 / kCsGroup;
+  // capturable entry: the grid covers the workspace's unit room, the unit count is on the device
+  if (ovf) {
+    if (*ovf) return;
+    nunits = (int64_t)*dunits;
+  }
   __shared__ CsRec<T> s_rec[NG][kCsStage];
   const int g = threadIdx.x / kCsGroup, gl = threadIdx.x % kCsGroup;
   const int64_t u = (int64_t)blockIdx.x * NG + g;
@@ -539,7 +546,8 @@ template <typename T>
 __global__ void __launch_bounds__(256)
     cs_finalize_kernel(int64_t P, int G, const int64_t *__restrict__ poffs, const CsPt<T> *__restrict__ sorted,
                        const float *__restrict__ mbox, const int *__restrict__ ucnt, const int *__restrict__ acc,
-                       T *__restrict__ counts, uint8_t *__restrict__ contains) {
+                       T *__restrict__ counts, uint8_t *__restrict__ contains, const int *__restrict__ ovf) {
+  if (ovf && *ovf) return;
   const int64_t b = blockIdx.y, GG = (int64_t)G * G;
   const int64_t s0 = poffs[b * GG] - poffs[0], s1 = poffs[(b + 1) * GG] - poffs[0];
   const int64_t j = s0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -548,6 +556,34 @@ __global__ void __launch_bounds__(256)
   if (ucnt[b * GG + cs_point_cell(pt.q, mbox + b * 8, G)] <= 1) return;
   const int64_t row = b * P + pt.p;
   const int count = acc[row];
+  if (counts) counts[row] = (T)count;
+  if (contains) contains[row] = (uint8_t)(count & 1);
+}
+
+// Capturable entry (no allocator): the face lists and the unit map must fit the workspace's
+// fixed room, known only on the device.  ovf = 1 when they do not; the list kernels then exit and
+// cs_brute_kernel answers every point against every face record instead -- the same cs_cross
+// tests over a superset of each point's cell list, so the same counts, at O(P F) cost.
+__global__ void cs_capacity_kernel(unsigned long long *__restrict__ ctl, unsigned long long list_cap,
+                                   unsigned long long unit_cap) {
+  if (threadIdx.x == 0) ((int *)(ctl + 2))[1] = (ctl[0] > list_cap || ctl[1] > unit_cap) ? 1 : 0;
+}
+template <typename T>
+__global__ void __launch_bounds__(256)
+    cs_brute_kernel(int64_t P, int64_t F, const T *__restrict__ points, const T *__restrict__ maxlen,
+                    const CsRec<T> *__restrict__ rec, T *__restrict__ counts, uint8_t *__restrict__ contains,
+                    const int *__restrict__ ovf) {
+  if (!*ovf) return;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, b = blockIdx.y;
+  if (i >= P) return;
+  const int64_t row = b * P + i;
+  T q[3];
+  cs_load_point(points, maxlen, b, row, q);
+  int count = 0;
+  for (int64_t f = 0; f < F; f++) {
+    const CsRec<T> &r = rec[b * F + f];
+    count += cs_cross(q[0], q[1], q[2], r.p, r.p + 3, r.p + 6, r.bb);
+  }
   if (counts) counts[row] = (T)count;
   if (contains) contains[row] = (uint8_t)(count & 1);
 }
@@ -634,7 +670,9 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   }
   const CsWs L = cs_ws_layout(B, F, P, sizeof(T));
   KL_REQUIRE(ws && ws_bytes >= L.total, "check_sign: workspace too small");
-  KL_REQUIRE(alloc != nullptr, "check_sign: allocator callback required");
+  // alloc == null: the capturable entry -- no host round trip (fixed room in the workspace,
+  // cs_brute_kernel past it; a bad face index is clamped, not reported)
+  const bool capturable = alloc == nullptr;
   int G = L.G;
   uint8_t *w = (uint8_t *)ws;
   int32_t *pslot = (int32_t *)(w + L.pslot);
@@ -647,6 +685,7 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   CsFaces<T> fsrc = src;
   fsrc.bad = (int *)(w + L.ctl + 16);
   int *acc = (int *)(w + L.acc);
+  int *d_ovf = (int *)(w + L.ctl + 20);
   const T *ml = (const T *)maxlen;
   if (src.faces && !maxlen) {
     KL_REQUIRE(src.V > 0, "check_sign: verts has no vertices");
@@ -658,7 +697,7 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   if (src.faces) fsrc.maxlen = ml;
   const int64_t ntiles = cdiv(F, kCsTile);
   // (dev flag 1 << 25: points in input order, no counting sort)
-  const bool sort_points = !(g_dev_flags & (1 << 25));
+  const bool sort_points = capturable || !(g_dev_flags & (1 << 25));
   KL_CHECK_RC(fill_async(w + L.ctl, 0, 32, st));
   hipLaunchKernelGGL(cs_prep_kernel<T>, dim3((unsigned)ntiles, (unsigned)B), dim3(kCsTile), 0, st, F, fsrc, rec,
                      tbox);
@@ -674,7 +713,8 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
     KL_CHECK_LAUNCH();
     KL_CHECK_RC(fill_async(cnt, 0, (size_t)(3 * ncells + 1) * 4, st));
     hipLaunchKernelGGL((cs_bin_kernel<false, T>), fgrid, dim3(256), 0, st, F, G, (const CsRec<T> *)rec,
-                       (const float *)mbox, cnt, (const int64_t *)nullptr, (CsRec<T> *)nullptr, d_total);
+                       (const float *)mbox, cnt, (const int64_t *)nullptr, (CsRec<T> *)nullptr, d_total,
+                       (const int *)nullptr);
     KL_CHECK_LAUNCH();
     if (sort_points) {
       hipLaunchKernelGGL(cs_pcount_kernel<T>, pgrid, dim3(256), 0, st, P, G, (const T *)points, ml,
@@ -686,6 +726,7 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
                          (const int *)cnt, cnt + 2 * ncells, d_total + 1);
       KL_CHECK_LAUNCH();
     }
+    if (capturable) break;
     KL_CHECK_HIP(hipMemcpyAsync(ctl, d_total, sizeof(CsCtl), hipMemcpyDeviceToHost, st));
     KL_CHECK_HIP(hipStreamSynchronize(st));
     KL_REQUIRE(!ctl->bad, "check_sign: index out of range in self (a face index is outside [0, num_vertices))");
@@ -695,19 +736,28 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
     G = G / 2 > 1 ? G / 2 : 1;
     KL_CHECK_RC(fill_async(d_total, 0, 16, st));
   }
-  const int64_t total = (int64_t)ctl->total;
-  KL_REQUIRE(total < ((int64_t)1 << 31), "check_sign: face lists too long");
   const int64_t ncells = B * (int64_t)G * G;
+  const int64_t unit_room = 2 * ncells;
+  if (capturable) {
+    // (dev flag 1 << 26: no list room, so that tests reach cs_brute_kernel on small meshes)
+    hipLaunchKernelGGL(cs_capacity_kernel, dim3(1), dim3(64), 0, st, d_total,
+                       (unsigned long long)((g_dev_flags & (1 << 26)) ? 0 : L.list_cap),
+                       (unsigned long long)unit_room);
+    KL_CHECK_LAUNCH();
+  }
+  const int64_t total = capturable ? 0 : (int64_t)ctl->total;
+  KL_REQUIRE(total < ((int64_t)1 << 31), "check_sign: face lists too long");
   size_t tb = L.temp_bytes;
   KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, CsCountIt(cnt, CsToI64()), offs, (int)(3 * ncells + 1),
                                                 st));
-  const int64_t nunits = sort_points ? (int64_t)ctl->units : 0;
+  // (capturable: an upper bound for the grid, the count itself is read on the device)
+  const int64_t nunits = capturable ? unit_room : sort_points ? (int64_t)ctl->units : 0;
   // the lists, then the unit -> cell map: in the workspace when both fit (its unit room is
   // 2 * ncells of the initial grid: units <= ncells + total / kCsStage, and total <= list_cap =
   // 16 entries per face <= kCsStage * ncells when kCsStage >= 16), else from the allocator
   static_assert(kCsStage >= 16, "check_sign: the workspace's unit room assumes >= 16 records per unit");
   const size_t list_bytes = (size_t)(total > 0 ? total : 1) * sizeof(CsRec<T>);
-  const bool in_ws = (size_t)total <= L.list_cap && nunits <= 2 * B * (int64_t)L.G * L.G;
+  const bool in_ws = capturable || ((size_t)total <= L.list_cap && nunits <= 2 * B * (int64_t)L.G * L.G);
   uint8_t *lbuf = in_ws ? w + L.list
                         : (uint8_t *)alloc(alloc_ctx, cs_align(list_bytes) + (size_t)(nunits > 0 ? nunits : 1) * 8);
   if (!lbuf) {
@@ -718,7 +768,8 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
   int64_t *unit_cell = (int64_t *)(lbuf + (in_ws ? L.list_cap * sizeof(CsRec<T>) : cs_align(list_bytes)));
   KL_CHECK_RC(fill_async(cnt, 0, (size_t)ncells * 4, st));
   hipLaunchKernelGGL((cs_bin_kernel<true, T>), fgrid, dim3(256), 0, st, F, G, (const CsRec<T> *)rec,
-                     (const float *)mbox, cnt, (const int64_t *)offs, list, (unsigned long long *)nullptr);
+                     (const float *)mbox, cnt, (const int64_t *)offs, list, (unsigned long long *)nullptr,
+                     capturable ? (const int *)d_ovf : nullptr);
   KL_CHECK_LAUNCH();
   if (sort_points) {
     const int64_t *poffs = offs + ncells, *uoffs = offs + 2 * ncells;
@@ -727,17 +778,24 @@ static int check_sign_grid(int64_t B, int64_t F, int64_t P, const void *points, 
                        (const float *)mbox, (const int32_t *)pslot, poffs, sorted);
     KL_CHECK_LAUNCH();
     hipLaunchKernelGGL(cs_unitmap_kernel, dim3((unsigned)cdiv(ncells, 256)), dim3(256), 0, st, ncells, ucnt, uoffs,
-                       unit_cell);
+                       unit_cell, capturable ? (const int *)d_ovf : nullptr);
     KL_CHECK_LAUNCH();
     KL_CHECK_RC(fill_async(acc, 0, (size_t)(B * P) * 4, st));
     if (nunits > 0) {
       hipLaunchKernelGGL(cs_cell_check_kernel<T>, dim3((unsigned)cdiv(nunits, 256 / kCsGroup)), dim3(256), 0, st, nunits, P,
                          (int64_t)G * G, (const int64_t *)unit_cell, uoffs, ucnt, poffs, (const CsPt<T> *)sorted,
-                         (const int *)cnt, (const int64_t *)offs, (const CsRec<T> *)list, acc, (T *)counts, contains);
+                         (const int *)cnt, (const int64_t *)offs, (const CsRec<T> *)list, acc, (T *)counts, contains,
+                         (const unsigned long long *)(d_total + 1), capturable ? (const int *)d_ovf : nullptr);
       KL_CHECK_LAUNCH();
     }
     hipLaunchKernelGGL(cs_finalize_kernel<T>, pgrid, dim3(256), 0, st, P, G, poffs, (const CsPt<T> *)sorted,
-                       (const float *)mbox, ucnt, (const int *)acc, (T *)counts, contains);
+                       (const float *)mbox, ucnt, (const int *)acc, (T *)counts, contains,
+                       capturable ? (const int *)d_ovf : nullptr);
+    if (capturable) {
+      KL_CHECK_LAUNCH();
+      hipLaunchKernelGGL(cs_brute_kernel<T>, pgrid, dim3(256), 0, st, P, F, (const T *)points, ml,
+                         (const CsRec<T> *)rec, (T *)counts, contains, (const int *)d_ovf);
+    }
   } else {
     hipLaunchKernelGGL(cs_grid_check_kernel<T>, pgrid, dim3(256), 0, st, P, G, (const T *)points, ml,
                        (const float *)mbox, (const int *)cnt, (const int64_t *)offs, (const CsRec<T> *)list,

@@ -867,11 +867,14 @@ struct RayIn {
 };
 
 // decide (raytrace_cuda.cu:63-222): info = children count / keep flag; depth at the target level
+// (fixed-capacity entry: the count is read from dnum on the device and info is zeroed up to span)
 __global__ void rt_decide_kernel(RayIn in, int64_t num, const int2 *__restrict__ nug, uint32_t *__restrict__ info,
-                                 float *__restrict__ depth, uint32_t level, int last, int with_depth, int with_exit) {
+                                 float *__restrict__ depth, uint32_t level, int last, int with_depth, int with_exit,
+                                 const uint32_t *__restrict__ dnum, int64_t span) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t > num) return;
-  if (t == num) {
+  if (dnum) num = *dnum;
+  if (t > span) return;
+  if (t >= num) {
     info[t] = 0;
     return;
   }
@@ -909,7 +912,7 @@ __global__ void rt_decide_kernel(RayIn in, int64_t num, const int2 *__restrict__
 
 __global__ void rt_subdivide_kernel(RayIn in, int64_t num, const int2 *__restrict__ nin, int2 *__restrict__ nout,
                                     const uint32_t *__restrict__ info, const uint32_t *__restrict__ psum,
-                                    uint32_t level) {
+                                    uint32_t level, int64_t cap) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= num || !info[t]) return;
   const int ridx = nin[t].x, pidx = nin[t].y;
@@ -931,25 +934,45 @@ __global__ void rt_subdivide_kernel(RayIn in, int64_t num, const int2 *__restric
     for (uint32_t j = 0; j < 8; j++) {
       if (__popc(code ^ j) != h || !(ob & (1u << j))) continue;
       const uint32_t c = (uint32_t)__popc(ob & ((2u << j) - 1));
-      nout[base] = make_int2(ridx, (int)(s + c));
+      if (base < cap) nout[base] = make_int2(ridx, (int)(s + c));
       base++;
     }
 }
 
 __global__ void rt_compact_kernel(int64_t num, const int2 *__restrict__ nin, const float *__restrict__ din,
                                   int2 *__restrict__ nout, float *__restrict__ dout, int dd,
-                                  const uint32_t *__restrict__ info, const uint32_t *__restrict__ psum) {
+                                  const uint32_t *__restrict__ info, const uint32_t *__restrict__ psum, int64_t cap) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= num || !info[t]) return;
   const uint32_t o = psum[t];
+  if (o >= cap) return;
   nout[o] = nin[t];
   if (dout)
     for (int k = 0; k < dd; k++) dout[(int64_t)o * dd + k] = din[t * dd + k];
 }
 
-__global__ void rt_init_kernel(int64_t n, int2 *__restrict__ nug) {
+__global__ void rt_init_kernel(int64_t n, int2 *__restrict__ nug, uint32_t *__restrict__ dnum,
+                               int64_t *__restrict__ result) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t < n) nug[t] = make_int2((int)t, 0);
+  if (t == 0 && dnum) {
+    *dnum = (uint32_t)n;
+    result[0] = 0;
+    result[1] = 0;
+  }
+}
+
+// fixed-capacity entry, after a level's scan: the next level's count on the device, clipped to
+// the capacity (the nuggets kept are then a prefix of the full list: the lists stay in ray,
+// front-to-back order and a nugget's children follow its predecessors'); result = (rows,
+// truncated)
+__global__ void rt_count_kernel(const uint32_t *__restrict__ total, uint32_t cap, uint32_t *__restrict__ dnum,
+                                int64_t *__restrict__ result, int last) {
+  if (threadIdx.x != 0) return;
+  const uint32_t n = *total;
+  *dnum = n < cap ? n : cap;
+  if (n > cap) result[1] = 1;
+  if (last) result[0] = n < cap ? n : cap;
 }
 
 template <typename S>
@@ -1092,7 +1115,8 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
   int2 *n0 = (int2 *)sc.get(num * sizeof(int2));
   if (!n0) return KL_E_ALLOC;
   if (num > 0) {
-    hipLaunchKernelGGL(rt_init_kernel, dim3((unsigned)cdiv(num, 256)), dim3(256), 0, st, num, n0);
+    hipLaunchKernelGGL(rt_init_kernel, dim3((unsigned)cdiv(num, 256)), dim3(256), 0, st, num, n0, (uint32_t *)nullptr,
+                       (int64_t *)nullptr);
     KL_CHECK_LAUNCH();
   }
   *depth = nullptr;
@@ -1104,7 +1128,7 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
     if (last && return_depth) d0 = (float *)sc.get(num * dd * sizeof(float));
     if (!info || !psum || (last && return_depth && !d0)) return KL_E_ALLOC;
     hipLaunchKernelGGL(rt_decide_kernel, dim3((unsigned)cdiv(num + 1, 256)), dim3(256), 0, st, in, num, n0, info, d0,
-                       l, last, return_depth, with_exit);
+                       l, last, return_depth, with_exit, (const uint32_t *)nullptr, num);
     KL_CHECK_LAUNCH();
     uint32_t cnt = 0;
     int rc = exclusive_scan(info, psum, num, sc, st, &cnt);
@@ -1119,7 +1143,7 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
     }
     if (!last) {
       hipLaunchKernelGGL(rt_subdivide_kernel, dim3((unsigned)cdiv(num, 256)), dim3(256), 0, st, in, num, n0, n1, info,
-                         psum, l);
+                         psum, l, (int64_t)INT64_MAX);
       KL_CHECK_LAUNCH();
     } else {
       float *d1 = nullptr;
@@ -1129,7 +1153,7 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
         *depth = d1;
       }
       hipLaunchKernelGGL(rt_compact_kernel, dim3((unsigned)cdiv(num, 256)), dim3(256), 0, st, num, n0, d0, n1, d1, dd,
-                         info, psum);
+                         info, psum, (int64_t)INT64_MAX);
       KL_CHECK_LAUNCH();
     }
     n0 = n1;
@@ -1137,6 +1161,87 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
   }
   *nuggets = (int32_t *)n0;
   *num_hits = num;
+  return KL_OK;
+}
+
+// Fixed-capacity raytrace: the same levels with every count kept on the device, so the call
+// reads nothing back and can be captured into a graph.  Each level's nugget list lives in a
+// workspace buffer of max(num_rays, capacity) rows; past `capacity` a level keeps its first
+// `capacity` nuggets (a prefix of the full list) and result[1] is set.  Output rows past
+// result[0] hold nugget (-1, -1) and depth 0.
+namespace {
+struct RtfWs {
+  size_t a, b, info, psum, dtmp, dnum, temp, temp_bytes, total;
+  int64_t cap0;
+};
+RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
+  RtfWs w{};
+  w.cap0 = std::max<int64_t>(std::max<int64_t>(num_rays, capacity), 1);
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t tb = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                         (int)w.cap0 + 1);
+  size_t o = 0;
+  w.a = o; o += al(w.cap0 * sizeof(int2));
+  w.b = o; o += al(w.cap0 * sizeof(int2));
+  w.info = o; o += al((w.cap0 + 1) * 4);
+  w.psum = o; o += al((w.cap0 + 2) * 4);
+  w.dtmp = o; o += al(w.cap0 * (with_exit ? 2 : 1) * 4);
+  w.dnum = o; o += 256;
+  w.temp = o; w.temp_bytes = al(tb > 0 ? tb : 16); o += w.temp_bytes;
+  w.total = o;
+  return w;
+}
+}  // namespace
+
+extern "C" size_t kl_raytrace_fixed_workspace_bytes(int64_t num_rays, int64_t capacity, int with_exit) {
+  return rtf_layout(num_rays, capacity, with_exit).total;
+}
+
+extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, const int32_t *exsum,
+                                 const float *ray_o, const float *ray_d, int64_t num_rays, uint32_t target_level,
+                                 int return_depth, int with_exit, int64_t capacity, int32_t *nuggets, float *depth,
+                                 int64_t *result, void *workspace, size_t workspace_bytes, kl_stream stream) {
+  KL_REQUIRE(num_rays >= 0 && capacity >= 0, "raytrace: negative size");
+  KL_REQUIRE(target_level < (uint32_t)SPC_MAX_LEVELS, "raytrace: level must be < 15");
+  const RtfWs L = rtf_layout(num_rays, capacity, with_exit);
+  KL_REQUIRE(L.cap0 < ((int64_t)1 << 28), "raytrace: num_rays and capacity must be < 2^28");
+  KL_REQUIRE(workspace && workspace_bytes >= L.total, "raytrace: workspace too small");
+  hipStream_t st = S(stream);
+  const int dd = with_exit ? 2 : 1;
+  uint8_t *w = (uint8_t *)workspace;
+  int2 *n0 = (int2 *)(w + L.a), *n1 = (int2 *)(w + L.b);
+  uint32_t *info = (uint32_t *)(w + L.info), *psum = (uint32_t *)(w + L.psum), *dnum = (uint32_t *)(w + L.dnum);
+  float *d0 = return_depth ? (float *)(w + L.dtmp) : nullptr;
+  if (capacity > 0) {
+    KL_CHECK_RC(fill_async(nuggets, 0xff, (size_t)capacity * 2 * 4, st));
+    if (return_depth) KL_CHECK_RC(fill_async(depth, 0, (size_t)capacity * dd * 4, st));
+  }
+  RayIn in{octree, points, exsum, ray_o, ray_d};
+  const int64_t cap0 = L.cap0;
+  hipLaunchKernelGGL(rt_init_kernel, dim3((unsigned)cdiv(std::max<int64_t>(num_rays, 1), 256)), dim3(256), 0, st,
+                     num_rays, n0, dnum, result);
+  KL_CHECK_LAUNCH();
+  const unsigned g = (unsigned)cdiv(cap0 + 1, 256);
+  for (uint32_t l = 0; l <= target_level; l++) {
+    const int last = l == target_level;
+    hipLaunchKernelGGL(rt_decide_kernel, dim3(g), dim3(256), 0, st, in, cap0, n0, info, last ? d0 : nullptr, l, last,
+                       return_depth, with_exit, (const uint32_t *)dnum, cap0);
+    KL_CHECK_LAUNCH();
+    size_t tb = L.temp_bytes;
+    KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, info, psum, (int)cap0 + 1, st));
+    if (!last) {
+      hipLaunchKernelGGL(rt_subdivide_kernel, dim3(g), dim3(256), 0, st, in, cap0, n0, n1, info, psum, l,
+                         (int64_t)capacity);
+    } else {
+      hipLaunchKernelGGL(rt_compact_kernel, dim3(g), dim3(256), 0, st, cap0, n0, d0, (int2 *)nuggets,
+                         return_depth ? depth : nullptr, dd, info, psum, (int64_t)capacity);
+    }
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rt_count_kernel, dim3(1), dim3(64), 0, st, psum + cap0, (uint32_t)capacity, dnum, result, last);
+    KL_CHECK_LAUNCH();
+    std::swap(n0, n1);
+  }
   return KL_OK;
 }
 

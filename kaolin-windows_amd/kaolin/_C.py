@@ -390,10 +390,11 @@ def unbatched_mesh_intersection_cuda(points, verts_1, verts_2, verts_3):
     code = N.dtype_code(points.dtype)
     ws_bytes = lib.kl_check_sign_workspace_bytes(code, 1, F, P)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    arena = N.Arena(dev)
+    # under graph capture: the entry without an allocator, which reads nothing back to the host
+    alloc = None if N.capturing(dev) else N.Arena(dev).fn
     with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_unbatched_mesh_intersection(code, P, F, N.ptr(points), N.ptr(verts_1), N.ptr(verts_2),
-                                                   N.ptr(verts_3), N.ptr(out), N.ptr(ws), ws_bytes, arena.fn, None,
+                                                   N.ptr(verts_3), N.ptr(out), N.ptr(ws), ws_bytes, alloc, None,
                                                    N.stream_of(dev)), func)
     return out
 
@@ -411,10 +412,10 @@ def check_sign_batched(verts, faces, points, maxlen):
     code = N.dtype_code(verts.dtype)
     ws_bytes = lib.kl_check_sign_workspace_bytes(code, B, F, P)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    arena = N.Arena(dev)
+    alloc = None if N.capturing(dev) else N.Arena(dev).fn  # as unbatched_mesh_intersection_cuda
     with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_check_sign(code, B, V, F, P, N.ptr(verts), N.ptr(faces), N.ptr(points), N.ptr(maxlen),
-                                  N.ptr(out), N.ptr(ws), ws_bytes, arena.fn, None, N.stream_of(dev)), func)
+                                  N.ptr(out), N.ptr(ws), ws_bytes, alloc, None, N.stream_of(dev)), func)
     return out
 
 
@@ -558,9 +559,8 @@ def generate_points_cuda(octrees, pyramids, exsum):
 
 
 # ------------------------------------------------------------------------------ render.spc
-def raytrace_cuda(octree, points, pyramid, exclusive_sum, ray_o, ray_d, target_level, return_depth, with_exit):
-    """raytrace.cpp:170-214."""
-    func = 'raytrace_cuda'
+def _raytrace_checks(func, octree, points, pyramid, exclusive_sum, ray_o, ray_d):
+    """raytrace.cpp:170-200's argument checks; returns the pyramid's max level."""
     args = [Arg(octree, 'octree', 1), Arg(points, 'points', 2), Arg(exclusive_sum, 'exclusive_sum', 4),
             Arg(ray_o, 'ray_o', 5), Arg(ray_d, 'ray_d', 6)]
     check_all_same_gpu(func, args)
@@ -585,6 +585,16 @@ def raytrace_cuda(octree, points, pyramid, exclusive_sum, ray_o, ray_d, target_l
     if not (int(pyr[max_level + 1]) == 0 and int(pyr[max_level + 2]) == 0):
         raise RuntimeError('SPC pyramid corrupt, check if the SPC pyramid has been sliced')
     N.require_gpu(func, octree)
+    return max_level
+
+
+def raytrace_cuda(octree, points, pyramid, exclusive_sum, ray_o, ray_d, target_level, return_depth, with_exit):
+    """raytrace.cpp:170-214."""
+    func = 'raytrace_cuda'
+    max_level = _raytrace_checks(func, octree, points, pyramid, exclusive_sum, ray_o, ray_d)
+    if N.capturing(octree.device):
+        raise RuntimeError(f'{func}: the output size is known only after the march (one host read per level); '
+                           'under graph capture call kaolin.render.spc.unbatched_raytrace(..., capacity=N)')
     dev = octree.device
     arena = N.Arena(dev)
     nug_p, dep_p, nh = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64()
@@ -601,6 +611,107 @@ def raytrace_cuda(octree, points, pyramid, exclusive_sum, ray_o, ray_d, target_l
         depth = arena.tensor(dep_p.value, n * dd, torch.float32, (n, dd))
         return [nuggets, depth]
     return [nuggets]
+
+
+def raytrace_fixed_cuda(octree, points, pyramid, exclusive_sum, ray_o, ray_d, target_level, return_depth, with_exit,
+                        capacity):
+    """raytrace_cuda with a fixed output size (not a reference _C name): nothing is read back to
+    the host, so it can be captured into a graph (kl_raytrace_fixed).  Returns [nuggets
+    (capacity, 2) int32, depth (capacity, 1|2) f32 if return_depth, result (2,) int64 = (rows
+    written, 1 if truncated)]; rows past result[0] hold (-1, -1) and depth 0."""
+    func = 'raytrace_cuda'
+    _raytrace_checks(func, octree, points, pyramid, exclusive_sum, ray_o, ray_d)
+    capacity = int(capacity)
+    if capacity < 0:
+        raise ValueError(f'capacity must be >= 0, got {capacity}')
+    dev = octree.device
+    dd = 2 if with_exit else 1
+    nuggets = torch.empty((capacity, 2), dtype=torch.int32, device=dev)
+    depth = torch.empty((capacity, dd), dtype=torch.float32, device=dev) if return_depth else None
+    result = torch.empty((2,), dtype=torch.int64, device=dev)
+    lib = N.lib()
+    nr = ray_o.shape[0]
+    ws_bytes = N.size('kl_raytrace_fixed_workspace_bytes', nr, capacity, int(bool(with_exit)))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    with N.on_device(dev):
+        N.check(lib.kl_raytrace_fixed(N.ptr(octree), N.ptr(points), N.ptr(exclusive_sum), N.ptr(ray_o), N.ptr(ray_d),
+                                      nr, int(target_level), int(bool(return_depth)), int(bool(with_exit)), capacity,
+                                      N.ptr(nuggets), N.ptr(depth), N.ptr(result), N.ptr(ws), ws_bytes,
+                                      N.stream_of(dev)), func)
+    return [nuggets, depth, result] if return_depth else [nuggets, result]
+
+
+def _host_f32(x, n):
+    """A host float array of a CPU tensor's values (the reference reads them through data_ptr)."""
+    a = (ctypes.c_float * n)(*x.reshape(-1)[:n].tolist())
+    return ctypes.cast(a, ctypes.c_void_p), a
+
+
+def generate_primary_rays_cuda(height, width, Eye, At, Up, fov, World):
+    """raytrace.cpp:111-166 (deprecated upstream, bindings.cpp:86): pinhole rays (origin,
+    direction) of a height x width image, (height*width, 3) float32 each on the current device."""
+    for name, t in (('Eye', Eye), ('At', At), ('Up', Up)):
+        if not t.is_contiguous():
+            raise RuntimeError(f'{name} must be contiguous')
+        if t.device.type != 'cpu':
+            raise RuntimeError(f'{name} must be a cpu tensor')
+        if t.dtype != torch.float32:
+            raise RuntimeError(f'{name} must be byte')  # the reference's CHECK_FLOAT message
+        if not (t.dim() == 1 and t.shape[0] == 3):
+            raise RuntimeError(f'{name} must be a triplet')
+    if not World.is_contiguous():
+        raise RuntimeError('World must be contiguous')
+    if World.device.type != 'cpu':
+        raise RuntimeError('World must be a cpu tensor')
+    if tuple(World.shape) != (4, 4):
+        raise RuntimeError('World must of size {4, 4}')
+    height, width = int(height), int(width)
+    num = height * width
+    N.require_gpu('generate_primary_rays_cuda')
+    dev = torch.device('cuda', torch.cuda.current_device())
+    org = torch.empty((num, 3), dtype=torch.float32, device=dev)
+    dirs = torch.empty((num, 3), dtype=torch.float32, device=dev)
+    keep = [_host_f32(t.float(), k) for t, k in ((Eye, 3), (At, 3), (Up, 3), (World, 16))]
+    with N.on_device(dev):
+        N.check(N.lib().kl_generate_primary_rays(height, width, keep[0][0], keep[1][0], keep[2][0], float(fov),
+                                                 keep[3][0], N.ptr(org), N.ptr(dirs), N.stream_of(dev)),
+                'generate_primary_rays_cuda')
+    return [org, dirs]
+
+
+def generate_shadow_rays_cuda(ray_o, ray_d, light, plane):
+    """raytrace.cpp:234-283 (deprecated upstream, bindings.cpp:88): for the rays that meet
+    `plane` ahead, rays from `light` to the hit point: [src, dst (normalised), map (ray
+    index)], the reference's count of rows (its exclusive scan's last entry)."""
+    func = 'generate_shadow_rays_cuda'
+    for t in (ray_o, ray_d):
+        if t.dtype != torch.float32:
+            raise RuntimeError(f'expected scalar type Float but found {_tname(t.dtype)}')
+    for name, t, k in (('light', light, 3), ('plane', plane, 4)):
+        if t.device.type != 'cpu':
+            raise RuntimeError(f'{func}: {name} must be a cpu tensor')
+        if t.dtype != torch.float32:
+            raise RuntimeError(f'expected scalar type Float but found {_tname(t.dtype)}')
+        if t.numel() < k:
+            raise RuntimeError(f'{func}: {name} must hold {k} values')
+    N.require_gpu(func, ray_o, ray_d)
+    dev = ray_o.device
+    ray_o, ray_d = ray_o.contiguous(), ray_d.contiguous()
+    num = ray_d.shape[0]
+    src = torch.empty((num, 3), dtype=torch.float32, device=dev)
+    dst = torch.empty((num, 3), dtype=torch.float32, device=dev)
+    mp = torch.empty((num,), dtype=torch.int32, device=dev)
+    lib = N.lib()
+    ws_bytes = lib.kl_generate_shadow_rays_workspace_bytes(num)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    lt, pl = _host_f32(light.contiguous(), 3), _host_f32(plane.contiguous(), 4)
+    cnt = ctypes.c_int64()
+    with N.on_device(dev):
+        N.check(lib.kl_generate_shadow_rays(num, N.ptr(ray_o), N.ptr(ray_d), lt[0], pl[0], N.ptr(src), N.ptr(dst),
+                                            N.ptr(mp), ctypes.byref(cnt), N.ptr(ws), ws_bytes, N.stream_of(dev)),
+                func)
+    c = cnt.value
+    return [src[:c], dst[:c], mp[:c]]
 
 
 def mark_pack_boundaries_cuda(pack_ids):
@@ -725,7 +836,9 @@ render.mesh = _module('kaolin._C.render.mesh', packed_rasterize_forward_cuda=pac
                       dibr_soft_mask_backward_cuda=dibr_soft_mask_backward_cuda,
                       deftet_sparse_render_forward_cuda=deftet_sparse_render_forward_cuda,
                       deftet_sparse_render_backward_cuda=deftet_sparse_render_backward_cuda)
-render.spc = _module('kaolin._C.render.spc', raytrace_cuda=raytrace_cuda,
+render.spc = _module('kaolin._C.render.spc', raytrace_cuda=raytrace_cuda, raytrace_fixed_cuda=raytrace_fixed_cuda,
+                     generate_primary_rays_cuda=generate_primary_rays_cuda,
+                     generate_shadow_rays_cuda=generate_shadow_rays_cuda,
                      mark_pack_boundaries_cuda=mark_pack_boundaries_cuda, diff_cuda=diff_cuda,
                      inclusive_sum_cuda=inclusive_sum_cuda, sum_reduce_cuda=sum_reduce_cuda,
                      cumsum_cuda=cumsum_cuda, cumprod_cuda=cumprod_cuda)

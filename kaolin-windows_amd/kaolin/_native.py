@@ -90,6 +90,11 @@ _SIGS = {
     'kl_generate_points': (_I, [_I, _I, _P, _P, _P, _P, _P]),
     'kl_points_to_morton': (_I, [_I64, _P, _P, _P]),
     'kl_morton_to_points': (_I, [_I64, _P, _P, _P]),
+    'kl_raytrace_fixed_workspace_bytes': (_SZ, [_I64, _I64, _I]),
+    'kl_raytrace_fixed': (_I, [_P, _P, _P, _P, _P, _I64, ctypes.c_uint32, _I, _I, _I64, _P, _P, _P, _P, _SZ, _P]),
+    'kl_generate_primary_rays': (_I, [ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P, _F, _P, _P, _P, _P]),
+    'kl_generate_shadow_rays_workspace_bytes': (_SZ, [_I64]),
+    'kl_generate_shadow_rays': (_I, [_I64, _P, _P, _P, _P, _P, _P, _P, ctypes.POINTER(_I64), _P, _SZ, _P]),
     'kl_raytrace': (_I, [_P, _I64, _P, _I64, _P, _I, _P, _P, _I64, ctypes.c_uint32, _I, _I, ALLOC_FN, _P, _PP, _PP,
                          ctypes.POINTER(_I64), _P]),
     'kl_mark_pack_boundaries': (_I, [_I, _I64, _P, _P, _P]),
@@ -170,6 +175,13 @@ def stream_of(device):
     """The current HIP stream of `device` as a pointer-sized int (the raw handle: no Stream object)."""
     idx = device.index
     return _raw_stream(torch.cuda.current_device() if idx is None else idx)
+
+
+def capturing(device):
+    """True while `device`'s current stream is being captured into a graph: the entries that
+    size outputs or lists on the host then take their capturable form (no allocator, nothing
+    read back)."""
+    return device.type == 'cuda' and torch.cuda.is_current_stream_capturing()
 
 
 _SIZES = {}

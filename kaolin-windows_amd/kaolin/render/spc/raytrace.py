@@ -14,10 +14,23 @@ __all__ = ['unbatched_raytrace', 'mark_pack_boundaries', 'mark_first_hit', 'diff
 
 
 def unbatched_raytrace(octree, point_hierarchy, pyramid, exsum, origin, direction, level,
-                       return_depth=True, with_exit=False):
+                       return_depth=True, with_exit=False, capacity=None):
     r"""Ray march an unbatched SPC ([-1, 1]^3) at ``level``.  Returns ray_index,
     point_index (int32, ray-major, front-to-back) and optionally the entry (and exit)
-    depth (N,1) / (N,2)."""
+    depth (N,1) / (N,2).
+
+    ``capacity`` (an extension; the reference sizes the output on the host, one count read per
+    level, raytrace_cuda.cu:557-560): fixed-size outputs of ``capacity`` rows and nothing read
+    back, so the call can be captured into a CUDA/HIP graph.  Then a fourth (third without depth)
+    value is returned, ``result`` (2,) int64 on the device = (rows written, 1 if the march held
+    more than ``capacity`` nuggets at some level; the rows are then the first ``capacity`` rows
+    of the full answer).  Rows past result[0] hold index -1 and depth 0."""
+    if capacity is not None:
+        out = _C.render.spc.raytrace_fixed_cuda(octree.contiguous(), point_hierarchy.contiguous(),
+                                                 pyramid.contiguous(), exsum.contiguous(), origin.contiguous(),
+                                                 direction.contiguous(), level, return_depth, with_exit, capacity)
+        ridx, pidx = out[0][..., 0], out[0][..., 1]
+        return (ridx, pidx, out[1], out[2]) if return_depth else (ridx, pidx, out[1])
     output = _C.render.spc.raytrace_cuda(octree.contiguous(), point_hierarchy.contiguous(), pyramid.contiguous(),
                                          exsum.contiguous(), origin.contiguous(), direction.contiguous(), level,
                                          return_depth, with_exit)

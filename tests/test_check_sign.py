@@ -199,3 +199,50 @@ def test_gpu_batch_nan_and_outside_points(kal, dtype):
     ref = orc.check_sign(vb, faces, pts)
     np.testing.assert_array_equal(out, ref)
     assert not out[1].any() and out[0].any() and out[2].any()
+
+
+def _captured(fn):
+    """fn() captured into a HIP graph (warmed up eagerly first) and replayed once."""
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = fn()
+    g.replay()
+    torch.cuda.synchronize()
+    return g, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('overflow', [False, True])
+def test_gpu_graph_capture(kal, overflow):
+    """Under graph capture the entries take their capturable form (no allocator, nothing read
+    back: the lists live in the workspace's fixed room).  Past that room (forced here with dev
+    flag 1 << 26) cs_brute_kernel answers every point against every face on the device.  Both
+    bit-exact to the oracle, and a replay after the inputs change answers the new inputs."""
+    verts, faces = _uv_sphere(12, 18, 0.8)
+    verts = verts.astype(np.float32)
+    rng = np.random.default_rng(7)
+    pts = rng.uniform(-1, 1, (2, 1500, 3)).astype(np.float32)
+    vb = np.stack([verts, verts * np.float32(1.3)])
+    tv, tf, tp = _T(vb), _T(faces), _T(pts)
+    v1, v2, v3 = (_T(verts[faces[:, k]]) for k in range(3))
+    _dev_flags(kal, (1 << 26) if overflow else 0)
+    try:
+        g, (out, cnt) = _captured(lambda: (kal.ops.mesh.check_sign(tv, tf, tp),
+                                           kal._C.ops.mesh.unbatched_mesh_intersection_cuda(tp[0], v1, v2, v3)))
+        np.testing.assert_array_equal(out.cpu().numpy(), orc.check_sign(vb, faces, pts))
+        np.testing.assert_array_equal(cnt.cpu().numpy().astype(np.int64),
+                                      orc.mesh_intersection_counts(pts[0], verts[faces[:, 0]], verts[faces[:, 1]],
+                                                                   verts[faces[:, 2]]))
+        pts2 = rng.uniform(-1, 1, pts.shape).astype(np.float32)
+        tp.copy_(_T(pts2))
+        g.replay()
+        torch.cuda.synchronize()
+    finally:
+        _dev_flags(kal, 0)
+    np.testing.assert_array_equal(out.cpu().numpy(), orc.check_sign(vb, faces, pts2))

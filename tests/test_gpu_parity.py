@@ -913,6 +913,84 @@ def test_raytrace_vs_oracle_mesh_spc(kal, with_exit):
     assert len(onug) > 1000
 
 
+@pytest.mark.parametrize('name', ['positive', 'negative', 'none', 'depth_exit', 'inside_nodepth', 'inside_exit'])
+def test_raytrace_fixed_kat(kal, golden, name):
+    """unbatched_raytrace(..., capacity=N) (kl_raytrace_fixed): the KAT rows, then padding."""
+    g = golden('spc.npz')
+    octree, pyr, ex, pts = _rt_setup(kal, g['rt_octree'])
+    lv, rd, we = (int(x) for x in g[f'rt_{name}_cfg'])
+    ref = g[f'rt_{name}_nuggets']
+    cap = len(ref) + 5
+    out = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(g[f'rt_{name}_origin']),
+                                            T(g[f'rt_{name}_direction']), lv, return_depth=bool(rd),
+                                            with_exit=bool(we), capacity=cap)
+    res = A(out[-1])
+    assert res.tolist() == [len(ref), 0]
+    nug = np.stack([A(out[0]), A(out[1])], -1)
+    assert np.array_equal(nug[:len(ref)], ref) and (nug[len(ref):] == -1).all()
+    if rd:
+        dep = A(out[2])
+        np.testing.assert_allclose(dep[:len(ref)], g[f'rt_{name}_depth'], rtol=1e-5, atol=1e-6)
+        assert (dep[len(ref):] == 0).all()
+
+
+def test_raytrace_fixed_capture_and_truncation(kal):
+    """The fixed-capacity march equals the host-sized one (nuggets and depth bit-equal); captured
+    into a graph and replayed with new rays it answers the new rays; with a capacity below the
+    intermediate levels' counts it returns the first `capacity` rows of the full answer and flags
+    the truncation."""
+    v, f = _uv_sphere(24, 36, 0.8)
+    L = 6
+    octree, _, _ = kal.ops.conversions.unbatched_mesh_to_spc(T(v[f].astype(np.float32)), L)
+    octree, pyr, ex, pts = _rt_setup(kal, A(octree))
+
+    def rays(shift):
+        n = 40
+        ii, jj = np.meshgrid(np.linspace(-0.9, 0.9, n) + shift, np.linspace(-0.9, 0.9, n), indexing='ij')
+        o = np.stack([ii, jj, np.full_like(ii, 3.)], -1).reshape(-1, 3).astype(np.float32)
+        d = np.stack([0.05 * ii, 0.03 * jj, -np.ones_like(ii)], -1).reshape(-1, 3)
+        return o, (d / np.linalg.norm(d, axis=-1, keepdims=True)).astype(np.float32)
+
+    o1, d1 = rays(0.0)
+    to, td = T(o1), T(d1)
+    r, p, dep = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True)
+    n1 = len(r)
+    cap = n1 + 4096
+    fr, fp, fd, res = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True,
+                                                        capacity=cap)
+    assert A(res).tolist() == [n1, 0]
+    assert torch.equal(fr[:n1], r) and torch.equal(fp[:n1], p) and torch.equal(fd[:n1], dep)
+    # captured
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True, capacity=cap)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        gr, gp, gd, gres = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True,
+                                                             capacity=cap)
+        with pytest.raises(RuntimeError, match='capacity'):
+            kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True)
+    o2, d2 = rays(0.05)
+    to.copy_(T(o2))
+    td.copy_(T(d2))
+    graph.replay()
+    torch.cuda.synchronize()
+    r2, p2, dep2 = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True)
+    n2 = len(r2)
+    assert A(gres).tolist() == [n2, 0] and not (n2 == n1 and torch.equal(p2, p))
+    assert torch.equal(gr[:n2], r2) and torch.equal(gp[:n2], p2) and torch.equal(gd[:n2], dep2)
+    # truncated: fewer rows than the intermediate levels hold
+    small = n2 // 3
+    tr, tp, tdp, tres = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True,
+                                                          capacity=small)
+    k, flag = A(tres).tolist()
+    assert flag == 1 and 0 < k <= small
+    assert torch.equal(tr[:k], r2[:k]) and torch.equal(tp[:k], p2[:k]) and torch.equal(tdp[:k], dep2[:k])
+
+
 @pytest.mark.parametrize('na,nb', [(0, 5), (7, 0), (3145728, 1048576), (1001, 333)])
 def test_loss_dot2(kal, na, nb):
     """bench.py's fused loss helper (kl_loss_dot2) vs an fp64 torch dot; replays reuse the workspace."""
