@@ -192,7 +192,8 @@ int kl_dibr_soft_mask_forward_compact(kl_dtype dtype, int batch, int height, int
                                       uint8_t *hits, uint32_t *rec_face, void *rec_prob, int *seg_tot, int *scratch,
                                       void *workspace, size_t workspace_bytes, kl_stream stream);
 /* dibr_soft_mask.cpp:110-183 on the compact state.  The terms are summed in double and
- * rounded once (order-independent); accumulate = 0: grad_face_vertices_image is overwritten
+ * rounded once (order-independent for f32 terms, which sum exactly in double; f64 terms are
+ * added with double atomics and may differ run to run in the last bits); accumulate = 0: grad_face_vertices_image is overwritten
  * with that sum; 1: the rounded sum is added onto its contents (one float add, as autograd
  * adds the soft-mask gradient to the rasterizer's).  scratch is left zeroed. */
 size_t kl_soft_mask_compact_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum);
@@ -412,7 +413,8 @@ int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int16_t *point
  * count back to size the next).  The same levels with every count kept on the device: nothing is
  * read back, so the call can be captured into a HIP graph.  nuggets (capacity,2) int32 and depth
  * (capacity, with_exit?2:1) f32 are caller-allocated; result (2) int64 device output = (rows
- * written, 1 if some level held more than `capacity` nuggets).  When truncated, the rows are the
+ * written, 1 if some level held more than `capacity` candidates: the last level's nuggets, or an
+ * earlier level's untested children, up to 8 per nugget of the level above).  When truncated, the rows are the
  * first rows of kl_raytrace's output (ray-major, front-to-back order is kept).  Rows past
  * result[0]: nugget (-1, -1), depth 0.  num_rays and capacity < 2^28. */
 size_t kl_raytrace_fixed_workspace_bytes(int64_t num_rays, int64_t capacity, int with_exit);

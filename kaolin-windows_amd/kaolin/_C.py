@@ -391,7 +391,7 @@ def unbatched_mesh_intersection_cuda(points, verts_1, verts_2, verts_3):
     ws_bytes = lib.kl_check_sign_workspace_bytes(code, 1, F, P)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     # under graph capture: the entry without an allocator, which reads nothing back to the host
-    alloc = None if N.capturing(dev) else N.Arena(dev).fn
+    alloc = N.ALLOC_FN() if N.capturing(dev) else N.Arena(dev).fn
     with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_unbatched_mesh_intersection(code, P, F, N.ptr(points), N.ptr(verts_1), N.ptr(verts_2),
                                                    N.ptr(verts_3), N.ptr(out), N.ptr(ws), ws_bytes, alloc, None,
@@ -412,7 +412,7 @@ def check_sign_batched(verts, faces, points, maxlen):
     code = N.dtype_code(verts.dtype)
     ws_bytes = lib.kl_check_sign_workspace_bytes(code, B, F, P)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    alloc = None if N.capturing(dev) else N.Arena(dev).fn  # as unbatched_mesh_intersection_cuda
+    alloc = N.ALLOC_FN() if N.capturing(dev) else N.Arena(dev).fn  # as unbatched_mesh_intersection_cuda
     with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_check_sign(code, B, V, F, P, N.ptr(verts), N.ptr(faces), N.ptr(points), N.ptr(maxlen),
                                   N.ptr(out), N.ptr(ws), ws_bytes, alloc, None, N.stream_of(dev)), func)
