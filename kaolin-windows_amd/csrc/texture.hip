@@ -14,8 +14,9 @@
 // in the tutorial every uncovered pixel (uv = 0 after the mask) samples the same corner texel,
 // so ~half a million pixels serialise on three addresses (10.8 ms per call at 4 x 512^2).  Here
 // terms with a zero incoming gradient are skipped (they add nothing) and the rest are summed in
-// double and rounded once: deterministic, and equal to the exact sum of torch's float terms
-// wherever those span less than ~2^29 (torch's own float atomics round in arbitrary order).
+// double and rounded once: for f32, deterministic and equal to the exact sum of torch's float
+// terms wherever those span less than ~2^29 (torch's own float atomics round in arbitrary order);
+// f64 terms added with double atomics round in arrival order.
 #include "common.h"
 
 namespace kl {

@@ -4,8 +4,10 @@ All tests need an MI355X.  Integer outputs (face indices, distance types, octree
 nuggets, voxels) must be bit-identical to the oracle; floating outputs of the forward
 kernels are bit-identical too where no transcendental is involved (same operation
 order, no contraction, IEEE div/sqrt); soft-mask probabilities differ only by expf
-ulps (tolerance 1e-6 relative); gradients accumulate with float atomics in a
-different order (tolerance 1e-5, the north-star bar).
+ulps (tolerance 1e-6 relative).  f32 gradients are the reference's float terms summed in
+double and rounded once, so they are bit-equal to the oracle's ordered double sum
+(dibr_util.assert_grads_equal: at most 1 element in 10^4 one ulp off, where a face's terms span
+more than ~2^29); f64 gradients that go through double atomics agree to ~1e-15 relative.
 """
 import math
 
@@ -994,7 +996,9 @@ def test_raytrace_fixed_capture_and_truncation(kal):
     tr, tp, tdp, tres = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True,
                                                           capacity=small)
     k, flag = A(tres).tolist()
-    assert flag == 1 and 0 < k <= small
+    # the kept rows are a prefix of the full answer (possibly empty: an earlier level's kept
+    # candidates may all miss at the target level)
+    assert flag == 1 and 0 <= k <= small
     assert torch.equal(tr[:k], r2[:k]) and torch.equal(tp[:k], p2[:k]) and torch.equal(tdp[:k], dep2[:k])
 
 
