@@ -1203,7 +1203,8 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather_kernel(
                             valid, nz, B, H, W, F, D, m, eps, grad_fvi, grad_ffeat, big, nbig, rng, soft);
 }
 
-// one 256-thread workgroup per large face; block reduction of the per-thread partials
+// one 256-thread workgroup per large face; the per-thread partials reduced per wave (butterfly)
+// and across the four waves
 template <typename T, int MAXD>
 __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
@@ -1211,7 +1212,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
     const T *__restrict__ nz, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
     T *__restrict__ grad_ffeat, const int *__restrict__ big, const int *__restrict__ nbig,
     const uint2 *__restrict__ rng, const double *__restrict__ soft) {
-  __shared__ double red[256];
+  __shared__ double red[4 * (6 + 3 * MAXD)];
   const int n = *nbig;
   const RastSrc<T> src{fvi, valid, (T)m, nz};
   for (int k = blockIdx.x; k < n; k += gridDim.x) {
@@ -1237,23 +1238,27 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
       if (face_idx[p] != f) continue;
       acc.add(v, c, D, wts[p * 3 + 0], wts[p * 3 + 1], wts[p * 3 + 2], grad_feat + p * D, eps);
     }
+    // per wave a butterfly of every value, then the four waves' sums added by thread q
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
     for (int q = 0; q < 6 + 3 * MAXD; q++) {
-      red[threadIdx.x] = q < 6 ? acc.gi[q] : acc.gf[q - 6];
-      __syncthreads();
-      for (int s = 128; s > 0; s >>= 1) {
-        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-        __syncthreads();
-      }
-      if (threadIdx.x == 0) {
-        if (q < 6) {
-          grad_fvi[tf * 6 + q] = soft ? (T)red[0] + (T)soft[tf * 6 + q] : (T)red[0];
-        } else {
-          const int r = q - 6, ii = r / MAXD, d = r % MAXD;
-          if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)red[0];
-        }
-      }
-      __syncthreads();
+      double x = q < 6 ? acc.gi[q] : acc.gf[q - 6];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+      if (lane == 0) red[wv * (6 + 3 * MAXD) + q] = x;
     }
+    __syncthreads();
+    const int q = threadIdx.x;
+    if (q < 6 + 3 * MAXD) {
+      const double x = red[q] + red[(6 + 3 * MAXD) + q] + red[2 * (6 + 3 * MAXD) + q] + red[3 * (6 + 3 * MAXD) + q];
+      if (q < 6) {
+        grad_fvi[tf * 6 + q] = soft ? (T)x + (T)soft[tf * 6 + q] : (T)x;
+      } else {
+        const int r = q - 6, ii = r / MAXD, d = r % MAXD;
+        if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)x;
+      }
+    }
+    __syncthreads();  // red is rewritten for the next face
   }
 }
 
