@@ -1098,6 +1098,12 @@ def main(argv=None):
                 dist.destroy_process_group()
     torch.cuda.set_device(local)
     device = torch.device('cuda', local)
+    if os.environ.get('KAOLIN_DEV_FLAGS'):  # development A/B timing only (kl_dev_set_flags); unset in the product run
+        import ctypes
+        from kaolin import _native
+        lib = _native.lib()
+        lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
+        lib.kl_dev_set_flags(int(os.environ['KAOLIN_DEV_FLAGS'], 0))
     if world > 1:
         dist.init_process_group('nccl', device_id=device)
     progress(f'rank {rank}/{world}: DIB-R {args.config} headline')

@@ -1545,15 +1545,20 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   KL_CHECK_LAUNCH();
   }
   const int split_from = 5, split_log2 = sizeof(T) == 4 ? 2 : 0;
-  // counts (many workgroups) then orders (one per bitmap): a one-launch version with the counts in
-  // the two ordering workgroups measured 85 us against 5 + 7 (r03i)
-  hipLaunchKernelGGL(tile_bucket2_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)rbm,
-                     (const uint32_t *)sbm, g.words, nt, rbk, sbk, rgh, sgh, s.scratch);
-  KL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(tile_order2_kernel, dim3(2), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh, items,
-                     split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt,
-                     soft_lp_min(K), snitems, soft_split(), 1);
-  KL_CHECK_LAUNCH();
+  if (nt <= ORD_LDS_TILES && !(g_dev_flags & (1 << 20))) {  // counts and orders in one launch
+    hipLaunchKernelGGL(tile_countorder2_kernel, dim3(2), dim3(1024), 0, st, (const uint32_t *)rbm,
+                       (const uint32_t *)sbm, g.words, items, split_from, split_log2, nitems, sorder, nt,
+                       soft_lp_min(K), snitems, soft_split(), 1, s.scratch);
+    KL_CHECK_LAUNCH();
+  } else {  // counts (a wave per tile) then orders (dev bit 20: this path, for A/B timing)
+    hipLaunchKernelGGL(tile_bucket2_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)rbm,
+                       (const uint32_t *)sbm, g.words, nt, rbk, sbk, rgh, sgh, s.scratch);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(tile_order2_kernel, dim3(2), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh, items,
+                       split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt,
+                       soft_lp_min(K), snitems, soft_split(), 1);
+    KL_CHECK_LAUNCH();
+  }
   uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.off_defer);
   RastTileArgs<T> args{src, fvz, feat, rbm, rec, rng, items, nitems, g, F, D, eps, out_feat, out_idx, out_w,
                        reinterpret_cast<uint64_t *>(g_dev_debug)};

@@ -269,4 +269,42 @@ static __global__ void __launch_bounds__(1024) tile_order2_kernel(const uint8_t 
     order_items(sb, sx, lpb, gh0, b, nt, order0, 0, split_from, split_log2, nitems0);
 }
 
+// tile_bucket2_kernel + tile_order2_kernel in one launch (nt <= ORD_LDS_TILES): each of the two
+// workgroups counts its bitmap's candidate chunks with one thread per tile (the tile's words
+// loaded eight at a time) into LDS buckets and histogram, then orders.  Block 0 also zeroes
+// `scratch`.  (Counting one tile per wave in turn, a reduction each, took 85 us.)
+static __global__ void __launch_bounds__(1024) tile_countorder2_kernel(
+    const uint32_t *__restrict__ bm0, const uint32_t *__restrict__ bm1, int words, int32_t *__restrict__ order0,
+    int split_from, int split_log2, int *__restrict__ nitems0, int32_t *__restrict__ order1, int nt, int lp_min1,
+    int *__restrict__ nitems1, SoftSplit sp, int skip_empty1, int *__restrict__ scratch) {
+  __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS], hist[ORD_HIST];
+  __shared__ uint8_t sbk[ORD_LDS_TILES];
+  const bool soft = blockIdx.x == 1;
+  const uint32_t *bm = soft ? bm1 : bm0;
+  if (!soft && threadIdx.x == 0 && scratch) *scratch = 0;
+  for (int i = threadIdx.x; i < ORD_HIST; i += blockDim.x) hist[i] = 0;
+  __syncthreads();
+  for (int t = threadIdx.x; t < nt; t += blockDim.x) {
+    const uint32_t *w = bm + (size_t)t * words;
+    unsigned n = 0;
+    int k = 0;
+    for (; k + 8 <= words; k += 8) {
+      uint32_t x[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) x[u] = w[k + u];
+#pragma unroll
+      for (int u = 0; u < 8; u++) n += __popc(x[u]);
+    }
+    for (; k < words; k++) n += __popc(w[k]);
+    const int q = 31 - __clz(n + 1u);
+    sbk[t] = (uint8_t)q;
+    atomicAdd(&hist[tile_band(t, nt) * ORD_BUCKETS + q], 1);
+  }
+  __syncthreads();
+  if (soft)
+    order_soft_items(sb, sx, lpb, sbk, hist, nt, order1, lp_min1, nitems1, sp, skip_empty1);
+  else
+    order_items(sb, sx, lpb, hist, sbk, nt, order0, 0, split_from, split_log2, nitems0);
+}
+
 }  // namespace kl
