@@ -5,6 +5,7 @@
 set -e
 OUT=${OUT:-gpurun_out}
 ROOT=$(pwd)
+mkdir -p "$OUT"
 ARGS=${BENCH_ARGS:---no-cpu-baseline --no-p2m --steps 5 --warmup 2}
 cd /tmp
 export TMPDIR=/tmp
