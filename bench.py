@@ -726,6 +726,29 @@ def tutorial_leg(device, steps, warmup=3):
         tutorial_shape_step(st)
     _native.set_timer(None)
     ops = {k: round(v, 4) for k, v in timer.summary_ms().items()}
+    # the same step captured once in a HIP graph and replayed (the caller's torch ops and autograd
+    # included): what is left of the step without the eager host path
+    ms_graph = None
+    try:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                tutorial_shape_step(st)
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            tutorial_shape_step(st)
+        for _ in range(warmup):
+            graph.replay()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            graph.replay()
+        torch.cuda.synchronize()
+        ms_graph = (time.perf_counter() - t0) / steps * 1e3
+    except RuntimeError as e:  # reported, not fatal: the eager line is the tutorial's own shape
+        ms_graph = f'capture failed: {e}'
     for _ in range(warmup):
         tutorial_step(st)
     ms_full = _wall_ms(lambda: tutorial_step(st), max(3, steps // 2))
@@ -733,6 +756,9 @@ def tutorial_leg(device, steps, warmup=3):
                       '-> L1 + mask_iou -> backward (4 views x 512^2, 50k faces)',
             'value': round(px / (ms_loop * 1e-3) / 1e6, 2), 'ms_per_step': round(ms_loop, 4),
             'ms_per_step_synced': round(ms, 4), 'native_op_ms': ops,
+            'graph': ({'value': round(px / (ms_graph * 1e-3) / 1e6, 2), 'ms_per_step': round(ms_graph, 4),
+                       'what': 'the same step captured once in a HIP graph and replayed (loss ops and autograd '
+                               'included)'} if isinstance(ms_graph, float) else ms_graph),
             'full_iteration': {'ms': round(ms_full, 4), 'value': round(px / (ms_full * 1e-3) / 1e6, 2),
                                'what': 'dibr_tutorial.ipynb cell 14 minus the laplacian term: + texture_mapping '
                                        '(bilinear, 512^2 texture), clamp, L1 image loss, both Adam steps'},

@@ -279,12 +279,24 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
           tbest = (T)d; tbest_f = f; tbest_t = t;
         }
       };
+      // two faces per iteration: both records' LDS reads and both evaluations in flight together
+      // (the fold still takes them in face order)
       while (mask) {
         const int sj = s0 + __builtin_ctzll(mask);
         mask &= mask - 1;
-        int t;
-        const float d = point_face<T>(p, sf[sj], t);
-        fold(start + sj, d, t);
+        if (mask) {
+          const int sk = s0 + __builtin_ctzll(mask);
+          mask &= mask - 1;
+          int t0, t1;
+          const float d0 = point_face<T>(p, sf[sj], t0);
+          const float d1 = point_face<T>(p, sf[sk], t1);
+          fold(start + sj, d0, t0);
+          fold(start + sk, d1, t1);
+        } else {
+          int t;
+          const float d = point_face<T>(p, sf[sj], t);
+          fold(start + sj, d, t);
+        }
       }
     }
     if (share && valid) {
