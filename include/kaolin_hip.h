@@ -540,6 +540,19 @@ int kl_texture_mapping_backward(kl_dtype dtype, int mode, int batch, int64_t num
                                 const void *texture, void *grad_coords, void *grad_texture, void *workspace,
                                 size_t workspace_bytes, kl_stream stream);
 
+/* metrics/render.py:18-40 mask_iou (the DIB-R tutorial's silhouette loss), fused: lhs / rhs
+ * (B, pixels_per_mask) of one dtype.  Outputs iou_up / iou_down (B) -- the two per-mask sums,
+ * formed in the dtype as the reference forms them, summed in double in a fixed order and rounded
+ * once -- and loss (1) = 1 - mean(up / (down + 1e-10)).  The backward writes autograd's gradient
+ * through the reference's ops (grad_loss: a device scalar; grad_lhs / grad_rhs may be NULL). */
+size_t kl_mask_iou_workspace_bytes(int batch, int64_t pixels_per_mask);
+int kl_mask_iou_forward(kl_dtype dtype, int batch, int64_t pixels_per_mask, const void *lhs, const void *rhs,
+                        void *iou_up, void *iou_down, void *loss, void *workspace, size_t workspace_bytes,
+                        kl_stream stream);
+int kl_mask_iou_backward(kl_dtype dtype, int batch, int64_t pixels_per_mask, const void *grad_loss, const void *lhs,
+                         const void *rhs, const void *iou_up, const void *iou_down, void *grad_lhs, void *grad_rhs,
+                         kl_stream stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -122,6 +122,9 @@ _SIGS = {
     'kl_texture_mapping_forward': (_I, [_I, _I, _I, _I64, _I, _I, _I, _P, _P, _P, _P]),
     'kl_texture_mapping_bwd_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'kl_texture_mapping_backward': (_I, [_I, _I, _I, _I64, _I, _I, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    'kl_mask_iou_workspace_bytes': (_SZ, [_I, _I64]),
+    'kl_mask_iou_forward': (_I, [_I, _I, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    'kl_mask_iou_backward': (_I, [_I, _I, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
 }
 
 
