@@ -1130,6 +1130,14 @@ def main(argv=None):
         lib = _native.lib()
         lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
         lib.kl_dev_set_flags(int(os.environ['KAOLIN_DEV_FLAGS'], 0))
+    if os.environ.get('KAOLIN_DEV_PARAMS'):  # "index=value,..." (kl_dev_set_param), development sweeps only
+        import ctypes
+        from kaolin import _native
+        lib = _native.lib()
+        lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
+        for kv in os.environ['KAOLIN_DEV_PARAMS'].split(','):
+            k, v = kv.split('=')
+            lib.kl_dev_set_param(int(k), int(v))
     if world > 1:
         dist.init_process_group('nccl', device_id=device)
     progress(f'rank {rank}/{world}: DIB-R {args.config} headline')

@@ -1544,7 +1544,10 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
                        srng, (T)pad);
   KL_CHECK_LAUNCH();
   }
-  const int split_from = 5, split_log2 = sizeof(T) == 4 ? 2 : 0;
+  // heavy tiles (>= 2^split_from - 1 candidate chunks) split into 2^split_log2 row parts (dev
+  // params 4 / 5 override, for sweeps)
+  const int split_from = g_dev_param[4] ? g_dev_param[4] : 5;
+  const int split_log2 = sizeof(T) == 4 ? (g_dev_param[5] ? g_dev_param[5] : 2) : 0;
   if (nt <= ORD_LDS_TILES && !(g_dev_flags & (1 << 20))) {  // counts and orders in one launch
     hipLaunchKernelGGL(tile_countorder2_kernel, dim3(2), dim3(1024), 0, st, (const uint32_t *)rbm,
                        (const uint32_t *)sbm, g.words, items, split_from, split_log2, nitems, sorder, nt,
