@@ -351,7 +351,7 @@ def survey_step_bytes(inp, stats):
 
 # kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
 OP_KERNELS = {
-    'dibr_forward': ('raster_bin_word_kernel<float, 2>', 'tile_bucket2_kernel', 'tile_order2_kernel', 'raster_tile_kernel<float',
+    'dibr_forward': ('raster_bin_word_kernel<float, 2>', 'tile_countorder2_kernel', 'raster_tile_kernel<float',
                      'soft_tile_fwd_kernel<float'),
     'dibr_backward': ('rasterize_bwd_gather_kernel<float', 'rasterize_bwd_bigface_kernel<float', 'soft_bwd_plan_kernel',
                       'soft_tile_bwd_kernel<float'),
