@@ -923,12 +923,23 @@ def cfg4_leg(device, steps):
     leaves = int(fidx.shape[0])
     n_steps = max(3, steps // 4)
     ms_vox = _wall_ms(vox, n_steps)
+    # the host-sized subdivision (one count read per level) beside the default device-counted one
+    from kaolin.ops.conversions import trianglemesh as _tm
+    _tm.HOST_SIZED = True
+    try:
+        grid_h = vox()
+        ms_vox_host = _wall_ms(vox, n_steps)
+    finally:
+        _tm.HOST_SIZED = False
+    vox_equal = bool(torch.equal(grid_h, vox()))
+    del grid_h
     ms_spc = _wall_ms(spc, n_steps)
     vox_bytes = 4 * R ** 3 + 12 * V + 24 * F
     # sum_l 28 N_l + sum_{l>=1} 16 N_l + N_L (32 + 36 + 8) + 9 * nodes
     spc_bytes = sum(28 * n for n in N) + sum(16 * n for n in N[1:]) + N[-1] * (32 + 36 + 8) + 9 * nodes
     return {'metric': 'cfg4: trianglemeshes_to_voxelgrids R=512 + unbatched_mesh_to_spc L=9, 200k-face sphere (f32)',
             'voxelgrid': {'ms': round(ms_vox, 3), 'occupied': n_occ, 'bytes': vox_bytes,
+                          'host_sized': {'ms': round(ms_vox_host, 3), 'equal': vox_equal},
                           'roofline': {'bound': 'hbm', 'achieved': round(vox_bytes / (ms_vox * 1e-3) / 1e9, 1),
                                        'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                                        'frac': round(vox_bytes / (ms_vox * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
@@ -937,7 +948,8 @@ def cfg4_leg(device, steps):
                             'roofline': {'bound': 'hbm', 'achieved': round(spc_bytes / (ms_spc * 1e-3) / 1e9, 1),
                                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                                          'frac': round(spc_bytes / (ms_spc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
-            'timing': 'wall clock per call incl. the per-level host count reads (median of runs)',
+            'timing': 'wall clock per call (median of runs); voxelgrid: device-counted levels, one status read; '
+                      'voxelgrid.host_sized and mesh_to_spc: incl. the per-level host count reads',
             'spc': (octree, fidx, bary)}
 
 
@@ -982,12 +994,23 @@ def raytrace_leg(device, steps, spc_tuple):
     per_level = [int(kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], exsum, o, d, lv,
                                                         return_depth=False)[0].shape[0]) for lv in range(L + 1)]
     ms = _wall_ms(rt, max(3, steps // 4))
+    # the fixed-capacity march (kl_raytrace_fixed: no host count read, graph-capturable), capacity
+    # above every level's candidates (a hit node's children before their own test, <= 8 each)
+    cap = 8 * max(per_level) + 64
+    rtf = lambda: kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], exsum, o, d, L, capacity=cap)  # noqa: E731
+    fr, fp, fd, fres = rtf()
+    fixed_equal = (fres.tolist() == [hits, 0] and torch.equal(fr[:hits], ridx) and torch.equal(fp[:hits], pidx)
+                   and torch.equal(fd[:hits], depth))
+    ms_fixed = _event_ms(rtf, max(3, steps // 4))
     R = n * n
     nbytes = 24 * R + sum(31 * per_level[lv] + 8 * (per_level[lv + 1] if lv + 1 <= L else 0)
                           for lv in range(L + 1)) + per_level[L] * (16 + 4)
     return {'metric': 'unbatched_raytrace Mrays/s (cfg4 SPC level 9, 512x512 rays, depth)',
             'value': round(R / (ms * 1e-3) / 1e6, 2), 'ms': round(ms, 4), 'hits': hits, 'hits_per_level': per_level,
             'bytes': nbytes, 'timing': 'wall clock per call incl. the per-level host count reads',
+            'fixed_capacity': {'value': round(R / (ms_fixed * 1e-3) / 1e6, 2), 'ms': round(ms_fixed, 4),
+                               'capacity': cap, 'equal_to_host_sized': bool(fixed_equal),
+                               'timing': 'HIP events over back-to-back calls (nothing read back)'},
             'roofline': {'bound': 'hbm', 'achieved': round(nbytes / (ms * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
 

@@ -525,6 +525,20 @@ int kl_voxelgrid_mark_f64(int64_t num_vertices, const double *points, int64_t nu
                           int resolution, kl_dtype grid_dtype, void *grid, kl_alloc_fn alloc, void *alloc_ctx,
                           kl_stream stream);
 
+/* The same marking with nothing read back to the host, so the call can be captured into a HIP
+ * graph (the reference, trianglemesh.py:339-457, sizes every round on the host; kl_voxelgrid_mark
+ * reads one count per round).  point_dtype KL_F32 | KL_F64.  Subdivision levels run from two
+ * device buffers of `capacity` triangles each; a level with more children to keep, or triangles
+ * still needing a split after the levels launched (vertices outside the unit cube), finish their
+ * subtree depth-first in the thread, so the grid equals kl_voxelgrid_mark's for any capacity >= 0
+ * (capacity sets speed only).  *status (device u32, written by the call): bit 0 = some
+ * depth-first walk exceeded 2^20 triangles and stopped (grid incomplete), bit 1 = some level
+ * overflowed `capacity`.  workspace: kl_voxelgrid_mark_async_workspace_bytes bytes. */
+size_t kl_voxelgrid_mark_async_workspace_bytes(kl_dtype point_dtype, int64_t capacity);
+int kl_voxelgrid_mark_async(kl_dtype point_dtype, int64_t num_vertices, const void *points, int64_t num_faces,
+                            const int64_t *faces, int resolution, kl_dtype grid_dtype, void *grid, int64_t capacity,
+                            uint32_t *status, void *workspace, size_t workspace_bytes, kl_stream stream);
+
 /* texture_mapping (kaolin/render/mesh/utils.py:23-75): coords (B, N, 2) in [0, 1] (OpenGL, y up;
  * clamped), texture (B, C, TH, TW) -> out (B, N, C), as torch.nn.functional.grid_sample with
  * align_corners=False and padding_mode='border' after the reference's [-1, 1] / y mapping.

@@ -201,6 +201,211 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
   return rc;
 }
 
+// ---- the capturable subdivision: nothing is read back to the host.
+// The levels run from fixed-capacity ping-pong buffers with every count kept on the device: a
+// level's kernel reads its input count from the counter the level before advanced, and its grid
+// strides over it.  The number of launched levels is fixed on the host from R alone: vertices
+// normalised into [0,1]^3 (the default origin / scale) have squared edges <= 3, and midpoint
+// splitting quarters them per level, so ceil(log4(3 / thr)) + 2 levels drain such a mesh.  Two
+// cases leave work beyond what the buffers hold -- a level with more than `capacity` children to
+// keep, or triangles still needing a split at the last launched level (a caller origin / scale
+// that leaves the unit cube) -- and there the thread finishes the triangle's subtree depth-first
+// itself.  The union of marked voxels does not depend on the order the subtrees are visited in,
+// so the grid is the host-sized path's bit for bit.  A depth-first walk longer than
+// VOX_DFS_BUDGET nodes stops and sets status bit 0 (the host-sized path fails its allocation
+// at such sizes); status bit 1 records that some level overflowed `capacity` (speed only).
+constexpr int VOX_DFS_BUDGET = 1 << 20;
+constexpr int VOX_MAX_LEVELS = 64;  // as the host-sized loop: levels 0..63 are subdivided
+constexpr size_t VOX_COUNTER_BYTES = 1024;
+
+template <typename T>
+__device__ __forceinline__ void midpoints(const Tri<T> &t, T *v4, T *v5, T *v6) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    v4[k] = (t.v[k] + t.v[6 + k]) / (T)2;
+    v5[k] = (t.v[k] + t.v[3 + k]) / (T)2;
+    v6[k] = (t.v[3 + k] + t.v[6 + k]) / (T)2;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void child_of(const Tri<T> &t, int c, Tri<T> &o) {
+  T v4[3], v5[3], v6[3];
+  midpoints(t, v4, v5, v6);
+  make_child(t, v4, v5, v6, c, o);
+}
+
+// marks t's three midpoints; returns the mask of its children that need a split (none at the
+// last subdivided level: their midpoints are never made)
+template <typename T, typename G>
+__device__ __forceinline__ uint32_t expand(const Tri<T> &t, int level, T thr, int R, G *grid) {
+  T v4[3], v5[3], v6[3];
+  midpoints(t, v4, v5, v6);
+  mark_point<T, G>(v4[0], v4[1], v4[2], R, grid);
+  mark_point<T, G>(v5[0], v5[1], v5[2], R, grid);
+  mark_point<T, G>(v6[0], v6[1], v6[2], R, grid);
+  if (level >= VOX_MAX_LEVELS - 1) return 0;
+  uint32_t keep = 0;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    Tri<T> o;
+    make_child(t, v4, v5, v6, c, o);
+    if (needs_split(o.v, thr)) keep |= 1u << c;
+  }
+  return keep;
+}
+
+// root (at `level`, needing a split) and its whole subtree, depth-first; the stack holds one
+// triangle and its unvisited children per level below root
+template <typename T, typename G>
+__device__ __noinline__ void subdivide_dfs(Tri<T> root, int level, T thr, int R, G *grid, unsigned *status) {
+  Tri<T> stk[VOX_MAX_LEVELS];
+  uint8_t msk[VOX_MAX_LEVELS];
+  stk[0] = root;
+  msk[0] = (uint8_t)expand<T, G>(root, level, thr, R, grid);
+  int sp = 0, budget = VOX_DFS_BUDGET;
+  while (sp >= 0) {
+    const uint32_t m = msk[sp];
+    if (!m) {
+      sp--;
+      continue;
+    }
+    if (--budget < 0) {
+      atomicOr(status, 1u);
+      return;
+    }
+    // one thread over budget stops the others (the grid is incomplete either way)
+    if ((budget & 1023) == 0 && (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1u)) return;
+    msk[sp] = (uint8_t)(m & (m - 1));
+    Tri<T> ch;
+    child_of(stk[sp], __ffs(m) - 1, ch);
+    // expand() returns 0 at level 63, so sp + 1 <= 63 - level
+    msk[sp + 1] = (uint8_t)expand<T, G>(ch, level + sp + 1, thr, R, grid);
+    stk[sp + 1] = ch;
+    sp++;
+  }
+}
+
+// One level.  faces != null: level 0, the triangles gathered from (pts, faces) and tested here;
+// else the first min(*n_in, cap) triangles of `in`.  last: every kept child is finished
+// depth-first instead of appended.  The loop trip count is uniform over the workgroup.
+template <typename T, typename G>
+__global__ void __launch_bounds__(256) subdivide_async_kernel(
+    const T *__restrict__ pts, const int64_t *__restrict__ faces, int64_t F, const Tri<T> *__restrict__ in,
+    const unsigned long long *__restrict__ n_in, int level, int last, int64_t cap, T thr, int R, G *__restrict__ grid,
+    Tri<T> *__restrict__ out, unsigned long long *__restrict__ n_out, unsigned *__restrict__ status) {
+  __shared__ int s_wave[4];
+  __shared__ unsigned long long s_base;
+  const int64_t n = faces ? F : (int64_t)min(*n_in, (unsigned long long)cap);
+  for (int64_t b0 = blockIdx.x * 256ll; b0 < n; b0 += (int64_t)gridDim.x * 256) {
+    const int64_t i = b0 + threadIdx.x;
+    Tri<T> t;
+    uint32_t keep = 0;
+    if (i < n) {
+      bool live = true;
+      if (faces) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          const int64_t v = faces[i * 3 + k];
+          t.v[k * 3 + 0] = pts[v * 3 + 0];
+          t.v[k * 3 + 1] = pts[v * 3 + 1];
+          t.v[k * 3 + 2] = pts[v * 3 + 2];
+        }
+        live = needs_split(t.v, thr);
+      } else {
+        t = in[i];
+      }
+      if (live) keep = expand<T, G>(t, level, thr, R, grid);
+    }
+    if (last) {  // kernel-uniform
+      for (uint32_t m = keep; m; m &= m - 1) {
+        Tri<T> ch;
+        child_of(t, __ffs(m) - 1, ch);
+        subdivide_dfs<T, G>(ch, level + 1, thr, R, grid, status);
+      }
+      continue;
+    }
+    int total = 0;
+    const int pre = block_exclusive_scan(__popc(keep), s_wave, &total);
+    if (total == 0) continue;  // uniform
+    if (threadIdx.x == 0) s_base = atomicAdd(n_out, (unsigned long long)total);
+    __syncthreads();
+    unsigned long long o = s_base + (unsigned long long)pre;
+    __syncthreads();  // s_base is rewritten by the next trip
+    for (uint32_t m = keep; m; m &= m - 1, o++) {
+      Tri<T> ch;
+      child_of(t, __ffs(m) - 1, ch);
+      if (o < (unsigned long long)cap) {
+        out[o] = ch;
+      } else {
+        atomicOr(status, 2u);
+        subdivide_dfs<T, G>(ch, level + 1, thr, R, grid, status);
+      }
+    }
+  }
+}
+
+template <typename T>
+static size_t voxel_async_ws_bytes(int64_t cap) {
+  return VOX_COUNTER_BYTES + 2 * (size_t)std::max<int64_t>(cap, 0) * sizeof(Tri<T>);
+}
+
+// levels launched: enough to drain a mesh inside the unit cube (see above), at most 64
+static int voxel_async_levels(int R) {
+  const double e = (double)(R - 1) / ((double)R * (double)R);
+  const int k = (int)std::ceil(std::log(3.0 / (e * e)) / std::log(4.0)) + 2;
+  return std::max(1, std::min(VOX_MAX_LEVELS, k));
+}
+
+template <typename T, typename G>
+static int voxel_mark_async(int64_t V, const T *pts, int64_t F, const int64_t *faces, int R, G *grid, int64_t cap,
+                            unsigned *status, void *ws, size_t ws_bytes, hipStream_t st) {
+  KL_REQUIRE(cap >= 0, "trianglemeshes_to_voxelgrids: capacity must be >= 0");
+  KL_REQUIRE(ws_bytes >= voxel_async_ws_bytes<T>(cap), "trianglemeshes_to_voxelgrids: workspace too small");
+  KL_REQUIRE(status != nullptr, "trianglemeshes_to_voxelgrids: status required");
+  int rc = fill_async(status, 0, sizeof(unsigned), st);
+  if (rc) return rc;
+  if (V > 0) {
+    hipLaunchKernelGGL((mark_vertices_kernel<T, G>), dim3((unsigned)cdiv(V, 256)), dim3(256), 0, st, V, pts, R, grid);
+    KL_CHECK_LAUNCH();
+  }
+  if (F == 0) return KL_OK;
+  const double thr_d = (double)(R - 1) / ((double)R * (double)R);
+  const T thr = (T)(thr_d * thr_d);
+  unsigned long long *counter = reinterpret_cast<unsigned long long *>(ws);
+  Tri<T> *buf[2] = {reinterpret_cast<Tri<T> *>((char *)ws + VOX_COUNTER_BYTES), nullptr};
+  buf[1] = buf[0] + cap;
+  rc = fill_async(counter, 0, (VOX_MAX_LEVELS + 1) * sizeof(unsigned long long), st);
+  if (rc) return rc;
+  const int levels = voxel_async_levels(R);
+  const unsigned g_rest = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(cap, 256), 2048));
+  for (int k = 0; k < levels; k++) {
+    // level k reads buf[(k - 1) & 1] (count counter[k]) and appends to buf[k & 1] (counter[k + 1])
+    const unsigned g = k == 0 ? (unsigned)std::min<int64_t>(cdiv(F, 256), 4096) : g_rest;
+    hipLaunchKernelGGL((subdivide_async_kernel<T, G>), dim3(g), dim3(256), 0, st, pts, k == 0 ? faces : nullptr, F,
+                       (const Tri<T> *)buf[(k + 1) & 1], (const unsigned long long *)counter + k, k,
+                       (int)(k == levels - 1), cap, thr, R, grid, buf[k & 1], counter + k + 1, status);
+    KL_CHECK_LAUNCH();
+  }
+  return KL_OK;
+}
+
+template <typename T>
+static int voxel_async_dispatch(int64_t V, const void *pts, int64_t F, const int64_t *faces, int R, kl_dtype gdt,
+                                void *grid, int64_t cap, unsigned *status, void *ws, size_t ws_bytes,
+                                hipStream_t st) {
+  const T *p = (const T *)pts;
+  switch (gdt) {
+    case KL_F32: return voxel_mark_async<T, float>(V, p, F, faces, R, (float *)grid, cap, status, ws, ws_bytes, st);
+    case KL_F64: return voxel_mark_async<T, double>(V, p, F, faces, R, (double *)grid, cap, status, ws, ws_bytes, st);
+    case KL_F16: return voxel_mark_async<T, __half>(V, p, F, faces, R, (__half *)grid, cap, status, ws, ws_bytes, st);
+    case KL_U8: return voxel_mark_async<T, uint8_t>(V, p, F, faces, R, (uint8_t *)grid, cap, status, ws, ws_bytes, st);
+    default: break;
+  }
+  set_error("voxelgrid: unsupported grid dtype");
+  return KL_E_INVALID;
+}
+
 template <typename T>
 static int voxel_dispatch_grid(int64_t V, const void *pts, int64_t F, const int64_t *faces, int R, kl_dtype gdt,
                                void *grid, kl_alloc_fn alloc, void *ctx, hipStream_t st) {
@@ -352,6 +557,24 @@ extern "C" int kl_voxelgrid_mark(int64_t V, const float *pts, int64_t F, const i
   KL_REQUIRE(R > 1, "trianglemeshes_to_voxelgrids: resolution must be > 1");
   KL_REQUIRE(alloc != nullptr, "trianglemeshes_to_voxelgrids: allocator required");
   return voxel_dispatch_grid<float>(V, pts, F, faces, R, grid_dtype, grid, alloc, ctx, S(stream));
+}
+
+extern "C" size_t kl_voxelgrid_mark_async_workspace_bytes(kl_dtype point_dtype, int64_t capacity) {
+  return point_dtype == KL_F64 ? voxel_async_ws_bytes<double>(capacity) : voxel_async_ws_bytes<float>(capacity);
+}
+
+extern "C" int kl_voxelgrid_mark_async(kl_dtype point_dtype, int64_t V, const void *pts, int64_t F,
+                                       const int64_t *faces, int R, kl_dtype grid_dtype, void *grid, int64_t capacity,
+                                       uint32_t *status, void *ws, size_t ws_bytes, kl_stream stream) {
+  KL_REQUIRE(R > 1, "trianglemeshes_to_voxelgrids: resolution must be > 1");
+  if (point_dtype == KL_F32)
+    return voxel_async_dispatch<float>(V, pts, F, faces, R, grid_dtype, grid, capacity, status, ws, ws_bytes,
+                                       S(stream));
+  if (point_dtype == KL_F64)
+    return voxel_async_dispatch<double>(V, pts, F, faces, R, grid_dtype, grid, capacity, status, ws, ws_bytes,
+                                        S(stream));
+  set_error("trianglemeshes_to_voxelgrids: f32 / f64 points only");
+  return KL_E_INVALID;
 }
 
 extern "C" int kl_voxelgrid_mark_f64(int64_t V, const double *pts, int64_t F, const int64_t *faces, int R,

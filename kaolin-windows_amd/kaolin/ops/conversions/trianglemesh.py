@@ -9,6 +9,10 @@ from ... import _native as N
 
 __all__ = ['trianglemeshes_to_voxelgrids', 'unbatched_mesh_to_spc']
 
+# True: the subdivision sized on the host (kl_voxelgrid_mark, one count read per round) instead of
+# the device-counted kl_voxelgrid_mark_async; the two grids are equal (tests / bench compare them)
+HOST_SIZED = False
+
 
 def trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin=None, scale=None, return_sparse=False):
     r"""Surface voxelgrids (B,R,R,R) of meshes: vertices are normalised by
@@ -50,14 +54,32 @@ def trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin=None, scale
     grid_dtype = out_dtype if not return_sparse else torch.float32
     grid = torch.zeros((batch_size, R, R, R), dtype=grid_dtype, device=vertices.device)
     lib = N.lib()
-    fn = lib.kl_voxelgrid_mark if work.dtype == torch.float32 else lib.kl_voxelgrid_mark_f64
     dev = vertices.device
-    with N.on_device(dev):
-        for i in range(batch_size):
-            arena = N.Arena(dev)
-            N.check(fn(points.shape[1], N.ptr(points[i]), faces.shape[0], N.ptr(faces), R,
-                       N.dtype_code(grid_dtype), N.ptr(grid[i]), arena.fn, None, N.stream_of(dev)),
-                    'trianglemeshes_to_voxelgrids')
+    if HOST_SIZED and not N.capturing(dev):
+        fn = lib.kl_voxelgrid_mark if work.dtype == torch.float32 else lib.kl_voxelgrid_mark_f64
+        with N.on_device(dev):
+            for i in range(batch_size):
+                arena = N.Arena(dev)
+                N.check(fn(points.shape[1], N.ptr(points[i]), faces.shape[0], N.ptr(faces), R,
+                           N.dtype_code(grid_dtype), N.ptr(grid[i]), arena.fn, None, N.stream_of(dev)),
+                        'trianglemeshes_to_voxelgrids')
+    else:
+        # nothing read back per round (graph-capturable); one status read per call in eager mode
+        F = faces.shape[0]
+        cap = min(max(16 * F, 1 << 20), 1 << 26)
+        code = N.dtype_code(work.dtype)
+        nb = lib.kl_voxelgrid_mark_async_workspace_bytes(code, cap)
+        ws = torch.empty(nb, dtype=torch.uint8, device=dev)
+        status = torch.zeros(max(batch_size, 1), dtype=torch.int32, device=dev)
+        with N.on_device(dev):
+            for i in range(batch_size):
+                N.check(lib.kl_voxelgrid_mark_async(code, points.shape[1], N.ptr(points[i]), F, N.ptr(faces), R,
+                                                    N.dtype_code(grid_dtype), N.ptr(grid[i]), cap,
+                                                    N.ptr(status[i:]), N.ptr(ws), nb, N.stream_of(dev)),
+                        'trianglemeshes_to_voxelgrids')
+        if not N.capturing(dev) and bool((status & 1).any()):
+            raise RuntimeError('trianglemeshes_to_voxelgrids: a triangle needs more than 2^20 subdivisions '
+                               '(vertices far outside the unit cube after origin / scale?)')
     if return_sparse:
         return grid.to_sparse()
     return grid

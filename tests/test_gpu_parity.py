@@ -822,6 +822,104 @@ def test_voxelgrid_vs_oracle_sphere(kal):
     assert np.array_equal(A(vg).astype(np.uint8), ov)
 
 
+def _voxel_async(points, faces, R, cap, grid_dtype=torch.float32):
+    """kl_voxelgrid_mark_async on one mesh at an explicit capacity -> (grid, status)."""
+    from kaolin import _native as N
+    lib = N.lib()
+    code = N.dtype_code(points.dtype)
+    nb = lib.kl_voxelgrid_mark_async_workspace_bytes(code, cap)
+    ws = torch.empty(max(nb, 1), dtype=torch.uint8, device=DEV)
+    grid = torch.zeros((R, R, R), dtype=grid_dtype, device=DEV)
+    status = torch.full((1,), -1, dtype=torch.int32, device=DEV)
+    N.check(lib.kl_voxelgrid_mark_async(code, points.shape[0], N.ptr(points), faces.shape[0], N.ptr(faces), R,
+                                        N.dtype_code(grid_dtype), N.ptr(grid), cap, N.ptr(status), N.ptr(ws), nb,
+                                        N.stream_of(points.device)), 'voxel async')
+    return grid, int(status.item())
+
+
+def _voxel_host_sized(kal, v, f, R, o=None, s=None):
+    from kaolin.ops.conversions import trianglemesh as tm
+    tm.HOST_SIZED = True
+    try:
+        return kal.ops.conversions.trianglemeshes_to_voxelgrids(v, f, R, o, s)
+    finally:
+        tm.HOST_SIZED = False
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+def test_voxelgrid_async_equals_host_sized_any_capacity(kal, dtype):
+    """The device-counted subdivision (no host reads) marks the host-sized path's grid for every
+    capacity: 0 (every triangle finished depth-first at level 0), capacities that overflow some
+    level part-way, and one that holds every level."""
+    v, f = _uv_sphere(20, 32, 0.95)
+    vt, ft = T(v, dtype).unsqueeze(0), T(f)
+    R = 64
+    ref = _voxel_host_sized(kal, vt, ft, R)
+    if dtype == torch.float32:
+        assert np.array_equal(A(ref[0]).astype(np.uint8), orc.voxelgrid(v[None].astype(np.float32), f, R))
+    o = torch.min(vt, dim=1)[0]
+    s = torch.max(torch.max(vt, dim=1)[0] - o, dim=1)[0]
+    pts = ((vt - o.unsqueeze(1)) / s.view(-1, 1, 1))[0].contiguous()
+    for cap in (0, 1, 300, 5000, 1 << 20):
+        grid, status = _voxel_async(pts, ft, R, cap)
+        assert torch.equal(grid, ref[0].float()), cap
+        assert status & 1 == 0
+        if cap == 0:
+            assert status == 2  # the first level overflowed
+        if cap == 1 << 20:
+            assert status == 0
+
+
+@pytest.mark.parametrize('grid_dtype', [torch.float64, torch.float16, torch.uint8])
+def test_voxelgrid_async_grid_dtypes_and_outside_unit_cube(kal, grid_dtype):
+    """An origin / scale that leaves the unit cube needs more levels than are launched: the last
+    level finishes those subtrees depth-first; the grid still equals the host-sized path's."""
+    v, f = _uv_sphere(12, 16, 0.95)
+    vt, ft = T(v, torch.float32).unsqueeze(0), T(f)
+    R = 16
+    o = torch.tensor([[-1.0, -1.0, -1.0]], device=DEV)
+    s = torch.tensor([0.03], device=DEV)  # coordinates up to ~60: ~6 more levels than launched
+    ref = _voxel_host_sized(kal, vt, ft, R, o, s)
+    pts = ((vt - o.unsqueeze(1)) / s.view(-1, 1, 1))[0].contiguous()
+    grid, status = _voxel_async(pts, ft, R, 1 << 16, grid_dtype)
+    assert status & 1 == 0
+    assert torch.equal(grid.float(), ref[0].float())
+    assert int(ref.sum()) > 0
+
+
+def test_voxelgrid_async_budget_exceeded_raises(kal):
+    """A triangle whose subtree exceeds the depth-first budget stops (all threads) and the
+    eager call raises, where the host-sized path would fail its allocation."""
+    v = torch.tensor([[[0.0, 0.0, 0.0], [1.0, 0.0, 0.0], [0.0, 1.0, 0.0]]], device=DEV)
+    f = torch.tensor([[0, 1, 2]], device=DEV)
+    with pytest.raises(RuntimeError, match='2\\^20'):
+        kal.ops.conversions.trianglemeshes_to_voxelgrids(v, f, 8, torch.zeros((1, 3), device=DEV),
+                                                         torch.tensor([1e-5], device=DEV))
+
+
+def test_voxelgrid_graph_capture(kal):
+    """trianglemeshes_to_voxelgrids (default origin / scale) captured into a HIP graph: nothing
+    is read back, and replays over new vertices give the eager grids."""
+    v, f = _uv_sphere(20, 32, 0.9)
+    vt, ft = T(v, torch.float32).unsqueeze(0), T(f)
+    R = 48
+    static_v = vt.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        kal.ops.conversions.trianglemeshes_to_voxelgrids(static_v, ft, R)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = kal.ops.conversions.trianglemeshes_to_voxelgrids(static_v, ft, R)
+    for k, scale in enumerate((1.0, 0.7)):
+        newv = vt * scale + 0.01 * k
+        static_v.copy_(newv)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, _voxel_host_sized(kal, newv, ft, R)), k
+
+
 # ------------------------------------------------------------------ SPC
 def test_mesh_to_spc_kat(kal, golden):
     g = golden('spc.npz')
