@@ -856,7 +856,7 @@ def test_voxelgrid_async_equals_host_sized_any_capacity(kal, dtype):
     R = 64
     ref = _voxel_host_sized(kal, vt, ft, R)
     if dtype == torch.float32:
-        assert np.array_equal(A(ref[0]).astype(np.uint8), orc.voxelgrid(v[None].astype(np.float32), f, R))
+        assert np.array_equal(A(ref[0]).astype(np.uint8), orc.voxelgrid(v[None].astype(np.float32), f, R)[0])
     o = torch.min(vt, dim=1)[0]
     s = torch.max(torch.max(vt, dim=1)[0] - o, dim=1)[0]
     pts = ((vt - o.unsqueeze(1)) / s.view(-1, 1, 1))[0].contiguous()
@@ -874,11 +874,13 @@ def test_voxelgrid_async_equals_host_sized_any_capacity(kal, dtype):
 def test_voxelgrid_async_grid_dtypes_and_outside_unit_cube(kal, grid_dtype):
     """An origin / scale that leaves the unit cube needs more levels than are launched: the last
     level finishes those subtrees depth-first; the grid still equals the host-sized path's."""
-    v, f = _uv_sphere(12, 16, 0.95)
+    v, f = _uv_sphere(6, 8, 0.95)
     vt, ft = T(v, torch.float32).unsqueeze(0), T(f)
     R = 16
-    o = torch.tensor([[-1.0, -1.0, -1.0]], device=DEV)
-    s = torch.tensor([0.03], device=DEV)  # coordinates up to ~60: ~6 more levels than launched
+    # the unit cube around the pole (0, 0.95, 0); the rest of the sphere reaches ~19: ~2 levels
+    # more than are launched
+    o = torch.tensor([[-0.05, 0.9, -0.05]], device=DEV)
+    s = torch.tensor([0.1], device=DEV)
     ref = _voxel_host_sized(kal, vt, ft, R, o, s)
     pts = ((vt - o.unsqueeze(1)) / s.view(-1, 1, 1))[0].contiguous()
     grid, status = _voxel_async(pts, ft, R, 1 << 16, grid_dtype)
