@@ -868,16 +868,9 @@ struct RayIn {
 
 // decide (raytrace_cuda.cu:63-222): info = children count / keep flag; depth at the target level
 // (fixed-capacity entry: the count is read from dnum on the device and info is zeroed up to span)
-__global__ void rt_decide_kernel(RayIn in, int64_t num, const int2 *__restrict__ nug, uint32_t *__restrict__ info,
-                                 float *__restrict__ depth, uint32_t level, int last, int with_depth, int with_exit,
-                                 const uint32_t *__restrict__ dnum, int64_t span) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (dnum) num = *dnum;
-  if (t > span) return;
-  if (t >= num) {
-    info[t] = 0;
-    return;
-  }
+__device__ __forceinline__ void rt_decide_one(const RayIn &in, int64_t t, const int2 *__restrict__ nug,
+                                              uint32_t *__restrict__ info, float *__restrict__ depth, uint32_t level,
+                                              int last, int with_depth, int with_exit) {
   const int ridx = nug[t].x, pidx = nug[t].y;
   const int16_t *p = in.points + (int64_t)pidx * 3;
   const float o[3] = {in.ro[ridx * 3], in.ro[ridx * 3 + 1], in.ro[ridx * 3 + 2]};
@@ -910,11 +903,18 @@ __global__ void rt_decide_kernel(RayIn in, int64_t num, const int2 *__restrict__
   }
 }
 
-__global__ void rt_subdivide_kernel(RayIn in, int64_t num, const int2 *__restrict__ nin, int2 *__restrict__ nout,
-                                    const uint32_t *__restrict__ info, const uint32_t *__restrict__ psum,
-                                    uint32_t level, int64_t cap) {
+__global__ void rt_decide_kernel(RayIn in, int64_t num, const int2 *__restrict__ nug, uint32_t *__restrict__ info,
+                                 float *__restrict__ depth, uint32_t level, int last, int with_depth, int with_exit) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= num || !info[t]) return;
+  if (t == num) info[t] = 0;
+  if (t >= num) return;
+  rt_decide_one(in, t, nug, info, depth, level, last, with_depth, with_exit);
+}
+
+__device__ __forceinline__ void rt_subdivide_one(const RayIn &in, int64_t t, const int2 *__restrict__ nin,
+                                                 int2 *__restrict__ nout, const uint32_t *__restrict__ info,
+                                                 const uint32_t *__restrict__ psum, uint32_t level, int64_t cap) {
+  if (!info[t]) return;
   const int ridx = nin[t].x, pidx = nin[t].y;
   const int16_t *p = in.points + (int64_t)pidx * 3;
   uint32_t base = psum[t];
@@ -937,6 +937,13 @@ __global__ void rt_subdivide_kernel(RayIn in, int64_t num, const int2 *__restric
       if (base < cap) nout[base] = make_int2(ridx, (int)(s + c));
       base++;
     }
+}
+
+__global__ void rt_subdivide_kernel(RayIn in, int64_t num, const int2 *__restrict__ nin, int2 *__restrict__ nout,
+                                    const uint32_t *__restrict__ info, const uint32_t *__restrict__ psum,
+                                    uint32_t level, int64_t cap) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t < num) rt_subdivide_one(in, t, nin, nout, info, psum, level, cap);
 }
 
 __global__ void rt_compact_kernel(int64_t num, const int2 *__restrict__ nin, const float *__restrict__ din,
@@ -966,13 +973,116 @@ __global__ void rt_init_kernel(int64_t n, int2 *__restrict__ nug, uint32_t *__re
 // the capacity (the nuggets kept are then a prefix of the full list: the lists stay in ray,
 // front-to-back order and a nugget's children follow its predecessors'); result = (rows,
 // truncated)
-__global__ void rt_count_kernel(const uint32_t *__restrict__ total, uint32_t cap, uint32_t *__restrict__ dnum,
+__global__ void rt_count_kernel(const uint32_t *__restrict__ psum, uint32_t cap, uint32_t *__restrict__ dnum,
                                 int64_t *__restrict__ result, int last) {
   if (threadIdx.x != 0) return;
-  const uint32_t n = *total;
+  const uint32_t n = psum[*dnum];  // the scan's total, at the level's count
   *dnum = n < cap ? n : cap;
   if (n > cap) result[1] = 1;
   if (last) result[0] = n < cap ? n : cap;
+}
+
+// Fixed-capacity level kernels: a fixed grid strides over the level's count read on the device
+// (a grid sized to the capacity paid ~10 us per launch for its empty workgroups at 13 M rows).
+constexpr int RTF_GRID = 2048;
+
+__global__ void __launch_bounds__(256) rtf_decide_kernel(RayIn in, const uint32_t *__restrict__ dnum,
+                                                         const int2 *__restrict__ nug, uint32_t *__restrict__ info,
+                                                         float *__restrict__ depth, uint32_t level, int last,
+                                                         int with_depth, int with_exit) {
+  const int64_t num = *dnum;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < num; t += (int64_t)gridDim.x * 256)
+    rt_decide_one(in, t, nug, info, depth, level, last, with_depth, with_exit);
+}
+
+__global__ void __launch_bounds__(256) rtf_subdivide_kernel(RayIn in, const uint32_t *__restrict__ dnum,
+                                                            const int2 *__restrict__ nin, int2 *__restrict__ nout,
+                                                            const uint32_t *__restrict__ info,
+                                                            const uint32_t *__restrict__ psum, uint32_t level,
+                                                            int64_t cap) {
+  const int64_t num = *dnum;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < num; t += (int64_t)gridDim.x * 256)
+    rt_subdivide_one(in, t, nin, nout, info, psum, level, cap);
+}
+
+__global__ void __launch_bounds__(256) rtf_compact_kernel(const uint32_t *__restrict__ dnum,
+                                                          const int2 *__restrict__ nin, const float *__restrict__ din,
+                                                          int2 *__restrict__ nout, float *__restrict__ dout, int dd,
+                                                          const uint32_t *__restrict__ info,
+                                                          const uint32_t *__restrict__ psum, int64_t cap) {
+  const int64_t num = *dnum;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < num; t += (int64_t)gridDim.x * 256) {
+    if (!info[t]) continue;
+    const uint32_t o = psum[t];
+    if (o >= cap) continue;
+    nout[o] = nin[t];
+    if (dout)
+      for (int k = 0; k < dd; k++) dout[(int64_t)o * dd + k] = din[t * dd + k];
+  }
+}
+
+// Exclusive scan of in[0, *dn) into out[0, *dn], out[*dn] = the total, with the count read on the
+// device: tile sums, one workgroup scanning them, then each tile's scan plus its offset.  Tiles
+// past the count exit at once.
+constexpr int DSCAN_PER = 16, DSCAN_TILE = 256 * DSCAN_PER;
+
+__global__ void __launch_bounds__(256) dscan_tile_sum_kernel(const uint32_t *__restrict__ in,
+                                                             const uint32_t *__restrict__ dn,
+                                                             uint32_t *__restrict__ tsum) {
+  __shared__ int s_wave[4];
+  const int64_t n = *dn, base = blockIdx.x * (int64_t)DSCAN_TILE;
+  if (base >= n) return;  // uniform
+  int v = 0;
+#pragma unroll
+  for (int k = 0; k < DSCAN_PER; k++) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    if (i < n) v += (int)in[i];
+  }
+  int tot = 0;
+  (void)block_exclusive_scan(v, s_wave, &tot);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = (uint32_t)tot;
+}
+
+__global__ void __launch_bounds__(1024) dscan_tile_offset_kernel(uint32_t *__restrict__ tsum,
+                                                                 const uint32_t *__restrict__ dn,
+                                                                 uint32_t *__restrict__ out) {
+  __shared__ int s_wave[16];
+  const int64_t n = *dn;
+  const int nt = (int)((n + DSCAN_TILE - 1) / DSCAN_TILE);
+  uint32_t carry = 0;
+  for (int b0 = 0; b0 < nt; b0 += 1024) {
+    const int i = b0 + threadIdx.x;
+    const int v = i < nt ? (int)tsum[i] : 0;
+    int tot = 0;
+    const int ex = block_exclusive_scan(v, s_wave, &tot);
+    if (i < nt) tsum[i] = carry + (uint32_t)ex;
+    carry += (uint32_t)tot;
+  }
+  if (threadIdx.x == 0) out[n] = carry;
+}
+
+__global__ void __launch_bounds__(256) dscan_apply_kernel(const uint32_t *__restrict__ in,
+                                                          const uint32_t *__restrict__ dn,
+                                                          const uint32_t *__restrict__ toff,
+                                                          uint32_t *__restrict__ out) {
+  __shared__ int s_wave[4];
+  const int64_t n = *dn, base = blockIdx.x * (int64_t)DSCAN_TILE;
+  if (base >= n) return;  // uniform
+  const int64_t i0 = base + threadIdx.x * DSCAN_PER;
+  uint32_t v[DSCAN_PER];
+  int sum = 0;
+#pragma unroll
+  for (int k = 0; k < DSCAN_PER; k++) {
+    v[k] = i0 + k < n ? in[i0 + k] : 0u;
+    sum += (int)v[k];
+  }
+  int tot = 0;
+  uint32_t run = toff[blockIdx.x] + (uint32_t)block_exclusive_scan(sum, s_wave, &tot);
+#pragma unroll
+  for (int k = 0; k < DSCAN_PER; k++) {
+    if (i0 + k < n) out[i0 + k] = run;
+    run += v[k];
+  }
 }
 
 template <typename S>
@@ -1128,7 +1238,7 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
     if (last && return_depth) d0 = (float *)sc.get(num * dd * sizeof(float));
     if (!info || !psum || (last && return_depth && !d0)) return KL_E_ALLOC;
     hipLaunchKernelGGL(rt_decide_kernel, dim3((unsigned)cdiv(num + 1, 256)), dim3(256), 0, st, in, num, n0, info, d0,
-                       l, last, return_depth, with_exit, (const uint32_t *)nullptr, num);
+                       l, last, return_depth, with_exit);
     KL_CHECK_LAUNCH();
     uint32_t cnt = 0;
     int rc = exclusive_scan(info, psum, num, sc, st, &cnt);
@@ -1171,16 +1281,14 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
 // result[0] hold nugget (-1, -1) and depth 0.
 namespace {
 struct RtfWs {
-  size_t a, b, info, psum, dtmp, dnum, temp, temp_bytes, total;
-  int64_t cap0;
+  size_t a, b, info, psum, dtmp, dnum, tsum, total;
+  int64_t cap0, ntiles;
 };
 RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
   RtfWs w{};
   w.cap0 = std::max<int64_t>(std::max<int64_t>(num_rays, capacity), 1);
+  w.ntiles = cdiv(w.cap0, (int64_t)DSCAN_TILE);
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  size_t tb = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                         (int)w.cap0 + 1);
   size_t o = 0;
   w.a = o; o += al(w.cap0 * sizeof(int2));
   w.b = o; o += al(w.cap0 * sizeof(int2));
@@ -1188,7 +1296,7 @@ RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
   w.psum = o; o += al((w.cap0 + 2) * 4);
   w.dtmp = o; o += al(w.cap0 * (with_exit ? 2 : 1) * 4);
   w.dnum = o; o += 256;
-  w.temp = o; w.temp_bytes = al(tb > 0 ? tb : 16); o += w.temp_bytes;
+  w.tsum = o; o += al(w.ntiles * 4);
   w.total = o;
   return w;
 }
@@ -1222,23 +1330,31 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
   hipLaunchKernelGGL(rt_init_kernel, dim3((unsigned)cdiv(std::max<int64_t>(num_rays, 1), 256)), dim3(256), 0, st,
                      num_rays, n0, dnum, result);
   KL_CHECK_LAUNCH();
-  const unsigned g = (unsigned)cdiv(cap0 + 1, 256);
+  const unsigned g = (unsigned)std::min<int64_t>(cdiv(cap0, 256), RTF_GRID);
+  const unsigned gt = (unsigned)L.ntiles;
+  uint32_t *tsum = (uint32_t *)(w + L.tsum);
   for (uint32_t l = 0; l <= target_level; l++) {
     const int last = l == target_level;
-    hipLaunchKernelGGL(rt_decide_kernel, dim3(g), dim3(256), 0, st, in, cap0, n0, info, last ? d0 : nullptr, l, last,
-                       return_depth, with_exit, (const uint32_t *)dnum, cap0);
+    hipLaunchKernelGGL(rtf_decide_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, n0, info,
+                       last ? d0 : nullptr, l, last, return_depth, with_exit);
     KL_CHECK_LAUNCH();
-    size_t tb = L.temp_bytes;
-    KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(w + L.temp, tb, info, psum, (int)cap0 + 1, st));
+    hipLaunchKernelGGL(dscan_tile_sum_kernel, dim3(gt), dim3(256), 0, st, (const uint32_t *)info,
+                       (const uint32_t *)dnum, tsum);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(dscan_tile_offset_kernel, dim3(1), dim3(1024), 0, st, tsum, (const uint32_t *)dnum, psum);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(dscan_apply_kernel, dim3(gt), dim3(256), 0, st, (const uint32_t *)info, (const uint32_t *)dnum,
+                       (const uint32_t *)tsum, psum);
+    KL_CHECK_LAUNCH();
     if (!last) {
-      hipLaunchKernelGGL(rt_subdivide_kernel, dim3(g), dim3(256), 0, st, in, cap0, n0, n1, info, psum, l,
-                         (int64_t)capacity);
+      hipLaunchKernelGGL(rtf_subdivide_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, n0, n1, info,
+                         psum, l, (int64_t)capacity);
     } else {
-      hipLaunchKernelGGL(rt_compact_kernel, dim3(g), dim3(256), 0, st, cap0, n0, d0, (int2 *)nuggets,
-                         return_depth ? depth : nullptr, dd, info, psum, (int64_t)capacity);
+      hipLaunchKernelGGL(rtf_compact_kernel, dim3(g), dim3(256), 0, st, (const uint32_t *)dnum, n0, d0,
+                         (int2 *)nuggets, return_depth ? depth : nullptr, dd, info, psum, (int64_t)capacity);
     }
     KL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(rt_count_kernel, dim3(1), dim3(64), 0, st, psum + cap0, (uint32_t)capacity, dnum, result, last);
+    hipLaunchKernelGGL(rt_count_kernel, dim3(1), dim3(64), 0, st, psum, (uint32_t)capacity, dnum, result, last);
     KL_CHECK_LAUNCH();
     std::swap(n0, n1);
   }

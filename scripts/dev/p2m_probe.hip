@@ -9,6 +9,11 @@
 #include <vector>
 
 namespace kl {
+int g_dev_flags = 0;
+template <typename T>
+int acc_finalize(const double *, T *, size_t, bool, hipStream_t, int *) { return 0; }  // backward: unused here
+template int acc_finalize<float>(const double *, float *, size_t, bool, hipStream_t, int *);
+template int acc_finalize<double>(const double *, double *, size_t, bool, hipStream_t, int *);
 void set_error(const std::string &msg) { fprintf(stderr, "error: %s\n", msg.c_str()); }
 int fill_async(void *p, int value, size_t bytes, hipStream_t st) { return hipMemsetAsync(p, value, bytes, st) == hipSuccess ? 0 : -2; }
 }  // namespace kl
