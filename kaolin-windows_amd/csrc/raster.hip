@@ -1589,12 +1589,20 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
   void *soft_ws = reinterpret_cast<char *>(ws) + acc_bytes;
   void *gath_ws = reinterpret_cast<char *>(soft_ws) + soft_bytes;
   bool has_soft = false;
-  // The two halves are independent until the final add, so they run concurrently: the
-  // soft-mask sums (fill, plan, backward; left in double) on the side stream, the
-  // rasterizer's gather (every face's own rounded gradient) on `st`; after the join each
-  // coordinate gets the soft sum rounded on its own and added, as autograd adds the two
-  // gradients.  The gather's big-face counter is the state's scratch int (zeroed by the
-  // forward), re-zeroed by that final add; the soft half does not touch it.
+  // The soft-mask sums first (fill, plan, backward; left in double), then the gather on the same
+  // stream: it adds each face's soft sum, rounded on its own, to the face's own rounded gradient
+  // as it writes it -- autograd's add of the two gradients -- so there is no final add.  The soft
+  // kernel zeroes the gather's big-face counter (the state's scratch int, left non-zero by the
+  // previous backward) before the gather runs.  (r03x: 0.221-0.224 ms per step against
+  // 0.224-0.228 for the two halves on two streams joined by a final add, whose fork and join
+  // cost ~5 + ~11 us in the graph; dev bit 23 keeps that variant for A/B timing.)
+  if (!((g_dev_flags >> 23) & 1)) {
+    KL_CHECK_RC(soft_tile_backward<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m, gfvi, true, soft_ws,
+                                      soft_bytes, st, acc, &has_soft));
+    return rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
+                                   gfeat, gath_ws, ws_bytes - acc_bytes - soft_bytes, s.scratch, st, face_ranges,
+                                   has_soft ? acc : nullptr);
+  }
   SideFork fork(st);
   SoftState<T> ss = s;
   ss.scratch = nullptr;
