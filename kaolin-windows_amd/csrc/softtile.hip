@@ -480,9 +480,19 @@ __global__ void __launch_bounds__(256) soft_tile_eval_kernel(SoftTileArgs<T> a) 
 // the item count; the backward kernel is persistent and takes the items round-robin.
 constexpr int SB_PIECE = 512;
 
+// Block 0 plans; blocks 1.. zero the backward's double accumulator (n doubles) meanwhile -- one
+// launch instead of a fill followed by the one-workgroup plan (5.4 + 7.8 us at cfg3).
+constexpr int SB_ZERO_BLOCKS = 128;
 __global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restrict__ seg_tot, BinGeom g,
-                                                             int2 *__restrict__ items, int *__restrict__ ctl) {
+                                                             int2 *__restrict__ items, int *__restrict__ ctl,
+                                                             double *__restrict__ acc, size_t n) {
   __shared__ int s_wave[16];
+  if (blockIdx.x > 0) {
+    for (size_t i = (blockIdx.x - 1) * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)(gridDim.x - 1) * blockDim.x)
+      acc[i] = 0.0;
+    return;
+  }
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   int carry = 0;
   for (int t0 = 0; t0 < nt; t0 += blockDim.x) {
@@ -796,8 +806,8 @@ int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T
   int2 *items = reinterpret_cast<int2 *>(reinterpret_cast<char *>(ws) + 256);
   double *acc = acc_out ? acc_out
                         : reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + soft_bwd_acc_offset(B, H, W, K));
-  KL_CHECK_RC(fill_async(acc, 0, n * sizeof(double), st));
-  hipLaunchKernelGGL(soft_bwd_plan_kernel, dim3(1), dim3(1024), 0, st, (const int *)s.seg_tot, g, items, ctl);
+  hipLaunchKernelGGL(soft_bwd_plan_kernel, dim3(1 + SB_ZERO_BLOCKS), dim3(1024), 0, st, (const int *)s.seg_tot, g,
+                     items, ctl, acc, n);
   KL_CHECK_LAUNCH();
   int dev_id = 0, ncu = 256;
   if (hipGetDevice(&dev_id) == hipSuccess)
