@@ -1301,7 +1301,9 @@ static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T 
   hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st,
                      grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
   KL_CHECK_LAUNCH();
-  hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(256), dim3(256), 0, st, grad, face_idx, w, fvi,
+  // large faces: a workgroup each, grid-stride over the list (dev param 6 overrides the grid)
+  const unsigned bgrid = g_dev_param[6] > 0 ? (unsigned)g_dev_param[6] : 256u;
+  hipLaunchKernelGGL((rasterize_bwd_bigface_kernel<T, MAXD>), dim3(bgrid), dim3(256), 0, st, grad, face_idx, w, fvi,
                      feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
   KL_CHECK_LAUNCH();
   return KL_OK;
