@@ -55,19 +55,29 @@ __global__ void __launch_bounds__(MIOU_THREADS) miou_partial_kernel(const T *__r
   }
 }
 
-// one workgroup: thread b adds view b's partials in block order; thread 0 forms the loss
+// one workgroup: a wave per view adds its partials (lane l the partials l, l + 64, ... in order,
+// then a fixed butterfly: deterministic; one thread adding all of them serially took 13.7 us at
+// 4 x 512^2); thread 0 then forms the loss
 template <typename T>
 __global__ void __launch_bounds__(MIOU_THREADS) miou_final_kernel(const double *__restrict__ part, int B, int nbx,
                                                                  T *__restrict__ up, T *__restrict__ down,
                                                                  T *__restrict__ loss) {
-  for (int b = threadIdx.x; b < B; b += MIOU_THREADS) {
+  const int lane = threadIdx.x & 63;
+  for (int b = threadIdx.x >> 6; b < B; b += MIOU_THREADS / 64) {  // uniform per wave
     double u = 0.0, d = 0.0;
-    for (int k = 0; k < nbx; k++) {
+    for (int k = lane; k < nbx; k += 64) {
       u += part[((size_t)b * nbx + k) * 2];
       d += part[((size_t)b * nbx + k) * 2 + 1];
     }
-    up[b] = (T)u;
-    down[b] = (T)d;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      u += __shfl_xor(u, o);
+      d += __shfl_xor(d, o);
+    }
+    if (lane == 0) {
+      up[b] = (T)u;
+      down[b] = (T)d;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
