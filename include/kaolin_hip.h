@@ -350,6 +350,16 @@ int kl_unbatched_triangle_distance_backward(kl_dtype dtype, int64_t num_points, 
                                             void *grad_face_vertices, void *workspace, size_t workspace_bytes,
                                             kl_stream stream);
 
+/* The backward above for a sharded caller (not a reference op; kaolin/distributed.py): grad_points
+ * (P,3) written; the face gradient's per-coordinate sums of the per-point float terms left in double,
+ * gf_sums (F*9 doubles, zeroed here), NOT rounded -- the ranks' sums are all-reduced, then rounded
+ * once, which gives the unsharded backward's gradient bit for bit (f32 terms sum exactly in double). */
+int kl_unbatched_triangle_distance_backward_sums(kl_dtype dtype, int64_t num_points, int64_t num_faces,
+                                                 const void *grad_dist, const void *points,
+                                                 const void *face_vertices, const int64_t *face_idx,
+                                                 const int32_t *dist_type, void *grad_points, double *gf_sums,
+                                                 kl_stream stream);
+
 /* sided_distance.cpp:65-89.  p1 (B,N,3), p2 (B,M,3) -> dist (B,N), idx (B,N) int64.
  * dtype: any kl_dtype (half/float/double and the integer types of DISPATCH_NUM_TYPES). */
 int kl_sided_distance_forward(kl_dtype dtype, int batch, int64_t n, int64_t m,

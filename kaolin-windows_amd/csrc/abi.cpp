@@ -10,7 +10,7 @@ static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 int g_dev_flags = 0;
 void *g_dev_debug = nullptr;
-int g_dev_param[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+int g_dev_param[16] = {};
 }  // namespace kl
 
 // Development hook (not part of include/kaolin_hip.h): bit flags that switch parts of
@@ -23,7 +23,7 @@ extern "C" void kl_dev_set_debug(void *buf) { kl::g_dev_debug = buf; }
 // Development hook: tuning parameters for sweeps (scripts/dev/stamps.py); 0 = built-in value.
 // 0..3: the soft-mask forward's split thresholds / caps (tileorder.h, SoftSplit).
 extern "C" void kl_dev_set_param(int idx, int value) {
-  if (idx >= 0 && idx < 8) kl::g_dev_param[idx] = value;
+  if (idx >= 0 && idx < 16) kl::g_dev_param[idx] = value;
 }
 
 namespace kl {

@@ -796,6 +796,19 @@ static int p2m_bwd(int64_t P, int64_t F, const void *grad, const void *pts, cons
   return acc_finalize<T>(acc, (T *)gf, n, false, st);
 }
 
+// The face gradient's double sums, not rounded (the sharded backward adds every rank's sums, then
+// rounds once: kaolin/distributed.py).
+template <typename T>
+static int p2m_bwd_sums(int64_t P, int64_t F, const void *grad, const void *pts, const void *fv, const int64_t *idx,
+                        const int32_t *type, void *gp, double *sums, hipStream_t st) {
+  KL_CHECK_RC(fill_async(sums, 0, (size_t)F * 9 * sizeof(double), st));
+  if (P == 0) return KL_OK;
+  hipLaunchKernelGGL((p2m_bwd_kernel<T, double>), dim3((unsigned)cdiv(P, 256)), dim3(256), 0, st, (const T *)grad,
+                     (const T *)pts, (const T *)fv, idx, type, P, (T *)gp, sums);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+
 template <typename S>
 static int sided_fwd(int B, int64_t N, int64_t M, const void *p1, const void *p2, void *dist, int64_t *idx,
                      hipStream_t st) {
@@ -856,6 +869,16 @@ extern "C" int kl_unbatched_triangle_distance_backward(kl_dtype dtype, int64_t P
                                                        size_t ws_bytes, kl_stream stream) {
   if (dtype == KL_F32) return p2m_bwd<float>(P, F, grad, pts, fv, idx, type, gp, gf, ws, ws_bytes, S(stream));
   if (dtype == KL_F64) return p2m_bwd<double>(P, F, grad, pts, fv, idx, type, gp, gf, ws, ws_bytes, S(stream));
+  set_error("unbatched_triangle_distance_backward_cuda not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_unbatched_triangle_distance_backward_sums(kl_dtype dtype, int64_t P, int64_t F, const void *grad,
+                                                            const void *pts, const void *fv, const int64_t *idx,
+                                                            const int32_t *type, void *gp, double *gf_sums,
+                                                            kl_stream stream) {
+  if (dtype == KL_F32) return p2m_bwd_sums<float>(P, F, grad, pts, fv, idx, type, gp, gf_sums, S(stream));
+  if (dtype == KL_F64) return p2m_bwd_sums<double>(P, F, grad, pts, fv, idx, type, gp, gf_sums, S(stream));
   set_error("unbatched_triangle_distance_backward_cuda not implemented for this dtype");
   return KL_E_INVALID;
 }

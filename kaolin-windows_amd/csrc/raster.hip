@@ -1262,6 +1262,225 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
   }
 }
 
+// ---------------------------------------------------------------- gather backward, v2
+// The per-face gather reorganised around what bounds it (r03 counters: ~600 VALU per wave of 8
+// faces, a third of it the 15-double butterfly; 126 VGPRs of double accumulators; each won pixel's
+// weights and grads loaded one after another, a memory round trip each):
+//  * 8 lanes per face as before (a wave = 8 faces; a wave whose faces cover no pixel writes their
+//    zero gradients and exits after one load);
+//  * a batch of 4 pixels per lane loads face_idx, weights and grads together (unconditional
+//    loads; a pixel's data is used only if the face won it): one memory round trip per batch
+//    instead of one for face_idx and one per won pixel;
+//  * every lane adds the reference's per-pixel float terms in double into its OWN LDS partials
+//    (value-major, so a wave's adds touch 64 consecutive doubles: no bank or address conflict);
+//    then each value's 8 partials are added in lane order and rounded once.  No accumulators in
+//    registers, no butterfly; the sum is the same on every run and equals the oracle's pixel-order
+//    sum whenever the float terms sum exactly in double (magnitudes within ~2^29, see GatherAcc).
+//    Measured dead ends (r04, cfg3, gather alone): one wave per 64 consecutive faces taking its
+//    active faces 8 at a time, 120-135 us against 57 -- waves over runs of front faces did 8
+//    rounds one after another and set the kernel's end; adding into one LDS slot per face
+//    (ds_add_f64 from the face's 8 lanes) serialised the lanes on each address.
+//  * faces covering more than VIS_SMALL_AREA pixel centres are summed by the first G2_BIG_BLOCKS
+//    workgroups of the same grid (a scan of the ranges, then the whole workgroup per face), so
+//    no second launch is needed when there are none.
+constexpr int G2_BIG_BLOCKS = 64;
+
+template <typename T, int MAXD, bool ATOM = false>
+__device__ __forceinline__ void g2_add(double *__restrict__ part, const T v[6], const T *__restrict__ c, int D, T wa,
+                                       T wb, T wc, const T *gv, float eps) {
+  // ATOM: ds_add_f64 into the lane's own partials -- 100 VGPRs at D = 3; a read-modify-write lets
+  // the compiler keep the partials in registers across the batch (173 VGPRs, 73 against 48 us)
+  if constexpr (ATOM) {
+    BaryGrad<T> bg;
+    bg.init(v, wa, wb, wc, eps);
+#pragma unroll
+    for (int d = 0; d < MAXD; d++) {
+      if (d < D) {
+        const T gd = gv[d];
+        atomicAdd(&part[(6 + d) * 64], (double)(gd * wa));
+        atomicAdd(&part[(6 + MAXD + d) * 64], (double)(gd * wb));
+        atomicAdd(&part[(6 + 2 * MAXD + d) * 64], (double)(gd * wc));
+        T o[6];
+        bg.terms(gd, c[d], c[D + d], c[2 * D + d], o);
+#pragma unroll
+        for (int q = 0; q < 6; q++) atomicAdd(&part[q * 64], (double)o[q]);
+      }
+    }
+    return;
+  }
+  // part: this thread's partials, value q at part[q * 64] (LDS no other thread touches until the sums)
+  BaryGrad<T> bg;
+  bg.init(v, wa, wb, wc, eps);
+#pragma unroll
+  for (int d = 0; d < MAXD; d++) {
+    if (d < D) {
+      const T gd = gv[d];
+      part[(6 + d) * 64] += (double)(gd * wa);
+      part[(6 + MAXD + d) * 64] += (double)(gd * wb);
+      part[(6 + 2 * MAXD + d) * 64] += (double)(gd * wc);
+      T o[6];
+      bg.terms(gd, c[d], c[D + d], c[2 * D + d], o);
+#pragma unroll
+      for (int q = 0; q < 6; q++) part[q * 64] += (double)o[q];
+    }
+  }
+}
+
+// value q of a face -> its gradient (q < 6: the vertex-coordinate gradient, + the soft mask's sum
+// rounded on its own; else a feature gradient)
+template <typename T, int MAXD>
+__device__ __forceinline__ void g2_store(int64_t tf, int q, double x, int D, const double *__restrict__ soft,
+                                         T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat) {
+  if (q < 6) {
+    grad_fvi[tf * 6 + q] = soft ? (T)x + (T)soft[tf * 6 + q] : (T)x;
+  } else {
+    const int r = q - 6, ii = r / MAXD, d = r % MAXD;
+    if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)x;
+  }
+}
+
+template <typename T, int MAXD, bool ATOM = false>
+__global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
+    const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
+    const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
+    const T *__restrict__ nz, int B, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
+    T *__restrict__ grad_ffeat, const uint2 *__restrict__ rng, const double *__restrict__ soft, int nbig) {
+  constexpr int NV = 6 + 3 * MAXD;
+  __shared__ double s_part[4][NV][64];  // per wave: per lane (thread) partial sums, value-major
+  __shared__ int s_nbig;
+  __shared__ int s_big[256];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t nf = (int64_t)B * F;
+  const RastSrc<T> src{fvi, valid, (T)m, nz};
+  auto range_of = [&](int64_t tf, int &ix0, int &ix1, int &iy0, int &iy1) -> bool {
+    return rng ? rng_range(rng, tf, ix0, ix1, iy0, iy1)
+               : (src.valid(tf) && face_range(src, tf, m, H, W, ix0, ix1, iy0, iy1));
+  };
+  double *part = &s_part[wid][0][lane];
+  if ((int)blockIdx.x < nbig) {
+    // ---- large faces: scan a slice of the faces, then one face at a time with the workgroup;
+    //      its 256 partials added in thread order
+#pragma unroll
+    for (int q = 0; q < NV; q++) part[q * 64] = 0.0;
+    const int64_t per = (nf + nbig - 1) / nbig;
+    const int64_t f0 = (int64_t)blockIdx.x * per, f1 = f0 + per < nf ? f0 + per : nf;
+    for (int64_t base = f0; base < f1; base += 256) {
+      if (threadIdx.x == 0) s_nbig = 0;
+      __syncthreads();
+      {
+        const int64_t tf = base + threadIdx.x;
+        int ix0, ix1, iy0, iy1;
+        if (tf < f1 && range_of(tf, ix0, ix1, iy0, iy1) &&
+            (int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) > VIS_SMALL_AREA)
+          s_big[atomicAdd(&s_nbig, 1)] = (int)threadIdx.x;
+      }
+      __syncthreads();
+      const int n = s_nbig;
+      for (int k = 0; k < n; k++) {
+        const int64_t bf = base + s_big[k];
+        const int b = (int)(bf / F);
+        const int64_t f = bf - (int64_t)b * F;
+        int ix0, ix1, iy0, iy1;
+        range_of(bf, ix0, ix1, iy0, iy1);
+        T v[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) v[q] = fvi[bf * 6 + q];
+        const T *c = feat + bf * 3 * D;
+        const int w = ix1 - ix0 + 1;
+        const int64_t area = (int64_t)w * (iy1 - iy0 + 1);
+        for (int64_t e = threadIdx.x; e < area; e += blockDim.x) {
+          const int64_t p = ((int64_t)b * H + iy0 + (int)(e / w)) * W + ix0 + (int)(e % w);
+          if (face_idx[p] != f) continue;
+          T gv[MAXD];
+#pragma unroll
+          for (int d = 0; d < MAXD; d++) gv[d] = d < D ? grad_feat[p * D + d] : (T)0;
+          g2_add<T, MAXD>(part, v, c, D, wts[p * 3 + 0], wts[p * 3 + 1], wts[p * 3 + 2], gv, eps);
+        }
+        __syncthreads();
+        if ((int)threadIdx.x < NV) {
+          const int q = threadIdx.x;
+          double x = 0.0;
+          for (int t = 0; t < 256; t++) x += s_part[t >> 6][q][t & 63];
+          g2_store<T, MAXD>(bf, q, x, D, soft, grad_fvi, grad_ffeat);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < NV; q++) part[q * 64] = 0.0;
+      }
+      __syncthreads();  // s_nbig / s_big are rewritten
+    }
+    return;
+  }
+  // ---- 8 lanes per face, a wave = 8 faces
+  const int s = lane & 7;
+  const int64_t tf = (((int64_t)(blockIdx.x - nbig) * 256 + threadIdx.x) >> 3);
+  const bool in = tf < nf;
+  int ix0 = 1, ix1 = 0, iy0 = 1, iy1 = 0;
+  const bool has = in && range_of(tf, ix0, ix1, iy0, iy1);
+  const bool act = has && (int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) <= VIS_SMALL_AREA;
+  if (in && !has) {  // no pixel: zero gradients (+ the soft mask's sums); lane s writes q = s, s + 8, ...
+#pragma unroll
+    for (int q = s; q < NV; q += 8) {
+      if (q < 6) {
+        grad_fvi[tf * 6 + q] = soft ? (T)0 + (T)soft[tf * 6 + q] : (T)0;
+      } else {
+        const int r = q - 6, ii = r / MAXD, d = r % MAXD;
+        if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)0;
+      }
+    }
+  }
+  if (!__any(act)) return;  // wave-uniform
+#pragma unroll
+  for (int q = 0; q < NV; q++) part[q * 64] = 0.0;
+  if (act) {
+    const int b = (int)(tf / F);
+    const int64_t f = tf - (int64_t)b * F;
+    T v[6];
+#pragma unroll
+    for (int q = 0; q < 6; q++) v[q] = fvi[tf * 6 + q];
+    const T *c = feat + tf * 3 * D;
+    const int64_t pbase = (int64_t)b * H * W;
+    const int64_t pfirst = pbase + (int64_t)iy0 * W + ix0;
+    RangeWalkN<8> rw(ix0, ix1, iy0, iy1, s);
+    while (rw.more()) {
+      // face_idx, weights and grads of GATHER_BATCH pixels in flight together (the range's first
+      // pixel stands in past the range's end)
+      int64_t fi[GATHER_BATCH];
+      T wv[GATHER_BATCH][3], gv[GATHER_BATCH][MAXD];
+      uint32_t inb = 0;
+#pragma unroll
+      for (int u = 0; u < GATHER_BATCH; u++) {
+        int64_t p = pfirst;
+        if (rw.more()) {
+          p = pbase + (int64_t)(iy0 + rw.row) * W + ix0 + rw.col;
+          inb |= 1u << u;
+        }
+        rw.next();
+        fi[u] = face_idx[p];
+#pragma unroll
+        for (int k = 0; k < 3; k++) wv[u][k] = wts[p * 3 + k];
+#pragma unroll
+        for (int d = 0; d < MAXD; d++) gv[u][d] = d < D ? grad_feat[p * D + d] : (T)0;
+      }
+#pragma unroll
+      for (int u = 0; u < GATHER_BATCH; u++)
+        if (((inb >> u) & 1u) && fi[u] == f) g2_add<T, MAXD, ATOM>(part, v, c, D, wv[u][0], wv[u][1], wv[u][2], gv[u], eps);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  if (act) {
+    // value q of the face: its 8 lanes' partials in lane order
+    const int g0 = lane & ~7;
+    for (int q = s; q < NV; q += 8) {
+      double x = 0.0;
+#pragma unroll
+      for (int l = 0; l < 8; l++) x += s_part[wid][q][g0 + l];
+      g2_store<T, MAXD>(tf, q, x, D, soft, grad_fvi, grad_ffeat);
+    }
+  }
+}
+
 // workspace of the scatter backward: the double accumulators of both gradients
 static size_t rast_scatter_ws_bytes(int B, int F, int D) {
   return al256((size_t)B * F * 6 * sizeof(double)) + al256((size_t)B * F * 3 * D * sizeof(double));
@@ -1295,8 +1514,21 @@ static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T 
                                      const T *w, const T *fvi, const T *feat, const uint8_t *valid, const T *nz,
                                      float m, float eps, T *gfvi, T *gfeat, int *big, int *nbig, bool zero_nbig,
                                      const uint2 *rng, const double *soft, hipStream_t st) {
-  if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   const int64_t nf = (int64_t)B * F;
+  if (g_dev_param[7] != 1) {  // dev param 7 = 1: the r03 gather (8 lanes per face, register sums) for A/B
+    const int nb = (int)std::min<int64_t>(G2_BIG_BLOCKS, cdiv(nf, 4096));
+    if (g_dev_param[8] != 1)  // dev param 8 = 1: read-modify-write partials (A/B: 73 against 48 us at cfg3)
+      hipLaunchKernelGGL((rasterize_bwd_gather2_kernel<T, MAXD, true>), dim3((unsigned)(nb + cdiv(nf * 8, 256))),
+                         dim3(256), 0, st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat,
+                         rng, soft, nb);
+    else
+      hipLaunchKernelGGL((rasterize_bwd_gather2_kernel<T, MAXD>), dim3((unsigned)(nb + cdiv(nf * 8, 256))), dim3(256),
+                         0, st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, rng, soft,
+                         nb);
+    KL_CHECK_LAUNCH();
+    return KL_OK;
+  }
+  if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   // 8 lanes per face (measured: 4 lanes 62.7 us, 8 lanes 58 us, 16 lanes 91 us at cfg3)
   hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st,
                      grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);

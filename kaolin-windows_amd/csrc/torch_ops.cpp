@@ -61,6 +61,11 @@ struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
     fvi = fvi.contiguous();
     feat = feat.contiguous();
     fnz = fnz.detach().contiguous();
+    // one dtype for every float input: the kernels read all of them as fvi's type
+    TORCH_CHECK(fvz.scalar_type() == fvi.scalar_type() && feat.scalar_type() == fvi.scalar_type() &&
+                    fnz.scalar_type() == fvi.scalar_type(),
+                "dibr_rasterization: face_vertices_z, face_vertices_image, face_features and face_normals_z must "
+                "share one dtype");
     const int64_t B = fvz.size(0), F = fvz.size(1), D = feat.size(-1);
     const int H = (int)height, W = (int)width, K = (int)knum;
     const auto opt = fvi.options();

@@ -43,6 +43,9 @@ def rasterize_forward(height, width, face_vertices_z, face_vertices_image, face_
     dtype = face_vertices_z.dtype
     if dtype not in (torch.float32, torch.float64):
         raise RuntimeError(f'"{func}" not implemented for {dtype}')
+    for name, t in (('face_vertices_image', face_vertices_image), ('face_features', face_features)):
+        if t.dtype != dtype:  # the reference's data_ptr<scalar_t>() check (rasterization_cuda.cu)
+            raise RuntimeError(f'{func}: expected {name} of dtype {dtype} (face_vertices_z), found {t.dtype}')
     fvz = face_vertices_z.contiguous()
     fvi = face_vertices_image.contiguous()
     feat = face_features.contiguous()
@@ -238,8 +241,12 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     D = face_features.shape[-1]
     dev = face_vertices_z.device
     dtype = face_vertices_z.dtype
-    if dtype not in (torch.float32, torch.float64) or face_normals_z.dtype != dtype:
-        raise RuntimeError(f'"{func}" fused forward needs f32/f64 inputs of one dtype')
+    if dtype not in (torch.float32, torch.float64):
+        raise RuntimeError(f'"{func}" not implemented for {dtype}')
+    for name, t in (('face_vertices_image', face_vertices_image), ('face_features', face_features),
+                    ('face_normals_z', face_normals_z)):
+        if t.dtype != dtype:  # the reference's data_ptr<scalar_t>() check (rasterization_cuda.cu)
+            raise RuntimeError(f'{func}: expected {name} of dtype {dtype} (face_vertices_z), found {t.dtype}')
     H, W, K = int(height), int(width), int(knum)
     fvz = face_vertices_z.contiguous()
     fvi = face_vertices_image.contiguous()

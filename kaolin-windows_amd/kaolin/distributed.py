@@ -2,21 +2,35 @@
 
 Kaolin itself is single-device; these helpers are what a data-parallel caller of its ops
 runs on every rank.  Nothing here changes an op's arithmetic: a shard's outputs are the
-unsharded op's outputs for those rows, bit for bit.
+unsharded op's outputs for those rows, bit for bit, and every gathered result equals the
+unsharded op's result bit for bit.
 
 * DIB-R: views are independent, so a rank renders a contiguous slice of them
   (``shard_bounds`` over the view count) with the mesh replicated; the caller gathers
-  per-shard losses (``gather_losses``).
+  per-shard losses (``gather_losses``).  In a training loop over a shared mesh (the reference's
+  dibr_tutorial.ipynb cell 14: one ``vertices`` / ``shift`` / texture, Adam) each rank's backward
+  gives the gradient of its views; ``allreduce_grads`` sums (or averages) the parameters'
+  gradients over the ranks in one flat bucket before the optimiser step.
 * point_to_mesh_distance on one large cloud: the points are split contiguously over the
-  ranks (``shard_bounds``), the faces are replicated.  ``sharded_point_to_mesh_distance``
-  evaluates the rank's points and all-gathers (dist, face_idx, dist_type) so every rank
-  holds the whole result.  In the backward the rank's points get their gradient locally
-  and the face gradient, a sum over all points, is all-reduced.
+  ranks, the faces replicated.  ``sharded_point_to_mesh_distance`` evaluates the rank's points
+  and all-gathers (dist, face_idx, dist_type).  In the backward each rank's points get their
+  gradient locally; the face gradient, a sum over all points, is all-reduced as the per-rank
+  DOUBLE sums of the per-point float terms and rounded once (GPU), which is the unsharded
+  backward's gradient bit for bit.
+* unbatched_raytrace (reference render/spc/raytrace.py:31-84): the rays are split contiguously,
+  the octree replicated; each rank marches its rays, offsets its ray indices by its first ray
+  and the nuggets are all-gathered with their per-rank counts (all-gather-v).  The reference's
+  output is ray-major, so the rank-order concatenation is the unsharded output.
+* trianglemeshes_to_voxelgrids (reference ops/conversions/trianglemesh.py:29-110): a batch is
+  split by mesh (grids all-gathered); one mesh (or fewer meshes than ranks) is split by face
+  and the per-rank grids are max-reduced -- the voxel set is a union over faces (every rank
+  also marks the vertices), so the OR of the shards is the unsharded grid.
 """
 import torch
 import torch.distributed as dist
 
-__all__ = ['shard_bounds', 'gather_losses', 'sharded_point_to_mesh_distance']
+__all__ = ['shard_bounds', 'gather_losses', 'allreduce_grads', 'sharded_point_to_mesh_distance',
+           'sharded_unbatched_raytrace', 'sharded_trianglemeshes_to_voxelgrids']
 
 
 def shard_bounds(n, rank, world):
@@ -31,26 +45,110 @@ def _world(group):
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
+def _rank(group):
+    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+
+
+def _staged(t, group):
+    """gloo has no all_gather for device tensors: such collectives go through host copies."""
+    return t.is_cuda and dist.get_backend(group) == 'gloo'
+
+
+def _all_gather(outs, t, group):
+    if _staged(t, group):
+        host = [torch.empty(o.shape, dtype=o.dtype) for o in outs]
+        dist.all_gather(host, t.cpu(), group=group)
+        for o, h in zip(outs, host):
+            o.copy_(h)
+    else:
+        dist.all_gather(outs, t, group=group)
+
+
+def _all_reduce(t, op, group):
+    if _staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
 def gather_losses(loss, group=None):
     """All-gather one scalar loss per rank -> (world,) in rank order."""
     world = _world(group)
     if world == 1:
         return loss.detach().reshape(1)
     out = [torch.empty_like(loss) for _ in range(world)]
-    dist.all_gather(out, loss.detach(), group=group)
+    _all_gather(out, loss.detach(), group)
     return torch.stack(out)
+
+
+def allreduce_grads(params, group=None, average=False):
+    """Sum (``average``: mean) the ``.grad`` of ``params`` over the ranks, in place: the shared
+    mesh's data-parallel step (each rank rendered its views; the unsharded gradient is the sum
+    over all views).  One flat bucket, one all_reduce per dtype/device (the tutorial's vertices,
+    shift and texture: ~0.3 MB + 3 MB at cfg3).  Parameters without a gradient on this rank
+    contribute zeros.  The per-rank gradients are rounded before the sum, so the result equals
+    the unsharded gradient up to float summation order (the exact variant needs the ops' double
+    sums, as sharded_point_to_mesh_distance does)."""
+    world = _world(group)
+    params = [p for p in params if p.requires_grad]
+    if world == 1 or not params:
+        return
+    buckets = {}
+    for p in params:
+        buckets.setdefault((p.dtype, p.device), []).append(p)
+    for ps in buckets.values():
+        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps])
+        _all_reduce(flat, dist.ReduceOp.SUM, group)
+        if average:
+            flat /= world
+        off = 0
+        for p in ps:
+            n = p.numel()
+            g = flat[off:off + n].view_as(p)
+            if p.grad is None:
+                p.grad = g.clone()
+            else:
+                p.grad.copy_(g)
+            off += n
+
+
+def _sizes(n, device, group):
+    """every rank's row count, in rank order"""
+    world = _world(group)
+    t = torch.tensor([n], dtype=torch.int64, device=device)
+    ns = [torch.empty_like(t) for _ in range(world)]
+    _all_gather(ns, t, group)
+    return [int(x) for x in ns]
 
 
 def _all_gather_rows(t, sizes, group):
     """Concatenate every rank's (n_r, ...) tensor in rank order (rows padded to the
-    largest share for the collective, then trimmed)."""
+    largest share for the collective, then trimmed): all-gather-v."""
     world = len(sizes)
     m = max(sizes)
+    if m == 0:
+        return t[:0]
     if t.shape[0] < m:
         t = torch.cat([t, t.new_zeros((m - t.shape[0],) + tuple(t.shape[1:]))])
     bufs = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(bufs, t.contiguous(), group=group)
+    _all_gather(bufs, t.contiguous(), group)
     return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+
+
+def _p2m_face_sums(g_local, lp, fv, i, t):
+    """(grad_points, the face gradient's double sums) of the rank's points (GPU, distance.hip)."""
+    from . import _native as N
+    P, F = lp.shape[0], fv.shape[0]
+    gp = torch.empty_like(lp)
+    sums = torch.empty((F, 3, 3), dtype=torch.float64, device=lp.device)
+    with N.on_device(lp.device):
+        N.check(N.lib().kl_unbatched_triangle_distance_backward_sums(
+            N.dtype_code(lp.dtype), P, F, N.ptr(g_local.contiguous()), N.ptr(lp.contiguous()),
+            N.ptr(fv.contiguous()), N.ptr(i.contiguous()), N.ptr(t.contiguous()), N.ptr(gp), N.ptr(sums),
+            N.stream_of(lp.device)), 'sharded_point_to_mesh_distance backward')
+    return gp, sums
 
 
 class _ShardedP2M(torch.autograd.Function):
@@ -58,30 +156,46 @@ class _ShardedP2M(torch.autograd.Function):
     @staticmethod
     def forward(ctx, local_points, face_vertices, sizes, group):
         from .metrics.trianglemesh import point_to_mesh_distance
-        with torch.enable_grad():
-            lp = local_points.detach().requires_grad_(local_points.requires_grad)
-            fv = face_vertices.detach().requires_grad_(face_vertices.requires_grad)
-            d, i, t = point_to_mesh_distance(lp.unsqueeze(0), fv.unsqueeze(0))
-        ctx.local = (lp, fv, d)  # the shard's own graph, replayed by backward
         ctx.sizes, ctx.group = sizes, group
+        ctx.exact = local_points.is_cuda and local_points.dtype in (torch.float32, torch.float64)
+        if ctx.exact:
+            # forward outputs only; the backward's face sums come from the double-sum entry point
+            with torch.no_grad():
+                d, i, t = point_to_mesh_distance(local_points.unsqueeze(0), face_vertices.unsqueeze(0))
+            ctx.save_for_backward(local_points, face_vertices, i[0], t[0])
+        else:
+            with torch.enable_grad():
+                lp = local_points.detach().requires_grad_(local_points.requires_grad)
+                fv = face_vertices.detach().requires_grad_(face_vertices.requires_grad)
+                d, i, t = point_to_mesh_distance(lp.unsqueeze(0), fv.unsqueeze(0))
+            ctx.local = (lp, fv, d)  # the shard's own graph, replayed by backward
         out_i, out_t = _all_gather_rows(i[0], sizes, group), _all_gather_rows(t[0], sizes, group)
         ctx.mark_non_differentiable(out_i, out_t)
         return _all_gather_rows(d[0].detach(), sizes, group), out_i, out_t
 
     @staticmethod
     def backward(ctx, g_dist, g_idx, g_type):
-        lp, fv, d = ctx.local
         rank = dist.get_rank(ctx.group)
         lo = sum(ctx.sizes[:rank])
-        g_local = g_dist[lo:lo + ctx.sizes[rank]].reshape(1, -1).contiguous()
+        g_local = g_dist[lo:lo + ctx.sizes[rank]]
+        if ctx.exact:
+            lp, fv, i, t = ctx.saved_tensors
+            gp, sums = _p2m_face_sums(g_local, lp, fv, i, t)
+            g_fv = None
+            if ctx.needs_input_grad[1]:
+                _all_reduce(sums, dist.ReduceOp.SUM, ctx.group)  # exact: f32 terms sum exactly in double
+                g_fv = sums.to(fv.dtype)                         # rounded once, as the unsharded backward
+            return (gp if ctx.needs_input_grad[0] else None), g_fv, None, None
+        lp, fv, d = ctx.local
         inputs = [x for x in (lp, fv) if x.requires_grad]
-        grads = torch.autograd.grad(d, inputs, g_local, allow_unused=True) if inputs else []
+        grads = torch.autograd.grad(d, inputs, g_local.reshape(1, -1).contiguous(), allow_unused=True) \
+            if inputs else []
         it = iter(grads)
         g_lp = next(it) if lp.requires_grad else None
         g_fv = next(it) if fv.requires_grad else None
         if g_fv is not None:
             g_fv = g_fv.contiguous()
-            dist.all_reduce(g_fv, op=dist.ReduceOp.SUM, group=ctx.group)
+            _all_reduce(g_fv, dist.ReduceOp.SUM, ctx.group)
         return g_lp, g_fv, None, None
 
 
@@ -93,15 +207,72 @@ def sharded_point_to_mesh_distance(local_points, face_vertices, group=None):
     rows of the cloud); ``face_vertices`` is the same on every rank.  Returns the whole
     cloud's (dist (P), face_idx (P) int64, dist_type (P) int32) on every rank.  Gradients:
     ``local_points`` gets the rows of its share; ``face_vertices`` gets the sum over every
-    rank's points (an all_reduce), i.e. the unsharded gradient.
+    rank's points.  On the GPU that sum is formed from the ranks' double sums of the per-point
+    float terms and rounded once: the unsharded gradient bit for bit.  On the CPU (the
+    reference's torch path, whose autograd sums in float) the ranks' float gradients are added:
+    equal to the unsharded gradient up to float summation order.
     """
     world = _world(group)
     if world == 1:
         from .metrics.trianglemesh import point_to_mesh_distance
         d, i, t = point_to_mesh_distance(local_points.unsqueeze(0), face_vertices.unsqueeze(0))
         return d[0], i[0], t[0]
-    n = torch.tensor([local_points.shape[0]], dtype=torch.int64, device=local_points.device)
-    ns = [torch.empty_like(n) for _ in range(world)]
-    dist.all_gather(ns, n, group=group)
-    sizes = [int(x) for x in ns]
+    sizes = _sizes(local_points.shape[0], local_points.device, group)
     return _ShardedP2M.apply(local_points, face_vertices, sizes, group)
+
+
+def sharded_unbatched_raytrace(octree, point_hierarchy, pyramid, exsum, origin, direction, level,
+                               return_depth=True, with_exit=False, group=None):
+    r"""unbatched_raytrace with the rays split contiguously over the ranks of ``group``.
+
+    Every argument is the unsharded call's (the rays replicated on every rank; the rank marches
+    rows ``shard_bounds(N, rank, world)`` of them).  Returns the unsharded call's outputs on every
+    rank: ray_index (offset by each shard's first ray), point_index and the depths, all-gathered
+    with the per-rank nugget counts -- the reference's ray-major order is the rank order."""
+    from .render.spc.raytrace import unbatched_raytrace
+    world, rank = _world(group), _rank(group)
+    lo, hi = shard_bounds(origin.shape[0], rank, world)
+    out = unbatched_raytrace(octree, point_hierarchy, pyramid, exsum, origin[lo:hi], direction[lo:hi], level,
+                             return_depth=return_depth, with_exit=with_exit)
+    if world == 1:
+        return out
+    ridx = out[0] + lo
+    sizes = _sizes(ridx.shape[0], ridx.device, group)
+    nug = _all_gather_rows(torch.stack([ridx, out[1].to(ridx.dtype)], -1), sizes, group)
+    res = (nug[:, 0].contiguous(), nug[:, 1].contiguous().to(out[1].dtype))
+    if return_depth:
+        res = res + (_all_gather_rows(out[2].contiguous(), sizes, group),)
+    return res
+
+
+def sharded_trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin=None, scale=None, split='auto',
+                                         group=None):
+    r"""trianglemeshes_to_voxelgrids (dense grids) over the ranks of ``group``; every argument is
+    the unsharded call's, replicated.  ``split``: 'batch' (each rank converts a contiguous share of
+    the meshes; the grids are all-gathered), 'faces' (each rank converts every mesh with a
+    contiguous share of the faces; the grids are max-reduced), or 'auto' ('batch' when there are
+    at least as many meshes as ranks).  The default origin / scale are the whole mesh's (computed
+    before splitting, so every shard normalises the same way).  Returns the unsharded (B,R,R,R)
+    grid on every rank."""
+    from .ops.conversions.trianglemesh import trianglemeshes_to_voxelgrids
+    world, rank = _world(group), _rank(group)
+    if world == 1:
+        return trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin, scale)
+    if origin is None:
+        origin = torch.min(vertices, dim=1)[0]
+    if scale is None:
+        scale = torch.max(torch.max(vertices, dim=1)[0] - origin, dim=1)[0]
+    B = vertices.shape[0]
+    if split == 'auto':
+        split = 'batch' if B >= world else 'faces'
+    if split == 'batch':
+        lo, hi = shard_bounds(B, rank, world)
+        grid = trianglemeshes_to_voxelgrids(vertices[lo:hi], faces, resolution, origin[lo:hi], scale[lo:hi])
+        return _all_gather_rows(grid, [b - a for a, b in (shard_bounds(B, r, world) for r in range(world))], group)
+    if split != 'faces':
+        raise ValueError(f"split must be 'auto', 'batch' or 'faces', got {split!r}")
+    lo, hi = shard_bounds(faces.shape[0], rank, world)
+    grid = trianglemeshes_to_voxelgrids(vertices, faces[lo:hi], resolution, origin, scale)
+    red = grid if grid.dtype.is_floating_point else grid.to(torch.uint8)
+    _all_reduce(red, dist.ReduceOp.MAX, group)
+    return red if red is grid else red.to(grid.dtype)

@@ -130,6 +130,8 @@ def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face
         dev = face_vertices_image.device
         if (ext is not None and N._TIMER is None and face_vertices_image.is_cuda
                 and face_normals_z.dtype == face_vertices_image.dtype
+                and face_vertices_z.dtype == face_vertices_image.dtype
+                and _face_features.dtype == face_vertices_image.dtype
                 and all(t.device == dev for t in (face_vertices_z, _face_features, face_normals_z))
                 and dev.index == torch.cuda.current_device()):
             # the same node compiled (csrc/torch_ops.cpp): the eager host path without Python in

@@ -118,3 +118,117 @@ def test_shard_bounds_cover_in_order():
             assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
             sizes = [hi - lo for lo, hi in spans]
             assert max(sizes) - min(sizes) <= 1
+
+
+# ------------------------------------------------------------------ raytrace / voxelgrid / grads sharding
+def _spc_fixture(level=4, npts=300, nrays=97, seed=3):
+    """A small SPC (oracle-built octree, pyramid, exsum, point hierarchy) and rays at it."""
+    import numpy as np
+    from oracle import oracle as orc
+    rs = np.random.RandomState(seed)
+    pts = np.unique(rs.randint(0, 2 ** level, size=(npts, 3)), axis=0)
+    mort = np.unique(orc.to_morton(pts))
+    octree = orc.morton_to_octree(mort, level)
+    _, pyramid, exsum = orc.scan_octrees(octree, np.array([octree.shape[0]], np.int32))
+    ph = orc.generate_points(octree, pyramid, exsum)
+    o = rs.normal(size=(nrays, 3))
+    o = 3.0 * o / np.linalg.norm(o, axis=1, keepdims=True)
+    d = -o + 0.6 * rs.normal(size=(nrays, 3))
+    d = d / np.linalg.norm(d, axis=1, keepdims=True)
+    t = torch.from_numpy
+    return (t(octree), t(ph), t(np.ascontiguousarray(pyramid[0])), t(exsum), t(o.astype(np.float32)),
+            t(d.astype(np.float32)), level)
+
+
+def _oracle_raytrace(octree, ph, pyramid, exsum, origin, direction, level, return_depth=True, with_exit=False):
+    """unbatched_raytrace's contract on CPU tensors, computed by the oracle (test stand-in for the
+    GPU op: the reference's raytrace is CUDA-only)."""
+    from oracle import oracle as orc
+    r = orc.raytrace(octree.numpy(), ph.numpy(), pyramid.numpy(), exsum.numpy(), origin.numpy(),
+                     direction.numpy(), level, return_depth, with_exit)
+    nug = torch.from_numpy(r[0])
+    out = (nug[:, 0].contiguous(), nug[:, 1].contiguous())
+    return out + (torch.from_numpy(r[1]),) if return_depth else out
+
+
+def _shard_ops_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import kaolin
+        import kaolin.render.spc.raytrace as rt
+        from kaolin import distributed as kd
+        rt.unbatched_raytrace = _oracle_raytrace
+        fx = _spc_fixture()
+        res = {}
+        for with_exit in (False, True):
+            res[f'ray{int(with_exit)}'] = [x.clone() for x in kd.sharded_unbatched_raytrace(*fx, with_exit=with_exit)]
+        res['ray_nodepth'] = [x.clone() for x in kd.sharded_unbatched_raytrace(*fx, return_depth=False)]
+        # voxelgrids: 3 meshes split by mesh ('auto' at world 2/3), one mesh split by face
+        g = torch.Generator().manual_seed(7)
+        verts = torch.rand((3, 40, 3), generator=g)
+        faces = torch.randint(0, 40, (37, 3), generator=g)
+        res['vox_batch'] = kd.sharded_trianglemeshes_to_voxelgrids(verts, faces, 16)
+        res['vox_faces'] = kd.sharded_trianglemeshes_to_voxelgrids(verts[:1], faces, 16)
+        res['vox_faces3'] = kd.sharded_trianglemeshes_to_voxelgrids(verts, faces, 16, split='faces')
+        # data-parallel gradients of a shared mesh
+        a = torch.zeros(5, requires_grad=True)
+        b = torch.zeros((2, 3), requires_grad=True)
+        a.grad = torch.arange(5.) * (rank + 1)
+        b.grad = torch.full((2, 3), float(rank))
+        c = torch.zeros(3, requires_grad=True)  # no gradient on rank 0
+        if rank:
+            c.grad = torch.ones(3)
+        kd.allreduce_grads([a, b, c])
+        res['grads_sum'] = (a.grad.clone(), b.grad.clone(), c.grad.clone())
+        kd.allreduce_grads([a], average=True)
+        res['grads_avg'] = a.grad.clone()
+        # by value: a tensor sent through the queue is shared memory the exiting worker may release
+        import numpy as np
+        conv = lambda x: [np.array(t) for t in x] if isinstance(x, (list, tuple)) else np.array(x)  # noqa
+        q.put((rank, {k: conv(v) for k, v in res.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_sharded_raytrace_voxelgrid_grads(world):
+    """sharded_unbatched_raytrace (rays split, nuggets all-gathered with ray offsets),
+    sharded_trianglemeshes_to_voxelgrids (mesh split; face split + max-reduce) and allreduce_grads
+    over gloo world 2 / 3: every rank holds the unsharded result, bit for bit."""
+    import kaolin
+    from kaolin.ops.conversions import trianglemeshes_to_voxelgrids
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_ops_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    fx = _spc_fixture()
+    want = {f'ray{int(e)}': _oracle_raytrace(*fx, with_exit=e) for e in (False, True)}
+    want['ray_nodepth'] = _oracle_raytrace(*fx, return_depth=False)
+    assert want['ray0'][0].numel() > 50  # the rays hit the octree
+    g = torch.Generator().manual_seed(7)
+    verts = torch.rand((3, 40, 3), generator=g)
+    faces = torch.randint(0, 40, (37, 3), generator=g)
+    full = trianglemeshes_to_voxelgrids(verts, faces, 16)
+    for rank in range(world):
+        r = {k: [torch.from_numpy(t) for t in v] if isinstance(v, list) else torch.from_numpy(v)
+             for k, v in res[rank].items()}
+        for k in ('ray0', 'ray1', 'ray_nodepth'):
+            assert len(r[k]) == len(want[k])
+            for x, y in zip(r[k], want[k]):
+                assert x.dtype == y.dtype and torch.equal(x, y), (rank, k)
+        assert torch.equal(r['vox_batch'], full)
+        assert torch.equal(r['vox_faces'], full[:1])
+        assert torch.equal(r['vox_faces3'], full)
+        a, b, c = r['grads_sum']
+        tot = sum(range(1, world + 1))
+        assert torch.equal(a, torch.arange(5.) * tot)
+        assert torch.equal(b, torch.full((2, 3), float(sum(range(world)))))
+        assert torch.equal(c, torch.full((3,), float(world - 1)))
+        assert torch.allclose(r['grads_avg'], torch.arange(5.) * tot, rtol=0, atol=1e-6)  # average of equal sums

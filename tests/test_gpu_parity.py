@@ -559,6 +559,29 @@ def test_compiled_node_equals_python_node(kal, monkeypatch):
         assert torch.equal(x, y)
 
 
+def test_dibr_mixed_dtypes_raise(kal, monkeypatch):
+    """A float input of another dtype than face_vertices_image raises (the reference's
+    data_ptr<scalar_t>() check) on the compiled node and on the Python node alike -- it is
+    never read as the wrong type."""
+    from kaolin import _ext
+    import bench
+    inp = bench.dibr_inputs([0.3], DEV, H=32, W=48)
+    fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+    for use_ext in (True, False):
+        if not use_ext:
+            monkeypatch.setattr(_ext, '_mod', None)
+        for args in ((fvz, fvi, feat.double(), fnz), (fvz.double(), fvi, feat, fnz),
+                     (fvz, fvi, [feat[..., :2].double(), feat[..., 2:].double()], fnz)):
+            with pytest.raises(RuntimeError):
+                kal.render.mesh.dibr_rasterization(32, 48, *args)
+        # and on the direct compiled entry point, past the front-end's routing
+        if use_ext and _ext.get() is not None:
+            from kaolin import _native as N
+            with pytest.raises(RuntimeError):
+                _ext.get().dibr_rasterization(32, 48, fvz, fvi, feat.double(), fnz, 7000., 0.02, 30, 1000., 1e-8,
+                                              N.stream_of(fvi.device))
+
+
 def test_dibr_bench_full_size_fused_equals_C_chain(kal):
     """cfg3 at full size (4 views, 512^2, 50k faces): the fused single-node path's
     outputs equal the reference-contract chain (packed _C rasterizer + _C soft mask)
