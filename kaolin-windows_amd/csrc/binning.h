@@ -4,9 +4,12 @@
 // dibr_soft_mask_cuda.cu:80-172).  Both walks depend on face ORDER (max-z with lowest
 // index on ties; first `knum` hits in index order), so bins must preserve it.  Here a
 // bin is a bitmap over 64-face chunks (chunk c = faces [64c, 64c+64) of one mesh):
-//   bitmap[b][tile][c/32] bit c%32  set  <=>  some face of chunk c may touch the tile.
+//   word c/32 of (mesh b, tile), bit c%32  set  <=>  some face of chunk c may touch the tile.
 // Consumers iterate set chunks in ascending order and, inside a chunk, faces in lane
 // order, so the walk order is exactly the reference's, restricted to candidate faces.
+// Layout: word-major, word w of tile t (tiles of all meshes numbered b * tiles_y * tiles_x + ...)
+// at bitmap[w * ntiles + t] (bm_index): the order kernels count a tile per lane with coalesced
+// loads; a tile walk reads its <= 32 words once per work item.
 // Bit setting is an idempotent atomicOr, so bins are deterministic.
 //
 // Tiles are TILE_W x TILE_H pixels (one wave = one 64-pixel row segment).
@@ -31,8 +34,10 @@ struct BinGeom {
   int tiles_x, tiles_y;
   int chunks;          // chunks per mesh (upper bound)
   int words;           // uint32 words per tile
-  size_t bytes() const { return (size_t)batch * tiles_x * tiles_y * words * sizeof(uint32_t); }
+  __host__ __device__ size_t ntiles() const { return (size_t)batch * tiles_x * tiles_y; }
+  size_t bytes() const { return ntiles() * words * sizeof(uint32_t); }
 };
+__host__ __device__ inline size_t bm_index(size_t ntiles, size_t tile, int word) { return (size_t)word * ntiles + tile; }
 
 inline BinGeom make_bin_geom(int batch, int height, int width, int64_t max_faces_per_mesh) {
   BinGeom g;
@@ -195,7 +200,7 @@ __device__ __forceinline__ void bin_mark(const BinGeom &g, int b, int c, int lan
       const int e = q * 64 + lane;
       if (e < area && wf[e]) {
         const int ty = uy0 + e / uw, tx = ux0 + e % uw;
-        atomicOr(&bitmap[(tile_base + (size_t)ty * g.tiles_x + tx) * g.words + (c >> 5)], bit);
+        atomicOr(&bitmap[bm_index(g.ntiles(), tile_base + (size_t)ty * g.tiles_x + tx, c >> 5)], bit);
       }
     }
     __builtin_amdgcn_wave_barrier();  // wf is reused by the wave's next call
@@ -203,7 +208,7 @@ __device__ __forceinline__ void bin_mark(const BinGeom &g, int b, int c, int lan
   } else if (has) {
     for (int ty = ty0; ty <= ty1; ty++)
       for (int tx = tx0; tx <= tx1; tx++)
-        atomicOr(&bitmap[(tile_base + (size_t)ty * g.tiles_x + tx) * g.words + (c >> 5)], bit);
+        atomicOr(&bitmap[bm_index(g.ntiles(), tile_base + (size_t)ty * g.tiles_x + tx, c >> 5)], bit);
   }
 }
 

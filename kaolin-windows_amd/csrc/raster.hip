@@ -544,7 +544,7 @@ __global__ void __launch_bounds__(BIN_WORD_THREADS) raster_bin_word_kernel(
   const int word = grp >> 2, byte = grp & 3;  // little-endian: chunk bits 8 byte .. 8 byte + 7
   uint8_t *rb = reinterpret_cast<uint8_t *>(bitmap), *sb = reinterpret_cast<uint8_t *>(sbitmap);
   for (int t = threadIdx.x; t < ntv; t += blockDim.x) {
-    const size_t o = ((base + t) * g.words + word) * 4 + byte;
+    const size_t o = bm_index(g.ntiles(), base + t, word) * 4 + byte;
     rb[o] = (uint8_t)sr[t];
     if (soft) sb[o] = (uint8_t)ss[t];
   }
@@ -609,7 +609,7 @@ __global__ void __launch_bounds__(512) raster_tile_kernel(RastTileArgs<T> a) {
   const int part = (item >> 24) & 15;
   const int lg = (item >> 28) & 7;
   ChunkSeq seq;
-  seq.init(a.bitmap + (size_t)tile * g.words, g.words, lane);
+  seq.init(a.bitmap + tile, g.words, g.ntiles(), lane);
   const int RG = R >> lg;     // rows of the workgroup
   const int WPR = 1 << lg;    // waves per row
   __shared__ uint32_t L_face[RT_CAP];
@@ -1328,11 +1328,19 @@ __device__ __forceinline__ void g2_add(double *__restrict__ part, const T v[6], 
 
 // value q of a face -> its gradient (q < 6: the vertex-coordinate gradient, + the soft mask's sum
 // rounded on its own; else a feature gradient)
+// The soft sums are zeroed again as they are read (only the non-zero ones are written), so the
+// forward's accumulator is zero after every backward: a retained second backward adds into zeros.
+__device__ __forceinline__ double take_soft(double *__restrict__ soft, int64_t i) {
+  const double v = soft[i];
+  if (__double_as_longlong(v) != 0) soft[i] = 0.0;
+  return v;
+}
+
 template <typename T, int MAXD>
-__device__ __forceinline__ void g2_store(int64_t tf, int q, double x, int D, const double *__restrict__ soft,
+__device__ __forceinline__ void g2_store(int64_t tf, int q, double x, int D, double *__restrict__ soft,
                                          T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat) {
   if (q < 6) {
-    grad_fvi[tf * 6 + q] = soft ? (T)x + (T)soft[tf * 6 + q] : (T)x;
+    grad_fvi[tf * 6 + q] = soft ? (T)x + (T)take_soft(soft, tf * 6 + q) : (T)x;
   } else {
     const int r = q - 6, ii = r / MAXD, d = r % MAXD;
     if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)x;
@@ -1344,7 +1352,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
     const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
     const T *__restrict__ nz, int B, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
-    T *__restrict__ grad_ffeat, const uint2 *__restrict__ rng, const double *__restrict__ soft, int nbig) {
+    T *__restrict__ grad_ffeat, const uint2 *__restrict__ rng, double *__restrict__ soft, int nbig) {
   constexpr int NV = 6 + 3 * MAXD;
   __shared__ double s_part[4][NV][64];  // per wave: per lane (thread) partial sums, value-major
   __shared__ int s_nbig;
@@ -1422,7 +1430,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
 #pragma unroll
     for (int q = s; q < NV; q += 8) {
       if (q < 6) {
-        grad_fvi[tf * 6 + q] = soft ? (T)0 + (T)soft[tf * 6 + q] : (T)0;
+        grad_fvi[tf * 6 + q] = soft ? (T)0 + (T)take_soft(soft, tf * 6 + q) : (T)0;
       } else {
         const int r = q - 6, ii = r / MAXD, d = r % MAXD;
         if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)0;
@@ -1462,9 +1470,32 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
 #pragma unroll
         for (int d = 0; d < MAXD; d++) gv[u][d] = d < D ? grad_feat[p * D + d] : (T)0;
       }
+      uint32_t hm = 0;
 #pragma unroll
       for (int u = 0; u < GATHER_BATCH; u++)
-        if (((inb >> u) & 1u) && fi[u] == f) g2_add<T, MAXD, ATOM>(part, v, c, D, wv[u][0], wv[u][1], wv[u][2], gv[u], eps);
+        if (((inb >> u) & 1u) && fi[u] == f) hm |= 1u << u;
+      // the lane's won pixels one per iteration (the wave runs max-over-lanes iterations, not one
+      // per batch slot): each iteration selects its pixel's values from the batch registers
+      while (__any(hm != 0)) {
+        if (hm) {
+          const int u = __builtin_ctz(hm);
+          hm &= hm - 1;
+          T a0 = wv[0][0], a1 = wv[0][1], a2 = wv[0][2], g[MAXD];
+#pragma unroll
+          for (int d = 0; d < MAXD; d++) g[d] = gv[0][d];
+#pragma unroll
+          for (int k = 1; k < GATHER_BATCH; k++) {
+            if (u == k) {
+              a0 = wv[k][0];
+              a1 = wv[k][1];
+              a2 = wv[k][2];
+#pragma unroll
+              for (int d = 0; d < MAXD; d++) g[d] = gv[k][d];
+            }
+          }
+          g2_add<T, MAXD, ATOM>(part, v, c, D, a0, a1, a2, g, eps);
+        }
+      }
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -1513,7 +1544,7 @@ template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
                                      const T *w, const T *fvi, const T *feat, const uint8_t *valid, const T *nz,
                                      float m, float eps, T *gfvi, T *gfeat, int *big, int *nbig, bool zero_nbig,
-                                     const uint2 *rng, const double *soft, hipStream_t st) {
+                                     const uint2 *rng, double *soft, hipStream_t st) {
   const int64_t nf = (int64_t)B * F;
   if (g_dev_param[7] != 1) {  // dev param 7 = 1: the r03 gather (8 lanes per face, register sums) for A/B
     const int nb = (int)std::min<int64_t>(G2_BIG_BLOCKS, cdiv(nf, 4096));
@@ -1547,7 +1578,7 @@ template <typename T>
 static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
                                 const void *w, const void *fvi, const void *feat, const uint8_t *valid, const T *nz,
                                 float m, float eps, void *gfvi, void *gfeat, void *ws, size_t ws_bytes, int *nbig,
-                                hipStream_t st, const uint2 *rng = nullptr, const double *soft = nullptr) {
+                                hipStream_t st, const uint2 *rng = nullptr, double *soft = nullptr) {
   const int64_t nf = (int64_t)B * F;
   if (nf == 0) return KL_OK;
   if (D > 8) {  // wide features: the scatter kernel
@@ -1738,13 +1769,21 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   KL_REQUIRE(H < 65536 && W < 65536, "dibr_rasterization forward: height and width must be < 65536");
   KL_REQUIRE(K >= 0 && K <= 255, "dibr_rasterization forward: the compact soft mask needs 0 <= knum <= 255");
   KL_REQUIRE(F < (1 << 28), "dibr_rasterization forward: too many faces");
+  KL_REQUIRE(s.scratch != nullptr, "dibr_rasterization forward: state (kl_dibr_state_bytes) missing");
+  const DibrState S(B, H, W, F, K);
+  char *state = reinterpret_cast<char *>(s.scratch);
+  int *bcnt = reinterpret_cast<int *>(state);
+  int2 *bitems = reinterpret_cast<int2 *>(state + S.off_items);
+  double *bacc = reinterpret_cast<double *>(state + S.off_acc);
   const size_t P = (size_t)B * H * W;
-  if (P == 0) return s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK;
-  if (F == 0 || (g_dev_flags & (1 << 13))) {  // no faces (or dev: the separate pipelines)
-    KL_REQUIRE(face_ranges == nullptr || F == 0, "dibr_rasterization forward: face_ranges needs the combined path");
+  if (P == 0 || F == 0) {  // no pixels / no faces: no soft-mask hits, nothing listed
+    KL_CHECK_RC(fill_async(bcnt, 0, DibrState::kZeroInts * sizeof(int), st));
+    if (P == 0) return KL_OK;
+    SoftState<T> s0 = s;
+    s0.scratch = nullptr;
     KL_CHECK_RC(dibr_rast_fwd<T>(RastSrc<T>{fvi, nullptr, (T)m, fnz}, H, W, B, D, F, fvz, feat, m, eps, out_feat,
                                  out_idx, out_w, ws, ws_bytes, st));
-    return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, ws, ws_bytes, st);
+    return soft_tile_forward<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s0, ws, ws_bytes, st);
   }
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
@@ -1783,17 +1822,20 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const int split_from = g_dev_param[4] ? g_dev_param[4] : 5;
   const int split_log2 = sizeof(T) == 4 ? (g_dev_param[5] ? g_dev_param[5] : 2) : 0;
   if (nt <= ORD_LDS_TILES && !(g_dev_flags & (1 << 20))) {  // counts and orders in one launch
-    hipLaunchKernelGGL(tile_countorder2_kernel, dim3(2), dim3(1024), 0, st, (const uint32_t *)rbm,
+    // + 254 workgroups that zero the backward's soft-mask accumulator while two order
+    const unsigned og = g_dev_param[9] >= 2 ? (unsigned)g_dev_param[9] : 256u;  // dev: grid (2 = no zero fill)
+    hipLaunchKernelGGL(tile_countorder2_kernel, dim3(og), dim3(1024), 0, st, (const uint32_t *)rbm,
                        (const uint32_t *)sbm, g.words, items, split_from, split_log2, nitems, sorder, nt,
-                       soft_lp_min(K), snitems, soft_split(), 1, s.scratch);
+                       soft_lp_min(K), snitems, soft_split(), 1, bcnt, DibrState::kZeroInts, bacc,
+                       (size_t)B * F * 6, kDevStamps ? reinterpret_cast<uint64_t *>(g_dev_debug) : nullptr);
     KL_CHECK_LAUNCH();
   } else {  // counts (a wave per tile) then orders (dev bit 20: this path, for A/B timing)
     hipLaunchKernelGGL(tile_bucket2_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)rbm,
-                       (const uint32_t *)sbm, g.words, nt, rbk, sbk, rgh, sgh, s.scratch);
+                       (const uint32_t *)sbm, g.words, nt, rbk, sbk, rgh, sgh, bcnt, DibrState::kZeroInts);
     KL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(tile_order2_kernel, dim3(2), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh, items,
-                       split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt,
-                       soft_lp_min(K), snitems, soft_split(), 1);
+    hipLaunchKernelGGL(tile_order2_kernel, dim3(256), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh,
+                       items, split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt,
+                       soft_lp_min(K), snitems, soft_split(), 1, bacc, (size_t)B * F * 6);
     KL_CHECK_LAUNCH();
   }
   uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.off_defer);
@@ -1806,7 +1848,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
   KL_CHECK_LAUNCH();
   return soft_tile_forward_main<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, sbm, sorder, snitems,
-                                   srng, defer, st, true);
+                                   srng, defer, st, true, bitems, bcnt, S.cap);
 }
 
 template <typename T>
@@ -1815,39 +1857,23 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
                     const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *ws,
                     size_t ws_bytes, hipStream_t st, const uint2 *face_ranges) {
   KL_REQUIRE(D <= 8, "dibr_rasterization backward: feature dimension > 8 is not supported by the fused path");
-  // workspace: the soft mask's double sums | its items | the gather's big-face list
-  const size_t acc_bytes = al256((size_t)B * F * 6 * sizeof(double));
-  const size_t soft_bytes = al256(soft_tile_bwd_items_bytes(B, H, W, K));
-  KL_REQUIRE(ws_bytes >= acc_bytes + soft_bytes, "dibr_rasterization backward: workspace too small");
-  double *acc = reinterpret_cast<double *>(ws);
-  void *soft_ws = reinterpret_cast<char *>(ws) + acc_bytes;
-  void *gath_ws = reinterpret_cast<char *>(soft_ws) + soft_bytes;
-  bool has_soft = false;
-  // The soft-mask sums first (fill, plan, backward; left in double), then the gather on the same
-  // stream: it adds each face's soft sum, rounded on its own, to the face's own rounded gradient
-  // as it writes it -- autograd's add of the two gradients -- so there is no final add.  The soft
-  // kernel zeroes the gather's big-face counter (the state's scratch int, left non-zero by the
-  // previous backward) before the gather runs.  (r03x: 0.221-0.224 ms per step against
-  // 0.224-0.228 for the two halves on two streams joined by a final add, whose fork and join
-  // cost ~5 + ~11 us in the graph; dev bit 23 keeps that variant for A/B timing.)
-  if (!((g_dev_flags >> 23) & 1)) {
-    KL_CHECK_RC(soft_tile_backward<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m, gfvi, true, soft_ws,
-                                      soft_bytes, st, acc, &has_soft));
-    return rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
-                                   gfeat, gath_ws, ws_bytes - acc_bytes - soft_bytes, s.scratch, st, face_ranges,
-                                   has_soft ? acc : nullptr);
-  }
-  SideFork fork(st);
-  SoftState<T> ss = s;
-  ss.scratch = nullptr;
-  KL_CHECK_RC(soft_tile_backward<T>(B, H, W, F, K, grad_mask, mask, ss, fvi, sigmainv, m, gfvi, true, soft_ws,
-                                    soft_bytes, fork.side(), acc, &has_soft));
-  KL_CHECK_RC(rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
-                                      gfeat, gath_ws, ws_bytes - acc_bytes - soft_bytes, s.scratch, st, face_ranges,
-                                      nullptr));
-  KL_CHECK_RC(fork.join());
-  return has_soft ? acc_finalize<T>(acc, gfvi, (size_t)B * F * 6, true, st, s.scratch)
-                  : (s.scratch ? fill_async(s.scratch, 0, sizeof(int), st) : KL_OK);
+  KL_REQUIRE(s.scratch != nullptr, "dibr_rasterization backward: state (kl_dibr_state_bytes) missing");
+  // The soft-mask terms first, summed in double into the state's accumulator (zeroed by the
+  // forward) over the work items the forward listed -- no plan kernel, no fill -- then the gather
+  // on the same stream, which adds each face's soft sum, rounded on its own, to the face's own
+  // rounded gradient as it writes it (autograd's add of the two gradients).  (r03: a plan kernel
+  // listed the items and zeroed the accumulator, 8.6 us per backward at cfg3; until r03x the two
+  // halves ran on two streams joined by a final add, ~16 us of fork / join gaps in the graph.)
+  const DibrState S(B, H, W, F, K);
+  char *state = reinterpret_cast<char *>(s.scratch);
+  double *acc = reinterpret_cast<double *>(state + S.off_acc);
+  const bool has_soft = grad_mask != nullptr && K > 0 && (int64_t)B * H * W > 0 && (int64_t)B * F > 0;
+  if (has_soft)
+    KL_CHECK_RC(soft_tile_backward_listed<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m,
+                                             reinterpret_cast<const int2 *>(state + S.off_items),
+                                             reinterpret_cast<const int *>(state), S.cap, acc, st));
+  return rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi, gfeat,
+                                 ws, ws_bytes, nullptr, st, face_ranges, has_soft ? acc : nullptr);
 }
 }  // namespace kl
 
@@ -1859,29 +1885,32 @@ extern "C" size_t kl_dibr_workspace_bytes(int batch, int height, int width, int 
 }
 
 extern "C" size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum) {
-  const size_t a = kl_dibr_rasterize_bwd_workspace_bytes(batch, height, width, num_faces, 8);
-  const size_t b = soft_tile_bwd_items_bytes(batch, height, width, knum);
-  return al256((size_t)batch * num_faces * 6 * sizeof(double)) + al256(b) + a;
+  (void)knum;
+  return kl_dibr_rasterize_bwd_workspace_bytes(batch, height, width, num_faces, 8);
+}
+
+extern "C" size_t kl_dibr_state_bytes(int batch, int height, int width, int num_faces, int knum) {
+  return DibrState(batch, height, width, num_faces, knum).bytes;
 }
 
 extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
                                int knum, const void *fvz, const void *fvi, const void *feat, const void *fnz,
                                float sigmainv, double bbox_pad, float multiplier, float eps, void *out_feat,
                                int64_t *out_idx, void *out_w, void *out_mask, uint8_t *hits, uint32_t *rec_face,
-                               void *rec_prob, int *seg_tot, int *scratch, uint32_t *face_ranges, void *ws,
+                               void *rec_prob, int *seg_tot, void *state, uint32_t *face_ranges, void *ws,
                                size_t ws_bytes, kl_stream stream) {
   uint2 *fr = reinterpret_cast<uint2 *>(face_ranges);
   if (dtype == KL_F32)
     return dibr_fwd<float>(batch, height, width, num_faces, feat_dim, knum, (const float *)fvz, (const float *)fvi,
                            (const float *)feat, (const float *)fnz, sigmainv, bbox_pad, multiplier, eps,
                            (float *)out_feat, out_idx, (float *)out_w, (float *)out_mask,
-                           SoftState<float>{hits, rec_face, (float *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
+                           SoftState<float>{hits, rec_face, (float *)rec_prob, seg_tot, (int *)state}, ws, ws_bytes,
                            S(stream), fr);
   if (dtype == KL_F64)
     return dibr_fwd<double>(batch, height, width, num_faces, feat_dim, knum, (const double *)fvz, (const double *)fvi,
                             (const double *)feat, (const double *)fnz, sigmainv, bbox_pad, multiplier, eps,
                             (double *)out_feat, out_idx, (double *)out_w, (double *)out_mask,
-                            SoftState<double>{hits, rec_face, (double *)rec_prob, seg_tot, scratch}, ws, ws_bytes,
+                            SoftState<double>{hits, rec_face, (double *)rec_prob, seg_tot, (int *)state}, ws, ws_bytes,
                             S(stream), fr);
   set_error("dibr_rasterization not implemented for this dtype");
   return KL_E_INVALID;
@@ -1892,21 +1921,21 @@ extern "C" int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width
                                 const void *w, const void *fvi, const void *feat, const void *fnz, const void *mask,
                                 const uint8_t *hits, const uint32_t *rec_face, const void *rec_prob,
                                 const int *seg_tot, float sigmainv, float multiplier, float eps, void *gfvi,
-                                void *gfeat, int *scratch, const uint32_t *face_ranges, void *ws, size_t ws_bytes,
+                                void *gfeat, void *state, const uint32_t *face_ranges, void *ws, size_t ws_bytes,
                                 kl_stream stream) {
   const uint2 *fr = reinterpret_cast<const uint2 *>(face_ranges);
   if (dtype == KL_F32)
     return dibr_bwd<float>(
         batch, height, width, num_faces, feat_dim, knum, (const float *)grad_feat, (const float *)grad_mask, face_idx,
         (const float *)w, (const float *)fvi, (const float *)feat, (const float *)fnz, (const float *)mask,
-        SoftState<float>{(uint8_t *)hits, (uint32_t *)rec_face, (float *)rec_prob, (int *)seg_tot, scratch},
+        SoftState<float>{(uint8_t *)hits, (uint32_t *)rec_face, (float *)rec_prob, (int *)seg_tot, (int *)state},
         sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream), fr);
   if (dtype == KL_F64)
     return dibr_bwd<double>(
         batch, height, width, num_faces, feat_dim, knum, (const double *)grad_feat, (const double *)grad_mask,
         face_idx, (const double *)w, (const double *)fvi, (const double *)feat, (const double *)fnz,
         (const double *)mask,
-        SoftState<double>{(uint8_t *)hits, (uint32_t *)rec_face, (double *)rec_prob, (int *)seg_tot, scratch},
+        SoftState<double>{(uint8_t *)hits, (uint32_t *)rec_face, (double *)rec_prob, (int *)seg_tot, (int *)state},
         sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream), fr);
   set_error("dibr_rasterization backward not implemented for this dtype");
   return KL_E_INVALID;

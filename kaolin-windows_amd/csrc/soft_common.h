@@ -172,6 +172,11 @@ struct FaceHash {
   }
 };
 
+// Shards of the soft-mask backward's work-item list (counters DS_CNT_STRIDE ints apart, one per
+// 64-byte line): the fused forward appends to shard blockIdx % DS_SHARDS.
+constexpr int DS_SHARDS = 8;
+constexpr int DS_CNT_STRIDE = 16;
+
 // The compact soft-mask state (softtile.hip): per pixel the filled-slot count; per hit a
 // record (face | type << 28, prob), packed per 64-pixel row segment; per segment its hit
 // total; and one scratch int the forward zeroes / the backward re-zeroes after use
@@ -191,13 +196,37 @@ template <typename T>
 int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv,
                            double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
                            const int32_t *order, const int *nitems, const uint2 *rng, uint8_t *defer,
-                           hipStream_t st, bool prefilled);
+                           hipStream_t st, bool prefilled, int2 *bwd_items = nullptr, int *bwd_cnt = nullptr,
+                           int bwd_cap = 0);
 int soft_lp_min(int K);
 template <typename T>
 int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
                        const T *fvi, float sigmainv, float m, T *gfvi, bool accumulate, void *ws, size_t ws_bytes,
                        hipStream_t st, double *acc_out = nullptr, bool *has_sum = nullptr);
 size_t soft_tile_bwd_items_bytes(int B, int H, int W, int K);
+// the most backward work items one fused forward can list (per shard)
+int soft_bwd_item_cap(int B, int H, int W, int K);
+// The fused path's backward on the forward's item list and zeroed accumulator (DibrState):
+// the per-face double sums are added into acc (B*F*6), not rounded.
+template <typename T>
+int soft_tile_backward_listed(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
+                              const T *fvi, float sigmainv, float m, const int2 *items, const int *cnt, int cap,
+                              double *acc, hipStream_t st);
+// Per-call state of kl_dibr_forward / kl_dibr_backward (kl_dibr_state_bytes):
+//   [0, 512)   DS_SHARDS item counters; int 128: the r03 gather's big-face counter (dev path)
+//   items      DS_SHARDS x cap backward work items (int2)
+//   acc        the soft mask's per-face double sums (B*F*6), zeroed by the forward
+struct DibrState {
+  int cap;
+  size_t off_items, off_acc, bytes;
+  DibrState(int B, int H, int W, int F, int K) {
+    cap = soft_bwd_item_cap(B, H, W, K);
+    off_items = 1024;
+    off_acc = al256(off_items + (size_t)DS_SHARDS * cap * sizeof(int2));
+    bytes = off_acc + (size_t)B * F * 6 * sizeof(double);
+  }
+  static constexpr int kZeroInts = 129;  // counters + big-face counter, zeroed by the forward
+};
 size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int F, int K);
 size_t soft_tile_ws_bytes(int B, int H, int W, int F);
 

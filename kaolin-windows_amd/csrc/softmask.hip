@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
   int kid = 0;
   bool active = !covered && K > 0;
   uint64_t amask = ballot(active);
-  const uint32_t *words = bitmap + ((size_t)(b * g.tiles_y + j / TILE_H) * g.tiles_x + tx) * g.words;
+  const uint32_t *words = bitmap + ((size_t)(b * g.tiles_y + j / TILE_H) * g.tiles_x + tx);  // word w: [w * ntiles]
   const int64_t f0 = (int64_t)b * F;
   const T *bb = bbox + f0 * 4;
   // candidate chunks: 64 bitmap words per vector load, non-empty words found by ballot
@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
       while (!wmask) {
         if (wg * 64 >= g.words) return -1;
         const int w = wg * 64 + lane;
-        wv = w < g.words ? words[w] : 0u;
+        wv = w < g.words ? words[(size_t)w * g.ntiles()] : 0u;
         wmask = ballot(wv != 0);
         wg++;
       }
@@ -319,9 +319,8 @@ __global__ void __launch_bounds__(256) tile_work_kernel(const uint32_t *__restri
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   if (t >= nt) return;
-  const uint32_t *w = bitmap + (size_t)t * g.words;
   uint32_t n = 0;
-  for (int k = 0; k < g.words; k++) n += __popc(w[k]);
+  for (int k = 0; k < g.words; k++) n += __popc(bitmap[bm_index(nt, t, k)]);
   keys[t] = 0xffffu - min(n, 0xffffu);  // ascending sort -> heaviest first
   vals[t] = t;
 }

@@ -41,6 +41,9 @@ namespace kl {
 // Forward work items (tileorder.h, order_soft_items): a 4-wave workgroup takes 8 >> lp rows of
 // a tile with Q = 4 / (8 >> lp) waves per row.
 constexpr int ST_WAVES = 4;
+// Backward work items: a forward item's hits taken row-major in pieces of SB_PIECE (one hit per
+// thread of a backward workgroup).
+constexpr int SB_PIECE = 512;
 
 template <typename T>
 struct SoftTileArgs {
@@ -63,6 +66,12 @@ struct SoftTileArgs {
   int dev;                   // dev ablation flags (kl_dev_set_flags), 0 in the product path
   int prefilled;             // mask / hits / seg_tot / defer already written for pixels and rows
                              // without hits (kl_dibr_forward's rasterizer): only hits are written
+  // kl_dibr_forward: the backward's work items, appended here (DibrState): a workgroup with hits
+  // adds (item, piece) for each SB_PIECE of its rows' hits to shard blockIdx % DS_SHARDS with one
+  // atomic; nullptr: not listed (the backward's plan kernel lists them from seg_tot)
+  int2 *bwd_items = nullptr;
+  int *bwd_cnt = nullptr;
+  int bwd_cap = 0;
 };
 
 // LDS of one row: its [K][64] slot lists (face ids, then probabilities in place), the
@@ -132,7 +141,7 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   if (!any && a.prefilled) return;  // no uncovered pixel: its outputs are written (workgroup-uniform)
   if (any) {
     ChunkSeq seq;
-    seq.init(a.bitmap + ((size_t)(b * g.tiles_y + ty) * g.tiles_x + tx) * g.words, g.words, lane);
+    seq.init(a.bitmap + ((size_t)(b * g.tiles_y + ty) * g.tiles_x + tx), g.words, g.ntiles(), lane);
     const uint2 *rg = a.rng + f0;
     // this wave's chunk of the next fill step (ordinal pos + wid) with its pixel ranges in
     // flight: an unconditional load from a clamped index (a guarded load is waited for at
@@ -369,6 +378,20 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
       a.defer[(size_t)(b * H + j) * g.tiles_x + tx] = inline_eval ? 0 : 1;
     }
   }
+  if (a.bwd_items) {  // workgroup-uniform; the rows' totals through LDS (s_wcnt is free by now)
+    if (qi == 0 && lane == 0) s_wcnt[r] = total;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int k = 0; k < RP; k++) tot += s_wcnt[k];
+      const int n = (tot + SB_PIECE - 1) / SB_PIECE;
+      if (n) {
+        const int sh = (int)(blockIdx.x & (DS_SHARDS - 1));
+        int2 *dst = a.bwd_items + (size_t)sh * a.bwd_cap + atomicAdd(&a.bwd_cnt[sh * DS_CNT_STRIDE], n);
+        for (int k = 0; k < n; k++) dst[k] = make_int2(item, k);
+      }
+    }
+  }
   if (dbg && lane == 0) {
     uint64_t *d = dbg + ((size_t)blockIdx.x * ST_WAVES + wid) * 10;
     d[8] = c_fill;
@@ -473,12 +496,13 @@ __global__ void __launch_bounds__(256) soft_tile_eval_kernel(SoftTileArgs<T> a) 
 }
 
 // ---------------------------------------------------------------- backward
-// Work items of the backward: per tile, the hits of its 8 rows taken row-major in pieces
-// of SB_PIECE (one hit per thread of a workgroup), so that the heavy tiles (the silhouette's
-// tight spots, ~10^4 hits) spread over many workgroups.  The plan kernel (one workgroup)
-// lists the items tile by tile from the forward's per-row-segment hit totals and writes
-// the item count; the backward kernel is persistent and takes the items round-robin.
-constexpr int SB_PIECE = 512;
+// Work items of the backward: (forward item code, piece): the hits of a tile's rows (all 8, or a
+// part of them) taken row-major in pieces of SB_PIECE (one hit per thread of a workgroup), so that
+// the heavy tiles (the silhouette's tight spots, ~10^4 hits) spread over many workgroups.  The
+// fused forward (kl_dibr_forward) lists them as it writes the hits (SoftTileArgs::bwd_items,
+// DS_SHARDS shards); for the standalone soft mask the plan kernel (one workgroup) lists whole
+// tiles from the forward's per-row-segment hit totals.  The backward kernel is persistent and
+// takes the items round-robin.
 
 // Block 0 plans; blocks 1.. zero the backward's double accumulator (n doubles) meanwhile -- one
 // launch instead of a fill followed by the one-workgroup plan (5.4 + 7.8 us at cfg3).
@@ -513,10 +537,10 @@ __global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restri
     }
     int all;
     const int excl = carry + block_exclusive_scan(np, s_wave, &all);
-    for (int q = 0; q < np; q++) items[excl + q] = make_int2(t, q);
+    for (int q = 0; q < np; q++) items[excl + q] = make_int2(t, q);  // code = tile: all 8 rows
     carry += all;
   }
-  if (threadIdx.x == 0) ctl[0] = carry;
+  if (threadIdx.x < DS_SHARDS) ctl[threadIdx.x * DS_CNT_STRIDE] = threadIdx.x == 0 ? carry : 0;  // one shard
 }
 
 // Per-face accumulation for one work item: LDS hash on the mesh-local face index with
@@ -586,7 +610,7 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const uint8_t *__restrict__ hits,
     const uint32_t *__restrict__ rec_face, const T *__restrict__ rec_prob, const T *__restrict__ fvi, BinGeom g,
     int F, int K, float sigmainv, float multiplier, double *__restrict__ gacc, const int2 *__restrict__ items,
-    int *__restrict__ ctl, int *__restrict__ scratch, int dev) {
+    const int *__restrict__ ctl, int cap, int *__restrict__ scratch, int dev) {
   constexpr int HC = 512;
   __shared__ int s_key[HC];
   __shared__ double s_val[HC * 6];
@@ -603,7 +627,13 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
   if (threadIdx.x == 0) s_nused = 0;
   if (scratch && threadIdx.x == 0 && blockIdx.x == 0) *scratch = 0;
   ItemHash<T, HC> hash{s_key, s_val, s_used, &s_nused};
-  const int nitems = ctl[0];
+  // the shards' item counts (ctl[s * DS_CNT_STRIDE]) and their prefix
+  int nsh[DS_SHARDS], nitems = 0;
+#pragma unroll
+  for (int k = 0; k < DS_SHARDS; k++) {
+    nsh[k] = ctl[k * DS_CNT_STRIDE];
+    nitems += nsh[k];
+  }
   const T ms = (T)multiplier;
   const float sx = multiplier / (float)W, sy = multiplier / (float)H;
   // items are taken round-robin (a claim counter's returning atomic costs more than the
@@ -611,12 +641,16 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
   for (int q = (int)blockIdx.x;; q += (int)gridDim.x) {
     __syncthreads();  // the previous item's hash reset is done
     if (q >= nitems) return;
-    const int2 it = items[q];
-    const int tile = it.x;
+    int sh = 0, qq = q;
+    while (qq >= nsh[sh]) qq -= nsh[sh++];
+    const int2 it = items[(size_t)sh * cap + qq];
+    const int tile = it.x & 0xffffff, part = (it.x >> 24) & 15, lp = (it.x >> 28) & 7;
+    const int RP = TILE_H >> lp;  // rows of the item
     const int tx = tile % g.tiles_x, ty = (tile / g.tiles_x) % g.tiles_y, b = tile / (g.tiles_x * g.tiles_y);
+    const int j0 = ty * TILE_H + part * RP;
     const int ibase = tx * TILE_W;
-    {  // row `wid` of the tile
-      const int j = ty * TILE_H + wid, i = ibase + lane;
+    if (wid < RP) {  // row `wid` of the item
+      const int j = j0 + wid, i = ibase + lane;
       int kid = 0;
       if (j < H && i < W) {
         const size_t p = ((size_t)b * H + j) * W + i;
@@ -636,20 +670,19 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
     __syncthreads();
     if (threadIdx.x == 0) {
       s_rowpre[0] = 0;
-      for (int r = 1; r <= TILE_H; r++) s_rowpre[r] += s_rowpre[r - 1];
+      for (int r = 1; r <= RP; r++) s_rowpre[r] += s_rowpre[r - 1];
     }
     __syncthreads();
     const int f = it.y * SB_PIECE + (int)threadIdx.x;
-    if (f < s_rowpre[TILE_H] && !(dev & 8)) {
+    if (f < s_rowpre[RP] && !(dev & 8)) {
       int r = 0;
-#pragma unroll
-      for (int k = 1; k < TILE_H; k++) r += s_rowpre[k] <= f ? 1 : 0;
+      for (int k = 1; k < RP; k++) r += s_rowpre[k] <= f ? 1 : 0;
       const int e = f - s_rowpre[r];
       int lo = 0;  // owner lane: last lane with s_pre[r][lo] <= e
 #pragma unroll
       for (int st = 32; st > 0; st >>= 1)
         if (s_pre[r][lo + st] <= e) lo += st;
-      const int j = ty * TILE_H + r;
+      const int j = j0 + r;
       const size_t o = ((size_t)(b * H + j) * g.tiles_x + tx) * 64 * (size_t)K + e;
       const uint32_t rr = rec_face[o];
       const T pr = rec_prob[o];
@@ -740,7 +773,7 @@ int soft_tile_forward(int B, int H, int W, int F, int K, const T *fvi, const int
   KL_CHECK_LAUNCH();
   uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.defer);
   return soft_tile_forward_main<T>(B, H, W, F, K, fvi, sel, sigmainv, pad, m, mask, s, bitmap, order, nitems, rng,
-                                   defer, st, false);
+                                   defer, st, false, nullptr, nullptr, 0);
 }
 
 // The selection and evaluation kernels on bins made by the caller: bitmap (SoftSrc bins),
@@ -750,7 +783,7 @@ template <typename T>
 int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv,
                            double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
                            const int32_t *order, const int *nitems, const uint2 *rng, uint8_t *defer,
-                           hipStream_t st, bool prefilled) {
+                           hipStream_t st, bool prefilled, int2 *bwd_items, int *bwd_cnt, int bwd_cap) {
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   if (nt == 0) return KL_OK;
@@ -761,6 +794,9 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   SoftTileArgs<T> args{src, rng,  sel,    bitmap, order,      nitems,     g,         F,     K,
                        sigmainv, m, mask, s.hits, s.rec_face, s.rec_prob, s.seg_tot, defer, (uint64_t *)g_dev_debug,
                        g_dev_flags, prefilled ? 1 : 0};
+  args.bwd_items = bwd_items;
+  args.bwd_cnt = bwd_cnt;
+  args.bwd_cap = bwd_cap;
   hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)soft_items_bound(nt, lp_min, soft_split())), dim3(64 * ST_WAVES), lds,
                      st, args);
   KL_CHECK_LAUNCH();
@@ -775,11 +811,20 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   return KL_OK;
 }
 
-// workspace: item count | items | the (B,F,3,2) double accumulator
+// workspace: item counters (DS_SHARDS, one used) | items | the (B,F,3,2) double accumulator
+constexpr size_t SB_CTL_BYTES = DS_SHARDS * DS_CNT_STRIDE * sizeof(int);
 static size_t soft_bwd_acc_offset(int B, int H, int W, int K) {
   const BinGeom g = make_bin_geom(B, H, W, 1);
   const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
-  return al256(256 + nt * (size_t)(K + 2) * sizeof(int2));
+  return al256(SB_CTL_BYTES + nt * (size_t)(K + 2) * sizeof(int2));
+}
+
+int soft_bwd_item_cap(int B, int H, int W, int K) {
+  const BinGeom g = make_bin_geom(B, H, W, 1);
+  const int64_t nt = (int64_t)g.batch * g.tiles_y * g.tiles_x;
+  const int64_t parts = soft_items_bound((int)nt, soft_lp_min(K), soft_split());
+  const int64_t hits = (int64_t)B * H * g.tiles_x * 64 * (K > 0 ? K : 0);
+  return (int)(parts + hits / SB_PIECE + 1);
 }
 size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int F, int K) {
   return soft_bwd_acc_offset(B, H, W, K) + al256((size_t)B * F * 6 * sizeof(double));
@@ -803,7 +848,7 @@ int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T
              "dibr_soft_mask backward: workspace too small");
   const BinGeom g = make_bin_geom(B, H, W, F);
   int *ctl = reinterpret_cast<int *>(ws);
-  int2 *items = reinterpret_cast<int2 *>(reinterpret_cast<char *>(ws) + 256);
+  int2 *items = reinterpret_cast<int2 *>(reinterpret_cast<char *>(ws) + SB_CTL_BYTES);
   double *acc = acc_out ? acc_out
                         : reinterpret_cast<double *>(reinterpret_cast<char *>(ws) + soft_bwd_acc_offset(B, H, W, K));
   hipLaunchKernelGGL(soft_bwd_plan_kernel, dim3(1 + SB_ZERO_BLOCKS), dim3(1024), 0, st, (const int *)s.seg_tot, g,
@@ -816,7 +861,7 @@ int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T
   const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
   hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
                      (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, acc,
-                     (const int2 *)items, ctl, s.scratch, g_dev_flags);
+                     (const int2 *)items, (const int *)ctl, 0, s.scratch, g_dev_flags);
   KL_CHECK_LAUNCH();
   if (acc_out) {
     if (has_sum) *has_sum = true;
@@ -826,6 +871,30 @@ int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T
 }
 size_t soft_tile_bwd_items_bytes(int B, int H, int W, int K) { return soft_bwd_acc_offset(B, H, W, K); }
 
+template <typename T>
+int soft_tile_backward_listed(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
+                              const T *fvi, float sigmainv, float m, const int2 *items, const int *cnt, int cap,
+                              double *acc, hipStream_t st) {
+  if ((int64_t)B * H * W == 0 || K <= 0 || grad == nullptr || (int64_t)B * F == 0) return KL_OK;
+  const BinGeom g = make_bin_geom(B, H, W, F);
+  int dev_id = 0, ncu = 256;
+  if (hipGetDevice(&dev_id) == hipSuccess)
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_id);
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
+  hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
+                     (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, acc, items, cnt,
+                     cap, (int *)nullptr, g_dev_flags);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
+template int soft_tile_backward_listed<float>(int, int, int, int, int, const float *, const float *,
+                                              const SoftState<float> &, const float *, float, float, const int2 *,
+                                              const int *, int, double *, hipStream_t);
+template int soft_tile_backward_listed<double>(int, int, int, int, int, const double *, const double *,
+                                               const SoftState<double> &, const double *, float, float, const int2 *,
+                                               const int *, int, double *, hipStream_t);
+
 template int soft_tile_forward<float>(int, int, int, int, int, const float *, const int64_t *, float, double, float,
                                       float *, const SoftState<float> &, void *, size_t, hipStream_t);
 template int soft_tile_forward<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
@@ -833,11 +902,11 @@ template int soft_tile_forward<double>(int, int, int, int, int, const double *, 
 template int soft_tile_forward_main<float>(int, int, int, int, int, const float *, const int64_t *, float, double,
                                            float, float *, const SoftState<float> &, const uint32_t *,
                                            const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t,
-                                           bool);
+                                           bool, int2 *, int *, int);
 template int soft_tile_forward_main<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
                                             float, double *, const SoftState<double> &, const uint32_t *,
                                             const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t,
-                                            bool);
+                                            bool, int2 *, int *, int);
 template int soft_tile_backward<float>(int, int, int, int, int, const float *, const float *,
                                        const SoftState<float> &, const float *, float, float, float *, bool, void *,
                                        size_t, hipStream_t, double *, bool *);

@@ -27,9 +27,8 @@ static __global__ void __launch_bounds__(256) tile_bucket_kernel(const uint32_t 
   __syncthreads();
   const int t = blockIdx.x * (blockDim.x >> 6) + wid;  // one wave per tile
   if (t < nt) {
-    const uint32_t *w = bitmap + (size_t)t * words;
     unsigned n = 0;
-    for (int k = lane; k < words; k += 64) n += __popc(w[k]);
+    for (int k = lane; k < words; k += 64) n += __popc(bitmap[bm_index(nt, t, k)]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
     if (lane == 0) {
@@ -62,7 +61,7 @@ constexpr int ORD_LDS_TILES = 16384;
 // threads of the (single) workgroup call it.
 __device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, const int *__restrict__ ghist,
                                             const uint8_t *__restrict__ bk, int nt, int32_t *__restrict__ order,
-                                            int *__restrict__ nitems) {
+                                            int *__restrict__ nitems, uint64_t *dbg = nullptr) {
   __syncthreads();  // lpb / staged buckets written
   // per band, the exclusive prefix over buckets, heaviest first: one lane per (band, bucket),
   // a 32-lane segmented scan (two bands per wave)
@@ -98,11 +97,32 @@ __device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, co
     if (nitems) *nitems = N;
   }
   __syncthreads();
-  for (int u = threadIdx.x; u < nt; u += blockDim.x) {
-    const int q = bk[u], g = tile_band(u, nt), lp = lpb[q];
-    if (lp < 0) continue;  // bucket without items
+  if (dbg && threadIdx.x == 0) dbg[2] = stamp_wall();
+  // the tiles' ranks in their (band, bucket): one LDS atomic per distinct key of a wave (a wave's
+  // tiles are consecutive, so they share a band and mostly a few buckets; one returning atomic per
+  // tile serialised up to 64 lanes on one address)
+  const int lane = threadIdx.x & 63;
+  for (int u0 = threadIdx.x - lane; u0 < nt; u0 += blockDim.x) {  // wave-uniform
+    const int u = u0 + lane;
+    const int q = u < nt ? bk[u] : 0, g = u < nt ? tile_band(u, nt) : 0, lp = u < nt ? lpb[q] : -1;
+    const int key = lp < 0 ? -1 : g * ORD_BUCKETS + q;
+    uint64_t todo = ballot(key >= 0);
+    int r0 = 0;
+    while (todo) {
+      const int kl = __builtin_ctzll(todo);
+      const int kk = __builtin_amdgcn_readlane(key, kl);
+      const uint64_t same = ballot(key == kk) & todo;
+      todo &= ~same;
+      const int npk = 1 << __builtin_amdgcn_readlane(lp < 0 ? 0 : lp, kl);
+      int base = 0;
+      if (lane == kl) base = atomicAdd(&sb[kk], npk * __popcll(same));
+      base = __builtin_amdgcn_readlane(base, kl);
+      if (key == kk)
+        r0 = base + npk * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
+    }
+    if (key < 0) continue;
     const int np = 1 << lp;
-    const int r0 = atomicAdd(&sb[g * ORD_BUCKETS + q], np);
     for (int k = 0; k < np; k++) {
       const int r = r0 + k;
       int pos;
@@ -125,14 +145,14 @@ __device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, co
 __device__ __forceinline__ void order_items(int *sb, int *sx, int *lpb, const int *__restrict__ ghist,
                                             const uint8_t *__restrict__ bk, int nt, int32_t *__restrict__ order,
                                             int identity, int split_from, int split_log2,
-                                            int *__restrict__ nitems) {
+                                            int *__restrict__ nitems, uint64_t *dbg = nullptr) {
   if (identity) {
     for (int u = threadIdx.x; u < nt; u += blockDim.x) order[u] = u;
     if (nitems && threadIdx.x == 0) *nitems = nt;
     return;
   }
   if (threadIdx.x < ORD_BUCKETS) lpb[threadIdx.x] = (int)threadIdx.x >= split_from ? split_log2 : 0;
-  place_items(sb, sx, lpb, ghist, bk, nt, order, nitems);
+  place_items(sb, sx, lpb, ghist, bk, nt, order, nitems, dbg);
 }
 
 // Soft-mask work items (softtile.hip).  A 4-wave workgroup takes one part.  lp is lp_min (set
@@ -152,7 +172,7 @@ inline int soft_items_bound(int nt, int lp_min, SoftSplit sp) {
 __device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, const uint8_t *__restrict__ bk,
                                                  const int *__restrict__ ghist, int nt, int32_t *__restrict__ order,
                                                  int lp_min, int *__restrict__ nitems, SoftSplit sp,
-                                                 int skip_empty = 0) {
+                                                 int skip_empty = 0, uint64_t *dbg = nullptr) {
   // tiles per bucket summed over the bands (one lane per bucket), then the caps walked
   // serially from the heaviest bucket down on LDS values
   if (threadIdx.x < ORD_BUCKETS) {
@@ -178,7 +198,7 @@ __device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, con
     }
   }
   __syncthreads();  // sx is reused by place_items
-  place_items(sb, sx, lpb, ghist, bk, nt, order, nitems);
+  place_items(sb, sx, lpb, ghist, bk, nt, order, nitems, dbg);
 }
 
 // the buckets of tiles [0, nt) into LDS when they fit (else the global array is used)
@@ -216,18 +236,19 @@ static __global__ void __launch_bounds__(256) tile_bucket2_kernel(const uint32_t
                                                                   const uint32_t *__restrict__ bm1, int words, int nt,
                                                                   uint8_t *__restrict__ bk0, uint8_t *__restrict__ bk1,
                                                                   int *__restrict__ gh0, int *__restrict__ gh1,
-                                                                  int *__restrict__ scratch) {
+                                                                  int *__restrict__ zero, int nzero) {
   __shared__ int hist[2][ORD_HIST];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < 2 * ORD_HIST; i += blockDim.x) hist[i / ORD_HIST][i % ORD_HIST] = 0;
-  if (threadIdx.x == 0 && blockIdx.x == 0 && scratch) *scratch = 0;
+  if (blockIdx.x == 0 && zero)
+    for (int i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0;
   __syncthreads();
   const int t = blockIdx.x * (blockDim.x >> 6) + wid;
   if (t < nt) {
     unsigned n0 = 0, n1 = 0;
     for (int k = lane; k < words; k += 64) {
-      n0 += __popc(bm0[(size_t)t * words + k]);
-      n1 += __popc(bm1[(size_t)t * words + k]);
+      n0 += __popc(bm0[bm_index(nt, t, k)]);
+      n1 += __popc(bm1[bm_index(nt, t, k)]);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -249,6 +270,16 @@ static __global__ void __launch_bounds__(256) tile_bucket2_kernel(const uint32_t
   }
 }
 
+// Blocks past the first two of the order kernels below zero `zacc` (zn doubles) meanwhile: the
+// chip is otherwise idle while two workgroups order (kl_dibr_forward's soft-mask accumulator).
+__device__ __forceinline__ void zero_doubles_share(double *__restrict__ z, size_t n, int part, int nparts) {
+  const size_t n2 = n / 2, per = (n2 + nparts - 1) / nparts;
+  const size_t e0 = (size_t)part * per, e1 = e0 + per < n2 ? e0 + per : n2;
+  double2 *z2 = reinterpret_cast<double2 *>(z);
+  for (size_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) z2[e] = make_double2(0.0, 0.0);
+  if ((n & 1) && part == 0 && threadIdx.x == 0) z[n - 1] = 0.0;
+}
+
 static __global__ void __launch_bounds__(1024) tile_order2_kernel(const uint8_t *__restrict__ bk0,
                                                                   const int *__restrict__ gh0,
                                                                   int32_t *__restrict__ order0, int split_from,
@@ -257,9 +288,14 @@ static __global__ void __launch_bounds__(1024) tile_order2_kernel(const uint8_t 
                                                                   const int *__restrict__ gh1,
                                                                   int32_t *__restrict__ order1, int nt, int lp_min1,
                                                                   int *__restrict__ nitems1, SoftSplit sp,
-                                                                  int skip_empty1) {
+                                                                  int skip_empty1, double *__restrict__ zacc,
+                                                                  size_t zn) {
   __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS];
   __shared__ uint8_t sbk[ORD_LDS_TILES];
+  if (blockIdx.x >= 2) {
+    zero_doubles_share(zacc, zn, blockIdx.x - 2, gridDim.x - 2);
+    return;
+  }
   // two workgroups: block 0 orders the rasterizer's items, block 1 the soft mask's
   const bool soft = blockIdx.x == 1;
   const uint8_t *b = stage_buckets(sbk, soft ? bk1 : bk0, nt);
@@ -272,39 +308,52 @@ static __global__ void __launch_bounds__(1024) tile_order2_kernel(const uint8_t 
 // tile_bucket2_kernel + tile_order2_kernel in one launch (nt <= ORD_LDS_TILES): each of the two
 // workgroups counts its bitmap's candidate chunks with one thread per tile (the tile's words
 // loaded eight at a time) into LDS buckets and histogram, then orders.  Block 0 also zeroes
-// `scratch`.  (Counting one tile per wave in turn, a reduction each, took 85 us.)
+// zero[0, nzero).  (Counting one tile per wave in turn, a reduction each, took 85 us.)
 static __global__ void __launch_bounds__(1024) tile_countorder2_kernel(
     const uint32_t *__restrict__ bm0, const uint32_t *__restrict__ bm1, int words, int32_t *__restrict__ order0,
     int split_from, int split_log2, int *__restrict__ nitems0, int32_t *__restrict__ order1, int nt, int lp_min1,
-    int *__restrict__ nitems1, SoftSplit sp, int skip_empty1, int *__restrict__ scratch) {
+    int *__restrict__ nitems1, SoftSplit sp, int skip_empty1, int *__restrict__ zero, int nzero,
+    double *__restrict__ zacc, size_t zn, uint64_t *dbg) {
   __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS], hist[ORD_HIST];
   __shared__ uint8_t sbk[ORD_LDS_TILES];
+  if (blockIdx.x >= 2) {
+    zero_doubles_share(zacc, zn, blockIdx.x - 2, gridDim.x - 2);
+    return;
+  }
   const bool soft = blockIdx.x == 1;
   const uint32_t *bm = soft ? bm1 : bm0;
-  if (!soft && threadIdx.x == 0 && scratch) *scratch = 0;
+  if (dbg) dbg += blockIdx.x * 4;  // dev stamps: start, counted, placed prefix, end (wall clock)
+  if (dbg && threadIdx.x == 0) dbg[0] = stamp_wall();
+  if (!soft && zero)
+    for (int i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0;
   for (int i = threadIdx.x; i < ORD_HIST; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   for (int t = threadIdx.x; t < nt; t += blockDim.x) {
-    const uint32_t *w = bm + (size_t)t * words;
+    // word-major bitmap: a lane per tile, each word load coalesced across the wave, up to 32
+    // words in flight together (one round trip per tile for the bench's 25 words; 8 at a time
+    // took 4 round trips per tile)
+    const uint32_t *w = bm + t;
     unsigned n = 0;
-    int k = 0;
-    for (; k + 8 <= words; k += 8) {
-      uint32_t x[8];
+    for (int k0 = 0; k0 < words; k0 += 32) {
+      uint32_t x[32];
+      // unconditional loads from a clamped word (a guarded load is waited for inside its branch)
 #pragma unroll
-      for (int u = 0; u < 8; u++) x[u] = w[k + u];
+      for (int u = 0; u < 32; u++) x[u] = w[(size_t)(k0 + u < words ? k0 + u : words - 1) * nt];
 #pragma unroll
-      for (int u = 0; u < 8; u++) n += __popc(x[u]);
+      for (int u = 0; u < 32; u++) n += k0 + u < words ? __popc(x[u]) : 0u;
     }
-    for (; k < words; k++) n += __popc(w[k]);
     const int q = 31 - __clz(n + 1u);
     sbk[t] = (uint8_t)q;
     atomicAdd(&hist[tile_band(t, nt) * ORD_BUCKETS + q], 1);
   }
   __syncthreads();
+  if (dbg && threadIdx.x == 0) dbg[1] = stamp_wall();
   if (soft)
-    order_soft_items(sb, sx, lpb, sbk, hist, nt, order1, lp_min1, nitems1, sp, skip_empty1);
+    order_soft_items(sb, sx, lpb, sbk, hist, nt, order1, lp_min1, nitems1, sp, skip_empty1, dbg);
   else
-    order_items(sb, sx, lpb, hist, sbk, nt, order0, 0, split_from, split_log2, nitems0);
+    order_items(sb, sx, lpb, hist, sbk, nt, order0, 0, split_from, split_log2, nitems0, dbg);
+  __syncthreads();
+  if (dbg && threadIdx.x == 0) dbg[3] = stamp_wall();
 }
 
 }  // namespace kl

@@ -51,13 +51,14 @@ __device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {
 // prefix of their bit counts.  Wave-uniform; every wave of the workgroup holds a copy.
 // at(n) must be called with non-decreasing n.
 struct ChunkSeq {
-  const uint32_t *words;
+  const uint32_t *words;  // the tile's word 0; word w at words[w * stride] (binning.h bm_index)
+  size_t stride;
   int nwords, grp, base, gtot, pc;
   uint32_t wv;
   __device__ __forceinline__ void load(int g, int lane) {
     grp = g;
     const int w = g * 64 + lane;
-    wv = w < nwords ? words[w] : 0u;
+    wv = w < nwords ? words[(size_t)w * stride] : 0u;
     const int c = __popc(wv);
     int inc = c;
 #pragma unroll
@@ -68,8 +69,9 @@ struct ChunkSeq {
     pc = inc - c;
     gtot = __shfl(inc, 63);
   }
-  __device__ __forceinline__ void init(const uint32_t *w, int n, int lane) {
+  __device__ __forceinline__ void init(const uint32_t *w, int n, size_t st, int lane) {
     words = w;
+    stride = st;
     nwords = n;
     base = 0;
     load(0, lane);

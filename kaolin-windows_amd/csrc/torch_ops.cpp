@@ -81,14 +81,15 @@ struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
     at::Tensor rec_prob = at::empty({nrec}, opt);
     at::Tensor seg_tot =
         at::empty({std::max<int64_t>((int64_t)kl_soft_mask_compact_segments((int)B, H, W), 1)}, opt.dtype(at::kInt));
-    at::Tensor scratch = at::empty({1}, opt.dtype(at::kInt));
+    // the backward's soft-mask work items and its zeroed accumulator (written by the forward)
+    at::Tensor scratch = at::empty({(int64_t)kl_dibr_state_bytes((int)B, H, W, (int)F, K)}, opt.dtype(at::kByte));
     at::Tensor ranges = at::empty({B, F, 2}, opt.dtype(at::kInt));
     const size_t nbytes = kl_dibr_workspace_bytes((int)B, H, W, (int)F);
     at::Tensor ws = workspace(nbytes, dev, stream);
     check(kl_dibr_forward(dt, (int)B, H, W, (int)F, (int)D, K, ptr(fvz), ptr(fvi), ptr(feat), ptr(fnz), (float)sigmainv,
                           boxlen * multiplier, (float)multiplier, (float)eps, ptr(feats), idx.data_ptr<int64_t>(),
                           ptr(w), ptr(mask), hits.data_ptr<uint8_t>(), (uint32_t *)rec_face.data_ptr(), ptr(rec_prob),
-                          seg_tot.data_ptr<int>(), scratch.data_ptr<int>(),
+                          seg_tot.data_ptr<int>(), scratch.data_ptr(),
                           F > 0 ? (uint32_t *)ranges.data_ptr() : nullptr, ws.data_ptr(), nbytes,
                           (kl_stream)stream),
           "dibr_rasterization");
@@ -127,7 +128,7 @@ struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
                            hits.data_ptr<uint8_t>(), (const uint32_t *)rec_face.data_ptr(), ptr(rec_prob),
                            seg_tot.data_ptr<int>(), (float)ctx->saved_data["sigmainv"].toDouble(),
                            (float)ctx->saved_data["multiplier"].toDouble(), (float)ctx->saved_data["eps"].toDouble(),
-                           ptr(g_img), ptr(g_feat), scratch.data_ptr<int>(),
+                           ptr(g_img), ptr(g_feat), scratch.data_ptr(),
                            ctx->saved_data["has_ranges"].toBool() ? (const uint32_t *)ranges.data_ptr() : nullptr,
                            ws.data_ptr(), nbytes, (kl_stream)stream),
           "dibr_rasterization backward");

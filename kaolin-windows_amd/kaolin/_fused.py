@@ -139,8 +139,9 @@ def soft_mask_backward(grad, mask, sel, prob, cidx, ctype, face_vertices_image, 
 
 class SoftMaskState:
     """The compact saved state of the soft mask (softtile.hip): per-pixel filled-slot
-    counts, the per-hit records, the per-row-segment hit totals and the zeroed int32
-    scratch word."""
+    counts, the per-hit records, the per-row-segment hit totals and ``scratch``: the zeroed
+    int32 word of the standalone soft mask, or dibr_forward's state bytes (the backward's work
+    items and its accumulator, kl_dibr_state_bytes)."""
     __slots__ = ('hits', 'rec_face', 'rec_prob', 'seg_tot', 'scratch', 'knum')
 
     def __init__(self, hits, rec_face, rec_prob, seg_tot, scratch, knum):
@@ -262,7 +263,8 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     rec_face = torch.empty(max(nrec, 1), dtype=torch.int32, device=dev)
     rec_prob = torch.empty(max(nrec, 1), dtype=dtype, device=dev)
     seg_tot = torch.empty(max(N.size('kl_soft_mask_compact_segments', B, H, W), 1), dtype=torch.int32, device=dev)
-    scratch = torch.empty(1, dtype=torch.int32, device=dev)
+    # the fused path's state: the backward's soft-mask work items and its zeroed accumulator
+    state = torch.empty(N.size('kl_dibr_state_bytes', B, H, W, F, K), dtype=torch.uint8, device=dev)
     ranges = torch.empty((B, F, 2), dtype=torch.int32, device=dev)
     nbytes = N.size('kl_dibr_workspace_bytes', B, H, W, F)
     ws = _ws(nbytes, dev)
@@ -270,6 +272,6 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
         N.check(lib.kl_dibr_forward(
             N.dtype_code(dtype), B, H, W, F, D, K, N.ptr(fvz), N.ptr(fvi), N.ptr(feat), N.ptr(fnz), float(sigmainv),
             float(boxlen * multiplier), float(multiplier), float(eps), N.ptr(feats), N.ptr(idx), N.ptr(w),
-            N.ptr(mask), N.ptr(hits), N.ptr(rec_face), N.ptr(rec_prob), N.ptr(seg_tot), N.ptr(scratch),
+            N.ptr(mask), N.ptr(hits), N.ptr(rec_face), N.ptr(rec_prob), N.ptr(seg_tot), N.ptr(state),
             N.ptr(ranges if F > 0 else None), N.ptr(ws), nbytes, N.stream_of(dev)), func)
-    return feats, idx, w, mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, scratch, K), ranges
+    return feats, idx, w, mask, SoftMaskState(hits, rec_face, rec_prob, seg_tot, state, K), ranges

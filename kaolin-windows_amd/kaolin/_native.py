@@ -14,7 +14,7 @@ _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib')
 # `make STAMPS=1 OUT=...`); the default is the in-tree build
 LIB_PATH = os.environ.get('KAOLIN_HIP_LIB') or os.path.join(_LIB_DIR, 'libkaolin_hip.so')
 
-ABI_VERSION = 2  # include/kaolin_hip.h KL_ABI_VERSION: the signatures below
+ABI_VERSION = 3  # include/kaolin_hip.h KL_ABI_VERSION: the signatures below
 
 KL_F32, KL_F64, KL_F16, KL_U8, KL_I8, KL_I16, KL_I32, KL_I64 = range(8)
 _DTYPES = {
@@ -65,6 +65,7 @@ _SIGS = {
                                                 _P, _P, _SZ, _P]),
     'kl_dibr_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'kl_dibr_bwd_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
+    'kl_dibr_state_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'kl_dibr_forward': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, ctypes.c_double, _F, _F, _P, _P, _P,
                              _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_backward': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F,

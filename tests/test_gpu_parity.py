@@ -485,6 +485,35 @@ def test_soft_mask_compact_vs_oracle(kal, dtype, K):
     assert int(state.scratch.item()) == 0
 
 
+@pytest.mark.parametrize('dname', ['float32', 'float64'])
+def test_soft_mask_backward_pinned_bench_mesh(kal, dname):
+    """The GPU soft-mask backward (compact state) on the bench's 50k-face UV sphere (2 views at
+    96x128) against the independent numpy restatement of dibr_soft_mask_cuda.cu:230-353
+    (tests/golden/make_soft_bwd_pin.py:soft_bwd_ref) run on the GPU forward's own saved slots:
+    f32 bit-equal to its float terms summed in double and rounded once; f64 within 1e-12 of each
+    entry's sum of |terms|."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), 'golden'))
+    import make_soft_bwd_pin as M
+    from kaolin import _fused
+    (name, fvi, fvz, H, W, sig, box, knum, mult, fnz), = [c for c in M.bench_cases() if c[0].endswith(dname)]
+    _, sel = kal.render.mesh.rasterize(H, W, T(fvz), T(fvi), T(np.zeros(fvz.shape + (1,), fvz.dtype)),
+                                       valid_faces=T(fnz >= 0))
+    mask, state = _fused.soft_mask_forward_compact(T(fvi), sel, sig, box, knum, mult)
+    up = np.random.RandomState(5).uniform(0, 1, mask.shape).astype(fvi.dtype)
+    g = A(_fused.soft_mask_backward_compact(T(up), mask, state, T(fvi), sig, mult)).reshape(-1)
+    idx, typ, prob = _decode_compact(state, H, W, knum)
+    fm = fvi * fvi.dtype.type(mult)
+    exp, ab, n = M.soft_bwd_ref(up, A(mask), A(sel), prob, idx, typ, fm, sig, mult)
+    assert n > 10000
+    exp, ab = exp.reshape(-1), ab.reshape(-1)
+    if g.dtype == np.float32:
+        assert_grads_equal(g, exp.astype(np.float32))
+    else:
+        assert np.all(np.abs(g - exp) <= 1e-12 * ab)
+
+
 @pytest.mark.parametrize('which', ['both', 'features', 'mask'])
 def test_dibr_rasterization_fused_grads_vs_oracle(kal, which):
     """The single-node dibr_rasterization backward (gather + soft terms added in place)
