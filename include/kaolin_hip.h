@@ -59,6 +59,9 @@ typedef void *(*kl_alloc_fn)(void *ctx, size_t bytes);
 
 const char *kl_last_error(void);
 int kl_abi_version(void);
+/* 1 while `stream` is being captured into a HIP graph (a caller that keeps scratch across calls
+ * gives a captured call its own buffer instead). */
+int kl_stream_is_capturing(kl_stream stream);
 
 /* Training-loop helper, not a reference op (bench.py's loss):
  *   out[0] = <a, ga> + <b, gb>   (fp32 inputs, fp64 accumulation, deterministic order).

@@ -119,6 +119,15 @@ SideFork::~SideFork() { (void)join(); }
 }  // namespace kl
 
 extern "C" const char *kl_last_error(void) { return kl::g_last_error.c_str(); }
+
+extern "C" int kl_stream_is_capturing(kl_stream stream) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(reinterpret_cast<hipStream_t>(stream), &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return cs == hipStreamCaptureStatusActive ? 1 : 0;
+}
 // 2: workspace arguments before the stream in kl_rasterize_backward, kl_dibr_soft_mask_backward(_fused),
 //    kl_unbatched_triangle_distance_backward; num_faces in kl_soft_mask_compact_bwd_workspace_bytes
 extern "C" int kl_abi_version(void) { return KL_ABI_VERSION; }

@@ -26,6 +26,10 @@ extern int g_dev_param[16];  // kl_dev_set_param (tuning sweeps; 0 = the built-i
 #define KL_DEV_STAMPS 0
 #endif
 constexpr bool kDevStamps = KL_DEV_STAMPS != 0;
+// The dev stamp buffer is shared by every stamping kernel (raster_tile_kernel and
+// soft_tile_fwd_kernel write per-wave stamps from index 0, up to ~2M entries at cfg3): the order
+// kernel's 8 stamps go this far in (the buffer must hold kOrderStampsAt + 8 entries).
+constexpr size_t kOrderStampsAt = (size_t)1 << 24;
 __device__ __forceinline__ uint64_t stamp_clk() { return __builtin_readcyclecounter(); }
 __device__ __forceinline__ uint64_t stamp_wall() { return __builtin_amdgcn_s_memrealtime(); }
 // memset as a kernel launch on `st` (graph-capture friendly); returns a kl_status

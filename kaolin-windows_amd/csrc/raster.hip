@@ -29,6 +29,8 @@
 //                                   can only be selected inside its bbox).
 #include <algorithm>
 
+#include "dibrtile.h"
+#include "rastcommon.h"
 #include "rastgrad.h"
 #include "soft_common.h"
 #include "tileorder.h"
@@ -55,26 +57,6 @@ __device__ __forceinline__ void load_face(const Src &src, const T *__restrict__ 
   r.cz = fvz[f * 3 + 2];
 }
 
-// The reference's per-(pixel, face) test, statement for statement: bbox reject, edge
-// functions, copysign(eps) normalisation, barycentric sign test.  true => (w0,w1,w2)
-// are the face's weights at the pixel centre (x0, y0).  tri_weights is the part after
-// the bbox reject.
-template <typename T>
-__device__ __forceinline__ bool tri_weights(const T *v, T x0, T y0, float eps, T &w0, T &w1, T &w2) {
-  const T aex = v[0] - x0, aey = v[1] - y0;
-  const T bex = v[2] - x0, bey = v[3] - y0;
-  const T cex = v[4] - x0, cey = v[5] - y0;
-  w0 = bex * cey - bey * cex;
-  w1 = cex * aey - cey * aex;
-  w2 = aex * bey - aey * bex;
-  T norm = w0 + w1 + w2;
-  norm = (T)((double)norm + copysign((double)eps, (double)norm));
-  w0 /= norm;
-  w1 /= norm;
-  w2 /= norm;
-  return !(w0 < (T)0 || w1 < (T)0 || w2 < (T)0);
-}
-
 template <typename T>
 __device__ __forceinline__ bool face_weights(const RastFace<T> &r, T x0, T y0, float eps, T &w0, T &w1, T &w2) {
   if (x0 < r.xmin || x0 >= r.xmax || y0 < r.ymin || y0 >= r.ymax) return false;
@@ -98,25 +80,6 @@ __device__ __forceinline__ void exact_axis(T lo, T hi, float m, int n, bool flip
   auto in = [&](int k) { return !(c(k) < lo || c(k) >= hi); };
   while (a <= b && !in(a)) a++;
   while (b >= a && !in(b)) b--;
-}
-
-// Depth-ordered visibility through one 64-bit atomicMax per covered (face, pixel):
-//   float : key = order(z0) << 32 | ~local_face   -> max depth, lowest index on ties,
-//           which is exactly the reference's `if (z0 <= max_z0) continue` fold over
-//           faces in index order;
-//   double: pass 0 maxes order(z0) (64 bit), pass 1 mins the index among the faces
-//           that reach it.
-// order() maps floats to unsigned keys monotonically with -0 == +0.  z0 = -inf never
-// wins in the reference (-inf <= -inf), so it is dropped.  A NaN z0 breaks the total
-// order (the reference then keeps the LAST passing face); such pixels are flagged and
-// re-walked sequentially by the resolve kernel.
-__device__ __forceinline__ uint32_t order32(float z) {
-  uint32_t u = __float_as_uint(z == 0.0f ? 0.0f : z);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ uint64_t order64(double z) {
-  uint64_t u = (uint64_t)__double_as_longlong(z == 0.0 ? 0.0 : z);
-  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
 }
 
 struct VisBuf {
@@ -383,10 +346,6 @@ static int launch_rast_fwd(Src src, int H, int W, int B, int D, int64_t nfaces, 
 constexpr int RT_CAP = 512;  // list entries per step: one chunk per wave
 constexpr int RT_VS = 12;    // LDS stride of a list entry: 6 coordinates, 3 depths, pad
 
-// Face records written by raster_bin_kernel: vertices x m (6), depths (3), pad (3); and
-// the exact pixel ranges of the reference's bbox test (rasterization_cuda.cu:101-104),
-// x0 | x1 << 16 and y0 | y1 << 16, empty (1, 0) for invalid faces.
-constexpr int RT_REC = 12;
 
 // VMODE: 0 all faces valid, 1 valid mask, 2 face_normals_z >= 0.  All loads are issued
 // up front (clamped index, no branch around them) and the stores come last.
@@ -526,7 +485,7 @@ __global__ void __launch_bounds__(BIN_WORD_THREADS) raster_bin_word_kernel(
   if (grp == 0 && b == 0)
     for (int t = threadIdx.x; t < nzero; t += blockDim.x) zero[t] = 0;
   uint32_t *sr = s_words, *ss = s_words + ntv;
-  const bool soft = sbitmap != nullptr;
+  const bool soft = sbitmap != nullptr, rast = bitmap != nullptr;  // (the fused tile kernel: soft bins only)
   for (int t = threadIdx.x; t < 2 * ntv; t += blockDim.x) s_words[t] = 0;
   __syncthreads();
   const int fl = grp * 512 + (int)threadIdx.x;
@@ -534,8 +493,9 @@ __global__ void __launch_bounds__(BIN_WORD_THREADS) raster_bin_word_kernel(
     int4 rt, st;
     bin_face<T, VMODE>(src, fvz, g, pp, (int64_t)b * F + fl, rec, rng, soft, srng, spad, rt, st);
     const uint32_t bit = 1u << ((fl >> 6) & 7);
-    for (int ty = rt.z; ty <= rt.w; ty++)
-      for (int tx = rt.x; tx <= rt.y; tx++) atomicOr(&sr[ty * g.tiles_x + tx], bit);
+    if (rast)
+      for (int ty = rt.z; ty <= rt.w; ty++)
+        for (int tx = rt.x; tx <= rt.y; tx++) atomicOr(&sr[ty * g.tiles_x + tx], bit);
     for (int ty = st.z; ty <= st.w; ty++)
       for (int tx = st.x; tx <= st.y; tx++) atomicOr(&ss[ty * g.tiles_x + tx], bit);
   }
@@ -545,7 +505,7 @@ __global__ void __launch_bounds__(BIN_WORD_THREADS) raster_bin_word_kernel(
   uint8_t *rb = reinterpret_cast<uint8_t *>(bitmap), *sb = reinterpret_cast<uint8_t *>(sbitmap);
   for (int t = threadIdx.x; t < ntv; t += blockDim.x) {
     const size_t o = bm_index(g.ntiles(), base + t, word) * 4 + byte;
-    rb[o] = (uint8_t)sr[t];
+    if (rast) rb[o] = (uint8_t)sr[t];
     if (soft) sb[o] = (uint8_t)ss[t];
   }
 }
@@ -1803,6 +1763,31 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   uint2 *srng = reinterpret_cast<uint2 *>(w + L.off_srng);
   const RastSrc<T> src{fvi, nullptr, (T)m, fnz};
   const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
+  if constexpr (sizeof(T) == 4) {
+    // the fused tile kernel (dibrtile.hip): the soft bins only, one order, ONE kernel for the
+    // rasterizer and the soft mask (needs bboxes inside the enlarged ones: boxlen >= 0; dev param
+    // 10 = 1 keeps the two-kernel path below, for A/B timing)
+    if (pad >= 0.0 && bin_word_lds_ok(g) && nt <= ORD_LDS_TILES && g_dev_param[10] != 1) {
+      KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, nullptr, rec, rng, sbm, srng, (T)pad, rgh,
+                                     (int)((L.zero - L.off_rgh) / sizeof(int)), st));
+      const int lpm = dt_lp_min(K);
+      // block 1 orders; block 0 zeroes the state's counters; the rest zero the backward's accumulator
+      const unsigned og = g_dev_param[9] >= 2 ? (unsigned)g_dev_param[9] : 256u;
+      hipLaunchKernelGGL(tile_countorder2_kernel, dim3(og), dim3(1024), 0, st, (const uint32_t *)sbm,
+                         (const uint32_t *)sbm, g.words, (int32_t *)nullptr, 0, 0, (int *)nullptr, sorder, nt, lpm,
+                         snitems, soft_split(), 0, bcnt, DibrState::kZeroInts, bacc, (size_t)B * F * 6,
+                         kDevStamps && g_dev_debug ? reinterpret_cast<uint64_t *>(g_dev_debug) + kOrderStampsAt
+                                                   : nullptr);
+      KL_CHECK_LAUNCH();
+      const DibrTileArgs da{reinterpret_cast<const float *>(rec), rng, srng,
+                            SoftSrc<float>{reinterpret_cast<const float *>(fvi), (float)m, (float)pad},
+                            reinterpret_cast<const float *>(feat), sbm, sorder, snitems, g, F, D, K, eps, sigmainv,
+                            m, reinterpret_cast<float *>(out_feat), out_idx, reinterpret_cast<float *>(out_w),
+                            reinterpret_cast<float *>(out_mask), s.hits, s.rec_face,
+                            reinterpret_cast<float *>(s.rec_prob), s.seg_tot, bitems, bcnt, S.cap};
+      return dibr_tile_launch(da, lpm, soft_items_bound(nt, lpm, soft_split()), st);
+    }
+  }
   if (bin_word_lds_ok(g) && !(g_dev_flags & (1 << 14))) {  // dev bit 14: the atomic binning
     KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, rbm, rec, rng, sbm, srng, (T)pad, rgh,
                                    (int)((L.zero - L.off_rgh) / sizeof(int)), st));  // + histograms zeroed
@@ -1827,7 +1812,8 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     hipLaunchKernelGGL(tile_countorder2_kernel, dim3(og), dim3(1024), 0, st, (const uint32_t *)rbm,
                        (const uint32_t *)sbm, g.words, items, split_from, split_log2, nitems, sorder, nt,
                        soft_lp_min(K), snitems, soft_split(), 1, bcnt, DibrState::kZeroInts, bacc,
-                       (size_t)B * F * 6, kDevStamps ? reinterpret_cast<uint64_t *>(g_dev_debug) : nullptr);
+                       (size_t)B * F * 6,
+                       kDevStamps && g_dev_debug ? reinterpret_cast<uint64_t *>(g_dev_debug) + kOrderStampsAt : nullptr);
     KL_CHECK_LAUNCH();
   } else {  // counts (a wave per tile) then orders (dev bit 20: this path, for A/B timing)
     hipLaunchKernelGGL(tile_bucket2_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)rbm,

@@ -172,6 +172,18 @@ struct FaceHash {
   }
 };
 
+// Forward work items (tileorder.h, order_soft_items): a 4-wave workgroup takes 8 >> lp rows of
+// a tile with Q = 4 / (8 >> lp) waves per row.
+constexpr int ST_WAVES = 4;
+// Backward work items: a forward item's hits taken row-major in pieces of SB_PIECE (one hit per
+// thread of a backward workgroup).
+constexpr int SB_PIECE = 512;
+// LDS of one row: its [K][64] slot lists (face ids, then probabilities in place), the
+// filled-slot prefix and the hit total
+__host__ __device__ constexpr size_t st_row_lds(int K) {
+  return (size_t)K * 64 * sizeof(uint32_t) + 72 * sizeof(int);  // slots | prefix, total
+}
+
 // Shards of the soft-mask backward's work-item list (counters DS_CNT_STRIDE ints apart, one per
 // 64-byte line): the fused forward appends to shard blockIdx % DS_SHARDS.
 constexpr int DS_SHARDS = 8;

@@ -38,12 +38,6 @@
 
 namespace kl {
 
-// Forward work items (tileorder.h, order_soft_items): a 4-wave workgroup takes 8 >> lp rows of
-// a tile with Q = 4 / (8 >> lp) waves per row.
-constexpr int ST_WAVES = 4;
-// Backward work items: a forward item's hits taken row-major in pieces of SB_PIECE (one hit per
-// thread of a backward workgroup).
-constexpr int SB_PIECE = 512;
 
 template <typename T>
 struct SoftTileArgs {
@@ -74,16 +68,12 @@ struct SoftTileArgs {
   int bwd_cap = 0;
 };
 
-// LDS of one row: its [K][64] slot lists (face ids, then probabilities in place), the
-// filled-slot prefix and the hit total
-__host__ __device__ constexpr size_t st_row_lds(int K) {
-  return (size_t)K * 64 * sizeof(uint32_t) + 72 * sizeof(int);  // slots | prefix, total
-}
 
 // The workgroup's face list: the candidate chunks' faces touching its rows, in index order
 // (face id; lane interval lo | hi << 6 and row bits << 12), refilled when full.
-constexpr int ST_LIST_CAP = 1024;
-constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int); }
+constexpr int ST_LIST_CAP = 960;  // (40.6 KB of LDS at knum 30 with 4 rows: 4 workgroups per CU)
+// list | per-wave scratch (16 ints) | the multi-wave walk's per-round counts ([Q][64] per row)
+constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int) + ST_WAVES * 64 * sizeof(int); }
 
 // Forward, one work item (a part of a tile's rows) per 4-wave workgroup: fill and walk (1a,
 // 1b below), the dense evaluation by the row's Q waves, the mask by its first wave.
@@ -233,8 +223,9 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
           amask = ballot(active);
         }
       } else {
-        // per-wave counts of this round, in the LDS of an unused row (RP <= 2)
-        int *s_cnt = reinterpret_cast<int *>(smem + st_head_lds() + st_row_lds(K) * (RP + r));
+        // per-wave counts of this round ([Q][64] per row, in the head: with knum > 55 the rows
+        // past RP are not allocated)
+        int *s_cnt = reinterpret_cast<int *>(smem + (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int)) + r * Q * 64;
         for (int b0 = 0; b0 < nb; b0 += Q) {  // workgroup-uniform rounds
           const int blk = b0 + qi;
           uint64_t cm = 0;

@@ -326,6 +326,7 @@ static __global__ void __launch_bounds__(1024) tile_countorder2_kernel(
   if (dbg && threadIdx.x == 0) dbg[0] = stamp_wall();
   if (!soft && zero)
     for (int i = threadIdx.x; i < nzero; i += blockDim.x) zero[i] = 0;
+  if (!soft && order0 == nullptr) return;  // one order only (the fused tile kernel's)
   for (int i = threadIdx.x; i < ORD_HIST; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   for (int t = threadIdx.x; t < nt; t += blockDim.x) {

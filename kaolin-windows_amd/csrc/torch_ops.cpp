@@ -40,8 +40,12 @@ kl_dtype dtype_code(at::ScalarType t) {
 
 // scratch reused across calls on one (device, stream), grown to the largest request: every entry
 // point treats its workspace as uninitialised and is done with it when the stream reaches the
-// call's end (the Python path's _native.workspace)
+// call's end (the Python path's _native.workspace).  A call being captured into a graph gets its
+// own buffer from the graph's memory pool instead (graphs replayed concurrently do not share it,
+// and a later, larger request cannot free what a graph points at).
 at::Tensor workspace(size_t bytes, const at::Device &dev, int64_t stream) {
+  if (kl_stream_is_capturing((kl_stream)stream))
+    return at::empty({(int64_t)std::max<size_t>(bytes, 16)}, at::TensorOptions().dtype(at::kByte).device(dev));
   static std::mutex mu;
   static std::map<std::pair<int, int64_t>, at::Tensor> cache;
   std::lock_guard<std::mutex> lock(mu);

@@ -36,6 +36,7 @@ _PP = ctypes.POINTER(ctypes.c_void_p)
 _SIGS = {
     'kl_last_error': (ctypes.c_char_p, []),
     'kl_abi_version': (_I, []),
+    'kl_stream_is_capturing': (_I, [_P]),
     'kl_loss_dot2_workspace_bytes': (ctypes.c_size_t, []),
     'kl_loss_dot2': (_I, [_P, _P, _I64, _P, _P, _I64, _P, _P, _P]),
     'kl_rasterize_workspace_bytes': (_SZ, [_I, _I, _I, _I64]),
@@ -213,12 +214,18 @@ def workspace(nbytes, device):
     call's end, so stream order makes reuse safe.  Grows to the largest request; the current
     stream is part of the key (graph capture has its own stream, hence its own buffer)."""
     nbytes = max(int(nbytes), 16)
+    if capturing(device):
+        # a captured call gets its own buffer from the graph's private memory pool, which the graph
+        # keeps for its replays: graphs captured on one stream do not share scratch (concurrent
+        # replays), and a later, larger request cannot free memory an earlier graph points at
+        return torch.empty(nbytes, dtype=torch.uint8, device=device)
     key = (device.index, stream_of(device))
     t = _WS.get(key)
     if t is None or t.numel() < nbytes:
         t = torch.empty(nbytes, dtype=torch.uint8, device=device)
         _WS[key] = t
     return t
+
 
 
 def require_gpu(func, *tensors):

@@ -4,6 +4,7 @@ GPU f32 / f64 masks take the fused HIP path (csrc/maskiou.hip: one pass for both
 one for both gradients); other inputs run the reference's torch ops."""
 import torch
 from torch.autograd import Function
+from torch.autograd.function import once_differentiable
 
 from .. import _native as N
 
@@ -31,6 +32,7 @@ class MaskIouHip(Function):
         return loss
 
     @staticmethod
+    @once_differentiable  # its backward is one opaque HIP call: a double backward raises, not drops
     def backward(ctx, grad):
         lhs, rhs, up, down = ctx.saved_tensors
         need_l, need_r = ctx.needs_input_grad

@@ -66,7 +66,9 @@ def trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin=None, scale
     else:
         # nothing read back per round (graph-capturable); one status read per call in eager mode
         F = faces.shape[0]
-        cap = min(max(16 * F, 1 << 20), 1 << 26)
+        # ping-pong triangle buffers (2 x cap x 9 coordinates): capped at 2^23 triangles (0.6 GB in
+        # f32) -- work past the cap is finished depth-first by the thread holding it, same grid
+        cap = min(max(16 * F, 1 << 20), 1 << 23)
         code = N.dtype_code(work.dtype)
         nb = lib.kl_voxelgrid_mark_async_workspace_bytes(code, cap)
         ws = torch.empty(nb, dtype=torch.uint8, device=dev)

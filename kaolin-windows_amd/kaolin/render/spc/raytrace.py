@@ -23,8 +23,10 @@ def unbatched_raytrace(octree, point_hierarchy, pyramid, exsum, origin, directio
     level, raytrace_cuda.cu:557-560): fixed-size outputs of ``capacity`` rows and nothing read
     back, so the call can be captured into a CUDA/HIP graph.  Then a fourth (third without depth)
     value is returned, ``result`` (2,) int64 on the device = (rows written, 1 if the march held
-    more than ``capacity`` nuggets at some level; the rows are then the first ``capacity`` rows
-    of the full answer).  Rows past result[0] hold index -1 and depth 0."""
+    more than ``capacity`` nuggets at some level).  The rows written are always the first
+    result[0] rows of the full answer; after a truncation (result[1] == 1) result[0] <= capacity --
+    a level truncated early can lose descendants that later levels would have culled anyway, so
+    fewer than ``capacity`` rows may come back.  Rows past result[0] hold index -1 and depth 0."""
     if capacity is not None:
         out = _C.render.spc.raytrace_fixed_cuda(octree.contiguous(), point_hierarchy.contiguous(),
                                                  pyramid.contiguous(), exsum.contiguous(), origin.contiguous(),

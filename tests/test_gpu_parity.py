@@ -556,6 +556,79 @@ def test_dibr_rasterization_fused_grads_vs_oracle(kal, which):
     assert torch.equal(a.grad, g1)
 
 
+def _dev_param(idx, val):
+    import ctypes
+    from kaolin import _native as N
+    lib = N.lib()
+    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.kl_dev_set_param(idx, val)
+
+
+def _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box=0.02):
+    from kaolin import _fused
+    f, i, w, m, st, rg = _fused.dibr_forward(H, W, fvz, fvi, feat, fnz, 7000., box, K, 1000., 1e-8)
+    from dibr_util import state_arrays
+    hits, rf, rp = state_arrays(st)
+    seg = A(st.seg_tot)
+    # the records of each row segment up to its hit total (the rest of a segment is unwritten)
+    R = 64 * K
+    keep = (np.arange(R)[None, :] < seg[:, None]).reshape(-1) if K > 0 else np.zeros(0, bool)
+    return [A(f), A(i), A(w), A(m), hits, seg, rf[:keep.size][keep], rp[:keep.size][keep], A(rg)]
+
+
+@pytest.mark.parametrize('case', ['bench', 'adversarial', 'knum64', 'knum255', 'bigbox'])
+def test_dibr_fused_tile_kernel_equals_two_kernel_path(kal, case):
+    """kl_dibr_forward's fused tile kernel (dibrtile.hip: the rasterizer and the soft mask in one
+    kernel over one chunk expansion) against its two-kernel path (dev param 10 = 1: raster_tile_kernel
+    then soft_tile_fwd_kernel): face_idx, weights, features, soft mask, the compact state's hits /
+    row totals / records, face ranges -- bit for bit; on the bench mesh, adversarial faces (NaN /
+    inf / ties / duplicates / big faces), knum 64 and 255 (1-2 rows per work item), and a large
+    boxlen whose enlarged bboxes overflow the kernel's LDS soft list (its second expansion)."""
+    import bench
+    if case in ('adversarial',):
+        z, v, f = _adversarial_faces(torch.float32)
+        fvz, fvi, feat = T(np.concatenate([z, z[:, ::-1]])), T(np.concatenate([v, v[:, ::-1]])), \
+            T(np.concatenate([f, f[:, ::-1]]))
+        fnz = T(np.random.default_rng(2).uniform(-0.3, 1, fvz.shape[:2]).astype(np.float32))
+        H, W, K, box = 97, 130, 30, 0.02
+    else:
+        inp = bench.dibr_inputs([0.3, 2.0], DEV, H=96, W=128)
+        fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+        H, W = 96, 128
+        K = {'knum64': 64, 'knum255': 255}.get(case, 30)
+        box = 0.2 if case == 'bigbox' else 0.02
+    try:
+        fused = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box)
+        _dev_param(10, 1)
+        two = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box)
+    finally:
+        _dev_param(10, 0)
+    names = ['features', 'face_idx', 'weights', 'soft_mask', 'hits', 'seg_tot', 'rec_face', 'rec_prob', 'ranges']
+    for n, x, y in zip(names, fused, two):
+        assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
+    assert fused[4].max() > 0  # the soft mask has hits
+
+
+def test_soft_mask_compact_knum_over_55(kal):
+    """knum > 55 puts at most 2 rows in a soft-mask work item (softtile.hip soft_lp_min), so
+    every row is walked by 2-4 waves: the compact standalone soft mask against the oracle there."""
+    from kaolin import _fused
+    import bench
+    inp = bench.dibr_inputs([0.3], DEV, H=64, W=96)
+    fvi = inp['fvi']
+    _, sel = kal.render.mesh.rasterize(64, 96, inp['fvz'], fvi, inp['feat'], valid_faces=inp['fnz'] >= 0)
+    for K in (64, 200):
+        mask, state = _fused.soft_mask_forward_compact(fvi, sel, 7000., 0.05, K, 1000.)
+        fm = A(fvi) * np.float32(1000.)
+        pad = np.float32(0.05 * 1000.)
+        bb = np.concatenate([fm.min(-2) - pad, fm.max(-2) + pad], -1)
+        om, op, oi, ot = orc.dibr_soft_mask_forward(fm, bb, A(sel), 7000., K, 1000.)
+        np.testing.assert_allclose(A(mask), om, rtol=1e-6, atol=1e-7)
+        idx, typ, prob = _decode_compact(state, 64, 96, K)
+        assert np.array_equal(idx, oi) and np.array_equal(typ, ot)
+        assert (oi >= 0).sum(-1).max() > 30  # deep slot lists
+
+
 def test_compiled_node_equals_python_node(kal, monkeypatch):
     """csrc/torch_ops.cpp's compiled autograd node (the eager default) against the ctypes / Python
     node (kaolin/_fused.py): forward and gradients bit-equal, features as a list, a retained
