@@ -214,8 +214,18 @@ def cpu_info():
                 break
     except OSError:
         pass
-    all_threads = int(os.environ.get('OMP_NUM_THREADS') or os.cpu_count() or 1)
-    return {'model': model, 'visible_cpus': os.cpu_count(), 'threads_used_for_nproc_leg': all_threads}
+    # the "all threads" CPU legs use the process's share of the host: OMP_NUM_THREADS when set (the
+    # GPU box sets it to its 16-CPU share; os.cpu_count() there reports the whole machine's CPUs,
+    # which this job may not use), else the CPUs the process may run on
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    all_threads = int(os.environ.get('OMP_NUM_THREADS') or affinity or 1)
+    return {'model': model, 'visible_cpus': os.cpu_count(), 'affinity_cpus': affinity,
+            'threads_used_for_nproc_leg': all_threads,
+            'threads_source': 'OMP_NUM_THREADS (the job\'s CPU share)' if os.environ.get('OMP_NUM_THREADS')
+            else 'sched_getaffinity'}
 
 
 def median_time(fn, reps=5):
@@ -506,11 +516,21 @@ def dibr_headline(args, world, rank, device):
         ref = dibr_step(inp, world)
         gstep()
         torch.cuda.synchronize()
-        # the replayed graph must reproduce the eager step (forward bit-exact, grads to float order)
-        ok = torch.equal(gout[4], ref[4]) and torch.equal(gout[3], ref[3]) and \
-            torch.allclose(gout[1], ref[1], rtol=1e-4, atol=1e-5) and torch.allclose(gout[2], ref[2], rtol=1e-4, atol=1e-5)
+        # the replayed graph must reproduce the eager step: forward bit-exact; gradients bit-exact
+        # (the float terms sum exactly in double), save the documented one-ulp allowance where a
+        # face's terms span more than ~2^29 -- at most 1 element in 10^4 (tests/dibr_util.py)
+        ok = torch.equal(gout[4], ref[4]) and torch.equal(gout[3], ref[3])
+        replay_grad_diffs = 0
+        for a, b in ((gout[1], ref[1]), (gout[2], ref[2])):
+            ne = a != b
+            n = int(ne.sum())
+            replay_grad_diffs += n
+            if n:
+                ulps = (a[ne].view(torch.int32).long() - b[ne].view(torch.int32).long()).abs().max()
+                ok = ok and n <= max(1, a.numel() // 10000) and int(ulps) <= 1
         if not ok:
             raise RuntimeError('graph replay differs from the eager step')
+        replay_check = {'forward_bit_equal': True, 'grad_elements_not_bit_equal': replay_grad_diffs}
         for _ in range(args.warmup):
             gstep()
         rank_times = per_rank(timed_loop(gstep, args.steps, world, device), device, world)
@@ -518,6 +538,7 @@ def dibr_headline(args, world, rank, device):
         mode = 'hip_graph'
     else:
         rank_times = eager_times
+        replay_check = None
     pg = process_group_info(world)
     if pg['world_size'] != world:
         raise RuntimeError(f'process group has {pg["world_size"]} ranks, WORLD_SIZE says {world}')
@@ -549,7 +570,7 @@ def dibr_headline(args, world, rank, device):
                          'scope': 'whole fwd+bwd step, SURVEY.md 8d cfg3 bytes (reference layout)',
                          'bytes_per_step': sb, 'achieved': round(sb / (elapsed / args.steps) / 1e9, 1),
                          'frac': round(sb / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}},
-        'ops': ops_report, 'workload_stats': stats, 'mode': mode,
+        'ops': ops_report, 'workload_stats': stats, 'mode': mode, 'graph_replay_check': replay_check,
         'process_group': dict(pg, per_rank_ms_per_step=[round(t / args.steps * 1e3, 4) for t in rank_times],
                               devices_visible=torch.cuda.device_count()),
         'eager': {'value': round(pixels / eager_elapsed / 1e6, 2),

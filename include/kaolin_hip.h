@@ -336,10 +336,11 @@ int kl_deftet_sparse_render_backward(kl_dtype dtype, int64_t batch_size, int64_t
 
 /* unbatched_triangle_distance.cpp:43-72.  points (P,3), face_vertices (F,3,3).
  * Outputs dist (P), face_idx (P) int64, dist_type (P) int32. dtype KL_F32 | KL_F64.
- * workspace (optional, NULL allowed): kl_unbatched_triangle_distance_workspace_bytes(P)
- * bytes, used to process points in Morton order so that whole waves can skip faces
- * that provably cannot be their nearest (results are unchanged). */
-size_t kl_unbatched_triangle_distance_workspace_bytes(int64_t num_points);
+ * workspace (optional, NULL allowed): kl_unbatched_triangle_distance_workspace_bytes(P, F)
+ * bytes, used to process points in Hilbert order so that whole waves can skip faces
+ * that provably cannot be their nearest, and to hold per-face records computed once per
+ * call (results are unchanged). */
+size_t kl_unbatched_triangle_distance_workspace_bytes(int64_t num_points, int64_t num_faces);
 int kl_unbatched_triangle_distance_forward(kl_dtype dtype, int64_t num_points, int64_t num_faces,
                                            const void *points, const void *face_vertices,
                                            void *dist, int64_t *face_idx, int32_t *dist_type,

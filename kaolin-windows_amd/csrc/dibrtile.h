@@ -30,6 +30,8 @@ struct DibrTileArgs {
   int2 *bwd_items;
   int *bwd_cnt;
   int bwd_cap;
+  int dev;  // dev param 12 (timing breakdowns; outputs invalid when set): 1 = stop after the
+            // rasterizer's outputs, 2 = skip the pair ranking, 3 = stop after the expansion
 };
 
 // fewest rows per work item (lp >= 1) for knum (order_soft_items' lp_min)

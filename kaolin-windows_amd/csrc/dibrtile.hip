@@ -167,6 +167,10 @@ __global__ void __launch_bounds__(256) dibr_tile_kernel(DibrTileArgs a) {
     }
     slen += stot;
     __syncthreads();
+    if (a.dev >= 2) {
+      __syncthreads();
+      return;
+    }
     // this row's (pixel, face) pairs of the step, 64 entries at a time, evaluated densely by the
     // row's Q waves: pair t belongs to the entry whose exclusive width prefix is the last <= t.
     // Each pair ranks its depth in the pixel's key (max depth, lowest index on ties: the
@@ -222,6 +226,7 @@ __global__ void __launch_bounds__(256) dibr_tile_kernel(DibrTileArgs a) {
     if (!more) break;
     step(PB, PA);
   }
+  if (a.dev == 3) return;
 
   // ---- 2. the rasterizer's outputs; the covered pixels of each row
   int win = -1;
@@ -268,6 +273,7 @@ __global__ void __launch_bounds__(256) dibr_tile_kernel(DibrTileArgs a) {
     if (lane == 0) s_cov[r] = cm;
   }
   __syncthreads();  // s_cov written; the step buffers and keys are dead from here on
+  if (a.dev == 1) return;
 
   // ---- 3. the soft mask's selection: per row, the first knum candidates (index order) of each
   //         uncovered pixel, over the soft list (softtile.hip, soft_tile_fwd_kernel 1b)

@@ -81,9 +81,17 @@ __device__ __forceinline__ void make_face(const T *v, FaceRec<T> &r) {
   r.thick = fmax(fabs(dot(r.e12, r.un)), fabs(dot(r.e31, r.un))) + (T)(64.0 / 16777216.0) * hm;
 }
 
-// squared distance (as float, :302) + type of one point to one face
+// The evaluation half of FaceRec as a global record (p2m_fwd_grec_kernel): a wave reads one
+// face's record with a wave-uniform index, so it comes through scalar loads into SGPRs.
 template <typename T>
-__device__ __forceinline__ float point_face(const V3<T> &p, const FaceRec<T> &f, int &type) {
+struct alignas(16) FaceRecS {
+  V3<T> v1, v2, v3, e12, e23, e31, un, en12, en23, en31;
+  T l12, l23, l31, pad0, pad1, pad2;
+};
+
+// squared distance (as float, :302) + type of one point to one face (R = FaceRec / FaceRecS)
+template <typename T, typename R>
+__device__ __forceinline__ float point_face(const V3<T> &p, const R &f, int &type) {
   const V3<T> pv1 = p - f.v1, pv2 = p - f.v2, pv3 = p - f.v3;
   const T uab = dot(pv1, f.e12) / f.l12;
   const T uca = dot(pv3, f.e31) / f.l31;
@@ -133,8 +141,9 @@ struct PruneTile {
   T dv[P2M_TILE];
 };
 
+// out[0..8] = o_e (3 per edge), out[9..11] = off_e, out[12] = dv
 template <typename T>
-__device__ __forceinline__ void make_prune(const FaceRec<T> &r, PruneTile<T> &pt, int s) {
+__device__ __forceinline__ void make_prune_vals(const FaceRec<T> &r, T *out) {
   const V3<T> e[3] = {r.e12, r.e23, r.e31};
   const V3<T> a[3] = {r.v1, r.v2, r.v3};
   const V3<T> b[3] = {r.v2, r.v3, r.v1};
@@ -147,12 +156,23 @@ __device__ __forceinline__ void make_prune(const FaceRec<T> &r, PruneTile<T> &pt
     o = o * inv;
     if (dot(opp[k] - a[k], o) > (T)0) o = mk(-o.x, -o.y, -o.z);
     const T d0 = dot(a[k], o), d1 = dot(b[k], o), d2 = dot(opp[k], o);
-    pt.o[3 * k][s] = o.x;
-    pt.o[3 * k + 1][s] = o.y;
-    pt.o[3 * k + 2][s] = o.z;
-    pt.off[k][s] = fmax(fmax(d0, d1), d2) + slack;
+    out[3 * k] = o.x;
+    out[3 * k + 1] = o.y;
+    out[3 * k + 2] = o.z;
+    out[9 + k] = fmax(fmax(d0, d1), d2) + slack;
   }
-  pt.dv[s] = dot(r.v1, r.un);
+  out[12] = dot(r.v1, r.un);
+}
+
+template <typename T>
+__device__ __forceinline__ void make_prune(const FaceRec<T> &r, PruneTile<T> &pt, int s) {
+  T v[13];
+  make_prune_vals<T>(r, v);
+#pragma unroll
+  for (int k = 0; k < 9; k++) pt.o[k][s] = v[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) pt.off[k][s] = v[9 + k];
+  pt.dv[s] = v[12];
 }
 
 // Face skipping.  The reference's fold (first face of each 512-face tile taken
@@ -313,6 +333,155 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
     atomicAdd(&::kl::g_p2m_evaluated, g_p2m_evaluated);
   }
 #endif
+  if (!valid) return;
+  if (f_end > f_begin && ((first_split && f_end <= 512) || best > tbest)) {
+    best = tbest; best_f = tbest_f; best_t = tbest_t;
+  }
+  if (part_dist) {
+    const int64_t o = (int64_t)blockIdx.y * P + si;
+    part_dist[o] = best;
+    part_idx[o] = best_f;
+    part_type[o] = best_t;
+  } else {
+    out_dist[pi] = best;
+    out_idx[pi] = best_f;
+    out_type[pi] = best_t;
+  }
+}
+
+// ---- global face records (the sorted path): p2m_faces_kernel writes, once per call, each face's
+// evaluation record (FaceRecS) and its pruning record as structure-of-arrays rows of length Fp:
+// rows 0..12 = make_prune_vals, 13..15 = un, 16 = thick, 17 = hmax.
+constexpr int P2M_PR_ROWS = 18;
+
+template <typename T>
+__global__ void __launch_bounds__(256) p2m_faces_kernel(const T *__restrict__ fv, int64_t F, int64_t Fp,
+                                                         FaceRecS<T> *__restrict__ rec, T *__restrict__ pr) {
+  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  FaceRec<T> r;
+  make_face<T>(fv + f * 9, r);
+  FaceRecS<T> g;
+  g.v1 = r.v1; g.v2 = r.v2; g.v3 = r.v3;
+  g.e12 = r.e12; g.e23 = r.e23; g.e31 = r.e31;
+  g.un = r.un; g.en12 = r.en12; g.en23 = r.en23; g.en31 = r.en31;
+  g.l12 = r.l12; g.l23 = r.l23; g.l31 = r.l31;
+  g.pad0 = g.pad1 = g.pad2 = (T)0;
+  rec[f] = g;
+  T v[13];
+  make_prune_vals<T>(r, v);
+#pragma unroll
+  for (int k = 0; k < 13; k++) pr[k * Fp + f] = v[k];
+  pr[13 * Fp + f] = r.un.x;
+  pr[14 * Fp + f] = r.un.y;
+  pr[15 * Fp + f] = r.un.z;
+  pr[16 * Fp + f] = r.thick;
+  pr[17 * Fp + f] = r.hmax;
+}
+
+// p2m_fwd_kernel with the face records read from global memory instead of staged through LDS:
+// each lane reads its face's pruning record (coalesced rows), and the evaluation loop reads the
+// picked face's record with a wave-uniform index -- scalar loads, the record in SGPRs -- so
+// the records take no VGPRs and no LDS, and the waves of a block never synchronise.  Same
+// skipping test, same fold, same results.
+template <typename T, bool PAIR>
+__global__ void __launch_bounds__(256) p2m_fwd_grec_kernel(const T *__restrict__ pts,
+                                                            const FaceRecS<T> *__restrict__ rec,
+                                                            const T *__restrict__ pr, int64_t Fp,
+                                                            const int32_t *__restrict__ order, int64_t P, int64_t F,
+                                                            int64_t split_faces, T *__restrict__ out_dist,
+                                                            int64_t *__restrict__ out_idx, int32_t *__restrict__ out_type,
+                                                            T *__restrict__ part_dist, int64_t *__restrict__ part_idx,
+                                                            int32_t *__restrict__ part_type,
+                                                            const int32_t *__restrict__ bounds, uint32_t *gbest) {
+  const int64_t si = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const bool valid = si < P;
+  const int64_t pi = valid ? (int64_t)order[si] : 0;
+  const bool first_split = blockIdx.y == 0;
+  const int64_t f_begin = (int64_t)blockIdx.y * split_faces;
+  const int64_t f_end = min(F, f_begin + split_faces);
+  const int lane = threadIdx.x & 63;
+  V3<T> p = mk((T)0, (T)0, (T)0);
+  if (valid) p = mk(pts[pi * 3], pts[pi * 3 + 1], pts[pi * 3 + 2]);
+  const V3<T> p0 = mk(__shfl(p.x, 0), __shfl(p.y, 0), __shfl(p.z, 0));
+  const V3<T> q = valid ? p : p0;
+  const bool fin = isfinite(q.x) && isfinite(q.y) && isfinite(q.z);
+  const bool all_fin = __all(fin);
+  V3<T> c = mk((T)0, (T)0, (T)0);
+  T R = (T)INFINITY, cinf = (T)0;
+  if (all_fin) {
+    c = mk((wave_min(q.x) + wave_max(q.x)) * (T)0.5, (wave_min(q.y) + wave_max(q.y)) * (T)0.5,
+           (wave_min(q.z) + wave_max(q.z)) * (T)0.5);
+    const V3<T> dq = q - c;
+    R = wave_max(kl_sqrt<T>(dot(dq, dq))) * (T)(1.0 + 16.0 * P2M_E);
+    cinf = fmax(fmax(fabs(c.x), fabs(c.y)), fabs(c.z));
+  }
+  const bool share = gbest != nullptr && all_fin && bounds[6] != 0 && cinf + R < (T)1e15;
+  float published = INFINITY;
+  T best = (T)INFINITY, tbest = (T)INFINITY;
+  int64_t best_f = 0, tbest_f = 0;
+  int best_t = 0, tbest_t = 0;
+  auto fold = [&](int64_t f, float d, int t) {
+    if ((f & 511) == 0) {
+      if (f > f_begin && ((first_split && f == 512) || best > tbest)) {
+        best = tbest; best_f = tbest_f; best_t = tbest_t;
+      }
+      tbest = (T)d; tbest_f = f; tbest_t = t;
+    } else if (tbest > (T)d) {
+      tbest = (T)d; tbest_f = f; tbest_t = t;
+    }
+  };
+  for (int64_t start = f_begin; start < f_end; start += 64) {
+    const int n = (int)min((int64_t)64, f_end - start);
+    T thr = fmin(best, tbest);
+    if (thr != thr || !valid) thr = valid ? (T)INFINITY : (T)0;
+    if (share && valid && (start & 127) == 0)
+      thr = fmin(thr, (T)__uint_as_float(__hip_atomic_load(gbest + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+    const T thr_max = wave_max(thr);
+    const int64_t f = start + lane;
+    bool eval = lane < n;
+    if (eval && all_fin && (f & 511) != 0 && thr_max < (T)INFINITY) {
+      const T *r = pr + f;
+      const T hmax = r[17 * Fp], thick = r[16 * Fp];
+      const V3<T> un = mk(r[13 * Fp], r[14 * Fp], r[15 * Fp]);
+      const T M = cinf + R + hmax;
+      const T sl = (T)(256.0 * P2M_E) * M;
+      const T A = fmax(fabs(dot(c, un) - r[12 * Fp]) - thick - sl, (T)0);
+      T b = dot(c, mk(r[0], r[Fp], r[2 * Fp])) - r[9 * Fp];
+      b = fmax(b, dot(c, mk(r[3 * Fp], r[4 * Fp], r[5 * Fp])) - r[10 * Fp]);
+      b = fmax(b, dot(c, mk(r[6 * Fp], r[7 * Fp], r[8 * Fp])) - r[11 * Fp]);
+      const T B = fmax(b - sl, (T)0);
+      const T K = (R + kl_sqrt<T>(thr_max)) * (T)(1.0 + 16.0 * P2M_E) + sl;
+      if ((A * A + B * B) * (T)(1.0 - 32.0 * P2M_E) > K * K * (T)(1.0 + 32.0 * P2M_E)) eval = false;
+    }
+    uint64_t mask = __ballot(eval);
+    while (mask) {
+      const int sj = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      if (PAIR && mask) {
+        const int sk = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        int t0, t1;
+        const FaceRecS<T> fa = rec[start + sj], fb = rec[start + sk];
+        const float d0 = point_face<T>(p, fa, t0);
+        const float d1 = point_face<T>(p, fb, t1);
+        fold(start + sj, d0, t0);
+        fold(start + sk, d1, t1);
+      } else {
+        int t;
+        const FaceRecS<T> fa = rec[start + sj];
+        const float d = point_face<T>(p, fa, t);
+        fold(start + sj, d, t);
+      }
+    }
+    if (share && valid && ((start + 64) & 127) == 0) {
+      const float cur = (float)fmin(best, tbest);
+      if (cur < published) {
+        atomicMin(gbest + si, __float_as_uint(cur));
+        published = cur;
+      }
+    }
+  }
   if (!valid) return;
   if (f_end > f_begin && ((first_split && f_end <= 512) || best > tbest)) {
     best = tbest; best_f = tbest_f; best_t = tbest_t;
@@ -503,8 +672,9 @@ static int g_p2m_target_blocks = 10240;
 constexpr int P2M_BOUND_BLOCKS = 64;  // blocks of p2m_bounds_kernel
 
 struct P2MWs {
-  size_t keys_in, keys_out, vals_in, vals_out, temp, temp_bytes, part, gbest, bytes;
-  explicit P2MWs(int64_t P) {
+  size_t keys_in, keys_out, vals_in, vals_out, temp, temp_bytes, part, gbest, rec, pr, bytes;
+  int64_t Fp;
+  P2MWs(int64_t P, int64_t F, size_t esize) {
     size_t tb = 0;
     (void)hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                        (const int32_t *)nullptr, (int32_t *)nullptr, (int)P, 0, P2M_KEY_BITS);
@@ -517,7 +687,10 @@ struct P2MWs {
     temp_bytes = tb;
     part = temp + al(tb);  // P2M_MAX_SPLITS x P x (dist 8 + idx 8 + type 4)
     gbest = part + al((size_t)P2M_MAX_SPLITS * P * 20);  // P x float bits (shared thresholds)
-    bytes = gbest + al(4 * (size_t)P);
+    Fp = (F + 63) & ~(int64_t)63;
+    rec = gbest + al(4 * (size_t)P);  // F x FaceRecS (36 values), then P2M_PR_ROWS rows of Fp
+    pr = rec + al((size_t)F * 36 * esize);
+    bytes = pr + al((size_t)P2M_PR_ROWS * Fp * esize);
   }
 };
 
@@ -728,7 +901,7 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
   int splits = 1;
   int64_t split_faces = F;
   if (ws && P * F >= P2M_SORT_MIN_PAIRS) {
-    const P2MWs L(P);
+    const P2MWs L(P, F, sizeof(T));
     KL_REQUIRE(ws_bytes >= L.bytes, "unbatched_triangle_distance_forward: workspace too small");
     char *w = reinterpret_cast<char *>(ws);
     int32_t *bounds = reinterpret_cast<int32_t *>(w);
@@ -762,8 +935,29 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
       pt = reinterpret_cast<int32_t *>(w + L.part + (size_t)P2M_MAX_SPLITS * P * 16);
     }
   }
-  hipLaunchKernelGGL(p2m_fwd_kernel<T>, dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
-                     (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
+  // dev param 11 = 2 / 3: face records read from global memory through scalar loads
+  // (p2m_fwd_grec_kernel, one / two faces per iteration) instead of staged through LDS -- measured
+  // slower at cfg2 (1.70 against 1.51 ms for two faces per iteration), kept for A/B
+  if (order && (g_dev_param[11] == 2 || g_dev_param[11] == 3)) {
+    char *w = reinterpret_cast<char *>(ws);
+    const P2MWs L(P, F, sizeof(T));
+    FaceRecS<T> *rec = reinterpret_cast<FaceRecS<T> *>(w + L.rec);
+    T *pr = reinterpret_cast<T *>(w + L.pr);
+    hipLaunchKernelGGL(p2m_faces_kernel<T>, dim3((unsigned)cdiv(F, 256)), dim3(256), 0, st, (const T *)fv, F, L.Fp,
+                       rec, pr);
+    KL_CHECK_LAUNCH();
+    if (g_dev_param[11] == 2)  // one face per iteration
+      hipLaunchKernelGGL((p2m_fwd_grec_kernel<T, false>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st,
+                         (const T *)pts, (const FaceRecS<T> *)rec, (const T *)pr, L.Fp, order, P, F, split_faces,
+                         (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
+    else
+      hipLaunchKernelGGL((p2m_fwd_grec_kernel<T, true>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st,
+                         (const T *)pts, (const FaceRecS<T> *)rec, (const T *)pr, L.Fp, order, P, F, split_faces,
+                         (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
+  } else {
+    hipLaunchKernelGGL(p2m_fwd_kernel<T>, dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
+                       (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
+  }
   KL_CHECK_LAUNCH();
   if (splits > 1) {
     hipLaunchKernelGGL(p2m_combine_kernel<T>, dim3(pblocks), dim3(256), 0, st, order, P, splits, pd, pidx, pt,
@@ -848,7 +1042,9 @@ static int sided_bwd(int B, int64_t N, int64_t M, const void *grad, const void *
 
 using namespace kl;
 
-extern "C" size_t kl_unbatched_triangle_distance_workspace_bytes(int64_t P) { return P2MWs(P > 0 ? P : 1).bytes; }
+extern "C" size_t kl_unbatched_triangle_distance_workspace_bytes(int64_t P, int64_t F) {
+  return P2MWs(P > 0 ? P : 1, F > 0 ? F : 1, sizeof(double)).bytes;
+}
 
 extern "C" int kl_unbatched_triangle_distance_forward(kl_dtype dtype, int64_t P, int64_t F, const void *pts,
                                                       const void *fv, void *dist, int64_t *idx, int32_t *type,

@@ -1071,7 +1071,7 @@ __device__ __forceinline__ void gather_one(
   // the soft mask's sum of coordinate s (written by lane s below), loaded now so that its
   // latency hides behind the walk: an unconditional load from a clamped index
   double sv = 0.0;
-  if (soft) sv = soft[(in ? tf : 0) * 6 + (s < 6 ? s : 5)];
+  if (soft) sv = soft[(in ? tf : 0) * DS_ACC_STRIDE + (s < 6 ? s : 5)];
   GatherAcc<T, MAXD> acc;
   acc.zero();
   int ix0, ix1, iy0, iy1;
@@ -1212,7 +1212,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
     if (q < 6 + 3 * MAXD) {
       const double x = red[q] + red[(6 + 3 * MAXD) + q] + red[2 * (6 + 3 * MAXD) + q] + red[3 * (6 + 3 * MAXD) + q];
       if (q < 6) {
-        grad_fvi[tf * 6 + q] = soft ? (T)x + (T)soft[tf * 6 + q] : (T)x;
+        grad_fvi[tf * 6 + q] = soft ? (T)x + (T)soft[tf * DS_ACC_STRIDE + q] : (T)x;
       } else {
         const int r = q - 6, ii = r / MAXD, d = r % MAXD;
         if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)x;
@@ -1300,7 +1300,7 @@ template <typename T, int MAXD>
 __device__ __forceinline__ void g2_store(int64_t tf, int q, double x, int D, double *__restrict__ soft,
                                          T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat) {
   if (q < 6) {
-    grad_fvi[tf * 6 + q] = soft ? (T)x + (T)take_soft(soft, tf * 6 + q) : (T)x;
+    grad_fvi[tf * 6 + q] = soft ? (T)x + (T)take_soft(soft, tf * DS_ACC_STRIDE + q) : (T)x;
   } else {
     const int r = q - 6, ii = r / MAXD, d = r % MAXD;
     if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)x;
@@ -1390,7 +1390,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
 #pragma unroll
     for (int q = s; q < NV; q += 8) {
       if (q < 6) {
-        grad_fvi[tf * 6 + q] = soft ? (T)0 + (T)take_soft(soft, tf * 6 + q) : (T)0;
+        grad_fvi[tf * 6 + q] = soft ? (T)0 + (T)take_soft(soft, tf * DS_ACC_STRIDE + q) : (T)0;
       } else {
         const int r = q - 6, ii = r / MAXD, d = r % MAXD;
         if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)0;
@@ -1765,17 +1765,18 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   const PixPitch pp{m / (float)W, m / (float)H, (float)W / m, (float)H / m};
   if constexpr (sizeof(T) == 4) {
     // the fused tile kernel (dibrtile.hip): the soft bins only, one order, ONE kernel for the
-    // rasterizer and the soft mask (needs bboxes inside the enlarged ones: boxlen >= 0; dev param
-    // 10 = 1 keeps the two-kernel path below, for A/B timing)
-    if (pad >= 0.0 && bin_word_lds_ok(g) && nt <= ORD_LDS_TILES && g_dev_param[10] != 1) {
+    // rasterizer and the soft mask (needs bboxes inside the enlarged ones: boxlen >= 0).  Dev param
+    // 10 = 2 only: measured slower than the two-kernel path below at cfg3 (105.9 against 32.1 +
+    // 51.3 us of tile kernels), kept tested bit-equal to it for the record.
+    if (pad >= 0.0 && bin_word_lds_ok(g) && nt <= ORD_LDS_TILES && g_dev_param[10] == 2) {
       KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, nullptr, rec, rng, sbm, srng, (T)pad, rgh,
                                      (int)((L.zero - L.off_rgh) / sizeof(int)), st));
-      const int lpm = dt_lp_min(K);
+      const int lpm = g_dev_param[13] ? g_dev_param[13] : dt_lp_min(K);  // dev param 13: rows 8 >> lp_min
       // block 1 orders; block 0 zeroes the state's counters; the rest zero the backward's accumulator
       const unsigned og = g_dev_param[9] >= 2 ? (unsigned)g_dev_param[9] : 256u;
       hipLaunchKernelGGL(tile_countorder2_kernel, dim3(og), dim3(1024), 0, st, (const uint32_t *)sbm,
                          (const uint32_t *)sbm, g.words, (int32_t *)nullptr, 0, 0, (int *)nullptr, sorder, nt, lpm,
-                         snitems, soft_split(), 0, bcnt, DibrState::kZeroInts, bacc, (size_t)B * F * 6,
+                         snitems, soft_split(), 0, bcnt, DibrState::kZeroInts, bacc, (size_t)B * F * DS_ACC_STRIDE,
                          kDevStamps && g_dev_debug ? reinterpret_cast<uint64_t *>(g_dev_debug) + kOrderStampsAt
                                                    : nullptr);
       KL_CHECK_LAUNCH();
@@ -1784,7 +1785,8 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
                             reinterpret_cast<const float *>(feat), sbm, sorder, snitems, g, F, D, K, eps, sigmainv,
                             m, reinterpret_cast<float *>(out_feat), out_idx, reinterpret_cast<float *>(out_w),
                             reinterpret_cast<float *>(out_mask), s.hits, s.rec_face,
-                            reinterpret_cast<float *>(s.rec_prob), s.seg_tot, bitems, bcnt, S.cap};
+                            reinterpret_cast<float *>(s.rec_prob), s.seg_tot, bitems, bcnt, S.cap,
+                            g_dev_param[12]};
       return dibr_tile_launch(da, lpm, soft_items_bound(nt, lpm, soft_split()), st);
     }
   }
@@ -1812,7 +1814,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     hipLaunchKernelGGL(tile_countorder2_kernel, dim3(og), dim3(1024), 0, st, (const uint32_t *)rbm,
                        (const uint32_t *)sbm, g.words, items, split_from, split_log2, nitems, sorder, nt,
                        soft_lp_min(K), snitems, soft_split(), 1, bcnt, DibrState::kZeroInts, bacc,
-                       (size_t)B * F * 6,
+                       (size_t)B * F * DS_ACC_STRIDE,
                        kDevStamps && g_dev_debug ? reinterpret_cast<uint64_t *>(g_dev_debug) + kOrderStampsAt : nullptr);
     KL_CHECK_LAUNCH();
   } else {  // counts (a wave per tile) then orders (dev bit 20: this path, for A/B timing)
@@ -1821,7 +1823,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     KL_CHECK_LAUNCH();
     hipLaunchKernelGGL(tile_order2_kernel, dim3(256), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh,
                        items, split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt,
-                       soft_lp_min(K), snitems, soft_split(), 1, bacc, (size_t)B * F * 6);
+                       soft_lp_min(K), snitems, soft_split(), 1, bacc, (size_t)B * F * DS_ACC_STRIDE);
     KL_CHECK_LAUNCH();
   }
   uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.off_defer);

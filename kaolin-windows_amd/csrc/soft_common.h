@@ -188,6 +188,10 @@ __host__ __device__ constexpr size_t st_row_lds(int K) {
 // 64-byte line): the fused forward appends to shard blockIdx % DS_SHARDS.
 constexpr int DS_SHARDS = 8;
 constexpr int DS_CNT_STRIDE = 16;
+// The fused path's per-face soft sums: 6 doubles padded to 8 (one 64-byte line per face, so a
+// face's flush leaves L2 as one request, not two for the half of the faces a 48-byte stride
+// puts across a line boundary)
+constexpr int DS_ACC_STRIDE = 8;
 
 // The compact soft-mask state (softtile.hip): per pixel the filled-slot count; per hit a
 // record (face | type << 28, prob), packed per 64-pixel row segment; per segment its hit
@@ -219,7 +223,7 @@ size_t soft_tile_bwd_items_bytes(int B, int H, int W, int K);
 // the most backward work items one fused forward can list (per shard)
 int soft_bwd_item_cap(int B, int H, int W, int K);
 // The fused path's backward on the forward's item list and zeroed accumulator (DibrState):
-// the per-face double sums are added into acc (B*F*6), not rounded.
+// the per-face double sums are added into acc (B*F x DS_ACC_STRIDE), not rounded.
 template <typename T>
 int soft_tile_backward_listed(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
                               const T *fvi, float sigmainv, float m, const int2 *items, const int *cnt, int cap,
@@ -227,7 +231,7 @@ int soft_tile_backward_listed(int B, int H, int W, int F, int K, const T *grad, 
 // Per-call state of kl_dibr_forward / kl_dibr_backward (kl_dibr_state_bytes):
 //   [0, 512)   DS_SHARDS item counters; int 128: the r03 gather's big-face counter (dev path)
 //   items      DS_SHARDS x cap backward work items (int2)
-//   acc        the soft mask's per-face double sums (B*F*6), zeroed by the forward
+//   acc        the soft mask's per-face double sums (B*F x DS_ACC_STRIDE), zeroed by the forward
 struct DibrState {
   int cap;
   size_t off_items, off_acc, bytes;
@@ -235,7 +239,7 @@ struct DibrState {
     cap = soft_bwd_item_cap(B, H, W, K);
     off_items = 1024;
     off_acc = al256(off_items + (size_t)DS_SHARDS * cap * sizeof(int2));
-    bytes = off_acc + (size_t)B * F * 6 * sizeof(double);
+    bytes = off_acc + (size_t)B * F * DS_ACC_STRIDE * sizeof(double);
   }
   static constexpr int kZeroInts = 129;  // counters + big-face counter, zeroed by the forward
 };

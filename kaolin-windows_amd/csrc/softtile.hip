@@ -561,7 +561,7 @@ struct ItemHash {
     }
     return -1;
   }
-  __device__ __forceinline__ void add(int f, int c0, int c1, T g0x, T g0y, T g1x, T g1y, double *gmesh) {
+  __device__ __forceinline__ void add(int f, int c0, int c1, T g0x, T g0y, T g1x, T g1y, double *gmesh, int ast) {
     const int s = slot(f);
     if (s >= 0) {
       atomicAdd(&val[s * 6 + c0 * 2], (double)g0x);
@@ -571,7 +571,7 @@ struct ItemHash {
         atomicAdd(&val[s * 6 + c1 * 2 + 1], (double)g1y);
       }
     } else {  // no free slot within the probe bound
-      global_add_pair<double>(gmesh + (size_t)f * 6, c0, c1, g0x, g0y, g1x, g1y);
+      global_add_pair<double>(gmesh + (size_t)f * ast, c0, c1, g0x, g0y, g1x, g1y);
     }
   }
   // one thread per (used slot, coordinate), coordinate fastest: a face's 6 sums go out from 6
@@ -579,12 +579,12 @@ struct ItemHash {
   // 64-B requests per face instead of one request per lane (memory-side atomics,
   // MI355X_MICROARCH.md: one lane per row is an order of magnitude slower).  Every thread of the
   // workgroup calls it (barrier before the key reset).
-  __device__ __forceinline__ void flush_reset(int tid, int nthreads, double *gmesh) {
+  __device__ __forceinline__ void flush_reset(int tid, int nthreads, double *gmesh, int ast) {
     const int n = *nused;
     for (int u = tid; u < n * 6; u += nthreads) {
       const int sl = used[u / 6], c = u % 6;
       const double v = val[sl * 6 + c];
-      if (v != 0.0) atomicAdd(gmesh + (size_t)key[sl] * 6 + c, v);
+      if (v != 0.0) atomicAdd(gmesh + (size_t)key[sl] * ast + c, v);
       val[sl * 6 + c] = 0.0;
     }
     __syncthreads();
@@ -601,7 +601,7 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const uint8_t *__restrict__ hits,
     const uint32_t *__restrict__ rec_face, const T *__restrict__ rec_prob, const T *__restrict__ fvi, BinGeom g,
     int F, int K, float sigmainv, float multiplier, double *__restrict__ gacc, const int2 *__restrict__ items,
-    const int *__restrict__ ctl, int cap, int *__restrict__ scratch, int dev) {
+    const int *__restrict__ ctl, int cap, int *__restrict__ scratch, int dev, int ast) {
   constexpr int HC = 512;
   __shared__ int s_key[HC];
   __shared__ double s_val[HC * 6];
@@ -692,10 +692,10 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
       if (dev & 2)
         asm volatile("" : : "v"(g0x), "v"(g0y), "v"(g1x), "v"(g1y), "v"(c0), "v"(c1));
       else
-        hash.add(face, c0, c1, g0x, g0y, g1x, g1y, gacc + (size_t)b * F * 6);
+        hash.add(face, c0, c1, g0x, g0y, g1x, g1y, gacc + (size_t)b * F * ast, ast);
     }
     __syncthreads();
-    hash.flush_reset(threadIdx.x, blockDim.x, gacc + (size_t)b * F * 6);
+    hash.flush_reset(threadIdx.x, blockDim.x, gacc + (size_t)b * F * ast, ast);
     __syncthreads();
     if (threadIdx.x == 0) s_nused = 0;
   }
@@ -852,7 +852,7 @@ int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T
   const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
   hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
                      (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, acc,
-                     (const int2 *)items, (const int *)ctl, 0, s.scratch, g_dev_flags);
+                     (const int2 *)items, (const int *)ctl, 0, s.scratch, g_dev_flags, 6);
   KL_CHECK_LAUNCH();
   if (acc_out) {
     if (has_sum) *has_sum = true;
@@ -875,7 +875,7 @@ int soft_tile_backward_listed(int B, int H, int W, int F, int K, const T *grad, 
   const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
   hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
                      (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, acc, items, cnt,
-                     cap, (int *)nullptr, g_dev_flags);
+                     cap, (int *)nullptr, g_dev_flags, DS_ACC_STRIDE);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

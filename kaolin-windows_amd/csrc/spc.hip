@@ -125,6 +125,43 @@ __device__ bool tri_voxel_test(const float *fa, const float *fb, const float *fc
   return true;
 }
 
+// A float pre-test of tri_voxel_test: false only where tri_voxel_test is false (the SAT is a
+// conjunction of independent axis tests, so any axis that separates decides it).
+//  * The box axes (1,0,0), (0,1,0), (0,0,1): sat_axis projects v_k exactly (d_k = v_k.x * 1 +
+//    v_k.y * 0 + v_k.z * 0 = v_k.x for finite coordinates, already a float) and compares
+//    (float)max(-max d, min d) with (float)(h * 1) = h -- the same float comparison as here, so
+//    these three decide exactly as the full test does.
+//  * The triangle's normal, conservatively: with E1 = vb - va, E2 = vc - vb and N = E1 x E2 in
+//    float, S = max(-max_k v_k.N, min_k v_k.N) - h |N|_1 differs from the exact (unit-normal)
+//    separation, scaled by |e1 x e2|, by far less than 2^-14 (Vm + h) 12 |E1|inf |E2|inf (Vm the
+//    largest |coordinate| of the v_k; float products and sums of 3 terms, the edge roundings, the
+//    full test's own double rounding and its two float casts are each a few 2^-24 of that), so
+//    S > that slack proves the full test's normal axis separates.  Non-finite inputs or a
+//    degenerate triangle (slack 0) are left to the full test.
+// Most of a level's proposals (8 children of each occupied parent per face) are separated by a
+// box axis or the plane; the full fp64 test then runs only on this test's survivors, compacted
+// into coherent waves (m2s_level_kernel).
+__device__ __forceinline__ bool tri_voxel_maybe(const float *fa, const float *fb, const float *fc, float cx, float cy,
+                                                float cz, float h) {
+  const float ax = fa[0] - cx, ay = fa[1] - cy, az = fa[2] - cz;
+  const float bx = fb[0] - cx, by = fb[1] - cy, bz = fb[2] - cz;
+  const float qx = fc[0] - cx, qy = fc[1] - cy, qz = fc[2] - cz;
+  const float vm = fmaxf(fmaxf(fmaxf(fabsf(ax), fabsf(ay)), fmaxf(fabsf(az), fabsf(bx))),
+                         fmaxf(fmaxf(fabsf(by), fabsf(bz)), fmaxf(fmaxf(fabsf(qx), fabsf(qy)), fabsf(qz))));
+  if (!(vm < 1e30f)) return true;  // NaN / inf / huge: the full test decides
+  if (fminf(ax, fminf(bx, qx)) > h || fmaxf(ax, fmaxf(bx, qx)) < -h) return false;
+  if (fminf(ay, fminf(by, qy)) > h || fmaxf(ay, fmaxf(by, qy)) < -h) return false;
+  if (fminf(az, fminf(bz, qz)) > h || fmaxf(az, fmaxf(bz, qz)) < -h) return false;
+  const float e1x = bx - ax, e1y = by - ay, e1z = bz - az;
+  const float e2x = qx - bx, e2y = qy - by, e2z = qz - bz;
+  const float nx = e1y * e2z - e1z * e2y, ny = e1z * e2x - e1x * e2z, nz = e1x * e2y - e1y * e2x;
+  const float d0 = ax * nx + ay * ny + az * nz, d1 = bx * nx + by * ny + bz * nz, d2 = qx * nx + qy * ny + qz * nz;
+  const float sep = fmaxf(-fmaxf(d0, fmaxf(d1, d2)), fminf(d0, fminf(d1, d2))) - h * (fabsf(nx) + fabsf(ny) + fabsf(nz));
+  const float e1m = fmaxf(fabsf(e1x), fmaxf(fabsf(e1y), fabsf(e1z))), e2m = fmaxf(fabsf(e2x), fmaxf(fabsf(e2y), fabsf(e2z)));
+  const float slack = (12.0f / 16384.0f) * (vm + h) * e1m * e2m;
+  return !(sep > slack);
+}
+
 __device__ __forceinline__ void voxel_center(uint64_t m, uint32_t level, float &cx, float &cy, float &cz,
                                              float &h) {
   const float two_level = (float)(1u << level);
@@ -149,7 +186,9 @@ __global__ void m2s_decide_kernel(int64_t num, const float *__restrict__ fv, con
   float cx, cy, cz, h;
   voxel_center(morton[t], level, cx, cy, cz, h);
   const float *v = fv + tri[t] * 9;
-  occ[t] = tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h) ? (not_done ? 8u : 1u) : 0u;
+  occ[t] = tri_voxel_maybe(v, v + 3, v + 6, cx, cy, cz, h) && tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h)
+               ? (not_done ? 8u : 1u)
+               : 0u;
 }
 
 __global__ void m2s_subdivide_kernel(int64_t num, const uint64_t *__restrict__ min_, const int64_t *__restrict__ tin,
@@ -482,8 +521,15 @@ __global__ void __launch_bounds__(256) m2s_level_kernel(const float *__restrict_
   __shared__ int s_wave[16];
   __shared__ unsigned long long s_base;
   __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
+  __shared__ uint16_t s_list[M2S_MAX_CHUNKS * 256];  // the pre-test's survivors: chunk << 8 | thread
+  __shared__ unsigned long long s_pass[256];
+  // After an overflow the shards hold unwritten holes below their clamped counts (the overflowing
+  // workgroups reserved past seg and wrote nothing): the levels after it must not read them (their
+  // face ids would index fv out of bounds).  The result is discarded and the host reruns the
+  // per-level path.
+  if (*(volatile int *)overflow) return;
   ShardIn in;
-  in.load(s_pre, cnt_in, seg);  // an overflowed shard is clamped (flagged, the result is discarded)
+  in.load(s_pre, cnt_in, seg);
   const unsigned long long n = in.total();
   const int g = blockIdx.x % M2S_SHARDS;
   const uint32_t kids = not_done ? 8u : 1u;
@@ -496,8 +542,8 @@ __global__ void __launch_bounds__(256) m2s_level_kernel(const float *__restrict_
     if (threadIdx.x == 0) *overflow = 1;
     return;
   }
-  // 1. test every proposal of the span
-  uint64_t pass = 0;
+  // 1. the float pre-test of every proposal of the span (tri_voxel_maybe); its survivors listed
+  uint64_t cand = 0;
 #pragma unroll 1
   for (int k = 0; k < nch; k++) {
     const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
@@ -506,8 +552,28 @@ __global__ void __launch_bounds__(256) m2s_level_kernel(const float *__restrict_
     float cx, cy, cz, h;
     voxel_center(min_[p], level, cx, cy, cz, h);
     const float *v = fv + (int64_t)tin[p] * 9;
-    if (tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h)) pass |= 1ull << k;
+    if (tri_voxel_maybe(v, v + 3, v + 6, cx, cy, cz, h)) cand |= 1ull << k;
   }
+  s_pass[threadIdx.x] = 0;
+  int ncand = 0;
+  {
+    int o = block_exclusive_scan(__popcll(cand), s_wave, &ncand);
+    for (uint64_t c = cand; c; c &= c - 1) s_list[o++] = (uint16_t)((__builtin_ctzll(c) << 8) | threadIdx.x);
+  }
+  __syncthreads();
+  // 1b. the full fp64 test (mesh_to_spc_cuda.cu:96-159) on the survivors, in coherent waves
+#pragma unroll 1
+  for (int e = threadIdx.x; e < ncand; e += blockDim.x) {
+    const int code = s_list[e], k = code >> 8, tt = code & 255;
+    const unsigned long long i = lo + (unsigned long long)k * blockDim.x + tt;
+    const unsigned long long p = in.pos(i, seg);
+    float cx, cy, cz, h;
+    voxel_center(min_[p], level, cx, cy, cz, h);
+    const float *v = fv + (int64_t)tin[p] * 9;
+    if (tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h)) atomicOr(&s_pass[tt], 1ull << k);
+  }
+  __syncthreads();
+  const uint64_t pass = s_pass[threadIdx.x];
   // 2. one reservation for the span
   int total = 0;
   (void)block_exclusive_scan(__popcll(pass) * (int)kids, s_wave, &total);
@@ -542,6 +608,234 @@ __global__ void __launch_bounds__(256) m2s_level_kernel(const float *__restrict_
           mout[o + c] = to_morton(2 * px + (c >> 2), 2 * py + ((c >> 1) & 1), 2 * pz + (c & 1));
           tout[o + c] = tr;
         }
+      }
+    }
+    o0 += (unsigned long long)ctot;
+  }
+}
+
+// ---- the 8 children of a parent (voxel, face) pair at once (m2s_children_kernel).
+// The reference's decision for a child c (tri_voxel_test: 13 SAT axes, each passing iff
+// (float)max(-max_k d_k, min_k d_k) <= (float)(h |a|_1), d_k = v_k . a, v_k = fl(f_k - c)) is
+// derived per axis from the PARENT's projections: with C the parent's centre and w_k = fl(f_k - C),
+// the child centre is c = C + delta, delta in {-h, +h}^3 (C and every child centre are exact
+// floats), so d_k = w_k . a - delta . a up to rounding, and the axis's separation is
+//   S = max(s - max_k P_k, min_k P_k - s) - h |a|_1,  P_k = w_k . a,  s = delta . a,
+// one add per sign pattern of delta.  Each axis is evaluated with float edges E = fl(f_b - f_a)
+// (unnormalised: a positive scale does not change the sign of S) and a margin M bounding the
+// difference to the reference's own S in that scale -- its rounded v_k (the edges it builds
+// differ from E by at most tau = 2^-22 U per component, U = max |w_k| + 2h + max |E|), its
+// normalisation, its double products and float casts, and this float evaluation (a few 2^-24 U
+// |a|_1 each):
+//   * box axes: decided EXACTLY, on the reference's own float differences f_k - (C +- h);
+//   * edge-cross axes (x/y/z cross each edge): |dS| <= 2 tau (V + 2h) + 2^-20 (V + 2h) |a|_1 <
+//     M = 2^-17 U^2;
+//   * the normal, E1 x E2: |dS| <= 9 * 2^-20 U^3 < M = 2^-15 U^3.
+// S > M proves the reference rejects the child on that axis, S < -M that it passes it; a child
+// every axis passes is accepted, one some axis rejects is rejected, and the rest (|S| <= M on
+// some axis, none rejecting) run the reference's test itself.  A reference edge of length 0
+// (its NaN axis rejects) needs |E| <= tau, where |S| < M: never decided here.  Non-finite or
+// huge inputs (U >= 1e12) leave all 8 children to the full test.
+// -> bit c set iff child c (to_morton(2p + (c >> 2), 2q + ((c >> 1) & 1), 2r + (c & 1))) passes.
+__device__ __forceinline__ void m2s_axis4(float pmax, float pmin, float R, float hp, float hq, float M,
+                                          uint32_t &rej4, uint32_t &amb4) {
+  // sign patterns j = (bp << 1) | bq of the two nonzero components: s = +-hp +-hq
+  rej4 = 0;
+  amb4 = 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const float sv = ((j >> 1) ? hp : -hp) + ((j & 1) ? hq : -hq);
+    const float S = fmaxf(sv - pmax, pmin - sv) - R;
+    rej4 |= (S > M ? 1u : 0u) << j;
+    amb4 |= (!(S < -M) && !(S > M) ? 1u : 0u) << j;
+  }
+}
+
+__device__ uint32_t m2s_children(const float *v, uint64_t m, uint32_t level) {
+  int16_t px, py, pz;
+  to_point(m, px, py, pz);
+  const float two_level = (float)(1u << level);
+  const float vs = 2.0f / two_level;  // child size
+  const float h = (float)(0.5 * vs);  // child half-size (voxel_center at `level`)
+  // parent centre: child (2p, 2q, 2r)'s centre + h, exact
+  const float Cx = fmaf((float)(2 * px), vs, h - 1.0f) + h;
+  const float Cy = fmaf((float)(2 * py), vs, h - 1.0f) + h;
+  const float Cz = fmaf((float)(2 * pz), vs, h - 1.0f) + h;
+  const float w[3][3] = {{v[0] - Cx, v[1] - Cy, v[2] - Cz}, {v[3] - Cx, v[4] - Cy, v[5] - Cz},
+                         {v[6] - Cx, v[7] - Cy, v[8] - Cz}};
+  const float E[3][3] = {{v[3] - v[0], v[4] - v[1], v[5] - v[2]},   // ab
+                         {v[6] - v[3], v[7] - v[4], v[8] - v[5]},   // bc
+                         {v[0] - v[6], v[1] - v[7], v[2] - v[8]}};  // ca
+  float V = 0.f, Em = 0.f;
+#pragma unroll
+  for (int k = 0; k < 3; k++)
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      V = fmaxf(V, fabsf(w[k][q]));
+      Em = fmaxf(Em, fabsf(E[k][q]));
+    }
+  const float U = V + 2.0f * h + Em;
+  uint32_t rej = 0, amb = 0;
+  if (!(U < 1e12f)) {
+    amb = 0xffu;
+  } else {
+    // box axes, exactly as the reference: per axis and half, the children's own differences
+    const float cen[3] = {Cx, Cy, Cz};
+    const uint32_t half_mask[3][2] = {{0x0fu, 0xf0u}, {0x33u, 0xccu}, {0x55u, 0xaau}};
+#pragma unroll
+    for (int q = 0; q < 3; q++)
+#pragma unroll
+      for (int b = 0; b < 2; b++) {
+        const float c = b ? cen[q] + h : cen[q] - h;
+        const float u0 = v[q] - c, u1 = v[3 + q] - c, u2 = v[6 + q] - c;
+        const float fd = fmaxf(-fmaxf(u0, fmaxf(u1, u2)), fminf(u0, fminf(u1, u2)));
+        if (!(fd <= h)) rej |= half_mask[q][b];
+      }
+    // edge-cross axes: x x e = (0, -e.z, e.y), y x e = (e.z, 0, -e.x), z x e = (-e.y, e.x, 0)
+    const float Me = (1.0f / 131072.0f) * U * U;
+#pragma unroll
+    for (int e = 0; e < 3; e++) {
+      const float ex = E[e][0], ey = E[e][1], ez = E[e][2];
+      uint32_t r4, a4;
+      {  // (0, -ez, ey): patterns over (y, z): child bits (c >> 1) & 1, c & 1
+        float P[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) P[k] = w[k][1] * -ez + w[k][2] * ey;
+        m2s_axis4(fmaxf(P[0], fmaxf(P[1], P[2])), fminf(P[0], fminf(P[1], P[2])), h * (fabsf(ez) + fabsf(ey)),
+                  h * -ez, h * ey, Me, r4, a4);
+        rej |= r4 | (r4 << 4);
+        amb |= a4 | (a4 << 4);
+      }
+      {  // (ez, 0, -ex): patterns over (x, z)
+        float P[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) P[k] = w[k][0] * ez + w[k][2] * -ex;
+        m2s_axis4(fmaxf(P[0], fmaxf(P[1], P[2])), fminf(P[0], fminf(P[1], P[2])), h * (fabsf(ez) + fabsf(ex)),
+                  h * ez, h * -ex, Me, r4, a4);
+        auto spread = [](uint32_t m4) {  // j = (bx << 1) | bz -> children bx * 4 + bz + {0, 2}
+          return ((m4 & 1u) ? 0x05u : 0u) | ((m4 & 2u) ? 0x0au : 0u) | ((m4 & 4u) ? 0x50u : 0u) |
+                 ((m4 & 8u) ? 0xa0u : 0u);
+        };
+        rej |= spread(r4);
+        amb |= spread(a4);
+      }
+      {  // (-ey, ex, 0): patterns over (x, y)
+        float P[3];
+#pragma unroll
+        for (int k = 0; k < 3; k++) P[k] = w[k][0] * -ey + w[k][1] * ex;
+        m2s_axis4(fmaxf(P[0], fmaxf(P[1], P[2])), fminf(P[0], fminf(P[1], P[2])), h * (fabsf(ey) + fabsf(ex)),
+                  h * -ey, h * ex, Me, r4, a4);
+        auto spread = [](uint32_t m4) {  // j = (bx << 1) | by -> children bx * 4 + by * 2 + {0, 1}
+          return ((m4 & 1u) ? 0x03u : 0u) | ((m4 & 2u) ? 0x0cu : 0u) | ((m4 & 4u) ? 0x30u : 0u) |
+                 ((m4 & 8u) ? 0xc0u : 0u);
+        };
+        rej |= spread(r4);
+        amb |= spread(a4);
+      }
+    }
+    // the normal E1 x E2 (the reference's cross(ab, bc))
+    {
+      const float nx = E[0][1] * E[1][2] - E[0][2] * E[1][1];
+      const float ny = E[0][2] * E[1][0] - E[0][0] * E[1][2];
+      const float nz = E[0][0] * E[1][1] - E[0][1] * E[1][0];
+      float P[3];
+#pragma unroll
+      for (int k = 0; k < 3; k++) P[k] = w[k][0] * nx + w[k][1] * ny + w[k][2] * nz;
+      const float pmax = fmaxf(P[0], fmaxf(P[1], P[2])), pmin = fminf(P[0], fminf(P[1], P[2]));
+      const float R = h * (fabsf(nx) + fabsf(ny) + fabsf(nz));
+      const float Mn = (1.0f / 32768.0f) * U * U * U;
+      const float hx = h * nx, hy = h * ny, hz = h * nz;
+#pragma unroll
+      for (int c = 0; c < 8; c++) {
+        const float sv = ((c >> 2) ? hx : -hx) + (((c >> 1) & 1) ? hy : -hy) + ((c & 1) ? hz : -hz);
+        const float S = fmaxf(sv - pmax, pmin - sv) - R;
+        rej |= (S > Mn ? 1u : 0u) << c;
+        amb |= (!(S < -Mn) && !(S > Mn) ? 1u : 0u) << c;
+      }
+    }
+  }
+  uint32_t pass = ~(rej | amb) & 0xffu;
+  uint32_t need = amb & ~rej & 0xffu;
+  while (need) {  // the reference's test itself, on its own child centre
+    const int c = __builtin_ctz(need);
+    need &= need - 1;
+    float cx, cy, cz, hh;
+    voxel_center(to_morton(2 * px + (c >> 2), 2 * py + ((c >> 1) & 1), 2 * pz + (c & 1)), level, cx, cy, cz, hh);
+    if (tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, hh)) pass |= 1u << c;
+  }
+  return pass;
+}
+
+// One level of the device-sized mesh_to_spc from the PARENTS: the input is the previous level's
+// passing (voxel, face) pairs, each thread decides its parent's 8 children (m2s_children) and the
+// passing children are appended (sharded counters, one reservation per workgroup, as
+// m2s_level_kernel) -- the pairs of this level, which the next level reads as its parents.
+__global__ void __launch_bounds__(256) m2s_children_kernel(const float *__restrict__ fv,
+                                                           const uint64_t *__restrict__ min_,
+                                                           const uint32_t *__restrict__ tin,
+                                                           const unsigned long long *__restrict__ cnt_in,
+                                                           uint64_t *__restrict__ mout, uint32_t *__restrict__ tout,
+                                                           unsigned long long *__restrict__ cnt_out,
+                                                           unsigned long long seg, int *__restrict__ overflow,
+                                                           uint32_t level) {
+  __shared__ int s_wave[16];
+  __shared__ unsigned long long s_base;
+  __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
+  __shared__ uint8_t s_kids[M2S_MAX_CHUNKS][256];
+  if (*(volatile int *)overflow) return;  // holes in the input (m2s_level_kernel)
+  ShardIn in;
+  in.load(s_pre, cnt_in, seg);
+  const unsigned long long n = in.total();
+  const int g = blockIdx.x % M2S_SHARDS;
+  const unsigned long long span = (n + gridDim.x - 1) / gridDim.x;
+  const unsigned long long lo = (unsigned long long)blockIdx.x * span;
+  const unsigned long long hi = lo + span < n ? lo + span : n;
+  if (lo >= hi) return;
+  const int nch = (int)((hi - lo + blockDim.x - 1) / blockDim.x);
+  if (nch > M2S_MAX_CHUNKS) {
+    if (threadIdx.x == 0) *overflow = 1;
+    return;
+  }
+  int mine = 0;
+#pragma unroll 1
+  for (int k = 0; k < nch; k++) {
+    const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
+    uint32_t kids = 0;
+    if (i < hi) {
+      const unsigned long long p = in.pos(i, seg);
+      kids = m2s_children(fv + (int64_t)tin[p] * 9, min_[p], level);
+    }
+    s_kids[k][threadIdx.x] = (uint8_t)kids;
+    mine += __popc(kids);
+  }
+  int total = 0;
+  (void)block_exclusive_scan(mine, s_wave, &total);
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(cnt_out + g, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  unsigned long long o0 = s_base;
+  if (total == 0) return;
+  if (o0 + (unsigned long long)total > seg) {
+    if (threadIdx.x == 0) *overflow = 1;
+    return;
+  }
+  o0 += (unsigned long long)g * seg;
+#pragma unroll 1
+  for (int k = 0; k < nch; k++) {
+    const uint32_t kids = s_kids[k][threadIdx.x];
+    int ctot = 0;
+    const int pre = block_exclusive_scan(__popc(kids), s_wave, &ctot);
+    if (kids) {
+      const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
+      const unsigned long long p = in.pos(i, seg);
+      int16_t px, py, pz;
+      to_point(min_[p], px, py, pz);
+      const uint32_t tr = tin[p];
+      unsigned long long o = o0 + (unsigned long long)pre;
+      for (uint32_t c = kids; c; c &= c - 1) {
+        const int q = __builtin_ctz(c);
+        mout[o] = to_morton(2 * px + (q >> 2), 2 * py + ((q >> 1) & 1), 2 * pz + (q & 1));
+        tout[o] = tr;
+        o++;
       }
     }
     o0 += (unsigned long long)ctot;
@@ -704,10 +998,20 @@ static int mesh_to_spc_async(int64_t F, const float *fv, uint32_t L, Scratch &sc
   KL_CHECK_LAUNCH();
   // one round of workgroups, each a span of at most M2S_MAX_CHUNKS chunks of 256 proposals
   const unsigned grid = (unsigned)std::max<int64_t>(M2S_GRID, cdiv((int64_t)cap, 256 * M2S_MAX_CHUNKS));
+  // level 0 tests the root against every face; each later level decides the children of the
+  // previous level's passing pairs (m2s_children_kernel; dev param 14 = 1: every level tests
+  // its 8-children proposals one by one, m2s_level_kernel, for A/B)
+  const bool by_parent = g_dev_param[14] != 1;
   for (uint32_t l = 0; l <= L; l++) {
     const int a = l & 1;
-    hipLaunchKernelGGL(m2s_level_kernel, dim3(grid), dim3(256), 0, st, fv, mb[a], tb[a], counts + l * M2S_SHARDS,
-                       mb[a ^ 1], tb[a ^ 1], counts + (l + 1) * M2S_SHARDS, seg, overflow, l, L - l);
+    if (by_parent && l > 0)
+      hipLaunchKernelGGL(m2s_children_kernel, dim3(grid), dim3(256), 0, st, fv, mb[a], tb[a],
+                         counts + l * M2S_SHARDS, mb[a ^ 1], tb[a ^ 1], counts + (l + 1) * M2S_SHARDS, seg, overflow,
+                         l);
+    else
+      hipLaunchKernelGGL(m2s_level_kernel, dim3(grid), dim3(256), 0, st, fv, mb[a], tb[a], counts + l * M2S_SHARDS,
+                         mb[a ^ 1], tb[a ^ 1], counts + (l + 1) * M2S_SHARDS, seg, overflow, l,
+                         by_parent ? 0u : L - l);
     KL_CHECK_LAUNCH();
   }
   unsigned long long *h = nullptr;
@@ -725,8 +1029,8 @@ static int mesh_to_spc_async(int64_t F, const float *fv, uint32_t L, Scratch &sc
     return (int64_t)t;
   };
   const int64_t cnt = rc == KL_OK ? level_total(L + 1) : 0;
-  if (rc == KL_OK && !over) {
-    for (uint32_t l = 0; l <= L; l++) t_m2s_counts[l] = level_total(l);
+  if (rc == KL_OK && !over) {  // proposals per level: the faces, then 8 per passing pair
+    for (uint32_t l = 0; l <= L; l++) t_m2s_counts[l] = (by_parent && l > 0 ? 8 : 1) * level_total(l);
     t_m2s_levels = (int)L + 1;
   }
   (void)hipHostFree(h);

@@ -285,7 +285,7 @@ def unbatched_triangle_distance_forward_cuda(points, face_vertices, dist, face_i
     N.require_gpu(func, points)
     dev = points.device
     lib = N.lib()
-    nbytes = lib.kl_unbatched_triangle_distance_workspace_bytes(P)
+    nbytes = lib.kl_unbatched_triangle_distance_workspace_bytes(P, F)
     ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     with N.on_device(dev), N.timed(func, dev):
         N.check(lib.kl_unbatched_triangle_distance_forward(

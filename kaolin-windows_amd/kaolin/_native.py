@@ -78,7 +78,7 @@ _SIGS = {
     'kl_prepare_vertices_bwd_workspace_bytes': (_SZ, [_I, _I64]),
     'kl_prepare_vertices_backward': (_I, [_I, _I, _I, _I, _I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                           _P, _P, _P, _SZ, _P]),
-    'kl_unbatched_triangle_distance_workspace_bytes': (_SZ, [_I64]),
+    'kl_unbatched_triangle_distance_workspace_bytes': (_SZ, [_I64, _I64]),
     'kl_unbatched_triangle_distance_forward': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_unbatched_triangle_distance_bwd_workspace_bytes': (_SZ, [_I64]),
     'kl_unbatched_triangle_distance_backward': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),

@@ -579,8 +579,8 @@ def _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box=0.02):
 @pytest.mark.parametrize('case', ['bench', 'adversarial', 'knum64', 'knum255', 'bigbox'])
 def test_dibr_fused_tile_kernel_equals_two_kernel_path(kal, case):
     """kl_dibr_forward's fused tile kernel (dibrtile.hip: the rasterizer and the soft mask in one
-    kernel over one chunk expansion) against its two-kernel path (dev param 10 = 1: raster_tile_kernel
-    then soft_tile_fwd_kernel): face_idx, weights, features, soft mask, the compact state's hits /
+    kernel over one chunk expansion; dev param 10 = 2) against the default two-kernel path
+    (raster_tile_kernel then soft_tile_fwd_kernel): face_idx, weights, features, soft mask, the compact state's hits /
     row totals / records, face ranges -- bit for bit; on the bench mesh, adversarial faces (NaN /
     inf / ties / duplicates / big faces), knum 64 and 255 (1-2 rows per work item), and a large
     boxlen whose enlarged bboxes overflow the kernel's LDS soft list (its second expansion)."""
@@ -598,9 +598,9 @@ def test_dibr_fused_tile_kernel_equals_two_kernel_path(kal, case):
         K = {'knum64': 64, 'knum255': 255}.get(case, 30)
         box = 0.2 if case == 'bigbox' else 0.02
     try:
-        fused = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box)
-        _dev_param(10, 1)
         two = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box)
+        _dev_param(10, 2)
+        fused = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box)
     finally:
         _dev_param(10, 0)
     names = ['features', 'face_idx', 'weights', 'soft_mask', 'hits', 'seg_tot', 'rec_face', 'rec_prob', 'ranges']
@@ -1060,6 +1060,51 @@ def test_mesh_to_spc_kat(kal, golden):
 def test_mesh_to_spc_vs_oracle(kal, level):
     v, f = _uv_sphere(16, 24, 0.9)
     fv = v[f].astype(np.float32)
+    octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(T(fv), level)
+    oo, of, ob = orc.mesh_to_spc(fv, level)
+    assert np.array_equal(A(octree), oo)
+    assert np.array_equal(A(fidx), of)
+    np.testing.assert_array_equal(A(bary), ob)
+
+
+def _grazing_triangles(level, seed=3):
+    """Triangles that sit on the SAT's decision boundaries at `level`: axis-aligned on voxel
+    planes (box-axis ties), planes through voxel corners (normal-axis ties, x + y + z = c and
+    x - y = c), near-collinear slivers and tiny triangles at corners, plus random ones."""
+    rng = np.random.RandomState(seed)
+    n = 2 ** level
+    g = lambda k: -1.0 + 2.0 * k / n  # noqa: E731  (voxel plane k, exact in float)
+    tris = []
+    for _ in range(200):
+        k = rng.randint(1, n)
+        a, b = np.sort(rng.uniform(-1, 1, 2)), np.sort(rng.uniform(-1, 1, 2))
+        ax = rng.randint(3)
+        t = np.array([[g(k), a[0], b[0]], [g(k), a[1], b[0]], [g(k), a[0], b[1]]])
+        tris.append(np.roll(t, ax, axis=1))
+    for _ in range(200):  # plane x + y + z = corner sum
+        c = g(rng.randint(0, n + 1)) + g(rng.randint(0, n + 1)) + g(rng.randint(0, n + 1))
+        p = rng.uniform(-1, 1, (3, 2))
+        tris.append(np.stack([p[:, 0], p[:, 1], c - p[:, 0] - p[:, 1]], 1))
+    for _ in range(200):  # plane x - y = corner difference, z free
+        c = g(rng.randint(0, n + 1)) - g(rng.randint(0, n + 1))
+        p = rng.uniform(-1, 1, (3, 2))
+        tris.append(np.stack([p[:, 0], p[:, 0] - c, p[:, 1]], 1))
+    for _ in range(200):  # slivers
+        a, d = rng.uniform(-0.9, 0.9, 3), rng.uniform(-0.5, 0.5, 3)
+        tris.append(np.stack([a, a + d, a + d * rng.uniform(0, 1) + rng.uniform(-1, 1, 3) * 1e-6]))
+    for _ in range(200):  # tiny, at a voxel corner
+        c = np.array([g(rng.randint(1, n)) for _ in range(3)])
+        tris.append(c + rng.uniform(-1, 1, (3, 3)) * 2.0 ** -(level + 4))
+    tris.extend(rng.uniform(-1, 1, (200, 3, 3)))
+    fv = np.clip(np.stack(tris), -1, 1).astype(np.float32)
+    return fv
+
+
+@pytest.mark.parametrize('level', [3, 5, 7])
+def test_mesh_to_spc_decision_boundaries_vs_oracle(kal, level):
+    """The level kernel's float pre-test (tri_voxel_maybe) only skips proposals the full fp64 SAT
+    rejects: grazing, coplanar-on-a-voxel-face and sliver triangles agree with the oracle bit for bit."""
+    fv = _grazing_triangles(level)
     octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(T(fv), level)
     oo, of, ob = orc.mesh_to_spc(fv, level)
     assert np.array_equal(A(octree), oo)
