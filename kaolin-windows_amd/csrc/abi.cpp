@@ -1,5 +1,6 @@
 // abi.cpp -- error channel and version of the libkaolin_hip.so C ABI.
 #include <algorithm>
+#include <cstring>
 #include <mutex>
 #include <string>
 
@@ -45,6 +46,29 @@ __global__ void __launch_bounds__(256) fill_kernel(uint8_t *__restrict__ p, size
   for (size_t i = t; i < nvec; i += nt) reinterpret_cast<uint4 *>(body)[i] = v;
   const size_t done = head + nvec * 16;
   if (t < bytes - done) p[done + t] = (uint8_t)v4;
+}
+
+int host_read(void *dst, const void *src, size_t bytes, hipStream_t st) {
+  static thread_local void *pinned = nullptr;
+  static thread_local size_t pinned_bytes = 0;
+  if (bytes > pinned_bytes) {
+    const size_t want = bytes < 4096 ? 4096 : bytes;
+    void *p = nullptr;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+      set_error("host_read: pinned allocation failed");
+      return KL_E_HIP;
+    }
+    if (pinned) (void)hipHostFree(pinned);  // grown: rare (the first calls only)
+    pinned = p;
+    pinned_bytes = want;
+  }
+  if (hipMemcpyAsync(pinned, src, bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    set_error("host_read: device to host copy failed");
+    return KL_E_HIP;
+  }
+  std::memcpy(dst, pinned, bytes);
+  return KL_OK;
 }
 
 int fill_async(void *p, int value, size_t bytes, hipStream_t st) {

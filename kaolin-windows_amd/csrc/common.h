@@ -34,6 +34,11 @@ __device__ __forceinline__ uint64_t stamp_clk() { return __builtin_readcyclecoun
 __device__ __forceinline__ uint64_t stamp_wall() { return __builtin_amdgcn_s_memrealtime(); }
 // memset as a kernel launch on `st` (graph-capture friendly); returns a kl_status
 int fill_async(void *p, int value, size_t bytes, hipStream_t st);
+// Reads `bytes` of device memory to the host once the stream reaches this point: a copy into a
+// thread-local pinned buffer (allocated once, grown when needed, never freed) and a stream
+// synchronise.  hipHostMalloc / hipHostFree per call, or a copy into pageable memory, cost
+// tens to hundreds of microseconds each (mesh_to_spc's three reads, r04).
+int host_read(void *dst, const void *src, size_t bytes, hipStream_t st);
 // Fork/join of one side stream of the current device inside one ABI call (event record +
 // wait, so it is captured into a HIP graph as two parallel branches).  SideFork's
 // constructor locks the device's side stream and makes it wait for `st`; side() is that

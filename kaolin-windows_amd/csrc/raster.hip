@@ -1400,6 +1400,9 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
   if (!__any(act)) return;  // wave-uniform
 #pragma unroll
   for (int q = 0; q < NV; q++) part[q * 64] = 0.0;
+  // lane s < 6's soft-mask sum, loaded now so that its latency hides behind the walk
+  double soft_v = 0.0;
+  if (act && soft && s < 6) soft_v = soft[tf * DS_ACC_STRIDE + s];
   if (act) {
     const int b = (int)(tf / F);
     const int64_t f = tf - (int64_t)b * F;
@@ -1467,7 +1470,12 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
       double x = 0.0;
 #pragma unroll
       for (int l = 0; l < 8; l++) x += s_part[wid][q][g0 + l];
-      g2_store<T, MAXD>(tf, q, x, D, soft, grad_fvi, grad_ffeat);
+      if (q < 6 && soft) {  // q == s: the prefetched sum, re-zeroed as take_soft does
+        grad_fvi[tf * 6 + q] = (T)x + (T)soft_v;
+        if (__double_as_longlong(soft_v) != 0) soft[tf * DS_ACC_STRIDE + q] = 0.0;
+      } else {
+        g2_store<T, MAXD>(tf, q, x, D, soft, grad_fvi, grad_ffeat);
+      }
     }
   }
 }

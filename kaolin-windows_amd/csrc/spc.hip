@@ -70,10 +70,7 @@ static int exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, Scratch 
   void *tmp = sc.get(tb);
   if (!tmp) return KL_E_ALLOC;
   KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, (int)n + 1, st));
-  if (total_host) {
-    KL_CHECK_HIP(hipMemcpyAsync(total_host, out + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    KL_CHECK_HIP(hipStreamSynchronize(st));
-  }
+  if (total_host) return host_read(total_host, out + n, sizeof(uint32_t), st);
   return KL_OK;
 }
 
@@ -861,6 +858,9 @@ __global__ void m2s_key_unique_kernel(int64_t n, const uint64_t *__restrict__ ke
 }
 
 // the first (lowest face) entry of every morton: the leaf, its face and barycentrics
+__device__ void leaf_out(uint64_t m, int64_t f, const float *__restrict__ fv, uint32_t level, uint32_t o,
+                         uint64_t *__restrict__ mout, int64_t *__restrict__ fout, float *__restrict__ bary);
+
 __global__ void m2s_key_leaves_kernel(int64_t n, const uint64_t *__restrict__ key, int fb,
                                       const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
                                       const float *__restrict__ fv, uint32_t level, uint64_t *__restrict__ mout,
@@ -868,8 +868,49 @@ __global__ void m2s_key_leaves_kernel(int64_t n, const uint64_t *__restrict__ ke
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t >= n || !flag[t]) return;
   const uint32_t o = psum[t];
-  const uint64_t m = key[t] >> fb;
-  const int64_t f = (int64_t)(key[t] & ((1ull << fb) - 1));
+  leaf_out(key[t] >> fb, (int64_t)(key[t] & ((1ull << fb) - 1)), fv, level, o, mout, fout, bary);
+}
+
+// (morton, face) pairs as 32-bit keys / values for levels with 3L <= 32: a radix sort over 3L key
+// bits moving 8 bytes per pair, against 3L + FB bits of 64-bit composite keys (cfg4 L = 9:
+// 27 against 45 bits).  The pairs' order among equal mortons is then arbitrary (appended through
+// sharded counters), so each leaf takes its run's least face -- the face the reference's stable
+// sort puts first (generation order is ascending face id, m2s_key_kernel's comment).
+__global__ void m2s_pair_kernel(int64_t n, const uint64_t *__restrict__ m, const uint32_t *__restrict__ t,
+                                const unsigned long long *__restrict__ cnt, unsigned long long seg,
+                                uint32_t *__restrict__ key, uint32_t *__restrict__ val) {
+  __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  ShardIn in;
+  in.load(s_pre, cnt, seg);
+  if (i >= n) return;
+  const unsigned long long p = in.pos((unsigned long long)i, seg);
+  key[i] = (uint32_t)m[p];
+  val[i] = t[p];
+}
+
+__global__ void m2s_pair_unique_kernel(int64_t n, const uint32_t *__restrict__ key, uint32_t *__restrict__ flag) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t > n) return;
+  flag[t] = (t == n) ? 0u : ((t == 0 || key[t - 1] != key[t]) ? 1u : 0u);
+}
+
+__global__ void m2s_pair_leaves_kernel(int64_t n, const uint32_t *__restrict__ key, const uint32_t *__restrict__ val,
+                                       const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
+                                       const float *__restrict__ fv, uint32_t level, uint64_t *__restrict__ mout,
+                                       int64_t *__restrict__ fout, float *__restrict__ bary) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= n || !flag[t]) return;
+  const uint32_t k = key[t];
+  uint32_t f = val[t];
+  for (int64_t s = t + 1; s < n && key[s] == k; s++) f = min(f, val[s]);
+  leaf_out(k, (int64_t)f, fv, level, psum[t], mout, fout, bary);
+}
+
+// leaf o: its morton, face, and the face's barycentrics at the voxel centre (spc_math.h:229-258)
+__device__ __forceinline__ void leaf_out_body(uint64_t m, int64_t f, const float *__restrict__ fv, uint32_t level,
+                                              uint32_t o, uint64_t *__restrict__ mout, int64_t *__restrict__ fout,
+                                              float *__restrict__ bary) {
   mout[o] = m;
   fout[o] = f;
   float cx, cy, cz, h;
@@ -894,6 +935,11 @@ __global__ void m2s_key_leaves_kernel(int64_t n, const uint64_t *__restrict__ ke
   const float sc = (float)(1. / (double)(bx + by + bz));
   bary[o * 2 + 0] = bx * sc;
   bary[o * 2 + 1] = by * sc;
+}
+
+__device__ void leaf_out(uint64_t m, int64_t f, const float *__restrict__ fv, uint32_t level, uint32_t o,
+                         uint64_t *__restrict__ mout, int64_t *__restrict__ fout, float *__restrict__ bary) {
+  leaf_out_body(m, f, fv, level, o, mout, fout, bary);
 }
 
 // Octree of sorted unique leaf mortons, all levels at once: row j (0..L-1) of `flag` marks
@@ -1014,14 +1060,9 @@ static int mesh_to_spc_async(int64_t F, const float *fv, uint32_t L, Scratch &sc
                          by_parent ? 0u : L - l);
     KL_CHECK_LAUNCH();
   }
-  unsigned long long *h = nullptr;
-  KL_CHECK_HIP(hipHostMalloc((void **)&h, cbytes, hipHostMallocDefault));
-  int rc = KL_OK;
-  if (hipMemcpyAsync(h, counts, cbytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess) {
-    set_error("mesh_to_spc: count read failed");
-    rc = KL_E_HIP;
-  }
+  std::vector<unsigned long long> hv(NC + 1);
+  unsigned long long *h = hv.data();
+  int rc = host_read(h, counts, cbytes, st);
   const bool over = rc == KL_OK && *(int *)(h + NC) != 0;
   auto level_total = [&](uint32_t l) {
     unsigned long long t = 0;
@@ -1033,12 +1074,43 @@ static int mesh_to_spc_async(int64_t F, const float *fv, uint32_t L, Scratch &sc
     for (uint32_t l = 0; l <= L; l++) t_m2s_counts[l] = (by_parent && l > 0 ? 8 : 1) * level_total(l);
     t_m2s_levels = (int)L + 1;
   }
-  (void)hipHostFree(h);
   if (rc) return rc;
   if (over) return 1;
   if (cnt == 0) return KL_OK;  // empty: (0,) u8, (0,) i64, (0,3) f32 built by the caller
   const uint32_t *fin_t = tb[(L + 1) & 1];
   const uint64_t *fin_m = mb[(L + 1) & 1];
+  if (3 * L <= 32 && g_dev_param[15] != 1) {  // 32-bit pairs (dev param 15 = 1: the 64-bit keys, A/B)
+    uint32_t *key = (uint32_t *)sc.get((size_t)cnt * 4), *val = (uint32_t *)sc.get((size_t)cnt * 4);
+    uint32_t *ks = (uint32_t *)sc.get((size_t)cnt * 4), *vs = (uint32_t *)sc.get((size_t)cnt * 4);
+    if (!key || !val || !ks || !vs) return KL_E_ALLOC;
+    hipLaunchKernelGGL(m2s_pair_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, fin_m, fin_t,
+                       counts + (L + 1) * M2S_SHARDS, seg, key, val);
+    KL_CHECK_LAUNCH();
+    size_t tbytes = 0;
+    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, key, ks, val, vs, (int)cnt, 0, (int)(3 * L), st));
+    void *tmp = sc.get(tbytes);
+    if (!tmp) return KL_E_ALLOC;
+    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tbytes, key, ks, val, vs, (int)cnt, 0, (int)(3 * L), st));
+    uint32_t *flag = (uint32_t *)sc.get((cnt + 1) * sizeof(uint32_t));
+    uint32_t *psum = (uint32_t *)sc.get((cnt + 2) * sizeof(uint32_t));
+    if (!flag || !psum) return KL_E_ALLOC;
+    hipLaunchKernelGGL(m2s_pair_unique_kernel, dim3((unsigned)cdiv(cnt + 1, 256)), dim3(256), 0, st, cnt, ks, flag);
+    KL_CHECK_LAUNCH();
+    uint32_t uniq = 0;
+    KL_CHECK_RC(exclusive_scan(flag, psum, cnt, sc, st, &uniq));
+    uint64_t *mu = (uint64_t *)sc.get((size_t)uniq * sizeof(uint64_t));
+    int64_t *fu = (int64_t *)sc.get((size_t)uniq * sizeof(int64_t));
+    float *bu = (float *)sc.get((size_t)uniq * 2 * sizeof(float));
+    if (!mu || !fu || !bu) return KL_E_ALLOC;
+    hipLaunchKernelGGL(m2s_pair_leaves_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, ks, vs, flag,
+                       psum, fv, L, mu, fu, bu);
+    KL_CHECK_LAUNCH();
+    KL_CHECK_RC(morton_to_octree_rows(uniq, mu, L, sc, octree, num_nodes, st));
+    *face_idx = fu;
+    *bary = bu;
+    *num_leaves = uniq;
+    return KL_OK;
+  }
   // keys into the free buffer pair's morton array, sorted into the other pair's
   uint64_t *key = mb[L & 1];
   hipLaunchKernelGGL(m2s_key_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, fin_m, fin_t,

@@ -329,23 +329,39 @@ static __global__ void __launch_bounds__(1024) tile_countorder2_kernel(
   if (!soft && order0 == nullptr) return;  // one order only (the fused tile kernel's)
   for (int i = threadIdx.x; i < ORD_HIST; i += blockDim.x) hist[i] = 0;
   __syncthreads();
-  for (int t = threadIdx.x; t < nt; t += blockDim.x) {
-    // word-major bitmap: a lane per tile, each word load coalesced across the wave, up to 32
-    // words in flight together (one round trip per tile for the bench's 25 words; 8 at a time
-    // took 4 round trips per tile)
-    const uint32_t *w = bm + t;
-    unsigned n = 0;
+  // word-major bitmap: a lane per tile, each word load coalesced across the wave; two tiles per
+  // lane with up to 2 x 32 words in flight together (one round trip per two tiles for the bench's
+  // 25 words and 2,048 tiles: the words were just written by every XCD's binning workgroups, so
+  // each round trip is a far one -- stamps: 7.6 us for the count with one tile per round trip).
+  // Raw buffer loads: the tile's byte offset in one VGPR, the word's in an SGPR (64 loads in
+  // flight need no per-load address registers), and words past the bitmap read as 0.
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)bm, (short)0, words * nt * 4, 0x00020000);
+  for (int t0 = threadIdx.x; t0 < nt; t0 += 2 * blockDim.x) {
+    const int t1 = t0 + blockDim.x;  // past nt: other words' bits, discarded
+    unsigned n0 = 0, n1 = 0;
     for (int k0 = 0; k0 < words; k0 += 32) {
-      uint32_t x[32];
-      // unconditional loads from a clamped word (a guarded load is waited for inside its branch)
+      uint32_t x[32], y[32];
 #pragma unroll
-      for (int u = 0; u < 32; u++) x[u] = w[(size_t)(k0 + u < words ? k0 + u : words - 1) * nt];
+      for (int u = 0; u < 32; u++) {
+        const int so = (k0 + u) * nt * 4;
+        x[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, t0 * 4, so, 0);
+        y[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, t1 * 4, so, 0);
+      }
 #pragma unroll
-      for (int u = 0; u < 32; u++) n += k0 + u < words ? __popc(x[u]) : 0u;
+      for (int u = 0; u < 32; u++) {
+        n0 += __popc(x[u]);
+        n1 += __popc(y[u]);
+      }
     }
-    const int q = 31 - __clz(n + 1u);
-    sbk[t] = (uint8_t)q;
-    atomicAdd(&hist[tile_band(t, nt) * ORD_BUCKETS + q], 1);
+    const int q0 = 31 - __clz(n0 + 1u);
+    sbk[t0] = (uint8_t)q0;
+    atomicAdd(&hist[tile_band(t0, nt) * ORD_BUCKETS + q0], 1);
+    if (t1 < nt) {
+      const int q1 = 31 - __clz(n1 + 1u);
+      sbk[t1] = (uint8_t)q1;
+      atomicAdd(&hist[tile_band(t1, nt) * ORD_BUCKETS + q1], 1);
+    }
   }
   __syncthreads();
   if (dbg && threadIdx.x == 0) dbg[1] = stamp_wall();

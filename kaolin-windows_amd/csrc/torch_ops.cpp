@@ -1,4 +1,5 @@
-// torch_ops.cpp -- the eager host path of dibr_rasterization as a compiled autograd node.
+// torch_ops.cpp -- the eager host path of dibr_rasterization (and of the tutorial loop's other
+// library ops: prepare_vertices, mask_iou, texture_mapping) as compiled autograd nodes.
 //
 // The reference's native layer is a compiled extension (kaolin/csrc/bindings.cpp); its Python
 // front-end (render/mesh/dibr.py:119-209) pays one autograd Function per op.  The ctypes route of
@@ -35,7 +36,7 @@ void check(int rc, const char *func) {
 kl_dtype dtype_code(at::ScalarType t) {
   if (t == at::kFloat) return KL_F32;
   if (t == at::kDouble) return KL_F64;
-  throw std::runtime_error("dibr_rasterization: f32 / f64 only");
+  throw std::runtime_error("kaolin compiled node: f32 / f64 only");
 }
 
 // scratch reused across calls on one (device, stream), grown to the largest request: every entry
@@ -142,6 +143,162 @@ struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
   }
 };
 
+// mask_iou (metrics/render.py MaskIouHip): kl_mask_iou_forward / _backward
+struct MaskIou : public torch::autograd::Function<MaskIou> {
+  static variable_list forward(AutogradContext *ctx, at::Tensor lhs, at::Tensor rhs, int64_t stream) {
+    lhs = lhs.contiguous();
+    rhs = rhs.contiguous();
+    const int64_t B = lhs.size(0), n = lhs.numel() / B;
+    const auto opt = lhs.options();
+    at::Tensor up = at::empty({B}, opt), down = at::empty({B}, opt), loss = at::empty({}, opt);
+    const size_t nbytes = kl_mask_iou_workspace_bytes((int)B, n);
+    at::Tensor ws = workspace(nbytes, lhs.device(), stream);
+    check(kl_mask_iou_forward(dtype_code(lhs.scalar_type()), (int)B, n, ptr(lhs), ptr(rhs), ptr(up), ptr(down),
+                              ptr(loss), ws.data_ptr(), nbytes, (kl_stream)stream),
+          "mask_iou");
+    ctx->saved_data["stream"] = stream;
+    ctx->save_for_backward({lhs, rhs, up, down});
+    return {loss};
+  }
+  static variable_list backward(AutogradContext *ctx, variable_list grads) {
+    const auto saved = ctx->get_saved_variables();
+    const at::Tensor &lhs = saved[0], &rhs = saved[1], &up = saved[2], &down = saved[3];
+    const bool need_l = ctx->needs_input_grad(0), need_r = ctx->needs_input_grad(1);
+    variable_list out(3);
+    if (!need_l && !need_r) return out;
+    at::Tensor gl = need_l ? at::empty_like(lhs) : at::Tensor(), gr = need_r ? at::empty_like(rhs) : at::Tensor();
+    at::Tensor g = grads[0].defined() ? grads[0].contiguous() : at::ones({}, lhs.options());
+    const int64_t B = lhs.size(0);
+    check(kl_mask_iou_backward(dtype_code(lhs.scalar_type()), (int)B, lhs.numel() / B, ptr(g), ptr(lhs), ptr(rhs),
+                               ptr(up), ptr(down), ptr(gl), ptr(gr), (kl_stream)ctx->saved_data["stream"].toInt()),
+          "mask_iou backward");
+    out[0] = gl;
+    out[1] = gr;
+    return out;
+  }
+};
+
+at::Tensor mask_iou(at::Tensor lhs, at::Tensor rhs, int64_t stream) { return MaskIou::apply(lhs, rhs, stream)[0]; }
+
+// prepare_vertices (render/mesh/utils.py PrepareVerticesHip): kl_prepare_vertices_forward / _backward.
+// cam_a, cam_b = rot, trans; or xf (camera_transform) twice (has_xf; the second slot gets no
+// gradient) -- autograd's apply takes no undefined tensors.  batches (B, Bv, Bc, Bp) as the Python
+// front-end computes them.
+struct PrepareVertices : public torch::autograd::Function<PrepareVertices> {
+  static variable_list forward(AutogradContext *ctx, at::Tensor vertices, at::Tensor faces, at::Tensor proj,
+                               at::Tensor cam_a, at::Tensor cam_b, bool has_xf, std::vector<int64_t> batches,
+                               int64_t stream) {
+    const int64_t B = batches[0], Bv = batches[1], Bc = batches[2], Bp = batches[3];
+    at::Tensor verts = vertices.contiguous(), fc = faces.contiguous(), pj = proj.contiguous();
+    at::Tensor r = has_xf ? at::Tensor() : cam_a.contiguous(), t = has_xf ? at::Tensor() : cam_b.contiguous();
+    at::Tensor x = has_xf ? cam_a.contiguous() : at::Tensor();
+    const int64_t V = verts.size(1), F = fc.size(0);
+    const auto opt = verts.options();
+    at::Tensor fvc = at::empty({B, F, 3, 3}, opt), fvi = at::empty({B, F, 3, 2}, opt), fn = at::empty({B, F, 3}, opt);
+    check(kl_prepare_vertices_forward(dtype_code(verts.scalar_type()), (int)B, (int)Bv, (int)Bc, (int)Bp, V, F,
+                                      ptr(verts), fc.data_ptr<int64_t>(), ptr(r), ptr(t), ptr(x), ptr(pj), ptr(fvc),
+                                      ptr(fvi), ptr(fn), (kl_stream)stream),
+          "prepare_vertices");
+    ctx->saved_data["batches"] = batches;
+    ctx->saved_data["stream"] = stream;
+    ctx->saved_data["proj_shape"] = proj.sizes().vec();
+    ctx->saved_data["trans_shape"] = has_xf ? std::vector<int64_t>{} : cam_b.sizes().vec();
+    ctx->saved_data["has_xf"] = has_xf;
+    ctx->set_materialize_grads(false);
+    ctx->save_for_backward({verts, fc, pj, r, t, x});
+    return {fvc, fvi, fn};
+  }
+  static variable_list backward(AutogradContext *ctx, variable_list grads) {
+    const auto saved = ctx->get_saved_variables();
+    const at::Tensor &verts = saved[0], &fc = saved[1], &pj = saved[2], &r = saved[3], &t = saved[4], &x = saved[5];
+    variable_list out(8);
+    if (!grads[0].defined() && !grads[1].defined() && !grads[2].defined()) return out;
+    const auto b = ctx->saved_data["batches"].toIntVector();
+    const int64_t B = b[0], Bv = b[1], Bc = b[2], Bp = b[3];
+    const bool has_xf = ctx->saved_data["has_xf"].toBool();
+    const bool need_v = ctx->needs_input_grad(0), need_p = ctx->needs_input_grad(2),
+               need_r = !has_xf && ctx->needs_input_grad(3), need_t = !has_xf && ctx->needs_input_grad(4),
+               need_x = has_xf && ctx->needs_input_grad(3);
+    const auto opt = verts.options();
+    at::Tensor g_v = need_v ? at::empty_like(verts) : at::Tensor();
+    at::Tensor g_cam = (need_r || need_t || need_x) ? at::empty({Bc, 12}, opt) : at::Tensor();
+    at::Tensor g_proj = need_p ? at::empty({Bp, 3}, opt) : at::Tensor();
+    const int64_t V = verts.size(1), F = fc.size(0);
+    const int64_t stream = ctx->saved_data["stream"].toInt();
+    const size_t nbytes = kl_prepare_vertices_bwd_workspace_bytes((int)B, V);
+    at::Tensor ws = workspace(nbytes, verts.device(), stream);
+    at::Tensor g0 = grads[0].defined() ? grads[0].contiguous() : at::Tensor();
+    at::Tensor g1 = grads[1].defined() ? grads[1].contiguous() : at::Tensor();
+    at::Tensor g2 = grads[2].defined() ? grads[2].contiguous() : at::Tensor();
+    check(kl_prepare_vertices_backward(dtype_code(verts.scalar_type()), (int)B, (int)Bv, (int)Bc, (int)Bp, V, F,
+                                       ptr(verts), fc.data_ptr<int64_t>(), ptr(r), ptr(t), ptr(x), ptr(pj), ptr(g0),
+                                       ptr(g1), ptr(g2), ptr(g_v), ptr(g_cam), ptr(g_proj), ws.data_ptr(), nbytes,
+                                       (kl_stream)stream),
+          "prepare_vertices backward");
+    out[0] = g_v;
+    if (need_p) out[2] = g_proj.reshape(ctx->saved_data["proj_shape"].toIntVector());
+    if (need_r) out[3] = g_cam.narrow(1, 0, 9).reshape({Bc, 3, 3});
+    if (need_t) out[4] = g_cam.narrow(1, 9, 3).reshape(ctx->saved_data["trans_shape"].toIntVector());
+    if (need_x) out[3] = g_cam.reshape({Bc, 4, 3});
+    return out;
+  }
+};
+
+std::tuple<at::Tensor, at::Tensor, at::Tensor> prepare_vertices(at::Tensor vertices, at::Tensor faces, at::Tensor proj,
+                                                                c10::optional<at::Tensor> rot,
+                                                                c10::optional<at::Tensor> trans,
+                                                                c10::optional<at::Tensor> xf,
+                                                                std::vector<int64_t> batches, int64_t stream) {
+  const bool has_xf = xf.has_value() && xf->defined();
+  TORCH_CHECK(has_xf || (rot.has_value() && trans.has_value()), "prepare_vertices: camera_rot and camera_trans, or "
+              "camera_transform");
+  auto r = has_xf ? PrepareVertices::apply(vertices, faces, proj, *xf, *xf, true, batches, stream)
+                  : PrepareVertices::apply(vertices, faces, proj, *rot, *trans, false, batches, stream);
+  return {r[0], r[1], r[2]};
+}
+
+// texture_mapping (render/mesh/utils.py TextureMappingHip): kl_texture_mapping_forward / _backward
+struct TextureMapping : public torch::autograd::Function<TextureMapping> {
+  static variable_list forward(AutogradContext *ctx, at::Tensor coords, at::Tensor tex, int64_t mode, int64_t stream) {
+    at::Tensor c = coords.contiguous(), t = tex.contiguous();
+    const int64_t B = t.size(0), C = t.size(1), TH = t.size(2), TW = t.size(3);
+    const int64_t n = B ? c.numel() / (2 * B) : 0;
+    at::Tensor out = at::empty({B, n, C}, t.options());
+    check(kl_texture_mapping_forward(dtype_code(t.scalar_type()), (int)mode, (int)B, n, (int)C, (int)TH, (int)TW,
+                                     ptr(c), ptr(t), ptr(out), (kl_stream)stream),
+          "texture_mapping");
+    ctx->saved_data["mode"] = mode;
+    ctx->saved_data["n"] = n;
+    ctx->saved_data["stream"] = stream;
+    ctx->save_for_backward({c, t});
+    return {out};
+  }
+  static variable_list backward(AutogradContext *ctx, variable_list grads) {
+    const auto saved = ctx->get_saved_variables();
+    const at::Tensor &c = saved[0], &t = saved[1];
+    const bool need_c = ctx->needs_input_grad(0), need_t = ctx->needs_input_grad(1);
+    variable_list out(4);
+    if ((!need_c && !need_t) || !grads[0].defined()) return out;
+    const int64_t B = t.size(0), C = t.size(1), TH = t.size(2), TW = t.size(3);
+    const int64_t stream = ctx->saved_data["stream"].toInt();
+    at::Tensor gc = need_c ? at::empty_like(c) : at::Tensor(), gt = need_t ? at::empty_like(t) : at::Tensor();
+    const size_t nbytes = need_t ? kl_texture_mapping_bwd_workspace_bytes((int)B, (int)C, (int)TH, (int)TW) : 0;
+    at::Tensor ws = need_t ? workspace(nbytes, t.device(), stream) : at::Tensor();
+    check(kl_texture_mapping_backward(dtype_code(t.scalar_type()), (int)ctx->saved_data["mode"].toInt(), (int)B,
+                                      ctx->saved_data["n"].toInt(), (int)C, (int)TH, (int)TW,
+                                      ptr(grads[0].contiguous()), ptr(c), ptr(t), ptr(gc), ptr(gt), ptr(ws), nbytes,
+                                      (kl_stream)stream),
+          "texture_mapping backward");
+    out[0] = gc;
+    out[1] = gt;
+    return out;
+  }
+};
+
+at::Tensor texture_mapping(at::Tensor coords, at::Tensor tex, int64_t mode, int64_t stream) {
+  return TextureMapping::apply(coords, tex, mode, stream)[0];
+}
+
 std::tuple<at::Tensor, at::Tensor, at::Tensor> dibr_rasterization(int64_t height, int64_t width, at::Tensor fvz,
                                                                    at::Tensor fvi, at::Tensor feat, at::Tensor fnz,
                                                                    double sigmainv, double boxlen, int64_t knum,
@@ -158,4 +315,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("abi_version", []() { return kl_abi_version(); });
   m.def("dibr_rasterization", &dibr_rasterization,
         "dibr_rasterization's fused node: (features, soft_mask, face_idx); see kaolin/render/mesh/dibr.py");
+  m.def("mask_iou", &mask_iou, "mask_iou's fused node; see kaolin/metrics/render.py");
+  m.def("prepare_vertices", &prepare_vertices, "prepare_vertices' node; see kaolin/render/mesh/utils.py");
+  m.def("texture_mapping", &texture_mapping, "texture_mapping's node; see kaolin/render/mesh/utils.py");
 }

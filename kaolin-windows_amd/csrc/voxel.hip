@@ -159,8 +159,7 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
     set_error("trianglemeshes_to_voxelgrids: allocation failed");
     return KL_E_ALLOC;
   }
-  unsigned long long *hcount = nullptr;
-  KL_CHECK_HIP(hipHostMalloc((void **)&hcount, sizeof(unsigned long long), hipHostMallocDefault));
+  unsigned long long hcount_v = 0, *hcount = &hcount_v;
   hipLaunchKernelGGL(gather_tris_kernel<T>, dim3((unsigned)cdiv(F, 256)), dim3(256), 0, st, F, pts, faces, cur);
   KL_CHECK_LAUNCH();
   int64_t n = F;
@@ -187,17 +186,16 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
     if (rc) break;
     hipLaunchKernelGGL((subdivide_kernel<T, G>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, n, buf[ci],
                        level == 0, thr, R, grid, nxt, counter);
-    if (hipGetLastError() != hipSuccess ||
-        hipMemcpyAsync(hcount, counter, sizeof(unsigned long long), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
+    if (hipGetLastError() != hipSuccess) {
       set_error("voxelgrid subdivision launch failed");
       rc = KL_E_HIP;
       break;
     }
+    rc = host_read(hcount, counter, sizeof(unsigned long long), st);
+    if (rc) break;
     n = (int64_t)*hcount;
     ci = ni;
   }
-  (void)hipHostFree(hcount);
   return rc;
 }
 

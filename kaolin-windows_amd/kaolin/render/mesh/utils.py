@@ -11,7 +11,7 @@ import weakref
 import torch
 from torch.autograd import Function
 
-from ... import _native as N
+from ... import _ext, _native as N
 from ...ops.mesh import face_normals as _face_normals
 from ...ops.mesh import index_vertices_by_faces
 from ..camera import perspective_camera, rotate_translate_points
@@ -172,6 +172,11 @@ def prepare_vertices(vertices, faces, camera_proj, camera_rot=None, camera_trans
     if batches is None:
         return _prepare_vertices_torch(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform)
     _check_faces(faces, vertices.shape[1])
+    ext = _ext.get()
+    if ext is not None and N._TIMER is None and vertices.device.index == torch.cuda.current_device():
+        # the same node compiled (csrc/torch_ops.cpp): no Python in the autograd node
+        return ext.prepare_vertices(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform,
+                                    list(batches), N.stream_of(vertices.device))
     return PrepareVerticesHip.apply(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform, batches)
 
 
@@ -230,7 +235,12 @@ def texture_mapping(texture_coordinates, texture_maps, mode='nearest'):
             and mode in ('nearest', 'bilinear') and texture_maps.dtype in (torch.float32, torch.float64)
             and texture_coordinates.dtype == texture_maps.dtype and texture_maps.dim() == 4
             and texture_coordinates.shape[-1] == 2 and texture_maps.shape[0] == batch_size):
-        out = TextureMappingHip.apply(texture_coordinates, texture_maps, 1 if mode == 'bilinear' else 0)
+        ext = _ext.get()
+        if ext is not None and texture_maps.device.index == torch.cuda.current_device():
+            out = ext.texture_mapping(texture_coordinates, texture_maps, 1 if mode == 'bilinear' else 0,
+                                      N.stream_of(texture_maps.device))
+        else:
+            out = TextureMappingHip.apply(texture_coordinates, texture_maps, 1 if mode == 'bilinear' else 0)
         return out.reshape(batch_size, *texture_coordinates.shape[1:-1], num_channels)
     coords = texture_coordinates.reshape(batch_size, -1, 1, 2)
     coords = torch.clamp(coords, 0., 1.) * 2 - 1

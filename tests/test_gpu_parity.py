@@ -661,6 +661,62 @@ def test_compiled_node_equals_python_node(kal, monkeypatch):
         assert torch.equal(x, y)
 
 
+@pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
+@pytest.mark.parametrize('cams', ['rot_trans', 'transform'])
+def test_compiled_tutorial_nodes_equal_python_nodes(kal, monkeypatch, dtype, cams):
+    """The tutorial loop's other library ops as compiled nodes (csrc/torch_ops.cpp: prepare_vertices,
+    mask_iou, texture_mapping) against their Python / ctypes nodes: outputs and every gradient
+    (vertices, cameras, projection, texture, coordinates, both masks) bit-equal."""
+    from kaolin import _ext
+    assert _ext.get() is not None, 'the compiled nodes are not built (kaolin/_lib/ext)'
+    g = torch.Generator(device='cpu').manual_seed(3)
+    B = 2
+    sv, sf = _uv_sphere(6, 8, 0.5)  # a well-conditioned mesh (random faces make f64 sums ill-conditioned)
+    verts = (torch.from_numpy(sv)[None] + (torch.rand((1, len(sv), 3), generator=g, dtype=torch.float64) - 0.5)
+             * 0.05).to(dtype)
+    faces = torch.from_numpy(np.asarray(sf, dtype=np.int64))
+    proj = torch.tensor([[2.0], [2.0], [-1.0]], dtype=dtype)
+    rot = torch.linalg.qr(torch.rand((B, 3, 3), generator=g, dtype=torch.float64))[0].to(dtype)
+    trans = torch.rand((B, 3), generator=g, dtype=dtype) * 0.1 + torch.tensor([0, 0, 3.], dtype=dtype)
+    xf = torch.cat([rot, trans[:, None]], 1)
+    tex = torch.rand((B, 3, 16, 24), generator=g, dtype=dtype)
+    uv = torch.rand((B, 12, 10, 2), generator=g, dtype=dtype) * 1.2 - 0.1
+    m1 = torch.rand((B, 12, 10), generator=g, dtype=dtype)
+    m2 = (torch.rand((B, 12, 10), generator=g) > 0.5).to(dtype)
+    runs = []
+    for use_ext in (True, False):
+        if not use_ext:
+            monkeypatch.setattr(_ext, '_mod', None)
+        leaves = [t.to(DEV).requires_grad_(True) for t in (verts, proj, rot, trans, xf, tex, uv, m1, m2)]
+        v_, p_, r_, t_, x_, tx_, uv_, a_, b_ = leaves
+        if cams == 'rot_trans':
+            fvc, fvi, fn = kal.render.mesh.prepare_vertices(v_, faces.to(DEV), p_, camera_rot=r_, camera_trans=t_)
+        else:
+            fvc, fvi, fn = kal.render.mesh.prepare_vertices(v_, faces.to(DEV), p_, camera_transform=x_)
+        img = kal.render.mesh.texture_mapping(uv_, tx_, mode='bilinear')
+        loss = kal.metrics.render.mask_iou(a_, b_)
+        def node(t):  # the op's own node under any view / reshape nodes
+            n = t.grad_fn
+            while 'View' in n.name() or 'Reshape' in n.name():
+                n = n.next_functions[0][0]
+            return n.name()
+        names = [node(fvc), node(img), node(loss)]
+        assert all('CppNode' in n for n in names) if use_ext else not any('CppNode' in n for n in names), names
+        gg = torch.Generator(device='cpu').manual_seed(9)
+        outs = [fvc, fvi, fn, img]
+        ups = [torch.rand(o.shape, generator=gg, dtype=dtype).to(DEV) for o in outs]
+        torch.autograd.backward(outs + [loss], ups + [torch.tensor(0.7, dtype=dtype, device=DEV)])
+        runs.append([o.detach() for o in outs + [loss]] + [t.grad if t.grad is not None else torch.zeros(())
+                                                           for t in leaves])
+    for k, (x, y) in enumerate(zip(runs[0], runs[1])):
+        if dtype == torch.float64 and k >= 5:
+            # f64 gradient terms are summed with double atomics (order-dependent last bits, DESIGN 4)
+            d = (x - y).abs().max().item() if x.numel() else 0.0
+            assert torch.allclose(x, y, rtol=1e-12, atol=1e-12), (k, d)
+        else:
+            assert torch.equal(x, y), k
+
+
 def test_dibr_mixed_dtypes_raise(kal, monkeypatch):
     """A float input of another dtype than face_vertices_image raises (the reference's
     data_ptr<scalar_t>() check) on the compiled node and on the Python node alike -- it is
