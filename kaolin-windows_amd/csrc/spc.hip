@@ -63,6 +63,33 @@ struct Scratch {
   void *get(size_t bytes) { return alloc(ctx, bytes > 0 ? bytes : 16); }
 };
 
+// Temporaries of one phase from ONE allocation: each allocation through the caller's allocator
+// is a host callback (torch's caching allocator via ctypes, ~5-10 us), and after a host read the
+// GPU idles while the host allocates.  Requests past the chunk go to the parent allocator;
+// outputs handed back to the caller must come from the parent itself.
+struct Bump {
+  Scratch *parent;
+  char *p;
+  size_t left;
+};
+static void *bump_alloc(void *ctx, size_t bytes) {
+  Bump *b = static_cast<Bump *>(ctx);
+  const size_t need = (std::max<size_t>(bytes, 16) + 255) & ~(size_t)255;
+  if (b->p && need <= b->left) {
+    void *r = b->p;
+    b->p += need;
+    b->left -= need;
+    return r;
+  }
+  return b->parent->get(bytes);
+}
+static size_t al256b(size_t v) { return (std::max<size_t>(v, 16) + 255) & ~(size_t)255; }
+static size_t scan_tmp_bytes(int64_t n) {
+  size_t tb = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)n + 1);
+  return tb;
+}
+
 static int exclusive_scan(const uint32_t *in, uint32_t *out, int64_t n, Scratch &sc, hipStream_t st,
                           uint32_t *total_host) {
   size_t tb = 0;
@@ -895,16 +922,42 @@ __global__ void m2s_pair_unique_kernel(int64_t n, const uint32_t *__restrict__ k
   flag[t] = (t == n) ? 0u : ((t == 0 || key[t - 1] != key[t]) ? 1u : 0u);
 }
 
-__global__ void m2s_pair_leaves_kernel(int64_t n, const uint32_t *__restrict__ key, const uint32_t *__restrict__ val,
-                                       const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
+// the runs' first positions, densely (leaf o's run starts at starts[o]): one thread per leaf in
+// the leaves kernel instead of one per pair with a quarter of the lanes busy (57 against ~15 us)
+__global__ void m2s_run_starts_kernel(int64_t n, const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
+                                      uint32_t *__restrict__ starts) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t < n && flag[t]) starts[psum[t]] = (uint32_t)t;
+}
+
+__global__ void m2s_pair_leaves_kernel(int64_t n, int64_t nleaves, const uint32_t *__restrict__ key,
+                                       const uint32_t *__restrict__ val, const uint32_t *__restrict__ starts,
                                        const float *__restrict__ fv, uint32_t level, uint64_t *__restrict__ mout,
                                        int64_t *__restrict__ fout, float *__restrict__ bary) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= n || !flag[t]) return;
+  const int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (o >= nleaves) return;
+  const int64_t t = starts[o];
   const uint32_t k = key[t];
   uint32_t f = val[t];
-  for (int64_t s = t + 1; s < n && key[s] == k; s++) f = min(f, val[s]);
-  leaf_out(k, (int64_t)f, fv, level, psum[t], mout, fout, bary);
+  // the run's least face: 8 entries per round trip (clamped, unconditional loads; a run is a few
+  // pairs -- 4.5 per leaf at cfg4 -- and one entry per dependent load took 92 us there)
+  for (int64_t s = t + 1;; s += 8) {
+    uint32_t kk[8], vv[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int64_t i = s + u < n ? s + u : n - 1;
+      kk[u] = key[i];
+      vv[u] = val[i];
+    }
+    bool run = true;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      run = run && s + u < n && kk[u] == k;
+      if (run) f = min(f, vv[u]);
+    }
+    if (!run) break;
+  }
+  leaf_out(k, (int64_t)f, fv, level, (uint32_t)o, mout, fout, bary);
 }
 
 // leaf o: its morton, face, and the face's barycentrics at the voxel centre (spc_math.h:229-258)
@@ -987,13 +1040,18 @@ __global__ void oct_byte_kernel(int64_t n, const uint64_t *__restrict__ m, uint3
   out[p] = (uint8_t)code;
 }
 
-static int morton_to_octree_rows(int64_t n, const uint64_t *morton, uint32_t L, Scratch &sc, uint8_t **octree,
+static int morton_to_octree_rows(int64_t n, const uint64_t *morton, uint32_t L, Scratch &psc, uint8_t **octree,
                                  int64_t *num_nodes, hipStream_t st) {
   *octree = nullptr;
   *num_nodes = 0;
-  if (L == 0 || n == 0) return morton_to_octree_impl(n, morton, L, sc, octree, num_nodes, st);
+  if (L == 0 || n == 0) return morton_to_octree_impl(n, morton, L, psc, octree, num_nodes, st);
   const int64_t len = (int64_t)L * (n + 1);
-  if (len + 1 >= ((int64_t)1 << 31)) return morton_to_octree_impl(n, morton, L, sc, octree, num_nodes, st);
+  if (len + 1 >= ((int64_t)1 << 31)) return morton_to_octree_impl(n, morton, L, psc, octree, num_nodes, st);
+  // the temporaries (rows, scan, first leaves: at most len nodes) from one allocation
+  const size_t chunk = al256b((size_t)len * 4) + al256b((size_t)(len + 1) * 4) + al256b(scan_tmp_bytes(len - 1)) +
+                       al256b((size_t)len * 4);
+  Bump bump{&psc, (char *)psc.get(chunk), chunk};
+  Scratch sc{bump_alloc, &bump};
   uint32_t *flag = (uint32_t *)sc.get((size_t)len * sizeof(uint32_t));
   uint32_t *psum = (uint32_t *)sc.get((size_t)(len + 1) * sizeof(uint32_t));
   if (!flag || !psum) return KL_E_ALLOC;
@@ -1002,7 +1060,7 @@ static int morton_to_octree_rows(int64_t n, const uint64_t *morton, uint32_t L, 
   uint32_t total = 0;
   KL_CHECK_RC(exclusive_scan(flag, psum, len - 1, sc, st, &total));  // psum[len - 1] = nodes (last sentinel 0)
   uint32_t *first = (uint32_t *)sc.get((size_t)total * sizeof(uint32_t));
-  uint8_t *out = (uint8_t *)sc.get((size_t)total);
+  uint8_t *out = (uint8_t *)psc.get((size_t)total);  // the caller's output
   if (!first || !out) return KL_E_ALLOC;
   hipLaunchKernelGGL(oct_first_kernel, dim3((unsigned)cdiv(n, 256), L), dim3(256), 0, st, n, flag, psum, first);
   KL_CHECK_LAUNCH();
@@ -1025,17 +1083,21 @@ static int mesh_to_spc_async(int64_t F, const float *fv, uint32_t L, Scratch &sc
   // capacity per level buffer: 96 proposals per face (cfg4: 9.4 M of 19.2 M at L = 9), in shards
   const unsigned long long cap = (unsigned long long)std::max<int64_t>(F * 96, (int64_t)1 << 20);
   if (cap >= (1ull << 31)) return 1;
-  uint64_t *mb[2];
-  uint32_t *tb[2];
-  for (int k = 0; k < 2; k++) {
-    mb[k] = (uint64_t *)sc.get((size_t)cap * sizeof(uint64_t));
-    tb[k] = (uint32_t *)sc.get((size_t)cap * sizeof(uint32_t));
-    if (!mb[k] || !tb[k]) return KL_E_ALLOC;
-  }
   // counts[l][shard] for l = 0 .. L+1 (proposals per level, then the final pairs), overflow flag
   const int NC = (SPC_MAX_LEVELS + 2) * M2S_SHARDS;
   const size_t cbytes = sizeof(unsigned long long) * (NC + 1);
-  unsigned long long *counts = (unsigned long long *)sc.get(cbytes);
+  // the level buffers and the counters from one allocation
+  const size_t chunk = 2 * (al256b((size_t)cap * 8) + al256b((size_t)cap * 4)) + al256b(cbytes);
+  Bump bump0{&sc, (char *)sc.get(chunk), chunk};
+  Scratch sc0{bump_alloc, &bump0};
+  uint64_t *mb[2];
+  uint32_t *tb[2];
+  for (int k = 0; k < 2; k++) {
+    mb[k] = (uint64_t *)sc0.get((size_t)cap * sizeof(uint64_t));
+    tb[k] = (uint32_t *)sc0.get((size_t)cap * sizeof(uint32_t));
+    if (!mb[k] || !tb[k]) return KL_E_ALLOC;
+  }
+  unsigned long long *counts = (unsigned long long *)sc0.get(cbytes);
   if (!counts) return KL_E_ALLOC;
   int *overflow = (int *)(counts + NC);
   const unsigned long long seg = cap / M2S_SHARDS;
@@ -1080,30 +1142,41 @@ static int mesh_to_spc_async(int64_t F, const float *fv, uint32_t L, Scratch &sc
   const uint32_t *fin_t = tb[(L + 1) & 1];
   const uint64_t *fin_m = mb[(L + 1) & 1];
   if (3 * L <= 32 && g_dev_param[15] != 1) {  // 32-bit pairs (dev param 15 = 1: the 64-bit keys, A/B)
-    uint32_t *key = (uint32_t *)sc.get((size_t)cnt * 4), *val = (uint32_t *)sc.get((size_t)cnt * 4);
-    uint32_t *ks = (uint32_t *)sc.get((size_t)cnt * 4), *vs = (uint32_t *)sc.get((size_t)cnt * 4);
+    size_t tbytes = 0;
+    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                    (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)cnt, 0,
+                                                    (int)(3 * L), st));
+    // this phase's temporaries (mortons of the leaves: at most cnt) from one allocation
+    const size_t chunk = 4 * al256b((size_t)cnt * 4) + al256b(tbytes) + al256b((cnt + 1) * 4) + al256b((cnt + 2) * 4) +
+                         al256b(scan_tmp_bytes(cnt)) + al256b((size_t)cnt * 8);
+    Bump bump{&sc, (char *)sc.get(chunk), chunk};
+    Scratch bsc{bump_alloc, &bump};
+    uint32_t *key = (uint32_t *)bsc.get((size_t)cnt * 4), *val = (uint32_t *)bsc.get((size_t)cnt * 4);
+    uint32_t *ks = (uint32_t *)bsc.get((size_t)cnt * 4), *vs = (uint32_t *)bsc.get((size_t)cnt * 4);
     if (!key || !val || !ks || !vs) return KL_E_ALLOC;
     hipLaunchKernelGGL(m2s_pair_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, fin_m, fin_t,
                        counts + (L + 1) * M2S_SHARDS, seg, key, val);
     KL_CHECK_LAUNCH();
-    size_t tbytes = 0;
-    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, key, ks, val, vs, (int)cnt, 0, (int)(3 * L), st));
-    void *tmp = sc.get(tbytes);
+    void *tmp = bsc.get(tbytes);
     if (!tmp) return KL_E_ALLOC;
     KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tbytes, key, ks, val, vs, (int)cnt, 0, (int)(3 * L), st));
-    uint32_t *flag = (uint32_t *)sc.get((cnt + 1) * sizeof(uint32_t));
-    uint32_t *psum = (uint32_t *)sc.get((cnt + 2) * sizeof(uint32_t));
+    uint32_t *flag = (uint32_t *)bsc.get((cnt + 1) * sizeof(uint32_t));
+    uint32_t *psum = (uint32_t *)bsc.get((cnt + 2) * sizeof(uint32_t));
     if (!flag || !psum) return KL_E_ALLOC;
     hipLaunchKernelGGL(m2s_pair_unique_kernel, dim3((unsigned)cdiv(cnt + 1, 256)), dim3(256), 0, st, cnt, ks, flag);
     KL_CHECK_LAUNCH();
     uint32_t uniq = 0;
-    KL_CHECK_RC(exclusive_scan(flag, psum, cnt, sc, st, &uniq));
-    uint64_t *mu = (uint64_t *)sc.get((size_t)uniq * sizeof(uint64_t));
+    KL_CHECK_RC(exclusive_scan(flag, psum, cnt, bsc, st, &uniq));
+    uint64_t *mu = (uint64_t *)bsc.get((size_t)uniq * sizeof(uint64_t));
+    uint32_t *starts = key;  // free since the sort
     int64_t *fu = (int64_t *)sc.get((size_t)uniq * sizeof(int64_t));
     float *bu = (float *)sc.get((size_t)uniq * 2 * sizeof(float));
     if (!mu || !fu || !bu) return KL_E_ALLOC;
-    hipLaunchKernelGGL(m2s_pair_leaves_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, ks, vs, flag,
-                       psum, fv, L, mu, fu, bu);
+    hipLaunchKernelGGL(m2s_run_starts_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, flag, psum,
+                       starts);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(m2s_pair_leaves_kernel, dim3((unsigned)cdiv(uniq, 256)), dim3(256), 0, st, cnt, (int64_t)uniq,
+                       ks, vs, starts, fv, L, mu, fu, bu);
     KL_CHECK_LAUNCH();
     KL_CHECK_RC(morton_to_octree_rows(uniq, mu, L, sc, octree, num_nodes, st));
     *face_idx = fu;
