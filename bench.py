@@ -363,8 +363,7 @@ def survey_step_bytes(inp, stats):
 OP_KERNELS = {
     'dibr_forward': ('raster_bin_word_kernel<float, 2>', 'tile_countorder2_kernel', 'raster_tile_kernel<float',
                      'soft_tile_fwd_kernel<float'),
-    'dibr_backward': ('rasterize_bwd_gather_kernel<float', 'rasterize_bwd_bigface_kernel<float', 'soft_bwd_plan_kernel',
-                      'soft_tile_bwd_kernel<float'),
+    'dibr_backward': ('rasterize_bwd_gather2_kernel<float', 'soft_tile_bwd_kernel<float'),
 }
 
 
@@ -511,6 +510,7 @@ def dibr_headline(args, world, rank, device):
     eager_elapsed = max(eager_times)
     pixels = cfg['views'] * cfg['H'] * cfg['W'] * world * args.steps
     mode, elapsed = 'eager', eager_elapsed
+    graph_elapsed = None
     if not args.eager:
         gstep, gout = graphed_step(inp, world)
         ref = dibr_step(inp, world)
@@ -533,9 +533,16 @@ def dibr_headline(args, world, rank, device):
         replay_check = {'forward_bit_equal': True, 'grad_elements_not_bit_equal': replay_grad_diffs}
         for _ in range(args.warmup):
             gstep()
-        rank_times = per_rank(timed_loop(gstep, args.steps, world, device), device, world)
-        elapsed = max(rank_times)
-        mode = 'hip_graph'
+        graph_times = per_rank(timed_loop(gstep, args.steps, world, device), device, world)
+        graph_elapsed = max(graph_times)
+        # the headline is the step in the faster of its two execution modes (same work, same
+        # outputs: the replay is checked against the eager step above); the other is reported
+        # beside it.  Eager can win: the graph's replay of ~10 small launches adds gaps the eager
+        # stream, its host far ahead of the GPU, does not.
+        if graph_elapsed <= eager_elapsed:
+            elapsed, mode, rank_times = graph_elapsed, 'hip_graph', graph_times
+        else:
+            elapsed, mode, rank_times = eager_elapsed, 'eager', eager_times
     else:
         rank_times = eager_times
         replay_check = None
@@ -575,6 +582,8 @@ def dibr_headline(args, world, rank, device):
                               devices_visible=torch.cuda.device_count()),
         'eager': {'value': round(pixels / eager_elapsed / 1e6, 2),
                   'ms_per_step': round(eager_elapsed / args.steps * 1e3, 4)},
+        'hip_graph': None if graph_elapsed is None else {'value': round(pixels / graph_elapsed / 1e6, 2),
+                                                         'ms_per_step': round(graph_elapsed / args.steps * 1e3, 4)},
     }
     return result, inp
 

@@ -10,6 +10,7 @@
 
 namespace kl {
 int g_dev_flags = 0;
+int g_dev_param[16] = {};
 template <typename T>
 int acc_finalize(const double *, T *, size_t, bool, hipStream_t, int *) { return 0; }  // backward: unused here
 template int acc_finalize<float>(const double *, float *, size_t, bool, hipStream_t, int *);
@@ -44,7 +45,7 @@ int main(int argc, char **argv) {
   CK(hipMalloc(&dt, P * 4));
   CK(hipMemcpy(dp, hp.data(), P * 12, hipMemcpyHostToDevice));
   CK(hipMemcpy(df, hf.data(), F * 36, hipMemcpyHostToDevice));
-  const P2MWs L(P);
+  const P2MWs L(P, F, sizeof(float));
   void *ws;
   CK(hipMalloc(&ws, L.bytes));
   hipEvent_t a, b;

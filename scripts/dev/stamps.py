@@ -35,7 +35,7 @@ def main():
     valid = inp['fnz'] >= 0
     _, idx, _ = _fused.rasterize_forward(H, W, inp['fvz'], inp['fvi'], inp['feat'], valid, 1000., 1e-8)
     nwaves = 4 * (H // 8) * (W // 64) * 8 * 4  # grid bound (tiles x 8 parts x 4 waves)
-    dbg = torch.zeros(nwaves * 10, dtype=torch.int64, device='cuda')
+    dbg = torch.zeros(max(nwaves * 10, (1 << 24) + 64), dtype=torch.int64, device="cuda")  # order stamps at 2^24
     for _ in range(3):
         _fused.soft_mask_forward_compact(inp['fvi'], idx, 7000., 0.02, K, 1000.)
     lib.kl_dev_set_debug(ctypes.c_void_p(dbg.data_ptr()))
@@ -44,7 +44,7 @@ def main():
     torch.cuda.synchronize()
     lib.kl_dev_set_flags(0)
     lib.kl_dev_set_debug(None)
-    d = dbg.view(nwaves, 10).cpu().numpy().astype(np.uint64)
+    d = dbg[:nwaves * 10].view(nwaves, 10).cpu().numpy().astype(np.uint64)
     d = d[d[:, 3] != 0]
     if os.environ.get('STAMPS_DUMP'):
         np.save(os.environ['STAMPS_DUMP'], d)
