@@ -58,6 +58,15 @@ at::Tensor workspace(size_t bytes, const at::Device &dev, int64_t stream) {
 
 void *ptr(const at::Tensor &t) { return t.defined() ? t.data_ptr() : nullptr; }
 
+// Each node's backward is one opaque HIP call, so its gradients cannot be differentiated again:
+// under create_graph (grad mode on inside the backward) raise rather than hand back gradients
+// that silently drop this op's second-order term (the Python nodes are once_differentiable).
+void no_double_backward(const char *op) {
+  TORCH_CHECK(!at::GradMode::is_enabled(), op,
+              ": backward with create_graph=True is not supported (the backward is one HIP call and is not "
+              "differentiable)");
+}
+
 struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
   static variable_list forward(AutogradContext *ctx, int64_t height, int64_t width, at::Tensor fvz, at::Tensor fvi,
                                at::Tensor feat, at::Tensor fnz, double sigmainv, double boxlen, int64_t knum,
@@ -115,6 +124,7 @@ struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
     const at::Tensor &idx = saved[0], &w = saved[1], &fvi = saved[2], &feat = saved[3], &fnz = saved[4],
                      &mask = saved[5], &ranges = saved[6], &hits = saved[7], &rec_face = saved[8],
                      &rec_prob = saved[9], &seg_tot = saved[10], &scratch = saved[11];
+    no_double_backward("dibr_rasterization");
     at::Tensor gf = grads[0], gm = grads[1];
     variable_list out(12);
     if (!gf.defined() && !gm.defined()) return out;
@@ -162,6 +172,7 @@ struct MaskIou : public torch::autograd::Function<MaskIou> {
   }
   static variable_list backward(AutogradContext *ctx, variable_list grads) {
     const auto saved = ctx->get_saved_variables();
+    no_double_backward("mask_iou");
     const at::Tensor &lhs = saved[0], &rhs = saved[1], &up = saved[2], &down = saved[3];
     const bool need_l = ctx->needs_input_grad(0), need_r = ctx->needs_input_grad(1);
     variable_list out(3);
@@ -210,6 +221,7 @@ struct PrepareVertices : public torch::autograd::Function<PrepareVertices> {
   }
   static variable_list backward(AutogradContext *ctx, variable_list grads) {
     const auto saved = ctx->get_saved_variables();
+    no_double_backward("prepare_vertices");
     const at::Tensor &verts = saved[0], &fc = saved[1], &pj = saved[2], &r = saved[3], &t = saved[4], &x = saved[5];
     variable_list out(8);
     if (!grads[0].defined() && !grads[1].defined() && !grads[2].defined()) return out;
@@ -275,6 +287,7 @@ struct TextureMapping : public torch::autograd::Function<TextureMapping> {
   }
   static variable_list backward(AutogradContext *ctx, variable_list grads) {
     const auto saved = ctx->get_saved_variables();
+    no_double_backward("texture_mapping");
     const at::Tensor &c = saved[0], &t = saved[1];
     const bool need_c = ctx->needs_input_grad(0), need_t = ctx->needs_input_grad(1);
     variable_list out(4);

@@ -717,6 +717,25 @@ def test_compiled_tutorial_nodes_equal_python_nodes(kal, monkeypatch, dtype, cam
             assert torch.equal(x, y), k
 
 
+def test_compiled_nodes_refuse_double_backward(kal):
+    """The compiled nodes' backwards are single HIP calls: backward(create_graph=True) raises
+    instead of returning gradients that silently drop the op's second-order term."""
+    from kaolin import _ext
+    assert _ext.get() is not None
+    import bench
+    inp = bench.dibr_inputs([0.3], DEV, H=32, W=48)
+    fvi = inp['fvi'].clone().requires_grad_(True)
+    f, m, _ = kal.render.mesh.dibr_rasterization(32, 48, inp['fvz'], fvi, inp['feat'], inp['fnz'])
+    with pytest.raises(RuntimeError, match='create_graph'):
+        torch.autograd.grad(m.sum() + f.sum(), fvi, create_graph=True)
+    a = torch.rand((2, 8, 8), device=DEV, requires_grad=True)
+    loss = kal.metrics.render.mask_iou(a, (torch.rand((2, 8, 8), device=DEV) > 0.5).float())
+    with pytest.raises(RuntimeError, match='create_graph'):
+        torch.autograd.grad(loss, a, create_graph=True)
+    # an ordinary backward is unaffected
+    torch.autograd.grad(kal.metrics.render.mask_iou(a, a.detach()), a)
+
+
 def test_dibr_mixed_dtypes_raise(kal, monkeypatch):
     """A float input of another dtype than face_vertices_image raises (the reference's
     data_ptr<scalar_t>() check) on the compiled node and on the Python node alike -- it is
