@@ -230,13 +230,15 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
   const V3<T> q = valid ? p : p0;
   const bool fin = isfinite(q.x) && isfinite(q.y) && isfinite(q.z);
   const bool all_fin = __all(fin);
-  V3<T> c = mk((T)0, (T)0, (T)0);
+  V3<T> c = mk((T)0, (T)0, (T)0), ext = mk((T)0, (T)0, (T)0);
   T R = (T)INFINITY, cinf = (T)0;
   if (all_fin) {
     c = mk((wave_min(q.x) + wave_max(q.x)) * (T)0.5, (wave_min(q.y) + wave_max(q.y)) * (T)0.5,
            (wave_min(q.z) + wave_max(q.z)) * (T)0.5);
     const V3<T> dq = q - c;
     R = wave_max(kl_sqrt<T>(dot(dq, dq))) * (T)(1.0 + 16.0 * P2M_E);
+    // the cluster's box half-extents about c (>= |p - c| per axis for every point of the wave)
+    ext = mk(wave_max(fabs(dq.x)), wave_max(fabs(dq.y)), wave_max(fabs(dq.z))) * (T)(1.0 + 4.0 * P2M_E);
     cinf = fmax(fmax(fabs(c.x), fabs(c.y)), fabs(c.z));
   }
   // Shared thresholds (all faces proper, finite bounded cluster): the fold is then the plain
@@ -282,6 +284,25 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
         const T B = fmax(b - sl, (T)0);
         const T K = (R + kl_sqrt<T>(thr_max)) * (T)(1.0 + 16.0 * P2M_E) + sl;
         if ((A * A + B * B) * (T)(1.0 - 32.0 * P2M_E) > K * K * (T)(1.0 + 32.0 * P2M_E)) eval = false;
+        // The same bound over the cluster's box instead of its sphere: for every point p of the box,
+        // |dot(p, u) - dot(c, u)| <= ext . |u| for the plane normal and each edge normal, so
+        // with those subtracted from A and B per direction (and no R) the distance bound holds for
+        // all points at once -- tighter than the sphere's single R for faces seen face-on or
+        // edge-on; either proof skips.
+        if (eval) {
+          auto sup = [&](T ux, T uy, T uz) {  // ext . |u|, rounded up
+            return (ext.x * fabs(ux) + ext.y * fabs(uy) + ext.z * fabs(uz)) * (T)(1.0 + 16.0 * P2M_E);
+          };
+          const T A2 = fmax(fabs(dot(c, fr.un) - sp.dv[s]) - fr.thick - sl - sup(fr.un.x, fr.un.y, fr.un.z), (T)0);
+          T b2 = dot(c, mk(sp.o[0][s], sp.o[1][s], sp.o[2][s])) - sp.off[0][s] - sup(sp.o[0][s], sp.o[1][s], sp.o[2][s]);
+          b2 = fmax(b2, dot(c, mk(sp.o[3][s], sp.o[4][s], sp.o[5][s])) - sp.off[1][s] -
+                            sup(sp.o[3][s], sp.o[4][s], sp.o[5][s]));
+          b2 = fmax(b2, dot(c, mk(sp.o[6][s], sp.o[7][s], sp.o[8][s])) - sp.off[2][s] -
+                            sup(sp.o[6][s], sp.o[7][s], sp.o[8][s]));
+          const T B2 = fmax(b2 - sl, (T)0);
+          const T K2 = kl_sqrt<T>(thr_max) * (T)(1.0 + 16.0 * P2M_E) + sl;
+          if ((A2 * A2 + B2 * B2) * (T)(1.0 - 32.0 * P2M_E) > K2 * K2 * (T)(1.0 + 32.0 * P2M_E)) eval = false;
+        }
       }
       uint64_t mask = __ballot(eval);
 #ifdef KL_P2M_PROBE
