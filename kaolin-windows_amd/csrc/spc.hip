@@ -654,7 +654,16 @@ __global__ void __launch_bounds__(256) m2s_level_kernel(const float *__restrict_
 //   * box axes: decided EXACTLY, on the reference's own float differences f_k - (C +- h);
 //   * edge-cross axes (x/y/z cross each edge): |dS| <= 2 tau (V + 2h) + 2^-20 (V + 2h) |a|_1 <
 //     M = 2^-17 U^2;
-//   * the normal, E1 x E2: |dS| <= 9 * 2^-20 U^3 < M = 2^-15 U^3.
+//   * the normal, E1 x E2 (r04: a margin linear in the edge scale Em = max |E|): every term of dS
+//     carries a factor of the axis (|n|_inf <= 2 Em^2) or of its error against the reference's
+//     rounded edges (|dn|_inf <= 4 tau Em + 2 tau^2 + 2^-21 Em^2 <= 2^-20 U Em + 2 tau^2): the
+//     rounded v_k / w_k (<= 2.3 * 2^-20 U^2 Em), v.dn (<= 3 * 2^-20 U^2 Em), the float dot, s, R
+//     and S (<= 3.7 * 2^-20 U^2 Em) and the reference's float casts of fd / fr (<= 0.8 * 2^-20
+//     U^2 Em), in all |dS| <= 10 * 2^-20 U^2 Em + 6 U tau^2 < M = 2^-15 U^2 (Em + 2^-10 U)
+//     (tau^2 <= 2^-46 U^2).  The r03 bound 2^-15 U^3 took Em <= U: with a triangle much smaller
+//     than the voxel (the first levels: cfg4's edges are ~1/100 of a level-2 voxel) a passing
+//     child's normal-axis separation, ~ -h |n|_1, fell inside it, and every such child ran the
+//     full test.
 // S > M proves the reference rejects the child on that axis, S < -M that it passes it; a child
 // every axis passes is accepted, one some axis rejects is rejected, and the rest (|S| <= M on
 // some axis, none rejecting) run the reference's test itself.  A reference edge of length 0
@@ -675,9 +684,7 @@ __device__ __forceinline__ void m2s_axis4(float pmax, float pmin, float R, float
   }
 }
 
-__device__ uint32_t m2s_children(const float *v, uint64_t m, uint32_t level) {
-  int16_t px, py, pz;
-  to_point(m, px, py, pz);
+__device__ uint32_t m2s_children_pt(const float *v, int px, int py, int pz, uint32_t level) {
   const float two_level = (float)(1u << level);
   const float vs = 2.0f / two_level;  // child size
   const float h = (float)(0.5 * vs);  // child half-size (voxel_center at `level`)
@@ -767,7 +774,7 @@ __device__ uint32_t m2s_children(const float *v, uint64_t m, uint32_t level) {
       for (int k = 0; k < 3; k++) P[k] = w[k][0] * nx + w[k][1] * ny + w[k][2] * nz;
       const float pmax = fmaxf(P[0], fmaxf(P[1], P[2])), pmin = fminf(P[0], fminf(P[1], P[2]));
       const float R = h * (fabsf(nx) + fabsf(ny) + fabsf(nz));
-      const float Mn = (1.0f / 32768.0f) * U * U * U;
+      const float Mn = (1.0f / 32768.0f) * U * U * (Em + (1.0f / 1024.0f) * U);
       const float hx = h * nx, hy = h * ny, hz = h * nz;
 #pragma unroll
       for (int c = 0; c < 8; c++) {
@@ -783,11 +790,19 @@ __device__ uint32_t m2s_children(const float *v, uint64_t m, uint32_t level) {
   while (need) {  // the reference's test itself, on its own child centre
     const int c = __builtin_ctz(need);
     need &= need - 1;
-    float cx, cy, cz, hh;
-    voxel_center(to_morton(2 * px + (c >> 2), 2 * py + ((c >> 1) & 1), 2 * pz + (c & 1)), level, cx, cy, cz, hh);
-    if (tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, hh)) pass |= 1u << c;
+    // the child's centre as voxel_center computes it
+    const float cx = fmaf((float)(2 * px + (c >> 2)), vs, h - 1.0f);
+    const float cy = fmaf((float)(2 * py + ((c >> 1) & 1)), vs, h - 1.0f);
+    const float cz = fmaf((float)(2 * pz + (c & 1)), vs, h - 1.0f);
+    if (tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h)) pass |= 1u << c;
   }
   return pass;
+}
+
+__device__ uint32_t m2s_children(const float *v, uint64_t m, uint32_t level) {
+  int16_t px, py, pz;
+  to_point(m, px, py, pz);
+  return m2s_children_pt(v, px, py, pz, level);
 }
 
 // One level of the device-sized mesh_to_spc from the PARENTS: the input is the previous level's
@@ -864,6 +879,344 @@ __global__ void __launch_bounds__(256) m2s_children_kernel(const float *__restri
     }
     o0 += (unsigned long long)ctot;
   }
+}
+
+// ---- mesh_to_spc by node ranks (r04, m2s_node_kernel / m2s_rank_kernel): no sort, one host read.
+// Level l's nodes are a list in morton order (U_l nodes).  Node j's octree byte oct_l[j] -- the OR
+// of the child masks its (node, face) pairs decide -- IS the octree row, and the exclusive popcount
+// scan S_l of the row numbers the next level: child c of node j is node
+//   S_l[j] + popc(oct_l[j] & ((1 << c) - 1))
+// of level l + 1, again in morton order (the parents are, and children follow in c); M_l keeps the
+// nodes' points (x | y << 16 | z << 32: no morton decode per pair).  A level's
+// pairs are appended in any order as (key = parent * 8 + c, face) and the next level resolves the
+// key through the parent level's S and octree row.  At the last level each (parent, child) slot
+// keeps its least face (atomicMin), the face the reference's stable sort puts first (generation
+// order is ascending face id, m2s_key_kernel's comment).  Per call: the root test, then per level
+// one decision launch and one scan launch (single pass, ordered tiles with look-back), the counts
+// read once at the end, and one launch writing the leaves' faces and barycentrics.
+struct M2sCtl {
+  unsigned long long counts[(SPC_MAX_LEVELS + 2) * M2S_SHARDS];  // pairs per level and shard
+  uint32_t U[SPC_MAX_LEVELS + 2];       // nodes per level
+  uint32_t O[SPC_MAX_LEVELS + 2];       // the level's first byte in the octree arena
+  uint32_t ticket[SPC_MAX_LEVELS + 2];  // tile tickets of the level's scan
+  int overflow;
+  uint32_t zero;
+  uint32_t root_S[2];  // the level above the root: one node whose child 0 is the root
+  uint32_t root_oct;   // its octree byte (1)
+};
+
+constexpr int M2S_TILE = 1024;  // nodes per scan tile (256 threads x 4)
+
+__device__ void leaf_out_pt(int px, int py, int pz, int64_t f, const float *__restrict__ fv, uint32_t level,
+                            uint32_t o, int64_t *__restrict__ fout, float *__restrict__ bary);
+
+// a node's point packed in 64 bits (x | y << 16 | z << 32): a child is 2 p + m2s_child_off(c)
+__device__ __forceinline__ uint64_t m2s_child_off(uint32_t c) {
+  return (uint64_t)(c >> 2) | ((uint64_t)((c >> 1) & 1) << 16) | ((uint64_t)(c & 1) << 32);
+}
+
+// level 0: the root voxel against every face; the passing faces are the pairs (key 0, face)
+__global__ void __launch_bounds__(256) m2s_root_kernel(int64_t F, const float *__restrict__ fv, uint32_t *__restrict__ kout,
+                                                       uint32_t *__restrict__ fout, unsigned long long seg,
+                                                       M2sCtl *__restrict__ ctl, uint64_t *__restrict__ M0,
+                                                       uint64_t *__restrict__ slots, uint32_t *__restrict__ fmin8,
+                                                       uint32_t L) {
+  __shared__ int s_wave[4];
+  __shared__ unsigned long long s_base;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    ctl->root_S[0] = 0;
+    ctl->root_S[1] = 1;
+    ctl->root_oct = 1;
+    ctl->U[0] = 1;
+    ctl->O[0] = 0;
+    M0[0] = 0;
+    if (L >= 2) slots[0] = 0;
+  }
+  if (blockIdx.x == 0 && L == 1 && threadIdx.x < 8) fmin8[threadIdx.x] = 0xffffffffu;
+  const int64_t f = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  bool pass = false;
+  if (f < F) {
+    float cx, cy, cz, h;
+    voxel_center(0, 0, cx, cy, cz, h);
+    const float *v = fv + f * 9;
+    pass = tri_voxel_maybe(v, v + 3, v + 6, cx, cy, cz, h) && tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h);
+  }
+  int total = 0;
+  const int pre = block_exclusive_scan(pass ? 1 : 0, s_wave, &total);
+  const int g = blockIdx.x % M2S_SHARDS;
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(ctl->counts + g, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  if (total == 0) return;
+  if (s_base + (unsigned long long)total > seg) {
+    if (threadIdx.x == 0) ctl->overflow = 1;
+    return;
+  }
+  if (pass) {
+    const unsigned long long o = (unsigned long long)g * seg + s_base + (unsigned long long)pre;
+    kout[o] = 0;
+    fout[o] = (uint32_t)f;
+  }
+}
+
+// the node a pair's key names: (its index at the pair's level, its morton)
+__device__ __forceinline__ uint32_t m2s_node(uint32_t key, const uint32_t *__restrict__ Spp,
+                                             const uint8_t *__restrict__ octpp) {
+  const uint32_t jp = key >> 3, c = key & 7;
+  return Spp[jp] + (uint32_t)__popc((uint32_t)octpp[jp] & ((1u << c) - 1u));
+}
+
+// One level l >= 1: each thread takes a pair of level l - 1, decides its node's 8 children
+// (m2s_children), flags them in the node's 8 child slots, and appends (node * 8 + c, face) for the
+// passing children (sharded, one reservation per workgroup, as m2s_children_kernel) -- or, at the
+// last level, keeps the least face per (node, child) slot.  The scan kernel then forms each node's
+// octree byte from its slots.
+template <bool LAST>
+__global__ void __launch_bounds__(256) m2s_node_kernel(const float *__restrict__ fv, const uint32_t *__restrict__ kin,
+                                                       const uint32_t *__restrict__ fin, uint32_t *__restrict__ kout,
+                                                       uint32_t *__restrict__ fout, unsigned long long seg,
+                                                       M2sCtl *__restrict__ ctl, uint32_t level,
+                                                       const uint32_t *__restrict__ Spp,
+                                                       const uint8_t *__restrict__ octpp_base,
+                                                       const uint32_t *__restrict__ opp,
+                                                       const uint64_t *__restrict__ Mp, uint8_t *__restrict__ slots,
+                                                       uint32_t *__restrict__ fmin8) {
+  __shared__ int s_wave[4];
+  __shared__ unsigned long long s_base;
+  __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
+  __shared__ uint8_t s_kids[M2S_MAX_CHUNKS][256];
+  if (*(volatile int *)&ctl->overflow) return;  // holes in the input (m2s_level_kernel)
+  ShardIn in;
+  in.load(s_pre, ctl->counts + (level - 1) * M2S_SHARDS, seg);
+  const unsigned long long n = in.total();
+  const int g = blockIdx.x % M2S_SHARDS;
+  // whole chunks of 256 pairs per workgroup (the first levels' ~200 k pairs fill 782 workgroups'
+  // lanes instead of spreading ~98 over each of 2,048)
+  const unsigned long long span = ((n + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+  const unsigned long long lo = (unsigned long long)blockIdx.x * span;
+  const unsigned long long hi = lo + span < n ? lo + span : n;
+  if (lo >= hi) return;
+  const int nch = (int)((hi - lo + blockDim.x - 1) / blockDim.x);
+  if (nch > M2S_MAX_CHUNKS) {
+    if (threadIdx.x == 0) ctl->overflow = 1;
+    return;
+  }
+  const uint8_t *octpp = octpp_base + *opp;
+  int mine = 0;
+#pragma unroll 1
+  for (int k = 0; k < nch; k++) {
+    const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
+    uint32_t kids = 0, j = 0, f = 0;
+    if (i < hi) {
+      const unsigned long long p = in.pos(i, seg);
+      f = fin[p];
+      j = m2s_node(kin[p], Spp, octpp);
+      const uint64_t q = Mp[j];
+      kids = m2s_children_pt(fv + (int64_t)f * 9, (int)(q & 0xffff), (int)((q >> 16) & 0xffff), (int)(q >> 32), level);
+    }
+    if (LAST) {  // the least face per (node, child) slot; a slot left at ~0 is no child
+      for (uint32_t c = kids; c; c &= c - 1) atomicMin(fmin8 + j * 8 + __builtin_ctz(c), f);
+    } else {
+      // the node's child flags: plain byte stores of 1 (idempotent, merged in the XCDs' L2s),
+      // not atomics -- global atomics execute at the memory side, ~12 ns apiece per address, and
+      // the first levels send every pair to a few nodes (293 us at level 3 with atomicOr)
+      uint8_t *fl = slots + (size_t)j * 8;
+#pragma unroll
+      for (int c = 0; c < 8; c++)
+        if ((kids >> c) & 1) fl[c] = 1;
+      s_kids[k][threadIdx.x] = (uint8_t)kids;
+      mine += __popc(kids);
+    }
+  }
+  if (LAST) return;
+  // the children's pairs, appended in any order (the next level's nodes are numbered by the scan,
+  // not by position): one reservation per workgroup (per wave and chunk: 21 -> 31 us per level)
+  int total = 0;
+  (void)block_exclusive_scan(mine, s_wave, &total);
+  unsigned long long *cnt_out = ctl->counts + level * M2S_SHARDS;
+  if (threadIdx.x == 0) s_base = total ? atomicAdd(cnt_out + g, (unsigned long long)total) : 0ull;
+  __syncthreads();
+  unsigned long long o0 = s_base;
+  if (total == 0) return;
+  if (o0 + (unsigned long long)total > seg) {
+    if (threadIdx.x == 0) ctl->overflow = 1;
+    return;
+  }
+  o0 += (unsigned long long)g * seg;
+#pragma unroll 1
+  for (int k = 0; k < nch; k++) {
+    const uint32_t kids = s_kids[k][threadIdx.x];
+    int ctot = 0;
+    const int pre = block_exclusive_scan(__popc(kids), s_wave, &ctot);
+    if (kids) {
+      const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
+      const unsigned long long p = in.pos(i, seg);
+      const uint32_t f = fin[p], j8 = m2s_node(kin[p], Spp, octpp) * 8;
+      unsigned long long o = o0 + (unsigned long long)pre;
+      for (uint32_t c = kids; c; c &= c - 1) {
+        kout[o] = j8 + (uint32_t)__builtin_ctz(c);
+        fout[o] = f;
+        o++;
+      }
+    }
+    o0 += (unsigned long long)ctot;
+  }
+}
+
+// Level l's octree row (l < L) from its nodes' child slots (flags, or at l = L - 1 the least-face
+// slots: a child iff not ~0) and its scan: S_l (exclusive popcounts, S_l[U_l] = U_{l+1}), the next
+// level's count and arena offset, and for each child its point (M_{l+1}) and zeroed slots (flags
+// for l + 2 < L, least faces ~0 for l + 2 == L).  Single
+// pass: workgroup b takes tile b (tiles past the grid by ticket), publishes the tile's sum tagged
+// with the level (aggregate, then inclusive once the prefix is known) and looks back over the
+// earlier tiles' tags, 64 per round; a workgroup only waits on tiles of workgroups dispatched or
+// ticketed before it, so the wait always ends.
+__global__ void __launch_bounds__(256) m2s_rank_kernel(M2sCtl *__restrict__ ctl, uint32_t l, uint32_t L,
+                                                       uint8_t *__restrict__ arena, const uint64_t *__restrict__ Ml,
+                                                       uint32_t *__restrict__ Sl, uint64_t *__restrict__ Mn,
+                                                       const uint64_t *__restrict__ slots,
+                                                       uint64_t *__restrict__ slots_next,
+                                                       unsigned long long *__restrict__ status,
+                                                       uint32_t *__restrict__ fmin8, uint32_t ncap, uint32_t oct_cap,
+                                                       uint32_t fmin_cap) {
+  __shared__ int s_wave[4];
+  __shared__ uint32_t s_tile, s_prefix;
+  if (*(volatile int *)&ctl->overflow) return;
+  const uint32_t n = ctl->U[l], O = ctl->O[l], On = O + n;
+  const uint32_t ntiles = (n + M2S_TILE - 1) / M2S_TILE;
+  const bool has_next = l + 1 < L, init_fmin = l + 2 == L, init_flags = l + 2 < L, last = l + 1 == L;
+  const unsigned long long tag_agg = (unsigned long long)(2 * l + 2) << 32,
+                           tag_inc = (unsigned long long)(2 * l + 3) << 32;
+  uint8_t *oct = arena + O;
+  // tile blockIdx.x first (workgroups are dispatched in index order, so a tile's predecessors are
+  // held by workgroups already running), then tiles past the grid by ticket
+  if (blockIdx.x >= ntiles) return;
+  uint32_t t = blockIdx.x;
+  for (;;) {
+    const uint32_t j0 = t * M2S_TILE + threadIdx.x * 4;
+    uint32_t b[4];
+    int local = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t j = j0 + q;
+      uint32_t byte = 0;
+      if (j < n) {
+        if (last) {
+          const uint4 *f4 = (const uint4 *)(fmin8 + (size_t)j * 8);
+          const uint4 a = f4[0], c = f4[1];
+          byte = (a.x != ~0u ? 1u : 0u) | (a.y != ~0u ? 2u : 0u) | (a.z != ~0u ? 4u : 0u) | (a.w != ~0u ? 8u : 0u) |
+                 (c.x != ~0u ? 16u : 0u) | (c.y != ~0u ? 32u : 0u) | (c.z != ~0u ? 64u : 0u) |
+                 (c.w != ~0u ? 128u : 0u);
+        } else {
+          const uint64_t v = slots[j];
+#pragma unroll
+          for (int c = 0; c < 8; c++) byte |= ((v >> (8 * c)) & 0xffu) ? 1u << c : 0u;
+        }
+        oct[j] = (uint8_t)byte;
+      }
+      b[q] = byte;
+      local += __popc(byte);
+    }
+    int agg = 0;
+    const int ex = block_exclusive_scan(local, s_wave, &agg);
+    if (threadIdx.x < 64) {  // wave 0: publish, then look back 64 tiles per round
+      uint32_t prefix = 0;
+      if (t == 0) {
+        if (threadIdx.x == 0)
+          __hip_atomic_store(status, tag_inc | (uint32_t)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        if (threadIdx.x == 0)
+          __hip_atomic_store(status + t, tag_agg | (uint32_t)agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int64_t end = t;  // lane i reads tile end - 1 - i (before tile 0: an inclusive 0)
+        for (;;) {
+          const int64_t k = end - 1 - (int64_t)threadIdx.x;
+          const unsigned long long v =
+              k >= 0 ? __hip_atomic_load(status + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag_inc;
+          const unsigned long long tg = v & 0xffffffff00000000ull;
+          const uint64_t inc = ballot(tg == tag_inc), any = ballot(tg == tag_inc || tg == tag_agg);
+          if (inc) {  // the nearest inclusive tile, once every tile after it has published
+            const int f = __builtin_ctzll(inc);
+            const uint64_t need = f == 63 ? ~0ull : ((2ull << f) - 1);
+            if ((any & need) == need) {
+              uint32_t x = (int)threadIdx.x <= f ? (uint32_t)v : 0u;
+#pragma unroll
+              for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+              prefix += x;
+              break;
+            }
+          } else if (any == ~0ull) {  // 64 aggregates: add them, look further back
+            uint32_t x = (uint32_t)v;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+            prefix += x;
+            end -= 64;
+            continue;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (threadIdx.x == 0)
+          __hip_atomic_store(status + t, tag_inc | (prefix + (uint32_t)agg), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (threadIdx.x == 0) s_prefix = prefix;
+    }
+    __syncthreads();
+    uint32_t s = s_prefix + (uint32_t)ex;
+    bool over = false;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const uint32_t j = j0 + q;
+      if (j >= n) break;
+      Sl[j] = s;
+      if (has_next && b[q]) {
+        const uint64_t m2 = Ml[j] * 2;
+        for (uint32_t c = b[q]; c; c &= c - 1, s++) {
+          if (s >= ncap || On + s >= oct_cap || (init_fmin && s * 8ull + 8 > fmin_cap)) {
+            over = true;
+            continue;
+          }
+          Mn[s] = m2 + m2s_child_off((uint32_t)__builtin_ctz(c));
+          if (init_flags) slots_next[s] = 0;
+          if (init_fmin) {
+#pragma unroll
+            for (int e = 0; e < 8; e++) fmin8[s * 8 + e] = 0xffffffffu;
+          }
+        }
+      } else {
+        s += (uint32_t)__popc(b[q]);
+      }
+    }
+    if (over) ctl->overflow = 1;
+    if (t + 1 == ntiles && threadIdx.x == 0) {
+      const uint32_t total = s_prefix + (uint32_t)agg;
+      Sl[n] = total;
+      ctl->U[l + 1] = total;
+      ctl->O[l + 1] = On;
+      if (total > ncap || (has_next && On + total > oct_cap)) ctl->overflow = 1;
+    }
+    if (ntiles <= gridDim.x) break;
+    __syncthreads();  // s_prefix and s_tile are rewritten for the next tile
+    if (threadIdx.x == 0) s_tile = gridDim.x + atomicAdd(&ctl->ticket[l], 1u);
+    __syncthreads();
+    t = s_tile;
+    if (t >= ntiles) break;
+  }
+}
+
+// the leaves (after the one host read): per (parent, child) slot of the last level's parents, a
+// leaf's number, least face, morton and barycentrics
+__global__ void m2s_node_leaves_kernel(int64_t nslots, const M2sCtl *__restrict__ ctl, uint32_t L,
+                                       const uint8_t *__restrict__ arena, const uint32_t *__restrict__ Sp,
+                                       const uint64_t *__restrict__ Mp, const uint32_t *__restrict__ fmin8,
+                                       const float *__restrict__ fv, int64_t *__restrict__ fout,
+                                       float *__restrict__ bary) {
+  const int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (s >= nslots) return;
+  const uint32_t jp = (uint32_t)(s >> 3), c = (uint32_t)(s & 7);
+  const uint32_t b = arena[ctl->O[L - 1] + jp];
+  if (!((b >> c) & 1)) return;
+  const uint32_t o = Sp[jp] + (uint32_t)__popc(b & ((1u << c) - 1u));
+  const uint64_t q = Mp[jp] * 2 + m2s_child_off(c);
+  leaf_out_pt((int)(q & 0xffff), (int)((q >> 16) & 0xffff), (int)(q >> 32), (int64_t)fmin8[s], fv, L, o, fout, bary);
 }
 
 __global__ void m2s_key_kernel(int64_t n, const uint64_t *__restrict__ m, const uint32_t *__restrict__ t,
@@ -961,13 +1314,9 @@ __global__ void m2s_pair_leaves_kernel(int64_t n, int64_t nleaves, const uint32_
 }
 
 // leaf o: its morton, face, and the face's barycentrics at the voxel centre (spc_math.h:229-258)
-__device__ __forceinline__ void leaf_out_body(uint64_t m, int64_t f, const float *__restrict__ fv, uint32_t level,
-                                              uint32_t o, uint64_t *__restrict__ mout, int64_t *__restrict__ fout,
-                                              float *__restrict__ bary) {
-  mout[o] = m;
+__device__ __forceinline__ void leaf_bary(float cx, float cy, float cz, int64_t f, const float *__restrict__ fv,
+                                          uint32_t o, int64_t *__restrict__ fout, float *__restrict__ bary) {
   fout[o] = f;
-  float cx, cy, cz, h;
-  voxel_center(m, level, cx, cy, cz, h);
   const float *v = fv + f * 9;
   const F3 v1 = f3(v[0], v[1], v[2]), v2 = f3(v[3], v[4], v[5]), v3 = f3(v[6], v[7], v[8]);
   const F3 cp = tri_closest(v1, v2, v3, f3(cx, cy, cz));
@@ -992,7 +1341,19 @@ __device__ __forceinline__ void leaf_out_body(uint64_t m, int64_t f, const float
 
 __device__ void leaf_out(uint64_t m, int64_t f, const float *__restrict__ fv, uint32_t level, uint32_t o,
                          uint64_t *__restrict__ mout, int64_t *__restrict__ fout, float *__restrict__ bary) {
-  leaf_out_body(m, f, fv, level, o, mout, fout, bary);
+  mout[o] = m;
+  float cx, cy, cz, h;
+  voxel_center(m, level, cx, cy, cz, h);
+  leaf_bary(cx, cy, cz, f, fv, o, fout, bary);
+}
+
+// the same from the leaf's point (voxel_center's arithmetic), no morton output
+__device__ void leaf_out_pt(int px, int py, int pz, int64_t f, const float *__restrict__ fv, uint32_t level,
+                            uint32_t o, int64_t *__restrict__ fout, float *__restrict__ bary) {
+  const float vs = 2.0f / (float)(1u << level);
+  const float h = (float)(0.5 * vs);
+  leaf_bary(fmaf((float)px, vs, h - 1.0f), fmaf((float)py, vs, h - 1.0f), fmaf((float)pz, vs, h - 1.0f), f, fv, o,
+            fout, bary);
 }
 
 // Octree of sorted unique leaf mortons, all levels at once: row j (0..L-1) of `flag` marks
@@ -1069,6 +1430,104 @@ static int morton_to_octree_rows(int64_t n, const uint64_t *morton, uint32_t L, 
   KL_CHECK_LAUNCH();
   *octree = out;
   *num_nodes = total;
+  return KL_OK;
+}
+
+// mesh_to_spc by node ranks (m2s_node_kernel): returns KL_OK, an error, or 1 = not taken
+// (capacity): the caller runs the per-level path.  One host read (the counts, after the levels).
+static int mesh_to_spc_nodes(int64_t F, const float *fv, uint32_t L, Scratch &sc, uint8_t **octree,
+                             int64_t *num_nodes, int64_t **face_idx, float **bary, int64_t *num_leaves,
+                             hipStream_t st) {
+  *octree = nullptr;
+  *face_idx = nullptr;
+  *bary = nullptr;
+  *num_nodes = 0;
+  *num_leaves = 0;
+  if (F <= 0 || F >= ((int64_t)1 << 31) || L == 0) return 1;
+  // pairs per level buffer: 96 per face (cfg4: 4.6 M at L = 9 against 19.2 M), in shards; nodes per
+  // level and octree bytes: a quarter of that; the last level's least-face slots (8 per parent)
+  // reuse the pair buffer that level would have written (2 cap words >= 8 ncap)
+  const unsigned long long cap = (unsigned long long)std::max<int64_t>(F * 96, (int64_t)1 << 20);
+  if (cap >= (1ull << 31)) return 1;
+  const unsigned long long seg = cap / M2S_SHARDS;
+  const uint32_t ncap = (uint32_t)(cap / 4), oct_cap = ncap, fmin_cap = (uint32_t)(2 * cap);
+  const int64_t tiles = cdiv(ncap, M2S_TILE);
+  const size_t qb = al256b((size_t)cap * 4), mbytes = al256b((size_t)ncap * 8), sbytes = al256b(((size_t)ncap + 1) * 4);
+  const size_t ctl_bytes = al256b(sizeof(M2sCtl) + (size_t)tiles * 8);
+  const size_t chunk = 4 * qb + 4 * mbytes + 2 * sbytes + al256b(oct_cap + 4) + ctl_bytes;
+  char *base = (char *)sc.get(chunk);
+  if (!base) return KL_E_ALLOC;
+  uint32_t *Qk[2], *Qf[2];
+  uint64_t *M[2];
+  uint32_t *S[2];
+  char *p = base;
+  for (int k = 0; k < 2; k++) {
+    Qk[k] = (uint32_t *)p;  // key then face: the pair of arrays is also 2 cap contiguous words
+    Qf[k] = (uint32_t *)(p + qb);
+    p += 2 * qb;
+  }
+  for (int k = 0; k < 2; k++, p += mbytes) M[k] = (uint64_t *)p;
+  uint64_t *SL[2];  // child slots (8 flag bytes per node) of levels l and l + 1
+  for (int k = 0; k < 2; k++, p += mbytes) SL[k] = (uint64_t *)p;
+  for (int k = 0; k < 2; k++, p += sbytes) S[k] = (uint32_t *)p;
+  uint8_t *arena = (uint8_t *)p;
+  p += al256b(oct_cap + 4);
+  M2sCtl *ctl = (M2sCtl *)p;
+  unsigned long long *status = (unsigned long long *)(p + sizeof(M2sCtl));
+  KL_CHECK_RC(fill_async(ctl, 0, ctl_bytes, st));
+  uint32_t *fmin8 = Qk[L & 1];
+  hipLaunchKernelGGL(m2s_root_kernel, dim3((unsigned)cdiv(F, 256)), dim3(256), 0, st, F, fv, Qk[0], Qf[0], seg, ctl,
+                     M[0], SL[0], fmin8, L);
+  KL_CHECK_LAUNCH();
+  const unsigned grid = (unsigned)std::max<int64_t>(M2S_GRID, cdiv((int64_t)cap, 256 * M2S_MAX_CHUNKS));
+  const unsigned rgrid = (unsigned)std::min<int64_t>(256, std::max<int64_t>(tiles, 1));  // one per CU
+  for (uint32_t l = 1; l <= L; l++) {
+    // level l - 2's S and octree row resolve the keys of level l - 1's pairs (level -1: ctl's root)
+    const uint32_t *Spp = l >= 2 ? S[l & 1] : ctl->root_S;
+    const uint8_t *octpp = l >= 2 ? arena : (const uint8_t *)&ctl->root_oct;
+    const uint32_t *opp = l >= 2 ? &ctl->O[l - 2] : &ctl->zero;
+    const int a = (l - 1) & 1;
+    if (l < L)
+      hipLaunchKernelGGL(m2s_node_kernel<false>, dim3(grid), dim3(256), 0, st, fv, Qk[a], Qf[a], Qk[a ^ 1], Qf[a ^ 1], seg,
+                         ctl, l, Spp, octpp, opp, M[a], (uint8_t *)SL[a], fmin8);
+    else
+      hipLaunchKernelGGL(m2s_node_kernel<true>, dim3(grid), dim3(256), 0, st, fv, Qk[a], Qf[a], Qk[a ^ 1], Qf[a ^ 1], seg,
+                         ctl, l, Spp, octpp, opp, M[a], (uint8_t *)SL[a], fmin8);
+    KL_CHECK_LAUNCH();
+    // level l - 1's row scanned: S_{l-1}, U_l, O_l, M_l
+    hipLaunchKernelGGL(m2s_rank_kernel, dim3(rgrid), dim3(256), 0, st, ctl, l - 1, L, arena, M[a], S[a], M[a ^ 1],
+                       SL[a], SL[a ^ 1], status, fmin8, ncap, oct_cap, fmin_cap);
+    KL_CHECK_LAUNCH();
+  }
+  std::vector<char> hbuf(sizeof(M2sCtl));
+  M2sCtl &h = *(M2sCtl *)hbuf.data();
+  KL_CHECK_RC(host_read(&h, ctl, sizeof(M2sCtl), st));
+  if (h.overflow) return 1;
+  t_m2s_counts[0] = F;
+  for (uint32_t l = 1; l <= L; l++) {
+    unsigned long long t = 0;
+    for (int g = 0; g < M2S_SHARDS; g++) t += h.counts[(l - 1) * M2S_SHARDS + g];
+    t_m2s_counts[l] = 8 * (int64_t)t;
+  }
+  t_m2s_levels = (int)L + 1;
+  const int64_t leaves = h.U[L];
+  if (leaves == 0) return KL_OK;  // empty: (0,) u8, (0,) i64, (0,3) f32 built by the caller
+  const int64_t nodes = h.O[L];
+  uint8_t *out = (uint8_t *)sc.get((size_t)nodes);
+  int64_t *fu = (int64_t *)sc.get((size_t)leaves * sizeof(int64_t));
+  float *bu = (float *)sc.get((size_t)leaves * 2 * sizeof(float));
+  if (!out || !fu || !bu) return KL_E_ALLOC;
+  KL_CHECK_HIP(hipMemcpyAsync(out, arena, (size_t)nodes, hipMemcpyDeviceToDevice, st));
+  const int64_t nslots = 8 * (int64_t)h.U[L - 1];
+  const int b = (int)((L - 1) & 1);
+  hipLaunchKernelGGL(m2s_node_leaves_kernel, dim3((unsigned)cdiv(nslots, 256)), dim3(256), 0, st, nslots, ctl, L,
+                     arena, S[b], M[b], fmin8, fv, fu, bu);
+  KL_CHECK_LAUNCH();
+  *octree = out;
+  *num_nodes = nodes;
+  *face_idx = fu;
+  *bary = bu;
+  *num_leaves = leaves;
   return KL_OK;
 }
 
@@ -1551,8 +2010,12 @@ extern "C" int kl_mesh_to_spc(int64_t num_faces, const float *fv, uint32_t level
   KL_REQUIRE(alloc != nullptr, "mesh_to_spc: allocator required");
   Scratch sc{alloc, ctx};
   if (!(g_dev_flags & (1 << 10))) {  // dev bit 10: the per-level path
-    const int rc = mesh_to_spc_async(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves,
-                                     S(stream));
+    // dev param 14 >= 1: the sorted-pairs path (A/B)
+    const int rc = g_dev_param[14] >= 1
+                       ? mesh_to_spc_async(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves,
+                                           S(stream))
+                       : mesh_to_spc_nodes(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves,
+                                           S(stream));
     if (rc != 1) return rc;
   }
   return mesh_to_spc_impl(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves, S(stream));

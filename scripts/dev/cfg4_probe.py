@@ -39,6 +39,11 @@ def main():
             ts.append((time.perf_counter() - t0) * 1e3)
         print(f'{name}: ' + ' '.join(f'{t:.3f}' for t in ts) + ' ms', flush=True)
     octree = kal.ops.conversions.unbatched_mesh_to_spc(fv, 9)[0]
+    import ctypes
+    from kaolin import _native
+    cnt = (ctypes.c_int64 * 16)()
+    nl = _native.lib().kl_mesh_to_spc_level_counts(cnt, 16)
+    print('mesh_to_spc proposals per level:', list(cnt)[:nl], 'nodes', octree.shape[0], flush=True)
     L, pyr, exsum = kal.ops.spc.scan_octrees(octree, torch.tensor([octree.shape[0]], dtype=torch.int32))
     pts = kal.ops.spc.generate_points(octree, pyr, exsum)
     n = 512

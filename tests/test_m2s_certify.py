@@ -76,7 +76,7 @@ def children(v, px, py, pz, level):
     n = np.stack([E[0][:, 1] * E[1][:, 2] - E[0][:, 2] * E[1][:, 1], E[0][:, 2] * E[1][:, 0] - E[0][:, 0] * E[1][:, 2],
                   E[0][:, 0] * E[1][:, 1] - E[0][:, 1] * E[1][:, 0]], -1).astype(f32)
     P = np.stack([((wk[:, 0] * n[:, 0]) + (wk[:, 1] * n[:, 1])) + wk[:, 2] * n[:, 2] for wk in w], -1).astype(f32)
-    axis(P, n, (f32(1 / 32768) * U * U * U).astype(f32))
+    axis(P, n, (f32(1 / 32768) * U * U * (Em + f32(1 / 1024) * U)).astype(f32))
     bad = ~(U < f32(1e12))
     amb[bad] = True; rej[bad] = False
     return rej, amb, h, cb
@@ -88,7 +88,7 @@ def test_children_certification_matches_reference():
     tot = cert = 0
     for level in (1, 3, 5, 7, 9, 12):
         n = 2 ** level
-        for kind in ('rand', 'plane', 'tiny', 'sliver', 'grid'):
+        for kind in ('rand', 'plane', 'tiny', 'sliver', 'grid', 'small', 'smallplane'):
             M = 3000
             P = rng.integers(0, n // 2 if level > 0 else 1, (M, 3))
             vsz = 2.0 / (n // 2)
@@ -107,6 +107,11 @@ def test_children_certification_matches_reference():
             elif kind == 'sliver':
                 a0 = Cc + rng.uniform(-1, 1, (M, 3)) * vsz; d = rng.normal(0, vsz, (M, 3))
                 v = np.stack([a0, a0 + d, a0 + d * rng.uniform(0, 1, (M, 1)) + rng.normal(0, 1e-8, (M, 3))], 1)
+            elif kind in ('small', 'smallplane'):  # edges ~1/100 of a level-2 voxel (cfg4's first levels)
+                at = 0.5 * rng.choice([-1.0, 0.0, 1.0], (M, 3)) if kind == 'smallplane' else rng.uniform(-0.6, 0.6, (M, 3))
+                es = 0.01 * rng.choice([1.0, 1e-2, 1e-4], (M, 1, 1))
+                v = (Cc + at * vsz + rng.normal(0, 0.01, (M, 3)) * (kind == 'smallplane'))[:, None, :] + \
+                    rng.normal(0, 1, (M, 3, 3)) * es
             else:  # axis aligned on child planes
                 k = rng.integers(0, 3, M)
                 base = Cc + rng.choice([-0.5, 0, 0.5], (M, 3)) * vsz
