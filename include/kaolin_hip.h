@@ -397,6 +397,20 @@ int kl_mesh_to_spc(int64_t num_faces, const float *face_vertices, uint32_t level
  * min(capacity, L+1) counts and returns L+1 (0 before any call). */
 int kl_mesh_to_spc_level_counts(int64_t *counts, int capacity);
 
+/* Fixed-capacity mesh_to_spc (no reference counterpart: mesh_to_spc_cuda.cu:351-352,438 read the
+ * counts back to size the outputs).  The same levels, every count on the device and nothing read
+ * back, so the call can be captured into a HIP graph.  octree (node_capacity) u8, face_idx
+ * (leaf_capacity) int64 and bary (leaf_capacity, 2) f32 are caller-allocated; result (3) int64
+ * device output = (num_nodes, num_leaves, status): status 0 = written (octree bytes past num_nodes
+ * are 0, face_idx rows past num_leaves -1, bary 0), 1 = num_nodes > node_capacity or num_leaves >
+ * leaf_capacity (nothing written; the first two entries are the sizes needed), 2 = the workspace's
+ * per-level pair buffers (96 per face) overflowed (nothing written: call kl_mesh_to_spc).
+ * level in [1, 15); workspace of kl_mesh_to_spc_fixed_workspace_bytes(num_faces) bytes. */
+size_t kl_mesh_to_spc_fixed_workspace_bytes(int64_t num_faces);
+int kl_mesh_to_spc_fixed(int64_t num_faces, const float *face_vertices, uint32_t level, int64_t node_capacity,
+                         int64_t leaf_capacity, uint8_t *octree, int64_t *face_idx, float *bary,
+                         int64_t *result, void *workspace, size_t workspace_bytes, kl_stream stream);
+
 /* spc.cpp:55-65 morton_to_octree: sorted unique leaf morton codes -> octree bytes. */
 int kl_morton_to_octree(int64_t num_points, const uint64_t *morton, uint32_t level,
                         kl_alloc_fn alloc, void *alloc_ctx, uint8_t **octree, int64_t *num_nodes,

@@ -1433,6 +1433,84 @@ static int morton_to_octree_rows(int64_t n, const uint64_t *morton, uint32_t L, 
   return KL_OK;
 }
 
+// The node-rank path's workspace: pair buffers of 96 pairs per face per level (cfg4: 1.18 M of
+// 19.2 M at L = 9), in shards; nodes per level and octree bytes: a quarter of that; the last
+// level's least-face slots (8 per parent) reuse the pair buffer that level would have written
+// (2 cap words >= 8 ncap).
+struct M2sNodes {
+  unsigned long long cap = 0, seg = 0;
+  uint32_t ncap = 0, oct_cap = 0, fmin_cap = 0;
+  int64_t tiles = 0;
+  size_t qb = 0, mbytes = 0, sbytes = 0, ctl_bytes = 0, total = 0;
+  uint32_t *Qk[2], *Qf[2], *S[2];
+  uint64_t *M[2], *SL[2];
+  uint8_t *arena = nullptr;
+  M2sCtl *ctl = nullptr;
+  unsigned long long *status = nullptr;
+  bool plan(int64_t F) {
+    cap = (unsigned long long)std::max<int64_t>(F * 96, (int64_t)1 << 20);
+    if (F >= ((int64_t)1 << 31) || cap >= (1ull << 31)) return false;
+    seg = cap / M2S_SHARDS;
+    ncap = (uint32_t)(cap / 4);
+    oct_cap = ncap;
+    fmin_cap = (uint32_t)(2 * cap);
+    tiles = cdiv(ncap, M2S_TILE);
+    qb = al256b((size_t)cap * 4);
+    mbytes = al256b((size_t)ncap * 8);
+    sbytes = al256b(((size_t)ncap + 1) * 4);
+    ctl_bytes = al256b(sizeof(M2sCtl) + (size_t)tiles * 8);
+    total = 4 * qb + 4 * mbytes + 2 * sbytes + al256b(oct_cap + 4) + ctl_bytes;
+    return true;
+  }
+  void place(char *p) {
+    for (int k = 0; k < 2; k++) {
+      Qk[k] = (uint32_t *)p;  // key then face: the pair of arrays is also 2 cap contiguous words
+      Qf[k] = (uint32_t *)(p + qb);
+      p += 2 * qb;
+    }
+    for (int k = 0; k < 2; k++, p += mbytes) M[k] = (uint64_t *)p;
+    for (int k = 0; k < 2; k++, p += mbytes) SL[k] = (uint64_t *)p;  // child slots of levels l, l + 1
+    for (int k = 0; k < 2; k++, p += sbytes) S[k] = (uint32_t *)p;
+    arena = (uint8_t *)p;
+    p += al256b(oct_cap + 4);
+    ctl = (M2sCtl *)p;
+    status = (unsigned long long *)(p + sizeof(M2sCtl));
+  }
+  uint32_t *fmin8(uint32_t L) const { return Qk[L & 1]; }
+};
+
+// the root test and levels 1..L (nothing read back): the octree rows in the arena, the counts in ctl
+static int m2s_nodes_levels(int64_t F, const float *fv, uint32_t L, M2sNodes &w, hipStream_t st) {
+  M2sCtl *ctl = w.ctl;
+  uint32_t *fmin8 = w.fmin8(L);
+  KL_CHECK_RC(fill_async(ctl, 0, w.ctl_bytes, st));
+  if (F == 0) return KL_OK;
+  hipLaunchKernelGGL(m2s_root_kernel, dim3((unsigned)cdiv(F, 256)), dim3(256), 0, st, F, fv, w.Qk[0], w.Qf[0], w.seg,
+                     ctl, w.M[0], w.SL[0], fmin8, L);
+  KL_CHECK_LAUNCH();
+  const unsigned grid = (unsigned)std::max<int64_t>(M2S_GRID, cdiv((int64_t)w.cap, 256 * M2S_MAX_CHUNKS));
+  const unsigned rgrid = (unsigned)std::min<int64_t>(256, std::max<int64_t>(w.tiles, 1));  // one per CU
+  for (uint32_t l = 1; l <= L; l++) {
+    // level l - 2's S and octree row resolve the keys of level l - 1's pairs (level -1: ctl's root)
+    const uint32_t *Spp = l >= 2 ? w.S[l & 1] : ctl->root_S;
+    const uint8_t *octpp = l >= 2 ? w.arena : (const uint8_t *)&ctl->root_oct;
+    const uint32_t *opp = l >= 2 ? &ctl->O[l - 2] : &ctl->zero;
+    const int a = (l - 1) & 1;
+    if (l < L)
+      hipLaunchKernelGGL(m2s_node_kernel<false>, dim3(grid), dim3(256), 0, st, fv, w.Qk[a], w.Qf[a], w.Qk[a ^ 1],
+                         w.Qf[a ^ 1], w.seg, ctl, l, Spp, octpp, opp, w.M[a], (uint8_t *)w.SL[a], fmin8);
+    else
+      hipLaunchKernelGGL(m2s_node_kernel<true>, dim3(grid), dim3(256), 0, st, fv, w.Qk[a], w.Qf[a], w.Qk[a ^ 1],
+                         w.Qf[a ^ 1], w.seg, ctl, l, Spp, octpp, opp, w.M[a], (uint8_t *)w.SL[a], fmin8);
+    KL_CHECK_LAUNCH();
+    // level l - 1's row scanned: S_{l-1}, U_l, O_l, M_l
+    hipLaunchKernelGGL(m2s_rank_kernel, dim3(rgrid), dim3(256), 0, st, ctl, l - 1, L, w.arena, w.M[a], w.S[a],
+                       w.M[a ^ 1], w.SL[a], w.SL[a ^ 1], w.status, fmin8, w.ncap, w.oct_cap, w.fmin_cap);
+    KL_CHECK_LAUNCH();
+  }
+  return KL_OK;
+}
+
 // mesh_to_spc by node ranks (m2s_node_kernel): returns KL_OK, an error, or 1 = not taken
 // (capacity): the caller runs the per-level path.  One host read (the counts, after the levels).
 static int mesh_to_spc_nodes(int64_t F, const float *fv, uint32_t L, Scratch &sc, uint8_t **octree,
@@ -1443,65 +1521,15 @@ static int mesh_to_spc_nodes(int64_t F, const float *fv, uint32_t L, Scratch &sc
   *bary = nullptr;
   *num_nodes = 0;
   *num_leaves = 0;
-  if (F <= 0 || F >= ((int64_t)1 << 31) || L == 0) return 1;
-  // pairs per level buffer: 96 per face (cfg4: 4.6 M at L = 9 against 19.2 M), in shards; nodes per
-  // level and octree bytes: a quarter of that; the last level's least-face slots (8 per parent)
-  // reuse the pair buffer that level would have written (2 cap words >= 8 ncap)
-  const unsigned long long cap = (unsigned long long)std::max<int64_t>(F * 96, (int64_t)1 << 20);
-  if (cap >= (1ull << 31)) return 1;
-  const unsigned long long seg = cap / M2S_SHARDS;
-  const uint32_t ncap = (uint32_t)(cap / 4), oct_cap = ncap, fmin_cap = (uint32_t)(2 * cap);
-  const int64_t tiles = cdiv(ncap, M2S_TILE);
-  const size_t qb = al256b((size_t)cap * 4), mbytes = al256b((size_t)ncap * 8), sbytes = al256b(((size_t)ncap + 1) * 4);
-  const size_t ctl_bytes = al256b(sizeof(M2sCtl) + (size_t)tiles * 8);
-  const size_t chunk = 4 * qb + 4 * mbytes + 2 * sbytes + al256b(oct_cap + 4) + ctl_bytes;
-  char *base = (char *)sc.get(chunk);
+  M2sNodes w;
+  if (F <= 0 || L == 0 || !w.plan(F)) return 1;
+  char *base = (char *)sc.get(w.total);
   if (!base) return KL_E_ALLOC;
-  uint32_t *Qk[2], *Qf[2];
-  uint64_t *M[2];
-  uint32_t *S[2];
-  char *p = base;
-  for (int k = 0; k < 2; k++) {
-    Qk[k] = (uint32_t *)p;  // key then face: the pair of arrays is also 2 cap contiguous words
-    Qf[k] = (uint32_t *)(p + qb);
-    p += 2 * qb;
-  }
-  for (int k = 0; k < 2; k++, p += mbytes) M[k] = (uint64_t *)p;
-  uint64_t *SL[2];  // child slots (8 flag bytes per node) of levels l and l + 1
-  for (int k = 0; k < 2; k++, p += mbytes) SL[k] = (uint64_t *)p;
-  for (int k = 0; k < 2; k++, p += sbytes) S[k] = (uint32_t *)p;
-  uint8_t *arena = (uint8_t *)p;
-  p += al256b(oct_cap + 4);
-  M2sCtl *ctl = (M2sCtl *)p;
-  unsigned long long *status = (unsigned long long *)(p + sizeof(M2sCtl));
-  KL_CHECK_RC(fill_async(ctl, 0, ctl_bytes, st));
-  uint32_t *fmin8 = Qk[L & 1];
-  hipLaunchKernelGGL(m2s_root_kernel, dim3((unsigned)cdiv(F, 256)), dim3(256), 0, st, F, fv, Qk[0], Qf[0], seg, ctl,
-                     M[0], SL[0], fmin8, L);
-  KL_CHECK_LAUNCH();
-  const unsigned grid = (unsigned)std::max<int64_t>(M2S_GRID, cdiv((int64_t)cap, 256 * M2S_MAX_CHUNKS));
-  const unsigned rgrid = (unsigned)std::min<int64_t>(256, std::max<int64_t>(tiles, 1));  // one per CU
-  for (uint32_t l = 1; l <= L; l++) {
-    // level l - 2's S and octree row resolve the keys of level l - 1's pairs (level -1: ctl's root)
-    const uint32_t *Spp = l >= 2 ? S[l & 1] : ctl->root_S;
-    const uint8_t *octpp = l >= 2 ? arena : (const uint8_t *)&ctl->root_oct;
-    const uint32_t *opp = l >= 2 ? &ctl->O[l - 2] : &ctl->zero;
-    const int a = (l - 1) & 1;
-    if (l < L)
-      hipLaunchKernelGGL(m2s_node_kernel<false>, dim3(grid), dim3(256), 0, st, fv, Qk[a], Qf[a], Qk[a ^ 1], Qf[a ^ 1], seg,
-                         ctl, l, Spp, octpp, opp, M[a], (uint8_t *)SL[a], fmin8);
-    else
-      hipLaunchKernelGGL(m2s_node_kernel<true>, dim3(grid), dim3(256), 0, st, fv, Qk[a], Qf[a], Qk[a ^ 1], Qf[a ^ 1], seg,
-                         ctl, l, Spp, octpp, opp, M[a], (uint8_t *)SL[a], fmin8);
-    KL_CHECK_LAUNCH();
-    // level l - 1's row scanned: S_{l-1}, U_l, O_l, M_l
-    hipLaunchKernelGGL(m2s_rank_kernel, dim3(rgrid), dim3(256), 0, st, ctl, l - 1, L, arena, M[a], S[a], M[a ^ 1],
-                       SL[a], SL[a ^ 1], status, fmin8, ncap, oct_cap, fmin_cap);
-    KL_CHECK_LAUNCH();
-  }
+  w.place(base);
+  KL_CHECK_RC(m2s_nodes_levels(F, fv, L, w, st));
   std::vector<char> hbuf(sizeof(M2sCtl));
   M2sCtl &h = *(M2sCtl *)hbuf.data();
-  KL_CHECK_RC(host_read(&h, ctl, sizeof(M2sCtl), st));
+  KL_CHECK_RC(host_read(&h, w.ctl, sizeof(M2sCtl), st));
   if (h.overflow) return 1;
   t_m2s_counts[0] = F;
   for (uint32_t l = 1; l <= L; l++) {
@@ -1517,11 +1545,11 @@ static int mesh_to_spc_nodes(int64_t F, const float *fv, uint32_t L, Scratch &sc
   int64_t *fu = (int64_t *)sc.get((size_t)leaves * sizeof(int64_t));
   float *bu = (float *)sc.get((size_t)leaves * 2 * sizeof(float));
   if (!out || !fu || !bu) return KL_E_ALLOC;
-  KL_CHECK_HIP(hipMemcpyAsync(out, arena, (size_t)nodes, hipMemcpyDeviceToDevice, st));
+  KL_CHECK_HIP(hipMemcpyAsync(out, w.arena, (size_t)nodes, hipMemcpyDeviceToDevice, st));
   const int64_t nslots = 8 * (int64_t)h.U[L - 1];
   const int b = (int)((L - 1) & 1);
-  hipLaunchKernelGGL(m2s_node_leaves_kernel, dim3((unsigned)cdiv(nslots, 256)), dim3(256), 0, st, nslots, ctl, L,
-                     arena, S[b], M[b], fmin8, fv, fu, bu);
+  hipLaunchKernelGGL(m2s_node_leaves_kernel, dim3((unsigned)cdiv(nslots, 256)), dim3(256), 0, st, nslots, w.ctl, L,
+                     w.arena, w.S[b], w.M[b], w.fmin8(L), fv, fu, bu);
   KL_CHECK_LAUNCH();
   *octree = out;
   *num_nodes = nodes;
@@ -1529,6 +1557,38 @@ static int mesh_to_spc_nodes(int64_t F, const float *fv, uint32_t L, Scratch &sc
   *bary = bu;
   *num_leaves = leaves;
   return KL_OK;
+}
+
+// The fixed-capacity form's last step, sized on the device: result = (nodes, leaves, status), status
+// 0 = written, 1 = an output capacity too small (nothing written; nodes / leaves say what is
+// needed), 2 = the workspace's pair buffers overflowed (counts unknown: run the eager call).
+__global__ void m2s_fixed_final_kernel(const M2sCtl *__restrict__ ctl, uint32_t L, const uint8_t *__restrict__ arena,
+                                       const uint32_t *__restrict__ Sp, const uint64_t *__restrict__ Mp,
+                                       const uint32_t *__restrict__ fmin8, const float *__restrict__ fv,
+                                       int64_t node_cap, int64_t leaf_cap, uint8_t *__restrict__ octree,
+                                       int64_t *__restrict__ fout, float *__restrict__ bary,
+                                       int64_t *__restrict__ result) {
+  const int64_t leaves = ctl->U[L], nodes = leaves ? (int64_t)ctl->O[L] : 0;
+  const int over = ctl->overflow;
+  const int status = over ? 2 : (nodes > node_cap || leaves > leaf_cap ? 1 : 0);
+  const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, step = (int64_t)gridDim.x * blockDim.x;
+  if (t0 == 0) {
+    result[0] = over ? 0 : nodes;
+    result[1] = over ? 0 : leaves;
+    result[2] = status;
+  }
+  if (status || leaves == 0) return;
+  for (int64_t t = t0; t < nodes; t += step) octree[t] = arena[t];
+  const int64_t nslots = 8 * (int64_t)ctl->U[L - 1];
+  const uint32_t OL1 = ctl->O[L - 1];
+  for (int64_t s = t0; s < nslots; s += step) {
+    const uint32_t jp = (uint32_t)(s >> 3), c = (uint32_t)(s & 7);
+    const uint32_t b = arena[OL1 + jp];
+    if (!((b >> c) & 1)) continue;
+    const uint32_t o = Sp[jp] + (uint32_t)__popc(b & ((1u << c) - 1u));
+    const uint64_t q = Mp[jp] * 2 + m2s_child_off(c);
+    leaf_out_pt((int)(q & 0xffff), (int)((q >> 16) & 0xffff), (int)(q >> 32), (int64_t)fmin8[s], fv, L, o, fout, bary);
+  }
 }
 
 // returns KL_OK, an error, or 1 = not taken (capacity / key width): the caller runs the
@@ -2019,6 +2079,34 @@ extern "C" int kl_mesh_to_spc(int64_t num_faces, const float *fv, uint32_t level
     if (rc != 1) return rc;
   }
   return mesh_to_spc_impl(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves, S(stream));
+}
+
+extern "C" size_t kl_mesh_to_spc_fixed_workspace_bytes(int64_t num_faces) {
+  M2sNodes w;
+  return num_faces >= 0 && w.plan(num_faces) ? w.total : 0;
+}
+
+extern "C" int kl_mesh_to_spc_fixed(int64_t num_faces, const float *fv, uint32_t level, int64_t node_capacity,
+                                    int64_t leaf_capacity, uint8_t *octree, int64_t *face_idx, float *bary,
+                                    int64_t *result, void *workspace, size_t workspace_bytes, kl_stream stream) {
+  KL_REQUIRE(level >= 1 && level < (uint32_t)SPC_MAX_LEVELS, "mesh_to_spc: level must be in [1, 15) with a capacity");
+  KL_REQUIRE(num_faces >= 0 && node_capacity >= 0 && leaf_capacity >= 0, "mesh_to_spc: negative size");
+  M2sNodes w;
+  KL_REQUIRE(w.plan(num_faces), "mesh_to_spc: too many faces for the fixed-capacity form");
+  KL_REQUIRE(workspace != nullptr && workspace_bytes >= w.total, "mesh_to_spc: workspace too small");
+  hipStream_t st = S(stream);
+  w.place((char *)workspace);
+  if (node_capacity) KL_CHECK_RC(fill_async(octree, 0, (size_t)node_capacity, st));
+  if (leaf_capacity) {
+    KL_CHECK_RC(fill_async(face_idx, 0xff, (size_t)leaf_capacity * 8, st));
+    KL_CHECK_RC(fill_async(bary, 0, (size_t)leaf_capacity * 8, st));
+  }
+  KL_CHECK_RC(m2s_nodes_levels(num_faces, fv, level, w, st));
+  const int b = (int)((level - 1) & 1);
+  hipLaunchKernelGGL(m2s_fixed_final_kernel, dim3(1024), dim3(256), 0, st, w.ctl, level, w.arena, w.S[b], w.M[b],
+                     w.fmin8(level), fv, node_capacity, leaf_capacity, octree, face_idx, bary, result);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
 }
 
 extern "C" int kl_mesh_to_spc_level_counts(int64_t *counts, int capacity) {

@@ -420,9 +420,7 @@ def check_sign_batched(verts, faces, points, maxlen):
 
 
 # ------------------------------------------------------------------- ops.conversions / spc
-def mesh_to_spc_cuda(face_vertices, target_level):
-    """mesh_to_spc.cpp:28-44."""
-    func = 'mesh_to_spc_cuda'
+def _mesh_to_spc_checks(face_vertices):
     if not face_vertices.is_cuda:
         raise RuntimeError('face_vertices must be a CUDA tensor')
     if not face_vertices.is_contiguous():
@@ -431,7 +429,16 @@ def mesh_to_spc_cuda(face_vertices, target_level):
         raise RuntimeError('face_vertices must be of shape (F, 3, 3)')
     if face_vertices.dtype != torch.float32:
         raise RuntimeError('face_vertices must be float')
+
+
+def mesh_to_spc_cuda(face_vertices, target_level):
+    """mesh_to_spc.cpp:28-44."""
+    func = 'mesh_to_spc_cuda'
+    _mesh_to_spc_checks(face_vertices)
     N.require_gpu(func, face_vertices)
+    if N.capturing(face_vertices.device):
+        raise RuntimeError(f'{func}: the output size is known only after the levels (one host read); '
+                           'under graph capture call kaolin.ops.conversions.unbatched_mesh_to_spc(..., capacity=N)')
     dev = face_vertices.device
     arena = N.Arena(dev)
     oct_p, fidx_p, bary_p = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
@@ -447,6 +454,41 @@ def mesh_to_spc_cuda(face_vertices, target_level):
     face_idx = arena.tensor(fidx_p.value, nl.value, torch.long, (nl.value,))
     bary = arena.tensor(bary_p.value, nl.value * 2, torch.float32, (nl.value, 2))
     return [octree, face_idx, bary]
+
+
+def mesh_to_spc_fixed_cuda(face_vertices, target_level, capacity):
+    """mesh_to_spc_cuda with fixed output sizes (not a reference _C name): nothing is read back to
+    the host, so it can be captured into a graph (kl_mesh_to_spc_fixed).  capacity: N (octree bytes
+    and leaves alike) or (node_capacity, leaf_capacity).  Returns [octree (node_capacity,) u8,
+    face_idx (leaf_capacity,) int64, bary (leaf_capacity, 2) f32, result (3,) int64 = (num_nodes,
+    num_leaves, status)]: status 0 = written (octree bytes past num_nodes 0, face_idx past
+    num_leaves -1, bary 0), 1 = a capacity too small (nothing written; num_nodes / num_leaves are
+    the sizes needed), 2 = the per-level pair buffers (96 per face) overflowed (nothing written:
+    call the eager form)."""
+    func = 'mesh_to_spc_cuda'
+    _mesh_to_spc_checks(face_vertices)
+    N.require_gpu(func, face_vertices)
+    if int(target_level) < 1:
+        raise ValueError(f'level must be >= 1 with a capacity, got {target_level}')
+    ncap, lcap = (int(capacity), int(capacity)) if not isinstance(capacity, (tuple, list)) else \
+        (int(capacity[0]), int(capacity[1]))
+    if ncap < 0 or lcap < 0:
+        raise ValueError(f'capacity must be >= 0, got {capacity}')
+    dev = face_vertices.device
+    octree = torch.empty((ncap,), dtype=torch.uint8, device=dev)
+    face_idx = torch.empty((lcap,), dtype=torch.long, device=dev)
+    bary = torch.empty((lcap, 2), dtype=torch.float32, device=dev)
+    result = torch.empty((3,), dtype=torch.int64, device=dev)
+    F = face_vertices.shape[0]
+    ws_bytes = N.size('kl_mesh_to_spc_fixed_workspace_bytes', F)
+    if ws_bytes == 0:
+        raise RuntimeError(f'{func}: too many faces for the fixed-capacity form')
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    with N.on_device(dev):
+        N.check(N.lib().kl_mesh_to_spc_fixed(F, N.ptr(face_vertices), int(target_level), ncap, lcap, N.ptr(octree),
+                                             N.ptr(face_idx), N.ptr(bary), N.ptr(result), N.ptr(ws), ws_bytes,
+                                             N.stream_of(dev)), func)
+    return [octree, face_idx, bary, result]
 
 
 def morton_to_octree(mortons, level):
@@ -848,7 +890,8 @@ metrics = _module('kaolin._C.metrics', sided_distance_forward_cuda=sided_distanc
                   unbatched_triangle_distance_backward_cuda=unbatched_triangle_distance_backward_cuda)
 ops = _module('kaolin._C.ops')
 ops.mesh = _module('kaolin._C.ops.mesh', unbatched_mesh_intersection_cuda=unbatched_mesh_intersection_cuda)
-ops.conversions = _module('kaolin._C.ops.conversions', mesh_to_spc_cuda=mesh_to_spc_cuda)
+ops.conversions = _module('kaolin._C.ops.conversions', mesh_to_spc_cuda=mesh_to_spc_cuda,
+                          mesh_to_spc_fixed_cuda=mesh_to_spc_fixed_cuda)
 ops.spc = _module('kaolin._C.ops.spc', morton_to_octree=morton_to_octree, points_to_octree=points_to_octree,
                   points_to_morton_cuda=points_to_morton_cuda, morton_to_points_cuda=morton_to_points_cuda,
                   scan_octrees_cuda=scan_octrees_cuda, generate_points_cuda=generate_points_cuda)

@@ -88,6 +88,8 @@ _SIGS = {
     'kl_mesh_to_spc': (_I, [_I64, _P, ctypes.c_uint32, ALLOC_FN, _P, _PP, ctypes.POINTER(_I64), _PP, _PP,
                             ctypes.POINTER(_I64), _P]),
     'kl_mesh_to_spc_level_counts': (_I, [_P, _I]),
+    'kl_mesh_to_spc_fixed_workspace_bytes': (_SZ, [_I64]),
+    'kl_mesh_to_spc_fixed': (_I, [_I64, _P, ctypes.c_uint32, _I64, _I64, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_morton_to_octree': (_I, [_I64, _P, ctypes.c_uint32, ALLOC_FN, _P, _PP, ctypes.POINTER(_I64), _P]),
     'kl_scan_octrees': (_I, [_I, _P, _P, _P, _P, ctypes.POINTER(_I), _P]),
     'kl_generate_points': (_I, [_I, _I, _P, _P, _P, _P, _P]),

@@ -132,9 +132,19 @@ def _voxelgrids_cpu(vertices, faces, R, origin, scale, return_sparse):
     return grid
 
 
-def unbatched_mesh_to_spc(face_vertices, level):
+def unbatched_mesh_to_spc(face_vertices, level, capacity=None):
     r"""Conservative voxelisation of a mesh in [-1, 1]^3 to an SPC of ``level`` levels.
-    Returns (octree u8, face_idx int64 per leaf, barycentric (num_leaves, 2) f32)."""
+    Returns (octree u8, face_idx int64 per leaf, barycentric (num_leaves, 2) f32).
+
+    ``capacity`` (an extension; the reference reads the counts back to size the outputs,
+    mesh_to_spc_cuda.cu:351-352,438): N or (node_capacity, leaf_capacity) gives fixed-size outputs
+    and nothing read back, so the call can be captured into a graph; it then returns (octree,
+    face_idx, bary, result) with result = (num_nodes, num_leaves, status) on the device -- status 0:
+    the first num_nodes / num_leaves rows are the eager call's; 1: a capacity too small (nothing
+    written, the sizes needed in result); 2: the per-level pair buffers overflowed (nothing
+    written: call without ``capacity``)."""
     if face_vertices.shape[-1] != 3:
         raise NotImplementedError("unbatched_mesh_to_spc is only implemented for triangle meshes")
+    if capacity is not None:
+        return _C.ops.conversions.mesh_to_spc_fixed_cuda(face_vertices.contiguous(), level, capacity)
     return _C.ops.conversions.mesh_to_spc_cuda(face_vertices.contiguous(), level)

@@ -60,7 +60,8 @@ def test_C_registry_layout():
                  'render.spc.raytrace_cuda', 'render.spc.mark_pack_boundaries_cuda', 'render.spc.diff_cuda',
                  'render.spc.inclusive_sum_cuda', 'render.spc.sum_reduce_cuda', 'render.spc.cumsum_cuda',
                  'render.spc.cumprod_cuda', 'render.spc.generate_primary_rays_cuda',
-                 'render.spc.generate_shadow_rays_cuda', 'render.spc.raytrace_fixed_cuda']:
+                 'render.spc.generate_shadow_rays_cuda', 'render.spc.raytrace_fixed_cuda',
+                 'ops.conversions.mesh_to_spc_fixed_cuda']:
         obj = C
         for part in path.split('.'):
             obj = getattr(obj, part)

@@ -1193,6 +1193,72 @@ def test_mesh_to_spc_empty(kal):
     assert octree.shape == (0,) and fidx.shape == (0,) and tuple(bary.shape) == (0, 3)
 
 
+def _m2s_fixed_check(kal, fv, level, ncap, lcap):
+    """unbatched_mesh_to_spc(..., capacity) against the eager call: the written prefix bit-equal,
+    padding (0, -1, 0) after it, or status 1 with the sizes needed and nothing written."""
+    octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(fv, level)
+    fo, ff, fb, res = kal.ops.conversions.unbatched_mesh_to_spc(fv, level, capacity=(ncap, lcap))
+    nn, nl, status = (int(x) for x in res.cpu())
+    leaves = fidx.shape[0]
+    nodes = octree.shape[0] if leaves else 0
+    assert (nn, nl) == (nodes, leaves)
+    assert fo.shape == (ncap,) and ff.shape == (lcap,) and tuple(fb.shape) == (lcap, 2)
+    if nodes > ncap or leaves > lcap:
+        assert status == 1
+        assert not fo.any() and bool((ff == -1).all()) and not fb.any()
+        return status
+    assert status == 0
+    assert torch.equal(fo[:nodes], octree[:nodes]) and not fo[nodes:].any()
+    assert torch.equal(ff[:leaves], fidx) and bool((ff[leaves:] == -1).all())
+    assert torch.equal(fb[:leaves], bary[:, :2] if leaves else fb[:0]) and not fb[leaves:].any()
+    return status
+
+
+@pytest.mark.parametrize('level', [1, 3, 6])
+def test_mesh_to_spc_fixed_capacity_equals_eager(kal, level):
+    """kl_mesh_to_spc_fixed (nothing read back): exact, generous and too-small capacities on a
+    sphere and on the grazing-triangle set, and the empty mesh."""
+    v, f = _uv_sphere(16, 24, 0.9)
+    for fv in (T(v[f].astype(np.float32)), T(_grazing_triangles(level))):
+        octree, fidx, _ = kal.ops.conversions.unbatched_mesh_to_spc(fv, level)
+        nodes, leaves = octree.shape[0], fidx.shape[0]
+        assert _m2s_fixed_check(kal, fv, level, nodes, leaves) == 0
+        assert _m2s_fixed_check(kal, fv, level, nodes + 100, leaves + 77) == 0
+        assert _m2s_fixed_check(kal, fv, level, nodes - 1, leaves) == 1
+        assert _m2s_fixed_check(kal, fv, level, nodes, max(leaves - 1, 0)) == 1
+    empty = torch.tensor([[[5., 5., 5.], [6., 5., 5.], [5., 6., 5.]]], device=DEV)
+    assert _m2s_fixed_check(kal, empty, level, 16, 16) == 0
+
+
+def test_mesh_to_spc_fixed_capacity_graph_replay(kal):
+    """The fixed-capacity call captured into a graph and replayed on new vertices (the same input
+    buffer) answers the new mesh; the eager call refuses to be captured."""
+    v, f = _uv_sphere(20, 30, 0.9)
+    fv0 = T(v[f].astype(np.float32))
+    buf = fv0.clone()
+    cap = 40000
+    for _ in range(2):  # warm-up (allocations) outside the capture
+        kal.ops.conversions.unbatched_mesh_to_spc(buf, 6, capacity=cap)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = kal.ops.conversions.unbatched_mesh_to_spc(buf, 6, capacity=cap)
+    for k, (scale, shift) in enumerate([(1.0, 0.0), (0.7, 0.1), (0.5, -0.3)]):
+        newfv = (fv0 * scale + shift).contiguous()
+        buf.copy_(newfv)
+        graph.replay()
+        torch.cuda.synchronize()
+        octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(newfv, 6)
+        nn, nl, status = (int(x) for x in out[3].cpu())
+        assert (nn, nl, status) == (octree.shape[0], fidx.shape[0], 0), k
+        assert torch.equal(out[0][:nn], octree) and torch.equal(out[1][:nl], fidx), k
+        assert torch.equal(out[2][:nl], bary), k
+    g2 = torch.cuda.CUDAGraph()
+    with pytest.raises(RuntimeError, match='capacity'):
+        with torch.cuda.graph(g2):
+            kal.ops.conversions.unbatched_mesh_to_spc(buf, 6)
+
+
 def test_scan_generate_kat(kal, golden):
     g = golden('spc.npz')
     level, pyr, ex = kal.ops.spc.scan_octrees(T(g['scan_octrees']), torch.from_numpy(g['scan_lengths']))
