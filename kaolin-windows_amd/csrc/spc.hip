@@ -12,11 +12,10 @@
 // Differences in structure (not in results):
 //   * every kernel runs on the caller's stream (the reference used the legacy default
 //     stream with synchronous cudaMemcpy);
-//   * mesh_to_spc sizes its per-level buffers on device (capacity + device counters, see
-//     mesh_to_spc_async) and builds every octree level with one scan: three host reads per
-//     call; the per-level path (one 4-byte count read per level) remains the fallback and
-//     the standalone morton_to_octree; the whole pyramid of scan_octrees is computed on
-//     device and read back once;
+//   * mesh_to_spc keeps each level's nodes as a sorted list numbered by a scan of its octree row
+//     (no sort; mesh_to_spc_nodes): one host read per call, none in the fixed-capacity form; the
+//     per-level path (one 4-byte count read per level) remains the overflow fallback; the whole
+//     pyramid of scan_octrees is computed on device and read back once;
 //   * the child order of the ray march (VOXEL_ORDER) is derived, not tabulated:
 //     children sorted by (popcount(code ^ j), j).
 #include "common.h"
@@ -164,7 +163,7 @@ __device__ bool tri_voxel_test(const float *fa, const float *fb, const float *fc
 //    degenerate triangle (slack 0) are left to the full test.
 // Most of a level's proposals (8 children of each occupied parent per face) are separated by a
 // box axis or the plane; the full fp64 test then runs only on this test's survivors, compacted
-// into coherent waves (m2s_level_kernel).
+// into coherent waves (r04's first step; now the per-level fallback's and the root's pre-test).
 __device__ __forceinline__ bool tri_voxel_maybe(const float *fa, const float *fb, const float *fc, float cx, float cy,
                                                 float cz, float h) {
   const float ax = fa[0] - cx, ay = fa[1] - cy, az = fa[2] - cz;
@@ -468,26 +467,6 @@ static int mesh_to_spc_impl(int64_t F, const float *fv, uint32_t L, Scratch &sc,
 }
 
 // ------------------------------------------------------------------ mesh_to_spc, device-sized
-// The same per-level proposals without a host round-trip per level: each level is ONE launch
-// that tests its proposals (the same SAT) and appends the survivors' children through a
-// device counter (one atomic per wave) into a buffer of capacity `cap`; the next level reads
-// its count from device memory (grid-stride).  Appending loses the generation order, which
-// the reference's stable sort kept among equal mortons -- that order is ascending face id
-// (level 0 is the faces in order; every level keeps its parents' order), so the final sort
-// is on the key (morton << FB) | face: same (morton, face) sequence, same leaves.  Host
-// round-trips: the final proposal count (+ overflow flag and the per-level counts), the
-// unique-leaf count and the octree size -- 3 instead of one per level and per octree level.
-// Overflow of `cap` (or a key wider than 64 bits) falls back to the per-level path.
-__global__ void m2s_init_kernel(int64_t n, uint64_t *__restrict__ m, uint32_t *__restrict__ t,
-                                unsigned long long *__restrict__ counts) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < n) {  // level 0: every face, in shard 0
-    m[i] = 0;
-    t[i] = (uint32_t)i;
-  }
-  if (i == 0) counts[0] = (unsigned long long)n;
-}
-
 // A returning atomic on one word saturates at ~88 per us (MI355X_MICROARCH.md), so the level
 // counters and the output are sharded M2S_SHARDS ways by workgroup (blockIdx % M2S_SHARDS,
 // which also keeps a shard on one XCD): shard g of a level is the region [g * seg,
@@ -526,119 +505,12 @@ struct ShardIn {
   }
 };
 
-// Each workgroup owns a contiguous span of the level's proposals (n / gridDim, up to 64
-// chunks of 256): it tests them all first (pass bits in a register per thread), reserves the
-// span's whole output with ONE atomic, then writes the survivors' children chunk by chunk
-// (block scans for the positions).  One round of workgroups per launch, one returning atomic
-// per workgroup and level.  (A grid-stride version with one chunk per pass paid a returning
-// atomic per chunk and its 16,384 mostly idle workgroups ~25 us per level.)
+// The level kernels' grid: a span of up to M2S_MAX_CHUNKS chunks of 256 pairs per workgroup,
+// one reservation per workgroup and level.
 constexpr int M2S_GRID = 2048;
 constexpr int M2S_MAX_CHUNKS = 64;
 
-__global__ void __launch_bounds__(256) m2s_level_kernel(const float *__restrict__ fv, const uint64_t *__restrict__ min_,
-                                                        const uint32_t *__restrict__ tin,
-                                                        const unsigned long long *__restrict__ cnt_in,
-                                                        uint64_t *__restrict__ mout, uint32_t *__restrict__ tout,
-                                                        unsigned long long *__restrict__ cnt_out,
-                                                        unsigned long long seg, int *__restrict__ overflow,
-                                                        uint32_t level, uint32_t not_done) {
-  __shared__ int s_wave[16];
-  __shared__ unsigned long long s_base;
-  __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
-  __shared__ uint16_t s_list[M2S_MAX_CHUNKS * 256];  // the pre-test's survivors: chunk << 8 | thread
-  __shared__ unsigned long long s_pass[256];
-  // After an overflow the shards hold unwritten holes below their clamped counts (the overflowing
-  // workgroups reserved past seg and wrote nothing): the levels after it must not read them (their
-  // face ids would index fv out of bounds).  The result is discarded and the host reruns the
-  // per-level path.
-  if (*(volatile int *)overflow) return;
-  ShardIn in;
-  in.load(s_pre, cnt_in, seg);
-  const unsigned long long n = in.total();
-  const int g = blockIdx.x % M2S_SHARDS;
-  const uint32_t kids = not_done ? 8u : 1u;
-  const unsigned long long span = (n + gridDim.x - 1) / gridDim.x;
-  const unsigned long long lo = (unsigned long long)blockIdx.x * span;
-  const unsigned long long hi = lo + span < n ? lo + span : n;
-  if (lo >= hi) return;
-  const int nch = (int)((hi - lo + blockDim.x - 1) / blockDim.x);
-  if (nch > M2S_MAX_CHUNKS) {  // the host sizes the grid so that this does not happen
-    if (threadIdx.x == 0) *overflow = 1;
-    return;
-  }
-  // 1. the float pre-test of every proposal of the span (tri_voxel_maybe); its survivors listed
-  uint64_t cand = 0;
-#pragma unroll 1
-  for (int k = 0; k < nch; k++) {
-    const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
-    if (i >= hi) continue;
-    const unsigned long long p = in.pos(i, seg);
-    float cx, cy, cz, h;
-    voxel_center(min_[p], level, cx, cy, cz, h);
-    const float *v = fv + (int64_t)tin[p] * 9;
-    if (tri_voxel_maybe(v, v + 3, v + 6, cx, cy, cz, h)) cand |= 1ull << k;
-  }
-  s_pass[threadIdx.x] = 0;
-  int ncand = 0;
-  {
-    int o = block_exclusive_scan(__popcll(cand), s_wave, &ncand);
-    for (uint64_t c = cand; c; c &= c - 1) s_list[o++] = (uint16_t)((__builtin_ctzll(c) << 8) | threadIdx.x);
-  }
-  __syncthreads();
-  // 1b. the full fp64 test (mesh_to_spc_cuda.cu:96-159) on the survivors, in coherent waves
-#pragma unroll 1
-  for (int e = threadIdx.x; e < ncand; e += blockDim.x) {
-    const int code = s_list[e], k = code >> 8, tt = code & 255;
-    const unsigned long long i = lo + (unsigned long long)k * blockDim.x + tt;
-    const unsigned long long p = in.pos(i, seg);
-    float cx, cy, cz, h;
-    voxel_center(min_[p], level, cx, cy, cz, h);
-    const float *v = fv + (int64_t)tin[p] * 9;
-    if (tri_voxel_test(v, v + 3, v + 6, cx, cy, cz, h)) atomicOr(&s_pass[tt], 1ull << k);
-  }
-  __syncthreads();
-  const uint64_t pass = s_pass[threadIdx.x];
-  // 2. one reservation for the span
-  int total = 0;
-  (void)block_exclusive_scan(__popcll(pass) * (int)kids, s_wave, &total);
-  if (threadIdx.x == 0) s_base = total ? atomicAdd(cnt_out + g, (unsigned long long)total) : 0ull;
-  __syncthreads();
-  unsigned long long o0 = s_base;
-  if (total == 0) return;
-  if (o0 + (unsigned long long)total > seg) {
-    if (threadIdx.x == 0) *overflow = 1;
-    return;
-  }
-  o0 += (unsigned long long)g * seg;
-  // 3. the survivors' children, chunk by chunk in order
-#pragma unroll 1
-  for (int k = 0; k < nch; k++) {
-    const bool ps = (pass >> k) & 1;
-    int ctot = 0;
-    const int pre = block_exclusive_scan(ps ? (int)kids : 0, s_wave, &ctot);
-    if (ps) {
-      const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
-      const unsigned long long p = in.pos(i, seg);
-      const uint64_t m = min_[p];
-      const uint32_t tr = tin[p];
-      const unsigned long long o = o0 + (unsigned long long)pre;
-      if (!not_done) {
-        mout[o] = m;
-        tout[o] = tr;
-      } else {
-        int16_t px, py, pz;
-        to_point(m, px, py, pz);
-        for (uint32_t c = 0; c < 8; c++) {
-          mout[o + c] = to_morton(2 * px + (c >> 2), 2 * py + ((c >> 1) & 1), 2 * pz + (c & 1));
-          tout[o + c] = tr;
-        }
-      }
-    }
-    o0 += (unsigned long long)ctot;
-  }
-}
-
-// ---- the 8 children of a parent (voxel, face) pair at once (m2s_children_kernel).
+// ---- the 8 children of a parent (voxel, face) pair at once (m2s_children_pt).
 // The reference's decision for a child c (tri_voxel_test: 13 SAT axes, each passing iff
 // (float)max(-max_k d_k, min_k d_k) <= (float)(h |a|_1), d_k = v_k . a, v_k = fl(f_k - c)) is
 // derived per axis from the PARENT's projections: with C the parent's centre and w_k = fl(f_k - C),
@@ -799,88 +671,6 @@ __device__ uint32_t m2s_children_pt(const float *v, int px, int py, int pz, uint
   return pass;
 }
 
-__device__ uint32_t m2s_children(const float *v, uint64_t m, uint32_t level) {
-  int16_t px, py, pz;
-  to_point(m, px, py, pz);
-  return m2s_children_pt(v, px, py, pz, level);
-}
-
-// One level of the device-sized mesh_to_spc from the PARENTS: the input is the previous level's
-// passing (voxel, face) pairs, each thread decides its parent's 8 children (m2s_children) and the
-// passing children are appended (sharded counters, one reservation per workgroup, as
-// m2s_level_kernel) -- the pairs of this level, which the next level reads as its parents.
-__global__ void __launch_bounds__(256) m2s_children_kernel(const float *__restrict__ fv,
-                                                           const uint64_t *__restrict__ min_,
-                                                           const uint32_t *__restrict__ tin,
-                                                           const unsigned long long *__restrict__ cnt_in,
-                                                           uint64_t *__restrict__ mout, uint32_t *__restrict__ tout,
-                                                           unsigned long long *__restrict__ cnt_out,
-                                                           unsigned long long seg, int *__restrict__ overflow,
-                                                           uint32_t level) {
-  __shared__ int s_wave[16];
-  __shared__ unsigned long long s_base;
-  __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
-  __shared__ uint8_t s_kids[M2S_MAX_CHUNKS][256];
-  if (*(volatile int *)overflow) return;  // holes in the input (m2s_level_kernel)
-  ShardIn in;
-  in.load(s_pre, cnt_in, seg);
-  const unsigned long long n = in.total();
-  const int g = blockIdx.x % M2S_SHARDS;
-  const unsigned long long span = (n + gridDim.x - 1) / gridDim.x;
-  const unsigned long long lo = (unsigned long long)blockIdx.x * span;
-  const unsigned long long hi = lo + span < n ? lo + span : n;
-  if (lo >= hi) return;
-  const int nch = (int)((hi - lo + blockDim.x - 1) / blockDim.x);
-  if (nch > M2S_MAX_CHUNKS) {
-    if (threadIdx.x == 0) *overflow = 1;
-    return;
-  }
-  int mine = 0;
-#pragma unroll 1
-  for (int k = 0; k < nch; k++) {
-    const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
-    uint32_t kids = 0;
-    if (i < hi) {
-      const unsigned long long p = in.pos(i, seg);
-      kids = m2s_children(fv + (int64_t)tin[p] * 9, min_[p], level);
-    }
-    s_kids[k][threadIdx.x] = (uint8_t)kids;
-    mine += __popc(kids);
-  }
-  int total = 0;
-  (void)block_exclusive_scan(mine, s_wave, &total);
-  if (threadIdx.x == 0) s_base = total ? atomicAdd(cnt_out + g, (unsigned long long)total) : 0ull;
-  __syncthreads();
-  unsigned long long o0 = s_base;
-  if (total == 0) return;
-  if (o0 + (unsigned long long)total > seg) {
-    if (threadIdx.x == 0) *overflow = 1;
-    return;
-  }
-  o0 += (unsigned long long)g * seg;
-#pragma unroll 1
-  for (int k = 0; k < nch; k++) {
-    const uint32_t kids = s_kids[k][threadIdx.x];
-    int ctot = 0;
-    const int pre = block_exclusive_scan(__popc(kids), s_wave, &ctot);
-    if (kids) {
-      const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
-      const unsigned long long p = in.pos(i, seg);
-      int16_t px, py, pz;
-      to_point(min_[p], px, py, pz);
-      const uint32_t tr = tin[p];
-      unsigned long long o = o0 + (unsigned long long)pre;
-      for (uint32_t c = kids; c; c &= c - 1) {
-        const int q = __builtin_ctz(c);
-        mout[o] = to_morton(2 * px + (q >> 2), 2 * py + ((q >> 1) & 1), 2 * pz + (q & 1));
-        tout[o] = tr;
-        o++;
-      }
-    }
-    o0 += (unsigned long long)ctot;
-  }
-}
-
 // ---- mesh_to_spc by node ranks (r04, m2s_node_kernel / m2s_rank_kernel): no sort, one host read.
 // Level l's nodes are a list in morton order (U_l nodes).  Node j's octree byte oct_l[j] -- the OR
 // of the child masks its (node, face) pairs decide -- IS the octree row, and the exclusive popcount
@@ -967,7 +757,7 @@ __device__ __forceinline__ uint32_t m2s_node(uint32_t key, const uint32_t *__res
 
 // One level l >= 1: each thread takes a pair of level l - 1, decides its node's 8 children
 // (m2s_children), flags them in the node's 8 child slots, and appends (node * 8 + c, face) for the
-// passing children (sharded, one reservation per workgroup, as m2s_children_kernel) -- or, at the
+// passing children (sharded, one reservation per workgroup) -- or, at the
 // last level, keeps the least face per (node, child) slot.  The scan kernel then forms each node's
 // octree byte from its slots.
 template <bool LAST>
@@ -984,7 +774,10 @@ __global__ void __launch_bounds__(256) m2s_node_kernel(const float *__restrict__
   __shared__ unsigned long long s_base;
   __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
   __shared__ uint8_t s_kids[M2S_MAX_CHUNKS][256];
-  if (*(volatile int *)&ctl->overflow) return;  // holes in the input (m2s_level_kernel)
+  // After an overflow the shards hold unwritten holes below their clamped counts (the overflowing
+  // workgroups reserved past seg and wrote nothing): the levels after it must not read them (their
+  // face ids would index fv out of bounds).  The host then runs the per-level path.
+  if (*(volatile int *)&ctl->overflow) return;
   ShardIn in;
   in.load(s_pre, ctl->counts + (level - 1) * M2S_SHARDS, seg);
   const unsigned long long n = in.total();
@@ -1219,101 +1012,7 @@ __global__ void m2s_node_leaves_kernel(int64_t nslots, const M2sCtl *__restrict_
   leaf_out_pt((int)(q & 0xffff), (int)((q >> 16) & 0xffff), (int)(q >> 32), (int64_t)fmin8[s], fv, L, o, fout, bary);
 }
 
-__global__ void m2s_key_kernel(int64_t n, const uint64_t *__restrict__ m, const uint32_t *__restrict__ t,
-                               const unsigned long long *__restrict__ cnt, unsigned long long seg, int fb,
-                               uint64_t *__restrict__ key) {
-  __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  ShardIn in;
-  in.load(s_pre, cnt, seg);
-  if (i >= n) return;
-  const unsigned long long p = in.pos((unsigned long long)i, seg);
-  key[i] = (m[p] << fb) | (uint64_t)t[p];
-}
-
-__global__ void m2s_key_unique_kernel(int64_t n, const uint64_t *__restrict__ key, int fb, uint32_t *__restrict__ flag) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t > n) return;
-  flag[t] = (t == n) ? 0u : ((t == 0 || (key[t - 1] >> fb) != (key[t] >> fb)) ? 1u : 0u);
-}
-
-// the first (lowest face) entry of every morton: the leaf, its face and barycentrics
-__device__ void leaf_out(uint64_t m, int64_t f, const float *__restrict__ fv, uint32_t level, uint32_t o,
-                         uint64_t *__restrict__ mout, int64_t *__restrict__ fout, float *__restrict__ bary);
-
-__global__ void m2s_key_leaves_kernel(int64_t n, const uint64_t *__restrict__ key, int fb,
-                                      const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
-                                      const float *__restrict__ fv, uint32_t level, uint64_t *__restrict__ mout,
-                                      int64_t *__restrict__ fout, float *__restrict__ bary) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t >= n || !flag[t]) return;
-  const uint32_t o = psum[t];
-  leaf_out(key[t] >> fb, (int64_t)(key[t] & ((1ull << fb) - 1)), fv, level, o, mout, fout, bary);
-}
-
-// (morton, face) pairs as 32-bit keys / values for levels with 3L <= 32: a radix sort over 3L key
-// bits moving 8 bytes per pair, against 3L + FB bits of 64-bit composite keys (cfg4 L = 9:
-// 27 against 45 bits).  The pairs' order among equal mortons is then arbitrary (appended through
-// sharded counters), so each leaf takes its run's least face -- the face the reference's stable
-// sort puts first (generation order is ascending face id, m2s_key_kernel's comment).
-__global__ void m2s_pair_kernel(int64_t n, const uint64_t *__restrict__ m, const uint32_t *__restrict__ t,
-                                const unsigned long long *__restrict__ cnt, unsigned long long seg,
-                                uint32_t *__restrict__ key, uint32_t *__restrict__ val) {
-  __shared__ unsigned long long s_pre[M2S_SHARDS + 1];
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  ShardIn in;
-  in.load(s_pre, cnt, seg);
-  if (i >= n) return;
-  const unsigned long long p = in.pos((unsigned long long)i, seg);
-  key[i] = (uint32_t)m[p];
-  val[i] = t[p];
-}
-
-__global__ void m2s_pair_unique_kernel(int64_t n, const uint32_t *__restrict__ key, uint32_t *__restrict__ flag) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t > n) return;
-  flag[t] = (t == n) ? 0u : ((t == 0 || key[t - 1] != key[t]) ? 1u : 0u);
-}
-
-// the runs' first positions, densely (leaf o's run starts at starts[o]): one thread per leaf in
-// the leaves kernel instead of one per pair with a quarter of the lanes busy (57 against ~15 us)
-__global__ void m2s_run_starts_kernel(int64_t n, const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
-                                      uint32_t *__restrict__ starts) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (t < n && flag[t]) starts[psum[t]] = (uint32_t)t;
-}
-
-__global__ void m2s_pair_leaves_kernel(int64_t n, int64_t nleaves, const uint32_t *__restrict__ key,
-                                       const uint32_t *__restrict__ val, const uint32_t *__restrict__ starts,
-                                       const float *__restrict__ fv, uint32_t level, uint64_t *__restrict__ mout,
-                                       int64_t *__restrict__ fout, float *__restrict__ bary) {
-  const int64_t o = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (o >= nleaves) return;
-  const int64_t t = starts[o];
-  const uint32_t k = key[t];
-  uint32_t f = val[t];
-  // the run's least face: 8 entries per round trip (clamped, unconditional loads; a run is a few
-  // pairs -- 4.5 per leaf at cfg4 -- and one entry per dependent load took 92 us there)
-  for (int64_t s = t + 1;; s += 8) {
-    uint32_t kk[8], vv[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int64_t i = s + u < n ? s + u : n - 1;
-      kk[u] = key[i];
-      vv[u] = val[i];
-    }
-    bool run = true;
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      run = run && s + u < n && kk[u] == k;
-      if (run) f = min(f, vv[u]);
-    }
-    if (!run) break;
-  }
-  leaf_out(k, (int64_t)f, fv, level, (uint32_t)o, mout, fout, bary);
-}
-
-// leaf o: its morton, face, and the face's barycentrics at the voxel centre (spc_math.h:229-258)
+// leaf o: its face and the face's barycentrics at the voxel centre (spc_math.h:229-258)
 __device__ __forceinline__ void leaf_bary(float cx, float cy, float cz, int64_t f, const float *__restrict__ fv,
                                           uint32_t o, int64_t *__restrict__ fout, float *__restrict__ bary) {
   fout[o] = f;
@@ -1339,98 +1038,13 @@ __device__ __forceinline__ void leaf_bary(float cx, float cy, float cz, int64_t 
   bary[o * 2 + 1] = by * sc;
 }
 
-__device__ void leaf_out(uint64_t m, int64_t f, const float *__restrict__ fv, uint32_t level, uint32_t o,
-                         uint64_t *__restrict__ mout, int64_t *__restrict__ fout, float *__restrict__ bary) {
-  mout[o] = m;
-  float cx, cy, cz, h;
-  voxel_center(m, level, cx, cy, cz, h);
-  leaf_bary(cx, cy, cz, f, fv, o, fout, bary);
-}
-
-// the same from the leaf's point (voxel_center's arithmetic), no morton output
+// the same from the leaf's point (voxel_center's arithmetic)
 __device__ void leaf_out_pt(int px, int py, int pz, int64_t f, const float *__restrict__ fv, uint32_t level,
                             uint32_t o, int64_t *__restrict__ fout, float *__restrict__ bary) {
   const float vs = 2.0f / (float)(1u << level);
   const float h = (float)(0.5 * vs);
   leaf_bary(fmaf((float)px, vs, h - 1.0f), fmaf((float)py, vs, h - 1.0f), fmaf((float)pz, vs, h - 1.0f), f, fv, o,
             fout, bary);
-}
-
-// Octree of sorted unique leaf mortons, all levels at once: row j (0..L-1) of `flag` marks
-// the first leaf under each level-j node (row stride n+1, a zero sentinel per row), so ONE
-// exclusive scan over the rows numbers the nodes level by level -- the octree's own order --
-// and each node's byte is the OR of its children's bits, gathered from their first leaves.
-__global__ void oct_flags_kernel(int64_t n, const uint64_t *__restrict__ m, uint32_t L, uint32_t *__restrict__ flag) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const uint32_t j = blockIdx.y;
-  if (t > n) return;
-  const int sh = 3 * (int)(L - j);
-  flag[(int64_t)j * (n + 1) + t] = (t == n) ? 0u : ((t == 0 || (m[t - 1] >> sh) != (m[t] >> sh)) ? 1u : 0u);
-}
-
-// first leaf of every node (the flagged (row, leaf) positions, numbered by the scan)
-__global__ void oct_first_kernel(int64_t n, const uint32_t *__restrict__ flag, const uint32_t *__restrict__ psum,
-                                 uint32_t *__restrict__ first) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t q = (int64_t)blockIdx.y * (n + 1) + t;
-  if (t < n && flag[q]) first[psum[q]] = (uint32_t)t;
-}
-
-// node p's byte: its children are the next level's nodes whose first leaves lie in p's leaf
-// range [first(p), first(p + 1) or n) -- numbered by the scan at those two positions -- or,
-// under the last level, the leaves themselves
-__global__ void oct_byte_kernel(int64_t n, const uint64_t *__restrict__ m, uint32_t L, uint32_t total,
-                                const uint32_t *__restrict__ psum, const uint32_t *__restrict__ first,
-                                uint8_t *__restrict__ out) {
-  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (p >= total) return;
-  uint32_t j = 0;
-  while (j + 1 < L && (int64_t)psum[(int64_t)(j + 1) * (n + 1)] <= p) j++;
-  const uint32_t lend = (j + 1 < L) ? psum[(int64_t)(j + 1) * (n + 1)] : total;  // level j's node end
-  const int64_t t0 = first[p];
-  const int64_t t1 = (p + 1 < (int64_t)lend) ? (int64_t)first[p + 1] : n;
-  const int sh = 3 * (int)(L - j - 1);
-  uint32_t code = 0;
-  if (j + 1 == L) {
-    for (int64_t t = t0; t < t1; t++) code |= 1u << (uint32_t)(m[t] & 7);
-  } else {
-    const int64_t r = (int64_t)(j + 1) * (n + 1);
-    const uint32_t c0 = psum[r + t0], c1 = psum[r + t1];
-    for (uint32_t c = c0; c < c1; c++) code |= 1u << (uint32_t)((m[first[c]] >> sh) & 7);
-  }
-  out[p] = (uint8_t)code;
-}
-
-static int morton_to_octree_rows(int64_t n, const uint64_t *morton, uint32_t L, Scratch &psc, uint8_t **octree,
-                                 int64_t *num_nodes, hipStream_t st) {
-  *octree = nullptr;
-  *num_nodes = 0;
-  if (L == 0 || n == 0) return morton_to_octree_impl(n, morton, L, psc, octree, num_nodes, st);
-  const int64_t len = (int64_t)L * (n + 1);
-  if (len + 1 >= ((int64_t)1 << 31)) return morton_to_octree_impl(n, morton, L, psc, octree, num_nodes, st);
-  // the temporaries (rows, scan, first leaves: at most len nodes) from one allocation
-  const size_t chunk = al256b((size_t)len * 4) + al256b((size_t)(len + 1) * 4) + al256b(scan_tmp_bytes(len - 1)) +
-                       al256b((size_t)len * 4);
-  Bump bump{&psc, (char *)psc.get(chunk), chunk};
-  Scratch sc{bump_alloc, &bump};
-  uint32_t *flag = (uint32_t *)sc.get((size_t)len * sizeof(uint32_t));
-  uint32_t *psum = (uint32_t *)sc.get((size_t)(len + 1) * sizeof(uint32_t));
-  if (!flag || !psum) return KL_E_ALLOC;
-  hipLaunchKernelGGL(oct_flags_kernel, dim3((unsigned)cdiv(n + 1, 256), L), dim3(256), 0, st, n, morton, L, flag);
-  KL_CHECK_LAUNCH();
-  uint32_t total = 0;
-  KL_CHECK_RC(exclusive_scan(flag, psum, len - 1, sc, st, &total));  // psum[len - 1] = nodes (last sentinel 0)
-  uint32_t *first = (uint32_t *)sc.get((size_t)total * sizeof(uint32_t));
-  uint8_t *out = (uint8_t *)psc.get((size_t)total);  // the caller's output
-  if (!first || !out) return KL_E_ALLOC;
-  hipLaunchKernelGGL(oct_first_kernel, dim3((unsigned)cdiv(n, 256), L), dim3(256), 0, st, n, flag, psum, first);
-  KL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(oct_byte_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0, st, n, morton, L, total, psum,
-                     first, out);
-  KL_CHECK_LAUNCH();
-  *octree = out;
-  *num_nodes = total;
-  return KL_OK;
 }
 
 // The node-rank path's workspace: pair buffers of 96 pairs per face per level (cfg4: 1.18 M of
@@ -1589,152 +1203,6 @@ __global__ void m2s_fixed_final_kernel(const M2sCtl *__restrict__ ctl, uint32_t 
     const uint64_t q = Mp[jp] * 2 + m2s_child_off(c);
     leaf_out_pt((int)(q & 0xffff), (int)((q >> 16) & 0xffff), (int)(q >> 32), (int64_t)fmin8[s], fv, L, o, fout, bary);
   }
-}
-
-// returns KL_OK, an error, or 1 = not taken (capacity / key width): the caller runs the
-// per-level path
-static int mesh_to_spc_async(int64_t F, const float *fv, uint32_t L, Scratch &sc, uint8_t **octree,
-                             int64_t *num_nodes, int64_t **face_idx, float **bary, int64_t *num_leaves,
-                             hipStream_t st) {
-  int fb = 1;
-  while (fb < 32 && ((int64_t)1 << fb) < F) fb++;
-  if (F <= 0 || F >= ((int64_t)1 << 31) || 3 * (int)L + fb > 64 || L == 0) return 1;
-  // capacity per level buffer: 96 proposals per face (cfg4: 9.4 M of 19.2 M at L = 9), in shards
-  const unsigned long long cap = (unsigned long long)std::max<int64_t>(F * 96, (int64_t)1 << 20);
-  if (cap >= (1ull << 31)) return 1;
-  // counts[l][shard] for l = 0 .. L+1 (proposals per level, then the final pairs), overflow flag
-  const int NC = (SPC_MAX_LEVELS + 2) * M2S_SHARDS;
-  const size_t cbytes = sizeof(unsigned long long) * (NC + 1);
-  // the level buffers and the counters from one allocation
-  const size_t chunk = 2 * (al256b((size_t)cap * 8) + al256b((size_t)cap * 4)) + al256b(cbytes);
-  Bump bump0{&sc, (char *)sc.get(chunk), chunk};
-  Scratch sc0{bump_alloc, &bump0};
-  uint64_t *mb[2];
-  uint32_t *tb[2];
-  for (int k = 0; k < 2; k++) {
-    mb[k] = (uint64_t *)sc0.get((size_t)cap * sizeof(uint64_t));
-    tb[k] = (uint32_t *)sc0.get((size_t)cap * sizeof(uint32_t));
-    if (!mb[k] || !tb[k]) return KL_E_ALLOC;
-  }
-  unsigned long long *counts = (unsigned long long *)sc0.get(cbytes);
-  if (!counts) return KL_E_ALLOC;
-  int *overflow = (int *)(counts + NC);
-  const unsigned long long seg = cap / M2S_SHARDS;
-  KL_CHECK_RC(fill_async(counts, 0, cbytes, st));
-  hipLaunchKernelGGL(m2s_init_kernel, dim3((unsigned)cdiv(F, 256)), dim3(256), 0, st, F, mb[0], tb[0], counts);
-  KL_CHECK_LAUNCH();
-  // one round of workgroups, each a span of at most M2S_MAX_CHUNKS chunks of 256 proposals
-  const unsigned grid = (unsigned)std::max<int64_t>(M2S_GRID, cdiv((int64_t)cap, 256 * M2S_MAX_CHUNKS));
-  // level 0 tests the root against every face; each later level decides the children of the
-  // previous level's passing pairs (m2s_children_kernel; dev param 14 = 1: every level tests
-  // its 8-children proposals one by one, m2s_level_kernel, for A/B)
-  const bool by_parent = g_dev_param[14] != 1;
-  for (uint32_t l = 0; l <= L; l++) {
-    const int a = l & 1;
-    if (by_parent && l > 0)
-      hipLaunchKernelGGL(m2s_children_kernel, dim3(grid), dim3(256), 0, st, fv, mb[a], tb[a],
-                         counts + l * M2S_SHARDS, mb[a ^ 1], tb[a ^ 1], counts + (l + 1) * M2S_SHARDS, seg, overflow,
-                         l);
-    else
-      hipLaunchKernelGGL(m2s_level_kernel, dim3(grid), dim3(256), 0, st, fv, mb[a], tb[a], counts + l * M2S_SHARDS,
-                         mb[a ^ 1], tb[a ^ 1], counts + (l + 1) * M2S_SHARDS, seg, overflow, l,
-                         by_parent ? 0u : L - l);
-    KL_CHECK_LAUNCH();
-  }
-  std::vector<unsigned long long> hv(NC + 1);
-  unsigned long long *h = hv.data();
-  int rc = host_read(h, counts, cbytes, st);
-  const bool over = rc == KL_OK && *(int *)(h + NC) != 0;
-  auto level_total = [&](uint32_t l) {
-    unsigned long long t = 0;
-    for (int g = 0; g < M2S_SHARDS; g++) t += h[l * M2S_SHARDS + g];
-    return (int64_t)t;
-  };
-  const int64_t cnt = rc == KL_OK ? level_total(L + 1) : 0;
-  if (rc == KL_OK && !over) {  // proposals per level: the faces, then 8 per passing pair
-    for (uint32_t l = 0; l <= L; l++) t_m2s_counts[l] = (by_parent && l > 0 ? 8 : 1) * level_total(l);
-    t_m2s_levels = (int)L + 1;
-  }
-  if (rc) return rc;
-  if (over) return 1;
-  if (cnt == 0) return KL_OK;  // empty: (0,) u8, (0,) i64, (0,3) f32 built by the caller
-  const uint32_t *fin_t = tb[(L + 1) & 1];
-  const uint64_t *fin_m = mb[(L + 1) & 1];
-  if (3 * L <= 32 && g_dev_param[15] != 1) {  // 32-bit pairs (dev param 15 = 1: the 64-bit keys, A/B)
-    size_t tbytes = 0;
-    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tbytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                    (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)cnt, 0,
-                                                    (int)(3 * L), st));
-    // this phase's temporaries (mortons of the leaves: at most cnt) from one allocation
-    const size_t chunk = 4 * al256b((size_t)cnt * 4) + al256b(tbytes) + al256b((cnt + 1) * 4) + al256b((cnt + 2) * 4) +
-                         al256b(scan_tmp_bytes(cnt)) + al256b((size_t)cnt * 8);
-    Bump bump{&sc, (char *)sc.get(chunk), chunk};
-    Scratch bsc{bump_alloc, &bump};
-    uint32_t *key = (uint32_t *)bsc.get((size_t)cnt * 4), *val = (uint32_t *)bsc.get((size_t)cnt * 4);
-    uint32_t *ks = (uint32_t *)bsc.get((size_t)cnt * 4), *vs = (uint32_t *)bsc.get((size_t)cnt * 4);
-    if (!key || !val || !ks || !vs) return KL_E_ALLOC;
-    hipLaunchKernelGGL(m2s_pair_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, fin_m, fin_t,
-                       counts + (L + 1) * M2S_SHARDS, seg, key, val);
-    KL_CHECK_LAUNCH();
-    void *tmp = bsc.get(tbytes);
-    if (!tmp) return KL_E_ALLOC;
-    KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tbytes, key, ks, val, vs, (int)cnt, 0, (int)(3 * L), st));
-    uint32_t *flag = (uint32_t *)bsc.get((cnt + 1) * sizeof(uint32_t));
-    uint32_t *psum = (uint32_t *)bsc.get((cnt + 2) * sizeof(uint32_t));
-    if (!flag || !psum) return KL_E_ALLOC;
-    hipLaunchKernelGGL(m2s_pair_unique_kernel, dim3((unsigned)cdiv(cnt + 1, 256)), dim3(256), 0, st, cnt, ks, flag);
-    KL_CHECK_LAUNCH();
-    uint32_t uniq = 0;
-    KL_CHECK_RC(exclusive_scan(flag, psum, cnt, bsc, st, &uniq));
-    uint64_t *mu = (uint64_t *)bsc.get((size_t)uniq * sizeof(uint64_t));
-    uint32_t *starts = key;  // free since the sort
-    int64_t *fu = (int64_t *)sc.get((size_t)uniq * sizeof(int64_t));
-    float *bu = (float *)sc.get((size_t)uniq * 2 * sizeof(float));
-    if (!mu || !fu || !bu) return KL_E_ALLOC;
-    hipLaunchKernelGGL(m2s_run_starts_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, flag, psum,
-                       starts);
-    KL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(m2s_pair_leaves_kernel, dim3((unsigned)cdiv(uniq, 256)), dim3(256), 0, st, cnt, (int64_t)uniq,
-                       ks, vs, starts, fv, L, mu, fu, bu);
-    KL_CHECK_LAUNCH();
-    KL_CHECK_RC(morton_to_octree_rows(uniq, mu, L, sc, octree, num_nodes, st));
-    *face_idx = fu;
-    *bary = bu;
-    *num_leaves = uniq;
-    return KL_OK;
-  }
-  // keys into the free buffer pair's morton array, sorted into the other pair's
-  uint64_t *key = mb[L & 1];
-  hipLaunchKernelGGL(m2s_key_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, fin_m, fin_t,
-                     counts + (L + 1) * M2S_SHARDS, seg, fb, key);
-  KL_CHECK_LAUNCH();
-  uint64_t *ks = (uint64_t *)sc.get((size_t)cnt * sizeof(uint64_t));
-  if (!ks) return KL_E_ALLOC;
-  size_t tbytes = 0;
-  const int end_bit = 3 * (int)L + fb;
-  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortKeys(nullptr, tbytes, key, ks, (int)cnt, 0, end_bit, st));
-  void *tmp = sc.get(tbytes);
-  if (!tmp) return KL_E_ALLOC;
-  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortKeys(tmp, tbytes, key, ks, (int)cnt, 0, end_bit, st));
-  uint32_t *flag = (uint32_t *)sc.get((cnt + 1) * sizeof(uint32_t));
-  uint32_t *psum = (uint32_t *)sc.get((cnt + 2) * sizeof(uint32_t));
-  if (!flag || !psum) return KL_E_ALLOC;
-  hipLaunchKernelGGL(m2s_key_unique_kernel, dim3((unsigned)cdiv(cnt + 1, 256)), dim3(256), 0, st, cnt, ks, fb, flag);
-  KL_CHECK_LAUNCH();
-  uint32_t uniq = 0;
-  KL_CHECK_RC(exclusive_scan(flag, psum, cnt, sc, st, &uniq));
-  uint64_t *mu = (uint64_t *)sc.get((size_t)uniq * sizeof(uint64_t));
-  int64_t *fu = (int64_t *)sc.get((size_t)uniq * sizeof(int64_t));
-  float *bu = (float *)sc.get((size_t)uniq * 2 * sizeof(float));
-  if (!mu || !fu || !bu) return KL_E_ALLOC;
-  hipLaunchKernelGGL(m2s_key_leaves_kernel, dim3((unsigned)cdiv(cnt, 256)), dim3(256), 0, st, cnt, ks, fb, flag, psum,
-                     fv, L, mu, fu, bu);
-  KL_CHECK_LAUNCH();
-  KL_CHECK_RC(morton_to_octree_rows(uniq, mu, L, sc, octree, num_nodes, st));
-  *face_idx = fu;
-  *bary = bu;
-  *num_leaves = uniq;
-  return KL_OK;
 }
 
 // ------------------------------------------------------------------ scan_octrees
@@ -2070,12 +1538,8 @@ extern "C" int kl_mesh_to_spc(int64_t num_faces, const float *fv, uint32_t level
   KL_REQUIRE(alloc != nullptr, "mesh_to_spc: allocator required");
   Scratch sc{alloc, ctx};
   if (!(g_dev_flags & (1 << 10))) {  // dev bit 10: the per-level path
-    // dev param 14 >= 1: the sorted-pairs path (A/B)
-    const int rc = g_dev_param[14] >= 1
-                       ? mesh_to_spc_async(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves,
-                                           S(stream))
-                       : mesh_to_spc_nodes(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves,
-                                           S(stream));
+    const int rc = mesh_to_spc_nodes(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves,
+                                     S(stream));
     if (rc != 1) return rc;
   }
   return mesh_to_spc_impl(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves, S(stream));
