@@ -65,8 +65,9 @@ int kl_stream_is_capturing(kl_stream stream);
 
 /* Training-loop helper, not a reference op (bench.py's loss):
  *   out[0] = <a, ga> + <b, gb>   (fp32 inputs, fp64 accumulation, deterministic order).
- * ws: kl_loss_dot2_workspace_bytes() bytes of scratch (no initialisation needed).
- * Two launches (per-block partials, then their ordered sum). */
+ * ws: kl_loss_dot2_workspace_bytes() bytes, zeroed before the first call (each call leaves it
+ * zeroed); one ws per stream in flight.  One launch (per-block partials, the last block adds them
+ * in block order). */
 size_t kl_loss_dot2_workspace_bytes(void);
 int kl_loss_dot2(const float *a, const float *ga, int64_t na, const float *b, const float *gb, int64_t nb, void *ws,
                  float *out, kl_stream stream);

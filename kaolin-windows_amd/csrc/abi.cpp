@@ -157,13 +157,17 @@ extern "C" int kl_stream_is_capturing(kl_stream stream) {
 extern "C" int kl_abi_version(void) { return KL_ABI_VERSION; }
 
 // ---- Training-loop helper (not a reference op): L = <a, ga> + <b, gb>.
-// A loss of this shape is what bench.py's step computes; two torch.dot calls plus their
-// add cost four launches.  dot2_partial_kernel folds float4 strips of both pairs in
-// double, one partial per block; dot2_final_kernel (one block) adds the partials in block
-// order: deterministic, and the kernel boundary orders the partials (a last-block ticket
-// needs a device-scope release per block, which measured 29 us here).
+// A loss of this shape is what bench.py's step computes; two torch.dot calls plus their add cost
+// four launches.  ONE launch: each workgroup folds float4 strips of both pairs in double and
+// publishes its partial; the workgroup whose ticket comes last adds the partials in block order
+// (deterministic) and resets the ticket.  The hand-off is MI355X_MICROARCH.md's first measured
+// `sc1` row: one lane per workgroup stores its 8-B partial `sc1` (a relaxed agent-scope atomic
+// store), waits vmcnt(0), then adds to ONE agent-scope counter; the last adder's workgroup loads
+// the partials `sc1` behind a workgroup barrier -- no release / acquire fences (a device-scope
+// release per block measured 29 us here in r03, hence the old second launch).  One workgroup per
+// CU, as that row was measured.
 namespace kl {
-constexpr int DOT2_BLOCKS = 2048;
+constexpr int DOT2_BLOCKS = 256;
 
 __device__ __forceinline__ double dot_strip(const float *__restrict__ a, const float *__restrict__ g, size_t n,
                                             size_t t, size_t nt) {
@@ -178,34 +182,48 @@ __device__ __forceinline__ double dot_strip(const float *__restrict__ a, const f
   return s;
 }
 
-__device__ __forceinline__ double block_sum256(double s, double *red) {
+constexpr int DOT2_THREADS = 1024;  // 16 waves: the loads in flight of one workgroup per CU
+
+__device__ __forceinline__ double block_sum(double s, double *red) {
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  return (red[0] + red[1]) + (red[2] + red[3]);
+  double r = 0.0;
+#pragma unroll
+  for (int w = 0; w < DOT2_THREADS / 64; w++) r += red[w];
+  __syncthreads();  // red is reused by the last workgroup's second sum
+  return r;
 }
 
-__global__ void __launch_bounds__(256) dot2_partial_kernel(const float *__restrict__ a, const float *__restrict__ ga,
-                                                           size_t na, const float *__restrict__ b,
-                                                           const float *__restrict__ gb, size_t nb,
-                                                           double *__restrict__ partial) {
-  __shared__ double red[4];
+__global__ void __launch_bounds__(DOT2_THREADS) dot2_kernel(const float *__restrict__ a, const float *__restrict__ ga, size_t na,
+                                                   const float *__restrict__ b, const float *__restrict__ gb,
+                                                   size_t nb, double *__restrict__ partial,
+                                                   unsigned int *__restrict__ ticket, float *__restrict__ out) {
+  __shared__ double red[DOT2_THREADS / 64];
+  __shared__ int s_last;
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x, nt = (size_t)gridDim.x * blockDim.x;
-  const double s = block_sum256(dot_strip(a, ga, na, t, nt) + dot_strip(b, gb, nb, t, nt), red);
-  if (threadIdx.x == 0) partial[blockIdx.x] = s;
-}
-
-__global__ void __launch_bounds__(256) dot2_final_kernel(const double *__restrict__ partial, int n,
-                                                         float *__restrict__ out) {
-  __shared__ double red[4];
+  const double s = block_sum(dot_strip(a, ga, na, t, nt) + dot_strip(b, gb, nb, t, nt), red);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(partial + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
   double v = 0.0;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) v += partial[i];
-  v = block_sum256(v, red);
-  if (threadIdx.x == 0) out[0] = (float)v;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
+    v += __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v = block_sum(v, red);
+  if (threadIdx.x == 0) {
+    out[0] = (float)v;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next call
+  }
 }
 }  // namespace kl
 
-extern "C" size_t kl_loss_dot2_workspace_bytes(void) { return kl::DOT2_BLOCKS * sizeof(double); }
+// workspace: the partials, then the ticket (zero before the first call; every call leaves it zero)
+extern "C" size_t kl_loss_dot2_workspace_bytes(void) { return kl::DOT2_BLOCKS * sizeof(double) + 256; }
 
 extern "C" int kl_loss_dot2(const float *a, const float *ga, int64_t na, const float *b, const float *gb, int64_t nb,
                             void *ws, float *out, kl_stream stream) {
@@ -214,12 +232,11 @@ extern "C" int kl_loss_dot2(const float *a, const float *ga, int64_t na, const f
     return KL_E_INVALID;
   }
   double *partial = (double *)ws;
+  unsigned int *ticket = (unsigned int *)(partial + kl::DOT2_BLOCKS);
   const int64_t vec = (na + nb) / 4;
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kl::DOT2_BLOCKS, (vec + 511) / 512));
-  hipLaunchKernelGGL(kl::dot2_partial_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a, ga, (size_t)na, b,
-                     gb, (size_t)nb, partial);
-  KL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(kl::dot2_final_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partial, blocks, out);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(kl::DOT2_BLOCKS, (vec + 2047) / 2048));
+  hipLaunchKernelGGL(kl::dot2_kernel, dim3(blocks), dim3(kl::DOT2_THREADS), 0, (hipStream_t)stream, a, ga, (size_t)na, b, gb,
+                     (size_t)nb, partial, ticket, out);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

@@ -1422,12 +1422,15 @@ def test_loss_dot2(kal, na, nb):
     a, ga, b, gb = (torch.rand(n, generator=g).to(DEV) for n in (na, na, nb, nb))
     ws = torch.zeros(_native.lib().kl_loss_dot2_workspace_bytes(), dtype=torch.uint8, device=DEV)
     ref = float(a.double() @ ga.double() + b.double() @ gb.double())
-    for _ in range(3):
+    seen = set()
+    for _ in range(3):  # deterministic: the last workgroup adds the partials in block order
         out = torch.full((1,), float('nan'), device=DEV)
         _native.check(_native.lib().kl_loss_dot2(_native.ptr(a), _native.ptr(ga), na, _native.ptr(b), _native.ptr(gb),
                                                  nb, _native.ptr(ws), _native.ptr(out), _native.stream_of(a.device)),
                       'kl_loss_dot2')
         assert abs(float(out) - ref) <= 1e-6 * max(1.0, abs(ref))
+        seen.add(float(out))
+    assert len(seen) == 1
 
 
 # ---------------------------------------------------------------- packed ray ops (§8f rank 1)
