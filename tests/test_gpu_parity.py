@@ -1193,6 +1193,22 @@ def test_mesh_to_spc_empty(kal):
     assert octree.shape == (0,) and fidx.shape == (0,) and tuple(bary.shape) == (0, 3)
 
 
+@pytest.mark.parametrize('level', [10, 12, 14])
+def test_mesh_to_spc_deep_levels_vs_oracle(kal, level):
+    """Deep levels (nodes kept as packed 16-bit points up to 2^14 - 1; keys past the 32 bits the
+    old sorted-pairs path needed): small random triangles, octree / face_idx / bary vs the oracle,
+    and the fixed-capacity form equal to it."""
+    rng = np.random.RandomState(level)
+    c = rng.uniform(-0.9, 0.9, (24, 1, 3))
+    fv = (c + rng.normal(0, 2.0 ** -(level - 5), (24, 3, 3))).astype(np.float32)
+    octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(T(fv), level)
+    oo, of, ob = orc.mesh_to_spc(fv, level)
+    assert np.array_equal(A(octree), oo)
+    assert np.array_equal(A(fidx), of)
+    np.testing.assert_array_equal(A(bary), ob)
+    assert _m2s_fixed_check(kal, T(fv), level, octree.shape[0], fidx.shape[0]) == 0
+
+
 def _m2s_fixed_check(kal, fv, level, ncap, lcap):
     """unbatched_mesh_to_spc(..., capacity) against the eager call: the written prefix bit-equal,
     padding (0, -1, 0) after it, or status 1 with the sizes needed and nothing written."""
@@ -1531,3 +1547,4 @@ def test_rayops_error_messages(kal):
     with pytest.raises(RuntimeError, match=r"argument #1 'feats' to be one of Half, Float, Double"):
         C.cumprod_cuda(torch.zeros(4, 2, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32,
                                                                                       device=DEV), False, False)
+
