@@ -998,9 +998,15 @@ __global__ void __launch_bounds__(256) rasterize_bwd_kernel(
 // ---------------------------------------------------------------- gather backward
 // One thread per face visits exactly the pixel range the forward visited for it (the
 // same in-kernel bbox and exact_axis), so every pixel the face can have won is seen;
-// pixels are taken 8 at a time with their face_idx / weights / grads loads in flight
-// together.  Faces whose range exceeds VIS_SMALL_AREA go to a workgroup per face.
-constexpr int GATHER_BATCH = 4;
+// pixels are taken GATHER_BATCH at a time with their face_idx / weights / grads loads in
+// flight together.  Faces whose range exceeds VIS_SMALL_AREA go to a workgroup per face.
+// GATHER_BATCH (gather2, r04aw A/B of builds, dibr_backward at cfg3): 1: 74.4, 2: 72.0, 3: 71.1,
+// 4: 75.0, 6: 76.5, 8: 77.5 us -- fewer registers per batch slot (93 VGPRs at 2 against 102 at 4)
+// buys occupancy that hides more than the deeper batch does.
+#ifndef KL_GATHER_BATCH  // A/B builds only
+#define KL_GATHER_BATCH 3
+#endif
+constexpr int GATHER_BATCH = KL_GATHER_BATCH;
 
 template <typename T>
 __device__ __forceinline__ bool face_range(const RastSrc<T> &src, int64_t tf, float m, int H, int W, int &ix0,
