@@ -382,6 +382,15 @@ int kl_sided_distance_backward(kl_dtype dtype, int batch, int64_t n, int64_t m,
                                const void *grad_dist, const void *p1, const void *p2,
                                const int64_t *idx, void *grad_p1, void *grad_p2, kl_stream stream);
 
+/* sided_distance.cpp:91-122 with grad_p2 formed deterministically (float32 / float64 only):
+ * grad_p1 (B,N,3) written; grad_p2's per-point float terms (sided_distance_cuda.cu's atomicAdd
+ * operands) summed per coordinate in double into g2_sums (B,M,3) (zeroed here first), and, when
+ * g2 != NULL, rounded once into g2 (B,M,3).  A caller that shards p1 all-reduces g2_sums and rounds
+ * once (kaolin.distributed.sharded_sided_distance): the unsharded gradient bit for bit. */
+int kl_sided_distance_backward_sums(kl_dtype dtype, int batch, int64_t n, int64_t m, const void *grad,
+                                    const void *p1, const void *p2, const int64_t *idx, void *g1,
+                                    double *g2_sums, void *g2, kl_stream stream);
+
 /* ------------------------------------------------------------------ SPC */
 
 /* mesh_to_spc.cpp:28-44 (mesh_to_spc_cuda_impl, mesh_to_spc_cuda.cu:309-463).

@@ -12,6 +12,7 @@ void set_error(const std::string &msg) { g_last_error = msg; }
 int g_dev_flags = 0;
 void *g_dev_debug = nullptr;
 int g_dev_param[16] = {};
+int g_dev_stat[4] = {};
 }  // namespace kl
 
 // Development hook (not part of include/kaolin_hip.h): bit flags that switch parts of
@@ -26,6 +27,9 @@ extern "C" void kl_dev_set_debug(void *buf) { kl::g_dev_debug = buf; }
 extern "C" void kl_dev_set_param(int idx, int value) {
   if (idx >= 0 && idx < 16) kl::g_dev_param[idx] = value;
 }
+// Development hook: what the last call took (tests assert a fallback branch ran).
+// 0: mesh_to_spc -- 0 the node-rank path, 1 its per-level fallback (the pair buffers overflowed).
+extern "C" int kl_dev_get_stat(int idx) { return idx >= 0 && idx < 4 ? kl::g_dev_stat[idx] : 0; }
 
 namespace kl {
 // Byte fill as an ordinary kernel: 16-byte stores over the aligned body, bytes at the

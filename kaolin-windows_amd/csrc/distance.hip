@@ -1035,6 +1035,47 @@ static int sided_fwd(int B, int64_t N, int64_t M, const void *p1, const void *p2
   return KL_OK;
 }
 
+// The double-sum form (f32 / f64): grad_p2's terms -- the same float products as sided_bwd_kernel's
+// -- added per coordinate in double and rounded once (acc_finalize), so the result does not
+// depend on the order of the atomics (exact whenever the terms' magnitudes span < ~2^29) and a
+// points-sharded caller (kaolin.distributed.sharded_sided_distance) can all-reduce the sums and
+// round once to get the unsharded gradient bit for bit.
+template <typename S>
+__global__ void __launch_bounds__(256) sided_bwd_sums_kernel(const S *__restrict__ grad, const S *__restrict__ p1,
+                                                              const S *__restrict__ p2,
+                                                              const int64_t *__restrict__ idx, int64_t N, int64_t M,
+                                                              S *__restrict__ g1, double *__restrict__ sums) {
+  const int b = blockIdx.y;
+  const int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int64_t mi = (int64_t)b * N + n;
+  const S x1 = p1[mi * 3], y1 = p1[mi * 3 + 1], z1 = p1[mi * 3 + 2];
+  const int64_t j = (idx[mi] + (int64_t)b * M) * 3;
+  const S x2 = p2[j], y2 = p2[j + 1], z2 = p2[j + 2];
+  const S g = grad[mi];
+  const S two = S(2);
+  g1[mi * 3 + 0] = two * (x1 - x2) * g;
+  g1[mi * 3 + 1] = two * (y1 - y2) * g;
+  g1[mi * 3 + 2] = two * (z1 - z2) * g;
+  atomicAdd(sums + j + 0, (double)(two * (x2 - x1) * g));
+  atomicAdd(sums + j + 1, (double)(two * (y2 - y1) * g));
+  atomicAdd(sums + j + 2, (double)(two * (z2 - z1) * g));
+}
+
+template <typename S>
+static int sided_bwd_sums(int B, int64_t N, int64_t M, const void *grad, const void *p1, const void *p2,
+                          const int64_t *idx, void *g1, double *sums, void *g2, hipStream_t st) {
+  const size_t n2 = (size_t)B * M * 3;
+  KL_REQUIRE(sums != nullptr || n2 == 0, "sided_distance_backward: the double sums buffer is missing");
+  KL_CHECK_RC(fill_async(sums, 0, sizeof(double) * n2, st));
+  if (B > 0 && N > 0) {
+    hipLaunchKernelGGL(sided_bwd_sums_kernel<S>, dim3((unsigned)cdiv(N, 256), B), dim3(256), 0, st, (const S *)grad,
+                       (const S *)p1, (const S *)p2, idx, N, M, (S *)g1, sums);
+    KL_CHECK_LAUNCH();
+  }
+  return g2 ? acc_finalize<S>(sums, (S *)g2, n2, false, st) : KL_OK;
+}
+
 template <typename S>
 static int sided_bwd(int B, int64_t N, int64_t M, const void *grad, const void *p1, const void *p2,
                      const int64_t *idx, void *g1, void *g2, hipStream_t st) {
@@ -1112,5 +1153,14 @@ extern "C" int kl_sided_distance_backward(kl_dtype dtype, int batch, int64_t n, 
                                           kl_stream stream) {
   KL_DISPATCH_NUM(dtype, sided_bwd, batch, n, m, grad, p1, p2, idx, g1, g2, S(stream));
   set_error("sided_distance_backward_cuda not implemented for this dtype");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_sided_distance_backward_sums(kl_dtype dtype, int batch, int64_t n, int64_t m, const void *grad,
+                                               const void *p1, const void *p2, const int64_t *idx, void *g1,
+                                               double *g2_sums, void *g2, kl_stream stream) {
+  if (dtype == KL_F32) return sided_bwd_sums<float>(batch, n, m, grad, p1, p2, idx, g1, g2_sums, g2, S(stream));
+  if (dtype == KL_F64) return sided_bwd_sums<double>(batch, n, m, grad, p1, p2, idx, g1, g2_sums, g2, S(stream));
+  set_error("sided_distance_backward_cuda (double sums) not implemented for this dtype");
   return KL_E_INVALID;
 }

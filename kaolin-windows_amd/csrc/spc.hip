@@ -689,6 +689,10 @@ struct M2sCtl {
   uint32_t U[SPC_MAX_LEVELS + 2];       // nodes per level
   uint32_t O[SPC_MAX_LEVELS + 2];       // the level's first byte in the octree arena
   uint32_t ticket[SPC_MAX_LEVELS + 2];  // tile tickets of the level's scan
+  // 0, or the launch sequence number (m2s_seq_*) of the first launch that overflowed a buffer.  A
+  // launch stops at its start only on an overflow of an EARLIER launch (seq < its own): that test
+  // is the same for all its workgroups, however late they start.  (Stopping on any overflow let a
+  // late scan workgroup return without publishing its tile while the tiles after it waited for it.)
   int overflow;
   uint32_t zero;
   uint32_t root_S[2];  // the level above the root: one node whose child 0 is the root
@@ -696,6 +700,16 @@ struct M2sCtl {
 };
 
 constexpr int M2S_TILE = 1024;  // nodes per scan tile (256 threads x 4)
+
+// launch sequence of the node-rank path: root 1, then per level l the node kernel (2 l) and the scan
+// of level l - 1's row (2 l + 1)
+constexpr int M2S_SEQ_ROOT = 1;
+__host__ __device__ constexpr int m2s_seq_node(uint32_t level) { return 2 * (int)level; }
+__host__ __device__ constexpr int m2s_seq_rank(uint32_t l) { return 2 * (int)l + 3; }
+__device__ __forceinline__ bool m2s_dead(const M2sCtl *ctl, int seq) {
+  const int ov = *(const volatile int *)&ctl->overflow;
+  return ov != 0 && ov < seq;
+}
 
 __device__ void leaf_out_pt(int px, int py, int pz, int64_t f, const float *__restrict__ fv, uint32_t level,
                             uint32_t o, int64_t *__restrict__ fout, float *__restrict__ bary);
@@ -738,7 +752,7 @@ __global__ void __launch_bounds__(256) m2s_root_kernel(int64_t F, const float *_
   __syncthreads();
   if (total == 0) return;
   if (s_base + (unsigned long long)total > seg) {
-    if (threadIdx.x == 0) ctl->overflow = 1;
+    if (threadIdx.x == 0) ctl->overflow = M2S_SEQ_ROOT;
     return;
   }
   if (pass) {
@@ -777,7 +791,7 @@ __global__ void __launch_bounds__(256) m2s_node_kernel(const float *__restrict__
   // After an overflow the shards hold unwritten holes below their clamped counts (the overflowing
   // workgroups reserved past seg and wrote nothing): the levels after it must not read them (their
   // face ids would index fv out of bounds).  The host then runs the per-level path.
-  if (*(volatile int *)&ctl->overflow) return;
+  if (m2s_dead(ctl, m2s_seq_node(level))) return;
   ShardIn in;
   in.load(s_pre, ctl->counts + (level - 1) * M2S_SHARDS, seg);
   const unsigned long long n = in.total();
@@ -790,7 +804,7 @@ __global__ void __launch_bounds__(256) m2s_node_kernel(const float *__restrict__
   if (lo >= hi) return;
   const int nch = (int)((hi - lo + blockDim.x - 1) / blockDim.x);
   if (nch > M2S_MAX_CHUNKS) {
-    if (threadIdx.x == 0) ctl->overflow = 1;
+    if (threadIdx.x == 0) ctl->overflow = m2s_seq_node(level);
     return;
   }
   const uint8_t *octpp = octpp_base + *opp;
@@ -831,7 +845,7 @@ __global__ void __launch_bounds__(256) m2s_node_kernel(const float *__restrict__
   unsigned long long o0 = s_base;
   if (total == 0) return;
   if (o0 + (unsigned long long)total > seg) {
-    if (threadIdx.x == 0) ctl->overflow = 1;
+    if (threadIdx.x == 0) ctl->overflow = m2s_seq_node(level);
     return;
   }
   o0 += (unsigned long long)g * seg;
@@ -873,7 +887,7 @@ __global__ void __launch_bounds__(256) m2s_rank_kernel(M2sCtl *__restrict__ ctl,
                                                        uint32_t fmin_cap) {
   __shared__ int s_wave[4];
   __shared__ uint32_t s_tile, s_prefix;
-  if (*(volatile int *)&ctl->overflow) return;
+  if (m2s_dead(ctl, m2s_seq_rank(l))) return;  // the same answer for every workgroup (M2sCtl)
   const uint32_t n = ctl->U[l], O = ctl->O[l], On = O + n;
   const uint32_t ntiles = (n + M2S_TILE - 1) / M2S_TILE;
   const bool has_next = l + 1 < L, init_fmin = l + 2 == L, init_flags = l + 2 < L, last = l + 1 == L;
@@ -978,13 +992,13 @@ __global__ void __launch_bounds__(256) m2s_rank_kernel(M2sCtl *__restrict__ ctl,
         s += (uint32_t)__popc(b[q]);
       }
     }
-    if (over) ctl->overflow = 1;
+    if (over) ctl->overflow = m2s_seq_rank(l);
     if (t + 1 == ntiles && threadIdx.x == 0) {
       const uint32_t total = s_prefix + (uint32_t)agg;
       Sl[n] = total;
       ctl->U[l + 1] = total;
       ctl->O[l + 1] = On;
-      if (total > ncap || (has_next && On + total > oct_cap)) ctl->overflow = 1;
+      if (total > ncap || (has_next && On + total > oct_cap)) ctl->overflow = m2s_seq_rank(l);
     }
     if (ntiles <= gridDim.x) break;
     __syncthreads();  // s_prefix and s_tile are rewritten for the next tile
@@ -1063,6 +1077,8 @@ struct M2sNodes {
   unsigned long long *status = nullptr;
   bool plan(int64_t F) {
     cap = (unsigned long long)std::max<int64_t>(F * 96, (int64_t)1 << 20);
+    // dev param 14: the pair capacity itself (tests force the overflow branch with a small one)
+    if (g_dev_param[14] > 0) cap = (unsigned long long)std::max(g_dev_param[14], 64 * M2S_SHARDS);
     if (F >= ((int64_t)1 << 31) || cap >= (1ull << 31)) return false;
     seg = cap / M2S_SHARDS;
     ncap = (uint32_t)(cap / 4);
@@ -1537,10 +1553,14 @@ extern "C" int kl_mesh_to_spc(int64_t num_faces, const float *fv, uint32_t level
   KL_REQUIRE(level < (uint32_t)SPC_MAX_LEVELS, "mesh_to_spc: level must be < 15");
   KL_REQUIRE(alloc != nullptr, "mesh_to_spc: allocator required");
   Scratch sc{alloc, ctx};
+  g_dev_stat[0] = 1;
   if (!(g_dev_flags & (1 << 10))) {  // dev bit 10: the per-level path
     const int rc = mesh_to_spc_nodes(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves,
                                      S(stream));
-    if (rc != 1) return rc;
+    if (rc != 1) {
+      g_dev_stat[0] = 0;
+      return rc;
+    }
   }
   return mesh_to_spc_impl(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves, S(stream));
 }

@@ -58,14 +58,29 @@ at::Tensor workspace(size_t bytes, const at::Device &dev, int64_t stream) {
 
 void *ptr(const at::Tensor &t) { return t.defined() ? t.data_ptr() : nullptr; }
 
-// Each node's backward is one opaque HIP call, so its gradients cannot be differentiated again:
-// under create_graph (grad mode on inside the backward) raise rather than hand back gradients
-// that silently drop this op's second-order term (the Python nodes are once_differentiable).
+// Each node's backward is one opaque HIP call, so its gradients cannot be differentiated again.
+// dibr_rasterization (whose reference backward is a CUDA kernel too) raises under create_graph
+// (grad mode on inside the backward) rather than hand back gradients that silently drop its
+// second-order term.  The nodes whose reference is plain torch (mask_iou, prepare_vertices,
+// texture_mapping) instead take the reference chain's own differentiable gradient then
+// (kaolin/_double_backward.py), as the reference would give.
 void no_double_backward(const char *op) {
   TORCH_CHECK(!at::GradMode::is_enabled(), op,
               ": backward with create_graph=True is not supported (the backward is one HIP call and is not "
               "differentiable)");
 }
+
+// kaolin._double_backward.<fn>(*args) -> its list of gradients (None -> undefined)
+template <typename... Args>
+variable_list torch_chain_grads(const char *fn, Args &&...args) {
+  pybind11::gil_scoped_acquire gil;
+  pybind11::object r = pybind11::module_::import("kaolin._double_backward").attr(fn)(std::forward<Args>(args)...);
+  variable_list out;
+  for (auto item : r) out.push_back(item.is_none() ? at::Tensor() : item.cast<at::Tensor>());
+  return out;
+}
+
+pybind11::object opt_obj(const at::Tensor &t) { return t.defined() ? pybind11::cast(t) : pybind11::none(); }
 
 struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
   static variable_list forward(AutogradContext *ctx, int64_t height, int64_t width, at::Tensor fvz, at::Tensor fvi,
@@ -155,9 +170,8 @@ struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
 
 // mask_iou (metrics/render.py MaskIouHip): kl_mask_iou_forward / _backward
 struct MaskIou : public torch::autograd::Function<MaskIou> {
-  static variable_list forward(AutogradContext *ctx, at::Tensor lhs, at::Tensor rhs, int64_t stream) {
-    lhs = lhs.contiguous();
-    rhs = rhs.contiguous();
+  static variable_list forward(AutogradContext *ctx, at::Tensor lhs_in, at::Tensor rhs_in, int64_t stream) {
+    const at::Tensor lhs = lhs_in.contiguous(), rhs = rhs_in.contiguous();
     const int64_t B = lhs.size(0), n = lhs.numel() / B;
     const auto opt = lhs.options();
     at::Tensor up = at::empty({B}, opt), down = at::empty({B}, opt), loss = at::empty({}, opt);
@@ -167,18 +181,24 @@ struct MaskIou : public torch::autograd::Function<MaskIou> {
                               ptr(loss), ws.data_ptr(), nbytes, (kl_stream)stream),
           "mask_iou");
     ctx->saved_data["stream"] = stream;
-    ctx->save_for_backward({lhs, rhs, up, down});
+    ctx->save_for_backward({lhs_in, rhs_in, up, down});  // the inputs themselves (double backward)
     return {loss};
   }
   static variable_list backward(AutogradContext *ctx, variable_list grads) {
     const auto saved = ctx->get_saved_variables();
-    no_double_backward("mask_iou");
-    const at::Tensor &lhs = saved[0], &rhs = saved[1], &up = saved[2], &down = saved[3];
+    const at::Tensor &up = saved[2], &down = saved[3];
     const bool need_l = ctx->needs_input_grad(0), need_r = ctx->needs_input_grad(1);
     variable_list out(3);
     if (!need_l && !need_r) return out;
+    at::Tensor g = grads[0].defined() ? grads[0].contiguous() : at::ones({}, saved[0].options());
+    if (at::GradMode::is_enabled()) {  // create_graph: the reference's torch gradient
+      auto r = torch_chain_grads("mask_iou", saved[0], saved[1], g);
+      out[0] = r[0];
+      out[1] = r[1];
+      return out;
+    }
+    const at::Tensor lhs = saved[0].contiguous(), rhs = saved[1].contiguous();
     at::Tensor gl = need_l ? at::empty_like(lhs) : at::Tensor(), gr = need_r ? at::empty_like(rhs) : at::Tensor();
-    at::Tensor g = grads[0].defined() ? grads[0].contiguous() : at::ones({}, lhs.options());
     const int64_t B = lhs.size(0);
     check(kl_mask_iou_backward(dtype_code(lhs.scalar_type()), (int)B, lhs.numel() / B, ptr(g), ptr(lhs), ptr(rhs),
                                ptr(up), ptr(down), ptr(gl), ptr(gr), (kl_stream)ctx->saved_data["stream"].toInt()),
@@ -216,18 +236,32 @@ struct PrepareVertices : public torch::autograd::Function<PrepareVertices> {
     ctx->saved_data["trans_shape"] = has_xf ? std::vector<int64_t>{} : cam_b.sizes().vec();
     ctx->saved_data["has_xf"] = has_xf;
     ctx->set_materialize_grads(false);
-    ctx->save_for_backward({verts, fc, pj, r, t, x});
+    // the inputs themselves (a double backward differentiates the reference's chain of them)
+    ctx->save_for_backward({vertices, faces, proj, has_xf ? at::Tensor() : cam_a, has_xf ? at::Tensor() : cam_b,
+                            has_xf ? cam_a : at::Tensor()});
     return {fvc, fvi, fn};
   }
   static variable_list backward(AutogradContext *ctx, variable_list grads) {
     const auto saved = ctx->get_saved_variables();
-    no_double_backward("prepare_vertices");
-    const at::Tensor &verts = saved[0], &fc = saved[1], &pj = saved[2], &r = saved[3], &t = saved[4], &x = saved[5];
     variable_list out(8);
     if (!grads[0].defined() && !grads[1].defined() && !grads[2].defined()) return out;
+    const bool has_xf = ctx->saved_data["has_xf"].toBool();
+    if (at::GradMode::is_enabled()) {  // create_graph: the reference's torch gradient
+      auto g = torch_chain_grads("prepare_vertices", saved[0], saved[1], saved[2], opt_obj(saved[3]),
+                                 opt_obj(saved[4]), opt_obj(saved[5]), opt_obj(grads[0]), opt_obj(grads[1]),
+                                 opt_obj(grads[2]));
+      out[0] = g[0];
+      out[2] = g[2];
+      out[3] = has_xf ? g[5] : g[3];
+      if (!has_xf) out[4] = g[4];
+      return out;
+    }
+    const at::Tensor verts = saved[0].contiguous(), fc = saved[1].contiguous(), pj = saved[2].contiguous();
+    const at::Tensor r = saved[3].defined() ? saved[3].contiguous() : at::Tensor();
+    const at::Tensor t = saved[4].defined() ? saved[4].contiguous() : at::Tensor();
+    const at::Tensor x = saved[5].defined() ? saved[5].contiguous() : at::Tensor();
     const auto b = ctx->saved_data["batches"].toIntVector();
     const int64_t B = b[0], Bv = b[1], Bc = b[2], Bp = b[3];
-    const bool has_xf = ctx->saved_data["has_xf"].toBool();
     const bool need_v = ctx->needs_input_grad(0), need_p = ctx->needs_input_grad(2),
                need_r = !has_xf && ctx->needs_input_grad(3), need_t = !has_xf && ctx->needs_input_grad(4),
                need_x = has_xf && ctx->needs_input_grad(3);
@@ -282,16 +316,21 @@ struct TextureMapping : public torch::autograd::Function<TextureMapping> {
     ctx->saved_data["mode"] = mode;
     ctx->saved_data["n"] = n;
     ctx->saved_data["stream"] = stream;
-    ctx->save_for_backward({c, t});
+    ctx->save_for_backward({coords, tex});  // the inputs themselves (double backward)
     return {out};
   }
   static variable_list backward(AutogradContext *ctx, variable_list grads) {
     const auto saved = ctx->get_saved_variables();
-    no_double_backward("texture_mapping");
-    const at::Tensor &c = saved[0], &t = saved[1];
     const bool need_c = ctx->needs_input_grad(0), need_t = ctx->needs_input_grad(1);
     variable_list out(4);
     if ((!need_c && !need_t) || !grads[0].defined()) return out;
+    if (at::GradMode::is_enabled()) {  // create_graph: the reference's torch gradient
+      auto g = torch_chain_grads("texture_mapping", saved[0], saved[1], ctx->saved_data["mode"].toInt(), grads[0]);
+      out[0] = g[0];
+      out[1] = g[1];
+      return out;
+    }
+    const at::Tensor c = saved[0].contiguous(), t = saved[1].contiguous();
     const int64_t B = t.size(0), C = t.size(1), TH = t.size(2), TW = t.size(3);
     const int64_t stream = ctx->saved_data["stream"].toInt();
     at::Tensor gc = need_c ? at::empty_like(c) : at::Tensor(), gt = need_t ? at::empty_like(t) : at::Tensor();

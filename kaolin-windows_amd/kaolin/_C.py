@@ -360,10 +360,37 @@ def sided_distance_backward_cuda(grad_output, p1, p2, idx):
     g1 = torch.empty_like(p1)
     g2 = torch.empty_like(p2)
     with N.on_device(dev), N.timed(func, dev):
-        N.check(N.lib().kl_sided_distance_backward(N.dtype_code(p1.dtype), B, N1, N2, N.ptr(grad_output),
-                                                   N.ptr(p1), N.ptr(p2), N.ptr(idx), N.ptr(g1), N.ptr(g2),
-                                                   N.stream_of(dev)), func)
+        if p1.dtype in (torch.float32, torch.float64):
+            # grad_p2's terms summed in double and rounded once: deterministic, and what a
+            # points-sharded caller reproduces bit for bit (kaolin.distributed.sharded_sided_distance)
+            sums = N.workspace(B * N2 * 3 * 8, dev)
+            N.check(N.lib().kl_sided_distance_backward_sums(N.dtype_code(p1.dtype), B, N1, N2, N.ptr(grad_output),
+                                                            N.ptr(p1), N.ptr(p2), N.ptr(idx), N.ptr(g1), N.ptr(sums),
+                                                            N.ptr(g2), N.stream_of(dev)), func)
+        else:  # half / integer types: the reference's atomics in the type itself
+            N.check(N.lib().kl_sided_distance_backward(N.dtype_code(p1.dtype), B, N1, N2, N.ptr(grad_output),
+                                                       N.ptr(p1), N.ptr(p2), N.ptr(idx), N.ptr(g1), N.ptr(g2),
+                                                       N.stream_of(dev)), func)
     return [g1, g2]
+
+
+def sided_distance_backward_sums(grad_output, p1, p2, idx):
+    """sided_distance_backward_cuda with grad_p2 left as its (B,M,3) float64 double sums (float32 /
+    float64 inputs): the per-rank half of kaolin.distributed.sharded_sided_distance's backward."""
+    func = 'sided_distance_backward_cuda'
+    if p1.dtype not in (torch.float32, torch.float64):
+        raise RuntimeError(f'"{func}" (double sums) not implemented for \'{_tname(p1.dtype)}\'')
+    N.require_gpu(func, p1, p2, idx, grad_output)
+    dev = p1.device
+    B, N1, N2 = p1.shape[0], p1.shape[1], p2.shape[1]
+    g1 = torch.empty_like(p1)
+    sums = torch.empty((B, N2, 3), dtype=torch.float64, device=dev)
+    with N.on_device(dev):
+        N.check(N.lib().kl_sided_distance_backward_sums(N.dtype_code(p1.dtype), B, N1, N2,
+                                                        N.ptr(grad_output.contiguous()), N.ptr(p1.contiguous()),
+                                                        N.ptr(p2.contiguous()), N.ptr(idx.contiguous()), N.ptr(g1),
+                                                        N.ptr(sums), None, N.stream_of(dev)), func)
+    return g1, sums
 
 
 # ----------------------------------------------------------------------------- ops.mesh

@@ -85,6 +85,7 @@ _SIGS = {
     'kl_unbatched_triangle_distance_backward_sums': (_I, [_I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     'kl_sided_distance_forward': (_I, [_I, _I, _I64, _I64, _P, _P, _P, _P, _P]),
     'kl_sided_distance_backward': (_I, [_I, _I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    'kl_sided_distance_backward_sums': (_I, [_I, _I, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     'kl_mesh_to_spc': (_I, [_I64, _P, ctypes.c_uint32, ALLOC_FN, _P, _PP, ctypes.POINTER(_I64), _PP, _PP,
                             ctypes.POINTER(_I64), _P]),
     'kl_mesh_to_spc_level_counts': (_I, [_P, _I]),

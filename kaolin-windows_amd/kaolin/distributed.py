@@ -15,21 +15,37 @@ unsharded op's result bit for bit.
   ranks, the faces replicated.  ``sharded_point_to_mesh_distance`` evaluates the rank's points
   and all-gathers (dist, face_idx, dist_type).  In the backward each rank's points get their
   gradient locally; the face gradient, a sum over all points, is all-reduced as the per-rank
-  DOUBLE sums of the per-point float terms and rounded once (GPU), which is the unsharded
-  backward's gradient bit for bit.
+  DOUBLE sums of the per-point float terms and rounded once (GPU, float32 inputs), which is the
+  unsharded backward's gradient (itself such a double sum rounded once) up to the one-ulp
+  allowance of the summation order that bench.py and tests/dibr_util.py document: float32 terms
+  add exactly in double unless their magnitudes span more than ~2^29.
+* point_to_mesh_distance on a batch (reference metrics/trianglemesh.py:79-91 loops over the
+  batch): ``sharded_batched_point_to_mesh_distance`` splits the batch elements over the ranks;
+  each element is independent, so the all-gathered outputs and gradients are the unsharded
+  ones bit for bit.
+* sided_distance / chamfer_distance (reference metrics/pointcloud.py:20-136):
+  ``sharded_sided_distance`` splits p1's points, p2 replicated; (dist, idx) are all-gathered and
+  grad_p2 is all-reduced as double sums and rounded once, as for point_to_mesh.
+  ``sharded_chamfer_distance`` runs both directions that way (p1 split for p1 -> p2, p2 split for
+  p2 -> p1) and applies the reference's means to the gathered distances.
 * unbatched_raytrace (reference render/spc/raytrace.py:31-84): the rays are split contiguously,
   the octree replicated; each rank marches its rays, offsets its ray indices by its first ray
   and the nuggets are all-gathered with their per-rank counts (all-gather-v).  The reference's
   output is ray-major, so the rank-order concatenation is the unsharded output.
 * trianglemeshes_to_voxelgrids (reference ops/conversions/trianglemesh.py:29-110): a batch is
   split by mesh (grids all-gathered); one mesh (or fewer meshes than ranks) is split by face
-  and the per-rank grids are max-reduced -- the voxel set is a union over faces (every rank
-  also marks the vertices), so the OR of the shards is the unsharded grid.
+  and the per-rank grids are OR-reduced as bit grids (R^3 / 8 bytes: 16 MB at R = 512, against
+  537 MB for the dense float grid) -- the voxel set is a union over faces (every rank also marks
+  the vertices), so the OR of the shards is the unsharded grid.  RCCL has no bitwise reduction:
+  the OR is a reduce-scatter done by hand (all_to_all of the packed bytes, an OR of the world's
+  copies of the rank's slice, all_gather of the slices), the same bytes on the links as a ring
+  all-reduce.
 """
 import torch
 import torch.distributed as dist
 
 __all__ = ['shard_bounds', 'gather_losses', 'allreduce_grads', 'sharded_point_to_mesh_distance',
+           'sharded_batched_point_to_mesh_distance', 'sharded_sided_distance', 'sharded_chamfer_distance',
            'sharded_unbatched_raytrace', 'sharded_trianglemeshes_to_voxelgrids']
 
 
@@ -71,6 +87,24 @@ def _all_reduce(t, op, group):
         t.copy_(h)
     else:
         dist.all_reduce(t, op=op, group=group)
+
+
+def _all_to_all(out, t, group):
+    if _staged(t, group):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(h, t.cpu(), group=group)
+        out.copy_(h)
+    else:
+        dist.all_to_all_single(out, t, group=group)
+
+
+def _all_gather_flat(out, t, group):
+    if _staged(t, group):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, t.cpu(), group=group)
+        out.copy_(h)
+    else:
+        dist.all_gather_into_tensor(out, t, group=group)
 
 
 def gather_losses(loss, group=None):
@@ -183,8 +217,10 @@ class _ShardedP2M(torch.autograd.Function):
             gp, sums = _p2m_face_sums(g_local, lp, fv, i, t)
             g_fv = None
             if ctx.needs_input_grad[1]:
-                _all_reduce(sums, dist.ReduceOp.SUM, ctx.group)  # exact: f32 terms sum exactly in double
-                g_fv = sums.to(fv.dtype)                         # rounded once, as the unsharded backward
+                # the ranks' double sums added (exact for float32 terms within ~2^29 of each other)
+                # and rounded once, as the unsharded backward rounds its own double sum
+                _all_reduce(sums, dist.ReduceOp.SUM, ctx.group)
+                g_fv = sums.to(fv.dtype)
             return (gp if ctx.needs_input_grad[0] else None), g_fv, None, None
         lp, fv, d = ctx.local
         inputs = [x for x in (lp, fv) if x.requires_grad]
@@ -199,6 +235,153 @@ class _ShardedP2M(torch.autograd.Function):
         return g_lp, g_fv, None, None
 
 
+def _split_sizes(n, world):
+    return [hi - lo for lo, hi in (shard_bounds(n, r, world) for r in range(world))]
+
+
+class _ShardedBatchedP2M(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, pointclouds, face_vertices, lo, hi, sizes, group):
+        from .metrics.trianglemesh import point_to_mesh_distance
+        ctx.lo, ctx.hi, ctx.sizes, ctx.group = lo, hi, sizes, group
+        with torch.enable_grad():
+            lp = pointclouds[lo:hi].detach().requires_grad_(pointclouds.requires_grad)
+            fv = face_vertices[lo:hi].detach().requires_grad_(face_vertices.requires_grad)
+            if hi > lo:
+                d, i, t = point_to_mesh_distance(lp, fv)
+            else:  # more ranks than batch elements: this rank has none
+                P = pointclouds.shape[1]
+                d = pointclouds.new_empty((0, P))
+                i = torch.empty((0, P), dtype=torch.long, device=pointclouds.device)
+                t = torch.empty((0, P), dtype=torch.int32, device=pointclouds.device)
+        ctx.local = (lp, fv, d)
+        out_i, out_t = _all_gather_rows(i, sizes, group), _all_gather_rows(t, sizes, group)
+        ctx.mark_non_differentiable(out_i, out_t)
+        return _all_gather_rows(d.detach(), sizes, group), out_i, out_t
+
+    @staticmethod
+    def backward(ctx, g_dist, g_idx, g_type):
+        lp, fv, d = ctx.local
+        inputs = [x for x in (lp, fv) if x.requires_grad]
+        grads = []
+        if inputs and ctx.hi > ctx.lo:
+            grads = torch.autograd.grad(d, inputs, g_dist[ctx.lo:ctx.hi].contiguous(), allow_unused=True)
+        it = iter(grads)
+        out = []
+        for x, need in ((lp, ctx.needs_input_grad[0]), (fv, ctx.needs_input_grad[1])):
+            g = next(it, None) if x.requires_grad else None
+            if not need:
+                out.append(None)
+                continue
+            g = torch.zeros_like(x) if g is None else g.contiguous()
+            out.append(_all_gather_rows(g, ctx.sizes, ctx.group))  # every element's own gradient
+        return out[0], out[1], None, None, None, None
+
+
+def sharded_batched_point_to_mesh_distance(pointclouds, face_vertices, group=None):
+    r"""point_to_mesh_distance of a batch, (B,P,3) points against (B,F,3,3) triangles, with the
+    batch elements split contiguously over the ranks of ``group`` (the reference loops over them,
+    metrics/trianglemesh.py:79-91).  Both inputs are the whole batch on every rank.  Returns the
+    unsharded (dist (B,P), face_idx (B,P) int64, dist_type (B,P) int32) on every rank; gradients
+    reach both inputs for every element (each rank's elements' gradients are all-gathered), so
+    every rank holds the unsharded gradients, bit for bit."""
+    world, rank = _world(group), _rank(group)
+    if world == 1:
+        from .metrics.trianglemesh import point_to_mesh_distance
+        return point_to_mesh_distance(pointclouds, face_vertices)
+    B = pointclouds.shape[0]
+    lo, hi = shard_bounds(B, rank, world)
+    return _ShardedBatchedP2M.apply(pointclouds, face_vertices, lo, hi, _split_sizes(B, world), group)
+
+
+def _all_gather_points(t, sizes, group):
+    """all-gather-v along dim 1 (points) of (B, n_r, ...) tensors, in rank order."""
+    return _all_gather_rows(t.transpose(0, 1).contiguous(), sizes, group).transpose(0, 1).contiguous()
+
+
+def _sided_forward(p1, p2):
+    from .metrics.pointcloud import sided_distance
+    with torch.no_grad():
+        return sided_distance(p1, p2)
+
+
+def _sided_backward_sums(grad, p1, p2, idx):
+    """(grad_p1, grad_p2's (B,M,3) float64 double sums) of the rank's p1 points (GPU, distance.hip)."""
+    from . import _C
+    return _C.sided_distance_backward_sums(grad, p1, p2, idx)
+
+
+class _ShardedSided(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, p1, p2, lo, hi, sizes, group, full):
+        # full: p1 is the whole cloud (replicated) and the rank evaluates points [lo, hi); its
+        # gradient is then all-gathered so that every rank holds all of it.  Else p1 is the
+        # rank's share and its gradient stays local.
+        lp = (p1[:, lo:hi] if full else p1).contiguous()
+        p2c = p2.contiguous()
+        d, i = _sided_forward(lp, p2c)
+        ctx.save_for_backward(lp, p2c, i)
+        ctx.lo, ctx.sizes, ctx.group, ctx.full = lo, sizes, group, full
+        out_i = _all_gather_points(i, sizes, group)
+        ctx.mark_non_differentiable(out_i)
+        return _all_gather_points(d, sizes, group), out_i
+
+    @staticmethod
+    def backward(ctx, g_dist, g_idx):
+        lp, p2, i = ctx.saved_tensors
+        n = lp.shape[1]
+        g1, sums = _sided_backward_sums(g_dist[:, ctx.lo:ctx.lo + n].contiguous(), lp, p2, i)
+        g2 = None
+        if ctx.needs_input_grad[1]:
+            _all_reduce(sums, dist.ReduceOp.SUM, ctx.group)  # exact double sums (float32 terms)
+            g2 = sums.to(p2.dtype)                           # rounded once, as the unsharded backward
+        if not ctx.needs_input_grad[0]:
+            g1 = None
+        elif ctx.full:
+            g1 = _all_gather_points(g1, ctx.sizes, ctx.group)
+        return g1, g2, None, None, None, None, None
+
+
+def sharded_sided_distance(local_p1, p2, group=None):
+    r"""sided_distance(p1, p2) with p1's points split over the ranks of ``group``.
+
+    ``local_p1`` (B, n_r, 3) is this rank's contiguous share of p1's points
+    (``shard_bounds(N, rank, world)``), ``p2`` (B,M,3) is the same on every rank.  Returns the
+    whole (dist (B,N), idx (B,N) int64) on every rank.  Gradients: ``local_p1`` gets its rows;
+    ``p2`` gets the sum over every rank's points, formed from the ranks' double sums of the
+    per-point float terms and rounded once (GPU, float32 / float64), which is the unsharded
+    backward's (itself a double sum rounded once, _C.sided_distance_backward_cuda) up to the
+    documented one-ulp allowance."""
+    world = _world(group)
+    if world == 1:
+        from .metrics.pointcloud import sided_distance
+        return sided_distance(local_p1, p2)
+    sizes = _sizes(local_p1.shape[1], local_p1.device, group)
+    lo = sum(sizes[:_rank(group)])
+    return _ShardedSided.apply(local_p1, p2, lo, lo + local_p1.shape[1], sizes, group, False)
+
+
+def sharded_chamfer_distance(p1, p2, w1=1., w2=1., squared=True, group=None):
+    r"""chamfer_distance (reference metrics/pointcloud.py:89-136) over the ranks of ``group``; both
+    clouds are the whole (B,N,3) / (B,M,3) on every rank.  The p1 -> p2 direction splits p1's
+    points, the p2 -> p1 direction splits p2's (``sharded_sided_distance``'s scheme); the gathered
+    distances go through the reference's means, so every rank holds the unsharded distance, and
+    both clouds' whole gradients (split rows all-gathered, replicated terms all-reduced as double
+    sums)."""
+    from .metrics.pointcloud import chamfer_distance, _chamfer_from_sided
+    world, rank = _world(group), _rank(group)
+    if world == 1:
+        return chamfer_distance(p1, p2, w1, w2, squared)
+    n, m = p1.shape[1], p2.shape[1]
+    lo1, hi1 = shard_bounds(n, rank, world)
+    lo2, hi2 = shard_bounds(m, rank, world)
+    sdist1 = _ShardedSided.apply(p1, p2, lo1, hi1, _split_sizes(n, world), group, True)[0]
+    sdist2 = _ShardedSided.apply(p2, p1, lo2, hi2, _split_sizes(m, world), group, True)[0]
+    return _chamfer_from_sided(sdist1, sdist2, w1, w2, squared)
+
+
 def sharded_point_to_mesh_distance(local_points, face_vertices, group=None):
     r"""point_to_mesh_distance of one (P,3) cloud against (F,3,3) triangles with the
     points split over the ranks of ``group``.
@@ -208,7 +391,9 @@ def sharded_point_to_mesh_distance(local_points, face_vertices, group=None):
     cloud's (dist (P), face_idx (P) int64, dist_type (P) int32) on every rank.  Gradients:
     ``local_points`` gets the rows of its share; ``face_vertices`` gets the sum over every
     rank's points.  On the GPU that sum is formed from the ranks' double sums of the per-point
-    float terms and rounded once: the unsharded gradient bit for bit.  On the CPU (the
+    float terms and rounded once: the unsharded gradient, for float32 inputs bit for bit up to the
+    documented one-ulp allowance of summation order (float64 terms do not add exactly in double,
+    so there the two agree to the last bits only).  On the CPU (the
     reference's torch path, whose autograd sums in float) the ranks' float gradients are added:
     equal to the unsharded gradient up to float summation order.
     """
@@ -250,7 +435,7 @@ def sharded_trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin=Non
     r"""trianglemeshes_to_voxelgrids (dense grids) over the ranks of ``group``; every argument is
     the unsharded call's, replicated.  ``split``: 'batch' (each rank converts a contiguous share of
     the meshes; the grids are all-gathered), 'faces' (each rank converts every mesh with a
-    contiguous share of the faces; the grids are max-reduced), or 'auto' ('batch' when there are
+    contiguous share of the faces; the grids are OR-reduced as bit grids), or 'auto' ('batch' when there are
     at least as many meshes as ranks).  The default origin / scale are the whole mesh's (computed
     before splitting, so every shard normalises the same way).  Returns the unsharded (B,R,R,R)
     grid on every rank."""
@@ -273,6 +458,49 @@ def sharded_trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin=Non
         raise ValueError(f"split must be 'auto', 'batch' or 'faces', got {split!r}")
     lo, hi = shard_bounds(faces.shape[0], rank, world)
     grid = trianglemeshes_to_voxelgrids(vertices, faces[lo:hi], resolution, origin, scale)
-    red = grid if grid.dtype.is_floating_point else grid.to(torch.uint8)
-    _all_reduce(red, dist.ReduceOp.MAX, group)
-    return red if red is grid else red.to(grid.dtype)
+    bits = _or_all_reduce(_pack_bits(grid), group)
+    return _unpack_bits(bits, grid)
+
+
+_BIT_WEIGHTS = {}
+
+
+def _bit_weights(device):
+    w = _BIT_WEIGHTS.get(device)
+    if w is None:
+        w = _BIT_WEIGHTS[device] = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=device)
+    return w
+
+
+def _pack_bits(grid):
+    """Occupancy (non-zero) of a dense grid as bits, 8 cells per byte in memory order."""
+    flat = grid.reshape(-1) != 0
+    pad = (-flat.numel()) % 8
+    if pad:
+        flat = torch.cat([flat, flat.new_zeros(pad)])
+    return (flat.view(-1, 8).to(torch.uint8) * _bit_weights(grid.device)).sum(-1, dtype=torch.uint8)
+
+
+def _unpack_bits(bits, like):
+    """The grid of `like`'s shape and dtype holding 1 where `bits` is set, else 0."""
+    cells = (bits.unsqueeze(-1) & _bit_weights(bits.device)) != 0
+    return cells.reshape(-1)[:like.numel()].reshape(like.shape).to(like.dtype)
+
+
+def _or_all_reduce(bits, group):
+    """Bitwise OR of a uint8 vector over the ranks: a reduce-scatter by hand (all_to_all of the
+    world's slices, OR of the copies of this rank's slice) and an all_gather of the slices."""
+    world = _world(group)
+    n = bits.numel()
+    chunk = -(-n // world)
+    buf = bits.new_zeros(world * chunk)
+    buf[:n] = bits
+    recv = torch.empty_like(buf)
+    _all_to_all(recv, buf, group)
+    part = recv.view(world, chunk)
+    mine = part[0].clone()
+    for r in range(1, world):
+        mine |= part[r]
+    out = torch.empty_like(buf)
+    _all_gather_flat(out, mine, group)
+    return out[:n]

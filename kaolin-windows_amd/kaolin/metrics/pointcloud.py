@@ -34,8 +34,12 @@ def sided_distance(p1, p2):
 
 def chamfer_distance(p1, p2, w1=1., w2=1., squared=True):
     r"""w1 * mean_i min_j |p1_i - p2_j|^2 + w2 * mean_j min_i |p2_j - p1_i|^2 (pointcloud.py:89-135)."""
-    sdist1 = sided_distance(p1, p2)[0]
-    sdist2 = sided_distance(p2, p1)[0]
+    return _chamfer_from_sided(sided_distance(p1, p2)[0], sided_distance(p2, p1)[0], w1, w2, squared)
+
+
+def _chamfer_from_sided(sdist1, sdist2, w1, w2, squared):
+    """chamfer_distance's reduction of the two sided distances (pointcloud.py:124-135); shared with
+    kaolin.distributed.sharded_chamfer_distance, which gathers the distances first."""
     if not squared:
         sdist1 = torch.sqrt(sdist1)
         sdist2 = torch.sqrt(sdist2)

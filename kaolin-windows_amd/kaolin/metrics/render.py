@@ -4,7 +4,6 @@ GPU f32 / f64 masks take the fused HIP path (csrc/maskiou.hip: one pass for both
 one for both gradients); other inputs run the reference's torch ops."""
 import torch
 from torch.autograd import Function
-from torch.autograd.function import once_differentiable
 
 from .. import _ext, _native as N
 
@@ -28,13 +27,16 @@ class MaskIouHip(Function):
             N.check(N.lib().kl_mask_iou_forward(N.dtype_code(lhs.dtype), B, n, N.ptr(lhs), N.ptr(rhs), N.ptr(up),
                                                 N.ptr(down), N.ptr(loss), N.ptr(ws), nbytes, N.stream_of(dev)),
                     'mask_iou')
-        ctx.save_for_backward(lhs, rhs, up, down)
+        ctx.save_for_backward(lhs_mask, rhs_mask, up, down)  # the inputs themselves (double backward)
         return loss
 
     @staticmethod
-    @once_differentiable  # its backward is one opaque HIP call: a double backward raises, not drops
     def backward(ctx, grad):
         lhs, rhs, up, down = ctx.saved_tensors
+        if torch.is_grad_enabled():  # create_graph: the reference's torch gradient, differentiable
+            from .._double_backward import mask_iou as dd
+            return tuple(dd(lhs, rhs, grad))
+        lhs, rhs = lhs.contiguous(), rhs.contiguous()
         need_l, need_r = ctx.needs_input_grad
         gl = torch.empty_like(lhs) if need_l else None
         gr = torch.empty_like(rhs) if need_r else None
@@ -61,6 +63,12 @@ def mask_iou(lhs_mask, rhs_mask):
         if ext is not None and N._TIMER is None and lhs_mask.device.index == torch.cuda.current_device():
             return ext.mask_iou(lhs_mask, rhs_mask, N.stream_of(lhs_mask.device))  # the node compiled
         return MaskIouHip.apply(lhs_mask, rhs_mask)
+    return _mask_iou_torch(lhs_mask, rhs_mask)
+
+
+def _mask_iou_torch(lhs_mask, rhs_mask):
+    """The reference's torch ops (render.py:34-37)."""
+    batch_size = lhs_mask.shape[0]
     sil_mul = lhs_mask * rhs_mask
     sil_add = lhs_mask + rhs_mask
     iou_up = torch.sum(sil_mul.reshape(batch_size, -1), dim=1)

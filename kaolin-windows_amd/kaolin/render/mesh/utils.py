@@ -106,13 +106,20 @@ class PrepareVerticesHip(Function):
                 N.ptr(proj), N.ptr(fvc), N.ptr(fvi), N.ptr(fn), N.stream_of(dev)), 'prepare_vertices')
         ctx.batches = batches
         ctx.shapes = (camera_proj.shape, None if camera_trans is None else camera_trans.shape)
-        ctx.save_for_backward(verts, fc, proj, rot, trans, xf)
+        # the inputs themselves (a double backward differentiates the reference's chain of them)
+        ctx.save_for_backward(vertices, faces, camera_proj, camera_rot, camera_trans, camera_transform)
         ctx.set_materialize_grads(False)
         return fvc, fvi, fn
 
     @staticmethod
     def backward(ctx, g_fvc, g_fvi, g_fn):
         verts, fc, proj, rot, trans, xf = ctx.saved_tensors
+        if torch.is_grad_enabled():  # create_graph: the reference's torch gradient, differentiable
+            from ..._double_backward import prepare_vertices as dd
+            g = dd(verts, fc, proj, rot, trans, xf, g_fvc, g_fvi, g_fn)
+            return g[0], None, g[2], g[3], g[4], g[5], None
+        verts, fc, proj = verts.contiguous(), fc.contiguous(), proj.contiguous()
+        rot, trans, xf = (None if x is None else x.contiguous() for x in (rot, trans, xf))
         B, Bv, Bc, Bp = ctx.batches
         need_v, _, need_p, need_r, need_t, need_x, _ = ctx.needs_input_grad
         if g_fvc is None and g_fvi is None and g_fn is None:
@@ -198,12 +205,17 @@ class TextureMappingHip(Function):
                                                        N.ptr(tex), N.ptr(out), N.stream_of(tex.device)),
                     'texture_mapping')
         ctx.mode, ctx.n = mode, n
-        ctx.save_for_backward(c, tex)
+        ctx.save_for_backward(coords, texture_maps)  # the inputs themselves (double backward)
         return out
 
     @staticmethod
     def backward(ctx, grad_out):
         c, tex = ctx.saved_tensors
+        if torch.is_grad_enabled():  # create_graph: the reference's torch gradient, differentiable
+            from ..._double_backward import texture_mapping as dd
+            g = dd(c, tex, ctx.mode, grad_out)
+            return g[0], g[1], None
+        c, tex = c.contiguous(), tex.contiguous()
         B, C, TH, TW = tex.shape
         need_c, need_t, _ = ctx.needs_input_grad
         gc = torch.empty_like(c) if need_c else None
@@ -236,12 +248,19 @@ def texture_mapping(texture_coordinates, texture_maps, mode='nearest'):
             and texture_coordinates.dtype == texture_maps.dtype and texture_maps.dim() == 4
             and texture_coordinates.shape[-1] == 2 and texture_maps.shape[0] == batch_size):
         ext = _ext.get()
-        if ext is not None and texture_maps.device.index == torch.cuda.current_device():
+        if ext is not None and N._TIMER is None and texture_maps.device.index == torch.cuda.current_device():
             out = ext.texture_mapping(texture_coordinates, texture_maps, 1 if mode == 'bilinear' else 0,
                                       N.stream_of(texture_maps.device))
         else:
             out = TextureMappingHip.apply(texture_coordinates, texture_maps, 1 if mode == 'bilinear' else 0)
         return out.reshape(batch_size, *texture_coordinates.shape[1:-1], num_channels)
+    return _texture_mapping_torch(texture_coordinates, texture_maps, mode)
+
+
+def _texture_mapping_torch(texture_coordinates, texture_maps, mode):
+    """The reference's torch chain (utils.py:64-75)."""
+    batch_size = texture_coordinates.shape[0]
+    num_channels = texture_maps.shape[1]
     coords = texture_coordinates.reshape(batch_size, -1, 1, 2)
     coords = torch.clamp(coords, 0., 1.) * 2 - 1
     coords[..., 1] = -coords[..., 1]

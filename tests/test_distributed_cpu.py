@@ -232,3 +232,149 @@ def test_sharded_raytrace_voxelgrid_grads(world):
         assert torch.equal(b, torch.full((2, 3), float(sum(range(world)))))
         assert torch.equal(c, torch.full((3,), float(world - 1)))
         assert torch.allclose(r['grads_avg'], torch.arange(5.) * tot, rtol=0, atol=1e-6)  # average of equal sums
+
+
+# ------------------------------------------------------------------ §8e: sided / chamfer / batched p2m
+def _sided_fwd_standin(p1, p2):
+    """sided_distance's forward on CPU tensors by the oracle (test stand-in: the reference op is
+    CUDA-only)."""
+    from oracle import oracle as orc
+    d, i = orc.sided_distance_forward(p1.detach().numpy(), p2.detach().numpy())
+    return torch.from_numpy(d), torch.from_numpy(i)
+
+
+def _sided_sums_standin(g, p1, p2, idx):
+    """(grad_p1, grad_p2's float64 double sums): the kernel's float terms, summed in double."""
+    B, M = p2.shape[0], p2.shape[1]
+    q = torch.gather(p2, 1, idx.unsqueeze(-1).expand(-1, -1, 3))
+    g1 = 2 * (p1 - q) * g.unsqueeze(-1)
+    t = (2 * (q - p1) * g.unsqueeze(-1)).double()
+    sums = torch.zeros((B, M, 3), dtype=torch.float64)
+    for b in range(B):
+        sums[b].index_add_(0, idx[b], t[b])
+    return g1, sums
+
+
+class _SidedOneRank(torch.autograd.Function):
+    """The unsharded sided_distance with the same stand-ins (grad_p2 rounded once)."""
+
+    @staticmethod
+    def forward(ctx, p1, p2):
+        d, i = _sided_fwd_standin(p1, p2)
+        ctx.save_for_backward(p1, p2, i)
+        return d
+
+    @staticmethod
+    def backward(ctx, g):
+        p1, p2, i = ctx.saved_tensors
+        g1, sums = _sided_sums_standin(g, p1, p2, i)
+        return g1, sums.to(p2.dtype)
+
+
+def _metric_inputs():
+    g = torch.Generator().manual_seed(11)
+    p1 = torch.rand((2, 37, 3), generator=g)
+    p2 = torch.rand((2, 23, 3), generator=g)
+    pc = torch.randn((5, 19, 3), generator=g)
+    fv = torch.randn((5, 13, 3, 3), generator=g)
+    gp = torch.rand((5, 19), generator=g)
+    return p1, p2, pc, fv, gp
+
+
+def _shard_metrics_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import numpy as np
+        import kaolin  # noqa: F401
+        from kaolin import distributed as kd
+        kd._sided_forward = _sided_fwd_standin
+        kd._sided_backward_sums = _sided_sums_standin
+        p1, p2, pc, fv, gp = _metric_inputs()
+        res = {}
+        # sided: p1 split, p2 replicated
+        lo, hi = kd.shard_bounds(p1.shape[1], rank, world)
+        a = p1[:, lo:hi].clone().requires_grad_(True)
+        b = p2.clone().requires_grad_(True)
+        d, i = kd.sharded_sided_distance(a, b)
+        (d * torch.arange(1., d.shape[1] + 1)).sum().backward()
+        res['sided'] = [d.detach(), i, a.grad, b.grad]
+        # chamfer (squared and not, weights)
+        for sq in (True, False):
+            a = p1.clone().requires_grad_(True)
+            b = p2.clone().requires_grad_(True)
+            c = kd.sharded_chamfer_distance(a, b, w1=0.7, w2=1.3, squared=sq)
+            c.sum().backward()
+            res[f'chamfer{int(sq)}'] = [c.detach(), a.grad, b.grad]
+        # batched point_to_mesh (CPU path), 5 elements; and 2 elements (world 3: one rank has none)
+        for nb in (5, 2):
+            x = pc[:nb].clone().requires_grad_(True)
+            y = fv[:nb].clone().requires_grad_(True)
+            dd, ii, tt = kd.sharded_batched_point_to_mesh_distance(x, y)
+            (dd * gp[:nb]).sum().backward()
+            res[f'p2m{nb}'] = [dd.detach(), ii, tt, x.grad, y.grad]
+        q.put((rank, {k: [np.array(t) for t in v] for k, v in res.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_sharded_sided_chamfer_batched_p2m(world):
+    """§8e row 2 over gloo world 2 / 3: sharded_sided_distance (p1 split, grad_p2 all-reduced as
+    double sums, rounded once), sharded_chamfer_distance (both directions split) and
+    sharded_batched_point_to_mesh_distance (batch elements split, gradients all-gathered) equal the
+    one-rank results on every rank, bit for bit."""
+    from kaolin.metrics.pointcloud import _chamfer_from_sided
+    from kaolin.metrics.trianglemesh import point_to_mesh_distance
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_metrics_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    p1, p2, pc, fv, gp = _metric_inputs()
+    want = {}
+    a, b = p1.clone().requires_grad_(True), p2.clone().requires_grad_(True)
+    d = _SidedOneRank.apply(a, b)
+    (d * torch.arange(1., d.shape[1] + 1)).sum().backward()
+    want['sided'] = [d.detach(), _sided_fwd_standin(p1, p2)[1], a.grad, b.grad]
+    for sq in (True, False):
+        a, b = p1.clone().requires_grad_(True), p2.clone().requires_grad_(True)
+        c = _chamfer_from_sided(_SidedOneRank.apply(a, b), _SidedOneRank.apply(b, a), 0.7, 1.3, sq)
+        c.sum().backward()
+        want[f'chamfer{int(sq)}'] = [c.detach(), a.grad, b.grad]
+    for nb in (5, 2):
+        x, y = pc[:nb].clone().requires_grad_(True), fv[:nb].clone().requires_grad_(True)
+        dd, ii, tt = point_to_mesh_distance(x, y)
+        (dd * gp[:nb]).sum().backward()
+        want[f'p2m{nb}'] = [dd.detach(), ii, tt, x.grad, y.grad]
+    from kaolin.distributed import shard_bounds
+    for rank in range(world):
+        for k, ws in want.items():
+            got = res[rank][k]
+            assert len(got) == len(ws)
+            for n, (x, y) in enumerate(zip(got, ws)):
+                if k == 'sided' and n == 2:  # local_p1's gradient: the rank's own rows
+                    lo, hi = shard_bounds(p1.shape[1], rank, world)
+                    y = y[:, lo:hi]
+                y = y.numpy()
+                assert x.dtype == y.dtype and x.shape == y.shape and (x == y).all(), (rank, k, n)
+
+
+def test_bit_grid_pack_unpack_roundtrip():
+    """The face split's bit grid (R^3 / 8 bytes) restores the dense grid exactly, also when R^3 is
+    not a multiple of 8, and OR of packed grids is the packed union."""
+    from kaolin.distributed import _pack_bits, _unpack_bits
+    g = torch.Generator().manual_seed(5)
+    for R in (5, 8, 13):
+        a = (torch.rand((1, R, R, R), generator=g) < 0.3).float()
+        b = (torch.rand((1, R, R, R), generator=g) < 0.3).float()
+        pa, pb = _pack_bits(a), _pack_bits(b)
+        assert pa.dtype == torch.uint8 and pa.numel() == -(-R ** 3 // 8)
+        assert torch.equal(_unpack_bits(pa, a), a)
+        assert torch.equal(_unpack_bits(pa | pb, a), torch.maximum(a, b))
+        assert torch.equal(_unpack_bits(_pack_bits(a.bool()), a.bool()), a.bool())

@@ -718,8 +718,9 @@ def test_compiled_tutorial_nodes_equal_python_nodes(kal, monkeypatch, dtype, cam
 
 
 def test_compiled_nodes_refuse_double_backward(kal):
-    """The compiled nodes' backwards are single HIP calls: backward(create_graph=True) raises
-    instead of returning gradients that silently drop the op's second-order term."""
+    """dibr_rasterization's backward is one HIP call (as the reference's CUDA backward):
+    backward(create_graph=True) raises instead of returning gradients that silently drop the op's
+    second-order term."""
     from kaolin import _ext
     assert _ext.get() is not None
     import bench
@@ -728,12 +729,57 @@ def test_compiled_nodes_refuse_double_backward(kal):
     f, m, _ = kal.render.mesh.dibr_rasterization(32, 48, inp['fvz'], fvi, inp['feat'], inp['fnz'])
     with pytest.raises(RuntimeError, match='create_graph'):
         torch.autograd.grad(m.sum() + f.sum(), fvi, create_graph=True)
-    a = torch.rand((2, 8, 8), device=DEV, requires_grad=True)
-    loss = kal.metrics.render.mask_iou(a, (torch.rand((2, 8, 8), device=DEV) > 0.5).float())
-    with pytest.raises(RuntimeError, match='create_graph'):
-        torch.autograd.grad(loss, a, create_graph=True)
-    # an ordinary backward is unaffected
-    torch.autograd.grad(kal.metrics.render.mask_iou(a, a.detach()), a)
+
+
+@pytest.mark.parametrize('route', ['compiled', 'python'])
+def test_torch_reference_nodes_double_backward(kal, monkeypatch, route):
+    """mask_iou, prepare_vertices and texture_mapping are plain torch in the reference, so their
+    gradients are differentiable there.  Under create_graph the HIP nodes take the
+    reference chain's gradient (kaolin/_double_backward.py): first AND second derivatives equal
+    the reference chain's own, bit for bit; an ordinary backward stays on the HIP path."""
+    from kaolin import _ext
+    from kaolin.metrics.render import _mask_iou_torch
+    from kaolin.render.mesh.utils import _prepare_vertices_torch, _texture_mapping_torch
+    if route == 'python':
+        monkeypatch.setattr(_ext, 'get', lambda: None)
+    else:
+        assert _ext.get() is not None
+
+    def both(fn, ref, inputs, consts=()):
+        outs = []
+        for f in (fn, ref):
+            xs = [x.detach().clone().requires_grad_(True) for x in inputs]
+            y = f(*xs, *consts)
+            ys = y if isinstance(y, tuple) else (y,)
+            w = [torch.rand(o.shape, generator=torch.Generator().manual_seed(k), dtype=o.dtype).to(DEV)
+                 for k, o in enumerate(ys)]
+            g = torch.autograd.grad(sum((o * wk).sum() for o, wk in zip(ys, w)), xs, create_graph=True)
+            hv = torch.autograd.grad(sum((gk * gk).sum() for gk in g), xs, allow_unused=True)
+            outs.append((g, hv))
+        (g0, h0), (g1, h1) = outs
+        for p, q in zip(g0 + h0, g1 + h1):
+            assert (p is None and q is None) or torch.equal(p, q)
+
+    gen = torch.Generator().manual_seed(4)
+    a = torch.rand((2, 8, 8), generator=gen).to(DEV)
+    b = torch.rand((2, 8, 8), generator=gen).to(DEV)
+    both(kal.metrics.render.mask_iou, _mask_iou_torch, [a, b])
+    verts = torch.rand((2, 30, 3), generator=gen).to(DEV)
+    faces = torch.randint(0, 30, (40, 3), generator=gen).to(DEV)
+    proj = torch.tensor([[1.8], [1.8], [-1.]], device=DEV)
+    rot = torch.linalg.qr(torch.randn((2, 3, 3), generator=gen))[0].to(DEV)
+    trans = torch.tensor([[0., 0., 3.], [0.1, 0., 3.2]], device=DEV)
+    both(lambda *x: kal.render.mesh.prepare_vertices(x[0], faces, x[1], x[2], x[3]),
+         lambda *x: _prepare_vertices_torch(x[0], faces, x[1], x[2], x[3], None), [verts, proj, rot, trans])
+    uv = torch.rand((2, 5, 7, 2), generator=gen).to(DEV)
+    tex = torch.rand((2, 3, 16, 16), generator=gen).to(DEV)
+    for mode in ('bilinear', 'nearest'):
+        both(lambda c, t: kal.render.mesh.texture_mapping(c, t, mode), lambda c, t: _texture_mapping_torch(c, t, mode),
+             [uv, tex])
+    # an ordinary backward stays on the HIP node (bit-equal to the reference chain is not expected:
+    # the HIP sums are double, rounded once)
+    x = a.clone().requires_grad_(True)
+    torch.autograd.grad(kal.metrics.render.mask_iou(x, b), x)
 
 
 def test_dibr_mixed_dtypes_raise(kal, monkeypatch):
@@ -1228,6 +1274,44 @@ def _m2s_fixed_check(kal, fv, level, ncap, lcap):
     assert torch.equal(ff[:leaves], fidx) and bool((ff[leaves:] == -1).all())
     assert torch.equal(fb[:leaves], bary[:, :2] if leaves else fb[:0]) and not fb[leaves:].any()
     return status
+
+
+@pytest.mark.parametrize('cap', [2048, 16384])
+def test_mesh_to_spc_pair_overflow_fallback(kal, cap):
+    """The node-rank path's pair buffers (96 pairs per face and level) overflowing -- the branch of
+    r04's GPU fault.  With the capacity shrunk (dev param 14: 2048 pairs overflow at the root, 16384
+    at a later level's node scan), the eager call takes the per-level fallback (kl_dev_get_stat) and
+    equals the oracle; the fixed-capacity form returns status 2 with nothing written; with the
+    capacity restored the node-rank path runs again and gives the same octree."""
+    import ctypes
+    from kaolin import _native as N
+    lib = N.lib()
+    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.kl_dev_get_stat.argtypes = [ctypes.c_int]
+    lib.kl_dev_get_stat.restype = ctypes.c_int
+    level = 6
+    v, f = _uv_sphere(16, 24, 0.9)
+    fv = v[f].astype(np.float32)
+    oo, of, ob = orc.mesh_to_spc(fv, level)
+    N._SIZES.clear()  # workspace sizes follow the capacity
+    lib.kl_dev_set_param(14, cap)
+    try:
+        octree, fidx, bary = kal.ops.conversions.unbatched_mesh_to_spc(T(fv), level)
+        torch.cuda.synchronize()
+        assert lib.kl_dev_get_stat(0) == 1  # the per-level fallback ran
+        assert np.array_equal(A(octree), oo) and np.array_equal(A(fidx), of)
+        np.testing.assert_array_equal(A(bary), ob)
+        fo, ff, fb, res = kal.ops.conversions.unbatched_mesh_to_spc(T(fv), level, capacity=(100000, 100000))
+        nn, nl, status = (int(x) for x in res.cpu())
+        assert (nn, nl, status) == (0, 0, 2)
+        assert not fo.any() and bool((ff == -1).all()) and not fb.any()
+    finally:
+        lib.kl_dev_set_param(14, 0)
+        N._SIZES.clear()
+    octree2, fidx2, _ = kal.ops.conversions.unbatched_mesh_to_spc(T(fv), level)
+    torch.cuda.synchronize()
+    assert lib.kl_dev_get_stat(0) == 0
+    assert torch.equal(octree2, octree) and torch.equal(fidx2, fidx)
 
 
 @pytest.mark.parametrize('level', [1, 3, 6])
