@@ -1709,8 +1709,8 @@ namespace kl {
 //   then:   face records | pixel ranges | raster buckets | soft buckets | raster items |
 //           item count | soft order | soft pixel ranges     (records sized for f64)
 struct DibrFwdWs {
-  size_t off_sbm, off_rgh, off_sgh, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder, off_sn,
-      off_srng, off_defer, bytes;
+  size_t off_sbm, off_rgh, off_sgh, off_tk, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder,
+      off_sn, off_srng, off_defer, off_pk, off_whist, bytes;
   DibrFwdWs(int B, int H, int W, int F) {
     const BinGeom g = make_bin_geom(B, H, W, F);
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
@@ -1718,7 +1718,8 @@ struct DibrFwdWs {
     off_sbm = g.bytes();
     off_rgh = off_sbm + g.bytes();
     off_sgh = off_rgh + ORD_HIST * sizeof(int);
-    zero = off_sgh + ORD_HIST * sizeof(int);
+    off_tk = off_sgh + ORD_HIST * sizeof(int);  // the chip-wide order kernel's two tickets
+    zero = off_tk + 16 * sizeof(int);
     off_rec = up(zero);
     off_rng = up(off_rec + (size_t)B * F * RT_REC * sizeof(double));
     off_rbk = up(off_rng + (size_t)B * F * sizeof(uint2));
@@ -1729,7 +1730,9 @@ struct DibrFwdWs {
     off_sn = off_sorder + nt * TILE_H * sizeof(int32_t);
     off_srng = up(off_sn + sizeof(int));
     off_defer = up(off_srng + (size_t)B * F * sizeof(uint2));
-    bytes = off_defer + (size_t)B * H * g.tiles_x;
+    off_pk = up(off_defer + (size_t)B * H * g.tiles_x);  // 2 x nt packed (rank, bucket)
+    off_whist = up(off_pk + 2 * nt * sizeof(uint32_t));    // 2 x nb x ORD_HIST workgroup histograms
+    bytes = off_whist + 2 * (size_t)cdiv((int64_t)nt, CO_THREADS) * ORD_HIST * sizeof(int);
   }
 };
 
@@ -1822,7 +1825,40 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   // params 4 / 5 override, for sweeps)
   const int split_from = g_dev_param[4] ? g_dev_param[4] : 5;
   const int split_log2 = sizeof(T) == 4 ? (g_dev_param[5] ? g_dev_param[5] : 2) : 0;
-  if (nt <= ORD_LDS_TILES && !(g_dev_flags & (1 << 20))) {  // counts and orders in one launch
+  if (nt <= ORD_LDS_TILES && !(g_dev_flags & (1 << 20)) && g_dev_param[15] != 1) {
+    // counts over the chip, orders by each bitmap's last count workgroup (tileorder.h); the other
+    // workgroups zero the backward's soft-mask accumulator meanwhile (dev param 15 = 1: the r04
+    // two-workgroup kernel below, for A/B)
+    const int nb = (int)cdiv(nt, CO_THREADS);
+    CountOrderArgs ca{};
+    ca.bm[0] = rbm;
+    ca.bm[1] = sbm;
+    ca.words = g.words;
+    ca.nt = nt;
+    ca.nb = nb;
+    ca.pk[0] = reinterpret_cast<uint32_t *>(w + L.off_pk);
+    ca.pk[1] = ca.pk[0] + nt;
+    ca.whist[0] = reinterpret_cast<int *>(w + L.off_whist);
+    ca.whist[1] = ca.whist[0] + (size_t)nb * ORD_HIST;
+    ca.ticket = reinterpret_cast<unsigned *>(w + L.off_tk);
+    ca.order[0] = items;
+    ca.order[1] = sorder;
+    ca.nitems[0] = nitems;
+    ca.nitems[1] = snitems;
+    ca.split_from = split_from;
+    ca.split_log2 = split_log2;
+    ca.lp_min1 = soft_lp_min(K);
+    ca.skip_empty1 = 1;
+    ca.sp = soft_split();
+    ca.zero = bcnt;
+    ca.nzero = DibrState::kZeroInts;
+    ca.zacc = bacc;
+    ca.zn = (size_t)B * F * DS_ACC_STRIDE;
+    const unsigned zg = g_dev_param[9] >= 2 ? (unsigned)g_dev_param[9] : 248u;  // zeroing workgroups
+    hipLaunchKernelGGL(tile_countorder_chip_kernel, dim3((unsigned)(2 * nb) + zg), dim3(CO_THREADS),
+                       (size_t)nb * ORD_HIST * sizeof(int), st, ca);
+    KL_CHECK_LAUNCH();
+  } else if (nt <= ORD_LDS_TILES && !(g_dev_flags & (1 << 20))) {  // counts and orders in one launch
     // + 254 workgroups that zero the backward's soft-mask accumulator while two order
     const unsigned og = g_dev_param[9] >= 2 ? (unsigned)g_dev_param[9] : 256u;  // dev: grid (2 = no zero fill)
     hipLaunchKernelGGL(tile_countorder2_kernel, dim3(og), dim3(1024), 0, st, (const uint32_t *)rbm,

@@ -59,9 +59,8 @@ constexpr int ORD_LDS_TILES = 16384;
 // lpb[q]: parts (log2) of a tile of bucket q; ghist: tiles per (band, bucket) (bucket kernels);
 // bk: the buckets, in LDS when nt <= ORD_LDS_TILES.  Shared scratch: sb[8*32], sx[32].  All
 // threads of the (single) workgroup call it.
-__device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, const int *__restrict__ ghist,
-                                            const uint8_t *__restrict__ bk, int nt, int32_t *__restrict__ order,
-                                            int *__restrict__ nitems, uint64_t *dbg = nullptr) {
+__device__ __forceinline__ void place_prefix(int *sb, int *sx, const int *lpb, const int *__restrict__ ghist,
+                                             int *__restrict__ nitems) {
   __syncthreads();  // lpb / staged buckets written
   // per band, the exclusive prefix over buckets, heaviest first: one lane per (band, bucket),
   // a 32-lane segmented scan (two bands per wave)
@@ -97,6 +96,21 @@ __device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, co
     if (nitems) *nitems = N;
   }
   __syncthreads();
+}
+
+// position of band g's item of rank r (heaviest first) after place_prefix
+__device__ __forceinline__ int place_pos(const int *sx, int g, int r) {
+  if (r < sx[g]) return r * 8 + g;
+  const int j = sx[16 + g] + r - sx[g];  // the j-th overflow item takes the j-th free position
+  int x = 0;
+  while (x < 7 && sx[24 + x + 1] <= j) x++;
+  return (sx[8 + x] + j - sx[24 + x]) * 8 + x;
+}
+
+__device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, const int *__restrict__ ghist,
+                                            const uint8_t *__restrict__ bk, int nt, int32_t *__restrict__ order,
+                                            int *__restrict__ nitems, uint64_t *dbg = nullptr) {
+  place_prefix(sb, sx, lpb, ghist, nitems);
   if (dbg && threadIdx.x == 0) dbg[2] = stamp_wall();
   // the tiles' ranks in their (band, bucket): one LDS atomic per distinct key of a wave (a wave's
   // tiles are consecutive, so they share a band and mostly a few buckets; one returning atomic per
@@ -123,19 +137,7 @@ __device__ __forceinline__ void place_items(int *sb, int *sx, const int *lpb, co
     }
     if (key < 0) continue;
     const int np = 1 << lp;
-    for (int k = 0; k < np; k++) {
-      const int r = r0 + k;
-      int pos;
-      if (r < sx[g]) {
-        pos = r * 8 + g;
-      } else {  // the j-th overflow item takes the j-th free position
-        const int j = sx[16 + g] + r - sx[g];
-        int x = 0;
-        while (x < 7 && sx[24 + x + 1] <= j) x++;
-        pos = (sx[8 + x] + j - sx[24 + x]) * 8 + x;
-      }
-      order[pos] = u | (k << 24) | (lp << 28);
-    }
+    for (int k = 0; k < np; k++) order[place_pos(sx, g, r0 + k)] = u | (k << 24) | (lp << 28);
   }
 }
 
@@ -169,10 +171,9 @@ inline int soft_items_bound(int nt, int lp_min, SoftSplit sp) {
   auto extra = [&](int lp, int cap) { return lp > lp_min ? cap * ((1 << lp) - (1 << lp_min)) : 0; };
   return (nt << lp_min) + extra(2, sp.cap4) + extra(3, sp.cap8);
 }
-__device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, const uint8_t *__restrict__ bk,
-                                                 const int *__restrict__ ghist, int nt, int32_t *__restrict__ order,
-                                                 int lp_min, int *__restrict__ nitems, SoftSplit sp,
-                                                 int skip_empty = 0, uint64_t *dbg = nullptr) {
+// parts (log2) per bucket of the soft mask's tiles; ghist (band, bucket) tile counts; sx scratch
+__device__ __forceinline__ void soft_parts(int *sx, int *lpb, const int *__restrict__ ghist, int lp_min, SoftSplit sp,
+                                           int skip_empty) {
   // tiles per bucket summed over the bands (one lane per bucket), then the caps walked
   // serially from the heaviest bucket down on LDS values
   if (threadIdx.x < ORD_BUCKETS) {
@@ -197,7 +198,14 @@ __device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, con
       lpb[q] = q == 0 && skip_empty ? -1 : lp;  // skip_empty: tiles without candidate faces get no item
     }
   }
-  __syncthreads();  // sx is reused by place_items
+  __syncthreads();  // sx is reused by place_prefix
+}
+
+__device__ __forceinline__ void order_soft_items(int *sb, int *sx, int *lpb, const uint8_t *__restrict__ bk,
+                                                 const int *__restrict__ ghist, int nt, int32_t *__restrict__ order,
+                                                 int lp_min, int *__restrict__ nitems, SoftSplit sp,
+                                                 int skip_empty = 0, uint64_t *dbg = nullptr) {
+  soft_parts(sx, lpb, ghist, lp_min, sp, skip_empty);
   place_items(sb, sx, lpb, ghist, bk, nt, order, nitems, dbg);
 }
 
@@ -371,6 +379,157 @@ static __global__ void __launch_bounds__(1024) tile_countorder2_kernel(
     order_items(sb, sx, lpb, hist, sbk, nt, order0, 0, split_from, split_log2, nitems0, dbg);
   __syncthreads();
   if (dbg && threadIdx.x == 0) dbg[3] = stamp_wall();
+}
+
+// ---- Chip-wide count and order of both bitmaps (kl_dibr_forward; replaces tile_countorder2_kernel,
+// whose two ordering workgroups counted 2 x 2,048 tiles alone: 13.9 us at cfg3, 7.6 of it the
+// count).  Workgroups [0, nb) count the rasterizer's bitmap, [nb, 2 nb) the soft mask's, one tile
+// per thread; each computes its tiles' ranks within (band, bucket) in tile order (per-wave counts
+// in LDS), then publishes its (band, bucket) histogram and every tile's (rank << 8 | bucket) with
+// sc1 stores and adds to its bitmap's ticket (MI355X_MICROARCH.md hand-off table, first row: every
+// storing wave waits vmcnt(0), a workgroup barrier, one lane's agent-scope add; the workgroup
+// whose add comes last loads everything sc1).  That last workgroup turns the histograms into each
+// workgroup's base per key (tile order again: the same ranks place_items gives), parts and
+// prefixes (place_prefix), and writes the items at place_pos -- the same order as before.
+// Workgroups [2 nb, grid) zero `zacc` (the backward's soft accumulator) and `zero` meanwhile.
+constexpr int CO_THREADS = 512;
+constexpr int CO_MAX_BLOCKS = ORD_LDS_TILES / CO_THREADS;  // count workgroups per bitmap
+struct CountOrderArgs {
+  const uint32_t *bm[2];
+  int words, nt, nb;
+  uint32_t *pk[2];      // per tile: rank in its workgroup and key << 8 | bucket
+  int *whist[2];        // per count workgroup: (band, bucket) histogram [nb][ORD_HIST]
+  unsigned *ticket;     // [2], zero on entry; left zero
+  int32_t *order[2];
+  int *nitems[2];
+  int split_from, split_log2;  // the rasterizer's parts
+  int lp_min1, skip_empty1;    // the soft mask's
+  SoftSplit sp;
+  int *zero;
+  int nzero;
+  double *zacc;
+  size_t zn;
+};
+
+static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel(CountOrderArgs a) {
+  __shared__ int s_wk[CO_THREADS / 64][ORD_HIST];  // per-wave key counts; the last workgroup: [nb][ORD_HIST] bases
+  __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS], hist[ORD_HIST];
+  __shared__ int s_last;
+  extern __shared__ int s_big[];  // last workgroup: [nb][ORD_HIST] per-workgroup bases
+  const int nb = a.nb, nt = a.nt;
+  if ((int)blockIdx.x >= 2 * nb) {
+    const int part = blockIdx.x - 2 * nb, nparts = gridDim.x - 2 * nb;
+    if (part == 0 && a.zero)
+      for (int i = threadIdx.x; i < a.nzero; i += blockDim.x) a.zero[i] = 0;
+    if (a.zacc) zero_doubles_share(a.zacc, a.zn, part, nparts);
+    return;
+  }
+  const int which = (int)blockIdx.x >= nb ? 1 : 0, blk = (int)blockIdx.x - which * nb;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int t = blk * CO_THREADS + threadIdx.x;
+  for (int i = threadIdx.x; i < (CO_THREADS / 64) * ORD_HIST; i += blockDim.x) (&s_wk[0][0])[i] = 0;
+  // the tile's candidate-chunk count: its words (word-major, coalesced across the wave), raw buffer
+  // loads from a clamped tile (words past the bitmap read as 0), all in flight together
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)a.bm[which], (short)0, a.words * nt * 4, 0x00020000);
+  const int tc = t < nt ? t : nt - 1;
+  unsigned n = 0;
+  for (int k0 = 0; k0 < a.words; k0 += 32) {
+    uint32_t x[32];
+#pragma unroll
+    for (int u = 0; u < 32; u++) x[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, tc * 4, (k0 + u) * nt * 4, 0);
+#pragma unroll
+    for (int u = 0; u < 32; u++) n += __popc(x[u]);
+  }
+  const int q = 31 - __clz(n + 1u);
+  const int key = t < nt ? tile_band(t, nt) * ORD_BUCKETS + q : -1;
+  // rank within the workgroup for its key, in tile order: the wave's own rank (same-key lanes
+  // below this one) now, the earlier waves' counts after the barrier
+  int wrank = 0;
+  {
+    uint64_t todo = ballot(key >= 0);
+    while (todo) {
+      const int kl = __builtin_ctzll(todo);
+      const int kk = __builtin_amdgcn_readlane(key, kl);
+      const uint64_t same = ballot(key == kk) & todo;
+      todo &= ~same;
+      if (key == kk)
+        wrank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
+      if (lane == kl) s_wk[wid][kk] = __popcll(same);
+    }
+  }
+  __syncthreads();
+  if (key >= 0) {
+    int r = wrank;
+    for (int w = 0; w < wid; w++) r += s_wk[w][key];
+    __hip_atomic_store(a.pk[which] + t, ((uint32_t)r << 8) | (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int k = threadIdx.x; k < ORD_HIST; k += blockDim.x) {
+    int h = 0;
+#pragma unroll
+    for (int w = 0; w < CO_THREADS / 64; w++) h += s_wk[w][k];
+    __hip_atomic_store(a.whist[which] + blk * ORD_HIST + k, h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.ticket + which, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (unsigned)nb - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // ---- the last workgroup of this bitmap: bases per (workgroup, key), totals, parts, prefix, items.
+  //      Every global read here is sc1 and issued eight at a time (one round trip per batch).
+  constexpr int BATCH = 8;
+  const int nh = nb * ORD_HIST;
+  for (int i0 = threadIdx.x; i0 < nh; i0 += BATCH * blockDim.x) {
+    int v[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; u++) {
+      const int i = i0 + u * blockDim.x;
+      v[u] = __hip_atomic_load(a.whist[which] + (i < nh ? i : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; u++)
+      if (i0 + u * (int)blockDim.x < nh) s_big[i0 + u * blockDim.x] = v[u];
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(a.ticket + which, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  for (int k = threadIdx.x; k < ORD_HIST; k += blockDim.x) {
+    int run = 0;
+    for (int b = 0; b < nb; b++) {
+      const int h = s_big[b * ORD_HIST + k];
+      s_big[b * ORD_HIST + k] = run;
+      run += h;
+    }
+    hist[k] = run;
+  }
+  __syncthreads();
+  if (which == 0) {
+    if (threadIdx.x < ORD_BUCKETS) lpb[threadIdx.x] = (int)threadIdx.x >= a.split_from ? a.split_log2 : 0;
+  } else {
+    soft_parts(sx, lpb, hist, a.lp_min1, a.sp, a.skip_empty1);
+  }
+  place_prefix(sb, sx, lpb, hist, a.nitems[which]);
+  int32_t *order = a.order[which];
+  for (int u0 = threadIdx.x; u0 < nt; u0 += BATCH * blockDim.x) {
+    uint32_t v[BATCH];
+#pragma unroll
+    for (int j = 0; j < BATCH; j++) {
+      const int u = u0 + j * blockDim.x;
+      v[j] = __hip_atomic_load(a.pk[which] + (u < nt ? u : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int j = 0; j < BATCH; j++) {
+      const int u = u0 + j * blockDim.x;
+      const int qq = (int)(v[j] & 0xffu), lp = u < nt ? lpb[qq] : -1;
+      if (lp < 0) continue;
+      const int g = tile_band(u, nt), kk = g * ORD_BUCKETS + qq;
+      const int np = 1 << lp;
+      const int r0 = sb[kk] + (s_big[(u / CO_THREADS) * ORD_HIST + kk] + (int)(v[j] >> 8)) * np;
+      for (int k = 0; k < np; k++) order[place_pos(sx, g, r0 + k)] = u | (k << 24) | (lp << 28);
+    }
+  }
 }
 
 }  // namespace kl

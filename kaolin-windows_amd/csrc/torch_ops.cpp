@@ -63,24 +63,101 @@ void *ptr(const at::Tensor &t) { return t.defined() ? t.data_ptr() : nullptr; }
 // (grad mode on inside the backward) rather than hand back gradients that silently drop its
 // second-order term.  The nodes whose reference is plain torch (mask_iou, prepare_vertices,
 // texture_mapping) instead take the reference chain's own differentiable gradient then
-// (kaolin/_double_backward.py), as the reference would give.
+// (the *_chain functions below), as the reference would give.
 void no_double_backward(const char *op) {
   TORCH_CHECK(!at::GradMode::is_enabled(), op,
               ": backward with create_graph=True is not supported (the backward is one HIP call and is not "
               "differentiable)");
 }
 
-// kaolin._double_backward.<fn>(*args) -> its list of gradients (None -> undefined)
-template <typename... Args>
-variable_list torch_chain_grads(const char *fn, Args &&...args) {
-  pybind11::gil_scoped_acquire gil;
-  pybind11::object r = pybind11::module_::import("kaolin._double_backward").attr(fn)(std::forward<Args>(args)...);
-  variable_list out;
-  for (auto item : r) out.push_back(item.is_none() ? at::Tensor() : item.cast<at::Tensor>());
-  return out;
+// The reference's torch chains (kaolin/_double_backward.py restates them for the Python nodes), in
+// ATen ops: the same kernels the Python front-ends' torch fallbacks dispatch to, so the gradients
+// taken through them are the reference's.  No Python here: the backward runs on the autograd
+// engine's device thread.
+// Every op is its own statement, in the order Python evaluates the reference's expressions: the
+// autograd engine orders the adds of a tensor's gradients by node creation order, and C++ leaves
+// the order of a call's argument expressions unspecified.
+at::Tensor mask_iou_chain(const at::Tensor &lhs, const at::Tensor &rhs) {  // metrics/render.py:34-37
+  const int64_t B = lhs.size(0);
+  const at::Tensor sil_mul = lhs * rhs;
+  const at::Tensor sil_add = lhs + rhs;
+  const at::Tensor up = at::sum(sil_mul.reshape({B, -1}), 1);
+  const at::Tensor diff = sil_add - sil_mul;
+  const at::Tensor down = at::sum(diff.reshape({B, -1}), 1);
+  const at::Tensor den = down + 1e-10;
+  const at::Tensor iou = up / den;
+  return at::rsub(at::mean(iou), 1.0);
 }
 
-pybind11::object opt_obj(const at::Tensor &t) { return t.defined() ? pybind11::cast(t) : pybind11::none(); }
+at::Tensor by_faces(const at::Tensor &x, const at::Tensor &faces) {  // index_vertices_by_faces
+  const at::Tensor inp = x.unsqueeze(2).expand({-1, -1, faces.size(-1), -1});
+  const at::Tensor idx = faces.unsqueeze(0).unsqueeze(-1).expand({x.size(0), -1, -1, x.size(-1)});
+  return at::gather(inp, 1, idx);
+}
+
+// render/mesh/utils.py:160-175 (rotate_translate_points / pad @ transform, perspective_camera,
+// index_vertices_by_faces, face_normals(unit=True))
+std::vector<at::Tensor> prepare_chain(const at::Tensor &v, const at::Tensor &faces, const at::Tensor &proj,
+                                      const at::Tensor &rot, const at::Tensor &trans, const at::Tensor &xf) {
+  at::Tensor vc;
+  if (xf.defined()) {
+    const at::Tensor padded = at::constant_pad_nd(v, {0, 1}, 1.0);
+    vc = at::matmul(padded, xf);
+  } else {
+    const at::Tensor tv = trans.view({-1, 1, 3});
+    const at::Tensor translated = v - tv;
+    const at::Tensor rt = rot.permute({0, 2, 1});
+    vc = at::matmul(translated, rt);
+  }
+  const at::Tensor pv = proj.view({-1, 1, 3});
+  const at::Tensor pp = vc * pv;
+  const at::Tensor pxy = pp.slice(2, 0, 2);
+  const at::Tensor pz = pp.slice(2, 2, 3);
+  const at::Tensor vi = pxy / pz;
+  const at::Tensor fvc = by_faces(vc, faces);
+  const at::Tensor fvi = by_faces(vi, faces);
+  const at::Tensor c1 = fvc.select(2, 1);
+  const at::Tensor c0 = fvc.select(2, 0);
+  const at::Tensor e0 = c1 - c0;
+  const at::Tensor c2 = fvc.select(2, 2);
+  const at::Tensor c0b = fvc.select(2, 0);
+  const at::Tensor e1 = c2 - c0b;
+  const at::Tensor n = at::cross(e0, e1, 2);
+  const at::Tensor len = at::linalg_vector_norm(n, 2, at::IntArrayRef{2}, true);
+  const at::Tensor den = len + 1e-10;
+  return {fvc, fvi, n / den};
+}
+
+at::Tensor texture_chain(const at::Tensor &coords, const at::Tensor &tex, int64_t mode) {  // utils.py:64-75
+  const int64_t B = coords.size(0);
+  const at::Tensor cl = at::clamp(coords.reshape({B, -1, 1, 2}), 0., 1.);
+  const at::Tensor c2 = cl * 2;
+  at::Tensor c = c2 - 1;
+  const at::Tensor ny = -c.select(3, 1);
+  c.select(3, 1).copy_(ny);
+  const at::Tensor out = at::grid_sampler(tex, c, mode == 1 ? 0 : 1, /*border*/ 1, false);
+  return out.permute({0, 2, 3, 1}).reshape({B, -1, tex.size(1)});
+}
+
+// d outputs / d inputs with the graph kept (create_graph): undefined where an input needs none
+variable_list chain_grads(const variable_list &outs, const variable_list &gouts, const variable_list &inputs) {
+  variable_list live, o, g;
+  for (const auto &x : inputs)
+    if (x.defined() && x.requires_grad()) live.push_back(x);
+  for (size_t k = 0; k < outs.size(); k++)
+    if (gouts[k].defined()) {
+      o.push_back(outs[k]);
+      g.push_back(gouts[k]);
+    }
+  variable_list res(inputs.size());
+  if (live.empty() || o.empty()) return res;
+  const variable_list got = torch::autograd::grad(o, live, g, /*retain_graph=*/true, /*create_graph=*/true,
+                                                  /*allow_unused=*/true);
+  size_t j = 0;
+  for (size_t k = 0; k < inputs.size(); k++)
+    if (inputs[k].defined() && inputs[k].requires_grad()) res[k] = got[j++];
+  return res;
+}
 
 struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
   static variable_list forward(AutogradContext *ctx, int64_t height, int64_t width, at::Tensor fvz, at::Tensor fvi,
@@ -192,7 +269,7 @@ struct MaskIou : public torch::autograd::Function<MaskIou> {
     if (!need_l && !need_r) return out;
     at::Tensor g = grads[0].defined() ? grads[0].contiguous() : at::ones({}, saved[0].options());
     if (at::GradMode::is_enabled()) {  // create_graph: the reference's torch gradient
-      auto r = torch_chain_grads("mask_iou", saved[0], saved[1], g);
+      const auto r = chain_grads({mask_iou_chain(saved[0], saved[1])}, {g}, {saved[0], saved[1]});
       out[0] = r[0];
       out[1] = r[1];
       return out;
@@ -247,13 +324,12 @@ struct PrepareVertices : public torch::autograd::Function<PrepareVertices> {
     if (!grads[0].defined() && !grads[1].defined() && !grads[2].defined()) return out;
     const bool has_xf = ctx->saved_data["has_xf"].toBool();
     if (at::GradMode::is_enabled()) {  // create_graph: the reference's torch gradient
-      auto g = torch_chain_grads("prepare_vertices", saved[0], saved[1], saved[2], opt_obj(saved[3]),
-                                 opt_obj(saved[4]), opt_obj(saved[5]), opt_obj(grads[0]), opt_obj(grads[1]),
-                                 opt_obj(grads[2]));
+      const auto g = chain_grads(prepare_chain(saved[0], saved[1], saved[2], saved[3], saved[4], saved[5]),
+                                 {grads[0], grads[1], grads[2]}, {saved[0], saved[2], saved[3], saved[4], saved[5]});
       out[0] = g[0];
-      out[2] = g[2];
-      out[3] = has_xf ? g[5] : g[3];
-      if (!has_xf) out[4] = g[4];
+      out[2] = g[1];
+      out[3] = has_xf ? g[4] : g[2];
+      if (!has_xf) out[4] = g[3];
       return out;
     }
     const at::Tensor verts = saved[0].contiguous(), fc = saved[1].contiguous(), pj = saved[2].contiguous();
@@ -325,7 +401,8 @@ struct TextureMapping : public torch::autograd::Function<TextureMapping> {
     variable_list out(4);
     if ((!need_c && !need_t) || !grads[0].defined()) return out;
     if (at::GradMode::is_enabled()) {  // create_graph: the reference's torch gradient
-      auto g = torch_chain_grads("texture_mapping", saved[0], saved[1], ctx->saved_data["mode"].toInt(), grads[0]);
+      const at::Tensor o = texture_chain(saved[0], saved[1], ctx->saved_data["mode"].toInt());
+      const auto g = chain_grads({o}, {grads[0].reshape(o.sizes())}, {saved[0], saved[1]});
       out[0] = g[0];
       out[1] = g[1];
       return out;
@@ -370,4 +447,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("mask_iou", &mask_iou, "mask_iou's fused node; see kaolin/metrics/render.py");
   m.def("prepare_vertices", &prepare_vertices, "prepare_vertices' node; see kaolin/render/mesh/utils.py");
   m.def("texture_mapping", &texture_mapping, "texture_mapping's node; see kaolin/render/mesh/utils.py");
+  // the double-backward reference chains, exposed for tests (tests/test_cpu_paths.py)
+  m.def("_mask_iou_chain", &mask_iou_chain);
+  m.def("_prepare_chain", [](at::Tensor v, at::Tensor faces, at::Tensor proj, c10::optional<at::Tensor> rot,
+                             c10::optional<at::Tensor> trans, c10::optional<at::Tensor> xf) {
+    return prepare_chain(v, faces, proj, rot.value_or(at::Tensor()), trans.value_or(at::Tensor()),
+                         xf.value_or(at::Tensor()));
+  });
+  m.def("_texture_chain", &texture_chain);
 }

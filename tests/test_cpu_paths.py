@@ -84,3 +84,62 @@ def test_voxelgrid_cpu_f64():
     expected = torch.tensor([[[1., 1., 1.], [0., 0., 0.], [0., 0., 0.]], [[1., 1., 0.], [0., 0., 0.], [0., 0., 0.]],
                              [[1., 0., 0.], [0., 0., 0.], [0., 0., 0.]]], dtype=torch.float64)
     assert torch.equal(grid[0], expected)
+
+
+def _distinct_faces(g, nv, nf):
+    """faces with three distinct vertices each (no zero-area face: its unit normal's second
+    derivative is NaN in the reference too)"""
+    return torch.stack([torch.randperm(nv, generator=g)[:3] for _ in range(nf)])
+
+
+def test_compiled_reference_chains_match_python():
+    """The compiled nodes' double-backward chains (csrc/torch_ops.cpp *_chain, ATen) are the
+    reference's torch chains (the Python front-ends' fallbacks) op for op: outputs, first and
+    second derivatives bit-equal on CPU tensors.  grid_sample's backward has no derivative in
+    torch, so texture_mapping's second derivative raises in both."""
+    from kaolin import _ext
+    e = _ext.get()
+    if e is None:
+        pytest.skip('compiled extension not built')
+    from kaolin.metrics.render import _mask_iou_torch
+    from kaolin.render.mesh.utils import _prepare_vertices_torch, _texture_mapping_torch
+    g = torch.Generator().manual_seed(0)
+
+    def derivs(f, inputs, second=True):
+        xs = [x.clone().requires_grad_(True) for x in inputs]
+        ys = f(*xs)
+        ys = list(ys) if isinstance(ys, (list, tuple)) else [ys]
+        loss = sum((y * (k + 1.5)).sum() for k, y in enumerate(ys))
+        d1 = torch.autograd.grad(loss, xs, create_graph=True, allow_unused=True)
+        out = [y.detach() for y in ys] + [d.detach() for d in d1 if d is not None]
+        if second:
+            out += [d for d in torch.autograd.grad(sum((d * d).sum() for d in d1 if d is not None), xs,
+                                                   allow_unused=True) if d is not None]
+        return out
+
+    def check(f1, f2, inputs, second=True):
+        a, b = derivs(f1, inputs, second), derivs(f2, inputs, second)
+        assert len(a) == len(b)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+
+    a, b = torch.rand((2, 8, 8), generator=g), torch.rand((2, 8, 8), generator=g)
+    check(e._mask_iou_chain, _mask_iou_torch, [a, b])
+    v = torch.rand((2, 30, 3), generator=g)
+    f = _distinct_faces(g, 30, 40)
+    proj = torch.tensor([[1.8], [1.8], [-1.]])
+    rot = torch.linalg.qr(torch.randn((2, 3, 3), generator=g))[0]
+    trans = torch.tensor([[0., 0., 3.], [0.1, 0., 3.2]])
+    xf = torch.randn((2, 4, 3), generator=g)
+    check(lambda *x: e._prepare_chain(x[0], f, x[1], x[2], x[3], None),
+          lambda *x: _prepare_vertices_torch(x[0], f, x[1], x[2], x[3], None), [v, proj, rot, trans])
+    check(lambda *x: e._prepare_chain(x[0], f, x[1], None, None, x[2]),
+          lambda *x: _prepare_vertices_torch(x[0], f, x[1], None, None, x[2]), [v, proj, xf])
+    uv, tex = torch.rand((2, 5, 7, 2), generator=g), torch.rand((2, 3, 16, 16), generator=g)
+    for mode, code in (('bilinear', 1), ('nearest', 0)):
+        f1 = lambda c, t: e._texture_chain(c, t, code)  # noqa: E731
+        f2 = lambda c, t: _texture_mapping_torch(c, t, mode).reshape(2, -1, 3)  # noqa: E731
+        check(f1, f2, [uv, tex], second=False)
+        for fn in (f1, f2):
+            with pytest.raises(RuntimeError, match='grid_sampler_2d_backward is not implemented'):
+                derivs(fn, [uv, tex])

@@ -735,8 +735,10 @@ def test_compiled_nodes_refuse_double_backward(kal):
 def test_torch_reference_nodes_double_backward(kal, monkeypatch, route):
     """mask_iou, prepare_vertices and texture_mapping are plain torch in the reference, so their
     gradients are differentiable there.  Under create_graph the HIP nodes take the
-    reference chain's gradient (kaolin/_double_backward.py): first AND second derivatives equal
-    the reference chain's own, bit for bit; an ordinary backward stays on the HIP path."""
+    reference chain's gradient (csrc/torch_ops.cpp *_chain; kaolin/_double_backward.py for the
+    Python nodes): first AND second derivatives equal the reference chain's own, bit for bit
+    (texture_mapping: its first derivative; grid_sample's backward has no derivative in torch, so
+    the second raises in both); an ordinary backward stays on the HIP path."""
     from kaolin import _ext
     from kaolin.metrics.render import _mask_iou_torch
     from kaolin.render.mesh.utils import _prepare_vertices_torch, _texture_mapping_torch
@@ -745,39 +747,45 @@ def test_torch_reference_nodes_double_backward(kal, monkeypatch, route):
     else:
         assert _ext.get() is not None
 
-    def both(fn, ref, inputs, consts=()):
-        outs = []
-        for f in (fn, ref):
-            xs = [x.detach().clone().requires_grad_(True) for x in inputs]
-            y = f(*xs, *consts)
-            ys = y if isinstance(y, tuple) else (y,)
-            w = [torch.rand(o.shape, generator=torch.Generator().manual_seed(k), dtype=o.dtype).to(DEV)
-                 for k, o in enumerate(ys)]
-            g = torch.autograd.grad(sum((o * wk).sum() for o, wk in zip(ys, w)), xs, create_graph=True)
-            hv = torch.autograd.grad(sum((gk * gk).sum() for gk in g), xs, allow_unused=True)
-            outs.append((g, hv))
-        (g0, h0), (g1, h1) = outs
-        for p, q in zip(g0 + h0, g1 + h1):
-            assert (p is None and q is None) or torch.equal(p, q)
+    def derivs(f, inputs, second=True):
+        xs = [x.detach().clone().requires_grad_(True) for x in inputs]
+        ys = f(*xs)
+        ys = list(ys) if isinstance(ys, (list, tuple)) else [ys]
+        loss = sum((y * (k + 1.5)).sum() for k, y in enumerate(ys))
+        d1 = torch.autograd.grad(loss, xs, create_graph=True, allow_unused=True)
+        out = [y.detach() for y in ys] + [d.detach() for d in d1 if d is not None]
+        if second:
+            out += [d for d in torch.autograd.grad(sum((d * d).sum() for d in d1 if d is not None), xs,
+                                                   allow_unused=True) if d is not None]
+        return out
+
+    def check(f1, f2, inputs, second=True):
+        a, b = derivs(f1, inputs, second), derivs(f2, inputs, second)
+        assert len(a) == len(b)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
 
     gen = torch.Generator().manual_seed(4)
     a = torch.rand((2, 8, 8), generator=gen).to(DEV)
     b = torch.rand((2, 8, 8), generator=gen).to(DEV)
-    both(kal.metrics.render.mask_iou, _mask_iou_torch, [a, b])
+    check(kal.metrics.render.mask_iou, _mask_iou_torch, [a, b])
     verts = torch.rand((2, 30, 3), generator=gen).to(DEV)
-    faces = torch.randint(0, 30, (40, 3), generator=gen).to(DEV)
+    faces = torch.stack([torch.randperm(30, generator=gen)[:3] for _ in range(40)]).to(DEV)
     proj = torch.tensor([[1.8], [1.8], [-1.]], device=DEV)
     rot = torch.linalg.qr(torch.randn((2, 3, 3), generator=gen))[0].to(DEV)
     trans = torch.tensor([[0., 0., 3.], [0.1, 0., 3.2]], device=DEV)
-    both(lambda *x: kal.render.mesh.prepare_vertices(x[0], faces, x[1], x[2], x[3]),
-         lambda *x: _prepare_vertices_torch(x[0], faces, x[1], x[2], x[3], None), [verts, proj, rot, trans])
+    check(lambda *x: kal.render.mesh.prepare_vertices(x[0], faces, x[1], x[2], x[3]),
+          lambda *x: _prepare_vertices_torch(x[0], faces, x[1], x[2], x[3], None), [verts, proj, rot, trans])
     uv = torch.rand((2, 5, 7, 2), generator=gen).to(DEV)
     tex = torch.rand((2, 3, 16, 16), generator=gen).to(DEV)
     for mode in ('bilinear', 'nearest'):
-        both(lambda c, t: kal.render.mesh.texture_mapping(c, t, mode), lambda c, t: _texture_mapping_torch(c, t, mode),
-             [uv, tex])
-    # an ordinary backward stays on the HIP node (bit-equal to the reference chain is not expected:
-    # the HIP sums are double, rounded once)
+        f1 = lambda c, t: kal.render.mesh.texture_mapping(c, t, mode)  # noqa: E731
+        f2 = lambda c, t: _texture_mapping_torch(c, t, mode)  # noqa: E731
+        check(f1, f2, [uv, tex], second=False)
+        for fn in (f1, f2):
+            with pytest.raises(RuntimeError, match='grid_sampler_2d_backward is not implemented'):
+                derivs(fn, [uv, tex])
+    # an ordinary backward stays on the HIP node
     x = a.clone().requires_grad_(True)
     torch.autograd.grad(kal.metrics.render.mask_iou(x, b), x)
 
