@@ -965,8 +965,9 @@ def cfg4_leg(device, steps):
     del grid_h
     ms_spc = _wall_ms(spc, n_steps)
     vox_bytes = 4 * R ** 3 + 12 * V + 24 * F
-    # sum_l 28 N_l + sum_{l>=1} 16 N_l + N_L (32 + 36 + 8) + 9 * nodes
-    spc_bytes = sum(28 * n for n in N) + sum(16 * n for n in N[1:]) + N[-1] * (32 + 36 + 8) + 9 * nodes
+    # SURVEY.md §8d (the reference's algorithm, sort and dedup included): an effective rate only
+    survey_spc_bytes = sum(28 * n for n in N) + sum(16 * n for n in N[1:]) + N[-1] * (32 + 36 + 8) + 9 * nodes
+    spc_bytes = m2s_build_bytes(N, F, nodes, leaves)
     return {'metric': 'cfg4: trianglemeshes_to_voxelgrids R=512 + unbatched_mesh_to_spc L=9, 200k-face sphere (f32)',
             'voxelgrid': {'ms': round(ms_vox, 3), 'occupied': n_occ, 'bytes': vox_bytes,
                           'host_sized': {'ms': round(ms_vox_host, 3), 'equal': vox_equal},
@@ -977,10 +978,38 @@ def cfg4_leg(device, steps):
                             'bytes': spc_bytes,
                             'roofline': {'bound': 'hbm', 'achieved': round(spc_bytes / (ms_spc * 1e-3) / 1e9, 1),
                                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                                         'frac': round(spc_bytes / (ms_spc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
+                                         'frac': round(spc_bytes / (ms_spc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                         'bytes_model': 'the node-rank algorithm (spc.hip): per pair its key, face, '
+                                                        'triangle, node point and scan entry, child pairs written, '
+                                                        '~31 B per node for the level scans, 52 B per leaf',
+                                         'survey_formula': {
+                                             'bytes': survey_spc_bytes,
+                                             'achieved': round(survey_spc_bytes / (ms_spc * 1e-3) / 1e9, 1),
+                                             'frac': round(survey_spc_bytes / (ms_spc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                             'note': 'SURVEY.md §8d prices the reference algorithm (sort, dedup); '
+                                                     'an effective rate: this build moves none of those bytes'}}},
             'timing': 'wall clock per call (median of runs); voxelgrid: device-counted levels, one status read; '
                       'voxelgrid.host_sized and mesh_to_spc: incl. the per-level host count reads',
             'spc': (octree, fidx, bary)}
+
+
+def m2s_build_bytes(N, F, nodes, leaves):
+    """Bytes the node-rank mesh_to_spc (csrc/spc.hip, m2s_*_kernel) moves at cfg4, from its per-level
+    proposal counts N (N[0] = F faces; N[l] = 8 x the passing (node, face) pairs of level l - 1):
+    the root test reads every triangle (36 B) and writes its passing pairs (8 B); each level's
+    node kernel reads a pair (key + face 8 B), its triangle (36 B), its node's point (8 B), scan
+    entry (4 B) and parent octree byte (1 B), and writes the passing children's pairs (8 B) and
+    child flags (1 B); the level scans read each node's child slots (8 B) and write its octree
+    byte, scan entry, its children's points and cleared slots (~31 B per node over the levels);
+    the leaves read their 8 least-face slots (32 B) and write face index and barycentrics (16 B),
+    plus the last level's least-face atomics (4 B per leaf)."""
+    pairs = [n // 8 for n in N[1:]]  # pairs of levels 0 .. L-1
+    b = F * 36 + pairs[0] * 8
+    for lvl in range(1, len(N)):
+        b += pairs[lvl - 1] * (8 + 36 + 8 + 4 + 1)
+        if lvl < len(pairs):
+            b += pairs[lvl] * (8 + 1)
+    return b + nodes * 31 + leaves * (32 + 16 + 4)
 
 
 def cfg4_cpu_leg(device, stride=32):
@@ -1033,16 +1062,39 @@ def raytrace_leg(device, steps, spc_tuple):
                    and torch.equal(fd[:hits], depth))
     ms_fixed = _event_ms(rtf, max(3, steps // 4))
     R = n * n
-    nbytes = 24 * R + sum(31 * per_level[lv] + 8 * (per_level[lv + 1] if lv + 1 <= L else 0)
-                          for lv in range(L + 1)) + per_level[L] * (16 + 4)
+    # SURVEY.md §8d's raytrace model (kept as survey_formula)
+    survey_bytes = 24 * R + sum(31 * per_level[lv] + 8 * (per_level[lv + 1] if lv + 1 <= L else 0)
+                                for lv in range(L + 1)) + per_level[L] * (16 + 4)
+    # the fused level march (spc.hip rt_level_kernel): level l tests its candidates (the hit
+    # nodes' children of level l - 1: popcount of their octree bytes) -- nugget 8 B (none at level
+    # 0: the ray itself), ray 24 B, node point 6 B, octree byte 1 B -- and writes each hit's
+    # children (8 B each; its exsum entry 4 B read); the target level writes nugget + depth (12 B)
+    cand = [R]
+    for lv in range(L):
+        _, pidx = kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], exsum, o, d, lv, return_depth=False)
+        cand.append(int(_popcount_u8(octree[pidx.long()]).sum()))
+    nbytes = sum(c * ((8 if lv else 0) + 24 + 6 + 1) for lv, c in enumerate(cand)) + \
+        sum(per_level[lv] * 4 + cand[lv + 1] * 8 for lv in range(L)) + per_level[L] * 12
     return {'metric': 'unbatched_raytrace Mrays/s (cfg4 SPC level 9, 512x512 rays, depth)',
             'value': round(R / (ms * 1e-3) / 1e6, 2), 'ms': round(ms, 4), 'hits': hits, 'hits_per_level': per_level,
             'bytes': nbytes, 'timing': 'wall clock per call incl. the per-level host count reads',
             'fixed_capacity': {'value': round(R / (ms_fixed * 1e-3) / 1e6, 2), 'ms': round(ms_fixed, 4),
                                'capacity': cap, 'equal_to_host_sized': bool(fixed_equal),
                                'timing': 'HIP events over back-to-back calls (nothing read back)'},
+            'candidates_per_level': cand,
             'roofline': {'bound': 'hbm', 'achieved': round(nbytes / (ms * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}
+                         'unit': 'GB/s', 'frac': round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         'bytes_model': 'the fused level march: per candidate nugget / ray / point / octree byte, '
+                                        'per hit its children and exsum entry, per target hit nugget + depth',
+                         'survey_formula': {'bytes': survey_bytes,
+                                            'achieved': round(survey_bytes / (ms * 1e-3) / 1e9, 1),
+                                            'frac': round(survey_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}}
+
+
+def _popcount_u8(t):
+    """per-entry popcounts of a uint8 tensor (numpy)"""
+    import numpy as np
+    return np.unpackbits(t.cpu().numpy().astype(np.uint8).reshape(-1, 1), axis=1).sum(1)
 
 
 # ----------------------------------------------------------------------------- deftet / check_sign

@@ -54,8 +54,11 @@ typedef void *(*kl_alloc_fn)(void *ctx, size_t bytes);
  *    kl_soft_mask_compact_bwd_workspace_bytes gained num_faces.
  * 3: kl_dibr_forward / kl_dibr_backward take a state buffer of kl_dibr_state_bytes() bytes
  *    where they took one scratch int32 (the forward lists the backward's work items and zeroes
- *    its accumulator there); added kl_unbatched_triangle_distance_backward_sums. */
-#define KL_ABI_VERSION 3
+ *    its accumulator there); added kl_unbatched_triangle_distance_backward_sums.
+ * 4: kl_dibr_backward takes `soft_acc` (kl_dibr_soft_acc_bytes(): zero on entry, left zero on
+ *    return) for the soft mask's per-face sums, which the forward's state no longer holds (the
+ *    forward zeroes nothing per call); added kl_sided_distance_backward_sums. */
+#define KL_ABI_VERSION 4
 
 const char *kl_last_error(void);
 int kl_abi_version(void);
@@ -216,13 +219,15 @@ int kl_dibr_soft_mask_backward_compact(kl_dtype dtype, int batch, int height, in
  * its face index.  Outputs: interpolated_features (B,H,W,D), face_idx (B,H,W) int64,
  * output_weights (B,H,W,3), soft_mask (B,H,W), and the compact soft-mask state (hits,
  * rec_face, rec_prob, seg_tot as above, and `state`: kl_dibr_state_bytes() bytes, no
- * initialisation needed, in which the forward lists the backward's soft-mask work items and
- * zeroes its double accumulator).  The backward writes grad_face_vertices_image /
- * grad_face_features (every face): the soft-mask terms are summed in double first (into the
- * state's accumulator), then the gather writes each face's gradient as the rounded sum of its
- * own terms (double) plus the soft mask's rounded sum -- autograd's add of the two gradients in
- * the reference (grad_soft_mask may be NULL).  The backward leaves the state as the forward
- * left it (the gather zeroes each sum it reads), so a retained second backward is the same.
+ * initialisation needed, in which the forward lists the backward's soft-mask work items).  The
+ * backward writes grad_face_vertices_image / grad_face_features (every face): the soft-mask terms
+ * are summed in double first into `soft_acc` (kl_dibr_soft_acc_bytes() bytes, ZERO on entry: per
+ * face 8 doubles and a touched flag), then the gather writes each face's gradient as the rounded
+ * sum of its own terms (double) plus the soft mask's rounded sum -- autograd's add of the two
+ * gradients in the reference (grad_soft_mask may be NULL; soft_acc may then be NULL too).  The
+ * gather reads, re-zeroes and unflags only the faces the soft half touched, so soft_acc is zero
+ * again on return: a caller keeps one per stream and zeroes it once.  The state is left as the
+ * forward left it, so a retained second backward is the same.
  * face_ranges: NULL, or (B*F) x 2 uint32 the forward fills with each face's exact pixel
  * ranges (x0 | x1 << 16, y0 | y1 << 16; empty for invalid faces) for the backward to reuse.
  * feat_dim <= 8.  Workspaces: kl_dibr_workspace_bytes (forward),
@@ -230,6 +235,7 @@ int kl_dibr_soft_mask_backward_compact(kl_dtype dtype, int batch, int height, in
 size_t kl_dibr_workspace_bytes(int batch, int height, int width, int num_faces);
 size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, int num_faces, int knum);
 size_t kl_dibr_state_bytes(int batch, int height, int width, int num_faces, int knum);
+size_t kl_dibr_soft_acc_bytes(int batch, int num_faces);
 int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim, int knum,
                     const void *face_vertices_z, const void *face_vertices_image, const void *face_features,
                     const void *face_normals_z, float sigmainv, double bbox_pad, float multiplier, float eps,
@@ -242,8 +248,8 @@ int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width, int num_f
                      const void *face_normals_z, const void *soft_mask, const uint8_t *hits,
                      const uint32_t *rec_face, const void *rec_prob, const int *seg_tot, float sigmainv,
                      float multiplier, float eps, void *grad_face_vertices_image, void *grad_face_features,
-                     void *state, const uint32_t *face_ranges, void *workspace, size_t workspace_bytes,
-                     kl_stream stream);
+                     void *state, const uint32_t *face_ranges, void *soft_acc, void *workspace,
+                     size_t workspace_bytes, kl_stream stream);
 
 /* dibr_soft_mask.cpp:110-183  dibr_soft_mask_backward_cuda.
  * Output grad_face_vertices_image (B,F,3,2) (fully written): the reference's per-hit float

@@ -29,6 +29,8 @@ extern "C" void kl_dev_set_param(int idx, int value) {
 }
 // Development hook: what the last call took (tests assert a fallback branch ran).
 // 0: mesh_to_spc -- 0 the node-rank path, 1 its per-level fallback (the pair buffers overflowed).
+// 1: raytrace -- 1 the fused march, 2 the fused march truncated and the per-level march rerun,
+//    0 the per-level march alone.
 extern "C" int kl_dev_get_stat(int idx) { return idx >= 0 && idx < 4 ? kl::g_dev_stat[idx] : 0; }
 
 namespace kl {

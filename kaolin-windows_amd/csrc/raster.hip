@@ -1293,9 +1293,12 @@ __device__ __forceinline__ void g2_add(double *__restrict__ part, const T v[6], 
 }
 
 // value q of a face -> its gradient (q < 6: the vertex-coordinate gradient, + the soft mask's sum
-// rounded on its own; else a feature gradient)
-// The soft sums are zeroed again as they are read (only the non-zero ones are written), so the
-// forward's accumulator is zero after every backward: a retained second backward adds into zeros.
+// rounded on its own, sv; else a feature gradient)
+// The soft sums live in kl_dibr_backward's zero-kept accumulator: only faces the soft backward
+// flagged are read, and their sums are zeroed and their flags cleared as they are read, so the
+// accumulator is zero again after every backward (a retained second backward adds into zeros).
+// An unflagged face's soft sum is 0: (T)x + 0.0f is (T)x, since (T)x is never -0.0 (x is +0.0 or a
+// nonzero sum of float terms, a multiple of 2^-149 of magnitude >= 2^-149).
 __device__ __forceinline__ double take_soft(double *__restrict__ soft, int64_t i) {
   const double v = soft[i];
   if (__double_as_longlong(v) != 0) soft[i] = 0.0;
@@ -1303,10 +1306,10 @@ __device__ __forceinline__ double take_soft(double *__restrict__ soft, int64_t i
 }
 
 template <typename T, int MAXD>
-__device__ __forceinline__ void g2_store(int64_t tf, int q, double x, int D, double *__restrict__ soft,
-                                         T *__restrict__ grad_fvi, T *__restrict__ grad_ffeat) {
+__device__ __forceinline__ void g2_store(int64_t tf, int q, double x, int D, double sv, T *__restrict__ grad_fvi,
+                                         T *__restrict__ grad_ffeat) {
   if (q < 6) {
-    grad_fvi[tf * 6 + q] = soft ? (T)x + (T)take_soft(soft, tf * DS_ACC_STRIDE + q) : (T)x;
+    grad_fvi[tf * 6 + q] = (T)x + (T)sv;
   } else {
     const int r = q - 6, ii = r / MAXD, d = r % MAXD;
     if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)x;
@@ -1318,7 +1321,8 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
     const T *__restrict__ grad_feat, const int64_t *__restrict__ face_idx, const T *__restrict__ wts,
     const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
     const T *__restrict__ nz, int B, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
-    T *__restrict__ grad_ffeat, const uint2 *__restrict__ rng, double *__restrict__ soft, int nbig) {
+    T *__restrict__ grad_ffeat, const uint2 *__restrict__ rng, double *__restrict__ soft,
+    uint8_t *__restrict__ sflag, int nbig) {
   constexpr int NV = 6 + 3 * MAXD;
   __shared__ double s_part[4][NV][64];  // per wave: per lane (thread) partial sums, value-major
   __shared__ int s_nbig;
@@ -1373,9 +1377,11 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
         __syncthreads();
         if ((int)threadIdx.x < NV) {
           const int q = threadIdx.x;
+          const bool fl = soft && q < 6 && sflag[bf];
           double x = 0.0;
           for (int t = 0; t < 256; t++) x += s_part[t >> 6][q][t & 63];
-          g2_store<T, MAXD>(bf, q, x, D, soft, grad_fvi, grad_ffeat);
+          g2_store<T, MAXD>(bf, q, x, D, fl ? take_soft(soft, bf * DS_ACC_STRIDE + q) : 0.0, grad_fvi, grad_ffeat);
+          if (fl && q == 0) sflag[bf] = 0;  // after the flag's use: every lane of the wave has read it
         }
         __syncthreads();
 #pragma unroll
@@ -1392,23 +1398,26 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
   int ix0 = 1, ix1 = 0, iy0 = 1, iy1 = 0;
   const bool has = in && range_of(tf, ix0, ix1, iy0, iy1);
   const bool act = has && (int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) <= VIS_SMALL_AREA;
+  // the face's soft-sum flag (all 8 lanes read the same byte)
+  const bool fl = soft && in && sflag[tf];
   if (in && !has) {  // no pixel: zero gradients (+ the soft mask's sums); lane s writes q = s, s + 8, ...
 #pragma unroll
     for (int q = s; q < NV; q += 8) {
       if (q < 6) {
-        grad_fvi[tf * 6 + q] = soft ? (T)0 + (T)take_soft(soft, tf * DS_ACC_STRIDE + q) : (T)0;
+        grad_fvi[tf * 6 + q] = fl ? (T)0 + (T)take_soft(soft, tf * DS_ACC_STRIDE + q) : (T)0;
       } else {
         const int r = q - 6, ii = r / MAXD, d = r % MAXD;
         if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)0;
       }
     }
+    if (fl && s == 0) sflag[tf] = 0;  // after the flag's use
   }
   if (!__any(act)) return;  // wave-uniform
 #pragma unroll
   for (int q = 0; q < NV; q++) part[q * 64] = 0.0;
   // lane s < 6's soft-mask sum, loaded now so that its latency hides behind the walk
   double soft_v = 0.0;
-  if (act && soft && s < 6) soft_v = soft[tf * DS_ACC_STRIDE + s];
+  if (act && fl && s < 6) soft_v = soft[tf * DS_ACC_STRIDE + s];
   if (act) {
     const int b = (int)(tf / F);
     const int64_t f = tf - (int64_t)b * F;
@@ -1476,13 +1485,14 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
       double x = 0.0;
 #pragma unroll
       for (int l = 0; l < 8; l++) x += s_part[wid][q][g0 + l];
-      if (q < 6 && soft) {  // q == s: the prefetched sum, re-zeroed as take_soft does
+      if (q < 6) {  // q == s: the prefetched sum, re-zeroed as take_soft does
         grad_fvi[tf * 6 + q] = (T)x + (T)soft_v;
         if (__double_as_longlong(soft_v) != 0) soft[tf * DS_ACC_STRIDE + q] = 0.0;
       } else {
-        g2_store<T, MAXD>(tf, q, x, D, soft, grad_fvi, grad_ffeat);
+        g2_store<T, MAXD>(tf, q, x, D, 0.0, grad_fvi, grad_ffeat);
       }
     }
+    if (fl && s == 0) sflag[tf] = 0;  // after the flag's use
   }
 }
 
@@ -1518,18 +1528,18 @@ template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
                                      const T *w, const T *fvi, const T *feat, const uint8_t *valid, const T *nz,
                                      float m, float eps, T *gfvi, T *gfeat, int *big, int *nbig, bool zero_nbig,
-                                     const uint2 *rng, double *soft, hipStream_t st) {
+                                     const uint2 *rng, double *soft, uint8_t *sflag, hipStream_t st) {
   const int64_t nf = (int64_t)B * F;
-  if (g_dev_param[7] != 1) {  // dev param 7 = 1: the r03 gather (8 lanes per face, register sums) for A/B
+  if (g_dev_param[7] != 1 || soft) {  // (the r03 gather does not read flagged soft sums)  // dev param 7 = 1: the r03 gather (8 lanes per face, register sums) for A/B
     const int nb = (int)std::min<int64_t>(G2_BIG_BLOCKS, cdiv(nf, 4096));
     if (g_dev_param[8] != 1)  // dev param 8 = 1: read-modify-write partials (A/B: 73 against 48 us at cfg3)
       hipLaunchKernelGGL((rasterize_bwd_gather2_kernel<T, MAXD, true>), dim3((unsigned)(nb + cdiv(nf * 8, 256))),
                          dim3(256), 0, st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat,
-                         rng, soft, nb);
+                         rng, soft, sflag, nb);
     else
       hipLaunchKernelGGL((rasterize_bwd_gather2_kernel<T, MAXD>), dim3((unsigned)(nb + cdiv(nf * 8, 256))), dim3(256),
                          0, st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, rng, soft,
-                         nb);
+                         sflag, nb);
     KL_CHECK_LAUNCH();
     return KL_OK;
   }
@@ -1552,7 +1562,8 @@ template <typename T>
 static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *grad, const int64_t *face_idx,
                                 const void *w, const void *fvi, const void *feat, const uint8_t *valid, const T *nz,
                                 float m, float eps, void *gfvi, void *gfeat, void *ws, size_t ws_bytes, int *nbig,
-                                hipStream_t st, const uint2 *rng = nullptr, double *soft = nullptr) {
+                                hipStream_t st, const uint2 *rng = nullptr, double *soft = nullptr,
+                                uint8_t *sflag = nullptr) {
   const int64_t nf = (int64_t)B * F;
   if (nf == 0) return KL_OK;
   if (D > 8) {  // wide features: the scatter kernel
@@ -1571,15 +1582,15 @@ static int rasterize_bwd_gather(int B, int H, int W, int F, int D, const void *g
   // MAXD = D where it is small (the accumulators are doubles: registers set the occupancy)
   if (D <= 2)
     return rasterize_bwd_gather_maxd<T, 2>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, sflag, st);
   if (D == 3)
     return rasterize_bwd_gather_maxd<T, 3>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, sflag, st);
   if (D <= 4)
     return rasterize_bwd_gather_maxd<T, 4>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                           (T *)gfeat, big, nbig, zero, rng, soft, st);
+                                           (T *)gfeat, big, nbig, zero, rng, soft, sflag, st);
   return rasterize_bwd_gather_maxd<T, 8>(B, H, W, F, D, g, face_idx, wt, fv, ft, valid, nz, m, eps, (T *)gfvi,
-                                         (T *)gfeat, big, nbig, zero, rng, soft, st);
+                                         (T *)gfeat, big, nbig, zero, rng, soft, sflag, st);
 }
 
 // The fused front-end path's forward: the tile rasterizer (dev flag bit 13 selects the
@@ -1751,7 +1762,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   char *state = reinterpret_cast<char *>(s.scratch);
   int *bcnt = reinterpret_cast<int *>(state);
   int2 *bitems = reinterpret_cast<int2 *>(state + S.off_items);
-  double *bacc = reinterpret_cast<double *>(state + S.off_acc);
+  double *bacc = nullptr;  // (ABI 4: the backward's soft accumulator is the caller's, kept zero)
   const size_t P = (size_t)B * H * W;
   if (P == 0 || F == 0) {  // no pixels / no faces: no soft-mask hits, nothing listed
     KL_CHECK_RC(fill_async(bcnt, 0, DibrState::kZeroInts * sizeof(int), st));
@@ -1793,7 +1804,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
       const unsigned og = g_dev_param[9] >= 2 ? (unsigned)g_dev_param[9] : 256u;
       hipLaunchKernelGGL(tile_countorder2_kernel, dim3(og), dim3(1024), 0, st, (const uint32_t *)sbm,
                          (const uint32_t *)sbm, g.words, (int32_t *)nullptr, 0, 0, (int *)nullptr, sorder, nt, lpm,
-                         snitems, soft_split(), 0, bcnt, DibrState::kZeroInts, bacc, (size_t)B * F * DS_ACC_STRIDE,
+                         snitems, soft_split(), 0, bcnt, DibrState::kZeroInts, bacc, (size_t)0,
                          kDevStamps && g_dev_debug ? reinterpret_cast<uint64_t *>(g_dev_debug) + kOrderStampsAt
                                                    : nullptr);
       KL_CHECK_LAUNCH();
@@ -1852,9 +1863,9 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     ca.sp = soft_split();
     ca.zero = bcnt;
     ca.nzero = DibrState::kZeroInts;
-    ca.zacc = bacc;
-    ca.zn = (size_t)B * F * DS_ACC_STRIDE;
-    const unsigned zg = g_dev_param[9] >= 2 ? (unsigned)g_dev_param[9] : 248u;  // zeroing workgroups
+    ca.zacc = nullptr;
+    ca.zn = 0;
+    const unsigned zg = 1u;  // one workgroup zeroes the state's counters
     hipLaunchKernelGGL(tile_countorder_chip_kernel, dim3((unsigned)(2 * nb) + zg), dim3(CO_THREADS),
                        (size_t)nb * ORD_HIST * sizeof(int), st, ca);
     KL_CHECK_LAUNCH();
@@ -1864,7 +1875,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     hipLaunchKernelGGL(tile_countorder2_kernel, dim3(og), dim3(1024), 0, st, (const uint32_t *)rbm,
                        (const uint32_t *)sbm, g.words, items, split_from, split_log2, nitems, sorder, nt,
                        soft_lp_min(K), snitems, soft_split(), 1, bcnt, DibrState::kZeroInts, bacc,
-                       (size_t)B * F * DS_ACC_STRIDE,
+                       (size_t)0,
                        kDevStamps && g_dev_debug ? reinterpret_cast<uint64_t *>(g_dev_debug) + kOrderStampsAt : nullptr);
     KL_CHECK_LAUNCH();
   } else {  // counts (a wave per tile) then orders (dev bit 20: this path, for A/B timing)
@@ -1873,7 +1884,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     KL_CHECK_LAUNCH();
     hipLaunchKernelGGL(tile_order2_kernel, dim3(256), dim3(1024), 0, st, (const uint8_t *)rbk, (const int *)rgh,
                        items, split_from, split_log2, nitems, (const uint8_t *)sbk, (const int *)sgh, sorder, nt,
-                       soft_lp_min(K), snitems, soft_split(), 1, bacc, (size_t)B * F * DS_ACC_STRIDE);
+                       soft_lp_min(K), snitems, soft_split(), 1, bacc, (size_t)0);
     KL_CHECK_LAUNCH();
   }
   uint8_t *defer = reinterpret_cast<uint8_t *>(w + L.off_defer);
@@ -1892,8 +1903,8 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
 template <typename T>
 static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat, const T *grad_mask,
                     const int64_t *face_idx, const T *w, const T *fvi, const T *feat, const T *fnz, const T *mask,
-                    const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *ws,
-                    size_t ws_bytes, hipStream_t st, const uint2 *face_ranges) {
+                    const SoftState<T> &s, float sigmainv, float m, float eps, T *gfvi, T *gfeat, void *soft_acc,
+                    void *ws, size_t ws_bytes, hipStream_t st, const uint2 *face_ranges) {
   KL_REQUIRE(D <= 8, "dibr_rasterization backward: feature dimension > 8 is not supported by the fused path");
   KL_REQUIRE(s.scratch != nullptr, "dibr_rasterization backward: state (kl_dibr_state_bytes) missing");
   // The soft-mask terms first, summed in double into the state's accumulator (zeroed by the
@@ -1904,14 +1915,20 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
   // halves ran on two streams joined by a final add, ~16 us of fork / join gaps in the graph.)
   const DibrState S(B, H, W, F, K);
   char *state = reinterpret_cast<char *>(s.scratch);
-  double *acc = reinterpret_cast<double *>(state + S.off_acc);
   const bool has_soft = grad_mask != nullptr && K > 0 && (int64_t)B * H * W > 0 && (int64_t)B * F > 0;
+  KL_REQUIRE(soft_acc != nullptr || !has_soft, "dibr_rasterization backward: soft accumulator (kl_dibr_soft_acc_bytes) missing");
+  const DibrSoftAcc A(B, F);
+  double *acc = reinterpret_cast<double *>(soft_acc);
+  uint8_t *sflag = has_soft ? reinterpret_cast<uint8_t *>(soft_acc) + A.off_flags : nullptr;
   if (has_soft)
     KL_CHECK_RC(soft_tile_backward_listed<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m,
                                              reinterpret_cast<const int2 *>(state + S.off_items),
-                                             reinterpret_cast<const int *>(state), S.cap, acc, st));
-  return rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi, gfeat,
-                                 ws, ws_bytes, nullptr, st, face_ranges, has_soft ? acc : nullptr);
+                                             reinterpret_cast<const int *>(state), S.cap, acc, sflag, st));
+  const int rc = rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
+                                         gfeat, ws, ws_bytes, nullptr, st, face_ranges, has_soft ? acc : nullptr, sflag);
+  // the accumulator must be zero for the next call: if the gather did not run, clear it here
+  if (rc != KL_OK && has_soft) (void)fill_async(soft_acc, 0, A.bytes, st);
+  return rc;
 }
 }  // namespace kl
 
@@ -1930,6 +1947,8 @@ extern "C" size_t kl_dibr_bwd_workspace_bytes(int batch, int height, int width, 
 extern "C" size_t kl_dibr_state_bytes(int batch, int height, int width, int num_faces, int knum) {
   return DibrState(batch, height, width, num_faces, knum).bytes;
 }
+
+extern "C" size_t kl_dibr_soft_acc_bytes(int batch, int num_faces) { return DibrSoftAcc(batch, num_faces).bytes; }
 
 extern "C" int kl_dibr_forward(kl_dtype dtype, int batch, int height, int width, int num_faces, int feat_dim,
                                int knum, const void *fvz, const void *fvi, const void *feat, const void *fnz,
@@ -1959,22 +1978,22 @@ extern "C" int kl_dibr_backward(kl_dtype dtype, int batch, int height, int width
                                 const void *w, const void *fvi, const void *feat, const void *fnz, const void *mask,
                                 const uint8_t *hits, const uint32_t *rec_face, const void *rec_prob,
                                 const int *seg_tot, float sigmainv, float multiplier, float eps, void *gfvi,
-                                void *gfeat, void *state, const uint32_t *face_ranges, void *ws, size_t ws_bytes,
-                                kl_stream stream) {
+                                void *gfeat, void *state, const uint32_t *face_ranges, void *soft_acc, void *ws,
+                                size_t ws_bytes, kl_stream stream) {
   const uint2 *fr = reinterpret_cast<const uint2 *>(face_ranges);
   if (dtype == KL_F32)
     return dibr_bwd<float>(
         batch, height, width, num_faces, feat_dim, knum, (const float *)grad_feat, (const float *)grad_mask, face_idx,
         (const float *)w, (const float *)fvi, (const float *)feat, (const float *)fnz, (const float *)mask,
         SoftState<float>{(uint8_t *)hits, (uint32_t *)rec_face, (float *)rec_prob, (int *)seg_tot, (int *)state},
-        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, ws, ws_bytes, S(stream), fr);
+        sigmainv, multiplier, eps, (float *)gfvi, (float *)gfeat, soft_acc, ws, ws_bytes, S(stream), fr);
   if (dtype == KL_F64)
     return dibr_bwd<double>(
         batch, height, width, num_faces, feat_dim, knum, (const double *)grad_feat, (const double *)grad_mask,
         face_idx, (const double *)w, (const double *)fvi, (const double *)feat, (const double *)fnz,
         (const double *)mask,
         SoftState<double>{(uint8_t *)hits, (uint32_t *)rec_face, (double *)rec_prob, (int *)seg_tot, (int *)state},
-        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, ws, ws_bytes, S(stream), fr);
+        sigmainv, multiplier, eps, (double *)gfvi, (double *)gfeat, soft_acc, ws, ws_bytes, S(stream), fr);
   set_error("dibr_rasterization backward not implemented for this dtype");
   return KL_E_INVALID;
 }

@@ -227,21 +227,30 @@ int soft_bwd_item_cap(int B, int H, int W, int K);
 template <typename T>
 int soft_tile_backward_listed(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
                               const T *fvi, float sigmainv, float m, const int2 *items, const int *cnt, int cap,
-                              double *acc, hipStream_t st);
+                              double *acc, uint8_t *sflag, hipStream_t st);
 // Per-call state of kl_dibr_forward / kl_dibr_backward (kl_dibr_state_bytes):
 //   [0, 512)   DS_SHARDS item counters; int 128: the r03 gather's big-face counter (dev path)
 //   items      DS_SHARDS x cap backward work items (int2)
-//   acc        the soft mask's per-face double sums (B*F x DS_ACC_STRIDE), zeroed by the forward
 struct DibrState {
   int cap;
-  size_t off_items, off_acc, bytes;
+  size_t off_items, bytes;
   DibrState(int B, int H, int W, int F, int K) {
+    (void)F;
     cap = soft_bwd_item_cap(B, H, W, K);
     off_items = 1024;
-    off_acc = al256(off_items + (size_t)DS_SHARDS * cap * sizeof(int2));
-    bytes = off_acc + (size_t)B * F * DS_ACC_STRIDE * sizeof(double);
+    bytes = off_items + (size_t)DS_SHARDS * cap * sizeof(int2);
   }
   static constexpr int kZeroInts = 129;  // counters + big-face counter, zeroed by the forward
+};
+// kl_dibr_backward's soft accumulator (ABI 4; the caller's, zero on entry and left zero): the soft
+// mask's per-face double sums (B*F x DS_ACC_STRIDE) and one touched flag byte per face.  The
+// soft backward flags the faces it adds to; the gather reads, re-zeroes and unflags only those.
+struct DibrSoftAcc {
+  size_t off_flags, bytes;
+  DibrSoftAcc(int B, int F) {
+    off_flags = al256((size_t)B * F * DS_ACC_STRIDE * sizeof(double));
+    bytes = off_flags + al256((size_t)B * F);
+  }
 };
 size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int F, int K);
 size_t soft_tile_ws_bytes(int B, int H, int W, int F);

@@ -133,52 +133,76 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
     ChunkSeq seq;
     seq.init(a.bitmap + ((size_t)(b * g.tiles_y + ty) * g.tiles_x + tx), g.words, g.ntiles(), lane);
     const uint2 *rg = a.rng + f0;
-    // this wave's chunk of the next fill step (ordinal pos + wid) with its pixel ranges in
-    // flight: an unconditional load from a clamped index (a guarded load is waited for at
-    // once), issued after the current step's ranges are tested
-    int pos = 0, nc = -1;
+    // this wave's two chunks of the next fill step (ordinals pos + wid and pos + ST_WAVES + wid)
+    // with their pixel ranges in flight: unconditional loads from clamped indices (a guarded load
+    // is waited for at once), issued after the current step's ranges are tested.  Two chunks per
+    // wave and step: the fill of a heavy tile (hundreds of candidate chunks) is a chain of steps
+    // that each wait for their loads, so twice the chunks per step halves the chain.
+    constexpr int FC = 2;  // chunks per wave and step
+    int pos = 0, nc[FC] = {-1, -1};
     bool nexists = false;
-    uint2 nr = make_uint2(1u, 1u);
+    uint2 nr[FC] = {make_uint2(1u, 1u), make_uint2(1u, 1u)};
     auto pf_next = [&]() {
       nexists = seq.at(pos, lane) >= 0;
-      nc = nexists ? seq.at(pos + wid, lane) : -1;
-      pos += ST_WAVES;
-      int fl = nc * 64 + lane;
-      fl = fl < 0 ? 0 : (fl < F ? fl : F - 1);
-      nr = rg[fl];
+#pragma unroll
+      for (int k = 0; k < FC; k++) nc[k] = nexists ? seq.at(pos + k * ST_WAVES + wid, lane) : -1;
+      pos += FC * ST_WAVES;
+#pragma unroll
+      for (int k = 0; k < FC; k++) {
+        int fl = nc[k] * 64 + lane;
+        fl = fl < 0 ? 0 : (fl < F ? fl : F - 1);
+        nr[k] = rg[fl];
+      }
     };
     pf_next();
     bool more = nexists;
     while (true) {
       // ---- 1a. fill: the candidate chunks' faces that touch the workgroup's rows, in index
-      //          order, with their lane interval and row bits, ST_WAVES chunks per step
+      //          order, with their lane interval and row bits, FC x ST_WAVES chunks per step
       int len = 0;
       if (dbg) tf = stamp_clk();
-      while (more && len + ST_WAVES * 64 <= ST_LIST_CAP) {
-        const int c = nc;
-        const int fl = c * 64 + lane;
-        const int ix0 = (int)(nr.x & 0xffffu), ix1 = (int)(nr.x >> 16);
-        const int iy0 = (int)(nr.y & 0xffffu), iy1 = (int)(nr.y >> 16);
-        const int ya = max(iy0, j0) - j0, yb = min(iy1, j0 + RP - 1) - j0;
-        const uint32_t rows = ya <= yb ? ((2u << yb) - 1u) & ~((1u << ya) - 1u) : 0u;
-        const int lo = max(ix0 - ibase, 0), hi = min(ix1 - ibase, 63);
-        const bool keep = c >= 0 && fl < F && rows != 0 && lo <= hi;
+      while (more && len + FC * ST_WAVES * 64 <= ST_LIST_CAP) {
+        bool keep[FC];
+        int flk[FC];
+        uint32_t pk[FC];
+        uint64_t km[FC];
+#pragma unroll
+        for (int k = 0; k < FC; k++) {
+          const int c = nc[k];
+          flk[k] = c * 64 + lane;
+          const int ix0 = (int)(nr[k].x & 0xffffu), ix1 = (int)(nr[k].x >> 16);
+          const int iy0 = (int)(nr[k].y & 0xffffu), iy1 = (int)(nr[k].y >> 16);
+          const int ya = max(iy0, j0) - j0, yb = min(iy1, j0 + RP - 1) - j0;
+          const uint32_t rows = ya <= yb ? ((2u << yb) - 1u) & ~((1u << ya) - 1u) : 0u;
+          const int lo = max(ix0 - ibase, 0), hi = min(ix1 - ibase, 63);
+          keep[k] = c >= 0 && flk[k] < F && rows != 0 && lo <= hi;
+          pk[k] = (uint32_t)lo | ((uint32_t)hi << 6) | (rows << 12);
+        }
         pf_next();  // consumed by the next step, in this fill or after the walk
         more = nexists;
-        const uint64_t km = ballot(keep);
-        if (lane == 0) s_wcnt[wid] = __popcll(km);
-        __syncthreads();
-        int pre = 0, tot = 0;
-        for (int w = 0; w < ST_WAVES; w++) {
-          const int v = s_wcnt[w];
-          pre += w < wid ? v : 0;
-          tot += v;
+#pragma unroll
+        for (int k = 0; k < FC; k++) {
+          km[k] = ballot(keep[k]);
+          if (lane == 0) s_wcnt[k * ST_WAVES + wid] = __popcll(km[k]);
         }
-        if (keep) {
-          const int p = len + pre + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
-                                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u));
-          L_face[p] = (uint32_t)fl;
-          L_pack[p] = (uint32_t)lo | ((uint32_t)hi << 6) | (rows << 12);
+        __syncthreads();
+        // list order = chunk order: every wave's first chunk (ordinals pos + w), then every wave's
+        // second (pos + ST_WAVES + w)
+        int tot = 0;
+#pragma unroll
+        for (int k = 0; k < FC; k++) {
+          int pre = tot;
+          for (int w = 0; w < ST_WAVES; w++) {
+            const int v = s_wcnt[k * ST_WAVES + w];
+            pre += w < wid ? v : 0;
+            tot += v;
+          }
+          if (keep[k]) {
+            const int p = len + pre + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(km[k] >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)km[k], 0u));
+            L_face[p] = (uint32_t)flk[k];
+            L_pack[p] = pk[k];
+          }
         }
         len += tot;
         __syncthreads();
@@ -276,7 +300,9 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
     if (lane == 63) s_pre[64] = pre;
   }
   if (dbg) t1 = stamp_clk();
-  if (Q > 1) {
+  const bool inline_eval = sizeof(T) == 4 && K > 0;
+  // every row's prefix and total are read by every wave of the workgroup below (f32)
+  if (Q > 1 || inline_eval) {
     __syncthreads();
   } else {
     __builtin_amdgcn_wave_barrier();
@@ -284,32 +310,49 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   }
   const int total = s_pre[64];
 
-  // ---- 2. the row's hits ((pixel, slot) order) -> records, evaluated here for f32; f64 leaves
-  //         face ids for soft_tile_eval_kernel and flags its rows for it.
-  const bool inline_eval = sizeof(T) == 4 && K > 0;
+  // ---- 2. the rows' hits ((pixel, slot) order) -> records, evaluated here for f32 by ALL the
+  //         workgroup's waves over the item's rows together (a row of ~1,000 hits no longer sits on
+  //         one wave while its neighbours' waves idle); f64 leaves face ids for
+  //         soft_tile_eval_kernel and flags its rows for it.
   const size_t rbase = ((size_t)(b * H + (row_ok ? j : 0)) * g.tiles_x + tx) * 64 * (size_t)K;
   if (inline_eval) {
-    // face ids straight from the slot lists; each slot's probability replaces its face id in
-    // place (the same thread reads and writes a slot)
-    T *s_prob = reinterpret_cast<T *>(s_face);
+    // the rows' hit totals and their exclusive prefix (RP <= 8 rows)
+    int rtot[8], rpre[9];
+    rpre[0] = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      rtot[q] = q < RP ? *reinterpret_cast<const int *>(smem + st_head_lds() + st_row_lds(K) * q +
+                                                          (size_t)K * 64 * sizeof(uint32_t) + 64 * sizeof(int))
+                       : 0;
+      rpre[q + 1] = rpre[q] + rtot[q];
+    }
+    const int all = rpre[8];
     const float m = a.m;
     const float sx = m / (float)W, sy = m / (float)H;
-    const T y0 = (T)(sy * (float)(H - 2 * (row_ok ? j : 0) - 1));  // == pix_y
     constexpr int U = 4;
-    const int S = 64 * Q;
-    for (int e0 = qi * 64 + lane; e0 < total; e0 += S * U) {
-      int pp[U], kk[U];
+    constexpr int S = 64 * ST_WAVES;
+    for (int e0 = (int)threadIdx.x; e0 < all; e0 += S * U) {
+      int pp[U], kk[U], rr[U], ee[U];
       uint32_t ff[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int e = e0 + S * u;
+        const int g0 = e0 + S * u;
+        int r0 = 0;  // the hit's row: last row with rpre <= g0
+#pragma unroll
+        for (int q = 1; q < 8; q++) r0 += (q < RP && rpre[q] <= g0) ? 1 : 0;
+        const int e = g0 - rpre[r0];
+        const int *pre_r = reinterpret_cast<const int *>(smem + st_head_lds() + st_row_lds(K) * r0 +
+                                                         (size_t)K * 64 * sizeof(uint32_t));
         int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
 #pragma unroll
         for (int st = 32; st > 0; st >>= 1)
-          if (s_pre[lo + st] <= e) lo += st;
+          if (pre_r[lo + st] <= e) lo += st;
         pp[u] = lo;
-        kk[u] = e - s_pre[lo];
-        ff[u] = e < total ? s_face[kk[u] * 64 + lo] : 0u;
+        kk[u] = e - pre_r[lo];
+        rr[u] = r0;
+        ee[u] = e;
+        const uint32_t *face_r = reinterpret_cast<const uint32_t *>(smem + st_head_lds() + st_row_lds(K) * r0);
+        ff[u] = g0 < all ? face_r[kk[u] * 64 + lo] : 0u;
         if (kDevStamps && a.dev) ff[u] = min(ff[u], (uint32_t)(F - 1));  // dev ablations leave no face ids
       }
       T v[U][6];
@@ -317,25 +360,25 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
       for (int u = 0; u < U; u++) a.src.verts(f0 + ff[u], v[u]);  // all in flight (ff = 0 past the end)
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int e = e0 + S * u;
-        if (e < total) {
+        const int g0 = e0 + S * u;
+        if (g0 < all) {
+          const int jr = ty * TILE_H + part * RP + rr[u];
+          const T y0 = (T)(sy * (float)(H - 2 * jr - 1));  // == pix_y
           T dsq;
           int edgeid;
           soft_dist<T>((T)(sx * (float)(2 * (ibase + pp[u]) + 1 - W)), y0, v[u], m, dsq, edgeid);
           const T z = (T)a.sigmainv * dsq / (T)m / (T)m;
           const T pr = kl_exp<T>(-z);
-          a.rec_face[rbase + e] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
-          a.rec_prob[rbase + e] = pr;
-          s_prob[kk[u] * 64 + pp[u]] = pr;
+          const size_t rb = ((size_t)(b * H + jr) * g.tiles_x + tx) * 64 * (size_t)K;
+          a.rec_face[rb + ee[u]] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
+          a.rec_prob[rb + ee[u]] = pr;
+          T *prob_r = reinterpret_cast<T *>(smem + st_head_lds() + st_row_lds(K) * rr[u]);
+          prob_r[kk[u] * 64 + pp[u]] = pr;
         }
       }
     }
-    if (Q > 1) {
-      __syncthreads();
-    } else {
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    }
+    __syncthreads();
+    T *s_prob = reinterpret_cast<T *>(s_face);
     if (qi == 0 && px_valid && kid > 0) {
       // 1 - prod(1 - p) in double, slot order (dibr_soft_mask_cuda.cu:174-182); slots read
       // eight at a time so that their LDS reads overlap
@@ -561,7 +604,10 @@ struct ItemHash {
     }
     return -1;
   }
-  __device__ __forceinline__ void add(int f, int c0, int c1, T g0x, T g0y, T g1x, T g1y, double *gmesh, int ast) {
+  // flags (kl_dibr_backward's soft accumulator, or nullptr): byte f set for every face whose sums
+  // this item adds to, so the gather reads (and re-zeroes) only those
+  __device__ __forceinline__ void add(int f, int c0, int c1, T g0x, T g0y, T g1x, T g1y, double *gmesh, int ast,
+                                      uint8_t *flags) {
     const int s = slot(f);
     if (s >= 0) {
       atomicAdd(&val[s * 6 + c0 * 2], (double)g0x);
@@ -572,6 +618,7 @@ struct ItemHash {
       }
     } else {  // no free slot within the probe bound
       global_add_pair<double>(gmesh + (size_t)f * ast, c0, c1, g0x, g0y, g1x, g1y);
+      if (flags) flags[f] = 1;
     }
   }
   // one thread per (used slot, coordinate), coordinate fastest: a face's 6 sums go out from 6
@@ -579,12 +626,13 @@ struct ItemHash {
   // 64-B requests per face instead of one request per lane (memory-side atomics,
   // MI355X_MICROARCH.md: one lane per row is an order of magnitude slower).  Every thread of the
   // workgroup calls it (barrier before the key reset).
-  __device__ __forceinline__ void flush_reset(int tid, int nthreads, double *gmesh, int ast) {
+  __device__ __forceinline__ void flush_reset(int tid, int nthreads, double *gmesh, int ast, uint8_t *flags) {
     const int n = *nused;
     for (int u = tid; u < n * 6; u += nthreads) {
       const int sl = used[u / 6], c = u % 6;
       const double v = val[sl * 6 + c];
       if (v != 0.0) atomicAdd(gmesh + (size_t)key[sl] * ast + c, v);
+      if (c == 0 && flags) flags[key[sl]] = 1;
       val[sl * 6 + c] = 0.0;
     }
     __syncthreads();
@@ -601,7 +649,7 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const uint8_t *__restrict__ hits,
     const uint32_t *__restrict__ rec_face, const T *__restrict__ rec_prob, const T *__restrict__ fvi, BinGeom g,
     int F, int K, float sigmainv, float multiplier, double *__restrict__ gacc, const int2 *__restrict__ items,
-    const int *__restrict__ ctl, int cap, int *__restrict__ scratch, int dev, int ast) {
+    const int *__restrict__ ctl, int cap, int *__restrict__ scratch, int dev, int ast, uint8_t *__restrict__ sflag) {
   constexpr int HC = 512;
   __shared__ int s_key[HC];
   __shared__ double s_val[HC * 6];
@@ -692,10 +740,11 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
       if (dev & 2)
         asm volatile("" : : "v"(g0x), "v"(g0y), "v"(g1x), "v"(g1y), "v"(c0), "v"(c1));
       else
-        hash.add(face, c0, c1, g0x, g0y, g1x, g1y, gacc + (size_t)b * F * ast, ast);
+        hash.add(face, c0, c1, g0x, g0y, g1x, g1y, gacc + (size_t)b * F * ast, ast,
+                 sflag ? sflag + (size_t)b * F : nullptr);
     }
     __syncthreads();
-    hash.flush_reset(threadIdx.x, blockDim.x, gacc + (size_t)b * F * ast, ast);
+    hash.flush_reset(threadIdx.x, blockDim.x, gacc + (size_t)b * F * ast, ast, sflag ? sflag + (size_t)b * F : nullptr);
     __syncthreads();
     if (threadIdx.x == 0) s_nused = 0;
   }
@@ -852,7 +901,7 @@ int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T
   const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
   hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
                      (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, acc,
-                     (const int2 *)items, (const int *)ctl, 0, s.scratch, g_dev_flags, 6);
+                     (const int2 *)items, (const int *)ctl, 0, s.scratch, g_dev_flags, 6, (uint8_t *)nullptr);
   KL_CHECK_LAUNCH();
   if (acc_out) {
     if (has_sum) *has_sum = true;
@@ -865,7 +914,7 @@ size_t soft_tile_bwd_items_bytes(int B, int H, int W, int K) { return soft_bwd_a
 template <typename T>
 int soft_tile_backward_listed(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,
                               const T *fvi, float sigmainv, float m, const int2 *items, const int *cnt, int cap,
-                              double *acc, hipStream_t st) {
+                              double *acc, uint8_t *sflag, hipStream_t st) {
   if ((int64_t)B * H * W == 0 || K <= 0 || grad == nullptr || (int64_t)B * F == 0) return KL_OK;
   const BinGeom g = make_bin_geom(B, H, W, F);
   int dev_id = 0, ncu = 256;
@@ -875,16 +924,16 @@ int soft_tile_backward_listed(int B, int H, int W, int F, int K, const T *grad, 
   const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
   hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
                      (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, acc, items, cnt,
-                     cap, (int *)nullptr, g_dev_flags, DS_ACC_STRIDE);
+                     cap, (int *)nullptr, g_dev_flags, DS_ACC_STRIDE, sflag);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }
 template int soft_tile_backward_listed<float>(int, int, int, int, int, const float *, const float *,
                                               const SoftState<float> &, const float *, float, float, const int2 *,
-                                              const int *, int, double *, hipStream_t);
+                                              const int *, int, double *, uint8_t *, hipStream_t);
 template int soft_tile_backward_listed<double>(int, int, int, int, int, const double *, const double *,
                                                const SoftState<double> &, const double *, float, float, const int2 *,
-                                               const int *, int, double *, hipStream_t);
+                                               const int *, int, double *, uint8_t *, hipStream_t);
 
 template int soft_tile_forward<float>(int, int, int, int, int, const float *, const int64_t *, float, double, float,
                                       float *, const SoftState<float> &, void *, size_t, hipStream_t);

@@ -56,6 +56,20 @@ at::Tensor workspace(size_t bytes, const at::Device &dev, int64_t stream) {
   return t;
 }
 
+// a buffer that is zero whenever the stream reaches a call that uses it, and that the call leaves
+// zero (kl_dibr_backward's soft accumulator): zeroed once when allocated, per (device, stream);
+// a captured call gets its own, zeroed by a fill recorded in the graph (_native.zero_kept)
+at::Tensor zero_kept(size_t bytes, const at::Device &dev, int64_t stream) {
+  const int64_t need = (int64_t)std::max<size_t>(bytes, 16);
+  if (kl_stream_is_capturing((kl_stream)stream)) return at::zeros({need}, at::TensorOptions().dtype(at::kByte).device(dev));
+  static std::mutex mu;
+  static std::map<std::pair<int, int64_t>, at::Tensor> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  at::Tensor &t = cache[{dev.index(), stream}];
+  if (!t.defined() || t.numel() < need) t = at::zeros({need}, at::TensorOptions().dtype(at::kByte).device(dev));
+  return t;
+}
+
 void *ptr(const at::Tensor &t) { return t.defined() ? t.data_ptr() : nullptr; }
 
 // Each node's backward is one opaque HIP call, so its gradients cannot be differentiated again.
@@ -187,7 +201,7 @@ struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
     at::Tensor rec_prob = at::empty({nrec}, opt);
     at::Tensor seg_tot =
         at::empty({std::max<int64_t>((int64_t)kl_soft_mask_compact_segments((int)B, H, W), 1)}, opt.dtype(at::kInt));
-    // the backward's soft-mask work items and its zeroed accumulator (written by the forward)
+    // the backward's soft-mask work items (written by the forward)
     at::Tensor scratch = at::empty({(int64_t)kl_dibr_state_bytes((int)B, H, W, (int)F, K)}, opt.dtype(at::kByte));
     at::Tensor ranges = at::empty({B, F, 2}, opt.dtype(at::kInt));
     const size_t nbytes = kl_dibr_workspace_bytes((int)B, H, W, (int)F);
@@ -230,6 +244,7 @@ struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
     at::Tensor g_feat = at::empty_like(feat);
     const size_t nbytes = kl_dibr_bwd_workspace_bytes((int)B, H, W, (int)F, K);
     at::Tensor ws = workspace(nbytes, fvi.device(), stream);
+    at::Tensor acc = gm.defined() ? zero_kept(kl_dibr_soft_acc_bytes((int)B, (int)F), fvi.device(), stream) : at::Tensor();
     check(kl_dibr_backward(dtype_code(fvi.scalar_type()), (int)B, H, W, (int)F, (int)D, K, ptr(gf), ptr(gm),
                            idx.data_ptr<int64_t>(), ptr(w), ptr(fvi), ptr(feat), ptr(fnz), ptr(mask),
                            hits.data_ptr<uint8_t>(), (const uint32_t *)rec_face.data_ptr(), ptr(rec_prob),
@@ -237,7 +252,7 @@ struct DibrRasterization : public torch::autograd::Function<DibrRasterization> {
                            (float)ctx->saved_data["multiplier"].toDouble(), (float)ctx->saved_data["eps"].toDouble(),
                            ptr(g_img), ptr(g_feat), scratch.data_ptr(),
                            ctx->saved_data["has_ranges"].toBool() ? (const uint32_t *)ranges.data_ptr() : nullptr,
-                           ws.data_ptr(), nbytes, (kl_stream)stream),
+                           ptr(acc), ws.data_ptr(), nbytes, (kl_stream)stream),
           "dibr_rasterization backward");
     out[3] = g_img;
     out[4] = g_feat;

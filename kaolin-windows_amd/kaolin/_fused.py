@@ -141,7 +141,7 @@ class SoftMaskState:
     """The compact saved state of the soft mask (softtile.hip): per-pixel filled-slot
     counts, the per-hit records, the per-row-segment hit totals and ``scratch``: the zeroed
     int32 word of the standalone soft mask, or dibr_forward's state bytes (the backward's work
-    items and its accumulator, kl_dibr_state_bytes)."""
+    items, kl_dibr_state_bytes)."""
     __slots__ = ('hits', 'rec_face', 'rec_prob', 'seg_tot', 'scratch', 'knum')
 
     def __init__(self, hits, rec_face, rec_prob, seg_tot, scratch, knum):
@@ -219,13 +219,14 @@ def dibr_backward(grad_feats, grad_soft_mask, face_idx, weights, face_vertices_i
     nbytes = N.size('kl_dibr_bwd_workspace_bytes', B, H, W, F, state.knum)
     ws = _ws(nbytes, dev)
     gm = grad_soft_mask.contiguous() if grad_soft_mask is not None else None
+    acc = N.zero_kept(N.size('kl_dibr_soft_acc_bytes', B, F), dev) if gm is not None else None
     with N.on_device(dev), N.timed('dibr_backward', dev):
         N.check(lib.kl_dibr_backward(
             N.dtype_code(face_vertices_image.dtype), B, H, W, F, D, state.knum, N.ptr(grad_feats.contiguous()),
             N.ptr(gm), N.ptr(face_idx), N.ptr(weights), N.ptr(face_vertices_image), N.ptr(face_features),
             N.ptr(face_normals_z), N.ptr(soft_mask), N.ptr(state.hits), N.ptr(state.rec_face), N.ptr(state.rec_prob),
             N.ptr(state.seg_tot), float(sigmainv), float(multiplier), float(eps), N.ptr(g_img), N.ptr(g_feat),
-            N.ptr(state.scratch), N.ptr(face_ranges), N.ptr(ws), nbytes, N.stream_of(dev)), func)
+            N.ptr(state.scratch), N.ptr(face_ranges), N.ptr(acc), N.ptr(ws), nbytes, N.stream_of(dev)), func)
     return g_img, g_feat
 
 
@@ -263,7 +264,7 @@ def dibr_forward(height, width, face_vertices_z, face_vertices_image, face_featu
     rec_face = torch.empty(max(nrec, 1), dtype=torch.int32, device=dev)
     rec_prob = torch.empty(max(nrec, 1), dtype=dtype, device=dev)
     seg_tot = torch.empty(max(N.size('kl_soft_mask_compact_segments', B, H, W), 1), dtype=torch.int32, device=dev)
-    # the fused path's state: the backward's soft-mask work items and its zeroed accumulator
+    # the fused path's state: the backward's soft-mask work items
     state = torch.empty(N.size('kl_dibr_state_bytes', B, H, W, F, K), dtype=torch.uint8, device=dev)
     ranges = torch.empty((B, F, 2), dtype=torch.int32, device=dev)
     nbytes = N.size('kl_dibr_workspace_bytes', B, H, W, F)

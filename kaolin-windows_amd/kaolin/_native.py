@@ -14,7 +14,7 @@ _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib')
 # `make STAMPS=1 OUT=...`); the default is the in-tree build
 LIB_PATH = os.environ.get('KAOLIN_HIP_LIB') or os.path.join(_LIB_DIR, 'libkaolin_hip.so')
 
-ABI_VERSION = 3  # include/kaolin_hip.h KL_ABI_VERSION: the signatures below
+ABI_VERSION = 4  # include/kaolin_hip.h KL_ABI_VERSION: the signatures below
 
 KL_F32, KL_F64, KL_F16, KL_U8, KL_I8, KL_I16, KL_I32, KL_I64 = range(8)
 _DTYPES = {
@@ -67,10 +67,11 @@ _SIGS = {
     'kl_dibr_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'kl_dibr_bwd_workspace_bytes': (_SZ, [_I, _I, _I, _I, _I]),
     'kl_dibr_state_bytes': (_SZ, [_I, _I, _I, _I, _I]),
+    'kl_dibr_soft_acc_bytes': (_SZ, [_I, _I]),
     'kl_dibr_forward': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _F, ctypes.c_double, _F, _F, _P, _P, _P,
                              _P, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_backward': (_I, [_I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _F, _F,
-                              _F, _P, _P, _P, _P, _P, _SZ, _P]),
+                              _F, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_forward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _SZ, _P]),
     'kl_dibr_soft_mask_backward': (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _SZ,
                                         _P]),
@@ -229,6 +230,24 @@ def workspace(nbytes, device):
         _WS[key] = t
     return t
 
+
+_ZK = {}
+
+
+def zero_kept(nbytes, device):
+    """A buffer that is zero whenever the stream reaches a call that uses it, and that the call
+    leaves zero (kl_dibr_backward's soft accumulator): zeroed once when allocated, one per
+    (device, stream), grown to the largest request.  A call being captured into a graph gets its
+    own buffer from the graph's pool, zeroed by a fill recorded in the graph."""
+    nbytes = max(int(nbytes), 16)
+    if capturing(device):
+        return torch.zeros(nbytes, dtype=torch.uint8, device=device)
+    key = (device.index, stream_of(device))
+    t = _ZK.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+        _ZK[key] = t
+    return t
 
 
 def require_gpu(func, *tensors):

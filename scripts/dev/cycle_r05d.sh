@@ -1,9 +1,8 @@
 #!/bin/bash
-# r05c: full GPU suite (chip-wide order kernel, new tests), soft-forward stamps, order kernel A/B,
-# bench kernel stats
+# r05d: the double-backward test, soft-forward stamps, order kernel A/B, bench kernel stats
 set -e
-R=$(pwd); OUT=gpurun_out/r05c; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1
+R=$(pwd); OUT=gpurun_out/r05d; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "double_backward" > $OUT/tests.log 2>&1
 STAMPS_FLAGS=0 KAOLIN_HIP_LIB=$R/devlib/stamps/libkaolin_hip.so STAMPS_DUMP=$R/$OUT/stamps_0.npy \
   timeout -k 10 120 python scripts/dev/stamps.py > $OUT/stamps_0.log 2>&1
 timeout -k 10 120 python scripts/dev/param_ab.py 15 0 1 0 1 > $OUT/param_ab.log 2>&1

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_error_channel():
     from kaolin import _native
     lib = _native.lib()
-    assert lib.kl_abi_version() == 3
+    assert lib.kl_abi_version() == 4
     # a dtype the rasterizer does not implement reports through kl_last_error (no GPU work)
     rc = lib.kl_packed_rasterize_forward(7, 4, 4, 1, 0, 1, 1, None, None, None, None, None, 1.0, 1e-8,
                                          None, None, None, None, 0, None)

@@ -736,9 +736,10 @@ def test_torch_reference_nodes_double_backward(kal, monkeypatch, route):
     """mask_iou, prepare_vertices and texture_mapping are plain torch in the reference, so their
     gradients are differentiable there.  Under create_graph the HIP nodes take the
     reference chain's gradient (csrc/torch_ops.cpp *_chain; kaolin/_double_backward.py for the
-    Python nodes): first AND second derivatives equal the reference chain's own, bit for bit
-    (texture_mapping: its first derivative; grid_sample's backward has no derivative in torch, so
-    the second raises in both); an ordinary backward stays on the HIP path."""
+    Python nodes): first derivatives equal the reference chain's own, bit for bit, and second
+    derivatives to the engine's summation order (texture_mapping: grid_sample's backward has no
+    derivative in torch, so its second derivative raises in both); an ordinary backward stays on
+    the HIP path."""
     from kaolin import _ext
     from kaolin.metrics.render import _mask_iou_torch
     from kaolin.render.mesh.utils import _prepare_vertices_torch, _texture_mapping_torch
@@ -753,17 +754,24 @@ def test_torch_reference_nodes_double_backward(kal, monkeypatch, route):
         ys = list(ys) if isinstance(ys, (list, tuple)) else [ys]
         loss = sum((y * (k + 1.5)).sum() for k, y in enumerate(ys))
         d1 = torch.autograd.grad(loss, xs, create_graph=True, allow_unused=True)
-        out = [y.detach() for y in ys] + [d.detach() for d in d1 if d is not None]
+        out = [d.detach() for d in d1 if d is not None]
+        sec = []
         if second:
-            out += [d for d in torch.autograd.grad(sum((d * d).sum() for d in d1 if d is not None), xs,
-                                                   allow_unused=True) if d is not None]
-        return out
+            sec = [d for d in torch.autograd.grad(sum((d * d).sum() for d in d1 if d is not None), xs,
+                                                  allow_unused=True) if d is not None]
+        return [y.detach() for y in ys], out, sec
 
     def check(f1, f2, inputs, second=True):
-        a, b = derivs(f1, inputs, second), derivs(f2, inputs, second)
-        assert len(a) == len(b)
-        for x, y in zip(a, b):
+        (ya, a, a2), (yb, b, b2) = derivs(f1, inputs, second), derivs(f2, inputs, second)
+        for x, y in zip(ya, yb):  # the HIP forward: within float rounding of torch's (not bit-equal)
+            torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-5)
+        assert len(a) == len(b) and len(a2) == len(b2)
+        for x, y in zip(a, b):  # first derivatives: the reference chain's, bit for bit
             assert torch.equal(x, y)
+        # second derivatives: the chain's, up to the order the autograd engine adds a tensor's
+        # gradient contributions in (node creation order: the chain is rebuilt inside the backward)
+        for x, y in zip(a2, b2):
+            torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
 
     gen = torch.Generator().manual_seed(4)
     a = torch.rand((2, 8, 8), generator=gen).to(DEV)
@@ -1520,6 +1528,44 @@ def test_raytrace_fixed_capture_and_truncation(kal):
     # candidates may all miss at the target level)
     assert flag == 1 and 0 <= k <= small
     assert torch.equal(tr[:k], r2[:k]) and torch.equal(tp[:k], p2[:k]) and torch.equal(tdp[:k], dep2[:k])
+
+
+@pytest.mark.parametrize('level,nrays', [(4, 1000), (6, 1000), (6, 5)])
+def test_raytrace_fused_equals_per_level(kal, level, nrays):
+    """The fused level march (rt_level_kernel: one launch per level, counts on the device, one host
+    read) against the per-level march (dev param 15 = 2), nuggets and depths bit-equal, on a dense
+    level-6 octree: level 4 fits its buffers (16 nuggets per ray, at least 65,536), level 6 with
+    1,000 rays does not (~100 nuggets per ray): the fused march reports the truncation and the
+    per-level march answers (kl_dev_get_stat(1) == 2)."""
+    import ctypes
+    from kaolin import _native as N
+    lib = N.lib()
+    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.kl_dev_get_stat.argtypes = [ctypes.c_int]
+    lib.kl_dev_get_stat.restype = ctypes.c_int
+    n_oct = sum(8 ** k for k in range(6))
+    octree, pyr, ex, pts = _rt_setup(kal, np.full(n_oct, 255, np.uint8))
+    rng = np.random.RandomState(level + nrays)
+    o = rng.normal(size=(nrays, 3))
+    o = (3.0 * o / np.linalg.norm(o, axis=1, keepdims=True)).astype(np.float32)
+    d = -o + 0.3 * rng.normal(size=(nrays, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    outs = {}
+    for mode in (0, 2):
+        lib.kl_dev_set_param(15, mode)
+        try:
+            outs[mode] = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level, with_exit=True)
+            torch.cuda.synchronize()
+            outs[mode] += (lib.kl_dev_get_stat(1),)
+        finally:
+            lib.kl_dev_set_param(15, 0)
+    (r0, p0, d0, s0), (r2, p2, d2, s2) = outs[0], outs[2]
+    # 2 = a level's candidates (its parents' children) exceeded the fused march's buffers
+    assert s2 == 0 and s0 in (1, 2) and (s0 == 2 or len(r2) <= max(16 * nrays, 65536))
+    assert (level, nrays) != (6, 1000) or s0 == 2
+    assert (level, nrays) != (6, 5) or s0 == 1
+    assert torch.equal(r0, r2) and torch.equal(p0, p2) and torch.equal(d0, d2)
+    assert len(r2) > (1000 if nrays > 5 else 0)
 
 
 @pytest.mark.parametrize('na,nb', [(0, 5), (7, 0), (3145728, 1048576), (1001, 333)])
