@@ -54,7 +54,10 @@ typedef void *(*kl_alloc_fn)(void *ctx, size_t bytes);
  *    kl_soft_mask_compact_bwd_workspace_bytes gained num_faces.
  * 3: kl_dibr_forward / kl_dibr_backward take a state buffer of kl_dibr_state_bytes() bytes
  *    where they took one scratch int32 (the forward lists the backward's work items and zeroes
- *    its accumulator there); added kl_unbatched_triangle_distance_backward_sums.
+ *    its accumulator there); added kl_unbatched_triangle_distance_backward_sums; kl_loss_dot2's
+ *    workspace holds its arrival ticket and must be ZERO before the first call (each call leaves
+ *    it zero; an uninitialised one would never elect a last workgroup, and out[0] would not be
+ *    written).
  * 4: kl_dibr_backward takes `soft_acc` (kl_dibr_soft_acc_bytes(): zero on entry, left zero on
  *    return) for the soft mask's per-face sums, which the forward's state no longer holds (the
  *    forward zeroes nothing per call); added kl_sided_distance_backward_sums. */

@@ -11,7 +11,7 @@ static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
 int g_dev_flags = 0;
 void *g_dev_debug = nullptr;
-int g_dev_param[16] = {};
+int g_dev_param[32] = {};
 int g_dev_stat[4] = {};
 }  // namespace kl
 
@@ -25,7 +25,7 @@ extern "C" void kl_dev_set_debug(void *buf) { kl::g_dev_debug = buf; }
 // Development hook: tuning parameters for sweeps (scripts/dev/stamps.py); 0 = built-in value.
 // 0..3: the soft-mask forward's split thresholds / caps (tileorder.h, SoftSplit).
 extern "C" void kl_dev_set_param(int idx, int value) {
-  if (idx >= 0 && idx < 16) kl::g_dev_param[idx] = value;
+  if (idx >= 0 && idx < 32) kl::g_dev_param[idx] = value;
 }
 // Development hook: what the last call took (tests assert a fallback branch ran).
 // 0: mesh_to_spc -- 0 the node-rank path, 1 its per-level fallback (the pair buffers overflowed).

@@ -17,7 +17,7 @@ namespace kl {
 void set_error(const std::string &msg);
 extern int g_dev_flags;    // kl_dev_set_flags (ablation timing only; 0 in the product path)
 extern void *g_dev_debug;  // kl_dev_set_debug (per-wave stamps; nullptr in the product path)
-extern int g_dev_param[16];  // kl_dev_set_param (tuning sweeps; 0 = the built-in value)
+extern int g_dev_param[32];  // kl_dev_set_param (tuning sweeps; 0 = the built-in value)
 extern int g_dev_stat[4];    // kl_dev_get_stat (what the last call took)
 
 // shader-clock and 100 MHz wall-clock stamps for the dev timing buffer

@@ -409,6 +409,8 @@ struct CountOrderArgs {
   int nzero;
   double *zacc;
   size_t zn;
+  uint64_t *dbg = nullptr;  // dev stamps (wall clock): count workgroup b at 4 b (start, counted, ticket);
+                            // bitmap w's last workgroup at 64 + 4 w (start, prefix, placed)
 };
 
 static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel(CountOrderArgs a) {
@@ -426,6 +428,8 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
   }
   const int which = (int)blockIdx.x >= nb ? 1 : 0, blk = (int)blockIdx.x - which * nb;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t *const dbg = kDevStamps && a.dbg && blockIdx.x < 16 ? a.dbg + blockIdx.x * 4 : nullptr;
+  if (dbg && threadIdx.x == 0) dbg[0] = stamp_wall();
   const int t = blk * CO_THREADS + threadIdx.x;
   for (int i = threadIdx.x; i < (CO_THREADS / 64) * ORD_HIST; i += blockDim.x) (&s_wk[0][0])[i] = 0;
   // the tile's candidate-chunk count: its words (word-major, coalesced across the wave), raw buffer
@@ -443,6 +447,7 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
   }
   const int q = 31 - __clz(n + 1u);
   const int key = t < nt ? tile_band(t, nt) * ORD_BUCKETS + q : -1;
+  if (dbg && threadIdx.x == 0) dbg[1] = stamp_wall();
   // rank within the workgroup for its key, in tile order: the wave's own rank (same-key lanes
   // below this one) now, the earlier waves' counts after the barrier
   int wrank = 0;
@@ -475,9 +480,12 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
   if (threadIdx.x == 0) {
     const unsigned prev = __hip_atomic_fetch_add(a.ticket + which, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = prev == (unsigned)nb - 1;
+    if (dbg) dbg[2] = stamp_wall();
   }
   __syncthreads();
   if (!s_last) return;
+  uint64_t *const ldbg = kDevStamps && a.dbg ? a.dbg + 64 + which * 4 : nullptr;
+  if (ldbg && threadIdx.x == 0) ldbg[0] = stamp_wall();
   // ---- the last workgroup of this bitmap: bases per (workgroup, key), totals, parts, prefix, items.
   //      Every global read here is sc1 and issued eight at a time (one round trip per batch).
   constexpr int BATCH = 8;
@@ -511,6 +519,7 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
     soft_parts(sx, lpb, hist, a.lp_min1, a.sp, a.skip_empty1);
   }
   place_prefix(sb, sx, lpb, hist, a.nitems[which]);
+  if (ldbg && threadIdx.x == 0) ldbg[1] = stamp_wall();
   int32_t *order = a.order[which];
   for (int u0 = threadIdx.x; u0 < nt; u0 += BATCH * blockDim.x) {
     uint32_t v[BATCH];
@@ -529,6 +538,10 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
       const int r0 = sb[kk] + (s_big[(u / CO_THREADS) * ORD_HIST + kk] + (int)(v[j] >> 8)) * np;
       for (int k = 0; k < np; k++) order[place_pos(sx, g, r0 + k)] = u | (k << 24) | (lp << 28);
     }
+  }
+  if (ldbg) {
+    __syncthreads();
+    if (threadIdx.x == 0) ldbg[2] = stamp_wall();
   }
 }
 

@@ -5,7 +5,7 @@ import torch
 
 def face_normals(face_vertices, unit=False):
     if face_vertices.shape[-2] != 3:
-        raise NotImplementedError("face_normals is only implemented for triangle meshes")
+        raise NotImplementedError("face_normals: triangle meshes only (3 vertices per face)")
     edges_dist0 = face_vertices[:, :, 1] - face_vertices[:, :, 0]
     edges_dist1 = face_vertices[:, :, 2] - face_vertices[:, :, 0]
     normals = torch.cross(edges_dist0, edges_dist1, dim=2)

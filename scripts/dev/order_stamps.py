@@ -1,5 +1,6 @@
-"""Wall-clock phase stamps of tile_countorder2_kernel (dev aid; a `make STAMPS=1` library loaded
-through KAOLIN_HIP_LIB).  Prints per block: count, prefix, placement in microseconds."""
+"""Wall-clock phase stamps of tile_countorder_chip_kernel (dev aid; a `make STAMPS=1` library
+loaded through KAOLIN_HIP_LIB).  Prints the count workgroups' (count, publish) and each bitmap's
+last workgroup's (prefix, placement) phases in microseconds from the earliest start."""
 import ctypes
 import os
 import sys
@@ -14,21 +15,24 @@ from kaolin import _fused, _native as N  # noqa: E402
 lib = N.lib()
 lib.kl_dev_set_debug.argtypes = [ctypes.c_void_p]
 inp = bench.dibr_inputs([0.0, 1.5707963, 3.1415927, 4.712389], 'cuda')
-# every stamping kernel writes into this buffer (per-wave stamps from 0); the order kernel's 8
-# at kOrderStampsAt = 2^24 (csrc/common.h)
-AT = 1 << 24
-dbg = torch.zeros(AT + 64, dtype=torch.int64, device='cuda')
+AT = 1 << 24  # kOrderStampsAt (csrc/common.h)
+dbg = torch.zeros(AT + 128, dtype=torch.int64, device='cuda')
 fw = lambda: _fused.dibr_forward(inp['H'], inp['W'], inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'], 7000., 0.02,  # noqa
                                  30, 1000., 1e-8)
 for _ in range(3):
     fw()
 lib.kl_dev_set_debug(ctypes.c_void_p(dbg.data_ptr()))
-for rep in range(5):
+for rep in range(4):
+    dbg.zero_()
     fw()
     torch.cuda.synchronize()
-    d = dbg[AT:AT + 8].cpu().tolist()
-    for blk in range(2):
-        t = d[blk * 4:blk * 4 + 4]
-        print(f'rep {rep} block {blk}: count {(t[1] - t[0]) / 100:.2f} us, prefix {(t[2] - t[1]) / 100:.2f} us, '
-              f'place {(t[3] - t[2]) / 100:.2f} us, total {(t[3] - t[0]) / 100:.2f} us')
+    d = dbg[AT:AT + 72].cpu().tolist()
+    t0 = min(x for x in d if x)
+    us = lambda x: (x - t0) / 100 if x else float('nan')  # noqa: E731
+    cw = [(us(d[4 * b]), us(d[4 * b + 1]), us(d[4 * b + 2])) for b in range(16) if d[4 * b]]
+    print(f'rep {rep}: count workgroups (start, counted, ticket) us: ' +
+          ' '.join(f'({a:.1f},{b:.1f},{c:.1f})' for a, b, c in cw))
+    for w in range(2):
+        s = d[64 + 4 * w:64 + 4 * w + 3]
+        print(f'  bitmap {w} last workgroup: start {us(s[0]):.2f} prefix {us(s[1]):.2f} placed {us(s[2]):.2f} us')
 lib.kl_dev_set_debug(None)

@@ -36,7 +36,7 @@ def main():
     inp = bench.dibr_inputs([0.0, 1.5707963, 3.1415927, 4.712389], 'cuda')
     H, W = inp['H'], inp['W']
     for combo in combos:
-        for i in range(16):
+        for i in range(32):
             lib.kl_dev_set_param(i, 0)
         for i, v in combo:
             lib.kl_dev_set_param(i, v)
@@ -47,7 +47,7 @@ def main():
         d = lambda: _fused.dibr_backward(inp['g_feat'], inp['g_mask'], idx_, w, inp['fvi'], inp['feat'],  # noqa
                                          inp['fnz'], mask, state, 7000., 1000., 1e-8, ranges)
         print(f'params {v}: dibr_forward {timeit(fw):.1f} us, dibr_backward {timeit(d):.1f} us', flush=True)
-    for i in range(16):
+    for i in range(32):
         lib.kl_dev_set_param(i, 0)
 
 
