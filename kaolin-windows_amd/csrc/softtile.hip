@@ -277,7 +277,13 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
           kid = min(K, kid + all);
           active = active && kid < K;
           amask = ballot(active);
+          if (lane == 0) s_wcnt[2 * ST_WAVES + wid] = amask != 0;
           __syncthreads();  // s_cnt is rewritten by the next round
+          // every row of the workgroup saturated (knum hits or covered): the remaining blocks
+          // cannot add a hit (workgroup-uniform exit; the pole tiles' rows fill in a few rounds)
+          int live = 0;
+          for (int w = 0; w < ST_WAVES; w++) live |= s_wcnt[2 * ST_WAVES + w];
+          if (!live) break;
         }
       }
       if (lane == 0) s_wcnt[wid] = amask != 0;
