@@ -206,7 +206,19 @@ __device__ __forceinline__ void make_prune(const FaceRec<T> &r, PruneTile<T> &pt
 #endif
 // occupancy: the float kernel is latency-bound at 4 waves per SIMD (113 VGPRs); asking
 // for 5 (96 VGPRs, 4 spilled) measured 3-5 % faster on cfg2, 6 (22 spills) no better
-template <typename T>
+// PAIRS (r05): with shared thresholds on (all faces proper, a finite bounded cluster -- the fold is
+// then the plain (distance, index) minimum, so pairs may be evaluated in any order), each (point,
+// face) pair the wave's test keeps goes through a second, per-point test -- the same bound with the
+// lane's own point and its own running best -- and the pairs that pass are queued per wave (LDS ring
+// of (face slot, lane)) and evaluated 64 at a time, one pair per lane, the point fetched from its
+// lane; each result is folded into its point's packed (distance bits, face << 3 | type) minimum with
+// an LDS 64-bit atomic min.  The wave-level walk evaluated every kept face for all 64 points, most of
+// them far from it; this evaluates ~one lane-slot per useful pair.  The minimum face itself is
+// never skipped (every threshold is a computed distance, and skipping needs d > thr strictly), so
+// the (distance, index) minimum -- the reference's result -- is exact.
+constexpr int P2M_QCAP = 128;  // per-wave pair ring (a face adds <= 64 pairs; batches of 64 drain it)
+
+template <typename T, bool PAIRS>
 __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1)) p2m_fwd_kernel(const T *__restrict__ pts, const T *__restrict__ fv,
                                                        const int32_t *__restrict__ order, int64_t P, int64_t F,
                                                        int64_t split_faces, T *__restrict__ out_dist,
@@ -247,6 +259,15 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
   // bits (distances are >= +0, so integer order is float order); reads may be stale, which
   // only weakens the bound.
   const bool share = gbest != nullptr && all_fin && bounds[6] != 0 && cinf + R < (T)1e15;
+  // the per-point pair path (wave-uniform); face ids and types packed in 32 bits
+  const bool pairs = PAIRS && share && F < ((int64_t)1 << 29);
+  constexpr unsigned long long KEY_NONE = 0x7f800000ull << 32 | 0xffffffffull;  // +inf, no face
+  __shared__ uint16_t s_q[PAIRS ? 4 : 1][P2M_QCAP];
+  __shared__ unsigned long long s_best[PAIRS ? 256 : 1];
+  const int wid = threadIdx.x >> 6;
+  uint32_t qhead = 0, qcnt = 0;  // the wave's ring (wave-uniform)
+  T pthr = (T)INFINITY, psq = (T)INFINITY;  // pairs: the lane's best distance so far and its root
+  if (pairs) s_best[threadIdx.x] = KEY_NONE;
   float published = INFINITY;
 #ifdef KL_P2M_PROBE
   unsigned long long g_p2m_skipped = 0, g_p2m_evaluated = 0;
@@ -259,21 +280,49 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
     float shared_thr = INFINITY;
     if (share && valid)
       shared_thr = __uint_as_float(__hip_atomic_load(gbest + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (pairs && (T)shared_thr < pthr) {
+      pthr = (T)shared_thr;
+      psq = kl_sqrt<T>(pthr) * (T)(1.0 + 16.0 * P2M_E);
+    }
     __syncthreads();
     for (int s = threadIdx.x; s < n; s += blockDim.x) {
       make_face<T>(fv + (start + s) * 9, sf[s]);
       make_prune<T>(sf[s], sp, s);
     }
     __syncthreads();
+    // pairs: evaluate the ring's first nb pairs, one per lane, folding into s_best; then every lane
+    // re-reads its own minimum as its threshold
+    auto run_batch = [&](int nb) {
+      const bool act = lane < nb;
+      const uint32_t e = s_q[wid][(qhead + (act ? lane : 0)) & (P2M_QCAP - 1)];
+      const int owner = (int)(e & 63u), sj = (int)(e >> 6);
+      const V3<T> pp = mk(__shfl(p.x, owner), __shfl(p.y, owner), __shfl(p.z, owner));
+      int t;
+      const float d = point_face<T>(pp, sf[sj], t);
+      if (act)
+        atomicMin(&s_best[wid * 64 + owner],
+                  (unsigned long long)__float_as_uint(d) << 32 | (uint32_t)(((start + sj) << 3) | t));
+      qhead += nb;
+      qcnt -= nb;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const unsigned long long mine = s_best[threadIdx.x];
+      const T bd = (T)__uint_as_float((uint32_t)(mine >> 32));
+      if (bd < pthr) {
+        pthr = bd;
+        psq = kl_sqrt<T>(pthr) * (T)(1.0 + 16.0 * P2M_E);
+      }
+    };
     for (int s0 = 0; s0 < n; s0 += 64) {
       // thresholds only decrease, so a stale maximum over the lanes is a safe upper bound
       T thr = fmin(best, tbest);
       if (thr != thr || !valid) thr = valid ? (T)INFINITY : (T)0;
       if (share) thr = fmin(thr, (T)shared_thr);
+      if (pairs) thr = valid ? pthr : (T)0;
       const T thr_max = wave_max(thr);
       const int s = s0 + lane;
       bool eval = s < n;
-      if (eval && all_fin && ((start + s) & 511) != 0 && thr_max < (T)INFINITY) {
+      if (eval && all_fin && (pairs || ((start + s) & 511) != 0) && thr_max < (T)INFINITY) {
         const FaceRec<T> &fr = sf[s];
         const T M = cinf + R + fr.hmax;
         const T sl = (T)(256.0 * P2M_E) * M;
@@ -309,6 +358,35 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
       g_p2m_evaluated += __popcll(mask);
       g_p2m_skipped += (uint64_t)min(64, n - s0) - __popcll(mask);
 #endif
+      if (pairs) {
+        // the per-point test of each kept face (the wave test's bound with this lane's point, R = 0),
+        // passing pairs appended to the ring
+        while (mask) {
+          const int sj = s0 + __builtin_ctzll(mask);
+          mask &= mask - 1;
+          const FaceRec<T> &fr = sf[sj];
+          const T sl = (T)(256.0 * P2M_E) * (cinf + R + fr.hmax);
+          const T A = fmax(fabs(dot(p, fr.un) - sp.dv[sj]) - fr.thick - sl, (T)0);
+          T b = dot(p, mk(sp.o[0][sj], sp.o[1][sj], sp.o[2][sj])) - sp.off[0][sj];
+          b = fmax(b, dot(p, mk(sp.o[3][sj], sp.o[4][sj], sp.o[5][sj])) - sp.off[1][sj]);
+          b = fmax(b, dot(p, mk(sp.o[6][sj], sp.o[7][sj], sp.o[8][sj])) - sp.off[2][sj]);
+          const T B = fmax(b - sl, (T)0);
+          const T K = psq + sl;
+          const bool pass = valid && !((A * A + B * B) * (T)(1.0 - 32.0 * P2M_E) > K * K * (T)(1.0 + 32.0 * P2M_E));
+          const uint64_t pm = __ballot(pass);
+          if (pass) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+            s_q[wid][(qhead + qcnt + rank) & (P2M_QCAP - 1)] = (uint16_t)(lane | (sj << 6));
+          }
+          qcnt += (uint32_t)__popcll(pm);
+          if (qcnt >= 64) {
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            run_batch(64);
+          }
+        }
+        continue;
+      }
       // fold one evaluated face into the reference's tile-wise running minimum
       auto fold = [&](int64_t f, float d, int t) {
         if ((f & 511) == 0) {  // a reference tile begins: merge the previous tile, restart
@@ -340,8 +418,13 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
         }
       }
     }
+    if (pairs && qcnt) {  // the tile's records are rewritten next: drain the ring
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      run_batch((int)qcnt);
+    }
     if (share && valid) {
-      const float cur = (float)fmin(best, tbest);
+      const float cur = pairs ? (float)pthr : (float)fmin(best, tbest);
       if (cur < published) {
         atomicMin(gbest + si, __float_as_uint(cur));
         published = cur;
@@ -355,7 +438,13 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
   }
 #endif
   if (!valid) return;
-  if (f_end > f_begin && ((first_split && f_end <= 512) || best > tbest)) {
+  if (pairs) {
+    const unsigned long long key = s_best[threadIdx.x];
+    // no pair of this split passed (another split holds a strictly better face): +inf, never chosen
+    best = key == KEY_NONE ? (T)INFINITY : (T)__uint_as_float((uint32_t)(key >> 32));
+    best_f = key == KEY_NONE ? 0 : (int64_t)((uint32_t)key >> 3);
+    best_t = key == KEY_NONE ? 0 : (int)(key & 7u);
+  } else if (f_end > f_begin && ((first_split && f_end <= 512) || best > tbest)) {
     best = tbest; best_f = tbest_f; best_t = tbest_t;
   }
   if (part_dist) {
@@ -975,8 +1064,11 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
       hipLaunchKernelGGL((p2m_fwd_grec_kernel<T, true>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st,
                          (const T *)pts, (const FaceRecS<T> *)rec, (const T *)pr, L.Fp, order, P, F, split_faces,
                          (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
+  } else if (g_dev_param[11] == 4 || !order) {  // dev param 11 = 4: the wave-level walk alone (r04)
+    hipLaunchKernelGGL((p2m_fwd_kernel<T, false>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
+                       (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
   } else {
-    hipLaunchKernelGGL(p2m_fwd_kernel<T>, dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
+    hipLaunchKernelGGL((p2m_fwd_kernel<T, true>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
                        (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
   }
   KL_CHECK_LAUNCH();

@@ -1305,52 +1305,6 @@ __device__ __forceinline__ double take_soft(double *__restrict__ soft, int64_t i
   return v;
 }
 
-// Columns [c0, c1] (relative to ix0, inclusive; c0 > c1: none) of pixel row j whose centres can
-// pass the rasterizer's inside test for the face (tri_weights, rasterization_cuda.cu:95-130): the
-// exact triangle's interval on the row, widened by a bound on the float test's error; the whole
-// [0, ix1 - ix0] where that bound is not tight (degenerate or non-finite faces; an edge whose
-// function changes by less than the bound across a pixel sets no limit).  vm: the face's
-// coordinates x multiplier, as the forward tested them.  Every pixel the face can have won lies
-// in the interval, so the gather visits a superset of its pixels, as with the whole bbox.
-template <typename T>
-__device__ __forceinline__ void face_row_cols(const T vm[6], float sx, float sy, int H, int W, int j, int ix0,
-                                              int ix1, int &c0, int &c1) {
-  c0 = 0;
-  c1 = ix1 - ix0;
-  const double y = (double)(T)(sy * (float)(H - 2 * j - 1));  // the forward's pixel centre
-  const double ax = vm[0], ay = vm[1], bx = vm[2], by = vm[3], cx = vm[4], cy = vm[5];
-  // edge functions E_i(x) = a_i x + b_i on the row, as tri_weights' w0, w1, w2 (exact here)
-  const double a[3] = {by - cy, cy - ay, ay - by};
-  const double b[3] = {bx * (cy - y) - cx * (by - y), cx * (ay - y) - ax * (cy - y), ax * (by - y) - bx * (ay - y)};
-  const double nrm = b[0] + b[1] + b[2];  // twice the signed area (the a_i sum to 0)
-  // |w_i - E_i| <= 8 u (|bex cey| + |bey cex|) <= 16 u ext^2 for the float evaluation at any
-  // candidate pixel (u = 2^-24; ext bounds |vertex - pixel centre|); err takes 4x that
-  const double ext = fmax(fmax(fabs(ax - bx), fabs(bx - cx)), fabs(cx - ax)) +
-                     fmax(fmax(fabs(ay - by), fabs(by - cy)), fabs(cy - ay)) + 4.0 * ((double)sx + (double)sy);
-  const double err = 64.0 * 5.9604644775390625e-8 * ext * ext;
-  if (!(fabs(nrm) > 8.0 * err) || !(ext < 1e30)) return;  // degenerate, NaN or inf: the whole row
-  const double sg = nrm > 0.0 ? 1.0 : -1.0, pitch = 2.0 * (double)sx;
-  double lo = -INFINITY, hi = INFINITY;
-#pragma unroll
-  for (int i = 0; i < 3; i++) {
-    const double ai = a[i] * sg, bi = b[i] * sg;  // a passing centre has ai x + bi >= -err
-    if (!(fabs(ai) * pitch > err)) continue;
-    const double xs = (-err - bi) / ai;
-    if (ai > 0.0) lo = fmax(lo, xs);
-    else hi = fmin(hi, xs);
-  }
-  // centre of column i: (float)(sx (2 i + 1 - W)), within 2^-23 |x| of the exact product
-  const double mg = 2.4e-7 * fmax(fabs(lo), fabs(hi)) + 1e-3 * pitch;
-  if (lo > -INFINITY) {
-    const double il = ceil(((lo - mg) / (double)sx + (double)(W - 1)) * 0.5);
-    if (il > (double)ix0) c0 = il > (double)ix1 ? ix1 - ix0 + 1 : (int)il - ix0;
-  }
-  if (hi < INFINITY) {
-    const double ih = floor(((hi + mg) / (double)sx + (double)(W - 1)) * 0.5);
-    if (ih < (double)ix1) c1 = ih < (double)ix0 ? -1 : (int)ih - ix0;
-  }
-}
-
 template <typename T, int MAXD>
 __device__ __forceinline__ void g2_store(int64_t tf, int q, double x, int D, double sv, T *__restrict__ grad_fvi,
                                          T *__restrict__ grad_ffeat) {
@@ -1368,7 +1322,9 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
     const T *__restrict__ fvi, const T *__restrict__ feat, const uint8_t *__restrict__ valid,
     const T *__restrict__ nz, int B, int H, int W, int F, int D, float m, float eps, T *__restrict__ grad_fvi,
     T *__restrict__ grad_ffeat, const uint2 *__restrict__ rng, double *__restrict__ soft,
-    uint8_t *__restrict__ sflag, int nbig, int spans) {
+    uint8_t *__restrict__ sflag, int nbig, int opts) {
+  // dev (param 17) opts bit 1: no soft / flag re-zeroing, bit 2: soft read unflagged (timing only)
+  const bool rz = !(opts & 2), nofl = opts & 4;
   constexpr int NV = 6 + 3 * MAXD;
   __shared__ double s_part[4][NV][64];  // per wave: per lane (thread) partial sums, value-major
   __shared__ int s_nbig;
@@ -1423,11 +1379,12 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
         __syncthreads();
         if ((int)threadIdx.x < NV) {
           const int q = threadIdx.x;
-          const bool fl = soft && q < 6 && sflag[bf];
+          const bool fl = soft && q < 6 && (nofl || sflag[bf]);
           double x = 0.0;
           for (int t = 0; t < 256; t++) x += s_part[t >> 6][q][t & 63];
-          g2_store<T, MAXD>(bf, q, x, D, fl ? take_soft(soft, bf * DS_ACC_STRIDE + q) : 0.0, grad_fvi, grad_ffeat);
-          if (fl && q == 0) sflag[bf] = 0;  // after the flag's use: every lane of the wave has read it
+          g2_store<T, MAXD>(bf, q, x, D, fl ? (rz ? take_soft(soft, bf * DS_ACC_STRIDE + q) : soft[bf * DS_ACC_STRIDE + q]) : 0.0,
+                            grad_fvi, grad_ffeat);
+          if (rz && fl && q == 0) sflag[bf] = 0;  // after the flag's use: every lane of the wave has read it
         }
         __syncthreads();
 #pragma unroll
@@ -1445,18 +1402,18 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
   const bool has = in && range_of(tf, ix0, ix1, iy0, iy1);
   const bool act = has && (int64_t)(ix1 - ix0 + 1) * (iy1 - iy0 + 1) <= VIS_SMALL_AREA;
   // the face's soft-sum flag (all 8 lanes read the same byte)
-  const bool fl = soft && in && sflag[tf];
+  const bool fl = soft && in && (nofl || sflag[tf]);
   if (in && !has) {  // no pixel: zero gradients (+ the soft mask's sums); lane s writes q = s, s + 8, ...
 #pragma unroll
     for (int q = s; q < NV; q += 8) {
       if (q < 6) {
-        grad_fvi[tf * 6 + q] = fl ? (T)0 + (T)take_soft(soft, tf * DS_ACC_STRIDE + q) : (T)0;
+        grad_fvi[tf * 6 + q] = fl ? (T)0 + (T)(rz ? take_soft(soft, tf * DS_ACC_STRIDE + q) : soft[tf * DS_ACC_STRIDE + q]) : (T)0;
       } else {
         const int r = q - 6, ii = r / MAXD, d = r % MAXD;
         if (d < D) grad_ffeat[tf * 3 * D + ii * D + d] = (T)0;
       }
     }
-    if (fl && s == 0) sflag[tf] = 0;  // after the flag's use
+    if (rz && fl && s == 0) sflag[tf] = 0;  // after the flag's use
   }
   if (!__any(act)) return;  // wave-uniform
 #pragma unroll
@@ -1473,14 +1430,21 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
     const T *c = feat + tf * 3 * D;
     const int64_t pbase = (int64_t)b * H * W;
     const int64_t pfirst = pbase + (int64_t)iy0 * W + ix0;
-    // one batch: face_idx, weights and grads of GATHER_BATCH pixels in flight together (the range's
-    // first pixel stands in for slots past the end), then the face's won pixels among them
-    auto batch = [&](const int64_t (&px)[GATHER_BATCH], uint32_t inb) {
+    RangeWalkN<8> rw(ix0, ix1, iy0, iy1, s);
+    while (rw.more()) {
+      // face_idx, weights and grads of GATHER_BATCH pixels in flight together (the range's first
+      // pixel stands in past the range's end)
       int64_t fi[GATHER_BATCH];
       T wv[GATHER_BATCH][3], gv[GATHER_BATCH][MAXD];
+      uint32_t inb = 0;
 #pragma unroll
       for (int u = 0; u < GATHER_BATCH; u++) {
-        const int64_t p = px[u];
+        int64_t p = pfirst;
+        if (rw.more()) {
+          p = pbase + (int64_t)(iy0 + rw.row) * W + ix0 + rw.col;
+          inb |= 1u << u;
+        }
+        rw.next();
         fi[u] = face_idx[p];
 #pragma unroll
         for (int k = 0; k < 3; k++) wv[u][k] = wts[p * 3 + k];
@@ -1513,67 +1477,6 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
           g2_add<T, MAXD, ATOM>(part, v, c, D, a0, a1, a2, g, eps);
         }
       }
-    };
-    if (spans && iy1 - iy0 < 8) {
-      // faces of <= 8 rows: only each row's columns the face can cover (face_row_cols; lane s
-      // computes row s), concatenated row by row, lane s taking elements s, s + 8, ...; every lane
-      // holds the rows' (first column, element prefix) packed in 8 registers
-      int c0 = 0, c1 = -1;
-      if (s <= iy1 - iy0) {
-        T vm[6];
-#pragma unroll
-        for (int q = 0; q < 6; q++) vm[q] = v[q] * (T)m;
-        face_row_cols<T>(vm, m / (float)W, m / (float)H, H, W, iy0 + s, ix0, ix1, c0, c1);
-      }
-      const int len = c1 >= c0 ? c1 - c0 + 1 : 0;
-      int pre = len;
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        const int u = __shfl_up(pre, o, 8);
-        if (s >= o) pre += u;
-      }
-      const int tot = __shfl(pre, 7, 8);
-      pre -= len;
-      int rk[8];  // row r: element prefix << 16 | first column
-#pragma unroll
-      for (int r = 0; r < 8; r++) rk[r] = __shfl((pre << 16) | c0, r, 8);
-      for (int base = 0; base < tot; base += 8 * GATHER_BATCH) {  // uniform over the face's lanes
-        int64_t px[GATHER_BATCH];
-        uint32_t inb = 0;
-#pragma unroll
-        for (int u = 0; u < GATHER_BATCH; u++) {
-          const int t = base + s + 8 * u;
-          int r = 0, sel = rk[0];
-#pragma unroll
-          for (int k = 1; k < 8; k++)
-            if ((rk[k] >> 16) <= t && k <= iy1 - iy0) {
-              r = k;
-              sel = rk[k];
-            }
-          px[u] = pfirst;
-          if (t < tot) {
-            px[u] = pbase + (int64_t)(iy0 + r) * W + ix0 + (sel & 0xffff) + (t - (sel >> 16));
-            inb |= 1u << u;
-          }
-        }
-        batch(px, inb);
-      }
-    } else {
-      RangeWalkN<8> rw(ix0, ix1, iy0, iy1, s);
-      while (rw.more()) {
-        int64_t px[GATHER_BATCH];
-        uint32_t inb = 0;
-#pragma unroll
-        for (int u = 0; u < GATHER_BATCH; u++) {
-          px[u] = pfirst;
-          if (rw.more()) {
-            px[u] = pbase + (int64_t)(iy0 + rw.row) * W + ix0 + rw.col;
-            inb |= 1u << u;
-          }
-          rw.next();
-        }
-        batch(px, inb);
-      }
     }
   }
   __builtin_amdgcn_wave_barrier();
@@ -1587,12 +1490,12 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
       for (int l = 0; l < 8; l++) x += s_part[wid][q][g0 + l];
       if (q < 6) {  // q == s: the prefetched sum, re-zeroed as take_soft does
         grad_fvi[tf * 6 + q] = (T)x + (T)soft_v;
-        if (__double_as_longlong(soft_v) != 0) soft[tf * DS_ACC_STRIDE + q] = 0.0;
+        if (rz && __double_as_longlong(soft_v) != 0) soft[tf * DS_ACC_STRIDE + q] = 0.0;
       } else {
         g2_store<T, MAXD>(tf, q, x, D, 0.0, grad_fvi, grad_ffeat);
       }
     }
-    if (fl && s == 0) sflag[tf] = 0;  // after the flag's use
+    if (rz && fl && s == 0) sflag[tf] = 0;  // after the flag's use
   }
 }
 
@@ -1623,6 +1526,9 @@ static int rasterize_bwd(int B, int H, int W, int F, int D, const void *grad, co
   return acc_finalize<T>(af, (T *)gfeat, nf, false, st);
 }
 
+// gather2 dev ablations (param 17; bits 1, 2: timing only, they break the zero-kept accumulator)
+static int gather_opts() { return (g_dev_param[17] & 3) << 1; }
+
 // nbig: a zeroed int (zero_nbig: this call zeroes it first).
 template <typename T, int MAXD>
 static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T *grad, const int64_t *face_idx,
@@ -1635,11 +1541,11 @@ static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T 
     if (g_dev_param[8] != 1)  // dev param 8 = 1: read-modify-write partials (A/B: 73 against 48 us at cfg3)
       hipLaunchKernelGGL((rasterize_bwd_gather2_kernel<T, MAXD, true>), dim3((unsigned)(nb + cdiv(nf * 8, 256))),
                          dim3(256), 0, st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat,
-                         rng, soft, sflag, nb, g_dev_param[16] != 1);
+                         rng, soft, sflag, nb, gather_opts());
     else
       hipLaunchKernelGGL((rasterize_bwd_gather2_kernel<T, MAXD>), dim3((unsigned)(nb + cdiv(nf * 8, 256))), dim3(256),
                          0, st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, rng, soft,
-                         sflag, nb, g_dev_param[16] != 1);
+                         sflag, nb, gather_opts());
     KL_CHECK_LAUNCH();
     return KL_OK;
   }
@@ -1821,7 +1727,7 @@ namespace kl {
 //           item count | soft order | soft pixel ranges     (records sized for f64)
 struct DibrFwdWs {
   size_t off_sbm, off_rgh, off_sgh, off_tk, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder,
-      off_sn, off_srng, off_defer, off_pk, off_whist, bytes;
+      off_sn, off_srng, off_defer, off_whist, bytes;
   DibrFwdWs(int B, int H, int W, int F) {
     const BinGeom g = make_bin_geom(B, H, W, F);
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
@@ -1841,8 +1747,7 @@ struct DibrFwdWs {
     off_sn = off_sorder + nt * TILE_H * sizeof(int32_t);
     off_srng = up(off_sn + sizeof(int));
     off_defer = up(off_srng + (size_t)B * F * sizeof(uint2));
-    off_pk = up(off_defer + (size_t)B * H * g.tiles_x);  // 2 x nt packed (rank, bucket)
-    off_whist = up(off_pk + 2 * nt * sizeof(uint32_t));    // 2 x nb x ORD_HIST workgroup histograms
+    off_whist = up(off_defer + (size_t)B * H * g.tiles_x);  // 2 x nb x ORD_HIST workgroup histograms
     bytes = off_whist + 2 * (size_t)cdiv((int64_t)nt, CO_THREADS) * ORD_HIST * sizeof(int);
   }
 };
@@ -1947,8 +1852,6 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     ca.words = g.words;
     ca.nt = nt;
     ca.nb = nb;
-    ca.pk[0] = reinterpret_cast<uint32_t *>(w + L.off_pk);
-    ca.pk[1] = ca.pk[0] + nt;
     ca.whist[0] = reinterpret_cast<int *>(w + L.off_whist);
     ca.whist[1] = ca.whist[0] + (size_t)nb * ORD_HIST;
     ca.ticket = reinterpret_cast<unsigned *>(w + L.off_tk);

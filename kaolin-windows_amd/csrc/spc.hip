@@ -1738,6 +1738,170 @@ __global__ void rt_fused_result_kernel(const RtlCtl *__restrict__ ctl, uint32_t 
   }
 }
 
+// ---- Per-ray depth-first march (r05, the eager entry): the level march's output is ray-major, and
+// within a ray each nugget's children follow it in front-to-back order, level by level -- which is
+// exactly the order of a depth-first walk that visits a node's children front to back (every level's
+// list restricted to one ray is that ray's walk order at that level, and a leaf's position is its
+// rank in the walk).  So each lane walks its own ray through the octree with the same per-node
+// decision (rt_decide_one's ray_aabb and keep rules, the same front-to-back child order as
+// rt_children): no nugget lists in HBM, no per-level scans or host reads.  A hit node is expanded
+// in two dependent loads: its point, octree byte and exsum, then ALL its children's points together,
+// whose decisions are made at once -- the hit ones pushed (a per-level LDS stack of child offsets),
+// or at the target level emitted.  Two passes: hits per ray (COUNT), then, after a scan over the
+// rays, the same walk writing each hit at its ray's offset.
+constexpr int RTD_THREADS = 64;
+constexpr int RTD_MAXL = SPC_MAX_LEVELS + 1;
+
+// children of a node in front-to-back order from the origin's octant code: increasing Hamming
+// distance to the code, then index (rt_children) -- one nibble per child index, 8 per code
+__constant__ uint32_t c_rt_perm[8] = {0x76534210u, 0x67425301u, 0x57416302u, 0x46507213u,
+                                      0x37216504u, 0x26307415u, 0x15307426u, 0x04216537u};
+
+template <bool WRITE>
+__global__ void __launch_bounds__(RTD_THREADS) rt_dfs_kernel(RayIn in, int64_t num_rays, uint32_t target_level,
+                                                             int with_depth, int with_exit,
+                                                             uint32_t *__restrict__ cnt,
+                                                             const uint32_t *__restrict__ off,
+                                                             int2 *__restrict__ nout, float *__restrict__ dout) {
+  __shared__ uint32_t s_list[RTD_MAXL][RTD_THREADS];  // pending hit nodes of a level (offsets 1..8)
+  __shared__ int32_t s_base[RTD_MAXL][RTD_THREADS];   // their parent's exsum
+  const int64_t ridx = blockIdx.x * (int64_t)RTD_THREADS + threadIdx.x;
+  if (ridx >= num_rays) return;
+  const int tx = threadIdx.x;
+  const float o[3] = {in.ro[ridx * 3], in.ro[ridx * 3 + 1], in.ro[ridx * 3 + 2]};
+  const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
+  const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
+  const float xs[3] = {signbit(-d[0]) ? 1.0f : -1.0f, signbit(-d[1]) ? 1.0f : -1.0f, signbit(-d[2]) ? 1.0f : -1.0f};
+  const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
+  const float oh[3] = {0.5f * o[0] + 0.5f, 0.5f * o[1] + 0.5f, 0.5f * o[2] + 0.5f};
+  const int dd = with_exit ? 2 : 1;
+  uint32_t n = 0;
+  uint32_t pos = WRITE ? off[ridx] : 0u;
+  // a node's decision at level lv (rt_decide_one): keep flag at the target level, else dv != 0
+  auto decide = [&](int16_t qx, int16_t qy, int16_t qz, uint32_t lv, float &en, float &ex) -> bool {
+    const float r = (float)(1.0 / (double)(float)(1u << lv));
+    const float vc[3] = {fmaf(r, fmaf(2.0f, (float)qx, 1.0f), -1.0f), fmaf(r, fmaf(2.0f, (float)qy, 1.0f), -1.0f),
+                         fmaf(r, fmaf(2.0f, (float)qz, 1.0f), -1.0f)};
+    en = ray_aabb(o, d, inv, sgn, vc, r);
+    if (lv != target_level) return en != 0.0f;
+    if (with_depth && with_exit) {
+      ex = ray_aabb(o, d, inv, xs, vc, r);
+      return en > 0.0f && ex > 0.0f;
+    }
+    return en > 0.0f;
+  };
+  auto emit = [&](int pidx, float en, float ex) {
+    if (WRITE) {
+      nout[pos] = make_int2((int)ridx, pidx);
+      if (dout && with_depth) {
+        dout[(int64_t)pos * dd] = en;
+        if (with_exit) dout[(int64_t)pos * dd + 1] = ex;
+      }
+      pos++;
+    } else {
+      n++;
+    }
+  };
+  {  // the root (level 0)
+    float en, ex = 0.0f;
+    const bool hit = decide(in.points[0], in.points[1], in.points[2], 0, en, ex);
+    if (target_level == 0) {
+      if (hit) emit(0, en, ex);
+    } else if (hit) {
+      int pidx = 0;
+      uint32_t l = 0;
+      for (;;) {
+        // ---- expand hit node pidx of level l < target: its point, octree byte and exsum
+        const int16_t *pp = in.points + (int64_t)pidx * 3;
+        const float px = (float)pp[0], py = (float)pp[1], pz = (float)pp[2];
+        const uint32_t ob = in.octree[pidx];
+        const int32_t s = in.exsum[pidx];
+        const float r = (float)(1.0 / (double)(float)(1u << l));
+        const float x = (float)((double)oh[0] - (double)r * ((double)px + 0.5));
+        const float y = (float)((double)oh[1] - (double)r * ((double)py + 0.5));
+        const float z = (float)((double)oh[2] - (double)r * ((double)pz + 0.5));
+        const uint32_t perm = c_rt_perm[(x > 0 ? 4u : 0u) + (y > 0 ? 2u : 0u) + (z > 0 ? 1u : 0u)];
+        // the children in front-to-back order (offsets 1..8 from s) and all their points at once
+        uint32_t cof[8];
+        int nk = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const uint32_t j = (perm >> (4 * q)) & 15u;
+          cof[q] = 0;
+          if (ob & (1u << j)) cof[nk++] = (uint32_t)__popc(ob & ((2u << j) - 1));
+        }
+        int16_t cp[8][3];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const int16_t *c = in.points + (int64_t)(k < nk ? s + (int)cof[k] : pidx) * 3;
+          cp[k][0] = c[0];
+          cp[k][1] = c[1];
+          cp[k][2] = c[2];
+        }
+        const uint32_t lc = l + 1;
+        uint32_t hits = 0;
+        int nh = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          if (k < nk) {
+            float en, ex = 0.0f;
+            if (decide(cp[k][0], cp[k][1], cp[k][2], lc, en, ex)) {
+              if (lc == target_level) {
+                emit(s + (int)cof[k], en, ex);
+              } else {
+                hits |= cof[k] << (4 * nh);
+                nh++;
+              }
+            }
+          }
+        }
+        uint32_t m = l;  // the deepest level with pending nodes
+        if (nh) {
+          s_list[lc][tx] = hits;
+          s_base[lc][tx] = s;
+          m = lc;
+        }
+        while (m > 0 && s_list[m][tx] == 0u) m--;
+        if (m == 0) break;
+        const uint32_t lst = s_list[m][tx];
+        s_list[m][tx] = lst >> 4;
+        pidx = s_base[m][tx] + (int)(lst & 15u);
+        l = m;
+      }
+    }
+  }
+  if (!WRITE) cnt[ridx] = n;
+}
+
+// host-sized raytrace by the depth-first march: counts, scan (one host read of the total), writes
+static int rt_dfs(const RayIn &in, int64_t num_rays, uint32_t target_level, int return_depth, int with_exit,
+                  Scratch &sc, int32_t **nuggets, float **depth, int64_t *num_hits, hipStream_t st) {
+  const int dd = with_exit ? 2 : 1;
+  const size_t cb = al256b((size_t)(num_rays + 1) * sizeof(uint32_t));
+  uint32_t *cnt = (uint32_t *)sc.get(cb + (size_t)(num_rays + 2) * sizeof(uint32_t));
+  if (!cnt) return KL_E_ALLOC;
+  uint32_t *off = (uint32_t *)((char *)cnt + cb);
+  KL_CHECK_RC(fill_async(cnt + num_rays, 0, sizeof(uint32_t), st));  // the scan's (n + 1)-th input
+  const unsigned grid = (unsigned)cdiv(num_rays, RTD_THREADS);
+  hipLaunchKernelGGL(rt_dfs_kernel<false>, dim3(grid), dim3(RTD_THREADS), 0, st, in, num_rays, target_level,
+                     return_depth, with_exit, cnt, (const uint32_t *)nullptr, (int2 *)nullptr, (float *)nullptr);
+  KL_CHECK_LAUNCH();
+  uint32_t total = 0;
+  KL_CHECK_RC(exclusive_scan(cnt, off, num_rays, sc, st, &total));
+  int2 *out = (int2 *)sc.get((size_t)total * sizeof(int2));
+  float *dout = return_depth ? (float *)sc.get(std::max<size_t>((size_t)total * dd * sizeof(float), 16)) : nullptr;
+  if (!out || (return_depth && !dout)) return KL_E_ALLOC;
+  if (total) {
+    hipLaunchKernelGGL(rt_dfs_kernel<true>, dim3(grid), dim3(RTD_THREADS), 0, st, in, num_rays, target_level,
+                       return_depth, with_exit, (uint32_t *)nullptr, (const uint32_t *)off, out, dout);
+    KL_CHECK_LAUNCH();
+  }
+  *nuggets = (int32_t *)out;
+  *depth = dout;
+  *num_hits = total;
+  return KL_OK;
+}
+
 template <typename S>
 __global__ void pack_bounds_kernel(int64_t n, const S *__restrict__ ids, int32_t *__restrict__ out) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -1909,9 +2073,16 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
   // the fused march (rt_level_kernel), every level's count on the device and ONE host read at the
   // end, with buffers of 16 nuggets per ray; a level with more falls back to the per-level march
   // below (dev param 15 = 2: that march always, for A/B)
-  const int64_t fcap = std::max<int64_t>(16 * num_rays, 1 << 16);
   g_dev_stat[1] = 0;
-  if (num_rays > 0 && fcap < ((int64_t)1 << 31) && g_dev_param[15] != 2) {
+  // default: the per-ray depth-first march (rt_dfs); dev param 15 = 2: the per-level march, 3: the
+  // fused level march first (both kept for A/B: at cfg4 2.85 and 1.11 ms)
+  if (num_rays > 0 && num_rays < ((int64_t)1 << 31) && g_dev_param[15] != 2 && g_dev_param[15] != 3 &&
+      target_level < (uint32_t)RTD_MAXL) {
+    g_dev_stat[1] = 3;
+    return rt_dfs(in, num_rays, target_level, return_depth, with_exit, sc, nuggets, depth, num_hits, st);
+  }
+  const int64_t fcap = std::max<int64_t>(16 * num_rays, 1 << 16);
+  if (num_rays > 0 && fcap < ((int64_t)1 << 31) && g_dev_param[15] == 3) {
     const int64_t ntiles_max = cdiv(fcap, (int64_t)RTL_TILE);
     const size_t buf = al256b((size_t)fcap * sizeof(int2));
     char *w = (char *)sc.get(al256b(sizeof(RtlCtl)) + al256b((size_t)ntiles_max * 8) + 2 * buf);

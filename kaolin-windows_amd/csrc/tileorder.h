@@ -385,21 +385,22 @@ static __global__ void __launch_bounds__(1024) tile_countorder2_kernel(
 // whose two ordering workgroups counted 2 x 2,048 tiles alone: 13.9 us at cfg3, 7.6 of it the
 // count).  Workgroups [0, nb) count the rasterizer's bitmap, [nb, 2 nb) the soft mask's, one tile
 // per thread; each computes its tiles' ranks within (band, bucket) in tile order (per-wave counts
-// in LDS), then publishes its (band, bucket) histogram and every tile's (rank << 8 | bucket) with
-// sc1 stores and adds to its bitmap's ticket (MI355X_MICROARCH.md hand-off table, first row: every
-// storing wave waits vmcnt(0), a workgroup barrier, one lane's agent-scope add; the workgroup
-// whose add comes last loads everything sc1).  That last workgroup turns the histograms into each
-// workgroup's base per key (tile order again: the same ranks place_items gives), parts and
-// prefixes (place_prefix), and writes the items at place_pos -- the same order as before.
-// Workgroups [2 nb, grid) zero `zacc` (the backward's soft accumulator) and `zero` meanwhile.
+// in LDS) and publishes its (band, bucket) histogram with sc1 stores, then meets its bitmap's other
+// count workgroups at a grid barrier (MI355X_MICROARCH.md hand-off table, first row: every storing
+// wave waits vmcnt(0), a workgroup barrier, one lane's agent-scope add; the readers load sc1).  Each
+// then loads all the histograms, computes its base per key (the earlier workgroups' counts: tile
+// order again, the same ranks place_items gives), the parts and prefixes (place_prefix), and writes
+// its OWN tiles' items at place_pos -- the same order as before.  (r05 before this: the bitmap's
+// last workgroup, found by a ticket, did the prefix and placed all nt tiles alone, reading every
+// tile's packed rank back: 3.7 + 3.8 us of the kernel's 12.7 behind the 3.4 us count, stamps.)
+// Workgroup 2 nb zeroes `zero` (and `zacc`, when given) meanwhile.
 constexpr int CO_THREADS = 512;
 constexpr int CO_MAX_BLOCKS = ORD_LDS_TILES / CO_THREADS;  // count workgroups per bitmap
 struct CountOrderArgs {
   const uint32_t *bm[2];
   int words, nt, nb;
-  uint32_t *pk[2];      // per tile: rank in its workgroup and key << 8 | bucket
   int *whist[2];        // per count workgroup: (band, bucket) histogram [nb][ORD_HIST]
-  unsigned *ticket;     // [2], zero on entry; left zero
+  unsigned *ticket;     // [2], zero on entry (the binning kernel's zeroed region): the grid barriers
   int32_t *order[2];
   int *nitems[2];
   int split_from, split_log2;  // the rasterizer's parts
@@ -409,15 +410,14 @@ struct CountOrderArgs {
   int nzero;
   double *zacc;
   size_t zn;
-  uint64_t *dbg = nullptr;  // dev stamps (wall clock): count workgroup b at 4 b (start, counted, ticket);
-                            // bitmap w's last workgroup at 64 + 4 w (start, prefix, placed)
+  uint64_t *dbg = nullptr;  // dev stamps (wall clock): count workgroup b at 4 b (start, counted, arrived);
+                            // bitmap w's workgroup 0 at 64 + 4 w (barrier passed, prefix, placed)
 };
 
 static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel(CountOrderArgs a) {
-  __shared__ int s_wk[CO_THREADS / 64][ORD_HIST];  // per-wave key counts; the last workgroup: [nb][ORD_HIST] bases
+  __shared__ int s_wk[CO_THREADS / 64][ORD_HIST];  // per-wave key counts; after the barrier: this workgroup's bases
   __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS], hist[ORD_HIST];
-  __shared__ int s_last;
-  extern __shared__ int s_big[];  // last workgroup: [nb][ORD_HIST] per-workgroup bases
+  extern __shared__ int s_big[];  // [nb][ORD_HIST]: every count workgroup's histogram
   const int nb = a.nb, nt = a.nt;
   if ((int)blockIdx.x >= 2 * nb) {
     const int part = blockIdx.x - 2 * nb, nparts = gridDim.x - 2 * nb;
@@ -464,11 +464,9 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
     }
   }
   __syncthreads();
-  if (key >= 0) {
-    int r = wrank;
-    for (int w = 0; w < wid; w++) r += s_wk[w][key];
-    __hip_atomic_store(a.pk[which] + t, ((uint32_t)r << 8) | (uint32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  int rank = wrank;  // the tile's rank among this workgroup's tiles of its key
+  if (key >= 0)
+    for (int w = 0; w < wid; w++) rank += s_wk[w][key];
   for (int k = threadIdx.x; k < ORD_HIST; k += blockDim.x) {
     int h = 0;
 #pragma unroll
@@ -477,17 +475,20 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // ---- grid barrier of the bitmap's nb count workgroups (all co-resident: at most 2 x 32 + 1
+  //      workgroups of 512 threads), on the ticket the binning kernel zeroed
   if (threadIdx.x == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(a.ticket + which, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == (unsigned)nb - 1;
+    __hip_atomic_fetch_add(a.ticket + which, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (dbg) dbg[2] = stamp_wall();
+    while (__hip_atomic_load(a.ticket + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nb)
+      __builtin_amdgcn_s_sleep(1);
   }
   __syncthreads();
-  if (!s_last) return;
-  uint64_t *const ldbg = kDevStamps && a.dbg ? a.dbg + 64 + which * 4 : nullptr;
+  uint64_t *const ldbg = kDevStamps && a.dbg && blk == 0 ? a.dbg + 64 + which * 4 : nullptr;
   if (ldbg && threadIdx.x == 0) ldbg[0] = stamp_wall();
-  // ---- the last workgroup of this bitmap: bases per (workgroup, key), totals, parts, prefix, items.
-  //      Every global read here is sc1 and issued eight at a time (one round trip per batch).
+  // ---- every count workgroup: all histograms (sc1 loads, eight per thread in flight), its own
+  //      base per key (the earlier workgroups' counts: tile order), the totals, parts and prefixes
+  //      (place_prefix), then its own tiles' items at place_pos -- the order the r04 kernel gave
   constexpr int BATCH = 8;
   const int nh = nb * ORD_HIST;
   for (int i0 = threadIdx.x; i0 < nh; i0 += BATCH * blockDim.x) {
@@ -501,42 +502,30 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
     for (int u = 0; u < BATCH; u++)
       if (i0 + u * (int)blockDim.x < nh) s_big[i0 + u * blockDim.x] = v[u];
   }
-  if (threadIdx.x == 0) __hip_atomic_store(a.ticket + which, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  int *const wbase = &s_wk[0][0];  // (the per-wave counts are consumed: this workgroup's base per key)
   for (int k = threadIdx.x; k < ORD_HIST; k += blockDim.x) {
-    int run = 0;
+    int run = 0, mine = 0;
     for (int b = 0; b < nb; b++) {
-      const int h = s_big[b * ORD_HIST + k];
-      s_big[b * ORD_HIST + k] = run;
-      run += h;
+      if (b == blk) mine = run;
+      run += s_big[b * ORD_HIST + k];
     }
     hist[k] = run;
+    wbase[k] = mine;
   }
-  __syncthreads();
   if (which == 0) {
     if (threadIdx.x < ORD_BUCKETS) lpb[threadIdx.x] = (int)threadIdx.x >= a.split_from ? a.split_log2 : 0;
   } else {
     soft_parts(sx, lpb, hist, a.lp_min1, a.sp, a.skip_empty1);
   }
-  place_prefix(sb, sx, lpb, hist, a.nitems[which]);
+  place_prefix(sb, sx, lpb, hist, blk == 0 ? a.nitems[which] : nullptr);
   if (ldbg && threadIdx.x == 0) ldbg[1] = stamp_wall();
-  int32_t *order = a.order[which];
-  for (int u0 = threadIdx.x; u0 < nt; u0 += BATCH * blockDim.x) {
-    uint32_t v[BATCH];
-#pragma unroll
-    for (int j = 0; j < BATCH; j++) {
-      const int u = u0 + j * blockDim.x;
-      v[j] = __hip_atomic_load(a.pk[which] + (u < nt ? u : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int j = 0; j < BATCH; j++) {
-      const int u = u0 + j * blockDim.x;
-      const int qq = (int)(v[j] & 0xffu), lp = u < nt ? lpb[qq] : -1;
-      if (lp < 0) continue;
-      const int g = tile_band(u, nt), kk = g * ORD_BUCKETS + qq;
-      const int np = 1 << lp;
-      const int r0 = sb[kk] + (s_big[(u / CO_THREADS) * ORD_HIST + kk] + (int)(v[j] >> 8)) * np;
-      for (int k = 0; k < np; k++) order[place_pos(sx, g, r0 + k)] = u | (k << 24) | (lp << 28);
+  if (key >= 0) {
+    const int lp = lpb[q];
+    if (lp >= 0) {
+      const int np = 1 << lp, g = key / ORD_BUCKETS;
+      const int r0 = sb[key] + (wbase[key] + rank) * np;
+      for (int k = 0; k < np; k++) a.order[which][place_pos(sx, g, r0 + k)] = t | (k << 24) | (lp << 28);
     }
   }
   if (ldbg) {

@@ -1,6 +1,6 @@
 """Wall-clock phase stamps of tile_countorder_chip_kernel (dev aid; a `make STAMPS=1` library
 loaded through KAOLIN_HIP_LIB).  Prints the count workgroups' (count, publish) and each bitmap's
-last workgroup's (prefix, placement) phases in microseconds from the earliest start."""
+workgroup 0's (barrier passed, prefix, placement) phases in microseconds from the earliest start."""
 import ctypes
 import os
 import sys
@@ -30,9 +30,9 @@ for rep in range(4):
     t0 = min(x for x in d if x)
     us = lambda x: (x - t0) / 100 if x else float('nan')  # noqa: E731
     cw = [(us(d[4 * b]), us(d[4 * b + 1]), us(d[4 * b + 2])) for b in range(16) if d[4 * b]]
-    print(f'rep {rep}: count workgroups (start, counted, ticket) us: ' +
+    print(f'rep {rep}: count workgroups (start, counted, arrived) us: ' +
           ' '.join(f'({a:.1f},{b:.1f},{c:.1f})' for a, b, c in cw))
     for w in range(2):
         s = d[64 + 4 * w:64 + 4 * w + 3]
-        print(f'  bitmap {w} last workgroup: start {us(s[0]):.2f} prefix {us(s[1]):.2f} placed {us(s[2]):.2f} us')
+        print(f'  bitmap {w} workgroup 0: barrier passed {us(s[0]):.2f} prefix {us(s[1]):.2f} placed {us(s[2]):.2f} us')
 lib.kl_dev_set_debug(None)

@@ -21,7 +21,7 @@ def main():
     fn = lambda: kal.metrics.trianglemesh.point_to_mesh_distance(pts, fv)  # noqa: E731
     ref = None
     for c in sys.argv[1:] or ['11=0']:
-        for i in range(16):
+        for i in range(32):
             lib.kl_dev_set_param(i, 0)
         for kv in c.split(','):
             i, v = (int(x) for x in kv.split('='))
@@ -37,7 +37,7 @@ def main():
         e.record()
         torch.cuda.synchronize()
         print(f'params {c}: point_to_mesh {s.elapsed_time(e) / 10:.3f} ms, equal to the first: {same}', flush=True)
-    for i in range(16):
+    for i in range(32):
         lib.kl_dev_set_param(i, 0)
 
 

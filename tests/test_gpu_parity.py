@@ -895,9 +895,16 @@ def test_p2m_vs_oracle(kal, P, F):
 
 
 def _p2m_stress(kind, dtype):
-    g = np.random.default_rng({'cfg2': 0, 'slivers': 1, 'scaled': 2, 'onsurface': 3}[kind])
+    g = np.random.default_rng({'cfg2': 0, 'slivers': 1, 'scaled': 2, 'onsurface': 3, 'dups': 4}[kind])
     if kind == 'cfg2':  # the bench distribution at a smaller size
         pts, fv = g.standard_normal((20000, 3)), g.standard_normal((1100, 3, 3))
+    elif kind == 'dups':  # proper faces duplicated within and across the face splits (distance ties)
+        fv = g.standard_normal((1100, 3, 3))
+        fv[600:700] = fv[0:100]
+        fv[1050:1100] = fv[20:70]
+        fv[300:310] = fv[290:300]
+        pts = g.standard_normal((20000, 3))
+        pts[:3000] = fv[g.integers(0, 100, 3000), 1]  # on duplicated vertices: distance-0 ties
     elif kind == 'slivers':  # needle / collinear / zero-area faces, duplicates across 512-tiles
         fv = g.standard_normal((1200, 3, 3))
         fv[::7, 2] = fv[::7, 0] + 1e-4 * g.standard_normal((len(fv[::7]), 3))       # needles
@@ -921,17 +928,25 @@ def _p2m_stress(kind, dtype):
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
-@pytest.mark.parametrize('kind', ['cfg2', 'slivers', 'scaled', 'onsurface'])
-def test_p2m_face_skipping_is_exact(kal, kind, dtype):
+@pytest.mark.parametrize('kind', ['cfg2', 'slivers', 'scaled', 'onsurface', 'dups'])
+@pytest.mark.parametrize('walk', ['pairs', 'wave'])
+def test_p2m_face_skipping_is_exact(kal, kind, dtype, walk):
     """P*F >= 2^24 takes the Morton-ordered path whose waves skip faces that provably cannot
-    be nearest; results must stay bit-identical to the oracle's full scan."""
+    be nearest; results must stay bit-identical to the oracle's full scan -- with the per-point pair
+    queue (default; proper faces and finite waves) and with the wave-level walk alone (dev param
+    11 = 4).  'dups': duplicated proper faces within and across the face splits, points on their
+    vertices (distance-0 ties: the earliest face wins)."""
     pts, fv = _p2m_stress(kind, dtype)
     P, F = len(pts), len(fv)
     assert P * F >= 1 << 24
     d = torch.empty(P, dtype=dtype, device=DEV)
     i = torch.empty(P, dtype=torch.long, device=DEV)
     t = torch.empty(P, dtype=torch.int32, device=DEV)
-    kal._C.metrics.unbatched_triangle_distance_forward_cuda(T(pts), T(fv), d, i, t)
+    try:
+        _dev_param(11, 4 if walk == 'wave' else 0)
+        kal._C.metrics.unbatched_triangle_distance_forward_cuda(T(pts), T(fv), d, i, t)
+    finally:
+        _dev_param(11, 0)
     od, oi, ot = orc.unbatched_triangle_distance_forward(pts, fv)
     assert np.array_equal(A(d), od, equal_nan=True)
     assert np.array_equal(A(i), oi) and np.array_equal(A(t), ot)
@@ -1530,13 +1545,15 @@ def test_raytrace_fixed_capture_and_truncation(kal):
     assert torch.equal(tr[:k], r2[:k]) and torch.equal(tp[:k], p2[:k]) and torch.equal(tdp[:k], dep2[:k])
 
 
-@pytest.mark.parametrize('level,nrays', [(4, 1000), (6, 1000), (6, 5)])
-def test_raytrace_fused_equals_per_level(kal, level, nrays):
-    """The fused level march (rt_level_kernel: one launch per level, counts on the device, one host
-    read) against the per-level march (dev param 15 = 2), nuggets and depths bit-equal, on a dense
-    level-6 octree: level 4 fits its buffers (16 nuggets per ray, at least 65,536), level 6 with
-    1,000 rays does not (~100 nuggets per ray): the fused march reports the truncation and the
-    per-level march answers (kl_dev_get_stat(1) == 2)."""
+@pytest.mark.parametrize('level,nrays', [(4, 1000), (6, 1000), (6, 5), (0, 64), (3, 130)])
+def test_raytrace_marches_agree(kal, level, nrays):
+    """The three marches of kl_raytrace, nuggets and depths (entry and exit) bit-equal: the per-ray
+    depth-first march (default, kl_dev_get_stat(1) == 3), the per-level march (dev param 15 = 2) and
+    the fused level march (dev param 15 = 3: one launch per level, counts on the device, one host
+    read), on a dense level-6 octree: level 4 fits the fused march's buffers (16 nuggets per ray, at
+    least 65,536), level 6 with 1,000 rays does not (~100 nuggets per ray): it reports the truncation
+    and the per-level march answers (stat 2).  Levels 0 and 3: the root alone, and ray counts that are
+    not a multiple of the depth-first march's 64-ray workgroups."""
     import ctypes
     from kaolin import _native as N
     lib = N.lib()
@@ -1551,7 +1568,7 @@ def test_raytrace_fused_equals_per_level(kal, level, nrays):
     d = -o + 0.3 * rng.normal(size=(nrays, 3))
     d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
     outs = {}
-    for mode in (0, 2):
+    for mode in (0, 2, 3):
         lib.kl_dev_set_param(15, mode)
         try:
             outs[mode] = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level, with_exit=True)
@@ -1559,13 +1576,23 @@ def test_raytrace_fused_equals_per_level(kal, level, nrays):
             outs[mode] += (lib.kl_dev_get_stat(1),)
         finally:
             lib.kl_dev_set_param(15, 0)
-    (r0, p0, d0, s0), (r2, p2, d2, s2) = outs[0], outs[2]
+    (r0, p0, d0, s0), (r2, p2, d2, s2), (r3, p3, d3, s3) = outs[0], outs[2], outs[3]
+    assert s0 == 3 and s2 == 0 and s3 in (1, 2) and (s3 == 2 or len(r2) <= max(16 * nrays, 65536))
     # 2 = a level's candidates (its parents' children) exceeded the fused march's buffers
-    assert s2 == 0 and s0 in (1, 2) and (s0 == 2 or len(r2) <= max(16 * nrays, 65536))
-    assert (level, nrays) != (6, 1000) or s0 == 2
-    assert (level, nrays) != (6, 5) or s0 == 1
-    assert torch.equal(r0, r2) and torch.equal(p0, p2) and torch.equal(d0, d2)
-    assert len(r2) > (1000 if nrays > 5 else 0)
+    assert (level, nrays) != (6, 1000) or s3 == 2
+    assert (level, nrays) != (6, 5) or s3 == 1
+    for r, p, dp in ((r0, p0, d0), (r3, p3, d3)):
+        assert torch.equal(r, r2) and torch.equal(p, p2) and torch.equal(dp, d2)
+    assert len(r2) > (1000 if nrays > 5 and level >= 4 else 0)
+    # without depth, and depth without exit
+    for kw in ({'return_depth': False}, {}):
+        lib.kl_dev_set_param(15, 2)
+        try:
+            ref = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level, **kw)
+        finally:
+            lib.kl_dev_set_param(15, 0)
+        got = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level, **kw)
+        assert len(got) == len(ref) and all(torch.equal(x, y) for x, y in zip(got, ref))
 
 
 @pytest.mark.parametrize('na,nb', [(0, 5), (7, 0), (3145728, 1048576), (1001, 333)])
