@@ -1863,6 +1863,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     ca.split_log2 = split_log2;
     ca.lp_min1 = soft_lp_min(K);
     ca.skip_empty1 = 1;
+    ca.noband = g_dev_param[18] & 3;  // dev param 18: bit 0 the rasterizer's, bit 1 the soft mask's items unbanded
     ca.sp = soft_split();
     ca.zero = bcnt;
     ca.nzero = DibrState::kZeroInts;

@@ -66,6 +66,10 @@ struct SoftTileArgs {
   int2 *bwd_items = nullptr;
   int *bwd_cnt = nullptr;
   int bwd_cap = 0;
+  // slot-list layout of soft_tile_fwd_kernel: slot k of lane p at k * 64 + ((p + (k & swz)) & 63).  The
+  // rotation (swz = 63) spreads a pixel's consecutive slots, which the evaluation's consecutive threads
+  // touch, over the banks; swz = 0 (dev param 19 = 1) is the plain [slot][lane] layout.
+  int swz = 63;
 };
 
 
@@ -111,6 +115,8 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   const bool covered = px_valid ? (a.sel[pix] >= 0) : true;
   const int64_t f0 = (int64_t)b * a.F;
   const int F = a.F;
+  const int swz = a.swz;
+  auto sl = [swz](int k, int p) { return k * 64 + ((p + (k & swz)) & 63); };
   uint64_t t0 = 0, w0 = 0, t1 = 0, c_fill = 0, tf = 0;
   int nchunks = 0;
   if (dbg) {
@@ -238,7 +244,7 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
           while (cm) {
             const int q = __builtin_ctzll(cm);
             cm &= cm - 1;
-            s_face[kid * 64 + lane] = L_face[base + q];
+            s_face[sl(kid, lane)] = L_face[base + q];
             if (++kid >= K) {
               active = false;
               cm = 0;
@@ -270,7 +276,7 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
           }
           const int base = blk * 64;
           while (cm && slot < K) {
-            s_face[slot * 64 + lane] = L_face[base + __builtin_ctzll(cm)];
+            s_face[sl(slot, lane)] = L_face[base + __builtin_ctzll(cm)];
             cm &= cm - 1;
             slot++;
           }
@@ -358,7 +364,7 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
         rr[u] = r0;
         ee[u] = e;
         const uint32_t *face_r = reinterpret_cast<const uint32_t *>(smem + st_head_lds() + st_row_lds(K) * r0);
-        ff[u] = g0 < all ? face_r[kk[u] * 64 + lo] : 0u;
+        ff[u] = g0 < all ? face_r[sl(kk[u], lo)] : 0u;
         if (kDevStamps && a.dev) ff[u] = min(ff[u], (uint32_t)(F - 1));  // dev ablations leave no face ids
       }
       T v[U][6];
@@ -379,7 +385,7 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
           a.rec_face[rb + ee[u]] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
           a.rec_prob[rb + ee[u]] = pr;
           T *prob_r = reinterpret_cast<T *>(smem + st_head_lds() + st_row_lds(K) * rr[u]);
-          prob_r[kk[u] * 64 + pp[u]] = pr;
+          prob_r[sl(kk[u], pp[u])] = pr;
         }
       }
     }
@@ -392,7 +398,7 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
       for (int k0 = 0; k0 < kid; k0 += 8) {
         T pk[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) pk[u] = s_prob[min(k0 + u, kid - 1) * 64 + lane];
+        for (int u = 0; u < 8; u++) pk[u] = s_prob[sl(min(k0 + u, kid - 1), lane)];
 #pragma unroll
         for (int u = 0; u < 8; u++)
           if (k0 + u < kid) allprob = (T)((double)allprob * (1.0 - (double)pk[u]));
@@ -405,7 +411,7 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
 #pragma unroll
       for (int st = 32; st > 0; st >>= 1)
         if (s_pre[lo + st] <= e) lo += st;
-      a.rec_face[rbase + e] = s_face[(e - s_pre[lo]) * 64 + lo];
+      a.rec_face[rbase + e] = s_face[sl(e - s_pre[lo], lo)];
     }
   }
   if (qi == 0 && (!a.prefilled || total > 0)) {
@@ -843,6 +849,7 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   args.bwd_items = bwd_items;
   args.bwd_cnt = bwd_cnt;
   args.bwd_cap = bwd_cap;
+  args.swz = g_dev_param[19] == 1 ? 0 : 63;
   hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)soft_items_bound(nt, lp_min, soft_split())), dim3(64 * ST_WAVES), lds,
                      st, args);
   KL_CHECK_LAUNCH();

@@ -405,6 +405,7 @@ struct CountOrderArgs {
   int *nitems[2];
   int split_from, split_log2;  // the rasterizer's parts
   int lp_min1, skip_empty1;    // the soft mask's
+  int noband = 0;              // bit w: bitmap w's items in plain heaviest-first order (no XCD bands)
   SoftSplit sp;
   int *zero;
   int nzero;
@@ -446,7 +447,8 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
     for (int u = 0; u < 32; u++) n += __popc(x[u]);
   }
   const int q = 31 - __clz(n + 1u);
-  const int key = t < nt ? tile_band(t, nt) * ORD_BUCKETS + q : -1;
+  const bool flat = (a.noband >> which) & 1;  // one band: plain heaviest-first positions
+  const int key = t < nt ? (flat ? 0 : tile_band(t, nt)) * ORD_BUCKETS + q : -1;
   if (dbg && threadIdx.x == 0) dbg[1] = stamp_wall();
   // rank within the workgroup for its key, in tile order: the wave's own rank (same-key lanes
   // below this one) now, the earlier waves' counts after the barrier
@@ -525,7 +527,8 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
     if (lp >= 0) {
       const int np = 1 << lp, g = key / ORD_BUCKETS;
       const int r0 = sb[key] + (wbase[key] + rank) * np;
-      for (int k = 0; k < np; k++) a.order[which][place_pos(sx, g, r0 + k)] = t | (k << 24) | (lp << 28);
+      for (int k = 0; k < np; k++)
+        a.order[which][flat ? r0 + k : place_pos(sx, g, r0 + k)] = t | (k << 24) | (lp << 28);
     }
   }
   if (ldbg) {
