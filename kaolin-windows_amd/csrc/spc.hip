@@ -1822,18 +1822,21 @@ __global__ void __launch_bounds__(RTD_THREADS) rt_dfs_kernel(RayIn in, int64_t n
         const float z = (float)((double)oh[2] - (double)r * ((double)pz + 0.5));
         const uint32_t perm = c_rt_perm[(x > 0 ? 4u : 0u) + (y > 0 ? 2u : 0u) + (z > 0 ? 1u : 0u)];
         // the children in front-to-back order (offsets 1..8 from s) and all their points at once
-        uint32_t cof[8];
+        // (packed in nibbles: a register array indexed by a running count would live in scratch)
+        uint32_t cl = 0;
         int nk = 0;
 #pragma unroll
         for (int q = 0; q < 8; q++) {
           const uint32_t j = (perm >> (4 * q)) & 15u;
-          cof[q] = 0;
-          if (ob & (1u << j)) cof[nk++] = (uint32_t)__popc(ob & ((2u << j) - 1));
+          if (ob & (1u << j)) {
+            cl |= (uint32_t)__popc(ob & ((2u << j) - 1)) << (4 * nk);
+            nk++;
+          }
         }
         int16_t cp[8][3];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-          const int16_t *c = in.points + (int64_t)(k < nk ? s + (int)cof[k] : pidx) * 3;
+          const int16_t *c = in.points + (int64_t)(k < nk ? s + (int)((cl >> (4 * k)) & 15u) : pidx) * 3;
           cp[k][0] = c[0];
           cp[k][1] = c[1];
           cp[k][2] = c[2];
@@ -1844,12 +1847,13 @@ __global__ void __launch_bounds__(RTD_THREADS) rt_dfs_kernel(RayIn in, int64_t n
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           if (k < nk) {
+            const uint32_t ck = (cl >> (4 * k)) & 15u;
             float en, ex = 0.0f;
             if (decide(cp[k][0], cp[k][1], cp[k][2], lc, en, ex)) {
               if (lc == target_level) {
-                emit(s + (int)cof[k], en, ex);
+                emit(s + (int)ck, en, ex);
               } else {
-                hits |= cof[k] << (4 * nh);
+                hits |= ck << (4 * nh);
                 nh++;
               }
             }

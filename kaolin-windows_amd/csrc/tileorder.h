@@ -174,29 +174,30 @@ inline int soft_items_bound(int nt, int lp_min, SoftSplit sp) {
 // parts (log2) per bucket of the soft mask's tiles; ghist (band, bucket) tile counts; sx scratch
 __device__ __forceinline__ void soft_parts(int *sx, int *lpb, const int *__restrict__ ghist, int lp_min, SoftSplit sp,
                                            int skip_empty) {
-  // tiles per bucket summed over the bands (one lane per bucket), then the caps walked
-  // serially from the heaviest bucket down on LDS values
-  if (threadIdx.x < ORD_BUCKETS) {
+  // tiles per bucket summed over the bands (one lane of wave 0 per bucket), then the caps walked from
+  // the heaviest bucket down in that wave's registers (each step reads the bucket's lane: no LDS
+  // round trip per step)
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
     int h = 0;
+    if (lane < ORD_BUCKETS) {
 #pragma unroll
-    for (int g = 0; g < 8; g++) h += ghist[g * ORD_BUCKETS + threadIdx.x];
-    sx[threadIdx.x] = h;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int n4 = 0, n8 = 0;
-    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
-      const int h = sx[q];
-      int lp = lp_min;
-      if (q >= sp.b8 && n8 + h <= sp.cap8) {
-        lp = lp > 3 ? lp : 3;
-        n8 += h;
-      } else if (q >= sp.b4 && n4 + h <= sp.cap4) {
-        lp = lp > 2 ? lp : 2;
-        n4 += h;
-      }
-      lpb[q] = q == 0 && skip_empty ? -1 : lp;  // skip_empty: tiles without candidate faces get no item
+      for (int g = 0; g < 8; g++) h += ghist[g * ORD_BUCKETS + lane];
     }
+    int n4 = 0, n8 = 0, mine = lp_min;
+    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
+      const int hq = __builtin_amdgcn_readlane(h, q);
+      int lp = lp_min;
+      if (q >= sp.b8 && n8 + hq <= sp.cap8) {
+        lp = lp > 3 ? lp : 3;
+        n8 += hq;
+      } else if (q >= sp.b4 && n4 + hq <= sp.cap4) {
+        lp = lp > 2 ? lp : 2;
+        n4 += hq;
+      }
+      if (lane == q) mine = lp;
+    }
+    if (lane < ORD_BUCKETS) lpb[lane] = lane == 0 && skip_empty ? -1 : mine;  // skip_empty: no item for tiles without candidates
   }
   __syncthreads();  // sx is reused by place_prefix
 }
@@ -515,6 +516,7 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
     hist[k] = run;
     wbase[k] = mine;
   }
+  __syncthreads();  // hist is read across waves (soft_parts, place_prefix)
   if (which == 0) {
     if (threadIdx.x < ORD_BUCKETS) lpb[threadIdx.x] = (int)threadIdx.x >= a.split_from ? a.split_log2 : 0;
   } else {
