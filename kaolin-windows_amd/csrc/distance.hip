@@ -120,7 +120,7 @@ __device__ __forceinline__ float point_face(const V3<T> &p, const R &f, int &typ
 }
 
 #ifdef KL_P2M_PROBE  // dev probe (scripts/dev/p2m_probe.hip): counts skipped / evaluated (wave, face) pairs
-__device__ unsigned long long g_p2m_skipped, g_p2m_evaluated;
+__device__ unsigned long long g_p2m_skipped, g_p2m_evaluated, g_p2m_pairs;  // pairs: per-point tests passed
 #define KL_P2M_COUNT(v) v++
 #else
 #define KL_P2M_COUNT(v)
@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
   if (pairs) s_best[threadIdx.x] = KEY_NONE;
   float published = INFINITY;
 #ifdef KL_P2M_PROBE
-  unsigned long long g_p2m_skipped = 0, g_p2m_evaluated = 0;
+  unsigned long long g_p2m_skipped = 0, g_p2m_evaluated = 0, g_p2m_pairs = 0;
 #endif
   T best = (T)INFINITY, tbest = (T)INFINITY;
   int64_t best_f = 0, tbest_f = 0;
@@ -379,6 +379,9 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
             s_q[wid][(qhead + qcnt + rank) & (P2M_QCAP - 1)] = (uint16_t)(lane | (sj << 6));
           }
           qcnt += (uint32_t)__popcll(pm);
+#ifdef KL_P2M_PROBE
+          g_p2m_pairs += __popcll(pm);
+#endif
           if (qcnt >= 64) {
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -435,6 +438,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
   if (lane == 0) {
     atomicAdd(&::kl::g_p2m_skipped, g_p2m_skipped);
     atomicAdd(&::kl::g_p2m_evaluated, g_p2m_evaluated);
+    atomicAdd(&::kl::g_p2m_pairs, g_p2m_pairs);
   }
 #endif
   if (!valid) return;

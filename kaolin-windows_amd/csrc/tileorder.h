@@ -185,6 +185,9 @@ __device__ __forceinline__ void soft_parts(int *sx, int *lpb, const int *__restr
       for (int g = 0; g < 8; g++) h += ghist[g * ORD_BUCKETS + lane];
     }
     int n4 = 0, n8 = 0, mine = lp_min;
+    // a compact loop, not unrolled: this code runs once per launch from a cold instruction cache,
+    // where a 32-step unrolled body (SGPR spills included) measured 1.6 us slower
+#pragma unroll 1
     for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
       const int hq = __builtin_amdgcn_readlane(h, q);
       int lp = lp_min;

@@ -10,7 +10,8 @@
 
 namespace kl {
 int g_dev_flags = 0;
-int g_dev_param[16] = {};
+int g_dev_param[32] = {};
+int g_dev_stat[4] = {};
 template <typename T>
 int acc_finalize(const double *, T *, size_t, bool, hipStream_t, int *) { return 0; }  // backward: unused here
 template int acc_finalize<float>(const double *, float *, size_t, bool, hipStream_t, int *);
@@ -58,6 +59,7 @@ int main(int argc, char **argv) {
     for (int rep = 0; rep < 2; rep++) {
       CK(hipMemcpyToSymbol(HIP_SYMBOL(g_p2m_skipped), &z, 8));
       CK(hipMemcpyToSymbol(HIP_SYMBOL(g_p2m_evaluated), &z, 8));
+      CK(hipMemcpyToSymbol(HIP_SYMBOL(g_p2m_pairs), &z, 8));
       CK(hipEventRecord(a, 0));
       int rc = p2m_fwd<float>(P, F, dp, df, dd, di, dt, ws, L.bytes, 0);
       CK(hipEventRecord(b, 0));
@@ -65,11 +67,12 @@ int main(int argc, char **argv) {
       if (rc) return 1;
       float ms;
       CK(hipEventElapsedTime(&ms, a, b));
-      unsigned long long sk, ev;
+      unsigned long long sk, ev, pr;
       CK(hipMemcpyFromSymbol(&sk, HIP_SYMBOL(g_p2m_skipped), 8));
       CK(hipMemcpyFromSymbol(&ev, HIP_SYMBOL(g_p2m_evaluated), 8));
-      printf("target=%d mode=%s rep=%d  %.3f ms  skipped=%llu evaluated=%llu (%.1f%% skipped)\n", g_p2m_target_blocks, mode ? "morton" : "plain", rep,
-             ms, sk, ev, 100.0 * sk / (double)(sk + ev + 1));
+      CK(hipMemcpyFromSymbol(&pr, HIP_SYMBOL(g_p2m_pairs), 8));
+      printf("target=%d mode=%s rep=%d  %.3f ms  skipped=%llu evaluated=%llu (%.1f%% skipped) point_pairs=%llu\n",
+             g_p2m_target_blocks, mode ? "morton" : "plain", rep, ms, sk, ev, 100.0 * sk / (double)(sk + ev + 1), pr);
     }
   }
   return 0;
