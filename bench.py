@@ -845,22 +845,25 @@ def p2m_leg(device, world, rank, steps, points=None, face_vertices=None, grad=No
 
 def p2m_roofline(P, F, t_f):
     """p2m forward against the FP32 VALU peak.  `frac` prices the EXECUTED FP32 work: the kernel
-    evaluates only the (wave, face) pairs its bounds cannot skip, and the committed counter profile
-    (profiles/r04_p2m_pmc.json: probe + SQ_INSTS_VALU_{ADD,MUL,FMA}_F32 passes on this round's kernel)
-    counts the flops one call executes; their rate at this call's time is the achieved figure.
-    The nominal figure (P*F x 50 flop) is beside it."""
+    evaluates only the pairs its bounds cannot skip (r05: the wave-level bound, then a per-point bound
+    whose passing pairs are evaluated one per lane), and the committed counter profile
+    (profiles/r05_p2m_pmc.json: probe + SQ_INSTS_VALU_{ADD,MUL,FMA}_F32 passes on this round's kernel;
+    r04's file for the r04 kernel) counts the flops one call executes; their rate at this call's time
+    is the achieved figure.  The nominal figure (P*F x 50 flop) is beside it."""
     nominal = P * F * 50 / t_f / 1e12
     r = {'bound': 'valu', 'unit': 'TFLOP/s', 'peak': FP32_PEAK_TFLOPS,
          'nominal': {'flop_per_pair': 50, 'achieved': round(nominal, 2), 'frac': round(nominal / FP32_PEAK_TFLOPS, 4),
                      'note': 'nominal pairs (P*F); pruned pairs are not evaluated'}}
-    path = os.path.join(ROOT, 'profiles', 'r04_p2m_pmc.json')
+    name = 'r05_p2m_pmc.json' if os.path.exists(os.path.join(ROOT, 'profiles', 'r05_p2m_pmc.json')) else 'r04_p2m_pmc.json'
+    path = os.path.join(ROOT, 'profiles', name)
     if P == 100000 and F == 20000 and os.path.exists(path):
         pm = json.load(open(path))
         executed = pm['executed_fp32_flop'] / t_f / 1e12
         r.update(achieved=round(executed, 2), frac=round(executed / FP32_PEAK_TFLOPS, 4),
                  executed_fp32_flop_per_call=pm['executed_fp32_flop'])
-        r['measured'] = {'source': 'profiles/r04_p2m_pmc.json (cfg2, one rank; this round\'s p2m_fwd_kernel)',
+        r['measured'] = {'source': f'profiles/{name} (cfg2, one rank; this round\'s p2m_fwd_kernel)',
                          'evaluated_pair_fraction': pm['wave_face_pairs']['evaluated_fraction'],
+                         'point_face_pairs_evaluated': pm['wave_face_pairs'].get('point_face_pairs_evaluated'),
                          'valu_insts_per_evaluated_wave_face_pair': pm['valu_insts_per_evaluated_wave_face_pair'],
                          'valu_issue_busy': pm['valu_issue_busy_est'],
                          'wait_any_fraction': pm['wait_any_fraction_of_wave_cycles']}

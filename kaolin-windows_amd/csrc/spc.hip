@@ -1744,37 +1744,35 @@ __global__ void rt_fused_result_kernel(const RtlCtl *__restrict__ ctl, uint32_t 
 // list restricted to one ray is that ray's walk order at that level, and a leaf's position is its
 // rank in the walk).  So each lane walks its own ray through the octree with the same per-node
 // decision (rt_decide_one's ray_aabb and keep rules, the same front-to-back child order as
-// rt_children): no nugget lists in HBM, no per-level scans, one host read.  Expanding a hit node
-// loads ALL its children's points, octree bytes and exsums together and decides them at once: the
-// first hit child is expanded next from those registers (one dependent load round trip per level
-// on the way down), its hit siblings are pushed (a per-level LDS stack of child offsets) and cost a
-// reload when popped; at the target level the hits are emitted.
-// Pass 1 (SLOTS) writes each ray's first RTD_SLOTS hits to a per-ray slot buffer and counts them
-// all; after a scan over the rays, a copy moves the slots to their final rows, and only rays with
-// more hits than slots are walked again (OVERFLOW) writing at their offsets.
+// rt_children): no nugget lists in HBM, no per-level scans or host reads.  A hit node is expanded
+// in two dependent loads: its point, octree byte and exsum, then ALL its children's points together,
+// whose decisions are made at once -- the hit ones pushed (a per-level LDS stack of child offsets),
+// or at the target level emitted.  Two passes: hits per ray (COUNT), then, after a scan over the
+// rays, the same walk writing each hit at its ray's offset.
+// Measured (cfg4, 512^2 rays, level 9): 1.22 ms against the per-level march's 1.20 -- each lane's
+// walk is a chain of ~40 dependent load round trips (two per expanded node) and all 4,096 waves are
+// resident at once, so the time is the longest chain, not the bytes.  A variant with each node's
+// children's octree bytes / exsums loaded with their points (one round trip on the way down) and a
+// slot buffer instead of the count pass measured 2.6 ms (102 VGPRs; rays past the 32 slots walked
+// again).  Kept as dev param 15 = 4, tested equal to the other marches.
 constexpr int RTD_THREADS = 64;
 constexpr int RTD_MAXL = SPC_MAX_LEVELS + 1;
-constexpr int RTD_SLOTS = 32;  // cfg4: 6.3 hits per ray on average
 
 // children of a node in front-to-back order from the origin's octant code: increasing Hamming
 // distance to the code, then index (rt_children) -- one nibble per child index, 8 per code
 __constant__ uint32_t c_rt_perm[8] = {0x76534210u, 0x67425301u, 0x57416302u, 0x46507213u,
                                       0x37216504u, 0x26307415u, 0x15307426u, 0x04216537u};
 
-enum { RTD_PASS_SLOTS = 0, RTD_PASS_OVERFLOW = 1 };
-
-template <int PASS>
+template <bool WRITE>
 __global__ void __launch_bounds__(RTD_THREADS) rt_dfs_kernel(RayIn in, int64_t num_rays, uint32_t target_level,
                                                              int with_depth, int with_exit,
                                                              uint32_t *__restrict__ cnt,
                                                              const uint32_t *__restrict__ off,
-                                                             int2 *__restrict__ nout, float *__restrict__ dout,
-                                                             unsigned *__restrict__ overflow) {
+                                                             int2 *__restrict__ nout, float *__restrict__ dout) {
   __shared__ uint32_t s_list[RTD_MAXL][RTD_THREADS];  // pending hit nodes of a level (offsets 1..8)
   __shared__ int32_t s_base[RTD_MAXL][RTD_THREADS];   // their parent's exsum
   const int64_t ridx = blockIdx.x * (int64_t)RTD_THREADS + threadIdx.x;
   if (ridx >= num_rays) return;
-  if (PASS == RTD_PASS_OVERFLOW && cnt[ridx] <= (uint32_t)RTD_SLOTS) return;  // its slots were copied
   const int tx = threadIdx.x;
   const float o[3] = {in.ro[ridx * 3], in.ro[ridx * 3 + 1], in.ro[ridx * 3 + 2]};
   const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
@@ -1783,14 +1781,13 @@ __global__ void __launch_bounds__(RTD_THREADS) rt_dfs_kernel(RayIn in, int64_t n
   const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
   const float oh[3] = {0.5f * o[0] + 0.5f, 0.5f * o[1] + 0.5f, 0.5f * o[2] + 0.5f};
   const int dd = with_exit ? 2 : 1;
-  uint32_t n = 0;  // hits so far
-  // SLOTS: rows ridx * RTD_SLOTS + n (n < RTD_SLOTS); OVERFLOW: rows off[ridx] + n
-  const int64_t row0 = PASS == RTD_PASS_SLOTS ? ridx * RTD_SLOTS : (int64_t)off[ridx];
+  uint32_t n = 0;
+  uint32_t pos = WRITE ? off[ridx] : 0u;
   // a node's decision at level lv (rt_decide_one): keep flag at the target level, else dv != 0
-  auto decide = [&](float qx, float qy, float qz, uint32_t lv, float &en, float &ex) -> bool {
+  auto decide = [&](int16_t qx, int16_t qy, int16_t qz, uint32_t lv, float &en, float &ex) -> bool {
     const float r = (float)(1.0 / (double)(float)(1u << lv));
-    const float vc[3] = {fmaf(r, fmaf(2.0f, qx, 1.0f), -1.0f), fmaf(r, fmaf(2.0f, qy, 1.0f), -1.0f),
-                         fmaf(r, fmaf(2.0f, qz, 1.0f), -1.0f)};
+    const float vc[3] = {fmaf(r, fmaf(2.0f, (float)qx, 1.0f), -1.0f), fmaf(r, fmaf(2.0f, (float)qy, 1.0f), -1.0f),
+                         fmaf(r, fmaf(2.0f, (float)qz, 1.0f), -1.0f)};
     en = ray_aabb(o, d, inv, sgn, vc, r);
     if (lv != target_level) return en != 0.0f;
     if (with_depth && with_exit) {
@@ -1800,37 +1797,38 @@ __global__ void __launch_bounds__(RTD_THREADS) rt_dfs_kernel(RayIn in, int64_t n
     return en > 0.0f;
   };
   auto emit = [&](int pidx, float en, float ex) {
-    if (PASS == RTD_PASS_OVERFLOW || n < (uint32_t)RTD_SLOTS) {
-      const int64_t row = row0 + n;
-      nout[row] = make_int2((int)ridx, pidx);
+    if (WRITE) {
+      nout[pos] = make_int2((int)ridx, pidx);
       if (dout && with_depth) {
-        dout[row * dd] = en;
-        if (with_exit) dout[row * dd + 1] = ex;
+        dout[(int64_t)pos * dd] = en;
+        if (with_exit) dout[(int64_t)pos * dd + 1] = ex;
       }
+      pos++;
+    } else {
+      n++;
     }
-    n++;
   };
   {  // the root (level 0)
     float en, ex = 0.0f;
-    const bool hit = decide((float)in.points[0], (float)in.points[1], (float)in.points[2], 0, en, ex);
+    const bool hit = decide(in.points[0], in.points[1], in.points[2], 0, en, ex);
     if (target_level == 0) {
       if (hit) emit(0, en, ex);
     } else if (hit) {
       int pidx = 0;
       uint32_t l = 0;
-      // the node to expand: its point, octree byte and exsum (carried from its parent's expansion, or
-      // loaded after a pop)
-      float px = (float)in.points[0], py = (float)in.points[1], pz = (float)in.points[2];
-      uint32_t ob = in.octree[0];
-      int32_t s = in.exsum[0];
       for (;;) {
+        // ---- expand hit node pidx of level l < target: its point, octree byte and exsum
+        const int16_t *pp = in.points + (int64_t)pidx * 3;
+        const float px = (float)pp[0], py = (float)pp[1], pz = (float)pp[2];
+        const uint32_t ob = in.octree[pidx];
+        const int32_t s = in.exsum[pidx];
         const float r = (float)(1.0 / (double)(float)(1u << l));
         const float x = (float)((double)oh[0] - (double)r * ((double)px + 0.5));
         const float y = (float)((double)oh[1] - (double)r * ((double)py + 0.5));
         const float z = (float)((double)oh[2] - (double)r * ((double)pz + 0.5));
         const uint32_t perm = c_rt_perm[(x > 0 ? 4u : 0u) + (y > 0 ? 2u : 0u) + (z > 0 ? 1u : 0u)];
-        // the children in front-to-back order (offsets 1..8 from s, packed in nibbles: a register
-        // array indexed by a running count would live in scratch), all their data at once
+        // the children in front-to-back order (offsets 1..8 from s) and all their points at once
+        // (packed in nibbles: a register array indexed by a running count would live in scratch)
         uint32_t cl = 0;
         int nk = 0;
 #pragma unroll
@@ -1841,145 +1839,73 @@ __global__ void __launch_bounds__(RTD_THREADS) rt_dfs_kernel(RayIn in, int64_t n
             nk++;
           }
         }
-        const uint32_t lc = l + 1;
-        const bool inner = lc != target_level;  // the children are expanded in turn
         int16_t cp[8][3];
-        uint8_t cob[8];
-        int32_t cs[8];
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-          const int64_t c = k < nk ? s + (int)((cl >> (4 * k)) & 15u) : pidx;
-          cp[k][0] = in.points[c * 3];
-          cp[k][1] = in.points[c * 3 + 1];
-          cp[k][2] = in.points[c * 3 + 2];
-          cob[k] = inner ? in.octree[c] : (uint8_t)0;
-          cs[k] = inner ? in.exsum[c] : 0;
+          const int16_t *c = in.points + (int64_t)(k < nk ? s + (int)((cl >> (4 * k)) & 15u) : pidx) * 3;
+          cp[k][0] = c[0];
+          cp[k][1] = c[1];
+          cp[k][2] = c[2];
         }
+        const uint32_t lc = l + 1;
         uint32_t hits = 0;
         int nh = 0;
-        float npx = 0.f, npy = 0.f, npz = 0.f;  // the first hit child's data
-        uint32_t nob = 0;
-        int32_t ns = 0, npidx = 0;
 #pragma unroll
         for (int k = 0; k < 8; k++) {
           if (k < nk) {
             const uint32_t ck = (cl >> (4 * k)) & 15u;
             float en, ex = 0.0f;
-            if (decide((float)cp[k][0], (float)cp[k][1], (float)cp[k][2], lc, en, ex)) {
-              if (!inner) {
+            if (decide(cp[k][0], cp[k][1], cp[k][2], lc, en, ex)) {
+              if (lc == target_level) {
                 emit(s + (int)ck, en, ex);
-              } else if (nh == 0) {
-                npx = (float)cp[k][0];
-                npy = (float)cp[k][1];
-                npz = (float)cp[k][2];
-                nob = cob[k];
-                ns = cs[k];
-                npidx = s + (int)ck;
-                nh = 1;
               } else {
-                hits |= ck << (4 * (nh - 1));
+                hits |= ck << (4 * nh);
                 nh++;
               }
             }
           }
         }
-        if (nh) {  // down to the first hit child; its hit siblings wait at level lc
+        uint32_t m = l;  // the deepest level with pending nodes
+        if (nh) {
           s_list[lc][tx] = hits;
           s_base[lc][tx] = s;
-          pidx = npidx;
-          l = lc;
-          px = npx;
-          py = npy;
-          pz = npz;
-          ob = nob;
-          s = ns;
-          continue;
+          m = lc;
         }
-        uint32_t m = l;  // the deepest level with pending nodes (every level <= l has been written)
         while (m > 0 && s_list[m][tx] == 0u) m--;
         if (m == 0) break;
         const uint32_t lst = s_list[m][tx];
         s_list[m][tx] = lst >> 4;
         pidx = s_base[m][tx] + (int)(lst & 15u);
         l = m;
-        const int16_t *pp = in.points + (int64_t)pidx * 3;
-        px = (float)pp[0];
-        py = (float)pp[1];
-        pz = (float)pp[2];
-        ob = in.octree[pidx];
-        s = in.exsum[pidx];
       }
     }
   }
-  if (PASS == RTD_PASS_SLOTS) {
-    cnt[ridx] = n;
-    if (n > (uint32_t)RTD_SLOTS) atomicOr(overflow, 1u);
-  }
+  if (!WRITE) cnt[ridx] = n;
 }
 
-// the rays' slot rows (pass 1) to their final rows; rays with more hits than slots are left to the
-// OVERFLOW walk
-__global__ void __launch_bounds__(256) rt_dfs_copy_kernel(int64_t num_rays, const uint32_t *__restrict__ cnt,
-                                                          const uint32_t *__restrict__ off,
-                                                          const int2 *__restrict__ snug, const float *__restrict__ sdep,
-                                                          int dd, int2 *__restrict__ nout, float *__restrict__ dout) {
-  const int64_t ridx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (ridx >= num_rays) return;
-  const uint32_t c = cnt[ridx];
-  if (c > (uint32_t)RTD_SLOTS) return;
-  const int64_t o = off[ridx];
-  for (uint32_t k = 0; k < c; k++) {
-    nout[o + k] = snug[ridx * RTD_SLOTS + k];
-    if (dout)
-      for (int e = 0; e < dd; e++) dout[(o + k) * dd + e] = sdep[(ridx * RTD_SLOTS + k) * dd + e];
-  }
-}
-
-// host-sized raytrace by the depth-first march: slots pass, scan (one host read: total and the
-// overflow flag), copy, overflow walk when needed
+// host-sized raytrace by the depth-first march: counts, scan (one host read of the total), writes
 static int rt_dfs(const RayIn &in, int64_t num_rays, uint32_t target_level, int return_depth, int with_exit,
                   Scratch &sc, int32_t **nuggets, float **depth, int64_t *num_hits, hipStream_t st) {
   const int dd = with_exit ? 2 : 1;
   const size_t cb = al256b((size_t)(num_rays + 1) * sizeof(uint32_t));
-  const size_t ob = al256b((size_t)(num_rays + 2) * sizeof(uint32_t));
-  const size_t nb = al256b((size_t)num_rays * RTD_SLOTS * sizeof(int2));
-  const size_t db = return_depth ? al256b((size_t)num_rays * RTD_SLOTS * dd * sizeof(float)) : 0;
-  char *w = (char *)sc.get(cb + ob + 256 + nb + db);
-  if (!w) return KL_E_ALLOC;
-  uint32_t *cnt = (uint32_t *)w, *off = (uint32_t *)(w + cb);
-  unsigned *flag = (unsigned *)(w + cb + ob);
-  int2 *snug = (int2 *)(w + cb + ob + 256);
-  float *sdep = return_depth ? (float *)(w + cb + ob + 256 + nb) : nullptr;
+  uint32_t *cnt = (uint32_t *)sc.get(cb + (size_t)(num_rays + 2) * sizeof(uint32_t));
+  if (!cnt) return KL_E_ALLOC;
+  uint32_t *off = (uint32_t *)((char *)cnt + cb);
   KL_CHECK_RC(fill_async(cnt + num_rays, 0, sizeof(uint32_t), st));  // the scan's (n + 1)-th input
-  KL_CHECK_RC(fill_async(flag, 0, sizeof(unsigned), st));
   const unsigned grid = (unsigned)cdiv(num_rays, RTD_THREADS);
-  hipLaunchKernelGGL(rt_dfs_kernel<RTD_PASS_SLOTS>, dim3(grid), dim3(RTD_THREADS), 0, st, in, num_rays, target_level,
-                     return_depth, with_exit, cnt, (const uint32_t *)nullptr, snug, sdep, flag);
+  hipLaunchKernelGGL(rt_dfs_kernel<false>, dim3(grid), dim3(RTD_THREADS), 0, st, in, num_rays, target_level,
+                     return_depth, with_exit, cnt, (const uint32_t *)nullptr, (int2 *)nullptr, (float *)nullptr);
   KL_CHECK_LAUNCH();
-  size_t tb = 0;
-  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, (int)num_rays + 1, st));
-  void *tmp = sc.get(tb);
-  if (!tmp) return KL_E_ALLOC;
-  KL_CHECK_HIP(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, off, (int)num_rays + 1, st));
-  KL_CHECK_HIP(hipMemcpyAsync(flag + 1, off + num_rays, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-  uint32_t h[2] = {0, 0};  // (overflow, total)
-  KL_CHECK_RC(host_read(h, flag, sizeof(h), st));
-  const uint32_t total = h[1];
+  uint32_t total = 0;
+  KL_CHECK_RC(exclusive_scan(cnt, off, num_rays, sc, st, &total));
   int2 *out = (int2 *)sc.get((size_t)total * sizeof(int2));
   float *dout = return_depth ? (float *)sc.get(std::max<size_t>((size_t)total * dd * sizeof(float), 16)) : nullptr;
   if (!out || (return_depth && !dout)) return KL_E_ALLOC;
   if (total) {
-    hipLaunchKernelGGL(rt_dfs_copy_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, num_rays,
-                       (const uint32_t *)cnt, (const uint32_t *)off, (const int2 *)snug, (const float *)sdep, dd, out,
-                       dout);
+    hipLaunchKernelGGL(rt_dfs_kernel<true>, dim3(grid), dim3(RTD_THREADS), 0, st, in, num_rays, target_level,
+                       return_depth, with_exit, (uint32_t *)nullptr, (const uint32_t *)off, out, dout);
     KL_CHECK_LAUNCH();
-    if (h[0]) {
-      hipLaunchKernelGGL(rt_dfs_kernel<RTD_PASS_OVERFLOW>, dim3(grid), dim3(RTD_THREADS), 0, st, in, num_rays,
-                         target_level, return_depth, with_exit, cnt, (const uint32_t *)off, out, dout, flag);
-      KL_CHECK_LAUNCH();
-    }
   }
-  g_dev_stat[2] = (int)h[0];
   *nuggets = (int32_t *)out;
   *depth = dout;
   *num_hits = total;
@@ -2158,10 +2084,10 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
   // end, with buffers of 16 nuggets per ray; a level with more falls back to the per-level march
   // below (dev param 15 = 2: that march always, for A/B)
   g_dev_stat[1] = 0;
-  // default: the per-ray depth-first march (rt_dfs); dev param 15 = 2: the per-level march, 3: the
-  // fused level march first (both kept for A/B: at cfg4 2.85 and 1.11 ms)
-  if (num_rays > 0 && num_rays < ((int64_t)1 << 31) && g_dev_param[15] != 2 && g_dev_param[15] != 3 &&
-      target_level < (uint32_t)RTD_MAXL) {
+  // default: the per-level march below.  Dev param 15 = 4: the per-ray depth-first march (rt_dfs),
+  // 3: the fused level march first (kept for A/B, tested equal: at cfg4 1.22 and 2.8 ms against the
+  // per-level march's 1.20)
+  if (num_rays > 0 && num_rays < ((int64_t)1 << 31) && g_dev_param[15] == 4 && target_level < (uint32_t)RTD_MAXL) {
     g_dev_stat[1] = 3;
     return rt_dfs(in, num_rays, target_level, return_depth, with_exit, sc, nuggets, depth, num_hits, st);
   }
@@ -2295,7 +2221,7 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
   }
   RayIn in{octree, points, exsum, ray_o, ray_d};
   const int64_t cap0 = L.cap0;
-  if (g_dev_param[15] != 2 && capacity > 0) {  // the fused march (dev param 15 = 2: the per-level kernels)
+  if (g_dev_param[15] == 3 && capacity > 0) {  // dev param 15 = 3: the fused march (2.2 against 1.09 ms at cfg4)
     RtlCtl *ctl = (RtlCtl *)dnum;
     static_assert(sizeof(RtlCtl) <= 256, "RtlCtl fits the dnum slot");
     KL_CHECK_RC(rt_fused_levels(in, num_rays, target_level, return_depth, with_exit, (uint32_t)capacity, ctl,

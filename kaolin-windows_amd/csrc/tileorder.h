@@ -520,6 +520,7 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
     wbase[k] = mine;
   }
   __syncthreads();  // hist is read across waves (soft_parts, place_prefix)
+  if (ldbg && threadIdx.x == 0) ldbg[3] = stamp_wall();  // (histograms loaded, bases summed)
   if (which == 0) {
     if (threadIdx.x < ORD_BUCKETS) lpb[threadIdx.x] = (int)threadIdx.x >= a.split_from ? a.split_log2 : 0;
   } else {

@@ -33,6 +33,6 @@ for rep in range(4):
     print(f'rep {rep}: count workgroups (start, counted, arrived) us: ' +
           ' '.join(f'({a:.1f},{b:.1f},{c:.1f})' for a, b, c in cw))
     for w in range(2):
-        s = d[64 + 4 * w:64 + 4 * w + 3]
-        print(f'  bitmap {w} workgroup 0: barrier passed {us(s[0]):.2f} prefix {us(s[1]):.2f} placed {us(s[2]):.2f} us')
+        s = d[64 + 4 * w:64 + 4 * w + 4]
+        print(f'  bitmap {w} workgroup 0: barrier passed {us(s[0]):.2f} histograms {us(s[3]):.2f} prefix {us(s[1]):.2f} placed {us(s[2]):.2f} us')
 lib.kl_dev_set_debug(None)
