@@ -361,7 +361,7 @@ def survey_step_bytes(inp, stats):
 
 # kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
 OP_KERNELS = {
-    'dibr_forward': ('raster_bin_word_kernel<float, 2>', 'tile_countorder2_kernel', 'raster_tile_kernel<float',
+    'dibr_forward': ('raster_bin_word_kernel<float, 2>', 'tile_countorder_chip_kernel', 'raster_tile_kernel<float',
                      'soft_tile_fwd_kernel<float'),
     'dibr_backward': ('rasterize_bwd_gather2_kernel<float', 'soft_tile_bwd_kernel<float'),
 }
@@ -1068,27 +1068,33 @@ def raytrace_leg(device, steps, spc_tuple):
     # SURVEY.md §8d's raytrace model (kept as survey_formula)
     survey_bytes = 24 * R + sum(31 * per_level[lv] + 8 * (per_level[lv + 1] if lv + 1 <= L else 0)
                                 for lv in range(L + 1)) + per_level[L] * (16 + 4)
-    # the fused level march (spc.hip rt_level_kernel): level l tests its candidates (the hit
-    # nodes' children of level l - 1: popcount of their octree bytes) -- nugget 8 B (none at level
-    # 0: the ray itself), ray 24 B, node point 6 B, octree byte 1 B -- and writes each hit's
-    # children (8 B each; its exsum entry 4 B read); the target level writes nugget + depth (12 B)
+    # the hit-list march (spc.hip rth_count_kernel / rth_write_kernel; lists of HIT nodes): level 0's
+    # list is the R rays at the root (8 B written); per level l < L, the count pass reads each listed
+    # node's nugget 8 B, ray 24 B, octree byte 1 B, exsum 4 B and its children's points (6 B per
+    # candidate: the popcount of the node's octree byte) and writes a mask byte and a count 4 B; the
+    # device scan reads the counts twice and writes the offsets (12 B per node); the write pass reads
+    # the mask (1 B) and, per node, nugget 8 + octree 1 + exsum 4 + point 6 + ray origin 12 + offset 4 B,
+    # and writes 8 B per hit child; the target level's hits also re-read their point 6 B and ray
+    # direction 12 B for the depth (4 B written)
     cand = [R]
     for lv in range(L):
         _, pidx = kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], exsum, o, d, lv, return_depth=False)
         cand.append(int(_popcount_u8(octree[pidx.long()]).sum()))
-    nbytes = sum(c * ((8 if lv else 0) + 24 + 6 + 1) for lv, c in enumerate(cand)) + \
-        sum(per_level[lv] * 4 + cand[lv + 1] * 8 for lv in range(L)) + per_level[L] * 12
+    listed = [R] + per_level[1:L]
+    nbytes = 8 * R + sum(n * (8 + 24 + 1 + 4 + 1 + 4 + 12 + 1 + 8 + 1 + 4 + 6 + 12 + 4) + 6 * cand[lv + 1] +
+                         8 * per_level[lv + 1] for lv, n in enumerate(listed)) + per_level[L] * (6 + 12 + 4)
     return {'metric': 'unbatched_raytrace Mrays/s (cfg4 SPC level 9, 512x512 rays, depth)',
             'value': round(R / (ms * 1e-3) / 1e6, 2), 'ms': round(ms, 4), 'hits': hits, 'hits_per_level': per_level,
-            'bytes': nbytes, 'timing': 'wall clock per call incl. the per-level host count reads',
+            'bytes': nbytes, 'timing': 'wall clock per call incl. its one host read and allocator calls',
             'fixed_capacity': {'value': round(R / (ms_fixed * 1e-3) / 1e6, 2), 'ms': round(ms_fixed, 4),
                                'capacity': cap, 'equal_to_host_sized': bool(fixed_equal),
                                'timing': 'HIP events over back-to-back calls (nothing read back)'},
             'candidates_per_level': cand,
             'roofline': {'bound': 'hbm', 'achieved': round(nbytes / (ms * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         'bytes_model': 'the fused level march: per candidate nugget / ray / point / octree byte, '
-                                        'per hit its children and exsum entry, per target hit nugget + depth',
+                         'bytes_model': 'the hit-list march: per listed hit node its nugget, ray, octree byte, exsum, '
+                                        'its children\'s points, mask / count / offsets, the write pass\'s reads and '
+                                        '8 B per hit child; per target hit its point and ray again + depth',
                          'survey_formula': {'bytes': survey_bytes,
                                             'achieved': round(survey_bytes / (ms * 1e-3) / 1e9, 1),
                                             'frac': round(survey_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}}

@@ -800,6 +800,8 @@ SoftSplit soft_split() {
 int soft_lp_min(int K) {
   int lp = 1;
   while (lp < 3 && st_head_lds() + (size_t)(TILE_H >> lp) * st_row_lds(K) > 64 * 1024) lp++;
+  // dev param 20: at least this many row halvings (fewer rows per work item, less LDS per workgroup)
+  if (g_dev_param[20] > lp && g_dev_param[20] <= 3) lp = g_dev_param[20];
   return lp;
 }
 

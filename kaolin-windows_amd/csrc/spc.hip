@@ -1311,6 +1311,11 @@ __device__ __forceinline__ float ray_aabb(const float o_q[3], const float d[3], 
   return 0.0f;
 }
 
+// children of a node in front-to-back order from the origin's octant code: increasing Hamming
+// distance to the code, then index (rt_children) -- one nibble per child index, 8 per code
+__constant__ uint32_t c_rt_perm[8] = {0x76534210u, 0x67425301u, 0x57416302u, 0x46507213u,
+                                      0x37216504u, 0x26307415u, 0x15307426u, 0x04216537u};
+
 struct RayIn {
   const uint8_t *octree;
   const int16_t *points;
@@ -1729,6 +1734,200 @@ static int rt_fused_levels(const RayIn &in, int64_t num_rays, uint32_t target_le
   return KL_OK;
 }
 
+// ---- Hit-list level march (r05, the eager entry's default): level l's list holds the nuggets that
+// HIT at level l (not the candidates).  Per level, one count pass decides every listed node's
+// children at level l + 1 together (their points are contiguous: points[s + 1 .. s + popc]), leaving
+// a byte of hit children and their count per node; a device scan of the counts places them; a write
+// pass lists the hit children in front-to-back order (rt_children's order) -- at the target level
+// with their depths.  Against the per-level march (decide every candidate, scan, then subdivide
+// every hit into its untested children): the candidates are never written or re-read, the ray is
+// read once per hit node instead of once per candidate, and no count goes back to the host until
+// the end (lists in `cap`-row buffers; a level past `cap` falls back to the per-level march).
+// Level 0's list is ray i at the root; the root's own test is made in the first count pass.
+__device__ __forceinline__ void rth_node(const int2 *__restrict__ list, int64_t i, int &ridx, int &pidx) {
+  const int2 nu = list[i];
+  ridx = nu.x;
+  pidx = nu.y;
+}
+
+__global__ void __launch_bounds__(256) rth_count_kernel(RayIn in, const uint32_t *__restrict__ dnum,
+                                                        const int2 *__restrict__ list, uint32_t level,
+                                                        uint32_t target_level, int root, int with_depth,
+                                                        int with_exit, uint8_t *__restrict__ hmask,
+                                                        uint32_t *__restrict__ cnt) {
+  const int64_t num = *dnum;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < num; i += (int64_t)gridDim.x * 256) {
+    int ridx, pidx;
+    rth_node(list, i, ridx, pidx);
+    const float o[3] = {in.ro[ridx * 3], in.ro[ridx * 3 + 1], in.ro[ridx * 3 + 2]};
+    const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
+    const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
+    const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
+    uint32_t m = 0;
+    bool self = true;
+    if (root) {  // the root's own test (rt_decide_one at level 0, not the target)
+      const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
+                           fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
+                           fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
+      self = ray_aabb(o, d, inv, sgn, vc, 1.0f) != 0.0f;
+    }
+    if (self) {
+      const uint32_t ob = in.octree[pidx];
+      const int32_t s = in.exsum[pidx];
+      const int nk = __popc(ob);
+      const uint32_t lc = level + 1;
+      const bool last = lc == target_level;
+      const float r = (float)(1.0 / (double)(float)(1u << lc));
+      int16_t cp[8][3];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {  // children k = 0..nk-1 at points[s + 1 + k] (index order)
+        const int64_t c = (int64_t)s + 1 + (k < nk ? k : 0);
+        cp[k][0] = in.points[c * 3];
+        cp[k][1] = in.points[c * 3 + 1];
+        cp[k][2] = in.points[c * 3 + 2];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if (k < nk) {
+          const float vc[3] = {fmaf(r, fmaf(2.0f, (float)cp[k][0], 1.0f), -1.0f),
+                               fmaf(r, fmaf(2.0f, (float)cp[k][1], 1.0f), -1.0f),
+                               fmaf(r, fmaf(2.0f, (float)cp[k][2], 1.0f), -1.0f)};
+          const float en = ray_aabb(o, d, inv, sgn, vc, r);
+          bool hit;
+          if (!last) {
+            hit = en != 0.0f;
+          } else if (with_depth && with_exit) {
+            const float xs[3] = {signbit(-d[0]) ? 1.0f : -1.0f, signbit(-d[1]) ? 1.0f : -1.0f,
+                                 signbit(-d[2]) ? 1.0f : -1.0f};
+            hit = en > 0.0f && ray_aabb(o, d, inv, xs, vc, r) > 0.0f;
+          } else {
+            hit = en > 0.0f;
+          }
+          if (hit) m |= 1u << k;
+        }
+      }
+    }
+    hmask[i] = (uint8_t)m;
+    cnt[i] = (uint32_t)__popc(m);
+  }
+}
+
+__global__ void __launch_bounds__(256) rth_write_kernel(RayIn in, const uint32_t *__restrict__ dnum,
+                                                        const int2 *__restrict__ list, uint32_t level,
+                                                        uint32_t target_level, int root, int with_depth,
+                                                        int with_exit, const uint8_t *__restrict__ hmask,
+                                                        const uint32_t *__restrict__ off, uint32_t cap,
+                                                        int2 *__restrict__ nout, float *__restrict__ dout) {
+  const int64_t num = *dnum;
+  const int dd = with_exit ? 2 : 1;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < num; i += (int64_t)gridDim.x * 256) {
+    const uint32_t m = hmask[i];
+    if (!m) continue;
+    int ridx, pidx;
+    rth_node(list, i, ridx, pidx);
+    const uint32_t ob = in.octree[pidx];
+    const int32_t s = in.exsum[pidx];
+    const int16_t *p = in.points + (int64_t)pidx * 3;
+    const float *org = in.ro + (int64_t)ridx * 3;
+    const float scale = (float)(1.0 / (double)(float)(1u << level));
+    const float x = (float)((double)(0.5f * org[0] + 0.5f) - (double)scale * ((double)(float)p[0] + 0.5));
+    const float y = (float)((double)(0.5f * org[1] + 0.5f) - (double)scale * ((double)(float)p[1] + 0.5));
+    const float z = (float)((double)(0.5f * org[2] + 0.5f) - (double)scale * ((double)(float)p[2] + 0.5));
+    const uint32_t perm = c_rt_perm[(x > 0 ? 4u : 0u) + (y > 0 ? 2u : 0u) + (z > 0 ? 1u : 0u)];
+    const uint32_t lc = level + 1;
+    const bool depth_out = dout != nullptr && with_depth && lc == target_level;
+    uint32_t base = off[i];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {  // front to back: the code's permutation of the child indices
+      const uint32_t j = (perm >> (4 * q)) & 15u;
+      if (!(ob & (1u << j))) continue;
+      const int c = __popc(ob & ((2u << j) - 1));  // 1..popc: the child's rank among the node's children
+      if (!((m >> (c - 1)) & 1u)) continue;
+      if (base < cap) {
+        nout[base] = make_int2(ridx, s + c);
+        if (depth_out) {
+          const int16_t *cp = in.points + (int64_t)(s + c) * 3;
+          const float o[3] = {org[0], org[1], org[2]};
+          const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
+          const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f,
+                                signbit(d[2]) ? 1.0f : -1.0f};
+          const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
+          const float r = (float)(1.0 / (double)(float)(1u << lc));
+          const float vc[3] = {fmaf(r, fmaf(2.0f, (float)cp[0], 1.0f), -1.0f), fmaf(r, fmaf(2.0f, (float)cp[1], 1.0f), -1.0f),
+                               fmaf(r, fmaf(2.0f, (float)cp[2], 1.0f), -1.0f)};
+          dout[(int64_t)base * dd] = ray_aabb(o, d, inv, sgn, vc, r);
+          if (with_exit) {
+            const float xs[3] = {signbit(-d[0]) ? 1.0f : -1.0f, signbit(-d[1]) ? 1.0f : -1.0f,
+                                 signbit(-d[2]) ? 1.0f : -1.0f};
+            dout[(int64_t)base * dd + 1] = ray_aabb(o, d, inv, xs, vc, r);
+          }
+        }
+      }
+      base++;
+    }
+  }
+}
+
+// the eager march over the hit lists; returns 1 when some level outgrew `cap` (the caller falls back)
+static int rt_hitlist(const RayIn &in, int64_t num_rays, uint32_t target_level, int return_depth, int with_exit,
+                      Scratch &sc, int32_t **nuggets, float **depth, int64_t *num_hits, hipStream_t st) {
+  if (target_level == 0 || num_rays == 0) return 1;  // (the per-level march: the root alone, or nothing)
+  const int dd = with_exit ? 2 : 1;
+  const int64_t cap = std::max<int64_t>(std::max<int64_t>(16 * num_rays, num_rays), 1 << 16);
+  if (cap >= ((int64_t)1 << 31)) return 1;
+  const int64_t ntiles = cdiv(cap, (int64_t)DSCAN_TILE);
+  const size_t lb = al256b((size_t)cap * sizeof(int2)), cb = al256b((size_t)(cap + 2) * 4), mb = al256b((size_t)cap),
+               tb = al256b((size_t)ntiles * 4);
+  char *w = (char *)sc.get(256 + 2 * lb + 2 * cb + mb + tb);
+  int2 *out = (int2 *)sc.get((size_t)cap * sizeof(int2));
+  float *dout = return_depth ? (float *)sc.get((size_t)cap * dd * sizeof(float)) : nullptr;
+  if (!w || !out || (return_depth && !dout)) return KL_E_ALLOC;
+  uint32_t *dnum = (uint32_t *)w;            // [0] the current list's count, [1] truncated
+  int64_t *flag = (int64_t *)(w + 64);       // rt_count_kernel's result (rows, truncated)
+  int2 *la = (int2 *)(w + 256), *lb2 = (int2 *)(w + 256 + lb);
+  uint32_t *cnt = (uint32_t *)(w + 256 + 2 * lb), *off = (uint32_t *)(w + 256 + 2 * lb + cb);
+  uint8_t *hm = (uint8_t *)(w + 256 + 2 * lb + 2 * cb);
+  uint32_t *tsum = (uint32_t *)(w + 256 + 2 * lb + 2 * cb + mb);
+  // level 0's list (ray i at the root), dnum = num_rays, result = (0, 0)
+  hipLaunchKernelGGL(rt_init_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, num_rays, la, dnum, flag);
+  KL_CHECK_LAUNCH();
+  const unsigned g = (unsigned)std::min<int64_t>(cdiv(cap, 256), RTF_GRID);
+  const unsigned gt = (unsigned)ntiles;
+  int2 *cur = la, *nxt = lb2;
+  for (uint32_t l = 0; l < target_level; l++) {
+    const int root = l == 0;
+    const int last = l + 1 == target_level;
+    int2 *dst = last ? out : nxt;
+    hipLaunchKernelGGL(rth_count_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
+                       target_level, root, return_depth, with_exit, hm, cnt);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(dscan_tile_sum_kernel, dim3(gt), dim3(256), 0, st, (const uint32_t *)cnt, (const uint32_t *)dnum,
+                       tsum);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(dscan_tile_offset_kernel, dim3(1), dim3(1024), 0, st, tsum, (const uint32_t *)dnum, off);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(dscan_apply_kernel, dim3(gt), dim3(256), 0, st, (const uint32_t *)cnt, (const uint32_t *)dnum,
+                       (const uint32_t *)tsum, off);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rth_write_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
+                       target_level, root, return_depth, with_exit, (const uint8_t *)hm, (const uint32_t *)off,
+                       (uint32_t)cap, dst, last ? dout : nullptr);
+    KL_CHECK_LAUNCH();
+    // the next list's count (clipped to cap; result[1] set past it)
+    hipLaunchKernelGGL(rt_count_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)off, (uint32_t)cap, dnum, flag,
+                       last);
+    KL_CHECK_LAUNCH();
+    std::swap(cur, nxt);
+  }
+  int64_t h[2] = {0, 0};
+  KL_CHECK_RC(host_read(h, flag, sizeof(h), st));
+  if (h[1]) return 1;
+  *nuggets = (int32_t *)out;
+  *depth = dout;
+  *num_hits = h[0];
+  return KL_OK;
+}
+
 // the fixed-capacity entry's result from the fused march: (rows, truncated)
 __global__ void rt_fused_result_kernel(const RtlCtl *__restrict__ ctl, uint32_t target_level,
                                        int64_t *__restrict__ result) {
@@ -1758,10 +1957,6 @@ __global__ void rt_fused_result_kernel(const RtlCtl *__restrict__ ctl, uint32_t 
 constexpr int RTD_THREADS = 64;
 constexpr int RTD_MAXL = SPC_MAX_LEVELS + 1;
 
-// children of a node in front-to-back order from the origin's octant code: increasing Hamming
-// distance to the code, then index (rt_children) -- one nibble per child index, 8 per code
-__constant__ uint32_t c_rt_perm[8] = {0x76534210u, 0x67425301u, 0x57416302u, 0x46507213u,
-                                      0x37216504u, 0x26307415u, 0x15307426u, 0x04216537u};
 
 template <bool WRITE>
 __global__ void __launch_bounds__(RTD_THREADS) rt_dfs_kernel(RayIn in, int64_t num_rays, uint32_t target_level,
@@ -2084,9 +2279,17 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
   // end, with buffers of 16 nuggets per ray; a level with more falls back to the per-level march
   // below (dev param 15 = 2: that march always, for A/B)
   g_dev_stat[1] = 0;
-  // default: the per-level march below.  Dev param 15 = 4: the per-ray depth-first march (rt_dfs),
-  // 3: the fused level march first (kept for A/B, tested equal: at cfg4 1.22 and 2.8 ms against the
-  // per-level march's 1.20)
+  // default: the hit-list march (rt_hitlist), falling back to the per-level march below when a level
+  // outgrows its buffers.  Dev param 15 = 2: the per-level march; 4: the per-ray depth-first march
+  // (rt_dfs); 3: the fused level march first (kept for A/B, tested equal: at cfg4 1.22 and 2.8 ms
+  // against the per-level march's 1.20)
+  if (g_dev_param[15] == 0 && num_rays < ((int64_t)1 << 31)) {
+    const int rc = rt_hitlist(in, num_rays, target_level, return_depth, with_exit, sc, nuggets, depth, num_hits, st);
+    if (rc <= 0) {
+      g_dev_stat[1] = 4;
+      return rc;
+    }
+  }
   if (num_rays > 0 && num_rays < ((int64_t)1 << 31) && g_dev_param[15] == 4 && target_level < (uint32_t)RTD_MAXL) {
     g_dev_stat[1] = 3;
     return rt_dfs(in, num_rays, target_level, return_depth, with_exit, sc, nuggets, depth, num_hits, st);

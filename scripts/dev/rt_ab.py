@@ -41,7 +41,7 @@ def main():
     d = tgt.reshape(-1, 3) - o
     d = (d / d.norm(dim=-1, keepdim=True)).contiguous()
     res = {}
-    for mode in (0, 3, 4):
+    for mode in (0, 2, 3, 4):
         lib.kl_dev_set_param(15, mode)
         rt = lambda: kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], exsum, o, d, L)  # noqa: E731
         out = rt()
@@ -53,10 +53,10 @@ def main():
         res[mode] = (out, fo)
         print(f'mode {mode}: host-sized {ms:.3f} ms, fixed {msf:.3f} ms, hits {out[0].shape[0]}', flush=True)
     lib.kl_dev_set_param(15, 0)
-    for m in (3, 4):
-        (a, fa), (b, fb) = res[m], res[0]
-        print(f'mode {m} vs 0 equal host-sized:', all(torch.equal(x, y) for x, y in zip(a, b)))
-        print(f'mode {m} vs 0 equal fixed:', all(torch.equal(x, y) for x, y in zip(fa, fb)))
+    for m in (0, 3, 4):
+        (a, fa), (b, fb) = res[m], res[2]
+        print(f'mode {m} vs 2 equal host-sized:', all(torch.equal(x, y) for x, y in zip(a, b)))
+        print(f'mode {m} vs 2 equal fixed:', all(torch.equal(x, y) for x, y in zip(fa, fb)))
 
 
 if __name__ == '__main__':

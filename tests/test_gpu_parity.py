@@ -1547,14 +1547,15 @@ def test_raytrace_fixed_capture_and_truncation(kal):
 
 @pytest.mark.parametrize('level,nrays', [(4, 1000), (6, 1000), (6, 5), (0, 64), (3, 130)])
 def test_raytrace_marches_agree(kal, level, nrays):
-    """The three marches of kl_raytrace, nuggets and depths (entry and exit) bit-equal: the per-level
-    march (default, kl_dev_get_stat(1) == 0), the fused level march (dev param 15 = 3: one launch per
-    level, counts on the device, one host read) and the per-ray depth-first march (dev param 15 = 4,
-    stat 3), on a dense level-6 octree: level 4 fits the fused march's buffers (16 nuggets per ray,
-    at least 65,536), level 6 with 1,000 rays does not (~100 nuggets per ray): it reports the
-    truncation and the per-level march answers (stat 2).  Levels 0 and 3: the root alone, and ray
-    counts that are not a multiple of the depth-first march's 64-ray workgroups.  The fixed-capacity
-    entry's fused march (dev param 15 = 3) against its per-level default too."""
+    """The four marches of kl_raytrace, nuggets and depths (entry and exit) bit-equal to the per-level
+    march (dev param 15 = 2, kl_dev_get_stat(1) == 0): the hit-list march (default, stat 4; level 0
+    and lists past its buffers fall back to the per-level march, stat 0), the fused level march
+    (dev param 15 = 3: one launch per level, counts on the device, one host read) and the per-ray
+    depth-first march (dev param 15 = 4, stat 3), on a dense level-6 octree: level 4 fits the hit-list
+    and fused buffers (16 nuggets per ray, at least 65,536), level 6 with 1,000 rays does not (~100
+    nuggets per ray): both report it and the per-level march answers (stat 0 / 2).  Levels 0 and 3:
+    the root alone, and ray counts that are not a multiple of the 64-ray workgroups.  The
+    fixed-capacity entry's fused march (dev param 15 = 3) against its per-level default too."""
     import ctypes
     from kaolin import _native as N
     lib = N.lib()
@@ -1569,39 +1570,43 @@ def test_raytrace_marches_agree(kal, level, nrays):
     d = -o + 0.3 * rng.normal(size=(nrays, 3))
     d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
     outs, fixed = {}, {}
-    for mode in (0, 3, 4):
+    for mode in (2, 0, 3, 4):
         lib.kl_dev_set_param(15, mode)
         try:
             outs[mode] = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level, with_exit=True)
             torch.cuda.synchronize()
             outs[mode] += (lib.kl_dev_get_stat(1),)
-            if mode in (0, 3):
+            if mode in (2, 3):
                 fixed[mode] = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level,
                                                                 with_exit=True, capacity=1000 * nrays + 64)
         finally:
             lib.kl_dev_set_param(15, 0)
-    (r0, p0, d0, s0), (r3, p3, d3, s3), (r4, p4, d4, s4) = outs[0], outs[3], outs[4]
-    assert s0 == 0 and s4 == 3 and s3 in (1, 2) and (s3 == 2 or len(r0) <= max(16 * nrays, 65536))
+    (r2, p2, d2, s2), (r0, p0, d0, s0) = outs[2], outs[0]
+    (r3, p3, d3, s3), (r4, p4, d4, s4) = outs[3], outs[4]
+    fits = (level, nrays) != (6, 1000)
+    assert s2 == 0 and s4 == 3 and s0 == (4 if level > 0 and fits else 0)
     # 2 = a level's candidates (its parents' children) exceeded the fused march's buffers
-    assert (level, nrays) != (6, 1000) or s3 == 2
+    assert s3 in (1, 2) and (s3 == 2 or len(r2) <= max(16 * nrays, 65536)) and (fits or s3 == 2)
     assert (level, nrays) != (6, 5) or s3 == 1
-    for r, p, dp in ((r3, p3, d3), (r4, p4, d4)):
-        assert torch.equal(r, r0) and torch.equal(p, p0) and torch.equal(dp, d0)
-    assert len(r0) > (1000 if nrays > 5 and level >= 4 else 0)
-    k = len(r0)
-    for mode in (0, 3):
+    for r, p, dp in ((r0, p0, d0), (r3, p3, d3), (r4, p4, d4)):
+        assert torch.equal(r, r2) and torch.equal(p, p2) and torch.equal(dp, d2)
+    assert len(r2) > (1000 if nrays > 5 and level >= 4 else 0)
+    k = len(r2)
+    for mode in (2, 3):
         fr, fp, fd, fres = fixed[mode]
         assert A(fres).tolist() == [k, 0]
-        assert torch.equal(fr[:k], r0) and torch.equal(fp[:k], p0) and torch.equal(fd[:k], d0)
-    # without depth, and depth without exit (the depth-first march against the default)
+        assert torch.equal(fr[:k], r2) and torch.equal(fp[:k], p2) and torch.equal(fd[:k], d2)
+    # without depth, and depth without exit: the default and the depth-first march against the per-level
     for kw in ({'return_depth': False}, {}):
-        lib.kl_dev_set_param(15, 4)
-        try:
-            got = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level, **kw)
-        finally:
-            lib.kl_dev_set_param(15, 0)
-        ref = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level, **kw)
-        assert len(got) == len(ref) and all(torch.equal(x, y) for x, y in zip(got, ref))
+        got = {}
+        for mode in (2, 0, 4):
+            lib.kl_dev_set_param(15, mode)
+            try:
+                got[mode] = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level, **kw)
+            finally:
+                lib.kl_dev_set_param(15, 0)
+        for mode in (0, 4):
+            assert len(got[mode]) == len(got[2]) and all(torch.equal(x, y) for x, y in zip(got[mode], got[2]))
 
 
 @pytest.mark.parametrize('na,nb', [(0, 5), (7, 0), (3145728, 1048576), (1001, 333)])
