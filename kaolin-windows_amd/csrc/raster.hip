@@ -1863,7 +1863,10 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     ca.split_log2 = split_log2;
     ca.lp_min1 = soft_lp_min(K);
     ca.skip_empty1 = 1;
-    ca.noband = g_dev_param[18] & 3;  // dev param 18: bit 0 the rasterizer's, bit 1 the soft mask's items unbanded
+    // the soft mask's items in plain heaviest-first order (r05: 1-3 us faster than XCD bands, whose
+    // band-local ranks started heavy silhouette items late); dev param 18 = 1 + v sets the bits to v
+    // (bit 0 the rasterizer's, bit 1 the soft mask's) for A/B
+    ca.noband = g_dev_param[18] ? (g_dev_param[18] - 1) & 3 : 2;
     ca.sp = soft_split();
     ca.zero = bcnt;
     ca.nzero = DibrState::kZeroInts;

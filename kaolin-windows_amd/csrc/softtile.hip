@@ -234,34 +234,22 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
         }
         return rm;
       };
-      // append the block's entries covering this lane's pixel (bits of cm, in order) at slots
-      // slot.. while slot < K: four entries per step, their list reads in flight together (one
-      // entry per step was a chain of dependent LDS round trips on the heavy rows)
-      auto append = [&](uint64_t cm, int slot, int base) -> int {
-        while (cm && slot < K) {
-          int q[4];
-#pragma unroll
-          for (int u = 0; u < 4; u++) {
-            q[u] = cm ? __builtin_ctzll(cm) : -1;
-            cm &= cm - 1;  // (0 stays 0)
-          }
-          uint32_t f[4];
-#pragma unroll
-          for (int u = 0; u < 4; u++) f[u] = L_face[base + (q[u] < 0 ? 0 : q[u])];
-#pragma unroll
-          for (int u = 0; u < 4; u++)
-            if (q[u] >= 0 && slot < K) s_face[sl(slot++, lane)] = f[u];
-        }
-        return slot;
-      };
       if (Q == 1) {
         for (int blk = 0; blk < nb && amask; blk++) {
           const uint64_t rm = block_mask(blk);
           if (!ballot((rm & amask) != 0)) continue;
           uint64_t cm = transpose64(rm, lane);
           if (!active) cm = 0;
-          kid = append(cm, kid, blk * 64);
-          if (kid >= K) active = false;
+          const int base = blk * 64;
+          while (cm) {
+            const int q = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            s_face[sl(kid, lane)] = L_face[base + q];
+            if (++kid >= K) {
+              active = false;
+              cm = 0;
+            }
+          }
           amask = ballot(active);
         }
       } else {
@@ -286,7 +274,12 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
             slot += q < qi ? v : 0;
             all += v;
           }
-          (void)append(cm, slot, blk * 64);
+          const int base = blk * 64;
+          while (cm && slot < K) {
+            s_face[sl(slot, lane)] = L_face[base + __builtin_ctzll(cm)];
+            cm &= cm - 1;
+            slot++;
+          }
           kid = min(K, kid + all);
           active = active && kid < K;
           amask = ballot(active);

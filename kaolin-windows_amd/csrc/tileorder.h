@@ -174,9 +174,11 @@ inline int soft_items_bound(int nt, int lp_min, SoftSplit sp) {
 // parts (log2) per bucket of the soft mask's tiles; ghist (band, bucket) tile counts; sx scratch
 __device__ __forceinline__ void soft_parts(int *sx, int *lpb, const int *__restrict__ ghist, int lp_min, SoftSplit sp,
                                            int skip_empty) {
-  // tiles per bucket summed over the bands (one lane of wave 0 per bucket), then the caps walked from
-  // the heaviest bucket down in that wave's registers (each step reads the bucket's lane: no LDS
-  // round trip per step)
+  // tiles per bucket summed over the bands (one lane of wave 0 per bucket); a bucket's tiles get 8
+  // parts when it and every heavier bucket >= b8 fit in cap8 together, else 4 parts when it and every
+  // heavier bucket >= b4 not given 8 fit in cap4 -- two suffix sums over the 32 bucket lanes (r05;
+  // the r04 rule walked the buckets serially and could skip a bucket that did not fit to give a
+  // lighter one the split: one lane's serial walk measured ~2 us from a cold instruction cache)
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     int h = 0;
@@ -184,23 +186,22 @@ __device__ __forceinline__ void soft_parts(int *sx, int *lpb, const int *__restr
 #pragma unroll
       for (int g = 0; g < 8; g++) h += ghist[g * ORD_BUCKETS + lane];
     }
-    int n4 = 0, n8 = 0, mine = lp_min;
-    // a compact loop, not unrolled: this code runs once per launch from a cold instruction cache,
-    // where a 32-step unrolled body (SGPR spills included) measured 1.6 us slower
-#pragma unroll 1
-    for (int q = ORD_BUCKETS - 1; q >= 0; q--) {
-      const int hq = __builtin_amdgcn_readlane(h, q);
-      int lp = lp_min;
-      if (q >= sp.b8 && n8 + hq <= sp.cap8) {
-        lp = lp > 3 ? lp : 3;
-        n8 += hq;
-      } else if (q >= sp.b4 && n4 + hq <= sp.cap4) {
-        lp = lp > 2 ? lp : 2;
-        n4 += hq;
+    auto suffix = [&](int v) {  // sum over lanes lane..31
+#pragma unroll
+      for (int o = 1; o < ORD_BUCKETS; o <<= 1) {
+        const int u = __shfl_down(v, o);
+        if (lane + o < ORD_BUCKETS) v += u;
       }
-      if (lane == q) mine = lp;
-    }
-    if (lane < ORD_BUCKETS) lpb[lane] = lane == 0 && skip_empty ? -1 : mine;  // skip_empty: no item for tiles without candidates
+      return v;
+    };
+    const bool e8 = lane < ORD_BUCKETS && lane >= sp.b8;
+    const bool acc8 = e8 && suffix(e8 ? h : 0) <= sp.cap8;
+    const bool e4 = lane < ORD_BUCKETS && lane >= sp.b4 && !acc8;
+    const bool acc4 = e4 && suffix(e4 ? h : 0) <= sp.cap4;
+    int lp = lp_min;
+    if (acc8) lp = lp > 3 ? lp : 3;
+    else if (acc4) lp = lp > 2 ? lp : 2;
+    if (lane < ORD_BUCKETS) lpb[lane] = lane == 0 && skip_empty ? -1 : lp;  // skip_empty: no item for tiles without candidates
   }
   __syncthreads();  // sx is reused by place_prefix
 }
