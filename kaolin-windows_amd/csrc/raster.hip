@@ -473,7 +473,14 @@ __device__ __forceinline__ void bin_face(const RastSrc<T> &src, const T *__restr
 constexpr int BIN_WORD_THREADS = 512;  // one face per thread: 8 chunks
 inline bool bin_word_lds_ok(const BinGeom &g) { return (size_t)g.tiles_x * g.tiles_y * 2 * 4 <= 64 * 1024; }
 
-template <typename T, int VMODE>
+// MARKS (r05): the chunk of a face is its wave (512 threads = 8 chunks), so every lane of a wave sets
+// the same bit: instead of an LDS atomicOr per (face, tile) -- 87 % of the LDS cycles were bank
+// conflicts of lanes hitting the same tile word (r05o counters) -- each lane stores a 1 byte into
+// its wave's mark of the tile (tile-major, 8 bytes per tile: plain stores of one value), and the
+// tile's byte is gathered from its 8 marks at the end.  LDS 16 bytes per tile (bin_word_marks_ok).
+inline bool bin_word_marks_ok(const BinGeom &g) { return (size_t)g.tiles_x * g.tiles_y * 16 <= 64 * 1024; }
+
+template <typename T, int VMODE, bool MARKS>
 __global__ void __launch_bounds__(BIN_WORD_THREADS) raster_bin_word_kernel(
     RastSrc<T> src, const T *__restrict__ fvz, int F, BinGeom g, PixPitch pp, uint32_t *__restrict__ bitmap,
     T *__restrict__ rec, uint2 *__restrict__ rng, uint32_t *__restrict__ sbitmap, uint2 *__restrict__ srng, T spad,
@@ -484,29 +491,44 @@ __global__ void __launch_bounds__(BIN_WORD_THREADS) raster_bin_word_kernel(
   // the bucket kernel's histograms, zeroed here instead of by a fill launch
   if (grp == 0 && b == 0)
     for (int t = threadIdx.x; t < nzero; t += blockDim.x) zero[t] = 0;
-  uint32_t *sr = s_words, *ss = s_words + ntv;
+  uint32_t *sr = s_words, *ss = s_words + (MARKS ? 2 * ntv : ntv);  // MARKS: [tile][8] bytes each
+  uint8_t *mr = reinterpret_cast<uint8_t *>(sr), *ms = reinterpret_cast<uint8_t *>(ss);
   const bool soft = sbitmap != nullptr, rast = bitmap != nullptr;  // (the fused tile kernel: soft bins only)
-  for (int t = threadIdx.x; t < 2 * ntv; t += blockDim.x) s_words[t] = 0;
+  for (int t = threadIdx.x; t < (MARKS ? 4 : 2) * ntv; t += blockDim.x) s_words[t] = 0;
   __syncthreads();
   const int fl = grp * 512 + (int)threadIdx.x;
   if (fl < F) {
     int4 rt, st;
     bin_face<T, VMODE>(src, fvz, g, pp, (int64_t)b * F + fl, rec, rng, soft, srng, spad, rt, st);
-    const uint32_t bit = 1u << ((fl >> 6) & 7);
+    const int w = (fl >> 6) & 7;
+    const uint32_t bit = 1u << w;
     if (rast)
       for (int ty = rt.z; ty <= rt.w; ty++)
-        for (int tx = rt.x; tx <= rt.y; tx++) atomicOr(&sr[ty * g.tiles_x + tx], bit);
+        for (int tx = rt.x; tx <= rt.y; tx++) {
+          if (MARKS) mr[(ty * g.tiles_x + tx) * 8 + w] = 1;
+          else atomicOr(&sr[ty * g.tiles_x + tx], bit);
+        }
     for (int ty = st.z; ty <= st.w; ty++)
-      for (int tx = st.x; tx <= st.y; tx++) atomicOr(&ss[ty * g.tiles_x + tx], bit);
+      for (int tx = st.x; tx <= st.y; tx++) {
+        if (MARKS) ms[(ty * g.tiles_x + tx) * 8 + w] = 1;
+        else atomicOr(&ss[ty * g.tiles_x + tx], bit);
+      }
   }
   __syncthreads();
   const size_t base = (size_t)b * ntv;
   const int word = grp >> 2, byte = grp & 3;  // little-endian: chunk bits 8 byte .. 8 byte + 7
   uint8_t *rb = reinterpret_cast<uint8_t *>(bitmap), *sb = reinterpret_cast<uint8_t *>(sbitmap);
+  // 8 mark bytes (0 / 1, byte w = chunk w) -> bit w
+  auto gather8 = [](uint64_t x) { return (uint8_t)((x * 0x0102040810204080ull) >> 56); };
   for (int t = threadIdx.x; t < ntv; t += blockDim.x) {
     const size_t o = bm_index(g.ntiles(), base + t, word) * 4 + byte;
-    if (rast) rb[o] = (uint8_t)sr[t];
-    if (soft) sb[o] = (uint8_t)ss[t];
+    if (MARKS) {
+      if (rast) rb[o] = gather8(reinterpret_cast<const uint64_t *>(mr)[t]);
+      if (soft) sb[o] = gather8(reinterpret_cast<const uint64_t *>(ms)[t]);
+    } else {
+      if (rast) rb[o] = (uint8_t)sr[t];
+      if (soft) sb[o] = (uint8_t)ss[t];
+    }
   }
 }
 
@@ -515,16 +537,16 @@ static int launch_bin_word(const RastSrc<T> &src, const T *fvz, int F, const Bin
                            uint32_t *bitmap, T *rec, uint2 *rng, uint32_t *sbitmap, uint2 *srng, T spad,
                            int *zero, int nzero, hipStream_t st) {
   const dim3 grid((unsigned)(g.words * 4), (unsigned)g.batch);  // every byte of every word
-  const size_t lds = (size_t)g.tiles_x * g.tiles_y * 2 * sizeof(uint32_t);
-  if (src.vmask)
-    hipLaunchKernelGGL((raster_bin_word_kernel<T, 1>), grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp,
-                       bitmap, rec, rng, sbitmap, srng, spad, zero, nzero);
-  else if (src.nz)
-    hipLaunchKernelGGL((raster_bin_word_kernel<T, 2>), grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp,
-                       bitmap, rec, rng, sbitmap, srng, spad, zero, nzero);
-  else
-    hipLaunchKernelGGL((raster_bin_word_kernel<T, 0>), grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp,
-                       bitmap, rec, rng, sbitmap, srng, spad, zero, nzero);
+  // dev param 22 = 1: the LDS-atomic marking for A/B (and the only one past 4,096 tiles per view)
+  const bool marks = bin_word_marks_ok(g) && g_dev_param[22] != 1;
+  const size_t lds = (size_t)g.tiles_x * g.tiles_y * (marks ? 16 : 8);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(BIN_WORD_THREADS), lds, st, src, fvz, F, g, pp, bitmap, rec, rng, sbitmap,
+                       srng, spad, zero, nzero);
+  };
+  if (src.vmask) marks ? go(raster_bin_word_kernel<T, 1, true>) : go(raster_bin_word_kernel<T, 1, false>);
+  else if (src.nz) marks ? go(raster_bin_word_kernel<T, 2, true>) : go(raster_bin_word_kernel<T, 2, false>);
+  else marks ? go(raster_bin_word_kernel<T, 0, true>) : go(raster_bin_word_kernel<T, 0, false>);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

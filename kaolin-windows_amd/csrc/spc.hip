@@ -1750,22 +1750,58 @@ __device__ __forceinline__ void rth_node(const int2 *__restrict__ list, int64_t 
   pidx = nu.y;
 }
 
+// The front-to-back rank of each child of node pidx (index order k -> rank nibble), from the ray's
+// octant code at the node (rt_children's order)
+__device__ __forceinline__ uint32_t rth_fb_ranks(const RayIn &in, int ridx, int pidx, uint32_t level, uint32_t ob) {
+  const int16_t *p = in.points + (int64_t)pidx * 3;
+  const float *org = in.ro + (int64_t)ridx * 3;
+  const float scale = (float)(1.0 / (double)(float)(1u << level));
+  const float x = (float)((double)(0.5f * org[0] + 0.5f) - (double)scale * ((double)(float)p[0] + 0.5));
+  const float y = (float)((double)(0.5f * org[1] + 0.5f) - (double)scale * ((double)(float)p[1] + 0.5));
+  const float z = (float)((double)(0.5f * org[2] + 0.5f) - (double)scale * ((double)(float)p[2] + 0.5));
+  const uint32_t perm = c_rt_perm[(x > 0 ? 4u : 0u) + (y > 0 ? 2u : 0u) + (z > 0 ? 1u : 0u)];
+  uint32_t ranks = 0;
+  int rk = 0;
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t j = (perm >> (4 * q)) & 15u;
+    if (ob & (1u << j)) {
+      const int k = __popc(ob & ((1u << j) - 1));  // index-order position of child j
+      ranks |= (uint32_t)rk << (4 * k);
+      rk++;
+    }
+  }
+  return ranks;
+}
+
+// Fixed-capacity mode (cbase != nullptr, kl_raytrace_fixed): the per-level march keeps each level's
+// first `cap` candidates (a hit node's children, untested) and drops the rest with their subtrees;
+// here a child is kept when its candidate index -- the node's candidate base (an exclusive scan of
+// the listed nodes' child counts `pc`) plus its front-to-back rank -- is below `cap`, so the hit
+// lists are exactly the hits among the per-level march's kept candidates.  pc[i] == 0: the node
+// has no candidates (level 0: the root missed), nothing to decide.
 __global__ void __launch_bounds__(256) rth_count_kernel(RayIn in, const uint32_t *__restrict__ dnum,
                                                         const int2 *__restrict__ list, uint32_t level,
                                                         uint32_t target_level, int root, int with_depth,
                                                         int with_exit, uint8_t *__restrict__ hmask,
-                                                        uint32_t *__restrict__ cnt) {
+                                                        uint32_t *__restrict__ cnt, const uint32_t *__restrict__ pc,
+                                                        const uint32_t *__restrict__ cbase, uint32_t cap) {
   const int64_t num = *dnum;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < num; i += (int64_t)gridDim.x * 256) {
     int ridx, pidx;
     rth_node(list, i, ridx, pidx);
+    uint32_t m = 0;
+    if (cbase && pc[i] == 0) {  // (fixed mode: no candidates)
+      hmask[i] = 0;
+      cnt[i] = 0;
+      continue;
+    }
     const float o[3] = {in.ro[ridx * 3], in.ro[ridx * 3 + 1], in.ro[ridx * 3 + 2]};
     const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
     const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
     const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
-    uint32_t m = 0;
     bool self = true;
-    if (root) {  // the root's own test (rt_decide_one at level 0, not the target)
+    if (root && !cbase) {  // the root's own test (rt_decide_one at level 0, not the target)
       const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
                            fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
                            fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
@@ -1778,6 +1814,13 @@ __global__ void __launch_bounds__(256) rth_count_kernel(RayIn in, const uint32_t
       const uint32_t lc = level + 1;
       const bool last = lc == target_level;
       const float r = (float)(1.0 / (double)(float)(1u << lc));
+      uint32_t kept = 0xffu;  // (fixed mode: children whose candidate index is below cap)
+      if (cbase) {
+        const uint32_t ranks = rth_fb_ranks(in, ridx, pidx, level, ob), cb = cbase[i];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+          if (cb + ((ranks >> (4 * k)) & 15u) >= cap) kept &= ~(1u << k);
+      }
       int16_t cp[8][3];
 #pragma unroll
       for (int k = 0; k < 8; k++) {  // children k = 0..nk-1 at points[s + 1 + k] (index order)
@@ -1806,6 +1849,7 @@ __global__ void __launch_bounds__(256) rth_count_kernel(RayIn in, const uint32_t
           if (hit) m |= 1u << k;
         }
       }
+      m &= kept;
     }
     hmask[i] = (uint8_t)m;
     cnt[i] = (uint32_t)__popc(m);
@@ -1817,7 +1861,8 @@ __global__ void __launch_bounds__(256) rth_write_kernel(RayIn in, const uint32_t
                                                         uint32_t target_level, int root, int with_depth,
                                                         int with_exit, const uint8_t *__restrict__ hmask,
                                                         const uint32_t *__restrict__ off, uint32_t cap,
-                                                        int2 *__restrict__ nout, float *__restrict__ dout) {
+                                                        int2 *__restrict__ nout, float *__restrict__ dout,
+                                                        uint32_t *__restrict__ pc_out) {
   const int64_t num = *dnum;
   const int dd = with_exit ? 2 : 1;
   for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < num; i += (int64_t)gridDim.x * 256) {
@@ -1845,6 +1890,7 @@ __global__ void __launch_bounds__(256) rth_write_kernel(RayIn in, const uint32_t
       if (!((m >> (c - 1)) & 1u)) continue;
       if (base < cap) {
         nout[base] = make_int2(ridx, s + c);
+        if (pc_out) pc_out[base] = (uint32_t)__popc(in.octree[s + c]);  // (fixed mode: its candidates)
         if (depth_out) {
           const int16_t *cp = in.points + (int64_t)(s + c) * 3;
           const float o[3] = {org[0], org[1], org[2]};
@@ -1866,6 +1912,27 @@ __global__ void __launch_bounds__(256) rth_write_kernel(RayIn in, const uint32_t
       base++;
     }
   }
+}
+
+// fixed mode, level 0: each ray's candidate count at level 1 -- the root's children when the root
+// is hit (rt_decide_one at level 0, not the target), else none
+__global__ void __launch_bounds__(256) rth_root_kernel(RayIn in, int64_t num_rays, uint32_t *__restrict__ pc) {
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= num_rays) return;
+  const float o[3] = {in.ro[i * 3], in.ro[i * 3 + 1], in.ro[i * 3 + 2]};
+  const float d[3] = {in.rd[i * 3], in.rd[i * 3 + 1], in.rd[i * 3 + 2]};
+  const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
+  const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
+  const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
+                       fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
+                       fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
+  pc[i] = ray_aabb(o, d, inv, sgn, vc, 1.0f) != 0.0f ? (uint32_t)__popc(in.octree[0]) : 0u;
+}
+
+// flags the truncation: some level's candidates (the scan of the child counts) exceeded cap
+__global__ void rth_cand_check_kernel(const uint32_t *__restrict__ cbase, const uint32_t *__restrict__ dnum,
+                                      uint32_t cap, int64_t *__restrict__ result) {
+  if (threadIdx.x == 0 && cbase[*dnum] > cap) result[1] = 1;
 }
 
 // the eager march over the hit lists; returns 1 when some level outgrew `cap` (the caller falls back)
@@ -1899,7 +1966,8 @@ static int rt_hitlist(const RayIn &in, int64_t num_rays, uint32_t target_level, 
     const int last = l + 1 == target_level;
     int2 *dst = last ? out : nxt;
     hipLaunchKernelGGL(rth_count_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
-                       target_level, root, return_depth, with_exit, hm, cnt);
+                       target_level, root, return_depth, with_exit, hm, cnt, (const uint32_t *)nullptr,
+                       (const uint32_t *)nullptr, 0u);
     KL_CHECK_LAUNCH();
     hipLaunchKernelGGL(dscan_tile_sum_kernel, dim3(gt), dim3(256), 0, st, (const uint32_t *)cnt, (const uint32_t *)dnum,
                        tsum);
@@ -1911,7 +1979,7 @@ static int rt_hitlist(const RayIn &in, int64_t num_rays, uint32_t target_level, 
     KL_CHECK_LAUNCH();
     hipLaunchKernelGGL(rth_write_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
                        target_level, root, return_depth, with_exit, (const uint8_t *)hm, (const uint32_t *)off,
-                       (uint32_t)cap, dst, last ? dout : nullptr);
+                       (uint32_t)cap, dst, last ? dout : nullptr, (uint32_t *)nullptr);
     KL_CHECK_LAUNCH();
     // the next list's count (clipped to cap; result[1] set past it)
     hipLaunchKernelGGL(rt_count_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)off, (uint32_t)cap, dnum, flag,
@@ -2377,7 +2445,7 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
 // result[0] hold nugget (-1, -1) and depth 0.
 namespace {
 struct RtfWs {
-  size_t a, b, info, psum, dtmp, dnum, tsum, total;
+  size_t a, b, info, psum, dtmp, dnum, tsum, hm, cb, total;
   int64_t cap0, ntiles;
 };
 RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
@@ -2394,6 +2462,9 @@ RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
   w.dnum = o; o += 256;
   // the per-level scan's tile sums, or the fused march's tile status words (8 B per RTL_TILE rows)
   w.tsum = o; o += al(std::max<int64_t>(w.ntiles * 4, cdiv(w.cap0, (int64_t)RTL_TILE) * 8));
+  // the hit-list march: child masks per listed node, candidate bases (pc, its child counts, in dtmp)
+  w.hm = o; o += al(w.cap0);
+  w.cb = o; o += al((w.cap0 + 2) * 4);
   w.total = o;
   return w;
 }
@@ -2440,6 +2511,49 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
   const unsigned g = (unsigned)std::min<int64_t>(cdiv(cap0, 256), RTF_GRID);
   const unsigned gt = (unsigned)L.ntiles;
   uint32_t *tsum = (uint32_t *)(w + L.tsum);
+  // default: the hit-list march with the per-level march's truncation (rth_count_kernel's fixed
+  // mode); dev param 15 = 2: the per-level march below
+  if (g_dev_param[15] != 2 && target_level > 0 && num_rays > 0) {
+    uint32_t *pc = (uint32_t *)(w + L.dtmp), *cb = (uint32_t *)(w + L.cb);
+    uint8_t *hm = (uint8_t *)(w + L.hm);
+    hipLaunchKernelGGL(rth_root_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, in, num_rays, pc);
+    KL_CHECK_LAUNCH();
+    auto scan = [&](const uint32_t *inp, uint32_t *out) -> int {  // exclusive scan of inp[0, *dnum), out[*dnum] = total
+      hipLaunchKernelGGL(dscan_tile_sum_kernel, dim3(gt), dim3(256), 0, st, inp, (const uint32_t *)dnum, tsum);
+      KL_CHECK_LAUNCH();
+      hipLaunchKernelGGL(dscan_tile_offset_kernel, dim3(1), dim3(1024), 0, st, tsum, (const uint32_t *)dnum, out);
+      KL_CHECK_LAUNCH();
+      hipLaunchKernelGGL(dscan_apply_kernel, dim3(gt), dim3(256), 0, st, inp, (const uint32_t *)dnum,
+                         (const uint32_t *)tsum, out);
+      KL_CHECK_LAUNCH();
+      return KL_OK;
+    };
+    int2 *cur = n0, *nxt = n1;
+    for (uint32_t l = 0; l < target_level; l++) {
+      const int last = l + 1 == target_level;
+      int2 *dst = last ? (int2 *)nuggets : nxt;
+      KL_CHECK_RC(scan(pc, cb));  // candidate bases
+      hipLaunchKernelGGL(rth_cand_check_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)cb, (const uint32_t *)dnum,
+                         (uint32_t)capacity, result);
+      KL_CHECK_LAUNCH();
+      hipLaunchKernelGGL(rth_count_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
+                         target_level, (int)(l == 0), return_depth, with_exit, hm, info, (const uint32_t *)pc,
+                         (const uint32_t *)cb, (uint32_t)capacity);
+      KL_CHECK_LAUNCH();
+      KL_CHECK_RC(scan(info, psum));  // hit positions
+      hipLaunchKernelGGL(rth_write_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
+                         target_level, (int)(l == 0), return_depth, with_exit, (const uint8_t *)hm,
+                         (const uint32_t *)psum, (uint32_t)capacity, dst, last && return_depth ? depth : nullptr,
+                         last ? (uint32_t *)nullptr : pc);
+      KL_CHECK_LAUNCH();
+      // the next list's count (the hits are kept candidates: <= capacity); result[0] at the last level
+      hipLaunchKernelGGL(rt_count_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)psum, (uint32_t)capacity, dnum,
+                         result, last);
+      KL_CHECK_LAUNCH();
+      std::swap(cur, nxt);
+    }
+    return KL_OK;
+  }
   for (uint32_t l = 0; l <= target_level; l++) {
     const int last = l == target_level;
     hipLaunchKernelGGL(rtf_decide_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, n0, info,

@@ -576,6 +576,31 @@ def _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box=0.02):
     return [A(f), A(i), A(w), A(m), hits, seg, rf[:keep.size][keep], rp[:keep.size][keep], A(rg)]
 
 
+@pytest.mark.parametrize('case', ['bench', 'adversarial', 'bigbox'])
+def test_dibr_bin_marks_equal_atomic_binning(kal, case):
+    """kl_dibr_forward's binning (raster_bin_word_kernel): the r05 per-wave byte marks against the LDS
+    atomicOr marking (dev param 22 = 1) -- every output and the compact state equal."""
+    import bench
+    if case == 'adversarial':
+        z, v, f = _adversarial_faces(torch.float32)
+        fvz, fvi, feat = T(z), T(v), T(f)
+        fnz = T(np.random.default_rng(2).uniform(-0.3, 1, fvz.shape[:2]).astype(np.float32))
+        H, W, box = 97, 130, 0.02
+    else:
+        inp = bench.dibr_inputs([0.3, 2.0], DEV, H=96, W=128)
+        fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+        H, W, box = 96, 128, (0.2 if case == 'bigbox' else 0.02)
+    marks = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, 30, box)
+    try:
+        _dev_param(22, 1)
+        atomic = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, 30, box)
+    finally:
+        _dev_param(22, 0)
+    names = ['features', 'face_idx', 'weights', 'soft_mask', 'hits', 'seg_tot', 'rec_face', 'rec_prob', 'ranges']
+    for n, x, y in zip(names, marks, atomic):
+        assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
+
+
 @pytest.mark.parametrize('case', ['bench', 'adversarial', 'knum64', 'knum255', 'bigbox'])
 def test_dibr_fused_tile_kernel_equals_two_kernel_path(kal, case):
     """kl_dibr_forward's fused tile kernel (dibrtile.hip: the rasterizer and the soft mask in one
@@ -1543,6 +1568,16 @@ def test_raytrace_fixed_capture_and_truncation(kal):
     # candidates may all miss at the target level)
     assert flag == 1 and 0 <= k <= small
     assert torch.equal(tr[:k], r2[:k]) and torch.equal(tp[:k], p2[:k]) and torch.equal(tdp[:k], dep2[:k])
+    # the default (hit-list) march truncates exactly as the per-level march does (dev param 15 = 2),
+    # every row and the result, at capacities below and around the intermediate levels' counts
+    for c in (small, n2 // 2, n2, 2 * n2, 4 * n2):
+        got = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True, capacity=c)
+        try:
+            _dev_param(15, 2)
+            ref = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, to, td, L, with_exit=True, capacity=c)
+        finally:
+            _dev_param(15, 0)
+        assert all(torch.equal(x, y) for x, y in zip(got, ref)), c
 
 
 @pytest.mark.parametrize('level,nrays', [(4, 1000), (6, 1000), (6, 5), (0, 64), (3, 130)])
@@ -1555,7 +1590,8 @@ def test_raytrace_marches_agree(kal, level, nrays):
     and fused buffers (16 nuggets per ray, at least 65,536), level 6 with 1,000 rays does not (~100
     nuggets per ray): both report it and the per-level march answers (stat 0 / 2).  Levels 0 and 3:
     the root alone, and ray counts that are not a multiple of the 64-ray workgroups.  The
-    fixed-capacity entry's fused march (dev param 15 = 3) against its per-level default too."""
+    fixed-capacity entry's hit-list march (default) and fused march (dev param 15 = 3) against its
+    per-level march (dev param 15 = 2) too."""
     import ctypes
     from kaolin import _native as N
     lib = N.lib()
@@ -1576,7 +1612,7 @@ def test_raytrace_marches_agree(kal, level, nrays):
             outs[mode] = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level, with_exit=True)
             torch.cuda.synchronize()
             outs[mode] += (lib.kl_dev_get_stat(1),)
-            if mode in (2, 3):
+            if mode in (2, 0, 3):
                 fixed[mode] = kal.render.spc.unbatched_raytrace(octree, pts, pyr, ex, T(o), T(d), level,
                                                                 with_exit=True, capacity=1000 * nrays + 64)
         finally:
@@ -1592,7 +1628,7 @@ def test_raytrace_marches_agree(kal, level, nrays):
         assert torch.equal(r, r2) and torch.equal(p, p2) and torch.equal(dp, d2)
     assert len(r2) > (1000 if nrays > 5 and level >= 4 else 0)
     k = len(r2)
-    for mode in (2, 3):
+    for mode in (2, 0, 3):
         fr, fp, fd, fres = fixed[mode]
         assert A(fres).tolist() == [k, 0]
         assert torch.equal(fr[:k], r2) and torch.equal(fp[:k], p2) and torch.equal(fd[:k], d2)
