@@ -1071,17 +1071,16 @@ def raytrace_leg(device, steps, spc_tuple):
     # the hit-list march (spc.hip rth_count_kernel / rth_write_kernel; lists of HIT nodes): level 0's
     # list is the R rays at the root (8 B written); per level l < L, the count pass reads each listed
     # node's nugget 8 B, ray 24 B, octree byte 1 B, exsum 4 B and its children's points (6 B per
-    # candidate: the popcount of the node's octree byte) and writes a mask byte and a count 4 B; the
-    # device scan reads the counts twice and writes the offsets (12 B per node); the write pass reads
-    # the mask (1 B) and, per node, nugget 8 + octree 1 + exsum 4 + point 6 + ray origin 12 + offset 4 B,
-    # and writes 8 B per hit child; the target level's hits also re-read their point 6 B and ray
-    # direction 12 B for the depth (4 B written)
+    # candidate: the popcount of the node's octree byte) and writes a mask byte (the tiles' totals,
+    # 4 B per 256 nodes, are left out); the write pass reads the mask (1 B) and, per node, nugget 8 +
+    # octree 1 + exsum 4 + point 6 + ray origin 12 B, and writes 8 B per hit child; the target level's
+    # hits also re-read their point 6 B and ray direction 12 B for the depth (4 B written)
     cand = [R]
     for lv in range(L):
         _, pidx = kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], exsum, o, d, lv, return_depth=False)
         cand.append(int(_popcount_u8(octree[pidx.long()]).sum()))
     listed = [R] + per_level[1:L]
-    nbytes = 8 * R + sum(n * (8 + 24 + 1 + 4 + 1 + 4 + 12 + 1 + 8 + 1 + 4 + 6 + 12 + 4) + 6 * cand[lv + 1] +
+    nbytes = 8 * R + sum(n * (8 + 24 + 1 + 4 + 1 + 1 + 8 + 1 + 4 + 6 + 12) + 6 * cand[lv + 1] +
                          8 * per_level[lv + 1] for lv, n in enumerate(listed)) + per_level[L] * (6 + 12 + 4)
     return {'metric': 'unbatched_raytrace Mrays/s (cfg4 SPC level 9, 512x512 rays, depth)',
             'value': round(R / (ms * 1e-3) / 1e6, 2), 'ms': round(ms, 4), 'hits': hits, 'hits_per_level': per_level,

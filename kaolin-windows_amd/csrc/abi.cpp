@@ -175,28 +175,14 @@ extern "C" int kl_abi_version(void) { return KL_ABI_VERSION; }
 namespace kl {
 constexpr int DOT2_BLOCKS = 256;
 
-// float4 strips of <a, g>: DOT2_BATCH strips per thread with all their loads issued before the first
-// product (a grid-stride loop with a running sum issued them one iteration at a time)
-constexpr int DOT2_BATCH = 4;
 __device__ __forceinline__ double dot_strip(const float *__restrict__ a, const float *__restrict__ g, size_t n,
                                             size_t t, size_t nt) {
   double s = 0.0;
   const size_t n4 = ((uintptr_t)a % 16 == 0 && (uintptr_t)g % 16 == 0) ? n / 4 : 0;
-  const float4 *a4 = reinterpret_cast<const float4 *>(a), *g4 = reinterpret_cast<const float4 *>(g);
-  for (size_t i0 = t; i0 < n4; i0 += DOT2_BATCH * nt) {
-    float4 x[DOT2_BATCH], y[DOT2_BATCH];
-#pragma unroll
-    for (int k = 0; k < DOT2_BATCH; k++) {
-      const size_t i = i0 + k * nt;
-      const size_t j = i < n4 ? i : i0;  // (a valid strip; its product is dropped below)
-      x[k] = a4[j];
-      y[k] = g4[j];
-    }
-#pragma unroll
-    for (int k = 0; k < DOT2_BATCH; k++)
-      if (i0 + k * nt < n4)
-        s += (double)(x[k].x * y[k].x) + (double)(x[k].y * y[k].y) + (double)(x[k].z * y[k].z) +
-             (double)(x[k].w * y[k].w);
+#pragma unroll 8
+  for (size_t i = t; i < n4; i += nt) {
+    const float4 x = reinterpret_cast<const float4 *>(a)[i], y = reinterpret_cast<const float4 *>(g)[i];
+    s += (double)(x.x * y.x) + (double)(x.y * y.y) + (double)(x.z * y.z) + (double)(x.w * y.w);
   }
   for (size_t i = n4 * 4 + t; i < n; i += nt) s += (double)(a[i] * g[i]);
   return s;

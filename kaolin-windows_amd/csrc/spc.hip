@@ -1734,16 +1734,22 @@ static int rt_fused_levels(const RayIn &in, int64_t num_rays, uint32_t target_le
   return KL_OK;
 }
 
-// ---- Hit-list level march (r05, the eager entry's default): level l's list holds the nuggets that
-// HIT at level l (not the candidates).  Per level, one count pass decides every listed node's
-// children at level l + 1 together (their points are contiguous: points[s + 1 .. s + popc]), leaving
-// a byte of hit children and their count per node; a device scan of the counts places them; a write
-// pass lists the hit children in front-to-back order (rt_children's order) -- at the target level
-// with their depths.  Against the per-level march (decide every candidate, scan, then subdivide
-// every hit into its untested children): the candidates are never written or re-read, the ray is
-// read once per hit node instead of once per candidate, and no count goes back to the host until
-// the end (lists in `cap`-row buffers; a level past `cap` falls back to the per-level march).
-// Level 0's list is ray i at the root; the root's own test is made in the first count pass.
+// ---- Hit-list level march (r05, the default of both entries): level l's list holds the nuggets
+// that HIT at level l (not the candidates).  Per level, one count pass decides every listed node's
+// children at l + 1 together (their points are contiguous: points[s + 1 .. s + popc]), leaving a
+// byte of hit children per node and each 256-node tile's total; one workgroup scans the tile totals;
+// the write pass re-scans its tile's counts locally and lists the hit children in front-to-back
+// order (rt_children's order) -- at the target level with their depths.  Against the per-level
+// march (decide every candidate, scan, then subdivide every hit into its untested children): the
+// candidates are never written or re-read, the ray is read once per hit node instead of once per
+// candidate, and no count goes back to the host until the end.
+// Fixed-capacity mode (kl_raytrace_fixed): the per-level march keeps each level's first `cap`
+// candidates (a hit node's children, untested) and drops the rest with their subtrees; here a child
+// is kept when its candidate index -- the node's candidate base (a scan of the listed nodes' child
+// counts `pc`, written by the previous write pass) plus its front-to-back rank -- is below `cap`,
+// so the lists are exactly the hits among the per-level march's kept candidates.
+constexpr int RTH_TILE = 256;  // nodes per tile = threads per workgroup
+
 __device__ __forceinline__ void rth_node(const int2 *__restrict__ list, int64_t i, int &ridx, int &pidx) {
   const int2 nu = list[i];
   ridx = nu.x;
@@ -1774,99 +1780,152 @@ __device__ __forceinline__ uint32_t rth_fb_ranks(const RayIn &in, int ridx, int 
   return ranks;
 }
 
-// Fixed-capacity mode (cbase != nullptr, kl_raytrace_fixed): the per-level march keeps each level's
-// first `cap` candidates (a hit node's children, untested) and drops the rest with their subtrees;
-// here a child is kept when its candidate index -- the node's candidate base (an exclusive scan of
-// the listed nodes' child counts `pc`) plus its front-to-back rank -- is below `cap`, so the hit
-// lists are exactly the hits among the per-level march's kept candidates.  pc[i] == 0: the node
-// has no candidates (level 0: the root missed), nothing to decide.
-__global__ void __launch_bounds__(256) rth_count_kernel(RayIn in, const uint32_t *__restrict__ dnum,
-                                                        const int2 *__restrict__ list, uint32_t level,
-                                                        uint32_t target_level, int root, int with_depth,
-                                                        int with_exit, uint8_t *__restrict__ hmask,
-                                                        uint32_t *__restrict__ cnt, const uint32_t *__restrict__ pc,
-                                                        const uint32_t *__restrict__ cbase, uint32_t cap) {
+// count pass: hmask[i] = the hit (fixed mode: and kept) children of listed node i in index order;
+// tsum[t] = their total over tile t.  root: level 0, the root's own test first (eager mode; in fixed
+// mode pc == 0 marks a missed root).  Fixed mode: cbt = the tiles' exclusive candidate offsets.
+__global__ void __launch_bounds__(RTH_TILE) rth_count_kernel(RayIn in, const uint32_t *__restrict__ dnum,
+                                                             const int2 *__restrict__ list, uint32_t level,
+                                                             uint32_t target_level, int root, int with_depth,
+                                                             int with_exit, uint8_t *__restrict__ hmask,
+                                                             uint32_t *__restrict__ tsum, const uint32_t *__restrict__ pc,
+                                                             const uint32_t *__restrict__ cbt, uint32_t cap) {
+  __shared__ int s_wave[RTH_TILE / 64];
   const int64_t num = *dnum;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < num; i += (int64_t)gridDim.x * 256) {
-    int ridx, pidx;
-    rth_node(list, i, ridx, pidx);
+  for (int64_t t = blockIdx.x; t * RTH_TILE < num; t += gridDim.x) {  // workgroup-uniform
+    const int64_t i = t * RTH_TILE + threadIdx.x;
+    const bool in_list = i < num;
+    uint32_t cb = 0;
+    if (cbt) {  // the node's candidate base: the tile's offset + the scan of pc within the tile
+      int tot;
+      cb = cbt[t] + (uint32_t)block_exclusive_scan(in_list ? (int)pc[i] : 0, s_wave, &tot);
+    }
     uint32_t m = 0;
-    if (cbase && pc[i] == 0) {  // (fixed mode: no candidates)
-      hmask[i] = 0;
-      cnt[i] = 0;
-      continue;
-    }
-    const float o[3] = {in.ro[ridx * 3], in.ro[ridx * 3 + 1], in.ro[ridx * 3 + 2]};
-    const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
-    const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
-    const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
-    bool self = true;
-    if (root && !cbase) {  // the root's own test (rt_decide_one at level 0, not the target)
-      const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
-                           fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
-                           fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
-      self = ray_aabb(o, d, inv, sgn, vc, 1.0f) != 0.0f;
-    }
-    if (self) {
-      const uint32_t ob = in.octree[pidx];
-      const int32_t s = in.exsum[pidx];
-      const int nk = __popc(ob);
-      const uint32_t lc = level + 1;
-      const bool last = lc == target_level;
-      const float r = (float)(1.0 / (double)(float)(1u << lc));
-      uint32_t kept = 0xffu;  // (fixed mode: children whose candidate index is below cap)
-      if (cbase) {
-        const uint32_t ranks = rth_fb_ranks(in, ridx, pidx, level, ob), cb = cbase[i];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-          if (cb + ((ranks >> (4 * k)) & 15u) >= cap) kept &= ~(1u << k);
+    if (in_list && !(cbt && pc[i] == 0)) {
+      int ridx, pidx;
+      rth_node(list, i, ridx, pidx);
+      const float o[3] = {in.ro[ridx * 3], in.ro[ridx * 3 + 1], in.ro[ridx * 3 + 2]};
+      const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
+      const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f,
+                            signbit(d[2]) ? 1.0f : -1.0f};
+      const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
+      bool self = true;
+      if (root && !cbt) {  // the root's own test (rt_decide_one at level 0, not the target)
+        const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
+                             fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
+                             fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
+        self = ray_aabb(o, d, inv, sgn, vc, 1.0f) != 0.0f;
       }
-      int16_t cp[8][3];
+      if (self) {
+        const uint32_t ob = in.octree[pidx];
+        const int32_t s = in.exsum[pidx];
+        const int nk = __popc(ob);
+        const uint32_t lc = level + 1;
+        const bool last = lc == target_level;
+        const float r = (float)(1.0 / (double)(float)(1u << lc));
+        uint32_t kept = 0xffu;  // (fixed mode: children whose candidate index is below cap)
+        if (cbt) {
+          const uint32_t ranks = rth_fb_ranks(in, ridx, pidx, level, ob);
 #pragma unroll
-      for (int k = 0; k < 8; k++) {  // children k = 0..nk-1 at points[s + 1 + k] (index order)
-        const int64_t c = (int64_t)s + 1 + (k < nk ? k : 0);
-        cp[k][0] = in.points[c * 3];
-        cp[k][1] = in.points[c * 3 + 1];
-        cp[k][2] = in.points[c * 3 + 2];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        if (k < nk) {
-          const float vc[3] = {fmaf(r, fmaf(2.0f, (float)cp[k][0], 1.0f), -1.0f),
-                               fmaf(r, fmaf(2.0f, (float)cp[k][1], 1.0f), -1.0f),
-                               fmaf(r, fmaf(2.0f, (float)cp[k][2], 1.0f), -1.0f)};
-          const float en = ray_aabb(o, d, inv, sgn, vc, r);
-          bool hit;
-          if (!last) {
-            hit = en != 0.0f;
-          } else if (with_depth && with_exit) {
-            const float xs[3] = {signbit(-d[0]) ? 1.0f : -1.0f, signbit(-d[1]) ? 1.0f : -1.0f,
-                                 signbit(-d[2]) ? 1.0f : -1.0f};
-            hit = en > 0.0f && ray_aabb(o, d, inv, xs, vc, r) > 0.0f;
-          } else {
-            hit = en > 0.0f;
-          }
-          if (hit) m |= 1u << k;
+          for (int k = 0; k < 8; k++)
+            if (cb + ((ranks >> (4 * k)) & 15u) >= cap) kept &= ~(1u << k);
         }
+        int16_t cp[8][3];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {  // children k = 0..nk-1 at points[s + 1 + k] (index order)
+          const int64_t c = (int64_t)s + 1 + (k < nk ? k : 0);
+          cp[k][0] = in.points[c * 3];
+          cp[k][1] = in.points[c * 3 + 1];
+          cp[k][2] = in.points[c * 3 + 2];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          if (k < nk) {
+            const float vc[3] = {fmaf(r, fmaf(2.0f, (float)cp[k][0], 1.0f), -1.0f),
+                                 fmaf(r, fmaf(2.0f, (float)cp[k][1], 1.0f), -1.0f),
+                                 fmaf(r, fmaf(2.0f, (float)cp[k][2], 1.0f), -1.0f)};
+            const float en = ray_aabb(o, d, inv, sgn, vc, r);
+            bool hit;
+            if (!last) {
+              hit = en != 0.0f;
+            } else if (with_depth && with_exit) {
+              const float xs[3] = {signbit(-d[0]) ? 1.0f : -1.0f, signbit(-d[1]) ? 1.0f : -1.0f,
+                                   signbit(-d[2]) ? 1.0f : -1.0f};
+              hit = en > 0.0f && ray_aabb(o, d, inv, xs, vc, r) > 0.0f;
+            } else {
+              hit = en > 0.0f;
+            }
+            if (hit) m |= 1u << k;
+          }
+        }
+        m &= kept;
       }
-      m &= kept;
     }
-    hmask[i] = (uint8_t)m;
-    cnt[i] = (uint32_t)__popc(m);
+    if (in_list) hmask[i] = (uint8_t)m;
+    int tot;
+    (void)block_exclusive_scan(__popc(m), s_wave, &tot);
+    if (threadIdx.x == 0) tsum[t] = (uint32_t)tot;
   }
 }
 
-__global__ void __launch_bounds__(256) rth_write_kernel(RayIn in, const uint32_t *__restrict__ dnum,
-                                                        const int2 *__restrict__ list, uint32_t level,
-                                                        uint32_t target_level, int root, int with_depth,
-                                                        int with_exit, const uint8_t *__restrict__ hmask,
-                                                        const uint32_t *__restrict__ off, uint32_t cap,
-                                                        int2 *__restrict__ nout, float *__restrict__ dout,
-                                                        uint32_t *__restrict__ pc_out) {
+// One workgroup: the exclusive scan of the tile totals tsum[0, cdiv(*dnum, RTH_TILE)) in place.
+// The total: > cap sets result[1]; with `next`, *next = min(total, cap) (the next list's count) and
+// at the last level result[0] = it.
+__global__ void __launch_bounds__(1024) rth_offsets_kernel(uint32_t *__restrict__ tsum, const uint32_t *__restrict__ dnum,
+                                                           uint32_t *__restrict__ next, uint32_t cap,
+                                                           int64_t *__restrict__ result, int last) {
+  __shared__ int s_wave[16];
+  const int64_t n = *dnum;
+  const int nt = (int)((n + RTH_TILE - 1) / RTH_TILE);
+  uint32_t carry = 0;
+  for (int b0 = 0; b0 < nt; b0 += 1024) {
+    const int i = b0 + threadIdx.x;
+    const int v = i < nt ? (int)tsum[i] : 0;
+    int tot = 0;
+    const int ex = block_exclusive_scan(v, s_wave, &tot);
+    if (i < nt) tsum[i] = carry + (uint32_t)ex;
+    carry += (uint32_t)tot;
+  }
+  if (threadIdx.x == 0) {
+    if (carry > cap) result[1] = 1;
+    if (next) {
+      const uint32_t c = carry < cap ? carry : cap;
+      *next = c;
+      if (last) result[0] = c;
+    }
+  }
+}
+
+// fixed mode: the tile totals of the listed nodes' child counts pc (the candidate offsets' input)
+__global__ void __launch_bounds__(RTH_TILE) rth_pcsum_kernel(const uint32_t *__restrict__ dnum,
+                                                             const uint32_t *__restrict__ pc, uint32_t *__restrict__ tsum) {
+  __shared__ int s_wave[RTH_TILE / 64];
+  const int64_t num = *dnum;
+  for (int64_t t = blockIdx.x; t * RTH_TILE < num; t += gridDim.x) {
+    const int64_t i = t * RTH_TILE + threadIdx.x;
+    int tot;
+    (void)block_exclusive_scan(i < num ? (int)pc[i] : 0, s_wave, &tot);
+    if (threadIdx.x == 0) tsum[t] = (uint32_t)tot;
+  }
+}
+
+// write pass: node i's hit children at toff[t] + (its tile's exclusive scan of the hit counts), in
+// front-to-back order; at the target level with depths.  pc_out (fixed mode, not the last level):
+// each listed child's own child count.
+__global__ void __launch_bounds__(RTH_TILE) rth_write_kernel(RayIn in, const uint32_t *__restrict__ dnum,
+                                                             const int2 *__restrict__ list, uint32_t level,
+                                                             uint32_t target_level, int with_depth, int with_exit,
+                                                             const uint8_t *__restrict__ hmask,
+                                                             const uint32_t *__restrict__ toff, uint32_t cap,
+                                                             int2 *__restrict__ nout, float *__restrict__ dout,
+                                                             uint32_t *__restrict__ pc_out) {
+  __shared__ int s_wave[RTH_TILE / 64];
   const int64_t num = *dnum;
   const int dd = with_exit ? 2 : 1;
-  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < num; i += (int64_t)gridDim.x * 256) {
-    const uint32_t m = hmask[i];
+  for (int64_t t = blockIdx.x; t * RTH_TILE < num; t += gridDim.x) {
+    const int64_t i = t * RTH_TILE + threadIdx.x;
+    const uint32_t m = i < num ? hmask[i] : 0u;
+    int tot;
+    uint32_t base = toff[t] + (uint32_t)block_exclusive_scan(__popc(m), s_wave, &tot);
     if (!m) continue;
     int ridx, pidx;
     rth_node(list, i, ridx, pidx);
@@ -1881,7 +1940,6 @@ __global__ void __launch_bounds__(256) rth_write_kernel(RayIn in, const uint32_t
     const uint32_t perm = c_rt_perm[(x > 0 ? 4u : 0u) + (y > 0 ? 2u : 0u) + (z > 0 ? 1u : 0u)];
     const uint32_t lc = level + 1;
     const bool depth_out = dout != nullptr && with_depth && lc == target_level;
-    uint32_t base = off[i];
 #pragma unroll
     for (int q = 0; q < 8; q++) {  // front to back: the code's permutation of the child indices
       const uint32_t j = (perm >> (4 * q)) & 15u;
@@ -1890,7 +1948,7 @@ __global__ void __launch_bounds__(256) rth_write_kernel(RayIn in, const uint32_t
       if (!((m >> (c - 1)) & 1u)) continue;
       if (base < cap) {
         nout[base] = make_int2(ridx, s + c);
-        if (pc_out) pc_out[base] = (uint32_t)__popc(in.octree[s + c]);  // (fixed mode: its candidates)
+        if (pc_out) pc_out[base] = (uint32_t)__popc(in.octree[s + c]);
         if (depth_out) {
           const int16_t *cp = in.points + (int64_t)(s + c) * 3;
           const float o[3] = {org[0], org[1], org[2]};
@@ -1915,24 +1973,88 @@ __global__ void __launch_bounds__(256) rth_write_kernel(RayIn in, const uint32_t
 }
 
 // fixed mode, level 0: each ray's candidate count at level 1 -- the root's children when the root
-// is hit (rt_decide_one at level 0, not the target), else none
-__global__ void __launch_bounds__(256) rth_root_kernel(RayIn in, int64_t num_rays, uint32_t *__restrict__ pc) {
-  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
-  if (i >= num_rays) return;
-  const float o[3] = {in.ro[i * 3], in.ro[i * 3 + 1], in.ro[i * 3 + 2]};
-  const float d[3] = {in.rd[i * 3], in.rd[i * 3 + 1], in.rd[i * 3 + 2]};
-  const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
-  const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
-  const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
-                       fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
-                       fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
-  pc[i] = ray_aabb(o, d, inv, sgn, vc, 1.0f) != 0.0f ? (uint32_t)__popc(in.octree[0]) : 0u;
+// is hit (rt_decide_one at level 0, not the target), else none -- and the tiles' totals
+__global__ void __launch_bounds__(RTH_TILE) rth_root_kernel(RayIn in, int64_t num_rays, uint32_t *__restrict__ pc,
+                                                            uint32_t *__restrict__ tsum) {
+  __shared__ int s_wave[RTH_TILE / 64];
+  const int64_t i = blockIdx.x * (int64_t)RTH_TILE + threadIdx.x;
+  uint32_t v = 0;
+  if (i < num_rays) {
+    const float o[3] = {in.ro[i * 3], in.ro[i * 3 + 1], in.ro[i * 3 + 2]};
+    const float d[3] = {in.rd[i * 3], in.rd[i * 3 + 1], in.rd[i * 3 + 2]};
+    const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
+    const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
+    const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
+                         fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
+                         fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
+    v = ray_aabb(o, d, inv, sgn, vc, 1.0f) != 0.0f ? (uint32_t)__popc(in.octree[0]) : 0u;
+    pc[i] = v;
+  }
+  int tot;
+  (void)block_exclusive_scan((int)v, s_wave, &tot);
+  if (threadIdx.x == 0) tsum[blockIdx.x] = (uint32_t)tot;
 }
 
-// flags the truncation: some level's candidates (the scan of the child counts) exceeded cap
-__global__ void rth_cand_check_kernel(const uint32_t *__restrict__ cbase, const uint32_t *__restrict__ dnum,
-                                      uint32_t cap, int64_t *__restrict__ result) {
-  if (threadIdx.x == 0 && cbase[*dnum] > cap) result[1] = 1;
+// The levels of the hit-list march.  lists a / b (`cap` rows each), hm (cap bytes), tsA / tsB
+// (cdiv(cap, RTH_TILE) each), dn[2] (the current / next list's count), result (rows, truncated)
+// zeroed by the caller; list a holds level 0 (ray i at the root) and dn[0] = num_rays.  Fixed mode:
+// pc (cap), cand_cap = the capacity the candidates are truncated at.
+struct RthBufs {
+  int2 *a, *b;
+  uint8_t *hm;
+  uint32_t *tsA, *tsB, *dn, *pc;
+  int64_t *result;
+};
+static int rth_levels(const RayIn &in, int64_t num_rays, uint32_t target_level, int return_depth, int with_exit,
+                      int64_t cap, bool fixed, const RthBufs &bf, int2 *out, float *dout, hipStream_t st) {
+  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(std::max(cap, num_rays), (int64_t)RTH_TILE),
+                                                                      RTF_GRID));
+  int2 *cur = bf.a, *nxt = bf.b;
+  if (fixed) {
+    hipLaunchKernelGGL(rth_root_kernel, dim3((unsigned)cdiv(num_rays, (int64_t)RTH_TILE)), dim3(RTH_TILE), 0, st, in,
+                       num_rays, bf.pc, bf.tsA);
+    KL_CHECK_LAUNCH();
+  }
+  for (uint32_t l = 0; l < target_level; l++) {
+    const int last = l + 1 == target_level;
+    const uint32_t *dcur = bf.dn + (l & 1);
+    uint32_t *dnext = bf.dn + ((l + 1) & 1);
+    if (fixed) {  // candidate offsets (the level's candidate total past cap flags the truncation)
+      if (l > 0) {
+        hipLaunchKernelGGL(rth_pcsum_kernel, dim3(g), dim3(RTH_TILE), 0, st, dcur, (const uint32_t *)bf.pc, bf.tsA);
+        KL_CHECK_LAUNCH();
+      }
+      hipLaunchKernelGGL(rth_offsets_kernel, dim3(1), dim3(1024), 0, st, bf.tsA, dcur, (uint32_t *)nullptr,
+                         (uint32_t)cap, bf.result, 0);
+      KL_CHECK_LAUNCH();
+    }
+    hipLaunchKernelGGL(rth_count_kernel, dim3(g), dim3(RTH_TILE), 0, st, in, dcur, (const int2 *)cur, l, target_level,
+                       (int)(l == 0), return_depth, with_exit, bf.hm, bf.tsB,
+                       fixed ? (const uint32_t *)bf.pc : (const uint32_t *)nullptr,
+                       fixed ? (const uint32_t *)bf.tsA : (const uint32_t *)nullptr, (uint32_t)cap);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rth_offsets_kernel, dim3(1), dim3(1024), 0, st, bf.tsB, dcur, dnext, (uint32_t)cap, bf.result,
+                       last);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rth_write_kernel, dim3(g), dim3(RTH_TILE), 0, st, in, dcur, (const int2 *)cur, l, target_level,
+                       return_depth, with_exit, (const uint8_t *)bf.hm, (const uint32_t *)bf.tsB, (uint32_t)cap,
+                       last ? out : nxt, last ? dout : nullptr, fixed && !last ? bf.pc : (uint32_t *)nullptr);
+    KL_CHECK_LAUNCH();
+    std::swap(cur, nxt);
+  }
+  return KL_OK;
+}
+
+__global__ void rth_init_kernel(int64_t n, int2 *__restrict__ list, uint32_t *__restrict__ dn,
+                                int64_t *__restrict__ result) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t < n) list[t] = make_int2((int)t, 0);
+  if (t == 0) {
+    dn[0] = (uint32_t)n;
+    dn[1] = 0;
+    result[0] = 0;
+    result[1] = 0;
+  }
 }
 
 // the eager march over the hit lists; returns 1 when some level outgrew `cap` (the caller falls back)
@@ -1942,53 +2064,25 @@ static int rt_hitlist(const RayIn &in, int64_t num_rays, uint32_t target_level, 
   const int dd = with_exit ? 2 : 1;
   const int64_t cap = std::max<int64_t>(std::max<int64_t>(16 * num_rays, num_rays), 1 << 16);
   if (cap >= ((int64_t)1 << 31)) return 1;
-  const int64_t ntiles = cdiv(cap, (int64_t)DSCAN_TILE);
-  const size_t lb = al256b((size_t)cap * sizeof(int2)), cb = al256b((size_t)(cap + 2) * 4), mb = al256b((size_t)cap),
-               tb = al256b((size_t)ntiles * 4);
-  char *w = (char *)sc.get(256 + 2 * lb + 2 * cb + mb + tb);
+  const int64_t ntiles = cdiv(cap, (int64_t)RTH_TILE);
+  const size_t lb = al256b((size_t)cap * sizeof(int2)), mb = al256b((size_t)cap), tb = al256b((size_t)ntiles * 4);
+  char *w = (char *)sc.get(256 + 2 * lb + mb + tb);
   int2 *out = (int2 *)sc.get((size_t)cap * sizeof(int2));
   float *dout = return_depth ? (float *)sc.get((size_t)cap * dd * sizeof(float)) : nullptr;
   if (!w || !out || (return_depth && !dout)) return KL_E_ALLOC;
-  uint32_t *dnum = (uint32_t *)w;            // [0] the current list's count, [1] truncated
-  int64_t *flag = (int64_t *)(w + 64);       // rt_count_kernel's result (rows, truncated)
-  int2 *la = (int2 *)(w + 256), *lb2 = (int2 *)(w + 256 + lb);
-  uint32_t *cnt = (uint32_t *)(w + 256 + 2 * lb), *off = (uint32_t *)(w + 256 + 2 * lb + cb);
-  uint8_t *hm = (uint8_t *)(w + 256 + 2 * lb + 2 * cb);
-  uint32_t *tsum = (uint32_t *)(w + 256 + 2 * lb + 2 * cb + mb);
-  // level 0's list (ray i at the root), dnum = num_rays, result = (0, 0)
-  hipLaunchKernelGGL(rt_init_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, num_rays, la, dnum, flag);
+  RthBufs bf{};
+  bf.dn = (uint32_t *)w;
+  bf.result = (int64_t *)(w + 64);  // (rows, truncated)
+  bf.a = (int2 *)(w + 256);
+  bf.b = (int2 *)(w + 256 + lb);
+  bf.hm = (uint8_t *)(w + 256 + 2 * lb);
+  bf.tsB = (uint32_t *)(w + 256 + 2 * lb + mb);
+  hipLaunchKernelGGL(rth_init_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, num_rays, bf.a, bf.dn,
+                     bf.result);
   KL_CHECK_LAUNCH();
-  const unsigned g = (unsigned)std::min<int64_t>(cdiv(cap, 256), RTF_GRID);
-  const unsigned gt = (unsigned)ntiles;
-  int2 *cur = la, *nxt = lb2;
-  for (uint32_t l = 0; l < target_level; l++) {
-    const int root = l == 0;
-    const int last = l + 1 == target_level;
-    int2 *dst = last ? out : nxt;
-    hipLaunchKernelGGL(rth_count_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
-                       target_level, root, return_depth, with_exit, hm, cnt, (const uint32_t *)nullptr,
-                       (const uint32_t *)nullptr, 0u);
-    KL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(dscan_tile_sum_kernel, dim3(gt), dim3(256), 0, st, (const uint32_t *)cnt, (const uint32_t *)dnum,
-                       tsum);
-    KL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(dscan_tile_offset_kernel, dim3(1), dim3(1024), 0, st, tsum, (const uint32_t *)dnum, off);
-    KL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(dscan_apply_kernel, dim3(gt), dim3(256), 0, st, (const uint32_t *)cnt, (const uint32_t *)dnum,
-                       (const uint32_t *)tsum, off);
-    KL_CHECK_LAUNCH();
-    hipLaunchKernelGGL(rth_write_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
-                       target_level, root, return_depth, with_exit, (const uint8_t *)hm, (const uint32_t *)off,
-                       (uint32_t)cap, dst, last ? dout : nullptr, (uint32_t *)nullptr);
-    KL_CHECK_LAUNCH();
-    // the next list's count (clipped to cap; result[1] set past it)
-    hipLaunchKernelGGL(rt_count_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)off, (uint32_t)cap, dnum, flag,
-                       last);
-    KL_CHECK_LAUNCH();
-    std::swap(cur, nxt);
-  }
+  KL_CHECK_RC(rth_levels(in, num_rays, target_level, return_depth, with_exit, cap, false, bf, out, dout, st));
   int64_t h[2] = {0, 0};
-  KL_CHECK_RC(host_read(h, flag, sizeof(h), st));
+  KL_CHECK_RC(host_read(h, bf.result, sizeof(h), st));
   if (h[1]) return 1;
   *nuggets = (int32_t *)out;
   *depth = dout;
@@ -2445,7 +2539,7 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
 // result[0] hold nugget (-1, -1) and depth 0.
 namespace {
 struct RtfWs {
-  size_t a, b, info, psum, dtmp, dnum, tsum, hm, cb, total;
+  size_t a, b, info, psum, dtmp, dnum, tsum, hm, tsa, tsb, total;
   int64_t cap0, ntiles;
 };
 RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
@@ -2462,9 +2556,11 @@ RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
   w.dnum = o; o += 256;
   // the per-level scan's tile sums, or the fused march's tile status words (8 B per RTL_TILE rows)
   w.tsum = o; o += al(std::max<int64_t>(w.ntiles * 4, cdiv(w.cap0, (int64_t)RTL_TILE) * 8));
-  // the hit-list march: child masks per listed node, candidate bases (pc, its child counts, in dtmp)
+  // the hit-list march: child masks per listed node, the candidate / hit tile totals (pc, the listed
+  // nodes' child counts, lives in dtmp)
   w.hm = o; o += al(w.cap0);
-  w.cb = o; o += al((w.cap0 + 2) * 4);
+  w.tsa = o; o += al(cdiv(w.cap0, (int64_t)RTH_TILE) * 4);
+  w.tsb = o; o += al(cdiv(w.cap0, (int64_t)RTH_TILE) * 4);
   w.total = o;
   return w;
 }
@@ -2505,55 +2601,30 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
     KL_CHECK_LAUNCH();
     return KL_OK;
   }
+  // default: the hit-list march with the per-level march's truncation (rth_count_kernel's fixed
+  // mode); dev param 15 = 2: the per-level march below
+  if (g_dev_param[15] != 2 && target_level > 0 && num_rays > 0 && capacity > 0) {
+    RthBufs bf{};
+    bf.a = n0;
+    bf.b = n1;
+    bf.hm = (uint8_t *)(w + L.hm);
+    bf.tsA = (uint32_t *)(w + L.tsa);
+    bf.tsB = (uint32_t *)(w + L.tsb);
+    bf.dn = dnum;
+    bf.pc = (uint32_t *)(w + L.dtmp);
+    bf.result = result;
+    hipLaunchKernelGGL(rth_init_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, num_rays, n0, dnum,
+                       result);
+    KL_CHECK_LAUNCH();
+    return rth_levels(in, num_rays, target_level, return_depth, with_exit, capacity, true, bf, (int2 *)nuggets,
+                      return_depth ? depth : nullptr, st);
+  }
   hipLaunchKernelGGL(rt_init_kernel, dim3((unsigned)cdiv(std::max<int64_t>(num_rays, 1), 256)), dim3(256), 0, st,
                      num_rays, n0, dnum, result);
   KL_CHECK_LAUNCH();
   const unsigned g = (unsigned)std::min<int64_t>(cdiv(cap0, 256), RTF_GRID);
   const unsigned gt = (unsigned)L.ntiles;
   uint32_t *tsum = (uint32_t *)(w + L.tsum);
-  // default: the hit-list march with the per-level march's truncation (rth_count_kernel's fixed
-  // mode); dev param 15 = 2: the per-level march below
-  if (g_dev_param[15] != 2 && target_level > 0 && num_rays > 0) {
-    uint32_t *pc = (uint32_t *)(w + L.dtmp), *cb = (uint32_t *)(w + L.cb);
-    uint8_t *hm = (uint8_t *)(w + L.hm);
-    hipLaunchKernelGGL(rth_root_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, in, num_rays, pc);
-    KL_CHECK_LAUNCH();
-    auto scan = [&](const uint32_t *inp, uint32_t *out) -> int {  // exclusive scan of inp[0, *dnum), out[*dnum] = total
-      hipLaunchKernelGGL(dscan_tile_sum_kernel, dim3(gt), dim3(256), 0, st, inp, (const uint32_t *)dnum, tsum);
-      KL_CHECK_LAUNCH();
-      hipLaunchKernelGGL(dscan_tile_offset_kernel, dim3(1), dim3(1024), 0, st, tsum, (const uint32_t *)dnum, out);
-      KL_CHECK_LAUNCH();
-      hipLaunchKernelGGL(dscan_apply_kernel, dim3(gt), dim3(256), 0, st, inp, (const uint32_t *)dnum,
-                         (const uint32_t *)tsum, out);
-      KL_CHECK_LAUNCH();
-      return KL_OK;
-    };
-    int2 *cur = n0, *nxt = n1;
-    for (uint32_t l = 0; l < target_level; l++) {
-      const int last = l + 1 == target_level;
-      int2 *dst = last ? (int2 *)nuggets : nxt;
-      KL_CHECK_RC(scan(pc, cb));  // candidate bases
-      hipLaunchKernelGGL(rth_cand_check_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)cb, (const uint32_t *)dnum,
-                         (uint32_t)capacity, result);
-      KL_CHECK_LAUNCH();
-      hipLaunchKernelGGL(rth_count_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
-                         target_level, (int)(l == 0), return_depth, with_exit, hm, info, (const uint32_t *)pc,
-                         (const uint32_t *)cb, (uint32_t)capacity);
-      KL_CHECK_LAUNCH();
-      KL_CHECK_RC(scan(info, psum));  // hit positions
-      hipLaunchKernelGGL(rth_write_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, (const int2 *)cur, l,
-                         target_level, (int)(l == 0), return_depth, with_exit, (const uint8_t *)hm,
-                         (const uint32_t *)psum, (uint32_t)capacity, dst, last && return_depth ? depth : nullptr,
-                         last ? (uint32_t *)nullptr : pc);
-      KL_CHECK_LAUNCH();
-      // the next list's count (the hits are kept candidates: <= capacity); result[0] at the last level
-      hipLaunchKernelGGL(rt_count_kernel, dim3(1), dim3(64), 0, st, (const uint32_t *)psum, (uint32_t)capacity, dnum,
-                         result, last);
-      KL_CHECK_LAUNCH();
-      std::swap(cur, nxt);
-    }
-    return KL_OK;
-  }
   for (uint32_t l = 0; l <= target_level; l++) {
     const int last = l == target_level;
     hipLaunchKernelGGL(rtf_decide_kernel, dim3(g), dim3(256), 0, st, in, (const uint32_t *)dnum, n0, info,
