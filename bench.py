@@ -1092,8 +1092,8 @@ def raytrace_leg(device, steps, spc_tuple):
             'roofline': {'bound': 'hbm', 'achieved': round(nbytes / (ms * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          'bytes_model': 'the hit-list march: per listed hit node its nugget, ray, octree byte, exsum, '
-                                        'its children\'s points, mask / count / offsets, the write pass\'s reads and '
-                                        '8 B per hit child; per target hit its point and ray again + depth',
+                                        'its children\'s points and mask byte, the write pass\'s reads and 8 B per hit '
+                                        'child; per target hit its point and ray again + depth',
                          'survey_formula': {'bytes': survey_bytes,
                                             'achieved': round(survey_bytes / (ms * 1e-3) / 1e9, 1),
                                             'frac': round(survey_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}}
