@@ -19,6 +19,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <limits>
 #include <type_traits>
 
 namespace kl {
@@ -895,19 +896,36 @@ __global__ void __launch_bounds__(256) p2m_bwd_kernel(const T *__restrict__ grad
 // type), as the reference's scalar_t arithmetic does.
 constexpr int SD_TILE = 512;
 
+// The largest value of S: a split's starting best (no tile best exceeds it; NaN never replaces it)
+template <typename S>
+__device__ __forceinline__ S sd_top() {
+  if constexpr (std::is_same<S, __half>::value) return __float2half(INFINITY);
+  else if constexpr (std::is_floating_point<S>::value) return (S)INFINITY;
+  else return std::numeric_limits<S>::max();
+}
+
+// grid (point blocks, batch, splits): split z takes the 512-point tiles [z tps, (z + 1) tps) of p2.
+// Split 0 folds as the reference (its first tile unconditional, then strict '>'); a later split
+// starts from sd_top(), so it takes its first non-NaN tile best, and sided_combine_kernel folds the
+// splits' results in order with the reference's strict '>' -- the reference's fold over all tiles,
+// NaN tile bests included (a NaN best never replaces, and a first NaN tile stays).  With one split
+// (part == nullptr) the result goes straight to dist / idx.
 template <typename S>
 __global__ void __launch_bounds__(256) sided_fwd_kernel(const S *__restrict__ p1, const S *__restrict__ p2,
                                                          int64_t N, int64_t M, S *__restrict__ dist,
-                                                         int64_t *__restrict__ idx) {
+                                                         int64_t *__restrict__ idx, int64_t tps,
+                                                         S *__restrict__ part_d, int64_t *__restrict__ part_i) {
   __shared__ S buf[SD_TILE * 3];
   const int b = blockIdx.y;
   const int64_t n = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const bool valid = n < N;
   const S *a = p1 + ((int64_t)b * N + (valid ? n : 0)) * 3;
   const S x1 = a[0], y1 = a[1], z1 = a[2];
-  S best_all = S(0);
+  const bool first_split = blockIdx.z == 0;
+  S best_all = first_split ? S(0) : sd_top<S>();
   int64_t best_all_i = 0;
-  for (int64_t k2 = 0; k2 < M; k2 += SD_TILE) {
+  const int64_t kb = (int64_t)blockIdx.z * tps * SD_TILE, ke = min(M, kb + tps * SD_TILE);
+  for (int64_t k2 = kb; k2 < ke; k2 += SD_TILE) {
     const int end_k = (int)min((int64_t)SD_TILE, M - k2);
     __syncthreads();
     for (int t = threadIdx.x; t < end_k * 3; t += blockDim.x) buf[t] = p2[((int64_t)b * M + k2) * 3 + t];
@@ -924,14 +942,39 @@ __global__ void __launch_bounds__(256) sided_fwd_kernel(const S *__restrict__ p1
         best_i = k + k2;
       }
     }
-    if (k2 == 0 || best_all > best) {
+    if ((first_split && k2 == 0) || best_all > best) {
       best_all = best;
       best_all_i = best_i;
     }
   }
   if (!valid) return;
-  dist[(int64_t)b * N + n] = best_all;
-  idx[(int64_t)b * N + n] = best_all_i;
+  if (part_d) {
+    const int64_t o = ((int64_t)blockIdx.z * gridDim.y + b) * N + n;
+    part_d[o] = best_all;
+    part_i[o] = best_all_i;
+  } else {
+    dist[(int64_t)b * N + n] = best_all;
+    idx[(int64_t)b * N + n] = best_all_i;
+  }
+}
+
+template <typename S>
+__global__ void __launch_bounds__(256) sided_combine_kernel(int64_t BN, int splits, const S *__restrict__ part_d,
+                                                             const int64_t *__restrict__ part_i, S *__restrict__ dist,
+                                                             int64_t *__restrict__ idx) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (t >= BN) return;
+  S best = part_d[t];
+  int64_t bi = part_i[t];
+  for (int z = 1; z < splits; z++) {
+    const S d = part_d[(int64_t)z * BN + t];
+    if (best > d) {
+      best = d;
+      bi = part_i[(int64_t)z * BN + t];
+    }
+  }
+  dist[t] = best;
+  idx[t] = bi;
 }
 
 template <typename S>
@@ -1125,9 +1168,33 @@ static int sided_fwd(int B, int64_t N, int64_t M, const void *p1, const void *p2
                      hipStream_t st) {
   if (B == 0 || N == 0) return KL_OK;
   KL_REQUIRE(M > 0, "sided_distance_forward: p2 must not be empty");
-  hipLaunchKernelGGL(sided_fwd_kernel<S>, dim3((unsigned)cdiv(N, 256), B), dim3(256), 0, st, (const S *)p1,
-                     (const S *)p2, N, M, (S *)dist, idx);
+  // few point blocks (cfg1: 2,048 points, 8 workgroups): split p2's tiles over a third grid
+  // dimension so the chip fills, partials in a stream-ordered scratch, folded in split order
+  const int64_t pblocks = cdiv(N, 256) * B, tiles = cdiv(M, (int64_t)SD_TILE);
+  int splits = 1;
+  if (pblocks < 256 && tiles > 1 && g_dev_param[23] != 1)  // dev param 23 = 1: one split (A/B)
+    splits = (int)std::min<int64_t>(tiles, cdiv(512, pblocks));
+  const int64_t tps = cdiv(tiles, (int64_t)splits);
+  splits = (int)cdiv(tiles, tps);
+  if (splits == 1) {
+    hipLaunchKernelGGL(sided_fwd_kernel<S>, dim3((unsigned)cdiv(N, 256), B), dim3(256), 0, st, (const S *)p1,
+                       (const S *)p2, N, M, (S *)dist, idx, tps, (S *)nullptr, (int64_t *)nullptr);
+    KL_CHECK_LAUNCH();
+    return KL_OK;
+  }
+  const int64_t BN = (int64_t)B * N;
+  void *ws = nullptr;
+  const size_t db = (((size_t)splits * BN * sizeof(S)) + 255) & ~(size_t)255;
+  KL_CHECK_HIP(hipMallocAsync(&ws, db + (size_t)splits * BN * sizeof(int64_t), st));
+  S *pd = (S *)ws;
+  int64_t *pi = (int64_t *)((char *)ws + db);
+  hipLaunchKernelGGL(sided_fwd_kernel<S>, dim3((unsigned)cdiv(N, 256), B, splits), dim3(256), 0, st, (const S *)p1,
+                     (const S *)p2, N, M, (S *)dist, idx, tps, pd, pi);
   KL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sided_combine_kernel<S>, dim3((unsigned)cdiv(BN, 256)), dim3(256), 0, st, BN, splits,
+                     (const S *)pd, (const int64_t *)pi, (S *)dist, idx);
+  KL_CHECK_LAUNCH();
+  KL_CHECK_HIP(hipFreeAsync(ws, st));
   return KL_OK;
 }
 

@@ -991,6 +991,39 @@ def test_sided_kat_and_ties(kal, golden):
     np.testing.assert_allclose(A(d), g['large_dist'])
 
 
+@pytest.mark.parametrize('dtype', [torch.float16, torch.float32, torch.float64, torch.int32, torch.uint8])
+def test_sided_tile_splits_equal_one_pass(kal, dtype):
+    """sided_distance's forward with p2's 512-point tiles split over workgroups (default when the
+    point blocks are few) against one pass over all tiles (dev param 23 = 1): distances and indices
+    bit-equal, with duplicated p2 points across tiles (ties: the earliest index), NaN p2 points at
+    tile starts and inside tiles (f32), and p2 sizes not a multiple of 512; f32 also against the
+    oracle."""
+    rng = np.random.default_rng(7)
+    for (B, N, M) in ((1, 300, 2600), (2, 77, 1537), (1, 2048, 2048)):
+        p1 = rng.random((B, N, 3)) * 4
+        p2 = rng.random((B, M, 3)) * 4
+        p2[:, 1024:1100] = p2[:, 0:76]   # ties across tiles
+        p2[:, 1600:1612] = p2[:, 520:532]
+        if dtype.is_floating_point:
+            if dtype == torch.float32:
+                p2[0, 512] = np.nan      # a tile's first point
+                p2[0, 1030] = np.nan     # inside a tile
+        else:
+            p1, p2 = np.floor(p1 * 3), np.floor(p2 * 3)
+        a, b = T(p1, dtype), T(p2, dtype)
+        d, i = kal.metrics.pointcloud.sided_distance(a, b)
+        try:
+            _dev_param(23, 1)
+            d1, i1 = kal.metrics.pointcloud.sided_distance(a, b)
+        finally:
+            _dev_param(23, 0)
+        assert torch.equal(i, i1) and np.array_equal(A(d), A(d1), equal_nan=True), (B, N, M)
+        if dtype == torch.float32:
+            for k in range(B):
+                od, oi = orc.sided_distance_forward(A(a[k:k + 1]), A(b[k:k + 1]))
+                assert np.array_equal(A(d[k:k + 1]), od, equal_nan=True) and np.array_equal(A(i[k:k + 1]), oi)
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
 def test_sided_vs_oracle_and_grad(kal, golden, dtype):
     g = golden('sided.npz')
