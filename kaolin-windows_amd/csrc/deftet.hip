@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(kDtTile)
     deftet_fwd_kernel(int64_t F, int64_t P, int K, const T *__restrict__ fvz, const T *__restrict__ fvi,
                       const T *__restrict__ bboxes, const T *__restrict__ pix, const T *__restrict__ ranges,
                       float eps, int64_t *__restrict__ out_idx, T *__restrict__ out_depth, T *__restrict__ out_w0,
-                      T *__restrict__ out_w1, const T *__restrict__ tbox) {
+                      T *__restrict__ out_w1, const T *__restrict__ tbox, const int32_t *__restrict__ perm) {
   __shared__ T s_f[13][kDtTile];  // ax ay bx by cx cy az bz cz xmin ymin xmax ymax
   __shared__ int s_id[kDtTile];
   __shared__ int s_tiles[kDtTile];
@@ -131,8 +131,12 @@ __global__ void __launch_bounds__(kDtTile)
 
   const int tid = threadIdx.x;
   const int64_t b = blockIdx.y;
-  const int64_t p = (int64_t)blockIdx.x * kDtTile + tid;
-  const bool active = p < P;
+  const int64_t slot = (int64_t)blockIdx.x * kDtTile + tid;
+  const bool active = slot < P;
+  // perm (r05): the view's pixels in a spatial (Morton) order, so that a workgroup's 256 pixels form
+  // a compact screen box instead of half an image row (each pixel's result is its own: the order
+  // changes only which faces a workgroup keeps)
+  const int64_t p = perm && active ? (int64_t)perm[b * P + slot] : slot;
   const int64_t prow = b * P + p;
 
   T x0 = 0, y0 = 0, lo = 0, hi = 0;
@@ -762,6 +766,93 @@ static int dt_grid_dim(int64_t F) {  // ~4 faces per cell per layer
 }
 // forward workspace: tile boxes, then (binned path) mesh boxes, per-face counts / offsets,
 // per-cell counts / offsets and the scan scratch
+// ---- pixel order of the tile walk (r05): per view, the finite pixels' box; each pixel's key is its
+// view over a 20-bit Morton code of its position quantised to 1,024 x 1,024 cells of that box
+// (non-finite pixels last); one radix sort of (key, pixel).
+template <typename T>
+__global__ void __launch_bounds__(1024) deftet_pixbox_kernel(int64_t P, const T *__restrict__ pix,
+                                                             float *__restrict__ pbox) {
+  __shared__ float s_r[4][16];
+  const int64_t b = blockIdx.x;
+  float r[4] = {INFINITY, INFINITY, -INFINITY, -INFINITY};
+  for (int64_t p = threadIdx.x; p < P; p += blockDim.x) {
+    const float x = (float)pix[(b * P + p) * 2], y = (float)pix[(b * P + p) * 2 + 1];
+    if (isfinite(x) && isfinite(y)) {
+      r[0] = fminf(r[0], x); r[1] = fminf(r[1], y); r[2] = fmaxf(r[2], x); r[3] = fmaxf(r[3], y);
+    }
+  }
+  r[0] = wave_min(r[0]); r[1] = wave_min(r[1]); r[2] = wave_max(r[2]); r[3] = wave_max(r[3]);
+  if ((threadIdx.x & 63) == 0)
+    for (int k = 0; k < 4; k++) s_r[k][threadIdx.x >> 6] = r[k];
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const int k = threadIdx.x;
+    float v = s_r[k][0];
+    for (int w = 1; w < 16; w++) v = k < 2 ? fminf(v, s_r[k][w]) : fmaxf(v, s_r[k][w]);
+    pbox[b * 4 + k] = v;
+  }
+}
+
+__device__ __forceinline__ uint32_t dt_spread10(uint32_t v) {  // 10 bits -> every other bit of 20
+  v &= 0x3ffu;
+  v = (v | (v << 8)) & 0x00ff00ffu;
+  v = (v | (v << 4)) & 0x0f0f0f0fu;
+  v = (v | (v << 2)) & 0x33333333u;
+  v = (v | (v << 1)) & 0x55555555u;
+  return v;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) deftet_pixkey_kernel(int64_t B, int64_t P, const T *__restrict__ pix,
+                                                            const float *__restrict__ pbox, uint64_t *__restrict__ keys,
+                                                            int32_t *__restrict__ vals) {
+  const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+  if (i >= B * P) return;
+  const int64_t b = i / P;
+  const float x = (float)pix[i * 2], y = (float)pix[i * 2 + 1];
+  uint32_t m = 0xfffffu;
+  if (isfinite(x) && isfinite(y)) {
+    const float *bx = pbox + b * 4;
+    const float sx = bx[2] > bx[0] ? 1023.0f / (bx[2] - bx[0]) : 0.0f, sy = bx[3] > bx[1] ? 1023.0f / (bx[3] - bx[1]) : 0.0f;
+    const uint32_t qx = (uint32_t)fminf(fmaxf((x - bx[0]) * sx, 0.0f), 1023.0f);
+    const uint32_t qy = (uint32_t)fminf(fmaxf((y - bx[1]) * sy, 0.0f), 1023.0f);
+    m = dt_spread10(qx) | (dt_spread10(qy) << 1);
+  }
+  keys[i] = ((uint64_t)b << 20) | m;
+  vals[i] = (int32_t)(i - b * P);
+}
+
+// the permutation (B*P int32, in scratch from hipMallocAsync), or nullptr when not worth it
+template <typename T>
+static int dt_pixel_order(int64_t B, int64_t P, const void *pix, int32_t **perm, void **scratch, hipStream_t st) {
+  *perm = nullptr;
+  *scratch = nullptr;
+  const int64_t n = B * P;
+  if (P < 4 * kDtTile || n >= ((int64_t)1 << 31) || g_dev_param[24] == 1) return KL_OK;  // dev param 24 = 1: off
+  int bits = 20;
+  while (bits < 64 && ((int64_t)1 << (bits - 20)) < B) bits++;
+  size_t tb = 0;
+  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, (const uint64_t *)nullptr, (uint64_t *)nullptr,
+                                                  (const int32_t *)nullptr, (int32_t *)nullptr, (int)n, 0, bits, st));
+  const size_t kb = dt_falign((size_t)n * 8), vb = dt_falign((size_t)n * 4), pb = dt_falign((size_t)B * 16);
+  void *w = nullptr;
+  KL_CHECK_HIP(hipMallocAsync(&w, 2 * kb + 2 * vb + pb + dt_falign(tb > 0 ? tb : 1), st));
+  uint8_t *c = (uint8_t *)w;
+  uint64_t *kin = (uint64_t *)c, *kout = (uint64_t *)(c + kb);
+  int32_t *vin = (int32_t *)(c + 2 * kb), *vout = (int32_t *)(c + 2 * kb + vb);
+  float *pbox = (float *)(c + 2 * kb + 2 * vb);
+  void *temp = c + 2 * kb + 2 * vb + pb;
+  hipLaunchKernelGGL(deftet_pixbox_kernel<T>, dim3((unsigned)B), dim3(1024), 0, st, P, (const T *)pix, pbox);
+  KL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(deftet_pixkey_kernel<T>, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, B, P, (const T *)pix,
+                     (const float *)pbox, kin, vin);
+  KL_CHECK_LAUNCH();
+  KL_CHECK_HIP(hipcub::DeviceRadixSort::SortPairs(temp, tb, kin, kout, vin, vout, (int)n, 0, bits, st));
+  *perm = vout;
+  *scratch = w;
+  return KL_OK;
+}
+
 struct DtFwdWs {
   size_t tbox, mbox, mscale, ctl, fcnt, foff, ccnt, coff, temp, temp_bytes, total;
   int G;
@@ -878,10 +969,14 @@ static int deftet_forward(int64_t B, int64_t F, int64_t P, int64_t K, const void
                                             (uint8_t *)ws, alloc, alloc_ctx, st, &too_long);
     if (rc || !too_long) return rc;
   }
+  int32_t *perm = nullptr;
+  void *scratch = nullptr;
+  KL_CHECK_RC(dt_pixel_order<T>(B, P, pix, &perm, &scratch, st));
   hipLaunchKernelGGL(deftet_fwd_kernel<T>, dim3((unsigned)cdiv(P, kDtTile), (unsigned)B), dim3(kDtTile), 0, st, F, P,
                      (int)K, (const T *)fvz, (const T *)fvi, (const T *)bboxes, (const T *)pix, (const T *)ranges, eps,
-                     idx, (T *)depth, (T *)w0, (T *)w1, (const T *)ws);
+                     idx, (T *)depth, (T *)w0, (T *)w1, (const T *)ws, (const int32_t *)perm);
   KL_CHECK_LAUNCH();
+  if (scratch) KL_CHECK_HIP(hipFreeAsync(scratch, st));
   return KL_OK;
 }
 

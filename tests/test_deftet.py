@@ -276,3 +276,32 @@ def test_gpu_binned_list_cap_falls_back_to_tile_walk(kal):
     ref = orc.deftet_sparse_render_forward(fvz, fvi, None, pix, ranges, K, 1e-8)
     for x, r in zip(a, ref):
         np.testing.assert_array_equal(_A(x), r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('order', ['grid', 'shuffled'])
+def test_gpu_tile_walk_pixel_order(kal, order):
+    """The tile walk visits the pixels in a spatial (Morton) order when there are enough of them
+    (r05; dev param 24 = 1 keeps the given order): the same slots either way, equal to the oracle,
+    with pixels in image order or shuffled, non-finite pixels and a second view."""
+    import ctypes
+    pix, ranges, fvz, fvi, feat, K = _grid_case(np.float32, B=2, F=1500, H=40, W=36, seed=11)
+    pix = pix.copy()
+    if order == 'shuffled':
+        perm = np.random.default_rng(3).permutation(pix.shape[1])
+        pix, ranges = pix[:, perm], ranges[:, perm]
+    pix[0, 17] = np.nan
+    pix[1, 100, 0] = np.inf
+    args = [_T(fvz), _T(fvi), None, _T(pix), _T(ranges), K, 1e-8]
+    lib = kal._native.lib()
+    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
+    a = kal._C.deftet_forward('deftet', *args, binned=False)
+    lib.kl_dev_set_param(24, 1)
+    try:
+        b = kal._C.deftet_forward('deftet', *args, binned=False)
+    finally:
+        lib.kl_dev_set_param(24, 0)
+    ref = orc.deftet_sparse_render_forward(fvz, fvi, None, pix, ranges, K, 1e-8)
+    for x, y, r in zip(a, b, ref):
+        np.testing.assert_array_equal(_A(x), _A(y))
+        np.testing.assert_array_equal(_A(x), r)
