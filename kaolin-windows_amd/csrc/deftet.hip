@@ -768,7 +768,9 @@ static int dt_grid_dim(int64_t F) {  // ~4 faces per cell per layer
 // per-cell counts / offsets and the scan scratch
 // ---- pixel order of the tile walk (r05): per view, the finite pixels' box; each pixel's key is its
 // view over a 20-bit Morton code of its position quantised to 1,024 x 1,024 cells of that box
-// (non-finite pixels last); one radix sort of (key, pixel).
+// (non-finite pixels last); one radix sort of (key, pixel). Measured r05t (cfg of bench_deftet): the walk
+// itself 526 vs 557 us, but the box + sort cost more than that saves, so the order is off by default
+// (dev param 24 = 1 turns it on).
 template <typename T>
 __global__ void __launch_bounds__(1024) deftet_pixbox_kernel(int64_t P, const T *__restrict__ pix,
                                                              float *__restrict__ pbox) {
@@ -828,7 +830,7 @@ static int dt_pixel_order(int64_t B, int64_t P, const void *pix, int32_t **perm,
   *perm = nullptr;
   *scratch = nullptr;
   const int64_t n = B * P;
-  if (P < 4 * kDtTile || n >= ((int64_t)1 << 31) || g_dev_param[24] == 1) return KL_OK;  // dev param 24 = 1: off
+  if (P < 4 * kDtTile || n >= ((int64_t)1 << 31) || g_dev_param[24] != 1) return KL_OK;  // dev param 24 = 1: on
   int bits = 20;
   while (bits < 64 && ((int64_t)1 << (bits - 20)) < B) bits++;
   size_t tb = 0;

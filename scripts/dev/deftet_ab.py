@@ -1,5 +1,5 @@
 """A/B of the deftet tile-walk forward on the bench workload (4 views x 512^2, 50k faces, knum 8):
-pixels in a Morton order (default) against the given image order (dev param 24 = 1); equality of
+pixels in the given image order (default) against a Morton order (dev param 24 = 1); equality of
 the slots (development aid)."""
 import ctypes
 import os

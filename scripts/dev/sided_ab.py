@@ -8,6 +8,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'kaolin-windows_amd'))
 import kaolin as kal  # noqa: E402
 from kaolin import _native as N  # noqa: E402
 

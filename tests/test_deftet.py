@@ -281,8 +281,8 @@ def test_gpu_binned_list_cap_falls_back_to_tile_walk(kal):
 @pytest.mark.gpu
 @pytest.mark.parametrize('order', ['grid', 'shuffled'])
 def test_gpu_tile_walk_pixel_order(kal, order):
-    """The tile walk visits the pixels in a spatial (Morton) order when there are enough of them
-    (r05; dev param 24 = 1 keeps the given order): the same slots either way, equal to the oracle,
+    """With dev param 24 = 1 the tile walk visits the pixels in a spatial (Morton) order when there
+    are enough of them (r05; off by default, it did not pay): the same slots either way, equal to the oracle,
     with pixels in image order or shuffled, non-finite pixels and a second view."""
     import ctypes
     pix, ranges, fvz, fvi, feat, K = _grid_case(np.float32, B=2, F=1500, H=40, W=36, seed=11)
