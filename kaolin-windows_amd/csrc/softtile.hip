@@ -75,6 +75,12 @@ struct SoftTileArgs {
 
 // The workgroup's face list: the candidate chunks' faces touching its rows, in index order
 // (face id; lane interval lo | hi << 6 and row bits << 12), refilled when full.
+#ifndef ST_EVAL_U
+#define ST_EVAL_U 4  // hits in flight per lane in the f32 evaluation (A/B builds: EXTRA=-DST_EVAL_U=2)
+#endif
+#ifndef ST_FWD_MIN_WAVES
+#define ST_FWD_MIN_WAVES 1  // the forward kernel's minimum waves per SIMD (A/B builds)
+#endif
 constexpr int ST_LIST_CAP = 960;  // (40.6 KB of LDS at knum 30 with 4 rows: 4 workgroups per CU)
 // list | per-wave scratch (16 ints) | the multi-wave walk's per-round counts ([Q][64] per row)
 constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int) + ST_WAVES * 64 * sizeof(int); }
@@ -82,7 +88,7 @@ constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(in
 // Forward, one work item (a part of a tile's rows) per 4-wave workgroup: fill and walk (1a,
 // 1b below), the dense evaluation by the row's Q waves, the mask by its first wave.
 template <typename T>
-__global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
+__global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   if ((int)blockIdx.x >= *a.nitems) return;
   uint64_t *const dbg = kDevStamps ? a.dbg : nullptr;  // compiled out unless KL_DEV_STAMPS
@@ -341,7 +347,7 @@ __global__ void __launch_bounds__(256) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
     const int all = rpre[8];
     const float m = a.m;
     const float sx = m / (float)W, sy = m / (float)H;
-    constexpr int U = 4;
+    constexpr int U = ST_EVAL_U;
     constexpr int S = 64 * ST_WAVES;
     for (int e0 = (int)threadIdx.x; e0 < all; e0 += S * U) {
       int pp[U], kk[U], rr[U], ee[U];

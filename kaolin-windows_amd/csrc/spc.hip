@@ -1867,22 +1867,35 @@ __global__ void __launch_bounds__(RTH_TILE) rth_count_kernel(RayIn in, const uin
   }
 }
 
-// One workgroup: the exclusive scan of the tile totals tsum[0, cdiv(*dnum, RTH_TILE)) in place.
+// One workgroup: the exclusive scan of the tile totals tsum[0, cdiv(*dnum, RTH_TILE)) in place, eight
+// per thread (their loads in flight together: one pass up to 8,192 tiles).
 // The total: > cap sets result[1]; with `next`, *next = min(total, cap) (the next list's count) and
-// at the last level result[0] = it.
+// at the last level result[0] = it.  zero (fixed mode): the next list's candidate tile totals, zeroed
+// here for the write pass to add into.
+constexpr int RTH_OFF_PT = 8;
 __global__ void __launch_bounds__(1024) rth_offsets_kernel(uint32_t *__restrict__ tsum, const uint32_t *__restrict__ dnum,
                                                            uint32_t *__restrict__ next, uint32_t cap,
-                                                           int64_t *__restrict__ result, int last) {
+                                                           int64_t *__restrict__ result, int last,
+                                                           uint32_t *__restrict__ zero) {
   __shared__ int s_wave[16];
   const int64_t n = *dnum;
   const int nt = (int)((n + RTH_TILE - 1) / RTH_TILE);
   uint32_t carry = 0;
-  for (int b0 = 0; b0 < nt; b0 += 1024) {
-    const int i = b0 + threadIdx.x;
-    const int v = i < nt ? (int)tsum[i] : 0;
+  for (int b0 = 0; b0 < nt; b0 += 1024 * RTH_OFF_PT) {
+    const int i0 = b0 + (int)threadIdx.x * RTH_OFF_PT;
+    uint32_t v[RTH_OFF_PT], sum = 0;
+#pragma unroll
+    for (int k = 0; k < RTH_OFF_PT; k++) {
+      v[k] = i0 + k < nt ? tsum[i0 + k] : 0u;
+      sum += v[k];
+    }
     int tot = 0;
-    const int ex = block_exclusive_scan(v, s_wave, &tot);
-    if (i < nt) tsum[i] = carry + (uint32_t)ex;
+    uint32_t ex = carry + (uint32_t)block_exclusive_scan((int)sum, s_wave, &tot);
+#pragma unroll
+    for (int k = 0; k < RTH_OFF_PT; k++) {
+      if (i0 + k < nt) tsum[i0 + k] = ex;
+      ex += v[k];
+    }
     carry += (uint32_t)tot;
   }
   if (threadIdx.x == 0) {
@@ -1892,6 +1905,11 @@ __global__ void __launch_bounds__(1024) rth_offsets_kernel(uint32_t *__restrict_
       *next = c;
       if (last) result[0] = c;
     }
+  }
+  if (zero) {
+    const uint32_t c = carry < cap ? carry : cap;
+    const int nz = (int)((c + RTH_TILE - 1) / RTH_TILE);
+    for (int i = threadIdx.x; i < nz; i += blockDim.x) zero[i] = 0u;
   }
 }
 
@@ -1910,65 +1928,95 @@ __global__ void __launch_bounds__(RTH_TILE) rth_pcsum_kernel(const uint32_t *__r
 
 // write pass: node i's hit children at toff[t] + (its tile's exclusive scan of the hit counts), in
 // front-to-back order; at the target level with depths.  pc_out (fixed mode, not the last level):
-// each listed child's own child count.
+// each listed child's own child count, and pc_ts (zeroed by the offsets pass) the next list's tile
+// totals of them -- summed per tile in LDS (a tile's outputs [t0, t0 + tot), tot <= 8 * RTH_TILE,
+// meet at most RTH_PTS of the next list's tiles), one global atomic per (tile, next tile).
+constexpr int RTH_PTS = 10;
 __global__ void __launch_bounds__(RTH_TILE) rth_write_kernel(RayIn in, const uint32_t *__restrict__ dnum,
                                                              const int2 *__restrict__ list, uint32_t level,
                                                              uint32_t target_level, int with_depth, int with_exit,
                                                              const uint8_t *__restrict__ hmask,
                                                              const uint32_t *__restrict__ toff, uint32_t cap,
                                                              int2 *__restrict__ nout, float *__restrict__ dout,
-                                                             uint32_t *__restrict__ pc_out) {
+                                                             uint32_t *__restrict__ pc_out, uint32_t *__restrict__ pc_ts) {
   __shared__ int s_wave[RTH_TILE / 64];
+  __shared__ uint32_t s_pts[RTH_PTS];
   const int64_t num = *dnum;
   const int dd = with_exit ? 2 : 1;
-  for (int64_t t = blockIdx.x; t * RTH_TILE < num; t += gridDim.x) {
+  for (int64_t t = blockIdx.x; t * RTH_TILE < num; t += gridDim.x) {  // workgroup-uniform
     const int64_t i = t * RTH_TILE + threadIdx.x;
     const uint32_t m = i < num ? hmask[i] : 0u;
+    if (pc_ts && threadIdx.x < RTH_PTS) s_pts[threadIdx.x] = 0u;  // (ordered by the scan's barriers)
+    const uint32_t t0 = toff[t], tile0 = t0 / RTH_TILE;
     int tot;
-    uint32_t base = toff[t] + (uint32_t)block_exclusive_scan(__popc(m), s_wave, &tot);
-    if (!m) continue;
-    int ridx, pidx;
-    rth_node(list, i, ridx, pidx);
-    const uint32_t ob = in.octree[pidx];
-    const int32_t s = in.exsum[pidx];
-    const int16_t *p = in.points + (int64_t)pidx * 3;
-    const float *org = in.ro + (int64_t)ridx * 3;
-    const float scale = (float)(1.0 / (double)(float)(1u << level));
-    const float x = (float)((double)(0.5f * org[0] + 0.5f) - (double)scale * ((double)(float)p[0] + 0.5));
-    const float y = (float)((double)(0.5f * org[1] + 0.5f) - (double)scale * ((double)(float)p[1] + 0.5));
-    const float z = (float)((double)(0.5f * org[2] + 0.5f) - (double)scale * ((double)(float)p[2] + 0.5));
-    const uint32_t perm = c_rt_perm[(x > 0 ? 4u : 0u) + (y > 0 ? 2u : 0u) + (z > 0 ? 1u : 0u)];
-    const uint32_t lc = level + 1;
-    const bool depth_out = dout != nullptr && with_depth && lc == target_level;
+    uint32_t base = t0 + (uint32_t)block_exclusive_scan(__popc(m), s_wave, &tot);
+    if (m) {
+      int ridx, pidx;
+      rth_node(list, i, ridx, pidx);
+      const uint32_t ob = in.octree[pidx];
+      const int32_t s = in.exsum[pidx];
+      const int16_t *p = in.points + (int64_t)pidx * 3;
+      const float *org = in.ro + (int64_t)ridx * 3;
+      const float scale = (float)(1.0 / (double)(float)(1u << level));
+      const float x = (float)((double)(0.5f * org[0] + 0.5f) - (double)scale * ((double)(float)p[0] + 0.5));
+      const float y = (float)((double)(0.5f * org[1] + 0.5f) - (double)scale * ((double)(float)p[1] + 0.5));
+      const float z = (float)((double)(0.5f * org[2] + 0.5f) - (double)scale * ((double)(float)p[2] + 0.5));
+      const uint32_t perm = c_rt_perm[(x > 0 ? 4u : 0u) + (y > 0 ? 2u : 0u) + (z > 0 ? 1u : 0u)];
+      const uint32_t lc = level + 1;
+      const bool depth_out = dout != nullptr && with_depth && lc == target_level;
 #pragma unroll
-    for (int q = 0; q < 8; q++) {  // front to back: the code's permutation of the child indices
-      const uint32_t j = (perm >> (4 * q)) & 15u;
-      if (!(ob & (1u << j))) continue;
-      const int c = __popc(ob & ((2u << j) - 1));  // 1..popc: the child's rank among the node's children
-      if (!((m >> (c - 1)) & 1u)) continue;
-      if (base < cap) {
-        nout[base] = make_int2(ridx, s + c);
-        if (pc_out) pc_out[base] = (uint32_t)__popc(in.octree[s + c]);
-        if (depth_out) {
-          const int16_t *cp = in.points + (int64_t)(s + c) * 3;
-          const float o[3] = {org[0], org[1], org[2]};
-          const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
-          const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f,
-                                signbit(d[2]) ? 1.0f : -1.0f};
-          const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
-          const float r = (float)(1.0 / (double)(float)(1u << lc));
-          const float vc[3] = {fmaf(r, fmaf(2.0f, (float)cp[0], 1.0f), -1.0f), fmaf(r, fmaf(2.0f, (float)cp[1], 1.0f), -1.0f),
-                               fmaf(r, fmaf(2.0f, (float)cp[2], 1.0f), -1.0f)};
-          dout[(int64_t)base * dd] = ray_aabb(o, d, inv, sgn, vc, r);
-          if (with_exit) {
-            const float xs[3] = {signbit(-d[0]) ? 1.0f : -1.0f, signbit(-d[1]) ? 1.0f : -1.0f,
-                                 signbit(-d[2]) ? 1.0f : -1.0f};
-            dout[(int64_t)base * dd + 1] = ray_aabb(o, d, inv, xs, vc, r);
+      for (int q = 0; q < 8; q++) {  // front to back: the code's permutation of the child indices
+        const uint32_t j = (perm >> (4 * q)) & 15u;
+        if (!(ob & (1u << j))) continue;
+        const int c = __popc(ob & ((2u << j) - 1));  // 1..popc: the child's rank among the node's children
+        if (!((m >> (c - 1)) & 1u)) continue;
+        if (base < cap) {
+          nout[base] = make_int2(ridx, s + c);
+          if (pc_out) {
+            const uint32_t pcv = (uint32_t)__popc(in.octree[s + c]);
+            pc_out[base] = pcv;
+            if (pc_ts) atomicAdd(&s_pts[base / RTH_TILE - tile0], pcv);
+          }
+          if (depth_out) {
+            const int16_t *cp = in.points + (int64_t)(s + c) * 3;
+            const float o[3] = {org[0], org[1], org[2]};
+            const float d[3] = {in.rd[ridx * 3], in.rd[ridx * 3 + 1], in.rd[ridx * 3 + 2]};
+            const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f,
+                                  signbit(d[2]) ? 1.0f : -1.0f};
+            const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
+            const float r = (float)(1.0 / (double)(float)(1u << lc));
+            const float vc[3] = {fmaf(r, fmaf(2.0f, (float)cp[0], 1.0f), -1.0f),
+                                 fmaf(r, fmaf(2.0f, (float)cp[1], 1.0f), -1.0f),
+                                 fmaf(r, fmaf(2.0f, (float)cp[2], 1.0f), -1.0f)};
+            dout[(int64_t)base * dd] = ray_aabb(o, d, inv, sgn, vc, r);
+            if (with_exit) {
+              const float xs[3] = {signbit(-d[0]) ? 1.0f : -1.0f, signbit(-d[1]) ? 1.0f : -1.0f,
+                                   signbit(-d[2]) ? 1.0f : -1.0f};
+              dout[(int64_t)base * dd + 1] = ray_aabb(o, d, inv, xs, vc, r);
+            }
           }
         }
+        base++;
       }
-      base++;
     }
+    if (pc_ts) {  // workgroup-uniform
+      __syncthreads();
+      if (threadIdx.x < RTH_PTS && s_pts[threadIdx.x]) atomicAdd(&pc_ts[tile0 + threadIdx.x], s_pts[threadIdx.x]);
+      __syncthreads();  // s_pts is reset by the next tile
+    }
+  }
+}
+
+// fixed mode, after the march: the rows past the result's count -- nuggets -1, depths 0 (the rows
+// below it are the march's own writes)
+__global__ void rth_tail_fill_kernel(const int64_t *__restrict__ result, int64_t capacity, int2 *__restrict__ nuggets,
+                                     float *__restrict__ depth, int dd) {
+  const int64_t r0 = result[0];
+  for (int64_t i = r0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < capacity;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    nuggets[i] = make_int2(-1, -1);
+    if (depth)
+      for (int k = 0; k < dd; k++) depth[i * dd + k] = 0.0f;
   }
 }
 
@@ -2019,13 +2067,17 @@ static int rth_levels(const RayIn &in, int64_t num_rays, uint32_t target_level, 
     const int last = l + 1 == target_level;
     const uint32_t *dcur = bf.dn + (l & 1);
     uint32_t *dnext = bf.dn + ((l + 1) & 1);
-    if (fixed) {  // candidate offsets (the level's candidate total past cap flags the truncation)
-      if (l > 0) {
+    // fixed mode: the candidate offsets (the level's candidate total past cap flags the truncation)
+    // from the candidate tile totals tsA -- level 0's by rth_root_kernel, later ones added by the
+    // previous write pass (dev param 25 = 1: a pass of their own, rth_pcsum_kernel)
+    const bool fold = g_dev_param[25] != 1;
+    if (fixed) {
+      if (l > 0 && !fold) {
         hipLaunchKernelGGL(rth_pcsum_kernel, dim3(g), dim3(RTH_TILE), 0, st, dcur, (const uint32_t *)bf.pc, bf.tsA);
         KL_CHECK_LAUNCH();
       }
       hipLaunchKernelGGL(rth_offsets_kernel, dim3(1), dim3(1024), 0, st, bf.tsA, dcur, (uint32_t *)nullptr,
-                         (uint32_t)cap, bf.result, 0);
+                         (uint32_t)cap, bf.result, 0, (uint32_t *)nullptr);
       KL_CHECK_LAUNCH();
     }
     hipLaunchKernelGGL(rth_count_kernel, dim3(g), dim3(RTH_TILE), 0, st, in, dcur, (const int2 *)cur, l, target_level,
@@ -2033,12 +2085,14 @@ static int rth_levels(const RayIn &in, int64_t num_rays, uint32_t target_level, 
                        fixed ? (const uint32_t *)bf.pc : (const uint32_t *)nullptr,
                        fixed ? (const uint32_t *)bf.tsA : (const uint32_t *)nullptr, (uint32_t)cap);
     KL_CHECK_LAUNCH();
+    const bool pc_next = fixed && !last;
     hipLaunchKernelGGL(rth_offsets_kernel, dim3(1), dim3(1024), 0, st, bf.tsB, dcur, dnext, (uint32_t)cap, bf.result,
-                       last);
+                       last, pc_next && fold ? bf.tsA : (uint32_t *)nullptr);
     KL_CHECK_LAUNCH();
     hipLaunchKernelGGL(rth_write_kernel, dim3(g), dim3(RTH_TILE), 0, st, in, dcur, (const int2 *)cur, l, target_level,
                        return_depth, with_exit, (const uint8_t *)bf.hm, (const uint32_t *)bf.tsB, (uint32_t)cap,
-                       last ? out : nxt, last ? dout : nullptr, fixed && !last ? bf.pc : (uint32_t *)nullptr);
+                       last ? out : nxt, last ? dout : nullptr, pc_next ? bf.pc : (uint32_t *)nullptr,
+                       pc_next && fold ? bf.tsA : (uint32_t *)nullptr);
     KL_CHECK_LAUNCH();
     std::swap(cur, nxt);
   }
@@ -2585,7 +2639,11 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
   int2 *n0 = (int2 *)(w + L.a), *n1 = (int2 *)(w + L.b);
   uint32_t *info = (uint32_t *)(w + L.info), *psum = (uint32_t *)(w + L.psum), *dnum = (uint32_t *)(w + L.dnum);
   float *d0 = return_depth ? (float *)(w + L.dtmp) : nullptr;
-  if (capacity > 0) {
+  // the hit-list march (default) fills the rows past its count afterwards (dev param 25 = 1: all rows
+  // first, as the other marches do)
+  const bool hitlist = g_dev_param[15] != 2 && g_dev_param[15] != 3 && target_level > 0 && num_rays > 0;
+  const bool tail_fill = hitlist && g_dev_param[25] != 1;
+  if (capacity > 0 && !tail_fill) {
     KL_CHECK_RC(fill_async(nuggets, 0xff, (size_t)capacity * 2 * 4, st));
     if (return_depth) KL_CHECK_RC(fill_async(depth, 0, (size_t)capacity * dd * 4, st));
   }
@@ -2603,7 +2661,7 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
   }
   // default: the hit-list march with the per-level march's truncation (rth_count_kernel's fixed
   // mode); dev param 15 = 2: the per-level march below
-  if (g_dev_param[15] != 2 && target_level > 0 && num_rays > 0 && capacity > 0) {
+  if (hitlist && capacity > 0) {
     RthBufs bf{};
     bf.a = n0;
     bf.b = n1;
@@ -2616,8 +2674,14 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
     hipLaunchKernelGGL(rth_init_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, num_rays, n0, dnum,
                        result);
     KL_CHECK_LAUNCH();
-    return rth_levels(in, num_rays, target_level, return_depth, with_exit, capacity, true, bf, (int2 *)nuggets,
-                      return_depth ? depth : nullptr, st);
+    KL_CHECK_RC(rth_levels(in, num_rays, target_level, return_depth, with_exit, capacity, true, bf, (int2 *)nuggets,
+                           return_depth ? depth : nullptr, st));
+    if (tail_fill) {
+      hipLaunchKernelGGL(rth_tail_fill_kernel, dim3((unsigned)std::min<int64_t>(cdiv(capacity, 256), 2048)), dim3(256), 0,
+                         st, (const int64_t *)result, capacity, (int2 *)nuggets, return_depth ? depth : nullptr, dd);
+      KL_CHECK_LAUNCH();
+    }
+    return KL_OK;
   }
   hipLaunchKernelGGL(rt_init_kernel, dim3((unsigned)cdiv(std::max<int64_t>(num_rays, 1), 256)), dim3(256), 0, st,
                      num_rays, n0, dnum, result);

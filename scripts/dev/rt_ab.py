@@ -1,6 +1,8 @@
-"""A/B of the raytrace marches on the bench's cfg4 SPC (development aid): the per-level march
-(default), the fused level march (dev param 15 = 3) and the depth-first march (4, host-sized entry
-only), host-sized and fixed-capacity, wall clock per call, and equality of the answers."""
+"""A/B of the raytrace marches on the bench's cfg4 SPC (development aid): the hit-list march
+(default, 0), the per-level march (dev param 15 = 2), the fused level march (3) and the depth-first
+march (4, host-sized entry only), host-sized and fixed-capacity, wall clock per call, and equality
+of the answers; then the hit-list march with dev param 25 = 1 (candidate tile totals in a pass of
+their own, all rows filled first) against the default."""
 import ctypes
 import os
 import sys
@@ -41,8 +43,9 @@ def main():
     d = tgt.reshape(-1, 3) - o
     d = (d / d.norm(dim=-1, keepdim=True)).contiguous()
     res = {}
-    for mode in (0, 2, 3, 4):
-        lib.kl_dev_set_param(15, mode)
+    for mode in (0, 2, 3, 4, 25):
+        lib.kl_dev_set_param(15, 0 if mode == 25 else mode)
+        lib.kl_dev_set_param(25, 1 if mode == 25 else 0)
         rt = lambda: kal.render.spc.unbatched_raytrace(octree, pts, pyr[0], exsum, o, d, L)  # noqa: E731
         out = rt()
         ms = wall(rt)
@@ -53,7 +56,8 @@ def main():
         res[mode] = (out, fo)
         print(f'mode {mode}: host-sized {ms:.3f} ms, fixed {msf:.3f} ms, hits {out[0].shape[0]}', flush=True)
     lib.kl_dev_set_param(15, 0)
-    for m in (0, 3, 4):
+    lib.kl_dev_set_param(25, 0)
+    for m in (0, 3, 4, 25):
         (a, fa), (b, fb) = res[m], res[2]
         print(f'mode {m} vs 2 equal host-sized:', all(torch.equal(x, y) for x, y in zip(a, b)))
         print(f'mode {m} vs 2 equal fixed:', all(torch.equal(x, y) for x, y in zip(fa, fb)))
