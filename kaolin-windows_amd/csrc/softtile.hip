@@ -76,7 +76,7 @@ struct SoftTileArgs {
 // The workgroup's face list: the candidate chunks' faces touching its rows, in index order
 // (face id; lane interval lo | hi << 6 and row bits << 12), refilled when full.
 #ifndef ST_EVAL_U
-#define ST_EVAL_U 4  // hits in flight per lane in the f32 evaluation (A/B builds: EXTRA=-DST_EVAL_U=2)
+#define ST_EVAL_U 2  // hits in flight per lane in the f32 evaluation: 89 VGPRs, 5 waves per SIMD (4: 115, 4)
 #endif
 #ifndef ST_FWD_MIN_WAVES
 #define ST_FWD_MIN_WAVES 1  // the forward kernel's minimum waves per SIMD (A/B builds)
@@ -785,8 +785,6 @@ struct StWs {
   }
 };
 
-// Fewest parts per tile (lp_min >= 1: at most 4 rows per workgroup) whose slot lists fit in
-// 64 KB of LDS (two workgroups per CU); knum near 255 takes one row per workgroup.
 SoftSplit soft_split() {
   SoftSplit sp = ST_SPLIT;
   if (g_dev_param[0]) sp.b4 = g_dev_param[0];
@@ -797,10 +795,14 @@ SoftSplit soft_split() {
 }
 
 int soft_lp_min(int K) {
+  // the fewest row halvings whose LDS lets five workgroups share a CU -- the forward kernel's VGPR
+  // occupancy (5 waves per SIMD at ST_EVAL_U = 2): at knum 30, 2-row items (24.7 KB) against 4-row
+  // ones (39.6 KB, four per CU): dibr_forward 98.3-99.1 against 103.1-103.8 us (r05u)
   int lp = 1;
-  while (lp < 3 && st_head_lds() + (size_t)(TILE_H >> lp) * st_row_lds(K) > 64 * 1024) lp++;
-  // dev param 20: at least this many row halvings (fewer rows per work item, less LDS per workgroup)
-  if (g_dev_param[20] > lp && g_dev_param[20] <= 3) lp = g_dev_param[20];
+  while (lp < 3 && st_head_lds() + (size_t)(TILE_H >> lp) * st_row_lds(K) > 32 * 1024) lp++;
+  // dev param 20 = 1..3: that many halvings where the LDS fits 64 KB (A/B)
+  const int dp = g_dev_param[20];
+  if (dp >= 1 && dp <= 3 && st_head_lds() + (size_t)(TILE_H >> dp) * st_row_lds(K) <= 64 * 1024) lp = dp;
   return lp;
 }
 

@@ -1737,18 +1737,26 @@ static int rt_fused_levels(const RayIn &in, int64_t num_rays, uint32_t target_le
 // ---- Hit-list level march (r05, the default of both entries): level l's list holds the nuggets
 // that HIT at level l (not the candidates).  Per level, one count pass decides every listed node's
 // children at l + 1 together (their points are contiguous: points[s + 1 .. s + popc]), leaving a
-// byte of hit children per node and each 256-node tile's total; one workgroup scans the tile totals;
-// the write pass re-scans its tile's counts locally and lists the hit children in front-to-back
-// order (rt_children's order) -- at the target level with their depths.  Against the per-level
-// march (decide every candidate, scan, then subdivide every hit into its untested children): the
+// byte of hit children per node; the write pass lists the hit children in front-to-back order
+// (rt_children's order) -- at the target level with their depths.  Against the per-level march
+// (decide every candidate, scan, then subdivide every hit into its untested children): the
 // candidates are never written or re-read, the ray is read once per hit node instead of once per
 // candidate, and no count goes back to the host until the end.
+// Each pass's workgroup takes a contiguous run of 256-node tiles (rth_span), so the list offsets
+// need only the workgroups' totals: each workgroup publishes its total (agent-scope store), and
+// the workgroup that finishes last (a ticket: MI355X_MICROARCH.md's hand-off -- vmcnt(0), barrier,
+// one agent-scope add; agent-scope loads) scans them for the next pass -- two launches per level.
 // Fixed-capacity mode (kl_raytrace_fixed): the per-level march keeps each level's first `cap`
 // candidates (a hit node's children, untested) and drops the rest with their subtrees; here a child
-// is kept when its candidate index -- the node's candidate base (a scan of the listed nodes' child
-// counts `pc`, written by the previous write pass) plus its front-to-back rank -- is below `cap`,
-// so the lists are exactly the hits among the per-level march's kept candidates.
-constexpr int RTH_TILE = 256;  // nodes per tile = threads per workgroup
+// is kept when its candidate index -- the node's candidate base (the listed nodes' child counts
+// `pc` summed over the list before it) plus its front-to-back rank -- is below `cap`, so the lists
+// are exactly the hits among the per-level march's kept candidates.  The candidate bases' workgroup
+// totals are added up by the previous write pass (per next-list workgroup) and scanned by its last
+// workgroup (level 0: rth_root_kernel).
+constexpr int RTH_TILE = 256;      // nodes per tile = threads per workgroup
+constexpr int RTH_SCAN_PT = 8;     // the last workgroup's scan: 8 totals per thread, 2,048 workgroups
+constexpr int RTH_PW = 32;         // the write pass's LDS sums of the next list's workgroup totals
+static_assert(RTF_GRID <= RTH_TILE * RTH_SCAN_PT, "one pass of the last workgroup's scan");
 
 __device__ __forceinline__ void rth_node(const int2 *__restrict__ list, int64_t i, int &ridx, int &pidx) {
   const int2 nu = list[i];
@@ -1780,27 +1788,129 @@ __device__ __forceinline__ uint32_t rth_fb_ranks(const RayIn &in, int ridx, int 
   return ranks;
 }
 
+// this workgroup's tiles [t0, t1) of a list of n nodes: contiguous runs, balanced (every workgroup
+// of the grid gets floor or ceil of tiles / grid, so all of them are in flight; the grid is a power
+// of two); rth_owner inverts it
+__device__ __forceinline__ int64_t rth_tile0(int64_t w, int64_t nt) {  // workgroup w's first tile
+  return (w * nt) >> __builtin_ctz(gridDim.x);
+}
+__device__ __forceinline__ void rth_span(int64_t n, int64_t &t0, int64_t &t1) {
+  const int64_t nt = (n + RTH_TILE - 1) / RTH_TILE;
+  t0 = rth_tile0(blockIdx.x, nt);
+  t1 = rth_tile0((int64_t)blockIdx.x + 1, nt);
+}
+// the workgroup whose run holds tile T of a list of nt tiles
+__device__ __forceinline__ uint32_t rth_owner(int64_t T, int64_t nt) {
+  const int64_t G = gridDim.x;
+  return (uint32_t)((T * G + G - 1) / nt);
+}
+
+// 64-bit exclusive scan over the RTH_TILE threads; *total = the sum
+__device__ __forceinline__ uint64_t rth_scan64(uint64_t v, uint64_t *s_w, uint64_t *total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) s_w[wid] = inc;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < RTH_TILE / 64; w++) {
+    const uint64_t t = s_w[w];
+    before += w < wid ? t : 0;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + inc - v;
+}
+
+// The hand-off: every workgroup's published values are complete (vmcnt(0)) before its barrier and
+// its agent-scope add on a ticket; the workgroup that takes the last ticket returns true.  Two
+// levels of tickets, 128 B apart: one per group of RTH_TGROUP workgroups, then the groups' last
+// workgroups on the top ticket (2,048 adds on one address cost ~25 us per pass: measured r05w).
+// Each last taker re-zeroes its ticket for the next pass (every add on it has been made).
+// tk: RTH_TICKETS tickets at a stride of 32 words (the top one last).  Workgroup-uniform.
+constexpr int RTH_TGROUP = 32;
+constexpr int RTH_TICKETS = RTF_GRID / RTH_TGROUP + 1;
+__device__ __forceinline__ bool rth_last(unsigned *tk, int *s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned G = gridDim.x, grp = blockIdx.x / RTH_TGROUP;
+    const unsigned ng = (G + RTH_TGROUP - 1) / RTH_TGROUP;
+    const unsigned gsize = min((unsigned)RTH_TGROUP, G - grp * RTH_TGROUP);
+    unsigned *t1 = tk + grp * 32, *t2 = tk + (RTH_TICKETS - 1) * 32;
+    bool last = false;
+    if (__hip_atomic_fetch_add(t1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      __hip_atomic_store(t1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(t2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+      if (last) __hip_atomic_store(t2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *s_flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
+// The last workgroup: the exclusive scan of vals[0, gridDim.x) in place (agent-scope loads), each
+// prefix clamped to clampv (rows at or past `cap` are never written); returns the total.
+__device__ __forceinline__ uint64_t rth_scan_totals(uint32_t *vals, uint32_t clampv, uint64_t *s_w) {
+  const int G = (int)gridDim.x, i0 = (int)threadIdx.x * RTH_SCAN_PT;
+  uint32_t v[RTH_SCAN_PT];
+  uint64_t sum = 0;
+#pragma unroll
+  for (int k = 0; k < RTH_SCAN_PT; k++) {
+    v[k] = i0 + k < G ? __hip_atomic_load(vals + i0 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    sum += v[k];
+  }
+  uint64_t total;
+  uint64_t ex = rth_scan64(sum, s_w, &total);
+#pragma unroll
+  for (int k = 0; k < RTH_SCAN_PT; k++) {
+    if (i0 + k < G) vals[i0 + k] = (uint32_t)(ex < clampv ? ex : clampv);
+    ex += v[k];
+  }
+  return total;
+}
+
 // count pass: hmask[i] = the hit (fixed mode: and kept) children of listed node i in index order;
-// tsum[t] = their total over tile t.  root: level 0, the root's own test first (eager mode; in fixed
-// mode pc == 0 marks a missed root).  Fixed mode: cbt = the tiles' exclusive candidate offsets.
+// wsum[w] = their total over workgroup w's tiles.  root: level 0, the root's own test first (eager
+// mode; in fixed mode pc == 0 marks a missed root).  Fixed mode: cwoff = the workgroups' exclusive
+// candidate offsets.  The last workgroup scans wsum into the write pass's offsets; the total past
+// cap sets result[1]; *next = min(total, cap) (the next list's count), at the last level result[0]
+// = it; pcw_zero (fixed, not the last level): the next candidate totals, zeroed for the write pass.
 __global__ void __launch_bounds__(RTH_TILE) rth_count_kernel(RayIn in, const uint32_t *__restrict__ dnum,
                                                              const int2 *__restrict__ list, uint32_t level,
                                                              uint32_t target_level, int root, int with_depth,
                                                              int with_exit, uint8_t *__restrict__ hmask,
-                                                             uint32_t *__restrict__ tsum, const uint32_t *__restrict__ pc,
-                                                             const uint32_t *__restrict__ cbt, uint32_t cap) {
+                                                             uint32_t *__restrict__ wsum, const uint32_t *__restrict__ pc,
+                                                             const uint32_t *__restrict__ cwoff, uint32_t cap,
+                                                             unsigned *__restrict__ ticket, uint32_t *__restrict__ next,
+                                                             int64_t *__restrict__ result, int last,
+                                                             uint32_t *__restrict__ pcw_zero) {
   __shared__ int s_wave[RTH_TILE / 64];
+  __shared__ uint64_t s_w64[RTH_TILE / 64];
+  __shared__ int s_flag;
   const int64_t num = *dnum;
-  for (int64_t t = blockIdx.x; t * RTH_TILE < num; t += gridDim.x) {  // workgroup-uniform
+  int64_t t0, t1;
+  rth_span(num, t0, t1);
+  uint32_t wt = 0;                                     // the workgroup's hit children
+  uint32_t cb_run = cwoff ? cwoff[blockIdx.x] : 0u;    // (fixed) the candidate base of its next tile
+  for (int64_t t = t0; t < t1; t++) {  // workgroup-uniform
     const int64_t i = t * RTH_TILE + threadIdx.x;
     const bool in_list = i < num;
     uint32_t cb = 0;
-    if (cbt) {  // the node's candidate base: the tile's offset + the scan of pc within the tile
+    if (cwoff) {  // the node's candidate base: the tile's base + the scan of pc within the tile
       int tot;
-      cb = cbt[t] + (uint32_t)block_exclusive_scan(in_list ? (int)pc[i] : 0, s_wave, &tot);
+      cb = cb_run + (uint32_t)block_exclusive_scan(in_list ? (int)pc[i] : 0, s_wave, &tot);
+      cb_run += (uint32_t)tot;
     }
     uint32_t m = 0;
-    if (in_list && !(cbt && pc[i] == 0)) {
+    if (in_list && !(cwoff && pc[i] == 0)) {
       int ridx, pidx;
       rth_node(list, i, ridx, pidx);
       const float o[3] = {in.ro[ridx * 3], in.ro[ridx * 3 + 1], in.ro[ridx * 3 + 2]};
@@ -1809,7 +1919,7 @@ __global__ void __launch_bounds__(RTH_TILE) rth_count_kernel(RayIn in, const uin
                             signbit(d[2]) ? 1.0f : -1.0f};
       const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
       bool self = true;
-      if (root && !cbt) {  // the root's own test (rt_decide_one at level 0, not the target)
+      if (root && !cwoff) {  // the root's own test (rt_decide_one at level 0, not the target)
         const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
                              fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
                              fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
@@ -1823,7 +1933,7 @@ __global__ void __launch_bounds__(RTH_TILE) rth_count_kernel(RayIn in, const uin
         const bool last = lc == target_level;
         const float r = (float)(1.0 / (double)(float)(1u << lc));
         uint32_t kept = 0xffu;  // (fixed mode: children whose candidate index is below cap)
-        if (cbt) {
+        if (cwoff) {
           const uint32_t ranks = rth_fb_ranks(in, ridx, pidx, level, ob);
 #pragma unroll
           for (int k = 0; k < 8; k++)
@@ -1863,93 +1973,59 @@ __global__ void __launch_bounds__(RTH_TILE) rth_count_kernel(RayIn in, const uin
     if (in_list) hmask[i] = (uint8_t)m;
     int tot;
     (void)block_exclusive_scan(__popc(m), s_wave, &tot);
-    if (threadIdx.x == 0) tsum[t] = (uint32_t)tot;
+    wt += (uint32_t)tot;
   }
-}
-
-// One workgroup: the exclusive scan of the tile totals tsum[0, cdiv(*dnum, RTH_TILE)) in place, eight
-// per thread (their loads in flight together: one pass up to 8,192 tiles).
-// The total: > cap sets result[1]; with `next`, *next = min(total, cap) (the next list's count) and
-// at the last level result[0] = it.  zero (fixed mode): the next list's candidate tile totals, zeroed
-// here for the write pass to add into.
-constexpr int RTH_OFF_PT = 8;
-__global__ void __launch_bounds__(1024) rth_offsets_kernel(uint32_t *__restrict__ tsum, const uint32_t *__restrict__ dnum,
-                                                           uint32_t *__restrict__ next, uint32_t cap,
-                                                           int64_t *__restrict__ result, int last,
-                                                           uint32_t *__restrict__ zero) {
-  __shared__ int s_wave[16];
-  const int64_t n = *dnum;
-  const int nt = (int)((n + RTH_TILE - 1) / RTH_TILE);
-  uint32_t carry = 0;
-  for (int b0 = 0; b0 < nt; b0 += 1024 * RTH_OFF_PT) {
-    const int i0 = b0 + (int)threadIdx.x * RTH_OFF_PT;
-    uint32_t v[RTH_OFF_PT], sum = 0;
-#pragma unroll
-    for (int k = 0; k < RTH_OFF_PT; k++) {
-      v[k] = i0 + k < nt ? tsum[i0 + k] : 0u;
-      sum += v[k];
-    }
-    int tot = 0;
-    uint32_t ex = carry + (uint32_t)block_exclusive_scan((int)sum, s_wave, &tot);
-#pragma unroll
-    for (int k = 0; k < RTH_OFF_PT; k++) {
-      if (i0 + k < nt) tsum[i0 + k] = ex;
-      ex += v[k];
-    }
-    carry += (uint32_t)tot;
-  }
-  if (threadIdx.x == 0) {
-    if (carry > cap) result[1] = 1;
-    if (next) {
-      const uint32_t c = carry < cap ? carry : cap;
+  if (threadIdx.x == 0) __hip_atomic_store(wsum + blockIdx.x, wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (rth_last(ticket, &s_flag)) {
+    const uint64_t total = rth_scan_totals(wsum, cap, s_w64);
+    if (threadIdx.x == 0) {
+      if (total > cap) result[1] = 1;
+      const uint32_t c = total < cap ? (uint32_t)total : cap;
       *next = c;
       if (last) result[0] = c;
     }
-  }
-  if (zero) {
-    const uint32_t c = carry < cap ? carry : cap;
-    const int nz = (int)((c + RTH_TILE - 1) / RTH_TILE);
-    for (int i = threadIdx.x; i < nz; i += blockDim.x) zero[i] = 0u;
+    if (pcw_zero)
+      for (int k = threadIdx.x; k < (int)gridDim.x; k += blockDim.x) pcw_zero[k] = 0u;
   }
 }
 
-// fixed mode: the tile totals of the listed nodes' child counts pc (the candidate offsets' input)
-__global__ void __launch_bounds__(RTH_TILE) rth_pcsum_kernel(const uint32_t *__restrict__ dnum,
-                                                             const uint32_t *__restrict__ pc, uint32_t *__restrict__ tsum) {
-  __shared__ int s_wave[RTH_TILE / 64];
-  const int64_t num = *dnum;
-  for (int64_t t = blockIdx.x; t * RTH_TILE < num; t += gridDim.x) {
-    const int64_t i = t * RTH_TILE + threadIdx.x;
-    int tot;
-    (void)block_exclusive_scan(i < num ? (int)pc[i] : 0, s_wave, &tot);
-    if (threadIdx.x == 0) tsum[t] = (uint32_t)tot;
-  }
-}
-
-// write pass: node i's hit children at toff[t] + (its tile's exclusive scan of the hit counts), in
+// write pass: workgroup w's hit children from woff[w] on (its tiles' scans of the hit counts), in
 // front-to-back order; at the target level with depths.  pc_out (fixed mode, not the last level):
-// each listed child's own child count, and pc_ts (zeroed by the offsets pass) the next list's tile
-// totals of them -- summed per tile in LDS (a tile's outputs [t0, t0 + tot), tot <= 8 * RTH_TILE,
-// meet at most RTH_PTS of the next list's tiles), one global atomic per (tile, next tile).
-constexpr int RTH_PTS = 10;
+// each listed child's own child count, and pcw (zeroed by the count pass) their totals per
+// workgroup of the next list's partition -- summed in LDS for the RTH_PW workgroups from the
+// first one this workgroup writes into, global atomics past them; the last workgroup scans pcw
+// into the next count pass's candidate offsets (the candidate total past cap sets result[1]).
 __global__ void __launch_bounds__(RTH_TILE) rth_write_kernel(RayIn in, const uint32_t *__restrict__ dnum,
                                                              const int2 *__restrict__ list, uint32_t level,
                                                              uint32_t target_level, int with_depth, int with_exit,
                                                              const uint8_t *__restrict__ hmask,
-                                                             const uint32_t *__restrict__ toff, uint32_t cap,
+                                                             const uint32_t *__restrict__ woff, uint32_t cap,
                                                              int2 *__restrict__ nout, float *__restrict__ dout,
-                                                             uint32_t *__restrict__ pc_out, uint32_t *__restrict__ pc_ts) {
+                                                             uint32_t *__restrict__ pc_out, uint32_t *__restrict__ pcw,
+                                                             const uint32_t *__restrict__ dnext,
+                                                             unsigned *__restrict__ ticket, int64_t *__restrict__ result) {
   __shared__ int s_wave[RTH_TILE / 64];
-  __shared__ uint32_t s_pts[RTH_PTS];
+  __shared__ uint64_t s_w64[RTH_TILE / 64];
+  __shared__ uint32_t s_pw[RTH_PW];
+  __shared__ int s_flag;
   const int64_t num = *dnum;
   const int dd = with_exit ? 2 : 1;
-  for (int64_t t = blockIdx.x; t * RTH_TILE < num; t += gridDim.x) {  // workgroup-uniform
+  int64_t t0, t1;
+  rth_span(num, t0, t1);
+  uint32_t run = woff[blockIdx.x];
+  int64_t nt2 = 1;   // (pcw) the next list's tiles
+  uint32_t pw0 = 0;  // (pcw) the next list's workgroup of this workgroup's first row
+  if (pcw) {
+    nt2 = max((int64_t)1, ((int64_t)*dnext + RTH_TILE - 1) / RTH_TILE);
+    pw0 = rth_owner(run / RTH_TILE, nt2);
+    if (threadIdx.x < RTH_PW) s_pw[threadIdx.x] = 0u;  // (ordered by the scans' barriers / the one below)
+  }
+  for (int64_t t = t0; t < t1; t++) {  // workgroup-uniform
     const int64_t i = t * RTH_TILE + threadIdx.x;
     const uint32_t m = i < num ? hmask[i] : 0u;
-    if (pc_ts && threadIdx.x < RTH_PTS) s_pts[threadIdx.x] = 0u;  // (ordered by the scan's barriers)
-    const uint32_t t0 = toff[t], tile0 = t0 / RTH_TILE;
     int tot;
-    uint32_t base = t0 + (uint32_t)block_exclusive_scan(__popc(m), s_wave, &tot);
+    uint32_t base = run + (uint32_t)block_exclusive_scan(__popc(m), s_wave, &tot);
+    run += (uint32_t)tot;
     if (m) {
       int ridx, pidx;
       rth_node(list, i, ridx, pidx);
@@ -1964,6 +2040,14 @@ __global__ void __launch_bounds__(RTH_TILE) rth_write_kernel(RayIn in, const uin
       const uint32_t perm = c_rt_perm[(x > 0 ? 4u : 0u) + (y > 0 ? 2u : 0u) + (z > 0 ? 1u : 0u)];
       const uint32_t lc = level + 1;
       const bool depth_out = dout != nullptr && with_depth && lc == target_level;
+      // (pcw) the next list's workgroup of row `base` and the row its successor starts at: one
+      // division per node, then steps as `base` advances
+      uint32_t ko = 0;
+      int64_t knext = INT64_MAX;
+      if (pcw && base < cap) {
+        ko = rth_owner(base / RTH_TILE, nt2);
+        knext = rth_tile0((int64_t)ko + 1, nt2) * RTH_TILE;
+      }
 #pragma unroll
       for (int q = 0; q < 8; q++) {  // front to back: the code's permutation of the child indices
         const uint32_t j = (perm >> (4 * q)) & 15u;
@@ -1975,7 +2059,12 @@ __global__ void __launch_bounds__(RTH_TILE) rth_write_kernel(RayIn in, const uin
           if (pc_out) {
             const uint32_t pcv = (uint32_t)__popc(in.octree[s + c]);
             pc_out[base] = pcv;
-            if (pc_ts) atomicAdd(&s_pts[base / RTH_TILE - tile0], pcv);
+            if (pcw) {
+              while ((int64_t)base >= knext) knext = rth_tile0((int64_t)(++ko) + 1, nt2) * RTH_TILE;
+              const uint32_t k = ko - pw0;
+              if (k < (uint32_t)RTH_PW) atomicAdd(&s_pw[k], pcv);
+              else atomicAdd(&pcw[pw0 + k], pcv);
+            }
           }
           if (depth_out) {
             const int16_t *cp = in.points + (int64_t)(s + c) * 3;
@@ -1999,10 +2088,13 @@ __global__ void __launch_bounds__(RTH_TILE) rth_write_kernel(RayIn in, const uin
         base++;
       }
     }
-    if (pc_ts) {  // workgroup-uniform
-      __syncthreads();
-      if (threadIdx.x < RTH_PTS && s_pts[threadIdx.x]) atomicAdd(&pc_ts[tile0 + threadIdx.x], s_pts[threadIdx.x]);
-      __syncthreads();  // s_pts is reset by the next tile
+  }
+  if (pcw) {  // workgroup-uniform
+    __syncthreads();
+    if (threadIdx.x < RTH_PW && s_pw[threadIdx.x]) atomicAdd(&pcw[pw0 + threadIdx.x], s_pw[threadIdx.x]);
+    if (rth_last(ticket, &s_flag)) {
+      const uint64_t total = rth_scan_totals(pcw, cap, s_w64);
+      if (threadIdx.x == 0 && total > cap) result[1] = 1;
     }
   }
 }
@@ -2021,78 +2113,85 @@ __global__ void rth_tail_fill_kernel(const int64_t *__restrict__ result, int64_t
 }
 
 // fixed mode, level 0: each ray's candidate count at level 1 -- the root's children when the root
-// is hit (rt_decide_one at level 0, not the target), else none -- and the tiles' totals
+// is hit (rt_decide_one at level 0, not the target), else none -- their workgroup totals over the
+// count pass's partition of the rays, scanned by the last workgroup (past cap: result[1])
 __global__ void __launch_bounds__(RTH_TILE) rth_root_kernel(RayIn in, int64_t num_rays, uint32_t *__restrict__ pc,
-                                                            uint32_t *__restrict__ tsum) {
+                                                            uint32_t *__restrict__ pcw, uint32_t cap,
+                                                            unsigned *__restrict__ ticket, int64_t *__restrict__ result) {
   __shared__ int s_wave[RTH_TILE / 64];
-  const int64_t i = blockIdx.x * (int64_t)RTH_TILE + threadIdx.x;
-  uint32_t v = 0;
-  if (i < num_rays) {
-    const float o[3] = {in.ro[i * 3], in.ro[i * 3 + 1], in.ro[i * 3 + 2]};
-    const float d[3] = {in.rd[i * 3], in.rd[i * 3 + 1], in.rd[i * 3 + 2]};
-    const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
-    const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
-    const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
-                         fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
-                         fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
-    v = ray_aabb(o, d, inv, sgn, vc, 1.0f) != 0.0f ? (uint32_t)__popc(in.octree[0]) : 0u;
-    pc[i] = v;
+  __shared__ uint64_t s_w64[RTH_TILE / 64];
+  __shared__ int s_flag;
+  int64_t t0, t1;
+  rth_span(num_rays, t0, t1);
+  uint32_t wt = 0;
+  for (int64_t t = t0; t < t1; t++) {
+    const int64_t i = t * RTH_TILE + threadIdx.x;
+    uint32_t v = 0;
+    if (i < num_rays) {
+      const float o[3] = {in.ro[i * 3], in.ro[i * 3 + 1], in.ro[i * 3 + 2]};
+      const float d[3] = {in.rd[i * 3], in.rd[i * 3 + 1], in.rd[i * 3 + 2]};
+      const float sgn[3] = {signbit(d[0]) ? 1.0f : -1.0f, signbit(d[1]) ? 1.0f : -1.0f, signbit(d[2]) ? 1.0f : -1.0f};
+      const float inv[3] = {(float)(1.0 / (double)d[0]), (float)(1.0 / (double)d[1]), (float)(1.0 / (double)d[2])};
+      const float vc[3] = {fmaf(1.0f, fmaf(2.0f, (float)in.points[0], 1.0f), -1.0f),
+                           fmaf(1.0f, fmaf(2.0f, (float)in.points[1], 1.0f), -1.0f),
+                           fmaf(1.0f, fmaf(2.0f, (float)in.points[2], 1.0f), -1.0f)};
+      v = ray_aabb(o, d, inv, sgn, vc, 1.0f) != 0.0f ? (uint32_t)__popc(in.octree[0]) : 0u;
+      pc[i] = v;
+    }
+    int tot;
+    (void)block_exclusive_scan((int)v, s_wave, &tot);
+    wt += (uint32_t)tot;
   }
-  int tot;
-  (void)block_exclusive_scan((int)v, s_wave, &tot);
-  if (threadIdx.x == 0) tsum[blockIdx.x] = (uint32_t)tot;
+  if (threadIdx.x == 0) __hip_atomic_store(pcw + blockIdx.x, wt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (rth_last(ticket, &s_flag)) {
+    const uint64_t total = rth_scan_totals(pcw, cap, s_w64);
+    if (threadIdx.x == 0 && total > cap) result[1] = 1;
+  }
 }
 
 // The levels of the hit-list march.  lists a / b (`cap` rows each), hm (cap bytes), tsA / tsB
-// (cdiv(cap, RTH_TILE) each), dn[2] (the current / next list's count), result (rows, truncated)
-// zeroed by the caller; list a holds level 0 (ray i at the root) and dn[0] = num_rays.  Fixed mode:
-// pc (cap), cand_cap = the capacity the candidates are truncated at.
+// (>= the grid's workgroups each: the candidate / hit totals), dn[2] (the current / next list's
+// count), tk (rth_last's tickets), result (rows, truncated) zeroed by the caller; list a holds level
+// 0 (ray i at the root) and dn[0] = num_rays.  Fixed mode: pc (cap), cap = the capacity the
+// candidates are truncated at.
 struct RthBufs {
   int2 *a, *b;
   uint8_t *hm;
   uint32_t *tsA, *tsB, *dn, *pc;
+  unsigned *tk;
   int64_t *result;
 };
+static unsigned rth_grid(int64_t cap, int64_t num_rays) {  // a power of two (rth_tile0)
+  const int64_t want = std::min<int64_t>(cdiv(std::max(cap, num_rays), (int64_t)RTH_TILE), RTF_GRID);
+  unsigned g = 1;
+  while ((int64_t)g * 2 <= want) g *= 2;
+  return g;
+}
 static int rth_levels(const RayIn &in, int64_t num_rays, uint32_t target_level, int return_depth, int with_exit,
                       int64_t cap, bool fixed, const RthBufs &bf, int2 *out, float *dout, hipStream_t st) {
-  const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(std::max(cap, num_rays), (int64_t)RTH_TILE),
-                                                                      RTF_GRID));
+  const unsigned g = rth_grid(cap, num_rays);
+  unsigned *ticket = bf.tk;
   int2 *cur = bf.a, *nxt = bf.b;
   if (fixed) {
-    hipLaunchKernelGGL(rth_root_kernel, dim3((unsigned)cdiv(num_rays, (int64_t)RTH_TILE)), dim3(RTH_TILE), 0, st, in,
-                       num_rays, bf.pc, bf.tsA);
+    hipLaunchKernelGGL(rth_root_kernel, dim3(g), dim3(RTH_TILE), 0, st, in, num_rays, bf.pc, bf.tsA, (uint32_t)cap,
+                       ticket, bf.result);
     KL_CHECK_LAUNCH();
   }
   for (uint32_t l = 0; l < target_level; l++) {
     const int last = l + 1 == target_level;
     const uint32_t *dcur = bf.dn + (l & 1);
     uint32_t *dnext = bf.dn + ((l + 1) & 1);
-    // fixed mode: the candidate offsets (the level's candidate total past cap flags the truncation)
-    // from the candidate tile totals tsA -- level 0's by rth_root_kernel, later ones added by the
-    // previous write pass (dev param 25 = 1: a pass of their own, rth_pcsum_kernel)
-    const bool fold = g_dev_param[25] != 1;
-    if (fixed) {
-      if (l > 0 && !fold) {
-        hipLaunchKernelGGL(rth_pcsum_kernel, dim3(g), dim3(RTH_TILE), 0, st, dcur, (const uint32_t *)bf.pc, bf.tsA);
-        KL_CHECK_LAUNCH();
-      }
-      hipLaunchKernelGGL(rth_offsets_kernel, dim3(1), dim3(1024), 0, st, bf.tsA, dcur, (uint32_t *)nullptr,
-                         (uint32_t)cap, bf.result, 0, (uint32_t *)nullptr);
-      KL_CHECK_LAUNCH();
-    }
+    const bool pc_next = fixed && !last;
     hipLaunchKernelGGL(rth_count_kernel, dim3(g), dim3(RTH_TILE), 0, st, in, dcur, (const int2 *)cur, l, target_level,
                        (int)(l == 0), return_depth, with_exit, bf.hm, bf.tsB,
                        fixed ? (const uint32_t *)bf.pc : (const uint32_t *)nullptr,
-                       fixed ? (const uint32_t *)bf.tsA : (const uint32_t *)nullptr, (uint32_t)cap);
-    KL_CHECK_LAUNCH();
-    const bool pc_next = fixed && !last;
-    hipLaunchKernelGGL(rth_offsets_kernel, dim3(1), dim3(1024), 0, st, bf.tsB, dcur, dnext, (uint32_t)cap, bf.result,
-                       last, pc_next && fold ? bf.tsA : (uint32_t *)nullptr);
+                       fixed ? (const uint32_t *)bf.tsA : (const uint32_t *)nullptr, (uint32_t)cap, ticket, dnext,
+                       bf.result, last, pc_next ? bf.tsA : (uint32_t *)nullptr);
     KL_CHECK_LAUNCH();
     hipLaunchKernelGGL(rth_write_kernel, dim3(g), dim3(RTH_TILE), 0, st, in, dcur, (const int2 *)cur, l, target_level,
                        return_depth, with_exit, (const uint8_t *)bf.hm, (const uint32_t *)bf.tsB, (uint32_t)cap,
                        last ? out : nxt, last ? dout : nullptr, pc_next ? bf.pc : (uint32_t *)nullptr,
-                       pc_next && fold ? bf.tsA : (uint32_t *)nullptr);
+                       pc_next ? bf.tsA : (uint32_t *)nullptr, (const uint32_t *)dnext, ticket, bf.result);
     KL_CHECK_LAUNCH();
     std::swap(cur, nxt);
   }
@@ -2100,9 +2199,10 @@ static int rth_levels(const RayIn &in, int64_t num_rays, uint32_t target_level, 
 }
 
 __global__ void rth_init_kernel(int64_t n, int2 *__restrict__ list, uint32_t *__restrict__ dn,
-                                int64_t *__restrict__ result) {
+                                int64_t *__restrict__ result, unsigned *__restrict__ tk) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t < n) list[t] = make_int2((int)t, 0);
+  if (tk && t < RTH_TICKETS) tk[t * 32] = 0u;  // the hit-list passes' tickets (rth_last)
   if (t == 0) {
     dn[0] = (uint32_t)n;
     dn[1] = 0;
@@ -2120,7 +2220,8 @@ static int rt_hitlist(const RayIn &in, int64_t num_rays, uint32_t target_level, 
   if (cap >= ((int64_t)1 << 31)) return 1;
   const int64_t ntiles = cdiv(cap, (int64_t)RTH_TILE);
   const size_t lb = al256b((size_t)cap * sizeof(int2)), mb = al256b((size_t)cap), tb = al256b((size_t)ntiles * 4);
-  char *w = (char *)sc.get(256 + 2 * lb + mb + tb);
+  const size_t kb = (size_t)RTH_TICKETS * 128;
+  char *w = (char *)sc.get(256 + 2 * lb + mb + tb + kb);
   int2 *out = (int2 *)sc.get((size_t)cap * sizeof(int2));
   float *dout = return_depth ? (float *)sc.get((size_t)cap * dd * sizeof(float)) : nullptr;
   if (!w || !out || (return_depth && !dout)) return KL_E_ALLOC;
@@ -2131,8 +2232,9 @@ static int rt_hitlist(const RayIn &in, int64_t num_rays, uint32_t target_level, 
   bf.b = (int2 *)(w + 256 + lb);
   bf.hm = (uint8_t *)(w + 256 + 2 * lb);
   bf.tsB = (uint32_t *)(w + 256 + 2 * lb + mb);
+  bf.tk = (unsigned *)(w + 256 + 2 * lb + mb + tb);
   hipLaunchKernelGGL(rth_init_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, num_rays, bf.a, bf.dn,
-                     bf.result);
+                     bf.result, bf.tk);
   KL_CHECK_LAUNCH();
   KL_CHECK_RC(rth_levels(in, num_rays, target_level, return_depth, with_exit, cap, false, bf, out, dout, st));
   int64_t h[2] = {0, 0};
@@ -2593,7 +2695,7 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
 // result[0] hold nugget (-1, -1) and depth 0.
 namespace {
 struct RtfWs {
-  size_t a, b, info, psum, dtmp, dnum, tsum, hm, tsa, tsb, total;
+  size_t a, b, info, psum, dtmp, dnum, tsum, hm, tsa, tsb, tk, total;
   int64_t cap0, ntiles;
 };
 RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
@@ -2615,6 +2717,7 @@ RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
   w.hm = o; o += al(w.cap0);
   w.tsa = o; o += al(cdiv(w.cap0, (int64_t)RTH_TILE) * 4);
   w.tsb = o; o += al(cdiv(w.cap0, (int64_t)RTH_TILE) * 4);
+  w.tk = o; o += al((size_t)RTH_TICKETS * 128);  // the hit-list passes' tickets
   w.total = o;
   return w;
 }
@@ -2670,9 +2773,10 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
     bf.tsB = (uint32_t *)(w + L.tsb);
     bf.dn = dnum;
     bf.pc = (uint32_t *)(w + L.dtmp);
+    bf.tk = (unsigned *)(w + L.tk);
     bf.result = result;
     hipLaunchKernelGGL(rth_init_kernel, dim3((unsigned)cdiv(num_rays, 256)), dim3(256), 0, st, num_rays, n0, dnum,
-                       result);
+                       result, bf.tk);
     KL_CHECK_LAUNCH();
     KL_CHECK_RC(rth_levels(in, num_rays, target_level, return_depth, with_exit, capacity, true, bf, (int2 *)nuggets,
                            return_depth ? depth : nullptr, st));

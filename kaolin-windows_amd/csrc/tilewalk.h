@@ -28,22 +28,37 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lane) {
   }
 }
 
+// One block-swap stage of the transpose on a lane's row split in 32-bit halves (S <= 16: the
+// stage's 2S-bit groups never cross the halves), branch-free: the partner's halves (lane ^ S), a
+// per-lane rotate that brings the partner's other half-group into place (rotl S on lanes with bit S
+// clear, rotr S on the others: one v_alignbit_b32) and a bit select (v_bfi_b32) keeping the lane's
+// own half-group (m on clear lanes, ~m on set lanes).
 template <int S>
-__device__ __forceinline__ uint64_t transpose_stage(uint64_t x, uint64_t m, int lane) {
-  const uint64_t p = ((uint64_t)xor_lane<S>((uint32_t)(x >> 32), lane) << 32) | xor_lane<S>((uint32_t)x, lane);
-  return (lane & S) ? ((x & ~m) | ((p & ~m) >> S)) : ((x & m) | ((p & m) << S));
+__device__ __forceinline__ void transpose_stage(uint32_t &lo, uint32_t &hi, uint32_t m, int lane) {
+  const uint32_t plo = xor_lane<S>(lo, lane), phi = xor_lane<S>(hi, lane);
+  const uint32_t sgn = (uint32_t)((int)((uint32_t)lane << (31 - __builtin_ctz(S))) >> 31);  // lane & S ? ~0 : 0
+  const uint32_t keep = m ^ sgn;
+  const uint32_t amt = (32u - S) + (sgn & (uint32_t)(2 * S - 32));  // rotr amount (mod 32)
+  const uint32_t qlo = __builtin_amdgcn_alignbit(plo, plo, amt), qhi = __builtin_amdgcn_alignbit(phi, phi, amt);
+  lo = (keep & lo) | (~keep & qlo);
+  hi = (keep & hi) | (~keep & qhi);
 }
 
 // 64x64 bit-matrix transpose across the wave: lane i holds row i (bit j = column j) on
-// entry and column i (bit j = row j) on exit.  Six block-swap stages.
+// entry and column i (bit j = row j) on exit.  Six block-swap stages; the first (32-bit
+// halves across lanes i, i ^ 32: lanes < 32 take the partner's low half as their high half, the
+// others the partner's high half as their low half) is one v_permlane32_swap of (lo, hi).
 __device__ __forceinline__ uint64_t transpose64(uint64_t x, int lane) {
-  x = transpose_stage<32>(x, 0x00000000ffffffffull, lane);
-  x = transpose_stage<16>(x, 0x0000ffff0000ffffull, lane);
-  x = transpose_stage<8>(x, 0x00ff00ff00ff00ffull, lane);
-  x = transpose_stage<4>(x, 0x0f0f0f0f0f0f0f0full, lane);
-  x = transpose_stage<2>(x, 0x3333333333333333ull, lane);
-  x = transpose_stage<1>(x, 0x5555555555555555ull, lane);
-  return x;
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const auto r = __builtin_amdgcn_permlane32_swap(lo, hi, false, false);
+  lo = r[0];
+  hi = r[1];
+  transpose_stage<16>(lo, hi, 0x0000ffffu, lane);
+  transpose_stage<8>(lo, hi, 0x00ff00ffu, lane);
+  transpose_stage<4>(lo, hi, 0x0f0f0f0fu, lane);
+  transpose_stage<2>(lo, hi, 0x33333333u, lane);
+  transpose_stage<1>(lo, hi, 0x55555555u, lane);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 // The candidate chunks of a tile (set bits of its bitmap words, ascending) as a sequence

@@ -1,8 +1,8 @@
 """A/B of the raytrace marches on the bench's cfg4 SPC (development aid): the hit-list march
 (default, 0), the per-level march (dev param 15 = 2), the fused level march (3) and the depth-first
 march (4, host-sized entry only), host-sized and fixed-capacity, wall clock per call, and equality
-of the answers; then the hit-list march with dev param 25 = 1 (candidate tile totals in a pass of
-their own, all rows filled first) against the default."""
+of the answers; then the hit-list march with dev param 25 = 1 (the fixed entry fills all rows first
+instead of the rows past its count afterwards) against the default."""
 import ctypes
 import os
 import sys

@@ -601,6 +601,25 @@ def test_dibr_bin_marks_equal_atomic_binning(kal, case):
         assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
 
 
+@pytest.mark.parametrize('knum,alt', [(30, 1), (30, 3), (8, 2)])
+def test_soft_item_rows_equal(kal, knum, alt):
+    """The soft forward's rows per work item (r05: the fewest halvings whose LDS lets 5 workgroups
+    share a CU -- 2 rows at knum 30, 4 at knum 8) against another split (dev param 20 = alt
+    halvings: 4, 1 or 2 rows) -- every output and the compact state equal."""
+    import bench
+    inp = bench.dibr_inputs([0.3, 2.0], DEV, H=96, W=128)
+    fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+    base = _dibr_fused_forward(fvz, fvi, feat, fnz, 96, 128, knum, 0.02)
+    try:
+        _dev_param(20, alt)
+        other = _dibr_fused_forward(fvz, fvi, feat, fnz, 96, 128, knum, 0.02)
+    finally:
+        _dev_param(20, 0)
+    names = ['features', 'face_idx', 'weights', 'soft_mask', 'hits', 'seg_tot', 'rec_face', 'rec_prob', 'ranges']
+    for n, x, y in zip(names, base, other):
+        assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
+
+
 @pytest.mark.parametrize('case', ['bench', 'adversarial', 'knum64', 'knum255', 'bigbox'])
 def test_dibr_fused_tile_kernel_equals_two_kernel_path(kal, case):
     """kl_dibr_forward's fused tile kernel (dibrtile.hip: the rasterizer and the soft mask in one
