@@ -168,7 +168,8 @@ extern "C" int kl_abi_version(void) { return KL_ABI_VERSION; }
 // publishes its partial; the workgroup whose ticket comes last adds the partials in block order
 // (deterministic) and resets the ticket.  The hand-off is MI355X_MICROARCH.md's first measured
 // `sc1` row: one lane per workgroup stores its 8-B partial `sc1` (a relaxed agent-scope atomic
-// store), waits vmcnt(0), then adds to ONE agent-scope counter; the last adder's workgroup loads
+// store), waits vmcnt(0), then adds to its group's agent-scope ticket (common.h grid_last: two
+// levels, r05); the last adder's workgroup loads
 // the partials `sc1` behind a workgroup barrier -- no release / acquire fences (a device-scope
 // release per block measured 29 us here in r03, hence the old second launch).  One workgroup per
 // CU, as that row was measured.
@@ -209,27 +210,20 @@ __global__ void __launch_bounds__(DOT2_THREADS) dot2_kernel(const float *__restr
   __shared__ int s_last;
   const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x, nt = (size_t)gridDim.x * blockDim.x;
   const double s = block_sum(dot_strip(a, ga, na, t, nt) + dot_strip(b, gb, nb, t, nt), red);
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(partial + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!s_last) return;
+  if (threadIdx.x == 0) __hip_atomic_store(partial + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!grid_last(ticket, &s_last)) return;
   double v = 0.0;
   for (int i = threadIdx.x; i < (int)gridDim.x; i += blockDim.x)
     v += __hip_atomic_load(partial + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   v = block_sum(v, red);
-  if (threadIdx.x == 0) {
-    out[0] = (float)v;
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next call
-  }
+  if (threadIdx.x == 0) out[0] = (float)v;
 }
 }  // namespace kl
 
-// workspace: the partials, then the ticket (zero before the first call; every call leaves it zero)
-extern "C" size_t kl_loss_dot2_workspace_bytes(void) { return kl::DOT2_BLOCKS * sizeof(double) + 256; }
+// workspace: the partials, then the tickets (zero before the first call; every call leaves them zero)
+extern "C" size_t kl_loss_dot2_workspace_bytes(void) {
+  return kl::DOT2_BLOCKS * sizeof(double) + kl::gl_ticket_words(kl::DOT2_BLOCKS) * 4;
+}
 
 extern "C" int kl_loss_dot2(const float *a, const float *ga, int64_t na, const float *b, const float *gb, int64_t nb,
                             void *ws, float *out, kl_stream stream) {

@@ -164,6 +164,35 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int *s_wave, int *tot
   return before + inc - v;
 }
 
+// Last-workgroup hand-off (MI355X_MICROARCH.md's measured `sc1` row): every workgroup's published
+// values are complete (vmcnt(0)) before its barrier and its agent-scope add on a ticket; the
+// workgroup that takes the last ticket returns true and may then read the published values with
+// agent-scope loads.  Two levels of tickets, 128 B apart: tk[32 * (1 + g)] for each group g of
+// GL_GROUP workgroups, then the groups' last workgroups on the top ticket tk[0] -- 2,048 adds on
+// one address cost ~25 us (r05w), a group's 32 ~0.4 us.  Each last taker re-zeroes its ticket, so
+// the tickets are zero again after every grid (zero them once: gl_ticket_words).  Workgroup-uniform.
+constexpr int GL_GROUP = 32;
+__host__ __device__ constexpr size_t gl_ticket_words(int grid) { return 32 * (size_t)(1 + (grid + GL_GROUP - 1) / GL_GROUP); }
+__device__ __forceinline__ bool grid_last(unsigned *tk, int *s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned G = gridDim.x, grp = blockIdx.x / GL_GROUP;
+    const unsigned ng = (G + GL_GROUP - 1) / GL_GROUP;
+    const unsigned gsize = min((unsigned)GL_GROUP, G - grp * GL_GROUP);
+    unsigned *t1 = tk + 32 * (1 + grp);
+    bool last = false;
+    if (__hip_atomic_fetch_add(t1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
+      __hip_atomic_store(t1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+      if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *s_flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *s_flag != 0;
+}
+
 // Adds v of every lane into *dst (64-bit): a wave sum, then one vector atomic per wave.
 // Every lane of the wave must call it (lanes with nothing to add pass 0).
 __device__ __forceinline__ void wave_add_u64(unsigned long long *dst, unsigned long long v) {

@@ -1828,33 +1828,9 @@ __device__ __forceinline__ uint64_t rth_scan64(uint64_t v, uint64_t *s_w, uint64
   return before + inc - v;
 }
 
-// The hand-off: every workgroup's published values are complete (vmcnt(0)) before its barrier and
-// its agent-scope add on a ticket; the workgroup that takes the last ticket returns true.  Two
-// levels of tickets, 128 B apart: one per group of RTH_TGROUP workgroups, then the groups' last
-// workgroups on the top ticket (2,048 adds on one address cost ~25 us per pass: measured r05w).
-// Each last taker re-zeroes its ticket for the next pass (every add on it has been made).
-// tk: RTH_TICKETS tickets at a stride of 32 words (the top one last).  Workgroup-uniform.
-constexpr int RTH_TGROUP = 32;
-constexpr int RTH_TICKETS = RTF_GRID / RTH_TGROUP + 1;
-__device__ __forceinline__ bool rth_last(unsigned *tk, int *s_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned G = gridDim.x, grp = blockIdx.x / RTH_TGROUP;
-    const unsigned ng = (G + RTH_TGROUP - 1) / RTH_TGROUP;
-    const unsigned gsize = min((unsigned)RTH_TGROUP, G - grp * RTH_TGROUP);
-    unsigned *t1 = tk + grp * 32, *t2 = tk + (RTH_TICKETS - 1) * 32;
-    bool last = false;
-    if (__hip_atomic_fetch_add(t1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1) {
-      __hip_atomic_store(t1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = __hip_atomic_fetch_add(t2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
-      if (last) __hip_atomic_store(t2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    *s_flag = last ? 1 : 0;
-  }
-  __syncthreads();
-  return *s_flag != 0;
-}
+// the hand-off of common.h (grid_last); its tickets for the largest grid
+constexpr int RTH_TICKET_WORDS = (int)gl_ticket_words(RTF_GRID);
+__device__ __forceinline__ bool rth_last(unsigned *tk, int *s_flag) { return grid_last(tk, s_flag); }
 
 // The last workgroup: the exclusive scan of vals[0, gridDim.x) in place (agent-scope loads), each
 // prefix clamped to clampv (rows at or past `cap` are never written); returns the total.
@@ -2202,7 +2178,7 @@ __global__ void rth_init_kernel(int64_t n, int2 *__restrict__ list, uint32_t *__
                                 int64_t *__restrict__ result, unsigned *__restrict__ tk) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t < n) list[t] = make_int2((int)t, 0);
-  if (tk && t < RTH_TICKETS) tk[t * 32] = 0u;  // the hit-list passes' tickets (rth_last)
+  if (tk && t < RTH_TICKET_WORDS) tk[t] = 0u;  // the hit-list passes' tickets (rth_last)
   if (t == 0) {
     dn[0] = (uint32_t)n;
     dn[1] = 0;
@@ -2220,7 +2196,7 @@ static int rt_hitlist(const RayIn &in, int64_t num_rays, uint32_t target_level, 
   if (cap >= ((int64_t)1 << 31)) return 1;
   const int64_t ntiles = cdiv(cap, (int64_t)RTH_TILE);
   const size_t lb = al256b((size_t)cap * sizeof(int2)), mb = al256b((size_t)cap), tb = al256b((size_t)ntiles * 4);
-  const size_t kb = (size_t)RTH_TICKETS * 128;
+  const size_t kb = (size_t)RTH_TICKET_WORDS * 4;
   char *w = (char *)sc.get(256 + 2 * lb + mb + tb + kb);
   int2 *out = (int2 *)sc.get((size_t)cap * sizeof(int2));
   float *dout = return_depth ? (float *)sc.get((size_t)cap * dd * sizeof(float)) : nullptr;
@@ -2717,7 +2693,7 @@ RtfWs rtf_layout(int64_t num_rays, int64_t capacity, int with_exit) {
   w.hm = o; o += al(w.cap0);
   w.tsa = o; o += al(cdiv(w.cap0, (int64_t)RTH_TILE) * 4);
   w.tsb = o; o += al(cdiv(w.cap0, (int64_t)RTH_TILE) * 4);
-  w.tk = o; o += al((size_t)RTH_TICKETS * 128);  // the hit-list passes' tickets
+  w.tk = o; o += al((size_t)RTH_TICKET_WORDS * 4);  // the hit-list passes' tickets
   w.total = o;
   return w;
 }
