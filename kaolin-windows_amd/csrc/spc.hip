@@ -2178,7 +2178,8 @@ __global__ void rth_init_kernel(int64_t n, int2 *__restrict__ list, uint32_t *__
                                 int64_t *__restrict__ result, unsigned *__restrict__ tk) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (t < n) list[t] = make_int2((int)t, 0);
-  if (tk && t < RTH_TICKET_WORDS) tk[t] = 0u;  // the hit-list passes' tickets (rth_last)
+  if (tk)  // the hit-list passes' tickets (rth_last): all of them, whatever the grid of this launch
+    for (int64_t k = t; k < RTH_TICKET_WORDS; k += (int64_t)gridDim.x * blockDim.x) tk[k] = 0u;
   if (t == 0) {
     dn[0] = (uint32_t)n;
     dn[1] = 0;
