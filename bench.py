@@ -361,7 +361,7 @@ def survey_step_bytes(inp, stats):
 
 # kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
 OP_KERNELS = {
-    'dibr_forward': ('raster_bin_word_kernel<float, 2>', 'tile_countorder_chip_kernel', 'raster_tile_kernel<float',
+    'dibr_forward': ('raster_bin_word_kernel<float, 2', 'tile_countorder_chip_kernel', 'raster_tile_kernel<float',
                      'soft_tile_fwd_kernel<float'),
     'dibr_backward': ('rasterize_bwd_gather2_kernel<float', 'soft_tile_bwd_kernel<float'),
 }

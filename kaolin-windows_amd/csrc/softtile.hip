@@ -795,11 +795,12 @@ SoftSplit soft_split() {
 }
 
 int soft_lp_min(int K) {
-  // the fewest row halvings whose LDS lets five workgroups share a CU -- the forward kernel's VGPR
-  // occupancy (5 waves per SIMD at ST_EVAL_U = 2): at knum 30, 2-row items (24.7 KB) against 4-row
-  // ones (39.6 KB, four per CU): dibr_forward 98.3-99.1 against 103.1-103.8 us (r05u)
+  // the fewest row halvings (at most 4 rows per workgroup) whose slot lists fit in 64 KB of LDS;
+  // knum near 255 takes one row per workgroup.  r05z: at knum 30, 2-row items (LDS for 5 workgroups
+  // per CU, the kernel's VGPR occupancy at ST_EVAL_U = 2) against these 4-row ones: cfg3 5,609-5,649
+  // against 5,618-5,646 Mpixels/s, cfg5 9,394-9,425 against 9,875-9,906 -- kept at 4 rows
   int lp = 1;
-  while (lp < 3 && st_head_lds() + (size_t)(TILE_H >> lp) * st_row_lds(K) > 32 * 1024) lp++;
+  while (lp < 3 && st_head_lds() + (size_t)(TILE_H >> lp) * st_row_lds(K) > 64 * 1024) lp++;
   // dev param 20 = 1..3: that many halvings where the LDS fits 64 KB (A/B)
   const int dp = g_dev_param[20];
   if (dp >= 1 && dp <= 3 && st_head_lds() + (size_t)(TILE_H >> dp) * st_row_lds(K) <= 64 * 1024) lp = dp;

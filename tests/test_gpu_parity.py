@@ -601,11 +601,11 @@ def test_dibr_bin_marks_equal_atomic_binning(kal, case):
         assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
 
 
-@pytest.mark.parametrize('knum,alt', [(30, 1), (30, 3), (8, 2)])
+@pytest.mark.parametrize('knum,alt', [(30, 2), (30, 3), (8, 2)])
 def test_soft_item_rows_equal(kal, knum, alt):
-    """The soft forward's rows per work item (r05: the fewest halvings whose LDS lets 5 workgroups
-    share a CU -- 2 rows at knum 30, 4 at knum 8) against another split (dev param 20 = alt
-    halvings: 4, 1 or 2 rows) -- every output and the compact state equal."""
+    """The soft forward's rows per work item (4 where the slot lists fit 64 KB of LDS) against
+    another split (dev param 20 = alt halvings: 2 or 1 rows) -- every output and the compact
+    state equal."""
     import bench
     inp = bench.dibr_inputs([0.3, 2.0], DEV, H=96, W=128)
     fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
