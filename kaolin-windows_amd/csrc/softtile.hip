@@ -78,6 +78,9 @@ struct SoftTileArgs {
 #ifndef ST_EVAL_U
 #define ST_EVAL_U 2  // hits in flight per lane in the f32 evaluation: 89 VGPRs, 5 waves per SIMD (4: 115, 4)
 #endif
+#ifndef ST_FC
+#define ST_FC 2  // candidate chunks per wave and fill step (A/B builds: EXTRA=-DST_FC=3)
+#endif
 #ifndef ST_FWD_MIN_WAVES
 #define ST_FWD_MIN_WAVES 1  // the forward kernel's minimum waves per SIMD (A/B builds)
 #endif
@@ -150,10 +153,15 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
     // is waited for at once), issued after the current step's ranges are tested.  Two chunks per
     // wave and step: the fill of a heavy tile (hundreds of candidate chunks) is a chain of steps
     // that each wait for their loads, so twice the chunks per step halves the chain.
-    constexpr int FC = 2;  // chunks per wave and step
-    int pos = 0, nc[FC] = {-1, -1};
+    constexpr int FC = ST_FC;  // chunks per wave and step
+    int pos = 0, nc[FC];
     bool nexists = false;
-    uint2 nr[FC] = {make_uint2(1u, 1u), make_uint2(1u, 1u)};
+    uint2 nr[FC];
+#pragma unroll
+    for (int k = 0; k < FC; k++) {
+      nc[k] = -1;
+      nr[k] = make_uint2(1u, 1u);
+    }
     auto pf_next = [&]() {
       nexists = seq.at(pos, lane) >= 0;
 #pragma unroll
