@@ -992,7 +992,8 @@ def cfg4_leg(device, steps):
                                              'note': 'SURVEY.md §8d prices the reference algorithm (sort, dedup); '
                                                      'an effective rate: this build moves none of those bytes'}}},
             'timing': 'wall clock per call (median of runs); voxelgrid: device-counted levels, one status read; '
-                      'voxelgrid.host_sized and mesh_to_spc: incl. the per-level host count reads',
+                      'voxelgrid.host_sized: incl. its per-level host count reads; mesh_to_spc: the node-rank '
+                      'levels, one host read of the counts after them',
             'spc': (octree, fidx, bary)}
 
 
