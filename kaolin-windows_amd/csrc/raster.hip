@@ -575,6 +575,10 @@ struct RastTileArgs {
   uint8_t *soft_hits = nullptr;
   int *soft_seg = nullptr;
   uint8_t *soft_defer = nullptr;
+  // r05: the soft items holding this tile's rows (CountOrderArgs::row_item) and their flags, set
+  // here for the items with an uncovered pixel (zeroed by the binning kernel; nullptr: not flagged)
+  const int32_t *soft_row_item = nullptr;
+  uint8_t *soft_live = nullptr;
 };
 
 template <typename T>
@@ -624,6 +628,8 @@ __global__ void __launch_bounds__(512) raster_tile_kernel(RastTileArgs<T> a) {
   const int64_t f0 = (int64_t)b * a.F;
   const T *rec = a.rec + f0 * RT_REC;
   const uint2 *rng = a.rng + f0;
+  // (soft_live) the soft item of this row, loaded now: its flag is set at the end
+  const int32_t srow = a.soft_live && sub == 0 ? a.soft_row_item[(size_t)tile * TILE_H + (j0 - ty * TILE_H) + r] : -1;
 
   T max_z0 = -INFINITY, mw0 = 0, mw1 = 0, mw2 = 0;
   int win = -1;
@@ -855,6 +861,10 @@ __global__ void __launch_bounds__(512) raster_tile_kernel(RastTileArgs<T> a) {
   }
   const size_t p = ((size_t)b * H + j) * W + i;
   const int D = a.D;
+  if (srow >= 0) {  // an uncovered pixel in this row: its soft item has work (px_valid lanes only here)
+    const uint64_t unc = ballot(win < 0);
+    if (unc && lane == __builtin_ctzll(unc)) a.soft_live[srow] = 1;
+  }
   if (a.soft_hits) {
     a.soft_hits[p] = 0;
     a.soft_mask[p] = win >= 0 ? (T)1.0 : (T)0.0;
@@ -1748,8 +1758,8 @@ namespace kl {
 //   then:   face records | pixel ranges | raster buckets | soft buckets | raster items |
 //           item count | soft order | soft pixel ranges     (records sized for f64)
 struct DibrFwdWs {
-  size_t off_sbm, off_rgh, off_sgh, off_tk, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n, off_sorder,
-      off_sn, off_srng, off_defer, off_whist, bytes;
+  size_t off_sbm, off_rgh, off_sgh, off_tk, off_live, zero, off_rec, off_rng, off_rbk, off_sbk, off_items, off_n,
+      off_sorder, off_sn, off_srng, off_defer, off_whist, off_rowitem, bytes;
   DibrFwdWs(int B, int H, int W, int F) {
     const BinGeom g = make_bin_geom(B, H, W, F);
     const size_t nt = (size_t)g.batch * g.tiles_y * g.tiles_x;
@@ -1758,7 +1768,8 @@ struct DibrFwdWs {
     off_rgh = off_sbm + g.bytes();
     off_sgh = off_rgh + ORD_HIST * sizeof(int);
     off_tk = off_sgh + ORD_HIST * sizeof(int);  // the chip-wide order kernel's two tickets
-    zero = off_tk + 16 * sizeof(int);
+    off_live = off_tk + 16 * sizeof(int);       // the soft items' live flags (<= 8 items per tile)
+    zero = off_live + ((nt * TILE_H + 3) & ~(size_t)3);
     off_rec = up(zero);
     off_rng = up(off_rec + (size_t)B * F * RT_REC * sizeof(double));
     off_rbk = up(off_rng + (size_t)B * F * sizeof(uint2));
@@ -1770,7 +1781,8 @@ struct DibrFwdWs {
     off_srng = up(off_sn + sizeof(int));
     off_defer = up(off_srng + (size_t)B * F * sizeof(uint2));
     off_whist = up(off_defer + (size_t)B * H * g.tiles_x);  // 2 x nb x ORD_HIST workgroup histograms
-    bytes = off_whist + 2 * (size_t)cdiv((int64_t)nt, CO_THREADS) * ORD_HIST * sizeof(int);
+    off_rowitem = up(off_whist + 2 * (size_t)cdiv((int64_t)nt, CO_THREADS) * ORD_HIST * sizeof(int));
+    bytes = off_rowitem + nt * TILE_H * sizeof(int32_t);  // the soft item of each tile row
   }
 };
 
@@ -1863,6 +1875,9 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   // params 4 / 5 override, for sweeps)
   const int split_from = g_dev_param[4] ? g_dev_param[4] : 5;
   const int split_log2 = sizeof(T) == 4 ? (g_dev_param[5] ? g_dev_param[5] : 2) : 0;
+  // r05: the soft items' live flags (set by the rasterizer, read by the soft kernel first) where the
+  // chip order kernel lists each tile row's item; dev param 26 = 1: off (A/B)
+  bool live = false;
   if (nt <= ORD_LDS_TILES && !(g_dev_flags & (1 << 20)) && g_dev_param[15] != 1) {
     // counts over the chip, orders by each bitmap's last count workgroup (tileorder.h); the other
     // workgroups zero the backward's soft-mask accumulator meanwhile (dev param 15 = 1: the r04
@@ -1895,6 +1910,8 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     ca.zacc = nullptr;
     ca.zn = 0;
     ca.dbg = kDevStamps && g_dev_debug ? reinterpret_cast<uint64_t *>(g_dev_debug) + kOrderStampsAt : nullptr;
+    live = g_dev_param[26] != 1;
+    ca.row_item = live ? reinterpret_cast<int32_t *>(w + L.off_rowitem) : nullptr;
     const unsigned zg = 1u;  // one workgroup zeroes the state's counters
     hipLaunchKernelGGL(tile_countorder_chip_kernel, dim3((unsigned)(2 * nb) + zg), dim3(CO_THREADS),
                        (size_t)nb * ORD_HIST * sizeof(int), st, ca);
@@ -1924,10 +1941,13 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   args.soft_hits = s.hits;
   args.soft_seg = s.seg_tot;
   args.soft_defer = defer;
+  uint8_t *live_flags = live ? reinterpret_cast<uint8_t *>(w + L.off_live) : nullptr;
+  args.soft_row_item = live ? reinterpret_cast<const int32_t *>(w + L.off_rowitem) : nullptr;
+  args.soft_live = live_flags;
   hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
   KL_CHECK_LAUNCH();
   return soft_tile_forward_main<T>(B, H, W, F, K, fvi, out_idx, sigmainv, pad, m, out_mask, s, sbm, sorder, snitems,
-                                   srng, defer, st, true, bitems, bcnt, S.cap);
+                                   srng, defer, st, true, bitems, bcnt, S.cap, live_flags);
 }
 
 template <typename T>

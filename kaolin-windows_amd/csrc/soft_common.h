@@ -213,7 +213,7 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
                            double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
                            const int32_t *order, const int *nitems, const uint2 *rng, uint8_t *defer,
                            hipStream_t st, bool prefilled, int2 *bwd_items = nullptr, int *bwd_cnt = nullptr,
-                           int bwd_cap = 0);
+                           int bwd_cap = 0, const uint8_t *live = nullptr);
 int soft_lp_min(int K);
 template <typename T>
 int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T *mask, const SoftState<T> &s,

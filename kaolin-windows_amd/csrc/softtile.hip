@@ -70,6 +70,10 @@ struct SoftTileArgs {
   // rotation (swz = 63) spreads a pixel's consecutive slots, which the evaluation's consecutive threads
   // touch, over the banks; swz = 0 (dev param 19 = 1) is the plain [slot][lane] layout.
   int swz = 63;
+  // (prefilled, r05) per work item: 1 when its rows hold an uncovered pixel (the rasterizer's flags,
+  // raster_tile_kernel); an item without is done at once -- one load, not the order -> sel chain
+  const uint8_t *live = nullptr;
+  int live_n = 0;  // its length: items <= TILE_H per tile (the grid's bound can exceed it)
 };
 
 
@@ -93,7 +97,12 @@ constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(in
 template <typename T>
 __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
   extern __shared__ __align__(16) unsigned char smem[];
-  if ((int)blockIdx.x >= *a.nitems) return;
+  {
+    const int ni = *a.nitems;
+    // (the two loads in flight together; an index past the flags is past the items too)
+    const bool lv = a.live ? a.live[min((int)blockIdx.x, a.live_n - 1)] != 0 : true;
+    if ((int)blockIdx.x >= ni || !lv) return;
+  }
   uint64_t *const dbg = kDevStamps ? a.dbg : nullptr;  // compiled out unless KL_DEV_STAMPS
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -854,7 +863,8 @@ template <typename T>
 int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, const int64_t *sel, float sigmainv,
                            double pad, float m, T *mask, const SoftState<T> &s, const uint32_t *bitmap,
                            const int32_t *order, const int *nitems, const uint2 *rng, uint8_t *defer,
-                           hipStream_t st, bool prefilled, int2 *bwd_items, int *bwd_cnt, int bwd_cap) {
+                           hipStream_t st, bool prefilled, int2 *bwd_items, int *bwd_cnt, int bwd_cap,
+                           const uint8_t *live) {
   const BinGeom g = make_bin_geom(B, H, W, F);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   if (nt == 0) return KL_OK;
@@ -869,6 +879,8 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   args.bwd_cnt = bwd_cnt;
   args.bwd_cap = bwd_cap;
   args.swz = g_dev_param[19] == 1 ? 0 : 63;
+  args.live = prefilled ? live : nullptr;
+  args.live_n = nt * TILE_H;
   hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)soft_items_bound(nt, lp_min, soft_split())), dim3(64 * ST_WAVES), lds,
                      st, args);
   KL_CHECK_LAUNCH();
@@ -974,11 +986,11 @@ template int soft_tile_forward<double>(int, int, int, int, int, const double *, 
 template int soft_tile_forward_main<float>(int, int, int, int, int, const float *, const int64_t *, float, double,
                                            float, float *, const SoftState<float> &, const uint32_t *,
                                            const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t,
-                                           bool, int2 *, int *, int);
+                                           bool, int2 *, int *, int, const uint8_t *);
 template int soft_tile_forward_main<double>(int, int, int, int, int, const double *, const int64_t *, float, double,
                                             float, double *, const SoftState<double> &, const uint32_t *,
                                             const int32_t *, const int *, const uint2 *, uint8_t *, hipStream_t,
-                                            bool, int2 *, int *, int);
+                                            bool, int2 *, int *, int, const uint8_t *);
 template int soft_tile_backward<float>(int, int, int, int, int, const float *, const float *,
                                        const SoftState<float> &, const float *, float, float, float *, bool, void *,
                                        size_t, hipStream_t, double *, bool *);

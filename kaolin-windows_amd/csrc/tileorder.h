@@ -418,6 +418,9 @@ struct CountOrderArgs {
   size_t zn;
   uint64_t *dbg = nullptr;  // dev stamps (wall clock): count workgroup b at 4 b (start, counted, arrived);
                             // bitmap w's workgroup 0 at 64 + 4 w (barrier passed, prefix, placed)
+  // (nt x TILE_H, or nullptr) the soft item holding row r of tile t, -1 for none: the rasterizer
+  // flags the items with an uncovered pixel by it (RastTileArgs::soft_live)
+  int32_t *row_item = nullptr;
 };
 
 static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel(CountOrderArgs a) {
@@ -531,11 +534,18 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
   if (ldbg && threadIdx.x == 0) ldbg[1] = stamp_wall();
   if (key >= 0) {
     const int lp = lpb[q];
+    int32_t *const ri = which == 1 ? a.row_item : nullptr;
     if (lp >= 0) {
       const int np = 1 << lp, g = key / ORD_BUCKETS;
       const int r0 = sb[key] + (wbase[key] + rank) * np;
-      for (int k = 0; k < np; k++)
-        a.order[which][flat ? r0 + k : place_pos(sx, g, r0 + k)] = t | (k << 24) | (lp << 28);
+      for (int k = 0; k < np; k++) {
+        const int pos = flat ? r0 + k : place_pos(sx, g, r0 + k);
+        a.order[which][pos] = t | (k << 24) | (lp << 28);
+        if (ri)
+          for (int r = k * (TILE_H >> lp); r < (k + 1) * (TILE_H >> lp); r++) ri[(size_t)t * TILE_H + r] = pos;
+      }
+    } else if (ri) {
+      for (int r = 0; r < TILE_H; r++) ri[(size_t)t * TILE_H + r] = -1;
     }
   }
   if (ldbg) {

@@ -601,6 +601,36 @@ def test_dibr_bin_marks_equal_atomic_binning(kal, case):
         assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
 
 
+@pytest.mark.parametrize('case', ['bench', 'adversarial', 'knum255', 'tiny'])
+def test_soft_live_flags_equal(kal, case):
+    """The soft forward's work items flagged live by the rasterizer (r05: an item whose rows hold no
+    uncovered pixel is done after one load) against the unflagged kernel (dev param 26 = 1) -- every
+    output and the compact state equal; knum 255 (1-row items), and a 40x24 image (fewer flags than
+    the launch's item bound)."""
+    import bench
+    K, H, W = 30, 96, 128
+    if case == 'adversarial':
+        z, v, f = _adversarial_faces(torch.float32)
+        fvz, fvi, feat = T(z), T(v), T(f)
+        fnz = T(np.random.default_rng(2).uniform(-0.3, 1, fvz.shape[:2]).astype(np.float32))
+        H, W = 97, 130
+    else:
+        if case == 'tiny':
+            H, W = 40, 24
+        inp = bench.dibr_inputs([0.3, 2.0], DEV, H=H, W=W)
+        fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+        K = 255 if case == 'knum255' else 30
+    flagged = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, 0.02)
+    try:
+        _dev_param(26, 1)
+        plain = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, 0.02)
+    finally:
+        _dev_param(26, 0)
+    names = ['features', 'face_idx', 'weights', 'soft_mask', 'hits', 'seg_tot', 'rec_face', 'rec_prob', 'ranges']
+    for n, x, y in zip(names, flagged, plain):
+        assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
+
+
 @pytest.mark.parametrize('knum,alt', [(30, 2), (30, 3), (8, 2)])
 def test_soft_item_rows_equal(kal, knum, alt):
     """The soft forward's rows per work item (4 where the slot lists fit 64 KB of LDS) against
