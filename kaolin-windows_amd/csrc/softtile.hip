@@ -82,6 +82,10 @@ struct SoftTileArgs {
 #ifndef ST_EVAL_U
 #define ST_EVAL_U 2  // hits in flight per lane in the f32 evaluation: 89 VGPRs, 5 waves per SIMD (4: 115, 4)
 #endif
+#ifndef SB_HC  // the soft backward's hash: slots and copies per slot (A/B builds)
+#define SB_HC 512
+#define SB_NC 1
+#endif
 #ifndef ST_FC
 #define ST_FC 2  // candidate chunks per wave and fill step (A/B builds: EXTRA=-DST_FC=3)
 #endif
@@ -615,10 +619,11 @@ __global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restri
 // Per-face accumulation for one work item: LDS hash on the mesh-local face index with
 // the list of used slots, so the flush and the reset touch only those.  Sums are in
 // double (see FaceHash, soft_common.h): HC = 512 slots keep the workgroup near 34 KB of LDS.
-template <typename T, int HC>
+template <typename T, int HC, int NC = 1>
 struct ItemHash {
   int *key;     // [HC], -1 = empty
-  double *val;  // [HC * 6]
+  double *val;  // [HC * NC * 6]: NC copies of a face's sums, copy = lane % NC (fewer lanes of an
+                // instruction on one address: a piece's neighbouring hits share faces)
   int *used;    // [HC]
   int *nused;
   __device__ __forceinline__ int slot(int f) {
@@ -645,11 +650,12 @@ struct ItemHash {
                                       uint8_t *flags) {
     const int s = slot(f);
     if (s >= 0) {
-      atomicAdd(&val[s * 6 + c0 * 2], (double)g0x);
-      atomicAdd(&val[s * 6 + c0 * 2 + 1], (double)g0y);
+      double *v = val + (s * NC + (int)(threadIdx.x & (NC - 1))) * 6;
+      atomicAdd(&v[c0 * 2], (double)g0x);
+      atomicAdd(&v[c0 * 2 + 1], (double)g0y);
       if (c1 >= 0) {
-        atomicAdd(&val[s * 6 + c1 * 2], (double)g1x);
-        atomicAdd(&val[s * 6 + c1 * 2 + 1], (double)g1y);
+        atomicAdd(&v[c1 * 2], (double)g1x);
+        atomicAdd(&v[c1 * 2 + 1], (double)g1y);
       }
     } else {  // no free slot within the probe bound
       global_add_pair<double>(gmesh + (size_t)f * ast, c0, c1, g0x, g0y, g1x, g1y);
@@ -665,10 +671,14 @@ struct ItemHash {
     const int n = *nused;
     for (int u = tid; u < n * 6; u += nthreads) {
       const int sl = used[u / 6], c = u % 6;
-      const double v = val[sl * 6 + c];
+      double v = 0.0;  // the copies in copy order (each sum is exact: the order does not matter)
+#pragma unroll
+      for (int k = 0; k < NC; k++) {
+        v += val[(sl * NC + k) * 6 + c];
+        val[(sl * NC + k) * 6 + c] = 0.0;
+      }
       if (v != 0.0) atomicAdd(gmesh + (size_t)key[sl] * ast + c, v);
       if (c == 0 && flags) flags[key[sl]] = 1;
-      val[sl * 6 + c] = 0.0;
     }
     __syncthreads();
     for (int u = tid; u < n; u += nthreads) key[used[u]] = -1;
@@ -685,9 +695,9 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
     const uint32_t *__restrict__ rec_face, const T *__restrict__ rec_prob, const T *__restrict__ fvi, BinGeom g,
     int F, int K, float sigmainv, float multiplier, double *__restrict__ gacc, const int2 *__restrict__ items,
     const int *__restrict__ ctl, int cap, int *__restrict__ scratch, int dev, int ast, uint8_t *__restrict__ sflag) {
-  constexpr int HC = 512;
+  constexpr int HC = SB_HC, NC = SB_NC;
   __shared__ int s_key[HC];
-  __shared__ double s_val[HC * 6];
+  __shared__ double s_val[HC * NC * 6];
   __shared__ int s_used[HC];
   __shared__ int s_nused;
   __shared__ double s_a[TILE_H][64];
@@ -697,10 +707,10 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
   const int wid = threadIdx.x >> 6;  // the item's row
   const int H = g.height, W = g.width;
   for (int q = threadIdx.x; q < HC; q += blockDim.x) s_key[q] = -1;
-  for (int q = threadIdx.x; q < HC * 6; q += blockDim.x) s_val[q] = 0.0;
+  for (int q = threadIdx.x; q < HC * NC * 6; q += blockDim.x) s_val[q] = 0.0;
   if (threadIdx.x == 0) s_nused = 0;
   if (scratch && threadIdx.x == 0 && blockIdx.x == 0) *scratch = 0;
-  ItemHash<T, HC> hash{s_key, s_val, s_used, &s_nused};
+  ItemHash<T, HC, NC> hash{s_key, s_val, s_used, &s_nused};
   // the shards' item counts (ctl[s * DS_CNT_STRIDE]) and their prefix
   int nsh[DS_SHARDS], nitems = 0;
 #pragma unroll
