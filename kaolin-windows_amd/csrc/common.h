@@ -140,17 +140,26 @@ __device__ __forceinline__ double bcast(double v, int src) {
   return __longlong_as_double(((int64_t)hi << 32) | (uint32_t)lo);
 }
 
-// Exclusive prefix sum over a workgroup (<= 1024 threads): wave scans with shuffles, then
+// Inclusive prefix sum over the 64 lanes of a wave by DPP -- no LDS round trips (a __shfl_up
+// scan is six dependent ds_bpermute): row_shr 1, 2, 4, 8 within each row of 16 lanes (lanes
+// without a source keep the 0 of `old`), then lane 15's sum broadcast into rows 1 and 3 and lane
+// 31's into rows 2 and 3.  All 64 lanes must be active (an inactive source lane reads as no source).
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// Exclusive prefix sum over a workgroup (<= 1024 threads): wave scans (DPP), then
 // the wave totals in `s_wave` (>= 16 ints of LDS).  Returns the thread's exclusive prefix;
 // *total gets the workgroup sum.  Every thread must call it (two barriers).
 __device__ __forceinline__ int block_exclusive_scan(int v, int *s_wave, int *total) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-  int inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(inc, o);
-    if (lane >= o) inc += u;
-  }
+  const int inc = wave_incl_scan(v);
   if (lane == 63) s_wave[wid] = inc;
   __syncthreads();
   int before = 0, all = 0;

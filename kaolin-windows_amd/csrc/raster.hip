@@ -731,13 +731,8 @@ __global__ void __launch_bounds__(512) raster_tile_kernel(RastTileArgs<T> a) {
             wdt = (int)((pk >> 6) & 63u) - lo + 1;
           }
         }
-        int inc = wdt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int u = __shfl_up(inc, o);
-          if (lane >= o) inc += u;
-        }
-        const int total = __shfl(inc, 63);
+        const int inc = wave_incl_scan(wdt);
+        const int total = __builtin_amdgcn_readlane(inc, 63);
         if (total == 0) continue;
         s_pre[wid * 64 + lane] = ((inc - wdt) << 8) | lo;
         __builtin_amdgcn_wave_barrier();

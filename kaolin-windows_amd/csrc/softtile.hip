@@ -329,12 +329,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
   }
   if (qi == 0) {
     if (!px_valid) kid = 0;
-    int pre = kid;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(pre, o);
-      if (lane >= o) pre += u;
-    }
+    const int pre = wave_incl_scan(kid);
     s_pre[lane] = pre - kid;
     if (lane == 63) s_pre[64] = pre;
   }
@@ -508,13 +503,8 @@ __global__ void __launch_bounds__(256) soft_tile_eval_kernel(SoftTileArgs<T> a) 
   const bool px_valid = i < W;
   const size_t pix = ((size_t)b * H + j) * W + (px_valid ? i : W - 1);
   const int kid = px_valid ? (int)a.hits[pix] : 0;
-  int pre = kid;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(pre, o);
-    if (lane >= o) pre += u;
-  }
-  const int total = __shfl(pre, 63);
+  const int pre = wave_incl_scan(kid);
+  const int total = __builtin_amdgcn_readlane(pre, 63);
   if (total == 0) return;
   s_pre[lane] = pre - kid;
   __builtin_amdgcn_wave_barrier();
@@ -742,12 +732,7 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
         // the reference's  -1.0 * sigmainv * dLdp * (1.0 - allprob), evaluated left to right
         if (kid) s_a[wid][lane] = -1.0 * (double)sigmainv * (double)grad[p] * (1.0 - (double)mask[p]);
       }
-      int pre = kid;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int u = __shfl_up(pre, o);
-        if (lane >= o) pre += u;
-      }
+      const int pre = wave_incl_scan(kid);
       s_pre[wid][lane] = pre - kid;
       if (lane == 63) s_rowpre[wid + 1] = pre;
     }

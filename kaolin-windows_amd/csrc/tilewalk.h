@@ -75,14 +75,9 @@ struct ChunkSeq {
     const int w = g * 64 + lane;
     wv = w < nwords ? words[(size_t)w * stride] : 0u;
     const int c = __popc(wv);
-    int inc = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int u = __shfl_up(inc, o);
-      if (lane >= o) inc += u;
-    }
+    const int inc = wave_incl_scan(c);
     pc = inc - c;
-    gtot = __shfl(inc, 63);
+    gtot = __builtin_amdgcn_readlane(inc, 63);
   }
   __device__ __forceinline__ void init(const uint32_t *w, int n, size_t st, int lane) {
     words = w;
