@@ -127,6 +127,30 @@ __device__ __forceinline__ T wave_max(T v) {
   }
   return v;
 }
+// wave_max by DPP for 32-bit values (a running maximum within rows of 16 lanes, then the row 15 / 31
+// broadcasts; lane 63's result read back as a scalar) -- no LDS round trips.  All 64 lanes must be
+// active.  NaN: like `u > v ? u : v`, a NaN is kept only where it entered first, so callers pass
+// no NaN (p2m's thresholds are finite or +inf).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_max_step(float v) {
+  const float u = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, ROW_MASK, 0xf,
+                                                             false));
+  return u > v ? u : v;
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = dpp_max_step<0x111, 0xf>(v);  // row_shr:1
+  v = dpp_max_step<0x112, 0xf>(v);  // row_shr:2
+  v = dpp_max_step<0x114, 0xf>(v);  // row_shr:4
+  v = dpp_max_step<0x118, 0xf>(v);  // row_shr:8
+  v = dpp_max_step<0x142, 0xa>(v);  // row_bcast:15
+  v = dpp_max_step<0x143, 0xc>(v);  // row_bcast:31
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+template <typename T>
+__device__ __forceinline__ T wave_max_all(T v) {
+  if constexpr (sizeof(T) == 4) return wave_max_dpp(v);
+  else return wave_max(v);
+}
 
 // Broadcast lane `src` (wave-uniform) of v to all lanes through the scalar unit.
 __device__ __forceinline__ float bcast(float v, int src) {

@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
       if (thr != thr || !valid) thr = valid ? (T)INFINITY : (T)0;
       if (share) thr = fmin(thr, (T)shared_thr);
       if (pairs) thr = valid ? pthr : (T)0;
-      const T thr_max = wave_max(thr);
+      const T thr_max = wave_max_all(thr);  // (every lane active: the chunk loop is wave-uniform)
       const int s = s0 + lane;
       bool eval = s < n;
       if (eval && all_fin && (pairs || ((start + s) & 511) != 0) && thr_max < (T)INFINITY) {
@@ -552,7 +552,7 @@ __global__ void __launch_bounds__(256) p2m_fwd_grec_kernel(const T *__restrict__
     if (thr != thr || !valid) thr = valid ? (T)INFINITY : (T)0;
     if (share && valid && (start & 127) == 0)
       thr = fmin(thr, (T)__uint_as_float(__hip_atomic_load(gbest + si, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
-    const T thr_max = wave_max(thr);
+    const T thr_max = wave_max_all(thr);  // (every lane active: the chunk loop is wave-uniform)
     const int64_t f = start + lane;
     bool eval = lane < n;
     if (eval && all_fin && (f & 511) != 0 && thr_max < (T)INFINITY) {

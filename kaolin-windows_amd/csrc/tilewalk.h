@@ -7,8 +7,7 @@
 
 namespace kl {
 
-// Lane exchange v <- v[lane ^ S] with cross-lane VALU ops (gfx950 permlane swaps, DPP)
-// where they exist and ds_swizzle (no memory access) for xor 4.
+// Lane exchange v <- v[lane ^ S] with cross-lane VALU ops (gfx950 permlane swaps, DPP).
 template <int S>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lane) {
   if constexpr (S == 32) {
@@ -20,7 +19,11 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t v, int lane) {
   } else if constexpr (S == 8) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
   } else if constexpr (S == 4) {
-    return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (4 << 10) | 0x1f);  // bitmask mode, xor 4
+    // lanes with bit 2 clear read lane + 4 (row_ror:12), the others lane - 4 (row_ror:4): two DPP
+    // moves and a select, no LDS pipe (r05; ds_swizzle before)
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+    const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12c, 0xf, 0xf, false);  // row_ror:12
+    return (lane & 4) ? dn : up;
   } else if constexpr (S == 2) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
   } else {
