@@ -178,6 +178,17 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   return v;
 }
 
+// The same within each 32-lane half of the wave (the row 15 broadcast only: rows 1 and 3 take the
+// sums of rows 0 and 2).  All 64 lanes must be active.
+__device__ __forceinline__ int wave_incl_scan32(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  return v;
+}
+
 // Exclusive prefix sum over a workgroup (<= 1024 threads): wave scans (DPP), then
 // the wave totals in `s_wave` (>= 16 ints of LDS).  Returns the thread's exclusive prefix;
 // *total gets the workgroup sum.  Every thread must call it (two barriers).

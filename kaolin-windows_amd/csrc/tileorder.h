@@ -67,12 +67,8 @@ __device__ __forceinline__ void place_prefix(int *sb, int *sx, const int *lpb, c
   if (threadIdx.x < 8 * ORD_BUCKETS) {
     const int t = threadIdx.x, g = t / ORD_BUCKETS, q = ORD_BUCKETS - 1 - t % ORD_BUCKETS;
     const int v = lpb[q] < 0 ? 0 : ghist[g * ORD_BUCKETS + q] << lpb[q];  // items of (band g, bucket q)
-    int inc = v;
-#pragma unroll
-    for (int o = 1; o < ORD_BUCKETS; o <<= 1) {
-      const int w = __shfl_up(inc, o);
-      if (t % ORD_BUCKETS >= o) inc += w;
-    }
+    static_assert(ORD_BUCKETS == 32, "the segmented scan is per 32-lane half");
+    const int inc = wave_incl_scan32(v);  // (threads < 256: four whole waves)
     sb[g * ORD_BUCKETS + q] = inc - v;
     if (q == 0) sx[8 + g] = inc;  // items of band g
   }
@@ -186,18 +182,16 @@ __device__ __forceinline__ void soft_parts(int *sx, int *lpb, const int *__restr
 #pragma unroll
       for (int g = 0; g < 8; g++) h += ghist[g * ORD_BUCKETS + lane];
     }
-    auto suffix = [&](int v) {  // sum over lanes lane..31
-#pragma unroll
-      for (int o = 1; o < ORD_BUCKETS; o <<= 1) {
-        const int u = __shfl_down(v, o);
-        if (lane + o < ORD_BUCKETS) v += u;
-      }
-      return v;
+    auto suffix = [&](int v) {  // sum over lanes lane..31: the lanes' total less the prefix before
+      const int inc = wave_incl_scan32(v);  // (lanes 32..63 hold 0)
+      return __builtin_amdgcn_readlane(inc, ORD_BUCKETS - 1) - inc + v;
     };
     const bool e8 = lane < ORD_BUCKETS && lane >= sp.b8;
-    const bool acc8 = e8 && suffix(e8 ? h : 0) <= sp.cap8;
+    const int s8 = suffix(e8 ? h : 0);  // (every lane of the wave: the scans are DPP)
+    const bool acc8 = e8 && s8 <= sp.cap8;
     const bool e4 = lane < ORD_BUCKETS && lane >= sp.b4 && !acc8;
-    const bool acc4 = e4 && suffix(e4 ? h : 0) <= sp.cap4;
+    const int s4 = suffix(e4 ? h : 0);
+    const bool acc4 = e4 && s4 <= sp.cap4;
     int lp = lp_min;
     if (acc8) lp = lp > 3 ? lp : 3;
     else if (acc4) lp = lp > 2 ? lp : 2;
