@@ -37,6 +37,7 @@ def main():
           f'won px {won_tot.sum()} (small faces {won_tot[small].sum()})')
     iters = 0
     iters_bal = 0
+    iters_round = 0
     rounds_tot = 0
     won_sum = 0
     nw = (B * F + 7) // 8
@@ -61,19 +62,23 @@ def main():
         # per round: each face's lanes s take elements round*8*GB + s + 8*u, u < GB
         for rr in range(R):
             mx = 0
+            mxb = 0
             for pad in per_face_lane:
                 seg = pad[rr * 8 * GB:(rr + 1) * 8 * GB]
                 if seg.size == 0:
                     continue
                 lanes = seg.reshape(GB, 8).sum(0)
                 mx = max(mx, lanes.max())
+                mxb = max(mxb, -(-int(seg.sum()) // 8))
             iters += mx
+            iters_round += mxb
         rounds_tot += R
         # balanced: each face's won pixels spread over its 8 lanes, the wave runs max over faces
         iters_bal += max(-(-int(p.sum()) // 8) for p in per_face_lane)
     print(f'GATHER_BATCH {GB}: waves with work {nw}, rounds {rounds_tot}, add iterations {iters}, '
           f'lane utilisation {won_sum / max(1, iters * 64):.3f}; balanced per face: iterations {iters_bal}, '
-          f'utilisation {won_sum / max(1, iters_bal * 64):.3f}')
+          f'utilisation {won_sum / max(1, iters_bal * 64):.3f}; balanced per face and round: iterations '
+          f'{iters_round}, utilisation {won_sum / max(1, iters_round * 64):.3f}')
 
 
 if __name__ == '__main__':
