@@ -82,6 +82,9 @@ struct SoftTileArgs {
 #ifndef ST_EVAL_U
 #define ST_EVAL_U 2  // hits in flight per lane in the f32 evaluation: 89 VGPRs, 5 waves per SIMD (4: 115, 4)
 #endif
+#ifndef SB_MIN_WAVES  // the soft backward's minimum waves per SIMD (A/B builds)
+#define SB_MIN_WAVES 1
+#endif
 #ifndef SB_HC  // the soft backward's hash: slots and copies per slot (A/B builds)
 #define SB_HC 512
 #define SB_NC 1
@@ -680,7 +683,7 @@ struct ItemHash {
 // a = -sigmainv * dLdp * (1 - allprob)), then every thread takes one hit of the piece:
 // its record, the reference's terms (soft_hit_grad), summed per face in the item hash.
 template <typename T>
-__global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
+__global__ void __launch_bounds__(512, SB_MIN_WAVES) soft_tile_bwd_kernel(
     const T *__restrict__ grad, const T *__restrict__ mask, const uint8_t *__restrict__ hits,
     const uint32_t *__restrict__ rec_face, const T *__restrict__ rec_prob, const T *__restrict__ fvi, BinGeom g,
     int F, int K, float sigmainv, float multiplier, double *__restrict__ gacc, const int2 *__restrict__ items,
@@ -715,8 +718,14 @@ __global__ void __launch_bounds__(512) soft_tile_bwd_kernel(
   for (int q = (int)blockIdx.x;; q += (int)gridDim.x) {
     __syncthreads();  // the previous item's hash reset is done
     if (q >= nitems) return;
+    // the item's shard and index in it (unrolled over the shards: nsh stays in registers, no scratch)
     int sh = 0, qq = q;
-    while (qq >= nsh[sh]) qq -= nsh[sh++];
+#pragma unroll
+    for (int k = 0; k < DS_SHARDS - 1; k++)
+      if (sh == k && qq >= nsh[k]) {
+        qq -= nsh[k];
+        sh = k + 1;
+      }
     const int2 it = items[(size_t)sh * cap + qq];
     const int tile = it.x & 0xffffff, part = (it.x >> 24) & 15, lp = (it.x >> 28) & 7;
     const int RP = TILE_H >> lp;  // rows of the item
@@ -890,6 +899,9 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   return KL_OK;
 }
 
+// persistent backward workgroups per CU (dev param 27 overrides; 4 fit by LDS and registers)
+static int sb_wgs_per_cu() { return g_dev_param[27] > 0 ? g_dev_param[27] : 3; }
+
 // workspace: item counters (DS_SHARDS, one used) | items | the (B,F,3,2) double accumulator
 constexpr size_t SB_CTL_BYTES = DS_SHARDS * DS_CNT_STRIDE * sizeof(int);
 static size_t soft_bwd_acc_offset(int B, int H, int W, int K) {
@@ -937,7 +949,7 @@ int soft_tile_backward(int B, int H, int W, int F, int K, const T *grad, const T
   if (hipGetDevice(&dev_id) == hipSuccess)
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_id);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
-  const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
+  const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * sb_wgs_per_cu()));
   hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
                      (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, acc,
                      (const int2 *)items, (const int *)ctl, 0, s.scratch, g_dev_flags, 6, (uint8_t *)nullptr);
@@ -960,7 +972,7 @@ int soft_tile_backward_listed(int B, int H, int W, int F, int K, const T *grad, 
   if (hipGetDevice(&dev_id) == hipSuccess)
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev_id);
   const int nt = g.batch * g.tiles_y * g.tiles_x;
-  const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * 3));
+  const unsigned grid = (unsigned)std::max(1, std::min(nt * (K + 1), ncu * sb_wgs_per_cu()));
   hipLaunchKernelGGL((soft_tile_bwd_kernel<T>), dim3(grid), dim3(512), 0, st, grad, mask, (const uint8_t *)s.hits,
                      (const uint32_t *)s.rec_face, (const T *)s.rec_prob, fvi, g, F, K, sigmainv, m, acc, items, cnt,
                      cap, (int *)nullptr, g_dev_flags, DS_ACC_STRIDE, sflag);
