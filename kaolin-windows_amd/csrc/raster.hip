@@ -1277,6 +1277,13 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
 //    workgroups of the same grid (a scan of the ranges, then the whole workgroup per face), so
 //    no second launch is needed when there are none.
 constexpr int G2_BIG_BLOCKS = 64;
+// Row stride of a wave's partials (doubles).  65, not 64: the final sums read value q = s, s + 8
+// of a face's 8 lanes, and at a stride of 64 doubles (128 dwords, 0 mod the 64 banks) the 8 lanes
+// of a face group and the groups 8 lanes apart all land on the same bank pair.
+#ifndef KL_G2_PAD  // A/B builds only
+#define KL_G2_PAD 0
+#endif
+constexpr int G2_PS = 64 + KL_G2_PAD;
 
 template <typename T, int MAXD, bool ATOM = false>
 __device__ __forceinline__ void g2_add(double *__restrict__ part, const T v[6], const T *__restrict__ c, int D, T wa,
@@ -1290,31 +1297,31 @@ __device__ __forceinline__ void g2_add(double *__restrict__ part, const T v[6], 
     for (int d = 0; d < MAXD; d++) {
       if (d < D) {
         const T gd = gv[d];
-        atomicAdd(&part[(6 + d) * 64], (double)(gd * wa));
-        atomicAdd(&part[(6 + MAXD + d) * 64], (double)(gd * wb));
-        atomicAdd(&part[(6 + 2 * MAXD + d) * 64], (double)(gd * wc));
+        atomicAdd(&part[(6 + d) * G2_PS], (double)(gd * wa));
+        atomicAdd(&part[(6 + MAXD + d) * G2_PS], (double)(gd * wb));
+        atomicAdd(&part[(6 + 2 * MAXD + d) * G2_PS], (double)(gd * wc));
         T o[6];
         bg.terms(gd, c[d], c[D + d], c[2 * D + d], o);
 #pragma unroll
-        for (int q = 0; q < 6; q++) atomicAdd(&part[q * 64], (double)o[q]);
+        for (int q = 0; q < 6; q++) atomicAdd(&part[q * G2_PS], (double)o[q]);
       }
     }
     return;
   }
-  // part: this thread's partials, value q at part[q * 64] (LDS no other thread touches until the sums)
+  // part: this thread's partials, value q at part[q * G2_PS] (LDS no other thread touches until the sums)
   BaryGrad<T> bg;
   bg.init(v, wa, wb, wc, eps);
 #pragma unroll
   for (int d = 0; d < MAXD; d++) {
     if (d < D) {
       const T gd = gv[d];
-      part[(6 + d) * 64] += (double)(gd * wa);
-      part[(6 + MAXD + d) * 64] += (double)(gd * wb);
-      part[(6 + 2 * MAXD + d) * 64] += (double)(gd * wc);
+      part[(6 + d) * G2_PS] += (double)(gd * wa);
+      part[(6 + MAXD + d) * G2_PS] += (double)(gd * wb);
+      part[(6 + 2 * MAXD + d) * G2_PS] += (double)(gd * wc);
       T o[6];
       bg.terms(gd, c[d], c[D + d], c[2 * D + d], o);
 #pragma unroll
-      for (int q = 0; q < 6; q++) part[q * 64] += (double)o[q];
+      for (int q = 0; q < 6; q++) part[q * G2_PS] += (double)o[q];
     }
   }
 }
@@ -1353,7 +1360,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
   // dev (param 17) opts bit 1: no soft / flag re-zeroing, bit 2: soft read unflagged (timing only)
   const bool rz = !(opts & 2), nofl = opts & 4;
   constexpr int NV = 6 + 3 * MAXD;
-  __shared__ double s_part[4][NV][64];  // per wave: per lane (thread) partial sums, value-major
+  __shared__ double s_part[4][NV][G2_PS];  // per wave: per lane (thread) partial sums, value-major
   __shared__ int s_nbig;
   __shared__ int s_big[256];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1368,7 +1375,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
     // ---- large faces: scan a slice of the faces, then one face at a time with the workgroup;
     //      its 256 partials added in thread order
 #pragma unroll
-    for (int q = 0; q < NV; q++) part[q * 64] = 0.0;
+    for (int q = 0; q < NV; q++) part[q * G2_PS] = 0.0;
     const int64_t per = (nf + nbig - 1) / nbig;
     const int64_t f0 = (int64_t)blockIdx.x * per, f1 = f0 + per < nf ? f0 + per : nf;
     for (int64_t base = f0; base < f1; base += 256) {
@@ -1415,7 +1422,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
         }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < NV; q++) part[q * 64] = 0.0;
+        for (int q = 0; q < NV; q++) part[q * G2_PS] = 0.0;
       }
       __syncthreads();  // s_nbig / s_big are rewritten
     }
@@ -1444,7 +1451,7 @@ __global__ void __launch_bounds__(256) rasterize_bwd_gather2_kernel(
   }
   if (!__any(act)) return;  // wave-uniform
 #pragma unroll
-  for (int q = 0; q < NV; q++) part[q * 64] = 0.0;
+  for (int q = 0; q < NV; q++) part[q * G2_PS] = 0.0;
   // lane s < 6's soft-mask sum, loaded now so that its latency hides behind the walk
   double soft_v = 0.0;
   if (act && fl && s < 6) soft_v = soft[tf * DS_ACC_STRIDE + s];
