@@ -1277,9 +1277,10 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
 //    workgroups of the same grid (a scan of the ranges, then the whole workgroup per face), so
 //    no second launch is needed when there are none.
 constexpr int G2_BIG_BLOCKS = 64;
-// Row stride of a wave's partials (doubles).  65, not 64: the final sums read value q = s, s + 8
-// of a face's 8 lanes, and at a stride of 64 doubles (128 dwords, 0 mod the 64 banks) the 8 lanes
-// of a face group and the groups 8 lanes apart all land on the same bank pair.
+// Row stride of a wave's partials (doubles).  The final sums read value q = s, s + 8 of a face's
+// 8 lanes; at a stride of 64 doubles (128 dwords, 0 mod the 64 banks) those reads share a bank
+// pair.  r05as A/B (KL_G2_PAD=1: stride 65): LDS bank-conflict share 0.19 -> 0.15 but the kernel
+// 49.6 against 48.6 us, cfg3 eager 5,590-5,783 against 5,739-5,763 Mpixels/s -- kept at 64.
 #ifndef KL_G2_PAD  // A/B builds only
 #define KL_G2_PAD 0
 #endif
