@@ -61,6 +61,9 @@ def parse_args(argv=None):
     ap.add_argument('--no-p2m', action='store_true')
     ap.add_argument('--no-extra', action='store_true', help='skip the cfg4 / raytrace / cfg1 / deftet / check_sign legs')
     ap.add_argument('--eager', action='store_true', help='time the eager step only (no HIP graph capture)')
+    ap.add_argument('--collectives', action='store_true',
+                    help='N=1: initialise a one-rank RCCL group and keep the loss all_gather (and the p2m leg\'s '
+                         'gathers / face-gradient all_reduce) in the timed steps, as the N-GPU job times them')
     return ap.parse_args(argv)
 
 
@@ -148,10 +151,40 @@ def views_for_rank(rank, world, per_rank):
     return [2 * math.pi * (rank * per_rank + k) / n for k in range(per_rank)]
 
 
+def collectives_on():
+    """An initialised process group (N > 1, or N = 1 with --collectives): the step's collectives run."""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized()
+
+
+_PENDING = []  # the previous step's loss gather (out, work), at most one in flight
+
+
 def gather_losses(loss, world):
-    """The step's only collective: all_gather of the per-shard scalar losses."""
+    """The step's only collective: all_gather of the per-shard scalar losses (RCCL whenever a
+    process group is initialised, at N = 1 too under --collectives).  Issued asynchronously; the
+    previous step's gather is waited for here, after this step's kernels are queued, so that the
+    gather's latency overlaps this step instead of sitting between steps.  timed_loop drains the
+    last one inside the timed region (drain_gathers), so every step's gather is timed."""
     from kaolin.distributed import gather_losses as gl
-    return gl(loss) if world > 1 else loss.detach().reshape(1)
+    if not collectives_on():
+        return loss.detach().reshape(1)
+    out, work = gl(loss, async_op=True)
+    if work is not None and not out.is_cuda:  # gloo on host tensors: the caller reads them now
+        work.wait()
+        work = None
+    prev = _PENDING.pop() if _PENDING else None
+    _PENDING.append((out, work))
+    if prev is not None and prev[1] is not None:
+        prev[1].wait()
+    return out
+
+
+def drain_gathers():
+    while _PENDING:
+        _, work = _PENDING.pop()
+        if work is not None:
+            work.wait()
 
 
 def max_over_ranks(elapsed, device, world):
@@ -174,8 +207,8 @@ def per_rank(elapsed, device, world):
 def process_group_info(world):
     """What the initialised process group says (not the environment): world size, backend."""
     import torch.distributed as dist
-    if world == 1 or not dist.is_initialized():
-        return {'initialized': dist.is_available() and dist.is_initialized(), 'world_size': 1, 'backend': None}
+    if not collectives_on():
+        return {'initialized': False, 'world_size': 1, 'backend': None}
     return {'initialized': True, 'world_size': dist.get_world_size(), 'backend': str(dist.get_backend())}
 
 
@@ -195,6 +228,7 @@ def timed_loop(fn, steps, world, device=None):
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
+    drain_gathers()
     _sync(device)
     if world > 1:
         dist.barrier()
@@ -290,7 +324,7 @@ def dibr_compute(inp, g_feat=None, g_mask=None):
 
 def dibr_step(inp, world):
     out = dibr_compute(inp)
-    if world > 1:  # per-shard losses all-gathered over RCCL / xGMI
+    if collectives_on():  # per-shard losses all-gathered over RCCL / xGMI
         gather_losses(out[0], world)
     return out
 
@@ -312,7 +346,7 @@ def graphed_step(inp, world):
 
     def step():
         graph.replay()
-        if world > 1:
+        if collectives_on():
             gather_losses(static_out[0], world)
         return static_out
     return step, static_out
@@ -567,7 +601,8 @@ def dibr_headline(args, world, rank, device):
         'data': f'synthetic (seeded UV sphere, {cfg["views"]} views/GPU)',
         'config': {'workload': cfg['workload'], 'config': args.config, 'global_batch': cfg['views'] * world,
                    'height': cfg['H'], 'width': cfg['W'], 'faces': 50000,
-                   'parallelism': f'batch-sharded x{world} (RCCL all_gather of per-shard losses)'},
+                   'parallelism': f'batch-sharded x{world} (RCCL all_gather of per-shard losses)'
+                                  + ('' if pg['initialized'] else ' -- N=1 without a process group: no collective in the step')},
         'roofline': {'bound': 'hbm', 'kernel': dom, 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS,
                      'unit': 'GB/s', 'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': pmc_traffic(dom, args.config),
                      'bytes_per_launch': dbytes, 'avg_launch_ms': round(ops_ms[dom], 4),
@@ -1209,17 +1244,39 @@ def cpu_selftest(args, world, rank):
         dist.all_gather_object(flags, ok)
     if rank == 0:
         res['parity_all_ranks'] = all(flags)
-        print(json.dumps({'metric': 'cpu self-test (sharded point_to_mesh_distance over gloo)', 'n_ranks': world,
-                          'steps': args.steps, 'p2m': res}))
+        emit({'metric': 'cpu self-test (sharded point_to_mesh_distance over gloo)', 'n_ranks': world,
+              'steps': args.steps, 'p2m': res})
     return 0 if all(flags) else 1
 
 
 # ----------------------------------------------------------------------------- main
+_LINE_OUT = None
+
+
+def emit(obj):
+    """The one JSON line, on the process's original stdout (library chatter went to stderr)."""
+    out = _LINE_OUT or sys.stdout
+    out.write(json.dumps(obj) + '\n')
+    out.flush()
+
+
+def _guard_stdout():
+    """Send everything written to fd 1 from here on to stderr, keeping the original stdout for the
+    JSON line: RCCL prints its version banner on stdout at communicator setup (seen on the GPU box,
+    gpurun_out/r06a), once per rank under torchrun, and the driver reads rank 0's stdout as ONE line."""
+    global _LINE_OUT
+    if _LINE_OUT is None:
+        sys.stdout.flush()
+        _LINE_OUT = os.fdopen(os.dup(1), 'w')
+        os.dup2(2, 1)
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
     if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
         return launch_ranks(args.gpus, argv)
+    _guard_stdout()
     world = int(os.environ.get('WORLD_SIZE', '1'))
     if world != args.gpus:
         print(f'bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; refusing to time a different job',
@@ -1259,6 +1316,10 @@ def main(argv=None):
         for kv in os.environ['KAOLIN_DEV_PARAMS'].split(','):
             k, v = kv.split('=')
             lib.kl_dev_set_param(int(k), int(v))
+    if world == 1 and args.collectives:  # a one-rank RCCL group on 127.0.0.1 (no launcher)
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', str(_free_port()))
+        dist.init_process_group('nccl', device_id=device, rank=0, world_size=1)
     if world > 1:
         if shared:
             dist.init_process_group('gloo')
@@ -1306,8 +1367,8 @@ def main(argv=None):
         result['cpu_baseline'] = cpu
         result['cpu_host'] = cpu_info()
     if rank == 0:
-        print(json.dumps(result))
-    if world > 1:
+        emit(result)
+    if collectives_on():
         dist.barrier()
         dist.destroy_process_group()
     return 0

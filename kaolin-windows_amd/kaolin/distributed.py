@@ -57,12 +57,20 @@ def shard_bounds(n, rank, world):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def _active():
+    """An initialised process group: the sharded paths then run their collectives, at world size 1
+    too (an RCCL group of one rank runs every all_gather / all_reduce / all_to_all on the device, so
+    the collective path is exercised on a one-GPU box, tests/test_gpu_rccl.py).  Without one, the
+    helpers call the unsharded op."""
+    return dist.is_available() and dist.is_initialized()
+
+
 def _world(group):
-    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+    return dist.get_world_size(group) if _active() else 1
 
 
 def _rank(group):
-    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+    return dist.get_rank(group) if _active() else 0
 
 
 def _staged(t, group):
@@ -107,14 +115,25 @@ def _all_gather_flat(out, t, group):
         dist.all_gather_into_tensor(out, t, group=group)
 
 
-def gather_losses(loss, group=None):
-    """All-gather one scalar loss per rank -> (world,) in rank order."""
+def gather_losses(loss, group=None, async_op=False):
+    """All-gather one scalar loss per rank -> (world,) in rank order.
+
+    ``async_op=True`` returns ``(out, work)``: ``out`` holds the losses once ``work.wait()`` has
+    returned (RCCL: the caller's current stream then waits for the gather; ``work`` is None when
+    the gather already completed, as with no process group or gloo's host-staged path).  A training
+    loop waits for step k's gather after queueing step k + 1, so the gather's latency over xGMI
+    overlaps the next step's kernels instead of sitting between the steps."""
     world = _world(group)
-    if world == 1:
-        return loss.detach().reshape(1)
-    out = [torch.empty_like(loss) for _ in range(world)]
-    _all_gather(out, loss.detach(), group)
-    return torch.stack(out)
+    flat = loss.detach().reshape(1)
+    if not _active():
+        return (flat, None) if async_op else flat
+    out = flat.new_empty(world)
+    work = None
+    if _staged(flat, group):
+        _all_gather_flat(out, flat, group)
+    else:
+        work = dist.all_gather_into_tensor(out, flat, group=group, async_op=async_op)
+    return (out, work) if async_op else out
 
 
 def allreduce_grads(params, group=None, average=False):
@@ -127,7 +146,7 @@ def allreduce_grads(params, group=None, average=False):
     sums, as sharded_point_to_mesh_distance does)."""
     world = _world(group)
     params = [p for p in params if p.requires_grad]
-    if world == 1 or not params:
+    if not _active() or not params:
         return
     buckets = {}
     for p in params:
@@ -287,7 +306,7 @@ def sharded_batched_point_to_mesh_distance(pointclouds, face_vertices, group=Non
     reach both inputs for every element (each rank's elements' gradients are all-gathered), so
     every rank holds the unsharded gradients, bit for bit."""
     world, rank = _world(group), _rank(group)
-    if world == 1:
+    if not _active():
         from .metrics.trianglemesh import point_to_mesh_distance
         return point_to_mesh_distance(pointclouds, face_vertices)
     B = pointclouds.shape[0]
@@ -321,15 +340,29 @@ class _ShardedSided(torch.autograd.Function):
         # rank's share and its gradient stays local.
         lp = (p1[:, lo:hi] if full else p1).contiguous()
         p2c = p2.contiguous()
-        d, i = _sided_forward(lp, p2c)
-        ctx.save_for_backward(lp, p2c, i)
         ctx.lo, ctx.sizes, ctx.group, ctx.full = lo, sizes, group, full
+        # the double-sum backward takes float32 / float64 GPU inputs; any other dtype (float16: the
+        # unsharded op's half atomics) replays the shard's own graph and all-reduces its float grad_p2
+        ctx.exact = not p1.is_cuda or p1.dtype in (torch.float32, torch.float64)
+        if ctx.exact:
+            d, i = _sided_forward(lp, p2c)
+            ctx.save_for_backward(lp, p2c, i)
+        else:
+            from .metrics.pointcloud import sided_distance
+            with torch.enable_grad():
+                lpg = lp.detach().requires_grad_(p1.requires_grad)
+                p2g = p2c.detach().requires_grad_(p2.requires_grad)
+                d, i = sided_distance(lpg, p2g)
+            ctx.local = (lpg, p2g, d)
+            d = d.detach()
         out_i = _all_gather_points(i, sizes, group)
         ctx.mark_non_differentiable(out_i)
         return _all_gather_points(d, sizes, group), out_i
 
     @staticmethod
     def backward(ctx, g_dist, g_idx):
+        if not ctx.exact:
+            return _ShardedSided._replayed_backward(ctx, g_dist)
         lp, p2, i = ctx.saved_tensors
         n = lp.shape[1]
         g1, sums = _sided_backward_sums(g_dist[:, ctx.lo:ctx.lo + n].contiguous(), lp, p2, i)
@@ -343,6 +376,29 @@ class _ShardedSided(torch.autograd.Function):
             g1 = _all_gather_points(g1, ctx.sizes, ctx.group)
         return g1, g2, None, None, None, None, None
 
+    @staticmethod
+    def _replayed_backward(ctx, g_dist):
+        """The shard's sided_distance graph replayed (its own dtype's backward); grad_p2 all-reduced
+        in the input dtype: the unsharded gradient up to the summation order of its atomics."""
+        lp, p2, d = ctx.local
+        n = lp.shape[1]
+        inputs = [x for x in (lp, p2) if x.requires_grad]
+        grads = torch.autograd.grad(d, inputs, g_dist[:, ctx.lo:ctx.lo + n].contiguous(), allow_unused=True) \
+            if inputs else []
+        it = iter(grads)
+        g1 = next(it) if lp.requires_grad else None
+        g2 = next(it) if p2.requires_grad else None
+        if ctx.needs_input_grad[1]:
+            g2 = torch.zeros_like(p2) if g2 is None else g2.contiguous()
+            _all_reduce(g2, dist.ReduceOp.SUM, ctx.group)
+        else:
+            g2 = None
+        if not ctx.needs_input_grad[0]:
+            g1 = None
+        elif g1 is not None and ctx.full:
+            g1 = _all_gather_points(g1.contiguous(), ctx.sizes, ctx.group)
+        return g1, g2, None, None, None, None, None
+
 
 def sharded_sided_distance(local_p1, p2, group=None):
     r"""sided_distance(p1, p2) with p1's points split over the ranks of ``group``.
@@ -354,8 +410,7 @@ def sharded_sided_distance(local_p1, p2, group=None):
     per-point float terms and rounded once (GPU, float32 / float64), which is the unsharded
     backward's (itself a double sum rounded once, _C.sided_distance_backward_cuda) up to the
     documented one-ulp allowance."""
-    world = _world(group)
-    if world == 1:
+    if not _active():
         from .metrics.pointcloud import sided_distance
         return sided_distance(local_p1, p2)
     sizes = _sizes(local_p1.shape[1], local_p1.device, group)
@@ -372,7 +427,7 @@ def sharded_chamfer_distance(p1, p2, w1=1., w2=1., squared=True, group=None):
     sums)."""
     from .metrics.pointcloud import chamfer_distance, _chamfer_from_sided
     world, rank = _world(group), _rank(group)
-    if world == 1:
+    if not _active():
         return chamfer_distance(p1, p2, w1, w2, squared)
     n, m = p1.shape[1], p2.shape[1]
     lo1, hi1 = shard_bounds(n, rank, world)
@@ -397,8 +452,7 @@ def sharded_point_to_mesh_distance(local_points, face_vertices, group=None):
     reference's torch path, whose autograd sums in float) the ranks' float gradients are added:
     equal to the unsharded gradient up to float summation order.
     """
-    world = _world(group)
-    if world == 1:
+    if not _active():
         from .metrics.trianglemesh import point_to_mesh_distance
         d, i, t = point_to_mesh_distance(local_points.unsqueeze(0), face_vertices.unsqueeze(0))
         return d[0], i[0], t[0]
@@ -419,7 +473,7 @@ def sharded_unbatched_raytrace(octree, point_hierarchy, pyramid, exsum, origin, 
     lo, hi = shard_bounds(origin.shape[0], rank, world)
     out = unbatched_raytrace(octree, point_hierarchy, pyramid, exsum, origin[lo:hi], direction[lo:hi], level,
                              return_depth=return_depth, with_exit=with_exit)
-    if world == 1:
+    if not _active():
         return out
     ridx = out[0] + lo
     sizes = _sizes(ridx.shape[0], ridx.device, group)
@@ -441,7 +495,7 @@ def sharded_trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin=Non
     grid on every rank."""
     from .ops.conversions.trianglemesh import trianglemeshes_to_voxelgrids
     world, rank = _world(group), _rank(group)
-    if world == 1:
+    if not _active():
         return trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin, scale)
     if origin is None:
         origin = torch.min(vertices, dim=1)[0]
