@@ -402,21 +402,51 @@ OP_KERNELS = {
 }
 
 
+# the sub-lines' kernels, each launched once per timed call (hipCUB's sorts / scans, shared by several
+# legs, are left out of their traffic: `traffic_scope` says so)
+SUB_KERNELS = {
+    'deftet': ('deftet_tilebox_kernel', 'deftet_fwd_kernel', 'deftet_resolve_slots_kernel', 'deftet_bwd_keys_kernel',
+               'deftet_bwd_gather_kernel'),
+    'check_sign': ('cs_prep_kernel', 'cs_bin_kernel<false', 'cs_pcount_kernel', 'cs_units_kernel',
+                   'cs_bin_kernel<true', 'cs_pscatter_kernel', 'cs_cell_check_kernel', 'cs_finalize_kernel'),
+    'cfg1_sided': ('sided_fwd_kernel<float', 'sided_combine_kernel<float'),
+    'soft_mask_C': ('soft_mask_fwd_kernel<float',),
+}
+
+
 def pmc_traffic(op, config):
-    """HBM bytes per call of `op` from the committed PMC summary (scripts/pmc_traffic.py), or None
-    (the summary was measured on the cfg3 workload only)."""
-    path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
-    if config != 'cfg3' or op not in OP_KERNELS or not os.path.exists(path):
+    """HBM bytes per call of `op` from the committed PMC summary of the config's workload
+    (scripts/pmc_traffic.py: profiles/pmc_traffic.json for cfg3 and its sub-lines,
+    profiles/pmc_traffic_cfg5.json for cfg5), or None when a kernel of the op is missing from it."""
+    name = 'pmc_traffic.json' if config == 'cfg3' else f'pmc_traffic_{config}.json'
+    path = os.path.join(ROOT, 'profiles', name)
+    kernels = OP_KERNELS.get(op) or SUB_KERNELS.get(op)
+    if not kernels or not os.path.exists(path):
         return None
     kern = json.load(open(path))['kernels']
     total, found = 0, 0
-    for pref in OP_KERNELS[op]:
+    for pref in kernels:
         for name, v in kern.items():
             if pref in name:
                 total += v['hbm_bytes']
                 found += 1
                 break
-    return total if found == len(OP_KERNELS[op]) else None
+    return total if found == len(kernels) else None
+
+
+def roofline_hbm(nbytes, ms, op, model, config='cfg3'):
+    """A sub-line's HBM roofline: algorithmic bytes per call / its mean call time, PMC traffic beside."""
+    ach = nbytes / (ms * 1e-3) / 1e9
+    return {'bound': 'hbm', 'achieved': round(ach, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+            'frac': round(ach / HBM_PEAK_GBS, 4), 'bytes_per_call': int(nbytes), 'bytes_model': model,
+            'traffic': pmc_traffic(op, config),
+            'traffic_scope': 'sum of the kernels ' + ', '.join(SUB_KERNELS.get(op, OP_KERNELS.get(op, ())))}
+
+
+def roofline_valu(flops, ms, model):
+    ach = flops / (ms * 1e-3) / 1e12
+    return {'bound': 'valu', 'achieved': round(ach, 4), 'peak': FP32_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+            'frac': round(ach / FP32_PEAK_TFLOPS, 6), 'flops_per_call': int(flops), 'flops_model': model}
 
 
 def workload_stats(inp):
@@ -534,6 +564,7 @@ def dibr_headline(args, world, rank, device):
     for _ in range(args.warmup):
         step()
     stats = workload_stats(inp)
+    inp['stats'] = stats
     # eager pass with per-op HIP events (the roofline's op durations), then the eager rate
     # without them (the events and their Python cost are not part of the step)
     timer = _native.OpTimer()
@@ -955,8 +986,14 @@ def sided_leg(device, steps):
     dist, _ = kal.metrics.pointcloud.sided_distance(d1, d2)
     ref = _sided_distance(p1, p2)
     rates = torch_cpu_legs(lambda: _sided_distance(p1, p2), 2048 * 2048, 1e6)
+    nbytes = 2 * 2048 * 12 + 2048 * (4 + 8)  # both clouds read, dist + idx written
     return {'metric': 'sided_distance Mpairs/s (2048 x 2048, f32, fwd)', 'value': round(2048 * 2048 / (ms * 1e-3) / 1e6, 1),
             'ms': round(ms, 4), 'parity_vs_cpu_reference_path': {'max_abs': float((dist.cpu() - ref).abs().max())},
+            'roofline': dict(roofline_valu(8 * 2048 * 2048, ms, 'SURVEY.md 8d cfg1: 8 FP32 flop per pair (3 sub, '
+                                           '3 mul, 2 add), 2048 x 2048 pairs'),
+                             hbm=roofline_hbm(nbytes, ms, 'cfg1_sided', 'p1 and p2 read (12 B per point), dist 4 + '
+                                                                        'idx 8 B per p1 point written'),
+                             note='a 30 us call: launch- and latency-bound, far from either roof'),
             'cpu': {'unit': 'Mpairs/s', 'kind': 'port', 'by_threads': rates,
                     'sample': 'full 2048 x 2048 (median of 5)', 'survey_reference_8_threads': 152.0}}
 
@@ -1014,19 +1051,21 @@ def cfg4_leg(device, steps):
                                        'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                                        'frac': round(vox_bytes / (ms_vox * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
             'mesh_to_spc': {'ms': round(ms_spc, 3), 'nodes': nodes, 'leaves': leaves, 'proposals_per_level': N,
-                            'bytes': spc_bytes,
-                            'roofline': {'bound': 'hbm', 'achieved': round(spc_bytes / (ms_spc * 1e-3) / 1e9, 1),
+                            'bytes': survey_spc_bytes,
+                            # headline: SURVEY.md §8d's formula, comparable across rounds; the
+                            # bytes this build's algorithm moves are the secondary build_model
+                            'roofline': {'bound': 'hbm', 'achieved': round(survey_spc_bytes / (ms_spc * 1e-3) / 1e9, 1),
                                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                                         'frac': round(spc_bytes / (ms_spc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                         'bytes_model': 'the node-rank algorithm (spc.hip): per pair its key, face, '
-                                                        'triangle, node point and scan entry, child pairs written, '
-                                                        '~31 B per node for the level scans, 52 B per leaf',
-                                         'survey_formula': {
-                                             'bytes': survey_spc_bytes,
-                                             'achieved': round(survey_spc_bytes / (ms_spc * 1e-3) / 1e9, 1),
-                                             'frac': round(survey_spc_bytes / (ms_spc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                             'note': 'SURVEY.md §8d prices the reference algorithm (sort, dedup); '
-                                                     'an effective rate: this build moves none of those bytes'}}},
+                                         'frac': round(survey_spc_bytes / (ms_spc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                         'bytes_source': 'SURVEY.md §8d (the reference algorithm: sort, dedup) -- an '
+                                                         'effective rate: this build moves none of those bytes',
+                                         'build_model': {
+                                             'bytes': spc_bytes,
+                                             'achieved': round(spc_bytes / (ms_spc * 1e-3) / 1e9, 1),
+                                             'frac': round(spc_bytes / (ms_spc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                             'model': 'the node-rank algorithm (spc.hip): per pair its key, face, '
+                                                      'triangle, node point and scan entry, child pairs written, '
+                                                      '~31 B per node for the level scans, 52 B per leaf'}}},
             'timing': 'wall clock per call (median of runs); voxelgrid: device-counted levels, one status read; '
                       'voxelgrid.host_sized: incl. its per-level host count reads; mesh_to_spc: the node-rank '
                       'levels, one host read of the counts after them',
@@ -1121,19 +1160,22 @@ def raytrace_leg(device, steps, spc_tuple):
                          8 * per_level[lv + 1] for lv, n in enumerate(listed)) + per_level[L] * (6 + 12 + 4)
     return {'metric': 'unbatched_raytrace Mrays/s (cfg4 SPC level 9, 512x512 rays, depth)',
             'value': round(R / (ms * 1e-3) / 1e6, 2), 'ms': round(ms, 4), 'hits': hits, 'hits_per_level': per_level,
-            'bytes': nbytes, 'timing': 'wall clock per call incl. its one host read and allocator calls',
+            'bytes': survey_bytes, 'timing': 'wall clock per call incl. its one host read and allocator calls',
             'fixed_capacity': {'value': round(R / (ms_fixed * 1e-3) / 1e6, 2), 'ms': round(ms_fixed, 4),
                                'capacity': cap, 'equal_to_host_sized': bool(fixed_equal),
                                'timing': 'HIP events over back-to-back calls (nothing read back)'},
             'candidates_per_level': cand,
-            'roofline': {'bound': 'hbm', 'achieved': round(nbytes / (ms * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         'bytes_model': 'the hit-list march: per listed hit node its nugget, ray, octree byte, exsum, '
-                                        'its children\'s points and mask byte, the write pass\'s reads and 8 B per hit '
-                                        'child; per target hit its point and ray again + depth',
-                         'survey_formula': {'bytes': survey_bytes,
-                                            'achieved': round(survey_bytes / (ms * 1e-3) / 1e9, 1),
-                                            'frac': round(survey_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}}}
+            # headline: SURVEY.md §8d's formula (comparable across rounds); this build's bytes beside it
+            'roofline': {'bound': 'hbm', 'achieved': round(survey_bytes / (ms * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': round(survey_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                         'bytes_source': 'SURVEY.md §8d raytrace model with the per-level hit counts',
+                         'build_model': {'bytes': nbytes,
+                                         'achieved': round(nbytes / (ms * 1e-3) / 1e9, 1),
+                                         'frac': round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                         'model': 'the hit-list march: per listed hit node its nugget, ray, octree '
+                                                  'byte, exsum, its children\'s points and mask byte, the write '
+                                                  'pass\'s reads and 8 B per hit child; per target hit its point and '
+                                                  'ray again + depth'}}}
 
 
 def _popcount_u8(t):
@@ -1197,11 +1239,20 @@ def deftet_bench(inp, steps, knum=8):
 
     ms_fwd = _event_ms(lambda: fwd(), steps)
     ms = _event_ms(step, steps)
-    _, idx = fwd()
+    out, idx = fwd()
     hits = int((idx >= 0).sum())
+    nb = lambda t: t.numel() * t.element_size()  # noqa: E731
+    F = fvz.shape[1]
+    # compulsory traffic of one fwd + bwd: the inputs read once (pixels, ranges, the faces' z, image
+    # coordinates and features), the outputs written once (slot features and face ids); the backward
+    # reads the upstream gradient and the saved slots, and writes both face gradients
+    nbytes = (nb(pix) + nb(rr) + nb(fvz) + nb(fvi) + nb(feat) + nb(out) + nb(idx)
+              + nb(g) + nb(idx) + B * F * 3 * 4 + nb(fvi) + nb(feat))
     return {'metric': f'deftet_sparse_render fwd+bwd Mpixels/s ({B} views, {H}x{W}, 50k faces, knum=8, f32)',
             'value': round(B * H * W / (ms * 1e-3) / 1e6, 1), 'ms': round(ms, 3), 'fwd_ms': round(ms_fwd, 3),
-            'hits': hits}
+            'hits': hits,
+            'roofline': roofline_hbm(nbytes, ms, 'deftet', 'compulsory: inputs read once, slot outputs written '
+                                     'once, backward reads grad + saved slots and writes the face gradients')}
 
 
 def check_sign_bench(device, steps, n_points=1000000):
@@ -1213,9 +1264,34 @@ def check_sign_bench(device, steps, n_points=1000000):
     pts = (torch.rand((1, n_points, 3), generator=g) * 2 - 1).to(device)
     v = verts.unsqueeze(0).contiguous()
     ms = _event_ms(lambda: kal.ops.mesh.check_sign(v, faces, pts), steps)
+    nbytes = n_points * (12 + 1) + v.numel() * 4 + faces.numel() * 8
     return {'metric': 'check_sign Mpoints/s (1M points vs 50k-face sphere, f32)',
             'value': round(n_points / (ms * 1e-3) / 1e6, 1), 'ms': round(ms, 3),
-            'nominal_mpairs_per_s': round(n_points * faces.shape[0] / (ms * 1e-3) / 1e6, 1)}
+            'nominal_mpairs_per_s': round(n_points * faces.shape[0] / (ms * 1e-3) / 1e6, 1),
+            'roofline': roofline_hbm(nbytes, ms, 'check_sign', 'compulsory: points 12 B read + 1 B written, the mesh '
+                                     'read once; the cell lists the kernels build and re-read are not counted')}
+
+
+def soft_mask_c_leg(inp, steps):
+    """The reference's _C contract soft-mask forward (dibr_soft_mask_forward_cuda: the (B,H,W,K) prob /
+    idx / type slot tensors, what the reference's own tests and direct _C callers use) on the cfg3
+    views, timed with HIP events; bytes by op_bytes (SURVEY.md 8d's soft-mask term)."""
+    import torch
+    import kaolin as kal
+    stats = inp['stats']
+    with torch.no_grad():
+        _, fidx = kal.render.mesh.rasterize(inp['H'], inp['W'], inp['fvz'], inp['fvi'], inp['feat'], inp['fnz'] >= 0)
+        fm = inp['fvi'] * 1000.
+        bb = torch.cat([fm.min(-2)[0] - 20., fm.max(-2)[0] + 20.], -1).contiguous()
+    fwd = lambda: kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, fidx, 7000., 30, 1000.)  # noqa: E731
+    ms = _event_ms(fwd, steps)
+    nbytes = op_bytes('dibr_soft_mask_forward_cuda', inp, stats)
+    B, H, W = inp['fvz'].shape[0], inp['H'], inp['W']
+    torch.cuda.empty_cache()
+    return {'metric': 'dibr_soft_mask_forward_cuda (_C contract, K=30 slot tensors) Mpixels/s, cfg3 views',
+            'value': round(B * H * W / (ms * 1e-3) / 1e6, 1), 'ms': round(ms, 4),
+            'roofline': roofline_hbm(nbytes, ms, 'soft_mask_C', 'SURVEY.md 8d soft fwd: sel 8 + mask 4 + K x (prob 4 '
+                                     '+ idx 8 + type 1) per px, fvi 24 + bbox 16 per face')}
 
 
 # ----------------------------------------------------------------------------- CPU self-test
@@ -1354,6 +1430,9 @@ def main(argv=None):
         if args.config == 'cfg3':
             result['deftet'] = deftet_bench(inp, max(3, args.steps // 4))
         result['check_sign'] = check_sign_bench(device, max(3, args.steps // 4))
+        if args.config == 'cfg3':
+            progress('_C soft mask leg')
+            result['soft_mask_C'] = soft_mask_c_leg(inp, max(5, args.steps // 2))
         progress('prepare_vertices leg')
         result['prepare_vertices'] = prepare_leg(device, args.steps)
         if args.config == 'cfg3':

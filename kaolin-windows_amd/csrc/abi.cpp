@@ -9,11 +9,15 @@
 namespace kl {
 static thread_local std::string g_last_error;
 void set_error(const std::string &msg) { g_last_error = msg; }
+#if KL_DEV
 int g_dev_flags = 0;
 void *g_dev_debug = nullptr;
 int g_dev_param[32] = {};
 int g_dev_stat[4] = {};
+#endif
 }  // namespace kl
+
+#if KL_DEV  // the dev build only (make dev): none of these is in the product library
 
 // Development hook (not part of include/kaolin_hip.h): bit flags that switch parts of
 // some kernels off for ablation timing (scripts/dev/ablate.py).  Results are wrong
@@ -29,9 +33,14 @@ extern "C" void kl_dev_set_param(int idx, int value) {
 }
 // Development hook: what the last call took (tests assert a fallback branch ran).
 // 0: mesh_to_spc -- 0 the node-rank path, 1 its per-level fallback (the pair buffers overflowed).
-// 1: raytrace -- 1 the fused march, 2 the fused march truncated and the per-level march rerun,
-//    0 the per-level march alone.
+// 1: raytrace (host-sized entry) -- 4 the hit-list march (the default), 5 the hit-list march
+//    outgrew its list buffers and the per-level march was rerun, 0 the per-level march alone
+//    (dev param 15 = 2), 1 the fused march (15 = 3), 2 the fused march truncated and the per-level
+//    march rerun, 3 the depth-first march (15 = 4).
 extern "C" int kl_dev_get_stat(int idx) { return idx >= 0 && idx < 4 ? kl::g_dev_stat[idx] : 0; }
+// 1 in the dev build (tests/conftest.py: the devlib tests need it)
+extern "C" int kl_dev_build() { return 1; }
+#endif
 
 namespace kl {
 // Byte fill as an ordinary kernel: 16-byte stores over the aligned body, bytes at the

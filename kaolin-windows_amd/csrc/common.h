@@ -15,10 +15,27 @@
 namespace kl {
 
 void set_error(const std::string &msg);
-extern int g_dev_flags;    // kl_dev_set_flags (ablation timing only; 0 in the product path)
-extern void *g_dev_debug;  // kl_dev_set_debug (per-wave stamps; nullptr in the product path)
-extern int g_dev_param[32];  // kl_dev_set_param (tuning sweeps; 0 = the built-in value)
+// Development controls exist only in the dev build (make dev: -DKL_DEV=1, kaolin/_lib/dev/): A/B
+// switches between the product path and measured alternatives, forced fallbacks for the tests
+// that cover them (tests marked devlib), stamps.  In the product library they are compile-time
+// zeros: no process-global mutable state, and every branch they select -- the dead ends DESIGN.md
+// records (the fused tile kernel, the fused / depth-first raytrace marches, the scalar-record p2m
+// kernel, the r03 gather) -- is compiled out.
+#ifndef KL_DEV
+#define KL_DEV 0
+#endif
+#if KL_DEV
+extern int g_dev_flags;    // kl_dev_set_flags (ablation timing only; 0 = the product path)
+extern void *g_dev_debug;  // kl_dev_set_debug (per-wave stamps; nullptr = none)
+extern int g_dev_param[32];  // kl_dev_set_param (tuning sweeps, forced fallbacks; 0 = the built-in value)
 extern int g_dev_stat[4];    // kl_dev_get_stat (what the last call took)
+#define KL_DEV_STAT(i, v) (::kl::g_dev_stat[(i)] = (v))
+#else
+constexpr int g_dev_flags = 0;
+constexpr void *g_dev_debug = nullptr;
+constexpr int g_dev_param[32] = {};
+#define KL_DEV_STAT(i, v) ((void)0)
+#endif
 
 // shader-clock and 100 MHz wall-clock stamps for the dev timing buffer
 // Dev stamps (kl_dev_set_debug) are compiled in only with -DKL_DEV_STAMPS=1 (make STAMPS=1):

@@ -23,6 +23,7 @@
 #include "rastcommon.h"
 #include "tilewalk.h"
 
+#if KL_DEV  // the whole fused tile kernel: built into the dev library only (make dev)
 namespace kl {
 
 constexpr int DT_WAVES = 4;
@@ -513,3 +514,5 @@ int dibr_tile_launch(const DibrTileArgs &a, int lp_min, int grid, hipStream_t st
 }
 
 }  // namespace kl
+
+#endif  // KL_DEV

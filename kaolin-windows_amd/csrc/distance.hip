@@ -464,10 +464,12 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
   }
 }
 
+// rows of the dev kernel's pruning records (the workspace keeps their room in every build)
+constexpr int P2M_PR_ROWS = 18;
+#if KL_DEV  // the scalar-record p2m kernel (dev param 11 = 2 / 3): a measured dead end, DESIGN.md 3.4
 // ---- global face records (the sorted path): p2m_faces_kernel writes, once per call, each face's
 // evaluation record (FaceRecS) and its pruning record as structure-of-arrays rows of length Fp:
 // rows 0..12 = make_prune_vals, 13..15 = un, 16 = thick, 17 = hmax.
-constexpr int P2M_PR_ROWS = 18;
 
 template <typename T>
 __global__ void __launch_bounds__(256) p2m_faces_kernel(const T *__restrict__ fv, int64_t F, int64_t Fp,
@@ -612,6 +614,7 @@ __global__ void __launch_bounds__(256) p2m_fwd_grec_kernel(const T *__restrict__
     out_type[pi] = best_t;
   }
 }
+#endif  // KL_DEV
 
 // folds the splits' partials in face order with the reference's strict '<'
 template <typename T>
@@ -1095,6 +1098,7 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
   // dev param 11 = 2 / 3: face records read from global memory through scalar loads
   // (p2m_fwd_grec_kernel, one / two faces per iteration) instead of staged through LDS -- measured
   // slower at cfg2 (1.70 against 1.51 ms for two faces per iteration), kept for A/B
+#if KL_DEV
   if (order && (g_dev_param[11] == 2 || g_dev_param[11] == 3)) {
     char *w = reinterpret_cast<char *>(ws);
     const P2MWs L(P, F, sizeof(T));
@@ -1111,7 +1115,9 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
       hipLaunchKernelGGL((p2m_fwd_grec_kernel<T, true>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st,
                          (const T *)pts, (const FaceRecS<T> *)rec, (const T *)pr, L.Fp, order, P, F, split_faces,
                          (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
-  } else if (g_dev_param[11] == 4 || !order) {  // dev param 11 = 4: the wave-level walk alone (r04)
+  } else
+#endif
+  if (g_dev_param[11] == 4 || !order) {  // dev param 11 = 4: the wave-level walk alone (r04)
     hipLaunchKernelGGL((p2m_fwd_kernel<T, false>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
                        (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
   } else {

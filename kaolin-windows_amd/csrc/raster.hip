@@ -1255,6 +1255,22 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
   }
 }
 
+// The chip order kernel's count workgroups meet at a grid barrier (a spin on an agent-scope
+// counter, tileorder.h): every one of its 2 nb + 1 workgroups must be resident at once.  Checked
+// here on the device's occupancy for the kernel's block size and LDS; when they may
+// not all fit, kl_dibr_forward takes the two-workgroup order kernel instead, which has no
+// barrier.  The answer depends only on the device and nb, so it is computed per call (a host
+// query, no state kept).
+static bool chip_order_resident(int nb) {
+  int dev = 0, ncu = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(tile_countorder_chip_kernel),
+                                                   CO_THREADS, (size_t)nb * ORD_HIST * sizeof(int)) != hipSuccess)
+    return false;
+  return (int64_t)per_cu * ncu >= 2 * (int64_t)nb + 1;
+}
+
 // ---------------------------------------------------------------- gather backward, v2
 // The per-face gather reorganised around what bounds it (r03 counters: ~600 VALU per wave of 8
 // faces, a third of it the 15-double butterfly; 126 VGPRs of double accumulators; each won pixel's
@@ -1573,17 +1589,20 @@ static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T 
   const int64_t nf = (int64_t)B * F;
   if (g_dev_param[7] != 1 || soft) {  // (the r03 gather does not read flagged soft sums)  // dev param 7 = 1: the r03 gather (8 lanes per face, register sums) for A/B
     const int nb = (int)std::min<int64_t>(G2_BIG_BLOCKS, cdiv(nf, 4096));
-    if (g_dev_param[8] != 1)  // dev param 8 = 1: read-modify-write partials (A/B: 73 against 48 us at cfg3)
-      hipLaunchKernelGGL((rasterize_bwd_gather2_kernel<T, MAXD, true>), dim3((unsigned)(nb + cdiv(nf * 8, 256))),
-                         dim3(256), 0, st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat,
-                         rng, soft, sflag, nb, gather_opts());
-    else
+#if KL_DEV
+    if (g_dev_param[8] == 1)  // dev param 8 = 1: read-modify-write partials (A/B: 73 against 48 us at cfg3)
       hipLaunchKernelGGL((rasterize_bwd_gather2_kernel<T, MAXD>), dim3((unsigned)(nb + cdiv(nf * 8, 256))), dim3(256),
                          0, st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat, rng, soft,
                          sflag, nb, gather_opts());
+    else
+#endif
+      hipLaunchKernelGGL((rasterize_bwd_gather2_kernel<T, MAXD, true>), dim3((unsigned)(nb + cdiv(nf * 8, 256))),
+                         dim3(256), 0, st, grad, face_idx, w, fvi, feat, valid, nz, B, H, W, F, D, m, eps, gfvi, gfeat,
+                         rng, soft, sflag, nb, gather_opts());
     KL_CHECK_LAUNCH();
     return KL_OK;
   }
+#if KL_DEV  // the r03 gather (dev param 7 = 1): a measured dead end, DESIGN.md 3.3
   if (zero_nbig) KL_CHECK_RC(fill_async(nbig, 0, sizeof(int), st));
   // 8 lanes per face (measured: 4 lanes 62.7 us, 8 lanes 58 us, 16 lanes 91 us at cfg3)
   hipLaunchKernelGGL((rasterize_bwd_gather_kernel<T, MAXD>), dim3((unsigned)cdiv(nf * LPF, 256)), dim3(256), 0, st,
@@ -1595,6 +1614,12 @@ static int rasterize_bwd_gather_maxd(int B, int H, int W, int F, int D, const T 
                      feat, valid, nz, H, W, F, D, m, eps, gfvi, gfeat, big, nbig, rng, soft);
   KL_CHECK_LAUNCH();
   return KL_OK;
+#else
+  (void)big;
+  (void)nbig;
+  (void)zero_nbig;
+  return KL_OK;
+#endif
 }
 
 // The gather backward writes every face's gradient (zeros where nothing was won).
@@ -1838,6 +1863,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     // rasterizer and the soft mask (needs bboxes inside the enlarged ones: boxlen >= 0).  Dev param
     // 10 = 2 only: measured slower than the two-kernel path below at cfg3 (105.9 against 32.1 +
     // 51.3 us of tile kernels), kept tested bit-equal to it for the record.
+#if KL_DEV  // the fused tile kernel (dev param 10 = 2): a measured dead end, DESIGN.md 3.1
     if (pad >= 0.0 && bin_word_lds_ok(g) && nt <= ORD_LDS_TILES && g_dev_param[10] == 2) {
       KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, nullptr, rec, rng, sbm, srng, (T)pad, rgh,
                                      (int)((L.zero - L.off_rgh) / sizeof(int)), st));
@@ -1859,6 +1885,8 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
                             g_dev_param[12]};
       return dibr_tile_launch(da, lpm, soft_items_bound(nt, lpm, soft_split()), st);
     }
+#endif
+
   }
   if (bin_word_lds_ok(g) && !(g_dev_flags & (1 << 14))) {  // dev bit 14: the atomic binning
     KL_CHECK_RC(launch_bin_word<T>(src, fvz, F, g, pp, rbm, rec, rng, sbm, srng, (T)pad, rgh,
@@ -1881,7 +1909,8 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
   // r05: the soft items' live flags (set by the rasterizer, read by the soft kernel first) where the
   // chip order kernel lists each tile row's item; dev param 26 = 1: off (A/B)
   bool live = false;
-  if (nt <= ORD_LDS_TILES && !(g_dev_flags & (1 << 20)) && g_dev_param[15] != 1) {
+  if (nt <= ORD_LDS_TILES && !(g_dev_flags & (1 << 20)) && g_dev_param[15] != 1 &&
+      chip_order_resident((int)cdiv(nt, CO_THREADS))) {
     // counts over the chip, orders by each bitmap's last count workgroup (tileorder.h); the other
     // workgroups zero the backward's soft-mask accumulator meanwhile (dev param 15 = 1: the r04
     // two-workgroup kernel below, for A/B)
@@ -1973,13 +2002,16 @@ static int dibr_bwd(int B, int H, int W, int F, int D, int K, const T *grad_feat
   const DibrSoftAcc A(B, F);
   double *acc = reinterpret_cast<double *>(soft_acc);
   uint8_t *sflag = has_soft ? reinterpret_cast<uint8_t *>(soft_acc) + A.off_flags : nullptr;
+  int rc = KL_OK;
   if (has_soft)
-    KL_CHECK_RC(soft_tile_backward_listed<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m,
-                                             reinterpret_cast<const int2 *>(state + S.off_items),
-                                             reinterpret_cast<const int *>(state), S.cap, acc, sflag, st));
-  const int rc = rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi,
-                                         gfeat, ws, ws_bytes, nullptr, st, face_ranges, has_soft ? acc : nullptr, sflag);
-  // the accumulator must be zero for the next call: if the gather did not run, clear it here
+    rc = soft_tile_backward_listed<T>(B, H, W, F, K, grad_mask, mask, s, fvi, sigmainv, m,
+                                      reinterpret_cast<const int2 *>(state + S.off_items),
+                                      reinterpret_cast<const int *>(state), S.cap, acc, sflag, st);
+  if (rc == KL_OK)
+    rc = rasterize_bwd_gather<T>(B, H, W, F, D, grad_feat, face_idx, w, fvi, feat, nullptr, fnz, m, eps, gfvi, gfeat,
+                                 ws, ws_bytes, nullptr, st, face_ranges, has_soft ? acc : nullptr, sflag);
+  // the accumulator must be zero for the next call: on ANY failure (the soft kernel may have added
+  // into it before a later step failed, and the gather that re-zeroes it may not have run) clear it
   if (rc != KL_OK && has_soft) (void)fill_async(soft_acc, 0, A.bytes, st);
   return rc;
 }

@@ -1554,7 +1554,7 @@ __global__ void __launch_bounds__(256) dscan_apply_kernel(const uint32_t *__rest
 // ticket order, so most tiles find an inclusive predecessor close by (with a workgroup per tile
 // and 4 nuggets per thread, ~1,600 tiles at cfg4's deepest level all looked back at once, up to
 // 25 rounds of 64 tiles each: the fused march took 2.35 ms against the per-level march's 1.17)
-constexpr int RTL_PER = 16, RTL_TILE = 256 * RTL_PER, RTL_GRID = 256;
+constexpr int RTL_PER = 16, RTL_TILE = 256 * RTL_PER;
 struct RtlCtl {
   uint32_t dnum[SPC_MAX_LEVELS + 2];    // nuggets of each level, clipped to the capacity
   uint32_t total[SPC_MAX_LEVELS + 2];   // the same, unclipped
@@ -1562,6 +1562,8 @@ struct RtlCtl {
   uint32_t truncated;                   // some level had more nuggets than the capacity
 };
 
+#if KL_DEV  // the fused level march (dev param 15 = 3): a measured dead end, DESIGN.md 3.5
+constexpr int RTL_GRID = 256;
 __device__ __forceinline__ void rt_children(const RayIn &in, int ridx, int pidx, uint32_t level, uint32_t base,
                                             int2 *__restrict__ nout, uint32_t cap) {
   const int16_t *p = in.points + (int64_t)pidx * 3;
@@ -1733,6 +1735,8 @@ static int rt_fused_levels(const RayIn &in, int64_t num_rays, uint32_t target_le
   }
   return KL_OK;
 }
+#endif  // KL_DEV
+
 
 // ---- Hit-list level march (r05, the default of both entries): level l's list holds the nuggets
 // that HIT at level l (not the candidates).  Per level, one count pass decides every listed node's
@@ -2223,6 +2227,7 @@ static int rt_hitlist(const RayIn &in, int64_t num_rays, uint32_t target_level, 
   return KL_OK;
 }
 
+#if KL_DEV  // the fused march
 // the fixed-capacity entry's result from the fused march: (rows, truncated)
 __global__ void rt_fused_result_kernel(const RtlCtl *__restrict__ ctl, uint32_t target_level,
                                        int64_t *__restrict__ result) {
@@ -2231,7 +2236,10 @@ __global__ void rt_fused_result_kernel(const RtlCtl *__restrict__ ctl, uint32_t 
     result[1] = ctl->truncated ? 1 : 0;
   }
 }
+#endif  // KL_DEV
 
+
+#if KL_DEV  // the depth-first march (dev param 15 = 4): a measured dead end, DESIGN.md 3.5
 // ---- Per-ray depth-first march (r05, the eager entry): the level march's output is ray-major, and
 // within a ray each nugget's children follow it in front-to-back order, level by level -- which is
 // exactly the order of a depth-first walk that visits a node's children front to back (every level's
@@ -2401,6 +2409,8 @@ static int rt_dfs(const RayIn &in, int64_t num_rays, uint32_t target_level, int 
   *num_hits = total;
   return KL_OK;
 }
+#endif  // KL_DEV
+
 
 template <typename S>
 __global__ void pack_bounds_kernel(int64_t n, const S *__restrict__ ids, int32_t *__restrict__ out) {
@@ -2418,12 +2428,12 @@ extern "C" int kl_mesh_to_spc(int64_t num_faces, const float *fv, uint32_t level
   KL_REQUIRE(level < (uint32_t)SPC_MAX_LEVELS, "mesh_to_spc: level must be < 15");
   KL_REQUIRE(alloc != nullptr, "mesh_to_spc: allocator required");
   Scratch sc{alloc, ctx};
-  g_dev_stat[0] = 1;
+  KL_DEV_STAT(0, 1);
   if (!(g_dev_flags & (1 << 10))) {  // dev bit 10: the per-level path
     const int rc = mesh_to_spc_nodes(num_faces, fv, level, sc, octree, num_nodes, face_idx, bary, num_leaves,
                                      S(stream));
     if (rc != 1) {
-      g_dev_stat[0] = 0;
+      KL_DEV_STAT(0, 0);
       return rc;
     }
   }
@@ -2573,7 +2583,7 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
   // the fused march (rt_level_kernel), every level's count on the device and ONE host read at the
   // end, with buffers of 16 nuggets per ray; a level with more falls back to the per-level march
   // below (dev param 15 = 2: that march always, for A/B)
-  g_dev_stat[1] = 0;
+  KL_DEV_STAT(1, 0);
   // default: the hit-list march (rt_hitlist), falling back to the per-level march below when a level
   // outgrows its buffers.  Dev param 15 = 2: the per-level march; 4: the per-ray depth-first march
   // (rt_dfs); 3: the fused level march first (kept for A/B, tested equal: at cfg4 1.22 and 2.8 ms
@@ -2581,12 +2591,14 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
   if (g_dev_param[15] == 0 && num_rays < ((int64_t)1 << 31)) {
     const int rc = rt_hitlist(in, num_rays, target_level, return_depth, with_exit, sc, nuggets, depth, num_hits, st);
     if (rc <= 0) {
-      g_dev_stat[1] = 4;
+      KL_DEV_STAT(1, 4);
       return rc;
     }
+    KL_DEV_STAT(1, 5);  // the lists outgrew their buffers: the per-level march below
   }
+#if KL_DEV  // the depth-first and fused marches (A/B)
   if (num_rays > 0 && num_rays < ((int64_t)1 << 31) && g_dev_param[15] == 4 && target_level < (uint32_t)RTD_MAXL) {
-    g_dev_stat[1] = 3;
+    KL_DEV_STAT(1, 3);
     return rt_dfs(in, num_rays, target_level, return_depth, with_exit, sc, nuggets, depth, num_hits, st);
   }
   const int64_t fcap = std::max<int64_t>(16 * num_rays, 1 << 16);
@@ -2604,7 +2616,7 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
                                 b1, out, dout, st));
     RtlCtl h;
     KL_CHECK_RC(host_read(&h, ctl, sizeof(RtlCtl), st));
-    g_dev_stat[1] = h.truncated ? 2 : 1;
+    KL_DEV_STAT(1, h.truncated ? 2 : 1);
     if (!h.truncated) {
       *nuggets = (int32_t *)out;
       *depth = dout;
@@ -2612,6 +2624,8 @@ extern "C" int kl_raytrace(const uint8_t *octree, int64_t octree_size, const int
       return KL_OK;
     }
   }
+#endif
+
   int64_t num = num_rays;
   int2 *n0 = (int2 *)sc.get(num * sizeof(int2));
   if (!n0) return KL_E_ALLOC;
@@ -2729,6 +2743,7 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
   }
   RayIn in{octree, points, exsum, ray_o, ray_d};
   const int64_t cap0 = L.cap0;
+#if KL_DEV  // the fused march (A/B)
   if (g_dev_param[15] == 3 && capacity > 0) {  // dev param 15 = 3: the fused march (2.2 against 1.09 ms at cfg4)
     RtlCtl *ctl = (RtlCtl *)dnum;
     static_assert(sizeof(RtlCtl) <= 256, "RtlCtl fits the dnum slot");
@@ -2739,6 +2754,8 @@ extern "C" int kl_raytrace_fixed(const uint8_t *octree, const int16_t *points, c
     KL_CHECK_LAUNCH();
     return KL_OK;
   }
+#endif
+
   // default: the hit-list march with the per-level march's truncation (rth_count_kernel's fixed
   // mode); dev param 15 = 2: the per-level march below
   if (hitlist && capacity > 0) {

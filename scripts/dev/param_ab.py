@@ -5,7 +5,12 @@ import ctypes
 import os
 import sys
 
-import torch
+ROOT0 = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the dev controls live in the dev library (make dev); the compiled node would load the product one
+os.environ.setdefault('KAOLIN_HIP_LIB', os.path.join(ROOT0, 'kaolin-windows_amd', 'kaolin', '_lib', 'dev',
+                                                     'libkaolin_hip.so'))
+os.environ.setdefault('KAOLIN_NO_EXT', '1')
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)

@@ -72,10 +72,10 @@ def main():
     for q in (0.5, 0.9, 0.99, 1.0):
         print(f'  wave end quantile {q}: {np.quantile(end_us, q):.1f} us, start {np.quantile(start_us, q):.1f} us')
     order = np.argsort(-(end_us - start_us) * lead)[:12]
-    print('slowest rows: tile row Q start_us end_us walk_cyc eval_cyc hits chunks')
+    print('slowest rows: tile row Q start_us end_us walk_cyc (fill_cyc) eval_cyc hits chunks')
     for k in order:
-        print(f'  {tile[k]:6d} {row[k]:4d} {Q[k]} {start_us[k]:7.1f} {end_us[k]:7.1f} {walk[k]:8.0f} {ev[k]:8.0f} '
-              f'{hits[k]:5d} {nch[k]:4d}')
+        print(f'  {tile[k]:6d} {row[k]:4d} {Q[k]} {start_us[k]:7.1f} {end_us[k]:7.1f} {walk[k]:8.0f} ({fill[k]:6.0f}) '
+              f'{ev[k]:8.0f} {hits[k]:5d} {nch[k]:4d}')
     bins = np.linspace(0, span, 21)
     busy = [int(((start_us <= b) & (end_us > b)).sum()) for b in bins[:-1]]
     print('waves in flight every 5% of the span:', busy)

@@ -14,6 +14,8 @@ GOLDEN = os.path.join(ROOT, 'tests', 'golden')
 
 def pytest_configure(config):
     config.addinivalue_line('markers', 'gpu: needs an MI355X (runs through the HIP C-ABI library)')
+    config.addinivalue_line('markers', 'devlib: uses the dev library\'s controls (make dev); run against it by '
+                                       'tests/test_gpu_devlib.py, parts skipped on the product library')
 
 
 def load_golden(name):

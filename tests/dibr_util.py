@@ -36,3 +36,49 @@ def state_arrays(state):
     """The compact state's tensors as numpy arrays (hits, rec_face, rec_prob)."""
     return (state.hits.detach().cpu().numpy(), state.rec_face.detach().cpu().numpy(),
             state.rec_prob.detach().cpu().numpy())
+
+
+# ---- the dev library (make dev: kaolin/_lib/dev/libkaolin_hip.so, KL_DEV=1).  The product library
+# has no dev controls; tests marked `devlib` switch between the product path and a measured
+# alternative, or force a fallback, through them.  They run in tests/test_gpu_devlib.py's child
+# process against the dev build; in a process on the product library they skip the parts that
+# need it (setting a control back to its default, 0, is a no-op there).
+def dev_lib():
+    """The loaded library's ctypes handle if it is the dev build, else None."""
+    import ctypes
+    from kaolin import _native as N
+    lib = N.lib()
+    if not hasattr(lib, 'kl_dev_build'):
+        return None
+    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
+    lib.kl_dev_get_stat.argtypes = [ctypes.c_int]
+    lib.kl_dev_get_stat.restype = ctypes.c_int
+    return lib
+
+
+def require_dev():
+    import pytest
+    lib = dev_lib()
+    if lib is None:
+        pytest.skip('needs the dev library (make dev): run by tests/test_gpu_devlib.py')
+    return lib
+
+
+def dev_param(idx, val):
+    """kl_dev_set_param on the dev library; 0 (the default) is a no-op on the product library."""
+    lib = dev_lib()
+    if lib is None:
+        if val == 0:
+            return
+        require_dev()
+    lib.kl_dev_set_param(idx, val)
+
+
+def dev_flags(flags):
+    lib = dev_lib()
+    if lib is None:
+        if flags == 0:
+            return
+        require_dev()
+    lib.kl_dev_set_flags(flags)

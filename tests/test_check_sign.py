@@ -136,12 +136,11 @@ def test_gpu_sphere_inside_property(kal):
 
 
 def _dev_flags(kal, flags):
-    import ctypes
-    lib = kal._native.lib()
-    lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
-    lib.kl_dev_set_flags(flags)
+    from dibr_util import dev_flags
+    dev_flags(flags)
 
 
+@pytest.mark.devlib
 @pytest.mark.gpu
 def test_gpu_list_total_coarsens_grid(kal):
     """The (y, z) cell lists' total is counted in 64 bits; past the int32 scan's range the grid
@@ -217,6 +216,7 @@ def _captured(fn):
     return g, out
 
 
+@pytest.mark.devlib
 @pytest.mark.gpu
 @pytest.mark.parametrize('overflow', [False, True])
 def test_gpu_graph_capture(kal, overflow):

@@ -259,15 +259,15 @@ def test_gpu_binned_and_tile_forward_agree(kal, dtype):
         np.testing.assert_array_equal(_A(x), r)
 
 
+@pytest.mark.devlib
 @pytest.mark.gpu
 def test_gpu_binned_list_cap_falls_back_to_tile_walk(kal):
     """The screen-grid lists' total is counted in 64 bits; past the int32 scan's range the forward
     takes the tile walk (forced here with a 2^10 test cap, dev flag 1 << 24): same slots."""
-    import ctypes
+    from dibr_util import require_dev
+    lib = require_dev()
     pix, ranges, fvz, fvi, feat, K = _grid_case(np.float32, B=2, F=2500, H=30, W=26, seed=9)
     args = [_T(fvz), _T(fvi), None, _T(pix), _T(ranges), K, 1e-8]
-    lib = kal._native.lib()
-    lib.kl_dev_set_flags.argtypes = [ctypes.c_int]
     lib.kl_dev_set_flags(1 << 24)
     try:
         a = kal._C.deftet_forward('deftet', *args, binned=True)
@@ -278,13 +278,15 @@ def test_gpu_binned_list_cap_falls_back_to_tile_walk(kal):
         np.testing.assert_array_equal(_A(x), r)
 
 
+@pytest.mark.devlib
 @pytest.mark.gpu
 @pytest.mark.parametrize('order', ['grid', 'shuffled'])
 def test_gpu_tile_walk_pixel_order(kal, order):
     """With dev param 24 = 1 the tile walk visits the pixels in a spatial (Morton) order when there
     are enough of them (r05; off by default, it did not pay): the same slots either way, equal to the oracle,
     with pixels in image order or shuffled, non-finite pixels and a second view."""
-    import ctypes
+    from dibr_util import require_dev
+    lib = require_dev()
     pix, ranges, fvz, fvi, feat, K = _grid_case(np.float32, B=2, F=1500, H=40, W=36, seed=11)
     pix = pix.copy()
     if order == 'shuffled':
@@ -293,8 +295,6 @@ def test_gpu_tile_walk_pixel_order(kal, order):
     pix[0, 17] = np.nan
     pix[1, 100, 0] = np.inf
     args = [_T(fvz), _T(fvi), None, _T(pix), _T(ranges), K, 1e-8]
-    lib = kal._native.lib()
-    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
     a = kal._C.deftet_forward('deftet', *args, binned=False)
     lib.kl_dev_set_param(24, 1)
     try:

@@ -557,11 +557,8 @@ def test_dibr_rasterization_fused_grads_vs_oracle(kal, which):
 
 
 def _dev_param(idx, val):
-    import ctypes
-    from kaolin import _native as N
-    lib = N.lib()
-    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
-    lib.kl_dev_set_param(idx, val)
+    from dibr_util import dev_param
+    dev_param(idx, val)
 
 
 def _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box=0.02):
@@ -576,6 +573,7 @@ def _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, box=0.02):
     return [A(f), A(i), A(w), A(m), hits, seg, rf[:keep.size][keep], rp[:keep.size][keep], A(rg)]
 
 
+@pytest.mark.devlib
 @pytest.mark.parametrize('case', ['bench', 'adversarial', 'bigbox'])
 def test_dibr_bin_marks_equal_atomic_binning(kal, case):
     """kl_dibr_forward's binning (raster_bin_word_kernel): the r05 per-wave byte marks against the LDS
@@ -601,6 +599,7 @@ def test_dibr_bin_marks_equal_atomic_binning(kal, case):
         assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
 
 
+@pytest.mark.devlib
 @pytest.mark.parametrize('case', ['bench', 'adversarial', 'knum255', 'tiny'])
 def test_soft_live_flags_equal(kal, case):
     """The soft forward's work items flagged live by the rasterizer (r05: an item whose rows hold no
@@ -631,6 +630,7 @@ def test_soft_live_flags_equal(kal, case):
         assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
 
 
+@pytest.mark.devlib
 @pytest.mark.parametrize('knum,alt', [(30, 2), (30, 3), (8, 2)])
 def test_soft_item_rows_equal(kal, knum, alt):
     """The soft forward's rows per work item (4 where the slot lists fit 64 KB of LDS) against
@@ -650,6 +650,7 @@ def test_soft_item_rows_equal(kal, knum, alt):
         assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
 
 
+@pytest.mark.devlib
 @pytest.mark.parametrize('case', ['bench', 'adversarial', 'knum64', 'knum255', 'bigbox'])
 def test_dibr_fused_tile_kernel_equals_two_kernel_path(kal, case):
     """kl_dibr_forward's fused tile kernel (dibrtile.hip: the rasterizer and the soft mask in one
@@ -1001,6 +1002,7 @@ def _p2m_stress(kind, dtype):
     return pts.astype(np_dt), fv.astype(np_dt)
 
 
+@pytest.mark.devlib
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
 @pytest.mark.parametrize('kind', ['cfg2', 'slivers', 'scaled', 'onsurface', 'dups'])
 @pytest.mark.parametrize('walk', ['pairs', 'wave'])
@@ -1040,6 +1042,7 @@ def test_sided_kat_and_ties(kal, golden):
     np.testing.assert_allclose(A(d), g['large_dist'])
 
 
+@pytest.mark.devlib
 @pytest.mark.parametrize('dtype', [torch.float16, torch.float32, torch.float64, torch.int32, torch.uint8])
 def test_sided_tile_splits_equal_one_pass(kal, dtype):
     """sided_distance's forward with p2's 512-point tiles split over workgroups (default when the
@@ -1415,6 +1418,7 @@ def _m2s_fixed_check(kal, fv, level, ncap, lcap):
     return status
 
 
+@pytest.mark.devlib
 @pytest.mark.parametrize('cap', [2048, 16384])
 def test_mesh_to_spc_pair_overflow_fallback(kal, cap):
     """The node-rank path's pair buffers (96 pairs per face and level) overflowing -- the branch of
@@ -1422,12 +1426,9 @@ def test_mesh_to_spc_pair_overflow_fallback(kal, cap):
     at a later level's node scan), the eager call takes the per-level fallback (kl_dev_get_stat) and
     equals the oracle; the fixed-capacity form returns status 2 with nothing written; with the
     capacity restored the node-rank path runs again and gives the same octree."""
-    import ctypes
+    from dibr_util import require_dev
     from kaolin import _native as N
-    lib = N.lib()
-    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
-    lib.kl_dev_get_stat.argtypes = [ctypes.c_int]
-    lib.kl_dev_get_stat.restype = ctypes.c_int
+    lib = require_dev()
     level = 6
     v, f = _uv_sphere(16, 24, 0.9)
     fv = v[f].astype(np.float32)
@@ -1594,6 +1595,7 @@ def test_raytrace_fixed_kat(kal, golden, name):
         assert (dep[len(ref):] == 0).all()
 
 
+@pytest.mark.devlib
 def test_raytrace_fixed_capture_and_truncation(kal):
     """The fixed-capacity march equals the host-sized one (nuggets and depth bit-equal); captured
     into a graph and replayed with new rays it answers the new rays; with a capacity below the
@@ -1663,11 +1665,12 @@ def test_raytrace_fixed_capture_and_truncation(kal):
         assert all(torch.equal(x, y) for x, y in zip(got, ref)), c
 
 
+@pytest.mark.devlib
 @pytest.mark.parametrize('level,nrays', [(4, 1000), (6, 1000), (6, 5), (0, 64), (3, 130)])
 def test_raytrace_marches_agree(kal, level, nrays):
     """The four marches of kl_raytrace, nuggets and depths (entry and exit) bit-equal to the per-level
     march (dev param 15 = 2, kl_dev_get_stat(1) == 0): the hit-list march (default, stat 4; level 0
-    and lists past its buffers fall back to the per-level march, stat 0), the fused level march
+    and lists past its buffers fall back to the per-level march, stat 5), the fused level march
     (dev param 15 = 3: one launch per level, counts on the device, one host read) and the per-ray
     depth-first march (dev param 15 = 4, stat 3), on a dense level-6 octree: level 4 fits the hit-list
     and fused buffers (16 nuggets per ray, at least 65,536), level 6 with 1,000 rays does not (~100
@@ -1675,12 +1678,8 @@ def test_raytrace_marches_agree(kal, level, nrays):
     the root alone, and ray counts that are not a multiple of the 64-ray workgroups.  The
     fixed-capacity entry's hit-list march (default) and fused march (dev param 15 = 3) against its
     per-level march (dev param 15 = 2) too."""
-    import ctypes
-    from kaolin import _native as N
-    lib = N.lib()
-    lib.kl_dev_set_param.argtypes = [ctypes.c_int, ctypes.c_int]
-    lib.kl_dev_get_stat.argtypes = [ctypes.c_int]
-    lib.kl_dev_get_stat.restype = ctypes.c_int
+    from dibr_util import require_dev
+    lib = require_dev()
     n_oct = sum(8 ** k for k in range(6))
     octree, pyr, ex, pts = _rt_setup(kal, np.full(n_oct, 255, np.uint8))
     rng = np.random.RandomState(level + nrays)
@@ -1703,7 +1702,7 @@ def test_raytrace_marches_agree(kal, level, nrays):
     (r2, p2, d2, s2), (r0, p0, d0, s0) = outs[2], outs[0]
     (r3, p3, d3, s3), (r4, p4, d4, s4) = outs[3], outs[4]
     fits = (level, nrays) != (6, 1000)
-    assert s2 == 0 and s4 == 3 and s0 == (4 if level > 0 and fits else 0)
+    assert s2 == 0 and s4 == 3 and s0 == (4 if level > 0 and fits else 5)
     # 2 = a level's candidates (its parents' children) exceeded the fused march's buffers
     assert s3 in (1, 2) and (s3 == 2 or len(r2) <= max(16 * nrays, 65536)) and (fits or s3 == 2)
     assert (level, nrays) != (6, 5) or s3 == 1
@@ -1846,3 +1845,35 @@ def test_rayops_error_messages(kal):
         C.cumprod_cuda(torch.zeros(4, 2, dtype=torch.int32, device=DEV), torch.zeros(1, dtype=torch.int32,
                                                                                       device=DEV), False, False)
 
+
+
+@pytest.mark.devlib
+@pytest.mark.parametrize('case', ['bench', 'adversarial', 'knum64', 'knum255'])
+def test_soft_slot_width_and_prob_readback_equal(kal, case):
+    """r06 soft forward layout: 16-bit slot lists (F <= 65536) against 32-bit ones (dev param 29 = 1),
+    and the mask's probabilities from LDS against the rec_prob read-back past the LDS capacity (dev
+    param 28 = n: capacity n - 1 floats; 1: every probability read back), and the multi-wave rows' walk
+    into per-wave lists merged in wave order against the per-block rounds over one shared row list
+    (dev param 30 = 1) -- every output and the compact state equal."""
+    import bench
+    if case == 'adversarial':
+        z, v, f = _adversarial_faces(torch.float32)
+        fvz, fvi, feat = T(z), T(v), T(f)
+        fnz = T(np.random.default_rng(2).uniform(-0.3, 1, fvz.shape[:2]).astype(np.float32))
+        H, W, K = 97, 130, 30
+    else:
+        inp = bench.dibr_inputs([0.3, 2.0], DEV, H=96, W=128)
+        fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+        H, W = 96, 128
+        K = {'knum64': 64, 'knum255': 255}.get(case, 30)
+    base = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, 0.02)
+    names = ['features', 'face_idx', 'weights', 'soft_mask', 'hits', 'seg_tot', 'rec_face', 'rec_prob', 'ranges']
+    for idx, val in ((29, 1), (28, 1), (28, 200), (30, 1)):
+        try:
+            _dev_param(idx, val)
+            other = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, 0.02)
+        finally:
+            _dev_param(idx, 0)
+        for n, x, y in zip(names, base, other):
+            assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), (idx, val, n)
+    assert base[4].max() > 0
