@@ -219,8 +219,12 @@ __device__ __forceinline__ void make_prune(const FaceRec<T> &r, PruneTile<T> &pt
 // the (distance, index) minimum -- the reference's result -- is exact.
 constexpr int P2M_QCAP = 128;  // per-wave pair ring (a face adds <= 64 pairs; batches of 64 drain it)
 
-template <typename T, bool PAIRS>
-__global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1)) p2m_fwd_kernel(const T *__restrict__ pts, const T *__restrict__ fv,
+// SUBC (r06): the pairs path's per-point test only for (face, 8-lane sub-cluster) pairs a sub-cluster
+// bound keeps, 8 such pairs per wave instruction (p2m_fwd_kernel's pairs branch)
+// (r06 A/B at cfg2: the sub-cluster kernel 0.818 ms at 4 waves per SIMD -- no spills -- against 0.85-0.89
+// at 5 with 54 VGPRs spilled; the r05 pairs kernel 0.85-0.92 at 5, 0.94 at 4)
+template <typename T, bool PAIRS, bool SUBC = true>
+__global__ void __launch_bounds__(256, (sizeof(T) == 4 ? (PAIRS && SUBC ? 4 : KL_P2M_WAVES_PER_EU) : 1)) p2m_fwd_kernel(const T *__restrict__ pts, const T *__restrict__ fv,
                                                        const int32_t *__restrict__ order, int64_t P, int64_t F,
                                                        int64_t split_faces, T *__restrict__ out_dist,
                                                        int64_t *__restrict__ out_idx, int32_t *__restrict__ out_type,
@@ -254,6 +258,25 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
     ext = mk(wave_max(fabs(dq.x)), wave_max(fabs(dq.y)), wave_max(fabs(dq.z))) * (T)(1.0 + 4.0 * P2M_E);
     cinf = fmax(fmax(fabs(c.x), fabs(c.y)), fabs(c.z));
   }
+  // (SUBC) this lane's 8-lane sub-cluster (lanes 8j .. 8j + 7, Morton-consecutive points): centre and
+  // radius, the wave cluster's construction over the group (xor shuffles 1, 2, 4 stay in the group)
+  V3<T> cj = mk((T)0, (T)0, (T)0);
+  T Rj = (T)INFINITY;
+  if (PAIRS && SUBC && all_fin) {
+    auto gmin = [](T v) {
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) v = fmin(v, __shfl_xor(v, o));
+      return v;
+    };
+    auto gmax = [](T v) {
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) v = fmax(v, __shfl_xor(v, o));
+      return v;
+    };
+    cj = mk((gmin(q.x) + gmax(q.x)) * (T)0.5, (gmin(q.y) + gmax(q.y)) * (T)0.5, (gmin(q.z) + gmax(q.z)) * (T)0.5);
+    const V3<T> dj = q - cj;
+    Rj = gmax(kl_sqrt<T>(dot(dj, dj))) * (T)(1.0 + 16.0 * P2M_E);
+  }
   // Shared thresholds (all faces proper, finite bounded cluster): the fold is then the plain
   // (distance, index) minimum, so the best distance any split has found for a point bounds
   // its result and is as good a threshold as this split's own.  gbest holds them as float
@@ -265,6 +288,7 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
   constexpr unsigned long long KEY_NONE = 0x7f800000ull << 32 | 0xffffffffull;  // +inf, no face
   __shared__ uint16_t s_q[PAIRS ? 4 : 1][P2M_QCAP];
   __shared__ unsigned long long s_best[PAIRS ? 256 : 1];
+  __shared__ uint8_t s_sp[PAIRS && SUBC ? 4 : 1][64];  // (SUBC) a batch's kept (face, sub-cluster) pairs
   const int wid = threadIdx.x >> 6;
   uint32_t qhead = 0, qcnt = 0;  // the wave's ring (wave-uniform)
   T pthr = (T)INFINITY, psq = (T)INFINITY;  // pairs: the lane's best distance so far and its root
@@ -359,6 +383,92 @@ __global__ void __launch_bounds__(256, (sizeof(T) == 4 ? KL_P2M_WAVES_PER_EU : 1
       g_p2m_evaluated += __popcll(mask);
       g_p2m_skipped += (uint64_t)min(64, n - s0) - __popcll(mask);
 #endif
+      if (pairs && SUBC) {
+        // r06: the kept faces 8 at a time.  Lane L bounds face L & 7 of the batch against its own
+        // sub-cluster (lanes 8 (L >> 3) ..; the wave test's sphere bound with the group's centre,
+        // radius and largest per-point threshold); the passing (face, sub-cluster) pairs are listed
+        // and take the per-point test 8 at a time -- lane l tests pair l >> 3 with the point of lane
+        // 8 j + (l & 7), fetched by ds_bpermute with its threshold -- so the per-point test is issued
+        // for the pairs some point of a sub-cluster can need, not for all 64 lanes per kept face.
+        // Each bound is conservative (a skip is proven, R and the thresholds only overestimate), so
+        // every pair the r05 per-point test passes still passes: the queued pairs and the minimum
+        // are unchanged.
+        const T gpsq = [&]() {
+          T v = valid ? psq : (T)INFINITY;
+#pragma unroll
+          for (int o = 1; o < 8; o <<= 1) v = fmax(v, __shfl_xor(v, o));
+          return v;
+        }();
+        while (mask) {
+          int myf = 0, nbf = 0;  // lane k < 8: the batch's k-th kept face slot
+#pragma unroll
+          for (int k = 0; k < 8; k++) {
+            if (mask) {
+              const int sj = s0 + __builtin_ctzll(mask);
+              mask &= mask - 1;
+              if (lane == k) myf = sj;
+              nbf++;
+            }
+          }
+          const int kf = lane & 7;
+          const int fk = __shfl(myf, kf);
+          bool sub = kf < nbf;
+          if (sub) {
+            const FaceRec<T> &fr = sf[fk];
+            const T sl = (T)(256.0 * P2M_E) * (cinf + R + fr.hmax);
+            const T A = fmax(fabs(dot(cj, fr.un) - sp.dv[fk]) - fr.thick - sl, (T)0);
+            T b = dot(cj, mk(sp.o[0][fk], sp.o[1][fk], sp.o[2][fk])) - sp.off[0][fk];
+            b = fmax(b, dot(cj, mk(sp.o[3][fk], sp.o[4][fk], sp.o[5][fk])) - sp.off[1][fk]);
+            b = fmax(b, dot(cj, mk(sp.o[6][fk], sp.o[7][fk], sp.o[8][fk])) - sp.off[2][fk]);
+            const T B = fmax(b - sl, (T)0);
+            const T K = (Rj + gpsq) * (T)(1.0 + 16.0 * P2M_E) + sl;
+            if ((A * A + B * B) * (T)(1.0 - 32.0 * P2M_E) > K * K * (T)(1.0 + 32.0 * P2M_E)) sub = false;
+          }
+          const uint64_t sm = __ballot(sub);
+          const int np = __popcll(sm);
+          // the kept (face, sub-cluster) pairs of the batch, in lane order: lane index L per entry
+          if (sub) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+            s_sp[wid][rank] = (uint8_t)lane;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          for (int c = 0; c < np; c += 8) {  // wave-uniform
+            const int e = c + (lane >> 3);
+            const bool on = e < np;
+            const int L = on ? (int)s_sp[wid][e] : 0;
+            const int sj = __shfl(myf, L & 7);
+            const int owner = (L & ~7) | (lane & 7);
+            const V3<T> pp = mk(__shfl(p.x, owner), __shfl(p.y, owner), __shfl(p.z, owner));
+            const T opsq = __shfl(psq, owner);
+            const bool ovalid = __shfl((int)valid, owner) != 0;
+            const FaceRec<T> &fr = sf[sj];
+            const T sl = (T)(256.0 * P2M_E) * (cinf + R + fr.hmax);
+            const T A = fmax(fabs(dot(pp, fr.un) - sp.dv[sj]) - fr.thick - sl, (T)0);
+            T b = dot(pp, mk(sp.o[0][sj], sp.o[1][sj], sp.o[2][sj])) - sp.off[0][sj];
+            b = fmax(b, dot(pp, mk(sp.o[3][sj], sp.o[4][sj], sp.o[5][sj])) - sp.off[1][sj]);
+            b = fmax(b, dot(pp, mk(sp.o[6][sj], sp.o[7][sj], sp.o[8][sj])) - sp.off[2][sj]);
+            const T B = fmax(b - sl, (T)0);
+            const T K = opsq + sl;
+            const bool pass = on && ovalid && !((A * A + B * B) * (T)(1.0 - 32.0 * P2M_E) > K * K * (T)(1.0 + 32.0 * P2M_E));
+            const uint64_t pm = __ballot(pass);
+            if (pass) {
+              const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+              s_q[wid][(qhead + qcnt + rank) & (P2M_QCAP - 1)] = (uint16_t)(owner | (sj << 6));
+            }
+            qcnt += (uint32_t)__popcll(pm);
+#ifdef KL_P2M_PROBE
+            g_p2m_pairs += __popcll(pm);
+#endif
+            if (qcnt >= 64) {
+              __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              run_batch(64);
+            }
+          }
+        }
+        continue;
+      }
       if (pairs) {
         // the per-point test of each kept face (the wave test's bound with this lane's point, R = 0),
         // passing pairs appended to the ring
@@ -1120,6 +1230,10 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
   if (g_dev_param[11] == 4 || !order) {  // dev param 11 = 4: the wave-level walk alone (r04)
     hipLaunchKernelGGL((p2m_fwd_kernel<T, false>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
                        (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);
+  } else if (g_dev_param[11] == 5) {  // dev param 11 = 5: the r05 pairs path (per-point test per kept face)
+    hipLaunchKernelGGL((p2m_fwd_kernel<T, true, false>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st,
+                       (const T *)pts, (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt,
+                       bounds_c, gbest);
   } else {
     hipLaunchKernelGGL((p2m_fwd_kernel<T, true>), dim3(pblocks, (unsigned)splits), dim3(256), 0, st, (const T *)pts,
                        (const T *)fv, order, P, F, split_faces, (T *)dist, idx, type, pd, pidx, pt, bounds_c, gbest);

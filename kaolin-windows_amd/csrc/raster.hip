@@ -954,8 +954,8 @@ static int launch_rast_tile(RastSrc<T> src, int H, int W, int B, int D, int F, c
   hipLaunchKernelGGL(tile_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt, items,
                      identity, split_from, split_log2, nitems);
   KL_CHECK_LAUNCH();
-  const RastTileArgs<T> args{src, fvz, feat, bitmap, rec, rng, items, nitems, g, F, D, eps, out_feat, out_idx, out_w,
-                             reinterpret_cast<uint64_t *>(g_dev_debug)};
+  RastTileArgs<T> args{src, fvz, feat, bitmap, rec, rng, items, nitems, g, F, D, eps, out_feat, out_idx, out_w,
+                       reinterpret_cast<uint64_t *>(g_dev_debug)};
   hipLaunchKernelGGL((raster_tile_kernel<T>), dim3((unsigned)(nt << split_log2)), dim3(512), 0, st, args);
   KL_CHECK_LAUNCH();
   return KL_OK;

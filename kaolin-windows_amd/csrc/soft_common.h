@@ -47,15 +47,15 @@ __device__ __forceinline__ void soft_dist(T x0, T y0, const T v[6], float multip
 // Pixel interval [lo, hi] (lane indices of the row segment starting at pixel ibase,
 // clipped to [0, 63]) whose centres c satisfy  x_lo <= c < x_hi  exactly as the
 // reference's float/double comparisons decide it: a float estimate, then corrected
-// against the exact centre formula (monotone in the index).  NaN bounds never reject.
+// against the exact centre formula (monotone in the index).  A NaN bound never rejects: its
+// comparison is false, so it stands for -inf (x_lo) or +inf (x_hi) -- the other bound still
+// applies (r06: a single NaN bound had widened the interval to the whole segment, unlike the
+// reference's `x0 < xmin || x0 >= xmax`; found by a caller-bbox test of the _C contract path).
 // sx = m / W (the reference's float pixel pitch), inv = W / m (estimate only).
 template <typename T>
 __device__ __forceinline__ void seg_range_s(T x_lo, T x_hi, float sx, float inv, int W, int ibase, int &lo, int &hi) {
-  if (!(x_lo == x_lo) || !(x_hi == x_hi)) {
-    lo = 0;
-    hi = 63;
-    return;
-  }
+  if (!(x_lo == x_lo)) x_lo = (T)-INFINITY;
+  if (!(x_hi == x_hi)) x_hi = (T)INFINITY;
   auto est = [&](T c) -> int {  // index = (c / s + W - 1) / 2
     const float t = ((float)c * inv + (float)(W - 1)) * 0.5f - (float)ibase;
     return t < -1.0f ? -1 : (t > 64.0f ? 64 : (int)ceilf(t));
@@ -172,6 +172,21 @@ struct FaceHash {
   }
 };
 
+// A wave's fill of [p, p + bytes) with the 32-bit pattern v (bytes of v in memory order): byte
+// stores up to the first 16-byte boundary, then 16-byte stores -- 1 KB per wave instruction --
+// then the tail bytes.
+__device__ __forceinline__ void wave_fill(uint8_t *p, size_t bytes, uint32_t v, int lane) {
+  size_t head = (16 - ((uintptr_t)p & 15)) & 15;
+  if (head > bytes) head = bytes;
+  if ((size_t)lane < head) p[lane] = (uint8_t)(v >> (8 * (((uintptr_t)p + lane) & 3)));
+  uint8_t *body = p + head;
+  const size_t nvec = (bytes - head) / 16;
+  const uint4 q = make_uint4(v, v, v, v);
+  for (size_t i = lane; i < nvec; i += 64) reinterpret_cast<uint4 *>(body)[i] = q;
+  const size_t done = head + nvec * 16;
+  if ((size_t)lane < bytes - done) p[done + lane] = (uint8_t)(v >> (8 * (((uintptr_t)p + done + lane) & 3)));
+}
+
 // Forward work items (tileorder.h, order_soft_items): a 4-wave workgroup takes 8 >> lp rows of
 // a tile with Q = 4 / (8 >> lp) waves per row.
 constexpr int ST_WAVES = 4;
@@ -257,6 +272,11 @@ struct DibrSoftAcc {
   }
 };
 size_t soft_tile_bwd_ws_bytes(int B, int H, int W, int F, int K);
+// the _C contract forward on the tile path (softtile.hip, f32, knum <= 255): the reference's slot tensors
+size_t soft_tile_slots_ws_bytes(int B, int H, int W, int F);
+int soft_tile_forward_slots(int B, int H, int W, int F, int K, const float *fvi, const float *bbox, const int64_t *sel,
+                            float sigmainv, float m, float *mask, float *prob, int64_t *cidx, uint8_t *ctype, void *ws,
+                            size_t ws_bytes, hipStream_t st);
 size_t soft_tile_ws_bytes(int B, int H, int W, int F);
 
 }  // namespace kl

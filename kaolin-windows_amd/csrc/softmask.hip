@@ -22,21 +22,6 @@
 
 namespace kl {
 
-// A wave's fill of [p, p + bytes) with the 32-bit pattern v (bytes of v in memory order): byte
-// stores up to the first 16-byte boundary, then 16-byte stores -- 1 KB per wave instruction --
-// then the tail bytes.
-__device__ __forceinline__ void wave_fill(uint8_t *p, size_t bytes, uint32_t v, int lane) {
-  size_t head = (16 - ((uintptr_t)p & 15)) & 15;
-  if (head > bytes) head = bytes;
-  if ((size_t)lane < head) p[lane] = (uint8_t)(v >> (8 * (((uintptr_t)p + lane) & 3)));
-  uint8_t *body = p + head;
-  const size_t nvec = (bytes - head) / 16;
-  const uint4 q = make_uint4(v, v, v, v);
-  for (size_t i = lane; i < nvec; i += 64) reinterpret_cast<uint4 *>(body)[i] = q;
-  const size_t done = head + nvec * 16;
-  if ((size_t)lane < bytes - done) p[done + lane] = (uint8_t)(v >> (8 * (((uintptr_t)p + done + lane) & 3)));
-}
-
 // Forward, one wave per 64-pixel row segment, three phases:
 //  1. selection: walk the candidate chunks of the tile in ascending order (the next
 //     chunk's bboxes are loaded while the current one is tested).  Each lane takes one
@@ -47,11 +32,7 @@ __device__ __forceinline__ void wave_fill(uint8_t *p, size_t bytes, uint32_t v, 
 //  2. evaluation: the wave's hits, flattened, are evaluated 64 at a time with every
 //     lane busy (distance, probability, type), written straight to their output slots
 //     and the probabilities kept in LDS for the in-order product;
-//  0. (r06) before the walk, the row segment's whole slot ranges are written as padding (idx -1,
-//     prob 0, type 0) with 16-byte stores (wave_fill): the padding is ~97 % of the 13 B x knum per
-//     pixel, and per-element predicated stores of it (the r05 phase 3: byte stores for the types,
-//     gaps at every hit) held the kernel to 0.40 of HBM; phase 2's hit stores overwrite their
-//     slots after these have completed.
+//  3. the unused slots (-1 / 0 / 0) are written with lane-contiguous stores.
 // LDS per wave: K x 64 slots of sizeof(T) (face id, then its probability) + 2 x 64 ints.
 template <typename T, typename Src>
 __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
@@ -88,15 +69,6 @@ __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
   // phase 1 view: the id of slot (k, lane) lives in the first 4 bytes of s_slot[k*64 + lane]
   uint32_t *s_face = reinterpret_cast<uint32_t *>(s_slot);
   constexpr int ID_STEP = (int)(sizeof(T) / sizeof(uint32_t));
-  const size_t rowpix0 = ((size_t)b * H + j) * W + (size_t)ibase;
-
-  // ---- phase 0: the row segment's slots as padding (in flight during the walk)
-  if (K > 0) {
-    const size_t ne = (size_t)min(64, W - ibase) * K;
-    wave_fill(reinterpret_cast<uint8_t *>(out_idx + rowpix0 * K), ne * sizeof(int64_t), 0xffffffffu, lane);
-    wave_fill(reinterpret_cast<uint8_t *>(out_prob + rowpix0 * K), ne * sizeof(T), 0u, lane);
-    wave_fill(out_type + rowpix0 * K, ne, 0u, lane);
-  }
 
   // ---- phase 1: selection
   int kid = 0;
@@ -192,9 +164,7 @@ __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
   s_pre[lane] = pre - kid;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  // the padding stores (other lanes' too) complete before any hit overwrites its slot
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
+  const size_t rowpix0 = ((size_t)b * H + j) * W + (size_t)ibase;
   for (int e = lane; e < total; e += 64) {
     int lo = 0;  // owner lane p: last lane with s_pre[p] <= e (and a hit)
 #pragma unroll
@@ -231,6 +201,30 @@ __global__ void __launch_bounds__(256) soft_mask_fwd_kernel(
     out_mask[pix] = res;
   }
 
+  // ---- phase 3: the unused slots of this row segment, lane-contiguous
+  if (K == 0) return;
+  const int n = min(64, W - ibase);
+  const int ne = n * K;
+  int p = 0, k = lane;  // element e = p*K + k, advanced incrementally (no division)
+  while (k >= K) {
+    k -= K;
+    p++;
+  }
+  const int dp = 64 / K, dk = 64 - dp * K;
+  for (int e = lane; e < ne; e += 64) {
+    if (k >= s_kid[p]) {
+      const size_t o = rowpix0 * K + e;
+      out_idx[o] = -1;
+      out_prob[o] = (T)0;
+      out_type[o] = 0;
+    }
+    p += dp;
+    k += dk;
+    if (k >= K) {
+      k -= K;
+      p++;
+    }
+  }
 }
 
 // Backward, aggregated: one 512-thread workgroup per 64x8 tile (one wave per row
@@ -423,7 +417,7 @@ static int soft_mask_bwd(int B, int H, int W, int F, int K, const void *grad, co
 using namespace kl;
 
 extern "C" size_t kl_soft_mask_workspace_bytes(int batch, int height, int width, int num_faces) {
-  return sm_ws_bytes(batch, height, width, num_faces);
+  return std::max(sm_ws_bytes(batch, height, width, num_faces), soft_tile_slots_ws_bytes(batch, height, width, num_faces));
 }
 
 extern "C" int kl_dibr_soft_mask_forward(kl_dtype dtype, int batch, int height, int width, int num_faces,
@@ -431,6 +425,13 @@ extern "C" int kl_dibr_soft_mask_forward(kl_dtype dtype, int batch, int height, 
                                          float sigmainv, float multiplier, void *mask, void *prob,
                                          int64_t *cidx, uint8_t *ctype, void *ws, size_t ws_bytes,
                                          kl_stream stream) {
+  // f32 with knum <= 255: the tile path (softtile.hip, soft_tile_forward_slots: multi-wave heavy rows,
+  // padding in 16-byte stores); else the per-row-wave kernel above.  Dev param 30 = 1: that kernel for
+  // f32 too (A/B).
+  if (dtype == KL_F32 && knum >= 0 && knum <= 255 && num_faces < (1 << 28) && g_dev_param[30] != 1)
+    return soft_tile_forward_slots(batch, height, width, num_faces, knum, (const float *)fvi, (const float *)bbox, sel,
+                                   sigmainv, multiplier, (float *)mask, (float *)prob, cidx, ctype, ws, ws_bytes,
+                                   S(stream));
   if (dtype == KL_F32)
     return soft_mask_fwd<float>(BboxSrc<float>{(const float *)bbox, (const float *)fvi}, (const float *)bbox, batch,
                                 height, width, num_faces, knum, sel, sigmainv, multiplier, mask, prob, cidx, ctype,

@@ -39,9 +39,10 @@
 namespace kl {
 
 
-template <typename T>
+template <typename T, typename Src = SoftSrc<T>>
 struct SoftTileArgs {
-  SoftSrc<T> src;            // unscaled face_vertices_image, multiplier, bbox pad
+  Src src;                   // SoftSrc: unscaled face_vertices_image, multiplier, bbox pad; BboxSrc (the
+                             // _C contract): multiplied face_vertices_image and the caller's bboxes
   const uint2 *rng;          // (B*F) exact pixel ranges of the enlarged bboxes (binning pass)
   const int64_t *sel;        // (B,H,W) rasterized face index
   const uint32_t *bitmap;
@@ -78,11 +79,15 @@ struct SoftTileArgs {
   // go to [0, pcap) floats -- the fill list, the walk's counts and the spare bytes up to the LDS
   // budget, all dead once the walk is done; the rest is read back from rec_prob
   int pcap = 0;
+  // The _C contract (kl_dibr_soft_mask_forward, r06): the reference's (B,H,W,knum) prob / idx / type
+  // slot tensors written directly.  Each item's rows are padded first (idx -1, prob 0, type 0: 16-byte
+  // stores issued before the walk, in flight during it), then every hit is stored at its slot after
+  // those stores completed; no compact records (rec_face == nullptr).
+  T *slot_prob = nullptr;
+  int64_t *slot_idx = nullptr;
+  uint8_t *slot_type = nullptr;
   int wcnt_off = 0;  // byte offset of the 16 per-wave scratch ints
   int rows_off = 0;  // byte offset of the rows' slot lists
-  // 1: the LDS holds ST_WAVES slot lists (lp_min 1) -- one per wave: a row's Q waves walk contiguous
-  // runs of the face list into their own lists, merged by the row's first wave (list r * Q)
-  int wave_lists = 0;
 };
 
 
@@ -135,8 +140,8 @@ struct StFwdLayout {
 
 // Forward, one work item (a part of a tile's rows) per 4-wave workgroup: fill and walk (1a,
 // 1b below), the dense evaluation by the row's Q waves, the mask by its first wave.
-template <typename T, typename S>
-__global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(SoftTileArgs<T> a) {
+template <typename T, typename S, typename Src = SoftSrc<T>>
+__global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(SoftTileArgs<T, Src> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   {
     const int ni = *a.nitems;
@@ -161,9 +166,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
   int *s_wcnt = reinterpret_cast<int *>(smem + a.wcnt_off);  // [16] per-wave scratch
   const size_t row_lds = st_row_lds_s(K, sizeof(S));
   unsigned char *const rows0 = smem + a.rows_off;
-  const bool wl = a.wave_lists != 0;
-  const int LQ = wl ? Q : 1;  // row r's list is list r * LQ (with wave lists: its first wave's)
-  unsigned char *rowmem = rows0 + row_lds * (wl ? wid : r);
+  unsigned char *rowmem = rows0 + row_lds * r;
   S *s_face = reinterpret_cast<S *>(rowmem);                                 // [K][64]
   int *s_pre = reinterpret_cast<int *>(rowmem + (size_t)K * 64 * sizeof(S));  // [64], then total
   const int tx = tile % g.tiles_x;
@@ -178,6 +181,13 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
   const bool covered = px_valid ? (a.sel[pix] >= 0) : true;
   const int64_t f0 = (int64_t)b * a.F;
   const int F = a.F;
+  const bool slots = a.slot_prob != nullptr;  // (launch-uniform)
+  if (slots && qi == 0 && row_ok && K > 0) {  // the row's slot ranges as padding (see SoftTileArgs)
+    const size_t e0 = ((size_t)b * H + j) * W + (size_t)ibase, ne = (size_t)min(64, W - ibase) * K;
+    wave_fill(reinterpret_cast<uint8_t *>(a.slot_idx + e0 * K), ne * sizeof(int64_t), 0xffffffffu, lane);
+    wave_fill(reinterpret_cast<uint8_t *>(a.slot_prob + e0 * K), ne * sizeof(T), 0u, lane);
+    wave_fill(a.slot_type + e0 * K, ne, 0u, lane);
+  }
   const int swz = a.swz;
   auto sl = [swz](int k, int p) { return k * 64 + ((p + (k & swz)) & 63); };
   uint64_t t0 = 0, w0 = 0, t1 = 0, c_fill = 0, tf = 0;
@@ -320,52 +330,6 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
           }
           amask = ballot(active);
         }
-      } else if (wl) {
-        // r06: the row's Q waves split this round's list into Q contiguous runs of blocks; each
-        // appends its run's hits to its OWN slot list with no barrier between blocks (the per-block
-        // rounds of the branch below take two workgroup barriers and a cross-wave prefix per block,
-        // and set the heavy pole items' walk); then the row's first wave appends the others' lists
-        // after its own in wave order -- their concatenation is index order -- up to knum.
-        int *s_cnt = reinterpret_cast<int *>(smem + (size_t)ST_LIST_CAP * 8);  // [ST_WAVES][64]
-        const int b0 = nb * qi / Q, b1 = nb * (qi + 1) / Q;
-        const int lim = K - kid;             // hits this wave may add per pixel (>= 1 where active)
-        const int pos0 = qi == 0 ? kid : 0;  // own-list slot of its first hit this round
-        int n = 0;
-        bool act = active;
-        uint64_t am = amask;
-        for (int blk = b0; blk < b1 && am; blk++) {
-          const uint64_t rm = block_mask(blk);
-          if (!ballot((rm & am) != 0)) continue;
-          uint64_t cm = transpose64(rm, lane);
-          if (!act) cm = 0;
-          const int base = blk * 64;
-          while (cm) {
-            const int q = __builtin_ctzll(cm);
-            cm &= cm - 1;
-            s_face[sl(pos0 + n, lane)] = (S)L_face[base + q];
-            if (++n >= lim) {
-              act = false;
-              cm = 0;
-            }
-          }
-          am = ballot(act);
-        }
-        s_cnt[wid * 64 + lane] = n;
-        __syncthreads();
-        int tot = 0;
-        for (int q = 0; q < Q; q++) tot += s_cnt[(r * Q + q) * 64 + lane];
-        if (qi == 0) {  // waves 1 .. Q-1's runs after this wave's, in wave order
-          int cur = kid + n;
-          for (int q = 1; q < Q && cur < K; q++) {
-            const int c = s_cnt[(wid + q) * 64 + lane];
-            const S *src = reinterpret_cast<const S *>(rows0 + row_lds * (wid + q));
-            for (int k = 0; k < c && cur < K; k++) s_face[sl(cur++, lane)] = src[sl(k, lane)];
-          }
-        }
-        // (every wave of the row: the merged count; the lists are read before the round-end barriers)
-        kid = min(K, kid + tot);
-        active = active && kid < K;
-        amask = ballot(active);
       } else {
         // per-wave counts of this round ([Q][64] per row, in the head: with knum > 55 the rows
         // past RP are not allocated)
@@ -422,7 +386,9 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
   }
   if (dbg) t1 = stamp_clk();
   const bool inline_eval = sizeof(T) == 4 && K > 0;
-  // every row's prefix and total are read by every wave of the workgroup below (f32)
+  // every row's prefix and total are read by every wave of the workgroup below (f32); with slot
+  // outputs the padding stores complete first, as any thread may store a hit over them
+  if (slots) __builtin_amdgcn_s_waitcnt(0);
   if (Q > 1 || inline_eval) {
     __syncthreads();
   } else {
@@ -442,7 +408,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
     rpre[0] = 0;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      rtot[q] = q < RP ? *reinterpret_cast<const int *>(rows0 + row_lds * (q * LQ) + (size_t)K * 64 * sizeof(S) +
+      rtot[q] = q < RP ? *reinterpret_cast<const int *>(rows0 + row_lds * q + (size_t)K * 64 * sizeof(S) +
                                                           64 * sizeof(int))
                        : 0;
       rpre[q + 1] = rpre[q] + rtot[q];
@@ -463,7 +429,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
 #pragma unroll
         for (int q = 1; q < 8; q++) r0 += (q < RP && rpre[q] <= g0) ? 1 : 0;
         const int e = g0 - rpre[r0];
-        const int *pre_r = reinterpret_cast<const int *>(rows0 + row_lds * (r0 * LQ) + (size_t)K * 64 * sizeof(S));
+        const int *pre_r = reinterpret_cast<const int *>(rows0 + row_lds * r0 + (size_t)K * 64 * sizeof(S));
         int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
 #pragma unroll
         for (int st = 32; st > 0; st >>= 1)
@@ -472,7 +438,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
         kk[u] = e - pre_r[lo];
         rr[u] = r0;
         ee[u] = e;
-        const S *face_r = reinterpret_cast<const S *>(rows0 + row_lds * (r0 * LQ));
+        const S *face_r = reinterpret_cast<const S *>(rows0 + row_lds * r0);
         ff[u] = g0 < all ? (uint32_t)face_r[sl(kk[u], lo)] : 0u;
         if (kDevStamps && a.dev) ff[u] = min(ff[u], (uint32_t)(F - 1));  // dev ablations leave no face ids
       }
@@ -490,9 +456,16 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
           soft_dist<T>((T)(sx * (float)(2 * (ibase + pp[u]) + 1 - W)), y0, v[u], m, dsq, edgeid);
           const T z = (T)a.sigmainv * dsq / (T)m / (T)m;
           const T pr = kl_exp<T>(-z);
-          const size_t rb = ((size_t)(b * H + jr) * g.tiles_x + tx) * 64 * (size_t)K;
-          a.rec_face[rb + ee[u]] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
-          a.rec_prob[rb + ee[u]] = pr;
+          if (slots) {
+            const size_t o = (((size_t)b * H + jr) * W + (size_t)(ibase + pp[u])) * K + kk[u];
+            a.slot_prob[o] = pr;
+            a.slot_idx[o] = (int64_t)ff[u];
+            a.slot_type[o] = (uint8_t)(edgeid + 1);
+          } else {
+            const size_t rb = ((size_t)(b * H + jr) * g.tiles_x + tx) * 64 * (size_t)K;
+            a.rec_face[rb + ee[u]] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
+            a.rec_prob[rb + ee[u]] = pr;
+          }
           if (g0 < a.pcap) s_prob[g0] = pr;  // item-wide (row, pixel, slot) order
         }
       }
@@ -509,7 +482,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
 #pragma unroll
       for (int q = 0; q < 8; q++) rp0 += q < r ? rtot[q] : 0;
       const int g1 = rp0 + s_pre[lane];
-      const T *gp = a.rec_prob + rbase + s_pre[lane];
+      const T *gp = slots ? a.slot_prob + pix * K : a.rec_prob + rbase + s_pre[lane];
       T allprob = (T)1.0;
       for (int k0 = 0; k0 < kid; k0 += 8) {
         T pk[8];
@@ -985,9 +958,6 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   args.pcap = sizeof(T) == 4 ? lay.pcap : 0;
   if (g_dev_param[28] > 0) args.pcap = std::min(args.pcap, g_dev_param[28] - 1);  // dev: force the read-back
   args.wcnt_off = (int)lay.wcnt_off;
-  // one slot list per wave where the layout holds ST_WAVES of them (dev param 30 = 1: the per-block
-  // rounds over shared row lists, A/B)
-  args.wave_lists = ((TILE_H >> lp_min) == ST_WAVES && g_dev_param[30] != 1) ? 1 : 0;
   args.rows_off = (int)lay.rows_off;
   const dim3 grid((unsigned)soft_items_bound(nt, lp_min, soft_split()));
   if (narrow)
@@ -1113,6 +1083,95 @@ template int soft_tile_backward<double>(int, int, int, int, int, const double *,
                                         void *, size_t, hipStream_t, double *, bool *);
 
 size_t soft_tile_ws_bytes(int B, int H, int W, int F) { return StWs(make_bin_geom(B, H, W, F), F).bytes; }
+
+// ---- The _C contract soft-mask forward on the tile machinery (r06; kl_dibr_soft_mask_forward, f32,
+// knum <= 255).  The reference's dibr_soft_mask_forward_cuda writes, per pixel, knum slots of prob /
+// idx / type -- 13 B x knum, 409 MB at cfg3, ~97 % of it padding.  softmask.hip's kernel walks every
+// row with ONE wave (a heavy pole row takes the whole kernel's time on its own, 140 us at cfg3); here
+// the caller's bboxes go through the same binning, heavy-first item order and multi-wave rows as the
+// compact path, and the kernel stores the slot tensors directly (SoftTileArgs::slot_*).  Workspace:
+// the compact path's (StWs) + hits (B*H*W bytes) + segment totals; no compact records.
+struct StSlotWs {
+  size_t hits, seg, scratch, bytes;
+  StSlotWs(int B, int H, int W, int F) {
+    const BinGeom g = make_bin_geom(B, H, W, F);
+    hits = al256(StWs(g, F).bytes);
+    seg = hits + al256((size_t)B * H * W);
+    scratch = seg + al256((size_t)B * H * g.tiles_x * sizeof(int));
+    bytes = scratch + 256;
+  }
+};
+size_t soft_tile_slots_ws_bytes(int B, int H, int W, int F) { return StSlotWs(B, H, W, F).bytes; }
+
+int soft_tile_forward_slots(int B, int H, int W, int F, int K, const float *fvi, const float *bbox, const int64_t *sel,
+                            float sigmainv, float m, float *mask, float *prob, int64_t *cidx, uint8_t *ctype, void *ws,
+                            size_t ws_bytes, hipStream_t st) {
+  const BinGeom g = make_bin_geom(B, H, W, F);
+  const StWs L(g, F);
+  const StSlotWs SL(B, H, W, F);
+  KL_REQUIRE(ws_bytes >= SL.bytes, "dibr_soft_mask_forward: workspace too small");
+  KL_REQUIRE(K >= 0 && K <= 255 && F < (1 << 28), "dibr_soft_mask_forward: tile path needs knum <= 255");
+  if ((int64_t)B * H * W == 0) return KL_OK;
+  char *w = reinterpret_cast<char *>(ws);
+  uint32_t *bitmap = reinterpret_cast<uint32_t *>(w);
+  int *ghist = reinterpret_cast<int *>(w + L.hist);
+  uint8_t *bk = reinterpret_cast<uint8_t *>(w + L.bk);
+  int32_t *order = reinterpret_cast<int32_t *>(w + L.order);
+  uint2 *rng = reinterpret_cast<uint2 *>(w + L.rng);
+  int *nitems = reinterpret_cast<int *>(w + L.nitems);
+  int *scratch = reinterpret_cast<int *>(w + SL.scratch);
+  const BboxSrc<float> src{bbox, fvi};
+  KL_CHECK_RC((launch_binning<float, BboxSrc<float>>(src, nullptr, F, g, m, bitmap, st, nullptr, L.zero, rng)));
+  const int nt = g.batch * g.tiles_y * g.tiles_x;
+  hipLaunchKernelGGL(tile_bucket_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)bitmap,
+                     g.words, nt, bk, ghist, scratch);
+  KL_CHECK_LAUNCH();
+  const int lp_min = soft_lp_min(K);
+  hipLaunchKernelGGL(soft_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt, order,
+                     lp_min, nitems, soft_split());
+  KL_CHECK_LAUNCH();
+  const bool narrow = F <= 65536 && g_dev_param[29] != 1;
+  const StFwdLayout lay(K, TILE_H >> lp_min, narrow ? 2 : 4, ST_LDS_BUDGET);
+  KL_REQUIRE(lay.bytes <= 160 * 1024, "dibr_soft_mask: knum too large for the LDS slot lists");
+  SoftTileArgs<float, BboxSrc<float>> a{};
+  a.src = src;
+  a.rng = rng;
+  a.sel = sel;
+  a.bitmap = bitmap;
+  a.order = order;
+  a.nitems = nitems;
+  a.g = g;
+  a.F = F;
+  a.K = K;
+  a.sigmainv = sigmainv;
+  a.m = m;
+  a.mask = mask;
+  a.hits = reinterpret_cast<uint8_t *>(w + SL.hits);
+  a.rec_face = nullptr;
+  a.rec_prob = nullptr;
+  a.seg_tot = reinterpret_cast<int *>(w + SL.seg);
+  a.defer = reinterpret_cast<uint8_t *>(w + L.defer);
+  a.dbg = (uint64_t *)g_dev_debug;
+  a.dev = g_dev_flags;
+  a.prefilled = 0;
+  a.swz = g_dev_param[19] == 1 ? 0 : 63;
+  a.pcap = lay.pcap;
+  if (g_dev_param[28] > 0) a.pcap = std::min(a.pcap, g_dev_param[28] - 1);
+  a.slot_prob = prob;
+  a.slot_idx = cidx;
+  a.slot_type = ctype;
+  a.wcnt_off = (int)lay.wcnt_off;
+  a.rows_off = (int)lay.rows_off;
+  const dim3 grid((unsigned)soft_items_bound(nt, lp_min, soft_split()));
+  if (narrow)
+    hipLaunchKernelGGL((soft_tile_fwd_kernel<float, uint16_t, BboxSrc<float>>), grid, dim3(64 * ST_WAVES), lay.bytes,
+                       st, a);
+  else
+    hipLaunchKernelGGL((soft_tile_fwd_kernel<float, uint32_t, BboxSrc<float>>), grid, dim3(64 * ST_WAVES), lay.bytes,
+                       st, a);
+  KL_CHECK_LAUNCH();
+  return KL_OK;
+}
 
 }  // namespace kl
 

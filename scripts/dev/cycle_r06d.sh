@@ -24,6 +24,11 @@ for i in 1 2; do
   timeout -k 10 120 python scripts/dev/param_ab.py 30 0 1 0 1 >> $OUT/ab.txt 2>&1
   KAOLIN_HIP_LIB=$R/scripts/dev/_bin/r05lib/libkaolin_hip.so timeout -k 10 120 python scripts/dev/param_ab.py 0 0 | sed 's/^/r05 /' >> $OUT/ab.txt 2>&1
 done
+for i in 1 2; do
+  timeout -k 10 120 python scripts/dev/param_ab.py 31 0 1 0 1 | sed 's/^/g2 /' >> $OUT/ab.txt 2>&1
+  KAOLIN_HIP_LIB=$R/scripts/dev/_bin/g2mw4/libkaolin_hip.so timeout -k 10 120 python scripts/dev/param_ab.py 0 0 | sed 's/^/g2mw4 /' >> $OUT/ab.txt 2>&1
+  KAOLIN_HIP_LIB=$R/scripts/dev/_bin/g2b2/libkaolin_hip.so timeout -k 10 120 python scripts/dev/param_ab.py 0 0 | sed 's/^/g2b2 /' >> $OUT/ab.txt 2>&1
+done
 grep params $OUT/ab.txt
 echo new; cut -c1-200 $OUT/csm_new.log | grep -o "'ms': [0-9.]*\|'frac': [0-9.]*"
 echo r05; cut -c1-200 $OUT/csm_r05.log | grep -o "'ms': [0-9.]*\|'frac': [0-9.]*"

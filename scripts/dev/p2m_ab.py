@@ -5,7 +5,11 @@ import ctypes
 import os
 import sys
 
-import torch
+ROOT0 = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault('KAOLIN_HIP_LIB', os.path.join(ROOT0, 'kaolin-windows_amd', 'kaolin', '_lib', 'dev',
+                                                     'libkaolin_hip.so'))
+os.environ.setdefault('KAOLIN_NO_EXT', '1')
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)

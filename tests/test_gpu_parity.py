@@ -1005,12 +1005,13 @@ def _p2m_stress(kind, dtype):
 @pytest.mark.devlib
 @pytest.mark.parametrize('dtype', [torch.float32, torch.float64])
 @pytest.mark.parametrize('kind', ['cfg2', 'slivers', 'scaled', 'onsurface', 'dups'])
-@pytest.mark.parametrize('walk', ['pairs', 'wave'])
+@pytest.mark.parametrize('walk', ['pairs', 'wave', 'pairs_r05'])
 def test_p2m_face_skipping_is_exact(kal, kind, dtype, walk):
     """P*F >= 2^24 takes the Morton-ordered path whose waves skip faces that provably cannot
     be nearest; results must stay bit-identical to the oracle's full scan -- with the per-point pair
-    queue (default; proper faces and finite waves) and with the wave-level walk alone (dev param
-    11 = 4).  'dups': duplicated proper faces within and across the face splits, points on their
+    queue (default, r06: per-point tests only for the (face, 8-point sub-cluster) pairs a sub-cluster
+    bound keeps; proper faces and finite waves), with the r05 pair queue (every kept face's per-point
+    test, dev param 11 = 5) and with the wave-level walk alone (dev param 11 = 4).  'dups': duplicated proper faces within and across the face splits, points on their
     vertices (distance-0 ties: the earliest face wins)."""
     pts, fv = _p2m_stress(kind, dtype)
     P, F = len(pts), len(fv)
@@ -1019,7 +1020,7 @@ def test_p2m_face_skipping_is_exact(kal, kind, dtype, walk):
     i = torch.empty(P, dtype=torch.long, device=DEV)
     t = torch.empty(P, dtype=torch.int32, device=DEV)
     try:
-        _dev_param(11, 4 if walk == 'wave' else 0)
+        _dev_param(11, {'wave': 4, 'pairs_r05': 5}.get(walk, 0))
         kal._C.metrics.unbatched_triangle_distance_forward_cuda(T(pts), T(fv), d, i, t)
     finally:
         _dev_param(11, 0)
@@ -1852,9 +1853,8 @@ def test_rayops_error_messages(kal):
 def test_soft_slot_width_and_prob_readback_equal(kal, case):
     """r06 soft forward layout: 16-bit slot lists (F <= 65536) against 32-bit ones (dev param 29 = 1),
     and the mask's probabilities from LDS against the rec_prob read-back past the LDS capacity (dev
-    param 28 = n: capacity n - 1 floats; 1: every probability read back), and the multi-wave rows' walk
-    into per-wave lists merged in wave order against the per-block rounds over one shared row list
-    (dev param 30 = 1) -- every output and the compact state equal."""
+    param 28 = n: capacity n - 1 floats; 1: every probability read back) -- every output and the
+    compact state equal."""
     import bench
     if case == 'adversarial':
         z, v, f = _adversarial_faces(torch.float32)
@@ -1868,7 +1868,7 @@ def test_soft_slot_width_and_prob_readback_equal(kal, case):
         K = {'knum64': 64, 'knum255': 255}.get(case, 30)
     base = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, 0.02)
     names = ['features', 'face_idx', 'weights', 'soft_mask', 'hits', 'seg_tot', 'rec_face', 'rec_prob', 'ranges']
-    for idx, val in ((29, 1), (28, 1), (28, 200), (30, 1)):
+    for idx, val in ((29, 1), (28, 1), (28, 200)):
         try:
             _dev_param(idx, val)
             other = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, 0.02)
@@ -1877,3 +1877,75 @@ def test_soft_slot_width_and_prob_readback_equal(kal, case):
         for n, x, y in zip(names, base, other):
             assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), (idx, val, n)
     assert base[4].max() > 0
+
+
+@pytest.mark.devlib
+@pytest.mark.parametrize('case', ['bench', 'adversarial', 'random_boxes', 'narrow_w'])
+@pytest.mark.parametrize('K', [30, 8, 1, 64, 255])
+def test_soft_mask_C_tile_path_equals_row_kernel(kal, case, K):
+    """r06: the _C contract's f32 forward (dibr_soft_mask_forward_cuda) on the tile path -- the caller's
+    bboxes binned, heavy rows split over waves, the (B,H,W,K) slot tensors padded with 16-byte stores
+    and each hit stored at its slot -- against the per-row-wave kernel (dev param 30 = 1): mask, prob,
+    idx and type bit-equal, on the bench mesh, adversarial faces (NaN / inf / ties / huge faces),
+    caller bboxes unrelated to the faces (empty, inverted, a single NaN bound: also against the
+    oracle) and a width that is not a multiple of 64; knum 1 .. 255."""
+    import bench
+    from dibr_util import require_dev
+    require_dev()
+    m, sig = 1000., 7000.
+    if case == 'adversarial':
+        z, v, f = _adversarial_faces(torch.float32)
+        fvz, fvi, feat = T(z), T(v), T(f)
+        H, W = 97, 130
+        _, sel = kal.render.mesh.rasterize(H, W, fvz, fvi, feat)
+    else:
+        H, W = (96, 128) if case != 'narrow_w' else (40, 70)
+        inp = bench.dibr_inputs([0.3, 2.0], DEV, H=H, W=W)
+        fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+        _, sel = kal.render.mesh.rasterize(H, W, fvz, fvi, feat, fnz >= 0)
+    fm = (fvi * m).contiguous()
+    bb = torch.cat([fm.min(-2)[0] - 20., fm.max(-2)[0] + 20.], -1).contiguous()
+    if case == 'random_boxes':
+        g = torch.Generator().manual_seed(5)
+        rb = (torch.rand(bb.shape, generator=g) * 2400 - 1200).to(DEV)
+        pick = (torch.rand(bb.shape[:2], generator=g) < 0.05).to(DEV)
+        bb = torch.where(pick[..., None], rb, bb)
+        bb[0, 7, 1] = float('nan')
+        bb[1, 11, 2] = float('nan')
+        bb = bb.contiguous()
+    tile = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, sel, sig, K, m)
+    try:
+        _dev_param(30, 1)
+        row = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, sel, sig, K, m)
+    finally:
+        _dev_param(30, 0)
+    for n, x, y in zip(['mask', 'prob', 'idx', 'type'], tile, row):
+        assert x.shape == y.shape and np.array_equal(A(x), A(y), equal_nan=True), n
+    assert (A(tile[2]) >= 0).any()
+    if case == 'random_boxes':  # single NaN bounds: the reference's per-comparison rule (the oracle)
+        om, op, oi, ot = orc.dibr_soft_mask_forward(A(fm), A(bb), A(sel), sig, K, m)
+        assert np.array_equal(A(tile[2]), oi) and np.array_equal(A(tile[3]), ot)
+        np.testing.assert_allclose(A(tile[1]), op, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(A(tile[0]), om, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('K', [30, 4])
+def test_soft_mask_C_bench_mesh_vs_oracle(kal, K):
+    """The _C contract forward at the bench mesh's heavy pole tiles (the tile path, r06): slot tensors
+    equal to the oracle's (probabilities and mask to expf ulps), and its backward on them."""
+    import bench
+    inp = bench.dibr_inputs([0.3, 2.0], DEV, H=96, W=128)
+    fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+    _, sel = kal.render.mesh.rasterize(96, 128, fvz, fvi, feat, fnz >= 0)
+    fm = (fvi * 1000.).contiguous()
+    bb = torch.cat([fm.min(-2)[0] - 20., fm.max(-2)[0] + 20.], -1).contiguous()
+    mask, prob, cidx, ctype = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, sel, 7000., K, 1000.)
+    om, op, oi, ot = orc.dibr_soft_mask_forward(A(fm), A(bb), A(sel), 7000., K, 1000.)
+    assert np.array_equal(A(cidx), oi) and np.array_equal(A(ctype), ot)
+    np.testing.assert_allclose(A(prob), op, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(A(mask), om, rtol=1e-6, atol=1e-7)
+    assert (oi >= 0).sum() > (10000 if K == 30 else 2000)
+    grad = torch.rand_like(mask)
+    gi = kal._C.render.mesh.dibr_soft_mask_backward_cuda(grad, mask, sel, prob, cidx, ctype, fm, 7000., 1000.)
+    ogi = orc.dibr_soft_mask_backward(A(grad), A(mask), A(sel), A(prob), oi, ot, A(fm), 7000., 1000.)
+    assert_grads_equal(A(gi), ogi)
