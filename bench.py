@@ -157,34 +157,14 @@ def collectives_on():
     return dist.is_available() and dist.is_initialized()
 
 
-_PENDING = []  # the previous step's loss gather (out, work), at most one in flight
-
-
 def gather_losses(loss, world):
     """The step's only collective: all_gather of the per-shard scalar losses (RCCL whenever a
-    process group is initialised, at N = 1 too under --collectives).  Issued asynchronously; the
-    previous step's gather is waited for here, after this step's kernels are queued, so that the
-    gather's latency overlaps this step instead of sitting between steps.  timed_loop drains the
-    last one inside the timed region (drain_gathers), so every step's gather is timed."""
+    process group is initialised, at N = 1 too under --collectives), waited for in its own step.
+    (r06: issuing it asynchronously and waiting for it after the next step's kernels were queued
+    measured slower at N = 1 on RCCL -- 0.2105 / 0.2261 against 0.1959 / 0.1968 ms per step,
+    profiles/r06/r06g_collectives_ab.txt -- so the plain form stays.)"""
     from kaolin.distributed import gather_losses as gl
-    if not collectives_on():
-        return loss.detach().reshape(1)
-    out, work = gl(loss, async_op=True)
-    if work is not None and not out.is_cuda:  # gloo on host tensors: the caller reads them now
-        work.wait()
-        work = None
-    prev = _PENDING.pop() if _PENDING else None
-    _PENDING.append((out, work))
-    if prev is not None and prev[1] is not None:
-        prev[1].wait()
-    return out
-
-
-def drain_gathers():
-    while _PENDING:
-        _, work = _PENDING.pop()
-        if work is not None:
-            work.wait()
+    return gl(loss) if collectives_on() else loss.detach().reshape(1)
 
 
 def max_over_ranks(elapsed, device, world):
@@ -228,7 +208,6 @@ def timed_loop(fn, steps, world, device=None):
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
-    drain_gathers()
     _sync(device)
     if world > 1:
         dist.barrier()
@@ -396,8 +375,9 @@ def survey_step_bytes(inp, stats):
 
 # kernels launched by each timed op (the roofline's traffic sums their PMC bytes)
 OP_KERNELS = {
+    # (the _C soft mask's tile-path kernel shares the name up to its BboxSrc source: match the SoftSrc one)
     'dibr_forward': ('raster_bin_word_kernel<float, 2', 'tile_countorder_chip_kernel', 'raster_tile_kernel<float',
-                     'soft_tile_fwd_kernel<float'),
+                     'soft_tile_fwd_kernel<float, kl::SoftSrc'),
     'dibr_backward': ('rasterize_bwd_gather2_kernel<float', 'soft_tile_bwd_kernel<float'),
 }
 
@@ -410,15 +390,17 @@ SUB_KERNELS = {
     'check_sign': ('cs_prep_kernel', 'cs_bin_kernel<false', 'cs_pcount_kernel', 'cs_units_kernel',
                    'cs_bin_kernel<true', 'cs_pscatter_kernel', 'cs_cell_check_kernel', 'cs_finalize_kernel'),
     'cfg1_sided': ('sided_fwd_kernel<float', 'sided_combine_kernel<float'),
-    'soft_mask_C': ('soft_mask_fwd_kernel<float',),
+    'soft_mask_C': ('bin_faces_kernel<float, kl::BboxSrc', 'soft_tile_fwd_kernel<float, kl::BboxSrc'),
 }
 
 
 def pmc_traffic(op, config):
     """HBM bytes per call of `op` from the committed PMC summary of the config's workload
-    (scripts/pmc_traffic.py: profiles/pmc_traffic.json for cfg3 and its sub-lines,
-    profiles/pmc_traffic_cfg5.json for cfg5), or None when a kernel of the op is missing from it."""
+    (scripts/pmc_traffic.py: profiles/pmc_traffic.json for the cfg3 step, pmc_traffic_cfg5.json for
+    cfg5, pmc_traffic_sub.json for the sub-lines), or None when a kernel of the op is missing from it."""
     name = 'pmc_traffic.json' if config == 'cfg3' else f'pmc_traffic_{config}.json'
+    if op in SUB_KERNELS:  # the sub-lines' passes ran over the bench's extra legs (their own summary)
+        name = 'pmc_traffic_sub.json'
     path = os.path.join(ROOT, 'profiles', name)
     kernels = OP_KERNELS.get(op) or SUB_KERNELS.get(op)
     if not kernels or not os.path.exists(path):

@@ -198,10 +198,7 @@ constexpr int SB_PIECE = 512;
 __host__ __device__ constexpr size_t st_row_lds(int K) {
   return (size_t)K * 64 * sizeof(uint32_t) + 72 * sizeof(int);  // slots | prefix, total
 }
-// the same with slot_bytes-wide slots (soft_tile_fwd_kernel<T, S>: 2 when face ids fit 16 bits)
-__host__ __device__ constexpr size_t st_row_lds_s(int K, size_t slot_bytes) {
-  return (((size_t)K * 64 * slot_bytes + 15) & ~(size_t)15) + 72 * sizeof(int);
-}
+
 
 // Shards of the soft-mask backward's work-item list (counters DS_CNT_STRIDE ints apart, one per
 // 64-byte line): the fused forward appends to shard blockIdx % DS_SHARDS.

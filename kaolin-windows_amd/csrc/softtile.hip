@@ -75,10 +75,6 @@ struct SoftTileArgs {
   // raster_tile_kernel); an item without is done at once -- one load, not the order -> sel chain
   const uint8_t *live = nullptr;
   int live_n = 0;  // its length: items <= TILE_H per tile (the grid's bound can exceed it)
-  // LDS layout (st_fwd_layout): the item's probabilities (f32, item-wide (row, pixel, slot) order)
-  // go to [0, pcap) floats -- the fill list, the walk's counts and the spare bytes up to the LDS
-  // budget, all dead once the walk is done; the rest is read back from rec_prob
-  int pcap = 0;
   // The _C contract (kl_dibr_soft_mask_forward, r06): the reference's (B,H,W,knum) prob / idx / type
   // slot tensors written directly.  Each item's rows are padded first (idx -1, prob 0, type 0: 16-byte
   // stores issued before the walk, in flight during it), then every hit is stored at its slot after
@@ -86,8 +82,6 @@ struct SoftTileArgs {
   T *slot_prob = nullptr;
   int64_t *slot_idx = nullptr;
   uint8_t *slot_type = nullptr;
-  int wcnt_off = 0;  // byte offset of the 16 per-wave scratch ints
-  int rows_off = 0;  // byte offset of the rows' slot lists
 };
 
 
@@ -107,40 +101,15 @@ struct SoftTileArgs {
 #define ST_FC 2  // candidate chunks per wave and fill step (A/B builds: EXTRA=-DST_FC=3)
 #endif
 #ifndef ST_FWD_MIN_WAVES
-#define ST_FWD_MIN_WAVES 5  // the forward kernel's minimum waves per SIMD: 95 VGPRs (97 unbounded: 4 waves)
+#define ST_FWD_MIN_WAVES 1  // the forward kernel's minimum waves per SIMD (A/B builds)
 #endif
-constexpr int ST_LIST_CAP = 960;
-// list | per-wave scratch (16 ints) | the multi-wave walk's per-round counts ([Q][64] per row): the
-// head of the r05 layout, which soft_lp_min and the fused dev kernel (dibrtile.hip) still size on
+constexpr int ST_LIST_CAP = 960;  // (40.6 KB of LDS at knum 30 with 4 rows: 4 workgroups per CU)
+// list | per-wave scratch (16 ints) | the multi-wave walk's per-round counts ([Q][64] per row)
 constexpr size_t st_head_lds() { return (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int) + ST_WAVES * 64 * sizeof(int); }
-// r06 layout of soft_tile_fwd_kernel<T, S> (st_fwd_layout): [fill list | walk counts | spare] [16 scratch
-// ints] [rows: S slot lists + prefix], the slots S = uint16_t when every mesh-local face id fits (F <=
-// 65536): 25.3 KB at knum 30 with 4 rows instead of 40.6 KB, so the LDS budget (ST_LDS_BUDGET) sets
-// the workgroups per CU rather than the slot lists.  The probabilities are no longer written over
-// the slots (a 16-bit slot cannot hold them): the evaluation stores them in item-wide hit order into
-// the head, dead after the walk, and past its capacity the mask reads them back from rec_prob.
-#ifndef ST_LDS_BUDGET
-#define ST_LDS_BUDGET 32768  // 5 workgroups per CU (the kernel's VGPRs allow 5 waves per SIMD)
-#endif
-constexpr size_t st_head_core() { return (size_t)ST_LIST_CAP * 8 + ST_WAVES * 64 * sizeof(int); }
-struct StFwdLayout {
-  size_t wcnt_off, rows_off, bytes;
-  int pcap;
-  StFwdLayout(int K, int rows, size_t slot_bytes, size_t budget) {
-    const size_t rl = st_row_lds_s(K, slot_bytes) * (size_t)rows;
-    size_t head = st_head_core();
-    const size_t need = head + 16 * sizeof(int) + rl;
-    if (need < budget) head += (budget - need) & ~(size_t)15;
-    wcnt_off = head;
-    rows_off = head + 16 * sizeof(int);
-    bytes = rows_off + rl;
-    pcap = (int)(head / sizeof(float));
-  }
-};
 
 // Forward, one work item (a part of a tile's rows) per 4-wave workgroup: fill and walk (1a,
 // 1b below), the dense evaluation by the row's Q waves, the mask by its first wave.
-template <typename T, typename S, typename Src = SoftSrc<T>>
+template <typename T, typename Src = SoftSrc<T>>
 __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(SoftTileArgs<T, Src> a) {
   extern __shared__ __align__(16) unsigned char smem[];
   {
@@ -163,12 +132,10 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
   const int r = wid / Q, qi = wid - r * Q;
   uint32_t *L_face = reinterpret_cast<uint32_t *>(smem);
   uint32_t *L_pack = L_face + ST_LIST_CAP;
-  int *s_wcnt = reinterpret_cast<int *>(smem + a.wcnt_off);  // [16] per-wave scratch
-  const size_t row_lds = st_row_lds_s(K, sizeof(S));
-  unsigned char *const rows0 = smem + a.rows_off;
-  unsigned char *rowmem = rows0 + row_lds * r;
-  S *s_face = reinterpret_cast<S *>(rowmem);                                 // [K][64]
-  int *s_pre = reinterpret_cast<int *>(rowmem + (size_t)K * 64 * sizeof(S));  // [64], then total
+  int *s_wcnt = reinterpret_cast<int *>(L_pack + ST_LIST_CAP);  // [ST_WAVES] per-wave scratch
+  unsigned char *rowmem = smem + st_head_lds() + st_row_lds(K) * r;
+  uint32_t *s_face = reinterpret_cast<uint32_t *>(rowmem);                          // [K][64]
+  int *s_pre = reinterpret_cast<int *>(rowmem + (size_t)K * 64 * sizeof(uint32_t));  // [64], then total
   const int tx = tile % g.tiles_x;
   const int ty = (tile / g.tiles_x) % g.tiles_y;
   const int b = tile / (g.tiles_x * g.tiles_y);
@@ -322,7 +289,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
           while (cm) {
             const int q = __builtin_ctzll(cm);
             cm &= cm - 1;
-            s_face[sl(kid, lane)] = (S)L_face[base + q];
+            s_face[sl(kid, lane)] = L_face[base + q];
             if (++kid >= K) {
               active = false;
               cm = 0;
@@ -333,7 +300,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
       } else {
         // per-wave counts of this round ([Q][64] per row, in the head: with knum > 55 the rows
         // past RP are not allocated)
-        int *s_cnt = reinterpret_cast<int *>(smem + (size_t)ST_LIST_CAP * 8) + r * Q * 64;
+        int *s_cnt = reinterpret_cast<int *>(smem + (size_t)ST_LIST_CAP * 8 + 16 * sizeof(int)) + r * Q * 64;
         for (int b0 = 0; b0 < nb; b0 += Q) {  // workgroup-uniform rounds
           const int blk = b0 + qi;
           uint64_t cm = 0;
@@ -354,7 +321,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
           }
           const int base = blk * 64;
           while (cm && slot < K) {
-            s_face[sl(slot, lane)] = (S)L_face[base + __builtin_ctzll(cm)];
+            s_face[sl(slot, lane)] = L_face[base + __builtin_ctzll(cm)];
             cm &= cm - 1;
             slot++;
           }
@@ -408,28 +375,28 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
     rpre[0] = 0;
 #pragma unroll
     for (int q = 0; q < 8; q++) {
-      rtot[q] = q < RP ? *reinterpret_cast<const int *>(rows0 + row_lds * q + (size_t)K * 64 * sizeof(S) +
-                                                          64 * sizeof(int))
+      rtot[q] = q < RP ? *reinterpret_cast<const int *>(smem + st_head_lds() + st_row_lds(K) * q +
+                                                          (size_t)K * 64 * sizeof(uint32_t) + 64 * sizeof(int))
                        : 0;
       rpre[q + 1] = rpre[q] + rtot[q];
     }
     const int all = rpre[8];
-    T *const s_prob = reinterpret_cast<T *>(smem);  // [pcap]: the fill list and counts are dead now
     const float m = a.m;
     const float sx = m / (float)W, sy = m / (float)H;
     constexpr int U = ST_EVAL_U;
-    constexpr int NT = 64 * ST_WAVES;
-    for (int e0 = (int)threadIdx.x; e0 < all; e0 += NT * U) {
+    constexpr int S = 64 * ST_WAVES;
+    for (int e0 = (int)threadIdx.x; e0 < all; e0 += S * U) {
       int pp[U], kk[U], rr[U], ee[U];
       uint32_t ff[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int g0 = e0 + NT * u;
+        const int g0 = e0 + S * u;
         int r0 = 0;  // the hit's row: last row with rpre <= g0
 #pragma unroll
         for (int q = 1; q < 8; q++) r0 += (q < RP && rpre[q] <= g0) ? 1 : 0;
         const int e = g0 - rpre[r0];
-        const int *pre_r = reinterpret_cast<const int *>(rows0 + row_lds * r0 + (size_t)K * 64 * sizeof(S));
+        const int *pre_r = reinterpret_cast<const int *>(smem + st_head_lds() + st_row_lds(K) * r0 +
+                                                         (size_t)K * 64 * sizeof(uint32_t));
         int lo = 0;  // owner lane p: last lane with s_pre[p] <= e
 #pragma unroll
         for (int st = 32; st > 0; st >>= 1)
@@ -438,8 +405,8 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
         kk[u] = e - pre_r[lo];
         rr[u] = r0;
         ee[u] = e;
-        const S *face_r = reinterpret_cast<const S *>(rows0 + row_lds * r0);
-        ff[u] = g0 < all ? (uint32_t)face_r[sl(kk[u], lo)] : 0u;
+        const uint32_t *face_r = reinterpret_cast<const uint32_t *>(smem + st_head_lds() + st_row_lds(K) * r0);
+        ff[u] = g0 < all ? face_r[sl(kk[u], lo)] : 0u;
         if (kDevStamps && a.dev) ff[u] = min(ff[u], (uint32_t)(F - 1));  // dev ablations leave no face ids
       }
       T v[U][6];
@@ -447,7 +414,7 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
       for (int u = 0; u < U; u++) a.src.verts(f0 + ff[u], v[u]);  // all in flight (ff = 0 past the end)
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int g0 = e0 + NT * u;
+        const int g0 = e0 + S * u;
         if (g0 < all) {
           const int jr = ty * TILE_H + part * RP + rr[u];
           const T y0 = (T)(sy * (float)(H - 2 * jr - 1));  // == pix_y
@@ -466,31 +433,21 @@ __global__ void __launch_bounds__(256, ST_FWD_MIN_WAVES) soft_tile_fwd_kernel(So
             a.rec_face[rb + ee[u]] = ff[u] | ((uint32_t)(edgeid + 1) << 28);
             a.rec_prob[rb + ee[u]] = pr;
           }
-          if (g0 < a.pcap) s_prob[g0] = pr;  // item-wide (row, pixel, slot) order
+          T *prob_r = reinterpret_cast<T *>(smem + st_head_lds() + st_row_lds(K) * rr[u]);
+          prob_r[sl(kk[u], pp[u])] = pr;
         }
       }
     }
-    // past the LDS capacity the mask reads rec_prob back: the workgroup's stores complete first
-    // (workgroup-uniform; waves of a workgroup share the CU's vector L1, and no line of these
-    // fresh records was loaded before)
-    if (all > a.pcap) __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+    T *s_prob = reinterpret_cast<T *>(s_face);
     if (qi == 0 && px_valid && kid > 0) {
       // 1 - prod(1 - p) in double, slot order (dibr_soft_mask_cuda.cu:174-182); slots read
-      // eight at a time so that their reads overlap
-      int rp0 = 0;  // this row's first item-wide hit
-#pragma unroll
-      for (int q = 0; q < 8; q++) rp0 += q < r ? rtot[q] : 0;
-      const int g1 = rp0 + s_pre[lane];
-      const T *gp = slots ? a.slot_prob + pix * K : a.rec_prob + rbase + s_pre[lane];
+      // eight at a time so that their LDS reads overlap
       T allprob = (T)1.0;
       for (int k0 = 0; k0 < kid; k0 += 8) {
         T pk[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int k = min(k0 + u, kid - 1);
-          pk[u] = g1 + k < a.pcap ? s_prob[g1 + k] : gp[k];
-        }
+        for (int u = 0; u < 8; u++) pk[u] = s_prob[sl(min(k0 + u, kid - 1), lane)];
 #pragma unroll
         for (int u = 0; u < 8; u++)
           if (k0 + u < kid) allprob = (T)((double)allprob * (1.0 - (double)pk[u]));
@@ -940,10 +897,7 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   const int nt = g.batch * g.tiles_y * g.tiles_x;
   if (nt == 0) return KL_OK;
   const int lp_min = soft_lp_min(K);
-  // 16-bit slots when every mesh-local face id fits (the face list holds ids < F)
-  const bool narrow = F <= 65536 && g_dev_param[29] != 1;  // dev param 29 = 1: 32-bit slots (A/B)
-  const StFwdLayout lay(K, TILE_H >> lp_min, narrow ? 2 : 4, ST_LDS_BUDGET);
-  const size_t lds = lay.bytes;
+  const size_t lds = st_head_lds() + (size_t)(TILE_H >> lp_min) * st_row_lds(K);
   KL_REQUIRE(lds <= 160 * 1024, "dibr_soft_mask: knum too large for the LDS slot lists");
   const SoftSrc<T> src{fvi, (T)m, (T)pad};
   SoftTileArgs<T> args{src, rng,  sel,    bitmap, order,      nitems,     g,         F,     K,
@@ -955,15 +909,8 @@ int soft_tile_forward_main(int B, int H, int W, int F, int K, const T *fvi, cons
   args.swz = g_dev_param[19] == 1 ? 0 : 63;
   args.live = prefilled ? live : nullptr;
   args.live_n = nt * TILE_H;
-  args.pcap = sizeof(T) == 4 ? lay.pcap : 0;
-  if (g_dev_param[28] > 0) args.pcap = std::min(args.pcap, g_dev_param[28] - 1);  // dev: force the read-back
-  args.wcnt_off = (int)lay.wcnt_off;
-  args.rows_off = (int)lay.rows_off;
-  const dim3 grid((unsigned)soft_items_bound(nt, lp_min, soft_split()));
-  if (narrow)
-    hipLaunchKernelGGL((soft_tile_fwd_kernel<T, uint16_t>), grid, dim3(64 * ST_WAVES), lds, st, args);
-  else
-    hipLaunchKernelGGL((soft_tile_fwd_kernel<T, uint32_t>), grid, dim3(64 * ST_WAVES), lds, st, args);
+  hipLaunchKernelGGL((soft_tile_fwd_kernel<T>), dim3((unsigned)soft_items_bound(nt, lp_min, soft_split())), dim3(64 * ST_WAVES), lds,
+                     st, args);
   KL_CHECK_LAUNCH();
   if (K > 0 && sizeof(T) != 4) {  // f64: the rows left for the evaluation kernel
     const size_t ew = (size_t)K * 64 * sizeof(T) + 64 * sizeof(int);
@@ -1130,9 +1077,8 @@ int soft_tile_forward_slots(int B, int H, int W, int F, int K, const float *fvi,
   hipLaunchKernelGGL(soft_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt, order,
                      lp_min, nitems, soft_split());
   KL_CHECK_LAUNCH();
-  const bool narrow = F <= 65536 && g_dev_param[29] != 1;
-  const StFwdLayout lay(K, TILE_H >> lp_min, narrow ? 2 : 4, ST_LDS_BUDGET);
-  KL_REQUIRE(lay.bytes <= 160 * 1024, "dibr_soft_mask: knum too large for the LDS slot lists");
+  const size_t lds = st_head_lds() + (size_t)(TILE_H >> lp_min) * st_row_lds(K);
+  KL_REQUIRE(lds <= 160 * 1024, "dibr_soft_mask: knum too large for the LDS slot lists");
   SoftTileArgs<float, BboxSrc<float>> a{};
   a.src = src;
   a.rng = rng;
@@ -1148,27 +1094,18 @@ int soft_tile_forward_slots(int B, int H, int W, int F, int K, const float *fvi,
   a.mask = mask;
   a.hits = reinterpret_cast<uint8_t *>(w + SL.hits);
   a.rec_face = nullptr;
-  a.rec_prob = nullptr;
+  a.rec_prob = nullptr;  // (slot mode: the mask reads the probabilities from the LDS slots, as r05)
   a.seg_tot = reinterpret_cast<int *>(w + SL.seg);
   a.defer = reinterpret_cast<uint8_t *>(w + L.defer);
   a.dbg = (uint64_t *)g_dev_debug;
   a.dev = g_dev_flags;
   a.prefilled = 0;
   a.swz = g_dev_param[19] == 1 ? 0 : 63;
-  a.pcap = lay.pcap;
-  if (g_dev_param[28] > 0) a.pcap = std::min(a.pcap, g_dev_param[28] - 1);
   a.slot_prob = prob;
   a.slot_idx = cidx;
   a.slot_type = ctype;
-  a.wcnt_off = (int)lay.wcnt_off;
-  a.rows_off = (int)lay.rows_off;
   const dim3 grid((unsigned)soft_items_bound(nt, lp_min, soft_split()));
-  if (narrow)
-    hipLaunchKernelGGL((soft_tile_fwd_kernel<float, uint16_t, BboxSrc<float>>), grid, dim3(64 * ST_WAVES), lay.bytes,
-                       st, a);
-  else
-    hipLaunchKernelGGL((soft_tile_fwd_kernel<float, uint32_t, BboxSrc<float>>), grid, dim3(64 * ST_WAVES), lay.bytes,
-                       st, a);
+  hipLaunchKernelGGL((soft_tile_fwd_kernel<float, BboxSrc<float>>), grid, dim3(64 * ST_WAVES), lds, st, a);
   KL_CHECK_LAUNCH();
   return KL_OK;
 }

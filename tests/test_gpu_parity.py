@@ -1849,37 +1849,6 @@ def test_rayops_error_messages(kal):
 
 
 @pytest.mark.devlib
-@pytest.mark.parametrize('case', ['bench', 'adversarial', 'knum64', 'knum255'])
-def test_soft_slot_width_and_prob_readback_equal(kal, case):
-    """r06 soft forward layout: 16-bit slot lists (F <= 65536) against 32-bit ones (dev param 29 = 1),
-    and the mask's probabilities from LDS against the rec_prob read-back past the LDS capacity (dev
-    param 28 = n: capacity n - 1 floats; 1: every probability read back) -- every output and the
-    compact state equal."""
-    import bench
-    if case == 'adversarial':
-        z, v, f = _adversarial_faces(torch.float32)
-        fvz, fvi, feat = T(z), T(v), T(f)
-        fnz = T(np.random.default_rng(2).uniform(-0.3, 1, fvz.shape[:2]).astype(np.float32))
-        H, W, K = 97, 130, 30
-    else:
-        inp = bench.dibr_inputs([0.3, 2.0], DEV, H=96, W=128)
-        fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
-        H, W = 96, 128
-        K = {'knum64': 64, 'knum255': 255}.get(case, 30)
-    base = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, 0.02)
-    names = ['features', 'face_idx', 'weights', 'soft_mask', 'hits', 'seg_tot', 'rec_face', 'rec_prob', 'ranges']
-    for idx, val in ((29, 1), (28, 1), (28, 200)):
-        try:
-            _dev_param(idx, val)
-            other = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, K, 0.02)
-        finally:
-            _dev_param(idx, 0)
-        for n, x, y in zip(names, base, other):
-            assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), (idx, val, n)
-    assert base[4].max() > 0
-
-
-@pytest.mark.devlib
 @pytest.mark.parametrize('case', ['bench', 'adversarial', 'random_boxes', 'narrow_w'])
 @pytest.mark.parametrize('K', [30, 8, 1, 64, 255])
 def test_soft_mask_C_tile_path_equals_row_kernel(kal, case, K):
