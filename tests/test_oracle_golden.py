@@ -352,10 +352,17 @@ def test_soft_mask_backward_pinned(golden):
                                                             valid=None if fnz is None else fnz >= 0)
         g = orc.dibr_soft_mask_backward(f[name + '_upstream'], mask, sel, prob, cidx, ctype, fm, sig, mult)
         g = g.reshape(-1)
-        exp = np.zeros(g.size)
-        exp[f[name + '_idx']] = f[name + '_val']
-        ab = np.zeros(g.size)
-        ab[f[name + '_idx']] = f[name + '_absum']
+        if fnz is None:  # the sphere cases: inputs from committed goldens, expected sums stored
+            exp = np.zeros(g.size)
+            exp[f[name + '_idx']] = f[name + '_val']
+            ab = np.zeros(g.size)
+            ab[f[name + '_idx']] = f[name + '_absum']
+        else:
+            # the bench mesh is made by torch's CPU trigonometry, whose last bits depend on the host's
+            # vector ISA (the stored sums were made on another host): the independent restatement runs
+            # here on the same inputs, as the GPU test (test_soft_mask_backward_pinned_bench_mesh) does
+            gr, ar, _ = M.soft_bwd_ref(f[name + '_upstream'], mask, sel, prob, cidx, ctype, fm, sig, mult)
+            exp, ab = gr.reshape(-1), ar.reshape(-1)
         if g.dtype == np.float32:
             assert np.array_equal(g, exp.astype(np.float32)), name
         else:
