@@ -1728,12 +1728,14 @@ def test_raytrace_marches_agree(kal, level, nrays):
             assert len(got[mode]) == len(got[2]) and all(torch.equal(x, y) for x, y in zip(got[mode], got[2]))
 
 
-@pytest.mark.parametrize('na,nb', [(0, 5), (7, 0), (3145728, 1048576), (1001, 333)])
-def test_loss_dot2(kal, na, nb):
-    """bench.py's fused loss helper (kl_loss_dot2) vs an fp64 torch dot; replays reuse the workspace."""
+@pytest.mark.parametrize('na,nb,off', [(0, 5, 0), (7, 0, 0), (3145728, 1048576, 0), (1001, 333, 0),
+                                       (3145728, 1048576, 1), (4000001, 77, 2)])
+def test_loss_dot2(kal, na, nb, off):
+    """bench.py's fused loss helper (kl_loss_dot2) vs an fp64 torch dot; replays reuse the workspace.
+    off > 0: views starting off floats into their storage (the scalar path for a misaligned pair)."""
     from kaolin import _native
     g = torch.Generator(device='cpu').manual_seed(3)
-    a, ga, b, gb = (torch.rand(n, generator=g).to(DEV) for n in (na, na, nb, nb))
+    a, ga, b, gb = (torch.rand(n + off, generator=g).to(DEV)[off:] for n in (na, na, nb, nb))
     ws = torch.zeros(_native.lib().kl_loss_dot2_workspace_bytes(), dtype=torch.uint8, device=DEV)
     ref = float(a.double() @ ga.double() + b.double() @ gb.double())
     seen = set()
