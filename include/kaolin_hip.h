@@ -586,11 +586,24 @@ int kl_voxelgrid_mark_f64(int64_t num_vertices, const double *points, int64_t nu
  * subtree depth-first in the thread, so the grid equals kl_voxelgrid_mark's for any capacity >= 0
  * (capacity sets speed only).  *status (device u32, written by the call): bit 0 = some
  * depth-first walk exceeded 2^20 triangles and stopped (grid incomplete), bit 1 = some level
- * overflowed `capacity`.  workspace: kl_voxelgrid_mark_async_workspace_bytes bytes. */
+ * overflowed `capacity`, bit 2 = (r06: levels after the third run in one launch of co-resident
+ * workgroups meeting at grid barriers) a barrier wait timed out (grid incomplete).  workspace: kl_voxelgrid_mark_async_workspace_bytes bytes. */
 size_t kl_voxelgrid_mark_async_workspace_bytes(kl_dtype point_dtype, int64_t capacity);
 int kl_voxelgrid_mark_async(kl_dtype point_dtype, int64_t num_vertices, const void *points, int64_t num_faces,
                             const int64_t *faces, int resolution, kl_dtype grid_dtype, void *grid, int64_t capacity,
                             uint32_t *status, void *workspace, size_t workspace_bytes, kl_stream stream);
+
+/* (r06) One mesh of trianglemeshes_to_voxelgrids' GPU body as the front-end calls it: `vertices` (V,3)
+ * as given (f32 / f64), normalised in the kernels as (v - origin[c]) / scale[0] (the front-end's
+ * tensor subtraction and division, each rounded in the vertex dtype; origin (3) and scale (1) device
+ * tensors of the vertex dtype), and `grid` written whole (zero-filled by the call: it need not be
+ * zeroed).  Otherwise kl_voxelgrid_mark_async: the same grid, capacity, status (bit 2 in addition:
+ * the persistent kernel of the later levels could not meet at a grid barrier -- grid incomplete) and
+ * workspace (kl_voxelgrid_mark_async_workspace_bytes). */
+int kl_voxelgrid_async(kl_dtype vertex_dtype, int64_t num_vertices, const void *vertices, const void *origin,
+                       const void *scale, int64_t num_faces, const int64_t *faces, int resolution, kl_dtype grid_dtype,
+                       void *grid, int64_t capacity, uint32_t *status, void *workspace, size_t workspace_bytes,
+                       kl_stream stream);
 
 /* texture_mapping (kaolin/render/mesh/utils.py:23-75): coords (B, N, 2) in [0, 1] (OpenGL, y up;
  * clamped), texture (B, C, TH, TW) -> out (B, N, C), as torch.nn.functional.grid_sample with

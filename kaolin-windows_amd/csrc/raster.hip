@@ -1944,6 +1944,7 @@ static int dibr_fwd(int B, int H, int W, int F, int D, int K, const T *fvz, cons
     ca.dbg = kDevStamps && g_dev_debug ? reinterpret_cast<uint64_t *>(g_dev_debug) + kOrderStampsAt : nullptr;
     live = g_dev_param[26] != 1;
     ca.row_item = live ? reinterpret_cast<int32_t *>(w + L.off_rowitem) : nullptr;
+    if (g_dev_param[16] == 1) ca.spin_limit = 0;  // dev: every workgroup counts the whole bitmap (test)
     const unsigned zg = 1u;  // one workgroup zeroes the state's counters
     hipLaunchKernelGGL(tile_countorder_chip_kernel, dim3((unsigned)(2 * nb) + zg), dim3(CO_THREADS),
                        (size_t)nb * ORD_HIST * sizeof(int), st, ca);

@@ -415,6 +415,10 @@ struct CountOrderArgs {
   // (nt x TILE_H, or nullptr) the soft item holding row r of tile t, -1 for none: the rasterizer
   // flags the items with an uncovered pixel by it (RastTileArgs::soft_live)
   int32_t *row_item = nullptr;
+  // (r06) the grid barrier's bounded wait: after this many s_sleep(1) rounds a workgroup stops waiting
+  // and counts every tile of its bitmap itself (the same histograms, so the same order); dev param
+  // 16 = 1 sets 0 (every workgroup takes that path, for the equality test)
+  unsigned spin_limit = 1u << 22;
 };
 
 static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel(CountOrderArgs a) {
@@ -439,18 +443,23 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
   // loads from a clamped tile (words past the bitmap read as 0), all in flight together
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc((void *)a.bm[which], (short)0, a.words * nt * 4, 0x00020000);
-  const int tc = t < nt ? t : nt - 1;
-  unsigned n = 0;
-  for (int k0 = 0; k0 < a.words; k0 += 32) {
-    uint32_t x[32];
-#pragma unroll
-    for (int u = 0; u < 32; u++) x[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, tc * 4, (k0 + u) * nt * 4, 0);
-#pragma unroll
-    for (int u = 0; u < 32; u++) n += __popc(x[u]);
-  }
-  const int q = 31 - __clz(n + 1u);
   const bool flat = (a.noband >> which) & 1;  // one band: plain heaviest-first positions
-  const int key = t < nt ? (flat ? 0 : tile_band(t, nt)) * ORD_BUCKETS + q : -1;
+  // tile tt's bucket q (log2 of its candidate-chunk count + 1) and (band, bucket) key (-1 past nt)
+  auto tile_key = [&](int tt, int &qq) -> int {
+    const int tc = tt < nt ? tt : nt - 1;
+    unsigned n = 0;
+    for (int k0 = 0; k0 < a.words; k0 += 32) {
+      uint32_t x[32];
+#pragma unroll
+      for (int u = 0; u < 32; u++) x[u] = __builtin_amdgcn_raw_buffer_load_b32(rs, tc * 4, (k0 + u) * nt * 4, 0);
+#pragma unroll
+      for (int u = 0; u < 32; u++) n += __popc(x[u]);
+    }
+    qq = 31 - __clz(n + 1u);
+    return tt < nt ? (flat ? 0 : tile_band(tt, nt)) * ORD_BUCKETS + qq : -1;
+  };
+  int q;
+  const int key = tile_key(t, q);
   if (dbg && threadIdx.x == 0) dbg[1] = stamp_wall();
   // rank within the workgroup for its key, in tile order: the wave's own rank (same-key lanes
   // below this one) now, the earlier waves' counts after the barrier
@@ -481,11 +490,23 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
   __syncthreads();
   // ---- grid barrier of the bitmap's nb count workgroups (all co-resident: at most 2 x 32 + 1
   //      workgroups of 512 threads), on the ticket the binning kernel zeroed
+  // (r06) the wait is bounded: a workgroup that has waited spin_limit rounds (the others cannot all be
+  // resident -- kl_dibr_forward checks the occupancy before choosing this kernel, so only a GPU shared
+  // with other work gets here) counts every tile of the bitmap itself instead
+  __shared__ int s_passed;
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(a.ticket + which, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (dbg) dbg[2] = stamp_wall();
-    while (__hip_atomic_load(a.ticket + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nb)
+    unsigned spins = 0;
+    bool passed = true;
+    while (__hip_atomic_load(a.ticket + which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nb) {
+      if (spins++ >= a.spin_limit) {
+        passed = false;
+        break;
+      }
       __builtin_amdgcn_s_sleep(1);
+    }
+    s_passed = passed;
   }
   __syncthreads();
   uint64_t *const ldbg = kDevStamps && a.dbg && blk == 0 ? a.dbg + 64 + which * 4 : nullptr;
@@ -495,16 +516,26 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
   //      (place_prefix), then its own tiles' items at place_pos -- the order the r04 kernel gave
   constexpr int BATCH = 8;
   const int nh = nb * ORD_HIST;
-  for (int i0 = threadIdx.x; i0 < nh; i0 += BATCH * blockDim.x) {
-    int v[BATCH];
+  if (s_passed) {
+    for (int i0 = threadIdx.x; i0 < nh; i0 += BATCH * blockDim.x) {
+      int v[BATCH];
 #pragma unroll
-    for (int u = 0; u < BATCH; u++) {
-      const int i = i0 + u * blockDim.x;
-      v[u] = __hip_atomic_load(a.whist[which] + (i < nh ? i : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int u = 0; u < BATCH; u++) {
+        const int i = i0 + u * blockDim.x;
+        v[u] = __hip_atomic_load(a.whist[which] + (i < nh ? i : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int u = 0; u < BATCH; u++)
+        if (i0 + u * (int)blockDim.x < nh) s_big[i0 + u * blockDim.x] = v[u];
     }
-#pragma unroll
-    for (int u = 0; u < BATCH; u++)
-      if (i0 + u * (int)blockDim.x < nh) s_big[i0 + u * blockDim.x] = v[u];
+  } else {  // every count workgroup's histogram, counted here from the bitmap
+    for (int i = threadIdx.x; i < nh; i += blockDim.x) s_big[i] = 0;
+    __syncthreads();
+    for (int b = 0; b < nb; b++) {
+      int qb;
+      const int kb = tile_key(b * CO_THREADS + threadIdx.x, qb);
+      if (kb >= 0) atomicAdd(&s_big[b * ORD_HIST + kb], 1);
+    }
   }
   __syncthreads();
   int *const wbase = &s_wk[0][0];  // (the per-wave counts are consumed: this workgroup's base per key)

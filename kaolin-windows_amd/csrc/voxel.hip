@@ -28,6 +28,15 @@ struct Tri {
   T v[9];
 };
 
+// (r06) the front-end's normalisation (v - origin) / scale (trianglemesh.py:78-80: a tensor subtraction
+// then a division, each rounded in the vertex dtype) applied as the vertices are read, so the call
+// needs no normalised copy; o == nullptr: the points are normalised already
+template <typename T>
+struct Norm {
+  const T *o = nullptr, *s = nullptr;
+  __device__ __forceinline__ T operator()(T v, int c) const { return o ? (v - o[c]) / s[0] : v; }
+};
+
 template <typename G>
 __device__ __forceinline__ G one_val() { return G(1); }
 template <>
@@ -43,10 +52,18 @@ __device__ __forceinline__ void mark_point(T x, T y, T z, int R, G *grid) {
   grid[(ix * R + iy) * R + iz] = one_val<G>();
 }
 
+// (r06) z0 / z1 (optional): words block 0 zeroes on the way (the async path's status word and level
+// counters: two launches fewer per call)
 template <typename T, typename G>
-__global__ void mark_vertices_kernel(int64_t V, const T *__restrict__ pts, int R, G *__restrict__ grid) {
+__global__ void mark_vertices_kernel(int64_t V, const T *__restrict__ pts, int R, G *__restrict__ grid,
+                                     Norm<T> nm = Norm<T>{}, uint32_t *z0 = nullptr, int n0 = 0,
+                                     uint32_t *z1 = nullptr, int n1 = 0) {
+  if (blockIdx.x == 0) {
+    for (int k = threadIdx.x; k < n0; k += blockDim.x) z0[k] = 0;
+    for (int k = threadIdx.x; k < n1; k += blockDim.x) z1[k] = 0;
+  }
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < V) mark_point<T, G>(pts[i * 3], pts[i * 3 + 1], pts[i * 3 + 2], R, grid);
+  if (i < V) mark_point<T, G>(nm(pts[i * 3], 0), nm(pts[i * 3 + 1], 1), nm(pts[i * 3 + 2], 2), R, grid);
 }
 
 template <typename T>
@@ -214,7 +231,8 @@ static int voxel_mark(int64_t V, const T *pts, int64_t F, const int64_t *faces, 
 // at such sizes); status bit 1 records that some level overflowed `capacity` (speed only).
 constexpr int VOX_DFS_BUDGET = 1 << 20;
 constexpr int VOX_MAX_LEVELS = 64;  // as the host-sized loop: levels 0..63 are subdivided
-constexpr size_t VOX_COUNTER_BYTES = 1024;
+constexpr size_t VOX_COUNTER_BYTES = 1024;  // level counters (65 x 8 B), then the tail kernel's ticket
+constexpr size_t VOX_TICKET_AT = 768;
 
 template <typename T>
 __device__ __forceinline__ void midpoints(const Tri<T> &t, T *v4, T *v5, T *v6) {
@@ -287,14 +305,15 @@ __device__ __noinline__ void subdivide_dfs(Tri<T> root, int level, T thr, int R,
 // One level.  faces != null: level 0, the triangles gathered from (pts, faces) and tested here;
 // else the first min(*n_in, cap) triangles of `in`.  last: every kept child is finished
 // depth-first instead of appended.  The loop trip count is uniform over the workgroup.
+// one level's grid-strided loop (subdivide_async_kernel and, per level, subdivide_tail_kernel); n is
+// uniform over the grid
 template <typename T, typename G>
-__global__ void __launch_bounds__(256) subdivide_async_kernel(
-    const T *__restrict__ pts, const int64_t *__restrict__ faces, int64_t F, const Tri<T> *__restrict__ in,
-    const unsigned long long *__restrict__ n_in, int level, int last, int64_t cap, T thr, int R, G *__restrict__ grid,
-    Tri<T> *__restrict__ out, unsigned long long *__restrict__ n_out, unsigned *__restrict__ status) {
-  __shared__ int s_wave[4];
-  __shared__ unsigned long long s_base;
-  const int64_t n = faces ? F : (int64_t)min(*n_in, (unsigned long long)cap);
+__device__ __forceinline__ void subdivide_level(const T *__restrict__ pts, const int64_t *__restrict__ faces,
+                                                Norm<T> nm, const Tri<T> *__restrict__ in, int64_t n, int level,
+                                                bool last, int64_t cap, T thr, int R, G *__restrict__ grid,
+                                                Tri<T> *__restrict__ out, unsigned long long *__restrict__ n_out,
+                                                unsigned *__restrict__ status, int *s_wave,
+                                                unsigned long long *s_base) {
   for (int64_t b0 = blockIdx.x * 256ll; b0 < n; b0 += (int64_t)gridDim.x * 256) {
     const int64_t i = b0 + threadIdx.x;
     Tri<T> t;
@@ -305,9 +324,9 @@ __global__ void __launch_bounds__(256) subdivide_async_kernel(
 #pragma unroll
         for (int k = 0; k < 3; k++) {
           const int64_t v = faces[i * 3 + k];
-          t.v[k * 3 + 0] = pts[v * 3 + 0];
-          t.v[k * 3 + 1] = pts[v * 3 + 1];
-          t.v[k * 3 + 2] = pts[v * 3 + 2];
+          t.v[k * 3 + 0] = nm(pts[v * 3 + 0], 0);
+          t.v[k * 3 + 1] = nm(pts[v * 3 + 1], 1);
+          t.v[k * 3 + 2] = nm(pts[v * 3 + 2], 2);
         }
         live = needs_split(t.v, thr);
       } else {
@@ -315,7 +334,7 @@ __global__ void __launch_bounds__(256) subdivide_async_kernel(
       }
       if (live) keep = expand<T, G>(t, level, thr, R, grid);
     }
-    if (last) {  // kernel-uniform
+    if (last) {  // grid-uniform
       for (uint32_t m = keep; m; m &= m - 1) {
         Tri<T> ch;
         child_of(t, __ffs(m) - 1, ch);
@@ -326,9 +345,9 @@ __global__ void __launch_bounds__(256) subdivide_async_kernel(
     int total = 0;
     const int pre = block_exclusive_scan(__popc(keep), s_wave, &total);
     if (total == 0) continue;  // uniform
-    if (threadIdx.x == 0) s_base = atomicAdd(n_out, (unsigned long long)total);
+    if (threadIdx.x == 0) *s_base = atomicAdd(n_out, (unsigned long long)total);
     __syncthreads();
-    unsigned long long o = s_base + (unsigned long long)pre;
+    unsigned long long o = *s_base + (unsigned long long)pre;
     __syncthreads();  // s_base is rewritten by the next trip
     for (uint32_t m = keep; m; m &= m - 1, o++) {
       Tri<T> ch;
@@ -340,6 +359,65 @@ __global__ void __launch_bounds__(256) subdivide_async_kernel(
         subdivide_dfs<T, G>(ch, level + 1, thr, R, grid, status);
       }
     }
+  }
+}
+
+template <typename T, typename G>
+__global__ void __launch_bounds__(256) subdivide_async_kernel(
+    const T *__restrict__ pts, const int64_t *__restrict__ faces, int64_t F, const Tri<T> *__restrict__ in,
+    const unsigned long long *__restrict__ n_in, int level, int last, int64_t cap, T thr, int R, G *__restrict__ grid,
+    Tri<T> *__restrict__ out, unsigned long long *__restrict__ n_out, unsigned *__restrict__ status,
+    Norm<T> nm = Norm<T>{}) {
+  __shared__ int s_wave[4];
+  __shared__ unsigned long long s_base;
+  const int64_t n = faces ? F : (int64_t)min(*n_in, (unsigned long long)cap);
+  subdivide_level<T, G>(pts, faces, nm, in, n, level, last != 0, cap, thr, R, grid, out, n_out, status, s_wave, &s_base);
+}
+
+// (r06) Levels k0 .. levels - 1 in ONE launch of co-resident workgroups: each level as
+// subdivide_async_kernel's, then a grid barrier (release fence, an agent-scope ticket, acquire
+// fence: the children written on one XCD are read on any other) before the next level reads its
+// count.  A level with no input ends the kernel: at cfg4 (R = 512) the subdivision is done after
+// level 2, and the nine empty levels it launched one by one cost ~5 us each.  The wait is bounded: a
+// workgroup that waits spin_limit rounds sets status bit 2 (grid incomplete; the eager call raises)
+// and stops.  buf: the two ping-pong buffers (level k reads buf[(k + 1) & 1], writes buf[k & 1]).
+template <typename T, typename G>
+__global__ void __launch_bounds__(256) subdivide_tail_kernel(Tri<T> *__restrict__ buf0, Tri<T> *__restrict__ buf1,
+                                                             unsigned long long *__restrict__ counter, int k0,
+                                                             int levels, int64_t cap, T thr, int R,
+                                                             G *__restrict__ grid, unsigned *__restrict__ status,
+                                                             unsigned *__restrict__ ticket, unsigned spin_limit) {
+  __shared__ int s_wave[4];
+  __shared__ unsigned long long s_base;
+  __shared__ int s_go;
+  for (int k = k0; k < levels; k++) {
+    const int64_t n = (int64_t)min(__hip_atomic_load(counter + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                   (unsigned long long)cap);
+    if (n == 0) return;  // grid-uniform: read after the barrier, every add to it done
+    const bool last = k == levels - 1;
+    subdivide_level<T, G>(nullptr, nullptr, Norm<T>{}, (k & 1) ? buf0 : buf1, n, k, last, cap, thr, R, grid,
+                          (k & 1) ? buf1 : buf0, counter + k + 1, status, s_wave, &s_base);
+    if (last) return;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this level's children and count
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned target = gridDim.x * (unsigned)(k - k0 + 1);
+      __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned spins = 0;
+      int go = 1;
+      while (__hip_atomic_load(ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        if (spins++ >= spin_limit) {
+          atomicOr(status, 4u);
+          go = 0;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_go = go;
+    }
+    __syncthreads();
+    if (!s_go) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
 }
 
@@ -355,34 +433,66 @@ static int voxel_async_levels(int R) {
   return std::max(1, std::min(VOX_MAX_LEVELS, k));
 }
 
+// co-resident workgroups of subdivide_tail_kernel<T, G> (0: not all resident / query failed)
+template <typename T, typename G>
+static int voxel_tail_grid(int64_t cap) {
+  int dev = 0, ncu = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(subdivide_tail_kernel<T, G>),
+                                                   256, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (int)std::max<int64_t>(0, std::min<int64_t>({(int64_t)per_cu * ncu, cdiv(cap, 256), 2048}));
+}
+
+// levels launched one by one before subdivide_tail_kernel takes the rest (dev param 21: 1 = every level
+// its own launch, as r05; 2 + v = v levels first)
+constexpr int VOX_HEAD_LEVELS = 3;
+
 template <typename T, typename G>
 static int voxel_mark_async(int64_t V, const T *pts, int64_t F, const int64_t *faces, int R, G *grid, int64_t cap,
-                            unsigned *status, void *ws, size_t ws_bytes, hipStream_t st) {
+                            unsigned *status, void *ws, size_t ws_bytes, hipStream_t st, Norm<T> nm = Norm<T>{}) {
   KL_REQUIRE(cap >= 0, "trianglemeshes_to_voxelgrids: capacity must be >= 0");
   KL_REQUIRE(ws_bytes >= voxel_async_ws_bytes<T>(cap), "trianglemeshes_to_voxelgrids: workspace too small");
   KL_REQUIRE(status != nullptr, "trianglemeshes_to_voxelgrids: status required");
-  int rc = fill_async(status, 0, sizeof(unsigned), st);
-  if (rc) return rc;
+  unsigned long long *counter = reinterpret_cast<unsigned long long *>(ws);
+  // the status word and (F > 0) the level counters with the tail kernel's ticket: zeroed by the
+  // vertex kernel's block 0, or by fills when there are no vertices
+  uint32_t *zc = F > 0 ? reinterpret_cast<uint32_t *>(counter) : nullptr;
+  const int nzc = F > 0 ? (int)(VOX_COUNTER_BYTES / 4) : 0;
   if (V > 0) {
-    hipLaunchKernelGGL((mark_vertices_kernel<T, G>), dim3((unsigned)cdiv(V, 256)), dim3(256), 0, st, V, pts, R, grid);
+    hipLaunchKernelGGL((mark_vertices_kernel<T, G>), dim3((unsigned)cdiv(V, 256)), dim3(256), 0, st, V, pts, R, grid,
+                       nm, (uint32_t *)status, 1, zc, nzc);
     KL_CHECK_LAUNCH();
+  } else {
+    KL_CHECK_RC(fill_async(status, 0, sizeof(unsigned), st));
+    if (zc) KL_CHECK_RC(fill_async(zc, 0, VOX_COUNTER_BYTES, st));
   }
   if (F == 0) return KL_OK;
   const double thr_d = (double)(R - 1) / ((double)R * (double)R);
   const T thr = (T)(thr_d * thr_d);
-  unsigned long long *counter = reinterpret_cast<unsigned long long *>(ws);
   Tri<T> *buf[2] = {reinterpret_cast<Tri<T> *>((char *)ws + VOX_COUNTER_BYTES), nullptr};
   buf[1] = buf[0] + cap;
-  rc = fill_async(counter, 0, (VOX_MAX_LEVELS + 1) * sizeof(unsigned long long), st);
-  if (rc) return rc;
   const int levels = voxel_async_levels(R);
   const unsigned g_rest = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(cap, 256), 2048));
-  for (int k = 0; k < levels; k++) {
+  const int dp = g_dev_param[21];
+  int k0 = dp == 1 ? levels : dp >= 2 ? std::max(1, dp - 2) : VOX_HEAD_LEVELS;
+  const int tg = k0 < levels ? voxel_tail_grid<T, G>(cap) : 0;
+  if (tg <= 0) k0 = levels;
+  for (int k = 0; k < std::min(k0, levels); k++) {
     // level k reads buf[(k - 1) & 1] (count counter[k]) and appends to buf[k & 1] (counter[k + 1])
     const unsigned g = k == 0 ? (unsigned)std::min<int64_t>(cdiv(F, 256), 4096) : g_rest;
     hipLaunchKernelGGL((subdivide_async_kernel<T, G>), dim3(g), dim3(256), 0, st, pts, k == 0 ? faces : nullptr, F,
                        (const Tri<T> *)buf[(k + 1) & 1], (const unsigned long long *)counter + k, k,
-                       (int)(k == levels - 1), cap, thr, R, grid, buf[k & 1], counter + k + 1, status);
+                       (int)(k == levels - 1), cap, thr, R, grid, buf[k & 1], counter + k + 1, status, nm);
+    KL_CHECK_LAUNCH();
+  }
+  if (k0 < levels) {
+    unsigned *ticket = reinterpret_cast<unsigned *>(reinterpret_cast<char *>(ws) + VOX_TICKET_AT);
+    hipLaunchKernelGGL((subdivide_tail_kernel<T, G>), dim3((unsigned)tg), dim3(256), 0, st, buf[0], buf[1], counter,
+                       k0, levels, cap, thr, R, grid, status, ticket, 1u << 22);
     KL_CHECK_LAUNCH();
   }
   return KL_OK;
@@ -398,6 +508,35 @@ static int voxel_async_dispatch(int64_t V, const void *pts, int64_t F, const int
     case KL_F64: return voxel_mark_async<T, double>(V, p, F, faces, R, (double *)grid, cap, status, ws, ws_bytes, st);
     case KL_F16: return voxel_mark_async<T, __half>(V, p, F, faces, R, (__half *)grid, cap, status, ws, ws_bytes, st);
     case KL_U8: return voxel_mark_async<T, uint8_t>(V, p, F, faces, R, (uint8_t *)grid, cap, status, ws, ws_bytes, st);
+    default: break;
+  }
+  set_error("voxelgrid: unsupported grid dtype");
+  return KL_E_INVALID;
+}
+
+// (r06) kl_voxelgrid_async: the grid zero-filled here (16-byte stores: 78 us for cfg4's 537 MB
+// against torch.zeros' 104) and the vertices normalised as they are read (Norm)
+template <typename T>
+static int voxel_full_dispatch(int64_t V, const void *verts, const void *origin, const void *scale, int64_t F,
+                               const int64_t *faces, int R, kl_dtype gdt, void *grid, int64_t cap, unsigned *status,
+                               void *ws, size_t ws_bytes, hipStream_t st) {
+  KL_REQUIRE(origin != nullptr && scale != nullptr, "trianglemeshes_to_voxelgrids: origin and scale required");
+  const T *p = (const T *)verts;
+  const Norm<T> nm{(const T *)origin, (const T *)scale};
+  const size_t nvox = (size_t)R * R * R;
+  switch (gdt) {
+    case KL_F32:
+      KL_CHECK_RC(fill_async(grid, 0, nvox * 4, st));
+      return voxel_mark_async<T, float>(V, p, F, faces, R, (float *)grid, cap, status, ws, ws_bytes, st, nm);
+    case KL_F64:
+      KL_CHECK_RC(fill_async(grid, 0, nvox * 8, st));
+      return voxel_mark_async<T, double>(V, p, F, faces, R, (double *)grid, cap, status, ws, ws_bytes, st, nm);
+    case KL_F16:
+      KL_CHECK_RC(fill_async(grid, 0, nvox * 2, st));
+      return voxel_mark_async<T, __half>(V, p, F, faces, R, (__half *)grid, cap, status, ws, ws_bytes, st, nm);
+    case KL_U8:
+      KL_CHECK_RC(fill_async(grid, 0, nvox, st));
+      return voxel_mark_async<T, uint8_t>(V, p, F, faces, R, (uint8_t *)grid, cap, status, ws, ws_bytes, st, nm);
     default: break;
   }
   set_error("voxelgrid: unsupported grid dtype");
@@ -572,6 +711,21 @@ extern "C" int kl_voxelgrid_mark_async(kl_dtype point_dtype, int64_t V, const vo
     return voxel_async_dispatch<double>(V, pts, F, faces, R, grid_dtype, grid, capacity, status, ws, ws_bytes,
                                         S(stream));
   set_error("trianglemeshes_to_voxelgrids: f32 / f64 points only");
+  return KL_E_INVALID;
+}
+
+extern "C" int kl_voxelgrid_async(kl_dtype dtype, int64_t V, const void *vertices, const void *origin,
+                                  const void *scale, int64_t F, const int64_t *faces, int R, kl_dtype grid_dtype,
+                                  void *grid, int64_t capacity, uint32_t *status, void *ws, size_t ws_bytes,
+                                  kl_stream stream) {
+  KL_REQUIRE(R > 1, "trianglemeshes_to_voxelgrids: resolution must be > 1");
+  if (dtype == KL_F32)
+    return voxel_full_dispatch<float>(V, vertices, origin, scale, F, faces, R, grid_dtype, grid, capacity, status, ws,
+                                      ws_bytes, S(stream));
+  if (dtype == KL_F64)
+    return voxel_full_dispatch<double>(V, vertices, origin, scale, F, faces, R, grid_dtype, grid, capacity, status, ws,
+                                       ws_bytes, S(stream));
+  set_error("trianglemeshes_to_voxelgrids: f32 / f64 vertices only");
   return KL_E_INVALID;
 }
 

@@ -128,6 +128,7 @@ _SIGS = {
     'kl_voxelgrid_mark_f64': (_I, [_I64, _P, _I64, _P, _I, _I, _P, ALLOC_FN, _P, _P]),
     'kl_voxelgrid_mark_async_workspace_bytes': (_SZ, [_I, _I64]),
     'kl_voxelgrid_mark_async': (_I, [_I, _I64, _P, _I64, _P, _I, _I, _P, _I64, _P, _P, _SZ, _P]),
+    'kl_voxelgrid_async': (_I, [_I, _I64, _P, _P, _P, _I64, _P, _I, _I, _P, _I64, _P, _P, _SZ, _P]),
     'kl_texture_mapping_forward': (_I, [_I, _I, _I, _I64, _I, _I, _I, _P, _P, _P, _P]),
     'kl_texture_mapping_bwd_workspace_bytes': (_SZ, [_I, _I, _I, _I]),
     'kl_texture_mapping_backward': (_I, [_I, _I, _I, _I64, _I, _I, _I, _P, _P, _P, _P, _P, _P, _SZ, _P]),

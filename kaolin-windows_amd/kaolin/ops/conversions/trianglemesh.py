@@ -48,14 +48,14 @@ def trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin=None, scale
     batch_size = vertices.shape[0]
     out_dtype = vertices.dtype
     work = vertices if vertices.dtype in (torch.float32, torch.float64) else vertices.float()
-    points = ((work - origin.to(work.dtype).unsqueeze(1)) / scale.to(work.dtype).view(-1, 1, 1)).contiguous()
     faces = faces.to(torch.int64).contiguous()
     R = resolution
     grid_dtype = out_dtype if not return_sparse else torch.float32
-    grid = torch.zeros((batch_size, R, R, R), dtype=grid_dtype, device=vertices.device)
     lib = N.lib()
     dev = vertices.device
     if HOST_SIZED and not N.capturing(dev):
+        points = ((work - origin.to(work.dtype).unsqueeze(1)) / scale.to(work.dtype).view(-1, 1, 1)).contiguous()
+        grid = torch.zeros((batch_size, R, R, R), dtype=grid_dtype, device=dev)
         fn = lib.kl_voxelgrid_mark if work.dtype == torch.float32 else lib.kl_voxelgrid_mark_f64
         with N.on_device(dev):
             for i in range(batch_size):
@@ -64,24 +64,37 @@ def trianglemeshes_to_voxelgrids(vertices, faces, resolution, origin=None, scale
                            N.dtype_code(grid_dtype), N.ptr(grid[i]), arena.fn, None, N.stream_of(dev)),
                         'trianglemeshes_to_voxelgrids')
     else:
-        # nothing read back per round (graph-capturable); one status read per call in eager mode
+        # nothing read back per round (graph-capturable); one status read per call in eager mode.
+        # (r06) kl_voxelgrid_async zero-fills each grid and normalises the vertices in its kernels
+        # ((v - origin) / scale, rounded as the tensor expression above): no normalised copy, no zeros
         F = faces.shape[0]
         # ping-pong triangle buffers (2 x cap x 9 coordinates): capped at 2^23 triangles (0.6 GB in
         # f32) -- work past the cap is finished depth-first by the thread holding it, same grid
         cap = min(max(16 * F, 1 << 20), 1 << 23)
         code = N.dtype_code(work.dtype)
+        verts = work.contiguous()
+        org = origin.to(device=dev, dtype=work.dtype).reshape(-1, 3).expand(batch_size, 3).contiguous()
+        scl = scale.to(device=dev, dtype=work.dtype).reshape(-1).expand(batch_size).contiguous()
+        grid = torch.empty((batch_size, R, R, R), dtype=grid_dtype, device=dev)
         nb = lib.kl_voxelgrid_mark_async_workspace_bytes(code, cap)
         ws = torch.empty(nb, dtype=torch.uint8, device=dev)
-        status = torch.zeros(max(batch_size, 1), dtype=torch.int32, device=dev)
+        status = torch.empty(max(batch_size, 1), dtype=torch.int32, device=dev)
         with N.on_device(dev):
             for i in range(batch_size):
-                N.check(lib.kl_voxelgrid_mark_async(code, points.shape[1], N.ptr(points[i]), F, N.ptr(faces), R,
-                                                    N.dtype_code(grid_dtype), N.ptr(grid[i]), cap,
-                                                    N.ptr(status[i:]), N.ptr(ws), nb, N.stream_of(dev)),
+                N.check(lib.kl_voxelgrid_async(code, verts.shape[1], N.ptr(verts[i]), N.ptr(org[i]), N.ptr(scl[i:]),
+                                               F, N.ptr(faces), R, N.dtype_code(grid_dtype), N.ptr(grid[i]), cap,
+                                               N.ptr(status[i:]), N.ptr(ws), nb, N.stream_of(dev)),
                         'trianglemeshes_to_voxelgrids')
-        if not N.capturing(dev) and bool((status & 1).any()):
-            raise RuntimeError('trianglemeshes_to_voxelgrids: a triangle needs more than 2^20 subdivisions '
-                               '(vertices far outside the unit cube after origin / scale?)')
+        if not N.capturing(dev) and batch_size > 0:
+            st = 0
+            for v in status.cpu().tolist():  # one device-to-host read
+                st |= v
+            if st & 1:
+                raise RuntimeError('trianglemeshes_to_voxelgrids: a triangle needs more than 2^20 subdivisions '
+                                   '(vertices far outside the unit cube after origin / scale?)')
+            if st & 4:
+                raise RuntimeError('trianglemeshes_to_voxelgrids: the subdivision kernel\'s workgroups could not '
+                                   'all be resident (GPU shared with other work?); grid incomplete')
     if return_sparse:
         return grid.to_sparse()
     return grid

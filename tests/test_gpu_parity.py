@@ -631,6 +631,29 @@ def test_soft_live_flags_equal(kal, case):
 
 
 @pytest.mark.devlib
+@pytest.mark.parametrize('case', ['bench', 'cfg3_views', 'tiny'])
+def test_chip_order_barrier_fallback_equal(kal, case):
+    """r06: the chip-wide order kernel's grid barrier has a bounded wait; a workgroup that gives up
+    counts every tile of its bitmap itself.  Dev param 16 = 1 makes every workgroup take that path at
+    once: every output and the compact state equal the barrier's (cfg3's 4 views at 512^2: 4 count
+    workgroups per bitmap; 96x128: one)."""
+    import bench
+    H, W = {'bench': (96, 128), 'cfg3_views': (512, 512), 'tiny': (40, 24)}[case]
+    views = [0.0, 1.5707963, 3.1415927, 4.712389] if case == 'cfg3_views' else [0.3, 2.0]
+    inp = bench.dibr_inputs(views, DEV, H=H, W=W)
+    fvz, fvi, feat, fnz = inp['fvz'], inp['fvi'], inp['feat'], inp['fnz']
+    base = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, 30, 0.02)
+    try:
+        _dev_param(16, 1)
+        fb = _dibr_fused_forward(fvz, fvi, feat, fnz, H, W, 30, 0.02)
+    finally:
+        _dev_param(16, 0)
+    names = ['features', 'face_idx', 'weights', 'soft_mask', 'hits', 'seg_tot', 'rec_face', 'rec_prob', 'ranges']
+    for n, x, y in zip(names, base, fb):
+        assert x.shape == y.shape and np.array_equal(x, y, equal_nan=True), n
+
+
+@pytest.mark.devlib
 @pytest.mark.parametrize('knum,alt', [(30, 2), (30, 3), (8, 2)])
 def test_soft_item_rows_equal(kal, knum, alt):
     """The soft forward's rows per work item (4 where the slot lists fit 64 KB of LDS) against
@@ -1224,6 +1247,52 @@ def _voxel_async(points, faces, R, cap, grid_dtype=torch.float32):
                                         N.dtype_code(grid_dtype), N.ptr(grid), cap, N.ptr(status), N.ptr(ws), nb,
                                         N.stream_of(points.device)), 'voxel async')
     return grid, int(status.item())
+
+
+@pytest.mark.devlib
+@pytest.mark.parametrize('R', [64, 300])
+def test_voxelgrid_tail_kernel_levels_equal(kal, R):
+    """r06: the subdivision's later levels in one persistent launch (grid barriers between levels)
+    against every level its own launch (dev param 21 = 1) and against the persistent kernel from level
+    1 on (21 = 3), at capacities that overflow some level and that hold every level: grids equal."""
+    from dibr_util import require_dev
+    require_dev()
+    v, f = _uv_sphere(20, 32, 0.95)
+    vt, ft = T(v, torch.float32).unsqueeze(0), T(f)
+    o = torch.min(vt, dim=1)[0]
+    sc = torch.max(torch.max(vt, dim=1)[0] - o, dim=1)[0]
+    pts = ((vt - o.unsqueeze(1)) / sc.view(-1, 1, 1))[0].contiguous()
+    for cap in (300, 1 << 20):
+        grids = {}
+        try:
+            for dp in (0, 1, 3):
+                _dev_param(21, dp)
+                grids[dp] = _voxel_async(pts, ft, R, cap)
+        finally:
+            _dev_param(21, 0)
+        for dp in (1, 3):
+            assert torch.equal(grids[dp][0], grids[0][0]), (cap, dp)
+            assert grids[dp][1] & 5 == 0
+        assert int(grids[0][0].sum()) > 0
+
+
+def test_voxelgrid_front_end_normalises_in_kernel(kal):
+    """r06: the front-end's kl_voxelgrid_async (vertices normalised in the kernels, grid zero-filled by
+    the call) equals kl_voxelgrid_mark_async on the torch-normalised points and a zeroed grid, with
+    caller origin / scale (f64 scale for f32 vertices: converted first, as the reference's tensor ops)
+    and a batch of two meshes."""
+    v, f = _uv_sphere(20, 32, 0.95)
+    vt = torch.stack([T(v, torch.float32), T(v * 0.5 + 0.1, torch.float32)])
+    ft = T(f)
+    for o, sc in ((None, None), (torch.tensor([[-1., -1., -1.], [-0.2, -0.3, -0.1]], device=DEV),
+                                 torch.tensor([2.0, 1.5], dtype=torch.float64, device=DEV))):
+        got = kal.ops.conversions.trianglemeshes_to_voxelgrids(vt, ft, 48, o, sc)
+        oo = torch.min(vt, dim=1)[0] if o is None else o
+        ss = torch.max(torch.max(vt, dim=1)[0] - oo, dim=1)[0] if sc is None else sc
+        pts = ((vt - oo.to(vt.dtype).unsqueeze(1)) / ss.to(vt.dtype).view(-1, 1, 1)).contiguous()
+        for b in range(2):
+            ref, st = _voxel_async(pts[b], ft, 48, 1 << 20)
+            assert torch.equal(got[b], ref) and st == 0, b
 
 
 def _voxel_host_sized(kal, v, f, R, o=None, s=None):
