@@ -1255,21 +1255,8 @@ __global__ void __launch_bounds__(256) rasterize_bwd_bigface_kernel(
   }
 }
 
-// The chip order kernel's count workgroups meet at a grid barrier (a spin on an agent-scope
-// counter, tileorder.h): every one of its 2 nb + 1 workgroups must be resident at once.  Checked
-// here on the device's occupancy for the kernel's block size and LDS; when they may
-// not all fit, kl_dibr_forward takes the two-workgroup order kernel instead, which has no
-// barrier.  The answer depends only on the device and nb, so it is computed per call (a host
-// query, no state kept).
-static bool chip_order_resident(int nb) {
-  int dev = 0, ncu = 0, per_cu = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(tile_countorder_chip_kernel),
-                                                   CO_THREADS, (size_t)nb * ORD_HIST * sizeof(int)) != hipSuccess)
-    return false;
-  return (int64_t)per_cu * ncu >= 2 * (int64_t)nb + 1;
-}
+// (The chip order kernel's count workgroups meet at a grid barrier: chip_order_resident, tileorder.h,
+// checks they can all be resident; when not, kl_dibr_forward takes the two-workgroup order kernel.)
 
 // ---------------------------------------------------------------- gather backward, v2
 // The per-face gather reorganised around what bounds it (r03 counters: ~600 VALU per wave of 8

@@ -1039,15 +1039,65 @@ size_t soft_tile_ws_bytes(int B, int H, int W, int F) { return StWs(make_bin_geo
 // compact path, and the kernel stores the slot tensors directly (SoftTileArgs::slot_*).  Workspace:
 // the compact path's (StWs) + hits (B*H*W bytes) + segment totals; no compact records.
 struct StSlotWs {
-  size_t hits, seg, scratch, bytes;
+  size_t hits, seg, scratch, whist, tk, bytes;
   StSlotWs(int B, int H, int W, int F) {
     const BinGeom g = make_bin_geom(B, H, W, F);
     hits = al256(StWs(g, F).bytes);
     seg = hits + al256((size_t)B * H * W);
     scratch = seg + al256((size_t)B * H * g.tiles_x * sizeof(int));
-    bytes = scratch + 256;
+    // (r06) the chip order kernel's per-workgroup histograms and its tickets (zeroed by the binning)
+    whist = scratch + 256;
+    tk = whist + al256((size_t)cdiv((int64_t)g.batch * g.tiles_y * g.tiles_x, CO_THREADS) * ORD_HIST * sizeof(int));
+    bytes = tk + 256;
   }
 };
+
+// (r06) The caller's bboxes binned without global atomics and without a zero fill (raster_bin_word_kernel's
+// scheme, soft bitmap only): workgroup (grp, b) bins mesh b's faces [512 grp, 512 grp + 512) -- 8 chunks,
+// one byte of every tile's bitmap word -- marking its tiles in LDS (8 mark bytes per tile) with the exact
+// pixel ranges of bin_faces_kernel, then stores that byte of every tile.  zero: ints zeroed by workgroup
+// (0, 0).
+constexpr int ST_BIN_THREADS = 512;
+inline bool st_bin_word_ok(const BinGeom &g) { return (size_t)g.tiles_x * g.tiles_y * 8 <= 64 * 1024; }
+__global__ void __launch_bounds__(ST_BIN_THREADS) bbox_bin_word_kernel(BboxSrc<float> src, int F, BinGeom g, float m,
+                                                                      uint32_t *__restrict__ bitmap,
+                                                                      uint2 *__restrict__ rng, int *__restrict__ zero,
+                                                                      int nzero) {
+  extern __shared__ uint32_t s_words[];
+  const int ntv = g.tiles_x * g.tiles_y;
+  const int grp = blockIdx.x, b = blockIdx.y;
+  if (grp == 0 && b == 0)
+    for (int t = threadIdx.x; t < nzero; t += blockDim.x) zero[t] = 0;
+  uint8_t *ms = reinterpret_cast<uint8_t *>(s_words);  // [tile][8] mark bytes
+  for (int t = threadIdx.x; t < 2 * ntv; t += blockDim.x) s_words[t] = 0;
+  __syncthreads();
+  const int fl = grp * ST_BIN_THREADS + (int)threadIdx.x;
+  if (fl < F) {
+    const int64_t f = (int64_t)b * F + fl;
+    float bx0, by0, bx1, by1;
+    src.get(f, bx0, by0, bx1, by1);
+    const float sx = m / (float)g.width, sy = m / (float)g.height;
+    int ix0, ix1, iy0, iy1;
+    exact_range(bx0, bx1, sx, (float)g.width / m, g.width, false, ix0, ix1);
+    exact_range(by0, by1, sy, (float)g.height / m, g.height, true, iy0, iy1);
+    const bool e = ix0 > ix1 || iy0 > iy1;
+    rng[f] = e ? make_uint2(1u, 1u) : make_uint2((uint32_t)ix0 | ((uint32_t)ix1 << 16), (uint32_t)iy0 | ((uint32_t)iy1 << 16));
+    if (!e) {
+      const int w = (fl >> 6) & 7;
+      for (int ty = iy0 / TILE_H; ty <= iy1 / TILE_H; ty++)
+        for (int tx = ix0 / TILE_W; tx <= ix1 / TILE_W; tx++) ms[(ty * g.tiles_x + tx) * 8 + w] = 1;
+    }
+  }
+  __syncthreads();
+  const size_t base = (size_t)b * ntv;
+  const int word = grp >> 2, byte = grp & 3;
+  uint8_t *sb = reinterpret_cast<uint8_t *>(bitmap);
+  for (int t = threadIdx.x; t < ntv; t += blockDim.x)
+    sb[bm_index(g.ntiles(), base + t, word) * 4 + byte] =
+        (uint8_t)((reinterpret_cast<const uint64_t *>(ms)[t] * 0x0102040810204080ull) >> 56);
+}
+
+// (dev param 31 = 1: the r06e preamble -- atomic binning, bucket and one-workgroup order kernels -- for A/B)
 size_t soft_tile_slots_ws_bytes(int B, int H, int W, int F) { return StSlotWs(B, H, W, F).bytes; }
 
 int soft_tile_forward_slots(int B, int H, int W, int F, int K, const float *fvi, const float *bbox, const int64_t *sel,
@@ -1068,15 +1118,43 @@ int soft_tile_forward_slots(int B, int H, int W, int F, int K, const float *fvi,
   int *nitems = reinterpret_cast<int *>(w + L.nitems);
   int *scratch = reinterpret_cast<int *>(w + SL.scratch);
   const BboxSrc<float> src{bbox, fvi};
-  KL_CHECK_RC((launch_binning<float, BboxSrc<float>>(src, nullptr, F, g, m, bitmap, st, nullptr, L.zero, rng)));
   const int nt = g.batch * g.tiles_y * g.tiles_x;
-  hipLaunchKernelGGL(tile_bucket_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)bitmap,
-                     g.words, nt, bk, ghist, scratch);
-  KL_CHECK_LAUNCH();
   const int lp_min = soft_lp_min(K);
-  hipLaunchKernelGGL(soft_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt, order,
-                     lp_min, nitems, soft_split());
-  KL_CHECK_LAUNCH();
+  const int nb = (int)cdiv(nt, CO_THREADS);
+  if (nt <= ORD_LDS_TILES && st_bin_word_ok(g) && g_dev_param[31] != 1 && chip_order_resident(nb)) {
+    // (r06) word binning + the chip-wide order kernel on the soft bitmap alone: 12.4 + ~7 us against the
+    // r06e chain's atomic binning (with its zero fill), bucket and one-workgroup order kernels (12.7 +
+    // 4.8 + 7.9 us)
+    unsigned *tk = reinterpret_cast<unsigned *>(w + SL.tk);
+    hipLaunchKernelGGL(bbox_bin_word_kernel, dim3((unsigned)(g.words * 4), (unsigned)g.batch), dim3(ST_BIN_THREADS),
+                       (size_t)g.tiles_x * g.tiles_y * 8, st, src, F, g, m, bitmap, rng, reinterpret_cast<int *>(tk), 16);
+    KL_CHECK_LAUNCH();
+    CountOrderArgs ca{};
+    ca.bm[0] = ca.bm[1] = bitmap;
+    ca.words = g.words;
+    ca.nt = nt;
+    ca.nb = nb;
+    ca.whist[0] = ca.whist[1] = reinterpret_cast<int *>(w + SL.whist);
+    ca.ticket = tk;
+    ca.order[0] = ca.order[1] = order;
+    ca.nitems[0] = ca.nitems[1] = nitems;
+    ca.lp_min1 = lp_min;
+    ca.skip_empty1 = 0;  // every tile gets its item: the kernel writes every pixel's slots and mask
+    ca.noband = 2;       // plain heaviest-first (as kl_dibr_forward's soft items)
+    ca.sp = soft_split();
+    ca.only1 = 1;
+    hipLaunchKernelGGL(tile_countorder_chip_kernel, dim3((unsigned)(nb + 1)), dim3(CO_THREADS),
+                       (size_t)nb * ORD_HIST * sizeof(int), st, ca);
+    KL_CHECK_LAUNCH();
+  } else {
+    KL_CHECK_RC((launch_binning<float, BboxSrc<float>>(src, nullptr, F, g, m, bitmap, st, nullptr, L.zero, rng)));
+    hipLaunchKernelGGL(tile_bucket_kernel, dim3((unsigned)cdiv(nt, 4)), dim3(256), 0, st, (const uint32_t *)bitmap,
+                       g.words, nt, bk, ghist, scratch);
+    KL_CHECK_LAUNCH();
+    hipLaunchKernelGGL(soft_order_kernel, dim3(1), dim3(1024), 0, st, (const uint8_t *)bk, (const int *)ghist, nt,
+                       order, lp_min, nitems, soft_split());
+    KL_CHECK_LAUNCH();
+  }
   const size_t lds = st_head_lds() + (size_t)(TILE_H >> lp_min) * st_row_lds(K);
   KL_REQUIRE(lds <= 160 * 1024, "dibr_soft_mask: knum too large for the LDS slot lists");
   SoftTileArgs<float, BboxSrc<float>> a{};

@@ -509,6 +509,7 @@ struct ShardIn {
 // one reservation per workgroup and level.
 constexpr int M2S_GRID = 2048;
 constexpr int M2S_MAX_CHUNKS = 64;
+constexpr int M2S_KEEP = 4;  // chunks whose (node, face) m2s_node_kernel keeps in registers (r06)
 
 // ---- the 8 children of a parent (voxel, face) pair at once (m2s_children_pt).
 // The reference's decision for a child c (tri_voxel_test: 13 SAT axes, each passing iff
@@ -809,6 +810,10 @@ __global__ void __launch_bounds__(256) m2s_node_kernel(const float *__restrict__
   }
   const uint8_t *octpp = octpp_base + *opp;
   int mine = 0;
+  // (r06) the first M2S_KEEP chunks' node and face per thread kept in registers for the append pass
+  // below, which re-resolved them (a chain of dependent loads per chunk); cfg4's levels have 1-3
+  // chunks per workgroup
+  uint32_t keep_j[M2S_KEEP], keep_f[M2S_KEEP];
 #pragma unroll 1
   for (int k = 0; k < nch; k++) {
     const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
@@ -820,6 +825,12 @@ __global__ void __launch_bounds__(256) m2s_node_kernel(const float *__restrict__
       const uint64_t q = Mp[j];
       kids = m2s_children_pt(fv + (int64_t)f * 9, (int)(q & 0xffff), (int)((q >> 16) & 0xffff), (int)(q >> 32), level);
     }
+#pragma unroll
+    for (int u = 0; u < M2S_KEEP; u++)
+      if (k == u) {
+        keep_j[u] = j;
+        keep_f[u] = f;
+      }
     if (LAST) {  // the least face per (node, child) slot; a slot left at ~0 is no child
       for (uint32_t c = kids; c; c &= c - 1) atomicMin(fmin8 + j * 8 + __builtin_ctz(c), f);
     } else {
@@ -855,9 +866,20 @@ __global__ void __launch_bounds__(256) m2s_node_kernel(const float *__restrict__
     int ctot = 0;
     const int pre = block_exclusive_scan(__popc(kids), s_wave, &ctot);
     if (kids) {
-      const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
-      const unsigned long long p = in.pos(i, seg);
-      const uint32_t f = fin[p], j8 = m2s_node(kin[p], Spp, octpp) * 8;
+      uint32_t f = 0, j8 = 0;
+      if (k < M2S_KEEP) {
+#pragma unroll
+        for (int u = 0; u < M2S_KEEP; u++)
+          if (k == u) {
+            f = keep_f[u];
+            j8 = keep_j[u] * 8;
+          }
+      } else {
+        const unsigned long long i = lo + (unsigned long long)k * blockDim.x + threadIdx.x;
+        const unsigned long long p = in.pos(i, seg);
+        f = fin[p];
+        j8 = m2s_node(kin[p], Spp, octpp) * 8;
+      }
       unsigned long long o = o0 + (unsigned long long)pre;
       for (uint32_t c = kids; c; c &= c - 1) {
         kout[o] = j8 + (uint32_t)__builtin_ctz(c);
@@ -1171,10 +1193,15 @@ static int mesh_to_spc_nodes(int64_t F, const float *fv, uint32_t L, Scratch &sc
   const int64_t leaves = h.U[L];
   if (leaves == 0) return KL_OK;  // empty: (0,) u8, (0,) i64, (0,3) f32 built by the caller
   const int64_t nodes = h.O[L];
-  uint8_t *out = (uint8_t *)sc.get((size_t)nodes);
-  int64_t *fu = (int64_t *)sc.get((size_t)leaves * sizeof(int64_t));
-  float *bu = (float *)sc.get((size_t)leaves * 2 * sizeof(float));
-  if (!out || !fu || !bu) return KL_E_ALLOC;
+  // (r06) the three outputs from ONE allocation (each is a host callback into the caller's allocator,
+  // made while the GPU idles after the count read): face ids | barycentrics | octree, 256-B aligned
+  const size_t ofu = 0, obu = al256b((size_t)leaves * sizeof(int64_t)),
+               oout = obu + al256b((size_t)leaves * 2 * sizeof(float));
+  char *blk = (char *)sc.get(oout + (size_t)nodes);
+  if (!blk) return KL_E_ALLOC;
+  int64_t *fu = (int64_t *)(blk + ofu);
+  float *bu = (float *)(blk + obu);
+  uint8_t *out = (uint8_t *)(blk + oout);
   KL_CHECK_HIP(hipMemcpyAsync(out, w.arena, (size_t)nodes, hipMemcpyDeviceToDevice, st));
   const int64_t nslots = 8 * (int64_t)h.U[L - 1];
   const int b = (int)((L - 1) & 1);

@@ -419,6 +419,9 @@ struct CountOrderArgs {
   // and counts every tile of its bitmap itself (the same histograms, so the same order); dev param
   // 16 = 1 sets 0 (every workgroup takes that path, for the equality test)
   unsigned spin_limit = 1u << 22;
+  // (r06, the _C contract's soft mask) only1: one bitmap, the soft mask's (count workgroups [0, nb)
+  // take bitmap 1)
+  int only1 = 0;
 };
 
 static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel(CountOrderArgs a) {
@@ -426,14 +429,16 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
   __shared__ int sb[ORD_HIST], sx[32], lpb[ORD_BUCKETS], hist[ORD_HIST];
   extern __shared__ int s_big[];  // [nb][ORD_HIST]: every count workgroup's histogram
   const int nb = a.nb, nt = a.nt;
-  if ((int)blockIdx.x >= 2 * nb) {
-    const int part = blockIdx.x - 2 * nb, nparts = gridDim.x - 2 * nb;
+  const int ncount = a.only1 ? nb : 2 * nb;
+  if ((int)blockIdx.x >= ncount) {
+    const int part = blockIdx.x - ncount, nparts = gridDim.x - ncount;
     if (part == 0 && a.zero)
       for (int i = threadIdx.x; i < a.nzero; i += blockDim.x) a.zero[i] = 0;
     if (a.zacc) zero_doubles_share(a.zacc, a.zn, part, nparts);
     return;
   }
-  const int which = (int)blockIdx.x >= nb ? 1 : 0, blk = (int)blockIdx.x - which * nb;
+  const int which = a.only1 ? 1 : ((int)blockIdx.x >= nb ? 1 : 0);
+  const int blk = (int)blockIdx.x - (a.only1 ? 0 : which * nb);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint64_t *const dbg = kDevStamps && a.dbg && blockIdx.x < 16 ? a.dbg + blockIdx.x * 4 : nullptr;
   if (dbg && threadIdx.x == 0) dbg[0] = stamp_wall();
@@ -577,6 +582,22 @@ static __global__ void __launch_bounds__(CO_THREADS) tile_countorder_chip_kernel
     __syncthreads();
     if (threadIdx.x == 0) ldbg[2] = stamp_wall();
   }
+}
+
+// Whether the 2 nb + 1 workgroups of tile_countorder_chip_kernel (nb per bitmap) can all be resident
+// here on the device's occupancy for the kernel's block size and LDS; when they may
+// not all fit, the callers take an order kernel without a grid barrier.  The answer depends only on
+// the device and nb, so it is computed per call (a host query, no state kept).
+static inline bool chip_order_resident(int nb) {
+  int dev = 0, ncu = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(tile_countorder_chip_kernel),
+                                                   CO_THREADS, (size_t)nb * ORD_HIST * sizeof(int)) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return (int64_t)per_cu * ncu >= 2 * (int64_t)nb + 1;
 }
 
 }  // namespace kl

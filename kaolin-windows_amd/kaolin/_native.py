@@ -283,11 +283,17 @@ class Arena:
         return self._cb
 
     def tensor(self, p, numel, dtype, shape):
-        """View of an arena allocation as a typed tensor of `shape` (numel elements)."""
+        """View of an arena allocation as a typed tensor of `shape` (numel elements); p may point inside
+        an allocation (several outputs carved from one request, r06)."""
         if numel == 0:
             return torch.empty(shape, dtype=dtype, device=self.device)
-        base = self.by_ptr[p]
         esize = torch.empty((), dtype=dtype).element_size()
+        base = self.by_ptr.get(p)
+        if base is None:
+            for q, t in self.by_ptr.items():
+                if q <= p < q + t.numel():
+                    base = t[p - q:]
+                    break
         return base[:numel * esize].view(dtype).reshape(shape)
 
 

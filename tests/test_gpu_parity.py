@@ -1928,7 +1928,8 @@ def test_soft_mask_C_tile_path_equals_row_kernel(kal, case, K):
     and each hit stored at its slot -- against the per-row-wave kernel (dev param 30 = 1): mask, prob,
     idx and type bit-equal, on the bench mesh, adversarial faces (NaN / inf / ties / huge faces),
     caller bboxes unrelated to the faces (empty, inverted, a single NaN bound: also against the
-    oracle) and a width that is not a multiple of 64; knum 1 .. 255."""
+    oracle) and a width that is not a multiple of 64; knum 1 .. 255.  Also against the r06e binning / order
+    preamble (dev param 31 = 1; default r06: word binning and the chip order kernel on the soft bitmap)."""
     import bench
     from dibr_util import require_dev
     require_dev()
@@ -1954,13 +1955,24 @@ def test_soft_mask_C_tile_path_equals_row_kernel(kal, case, K):
         bb[1, 11, 2] = float('nan')
         bb = bb.contiguous()
     tile = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, sel, sig, K, m)
+    others = []
     try:
         _dev_param(30, 1)
-        row = kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, sel, sig, K, m)
-    finally:
+        others.append(kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, sel, sig, K, m))
         _dev_param(30, 0)
-    for n, x, y in zip(['mask', 'prob', 'idx', 'type'], tile, row):
-        assert x.shape == y.shape and np.array_equal(A(x), A(y), equal_nan=True), n
+        # r06: the r06e preamble (atomic binning, bucket and one-workgroup order kernels: 31 = 1)
+        for combo in ({31: 1},):
+            for i, v in combo.items():
+                _dev_param(i, v)
+            others.append(kal._C.render.mesh.dibr_soft_mask_forward_cuda(fm, bb, sel, sig, K, m))
+            for i in combo:
+                _dev_param(i, 0)
+    finally:
+        for i in (30, 31):
+            _dev_param(i, 0)
+    for other in others:
+        for n, x, y in zip(['mask', 'prob', 'idx', 'type'], tile, other):
+            assert x.shape == y.shape and np.array_equal(A(x), A(y), equal_nan=True), n
     assert (A(tile[2]) >= 0).any()
     if case == 'random_boxes':  # single NaN bounds: the reference's per-comparison rule (the oracle)
         om, op, oi, ot = orc.dibr_soft_mask_forward(A(fm), A(bb), A(sel), sig, K, m)
