@@ -97,6 +97,9 @@ struct SoftTileArgs {
 #define SB_HC 512
 #define SB_NC 1
 #endif
+#ifndef SB_VS  // doubles per hash slot: the 6 sums (A/B builds; r06r: 7, spreading slots 16 apart over the banks, measured equal)
+#define SB_VS 6
+#endif
 #ifndef ST_FC
 #define ST_FC 2  // candidate chunks per wave and fill step (A/B builds: EXTRA=-DST_FC=3)
 #endif
@@ -639,7 +642,7 @@ __global__ void __launch_bounds__(1024) soft_bwd_plan_kernel(const int *__restri
 template <typename T, int HC, int NC = 1>
 struct ItemHash {
   int *key;     // [HC], -1 = empty
-  double *val;  // [HC * NC * 6]: NC copies of a face's sums, copy = lane % NC (fewer lanes of an
+  double *val;  // [HC * NC * SB_VS]: NC copies of a face's sums, copy = lane % NC (fewer lanes of an
                 // instruction on one address: a piece's neighbouring hits share faces)
   int *used;    // [HC]
   int *nused;
@@ -667,7 +670,7 @@ struct ItemHash {
                                       uint8_t *flags) {
     const int s = slot(f);
     if (s >= 0) {
-      double *v = val + (s * NC + (int)(threadIdx.x & (NC - 1))) * 6;
+      double *v = val + (s * NC + (int)(threadIdx.x & (NC - 1))) * SB_VS;
       atomicAdd(&v[c0 * 2], (double)g0x);
       atomicAdd(&v[c0 * 2 + 1], (double)g0y);
       if (c1 >= 0) {
@@ -691,8 +694,8 @@ struct ItemHash {
       double v = 0.0;  // the copies in copy order (each sum is exact: the order does not matter)
 #pragma unroll
       for (int k = 0; k < NC; k++) {
-        v += val[(sl * NC + k) * 6 + c];
-        val[(sl * NC + k) * 6 + c] = 0.0;
+        v += val[(sl * NC + k) * SB_VS + c];
+        val[(sl * NC + k) * SB_VS + c] = 0.0;
       }
       if (v != 0.0) atomicAdd(gmesh + (size_t)key[sl] * ast + c, v);
       if (c == 0 && flags) flags[key[sl]] = 1;
@@ -714,7 +717,7 @@ __global__ void __launch_bounds__(512, SB_MIN_WAVES) soft_tile_bwd_kernel(
     const int *__restrict__ ctl, int cap, int *__restrict__ scratch, int dev, int ast, uint8_t *__restrict__ sflag) {
   constexpr int HC = SB_HC, NC = SB_NC;
   __shared__ int s_key[HC];
-  __shared__ double s_val[HC * NC * 6];
+  __shared__ double s_val[HC * NC * SB_VS];
   __shared__ int s_used[HC];
   __shared__ int s_nused;
   __shared__ double s_a[TILE_H][64];
@@ -724,7 +727,7 @@ __global__ void __launch_bounds__(512, SB_MIN_WAVES) soft_tile_bwd_kernel(
   const int wid = threadIdx.x >> 6;  // the item's row
   const int H = g.height, W = g.width;
   for (int q = threadIdx.x; q < HC; q += blockDim.x) s_key[q] = -1;
-  for (int q = threadIdx.x; q < HC * NC * 6; q += blockDim.x) s_val[q] = 0.0;
+  for (int q = threadIdx.x; q < HC * NC * SB_VS; q += blockDim.x) s_val[q] = 0.0;
   if (threadIdx.x == 0) s_nused = 0;
   if (scratch && threadIdx.x == 0 && blockIdx.x == 0) *scratch = 0;
   ItemHash<T, HC, NC> hash{s_key, s_val, s_used, &s_nused};
