@@ -1,7 +1,7 @@
 // abi.cpp -- error channel and version of the libkaolin_hip.so C ABI.
 #include <algorithm>
 #include <cstring>
-#include <mutex>
+
 #include <string>
 
 #include "common.h"
@@ -99,65 +99,6 @@ int fill_async(void *p, int value, size_t bytes, hipStream_t st) {
 }
 }  // namespace kl
 
-namespace kl {
-// One side stream and two events per device, made on first use (outside graph capture:
-// the first fused call of a process runs eagerly before any capture in practice; if the
-// creation fails -- e.g. during a capture -- the call runs on its own stream).
-namespace {
-struct SideSlot {
-  std::mutex mu;
-  bool tried = false;
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-constexpr int kMaxDevices = 64;
-SideSlot g_side[kMaxDevices];
-}  // namespace
-
-SideFork::SideFork(hipStream_t st) : st_(st), side_(st), slot_(nullptr), joined_(true) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return;
-  SideSlot &s = g_side[dev];
-  s.mu.lock();
-  if (!s.tried) {
-    s.tried = true;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone &&
-        hipStreamCreateWithFlags(&s.side, hipStreamNonBlocking) == hipSuccess &&
-        hipEventCreateWithFlags(&s.fork, hipEventDisableTiming) == hipSuccess &&
-        hipEventCreateWithFlags(&s.join, hipEventDisableTiming) == hipSuccess) {
-    } else {
-      s.side = nullptr;
-      s.tried = false;  // try again on a later (uncaptured) call
-    }
-    (void)hipGetLastError();
-  }
-  if (!s.side || hipEventRecord(s.fork, st) != hipSuccess || hipStreamWaitEvent(s.side, s.fork, 0) != hipSuccess) {
-    (void)hipGetLastError();
-    s.mu.unlock();
-    return;
-  }
-  slot_ = &s;
-  side_ = s.side;
-  joined_ = false;
-}
-
-int SideFork::join() {
-  if (joined_) return KL_OK;
-  joined_ = true;
-  SideSlot &s = *static_cast<SideSlot *>(slot_);
-  const hipError_t a = hipEventRecord(s.join, side_);
-  const hipError_t b = a == hipSuccess ? hipStreamWaitEvent(st_, s.join, 0) : a;
-  s.mu.unlock();
-  if (b != hipSuccess) {
-    set_error(std::string("side stream join: ") + hipGetErrorString(b));
-    return KL_E_HIP;
-  }
-  return KL_OK;
-}
-
-SideFork::~SideFork() { (void)join(); }
-}  // namespace kl
 
 extern "C" const char *kl_last_error(void) { return kl::g_last_error.c_str(); }
 

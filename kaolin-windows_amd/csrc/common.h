@@ -57,22 +57,6 @@ int fill_async(void *p, int value, size_t bytes, hipStream_t st);
 // synchronise.  hipHostMalloc / hipHostFree per call, or a copy into pageable memory, cost
 // tens to hundreds of microseconds each (mesh_to_spc's three reads, r04).
 int host_read(void *dst, const void *src, size_t bytes, hipStream_t st);
-// Fork/join of one side stream of the current device inside one ABI call (event record +
-// wait, so it is captured into a HIP graph as two parallel branches).  SideFork's
-// constructor locks the device's side stream and makes it wait for `st`; side() is that
-// stream, or `st` itself when none could be made (the work then runs in order); join()
-// makes `st` wait for the side work.  The destructor joins if join() was not called.
-class SideFork {
- public:
-  explicit SideFork(hipStream_t st);
-  ~SideFork();
-  hipStream_t side() const { return side_; }
-  int join();
- private:
-  hipStream_t st_, side_;
-  void *slot_;
-  bool joined_;
-};
 // out[i] = (T)acc[i], or out[i] + (T)acc[i] with accumulate: the single rounding of a gradient
 // summed in double (raster.hip)
 // `reset` (optional): an int zeroed by the same launch.
