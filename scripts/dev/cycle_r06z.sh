@@ -8,6 +8,7 @@ rc=0; timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -rs --timeout 300
 tail -4 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1
 tail -1 $OUT/smoke.log
+for i in 1 2; do timeout -k 10 100 python scripts/dev/rt_trace.py >> $OUT/rt.txt 2>&1; done; grep raytrace $OUT/rt.txt
 cd /tmp; export TMPDIR=/tmp
 pmc() {  # name, kernel regex, bench args
   local n=0
