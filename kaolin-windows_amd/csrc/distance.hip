@@ -896,7 +896,7 @@ __global__ void __launch_bounds__(256) p2m_morton_kernel(const T *__restrict__ p
 #endif
 constexpr int P2M_MAX_SPLITS = KL_P2M_MAX_SPLITS;
 // workgroups the (point block, face split) grid aims for (scripts/dev/p2m_probe.hip sweeps it)
-static int g_p2m_target_blocks = 10240;
+constexpr int P2M_TARGET_BLOCKS = 10240;  // dev param 28 = N overrides (A/B)
 constexpr int P2M_BOUND_BLOCKS = 64;  // blocks of p2m_bounds_kernel
 
 struct P2MWs {
@@ -1195,7 +1195,8 @@ static int p2m_fwd(int64_t P, int64_t F, const void *pts, const void *fv, void *
     // 20 splits of 1024 faces, 1.6 ms; 14 of 1536: 2.0 ms; 40 of 512: 2.1 ms);
     // splits cover whole 512-face reference tiles
     const int64_t tiles = cdiv(F, 512);
-    const int64_t want = std::max<int64_t>(1, cdiv(g_p2m_target_blocks, pblocks));
+    const int64_t target = g_dev_param[28] > 0 ? g_dev_param[28] : P2M_TARGET_BLOCKS;
+    const int64_t want = std::max<int64_t>(1, cdiv(target, pblocks));
     splits = (int)std::min<int64_t>(std::min<int64_t>(want, tiles), P2M_MAX_SPLITS);
     split_faces = cdiv(tiles, splits) * 512;
     splits = (int)cdiv(F, split_faces);

@@ -2230,9 +2230,13 @@ static int rt_hitlist(const RayIn &in, int64_t num_rays, uint32_t target_level, 
   const size_t lb = al256b((size_t)cap * sizeof(int2)), mb = al256b((size_t)cap), tb = al256b((size_t)ntiles * 4);
   const size_t kb = (size_t)RTH_TICKET_WORDS * 4;
   char *w = (char *)sc.get(256 + 2 * lb + mb + tb + kb);
-  int2 *out = (int2 *)sc.get((size_t)cap * sizeof(int2));
-  float *dout = return_depth ? (float *)sc.get((size_t)cap * dd * sizeof(float)) : nullptr;
-  if (!w || !out || (return_depth && !dout)) return KL_E_ALLOC;
+  // (r06) the two outputs from ONE allocation (each is a host callback into the caller's allocator
+  // before the first launch, the GPU idle meanwhile): nuggets | depths
+  const size_t ob = al256b((size_t)cap * sizeof(int2));
+  char *ob_p = (char *)sc.get(ob + (return_depth ? (size_t)cap * dd * sizeof(float) : 0));
+  int2 *out = (int2 *)ob_p;
+  float *dout = return_depth && ob_p ? (float *)(ob_p + ob) : nullptr;
+  if (!w || !out) return KL_E_ALLOC;
   RthBufs bf{};
   bf.dn = (uint32_t *)w;
   bf.result = (int64_t *)(w + 64);  // (rows, truncated)

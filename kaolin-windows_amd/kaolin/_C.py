@@ -646,7 +646,7 @@ def _raytrace_checks(func, octree, points, pyramid, exclusive_sum, ray_o, ray_d)
     max_level = pyramid.shape[1] - 2
     if not max_level < 15:
         raise RuntimeError('SPC pyramid too big')
-    pyr = pyramid.reshape(-1)
+    pyr = pyramid.reshape(-1).tolist()  # (one conversion: four tensor indexings cost ~15 us of host time)
     osize = int(pyr[2 * max_level + 2])
     psize = int(pyr[2 * max_level + 3])
     check_size_dim(func, Arg(octree, 'octree', 1), 0, osize)

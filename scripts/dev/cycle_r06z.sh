@@ -46,3 +46,6 @@ f=glob.glob('gpurun_out/r06z/prof/**/*kernel_stats.csv',recursive=True)[0]
 for r in list(csv.DictReader(open(f)))[:8]:
     print(r['Name'][:70], r['Calls'], r['AverageNs'])
 PY
+# p2m face splits (dev param 28 = target workgroups: 10240 -> 20 splits of 1024 faces at cfg2)
+timeout -k 10 200 python scripts/dev/p2m_ab.py 28=0 28=5000 28=16000 28=0 28=5000 28=16000 > $OUT/p2m_ab.txt 2>&1 || true
+grep params $OUT/p2m_ab.txt || true
