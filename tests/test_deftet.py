@@ -241,6 +241,31 @@ def test_gpu_knum_paths(kal, knum):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('binned', [False, True])
+def test_gpu_walk_quotient_underflow_edge(kal, binned):
+    """Barycentric quotients at the underflow edge: face 0's first quotient at pixel 0 underflows to
+    -0, a hit under the reference's `w >= 0`; face 1's is a tiny negative normal (a miss); faces 2-3
+    are plain.  Both forwards, f64, vs the oracle (r06: guards any shortcut taken before the
+    divisions, like the sign pre-test measured in DESIGN.md §3.6)."""
+    dt = np.float64
+    fvi = np.zeros((1, 4, 3, 2), dt)
+    fvi[0, 0] = [[1e180, -1e180], [1e-150, 0.], [0., -1e-150]]
+    fvi[0, 1] = [[1e20, -1e20], [1e-150, 0.], [0., -1e-150]]
+    fvi[0, 2] = [[0.5, 0.5], [0.9, 0.5], [0.5, 0.9]]
+    fvi[0, 3] = [[-0.5, -0.5], [0.5, -0.5], [0., 0.5]]
+    fvz = np.full((1, 4, 3), -1.5, dt)
+    fvz[0, 0] = [-1.4, -1.5, -1.6]
+    pix = np.array([[[0., -1e-160], [0., -0.1], [0.6, 0.6]]], dt)
+    ranges = np.tile(np.array([-2.6, -1.2], dt), (1, 3, 1))
+    args = [_T(fvz), _T(fvi), None, _T(pix), _T(ranges), 4, 1e-8]
+    out = kal._C.deftet_forward('deftet', *args, binned=binned)
+    ref = orc.deftet_sparse_render_forward(fvz, fvi, None, pix, ranges, 4, 1e-8)
+    assert ref[0][0, 0, 0] == 0 and np.signbit(ref[2][0, 0, 0])
+    for x, r in zip(out, ref):
+        np.testing.assert_array_equal(_A(x), r)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('dtype', [np.float32, np.float64])
 def test_gpu_binned_and_tile_forward_agree(kal, dtype):
     """The screen-grid forward (with an allocator) and the tile-walk forward (without) give the
