@@ -117,8 +117,8 @@ __global__ void __launch_bounds__(kDtTile)
 }
 
 // deftet_cuda.cu:32-190
-template <typename T>
-__global__ void __launch_bounds__(kDtTile)
+template <typename T, int MINW>
+__global__ void __launch_bounds__(kDtTile, MINW)
     deftet_fwd_kernel(int64_t F, int64_t P, int K, const T *__restrict__ fvz, const T *__restrict__ fvi,
                       const T *__restrict__ bboxes, const T *__restrict__ pix, const T *__restrict__ ranges,
                       float eps, int64_t *__restrict__ out_idx, T *__restrict__ out_depth, T *__restrict__ out_w0,
@@ -974,9 +974,12 @@ static int deftet_forward(int64_t B, int64_t F, int64_t P, int64_t K, const void
   int32_t *perm = nullptr;
   void *scratch = nullptr;
   KL_CHECK_RC(dt_pixel_order<T>(B, P, pix, &perm, &scratch, st));
-  hipLaunchKernelGGL(deftet_fwd_kernel<T>, dim3((unsigned)cdiv(P, kDtTile), (unsigned)B), dim3(kDtTile), 0, st, F, P,
-                     (int)K, (const T *)fvz, (const T *)fvi, (const T *)bboxes, (const T *)pix, (const T *)ranges, eps,
-                     idx, (T *)depth, (T *)w0, (T *)w1, (const T *)ws, (const int32_t *)perm);
+  // (dev param 29 = 1: no occupancy bound, the r05 walk)
+  constexpr int kMinW = sizeof(T) == 4 ? 8 : 1;
+  hipLaunchKernelGGL((g_dev_param[29] == 1 ? deftet_fwd_kernel<T, 1> : deftet_fwd_kernel<T, kMinW>),
+                     dim3((unsigned)cdiv(P, kDtTile), (unsigned)B), dim3(kDtTile), 0, st, F, P, (int)K,
+                     (const T *)fvz, (const T *)fvi, (const T *)bboxes, (const T *)pix, (const T *)ranges, eps, idx,
+                     (T *)depth, (T *)w0, (T *)w1, (const T *)ws, (const int32_t *)perm);
   KL_CHECK_LAUNCH();
   if (scratch) KL_CHECK_HIP(hipFreeAsync(scratch, st));
   return KL_OK;
