@@ -305,6 +305,9 @@ __device__ __noinline__ void subdivide_dfs(Tri<T> root, int level, T thr, int R,
 // One level.  faces != null: level 0, the triangles gathered from (pts, faces) and tested here;
 // else the first min(*n_in, cap) triangles of `in`.  last: every kept child is finished
 // depth-first instead of appended.  The loop trip count is uniform over the workgroup.
+#ifndef VOX_MIN_WAVES  // subdivide_async / tail kernels' minimum waves per SIMD (A/B builds)
+#define VOX_MIN_WAVES 5  // r06: 96 VGPRs, 5 waves (98 / 97 and 4 unbounded), no spills: 1-2 % faster
+#endif
 // one level's grid-strided loop (subdivide_async_kernel and, per level, subdivide_tail_kernel); n is
 // uniform over the grid
 template <typename T, typename G>
@@ -363,7 +366,7 @@ __device__ __forceinline__ void subdivide_level(const T *__restrict__ pts, const
 }
 
 template <typename T, typename G>
-__global__ void __launch_bounds__(256) subdivide_async_kernel(
+__global__ void __launch_bounds__(256, VOX_MIN_WAVES) subdivide_async_kernel(
     const T *__restrict__ pts, const int64_t *__restrict__ faces, int64_t F, const Tri<T> *__restrict__ in,
     const unsigned long long *__restrict__ n_in, int level, int last, int64_t cap, T thr, int R, G *__restrict__ grid,
     Tri<T> *__restrict__ out, unsigned long long *__restrict__ n_out, unsigned *__restrict__ status,
@@ -382,7 +385,7 @@ __global__ void __launch_bounds__(256) subdivide_async_kernel(
 // workgroup that waits spin_limit rounds sets status bit 2 (grid incomplete; the eager call raises)
 // and stops.  buf: the two ping-pong buffers (level k reads buf[(k + 1) & 1], writes buf[k & 1]).
 template <typename T, typename G>
-__global__ void __launch_bounds__(256) subdivide_tail_kernel(Tri<T> *__restrict__ buf0, Tri<T> *__restrict__ buf1,
+__global__ void __launch_bounds__(256, VOX_MIN_WAVES) subdivide_tail_kernel(Tri<T> *__restrict__ buf0, Tri<T> *__restrict__ buf1,
                                                              unsigned long long *__restrict__ counter, int k0,
                                                              int levels, int64_t cap, T thr, int R,
                                                              G *__restrict__ grid, unsigned *__restrict__ status,
